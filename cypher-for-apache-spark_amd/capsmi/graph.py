@@ -1,0 +1,152 @@
+"""Graph fast path over the C ABI: node-scan bitmaps and fused Expand kernels.
+
+The relational planner lowers ``(a)-[r]->(b)`` to two joins
+(okapi-relational/.../planning/RelationalPlanner.scala:113-137); when the joined scans are base
+entity tables with dense Long ids these entry points compute the same row multisets in one
+streaming pass per hop (see include/capsmi.h, "graph fast path").
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence, Tuple
+
+from . import _lib
+from .expr import Expr, compile_program, to_ctypes
+from .table import GpuTable, Session
+
+RMAT_GRAPH500 = (57, 19, 19)  # (A, B, C) percent, D = 5  -- SURVEY.md §8d
+RMAT_LDBC = (45, 15, 15)      # C5 "LDBC-shaped" proposal
+
+
+class NodeBitmap:
+    """Node scan (+ label/property predicate) collapsed to one bit per id in [lo, hi)."""
+
+    def __init__(self, session: Session, lo: int, hi: int):
+        self.session = session
+        self.lo, self.hi = lo, hi
+        self._h = ctypes.c_void_p()
+        _lib.call("capsmi_bitmap_create", session.handle, lo, hi, ctypes.byref(self._h))
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def nwords(self) -> int:
+        return (self.hi - self.lo + 31) // 32
+
+    def add_scan(self, nodes: GpuTable, id_col: str = "id", predicate: Optional[Expr] = None) -> "NodeBitmap":
+        if predicate is None:
+            _lib.call("capsmi_bitmap_add_scan", self._h, nodes.handle, id_col.encode(), 0, None)
+        else:
+            names = nodes.physicalColumns
+            index = {n: i for i, n in enumerate(names)}
+            prog = compile_program(predicate, lambda c: index[c], self.session.encode_str)
+            _lib.call("capsmi_bitmap_add_scan", self._h, nodes.handle, id_col.encode(), len(prog), to_ctypes(prog))
+        return self
+
+    def stats(self) -> Tuple[int, bool]:
+        bits, uniq = ctypes.c_int64(), ctypes.c_int32()
+        _lib.call("capsmi_bitmap_stats", self._h, ctypes.byref(bits), ctypes.byref(uniq))
+        return bits.value, bool(uniq.value)
+
+    def release(self) -> None:
+        if self._h:
+            _lib.call("capsmi_bitmap_release", self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            if self._h and _lib._lib is not None:
+                _lib._lib.capsmi_bitmap_release(self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+
+def _handles(rels: Sequence[GpuTable]):
+    arr = (ctypes.c_void_p * max(1, len(rels)))()
+    for i, t in enumerate(rels):
+        arr[i] = t.handle
+    return arr
+
+
+def expand_filter(session: Session, rels: GpuTable, src_ok: NodeBitmap, dst_ok: NodeBitmap,
+                  out_cols: Sequence[str], out_names: Optional[Sequence[str]] = None,
+                  src_col: str = "source", dst_col: str = "target") -> GpuTable:
+    """``MATCH (a)-[r]->(b) WHERE src_ok(a) AND dst_ok(b)`` -> the surviving rel rows, projected."""
+    out = ctypes.c_void_p()
+    _lib.call("capsmi_expand_filter", session.handle, rels.handle, src_col.encode(), dst_col.encode(),
+              src_ok.handle, dst_ok.handle, len(out_cols), _lib.strs(out_cols),
+              _lib.strs(out_names) if out_names else None, ctypes.byref(out))
+    return GpuTable(session, out)
+
+
+def two_hop_count_distinct(session: Session, rels: Sequence[GpuTable], a_ok: NodeBitmap, b_ok: NodeBitmap,
+                           c_ok: NodeBitmap, src_col: str = "source", dst_col: str = "target") -> int:
+    """``MATCH (a)-[r1]->(b)-[r2]->(c) RETURN count(DISTINCT c)`` (r1 <> r2 implied)."""
+    v = ctypes.c_int64()
+    _lib.call("capsmi_two_hop_count_distinct", session.handle, len(rels), _handles(rels), src_col.encode(),
+              dst_col.encode(), a_ok.handle, b_ok.handle, c_ok.handle, ctypes.byref(v))
+    return v.value
+
+
+def two_hop_count(session: Session, rels: Sequence[GpuTable], a_ok: NodeBitmap, b_ok: NodeBitmap, c_ok: NodeBitmap,
+                  src_col: str = "source", dst_col: str = "target") -> int:
+    """count(*) of the same 2-hop MATCH, closed form (sum_b inA(b) outC(b) - eligible self-loops)."""
+    v = ctypes.c_int64()
+    _lib.call("capsmi_two_hop_count", session.handle, len(rels), _handles(rels), src_col.encode(), dst_col.encode(),
+              a_ok.handle, b_ok.handle, c_ok.handle, ctypes.byref(v))
+    return v.value
+
+
+def two_hop_mark_mid(session: Session, rels: Sequence[GpuTable], a_ok: NodeBitmap, b_ok: NodeBitmap,
+                     mid_ptr: int, scratch_ptr: int, src_col: str = "source", dst_col: str = "target") -> None:
+    _lib.call("capsmi_two_hop_mark_mid", session.handle, len(rels), _handles(rels), src_col.encode(),
+              dst_col.encode(), a_ok.handle, b_ok.handle, ctypes.c_void_p(mid_ptr), ctypes.c_void_p(scratch_ptr))
+
+
+def two_hop_mark_dst(session: Session, rels: Sequence[GpuTable], b_ok: NodeBitmap, c_ok: NodeBitmap, mid_ptr: int,
+                     dst_ptr: int, src_col: str = "source", dst_col: str = "target") -> None:
+    _lib.call("capsmi_two_hop_mark_dst", session.handle, len(rels), _handles(rels), src_col.encode(),
+              dst_col.encode(), b_ok.handle, c_ok.handle, ctypes.c_void_p(mid_ptr), ctypes.c_void_p(dst_ptr))
+
+
+def words_popcount(session: Session, words_ptr: int, w_begin: int, w_end: int) -> int:
+    v = ctypes.c_int64()
+    _lib.call("capsmi_words_popcount", session.handle, ctypes.c_void_p(words_ptr), w_begin, w_end, ctypes.byref(v))
+    return v.value
+
+
+def cluster_by(rels: GpuTable, key_col: str, lo: int, hi: int) -> GpuTable:
+    out = ctypes.c_void_p()
+    _lib.call("capsmi_cluster_by", rels.handle, key_col.encode(), lo, hi, ctypes.byref(out))
+    return GpuTable(rels.session, out)
+
+
+def owner_words(nbits: int, part: int, nparts: int) -> Tuple[int, int]:
+    b, e = ctypes.c_int64(), ctypes.c_int64()
+    _lib.call("capsmi_owner_words", nbits, part, nparts, ctypes.byref(b), ctypes.byref(e))
+    return b.value, e.value
+
+
+PART_NONE, PART_SOURCE, PART_TARGET = -1, 0, 1
+
+
+def rmat_rels(session: Session, scale: int, e_begin: int, e_end: int, probs=RMAT_GRAPH500, seed: int = 42,
+              part_col: int = PART_NONE, part: int = 0, nparts: int = 1) -> GpuTable:
+    """R-MAT relationship table [id, source, target] (definition: oracle/rmat.c)."""
+    out = ctypes.c_void_p()
+    pa, pb, pc = probs
+    _lib.call("capsmi_rmat_rels", session.handle, scale, e_begin, e_end, pa, pb, pc, seed, part_col, part, nparts,
+              ctypes.byref(out))
+    return GpuTable(session, out)
+
+
+NODES_ALL, NODES_PERSON, NODES_COMPANY = 0, 1, 2
+
+
+def rmat_nodes(session: Session, scale: int, kind: int = NODES_ALL, seed: int = 42) -> GpuTable:
+    out = ctypes.c_void_p()
+    _lib.call("capsmi_rmat_nodes", session.handle, scale, kind, seed, ctypes.byref(out))
+    return GpuTable(session, out)

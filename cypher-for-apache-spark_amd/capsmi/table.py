@@ -1,0 +1,338 @@
+"""Host mirror of CAPS's backend table interface over the C ABI.
+
+``GpuTable`` follows the member names, argument meaning and error behaviour of
+    trait Table[T <: Table[T]] extends CypherTable
+    okapi-relational/src/main/scala/org/opencypher/okapi/relational/api/table/Table.scala:43-176
+as implemented for Spark by DataFrameTable (spark-cypher/.../impl/table/SparkTable.scala:47-257),
+so that a relational plan written against ``Table`` runs unchanged on the device.
+Every operator executes in libcapsmi.so (HIP, gfx950); Python only marshals handles.
+"""
+from __future__ import annotations
+
+import bisect
+import ctypes
+from dataclasses import dataclass
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from .expr import BOOL, F64, I64, STR, Expr, compile_program, to_ctypes
+
+JOIN_TYPES = {"inner": 0, "left_outer": 1, "right_outer": 2, "full_outer": 3, "cross": 4}
+AGG_KINDS = {"count_star": 0, "count": 1, "min": 2, "max": 3, "sum": 4, "avg": 5}
+
+
+@dataclass
+class ColumnData:
+    """Host column: ``values`` int64 (I64/BOOL/STR codes) or float64 (F64); ``valid`` bool mask or None."""
+    name: str
+    type: int
+    values: np.ndarray
+    valid: Optional[np.ndarray] = None
+
+    def words(self) -> np.ndarray:
+        v = np.asarray(self.values)
+        if self.type == F64:
+            return np.ascontiguousarray(v.astype(np.float64)).view(np.int64)
+        return np.ascontiguousarray(v.astype(np.int64))
+
+
+class StringDictionary:
+    """Order-preserving dictionary for CTString values (include/capsmi.h: STR columns are codes).
+
+    Known strings get even codes 2*rank; an unknown literal gets the odd code between its sorted
+    neighbours, so equality and ordering on codes equal equality and ordering on strings."""
+
+    def __init__(self, strings: Iterable[str] = ()):
+        self._sorted: List[str] = sorted(set(strings))
+
+    def extend(self, strings: Iterable[str]) -> None:
+        new = set(strings) - set(self._sorted)
+        if new:
+            self._sorted = sorted(set(self._sorted) | new)
+
+    def encode(self, s: str) -> int:
+        i = bisect.bisect_left(self._sorted, s)
+        if i < len(self._sorted) and self._sorted[i] == s:
+            return 2 * i
+        return 2 * i - 1
+
+    def decode(self, code: int) -> str:
+        if code % 2:
+            raise KeyError(f"code {code} is not a dictionary string")
+        return self._sorted[code // 2]
+
+    def __len__(self) -> int:
+        return len(self._sorted)
+
+
+class Session:
+    """One device, one HIP stream (CAPSSession.local analogue, spark-cypher/.../api/CAPSSession.scala:110-131)."""
+
+    def __init__(self, device: int = 0, dictionary: Optional[StringDictionary] = None):
+        self._h = ctypes.c_void_p()
+        _lib.call("capsmi_session_create", device, ctypes.byref(self._h))
+        self.device = device
+        self.dictionary = dictionary or StringDictionary()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_stream(self, hip_stream: Optional[int]) -> None:
+        _lib.call("capsmi_session_set_stream", self._h, ctypes.c_void_p(hip_stream or 0))
+
+    def sync(self) -> None:
+        _lib.call("capsmi_session_sync", self._h)
+
+    def close(self) -> None:
+        if self._h:
+            _lib.call("capsmi_session_destroy", self._h)
+            self._h = ctypes.c_void_p()
+
+    def table(self, columns: Sequence[ColumnData]) -> "GpuTable":
+        """CAPSNodeTable / CAPSRelationshipTable ingest: copies host columns to the device."""
+        n = len(columns[0].values) if columns else 0
+        descs = (_lib.ColDesc * max(1, len(columns)))()
+        keep = []
+        for i, c in enumerate(columns):
+            if len(c.values) != n:
+                raise _lib.IllegalArgumentException(f"column {c.name} has {len(c.values)} rows, expected {n}")
+            w = c.words()
+            keep.append(w)
+            descs[i].name = c.name.encode()
+            descs[i].type = c.type
+            descs[i].data = w.ctypes.data if n else None
+            if c.valid is not None:
+                vb = np.ascontiguousarray(np.asarray(c.valid, dtype=np.uint8))
+                keep.append(vb)
+                descs[i].valid = vb.ctypes.data if n else None
+            else:
+                descs[i].valid = None
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_table_from_host", self._h, len(columns), descs, n, ctypes.byref(out))
+        return GpuTable(self, out)
+
+    def encode_str(self, s: str) -> int:
+        return self.dictionary.encode(s)
+
+
+class GpuTable:
+    """A device-resident, immutable table; each operator returns a new GpuTable."""
+
+    def __init__(self, session: Session, handle: ctypes.c_void_p):
+        self.session = session
+        self._h = handle
+
+    # ---- lifetime ------------------------------------------------------------------------
+    @property
+    def handle(self):
+        return self._h
+
+    def release(self) -> None:
+        if self._h:
+            _lib.call("capsmi_table_release", self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            if self._h and _lib._lib is not None:
+                _lib._lib.capsmi_table_release(self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+    def _wrap(self, h) -> "GpuTable":
+        return GpuTable(self.session, h)
+
+    # ---- CypherTable (okapi-api/.../api/table/CypherTable.scala:41-68) -------------------
+    @property
+    def size(self) -> int:
+        v = ctypes.c_int64()
+        _lib.call("capsmi_table_size", self._h, ctypes.byref(v))
+        return v.value
+
+    @property
+    def physicalColumns(self) -> List[str]:
+        n = ctypes.c_int32()
+        _lib.call("capsmi_table_num_columns", self._h, ctypes.byref(n))
+        buf = ctypes.create_string_buffer(1024)
+        out = []
+        for i in range(n.value):
+            _lib.call("capsmi_table_column_name", self._h, i, buf, 1024)
+            out.append(buf.value.decode())
+        return out
+
+    @property
+    def columnType(self) -> dict:
+        out = {}
+        t = ctypes.c_int32()
+        for i, name in enumerate(self.physicalColumns):
+            _lib.call("capsmi_table_column_type", self._h, i, ctypes.byref(t))
+            out[name] = t.value
+        return out
+
+    def column_index(self, name: str) -> int:
+        v = ctypes.c_int32()
+        _lib.call("capsmi_table_column_index", self._h, name.encode(), ctypes.byref(v))
+        if v.value < 0:
+            raise _lib.IllegalArgumentException(f"no column named '{name}'")
+        return v.value
+
+    def column(self, name: str, offset: int = 0, n: Optional[int] = None) -> ColumnData:
+        idx = self.column_index(name)
+        size = self.size
+        if n is None:
+            n = size - offset
+        ty = self.columnType[name]
+        vals = np.empty(n, dtype=np.int64)
+        valid = np.empty(n, dtype=np.uint8)
+        _lib.call("capsmi_table_export", self._h, idx, vals.ctypes.data if n else None,
+                  valid.ctypes.data if n else None, offset, n)
+        nullable = ctypes.c_int32()
+        _lib.call("capsmi_table_column_nullable", self._h, idx, ctypes.byref(nullable))
+        if ty == F64:
+            vals = vals.view(np.float64)
+        return ColumnData(name, ty, vals, valid.astype(bool) if nullable.value else None)
+
+    def to_columns(self) -> List[ColumnData]:
+        return [self.column(c) for c in self.physicalColumns]
+
+    def rows(self) -> List[dict]:
+        """CypherTable.rows: host rows with strings decoded."""
+        cols = self.to_columns()
+        n = self.size
+        out = []
+        for r in range(n):
+            row = {}
+            for c in cols:
+                if c.valid is not None and not c.valid[r]:
+                    row[c.name] = None
+                    continue
+                v = c.values[r]
+                if c.type == BOOL:
+                    v = bool(v)
+                elif c.type == STR:
+                    v = self.session.dictionary.decode(int(v))
+                elif c.type == F64:
+                    v = float(v)
+                else:
+                    v = int(v)
+                row[c.name] = v
+            out.append(row)
+        return out
+
+    def fingerprint(self, cols: Sequence[str]) -> Tuple[int, int, int]:
+        cnt, s, x = ctypes.c_int64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.call("capsmi_table_fingerprint", self._h, len(cols), _lib.strs(cols), ctypes.byref(cnt),
+                  ctypes.byref(s), ctypes.byref(x))
+        return cnt.value, s.value, x.value
+
+    # ---- Table[T] operators ----------------------------------------------------------------
+    def cache(self) -> "GpuTable":
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_cache", self._h, ctypes.byref(out))
+        return self._wrap(out)
+
+    def select(self, *cols: str) -> "GpuTable":
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_select", self._h, len(cols), _lib.strs(cols), ctypes.byref(out))
+        return self._wrap(out)
+
+    def _program(self, e: Expr):
+        names = self.physicalColumns
+        index = {n: i for i, n in enumerate(names)}
+
+        def col(name: str) -> int:
+            if name not in index:
+                raise _lib.IllegalArgumentException(f"expression references unknown column '{name}'")
+            return index[name]
+
+        prog = compile_program(e, col, self.session.encode_str)
+        return len(prog), to_ctypes(prog)
+
+    def filter(self, expr: Expr) -> "GpuTable":
+        n, prog = self._program(expr)
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_filter", self._h, n, prog, ctypes.byref(out))
+        return self._wrap(out)
+
+    def drop(self, *cols: str) -> "GpuTable":
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_drop", self._h, len(cols), _lib.strs(cols), ctypes.byref(out))
+        return self._wrap(out)
+
+    def join(self, other: "GpuTable", join_type: str, *join_cols: Tuple[str, str]) -> "GpuTable":
+        if join_type not in JOIN_TYPES:
+            raise _lib.IllegalArgumentException(f"join type {join_type}")
+        out = ctypes.c_void_p()
+        lc = [a for a, _ in join_cols]
+        rc = [b for _, b in join_cols]
+        _lib.call("capsmi_join", self._h, other._h, JOIN_TYPES[join_type], len(join_cols), _lib.strs(lc),
+                  _lib.strs(rc), ctypes.byref(out))
+        return self._wrap(out)
+
+    def unionAll(self, other: "GpuTable") -> "GpuTable":
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_union_all", self._h, other._h, ctypes.byref(out))
+        return self._wrap(out)
+
+    def orderBy(self, *items: Tuple[str, str]) -> "GpuTable":
+        cols = [c for c, _ in items]
+        desc = (ctypes.c_int32 * max(1, len(items)))(*[1 if o.lower().startswith("desc") else 0 for _, o in items])
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_order_by", self._h, len(items), _lib.strs(cols), desc, ctypes.byref(out))
+        return self._wrap(out)
+
+    def skip(self, n: int) -> "GpuTable":
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_skip", self._h, n, ctypes.byref(out))
+        return self._wrap(out)
+
+    def limit(self, n: int) -> "GpuTable":
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_limit", self._h, n, ctypes.byref(out))
+        return self._wrap(out)
+
+    def distinct(self, *cols: str) -> "GpuTable":
+        out = ctypes.c_void_p()
+        if cols:  # DataFrameTable.distinct(cols) = dropDuplicates(cols), SparkTable.scala:234-235
+            _lib.call("capsmi_distinct_on", self._h, len(cols), _lib.strs(cols), ctypes.byref(out))
+        else:
+            _lib.call("capsmi_distinct", self._h, ctypes.byref(out))
+        return self._wrap(out)
+
+    def group(self, by: Sequence[str], aggregations: Sequence[Tuple[str, Optional[str], bool, str]]) -> "GpuTable":
+        """``aggregations``: (kind, input column, distinct, output column); kind in AGG_KINDS."""
+        aggs = (_lib.Agg * max(1, len(aggregations)))()
+        for i, (kind, inp, distinct, outname) in enumerate(aggregations):
+            aggs[i].kind = AGG_KINDS[kind]
+            aggs[i].distinct = 1 if distinct else 0
+            aggs[i].input = inp.encode() if inp else None
+            aggs[i].output = outname.encode()
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_group", self._h, len(by), _lib.strs(by), len(aggregations), aggs, ctypes.byref(out))
+        return self._wrap(out)
+
+    def withColumns(self, *columns: Tuple[Expr, str]) -> "GpuTable":
+        arr = (_lib.ExprColumn * max(1, len(columns)))()
+        keep = []
+        for i, (e, name) in enumerate(columns):
+            n, prog = self._program(e)
+            keep.append(prog)
+            arr[i].name = name.encode()
+            arr[i].nnodes = n
+            arr[i].prog = ctypes.cast(prog, ctypes.POINTER(type(prog._type_())))
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_with_columns", self._h, len(columns), arr, ctypes.byref(out))
+        return self._wrap(out)
+
+    def withColumnRenamed(self, old: str, new: str) -> "GpuTable":
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_with_column_renamed", self._h, old.encode(), new.encode(), ctypes.byref(out))
+        return self._wrap(out)
+
+    def show(self, rows: int = 20) -> None:
+        for r in self.limit(rows).rows():
+            print(r)

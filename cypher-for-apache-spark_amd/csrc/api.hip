@@ -1,0 +1,1191 @@
+// api.hip -- the C ABI (include/capsmi.h): CAPS Table[T] operators on device tables.
+//
+// Each capsmi_* operator mirrors one member of
+//   okapi-relational/src/main/scala/org/opencypher/okapi/relational/api/table/Table.scala
+// with the semantics DataFrameTable gives it
+//   spark-cypher/src/main/scala/org/opencypher/spark/impl/table/SparkTable.scala
+// Errors surface as status codes + a thread-local message, mapping the okapi exceptions.
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <unordered_set>
+
+#include "capsmi_impl.h"
+
+namespace capsmi {
+
+namespace graph {
+void expand_filter(capsmi_session* s, const int64_t* src, const int64_t* dst, int64_t m, const capsmi_bitmap* a,
+                   const capsmi_bitmap* b, int nout, const int64_t* const* in_d, const uint8_t* const* in_v,
+                   int64_t* const* out_d, uint8_t* const* out_v, int64_t* dev_count);
+void hop1(capsmi_session* s, const int64_t* src, const int64_t* dst, int64_t m, const capsmi_bitmap* a,
+          const capsmi_bitmap* b, uint32_t* M, uint32_t* S1, uint32_t* S2);
+void mid_combine(capsmi_session* s, uint32_t* X1, uint32_t* X2, const uint32_t* S1, int64_t nw);
+void hop2(capsmi_session* s, const int64_t* src, const int64_t* dst, int64_t m, const capsmi_bitmap* c,
+          const uint32_t* X1, const uint32_t* X2, int64_t mid_lo, int64_t mid_hi, uint32_t* C);
+void degrees(capsmi_session* s, const int64_t* src, const int64_t* dst, int64_t m, const capsmi_bitmap* a,
+             const capsmi_bitmap* b, const capsmi_bitmap* c, uint32_t* inA, uint32_t* outC, int64_t* loops);
+void deg_product(capsmi_session* s, const uint32_t* inA, const uint32_t* outC, int64_t n, const capsmi_bitmap* b,
+                 int64_t* out);
+int64_t rmat(capsmi_session* s, int scale, int64_t e_begin, int64_t e_end, int pa, int pb, int pc, uint64_t seed,
+             int part_col, int part, int nparts, Buf& id, Buf& so, Buf& dout);
+void person_flags(capsmi_session* s, int64_t n, bool want_person, uint8_t* f);
+void ages(capsmi_session* s, const int64_t* ids, int64_t n, uint64_t seed, int64_t* age);
+void fingerprint(capsmi_session* s, int ncols, const int64_t* const* d, const uint8_t* const* v, int64_t n,
+                 uint64_t* out_sum, uint64_t* out_xor);
+}  // namespace graph
+
+static thread_local std::string g_err;
+
+[[noreturn]] void throw_hip(hipError_t e, const char* what, const char* file, int line) {
+    const std::string msg = std::string("HIP error ") + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ") at " +
+                            file + ":" + std::to_string(line) + ": " + what;
+    throw Error(e == hipErrorOutOfMemory ? CAPSMI_ERR_OUT_OF_MEMORY : CAPSMI_ERR_DEVICE, msg);
+}
+
+DevBuf::~DevBuf() {
+    if (ptr) (void)hipFreeAsync(ptr, stream);
+}
+
+Buf dev_alloc(size_t bytes, hipStream_t stream) {
+    auto b = std::make_shared<DevBuf>();
+    b->bytes = bytes ? bytes : 8;
+    b->stream = stream;
+    HIP_CHECK(hipMallocAsync(&b->ptr, b->bytes, stream));
+    return b;
+}
+
+}  // namespace capsmi
+
+using namespace capsmi;
+
+namespace {
+
+void set_err(const std::string& m) { g_err = m; }
+
+#define API_BEGIN try {
+#define API_END                                                         \
+    }                                                                   \
+    catch (const capsmi::Error& e) {                                    \
+        set_err(e.what());                                              \
+        return e.code;                                                  \
+    }                                                                   \
+    catch (const std::bad_alloc&) {                                     \
+        set_err("host allocation failed");                              \
+        return CAPSMI_ERR_OUT_OF_MEMORY;                                \
+    }                                                                   \
+    catch (const std::exception& e) {                                   \
+        set_err(e.what());                                              \
+        return CAPSMI_ERR_INTERNAL;                                     \
+    }                                                                   \
+    return CAPSMI_OK;
+
+void need(const void* p, const char* what) {
+    REQUIRE(p != nullptr, CAPSMI_ERR_ILLEGAL_ARGUMENT, std::string("null argument: ") + what);
+}
+
+void use_device(capsmi_session* s) { HIP_CHECK(hipSetDevice(s->device)); }
+
+capsmi_table* new_table(capsmi_session* s, int64_t nrows) {
+    auto* t = new capsmi_table();
+    t->sess = s;
+    t->nrows = nrows;
+    return t;
+}
+
+int col_index(const capsmi_table* t, const char* name) {
+    need(name, "column name");
+    const int i = t->find(name);
+    REQUIRE(i >= 0, CAPSMI_ERR_ILLEGAL_ARGUMENT, std::string("no column named '") + name + "'");
+    return i;
+}
+
+// gather every column of `t` at `idx` (n entries; -1 -> NULL)
+void gather_into(capsmi_table* out, const capsmi_table* t, const Buf& idx, int64_t n, bool may_miss) {
+    capsmi_session* s = t->sess;
+    for (const Column& c : t->cols) {
+        Column o;
+        o.name = c.name;
+        o.type = c.type;
+        o.data = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s->stream);
+        if (c.valid || may_miss) o.valid = dev_alloc(n > 0 ? n : 1, s->stream);
+        gather_col(c.d(), c.v(), P<int64_t>(idx), n, P<int64_t>(o.data), P<uint8_t>(o.valid), s->stream);
+        out->cols.push_back(std::move(o));
+    }
+}
+
+KeyCols key_cols(const capsmi_table* t, const std::vector<int>& idx) {
+    REQUIRE((int)idx.size() <= kMaxKeys, CAPSMI_ERR_NOT_IMPLEMENTED, "more than 8 key columns");
+    KeyCols k;
+    k.n = (int)idx.size();
+    for (int i = 0; i < kMaxKeys; ++i) {
+        k.data[i] = i < k.n ? t->cols[idx[i]].d() : nullptr;
+        k.valid[i] = i < k.n ? t->cols[idx[i]].v() : nullptr;
+    }
+    return k;
+}
+
+bool types_joinable(int a, int b) {
+    const bool na = a == CAPSMI_I64 || a == CAPSMI_F64, nb = b == CAPSMI_I64 || b == CAPSMI_F64;
+    return a == b || (na && nb);
+}
+
+capsmi_table* join_impl(capsmi_table* l, capsmi_table* r, int jt, const std::vector<int>& lk,
+                        const std::vector<int>& rk) {
+    capsmi_session* s = l->sess;
+    hipStream_t st = s->stream;
+    for (const Column& a : l->cols)
+        for (const Column& b : r->cols)
+            REQUIRE(a.name != b.name, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                    "join inputs share column '" + a.name + "' (RelationalPlanner renames to disjoint columns)");
+    Buf li, ri;
+    int64_t total = 0;
+    bool lmiss = false, rmiss = false;
+    if (jt == CAPSMI_JOIN_CROSS) {
+        total = l->nrows * r->nrows;
+        li = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), st);
+        ri = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), st);
+        cross_pairs(l->nrows, r->nrows, P<int64_t>(li), P<int64_t>(ri), st);
+    } else {
+        for (size_t i = 0; i < lk.size(); ++i)
+            REQUIRE(types_joinable(l->cols[lk[i]].type, r->cols[rk[i]].type), CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                    "join key types differ: " + l->cols[lk[i]].name + " vs " + r->cols[rk[i]].name);
+        // inner: build on the smaller side; left outer / full outer: build right; right outer: build left
+        bool build_left = false;
+        if (jt == CAPSMI_JOIN_INNER) build_left = l->nrows < r->nrows;
+        else if (jt == CAPSMI_JOIN_RIGHT_OUTER) build_left = true;
+        capsmi_table* B = build_left ? l : r;
+        capsmi_table* Pr = build_left ? r : l;
+        const KeyCols bk = key_cols(B, build_left ? lk : rk);
+        const KeyCols pk = key_cols(Pr, build_left ? rk : lk);
+        HashTable ht;
+        Buf slot_of_row, slot_of_probe, offsets, rows;
+        hash_build(s, bk, B->nrows, /*skip_null_keys=*/true, ht, slot_of_row);
+        hash_group_rows(s, ht, slot_of_row, B->nrows, offsets, rows);
+        hash_probe(s, pk, bk, Pr->nrows, ht, slot_of_probe);
+        const bool outer = jt != CAPSMI_JOIN_INNER;
+        Buf pi, bi, matched;
+        total = join_expand(s, slot_of_probe, Pr->nrows, ht, offsets, rows, outer, pi, bi,
+                            jt == CAPSMI_JOIN_FULL_OUTER ? &matched : nullptr, B->nrows);
+        if (outer) (build_left ? lmiss : rmiss) = true;
+        if (jt == CAPSMI_JOIN_FULL_OUTER) {
+            // append build (right) rows that never matched, left side NULL
+            Buf unm_flags = dev_alloc(B->nrows > 0 ? B->nrows : 1, st);
+            invert_u8(P<uint8_t>(matched), P<uint8_t>(unm_flags), B->nrows, st);
+            Buf unm_idx;
+            const int64_t nu = flags_to_indices(s, P<uint8_t>(unm_flags), B->nrows, unm_idx);
+            Buf pi2 = dev_alloc(sizeof(int64_t) * (total + nu > 0 ? total + nu : 1), st);
+            Buf bi2 = dev_alloc(sizeof(int64_t) * (total + nu > 0 ? total + nu : 1), st);
+            if (total) {
+                HIP_CHECK(hipMemcpyAsync(P<void>(pi2), P<void>(pi), sizeof(int64_t) * total, hipMemcpyDeviceToDevice, st));
+                HIP_CHECK(hipMemcpyAsync(P<void>(bi2), P<void>(bi), sizeof(int64_t) * total, hipMemcpyDeviceToDevice, st));
+            }
+            fill_i64(P<int64_t>(pi2) + total, -1, nu, st);
+            if (nu) HIP_CHECK(hipMemcpyAsync(P<int64_t>(bi2) + total, P<void>(unm_idx), sizeof(int64_t) * nu,
+                                             hipMemcpyDeviceToDevice, st));
+            total += nu;
+            pi = pi2;
+            bi = bi2;
+            lmiss = rmiss = true;
+        }
+        li = build_left ? bi : pi;
+        ri = build_left ? pi : bi;
+    }
+    capsmi_table* out = new_table(s, total);
+    gather_into(out, l, li, total, lmiss);
+    capsmi_table tmp;
+    tmp.sess = s;
+    gather_into(&tmp, r, ri, total, rmiss);
+    for (auto& c : tmp.cols) out->cols.push_back(std::move(c));
+    return out;
+}
+
+// stable row permutation ordering `t` by keys (LSD: last key first; per key a 64-bit value pass,
+// then an 8-bit pass on the null flag so that the flag dominates)
+Buf order_perm(capsmi_table* t, const std::vector<int>& keys, const std::vector<int>& desc) {
+    capsmi_session* s = t->sess;
+    hipStream_t st = s->stream;
+    const int64_t n = t->nrows;
+    Buf perm = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), st);
+    iota_i64(P<int64_t>(perm), 0, n, st);
+    if (n <= 1) return perm;
+    Buf kbuf = dev_alloc(sizeof(uint64_t) * n, st);
+    for (int k = (int)keys.size() - 1; k >= 0; --k) {
+        const Column& c = t->cols[keys[k]];
+        order_keys(s, c.d(), c.v(), c.type, desc[k] != 0, false, P<int64_t>(perm), n, P<uint64_t>(kbuf));
+        radix_sort_pairs(s, P<uint64_t>(kbuf), P<int64_t>(perm), n, 0, 64);
+        if (c.valid) {
+            order_keys(s, c.d(), c.v(), c.type, desc[k] != 0, true, P<int64_t>(perm), n, P<uint64_t>(kbuf));
+            radix_sort_pairs(s, P<uint64_t>(kbuf), P<int64_t>(perm), n, 0, 8);
+        }
+    }
+    return perm;
+}
+
+std::vector<int> names_to_idx(const capsmi_table* t, int32_t n, const char* const* names) {
+    std::vector<int> v;
+    for (int i = 0; i < n; ++i) v.push_back(col_index(t, names[i]));
+    return v;
+}
+
+const Column& rel_col(const capsmi_table* t, const char* name) {
+    const Column& c = t->cols[col_index(t, name)];
+    REQUIRE(c.type == CAPSMI_I64, CAPSMI_ERR_ILLEGAL_ARGUMENT, std::string("id column '") + name + "' must be Long");
+    REQUIRE(c.valid == nullptr, CAPSMI_ERR_UNSUPPORTED,
+            std::string("fused path needs a non-nullable id column ('") + name + "'; EntityTable.verify)");
+    return c;
+}
+
+void check_bitmap(const capsmi_bitmap* b, const char* what) {
+    need(b, what);
+}
+
+}  // namespace
+
+// =============================== C ABI ========================================================
+extern "C" {
+
+size_t capsmi_last_error(char* buf, size_t n) {
+    if (buf && n) {
+        const size_t k = std::min(n - 1, g_err.size());
+        std::memcpy(buf, g_err.data(), k);
+        buf[k] = 0;
+    }
+    return g_err.size();
+}
+
+const char* capsmi_version(void) { return "capsmi 0.1.0 (gfx950)"; }
+
+capsmi_status capsmi_session_create(int32_t device, capsmi_session** out) {
+    API_BEGIN
+    need(out, "out");
+    int n = 0;
+    HIP_CHECK(hipGetDeviceCount(&n));
+    REQUIRE(device >= 0 && device < n, CAPSMI_ERR_ILLEGAL_ARGUMENT, "no such HIP device " + std::to_string(device));
+    HIP_CHECK(hipSetDevice(device));
+    auto* s = new capsmi_session();
+    s->device = device;
+    HIP_CHECK(hipStreamCreateWithFlags(&s->own_stream, hipStreamNonBlocking));
+    s->stream = s->own_stream;
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    s->num_cus = prop.multiProcessorCount;
+    HIP_CHECK(hipHostMalloc((void**)&s->pinned, 64, hipHostMallocDefault));
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+        uint64_t thr = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    }
+    *out = s;
+    API_END
+}
+
+capsmi_status capsmi_session_destroy(capsmi_session* s) {
+    API_BEGIN
+    if (!s) return CAPSMI_OK;
+    use_device(s);
+    (void)hipStreamSynchronize(s->stream);
+    (void)hipStreamSynchronize(s->own_stream);
+    (void)hipHostFree(s->pinned);
+    (void)hipStreamDestroy(s->own_stream);
+    delete s;
+    API_END
+}
+
+capsmi_status capsmi_session_set_stream(capsmi_session* s, void* hip_stream) {
+    API_BEGIN
+    need(s, "session");
+    s->stream = hip_stream ? (hipStream_t)hip_stream : s->own_stream;
+    API_END
+}
+
+capsmi_status capsmi_session_set_profiling(capsmi_session* s, int32_t enabled) {
+    API_BEGIN
+    need(s, "session");
+    s->prof = enabled != 0;
+    API_END
+}
+
+capsmi_status capsmi_session_kernel_time(capsmi_session* s, const char* name, int64_t* launches, double* total_ms) {
+    API_BEGIN
+    need(s, "session");
+    need(name, "name");
+    use_device(s);
+    for (auto& p : s->pending) {
+        HIP_CHECK(hipEventSynchronize(p.b));
+        float ms = 0.f;
+        HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
+        auto& t = s->totals[p.name];
+        t.first += 1;
+        t.second += ms;
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    s->pending.clear();
+    auto it = s->totals.find(name);
+    if (launches) *launches = it == s->totals.end() ? 0 : it->second.first;
+    if (total_ms) *total_ms = it == s->totals.end() ? 0.0 : it->second.second;
+    if (it != s->totals.end()) s->totals.erase(it);
+    API_END
+}
+
+capsmi_status capsmi_session_sync(capsmi_session* s) {
+    API_BEGIN
+    need(s, "session");
+    use_device(s);
+    HIP_CHECK(hipStreamSynchronize(s->stream));
+    API_END
+}
+
+static capsmi_status table_from(capsmi_session* s, int32_t ncols, const capsmi_col_desc* cols, int64_t nrows,
+                                capsmi_table** out, hipMemcpyKind kind) {
+    API_BEGIN
+    need(s, "session");
+    need(out, "out");
+    REQUIRE(nrows >= 0 && ncols >= 0, CAPSMI_ERR_ILLEGAL_ARGUMENT, "negative table size");
+    use_device(s);
+    std::unordered_set<std::string> seen;
+    auto* t = new_table(s, nrows);
+    std::unique_ptr<capsmi_table> guard(t);
+    for (int i = 0; i < ncols; ++i) {
+        need(cols[i].name, "column name");
+        REQUIRE(seen.insert(cols[i].name).second, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                std::string("duplicate column '") + cols[i].name + "'");
+        REQUIRE(cols[i].type >= CAPSMI_I64 && cols[i].type <= CAPSMI_STR, CAPSMI_ERR_ILLEGAL_ARGUMENT, "bad column type");
+        REQUIRE(nrows == 0 || cols[i].data, CAPSMI_ERR_ILLEGAL_ARGUMENT, "null column data");
+        Column c;
+        c.name = cols[i].name;
+        c.type = cols[i].type;
+        c.data = dev_alloc(sizeof(int64_t) * (nrows > 0 ? nrows : 1), s->stream);
+        if (nrows) HIP_CHECK(hipMemcpyAsync(P<void>(c.data), cols[i].data, sizeof(int64_t) * nrows, kind, s->stream));
+        if (cols[i].valid) {
+            c.valid = dev_alloc(nrows > 0 ? nrows : 1, s->stream);
+            if (nrows) HIP_CHECK(hipMemcpyAsync(P<void>(c.valid), cols[i].valid, nrows, kind, s->stream));
+        }
+        t->cols.push_back(std::move(c));
+    }
+    if (kind == hipMemcpyHostToDevice) HIP_CHECK(hipStreamSynchronize(s->stream));  // host buffers may go away
+    *out = guard.release();
+    API_END
+}
+
+capsmi_status capsmi_table_from_host(capsmi_session* s, int32_t ncols, const capsmi_col_desc* cols, int64_t nrows,
+                                     capsmi_table** out) {
+    return table_from(s, ncols, cols, nrows, out, hipMemcpyHostToDevice);
+}
+
+capsmi_status capsmi_table_from_device(capsmi_session* s, int32_t ncols, const capsmi_col_desc* cols, int64_t nrows,
+                                       capsmi_table** out) {
+    return table_from(s, ncols, cols, nrows, out, hipMemcpyDeviceToDevice);
+}
+
+capsmi_status capsmi_table_retain(capsmi_table* t) {
+    API_BEGIN
+    need(t, "table");
+    t->refs.fetch_add(1);
+    API_END
+}
+
+capsmi_status capsmi_table_release(capsmi_table* t) {
+    API_BEGIN
+    if (!t) return CAPSMI_OK;
+    if (t->refs.fetch_sub(1) == 1) {
+        use_device(t->sess);
+        delete t;
+    }
+    API_END
+}
+
+capsmi_status capsmi_table_size(const capsmi_table* t, int64_t* out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    *out = t->nrows;
+    API_END
+}
+
+capsmi_status capsmi_table_num_columns(const capsmi_table* t, int32_t* out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    *out = (int32_t)t->cols.size();
+    API_END
+}
+
+capsmi_status capsmi_table_column_name(const capsmi_table* t, int32_t col, char* buf, size_t n) {
+    API_BEGIN
+    need(t, "table");
+    REQUIRE(col >= 0 && col < (int)t->cols.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT, "column index out of range");
+    const std::string& nm = t->cols[col].name;
+    REQUIRE(buf && n > nm.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT, "name buffer too small");
+    std::memcpy(buf, nm.c_str(), nm.size() + 1);
+    API_END
+}
+
+capsmi_status capsmi_table_column_type(const capsmi_table* t, int32_t col, int32_t* out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    REQUIRE(col >= 0 && col < (int)t->cols.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT, "column index out of range");
+    *out = t->cols[col].type;
+    API_END
+}
+
+capsmi_status capsmi_table_column_index(const capsmi_table* t, const char* name, int32_t* out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    need(name, "name");
+    *out = t->find(name);
+    API_END
+}
+
+capsmi_status capsmi_table_column_nullable(const capsmi_table* t, int32_t col, int32_t* out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    REQUIRE(col >= 0 && col < (int)t->cols.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT, "column index out of range");
+    *out = t->cols[col].valid ? 1 : 0;
+    API_END
+}
+
+capsmi_status capsmi_table_export(const capsmi_table* t, int32_t col, void* host_data, uint8_t* host_valid,
+                                  int64_t offset, int64_t n) {
+    API_BEGIN
+    need(t, "table");
+    REQUIRE(col >= 0 && col < (int)t->cols.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT, "column index out of range");
+    REQUIRE(offset >= 0 && n >= 0 && offset + n <= t->nrows, CAPSMI_ERR_ILLEGAL_ARGUMENT, "export range out of bounds");
+    use_device(t->sess);
+    const Column& c = t->cols[col];
+    hipStream_t st = t->sess->stream;
+    if (n && host_data)
+        HIP_CHECK(hipMemcpyAsync(host_data, c.d() + offset, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
+    if (n && host_valid) {
+        if (c.valid) HIP_CHECK(hipMemcpyAsync(host_valid, c.v() + offset, n, hipMemcpyDeviceToHost, st));
+        else std::memset(host_valid, 1, n);
+    }
+    HIP_CHECK(hipStreamSynchronize(st));
+    API_END
+}
+
+capsmi_status capsmi_table_column_device_ptr(const capsmi_table* t, int32_t col, const void** data,
+                                             const uint8_t** valid) {
+    API_BEGIN
+    need(t, "table");
+    REQUIRE(col >= 0 && col < (int)t->cols.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT, "column index out of range");
+    if (data) *data = t->cols[col].d();
+    if (valid) *valid = t->cols[col].v();
+    API_END
+}
+
+// ---- Table[T] operators ---------------------------------------------------------------------
+capsmi_status capsmi_cache(capsmi_table* t, capsmi_table** out) {
+    // device tables are already materialised (DataFrameTable.cache, SparkTable.scala:240-246)
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    t->refs.fetch_add(1);
+    *out = t;
+    API_END
+}
+
+capsmi_status capsmi_select(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    auto idx = names_to_idx(t, ncols, cols);
+    auto* o = new_table(t->sess, t->nrows);
+    for (int i : idx) o->cols.push_back(t->cols[i]);
+    *out = o;
+    API_END
+}
+
+capsmi_status capsmi_drop(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    std::unordered_set<std::string> d;
+    for (int i = 0; i < ncols; ++i) d.insert(cols[i]);  // Spark drop ignores unknown names
+    auto* o = new_table(t->sess, t->nrows);
+    for (const Column& c : t->cols)
+        if (!d.count(c.name)) o->cols.push_back(c);
+    *out = o;
+    API_END
+}
+
+capsmi_status capsmi_with_column_renamed(capsmi_table* t, const char* old_name, const char* new_name,
+                                         capsmi_table** out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    need(new_name, "new name");
+    const int i = col_index(t, old_name);
+    const int j = t->find(new_name);
+    REQUIRE(j < 0 || j == i, CAPSMI_ERR_ILLEGAL_ARGUMENT, std::string("column '") + new_name + "' already exists");
+    auto* o = new_table(t->sess, t->nrows);
+    o->cols = t->cols;
+    o->cols[i].name = new_name;
+    *out = o;
+    API_END
+}
+
+capsmi_status capsmi_filter(capsmi_table* t, int32_t nnodes, const capsmi_expr* prog, capsmi_table** out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    REQUIRE(nnodes == 0 || prog, CAPSMI_ERR_ILLEGAL_ARGUMENT, "null program");
+    capsmi_session* s = t->sess;
+    use_device(s);
+    Buf flags = dev_alloc(t->nrows > 0 ? t->nrows : 1, s->stream);
+    eval_predicate(s, t, nnodes, prog, P<uint8_t>(flags));
+    Buf idx;
+    const int64_t n = flags_to_indices(s, P<uint8_t>(flags), t->nrows, idx);
+    auto* o = new_table(s, n);
+    gather_into(o, t, idx, n, false);
+    *out = o;
+    API_END
+}
+
+capsmi_status capsmi_with_columns(capsmi_table* t, int32_t ncols, const capsmi_expr_column* cols, capsmi_table** out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    capsmi_session* s = t->sess;
+    use_device(s);
+    auto* o = new_table(s, t->nrows);
+    o->cols = t->cols;
+    for (int i = 0; i < ncols; ++i) {
+        need(cols[i].name, "column name");
+        Column c;
+        c.name = cols[i].name;
+        c.data = dev_alloc(sizeof(int64_t) * (t->nrows > 0 ? t->nrows : 1), s->stream);
+        c.valid = dev_alloc(t->nrows > 0 ? t->nrows : 1, s->stream);
+        eval_expr(s, t, cols[i].nnodes, cols[i].prog, P<int64_t>(c.data), P<uint8_t>(c.valid), &c.type);
+        const int j = o->find(c.name);
+        if (j >= 0) o->cols[j] = std::move(c);  // replaced in place (SparkTable.scala:82-87)
+        else o->cols.push_back(std::move(c));
+    }
+    *out = o;
+    API_END
+}
+
+capsmi_status capsmi_join(capsmi_table* l, capsmi_table* r, int32_t join_type, int32_t npairs,
+                          const char* const* lcols, const char* const* rcols, capsmi_table** out) {
+    API_BEGIN
+    need(l, "left");
+    need(r, "right");
+    need(out, "out");
+    REQUIRE(l->sess == r->sess, CAPSMI_ERR_ILLEGAL_ARGUMENT, "tables belong to different sessions");
+    REQUIRE(join_type >= CAPSMI_JOIN_INNER && join_type <= CAPSMI_JOIN_CROSS, CAPSMI_ERR_ILLEGAL_ARGUMENT, "join type");
+    REQUIRE(join_type == CAPSMI_JOIN_CROSS || npairs > 0, CAPSMI_ERR_ILLEGAL_ARGUMENT, "equi-join needs key pairs");
+    use_device(l->sess);
+    std::vector<int> lk = names_to_idx(l, join_type == CAPSMI_JOIN_CROSS ? 0 : npairs, lcols);
+    std::vector<int> rk = names_to_idx(r, join_type == CAPSMI_JOIN_CROSS ? 0 : npairs, rcols);
+    *out = join_impl(l, r, join_type, lk, rk);
+    API_END
+}
+
+capsmi_status capsmi_union_all(capsmi_table* a, capsmi_table* b, capsmi_table** out) {
+    API_BEGIN
+    need(a, "left");
+    need(b, "right");
+    need(out, "out");
+    REQUIRE(a->cols.size() == b->cols.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT, "union all: column counts differ");
+    for (size_t i = 0; i < a->cols.size(); ++i)
+        REQUIRE(a->cols[i].type == b->cols[i].type, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                "Equal column data types for union all (differing nullability is OK): " + a->cols[i].name + " vs " +
+                    b->cols[i].name);
+    capsmi_session* s = a->sess;
+    use_device(s);
+    const int64_t n = a->nrows + b->nrows;
+    auto* o = new_table(s, n);
+    for (size_t i = 0; i < a->cols.size(); ++i) {
+        const Column &x = a->cols[i], &y = b->cols[i];
+        Column c;
+        c.name = x.name;  // positional union, left names (Dataset.union)
+        c.type = x.type;
+        c.data = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s->stream);
+        if (a->nrows)
+            HIP_CHECK(hipMemcpyAsync(P<int64_t>(c.data), x.d(), sizeof(int64_t) * a->nrows, hipMemcpyDeviceToDevice, s->stream));
+        if (b->nrows)
+            HIP_CHECK(hipMemcpyAsync(P<int64_t>(c.data) + a->nrows, y.d(), sizeof(int64_t) * b->nrows,
+                                     hipMemcpyDeviceToDevice, s->stream));
+        if (x.valid || y.valid) {
+            c.valid = dev_alloc(n > 0 ? n : 1, s->stream);
+            if (x.valid) { if (a->nrows) HIP_CHECK(hipMemcpyAsync(P<uint8_t>(c.valid), x.v(), a->nrows, hipMemcpyDeviceToDevice, s->stream)); }
+            else fill_u8(P<uint8_t>(c.valid), 1, a->nrows, s->stream);
+            if (y.valid) { if (b->nrows) HIP_CHECK(hipMemcpyAsync(P<uint8_t>(c.valid) + a->nrows, y.v(), b->nrows, hipMemcpyDeviceToDevice, s->stream)); }
+            else fill_u8(P<uint8_t>(c.valid) + a->nrows, 1, b->nrows, s->stream);
+        }
+        o->cols.push_back(std::move(c));
+    }
+    *out = o;
+    API_END
+}
+
+capsmi_status capsmi_order_by(capsmi_table* t, int32_t nkeys, const char* const* cols, const int32_t* descending,
+                              capsmi_table** out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    use_device(t->sess);
+    auto keys = names_to_idx(t, nkeys, cols);
+    std::vector<int> desc(nkeys);
+    for (int i = 0; i < nkeys; ++i) desc[i] = descending ? descending[i] : 0;
+    Buf perm = order_perm(t, keys, desc);
+    auto* o = new_table(t->sess, t->nrows);
+    gather_into(o, t, perm, t->nrows, false);
+    *out = o;
+    API_END
+}
+
+capsmi_status capsmi_skip(capsmi_table* t, int64_t n, capsmi_table** out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    REQUIRE(n >= 0, CAPSMI_ERR_ILLEGAL_ARGUMENT, "negative skip");
+    const int64_t k = std::min(n, t->nrows);
+    auto* o = new_table(t->sess, t->nrows - k);
+    o->cols = t->cols;
+    for (auto& c : o->cols) c.offset += k;
+    *out = o;
+    API_END
+}
+
+capsmi_status capsmi_limit(capsmi_table* t, int64_t n, capsmi_table** out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    REQUIRE(n >= 0 && n <= 2147483647LL, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            "an integer: limit must fit an Int (SparkTable.scala:117)");
+    auto* o = new_table(t->sess, std::min(n, t->nrows));
+    o->cols = t->cols;
+    *out = o;
+    API_END
+}
+
+static capsmi_status distinct_impl(capsmi_table* t, const std::vector<int>& keys, capsmi_table** out) {
+    API_BEGIN
+    capsmi_session* s = t->sess;
+    use_device(s);
+    HashTable ht;
+    Buf sor, gid, rep;
+    hash_build(s, key_cols(t, keys), t->nrows, /*skip_null_keys=*/false, ht, sor);
+    const int64_t ng = hash_group_ids(s, ht, sor, t->nrows, gid, rep);
+    auto* o = new_table(s, ng);
+    gather_into(o, t, rep, ng, false);
+    *out = o;
+    API_END
+}
+
+capsmi_status capsmi_distinct(capsmi_table* t, capsmi_table** out) {
+    if (!t || !out) { set_err("null argument"); return CAPSMI_ERR_ILLEGAL_ARGUMENT; }
+    std::vector<int> keys;
+    for (size_t i = 0; i < t->cols.size(); ++i) keys.push_back((int)i);
+    if (keys.size() > (size_t)kMaxKeys) { set_err("distinct over more than 8 columns"); return CAPSMI_ERR_NOT_IMPLEMENTED; }
+    return distinct_impl(t, keys, out);
+}
+
+capsmi_status capsmi_distinct_on(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    auto keys = names_to_idx(t, ncols, cols);
+    const capsmi_status st = distinct_impl(t, keys, out);
+    if (st != CAPSMI_OK) return st;
+    API_END
+}
+
+capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, int32_t naggs, const capsmi_agg* aggs,
+                           capsmi_table** out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    REQUIRE(naggs == 0 || aggs, CAPSMI_ERR_ILLEGAL_ARGUMENT, "null aggregations");
+    capsmi_session* s = t->sess;
+    hipStream_t st = s->stream;
+    use_device(s);
+    const int64_t n = t->nrows;
+    auto keys = names_to_idx(t, nby, by);
+    Buf gid, rep;
+    int64_t ng;
+    HashTable ht;
+    Buf sor;
+    if (nby > 0) {
+        hash_build(s, key_cols(t, keys), n, /*skip_null_keys=*/false, ht, sor);
+        ng = hash_group_ids(s, ht, sor, n, gid, rep);
+    } else {
+        ng = 1;  // global aggregate: exactly one row, also over empty input (Spark)
+        gid = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), st);
+        fill_i64(P<int64_t>(gid), 0, n, st);
+    }
+    auto* o = new_table(s, ng);
+    std::unique_ptr<capsmi_table> guard(o);
+    if (nby > 0) {
+        capsmi_table keyt;
+        keyt.sess = s;
+        keyt.nrows = n;
+        for (int k : keys) keyt.cols.push_back(t->cols[k]);
+        gather_into(o, &keyt, rep, ng, false);
+    }
+    for (int a = 0; a < naggs; ++a) {
+        const capsmi_agg& ag = aggs[a];
+        need(ag.output, "aggregate output name");
+        Column c;
+        c.name = ag.output;
+        c.data = dev_alloc(sizeof(int64_t) * ng, st);
+        const Column* in = nullptr;
+        if (ag.kind != CAPSMI_AGG_COUNT_STAR) in = &t->cols[col_index(t, ag.input)];
+        switch (ag.kind) {
+            case CAPSMI_AGG_COUNT_STAR:
+                c.type = CAPSMI_I64;
+                HIP_CHECK(hipMemsetAsync(P<void>(c.data), 0, sizeof(int64_t) * ng, st));
+                agg_count(P<int64_t>(gid), nullptr, n, P<int64_t>(c.data), st);
+                break;
+            case CAPSMI_AGG_COUNT: {
+                c.type = CAPSMI_I64;
+                HIP_CHECK(hipMemsetAsync(P<void>(c.data), 0, sizeof(int64_t) * ng, st));
+                if (!ag.distinct) {
+                    agg_count(P<int64_t>(gid), in->v(), n, P<int64_t>(c.data), st);
+                } else {
+                    // countDistinct: distinct (group, value) pairs with a non-null value, counted per group
+                    KeyCols k;
+                    k.n = 2;
+                    for (int i = 0; i < kMaxKeys; ++i) { k.data[i] = nullptr; k.valid[i] = nullptr; }
+                    k.data[0] = P<int64_t>(gid);
+                    k.data[1] = in->d();
+                    k.valid[1] = in->v();
+                    HashTable h2;
+                    Buf sor2, gid2, rep2;
+                    hash_build(s, k, n, /*skip_null_keys=*/true, h2, sor2);
+                    const int64_t np = hash_group_ids(s, h2, sor2, n, gid2, rep2);
+                    Buf pg = dev_alloc(sizeof(int64_t) * (np > 0 ? np : 1), st);
+                    gather_col(P<int64_t>(gid), nullptr, P<int64_t>(rep2), np, P<int64_t>(pg), nullptr, st);
+                    agg_count(P<int64_t>(pg), nullptr, np, P<int64_t>(c.data), st);
+                }
+                break;
+            }
+            case CAPSMI_AGG_SUM: {
+                REQUIRE(in->type == CAPSMI_I64 || in->type == CAPSMI_F64, CAPSMI_ERR_ILLEGAL_ARGUMENT, "sum of non-number");
+                c.type = in->type;
+                c.valid = dev_alloc(ng, st);
+                HIP_CHECK(hipMemsetAsync(P<void>(c.data), 0, sizeof(int64_t) * ng, st));
+                HIP_CHECK(hipMemsetAsync(P<void>(c.valid), 0, ng, st));
+                if (in->type == CAPSMI_I64) agg_sum_i64(P<int64_t>(gid), in->d(), in->v(), n, P<int64_t>(c.data), P<uint8_t>(c.valid), st);
+                else agg_sum_f64(P<int64_t>(gid), in->d(), in->v(), n, P<double>(c.data), P<uint8_t>(c.valid), st);
+                break;
+            }
+            case CAPSMI_AGG_MIN:
+            case CAPSMI_AGG_MAX: {
+                const bool mx = ag.kind == CAPSMI_AGG_MAX;
+                c.type = in->type;
+                c.valid = dev_alloc(ng, st);
+                fill_i64(P<int64_t>(c.data), mx ? INT64_MIN : INT64_MAX, ng, st);
+                HIP_CHECK(hipMemsetAsync(P<void>(c.valid), 0, ng, st));
+                agg_minmax(P<int64_t>(gid), in->d(), in->v(), n, in->type, mx, P<int64_t>(c.data), P<uint8_t>(c.valid), st);
+                minmax_finish(P<int64_t>(c.data), in->type, mx, ng, st);
+                break;
+            }
+            case CAPSMI_AGG_AVG: {
+                REQUIRE(in->type == CAPSMI_I64 || in->type == CAPSMI_F64, CAPSMI_ERR_ILLEGAL_ARGUMENT, "avg of non-number");
+                c.type = CAPSMI_F64;
+                c.valid = dev_alloc(ng, st);
+                Buf sum = dev_alloc(sizeof(double) * ng, st), cnt = dev_alloc(sizeof(int64_t) * ng, st), seen = dev_alloc(ng, st);
+                HIP_CHECK(hipMemsetAsync(P<void>(sum), 0, sizeof(double) * ng, st));
+                HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, sizeof(int64_t) * ng, st));
+                if (in->type == CAPSMI_I64) {
+                    // Spark casts Long input to Double before summing
+                    Buf dv = dev_alloc(sizeof(double) * (n > 0 ? n : 1), st);
+                    i64_to_f64(in->d(), P<int64_t>(dv), n, st);
+                    agg_sum_f64(P<int64_t>(gid), P<int64_t>(dv), in->v(), n, P<double>(sum), P<uint8_t>(seen), st);
+                } else {
+                    agg_sum_f64(P<int64_t>(gid), in->d(), in->v(), n, P<double>(sum), P<uint8_t>(seen), st);
+                }
+                agg_count(P<int64_t>(gid), in->v(), n, P<int64_t>(cnt), st);
+                avg_finish(P<double>(sum), P<int64_t>(cnt), ng, P<int64_t>(c.data), P<uint8_t>(c.valid), st);
+                break;
+            }
+            default:
+                throw Error(CAPSMI_ERR_NOT_IMPLEMENTED, "Aggregation function " + std::to_string(ag.kind));
+        }
+        o->cols.push_back(std::move(c));
+    }
+    *out = guard.release();
+    API_END
+}
+
+// ---- graph fast path ------------------------------------------------------------------------------
+capsmi_status capsmi_bitmap_create(capsmi_session* s, int64_t id_lo, int64_t id_hi, capsmi_bitmap** out) {
+    API_BEGIN
+    need(s, "session");
+    need(out, "out");
+    REQUIRE(id_hi >= id_lo, CAPSMI_ERR_ILLEGAL_ARGUMENT, "bitmap range");
+    REQUIRE(id_hi - id_lo <= (int64_t(1) << 40), CAPSMI_ERR_UNSUPPORTED, "bitmap range above 2^40 ids");
+    use_device(s);
+    auto* b = new capsmi_bitmap();
+    b->sess = s;
+    b->lo = id_lo;
+    b->hi = id_hi;
+    b->nwords = (id_hi - id_lo + 31) / 32;
+    b->words = dev_alloc(sizeof(uint32_t) * (b->nwords > 0 ? b->nwords : 1), s->stream);
+    HIP_CHECK(hipMemsetAsync(P<void>(b->words), 0, sizeof(uint32_t) * (b->nwords > 0 ? b->nwords : 1), s->stream));
+    b->set_bits = 0;
+    b->full = id_hi == id_lo;
+    *out = b;
+    API_END
+}
+
+capsmi_status capsmi_bitmap_add_scan(capsmi_bitmap* b, capsmi_table* nodes, const char* id_col, int32_t nnodes,
+                                     const capsmi_expr* pred) {
+    API_BEGIN
+    need(b, "bitmap");
+    need(nodes, "nodes");
+    capsmi_session* s = b->sess;
+    use_device(s);
+    const Column& idc = nodes->cols[col_index(nodes, id_col)];
+    REQUIRE(idc.type == CAPSMI_I64, CAPSMI_ERR_ILLEGAL_ARGUMENT, "node id column must be Long");
+    Buf flags;
+    if (nnodes > 0) {
+        flags = dev_alloc(nodes->nrows > 0 ? nodes->nrows : 1, s->stream);
+        eval_predicate(s, nodes, nnodes, pred, P<uint8_t>(flags));
+    }
+    Buf cnt = dev_alloc(3 * sizeof(int64_t), s->stream);
+    HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, 3 * sizeof(int64_t), s->stream));
+    bitmap_add_rows(b, idc.d(), idc.v(), P<uint8_t>(flags), nodes->nrows, P<int64_t>(cnt));
+    int64_t h[3];
+    HIP_CHECK(hipMemcpyAsync(h, P<void>(cnt), sizeof(h), hipMemcpyDeviceToHost, s->stream));
+    HIP_CHECK(hipStreamSynchronize(s->stream));
+    REQUIRE(h[2] == 0, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            std::to_string(h[2]) + " node ids are null or outside the bitmap range [" + std::to_string(b->lo) + ", " +
+                std::to_string(b->hi) + ")");
+    b->rows_added += h[0];
+    b->any_dup = b->any_dup || h[1] > 0;
+    b->set_bits = words_popcount(s, P<uint32_t>(b->words), 0, b->nwords);
+    b->full = b->set_bits == b->hi - b->lo;
+    API_END
+}
+
+capsmi_status capsmi_bitmap_stats(capsmi_bitmap* b, int64_t* set_bits, int32_t* unique_rows) {
+    API_BEGIN
+    need(b, "bitmap");
+    if (set_bits) *set_bits = b->set_bits;
+    if (unique_rows) *unique_rows = b->any_dup ? 0 : 1;
+    API_END
+}
+
+capsmi_status capsmi_bitmap_release(capsmi_bitmap* b) {
+    API_BEGIN
+    if (b) {
+        use_device(b->sess);
+        delete b;
+    }
+    API_END
+}
+
+capsmi_status capsmi_expand_filter(capsmi_session* s, capsmi_table* rels, const char* src_col, const char* dst_col,
+                                   const capsmi_bitmap* src_ok, const capsmi_bitmap* dst_ok, int32_t nout,
+                                   const char* const* out_cols, const char* const* out_names, capsmi_table** out) {
+    API_BEGIN
+    need(s, "session");
+    need(rels, "rels");
+    need(out, "out");
+    check_bitmap(src_ok, "src_ok");
+    check_bitmap(dst_ok, "dst_ok");
+    REQUIRE(nout >= 1 && nout <= 4, CAPSMI_ERR_ILLEGAL_ARGUMENT, "expand_filter projects 1..4 columns");
+    REQUIRE(!src_ok->any_dup && !dst_ok->any_dup, CAPSMI_ERR_UNSUPPORTED,
+            "fused expand needs each node id in one scanned row (ScanGraph.scala:72-76); use join");
+    use_device(s);
+    const Column& sc = rel_col(rels, src_col);
+    const Column& dc = rel_col(rels, dst_col);
+    const int64_t m = rels->nrows;
+    auto* o = new_table(s, 0);
+    std::unique_ptr<capsmi_table> guard(o);
+    const int64_t* in_d[4];
+    const uint8_t* in_v[4];
+    int64_t* out_d[4];
+    uint8_t* out_v[4];
+    std::unordered_set<std::string> names;
+    for (int i = 0; i < nout; ++i) {
+        const Column& c = rels->cols[col_index(rels, out_cols[i])];
+        Column oc;
+        oc.name = out_names && out_names[i] ? out_names[i] : c.name;
+        REQUIRE(names.insert(oc.name).second, CAPSMI_ERR_ILLEGAL_ARGUMENT, "duplicate output column " + oc.name);
+        oc.type = c.type;
+        oc.data = dev_alloc(sizeof(int64_t) * (m > 0 ? m : 1), s->stream);
+        if (c.valid) oc.valid = dev_alloc(m > 0 ? m : 1, s->stream);
+        in_d[i] = c.d();
+        in_v[i] = c.v();
+        out_d[i] = P<int64_t>(oc.data);
+        out_v[i] = P<uint8_t>(oc.valid);
+        o->cols.push_back(std::move(oc));
+    }
+    Buf cnt = dev_alloc(8, s->stream);
+    HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, 8, s->stream));
+    graph::expand_filter(s, sc.d(), dc.d(), m, src_ok, dst_ok, nout, in_d, in_v, out_d, out_v, P<int64_t>(cnt));
+    o->nrows = read_scalar(s, P<int64_t>(cnt));
+    *out = guard.release();
+    API_END
+}
+
+static void two_hop_mid(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                        const char* dst_col, const capsmi_bitmap* a, const capsmi_bitmap* b, uint32_t* X1, uint32_t* X2,
+                        uint32_t* S1) {
+    const int64_t nw = b->nwords;
+    HIP_CHECK(hipMemsetAsync(X1, 0, sizeof(uint32_t) * nw, s->stream));
+    HIP_CHECK(hipMemsetAsync(X2, 0, sizeof(uint32_t) * nw, s->stream));
+    HIP_CHECK(hipMemsetAsync(S1, 0, sizeof(uint32_t) * nw, s->stream));
+    for (int i = 0; i < nrels; ++i) {
+        need(rels[i], "rels[i]");
+        const Column& sc = rel_col(rels[i], src_col);
+        const Column& dc = rel_col(rels[i], dst_col);
+        graph::hop1(s, sc.d(), dc.d(), rels[i]->nrows, a, b, X1, S1, X2);
+    }
+    graph::mid_combine(s, X1, X2, S1, nw);
+}
+
+static void two_hop_dst(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                        const char* dst_col, const capsmi_bitmap* b, const capsmi_bitmap* c, const uint32_t* X1,
+                        const uint32_t* X2, uint32_t* C) {
+    HIP_CHECK(hipMemsetAsync(C, 0, sizeof(uint32_t) * c->nwords, s->stream));
+    for (int i = 0; i < nrels; ++i) {
+        const Column& sc = rel_col(rels[i], src_col);
+        const Column& dc = rel_col(rels[i], dst_col);
+        graph::hop2(s, sc.d(), dc.d(), rels[i]->nrows, c, X1, X2, b->lo, b->hi, C);
+    }
+}
+
+capsmi_status capsmi_two_hop_count_distinct(capsmi_session* s, int32_t nrels, capsmi_table* const* rels,
+                                            const char* src_col, const char* dst_col, const capsmi_bitmap* a_ok,
+                                            const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok, int64_t* out_distinct) {
+    API_BEGIN
+    need(s, "session");
+    need(out_distinct, "out");
+    REQUIRE(nrels >= 0 && (nrels == 0 || rels), CAPSMI_ERR_ILLEGAL_ARGUMENT, "rels");
+    check_bitmap(a_ok, "a_ok");
+    check_bitmap(b_ok, "b_ok");
+    check_bitmap(c_ok, "c_ok");
+    use_device(s);
+    const int64_t nw = b_ok->nwords > 0 ? b_ok->nwords : 1;
+    Buf x = dev_alloc(sizeof(uint32_t) * nw * 3, s->stream);
+    Buf cw = dev_alloc(sizeof(uint32_t) * (c_ok->nwords > 0 ? c_ok->nwords : 1), s->stream);
+    uint32_t* X1 = P<uint32_t>(x);
+    two_hop_mid(s, nrels, rels, src_col, dst_col, a_ok, b_ok, X1, X1 + nw, X1 + 2 * nw);
+    two_hop_dst(s, nrels, rels, src_col, dst_col, b_ok, c_ok, X1, X1 + nw, P<uint32_t>(cw));
+    *out_distinct = words_popcount(s, P<uint32_t>(cw), 0, c_ok->nwords);
+    API_END
+}
+
+capsmi_status capsmi_two_hop_mark_mid(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                                      const char* dst_col, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok,
+                                      uint32_t* mid_words, uint32_t* scratch_words) {
+    API_BEGIN
+    need(s, "session");
+    need(mid_words, "mid_words");
+    need(scratch_words, "scratch_words");
+    check_bitmap(a_ok, "a_ok");
+    check_bitmap(b_ok, "b_ok");
+    use_device(s);
+    two_hop_mid(s, nrels, rels, src_col, dst_col, a_ok, b_ok, mid_words, mid_words + b_ok->nwords, scratch_words);
+    API_END
+}
+
+capsmi_status capsmi_two_hop_mark_dst(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                                      const char* dst_col, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok,
+                                      const uint32_t* mid_words, uint32_t* dst_words) {
+    API_BEGIN
+    need(s, "session");
+    need(mid_words, "mid_words");
+    need(dst_words, "dst_words");
+    check_bitmap(b_ok, "b_ok");
+    check_bitmap(c_ok, "c_ok");
+    use_device(s);
+    two_hop_dst(s, nrels, rels, src_col, dst_col, b_ok, c_ok, mid_words, mid_words + b_ok->nwords, dst_words);
+    API_END
+}
+
+capsmi_status capsmi_words_popcount(capsmi_session* s, const uint32_t* words, int64_t w_begin, int64_t w_end,
+                                    int64_t* out) {
+    API_BEGIN
+    need(s, "session");
+    need(words, "words");
+    need(out, "out");
+    use_device(s);
+    *out = words_popcount(s, words, w_begin, w_end);
+    API_END
+}
+
+capsmi_status capsmi_two_hop_count(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                                   const char* dst_col, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok,
+                                   const capsmi_bitmap* c_ok, int64_t* out_rows) {
+    API_BEGIN
+    need(s, "session");
+    need(out_rows, "out");
+    check_bitmap(a_ok, "a_ok");
+    check_bitmap(b_ok, "b_ok");
+    check_bitmap(c_ok, "c_ok");
+    REQUIRE(!a_ok->any_dup && !b_ok->any_dup && !c_ok->any_dup, CAPSMI_ERR_UNSUPPORTED,
+            "closed-form count(*) needs each node id in one scanned row");
+    use_device(s);
+    const int64_t n = b_ok->hi - b_ok->lo;
+    Buf inA = dev_alloc(sizeof(uint32_t) * (n > 0 ? n : 1), s->stream);
+    Buf outC = dev_alloc(sizeof(uint32_t) * (n > 0 ? n : 1), s->stream);
+    Buf acc = dev_alloc(16, s->stream);  // [0] = loops, [1] = sum of products
+    HIP_CHECK(hipMemsetAsync(P<void>(inA), 0, sizeof(uint32_t) * (n > 0 ? n : 1), s->stream));
+    HIP_CHECK(hipMemsetAsync(P<void>(outC), 0, sizeof(uint32_t) * (n > 0 ? n : 1), s->stream));
+    HIP_CHECK(hipMemsetAsync(P<void>(acc), 0, 16, s->stream));
+    for (int i = 0; i < nrels; ++i) {
+        const Column& sc = rel_col(rels[i], src_col);
+        const Column& dc = rel_col(rels[i], dst_col);
+        graph::degrees(s, sc.d(), dc.d(), rels[i]->nrows, a_ok, b_ok, c_ok, P<uint32_t>(inA), P<uint32_t>(outC),
+                       P<int64_t>(acc));
+    }
+    graph::deg_product(s, P<uint32_t>(inA), P<uint32_t>(outC), n, b_ok, P<int64_t>(acc) + 1);
+    int64_t h[2];
+    HIP_CHECK(hipMemcpyAsync(h, P<void>(acc), 16, hipMemcpyDeviceToHost, s->stream));
+    HIP_CHECK(hipStreamSynchronize(s->stream));
+    *out_rows = h[1] - h[0];
+    API_END
+}
+
+capsmi_status capsmi_cluster_by(capsmi_table* rels, const char* key_col, int64_t id_lo, int64_t id_hi,
+                                capsmi_table** out) {
+    API_BEGIN
+    need(rels, "rels");
+    need(out, "out");
+    capsmi_session* s = rels->sess;
+    use_device(s);
+    const Column& kc = rel_col(rels, key_col);
+    const int64_t n = rels->nrows;
+    // keys relative to id_lo; range checked on the host copy of min/max is avoided: ids outside
+    // [lo, hi) would break the bit budget, so the sort covers all 64 bits when the range is unknown
+    int bits = 1;
+    while (bits < 64 && (int64_t(1) << bits) < (id_hi - id_lo)) ++bits;
+    Buf keys = dev_alloc(sizeof(uint64_t) * (n > 0 ? n : 1), s->stream);
+    Buf perm = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s->stream);
+    HIP_CHECK(hipMemcpyAsync(P<void>(keys), kc.d(), sizeof(int64_t) * n, hipMemcpyDeviceToDevice, s->stream));
+    iota_i64(P<int64_t>(perm), 0, n, s->stream);
+    // validate range on device via a bitmap scan of the key column
+    {
+        capsmi_bitmap tmp;
+        tmp.sess = s;
+        tmp.lo = id_lo;
+        tmp.hi = id_hi;
+        tmp.nwords = (id_hi - id_lo + 31) / 32;
+        tmp.words = dev_alloc(sizeof(uint32_t) * (tmp.nwords > 0 ? tmp.nwords : 1), s->stream);
+        HIP_CHECK(hipMemsetAsync(P<void>(tmp.words), 0, sizeof(uint32_t) * (tmp.nwords > 0 ? tmp.nwords : 1), s->stream));
+        Buf cnt = dev_alloc(24, s->stream);
+        HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, 24, s->stream));
+        bitmap_add_rows(&tmp, kc.d(), nullptr, nullptr, n, P<int64_t>(cnt));
+        int64_t h[3];
+        HIP_CHECK(hipMemcpyAsync(h, P<void>(cnt), 24, hipMemcpyDeviceToHost, s->stream));
+        HIP_CHECK(hipStreamSynchronize(s->stream));
+        REQUIRE(h[2] == 0, CAPSMI_ERR_ILLEGAL_ARGUMENT, "cluster_by: key outside [id_lo, id_hi)");
+    }
+    if (id_lo != 0) {
+        // shift keys: reuse the expression-free path through a host round trip is too slow; fold lo into the
+        // sort by sorting raw keys (order is the same for keys in [lo, hi)) over enough bits
+        bits = 64;
+    }
+    radix_sort_pairs(s, P<uint64_t>(keys), P<int64_t>(perm), n, 0, (bits + 7) / 8 * 8);
+    auto* o = new_table(s, n);
+    gather_into(o, rels, perm, n, false);
+    *out = o;
+    API_END
+}
+
+capsmi_status capsmi_owner_words(int64_t nbits, int32_t part, int32_t nparts, int64_t* w_begin, int64_t* w_end) {
+    API_BEGIN
+    REQUIRE(nparts >= 1 && part >= 0 && part < nparts && nbits >= 0, CAPSMI_ERR_ILLEGAL_ARGUMENT, "owner_words");
+    need(w_begin, "w_begin");
+    need(w_end, "w_end");
+    const int64_t nw = (nbits + 31) / 32;
+    *w_begin = (int64_t)part * nw / nparts;
+    *w_end = (int64_t)(part + 1) * nw / nparts;
+    API_END
+}
+
+capsmi_status capsmi_rmat_rels(capsmi_session* s, int32_t scale, int64_t e_begin, int64_t e_end, int32_t pa, int32_t pb,
+                               int32_t pc, uint64_t seed, int32_t part_col, int32_t part, int32_t nparts,
+                               capsmi_table** out) {
+    API_BEGIN
+    need(s, "session");
+    need(out, "out");
+    REQUIRE(scale >= 1 && scale <= 40, CAPSMI_ERR_ILLEGAL_ARGUMENT, "R-MAT scale must be in 1..40");
+    REQUIRE(e_begin >= 0 && e_end >= e_begin && e_end < (int64_t(1) << 35), CAPSMI_ERR_ILLEGAL_ARGUMENT, "edge range");
+    REQUIRE(seed < (1ULL << 24), CAPSMI_ERR_ILLEGAL_ARGUMENT, "seed must be < 2^24");
+    REQUIRE(pa >= 0 && pb >= 0 && pc >= 0 && pa + pb + pc <= 100, CAPSMI_ERR_ILLEGAL_ARGUMENT, "R-MAT probabilities");
+    REQUIRE(nparts >= 1 && part >= 0 && part < nparts, CAPSMI_ERR_ILLEGAL_ARGUMENT, "partition");
+    use_device(s);
+    Buf id, so, d;
+    const int64_t m = graph::rmat(s, scale, e_begin, e_end, pa, pb, pc, seed, part_col, part, nparts, id, so, d);
+    auto* o = new_table(s, m);
+    const char* names[3] = {"id", "source", "target"};
+    Buf bufs[3] = {id, so, d};
+    for (int i = 0; i < 3; ++i) {
+        Column c;
+        c.name = names[i];
+        c.type = CAPSMI_I64;
+        c.data = bufs[i];
+        o->cols.push_back(std::move(c));
+    }
+    *out = o;
+    API_END
+}
+
+capsmi_status capsmi_rmat_nodes(capsmi_session* s, int32_t scale, int32_t kind, uint64_t seed, capsmi_table** out) {
+    API_BEGIN
+    need(s, "session");
+    need(out, "out");
+    REQUIRE(scale >= 1 && scale <= 40, CAPSMI_ERR_ILLEGAL_ARGUMENT, "scale");
+    REQUIRE(kind >= 0 && kind <= 2, CAPSMI_ERR_ILLEGAL_ARGUMENT, "kind");
+    use_device(s);
+    const int64_t n = int64_t(1) << scale;
+    Buf ids;
+    int64_t rows = n;
+    if (kind == 0) {
+        ids = dev_alloc(sizeof(int64_t) * n, s->stream);
+        iota_i64(P<int64_t>(ids), 0, n, s->stream);
+    } else {
+        Buf f = dev_alloc(n, s->stream);
+        graph::person_flags(s, n, kind == 1, P<uint8_t>(f));
+        rows = flags_to_indices(s, P<uint8_t>(f), n, ids);  // id == row index of the full range
+    }
+    auto* o = new_table(s, rows);
+    Column c;
+    c.name = "id";
+    c.type = CAPSMI_I64;
+    c.data = ids;
+    o->cols.push_back(c);
+    if (kind == 1) {
+        Column a;
+        a.name = "age";
+        a.type = CAPSMI_I64;
+        a.data = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), s->stream);
+        graph::ages(s, P<int64_t>(ids), rows, seed, P<int64_t>(a.data));
+        o->cols.push_back(std::move(a));
+    }
+    *out = o;
+    API_END
+}
+
+capsmi_status capsmi_table_fingerprint(capsmi_table* t, int32_t ncols, const char* const* cols, int64_t* count,
+                                       uint64_t* sum, uint64_t* xr) {
+    API_BEGIN
+    need(t, "table");
+    use_device(t->sess);
+    auto idx = names_to_idx(t, ncols, cols);
+    std::vector<const int64_t*> d;
+    std::vector<const uint8_t*> v;
+    for (int i : idx) {
+        d.push_back(t->cols[i].d());
+        v.push_back(t->cols[i].v());
+    }
+    uint64_t hs = 0, hx = 0;
+    graph::fingerprint(t->sess, ncols, d.data(), v.data(), t->nrows, &hs, &hx);
+    if (count) *count = t->nrows;
+    if (sum) *sum = hs;
+    if (xr) *xr = hx;
+    API_END
+}
+
+}  // extern "C"

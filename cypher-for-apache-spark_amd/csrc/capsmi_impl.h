@@ -1,0 +1,205 @@
+// capsmi_impl.h -- internal runtime of libcapsmi (not part of the ABI).
+//
+// Device tables are column-major: one 8-byte word per row and column, plus an
+// optional byte-per-row validity map.  Columns share ref-counted device buffers,
+// so select/drop/rename/skip/limit are metadata-only (the Spark analogue is a
+// Catalyst projection, SparkTable.scala:61-92).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/capsmi.h"
+
+namespace capsmi {
+
+// ---- errors ---------------------------------------------------------------------
+struct Error : std::runtime_error {
+    capsmi_status code;
+    Error(capsmi_status c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+[[noreturn]] void throw_hip(hipError_t e, const char* what, const char* file, int line);
+#define HIP_CHECK(x)                                                     \
+    do {                                                                 \
+        hipError_t e__ = (x);                                            \
+        if (e__ != hipSuccess) ::capsmi::throw_hip(e__, #x, __FILE__, __LINE__); \
+    } while (0)
+#define REQUIRE(cond, code, msg)                      \
+    do {                                              \
+        if (!(cond)) throw ::capsmi::Error((code), (msg)); \
+    } while (0)
+
+// ---- device memory --------------------------------------------------------------
+// Stream-ordered allocations from the device's default pool (release threshold
+// raised at session create, so freed blocks are recycled instead of unmapped).
+struct DevBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    hipStream_t stream = nullptr;
+    ~DevBuf();
+};
+using Buf = std::shared_ptr<DevBuf>;
+Buf dev_alloc(size_t bytes, hipStream_t stream);
+
+template <class T>
+inline T* P(const Buf& b) { return b ? static_cast<T*>(b->ptr) : nullptr; }
+
+struct Column {
+    std::string name;
+    int32_t type = CAPSMI_I64;
+    Buf data;              // int64 words
+    Buf valid;             // uint8 per row, may be null (no nulls)
+    int64_t offset = 0;    // row offset into data/valid (zero-copy skip)
+    const int64_t* d() const { return P<int64_t>(data) + offset; }
+    const uint8_t* v() const { return valid ? P<uint8_t>(valid) + offset : nullptr; }
+};
+
+}  // namespace capsmi
+
+struct capsmi_session {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;  // current (own or external)
+    int num_cus = 256;
+    // small pinned staging buffer for scalar read-backs
+    int64_t* pinned = nullptr;
+    // per-kernel event timing (capsmi_session_set_profiling)
+    bool prof = false;
+    struct Pending {
+        std::string name;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    std::map<std::string, std::pair<int64_t, double>> totals;
+};
+
+namespace capsmi {
+// brackets one kernel launch with events on the session stream when profiling is on
+struct KernelTimer {
+    capsmi_session* s;
+    const char* name;
+    hipEvent_t a = nullptr, b = nullptr;
+    KernelTimer(capsmi_session* s_, const char* n) : s(s_), name(n) {
+        if (s->prof && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
+            (void)hipEventRecord(a, s->stream);
+    }
+    ~KernelTimer() {
+        if (a && b) {
+            (void)hipEventRecord(b, s->stream);
+            s->pending.push_back({name, a, b});
+        }
+    }
+};
+}  // namespace capsmi
+
+struct capsmi_table {
+    std::atomic<int> refs{1};
+    capsmi_session* sess = nullptr;
+    int64_t nrows = 0;
+    std::vector<capsmi::Column> cols;
+    int find(const std::string& n) const {
+        for (size_t i = 0; i < cols.size(); ++i)
+            if (cols[i].name == n) return (int)i;
+        return -1;
+    }
+};
+
+struct capsmi_bitmap {
+    capsmi_session* sess = nullptr;
+    int64_t lo = 0, hi = 0;  // id range
+    int64_t nwords = 0;      // ceil((hi - lo) / 32)
+    capsmi::Buf words;       // uint32 per 32 ids
+    int64_t rows_added = 0;  // rows that set a bit (duplicate detection)
+    bool any_dup = false;
+    int64_t set_bits = -1;   // cached popcount (-1 = stale)
+    bool full = false;       // every id in [lo, hi) is set
+};
+
+namespace capsmi {
+
+// ---- kernel launchers (k_*.hip) ------------------------------------------------
+// scan / compaction / gather (k_basic.hip)
+void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t st);  // out has n+1 entries
+void fill_i64(int64_t* p, int64_t v, int64_t n, hipStream_t st);
+void fill_u8(uint8_t* p, uint8_t v, int64_t n, hipStream_t st);
+void iota_i64(int64_t* p, int64_t start, int64_t n, hipStream_t st);
+// indices i (ascending) with flags[i] != 0; returns count (synchronises)
+int64_t flags_to_indices(capsmi_session* s, const uint8_t* flags, int64_t n, Buf& out_idx);
+// dst[i] = idx[i] < 0 ? null : src[idx[i]]; dst_valid written iff non-null
+void gather_col(const int64_t* src, const uint8_t* src_valid, const int64_t* idx, int64_t n,
+                int64_t* dst, uint8_t* dst_valid, hipStream_t st);
+int64_t read_scalar(capsmi_session* s, const int64_t* dev);
+void invert_u8(const uint8_t* a, uint8_t* b, int64_t n, hipStream_t st);
+void i64_to_f64(const int64_t* a, int64_t* b, int64_t n, hipStream_t st);
+
+// hashing & grouping (k_hash.hip)
+constexpr int kMaxKeys = 8;
+struct KeyCols {
+    const int64_t* data[kMaxKeys];
+    const uint8_t* valid[kMaxKeys];
+    int32_t n;
+};
+struct HashTable {
+    Buf slot_row;    // int64, -1 = empty; representative row
+    Buf slot_count;  // int64 rows per slot
+    int64_t cap = 0; // power of two
+};
+// Insert rows (skipping rows with a null key when skip_null_keys) into a fresh table.
+// slot_of_row[i] = slot id or -1.  count=true maintains slot_count.
+void hash_build(capsmi_session* s, const KeyCols& k, int64_t n, bool skip_null_keys, HashTable& ht,
+                Buf& slot_of_row);
+// For each probe row, the slot holding an equal key of the build side, or -1 (null keys never match).
+void hash_probe(capsmi_session* s, const KeyCols& probe, const KeyCols& build, int64_t n,
+                const HashTable& ht, Buf& slot_of_probe);
+// group ids: dense numbering of occupied slots; gid_of_row[i] (-1 for skipped rows); returns #groups
+int64_t hash_group_ids(capsmi_session* s, const HashTable& ht, const Buf& slot_of_row, int64_t n,
+                       Buf& gid_of_row, Buf& rep_row_of_gid);
+// join: rows of the build side grouped by slot: offsets[cap+1], rows[nbuild]
+void hash_group_rows(capsmi_session* s, const HashTable& ht, const Buf& slot_of_row, int64_t n,
+                     Buf& offsets, Buf& rows);
+// load-balanced expansion: for each probe row p with cnt(p) matches emit (p, k) pairs.
+//   cnt(p) = slot>=0 ? count[slot] : (outer ? 1 : 0); pairs written to out_l/out_r (r = -1 for outer pad).
+int64_t join_expand(capsmi_session* s, const Buf& slot_of_probe, int64_t nprobe, const HashTable& ht,
+                    const Buf& offsets, const Buf& rows, bool left_outer, Buf& out_l, Buf& out_r,
+                    Buf* matched_build, int64_t nbuild);
+// aggregates (per gid)
+void agg_count(const int64_t* gid, const uint8_t* valid, int64_t n, int64_t* out, hipStream_t st);
+void agg_sum_i64(const int64_t* gid, const int64_t* v, const uint8_t* valid, int64_t n, int64_t* sum,
+                 uint8_t* seen, hipStream_t st);
+void agg_sum_f64(const int64_t* gid, const int64_t* v, const uint8_t* valid, int64_t n, double* sum,
+                 uint8_t* seen, hipStream_t st);
+void agg_minmax(const int64_t* gid, const int64_t* v, const uint8_t* valid, int64_t n, int type, bool is_max,
+                int64_t* out, uint8_t* seen, hipStream_t st);
+void avg_finish(const double* sum, const int64_t* cnt, int64_t ng, int64_t* out, uint8_t* valid,
+                hipStream_t st);
+void minmax_finish(int64_t* v, int type, bool is_max, int64_t ng, hipStream_t st);
+void cross_pairs(int64_t nl, int64_t nr, int64_t* out_l, int64_t* out_r, hipStream_t st);
+
+// expressions (k_expr.hip)
+struct ExprArgs;
+void eval_expr(capsmi_session* s, const capsmi_table* t, int32_t nnodes, const capsmi_expr* prog,
+               int64_t* out, uint8_t* out_valid, int32_t* out_type);
+// filter flags: 1 where the predicate is TRUE
+void eval_predicate(capsmi_session* s, const capsmi_table* t, int32_t nnodes, const capsmi_expr* prog,
+                    uint8_t* flags);
+
+// sort (k_sort.hip): stable ascending permutation of row indices by a 64-bit key
+void radix_sort_pairs(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, int begin_bit,
+                      int end_bit);
+void order_keys(capsmi_session* s, const int64_t* col, const uint8_t* valid, int type, bool desc, bool null_pass,
+                const int64_t* perm, int64_t n, uint64_t* key);
+
+// graph (k_graph.hip)
+void bitmap_add_rows(capsmi_bitmap* b, const int64_t* ids, const uint8_t* ids_valid,
+                     const uint8_t* flags, int64_t n, int64_t* dev_counters);
+int64_t words_popcount(capsmi_session* s, const uint32_t* w, int64_t w_begin, int64_t w_end);
+
+}  // namespace capsmi

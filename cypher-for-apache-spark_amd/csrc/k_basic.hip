@@ -1,0 +1,246 @@
+// k_basic.hip -- scan, stream compaction, gather: the building blocks every
+// Table operator uses (filter = predicate + compaction + gather; join/group =
+// hash + scan + gather).  Wave64 throughout: __ballot is 64-bit and the
+// per-wave scans run over 64 lanes.
+#include "capsmi_impl.h"
+
+namespace capsmi {
+
+namespace {
+
+constexpr int kBlock = 256;           // 4 waves
+constexpr int kItems = 8;             // items per thread in tiled kernels
+constexpr int kTile = kBlock * kItems;  // 2048 rows per tile
+
+__device__ __forceinline__ int64_t wave_incl_scan(int64_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+
+// exclusive block scan of one value per thread; returns prefix, writes block total
+__device__ __forceinline__ int64_t block_excl_scan(int64_t x, int64_t* lds4, int64_t* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int64_t inc = wave_incl_scan(x);
+    if (lane == 63) lds4[wid] = inc;
+    __syncthreads();
+    int64_t base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        const int64_t v = lds4[w];
+        if (w < wid) base += v;
+        tot += v;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + inc - x;
+}
+
+__global__ void __launch_bounds__(kBlock) k_tile_sum(const int64_t* __restrict__ in, int64_t n,
+                                                     int64_t* __restrict__ sums) {
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+    int64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+        const int64_t i = base + j * kBlock + threadIdx.x;
+        if (i < n) s += in[i];
+    }
+    __shared__ int64_t lds[kBlock / 64];
+    int64_t tot;
+    block_excl_scan(s, lds, &tot);
+    if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// blocked per-thread scan via an LDS transpose (coalesced global loads)
+__global__ void __launch_bounds__(kBlock) k_tile_scan(const int64_t* __restrict__ in, int64_t n,
+                                                      const int64_t* __restrict__ tile_off,
+                                                      int64_t* __restrict__ out) {
+    __shared__ int64_t tile[kTile];
+    __shared__ int64_t lds[kBlock / 64];
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+        const int64_t i = base + j * kBlock + threadIdx.x;
+        tile[j * kBlock + threadIdx.x] = i < n ? in[i] : 0;
+    }
+    __syncthreads();
+    int64_t v[kItems];
+    int64_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+        v[j] = tile[threadIdx.x * kItems + j];
+        s += v[j];
+    }
+    int64_t tot;
+    int64_t pre = block_excl_scan(s, lds, &tot) + tile_off[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+        tile[threadIdx.x * kItems + j] = pre;
+        pre += v[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+        const int64_t i = base + j * kBlock + threadIdx.x;
+        if (i < n) out[i] = tile[j * kBlock + threadIdx.x];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kBlock - 1) out[n] = tile_off[blockIdx.x] + tot;
+}
+
+__global__ void k_fill_i64(int64_t* p, int64_t v, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = v;
+}
+__global__ void k_fill_u8(uint8_t* p, uint8_t v, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = v;
+}
+__global__ void k_iota_i64(int64_t* p, int64_t start, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        p[i] = start + i;
+}
+
+// per-tile count of set flags (blocked: thread t owns rows [t*8, t*8+8) of the tile)
+__global__ void __launch_bounds__(kBlock) k_flag_count(const uint8_t* __restrict__ f, int64_t n,
+                                                       int64_t* __restrict__ cnt) {
+    const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kItems;
+    int64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) c += (base + j < n && f[base + j]) ? 1 : 0;
+    __shared__ int64_t lds[kBlock / 64];
+    int64_t tot;
+    block_excl_scan(c, lds, &tot);
+    if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
+}
+
+__global__ void __launch_bounds__(kBlock) k_flag_write(const uint8_t* __restrict__ f, int64_t n,
+                                                       const int64_t* __restrict__ off,
+                                                       int64_t* __restrict__ idx) {
+    const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kItems;
+    uint8_t fl[kItems];
+    int64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+        fl[j] = (base + j < n && f[base + j]) ? 1 : 0;
+        c += fl[j];
+    }
+    __shared__ int64_t lds[kBlock / 64];
+    int64_t tot;
+    int64_t pos = block_excl_scan(c, lds, &tot) + off[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < kItems; ++j)
+        if (fl[j]) idx[pos++] = base + j;
+}
+
+__global__ void k_gather(const int64_t* __restrict__ src, const uint8_t* __restrict__ sv,
+                         const int64_t* __restrict__ idx, int64_t n, int64_t* __restrict__ dst,
+                         uint8_t* __restrict__ dv) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = idx[i];
+        const bool ok = j >= 0 && (sv == nullptr || sv[j]);
+        dst[i] = ok ? src[j] : 0;
+        if (dv) dv[i] = ok ? 1 : 0;
+    }
+}
+
+inline int grid_for(int64_t n, int block = 256) {
+    int64_t g = (n + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > 8192) g = 8192;
+    return (int)g;
+}
+
+}  // namespace
+
+void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t st) {
+    const int64_t ntiles = (n + kTile - 1) / kTile;
+    if (n == 0) {
+        HIP_CHECK(hipMemsetAsync(out, 0, sizeof(int64_t), st));
+        return;
+    }
+    Buf sums = dev_alloc(sizeof(int64_t) * ntiles, st);
+    Buf offs = dev_alloc(sizeof(int64_t) * (ntiles + 1), st);
+    hipLaunchKernelGGL(k_tile_sum, dim3((unsigned)ntiles), dim3(kBlock), 0, st, in, n, P<int64_t>(sums));
+    if (ntiles == 1) {
+        HIP_CHECK(hipMemsetAsync(P<int64_t>(offs), 0, sizeof(int64_t), st));
+    } else {
+        exclusive_scan_i64(P<int64_t>(sums), P<int64_t>(offs), ntiles, st);
+    }
+    hipLaunchKernelGGL(k_tile_scan, dim3((unsigned)ntiles), dim3(kBlock), 0, st, in, n, P<int64_t>(offs), out);
+    HIP_CHECK(hipGetLastError());
+}
+
+void fill_i64(int64_t* p, int64_t v, int64_t n, hipStream_t st) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_fill_i64, dim3(grid_for(n)), dim3(256), 0, st, p, v, n);
+}
+void fill_u8(uint8_t* p, uint8_t v, int64_t n, hipStream_t st) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_fill_u8, dim3(grid_for(n)), dim3(256), 0, st, p, v, n);
+}
+void iota_i64(int64_t* p, int64_t start, int64_t n, hipStream_t st) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_iota_i64, dim3(grid_for(n)), dim3(256), 0, st, p, start, n);
+}
+
+int64_t read_scalar(capsmi_session* s, const int64_t* dev) {
+    HIP_CHECK(hipMemcpyAsync(s->pinned, dev, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream));
+    HIP_CHECK(hipStreamSynchronize(s->stream));
+    return s->pinned[0];
+}
+
+int64_t flags_to_indices(capsmi_session* s, const uint8_t* flags, int64_t n, Buf& out_idx) {
+    hipStream_t st = s->stream;
+    if (n == 0) {
+        out_idx = dev_alloc(8, st);
+        return 0;
+    }
+    const int64_t ntiles = (n + kTile - 1) / kTile;
+    Buf cnt = dev_alloc(sizeof(int64_t) * ntiles, st);
+    Buf off = dev_alloc(sizeof(int64_t) * (ntiles + 1), st);
+    hipLaunchKernelGGL(k_flag_count, dim3((unsigned)ntiles), dim3(kBlock), 0, st, flags, n, P<int64_t>(cnt));
+    exclusive_scan_i64(P<int64_t>(cnt), P<int64_t>(off), ntiles, st);
+    const int64_t total = read_scalar(s, P<int64_t>(off) + ntiles);
+    out_idx = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), st);
+    hipLaunchKernelGGL(k_flag_write, dim3((unsigned)ntiles), dim3(kBlock), 0, st, flags, n, P<int64_t>(off),
+                       P<int64_t>(out_idx));
+    HIP_CHECK(hipGetLastError());
+    return total;
+}
+
+void gather_col(const int64_t* src, const uint8_t* src_valid, const int64_t* idx, int64_t n, int64_t* dst,
+                uint8_t* dst_valid, hipStream_t st) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(n)), dim3(256), 0, st, src, src_valid, idx, n, dst, dst_valid);
+    HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace capsmi
+
+namespace capsmi {
+namespace {
+__global__ void k_invert_u8(const uint8_t* __restrict__ a, uint8_t* __restrict__ b, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        b[i] = a[i] ? 0 : 1;
+}
+__global__ void k_i64_to_f64(const int64_t* __restrict__ a, int64_t* __restrict__ b, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        b[i] = __double_as_longlong((double)a[i]);
+}
+}  // namespace
+
+void invert_u8(const uint8_t* a, uint8_t* b, int64_t n, hipStream_t st) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_invert_u8, dim3(grid_for(n)), dim3(256), 0, st, a, b, n);
+    HIP_CHECK(hipGetLastError());
+}
+void i64_to_f64(const int64_t* a, int64_t* b, int64_t n, hipStream_t st) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_i64_to_f64, dim3(grid_for(n)), dim3(256), 0, st, a, b, n);
+    HIP_CHECK(hipGetLastError());
+}
+}  // namespace capsmi

@@ -1,0 +1,554 @@
+// k_graph.hip -- fused pattern kernels over relationship tables (the hot path).
+//
+// CAPS lowers `(a)-[r]->(b)` to `a ⋈[a.id = r.source] rels ⋈[r.target = b.id] b`
+// (RelationalPlanner.scala:113-124).  When both node scans are base node tables with
+// dense Long ids, each node scan + label/property filter collapses to one bit per id,
+// and each join against it is a bit test.  The relationship table is then streamed
+// once per hop -- the HBM-bound part -- and no binding is ever materialised.
+//
+// Layout in HBM: a relationship table is three int64 columns (id, source, target),
+// 8 B per value, coalesced 16 B per lane per load.  Node predicates are uint32 word
+// bitmaps over [lo, hi): 2^26 ids -> 8 MiB, resident in the Infinity Cache.
+#include "capsmi_impl.h"
+
+namespace capsmi {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+namespace {
+
+// id-domain predicate view passed to kernels
+struct BitView {
+    const uint32_t* w;
+    int64_t lo, hi;
+    int full;  // every id in [lo, hi) set: only a range test is needed
+};
+
+__device__ __forceinline__ bool bit_ok(const BitView& b, int64_t id) {
+    if (id < b.lo || id >= b.hi) return false;
+    if (b.full) return true;
+    const uint64_t x = (uint64_t)(id - b.lo);
+    return (b.w[x >> 5] >> (x & 31)) & 1u;
+}
+
+// Set bit `x` (relative id) in `w` for every active lane, combining lanes that hit the same
+// word first (segmented OR over the wave; clustered inputs put runs of equal words in
+// adjacent lanes), then one check-before-atomicOr per distinct word run.  A plain read that
+// misses a bit set on another XCD only costs a redundant atomic: bits are only ever set.
+__device__ __forceinline__ void wave_set_bit(uint32_t* w, int64_t x, bool act) {
+    const int lane = threadIdx.x & 63;
+    int64_t word = act ? (x >> 5) : -1;
+    uint32_t m = act ? (1u << (x & 31)) : 0u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t wo = __shfl_down(word, o, 64);
+        const uint32_t mo = __shfl_down(m, o, 64);
+        if (lane + o < 64 && wo == word) m |= mo;
+    }
+    const int64_t prev = __shfl_up(word, 1, 64);
+    const bool head = act && (lane == 0 || prev != word);
+    if (head) {
+        const uint32_t cur = w[word];
+        if ((cur & m) != m) atomicOr(&w[word], m);
+    }
+}
+
+// ---- node-scan bitmaps ----------------------------------------------------------
+__global__ void k_bitmap_add(uint32_t* w, int64_t lo, int64_t hi, const int64_t* __restrict__ ids,
+                             const uint8_t* __restrict__ ids_valid, const uint8_t* __restrict__ flags, int64_t n,
+                             unsigned long long* counters /* [0]=rows added, [1]=duplicates, [2]=out of range */) {
+    unsigned long long added = 0, dups = 0, bad = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (flags && !flags[i]) continue;
+        if (ids_valid && !ids_valid[i]) { ++bad; continue; }
+        const int64_t id = ids[i];
+        if (id < lo || id >= hi) { ++bad; continue; }
+        const uint64_t x = (uint64_t)(id - lo);
+        const uint32_t bit = 1u << (x & 31);
+        const uint32_t old = atomicOr(&w[x >> 5], bit);
+        ++added;
+        if (old & bit) ++dups;
+    }
+    if (added) atomicAdd(&counters[0], added);
+    if (dups) atomicAdd(&counters[1], dups);
+    if (bad) atomicAdd(&counters[2], bad);
+}
+
+__global__ void k_popcount(const uint32_t* __restrict__ w, int64_t b, int64_t e, unsigned long long* out) {
+    unsigned long long c = 0;
+    for (int64_t i = b + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < e; i += (int64_t)gridDim.x * blockDim.x)
+        c += __popc(w[i]);
+    // wave reduce, one atomic per wave
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+
+// ---- C2: 1-hop expand with fused node filters --------------------------------------
+// Output rows are reserved per block with one atomic (row order across blocks is
+// unspecified: results are multisets, as Spark's).
+constexpr int kMaxOut = 4;
+struct OutCols {
+    const int64_t* src[kMaxOut];
+    const uint8_t* srcv[kMaxOut];
+    int64_t* dst[kMaxOut];
+    uint8_t* dstv[kMaxOut];
+    int n;
+};
+
+__global__ void __launch_bounds__(256) k_expand_filter(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                       int64_t m, BitView a, BitView b, OutCols oc,
+                                                       unsigned long long* __restrict__ out_count) {
+    __shared__ unsigned int wsum[4];
+    __shared__ unsigned long long block_base;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const unsigned long long lt = lane == 0 ? 0ULL : (~0ULL >> (64 - lane));
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < m; base += stride) {
+        const int64_t e = base + threadIdx.x;
+        bool keep = false;
+        if (e < m) keep = bit_ok(a, src[e]) && bit_ok(b, dst[e]);
+        const unsigned long long bal = __ballot(keep);
+        if (lane == 0) wsum[wid] = (unsigned)__popcll(bal);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+            block_base = tot ? atomicAdd(out_count, (unsigned long long)tot) : 0ULL;
+        }
+        __syncthreads();
+        if (keep) {
+            unsigned long long pos = block_base + __popcll(bal & lt);
+            for (int w = 0; w < wid; ++w) pos += wsum[w];
+            for (int c = 0; c < oc.n; ++c) {
+                oc.dst[c][pos] = oc.src[c][e];
+                if (oc.dstv[c]) oc.dstv[c][pos] = oc.srcv[c] ? oc.srcv[c][e] : 1;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---- C3: 2-hop count(DISTINCT c) ------------------------------------------------------
+// hop 1: for every rel (s -> t):
+//   s != t, a_ok(s), b_ok(t)           -> M(t)  (b has an in-edge that differs from any r2 leaving b
+//                                                 towards c != b)
+//   s == t, a_ok(s), b_ok(s)           -> S1(s); a second such self-loop -> S2(s)
+// combine: X1 = M | S1 (middle for r2 not a self-loop), X2 = M | S2 (middle for a self-loop r2,
+//   which needs an a_ok in-edge other than r2 itself).
+// hop 2: for every rel (b -> c) with c_ok(c): (b != c ? X1(b) : X2(b)) -> C(c)
+// count(DISTINCT c) = popcount(C).  Matches the enumeration in oracle/rmat.c.
+// two consecutive rels per lane: one 16-B load per column when the column view is 16-B aligned
+__device__ __forceinline__ void load2(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t e0,
+                                      int64_t m, int aligned, int64_t (&s)[2], int64_t (&t)[2]) {
+    if (aligned && e0 + 1 < m) {
+        const longlong2 sv = *reinterpret_cast<const longlong2*>(src + e0);
+        const longlong2 tv = *reinterpret_cast<const longlong2*>(dst + e0);
+        s[0] = sv.x; s[1] = sv.y; t[0] = tv.x; t[1] = tv.y;
+    } else {
+        s[0] = e0 < m ? src[e0] : -1;
+        t[0] = e0 < m ? dst[e0] : -1;
+        s[1] = e0 + 1 < m ? src[e0 + 1] : -1;
+        t[1] = e0 + 1 < m ? dst[e0 + 1] : -1;
+    }
+}
+
+template <bool A_FULL, bool B_FULL>
+__global__ void __launch_bounds__(256) k_hop1(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                              int64_t m, int aligned, BitView a, BitView b, uint32_t* __restrict__ M,
+                                              uint32_t* __restrict__ S1, uint32_t* __restrict__ S2) {
+    // wave-uniform trip count: every lane of a wave runs the same iterations, so the
+    // cross-lane bit combining in wave_set_bit never reads an exited lane
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 2;
+    const int lane = threadIdx.x & 63;
+    for (int64_t wbase = ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63)) * 2; wbase < m; wbase += stride) {
+        const int64_t e0 = wbase + 2 * lane;
+        int64_t s[2], t[2];
+        load2(src, dst, e0, m, aligned, s, t);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const bool valid = (e0 + k < m);
+            const bool aok = valid && (A_FULL ? (s[k] >= a.lo && s[k] < a.hi) : bit_ok(a, s[k]));
+            const bool bok = aok && (B_FULL ? (t[k] >= b.lo && t[k] < b.hi) : bit_ok(b, t[k]));
+            const bool loop = s[k] == t[k];
+            wave_set_bit(M, t[k] - b.lo, bok && !loop);
+            if (bok && loop) {  // rare: self-loops
+                const uint64_t x = (uint64_t)(t[k] - b.lo);
+                const uint32_t bit = 1u << (x & 31);
+                const uint32_t old = atomicOr(&S1[x >> 5], bit);
+                if (old & bit) atomicOr(&S2[x >> 5], bit);
+            }
+        }
+    }
+}
+
+__global__ void k_mid_combine(uint32_t* __restrict__ X1 /* in: M */, uint32_t* __restrict__ X2 /* in: S2 */,
+                              const uint32_t* __restrict__ S1, int64_t nw) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t m = X1[i];
+        X1[i] = m | S1[i];
+        X2[i] = m | X2[i];
+    }
+}
+
+template <bool C_FULL>
+__global__ void __launch_bounds__(256) k_hop2(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                              int64_t m, int aligned, BitView c, const uint32_t* __restrict__ X1,
+                                              const uint32_t* __restrict__ X2, int64_t mid_lo, int64_t mid_hi,
+                                              uint32_t* __restrict__ C) {
+    // wave-uniform trip count: every lane of a wave runs the same iterations, so the
+    // cross-lane bit combining in wave_set_bit never reads an exited lane
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * 2;
+    const int lane = threadIdx.x & 63;
+    for (int64_t wbase = ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63)) * 2; wbase < m; wbase += stride) {
+        const int64_t e0 = wbase + 2 * lane;
+        int64_t s[2], t[2];
+        load2(src, dst, e0, m, aligned, s, t);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const bool valid = (e0 + k < m);
+            const bool cok = valid && (C_FULL ? (t[k] >= c.lo && t[k] < c.hi) : bit_ok(c, t[k]));
+            bool hit = false;
+            if (cok && s[k] >= mid_lo && s[k] < mid_hi) {
+                const uint64_t x = (uint64_t)(s[k] - mid_lo);
+                const uint32_t* X = (s[k] == t[k]) ? X2 : X1;
+                hit = (X[x >> 5] >> (x & 31)) & 1u;
+            }
+            wave_set_bit(C, t[k] - c.lo, hit);
+        }
+    }
+}
+
+// ---- closed-form count(*) (matched rows) --------------------------------------------
+// inA(b) = #rels x->b with a_ok(x); outC(b) = #rels b->y with c_ok(y)
+__global__ void k_degrees(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, BitView a,
+                          BitView b, BitView c, unsigned int* __restrict__ inA, unsigned int* __restrict__ outC,
+                          unsigned long long* __restrict__ loops) {
+    unsigned long long nl = 0;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = src[e], t = dst[e];
+        const bool sa = bit_ok(a, s), tc = bit_ok(c, t);
+        if (sa && t >= b.lo && t < b.hi) atomicAdd(&inA[t - b.lo], 1u);
+        if (tc && s >= b.lo && s < b.hi) atomicAdd(&outC[s - b.lo], 1u);
+        if (s == t && sa && tc && bit_ok(b, s)) ++nl;
+    }
+    if (nl) atomicAdd(loops, nl);
+}
+
+__global__ void k_deg_product(const unsigned int* __restrict__ inA, const unsigned int* __restrict__ outC, int64_t n,
+                              BitView b, unsigned long long* __restrict__ out) {
+    unsigned long long acc = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        if (bit_ok(b, b.lo + i)) acc += (unsigned long long)inA[i] * (unsigned long long)outC[i];
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+
+// ---- synthetic R-MAT (definition: oracle/rmat.c rmat_edge) -----------------------------
+__device__ __forceinline__ void rmat_edge(int scale, uint64_t tA, uint64_t tAB, uint64_t tABC, uint64_t seed, uint64_t e,
+                                          int64_t* so, int64_t* dout) {
+    uint64_t s = 0, d = 0, r = 0;
+    for (int l = 0; l < scale; ++l) {
+        if ((l & 1) == 0) r = splitmix64((seed << 40) | (e << 5) | (uint64_t)(l >> 1));
+        const uint64_t u = (l & 1) == 0 ? (r >> 32) : (r & 0xffffffffULL);
+        const uint64_t sb = u >= tAB;                       // quadrants C, D
+        const uint64_t db = (u >= tA && u < tAB) || u >= tABC;  // quadrants B, D
+        s |= sb << (scale - 1 - l);
+        d |= db << (scale - 1 - l);
+    }
+    const uint64_t mask = (1ULL << scale) - 1;
+    *so = (int64_t)((s * 0x9E3779B97F4A7C15ULL) & mask);
+    *dout = (int64_t)((d * 0x9E3779B97F4A7C15ULL) & mask);
+}
+
+__device__ __forceinline__ int owner_of_word(int64_t word, int64_t nwords, int nparts) {
+    int p = (int)((word * nparts) / nwords);
+    while (p + 1 < nparts && ((int64_t)(p + 1) * nwords) / nparts <= word) ++p;
+    while (p > 0 && ((int64_t)p * nwords) / nparts > word) --p;
+    return p;
+}
+
+struct RmatArgs {
+    int scale;
+    uint64_t tA, tAB, tABC, seed;
+    int64_t e_begin, e_end;
+    int part_col, part, nparts;
+    int64_t nwords;
+};
+
+__device__ __forceinline__ bool rmat_keep(const RmatArgs& g, int64_t s, int64_t d) {
+    if (g.part_col < 0 || g.nparts <= 1) return true;
+    const int64_t id = g.part_col == 0 ? s : d;
+    return owner_of_word(id >> 5, g.nwords, g.nparts) == g.part;
+}
+
+__global__ void k_rmat_count(RmatArgs g, unsigned long long* __restrict__ tile_cnt) {
+    const int64_t e = g.e_begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool keep = false;
+    if (e < g.e_end) {
+        int64_t s, d;
+        rmat_edge(g.scale, g.tA, g.tAB, g.tABC, g.seed, (uint64_t)e, &s, &d);
+        keep = rmat_keep(g, s, d);
+    }
+    const unsigned long long bal = __ballot(keep);
+    __shared__ unsigned int ws[4];
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = (unsigned)__popcll(bal);
+    __syncthreads();
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ void k_rmat_write(RmatArgs g, const int64_t* __restrict__ tile_off, int64_t* __restrict__ id,
+                             int64_t* __restrict__ so, int64_t* __restrict__ dout) {
+    const int64_t e = g.e_begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool keep = false;
+    int64_t s = 0, d = 0;
+    if (e < g.e_end) {
+        rmat_edge(g.scale, g.tA, g.tAB, g.tABC, g.seed, (uint64_t)e, &s, &d);
+        keep = rmat_keep(g, s, d);
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const unsigned long long bal = __ballot(keep);
+    __shared__ unsigned int ws[4];
+    if (lane == 0) ws[wid] = (unsigned)__popcll(bal);
+    __syncthreads();
+    if (keep) {
+        const unsigned long long lt = lane == 0 ? 0ULL : (~0ULL >> (64 - lane));
+        int64_t pos = tile_off[blockIdx.x] + __popcll(bal & lt);
+        for (int w = 0; w < wid; ++w) pos += ws[w];
+        id[pos] = e;
+        so[pos] = s;
+        dout[pos] = d;
+    }
+}
+
+__global__ void k_person_flags(int64_t n, int want_person, uint8_t* __restrict__ f) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const bool p = (splitmix64((uint64_t)i) & 3ULL) != 0;
+        f[i] = (p == (want_person != 0)) ? 1 : 0;
+    }
+}
+
+__global__ void k_age(const int64_t* __restrict__ ids, int64_t n, uint64_t seed, int64_t* __restrict__ age) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        age[i] = (int64_t)(splitmix64(seed ^ (uint64_t)ids[i]) % 100ULL);
+}
+
+// ---- row fingerprint ---------------------------------------------------
+constexpr int kMaxFp = 8;
+struct FpCols {
+    const int64_t* d[kMaxFp];
+    const uint8_t* v[kMaxFp];
+    int n;
+};
+__global__ void k_fingerprint(FpCols fc, int64_t n, unsigned long long* __restrict__ out /* sum, xor */) {
+    unsigned long long hs = 0, hx = 0;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t h = 0x243F6A8885A308D3ULL;
+        for (int c = 0; c < fc.n; ++c) {
+            const bool ok = fc.v[c] == nullptr || fc.v[c][r];
+            const uint64_t v = ok ? (uint64_t)fc.d[c][r] : 0x7FF8DEADBEEF0001ULL;  // NULL sentinel
+            h = splitmix64(h ^ v);
+        }
+        hs += h;
+        hx ^= h;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        hs += __shfl_down(hs, o, 64);
+        hx ^= __shfl_down(hx, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&out[0], hs);
+        atomicXor(&out[1], hx);
+    }
+}
+
+inline int grid_cap(int64_t n, int64_t cap) {
+    int64_t g = (n + 255) / 256;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (int)g;
+}
+
+}  // namespace
+
+// ================================ host side =================================================
+
+void bitmap_add_rows(capsmi_bitmap* b, const int64_t* ids, const uint8_t* ids_valid, const uint8_t* flags, int64_t n,
+                     int64_t* dev_counters) {
+    if (n <= 0) return;
+    KernelTimer kt(b->sess, "bitmap_add");
+    hipLaunchKernelGGL(k_bitmap_add, dim3(grid_cap(n, 4096)), dim3(256), 0, b->sess->stream, P<uint32_t>(b->words),
+                       b->lo, b->hi, ids, ids_valid, flags, n, (unsigned long long*)dev_counters);
+    HIP_CHECK(hipGetLastError());
+}
+
+int64_t words_popcount(capsmi_session* s, const uint32_t* w, int64_t w_begin, int64_t w_end) {
+    Buf out = dev_alloc(8, s->stream);
+    HIP_CHECK(hipMemsetAsync(P<void>(out), 0, 8, s->stream));
+    if (w_end > w_begin)
+        hipLaunchKernelGGL(k_popcount, dim3(grid_cap(w_end - w_begin, 2048)), dim3(256), 0, s->stream, w, w_begin, w_end,
+                           P<unsigned long long>(out));
+    HIP_CHECK(hipGetLastError());
+    return read_scalar(s, P<int64_t>(out));
+}
+
+namespace graph {
+
+static BitView view(const capsmi_bitmap* b) {
+    BitView v;
+    v.w = P<uint32_t>(b->words);
+    v.lo = b->lo;
+    v.hi = b->hi;
+    v.full = b->full ? 1 : 0;
+    return v;
+}
+
+int hop_grid(capsmi_session* s, int64_t m) {
+    // 2 rels per thread per iteration; enough waves to keep ~16 KB in flight per CU
+    int64_t g = (m / 2 + 255) / 256;
+    const int64_t cap = (int64_t)s->num_cus * 16;
+    if (g > cap) g = cap;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+void expand_filter(capsmi_session* s, const int64_t* src, const int64_t* dst, int64_t m, const capsmi_bitmap* a,
+                   const capsmi_bitmap* b, int nout, const int64_t* const* in_d, const uint8_t* const* in_v,
+                   int64_t* const* out_d, uint8_t* const* out_v, int64_t* dev_count) {
+    OutCols oc;
+    oc.n = nout;
+    for (int c = 0; c < kMaxOut; ++c) {
+        oc.src[c] = c < nout ? in_d[c] : nullptr;
+        oc.srcv[c] = c < nout ? in_v[c] : nullptr;
+        oc.dst[c] = c < nout ? out_d[c] : nullptr;
+        oc.dstv[c] = c < nout ? out_v[c] : nullptr;
+    }
+    if (m <= 0) return;
+    int64_t g = (m + 255) / 256;
+    const int64_t cap = (int64_t)s->num_cus * 8;
+    if (g > cap) g = cap;
+    KernelTimer kt(s, "expand_filter");
+    hipLaunchKernelGGL(k_expand_filter, dim3((unsigned)g), dim3(256), 0, s->stream, src, dst, m, view(a), view(b), oc,
+                       (unsigned long long*)dev_count);
+    HIP_CHECK(hipGetLastError());
+}
+
+void hop1(capsmi_session* s, const int64_t* src, const int64_t* dst, int64_t m, const capsmi_bitmap* a,
+          const capsmi_bitmap* b, uint32_t* M, uint32_t* S1, uint32_t* S2) {
+    if (m <= 0) return;
+    const BitView av = view(a), bv = view(b);
+    const int al = ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) == 0;
+    const dim3 g(hop_grid(s, m)), blk(256);
+    KernelTimer kt(s, "hop1");
+    if (a->full && b->full) hipLaunchKernelGGL((k_hop1<true, true>), g, blk, 0, s->stream, src, dst, m, al, av, bv, M, S1, S2);
+    else if (a->full) hipLaunchKernelGGL((k_hop1<true, false>), g, blk, 0, s->stream, src, dst, m, al, av, bv, M, S1, S2);
+    else if (b->full) hipLaunchKernelGGL((k_hop1<false, true>), g, blk, 0, s->stream, src, dst, m, al, av, bv, M, S1, S2);
+    else hipLaunchKernelGGL((k_hop1<false, false>), g, blk, 0, s->stream, src, dst, m, al, av, bv, M, S1, S2);
+    HIP_CHECK(hipGetLastError());
+}
+
+void mid_combine(capsmi_session* s, uint32_t* X1, uint32_t* X2, const uint32_t* S1, int64_t nw) {
+    KernelTimer kt(s, "mid_combine");
+    hipLaunchKernelGGL(k_mid_combine, dim3(grid_cap(nw, 4096)), dim3(256), 0, s->stream, X1, X2, S1, nw);
+    HIP_CHECK(hipGetLastError());
+}
+
+void hop2(capsmi_session* s, const int64_t* src, const int64_t* dst, int64_t m, const capsmi_bitmap* c,
+          const uint32_t* X1, const uint32_t* X2, int64_t mid_lo, int64_t mid_hi, uint32_t* C) {
+    if (m <= 0) return;
+    const BitView cv = view(c);
+    const int al = ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) == 0;
+    const dim3 g(hop_grid(s, m)), blk(256);
+    KernelTimer kt(s, "hop2");
+    if (c->full) hipLaunchKernelGGL((k_hop2<true>), g, blk, 0, s->stream, src, dst, m, al, cv, X1, X2, mid_lo, mid_hi, C);
+    else hipLaunchKernelGGL((k_hop2<false>), g, blk, 0, s->stream, src, dst, m, al, cv, X1, X2, mid_lo, mid_hi, C);
+    HIP_CHECK(hipGetLastError());
+}
+
+void degrees(capsmi_session* s, const int64_t* src, const int64_t* dst, int64_t m, const capsmi_bitmap* a,
+             const capsmi_bitmap* b, const capsmi_bitmap* c, uint32_t* inA, uint32_t* outC, int64_t* loops) {
+    if (m <= 0) return;
+    KernelTimer kt(s, "degrees");
+    hipLaunchKernelGGL(k_degrees, dim3(grid_cap(m, (int64_t)s->num_cus * 16)), dim3(256), 0, s->stream, src, dst, m,
+                       view(a), view(b), view(c), inA, outC, (unsigned long long*)loops);
+    HIP_CHECK(hipGetLastError());
+}
+
+void deg_product(capsmi_session* s, const uint32_t* inA, const uint32_t* outC, int64_t n, const capsmi_bitmap* b,
+                 int64_t* out) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_deg_product, dim3(grid_cap(n, 4096)), dim3(256), 0, s->stream, inA, outC, n, view(b),
+                       (unsigned long long*)out);
+    HIP_CHECK(hipGetLastError());
+}
+
+int64_t rmat(capsmi_session* s, int scale, int64_t e_begin, int64_t e_end, int pa, int pb, int pc, uint64_t seed,
+             int part_col, int part, int nparts, Buf& id, Buf& so, Buf& dout) {
+    RmatArgs g;
+    g.scale = scale;
+    g.tA = ((uint64_t)pa << 32) / 100;
+    g.tAB = ((uint64_t)(pa + pb) << 32) / 100;
+    g.tABC = ((uint64_t)(pa + pb + pc) << 32) / 100;
+    g.seed = seed;
+    g.e_begin = e_begin;
+    g.e_end = e_end;
+    g.part_col = part_col;
+    g.part = part;
+    g.nparts = nparts;
+    g.nwords = ((int64_t(1) << scale) + 31) / 32;
+    const int64_t m = e_end - e_begin;
+    const int64_t nb = (m + 255) / 256;
+    hipStream_t st = s->stream;
+    Buf cnt = dev_alloc(sizeof(int64_t) * (nb > 0 ? nb : 1), st);
+    Buf off = dev_alloc(sizeof(int64_t) * (nb + 1), st);
+    if (nb > 0) hipLaunchKernelGGL(k_rmat_count, dim3((unsigned)nb), dim3(256), 0, st, g, P<unsigned long long>(cnt));
+    exclusive_scan_i64(P<int64_t>(cnt), P<int64_t>(off), nb, st);
+    const int64_t total = read_scalar(s, P<int64_t>(off) + nb);
+    id = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), st);
+    so = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), st);
+    dout = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), st);
+    if (nb > 0)
+        hipLaunchKernelGGL(k_rmat_write, dim3((unsigned)nb), dim3(256), 0, st, g, P<int64_t>(off), P<int64_t>(id),
+                           P<int64_t>(so), P<int64_t>(dout));
+    HIP_CHECK(hipGetLastError());
+    return total;
+}
+
+void person_flags(capsmi_session* s, int64_t n, bool want_person, uint8_t* f) {
+    hipLaunchKernelGGL(k_person_flags, dim3(grid_cap(n, 8192)), dim3(256), 0, s->stream, n, want_person ? 1 : 0, f);
+    HIP_CHECK(hipGetLastError());
+}
+
+void ages(capsmi_session* s, const int64_t* ids, int64_t n, uint64_t seed, int64_t* age) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_age, dim3(grid_cap(n, 8192)), dim3(256), 0, s->stream, ids, n, seed, age);
+    HIP_CHECK(hipGetLastError());
+}
+
+void fingerprint(capsmi_session* s, int ncols, const int64_t* const* d, const uint8_t* const* v, int64_t n,
+                 uint64_t* out_sum, uint64_t* out_xor) {
+    REQUIRE(ncols <= kMaxFp, CAPSMI_ERR_NOT_IMPLEMENTED, "fingerprint over more than 8 columns");
+    FpCols fc;
+    fc.n = ncols;
+    for (int c = 0; c < kMaxFp; ++c) {
+        fc.d[c] = c < ncols ? d[c] : nullptr;
+        fc.v[c] = c < ncols ? v[c] : nullptr;
+    }
+    Buf out = dev_alloc(16, s->stream);
+    HIP_CHECK(hipMemsetAsync(P<void>(out), 0, 16, s->stream));
+    if (n > 0)
+        hipLaunchKernelGGL(k_fingerprint, dim3(grid_cap(n, 4096)), dim3(256), 0, s->stream, fc, n,
+                           P<unsigned long long>(out));
+    HIP_CHECK(hipGetLastError());
+    uint64_t host[2];
+    HIP_CHECK(hipMemcpyAsync(host, P<void>(out), 16, hipMemcpyDeviceToHost, s->stream));
+    HIP_CHECK(hipStreamSynchronize(s->stream));
+    *out_sum = host[0];
+    *out_xor = host[1];
+}
+
+}  // namespace graph
+}  // namespace capsmi

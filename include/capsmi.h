@@ -1,0 +1,295 @@
+/*
+ * capsmi.h -- C ABI of the MI355X execution backend for CAPS pattern matching.
+ *
+ * This is the drop-in boundary.  In CAPS the backend plug-in
+ * point is the Scala trait
+ *     trait Table[T <: Table[T]] extends CypherTable
+ *     okapi-relational/src/main/scala/org/opencypher/okapi/relational/api/table/Table.scala:43-176
+ * implemented for Spark by DataFrameTable
+ *     spark-cypher/src/main/scala/org/opencypher/spark/impl/table/SparkTable.scala:47-257
+ * A JVM shim (`GpuTable extends Table[GpuTable]`) binds each
+ * method below over JNI.  Every entry point cites the Scala member it replaces.
+ *
+ * Conventions
+ *  - Every call returns capsmi_status (0 = OK).  On failure capsmi_last_error()
+ *    returns a thread-local message.  The shim maps the codes to the okapi
+ *    exception classes (okapi-api/.../impl/exception/InternalException.scala:34-59).
+ *  - Handles are opaque and reference counted.  Tables are immutable: every op
+ *    returns a NEW table and never modifies its inputs (Table.scala: each op
+ *    returns T; inputs stay valid for DAG sharing / cached sub-trees).
+ *  - Columns are addressed by name, as in Table.scala (`cols: String*`).
+ *  - Values are 8 bytes per row: I64 (Spark LongType), BOOL (0/1), F64 (bits of
+ *    an IEEE double), STR (order-preserving dictionary code assigned by the
+ *    caller; equal strings <=> equal codes, string order <=> code order).
+ *    Nullability is a byte per row (1 = valid), or absent when a column has no nulls.
+ *  - A session is externally synchronised (one caller thread, like a CAPS
+ *    driver) and owns one HIP stream on one gfx950 device.  Device work is
+ *    stream-ordered; calls that return a size to the host synchronise.
+ */
+#ifndef CAPSMI_H
+#define CAPSMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------------- */
+typedef int32_t capsmi_status;
+enum {
+    CAPSMI_OK = 0,
+    CAPSMI_ERR_ILLEGAL_ARGUMENT = 1, /* okapi IllegalArgumentException */
+    CAPSMI_ERR_NOT_IMPLEMENTED = 2,  /* okapi NotImplementedException */
+    CAPSMI_ERR_UNSUPPORTED = 3,      /* okapi UnsupportedOperationException */
+    CAPSMI_ERR_DEVICE = 4,           /* HIP runtime error (no GPU, fault, ...) */
+    CAPSMI_ERR_OUT_OF_MEMORY = 5,
+    CAPSMI_ERR_INTERNAL = 6          /* okapi InternalException */
+};
+
+/* ---- handles ----------------------------------------------------------------- */
+typedef struct capsmi_session capsmi_session;
+typedef struct capsmi_table capsmi_table;
+typedef struct capsmi_bitmap capsmi_bitmap;
+
+/* ---- value types (CypherType -> physical type, SparkConversions.scala:55-168) -- */
+enum {
+    CAPSMI_I64 = 0,  /* CTInteger, CTNode/CTRelationship ids (Long) */
+    CAPSMI_BOOL = 1, /* CTBoolean, label / rel-type flag columns */
+    CAPSMI_F64 = 2,  /* CTFloat */
+    CAPSMI_STR = 3   /* CTString, dictionary code */
+};
+
+typedef struct {
+    const char* name;
+    int32_t type;         /* CAPSMI_I64 ... CAPSMI_STR */
+    const void* data;     /* nrows x 8 bytes */
+    const uint8_t* valid; /* nrows bytes (1 = non-null) or NULL (no nulls) */
+} capsmi_col_desc;
+
+/* ---- expressions: postfix programs over one row -------------------------------
+ * Subset of SparkSQLExprMapper.asSparkSQLExpr (spark-cypher/.../impl/SparkSQLExprMapper.scala:81-312)
+ * that the pattern-matching path needs: column refs (Var/Property/HasLabel/HasType/StartNode/EndNode
+ * resolve to columns, :97-105), literals and params (:86-92, :111-117), Equals (:120), Not (:121),
+ * IsNull/IsNotNull (:122-123), Ands/Ors (:132-136), In (:138-145), < <= > >= (:147-150), arithmetic.
+ * Evaluation follows SQL three-valued logic; Filter keeps rows whose value is TRUE. */
+enum {
+    CAPSMI_X_COL = 0,      /* push column `arg` (index into the input table) */
+    CAPSMI_X_LIT = 1,      /* push literal of type `type`, bits in `ival` */
+    CAPSMI_X_NULL = 2,     /* push NULL; arg = 1 + declared type (0 = untyped) */
+    CAPSMI_X_EQ = 3,       /* pop b, a; push a = b */
+    CAPSMI_X_NEQ = 4,
+    CAPSMI_X_LT = 5,
+    CAPSMI_X_LE = 6,
+    CAPSMI_X_GT = 7,
+    CAPSMI_X_GE = 8,
+    CAPSMI_X_NOT = 9,
+    CAPSMI_X_AND = 10,     /* pop `arg` operands, push conjunction (3VL) */
+    CAPSMI_X_OR = 11,      /* pop `arg` operands, push disjunction (3VL) */
+    CAPSMI_X_ISNULL = 12,
+    CAPSMI_X_ISNOTNULL = 13,
+    CAPSMI_X_IN = 14,      /* stack [x, v1..v_arg]: x IN (v1..v_arg), 3VL */
+    CAPSMI_X_ADD = 15,
+    CAPSMI_X_SUB = 16,
+    CAPSMI_X_MUL = 17,
+    CAPSMI_X_NEG = 18,
+    CAPSMI_X_COALESCE = 19 /* pop `arg` operands, push the first non-null */
+};
+
+typedef struct {
+    int32_t op;
+    int32_t arg;
+    int32_t type; /* literal type for CAPSMI_X_LIT */
+    int32_t reserved;
+    int64_t ival; /* literal payload (int64 / 0|1 / dictionary code / double bits) */
+} capsmi_expr;
+
+typedef struct {
+    const char* name;        /* output column (replaced if it exists, else appended) */
+    int32_t nnodes;
+    const capsmi_expr* prog;
+} capsmi_expr_column;
+
+/* ---- joins and aggregates (PhysicalConstants.scala:29-40, SparkTable.scala:121-188) ---- */
+enum {
+    CAPSMI_JOIN_INNER = 0,
+    CAPSMI_JOIN_LEFT_OUTER = 1,
+    CAPSMI_JOIN_RIGHT_OUTER = 2,
+    CAPSMI_JOIN_FULL_OUTER = 3,
+    CAPSMI_JOIN_CROSS = 4
+};
+
+enum {
+    CAPSMI_AGG_COUNT_STAR = 0, /* count(lit 0)                  SparkTable.scala:148-149 */
+    CAPSMI_AGG_COUNT = 1,      /* count / countDistinct         SparkTable.scala:152-158 */
+    CAPSMI_AGG_MIN = 2,        /*                               SparkTable.scala:163-164 */
+    CAPSMI_AGG_MAX = 3,        /*                               SparkTable.scala:160-161 */
+    CAPSMI_AGG_SUM = 4,        /*                               SparkTable.scala:166-167 */
+    CAPSMI_AGG_AVG = 5         /* avg -> F64                    SparkTable.scala:141-146 */
+};
+
+typedef struct {
+    int32_t kind;
+    int32_t distinct;        /* COUNT only */
+    const char* input;       /* input column (ignored for COUNT_STAR) */
+    const char* output;      /* result column name */
+} capsmi_agg;
+
+/* ---- errors / session ----------------------------------------------------------- */
+/* copies the calling thread's last error message into buf (NUL-terminated); returns its length */
+size_t capsmi_last_error(char* buf, size_t n);
+const char* capsmi_version(void);
+
+/* CAPSSession.local()/create (spark-cypher/.../api/CAPSSession.scala:110-131): one device, one stream */
+capsmi_status capsmi_session_create(int32_t device, capsmi_session** out);
+capsmi_status capsmi_session_destroy(capsmi_session* s);
+/* run subsequent work on an external hipStream_t (e.g. torch's current stream); NULL = session stream */
+capsmi_status capsmi_session_set_stream(capsmi_session* s, void* hip_stream);
+capsmi_status capsmi_session_sync(capsmi_session* s);
+/* per-kernel HIP-event timing of the fused graph kernels (off by default; SURVEY.md §5 tracing).
+ * While enabled, each hot launch is bracketed by events on the session stream. */
+capsmi_status capsmi_session_set_profiling(capsmi_session* s, int32_t enabled);
+/* resolve pending events (synchronises) and report totals for kernel `name` ("hop1", "hop2",
+ * "expand_filter", "bitmap_add", ...): launches and summed milliseconds; then the counters reset. */
+capsmi_status capsmi_session_kernel_time(capsmi_session* s, const char* name, int64_t* launches, double* total_ms);
+
+/* ---- tables (CypherTable: okapi-api/.../api/table/CypherTable.scala:41-68) -------- */
+/* CAPSNodeTable/CAPSRelationshipTable ingest (spark-cypher/.../api/io/CAPSTable.scala:47-214): copies */
+capsmi_status capsmi_table_from_host(capsmi_session* s, int32_t ncols, const capsmi_col_desc* cols,
+                                     int64_t nrows, capsmi_table** out);
+/* same, but `data`/`valid` are device pointers on this session's device (copied, stream-ordered) */
+capsmi_status capsmi_table_from_device(capsmi_session* s, int32_t ncols, const capsmi_col_desc* cols,
+                                       int64_t nrows, capsmi_table** out);
+capsmi_status capsmi_table_retain(capsmi_table* t);
+capsmi_status capsmi_table_release(capsmi_table* t);
+/* CypherTable.size -> DataFrameTable.size = df.count() (SparkTable.scala:59) */
+capsmi_status capsmi_table_size(const capsmi_table* t, int64_t* out);
+/* CypherTable.physicalColumns / columnType (SparkTable.scala:51-53) */
+capsmi_status capsmi_table_num_columns(const capsmi_table* t, int32_t* out);
+capsmi_status capsmi_table_column_name(const capsmi_table* t, int32_t col, char* buf, size_t n);
+capsmi_status capsmi_table_column_type(const capsmi_table* t, int32_t col, int32_t* out);
+capsmi_status capsmi_table_column_index(const capsmi_table* t, const char* name, int32_t* out);
+capsmi_status capsmi_table_column_nullable(const capsmi_table* t, int32_t col, int32_t* out);
+/* CypherTable.rows / CAPSRecords.collect (SparkTable.scala:55-57, CAPSRecords.scala:136-143):
+ * copies rows [offset, offset+n) of one column to the host; host_valid may be NULL */
+capsmi_status capsmi_table_export(const capsmi_table* t, int32_t col, void* host_data, uint8_t* host_valid,
+                                  int64_t offset, int64_t n);
+/* zero-copy device view of a column (valid pointer NULL when the column has no nulls) */
+capsmi_status capsmi_table_column_device_ptr(const capsmi_table* t, int32_t col, const void** data,
+                                             const uint8_t** valid);
+
+/* ---- Table[T] operators ------------------------------------------------------------- */
+capsmi_status capsmi_cache(capsmi_table* t, capsmi_table** out);                         /* Table.scala:52  */
+capsmi_status capsmi_select(capsmi_table* t, int32_t ncols, const char* const* cols,
+                            capsmi_table** out);                                        /* Table.scala:60  */
+capsmi_status capsmi_filter(capsmi_table* t, int32_t nnodes, const capsmi_expr* prog,
+                            capsmi_table** out);                                        /* Table.scala:70  */
+capsmi_status capsmi_drop(capsmi_table* t, int32_t ncols, const char* const* cols,
+                          capsmi_table** out);                                          /* Table.scala:78  */
+capsmi_status capsmi_join(capsmi_table* l, capsmi_table* r, int32_t join_type, int32_t npairs,
+                          const char* const* lcols, const char* const* rcols,
+                          capsmi_table** out);                                          /* Table.scala:88  */
+capsmi_status capsmi_union_all(capsmi_table* a, capsmi_table* b, capsmi_table** out);   /* Table.scala:96  */
+capsmi_status capsmi_order_by(capsmi_table* t, int32_t nkeys, const char* const* cols,
+                              const int32_t* descending, capsmi_table** out);           /* Table.scala:104 */
+capsmi_status capsmi_skip(capsmi_table* t, int64_t n, capsmi_table** out);              /* Table.scala:112 */
+capsmi_status capsmi_limit(capsmi_table* t, int64_t n, capsmi_table** out);             /* Table.scala:120 */
+capsmi_status capsmi_distinct(capsmi_table* t, capsmi_table** out);                     /* Table.scala:127 */
+capsmi_status capsmi_distinct_on(capsmi_table* t, int32_t ncols, const char* const* cols,
+                                 capsmi_table** out);                                   /* SparkTable.scala:234-235 */
+capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, int32_t naggs,
+                           const capsmi_agg* aggs, capsmi_table** out);                 /* Table.scala:147 */
+capsmi_status capsmi_with_columns(capsmi_table* t, int32_t ncols, const capsmi_expr_column* cols,
+                                  capsmi_table** out);                                  /* Table.scala:159 */
+capsmi_status capsmi_with_column_renamed(capsmi_table* t, const char* old_name, const char* new_name,
+                                         capsmi_table** out);                           /* Table.scala:168 */
+
+/* ---- graph fast path ------------------------------------------------------------------
+ * The relational planner lowers Expand into `join(relScan, source = start)` then
+ * `join(nodeScan, end = target)` (RelationalPlanner.scala:113-137).  When the shim sees that
+ * shape over base entity tables with dense Long ids it calls these fused entry points
+ * instead; results are identical row multisets.
+ *
+ * A capsmi_bitmap is a node scan + label/property predicate (ScanGraph.scanOperator,
+ * ScanGraph.scala:61-96, plus Filter) collapsed to one bit per id in [id_lo, id_hi). */
+capsmi_status capsmi_bitmap_create(capsmi_session* s, int64_t id_lo, int64_t id_hi, capsmi_bitmap** out);
+/* OR in the ids of node-table rows whose predicate is TRUE (nnodes = 0: every row).
+ * Ids outside [id_lo, id_hi) or null ids are an ILLEGAL_ARGUMENT error. */
+capsmi_status capsmi_bitmap_add_scan(capsmi_bitmap* b, capsmi_table* nodes, const char* id_col,
+                                     int32_t nnodes, const capsmi_expr* pred);
+/* number of set bits, and whether every scanned row contributed a distinct id (no id in two
+ * scanned rows: the fused paths require it, since CAPS would emit one row per table occurrence,
+ * ScanGraph.scala:72-76) */
+capsmi_status capsmi_bitmap_stats(capsmi_bitmap* b, int64_t* set_bits, int32_t* unique_rows);
+capsmi_status capsmi_bitmap_release(capsmi_bitmap* b);
+
+/* 1-hop Expand + node filters, fused (C2):
+ *   MATCH (a)-[r]->(b) WHERE src_ok(a) AND dst_ok(b)
+ * = rels ⋈ a-scan ⋈ b-scan; returns the rel rows that survive, projected on `out_cols`
+ * (renamed to `out_names`, or kept when out_names == NULL). */
+capsmi_status capsmi_expand_filter(capsmi_session* s, capsmi_table* rels, const char* src_col,
+                                   const char* dst_col, const capsmi_bitmap* src_ok,
+                                   const capsmi_bitmap* dst_ok, int32_t nout, const char* const* out_cols,
+                                   const char* const* out_names, capsmi_table** out);
+
+/* 2-hop with relationship uniqueness (C3), fused, never materialising the bindings:
+ *   MATCH (a)-[r1]->(b)-[r2]->(c) WHERE a_ok(a) AND b_ok(b) AND c_ok(c)   [r1 <> r2 implied]
+ *   RETURN count(DISTINCT c)
+ * `rels` is one or more relationship tables of the scanned type (their union is the rel scan). */
+capsmi_status capsmi_two_hop_count_distinct(capsmi_session* s, int32_t nrels, capsmi_table* const* rels,
+                                            const char* src_col, const char* dst_col,
+                                            const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok,
+                                            const capsmi_bitmap* c_ok, int64_t* out_distinct);
+/* count(*) of the same MATCH, closed form: sum_b [b_ok] inA(b) * outC(b) - #eligible self-loops */
+capsmi_status capsmi_two_hop_count(capsmi_session* s, int32_t nrels, capsmi_table* const* rels,
+                                   const char* src_col, const char* dst_col, const capsmi_bitmap* a_ok,
+                                   const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok, int64_t* out_rows);
+
+/* Phased form of capsmi_two_hop_count_distinct for the multi-GPU path.  The caller
+ * owns the exchange (RCCL all-gather of the owned bitmap slice between the two phases).
+ * Bitmaps are uint32 words, bit i of word w <-> id lo+32w+i; mid_words span b_ok's id range and
+ * dst_words c_ok's.
+ * mid_words:  2 x nwords (X1 then X2), zeroed by the call.  X1(b): b can be the middle of a 2-hop
+ *             whose second edge is not a self-loop; X2(b): ... whose second edge is a self-loop at b.
+ * dst_words:  nwords, zeroed by the call; marks every reachable c.  `scratch_words`: nwords. */
+capsmi_status capsmi_two_hop_mark_mid(capsmi_session* s, int32_t nrels, capsmi_table* const* rels,
+                                      const char* src_col, const char* dst_col, const capsmi_bitmap* a_ok,
+                                      const capsmi_bitmap* b_ok, uint32_t* mid_words, uint32_t* scratch_words);
+capsmi_status capsmi_two_hop_mark_dst(capsmi_session* s, int32_t nrels, capsmi_table* const* rels,
+                                      const char* src_col, const char* dst_col, const capsmi_bitmap* b_ok,
+                                      const capsmi_bitmap* c_ok, const uint32_t* mid_words, uint32_t* dst_words);
+/* popcount of words [w_begin, w_end) of a device bitmap, result in *out (host) */
+capsmi_status capsmi_words_popcount(capsmi_session* s, const uint32_t* words, int64_t w_begin, int64_t w_end,
+                                    int64_t* out);
+
+/* Cache analogue (Table.cache -> DataFrameTable.cache, SparkTable.scala:240-246): a copy of a
+ * relationship table with rows clustered by `key_col` (dense ids in [id_lo, id_hi)).  Row multiset
+ * unchanged; the fused kernels then touch bitmaps in id order. */
+capsmi_status capsmi_cluster_by(capsmi_table* rels, const char* key_col, int64_t id_lo, int64_t id_hi,
+                                capsmi_table** out);
+
+/* ---- synthetic input -----------------------------------------------------
+ * R-MAT relationship table [id, source, target] generated on the device, identical edge for edge
+ * to oracle/rmat.c.  Keeps edges e in [e_begin, e_end) whose `part_col` (0 = source, 1 = target,
+ * -1 = no filter) id falls in the word-aligned owner range of part `part` of `nparts`. */
+capsmi_status capsmi_rmat_rels(capsmi_session* s, int32_t scale, int64_t e_begin, int64_t e_end,
+                               int32_t pa, int32_t pb, int32_t pc, uint64_t seed, int32_t part_col,
+                               int32_t part, int32_t nparts, capsmi_table** out);
+/* word range [w_begin, w_end) of part `part` of `nparts` for ids in [0, 2^scale) */
+capsmi_status capsmi_owner_words(int64_t nbits, int32_t part, int32_t nparts, int64_t* w_begin,
+                                 int64_t* w_end);
+/* R-MAT node table(s): kind 0 -> one table [id] with every id 0..2^scale-1 (all Person);
+ * kind 1 -> Person ids (splitmix64(id) & 3 != 0) with [id, age], age = splitmix64(seed ^ id) % 100;
+ * kind 2 -> Company ids (the complement) with [id] */
+capsmi_status capsmi_rmat_nodes(capsmi_session* s, int32_t scale, int32_t kind, uint64_t seed,
+                                capsmi_table** out);
+/* order-insensitive row fingerprint over `ncols` I64 columns (SURVEY.md §8d parity check):
+ * count, sum and xor of h(row), h = fold splitmix64(h ^ v) from 0x243F6A8885A308D3 */
+capsmi_status capsmi_table_fingerprint(capsmi_table* t, int32_t ncols, const char* const* cols,
+                                       int64_t* count, uint64_t* sum, uint64_t* xr);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CAPSMI_H */

@@ -1,0 +1,153 @@
+"""ctypes binding of oracle/liboracle.so (oracle/rmat.c) -- TEST INFRASTRUCTURE ONLY."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+I64P = ctypes.POINTER(ctypes.c_int64)
+U8P = ctypes.POINTER(ctypes.c_uint8)
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        lib = ctypes.CDLL(_LIB)
+        lib.orc_splitmix64.restype = ctypes.c_uint64
+        lib.orc_splitmix64.argtypes = [ctypes.c_uint64]
+        lib.orc_rmat_edges.restype = None
+        lib.orc_rmat_edges.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                       ctypes.c_int64, ctypes.c_int64, I64P, I64P]
+        lib.orc_is_person.restype = ctypes.c_int
+        lib.orc_is_person.argtypes = [ctypes.c_int64]
+        lib.orc_age.restype = ctypes.c_int64
+        lib.orc_age.argtypes = [ctypes.c_int64, ctypes.c_uint64]
+        lib.orc_row_hash.restype = ctypes.c_uint64
+        lib.orc_row_hash.argtypes = [I64P, ctypes.c_int]
+        lib.orc_two_hop_enumerate.restype = ctypes.c_int
+        lib.orc_two_hop_enumerate.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, U8P, U8P, U8P, I64P, I64P,
+                                              I64P, I64P, ctypes.c_int]
+        lib.orc_two_hop_closed_form.restype = ctypes.c_int
+        lib.orc_two_hop_closed_form.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, U8P, U8P, U8P, I64P, I64P]
+        lib.orc_expand_filter.restype = None
+        lib.orc_expand_filter.argtypes = [ctypes.c_int64, I64P, I64P, U8P, U8P, I64P,
+                                          ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        lib.orc_triangle_enumerate.restype = ctypes.c_int
+        lib.orc_triangle_enumerate.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, I64P, ctypes.c_int]
+        lib.orc_var_length_count.restype = ctypes.c_int
+        lib.orc_var_length_count.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, ctypes.c_int, ctypes.c_int,
+                                             I64P, I64P, ctypes.c_int]
+        _lib = lib
+    return _lib
+
+
+def _p64(a):
+    return a.ctypes.data_as(I64P) if a is not None else None
+
+
+def _p8(a):
+    return a.ctypes.data_as(U8P) if a is not None else None
+
+
+def splitmix64(x: int) -> int:
+    return load().orc_splitmix64(x & 0xFFFFFFFFFFFFFFFF)
+
+
+def rmat_edges(scale: int, e_begin: int, e_end: int, probs=(57, 19, 19), seed: int = 42):
+    n = e_end - e_begin
+    src = np.empty(n, dtype=np.int64)
+    dst = np.empty(n, dtype=np.int64)
+    load().orc_rmat_edges(scale, probs[0], probs[1], probs[2], seed, e_begin, e_end, _p64(src), _p64(dst))
+    return src, dst
+
+
+def person_mask(n: int) -> np.ndarray:
+    lib = load()
+    return np.array([lib.orc_is_person(i) for i in range(n)], dtype=np.uint8)
+
+
+def ages(ids: np.ndarray, seed: int = 42) -> np.ndarray:
+    lib = load()
+    return np.array([lib.orc_age(int(i), seed) for i in ids], dtype=np.int64)
+
+
+def row_hash(row) -> int:
+    a = np.ascontiguousarray(np.asarray(row, dtype=np.int64))
+    return load().orc_row_hash(_p64(a), len(a))
+
+
+def fingerprint(cols) -> tuple:
+    """(count, sum, xor) of row hashes over int64 columns (vectorised restatement of orc_row_hash)."""
+    cols = [np.asarray(c, dtype=np.int64).astype(np.uint64) for c in cols]
+    n = len(cols[0]) if cols else 0
+    h = np.full(n, 0x243F6A8885A308D3, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        for c in cols:
+            z = (h ^ c) + np.uint64(0x9E3779B97F4A7C15)
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            h = z ^ (z >> np.uint64(31))
+        s = int(h.sum(dtype=np.uint64)) if n else 0
+    x = int(np.bitwise_xor.reduce(h)) if n else 0
+    return n, s, x
+
+
+def two_hop_enumerate(n, src, dst, a_ok=None, b_ok=None, c_ok=None, grouped=False, threads=0):
+    lib = load()
+    rows, dist = ctypes.c_int64(), ctypes.c_int64()
+    grows = np.zeros(n, dtype=np.int64) if grouped else None
+    gdist = np.zeros(n, dtype=np.int64) if grouped else None
+    rc = lib.orc_two_hop_enumerate(n, len(src), _p64(src), _p64(dst), _p8(a_ok), _p8(b_ok), _p8(c_ok),
+                                   ctypes.byref(rows), ctypes.byref(dist), _p64(grows), _p64(gdist), threads)
+    if rc:
+        raise MemoryError("orc_two_hop_enumerate")
+    if grouped:
+        return rows.value, dist.value, grows, gdist
+    return rows.value, dist.value
+
+
+def two_hop_closed_form(n, src, dst, a_ok=None, b_ok=None, c_ok=None):
+    lib = load()
+    rows, dist = ctypes.c_int64(), ctypes.c_int64()
+    rc = lib.orc_two_hop_closed_form(n, len(src), _p64(src), _p64(dst), _p8(a_ok), _p8(b_ok), _p8(c_ok),
+                                     ctypes.byref(rows), ctypes.byref(dist))
+    if rc:
+        raise MemoryError("orc_two_hop_closed_form")
+    return rows.value, dist.value
+
+
+def expand_filter(src, dst, a_ok=None, b_ok=None):
+    lib = load()
+    rows, s, x = ctypes.c_int64(), ctypes.c_uint64(), ctypes.c_uint64()
+    lib.orc_expand_filter(len(src), _p64(src), _p64(dst), _p8(a_ok), _p8(b_ok), ctypes.byref(rows), ctypes.byref(s),
+                          ctypes.byref(x))
+    return rows.value, s.value, x.value
+
+
+def triangle_enumerate(n, src, dst, threads=0):
+    rows = ctypes.c_int64()
+    if load().orc_triangle_enumerate(n, len(src), _p64(src), _p64(dst), ctypes.byref(rows), threads):
+        raise MemoryError("orc_triangle_enumerate")
+    return rows.value
+
+
+def var_length_count(n, src, dst, lo, hi, threads=0):
+    rows = ctypes.c_int64()
+    g = np.zeros(n, dtype=np.int64)
+    rc = load().orc_var_length_count(n, len(src), _p64(src), _p64(dst), lo, hi, _p64(g), ctypes.byref(rows), threads)
+    if rc:
+        raise ValueError(f"orc_var_length_count rc={rc}")
+    return rows.value, g
