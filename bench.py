@@ -5,17 +5,24 @@
 
 Workload: R-MAT scale 26 (2^26 nodes, all Person), edge factor 16 (2^30
 relationships), (A,B,C,D) = (.57,.19,.19,.05), seed 42, self-loops and multi-edges kept.  The
-relationship table [id, source, target] (int64) is generated on the device; with N ranks each rank
-holds the relationships whose target falls in its owner range (one rank per GPU, strong scaling:
-the graph is fixed).  A step = the whole query from resident entity tables: node-scan bitmap
-build, hop 1, the RCCL all-gather of the hop-1 frontier (N > 1), hop 2, popcount, all-reduce.
+relationship table [id, source, target] (int64, generation order) is generated on the device; with N
+ranks each rank holds the relationships whose target falls in its owner range (one rank per GPU,
+strong scaling: the graph is fixed).
+
+A step = the whole query from the resident entity tables:
+  cold (the reported value): node-scan bitmap, radix partition of the relationship table,
+       hop 1, RCCL all-gather of the hop-1 frontier (N > 1), hop 2, popcount (+ all-reduce);
+  warm: the same with the partition kept from an earlier query (Cache analogue);
+  stream: no partition, both hops stream the table in generation order (comparison).
 
 metric value = matched rows / s, where matched rows = count(*) of the same MATCH, i.e. the bindings
-CAPS's joins would emit.  It is computed once in closed form (sum_b in(b)*out(b) - self-loops) on
-the device outside the timed region -- the query never enumerates them.
-Run: python bench.py [--gpus N --steps K --warmup W]  (torchrun for N > 1)
+CAPS's joins would emit.  It is computed once in closed form (sum_b in(b)*out(b) - self-loops) on the
+device outside the timed region; the query itself never enumerates bindings.
+Run: python bench.py [--gpus N --steps K --warmup W]  (torch.distributed.run for N > 1)
 """
 import argparse
+import ctypes
+import glob
 import json
 import os
 import sys
@@ -27,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "matched rows/sec for 2-hop MATCH on R-MAT 2^30 edges; % HBM roofline @1/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+KERNELS = ("part_hist", "part_scatter", "hop1", "hop2", "mid_combine", "bitmap_add")
 
 
 def parse():
@@ -36,8 +44,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--scale", type=int, default=26)
     p.add_argument("--edge-factor", type=int, default=16)
-    p.add_argument("--layout", choices=["ingest", "clustered"], default="ingest",
-                   help="ingest: rel rows in generation order; clustered: Cache-analogue copy sorted by target")
+    p.add_argument("--modes", default="cold,warm", help="comma list of cold, warm, stream (first = value)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-scale", type=int, default=20)
     return p.parse_args()
@@ -58,6 +65,22 @@ def cpu_baseline(scale, ef):
                       f"count(DISTINCT c)={dist}, {dt:.2f} s"}
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (profiles/*pmc*.json),
+    FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B reads at 64 B), or None."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+            k = d.get("kernels", {}).get(kernel)
+            if k and "hbm_bytes_per_launch" in k:
+                return k["hbm_bytes_per_launch"]
+        except (OSError, ValueError):
+            continue
+    return None
+
+
 def main():
     args = parse()
     import torch
@@ -66,34 +89,31 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit("run with torch.distributed.run for --gpus > 1")
+    if world == 1 and args.gpus > 1:
+        sys.exit("run with torch.distributed.run for --gpus > 1")
     distributed = world > 1
     torch.cuda.set_device(local)
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from capsmi import Session, graph
+    from capsmi import Session, _lib, graph
 
     sess = Session(local)
-    stream = torch.cuda.current_stream()
-    sess.set_stream(stream.cuda_stream)  # library kernels and RCCL collectives share one stream
+    sess.set_stream(torch.cuda.current_stream().cuda_stream)  # library kernels + RCCL on one stream
 
     scale, ef = args.scale, args.edge_factor
     n = 1 << scale
     m_total = ef << scale
     nw = (n + 31) // 32
-    assert nw % world == 0, "owner slices must be equal for all-gather"
+    assert nw % world == 0, "owner slices must be equal for the all-gather"
     wb, we = graph.owner_words(n, rank, world)
+    modes = [m.strip() for m in args.modes.split(",") if m.strip()]
 
-    # ---- ingest (untimed): partitioned relationship table + replicated Person node table ----------
+    # ---- ingest (untimed): partitioned relationship table + Person node table --------------------
     t0 = time.perf_counter()
     rels = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42,
                            part_col=graph.PART_TARGET if distributed else graph.PART_NONE, part=rank, nparts=world)
-    if args.layout == "clustered":
-        rels = graph.cluster_by(rels, "target", 0, n)
     persons = graph.rmat_nodes(sess, scale, graph.NODES_ALL)
     m_local = rels.size
     sess.sync()
@@ -103,15 +123,14 @@ def main():
     scratch = torch.zeros(nw, dtype=torch.int32, device="cuda")
     dstw = torch.zeros(nw, dtype=torch.int32, device="cuda")
     x1, x2 = mid[:nw], mid[nw:]
-    sl = slice(wb, we)
+    own = slice(wb, we)
+    cached = {}
 
-    def step():
-        p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")  # node scan of :Person (a, b, c)
-        graph.two_hop_mark_mid(sess, [rels], p, p, mid.data_ptr(), scratch.data_ptr())
-        if distributed:  # frontier exchange: every rank needs X1/X2 of every middle node b
-            dist.all_gather_into_tensor(x1, x1[sl].clone())
-            dist.all_gather_into_tensor(x2, x2[sl].clone())
-        graph.two_hop_mark_dst(sess, [rels], p, p, mid.data_ptr(), dstw.data_ptr())
+    def exchange_and_finish(p, mark_dst):
+        if distributed:  # hop-1 frontier: every rank needs X1/X2 of every middle node
+            dist.all_gather_into_tensor(x1, x1[own].clone())
+            dist.all_gather_into_tensor(x2, x2[own].clone())
+        mark_dst(p)
         local_cnt = graph.words_popcount(sess, dstw.data_ptr(), wb, we)
         if distributed:
             t = torch.tensor([local_cnt], dtype=torch.int64, device="cuda")
@@ -119,72 +138,96 @@ def main():
             return int(t.item())
         return local_cnt
 
-    for _ in range(args.warmup):
-        result = step()
+    def step_cold():
+        p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")  # node scan of :Person (a, b, c)
+        rp = graph.RelPartition(sess, [rels], 0, n)
+        rp.mark_mid(p, p, mid.data_ptr(), scratch.data_ptr())
+        r = exchange_and_finish(p, lambda q: rp.mark_dst(q, q, mid.data_ptr(), dstw.data_ptr()))
+        rp.release()
+        return r
 
-    # ---- timed region --------------------------------------------------------------------------
-    from capsmi import _lib
-    import ctypes
-    _lib.call("capsmi_session_set_profiling", sess.handle, 1)
-    for k in ("hop1", "hop2", "mid_combine", "bitmap_add"):
-        _lib.call("capsmi_session_kernel_time", sess.handle, k.encode(), ctypes.byref(ctypes.c_int64()),
-                  ctypes.byref(ctypes.c_double()))
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        result = step()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kt = {}
-    for k in ("hop1", "hop2", "mid_combine", "bitmap_add"):
-        cnt, ms = ctypes.c_int64(), ctypes.c_double()
-        _lib.call("capsmi_session_kernel_time", sess.handle, k.encode(), ctypes.byref(cnt), ctypes.byref(ms))
-        kt[k] = (cnt.value, ms.value)
-    _lib.call("capsmi_session_set_profiling", sess.handle, 0)
-    if distributed:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    def step_warm():
+        if "rp" not in cached:
+            cached["rp"] = graph.RelPartition(sess, [rels], 0, n)
+        rp = cached["rp"]
+        p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")
+        rp.mark_mid(p, p, mid.data_ptr(), scratch.data_ptr())
+        return exchange_and_finish(p, lambda q: rp.mark_dst(q, q, mid.data_ptr(), dstw.data_ptr()))
 
-    # ---- untimed checks: matched rows (closed form) and the unpartitioned answer on rank 0 -------
-    matched = None
-    check = None
-    if rank == 0:
+    def step_stream():
+        p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")
+        graph.two_hop_mark_mid(sess, [rels], p, p, mid.data_ptr(), scratch.data_ptr())
+        return exchange_and_finish(p, lambda q: graph.two_hop_mark_dst(sess, [rels], q, q, mid.data_ptr(),
+                                                                          dstw.data_ptr()))
+
+    steps = {"cold": step_cold, "warm": step_warm, "stream": step_stream}
+
+    def kernel_times():
+        out = {}
+        for k in KERNELS:
+            cnt, ms = ctypes.c_int64(), ctypes.c_double()
+            _lib.call("capsmi_session_kernel_time", sess.handle, k.encode(), ctypes.byref(cnt), ctypes.byref(ms))
+            out[k] = (cnt.value, ms.value)
+        return out
+
+    results = {}
+    for mode in modes:
+        step = steps[mode]
+        for _ in range(args.warmup):
+            res = step()
+        _lib.call("capsmi_session_set_profiling", sess.handle, 1)
+        kernel_times()  # reset
         if distributed:
-            full = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42)
-        else:
-            full = rels
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            res = step()
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        kt = kernel_times()
+        _lib.call("capsmi_session_set_profiling", sess.handle, 0)
+        if distributed:
+            tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
+        results[mode] = (elapsed / args.steps, res, kt)
+    if "rp" in cached:
+        cached["rp"].release()
+
+    # ---- untimed checks: matched rows (closed form) and the unpartitioned answer on rank 0 -----------
+    matched = check = None
+    if rank == 0:
+        full = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42) if distributed else rels
         p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")
         matched = graph.two_hop_count(sess, [full], p, p, p)
-        ref_distinct = graph.two_hop_count_distinct(sess, [full], p, p, p)
-        check = "ok" if ref_distinct == result else f"MISMATCH partitioned={result} full={ref_distinct}"
+        ref = graph.two_hop_count_distinct(sess, [full], p, p, p)
+        answers = {m: r[1] for m, r in results.items()}
+        check = "ok" if all(v == ref for v in answers.values()) else f"MISMATCH {answers} vs unpartitioned {ref}"
         del full
 
     if rank == 0:
-        ms_per_step = elapsed / args.steps * 1e3
-        hop2_n, hop2_ms = kt["hop2"]
-        hop1_n, hop1_ms = kt["hop1"]
-        avg2 = hop2_ms / max(hop2_n, 1)
-        avg1 = hop1_ms / max(hop1_n, 1)
-        # algorithmic bytes: a rel scan = E * (16 + 8 [rel id referenced by r1 <> r2]),
-        # a node scan = N * 8.  hop2 processes rel scan r2 + node scan c on this rank's rels.
-        alg2 = m_local * 24 + n * 8
-        alg1 = m_local * 24 + 2 * n * 8
-        dom, avg, alg = ("hop2", avg2, alg2) if avg2 >= avg1 else ("hop1", avg1, alg1)
-        achieved = alg / (avg * 1e-3) / 1e9
-        query_alg = 2 * 24 * m_total + 3 * 8 * n
+        head = modes[0]
+        sec, res, kt = results[head]
+        # per-kernel algorithmic bytes (this rank's rels): what each kernel must touch by its function
+        alg = {"part_hist": m_local * 8, "part_scatter": m_local * 24, "hop1": m_local * 8 + n // 8,
+               "hop2": m_local * 8 + n // 8 * 2, "mid_combine": n // 8 * 5, "bitmap_add": n * 8}
+        timed = {k: (c, ms) for k, (c, ms) in kt.items() if c > 0}
+        dom = max(timed, key=lambda k: timed[k][1])
+        avg_ms = timed[dom][1] / timed[dom][0]
+        achieved = alg[dom] / (avg_ms * 1e-3) / 1e9
+        traffic = pmc_traffic("k_" + dom if not dom.startswith("part") else "k_" + dom)
+        query_alg = 2 * 24 * m_total + 3 * 8 * n  # SURVEY.md §8d C3 B_alg (whole query, all ranks)
         line = {
             "metric": METRIC,
-            "value": matched / (elapsed / args.steps),
+            "value": matched / sec,
             "unit": "matched rows/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
+            "ms_per_step": sec * 1e3,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -192,23 +235,26 @@ def main():
             "data": "synthetic R-MAT (on-device counter-based generator, oracle/rmat.c definition)",
             "config": {"workload": "C3: MATCH (a:Person)-[:FRIEND_OF]->(b:Person)-[:FRIEND_OF]->(c:Person) "
                                    "RETURN count(DISTINCT c)",
-                       "scale": scale, "nodes": n, "relationships": m_total, "rmat": [0.57, 0.19, 0.19, 0.05],
-                       "seed": 42, "layout": args.layout,
+                       "mode": head, "scale": scale, "nodes": n, "relationships": m_total,
+                       "rmat": [0.57, 0.19, 0.19, 0.05], "seed": 42,
                        "parallelism": f"rels partitioned by owner(target) over {world} GPU(s); "
                                       "hop-1 frontier all-gather + count all-reduce over RCCL"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": f"k_{dom}",
-                         "kernel_ms": avg, "alg_bytes_per_launch": alg},
-            "query": {"count_distinct_c": result, "matched_rows": matched, "check_vs_unpartitioned": check,
-                      "hop1_ms": avg1, "hop2_ms": avg2,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_" + dom,
+                         "kernel_ms": avg_ms, "alg_bytes_per_launch": alg[dom]},
+            "query": {"count_distinct_c": res, "matched_rows": matched, "check_vs_unpartitioned": check,
                       "alg_bytes_query": query_alg,
-                      "alg_GBs_query_per_gpu": query_alg / world / (ms_per_step * 1e-3) / 1e9,
+                      "query_alg_GBs": query_alg / sec / 1e9,
+                      "query_frac_of_peak": query_alg / sec / 1e9 / (HBM_PEAK_GBS * world),
+                      "kernel_ms": {k: v[1] / v[0] for k, v in timed.items()},
                       "rels_local_rank0": m_local, "ingest_s": ingest_s},
         }
-        if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_scale, ef)
-        else:
-            line["cpu_baseline"] = None
+        for mode in modes[1:]:
+            s2, r2, kt2 = results[mode]
+            line["query"][mode] = {"ms_per_step": s2 * 1e3, "value": matched / s2, "count_distinct_c": r2,
+                                   "query_frac_of_peak": query_alg / s2 / 1e9 / (HBM_PEAK_GBS * world),
+                                   "kernel_ms": {k: v[1] / v[0] for k, v in kt2.items() if v[0] > 0}}
+        line["cpu_baseline"] = cpu_baseline(args.cpu_scale, ef) if (not args.no_cpu_baseline and world == 1) else None
         print(json.dumps(line), flush=True)
     sess.close()
     if distributed:

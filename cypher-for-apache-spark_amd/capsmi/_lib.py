@@ -118,6 +118,12 @@ _SIGS = {
     "capsmi_two_hop_mark_mid": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, P, c_void_p, c_void_p]),
     "capsmi_two_hop_mark_dst": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, P, c_void_p, c_void_p]),
     "capsmi_words_popcount": (c_int32, [P, c_void_p, c_int64, c_int64, POINTER(c_int64)]),
+    "capsmi_relpart_build": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, c_int64, c_int64, PP]),
+    "capsmi_relpart_size": (c_int32, [P, POINTER(c_int64)]),
+    "capsmi_relpart_release": (c_int32, [P]),
+    "capsmi_two_hop_mark_mid_part": (c_int32, [P, P, P, P, c_void_p, c_void_p]),
+    "capsmi_two_hop_mark_dst_part": (c_int32, [P, P, P, P, c_void_p, c_void_p]),
+    "capsmi_two_hop_count_distinct_part": (c_int32, [P, P, P, P, P, POINTER(c_int64)]),
     "capsmi_cluster_by": (c_int32, [P, c_char_p, c_int64, c_int64, PP]),
     "capsmi_rmat_rels": (c_int32, [P, c_int32, c_int64, c_int64, c_int32, c_int32, c_int32, c_uint64, c_int32,
                                    c_int32, c_int32, PP]),

@@ -112,6 +112,55 @@ def two_hop_mark_dst(session: Session, rels: Sequence[GpuTable], b_ok: NodeBitma
               dst_col.encode(), b_ok.handle, c_ok.handle, ctypes.c_void_p(mid_ptr), ctypes.c_void_p(dst_ptr))
 
 
+class RelPartition:
+    """Radix-partitioned relationship layout (include/capsmi.h capsmi_relpart_*): built per query
+    on the cold path, or kept across queries as the Cache analogue."""
+
+    def __init__(self, session: Session, rels: Sequence[GpuTable], lo: int, hi: int, src_col: str = "source",
+                 dst_col: str = "target"):
+        self.session = session
+        self._h = ctypes.c_void_p()
+        _lib.call("capsmi_relpart_build", session.handle, len(rels), _handles(rels), src_col.encode(),
+                  dst_col.encode(), lo, hi, ctypes.byref(self._h))
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def size(self) -> int:
+        v = ctypes.c_int64()
+        _lib.call("capsmi_relpart_size", self._h, ctypes.byref(v))
+        return v.value
+
+    def release(self) -> None:
+        if self._h:
+            _lib.call("capsmi_relpart_release", self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            if self._h and _lib._lib is not None:
+                _lib._lib.capsmi_relpart_release(self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+    def count_distinct(self, a_ok: NodeBitmap, b_ok: NodeBitmap, c_ok: NodeBitmap) -> int:
+        v = ctypes.c_int64()
+        _lib.call("capsmi_two_hop_count_distinct_part", self.session.handle, self._h, a_ok.handle, b_ok.handle,
+                  c_ok.handle, ctypes.byref(v))
+        return v.value
+
+    def mark_mid(self, a_ok: NodeBitmap, b_ok: NodeBitmap, mid_ptr: int, scratch_ptr: int) -> None:
+        _lib.call("capsmi_two_hop_mark_mid_part", self.session.handle, self._h, a_ok.handle, b_ok.handle,
+                  ctypes.c_void_p(mid_ptr), ctypes.c_void_p(scratch_ptr))
+
+    def mark_dst(self, b_ok: NodeBitmap, c_ok: NodeBitmap, mid_ptr: int, dst_ptr: int) -> None:
+        _lib.call("capsmi_two_hop_mark_dst_part", self.session.handle, self._h, b_ok.handle, c_ok.handle,
+                  ctypes.c_void_p(mid_ptr), ctypes.c_void_p(dst_ptr))
+
+
 def words_popcount(session: Session, words_ptr: int, w_begin: int, w_end: int) -> int:
     v = ctypes.c_int64()
     _lib.call("capsmi_words_popcount", session.handle, ctypes.c_void_p(words_ptr), w_begin, w_end, ctypes.byref(v))

@@ -112,12 +112,22 @@ def _column(name: str, ty: int, values: Sequence, encode) -> ColumnData:
     return ColumnData(name, ty, arr.reshape(n), None if valid.all() else valid)
 
 
+# physical column names of the entity keys (CAPS keeps them apart from property columns too:
+# EntityMapping.allSourceKeys = idKeys ++ labels ++ relType ++ properties, EntityMapping.scala:50)
+ID, SRC, DST = "__id", "__source", "__target"
+
+
 @dataclass
 class EntityTable:
+    """A node or relationship table plus its mapping (NodeMapping / RelationshipMapping analogue,
+    okapi-api/.../io/conversion/{Node,Relationship}Mapping.scala)."""
     kind: str                   # "node" | "rel"
     labels: FrozenSet[str]      # node: implied labels; rel: {type}
-    props: Dict[str, int]       # key -> type
-    table: object               # backend table with columns id[, source, target] + props
+    props: Dict[str, int]       # property key -> type (column name = key)
+    table: object               # backend table
+    id_col: str = ID
+    src_col: str = SRC
+    dst_col: str = DST
 
 
 class ScanGraph:
@@ -140,7 +150,7 @@ class ScanGraph:
         for labels in sorted(combos, key=lambda s: sorted(s)):
             ns = combos[labels]
             pt = _prop_types(ns)
-            cols = [_column("id", I64, [n.id for n in ns], enc)]
+            cols = [_column(ID, I64, [n.id for n in ns], enc)]
             for k in sorted(pt):
                 cols.append(_column(k, pt[k], [n.props.get(k) for n in ns], enc))
             nodes.append(EntityTable("node", labels, pt, backend.table(cols)))
@@ -151,8 +161,8 @@ class ScanGraph:
         for t in sorted(types):
             rs = types[t]
             pt = _prop_types(rs)
-            cols = [_column("id", I64, [r.id for r in rs], enc), _column("source", I64, [r.src for r in rs], enc),
-                    _column("target", I64, [r.dst for r in rs], enc)]
+            cols = [_column(ID, I64, [r.id for r in rs], enc), _column(SRC, I64, [r.src for r in rs], enc),
+                    _column(DST, I64, [r.dst for r in rs], enc)]
             for k in sorted(pt):
                 cols.append(_column(k, pt[k], [r.props.get(k) for r in rs], enc))
             rels.append(EntityTable("rel", frozenset([t]), pt, backend.table(cols)))
@@ -174,7 +184,7 @@ class ScanGraph:
             return self._empty([(var, I64)] + [(f"{var}:{l}", BOOL) for l in all_labels]), header
         ops = []
         for t in sel:
-            cols = [(Col("id"), var)]
+            cols = [(Col(t.id_col), var)]
             cols += [(Lit(l in t.labels), f"{var}:{l}") for l in all_labels]
             cols += [(Col(k) if k in t.props else Lit(None, props[k]), f"{var}.{k}") for k in sorted(props)]
             ops.append(t.table.withColumns(*cols).select(*header))
@@ -198,7 +208,7 @@ class ScanGraph:
         ops = []
         for t in sel:
             (ty_name,) = tuple(t.labels)
-            cols = [(Col("id"), var), (Col("source"), f"{var}.__src"), (Col("target"), f"{var}.__dst"),
+            cols = [(Col(t.id_col), var), (Col(t.src_col), f"{var}.__src"), (Col(t.dst_col), f"{var}.__dst"),
                     (Lit(ty_name), f"{var}.__type")]
             cols += [(Col(k) if k in t.props else Lit(None, props[k]), f"{var}.{k}") for k in sorted(props)]
             ops.append(t.table.withColumns(*cols).select(*header))
@@ -551,6 +561,8 @@ class Planner:
                 if k >= lower and upper >= 1:
                     paths.append((add_target(o, k, "out").unionAll(add_target(n_, k, "in")), k))
 
+        if upper == 0:  # `*0`: only the zero-length copy (VarLengthExpandPlanner.scala:150-152)
+            paths = []
         target_header = cur.header + [c for i in range(1, upper + 1) for c in seg_cols(i)] + ([] if into else nh)
         aligned = []
         for t, k in paths:

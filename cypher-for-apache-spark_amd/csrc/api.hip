@@ -788,7 +788,7 @@ capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, 
             }
             case CAPSMI_AGG_AVG: {
                 REQUIRE(in->type == CAPSMI_I64 || in->type == CAPSMI_F64, CAPSMI_ERR_ILLEGAL_ARGUMENT, "avg of non-number");
-                c.type = CAPSMI_F64;
+                c.type = in->type;  // avg(..).cast(cypherType): integer averages come back as Long
                 c.valid = dev_alloc(ng, st);
                 Buf sum = dev_alloc(sizeof(double) * ng, st), cnt = dev_alloc(sizeof(int64_t) * ng, st), seen = dev_alloc(ng, st);
                 HIP_CHECK(hipMemsetAsync(P<void>(sum), 0, sizeof(double) * ng, st));
@@ -802,7 +802,8 @@ capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, 
                     agg_sum_f64(P<int64_t>(gid), in->d(), in->v(), n, P<double>(sum), P<uint8_t>(seen), st);
                 }
                 agg_count(P<int64_t>(gid), in->v(), n, P<int64_t>(cnt), st);
-                avg_finish(P<double>(sum), P<int64_t>(cnt), ng, P<int64_t>(c.data), P<uint8_t>(c.valid), st);
+                avg_finish(P<double>(sum), P<int64_t>(cnt), ng, in->type == CAPSMI_I64, P<int64_t>(c.data),
+                           P<uint8_t>(c.valid), st);
                 break;
             }
             default:
@@ -927,6 +928,35 @@ capsmi_status capsmi_expand_filter(capsmi_session* s, capsmi_table* rels, const 
     API_END
 }
 
+static bool same_domain(const capsmi_bitmap* a, const capsmi_bitmap* b, const capsmi_bitmap* c) {
+    return a->lo == b->lo && a->hi == b->hi && b->lo == c->lo && b->hi == c->hi && b->hi > b->lo &&
+           (uint64_t)(b->hi - b->lo) <= (uint64_t(1) << 32);
+}
+
+static void build_part(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                       const char* dst_col, int64_t lo, int64_t hi, RelPart& rp) {
+    std::vector<const int64_t*> srcs, dsts;
+    std::vector<int64_t> ms;
+    for (int i = 0; i < nrels; ++i) {
+        need(rels[i], "rels[i]");
+        srcs.push_back(rel_col(rels[i], src_col).d());
+        dsts.push_back(rel_col(rels[i], dst_col).d());
+        ms.push_back(rels[i]->nrows);
+    }
+    relpart_build(s, srcs.data(), dsts.data(), ms.data(), nrels, lo, hi, rp);
+}
+
+// hop 1 on a partitioned layout into X1 (= M | S1) and X2 (= M | S2); S1 scratch
+static void part_mid(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* a, const capsmi_bitmap* b, uint32_t* X1,
+                     uint32_t* X2, uint32_t* S1) {
+    const int64_t nw = b->nwords;
+    HIP_CHECK(hipMemsetAsync(X1, 0, sizeof(uint32_t) * nw, s->stream));
+    HIP_CHECK(hipMemsetAsync(X2, 0, sizeof(uint32_t) * nw, s->stream));
+    HIP_CHECK(hipMemsetAsync(S1, 0, sizeof(uint32_t) * nw, s->stream));
+    relpart_hop1(s, rp, a, b, X1, S1, X2);
+    graph::mid_combine(s, X1, X2, S1, nw);
+}
+
 static void two_hop_mid(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
                         const char* dst_col, const capsmi_bitmap* a, const capsmi_bitmap* b, uint32_t* X1, uint32_t* X2,
                         uint32_t* S1) {
@@ -969,9 +999,111 @@ capsmi_status capsmi_two_hop_count_distinct(capsmi_session* s, int32_t nrels, ca
     Buf x = dev_alloc(sizeof(uint32_t) * nw * 3, s->stream);
     Buf cw = dev_alloc(sizeof(uint32_t) * (c_ok->nwords > 0 ? c_ok->nwords : 1), s->stream);
     uint32_t* X1 = P<uint32_t>(x);
-    two_hop_mid(s, nrels, rels, src_col, dst_col, a_ok, b_ok, X1, X1 + nw, X1 + 2 * nw);
-    two_hop_dst(s, nrels, rels, src_col, dst_col, b_ok, c_ok, X1, X1 + nw, P<uint32_t>(cw));
+    if (same_domain(a_ok, b_ok, c_ok)) {
+        // cold radix-partitioned path: partition + two LDS-resident hops
+        RelPart rp;
+        build_part(s, nrels, rels, src_col, dst_col, b_ok->lo, b_ok->hi, rp);
+        part_mid(s, rp, a_ok, b_ok, X1, X1 + nw, X1 + 2 * nw);
+        HIP_CHECK(hipMemsetAsync(P<void>(cw), 0, sizeof(uint32_t) * c_ok->nwords, s->stream));
+        relpart_hop2(s, rp, c_ok, X1, X1 + nw, P<uint32_t>(cw));
+    } else {
+        two_hop_mid(s, nrels, rels, src_col, dst_col, a_ok, b_ok, X1, X1 + nw, X1 + 2 * nw);
+        two_hop_dst(s, nrels, rels, src_col, dst_col, b_ok, c_ok, X1, X1 + nw, P<uint32_t>(cw));
+    }
     *out_distinct = words_popcount(s, P<uint32_t>(cw), 0, c_ok->nwords);
+    API_END
+}
+
+}  // extern "C"
+
+struct capsmi_relpart {
+    capsmi_session* sess = nullptr;
+    capsmi::RelPart rp;
+};
+
+extern "C" {
+
+capsmi_status capsmi_relpart_build(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                                   const char* dst_col, int64_t id_lo, int64_t id_hi, capsmi_relpart** out) {
+    API_BEGIN
+    need(s, "session");
+    need(out, "out");
+    REQUIRE(nrels >= 0 && (nrels == 0 || rels), CAPSMI_ERR_ILLEGAL_ARGUMENT, "rels");
+    use_device(s);
+    auto* p = new capsmi_relpart();
+    std::unique_ptr<capsmi_relpart> guard(p);
+    p->sess = s;
+    build_part(s, nrels, rels, src_col, dst_col, id_lo, id_hi, p->rp);
+    *out = guard.release();
+    API_END
+}
+
+capsmi_status capsmi_relpart_size(const capsmi_relpart* p, int64_t* kept_rows) {
+    API_BEGIN
+    need(p, "relpart");
+    need(kept_rows, "out");
+    *kept_rows = p->rp.kept;
+    API_END
+}
+
+capsmi_status capsmi_relpart_release(capsmi_relpart* p) {
+    API_BEGIN
+    if (p) {
+        use_device(p->sess);
+        delete p;
+    }
+    API_END
+}
+
+capsmi_status capsmi_two_hop_mark_mid_part(capsmi_session* s, const capsmi_relpart* p, const capsmi_bitmap* a_ok,
+                                           const capsmi_bitmap* b_ok, uint32_t* mid_words, uint32_t* scratch_words) {
+    API_BEGIN
+    need(s, "session");
+    need(p, "relpart");
+    need(mid_words, "mid_words");
+    need(scratch_words, "scratch_words");
+    check_bitmap(a_ok, "a_ok");
+    check_bitmap(b_ok, "b_ok");
+    use_device(s);
+    part_mid(s, p->rp, a_ok, b_ok, mid_words, mid_words + b_ok->nwords, scratch_words);
+    API_END
+}
+
+capsmi_status capsmi_two_hop_mark_dst_part(capsmi_session* s, const capsmi_relpart* p, const capsmi_bitmap* b_ok,
+                                           const capsmi_bitmap* c_ok, const uint32_t* mid_words, uint32_t* dst_words) {
+    API_BEGIN
+    need(s, "session");
+    need(p, "relpart");
+    need(mid_words, "mid_words");
+    need(dst_words, "dst_words");
+    check_bitmap(b_ok, "b_ok");
+    check_bitmap(c_ok, "c_ok");
+    REQUIRE(b_ok->lo == c_ok->lo && b_ok->hi == c_ok->hi, CAPSMI_ERR_UNSUPPORTED, "b and c scans need one id domain");
+    use_device(s);
+    HIP_CHECK(hipMemsetAsync(dst_words, 0, sizeof(uint32_t) * c_ok->nwords, s->stream));
+    relpart_hop2(s, p->rp, c_ok, mid_words, mid_words + b_ok->nwords, dst_words);
+    API_END
+}
+
+capsmi_status capsmi_two_hop_count_distinct_part(capsmi_session* s, const capsmi_relpart* p, const capsmi_bitmap* a_ok,
+                                                 const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok,
+                                                 int64_t* out_distinct) {
+    API_BEGIN
+    need(s, "session");
+    need(p, "relpart");
+    need(out_distinct, "out");
+    check_bitmap(a_ok, "a_ok");
+    check_bitmap(b_ok, "b_ok");
+    check_bitmap(c_ok, "c_ok");
+    REQUIRE(same_domain(a_ok, b_ok, c_ok), CAPSMI_ERR_UNSUPPORTED, "a, b, c scans need one id domain");
+    use_device(s);
+    const int64_t nw = b_ok->nwords > 0 ? b_ok->nwords : 1;
+    Buf x = dev_alloc(sizeof(uint32_t) * nw * 4, s->stream);
+    uint32_t* X1 = P<uint32_t>(x);
+    part_mid(s, p->rp, a_ok, b_ok, X1, X1 + nw, X1 + 2 * nw);
+    HIP_CHECK(hipMemsetAsync(X1 + 3 * nw, 0, sizeof(uint32_t) * nw, s->stream));
+    relpart_hop2(s, p->rp, c_ok, X1, X1 + nw, X1 + 3 * nw);
+    *out_distinct = words_popcount(s, X1 + 3 * nw, 0, c_ok->nwords);
     API_END
 }
 

@@ -178,7 +178,7 @@ void agg_sum_f64(const int64_t* gid, const int64_t* v, const uint8_t* valid, int
                  uint8_t* seen, hipStream_t st);
 void agg_minmax(const int64_t* gid, const int64_t* v, const uint8_t* valid, int64_t n, int type, bool is_max,
                 int64_t* out, uint8_t* seen, hipStream_t st);
-void avg_finish(const double* sum, const int64_t* cnt, int64_t ng, int64_t* out, uint8_t* valid,
+void avg_finish(const double* sum, const int64_t* cnt, int64_t ng, bool to_i64, int64_t* out, uint8_t* valid,
                 hipStream_t st);
 void minmax_finish(int64_t* v, int type, bool is_max, int64_t ng, hipStream_t st);
 void cross_pairs(int64_t nl, int64_t nr, int64_t* out_l, int64_t* out_r, hipStream_t st);
@@ -196,6 +196,26 @@ void radix_sort_pairs(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t 
                       int end_bit);
 void order_keys(capsmi_session* s, const int64_t* col, const uint8_t* valid, int type, bool desc, bool null_pass,
                 const int64_t* perm, int64_t n, uint64_t* key);
+
+// partitioned relationship layout (k_part.hip)
+struct PartLayout {
+    int64_t lo, hi;  // id domain of both endpoints
+    int nslices;     // target slices of 2^19 ids
+    int sx_shift;    // source super-slice = (src - lo) >> sx_shift  (< 8, one per XCD)
+    int nbuckets;    // 8 * nslices
+};
+struct RelPart {
+    PartLayout L;
+    Buf pairs;  // uint2 (source - lo, target - lo) per kept relationship, grouped by bucket
+    Buf boff;   // int64 bucket offsets (nbuckets + 1)
+    int64_t kept = 0;
+};
+void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
+                   int64_t lo, int64_t hi, RelPart& rp);
+void relpart_hop1(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* a, const capsmi_bitmap* b, uint32_t* M,
+                  uint32_t* S1, uint32_t* S2);
+void relpart_hop2(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* c, const uint32_t* X1, const uint32_t* X2,
+                  uint32_t* C);
 
 // graph (k_graph.hip)
 void bitmap_add_rows(capsmi_bitmap* b, const int64_t* ids, const uint8_t* ids_valid,

@@ -217,11 +217,13 @@ __global__ void k_minmax_finish(int64_t* v, int64_t ng) {
         v[g] = f64_key(v[g]);  // the image is an involution
 }
 
+// avg(..).cast(cypherType) (SparkTable.scala:141-146): an integer input's average is cast back to Long
 __global__ void k_avg_finish(const double* __restrict__ sum, const int64_t* __restrict__ cnt, int64_t ng,
-                             int64_t* __restrict__ out, uint8_t* __restrict__ valid) {
+                             int to_i64, int64_t* __restrict__ out, uint8_t* __restrict__ valid) {
     for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += (int64_t)gridDim.x * blockDim.x) {
         const int64_t c = cnt[g];
-        out[g] = c > 0 ? __double_as_longlong(sum[g] / (double)c) : 0;
+        const double a = c > 0 ? sum[g] / (double)c : 0.0;
+        out[g] = to_i64 ? (int64_t)a : __double_as_longlong(a);
         valid[g] = c > 0 ? 1 : 0;
     }
 }
@@ -367,9 +369,10 @@ void minmax_finish(int64_t* v, int type, bool, int64_t ng, hipStream_t st) {
     HIP_CHECK(hipGetLastError());
 }
 
-void avg_finish(const double* sum, const int64_t* cnt, int64_t ng, int64_t* out, uint8_t* valid, hipStream_t st) {
+void avg_finish(const double* sum, const int64_t* cnt, int64_t ng, bool to_i64, int64_t* out, uint8_t* valid,
+                hipStream_t st) {
     if (ng <= 0) return;
-    hipLaunchKernelGGL(k_avg_finish, dim3(grid_for(ng)), dim3(256), 0, st, sum, cnt, ng, out, valid);
+    hipLaunchKernelGGL(k_avg_finish, dim3(grid_for(ng)), dim3(256), 0, st, sum, cnt, ng, to_i64 ? 1 : 0, out, valid);
     HIP_CHECK(hipGetLastError());
 }
 

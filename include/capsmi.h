@@ -259,6 +259,24 @@ capsmi_status capsmi_two_hop_mark_mid(capsmi_session* s, int32_t nrels, capsmi_t
 capsmi_status capsmi_two_hop_mark_dst(capsmi_session* s, int32_t nrels, capsmi_table* const* rels,
                                       const char* src_col, const char* dst_col, const capsmi_bitmap* b_ok,
                                       const capsmi_bitmap* c_ok, const uint32_t* mid_words, uint32_t* dst_words);
+/* Radix-partitioned relationship layout for the 2-hop kernels: rows of the union of `rels` with both
+ * endpoints in [id_lo, id_hi) (hi - lo <= 2^32), packed to 32-bit ids and bucketed by
+ * (source super-slice per XCD) x (target slice of 2^19 ids).  Building it is part of the cold query;
+ * keeping it across queries is the Cache analogue (DataFrameTable.cache, SparkTable.scala:240-246). */
+typedef struct capsmi_relpart capsmi_relpart;
+capsmi_status capsmi_relpart_build(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                                   const char* dst_col, int64_t id_lo, int64_t id_hi, capsmi_relpart** out);
+capsmi_status capsmi_relpart_size(const capsmi_relpart* p, int64_t* kept_rows);
+capsmi_status capsmi_relpart_release(capsmi_relpart* p);
+/* the phased 2-hop over a partitioned layout (same contract as capsmi_two_hop_mark_mid/_dst) */
+capsmi_status capsmi_two_hop_mark_mid_part(capsmi_session* s, const capsmi_relpart* p, const capsmi_bitmap* a_ok,
+                                           const capsmi_bitmap* b_ok, uint32_t* mid_words, uint32_t* scratch_words);
+capsmi_status capsmi_two_hop_mark_dst_part(capsmi_session* s, const capsmi_relpart* p, const capsmi_bitmap* b_ok,
+                                           const capsmi_bitmap* c_ok, const uint32_t* mid_words, uint32_t* dst_words);
+/* whole query over a cached layout */
+capsmi_status capsmi_two_hop_count_distinct_part(capsmi_session* s, const capsmi_relpart* p, const capsmi_bitmap* a_ok,
+                                                 const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok,
+                                                 int64_t* out_distinct);
 /* popcount of words [w_begin, w_end) of a device bitmap, result in *out (host) */
 capsmi_status capsmi_words_popcount(capsmi_session* s, const uint32_t* words, int64_t w_begin, int64_t w_end,
                                     int64_t* out);

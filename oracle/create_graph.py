@@ -19,7 +19,7 @@ from typing import Dict, List, Tuple
 
 _TOKEN = re.compile(r"""\s*(?:
     (?P<str>'(?:[^'\\]|\\.)*'|"(?:[^"\\]|\\.)*")
-  | (?P<num>-?\d+(?:\.\d+)?(?:[eE][-+]?\d+)?L?)
+  | (?P<num>-?\d+(?:\.\d+)?(?:[eE][-+]?\d+)?[LDF]?)
   | (?P<arrow><-|->)
   | (?P<punct>[()\[\]{}:,\-])
   | (?P<word>[A-Za-z_][A-Za-z_0-9]*)
@@ -80,8 +80,9 @@ class _Parser:
             return v[1:-1].encode().decode("unicode_escape")
         if k == "num":
             self.i += 1
-            v = v.rstrip("L")
-            return float(v) if any(c in v for c in ".eE") else int(v)
+            is_float = v[-1] in "DF" or any(c in v for c in ".eE")
+            v = v.rstrip("LDF")
+            return float(v) if is_float else int(v)
         if k == "word" and v.lower() in ("true", "false", "null"):
             self.i += 1
             return {"true": True, "false": False, "null": None}[v.lower()]

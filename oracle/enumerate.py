@@ -308,7 +308,12 @@ def project(g: Graph, rows: List[dict], ret: dict) -> List[dict]:
                 row[a] = max(vals) if vals else None
             elif s[0] == "sum":
                 row[a] = sum(vals) if vals else None
-            elif s[0] == "avg":
-                row[a] = (sum(vals) / len(vals)) if vals else None
+            elif s[0] == "avg":  # avg(..).cast(cypherType): integer input -> Long (truncated)
+                if not vals:
+                    row[a] = None
+                elif all(isinstance(v, int) and not isinstance(v, bool) for v in vals):
+                    row[a] = int(sum(vals) / len(vals))
+                else:
+                    row[a] = sum(vals) / len(vals)
         out.append(row)
     return out

@@ -236,7 +236,10 @@ class NumpyTable:
                     cnt = np.bincount(g, minlength=ng)
                     with np.errstate(invalid="ignore", divide="ignore"):
                         res = np.where(cnt > 0, acc / np.maximum(cnt, 1), 0.0)
-                    out[name] = Col_(F64, res, seen)
+                    if c.type == I64:  # avg(..).cast(cypherType): an integer average is cast back to Long
+                        out[name] = Col_(I64, np.trunc(res).astype(np.int64), seen)
+                    else:
+                        out[name] = Col_(F64, res, seen)
                 else:
                     if c.type == F64:
                         acc = np.full(ng, np.inf if kind == "min" else -np.inf)

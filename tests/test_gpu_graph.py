@@ -97,6 +97,52 @@ def test_two_hop_self_loop_rules(session):
     assert graph.two_hop_count_distinct(session, [t1, t2], bm, bm, bm) == dist
 
 
+@pytest.mark.parametrize("scale,kind", [(8, "all"), (12, "person"), (15, "all"), (16, "person")])
+def test_two_hop_partitioned(session, scale, kind):
+    """Radix-partitioned layout (cold and cached) vs the oracle; more than one target slice at 2^20+."""
+    from capsmi import graph
+    n = 1 << scale
+    rels = _rels(session, scale)
+    bm, _ = _bitmaps(session, scale, kind)
+    src, dst = cpu.rmat_edges(scale, 0, 16 << scale)
+    mask = None if kind == "all" else cpu.person_mask(n)
+    rows, dist = cpu.two_hop_closed_form(n, src, dst, mask, mask, mask)
+    rp = graph.RelPartition(session, [rels], 0, n)
+    assert rp.size == 16 << scale
+    assert rp.count_distinct(bm, bm, bm) == dist
+    assert graph.two_hop_count_distinct(session, [rels], bm, bm, bm) == dist
+
+
+def test_two_hop_partitioned_multislice(session):
+    """id domain of 2^21 (4 target slices, all 8 source super-slices) with a sparse edge set,
+    plus ids outside the domain that the partition must drop."""
+    from capsmi import ColumnData, I64, graph
+    rng = np.random.default_rng(5)
+    n = 1 << 21
+    m = 200000
+    src = rng.integers(0, n, m)
+    dst = rng.integers(0, n, m)
+    hubs = rng.integers(0, n, 50)
+    src[: m // 4] = hubs[rng.integers(0, 50, m // 4)]
+    dst[m // 4: m // 2] = hubs[rng.integers(0, 50, m // 4)]
+    src[:20] = dst[:20]  # self-loops
+    src[20:30] = dst[20:30] = dst[10]
+    outside = np.array([n + 5, -3, 7], dtype=np.int64)
+    s_all = np.concatenate([src, outside, [1, 2]])
+    d_all = np.concatenate([dst, [4, 5, n + 1], outside[:2]])
+    t = session.table([ColumnData("id", I64, np.arange(len(s_all))), ColumnData("source", I64, s_all),
+                       ColumnData("target", I64, d_all)])
+    person = (rng.random(n) < 0.8).astype(np.uint8)
+    nodes = session.table([ColumnData("id", I64, np.nonzero(person)[0])])
+    bm = graph.NodeBitmap(session, 0, n).add_scan(nodes)
+    keep = (s_all >= 0) & (s_all < n) & (d_all >= 0) & (d_all < n)
+    rows, dist = cpu.two_hop_closed_form(n, s_all[keep], d_all[keep], person, person, person)
+    rp = graph.RelPartition(session, [t], 0, n)
+    assert rp.size == int(keep.sum())
+    assert rp.count_distinct(bm, bm, bm) == dist
+    assert graph.two_hop_count_distinct(session, [t], bm, bm, bm) == dist
+
+
 def test_two_hop_phased_matches_fused(session):
     """The multi-GPU phase entry points, run as one 'rank', equal the fused call."""
     import torch
