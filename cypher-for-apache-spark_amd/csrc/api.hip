@@ -1038,6 +1038,50 @@ capsmi_status capsmi_relpart_build(capsmi_session* s, int32_t nrels, capsmi_tabl
     API_END
 }
 
+capsmi_status capsmi_var_length_count(capsmi_session* s, int32_t nrels, capsmi_table* const* rels,
+                                      const char* src_col, const char* dst_col, const capsmi_bitmap* a_ok,
+                                      const capsmi_bitmap* b_ok, int32_t lower, int32_t upper, const char* id_name,
+                                      const char* count_name, capsmi_table** out) {
+    API_BEGIN
+    need(s, "session");
+    need(out, "out");
+    need(id_name, "id_name");
+    need(count_name, "count_name");
+    check_bitmap(a_ok, "a_ok");
+    check_bitmap(b_ok, "b_ok");
+    REQUIRE(nrels >= 0 && (nrels == 0 || rels), CAPSMI_ERR_ILLEGAL_ARGUMENT, "rels");
+    REQUIRE(lower >= 1 && lower <= upper && upper <= 3, CAPSMI_ERR_NOT_IMPLEMENTED,
+            "fused var-length count supports 1 <= lower <= upper <= 3 (use the join plan otherwise)");
+    REQUIRE(a_ok->lo == b_ok->lo && a_ok->hi == b_ok->hi, CAPSMI_ERR_UNSUPPORTED, "a and b scans need one id domain");
+    REQUIRE(!a_ok->any_dup && !b_ok->any_dup, CAPSMI_ERR_UNSUPPORTED,
+            "fused count(*) needs each node id in one scanned row");
+    REQUIRE(std::string(id_name) != count_name, CAPSMI_ERR_ILLEGAL_ARGUMENT, "output names must differ");
+    use_device(s);
+    std::vector<const int64_t*> srcs, dsts;
+    std::vector<int64_t> ms;
+    for (int i = 0; i < nrels; ++i) {
+        need(rels[i], "rels[i]");
+        srcs.push_back(rel_col(rels[i], src_col).d());
+        dsts.push_back(rel_col(rels[i], dst_col).d());
+        ms.push_back(rels[i]->nrows);
+    }
+    Buf ids, cnt;
+    const int64_t rows =
+        var_length_count(s, srcs.data(), dsts.data(), ms.data(), nrels, a_ok, b_ok, lower, upper, ids, cnt);
+    auto* o = new_table(s, rows);
+    Column a, c;
+    a.name = id_name;
+    a.type = CAPSMI_I64;
+    a.data = ids;
+    c.name = count_name;
+    c.type = CAPSMI_I64;
+    c.data = cnt;
+    o->cols.push_back(std::move(a));
+    o->cols.push_back(std::move(c));
+    *out = o;
+    API_END
+}
+
 capsmi_status capsmi_relpart_size(const capsmi_relpart* p, int64_t* kept_rows) {
     API_BEGIN
     need(p, "relpart");

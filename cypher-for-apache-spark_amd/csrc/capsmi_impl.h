@@ -138,6 +138,7 @@ void gather_col(const int64_t* src, const uint8_t* src_valid, const int64_t* idx
                 int64_t* dst, uint8_t* dst_valid, hipStream_t st);
 int64_t read_scalar(capsmi_session* s, const int64_t* dev);
 void invert_u8(const uint8_t* a, uint8_t* b, int64_t n, hipStream_t st);
+void add_i64(int64_t* p, int64_t v, int64_t n, hipStream_t st);
 void i64_to_f64(const int64_t* a, int64_t* b, int64_t n, hipStream_t st);
 
 // hashing & grouping (k_hash.hip)
@@ -216,6 +217,11 @@ void relpart_hop1(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* a, 
                   uint32_t* S1, uint32_t* S2);
 void relpart_hop2(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* c, const uint32_t* X1, const uint32_t* X2,
                   uint32_t* C);
+
+// fused var-length grouped count (k_varlen.hip)
+int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
+                         int nt, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, int lower, int upper,
+                         Buf& out_ids, Buf& out_cnt);
 
 // graph (k_graph.hip)
 void bitmap_add_rows(capsmi_bitmap* b, const int64_t* ids, const uint8_t* ids_valid,

@@ -244,3 +244,18 @@ void i64_to_f64(const int64_t* a, int64_t* b, int64_t n, hipStream_t st) {
     HIP_CHECK(hipGetLastError());
 }
 }  // namespace capsmi
+
+namespace capsmi {
+namespace {
+__global__ void k_add_i64(int64_t* p, int64_t v, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        p[i] += v;
+}
+}  // namespace
+
+void add_i64(int64_t* p, int64_t v, int64_t n, hipStream_t st) {
+    if (n <= 0 || v == 0) return;
+    hipLaunchKernelGGL(k_add_i64, dim3(grid_for(n)), dim3(256), 0, st, p, v, n);
+    HIP_CHECK(hipGetLastError());
+}
+}  // namespace capsmi

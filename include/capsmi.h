@@ -277,6 +277,14 @@ capsmi_status capsmi_two_hop_mark_dst_part(capsmi_session* s, const capsmi_relpa
 capsmi_status capsmi_two_hop_count_distinct_part(capsmi_session* s, const capsmi_relpart* p, const capsmi_bitmap* a_ok,
                                                  const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok,
                                                  int64_t* out_distinct);
+/* BoundedVarLengthExpand + grouped count, fused (C5):
+ *   MATCH (a)-[r*lower..upper]->(b) WHERE a_ok(a) AND b_ok(b) RETURN id(a) AS <id_name>, count(*) AS <count_name>
+ * with edge-distinct paths (VarLengthExpandPlanner.scala:83-136, 179-180), 1 <= lower <= upper <= 3.
+ * One output row per a with at least one path.  a_ok and b_ok must share one id domain. */
+capsmi_status capsmi_var_length_count(capsmi_session* s, int32_t nrels, capsmi_table* const* rels,
+                                      const char* src_col, const char* dst_col, const capsmi_bitmap* a_ok,
+                                      const capsmi_bitmap* b_ok, int32_t lower, int32_t upper, const char* id_name,
+                                      const char* count_name, capsmi_table** out);
 /* popcount of words [w_begin, w_end) of a device bitmap, result in *out (host) */
 capsmi_status capsmi_words_popcount(capsmi_session* s, const uint32_t* words, int64_t w_begin, int64_t w_end,
                                     int64_t* out);

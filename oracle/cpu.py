@@ -48,8 +48,8 @@ def load():
         lib.orc_triangle_enumerate.restype = ctypes.c_int
         lib.orc_triangle_enumerate.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, I64P, ctypes.c_int]
         lib.orc_var_length_count.restype = ctypes.c_int
-        lib.orc_var_length_count.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, ctypes.c_int, ctypes.c_int,
-                                             I64P, I64P, ctypes.c_int]
+        lib.orc_var_length_count.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, U8P, U8P, ctypes.c_int,
+                                             ctypes.c_int, I64P, I64P, ctypes.c_int]
         _lib = lib
     return _lib
 
@@ -144,10 +144,11 @@ def triangle_enumerate(n, src, dst, threads=0):
     return rows.value
 
 
-def var_length_count(n, src, dst, lo, hi, threads=0):
+def var_length_count(n, src, dst, lo, hi, a_ok=None, b_ok=None, threads=0):
     rows = ctypes.c_int64()
     g = np.zeros(n, dtype=np.int64)
-    rc = load().orc_var_length_count(n, len(src), _p64(src), _p64(dst), lo, hi, _p64(g), ctypes.byref(rows), threads)
+    rc = load().orc_var_length_count(n, len(src), _p64(src), _p64(dst), _p8(a_ok), _p8(b_ok), lo, hi, _p64(g),
+                                     ctypes.byref(rows), threads)
     if rc:
         raise ValueError(f"orc_var_length_count rc={rc}")
     return rows.value, g

@@ -263,10 +263,10 @@ int orc_triangle_enumerate(int64_t n, int64_t m, const int64_t* src, const int64
     return 0;
 }
 
-/* C5 by enumeration: MATCH (a)-[:KNOWS*lo..hi]->(b) RETURN id(a), count(*)
+/* C5 by enumeration: MATCH (a)-[:KNOWS*lo..hi]->(b) WHERE a_ok(a) AND b_ok(b) RETURN id(a), count(*)
  * Paths never repeat an edge (VarLengthExpandPlanner.scala:97,133,179-180).
  * group_rows[a] += number of paths starting at a (all lengths lo..hi, lo >= 1). */
-static void var_dfs(const int64_t* off, const int64_t* adj, const int64_t* dst, int64_t v,
+static void var_dfs(const int64_t* off, const int64_t* adj, const int64_t* dst, const uint8_t* b_ok, int64_t v,
                     int depth, int lo, int hi, int64_t* path, int64_t* cnt) {
     for (int64_t i = off[v]; i < off[v + 1]; ++i) {
         const int64_t r = adj[i];
@@ -274,13 +274,13 @@ static void var_dfs(const int64_t* off, const int64_t* adj, const int64_t* dst, 
         for (int k = 0; k < depth; ++k) if (path[k] == r) { dup = 1; break; }
         if (dup) continue;
         path[depth] = r;
-        if (depth + 1 >= lo) (*cnt)++;
-        if (depth + 1 < hi) var_dfs(off, adj, dst, dst[r], depth + 1, lo, hi, path, cnt);
+        if (depth + 1 >= lo && OK(b_ok, dst[r])) (*cnt)++;
+        if (depth + 1 < hi) var_dfs(off, adj, dst, b_ok, dst[r], depth + 1, lo, hi, path, cnt);
     }
 }
 
-int orc_var_length_count(int64_t n, int64_t m, const int64_t* src, const int64_t* dst,
-                         int lo, int hi, int64_t* group_rows, int64_t* out_rows, int nthreads) {
+int orc_var_length_count(int64_t n, int64_t m, const int64_t* src, const int64_t* dst, const uint8_t* a_ok,
+                         const uint8_t* b_ok, int lo, int hi, int64_t* group_rows, int64_t* out_rows, int nthreads) {
     if (lo < 1 || hi < lo || hi > 16) return -2;
     int64_t* off = csr_offsets(n, m, src);
     if (!off) return -1;
@@ -294,7 +294,7 @@ int orc_var_length_count(int64_t n, int64_t m, const int64_t* src, const int64_t
     for (int64_t a = 0; a < n; ++a) {
         int64_t path[16];
         int64_t c = 0;
-        var_dfs(off, adj, dst, a, 0, lo, hi, path, &c);
+        if (OK(a_ok, a)) var_dfs(off, adj, dst, b_ok, a, 0, lo, hi, path, &c);
         if (group_rows) group_rows[a] = c;
         rows += c;
     }
