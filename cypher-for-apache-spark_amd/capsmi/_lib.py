@@ -120,6 +120,10 @@ _SIGS = {
     "capsmi_words_popcount": (c_int32, [P, c_void_p, c_int64, c_int64, POINTER(c_int64)]),
     "capsmi_relpart_build": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, c_int64, c_int64, PP]),
     "capsmi_relpart_size": (c_int32, [P, POINTER(c_int64)]),
+    "capsmi_trigraph_build": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, PP]),
+    "capsmi_trigraph_count": (c_int32, [P, P, c_int32, c_int32, POINTER(c_int64)]),
+    "capsmi_trigraph_release": (c_int32, [P]),
+    "capsmi_triangle_count": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, POINTER(c_int64)]),
     "capsmi_var_length_count": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, P, c_int32, c_int32, c_char_p,
                                           c_char_p, PP]),
     "capsmi_relpart_release": (c_int32, [P]),

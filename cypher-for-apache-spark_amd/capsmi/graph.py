@@ -122,6 +122,44 @@ def var_length_count(session: Session, rels: Sequence[GpuTable], a_ok: NodeBitma
     return GpuTable(session, out)
 
 
+class TriGraph:
+    """Oriented simple graph with directed multiplicities for the cyclic triangle count (C4)."""
+
+    def __init__(self, session: Session, rels: Sequence[GpuTable], n_ok: NodeBitmap, src_col: str = "source",
+                 dst_col: str = "target"):
+        self.session = session
+        self._h = ctypes.c_void_p()
+        _lib.call("capsmi_trigraph_build", session.handle, len(rels), _handles(rels), src_col.encode(),
+                  dst_col.encode(), n_ok.handle, ctypes.byref(self._h))
+
+    def count(self, part: int = 0, nparts: int = 1) -> int:
+        v = ctypes.c_int64()
+        _lib.call("capsmi_trigraph_count", self.session.handle, self._h, part, nparts, ctypes.byref(v))
+        return v.value
+
+    def release(self) -> None:
+        if self._h:
+            _lib.call("capsmi_trigraph_release", self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            if self._h and _lib._lib is not None:
+                _lib._lib.capsmi_trigraph_release(self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+
+def triangle_count(session: Session, rels: Sequence[GpuTable], n_ok: NodeBitmap, src_col: str = "source",
+                   dst_col: str = "target") -> int:
+    """``MATCH (a)-[r1]->(b)-[r2]->(c)-[r3]->(a) RETURN count(*)`` (pairwise-distinct relationships)."""
+    v = ctypes.c_int64()
+    _lib.call("capsmi_triangle_count", session.handle, len(rels), _handles(rels), src_col.encode(), dst_col.encode(),
+              n_ok.handle, ctypes.byref(v))
+    return v.value
+
+
 class RelPartition:
     """Radix-partitioned relationship layout (include/capsmi.h capsmi_relpart_*): built per query
     on the cold path, or kept across queries as the Cache analogue."""

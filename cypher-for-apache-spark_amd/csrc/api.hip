@@ -1082,6 +1082,78 @@ capsmi_status capsmi_var_length_count(capsmi_session* s, int32_t nrels, capsmi_t
     API_END
 }
 
+}  // extern "C"
+
+struct capsmi_trigraph {
+    capsmi_session* sess = nullptr;
+    capsmi::TriGraph g;
+};
+
+static void rel_cols(int32_t nrels, capsmi_table* const* rels, const char* src_col, const char* dst_col,
+                     std::vector<const int64_t*>& srcs, std::vector<const int64_t*>& dsts, std::vector<int64_t>& ms) {
+    for (int i = 0; i < nrels; ++i) {
+        need(rels[i], "rels[i]");
+        srcs.push_back(rel_col(rels[i], src_col).d());
+        dsts.push_back(rel_col(rels[i], dst_col).d());
+        ms.push_back(rels[i]->nrows);
+    }
+}
+
+extern "C" {
+
+capsmi_status capsmi_trigraph_build(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                                    const char* dst_col, const capsmi_bitmap* n_ok, capsmi_trigraph** out) {
+    API_BEGIN
+    need(s, "session");
+    need(out, "out");
+    check_bitmap(n_ok, "n_ok");
+    REQUIRE(!n_ok->any_dup, CAPSMI_ERR_UNSUPPORTED, "fused count(*) needs each node id in one scanned row");
+    REQUIRE(nrels >= 0 && (nrels == 0 || rels), CAPSMI_ERR_ILLEGAL_ARGUMENT, "rels");
+    use_device(s);
+    std::vector<const int64_t*> srcs, dsts;
+    std::vector<int64_t> ms;
+    rel_cols(nrels, rels, src_col, dst_col, srcs, dsts, ms);
+    auto* g = new capsmi_trigraph();
+    std::unique_ptr<capsmi_trigraph> guard(g);
+    g->sess = s;
+    tri_build(s, srcs.data(), dsts.data(), ms.data(), nrels, n_ok, g->g);
+    *out = guard.release();
+    API_END
+}
+
+capsmi_status capsmi_trigraph_count(capsmi_session* s, const capsmi_trigraph* g, int32_t part, int32_t nparts,
+                                    int64_t* out_rows) {
+    API_BEGIN
+    need(s, "session");
+    need(g, "trigraph");
+    need(out_rows, "out");
+    REQUIRE(nparts >= 1 && part >= 0 && part < nparts, CAPSMI_ERR_ILLEGAL_ARGUMENT, "part");
+    use_device(s);
+    const int64_t ne = g->g.ne;
+    const int64_t b = ne * part / nparts, e = ne * (part + 1) / nparts;
+    *out_rows = (int64_t)tri_count(s, g->g, b, e, part == 0);
+    API_END
+}
+
+capsmi_status capsmi_trigraph_release(capsmi_trigraph* g) {
+    API_BEGIN
+    if (g) {
+        use_device(g->sess);
+        delete g;
+    }
+    API_END
+}
+
+capsmi_status capsmi_triangle_count(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                                    const char* dst_col, const capsmi_bitmap* n_ok, int64_t* out_rows) {
+    capsmi_trigraph* g = nullptr;
+    capsmi_status st = capsmi_trigraph_build(s, nrels, rels, src_col, dst_col, n_ok, &g);
+    if (st != CAPSMI_OK) return st;
+    st = capsmi_trigraph_count(s, g, 0, 1, out_rows);
+    capsmi_trigraph_release(g);
+    return st;
+}
+
 capsmi_status capsmi_relpart_size(const capsmi_relpart* p, int64_t* kept_rows) {
     API_BEGIN
     need(p, "relpart");

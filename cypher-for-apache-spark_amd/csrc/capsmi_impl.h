@@ -218,6 +218,16 @@ void relpart_hop1(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* a, 
 void relpart_hop2(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* c, const uint32_t* X1, const uint32_t* X2,
                   uint32_t* C);
 
+// fused cyclic triangle count (k_tri.hip): the oriented simple graph with multiplicities
+struct TriGraph {
+    int64_t lo = 0, n = 0, ne = 0;
+    Buf ok, ov, off;  // oriented keys (from<<32|to), payload (m(from,to)<<32|m(to,from)), CSR offsets (n + 1)
+    Buf ek, ev, sl;   // undirected keys / payload (pair terms), self-loop counts
+};
+void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
+               const capsmi_bitmap* n_ok, TriGraph& g);
+uint64_t tri_count(capsmi_session* s, const TriGraph& g, int64_t e_begin, int64_t e_end, bool with_terms);
+
 // fused var-length grouped count (k_varlen.hip)
 int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
                          int nt, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, int lower, int upper,

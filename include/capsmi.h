@@ -285,6 +285,19 @@ capsmi_status capsmi_var_length_count(capsmi_session* s, int32_t nrels, capsmi_t
                                       const char* src_col, const char* dst_col, const capsmi_bitmap* a_ok,
                                       const capsmi_bitmap* b_ok, int32_t lower, int32_t upper, const char* id_name,
                                       const char* count_name, capsmi_table** out);
+/* Cyclic triangle count (C4), fused:
+ *   MATCH (a)-[r1]->(b)-[r2]->(c)-[r3]->(a) WHERE n_ok(a) AND n_ok(b) AND n_ok(c) RETURN count(*)
+ * (two Expands + ExpandInto on (c, a), RelationalPlanner.scala:113-154, plus pairwise uniqueness).
+ * The oriented simple graph with multiplicities (a trigraph) is built once; counting can be split into
+ * `nparts` slices of its oriented edges (multi-GPU replicas: each rank counts its part, results sum). */
+typedef struct capsmi_trigraph capsmi_trigraph;
+capsmi_status capsmi_trigraph_build(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                                    const char* dst_col, const capsmi_bitmap* n_ok, capsmi_trigraph** out);
+capsmi_status capsmi_trigraph_count(capsmi_session* s, const capsmi_trigraph* g, int32_t part, int32_t nparts,
+                                    int64_t* out_rows);
+capsmi_status capsmi_trigraph_release(capsmi_trigraph* g);
+capsmi_status capsmi_triangle_count(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                                    const char* dst_col, const capsmi_bitmap* n_ok, int64_t* out_rows);
 /* popcount of words [w_begin, w_end) of a device bitmap, result in *out (host) */
 capsmi_status capsmi_words_popcount(capsmi_session* s, const uint32_t* words, int64_t w_begin, int64_t w_end,
                                     int64_t* out);
