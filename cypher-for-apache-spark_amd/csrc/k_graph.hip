@@ -59,24 +59,65 @@ __device__ __forceinline__ void wave_set_bit(uint32_t* w, int64_t x, bool act) {
 }
 
 // ---- node-scan bitmaps ----------------------------------------------------------
-__global__ void k_bitmap_add(uint32_t* w, int64_t lo, int64_t hi, const int64_t* __restrict__ ids,
-                             const uint8_t* __restrict__ ids_valid, const uint8_t* __restrict__ flags, int64_t n,
-                             unsigned long long* counters /* [0]=rows added, [1]=duplicates, [2]=out of range */) {
+// One lane per scanned node row; lanes hitting the same bitmap word are combined with a
+// segmented OR (and a segmented count, for the duplicate check) so a sorted id column costs
+// one atomic per word, not per row.  Counters are reduced per wave before the atomics.
+__global__ void __launch_bounds__(256) k_bitmap_add(uint32_t* w, int64_t lo, int64_t hi, const int64_t* __restrict__ ids,
+                                                    const uint8_t* __restrict__ ids_valid,
+                                                    const uint8_t* __restrict__ flags, int64_t n,
+                                                    unsigned long long* counters /* [0]=added, [1]=dups, [2]=bad */) {
+    const int lane = threadIdx.x & 63;
     unsigned long long added = 0, dups = 0, bad = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        if (flags && !flags[i]) continue;
-        if (ids_valid && !ids_valid[i]) { ++bad; continue; }
-        const int64_t id = ids[i];
-        if (id < lo || id >= hi) { ++bad; continue; }
-        const uint64_t x = (uint64_t)(id - lo);
-        const uint32_t bit = 1u << (x & 31);
-        const uint32_t old = atomicOr(&w[x >> 5], bit);
-        ++added;
-        if (old & bit) ++dups;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < n; base += stride) {
+        const int64_t i = base + lane;
+        bool act = i < n && (!flags || flags[i]);
+        int64_t x = 0;
+        if (act) {
+            const int64_t id = ids[i];
+            if ((ids_valid && !ids_valid[i]) || id < lo || id >= hi) {
+                ++bad;
+                act = false;
+            } else {
+                x = id - lo;
+            }
+        }
+        int64_t word = act ? (x >> 5) : -1;
+        uint32_t m = act ? (1u << (x & 31)) : 0u;
+        uint32_t cnt = act ? 1u : 0u;
+        // segmented suffix reduction over runs of equal `word` in adjacent lanes: `tail` marks
+        // that the lane's current window [lane, lane+o) already contains the end of its run
+        const int64_t next = __shfl_down(word, 1, 64);
+        bool tail = lane == 63 || next != word;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t mo = __shfl_down(m, o, 64);
+            const uint32_t co = __shfl_down(cnt, o, 64);
+            const bool to = __shfl_down((int)tail, o, 64) != 0;
+            if (!tail) {
+                m |= mo;
+                cnt += co;
+                tail = to;
+            }
+        }
+        const int64_t prev = __shfl_up(word, 1, 64);
+        if (act && (lane == 0 || prev != word)) {
+            const uint32_t old = atomicOr(&w[word], m);
+            added += cnt;
+            dups += (cnt - (uint32_t)__popc(m)) + (uint32_t)__popc(old & m);
+        }
     }
-    if (added) atomicAdd(&counters[0], added);
-    if (dups) atomicAdd(&counters[1], dups);
-    if (bad) atomicAdd(&counters[2], bad);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        added += __shfl_down(added, o, 64);
+        dups += __shfl_down(dups, o, 64);
+        bad += __shfl_down(bad, o, 64);
+    }
+    if (lane == 0) {
+        if (added) atomicAdd(&counters[0], added);
+        if (dups) atomicAdd(&counters[1], dups);
+        if (bad) atomicAdd(&counters[2], bad);
+    }
 }
 
 __global__ void k_popcount(const uint32_t* __restrict__ w, int64_t b, int64_t e, unsigned long long* out) {

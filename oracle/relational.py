@@ -96,6 +96,10 @@ class NumpyTable:
     def to_columns(self):
         return [ColumnOut(k, c.type, c.values, None if c.valid.all() else c.valid) for k, c in self.cols.items()]
 
+    def column(self, name):
+        c = self.cols[name]
+        return ColumnOut(name, c.type, c.values, None if c.valid.all() else c.valid)
+
     def _new(self, cols, n) -> "NumpyTable":
         return NumpyTable(self.backend, cols, n)
 

@@ -184,3 +184,27 @@ def test_expand_filter_c2(session, scale):
     got_ids = persons.column("id").values
     np.testing.assert_array_equal(got_ids, np.nonzero(pm)[0])
     np.testing.assert_array_equal(persons.column("age").values, age[got_ids])
+
+
+@pytest.mark.parametrize("layout", ["sorted", "shuffled", "dups_adjacent", "dups_far", "sparse"])
+def test_bitmap_add_scan_stats(session, layout):
+    """Wave-combined bitmap marking: set bits and the duplicate flag must not depend on lane layout."""
+    from capsmi import ColumnData, I64, graph
+    rng = np.random.default_rng(7)
+    n = 5000
+    if layout == "sorted":
+        ids = np.arange(n)
+    elif layout == "shuffled":
+        ids = rng.permutation(n)
+    elif layout == "dups_adjacent":
+        ids = np.sort(np.concatenate([np.arange(n), [17, 4000]]))
+    elif layout == "dups_far":
+        ids = np.concatenate([np.arange(0, n, 2), [0, 64, 96, 127]])
+        rng.shuffle(ids)
+    else:
+        ids = rng.choice(n, 300, replace=False) * 1
+    nodes = session.table([ColumnData("id", I64, ids.astype(np.int64))])
+    bm = graph.NodeBitmap(session, 0, n).add_scan(nodes)
+    bits, uniq = bm.stats()
+    assert bits == len(np.unique(ids))
+    assert uniq == (len(np.unique(ids)) == len(ids))
