@@ -34,7 +34,11 @@ sys.path.insert(0, ROOT)
 
 METRIC = "matched rows/sec for 2-hop MATCH on R-MAT 2^30 edges; % HBM roofline @1/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-KERNELS = ("part_hist", "part_scatter", "hop1", "hop2", "mid_combine", "bitmap_add")
+KERNELS = ("part_hist", "part_scatter_t", "part_scatter_s", "hop1", "hop2", "mid_combine", "bitmap_add")
+# timer name -> kernel symbol as rocprofv3 reports it (hop1/hop2 are instances of one template)
+KERNEL_SYMBOL = {"part_hist": "k_part_hist", "part_scatter_t": "k_scatter_t", "part_scatter_s": "k_scatter_s",
+                 "hop1": "k_hop_2d<true, *>", "hop2": "k_hop_2d<false, false>", "mid_combine": "k_mid_combine",
+                 "bitmap_add": "k_bitmap_add"}
 
 
 def parse():
@@ -212,13 +216,17 @@ def main():
         head = modes[0]
         sec, res, kt = results[head]
         # per-kernel algorithmic bytes (this rank's rels): what each kernel must touch by its function
-        alg = {"part_hist": m_local * 8, "part_scatter": m_local * 24, "hop1": m_local * 8 + n // 8,
-               "hop2": m_local * 8 + n // 8 * 2, "mid_combine": n // 8 * 5, "bitmap_add": n * 8}
+        alg = {"part_hist": m_local * 16,            # read source + target
+               "part_scatter_t": m_local * 24,       # read 2 x int64, write packed uint2
+               "part_scatter_s": m_local * 16,       # read + write uint2
+               "hop1": m_local * 8 + n // 8,         # read uint2 pairs, write M
+               "hop2": m_local * 8 + n // 8 * 3,     # read uint2 pairs + X1 + X2, write C
+               "mid_combine": n // 8 * 5, "bitmap_add": n * 8}
         timed = {k: (c, ms) for k, (c, ms) in kt.items() if c > 0}
         dom = max(timed, key=lambda k: timed[k][1])
         avg_ms = timed[dom][1] / timed[dom][0]
         achieved = alg[dom] / (avg_ms * 1e-3) / 1e9
-        traffic = pmc_traffic("k_" + dom if not dom.startswith("part") else "k_" + dom)
+        traffic = pmc_traffic(KERNEL_SYMBOL[dom])
         query_alg = 2 * 24 * m_total + 3 * 8 * n  # SURVEY.md §8d C3 B_alg (whole query, all ranks)
         line = {
             "metric": METRIC,
@@ -240,7 +248,7 @@ def main():
                        "parallelism": f"rels partitioned by owner(target) over {world} GPU(s); "
                                       "hop-1 frontier all-gather + count all-reduce over RCCL"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_" + dom,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": KERNEL_SYMBOL[dom],
                          "kernel_ms": avg_ms, "alg_bytes_per_launch": alg[dom]},
             "query": {"count_distinct_c": res, "matched_rows": matched, "check_vs_unpartitioned": check,
                       "alg_bytes_query": query_alg,

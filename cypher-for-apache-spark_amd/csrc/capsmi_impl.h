@@ -201,14 +201,15 @@ void order_keys(capsmi_session* s, const int64_t* col, const uint8_t* valid, int
 // partitioned relationship layout (k_part.hip)
 struct PartLayout {
     int64_t lo, hi;  // id domain of both endpoints
-    int nslices;     // target slices of 2^19 ids
-    int sx_shift;    // source super-slice = (src - lo) >> sx_shift  (< 8, one per XCD)
-    int nbuckets;    // 8 * nslices
+    int nt;          // target slices of 2^19 ids
+    int ns;          // source slices of 2^sbits ids
+    int sbits;       // 19 while nt * ns <= 16384, coarser for larger domains
+    int ncells;      // nt * ns, j-major (target slice major)
 };
 struct RelPart {
     PartLayout L;
-    Buf pairs;  // uint2 (source - lo, target - lo) per kept relationship, grouped by bucket
-    Buf boff;   // int64 bucket offsets (nbuckets + 1)
+    Buf pairs;  // uint2 (source - lo, target - lo) per kept relationship, grouped by cell
+    Buf boff;   // int64 [cell offsets (ncells + 1) | target-slice offsets (nt + 1) | chunk prefix (nt + 1)]
     int64_t kept = 0;
 };
 void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,

@@ -1,0 +1,96 @@
+"""2-D partitioned layout (k_part.hip) at sizes with several target/source slices.
+
+The small-scale parity tests (test_gpu_graph.py) fit one 2^19-id slice, so the multi-cell walk,
+the LDS pull of source slices (>= 8192 rels of one cell per workgroup) and coarse source slices
+(domains > 2^26 ids) are exercised here.  The reference answer is a numpy restatement of the
+X1/X2 frontier semantics (oracle/rmat.c orc_two_hop_closed), exact integer comparison.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _np_count_distinct(n, src, dst, a_ok, b_ok, c_ok):
+    loop = src == dst
+    sel = a_ok[src] & b_ok[dst]
+    M = np.zeros(n, bool)
+    M[dst[sel & ~loop]] = True
+    selfc = np.bincount(dst[sel & loop], minlength=n)
+    X1, X2 = M | (selfc >= 1), M | (selfc >= 2)
+    hit = c_ok[dst] & np.where(loop, X2[src], X1[src])
+    C = np.zeros(n, bool)
+    C[dst[hit]] = True
+    return int(C.sum())
+
+
+def _bitmap(session, n, ids):
+    from capsmi import ColumnData, I64, graph
+    t = session.table([ColumnData("id", I64, np.asarray(ids, dtype=np.int64))])
+    return graph.NodeBitmap(session, 0, n).add_scan(t)
+
+
+@pytest.mark.parametrize("person_only", [False, True])
+def test_rmat_multi_slice(session, person_only):
+    from capsmi import graph
+    scale = 21  # 4 x 4 cells of 2^19 ids; 16M rels -> every workgroup pulls source slices
+    n = 1 << scale
+    rels = graph.rmat_rels(session, scale, 0, 8 << scale)
+    src = rels.column("source").values
+    dst = rels.column("target").values
+    rng = np.random.default_rng(3)
+    ok = rng.random(n) < 0.8 if person_only else np.ones(n, bool)
+    okc = rng.random(n) < 0.6 if person_only else ok
+    a, c = _bitmap(session, n, np.nonzero(ok)[0]), _bitmap(session, n, np.nonzero(okc)[0])
+    want = _np_count_distinct(n, src, dst, ok, ok, okc)
+    rp = graph.RelPartition(session, [rels], 0, n)
+    assert rp.size == len(src)
+    assert rp.count_distinct(a, a, c) == want
+    # one call builds its own layout
+    assert graph.two_hop_count_distinct(session, [rels], a, a, c) == want
+    rp.release()
+
+
+def test_coarse_source_slices(session):
+    """2^27-id domain: 256 target slices x 64 source slices of 2^21 ids (no LDS pull)."""
+    from capsmi import ColumnData, I64, graph
+    n = 1 << 27
+    rng = np.random.default_rng(5)
+    m = 1 << 20
+    hubs = rng.integers(0, n, 4096)
+    src = np.concatenate([rng.integers(0, n, m // 2), rng.choice(hubs, m // 2)]).astype(np.int64)
+    dst = np.concatenate([rng.choice(hubs, m // 2), rng.integers(0, n, m // 2)]).astype(np.int64)
+    src[:1000] = dst[:1000]  # self-loops
+    src[1000:1500] = dst[:500]
+    dst[1000:1500] = dst[:500]  # repeated self-loops
+    rels = session.table([ColumnData("id", I64, np.arange(m)), ColumnData("source", I64, src),
+                          ColumnData("target", I64, dst)])
+    touched = np.unique(np.concatenate([src, dst]))
+    keep = touched[rng.random(len(touched)) < 0.9]
+    ok = np.zeros(n, bool)
+    ok[keep] = True
+    bm = _bitmap(session, n, keep)
+    want = _np_count_distinct(n, src, dst, ok, ok, ok)
+    assert graph.two_hop_count_distinct(session, [rels], bm, bm, bm) == want
+
+
+def test_rels_outside_domain_are_dropped(session):
+    from capsmi import ColumnData, I64, graph
+    lo, hi = 1 << 20, 3 << 20
+    rng = np.random.default_rng(9)
+    m = 1 << 20
+    src = rng.integers(0, 4 << 20, m).astype(np.int64)
+    dst = rng.integers(0, 4 << 20, m).astype(np.int64)
+    rels = session.table([ColumnData("id", I64, np.arange(m)), ColumnData("source", I64, src),
+                          ColumnData("target", I64, dst)])
+    ids = np.arange(lo, hi)
+    t = session.table([ColumnData("id", I64, ids)])
+    bm = graph.NodeBitmap(session, lo, hi).add_scan(t)
+    inside = (src >= lo) & (src < hi) & (dst >= lo) & (dst < hi)
+    rp = graph.RelPartition(session, [rels], lo, hi)
+    assert rp.size == int(inside.sum())
+    n = hi - lo
+    s, d = src[inside] - lo, dst[inside] - lo
+    allok = np.ones(n, bool)
+    assert rp.count_distinct(bm, bm, bm) == _np_count_distinct(n, s, d, allok, allok, allok)
+    rp.release()
