@@ -35,10 +35,9 @@ sys.path.insert(0, ROOT)
 METRIC = "matched rows/sec for 2-hop MATCH on R-MAT 2^30 edges; % HBM roofline @1/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 KERNELS = ("part_hist", "part_scatter_t", "part_scatter_s", "hop1", "hop2", "mid_combine", "bitmap_add")
-# timer name -> kernel symbol as rocprofv3 reports it (hop1/hop2 are instances of one template)
+# timer name -> kernel name as rocprofv3 reports it (hop1 and hop2 are two instances of k_hop_2d)
 KERNEL_SYMBOL = {"part_hist": "k_part_hist", "part_scatter_t": "k_scatter_t", "part_scatter_s": "k_scatter_s",
-                 "hop1": "k_hop_2d<true, *>", "hop2": "k_hop_2d<false, false>", "mid_combine": "k_mid_combine",
-                 "bitmap_add": "k_bitmap_add"}
+                 "hop1": "k_hop_2d", "hop2": "k_hop_2d", "mid_combine": "k_mid_combine", "bitmap_add": "k_bitmap_add"}
 
 
 def parse():
