@@ -205,12 +205,11 @@ struct PartLayout {
     int ns;          // source slices of 2^sbits ids
     int sbits;       // 19 while nt * ns <= 16384, coarser for larger domains
     int ncells;      // nt * ns, j-major (target slice major)
-    int tbits_n, sbits_n, cbits;  // key bits of a target slice / source slice / cell index
 };
 struct RelPart {
     PartLayout L;
     Buf pairs;  // uint2 (source - lo, target - lo) per kept relationship, grouped by cell
-    Buf boff;   // int64 [cell offsets (ncells + 1) | target-slice offsets (nt + 1) | chunk prefix (nt + 1)]
+    Buf boff;   // int64 cell offsets (ncells + 1)
     int64_t kept = 0;
 };
 void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,

@@ -32,6 +32,7 @@ constexpr int kItems = 8;
 constexpr int kTile = kBlock * kItems;           // relationships per scatter tile
 constexpr int kUnroll = 4;                       // loads in flight per lane in the hops
 constexpr int64_t kLoadMin = 8192;               // pull a source slice into LDS for >= this many rels
+constexpr int kReps = 32;                        // cursor replicas per bucket (see TileWalk)
 
 using Layout = PartLayout;
 
@@ -78,50 +79,83 @@ __device__ __forceinline__ int cell_of(const Layout& L, uint32_t s, uint32_t t) 
     return (int)(t >> kSliceBits) * L.ns + (int)(s >> L.sbits);
 }
 
-// Rank of this lane's item among the items of bucket `b` (b < 2^nbits), counted in LDS `cnt`.
-// Lanes holding the same bucket are found with nbits ballots (one per key bit), then only the
-// lowest such lane touches the LDS counter: a skewed key distribution (R-MAT puts ~15 % of all
-// relationships in one target slice) would otherwise serialise up to 64 same-address atomics
-// per wave instruction.  Must be called by all lanes of the wave (`act` masks the item).
-__device__ __forceinline__ uint32_t wave_rank(int b, bool act, int nbits, uint32_t* cnt) {
-    uint64_t mask = __ballot(act);
-    for (int k = 0; k < nbits; ++k) {
-        const bool bit = (b >> k) & 1;
-        const uint64_t bb = __ballot(act && bit);
-        mask &= bit ? bb : ~bb;
-    }
-    const int lane = threadIdx.x & 63;
-    const int leader = mask ? __ffsll((unsigned long long)mask) - 1 : 0;
-    uint32_t base = 0;
-    if (act && lane == leader) base = atomicAdd(&cnt[b], (uint32_t)__popcll(mask));
-    base = __shfl(base, leader, 64);
-    return base + (uint32_t)__popcll(mask & ((uint64_t(1) << lane) - 1));
-}
+// Input tiles are dealt to kReps replicas (tile t -> replica t % kReps).  Each replica owns a
+// contiguous share of every bucket, so a bucket's write cursor is advanced only by the tiles of
+// one replica: with one cursor per bucket every tile of the whole input would serialise on the
+// hottest bucket's atomic (R-MAT puts ~15 % of all relationships in one target slice).
+// Block b works for replica b % kReps and takes that replica's tiles round-robin.
+struct TileWalk {
+    int r, q, bpr;
+    __device__ TileWalk() : r(blockIdx.x % kReps), q(blockIdx.x / kReps), bpr(gridDim.x / kReps) {}
+    __device__ int64_t tile(int64_t k) const { return (int64_t)r + (int64_t)kReps * ((int64_t)q + k * bpr); }
+};
 
-// pass 0: cell sizes (rels with an endpoint outside [lo, hi) can never match a node scan
-// over that domain and are dropped here -- an inner join drops them the same way)
+// pass 0: per-replica cell sizes (rels with an endpoint outside [lo, hi) can never match a node
+// scan over that domain and are dropped here -- an inner join drops them the same way)
 __global__ void __launch_bounds__(kBlock) k_part_hist(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                       int64_t m, Layout L, unsigned int* __restrict__ counts) {
     extern __shared__ __attribute__((aligned(16))) unsigned int h[];
     for (int i = threadIdx.x; i < L.ncells; i += kBlock) h[i] = 0;
     __syncthreads();
     const uint64_t range = (uint64_t)(L.hi - L.lo);
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    const int nbits = L.cbits;
-    for (int64_t e0 = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63); e0 < m; e0 += stride) {  // wave-uniform
-        const int64_t e = e0 + (threadIdx.x & 63);
-        bool act = false;
-        int c = 0;
-        if (e < m) {
-            const uint64_t s = (uint64_t)(src[e] - L.lo), t = (uint64_t)(dst[e] - L.lo);
-            act = s < range && t < range;
-            if (act) c = cell_of(L, (uint32_t)s, (uint32_t)t);
+    const TileWalk w;
+    for (int64_t k = 0;; ++k) {
+        const int64_t t0 = w.tile(k) * kTile;
+        if (t0 >= m) break;
+#pragma unroll
+        for (int u = 0; u < kItems; ++u) {
+            const int64_t e = t0 + (int64_t)u * kBlock + threadIdx.x;
+            if (e < m) {
+                const uint64_t s = (uint64_t)(src[e] - L.lo), t = (uint64_t)(dst[e] - L.lo);
+                if (s < range && t < range) atomicAdd(&h[cell_of(L, (uint32_t)s, (uint32_t)t)], 1u);
+            }
         }
-        (void)wave_rank(c, act, nbits, h);
     }
     __syncthreads();
+    unsigned int* out = counts + (size_t)w.r * L.ncells;
     for (int i = threadIdx.x; i < L.ncells; i += kBlock)
-        if (h[i]) atomicAdd(&counts[i], h[i]);
+        if (h[i]) atomicAdd(&out[i], h[i]);
+}
+
+// offsets, one thread per cell: pre[r][c] = sum_{r' < r} cnt[r'][c], tot[c] = sum_r cnt[r][c]
+__global__ void k_cell_prefix(const unsigned int* __restrict__ cnt, int ncells, int64_t* __restrict__ pre,
+                              int64_t* __restrict__ tot) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncells) return;
+    int64_t run = 0;
+    for (int r = 0; r < kReps; ++r) {
+        pre[(size_t)r * ncells + c] = run;
+        run += cnt[(size_t)r * ncells + c];
+    }
+    tot[c] = run;
+}
+
+// one thread per pass-2 unit u = j * kReps + r (the pairs replica r put in target slice j):
+// its start (= replica r's pass-1 cursor for slice j), length and tile count
+__global__ void k_units(const unsigned int* __restrict__ cnt, const int64_t* __restrict__ pre,
+                        const int64_t* __restrict__ coff, Layout L, int64_t* __restrict__ cur1,
+                        int64_t* __restrict__ ustart, int64_t* __restrict__ ulen, int64_t* __restrict__ utiles) {
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= L.nt * kReps) return;
+    const int j = u / kReps, r = u % kReps;
+    int64_t before = 0, len = 0;
+    for (int i = 0; i < L.ns; ++i) {
+        const size_t c = (size_t)r * L.ncells + (size_t)j * L.ns + i;
+        before += pre[c];
+        len += cnt[c];
+    }
+    const int64_t st = coff[(size_t)j * L.ns] + before;
+    cur1[(size_t)r * L.nt + j] = st;
+    ustart[u] = st;
+    ulen[u] = len;
+    utiles[u] = (len + kTile - 1) / kTile;
+}
+
+// pass-2 cursors: cur2[r][c] = coff[c] + pre[r][c] (in place)
+__global__ void k_add_coff(int64_t* __restrict__ pre, const int64_t* __restrict__ coff, int ncells) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)kReps * ncells) return;
+    pre[i] += coff[i % ncells];
 }
 
 // LDS carve-up shared by both scatters: stage[kTile] | base[nb] (u64) | cnt[nb] | loc[nb] | wtot[16]
@@ -130,7 +164,8 @@ __host__ __device__ constexpr size_t scatter_lds(int nb) {
 }
 
 // Tile body: items (s, t, bucket) are in registers with their rank within the bucket; reserve
-// each bucket's run with one global atomic, regroup the tile in LDS, write the runs out.
+// each bucket's run with one atomic on the replica's cursor, regroup the tile in LDS, write the
+// runs out.
 __device__ __forceinline__ void scatter_tile(const uint32_t (&sv)[kItems], const uint32_t (&tv)[kItems],
                                              const int (&bk)[kItems], const uint32_t (&rk)[kItems], int nb,
                                              unsigned long long* __restrict__ cursor, uint2* __restrict__ out,
@@ -153,9 +188,10 @@ __device__ __forceinline__ void scatter_tile(const uint32_t (&sv)[kItems], const
     __syncthreads();
 }
 
-// pass 1: int64 (source, target) -> uint32 pairs grouped by target slice
+// pass 1: int64 (source, target) -> uint32 pairs grouped by target slice, replica-major within
+// each slice; cursor = cur1[r][j]
 __global__ void __launch_bounds__(kBlock) k_scatter_t(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
-                                                      int64_t m, Layout L, unsigned long long* __restrict__ cursor,
+                                                      int64_t m, Layout L, unsigned long long* __restrict__ cur1,
                                                       uint2* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     const int nb = L.nt;
@@ -165,37 +201,43 @@ __global__ void __launch_bounds__(kBlock) k_scatter_t(const int64_t* __restrict_
     uint32_t* loc = cnt + nb;
     uint32_t* wtot = loc + nb;
     const uint64_t range = (uint64_t)(L.hi - L.lo);
-    for (int64_t t0 = (int64_t)blockIdx.x * kTile; t0 < m; t0 += (int64_t)gridDim.x * kTile) {
+    const TileWalk w;
+    unsigned long long* cursor = cur1 + (size_t)w.r * nb;
+    for (int64_t k = 0;; ++k) {
+        const int64_t t0 = w.tile(k) * kTile;
+        if (t0 >= m) break;  // block-uniform
         for (int i = threadIdx.x; i < nb; i += kBlock) cnt[i] = 0;
         __syncthreads();
         uint32_t sv[kItems], tv[kItems], rk[kItems];
         int bk[kItems];
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {
-            const int64_t e = t0 + (int64_t)k * kBlock + threadIdx.x;
-            bk[k] = -1;
-            sv[k] = tv[k] = rk[k] = 0;
+        for (int u = 0; u < kItems; ++u) {
+            const int64_t e = t0 + (int64_t)u * kBlock + threadIdx.x;
+            bk[u] = -1;
+            sv[u] = tv[u] = rk[u] = 0;
             if (e < m) {
                 const uint64_t s = (uint64_t)(src[e] - L.lo), t = (uint64_t)(dst[e] - L.lo);
                 if (s < range && t < range) {
-                    sv[k] = (uint32_t)s;
-                    tv[k] = (uint32_t)t;
-                    bk[k] = (int)(tv[k] >> kSliceBits);
+                    sv[u] = (uint32_t)s;
+                    tv[u] = (uint32_t)t;
+                    bk[u] = (int)(tv[u] >> kSliceBits);
                 }
             }
         }
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) rk[k] = wave_rank(bk[k], bk[k] >= 0, L.tbits_n, cnt);
+        for (int u = 0; u < kItems; ++u)
+            if (bk[u] >= 0) rk[u] = atomicAdd(&cnt[bk[u]], 1u);
         __syncthreads();
         scatter_tile(sv, tv, bk, rk, nb, cursor, out, stage, base, cnt, loc, wtot, true, L.sbits);
     }
 }
 
-// pass 2: each target slice's pairs -> its source cells.  Work unit = one tile of one target
-// slice; chunk k of slice j is global chunk cpre[j] + k.
-__global__ void __launch_bounds__(kBlock) k_scatter_s(const uint2* __restrict__ in, const int64_t* __restrict__ toff,
-                                                      const int64_t* __restrict__ cpre, Layout L,
-                                                      unsigned long long* __restrict__ cursor,
+// pass 2: unit u = (target slice j, replica r) -> the source cells of slice j; cursor cur2[r][j][*].
+// Global tile k belongs to the unit with upre[u] <= k < upre[u + 1].
+__global__ void __launch_bounds__(kBlock) k_scatter_s(const uint2* __restrict__ in, const int64_t* __restrict__ ustart,
+                                                      const int64_t* __restrict__ ulen,
+                                                      const int64_t* __restrict__ upre, Layout L,
+                                                      unsigned long long* __restrict__ cur2,
                                                       uint2* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     const int nb = L.ns;
@@ -204,16 +246,17 @@ __global__ void __launch_bounds__(kBlock) k_scatter_s(const uint2* __restrict__ 
     uint32_t* cnt = reinterpret_cast<uint32_t*>(base + nb);
     uint32_t* loc = cnt + nb;
     uint32_t* wtot = loc + nb;
-    const int64_t nchunks = cpre[L.nt];
-    for (int64_t ck = blockIdx.x; ck < nchunks; ck += gridDim.x) {
-        int lo = 0, hi = L.nt;  // last j with cpre[j] <= ck
+    const int nunits = L.nt * kReps;
+    const int64_t ntiles = upre[nunits];
+    for (int64_t ck = blockIdx.x; ck < ntiles; ck += gridDim.x) {
+        int lo = 0, hi = nunits;  // last u with upre[u] <= ck
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
-            if (cpre[mid] <= ck) lo = mid; else hi = mid;
+            if (upre[mid] <= ck) lo = mid; else hi = mid;
         }
-        const int j = lo;
-        const int64_t b0 = toff[j] + (ck - cpre[j]) * kTile;
-        const int64_t b1 = min(b0 + (int64_t)kTile, toff[j + 1]);
+        const int u = lo, j = u / kReps, r = u % kReps;
+        const int64_t b0 = ustart[u] + (ck - upre[u]) * kTile;
+        const int64_t b1 = min(b0 + (int64_t)kTile, ustart[u] + ulen[u]);
         for (int i = threadIdx.x; i < nb; i += kBlock) cnt[i] = 0;
         __syncthreads();
         uint32_t sv[kItems], tv[kItems], rk[kItems];
@@ -231,9 +274,11 @@ __global__ void __launch_bounds__(kBlock) k_scatter_s(const uint2* __restrict__ 
             }
         }
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) rk[k] = wave_rank(bk[k], bk[k] >= 0, L.sbits_n, cnt);
+        for (int k = 0; k < kItems; ++k)
+            if (bk[k] >= 0) rk[k] = atomicAdd(&cnt[bk[k]], 1u);
         __syncthreads();
-        scatter_tile(sv, tv, bk, rk, nb, cursor + (int64_t)j * nb, out, stage, base, cnt, loc, wtot, false, L.sbits);
+        scatter_tile(sv, tv, bk, rk, nb, cur2 + (size_t)r * L.ncells + (size_t)j * nb, out, stage, base, cnt, loc,
+                     wtot, false, L.sbits);
     }
 }
 
@@ -344,11 +389,6 @@ __global__ void __launch_bounds__(kBlock) k_hop_2d(const uint2* __restrict__ pai
     flush_slice(tl, out, cur_j, gwords, tmask);
 }
 
-inline int ceil_log2(uint64_t v) {
-    int b = 0;
-    while ((uint64_t(1) << b) < v) ++b;
-    return b;
-}
 
 }  // namespace part
 
@@ -368,9 +408,6 @@ static part::Layout make_layout(int64_t lo, int64_t hi) {
     L.ns = (int)((range + (uint64_t(1) << L.sbits) - 1) >> L.sbits);
     if (L.ns < 1) L.ns = 1;
     L.ncells = L.nt * L.ns;
-    L.tbits_n = part::ceil_log2((uint64_t)L.nt);
-    L.sbits_n = part::ceil_log2((uint64_t)L.ns);
-    L.cbits = part::ceil_log2((uint64_t)L.ncells);
     return L;
 }
 
@@ -384,63 +421,63 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
                    int64_t lo, int64_t hi, RelPart& rp) {
     REQUIRE(hi > lo && (uint64_t)(hi - lo) <= (uint64_t(1) << 31), CAPSMI_ERR_UNSUPPORTED,
             "partitioned layout needs an id domain of at most 2^31 ids");
+    using namespace part;
     hipStream_t st = s->stream;
     rp.L = make_layout(lo, hi);
-    const part::Layout& L = rp.L;
-    REQUIRE(L.nt <= part::kMaxTSlices && L.ncells <= part::kMaxCells, CAPSMI_ERR_INTERNAL, "layout too large");
-    Buf counts = dev_alloc(sizeof(unsigned int) * L.ncells, st);
-    HIP_CHECK(hipMemsetAsync(P<void>(counts), 0, sizeof(unsigned int) * L.ncells, st));
-    const int64_t cap = (int64_t)s->num_cus;
+    const Layout& L = rp.L;
+    REQUIRE(L.nt <= kMaxTSlices && L.ncells <= kMaxCells, CAPSMI_ERR_INTERNAL, "layout too large");
+    const int nunits = L.nt * kReps;
+    // blocks: a multiple of kReps, about two 1024-lane blocks per CU
+    const int grid = kReps * (int)std::max<int64_t>(1, (2 * (int64_t)s->num_cus + kReps - 1) / kReps);
+
+    Buf cnt = dev_alloc(sizeof(unsigned int) * kReps * L.ncells, st);
+    HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, sizeof(unsigned int) * kReps * L.ncells, st));
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
-        int64_t g = (ms[i] + part::kBlock * 16 - 1) / (part::kBlock * 16);
-        if (g > cap) g = cap;
         KernelTimer kt(s, "part_hist");
-        hipLaunchKernelGGL(part::k_part_hist, dim3((unsigned)g), dim3(part::kBlock),
-                           sizeof(unsigned int) * L.ncells, st, srcs[i], dsts[i], ms[i], L, P<unsigned int>(counts));
+        hipLaunchKernelGGL(k_part_hist, dim3(grid), dim3(kBlock), sizeof(unsigned int) * L.ncells, st, srcs[i], dsts[i],
+                           ms[i], L, P<unsigned int>(cnt));
     }
-    // offsets: cells (j-major), target slices, and pass-2 chunks per target slice
-    std::vector<unsigned int> hc(L.ncells);
-    HIP_CHECK(hipMemcpyAsync(hc.data(), P<void>(counts), sizeof(unsigned int) * L.ncells, hipMemcpyDeviceToHost, st));
+    // offsets, all on the device: cells, pass-1 cursors per (replica, slice), pass-2 units
+    Buf pre = dev_alloc(sizeof(int64_t) * kReps * L.ncells, st);  // becomes cur2
+    Buf tot = dev_alloc(sizeof(int64_t) * L.ncells, st);
+    rp.boff = dev_alloc(sizeof(int64_t) * (L.ncells + 1), st);  // coff
+    Buf cur1 = dev_alloc(sizeof(int64_t) * nunits, st);
+    Buf units = dev_alloc(sizeof(int64_t) * (4 * (size_t)nunits + 1), st);  // ustart | ulen | utiles | upre
+    int64_t* ustart = P<int64_t>(units);
+    int64_t* ulen = ustart + nunits;
+    int64_t* utiles = ulen + nunits;
+    int64_t* upre = utiles + nunits;
+    hipLaunchKernelGGL(k_cell_prefix, dim3((L.ncells + 255) / 256), dim3(256), 0, st, P<unsigned int>(cnt), L.ncells,
+                       P<int64_t>(pre), P<int64_t>(tot));
+    exclusive_scan_i64(P<int64_t>(tot), P<int64_t>(rp.boff), L.ncells, st);
+    hipLaunchKernelGGL(k_units, dim3((nunits + 255) / 256), dim3(256), 0, st, P<unsigned int>(cnt), P<int64_t>(pre),
+                       P<int64_t>(rp.boff), L, P<int64_t>(cur1), ustart, ulen, utiles);
+    hipLaunchKernelGGL(k_add_coff, dim3((unsigned)(((int64_t)kReps * L.ncells + 255) / 256)), dim3(256), 0, st,
+                       P<int64_t>(pre), P<int64_t>(rp.boff), L.ncells);
+    exclusive_scan_i64(utiles, upre, nunits, st);
+    HIP_CHECK(hipGetLastError());
+    int64_t kept = 0;
+    HIP_CHECK(hipMemcpyAsync(&kept, P<int64_t>(rp.boff) + L.ncells, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    // host block: [coff (ncells+1) | toff (nt+1) | cpre (nt+1)]
-    std::vector<int64_t> hb((size_t)L.ncells + 1 + 2 * ((size_t)L.nt + 1), 0);
-    int64_t* coff = hb.data();
-    int64_t* toff = coff + L.ncells + 1;
-    int64_t* cpre = toff + L.nt + 1;
-    for (int c = 0; c < L.ncells; ++c) coff[c + 1] = coff[c] + hc[c];
-    for (int j = 0; j <= L.nt; ++j) toff[j] = coff[(int64_t)j * L.ns];
-    for (int j = 0; j < L.nt; ++j) cpre[j + 1] = cpre[j] + (toff[j + 1] - toff[j] + part::kTile - 1) / part::kTile;
-    rp.kept = coff[L.ncells];
-    rp.boff = dev_alloc(sizeof(int64_t) * hb.size(), st);
-    HIP_CHECK(hipMemcpyAsync(P<void>(rp.boff), hb.data(), sizeof(int64_t) * hb.size(), hipMemcpyHostToDevice, st));
-    // scatter cursors start at the bucket offsets
-    Buf cur = dev_alloc(sizeof(int64_t) * ((size_t)L.ncells + L.nt), st);
-    HIP_CHECK(hipMemcpyAsync(P<void>(cur), toff, sizeof(int64_t) * L.nt, hipMemcpyHostToDevice, st));
-    HIP_CHECK(hipMemcpyAsync(P<int64_t>(cur) + L.nt, coff, sizeof(int64_t) * L.ncells, hipMemcpyHostToDevice, st));
-    HIP_CHECK(hipStreamSynchronize(st));  // host vectors go out of scope
+    rp.kept = kept;
     const size_t bytes = sizeof(uint2) * (rp.kept > 0 ? rp.kept : 1);
-    Buf tmp = dev_alloc(bytes, st);
     rp.pairs = dev_alloc(bytes, st);
     if (rp.kept == 0) return;
-    const size_t lds1 = part::scatter_lds(L.nt), lds2 = part::scatter_lds(L.ns);
-    allow_lds(part::k_scatter_t, lds1);
-    allow_lds(part::k_scatter_s, lds2);
+    Buf tmp = dev_alloc(bytes, st);
+    const size_t lds1 = scatter_lds(L.nt), lds2 = scatter_lds(L.ns);
+    allow_lds(k_scatter_t, lds1);
+    allow_lds(k_scatter_s, lds2);
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
-        int64_t g = (ms[i] + part::kTile - 1) / part::kTile;
-        if (g > cap * 2) g = cap * 2;
         KernelTimer kt(s, "part_scatter_t");
-        hipLaunchKernelGGL(part::k_scatter_t, dim3((unsigned)g), dim3(part::kBlock), lds1, st, srcs[i], dsts[i], ms[i],
-                           L, P<unsigned long long>(cur), P<uint2>(tmp));
+        hipLaunchKernelGGL(k_scatter_t, dim3(grid), dim3(kBlock), lds1, st, srcs[i], dsts[i], ms[i], L,
+                           P<unsigned long long>(cur1), P<uint2>(tmp));
     }
     {
-        int64_t g = cpre[L.nt];
-        if (g > cap * 2) g = cap * 2;
         KernelTimer kt(s, "part_scatter_s");
-        hipLaunchKernelGGL(part::k_scatter_s, dim3((unsigned)g), dim3(part::kBlock), lds2, st, P<uint2>(tmp),
-                           P<int64_t>(rp.boff) + L.ncells + 1, P<int64_t>(rp.boff) + L.ncells + 1 + L.nt + 1, L,
-                           P<unsigned long long>(cur) + L.nt, P<uint2>(rp.pairs));
+        hipLaunchKernelGGL(k_scatter_s, dim3(grid), dim3(kBlock), lds2, st, P<uint2>(tmp), ustart, ulen, upre, L,
+                           P<unsigned long long>(pre), P<uint2>(rp.pairs));
     }
     HIP_CHECK(hipGetLastError());
 }

@@ -94,3 +94,21 @@ def test_rels_outside_domain_are_dropped(session):
     allok = np.ones(n, bool)
     assert rp.count_distinct(bm, bm, bm) == _np_count_distinct(n, s, d, allok, allok, allok)
     rp.release()
+
+
+def test_several_rel_tables(session):
+    """Relationship types as separate tables (a union of rel scans): same answer as one table."""
+    from capsmi import graph
+    scale = 20
+    n, m = 1 << scale, 8 << scale
+    cut = [0, m // 3, m // 3 + 12345, m]
+    parts = [graph.rmat_rels(session, scale, cut[k], cut[k + 1]) for k in range(3)]
+    whole = graph.rmat_rels(session, scale, 0, m)
+    src, dst = whole.column("source").values, whole.column("target").values
+    ok = np.ones(n, bool)
+    bm = _bitmap(session, n, np.arange(n))
+    want = _np_count_distinct(n, src, dst, ok, ok, ok)
+    rp = graph.RelPartition(session, parts, 0, n)
+    assert rp.size == m
+    assert rp.count_distinct(bm, bm, bm) == want
+    rp.release()
