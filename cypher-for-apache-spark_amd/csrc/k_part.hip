@@ -30,7 +30,7 @@ constexpr int kMaxTSlices = 4096;                // domain <= 2^31 ids
 constexpr int kBlock = 1024;
 constexpr int kItems = 8;
 constexpr int kTile = kBlock * kItems;           // relationships per scatter tile
-constexpr int kUnroll = 4;                       // loads in flight per lane in the hops
+constexpr int kUnroll = 8;                       // loads in flight per lane in the hops
 constexpr int64_t kLoadMin = 8192;               // pull a source slice into LDS for >= this many rels
 constexpr int kReps = 32;                        // cursor replicas per bucket (see TileWalk)
 
@@ -90,9 +90,33 @@ struct TileWalk {
     __device__ int64_t tile(int64_t k) const { return (int64_t)r + (int64_t)kReps * ((int64_t)q + k * bpr); }
 };
 
+// Issue all of a tile's loads before any test (indices clamped into [0, m)): with a branch
+// around each load the compiler waits for every load before issuing the next.
+__device__ __forceinline__ void load_tile(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t t0,
+                                          int64_t m, int64_t (&sr)[kItems], int64_t (&tr)[kItems]) {
+    const int64_t* __restrict__ sp = src + t0;  // wave-uniform bases, 32-bit lane offsets
+    const int64_t* __restrict__ dp = dst + t0;
+    if (t0 + kTile <= m) {
+#pragma unroll
+        for (int u = 0; u < kItems; ++u) {
+            const int i = u * kBlock + (int)threadIdx.x;
+            sr[u] = sp[i];
+            tr[u] = dp[i];
+        }
+    } else {
+        const int last = (int)(m - 1 - t0);
+#pragma unroll
+        for (int u = 0; u < kItems; ++u) {
+            const int i = min(u * kBlock + (int)threadIdx.x, last);
+            sr[u] = sp[i];
+            tr[u] = dp[i];
+        }
+    }
+}
+
 // pass 0: per-replica cell sizes (rels with an endpoint outside [lo, hi) can never match a node
 // scan over that domain and are dropped here -- an inner join drops them the same way)
-__global__ void __launch_bounds__(kBlock) k_part_hist(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) k_part_hist(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                       int64_t m, Layout L, unsigned int* __restrict__ counts) {
     extern __shared__ __attribute__((aligned(16))) unsigned int h[];
     for (int i = threadIdx.x; i < L.ncells; i += kBlock) h[i] = 0;
@@ -102,13 +126,13 @@ __global__ void __launch_bounds__(kBlock) k_part_hist(const int64_t* __restrict_
     for (int64_t k = 0;; ++k) {
         const int64_t t0 = w.tile(k) * kTile;
         if (t0 >= m) break;
+        int64_t sr[kItems], tr[kItems];
+        load_tile(src, dst, t0, m, sr, tr);
 #pragma unroll
         for (int u = 0; u < kItems; ++u) {
             const int64_t e = t0 + (int64_t)u * kBlock + threadIdx.x;
-            if (e < m) {
-                const uint64_t s = (uint64_t)(src[e] - L.lo), t = (uint64_t)(dst[e] - L.lo);
-                if (s < range && t < range) atomicAdd(&h[cell_of(L, (uint32_t)s, (uint32_t)t)], 1u);
-            }
+            const uint64_t s = (uint64_t)(sr[u] - L.lo), t = (uint64_t)(tr[u] - L.lo);
+            if (e < m && s < range && t < range) atomicAdd(&h[cell_of(L, (uint32_t)s, (uint32_t)t)], 1u);
         }
     }
     __syncthreads();
@@ -167,7 +191,7 @@ __host__ __device__ constexpr size_t scatter_lds(int nb) {
 // each bucket's run with one atomic on the replica's cursor, regroup the tile in LDS, write the
 // runs out.
 __device__ __forceinline__ void scatter_tile(const uint32_t (&sv)[kItems], const uint32_t (&tv)[kItems],
-                                             const int (&bk)[kItems], const uint32_t (&rk)[kItems], int nb,
+                                             uint32_t valid, const uint32_t (&rk)[kItems], int nb,
                                              unsigned long long* __restrict__ cursor, uint2* __restrict__ out,
                                              uint2* stage, unsigned long long* base, uint32_t* cnt, uint32_t* loc,
                                              uint32_t* wtot, bool by_target, int sbits) {
@@ -178,7 +202,10 @@ __device__ __forceinline__ void scatter_tile(const uint32_t (&sv)[kItems], const
     const uint32_t total = block_exclusive_scan(cnt, loc, nb, wtot);
 #pragma unroll
     for (int k = 0; k < kItems; ++k)
-        if (bk[k] >= 0) stage[loc[bk[k]] + rk[k]] = make_uint2(sv[k], tv[k]);
+        if ((valid >> k) & 1u) {
+            const int b = by_target ? (int)(tv[k] >> kSliceBits) : (int)(sv[k] >> sbits);
+            stage[loc[b] + rk[k]] = make_uint2(sv[k], tv[k]);
+        }
     __syncthreads();
     for (uint32_t idx = threadIdx.x; idx < total; idx += kBlock) {
         const uint2 p = stage[idx];
@@ -190,7 +217,7 @@ __device__ __forceinline__ void scatter_tile(const uint32_t (&sv)[kItems], const
 
 // pass 1: int64 (source, target) -> uint32 pairs grouped by target slice, replica-major within
 // each slice; cursor = cur1[r][j]
-__global__ void __launch_bounds__(kBlock) k_scatter_t(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) k_scatter_t(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                       int64_t m, Layout L, unsigned long long* __restrict__ cur1,
                                                       uint2* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
@@ -209,32 +236,32 @@ __global__ void __launch_bounds__(kBlock) k_scatter_t(const int64_t* __restrict_
         for (int i = threadIdx.x; i < nb; i += kBlock) cnt[i] = 0;
         __syncthreads();
         uint32_t sv[kItems], tv[kItems], rk[kItems];
-        int bk[kItems];
+        uint32_t valid = 0;  // bit u: item u is kept
+        {
+            int64_t sr[kItems], tr[kItems];
+            load_tile(src, dst, t0, m, sr, tr);
 #pragma unroll
-        for (int u = 0; u < kItems; ++u) {
-            const int64_t e = t0 + (int64_t)u * kBlock + threadIdx.x;
-            bk[u] = -1;
-            sv[u] = tv[u] = rk[u] = 0;
-            if (e < m) {
-                const uint64_t s = (uint64_t)(src[e] - L.lo), t = (uint64_t)(dst[e] - L.lo);
-                if (s < range && t < range) {
-                    sv[u] = (uint32_t)s;
-                    tv[u] = (uint32_t)t;
-                    bk[u] = (int)(tv[u] >> kSliceBits);
-                }
+            for (int u = 0; u < kItems; ++u) {
+                const int64_t e = t0 + (int64_t)u * kBlock + threadIdx.x;
+                const uint64_t s = (uint64_t)(sr[u] - L.lo), t = (uint64_t)(tr[u] - L.lo);
+                const bool ok = e < m && s < range && t < range;
+                sv[u] = (uint32_t)s;
+                tv[u] = (uint32_t)t;
+                valid |= (ok ? 1u : 0u) << u;
+                rk[u] = 0;
             }
         }
 #pragma unroll
         for (int u = 0; u < kItems; ++u)
-            if (bk[u] >= 0) rk[u] = atomicAdd(&cnt[bk[u]], 1u);
+            if ((valid >> u) & 1u) rk[u] = atomicAdd(&cnt[tv[u] >> kSliceBits], 1u);
         __syncthreads();
-        scatter_tile(sv, tv, bk, rk, nb, cursor, out, stage, base, cnt, loc, wtot, true, L.sbits);
+        scatter_tile(sv, tv, valid, rk, nb, cursor, out, stage, base, cnt, loc, wtot, true, L.sbits);
     }
 }
 
 // pass 2: unit u = (target slice j, replica r) -> the source cells of slice j; cursor cur2[r][j][*].
 // Global tile k belongs to the unit with upre[u] <= k < upre[u + 1].
-__global__ void __launch_bounds__(kBlock) k_scatter_s(const uint2* __restrict__ in, const int64_t* __restrict__ ustart,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) k_scatter_s(const uint2* __restrict__ in, const int64_t* __restrict__ ustart,
                                                       const int64_t* __restrict__ ulen,
                                                       const int64_t* __restrict__ upre, Layout L,
                                                       unsigned long long* __restrict__ cur2,
@@ -260,24 +287,26 @@ __global__ void __launch_bounds__(kBlock) k_scatter_s(const uint2* __restrict__ 
         for (int i = threadIdx.x; i < nb; i += kBlock) cnt[i] = 0;
         __syncthreads();
         uint32_t sv[kItems], tv[kItems], rk[kItems];
-        int bk[kItems];
+        uint32_t valid = 0;
+        uint2 pr[kItems];
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {  // all loads first (clamped), then the tests
+            const int64_t e = b0 + (int64_t)k * kBlock + threadIdx.x;
+            pr[k] = in[e < b1 ? e : b0];
+        }
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {
             const int64_t e = b0 + (int64_t)k * kBlock + threadIdx.x;
-            bk[k] = -1;
-            sv[k] = tv[k] = rk[k] = 0;
-            if (e < b1) {
-                const uint2 p = in[e];
-                sv[k] = p.x;
-                tv[k] = p.y;
-                bk[k] = (int)(p.x >> L.sbits);
-            }
+            sv[k] = pr[k].x;
+            tv[k] = pr[k].y;
+            valid |= (e < b1 ? 1u : 0u) << k;
+            rk[k] = 0;
         }
 #pragma unroll
         for (int k = 0; k < kItems; ++k)
-            if (bk[k] >= 0) rk[k] = atomicAdd(&cnt[bk[k]], 1u);
+            if ((valid >> k) & 1u) rk[k] = atomicAdd(&cnt[sv[k] >> L.sbits], 1u);
         __syncthreads();
-        scatter_tile(sv, tv, bk, rk, nb, cur2 + (size_t)r * L.ncells + (size_t)j * nb, out, stage, base, cnt, loc,
+        scatter_tile(sv, tv, valid, rk, nb, cur2 + (size_t)r * L.ncells + (size_t)j * nb, out, stage, base, cnt, loc,
                      wtot, false, L.sbits);
     }
 }
@@ -359,14 +388,14 @@ __global__ void __launch_bounds__(kBlock) k_hop_2d(const uint2* __restrict__ pai
         for (int64_t e = e0 + threadIdx.x; e < ce; e += (int64_t)kBlock * kUnroll) {
             uint2 p[kUnroll];
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
+            for (int u = 0; u < kUnroll; ++u) {  // all loads first (clamped), then the tests
                 const int64_t eu = e + (int64_t)u * kBlock;
-                p[u] = eu < ce ? pairs[eu] : make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+                p[u] = pairs[eu < ce ? eu : e];
             }
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
+                if (e + (int64_t)u * kBlock >= ce) continue;
                 const uint32_t s = p[u].x, t = p[u].y;
-                if (s == 0xFFFFFFFFu && t == 0xFFFFFFFFu) continue;
                 if (s != t) {
                     const bool ok = SRC_FULL || (pull ? gbit(sl, s - sbase) : gbit(sb.w, s));
                     if (ok) lds_set(tl, t - tbase);
