@@ -27,19 +27,22 @@ constexpr int kSliceBits = 19;                   // 2^19 ids per slice = 64 KiB 
 constexpr int kSliceWords = 1 << (kSliceBits - 5);
 constexpr int kMaxCells = 16384;                 // cell histogram = 64 KiB of LDS
 constexpr int kMaxTSlices = 4096;                // domain <= 2^31 ids
-constexpr int kBlock = 1024;
-constexpr int kItems = 8;
-constexpr int kTile = kBlock * kItems;           // relationships per scatter tile
+constexpr int kBlock = 1024;                     // histogram and hop workgroups
+constexpr int kItems = 8;                        // relationships per lane per tile
+constexpr int kRepTile = kBlock * kItems;        // replica assignment unit (8192 rels, see TileWalk)
+constexpr int kSBlock = 512;                     // scatter workgroups: 4 per CU overlap their phases
+constexpr int kTile = kSBlock * kItems;          // relationships per scatter tile (4096)
 constexpr int kUnroll = 8;                       // loads in flight per lane in the hops
 constexpr int64_t kLoadMin = 8192;               // pull a source slice into LDS for >= this many rels
 constexpr int kReps = 32;                        // cursor replicas per bucket (see TileWalk)
 
 using Layout = PartLayout;
 
-// Exclusive scan of in[0..n) into out[0..n) by a 1024-lane block; returns the total.
-// `wtot` is 16 words of LDS scratch.  Contains barriers: call from block-uniform code.
+// Exclusive scan of in[0..n) into out[0..n) by a B-lane block; returns the total.
+// `wtot` is B/64 words of LDS scratch.  Contains barriers: call from block-uniform code.
+template <int B>
 __device__ uint32_t block_exclusive_scan(const uint32_t* in, uint32_t* out, int n, uint32_t* wtot) {
-    const int per = (n + kBlock - 1) / kBlock;
+    const int per = (n + B - 1) / B;
     const int b = threadIdx.x * per;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t sum = 0;
@@ -54,13 +57,13 @@ __device__ uint32_t block_exclusive_scan(const uint32_t* in, uint32_t* out, int 
     if (lane == 63) wtot[wave] = x;
     __syncthreads();
     if (threadIdx.x < 64) {
-        uint32_t v = lane < kBlock / 64 ? wtot[lane] : 0u;
+        uint32_t v = lane < B / 64 ? wtot[lane] : 0u;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = __shfl_up(v, o, 64);
             if (lane >= o) v += y;
         }
-        if (lane < kBlock / 64) wtot[lane] = v;
+        if (lane < B / 64) wtot[lane] = v;
     }
     __syncthreads();
     uint32_t pre = x - sum + (wave > 0 ? wtot[wave - 1] : 0u);
@@ -70,7 +73,7 @@ __device__ uint32_t block_exclusive_scan(const uint32_t* in, uint32_t* out, int 
             out[b + k] = pre;
             pre += c;
         }
-    const uint32_t total = wtot[kBlock / 64 - 1];
+    const uint32_t total = wtot[B / 64 - 1];
     __syncthreads();
     return total;
 }
@@ -92,14 +95,15 @@ struct TileWalk {
 
 // Issue all of a tile's loads before any test (indices clamped into [0, m)): with a branch
 // around each load the compiler waits for every load before issuing the next.
+template <int B>
 __device__ __forceinline__ void load_tile(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t t0,
                                           int64_t m, int64_t (&sr)[kItems], int64_t (&tr)[kItems]) {
     const int64_t* __restrict__ sp = src + t0;  // wave-uniform bases, 32-bit lane offsets
     const int64_t* __restrict__ dp = dst + t0;
-    if (t0 + kTile <= m) {
+    if (t0 + B * kItems <= m) {
 #pragma unroll
         for (int u = 0; u < kItems; ++u) {
-            const int i = u * kBlock + (int)threadIdx.x;
+            const int i = u * B + (int)threadIdx.x;
             sr[u] = sp[i];
             tr[u] = dp[i];
         }
@@ -107,7 +111,7 @@ __device__ __forceinline__ void load_tile(const int64_t* __restrict__ src, const
         const int last = (int)(m - 1 - t0);
 #pragma unroll
         for (int u = 0; u < kItems; ++u) {
-            const int i = min(u * kBlock + (int)threadIdx.x, last);
+            const int i = min(u * B + (int)threadIdx.x, last);
             sr[u] = sp[i];
             tr[u] = dp[i];
         }
@@ -124,10 +128,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
     const uint64_t range = (uint64_t)(L.hi - L.lo);
     const TileWalk w;
     for (int64_t k = 0;; ++k) {
-        const int64_t t0 = w.tile(k) * kTile;
+        const int64_t t0 = w.tile(k) * kRepTile;
         if (t0 >= m) break;
         int64_t sr[kItems], tr[kItems];
-        load_tile(src, dst, t0, m, sr, tr);
+        load_tile<kBlock>(src, dst, t0, m, sr, tr);
 #pragma unroll
         for (int u = 0; u < kItems; ++u) {
             const int64_t e = t0 + (int64_t)u * kBlock + threadIdx.x;
@@ -182,9 +186,16 @@ __global__ void k_add_coff(int64_t* __restrict__ pre, const int64_t* __restrict_
     pre[i] += coff[i % ncells];
 }
 
-// LDS carve-up shared by both scatters: stage[kTile] | base[nb] (u64) | cnt[nb] | loc[nb] | wtot[16]
+// tile -> unit map for pass 2, one thread per unit
+__global__ void k_tile_unit(const int64_t* __restrict__ upre, int nunits, int* __restrict__ tile_unit) {
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= nunits) return;
+    for (int64_t k = upre[u]; k < upre[u + 1]; ++k) tile_unit[k] = u;
+}
+
+// LDS carve-up shared by both scatters: stage[kTile] | base[nb] (u64) | cnt[nb] | loc[nb] | wtot[kSBlock/64]
 __host__ __device__ constexpr size_t scatter_lds(int nb) {
-    return sizeof(uint2) * kTile + sizeof(unsigned long long) * nb + sizeof(uint32_t) * (2 * nb + 16);
+    return sizeof(uint2) * kTile + sizeof(unsigned long long) * nb + sizeof(uint32_t) * (2 * nb + kSBlock / 64);
 }
 
 // Tile body: items (s, t, bucket) are in registers with their rank within the bucket; reserve
@@ -195,11 +206,11 @@ __device__ __forceinline__ void scatter_tile(const uint32_t (&sv)[kItems], const
                                              unsigned long long* __restrict__ cursor, uint2* __restrict__ out,
                                              uint2* stage, unsigned long long* base, uint32_t* cnt, uint32_t* loc,
                                              uint32_t* wtot, bool by_target, int sbits) {
-    for (int i = threadIdx.x; i < nb; i += kBlock) {
+    for (int i = threadIdx.x; i < nb; i += kSBlock) {
         const uint32_t c = cnt[i];
         base[i] = c ? atomicAdd(&cursor[i], (unsigned long long)c) : 0ULL;
     }
-    const uint32_t total = block_exclusive_scan(cnt, loc, nb, wtot);
+    const uint32_t total = block_exclusive_scan<kSBlock>(cnt, loc, nb, wtot);
 #pragma unroll
     for (int k = 0; k < kItems; ++k)
         if ((valid >> k) & 1u) {
@@ -207,7 +218,7 @@ __device__ __forceinline__ void scatter_tile(const uint32_t (&sv)[kItems], const
             stage[loc[b] + rk[k]] = make_uint2(sv[k], tv[k]);
         }
     __syncthreads();
-    for (uint32_t idx = threadIdx.x; idx < total; idx += kBlock) {
+    for (uint32_t idx = threadIdx.x; idx < total; idx += kSBlock) {
         const uint2 p = stage[idx];
         const int b = by_target ? (int)(p.y >> kSliceBits) : (int)(p.x >> sbits);
         out[base[b] + (idx - loc[b])] = p;
@@ -217,7 +228,7 @@ __device__ __forceinline__ void scatter_tile(const uint32_t (&sv)[kItems], const
 
 // pass 1: int64 (source, target) -> uint32 pairs grouped by target slice, replica-major within
 // each slice; cursor = cur1[r][j]
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) k_scatter_t(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+__global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(8))) k_scatter_t(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                       int64_t m, Layout L, unsigned long long* __restrict__ cur1,
                                                       uint2* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
@@ -231,18 +242,19 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
     const TileWalk w;
     unsigned long long* cursor = cur1 + (size_t)w.r * nb;
     for (int64_t k = 0;; ++k) {
-        const int64_t t0 = w.tile(k) * kTile;
-        if (t0 >= m) break;  // block-uniform
-        for (int i = threadIdx.x; i < nb; i += kBlock) cnt[i] = 0;
+      const int64_t r0 = w.tile(k) * kRepTile;
+      if (r0 >= m) break;  // block-uniform
+      for (int64_t t0 = r0; t0 < min(r0 + (int64_t)kRepTile, m); t0 += kTile) {
+        for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
         __syncthreads();
         uint32_t sv[kItems], tv[kItems], rk[kItems];
         uint32_t valid = 0;  // bit u: item u is kept
         {
             int64_t sr[kItems], tr[kItems];
-            load_tile(src, dst, t0, m, sr, tr);
+            load_tile<kSBlock>(src, dst, t0, m, sr, tr);
 #pragma unroll
             for (int u = 0; u < kItems; ++u) {
-                const int64_t e = t0 + (int64_t)u * kBlock + threadIdx.x;
+                const int64_t e = t0 + (int64_t)u * kSBlock + threadIdx.x;
                 const uint64_t s = (uint64_t)(sr[u] - L.lo), t = (uint64_t)(tr[u] - L.lo);
                 const bool ok = e < m && s < range && t < range;
                 sv[u] = (uint32_t)s;
@@ -256,14 +268,16 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
             if ((valid >> u) & 1u) rk[u] = atomicAdd(&cnt[tv[u] >> kSliceBits], 1u);
         __syncthreads();
         scatter_tile(sv, tv, valid, rk, nb, cursor, out, stage, base, cnt, loc, wtot, true, L.sbits);
+      }
     }
 }
 
 // pass 2: unit u = (target slice j, replica r) -> the source cells of slice j; cursor cur2[r][j][*].
-// Global tile k belongs to the unit with upre[u] <= k < upre[u + 1].
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) k_scatter_s(const uint2* __restrict__ in, const int64_t* __restrict__ ustart,
+// Global tile k belongs to unit tile_unit[k] (upre[u] <= k < upre[u + 1]).
+__global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(8))) k_scatter_s(const uint2* __restrict__ in, const int64_t* __restrict__ ustart,
                                                       const int64_t* __restrict__ ulen,
-                                                      const int64_t* __restrict__ upre, Layout L,
+                                                      const int64_t* __restrict__ upre,
+                                                      const int* __restrict__ tile_unit, int64_t ntiles, Layout L,
                                                       unsigned long long* __restrict__ cur2,
                                                       uint2* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
@@ -273,30 +287,23 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
     uint32_t* cnt = reinterpret_cast<uint32_t*>(base + nb);
     uint32_t* loc = cnt + nb;
     uint32_t* wtot = loc + nb;
-    const int nunits = L.nt * kReps;
-    const int64_t ntiles = upre[nunits];
     for (int64_t ck = blockIdx.x; ck < ntiles; ck += gridDim.x) {
-        int lo = 0, hi = nunits;  // last u with upre[u] <= ck
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (upre[mid] <= ck) lo = mid; else hi = mid;
-        }
-        const int u = lo, j = u / kReps, r = u % kReps;
+        const int u = tile_unit[ck], j = u / kReps, r = u % kReps;
         const int64_t b0 = ustart[u] + (ck - upre[u]) * kTile;
         const int64_t b1 = min(b0 + (int64_t)kTile, ustart[u] + ulen[u]);
-        for (int i = threadIdx.x; i < nb; i += kBlock) cnt[i] = 0;
+        for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
         __syncthreads();
         uint32_t sv[kItems], tv[kItems], rk[kItems];
         uint32_t valid = 0;
         uint2 pr[kItems];
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {  // all loads first (clamped), then the tests
-            const int64_t e = b0 + (int64_t)k * kBlock + threadIdx.x;
+            const int64_t e = b0 + (int64_t)k * kSBlock + threadIdx.x;
             pr[k] = in[e < b1 ? e : b0];
         }
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {
-            const int64_t e = b0 + (int64_t)k * kBlock + threadIdx.x;
+            const int64_t e = b0 + (int64_t)k * kSBlock + threadIdx.x;
             sv[k] = pr[k].x;
             tv[k] = pr[k].y;
             valid |= (e < b1 ? 1u : 0u) << k;
@@ -486,8 +493,9 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
                        P<int64_t>(pre), P<int64_t>(rp.boff), L.ncells);
     exclusive_scan_i64(utiles, upre, nunits, st);
     HIP_CHECK(hipGetLastError());
-    int64_t kept = 0;
+    int64_t kept = 0, ntiles = 0;
     HIP_CHECK(hipMemcpyAsync(&kept, P<int64_t>(rp.boff) + L.ncells, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(&ntiles, upre + nunits, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
     rp.kept = kept;
     const size_t bytes = sizeof(uint2) * (rp.kept > 0 ? rp.kept : 1);
@@ -497,16 +505,20 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
     const size_t lds1 = scatter_lds(L.nt), lds2 = scatter_lds(L.ns);
     allow_lds(k_scatter_t, lds1);
     allow_lds(k_scatter_s, lds2);
+    Buf tmap = dev_alloc(sizeof(int) * (ntiles > 0 ? ntiles : 1), st);
+    hipLaunchKernelGGL(k_tile_unit, dim3((nunits + 255) / 256), dim3(256), 0, st, upre, nunits, P<int>(tmap));
+    // scatter blocks: kSBlock lanes, about four per CU, a multiple of kReps
+    const int sgrid = kReps * (int)std::max<int64_t>(1, (4 * (int64_t)s->num_cus + kReps - 1) / kReps);
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
         KernelTimer kt(s, "part_scatter_t");
-        hipLaunchKernelGGL(k_scatter_t, dim3(grid), dim3(kBlock), lds1, st, srcs[i], dsts[i], ms[i], L,
+        hipLaunchKernelGGL(k_scatter_t, dim3(sgrid), dim3(kSBlock), lds1, st, srcs[i], dsts[i], ms[i], L,
                            P<unsigned long long>(cur1), P<uint2>(tmp));
     }
     {
         KernelTimer kt(s, "part_scatter_s");
-        hipLaunchKernelGGL(k_scatter_s, dim3(grid), dim3(kBlock), lds2, st, P<uint2>(tmp), ustart, ulen, upre, L,
-                           P<unsigned long long>(pre), P<uint2>(rp.pairs));
+        hipLaunchKernelGGL(k_scatter_s, dim3(sgrid), dim3(kSBlock), lds2, st, P<uint2>(tmp), ustart, ulen, upre,
+                           P<int>(tmap), ntiles, L, P<unsigned long long>(pre), P<uint2>(rp.pairs));
     }
     HIP_CHECK(hipGetLastError());
 }
