@@ -30,10 +30,11 @@ constexpr int kMaxTSlices = 4096;                // domain <= 2^31 ids
 constexpr int kBlock = 1024;                     // histogram and hop workgroups
 constexpr int kItems = 8;                        // relationships per lane per tile
 constexpr int kRepTile = kBlock * kItems;        // replica assignment unit (8192 rels, see TileWalk)
-constexpr int kSBlock = 512;                     // scatter workgroups: 4 per CU overlap their phases
-constexpr int kTile = kSBlock * kItems;          // relationships per scatter tile (4096)
+constexpr int kSBlock = 1024;                    // scatter workgroups (512 lanes x 4096 rels measured slower)
+constexpr int kTile = kSBlock * kItems;          // relationships per scatter tile (8192)
 constexpr int kUnroll = 8;                       // loads in flight per lane in the hops
 constexpr int64_t kLoadMin = 8192;               // pull a source slice into LDS for >= this many rels
+constexpr int kPad = 2 * 8192;                   // slack pairs after every pair array (load_pairs)
 constexpr int kReps = 32;                        // cursor replicas per bucket (see TileWalk)
 
 using Layout = PartLayout;
@@ -93,28 +94,54 @@ struct TileWalk {
     __device__ int64_t tile(int64_t k) const { return (int64_t)r + (int64_t)kReps * ((int64_t)q + k * bpr); }
 };
 
-// Issue all of a tile's loads before any test (indices clamped into [0, m)): with a branch
-// around each load the compiler waits for every load before issuing the next.
+// Tile item u of this lane is relationship t0 + item_off<B>(u): lanes read 16-byte pairs of
+// consecutive relationships (2 int64 per load, the calibrated streaming width), pair k of the
+// tile at offset 2 * (k * B + lane).
+template <int B>
+__device__ __forceinline__ int item_off(int u) {
+    return 2 * ((u >> 1) * B + (int)threadIdx.x) + (u & 1);
+}
+
+// Issue all of a tile's loads before any test: with a branch around each load the compiler
+// waits for every load before issuing the next.  `vec` = both columns 16-byte aligned.
 template <int B>
 __device__ __forceinline__ void load_tile(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t t0,
-                                          int64_t m, int64_t (&sr)[kItems], int64_t (&tr)[kItems]) {
+                                          int64_t m, bool vec, int64_t (&sr)[kItems], int64_t (&tr)[kItems]) {
     const int64_t* __restrict__ sp = src + t0;  // wave-uniform bases, 32-bit lane offsets
     const int64_t* __restrict__ dp = dst + t0;
-    if (t0 + B * kItems <= m) {
+    if (vec && t0 + B * kItems <= m) {
+        const longlong2* __restrict__ sv = reinterpret_cast<const longlong2*>(sp);
+        const longlong2* __restrict__ dv = reinterpret_cast<const longlong2*>(dp);
 #pragma unroll
-        for (int u = 0; u < kItems; ++u) {
-            const int i = u * B + (int)threadIdx.x;
-            sr[u] = sp[i];
-            tr[u] = dp[i];
+        for (int k = 0; k < kItems / 2; ++k) {
+            const longlong2 a = sv[k * B + (int)threadIdx.x], b = dv[k * B + (int)threadIdx.x];
+            sr[2 * k] = a.x;
+            sr[2 * k + 1] = a.y;
+            tr[2 * k] = b.x;
+            tr[2 * k + 1] = b.y;
         }
     } else {
-        const int last = (int)(m - 1 - t0);
+        const int last = (int)(min(m - t0, (int64_t)B * kItems) - 1);
 #pragma unroll
         for (int u = 0; u < kItems; ++u) {
-            const int i = min(u * B + (int)threadIdx.x, last);
+            const int i = min(item_off<B>(u), last);
             sr[u] = sp[i];
             tr[u] = dp[i];
         }
+    }
+}
+
+// The B * N pairs of a packed uint2 array starting at the even, wave-uniform index b, as 16-byte
+// loads: this lane's item u is b + item_off<B>(u).  Pair arrays are allocated with kPad pairs of
+// slack so a tile may run past the last pair; callers mask items outside their range.
+template <int B, int N>
+__device__ __forceinline__ void load_pairs(const uint2* __restrict__ in, int64_t b, uint2 (&p)[N]) {
+    const uint4* __restrict__ v = reinterpret_cast<const uint4*>(in + b);
+#pragma unroll
+    for (int k = 0; k < N / 2; ++k) {
+        const uint4 x = v[k * B + (int)threadIdx.x];
+        p[2 * k] = make_uint2(x.x, x.y);
+        p[2 * k + 1] = make_uint2(x.z, x.w);
     }
 }
 
@@ -126,15 +153,16 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
     for (int i = threadIdx.x; i < L.ncells; i += kBlock) h[i] = 0;
     __syncthreads();
     const uint64_t range = (uint64_t)(L.hi - L.lo);
+    const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
     const TileWalk w;
     for (int64_t k = 0;; ++k) {
         const int64_t t0 = w.tile(k) * kRepTile;
         if (t0 >= m) break;
         int64_t sr[kItems], tr[kItems];
-        load_tile<kBlock>(src, dst, t0, m, sr, tr);
+        load_tile<kBlock>(src, dst, t0, m, vec, sr, tr);
 #pragma unroll
         for (int u = 0; u < kItems; ++u) {
-            const int64_t e = t0 + (int64_t)u * kBlock + threadIdx.x;
+            const int64_t e = t0 + item_off<kBlock>(u);
             const uint64_t s = (uint64_t)(sr[u] - L.lo), t = (uint64_t)(tr[u] - L.lo);
             if (e < m && s < range && t < range) atomicAdd(&h[cell_of(L, (uint32_t)s, (uint32_t)t)], 1u);
         }
@@ -176,7 +204,7 @@ __global__ void k_units(const unsigned int* __restrict__ cnt, const int64_t* __r
     cur1[(size_t)r * L.nt + j] = st;
     ustart[u] = st;
     ulen[u] = len;
-    utiles[u] = (len + kTile - 1) / kTile;
+    utiles[u] = len > 0 ? (st + len - (st & ~int64_t(1)) + kTile - 1) / kTile : 0;  // tiles on an even grid
 }
 
 // pass-2 cursors: cur2[r][c] = coff[c] + pre[r][c] (in place)
@@ -201,8 +229,7 @@ __host__ __device__ constexpr size_t scatter_lds(int nb) {
 // Tile body: items (s, t, bucket) are in registers with their rank within the bucket; reserve
 // each bucket's run with one atomic on the replica's cursor, regroup the tile in LDS, write the
 // runs out.
-__device__ __forceinline__ void scatter_tile(const uint32_t (&sv)[kItems], const uint32_t (&tv)[kItems],
-                                             uint32_t valid, const uint32_t (&rk)[kItems], int nb,
+__device__ __forceinline__ void scatter_tile(const uint2 (&pr)[kItems], uint32_t valid, const uint32_t (&rk)[kItems], int nb,
                                              unsigned long long* __restrict__ cursor, uint2* __restrict__ out,
                                              uint2* stage, unsigned long long* base, uint32_t* cnt, uint32_t* loc,
                                              uint32_t* wtot, bool by_target, int sbits) {
@@ -214,8 +241,8 @@ __device__ __forceinline__ void scatter_tile(const uint32_t (&sv)[kItems], const
 #pragma unroll
     for (int k = 0; k < kItems; ++k)
         if ((valid >> k) & 1u) {
-            const int b = by_target ? (int)(tv[k] >> kSliceBits) : (int)(sv[k] >> sbits);
-            stage[loc[b] + rk[k]] = make_uint2(sv[k], tv[k]);
+            const int b = by_target ? (int)(pr[k].y >> kSliceBits) : (int)(pr[k].x >> sbits);
+            stage[loc[b] + rk[k]] = pr[k];
         }
     __syncthreads();
     for (uint32_t idx = threadIdx.x; idx < total; idx += kSBlock) {
@@ -239,6 +266,7 @@ __global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(8)
     uint32_t* loc = cnt + nb;
     uint32_t* wtot = loc + nb;
     const uint64_t range = (uint64_t)(L.hi - L.lo);
+    const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
     const TileWalk w;
     unsigned long long* cursor = cur1 + (size_t)w.r * nb;
     for (int64_t k = 0;; ++k) {
@@ -247,27 +275,27 @@ __global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(8)
       for (int64_t t0 = r0; t0 < min(r0 + (int64_t)kRepTile, m); t0 += kTile) {
         for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
         __syncthreads();
-        uint32_t sv[kItems], tv[kItems], rk[kItems];
+        uint2 pr[kItems];
+        uint32_t rk[kItems];
         uint32_t valid = 0;  // bit u: item u is kept
         {
             int64_t sr[kItems], tr[kItems];
-            load_tile<kSBlock>(src, dst, t0, m, sr, tr);
+            load_tile<kSBlock>(src, dst, t0, m, vec, sr, tr);
 #pragma unroll
             for (int u = 0; u < kItems; ++u) {
-                const int64_t e = t0 + (int64_t)u * kSBlock + threadIdx.x;
+                const int64_t e = t0 + item_off<kSBlock>(u);
                 const uint64_t s = (uint64_t)(sr[u] - L.lo), t = (uint64_t)(tr[u] - L.lo);
                 const bool ok = e < m && s < range && t < range;
-                sv[u] = (uint32_t)s;
-                tv[u] = (uint32_t)t;
+                pr[u] = make_uint2((uint32_t)s, (uint32_t)t);
                 valid |= (ok ? 1u : 0u) << u;
                 rk[u] = 0;
             }
         }
 #pragma unroll
         for (int u = 0; u < kItems; ++u)
-            if ((valid >> u) & 1u) rk[u] = atomicAdd(&cnt[tv[u] >> kSliceBits], 1u);
+            if ((valid >> u) & 1u) rk[u] = atomicAdd(&cnt[pr[u].y >> kSliceBits], 1u);
         __syncthreads();
-        scatter_tile(sv, tv, valid, rk, nb, cursor, out, stage, base, cnt, loc, wtot, true, L.sbits);
+        scatter_tile(pr, valid, rk, nb, cursor, out, stage, base, cnt, loc, wtot, true, L.sbits);
       }
     }
 }
@@ -289,31 +317,26 @@ __global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(8)
     uint32_t* wtot = loc + nb;
     for (int64_t ck = blockIdx.x; ck < ntiles; ck += gridDim.x) {
         const int u = tile_unit[ck], j = u / kReps, r = u % kReps;
-        const int64_t b0 = ustart[u] + (ck - upre[u]) * kTile;
-        const int64_t b1 = min(b0 + (int64_t)kTile, ustart[u] + ulen[u]);
+        const int64_t tb = (ustart[u] & ~int64_t(1)) + (ck - upre[u]) * kTile;  // even tile base
+        const int64_t b0 = max(tb, ustart[u]), b1 = min(tb + (int64_t)kTile, ustart[u] + ulen[u]);
         for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
         __syncthreads();
-        uint32_t sv[kItems], tv[kItems], rk[kItems];
+        uint32_t rk[kItems];
         uint32_t valid = 0;
         uint2 pr[kItems];
-#pragma unroll
-        for (int k = 0; k < kItems; ++k) {  // all loads first (clamped), then the tests
-            const int64_t e = b0 + (int64_t)k * kSBlock + threadIdx.x;
-            pr[k] = in[e < b1 ? e : b0];
-        }
+        load_pairs<kSBlock, kItems>(in, tb, pr);
+        const int lo = (int)(b0 - tb), hi = (int)(b1 - tb);  // 32-bit tile-relative bounds
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {
-            const int64_t e = b0 + (int64_t)k * kSBlock + threadIdx.x;
-            sv[k] = pr[k].x;
-            tv[k] = pr[k].y;
-            valid |= (e < b1 ? 1u : 0u) << k;
+            const int e = item_off<kSBlock>(k);
+            valid |= (e >= lo && e < hi ? 1u : 0u) << k;
             rk[k] = 0;
         }
 #pragma unroll
         for (int k = 0; k < kItems; ++k)
-            if ((valid >> k) & 1u) rk[k] = atomicAdd(&cnt[sv[k] >> L.sbits], 1u);
+            if ((valid >> k) & 1u) rk[k] = atomicAdd(&cnt[pr[k].x >> L.sbits], 1u);
         __syncthreads();
-        scatter_tile(sv, tv, valid, rk, nb, cur2 + (size_t)r * L.ncells + (size_t)j * nb, out, stage, base, cnt, loc,
+        scatter_tile(pr, valid, rk, nb, cur2 + (size_t)r * L.ncells + (size_t)j * nb, out, stage, base, cnt, loc,
                      wtot, false, L.sbits);
     }
 }
@@ -392,29 +415,29 @@ __global__ void __launch_bounds__(kBlock) k_hop_2d(const uint2* __restrict__ pai
         }
         __syncthreads();
         const uint32_t tbase = (uint32_t)j << kSliceBits, sbase = (uint32_t)i << kSliceBits;
-        for (int64_t e = e0 + threadIdx.x; e < ce; e += (int64_t)kBlock * kUnroll) {
-            uint2 p[kUnroll];
-#pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {  // all loads first (clamped), then the tests
-                const int64_t eu = e + (int64_t)u * kBlock;
-                p[u] = pairs[eu < ce ? eu : e];
+        auto visit = [&](const uint2 pr) {
+            const uint32_t s = pr.x, t = pr.y;
+            if (s != t) {
+                const bool ok = SRC_FULL || (pull ? gbit(sl, s - sbase) : gbit(sb.w, s));
+                if (ok) lds_set(tl, t - tbase);
+            } else if (HOP1) {  // rare: self-loops
+                if ((SRC_FULL || gbit(sb.w, s)) && (tmask.full || gbit(tmask.w, t))) {
+                    const uint32_t bit = 1u << (t & 31);
+                    const uint32_t old = atomicOr(&S1[t >> 5], bit);
+                    if (old & bit) atomicOr(&S2[t >> 5], bit);
+                }
+            } else {
+                if (gbit(X2, s)) lds_set(tl, t - tbase);
             }
+        };
+        for (int64_t cb = e0 & ~int64_t(1); cb < ce; cb += (int64_t)kBlock * kUnroll) {  // block-uniform, even
+            uint2 p[kUnroll];
+            load_pairs<kBlock, kUnroll>(pairs, cb, p);
+            const int lo = (int)max(e0 - cb, (int64_t)0), hi = (int)min(ce - cb, (int64_t)kBlock * kUnroll);
 #pragma unroll
             for (int u = 0; u < kUnroll; ++u) {
-                if (e + (int64_t)u * kBlock >= ce) continue;
-                const uint32_t s = p[u].x, t = p[u].y;
-                if (s != t) {
-                    const bool ok = SRC_FULL || (pull ? gbit(sl, s - sbase) : gbit(sb.w, s));
-                    if (ok) lds_set(tl, t - tbase);
-                } else if (HOP1) {  // rare: self-loops
-                    if ((SRC_FULL || gbit(sb.w, s)) && (tmask.full || gbit(tmask.w, t))) {
-                        const uint32_t bit = 1u << (t & 31);
-                        const uint32_t old = atomicOr(&S1[t >> 5], bit);
-                        if (old & bit) atomicOr(&S2[t >> 5], bit);
-                    }
-                } else {
-                    if (gbit(X2, s)) lds_set(tl, t - tbase);
-                }
+                const int e = item_off<kBlock>(u);
+                if (e >= lo && e < hi) visit(p[u]);
             }
         }
         e0 = ce;
@@ -498,7 +521,7 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
     HIP_CHECK(hipMemcpyAsync(&ntiles, upre + nunits, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
     rp.kept = kept;
-    const size_t bytes = sizeof(uint2) * (rp.kept > 0 ? rp.kept : 1);
+    const size_t bytes = sizeof(uint2) * ((rp.kept > 0 ? rp.kept : 1) + kPad);
     rp.pairs = dev_alloc(bytes, st);
     if (rp.kept == 0) return;
     Buf tmp = dev_alloc(bytes, st);
@@ -507,8 +530,8 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
     allow_lds(k_scatter_s, lds2);
     Buf tmap = dev_alloc(sizeof(int) * (ntiles > 0 ? ntiles : 1), st);
     hipLaunchKernelGGL(k_tile_unit, dim3((nunits + 255) / 256), dim3(256), 0, st, upre, nunits, P<int>(tmap));
-    // scatter blocks: kSBlock lanes, about four per CU, a multiple of kReps
-    const int sgrid = kReps * (int)std::max<int64_t>(1, (4 * (int64_t)s->num_cus + kReps - 1) / kReps);
+    // scatter blocks: kSBlock lanes, about two per CU, a multiple of kReps
+    const int sgrid = kReps * (int)std::max<int64_t>(1, (2 * (int64_t)s->num_cus + kReps - 1) / kReps);
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
         KernelTimer kt(s, "part_scatter_t");
