@@ -30,9 +30,8 @@ constexpr int kMaxTSlices = 4096;                // domain <= 2^31 ids
 constexpr int kBlock = 1024;                     // histogram and hop workgroups
 constexpr int kItems = 8;                        // relationships per lane per tile
 constexpr int kRepTile = kBlock * kItems;        // replica assignment unit (8192 rels, see TileWalk)
-constexpr int kSBlock = 512;                     // scatter workgroups: 2 per CU, 4 waves per SIMD ...
-constexpr int kSItems = 16;                      // ... with 16 rels per lane (registers for all loads in flight)
-constexpr int kTile = kSBlock * kSItems;         // relationships per scatter tile (8192)
+constexpr int kSBlock = 1024;                    // scatter workgroups (512 lanes x 4096 rels measured slower)
+constexpr int kTile = kSBlock * kItems;          // relationships per scatter tile (8192)
 constexpr int kUnroll = 8;                       // loads in flight per lane in the hops
 constexpr int64_t kLoadMin = 8192;               // pull a source slice into LDS for >= this many rels
 constexpr int kPad = 2 * 8192;                   // slack pairs after every pair array (load_pairs)
@@ -105,16 +104,16 @@ __device__ __forceinline__ int item_off(int u) {
 
 // Issue all of a tile's loads before any test: with a branch around each load the compiler
 // waits for every load before issuing the next.  `vec` = both columns 16-byte aligned.
-template <int B, int N>
+template <int B>
 __device__ __forceinline__ void load_tile(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t t0,
-                                          int64_t m, bool vec, int64_t (&sr)[N], int64_t (&tr)[N]) {
+                                          int64_t m, bool vec, int64_t (&sr)[kItems], int64_t (&tr)[kItems]) {
     const int64_t* __restrict__ sp = src + t0;  // wave-uniform bases, 32-bit lane offsets
     const int64_t* __restrict__ dp = dst + t0;
-    if (vec && t0 + B * N <= m) {
+    if (vec && t0 + B * kItems <= m) {
         const longlong2* __restrict__ sv = reinterpret_cast<const longlong2*>(sp);
         const longlong2* __restrict__ dv = reinterpret_cast<const longlong2*>(dp);
 #pragma unroll
-        for (int k = 0; k < N / 2; ++k) {
+        for (int k = 0; k < kItems / 2; ++k) {
             const longlong2 a = sv[k * B + (int)threadIdx.x], b = dv[k * B + (int)threadIdx.x];
             sr[2 * k] = a.x;
             sr[2 * k + 1] = a.y;
@@ -122,9 +121,9 @@ __device__ __forceinline__ void load_tile(const int64_t* __restrict__ src, const
             tr[2 * k + 1] = b.y;
         }
     } else {
-        const int last = (int)(min(m - t0, (int64_t)B * N) - 1);
+        const int last = (int)(min(m - t0, (int64_t)B * kItems) - 1);
 #pragma unroll
-        for (int u = 0; u < N; ++u) {
+        for (int u = 0; u < kItems; ++u) {
             const int i = min(item_off<B>(u), last);
             sr[u] = sp[i];
             tr[u] = dp[i];
@@ -160,7 +159,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))
         const int64_t t0 = w.tile(k) * kRepTile;
         if (t0 >= m) break;
         int64_t sr[kItems], tr[kItems];
-        load_tile<kBlock, kItems>(src, dst, t0, m, vec, sr, tr);
+        load_tile<kBlock>(src, dst, t0, m, vec, sr, tr);
 #pragma unroll
         for (int u = 0; u < kItems; ++u) {
             const int64_t e = t0 + item_off<kBlock>(u);
@@ -230,32 +229,21 @@ __host__ __device__ constexpr size_t scatter_lds(int nb) {
 // Tile body: items (s, t, bucket) are in registers with their rank within the bucket; reserve
 // each bucket's run with one atomic on the replica's cursor, regroup the tile in LDS, write the
 // runs out.
-__device__ __forceinline__ void scatter_tile(const uint2 (&pr)[kSItems], uint32_t valid, const uint32_t (&rk)[kSItems], int nb,
+__device__ __forceinline__ void scatter_tile(const uint2 (&pr)[kItems], uint32_t valid, const uint32_t (&rk)[kItems], int nb,
                                              unsigned long long* __restrict__ cursor, uint2* __restrict__ out,
                                              uint2* stage, unsigned long long* base, uint32_t* cnt, uint32_t* loc,
                                              uint32_t* wtot, bool by_target, int sbits) {
-    // the run reservations are returning atomics: with one bucket per lane they stay in flight
-    // (in registers) across the scan and the regrouping, and land in LDS only before the writes
-    unsigned long long mine = 0;
-    if (nb <= kSBlock) {
-        if ((int)threadIdx.x < nb) {
-            const uint32_t c = cnt[threadIdx.x];
-            if (c) mine = atomicAdd(&cursor[threadIdx.x], (unsigned long long)c);
-        }
-    } else {
-        for (int i = threadIdx.x; i < nb; i += kSBlock) {
-            const uint32_t c = cnt[i];
-            base[i] = c ? atomicAdd(&cursor[i], (unsigned long long)c) : 0ULL;
-        }
+    for (int i = threadIdx.x; i < nb; i += kSBlock) {
+        const uint32_t c = cnt[i];
+        base[i] = c ? atomicAdd(&cursor[i], (unsigned long long)c) : 0ULL;
     }
     const uint32_t total = block_exclusive_scan<kSBlock>(cnt, loc, nb, wtot);
 #pragma unroll
-    for (int k = 0; k < kSItems; ++k)
+    for (int k = 0; k < kItems; ++k)
         if ((valid >> k) & 1u) {
             const int b = by_target ? (int)(pr[k].y >> kSliceBits) : (int)(pr[k].x >> sbits);
             stage[loc[b] + rk[k]] = pr[k];
         }
-    if (nb <= kSBlock && (int)threadIdx.x < nb) base[threadIdx.x] = mine;
     __syncthreads();
     for (uint32_t idx = threadIdx.x; idx < total; idx += kSBlock) {
         const uint2 p = stage[idx];
@@ -267,7 +255,7 @@ __device__ __forceinline__ void scatter_tile(const uint2 (&pr)[kSItems], uint32_
 
 // pass 1: int64 (source, target) -> uint32 pairs grouped by target slice, replica-major within
 // each slice; cursor = cur1[r][j]
-__global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(4))) k_scatter_t(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+__global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(8))) k_scatter_t(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                       int64_t m, Layout L, unsigned long long* __restrict__ cur1,
                                                       uint2* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
@@ -287,14 +275,14 @@ __global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(4)
       for (int64_t t0 = r0; t0 < min(r0 + (int64_t)kRepTile, m); t0 += kTile) {
         for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
         __syncthreads();
-        uint2 pr[kSItems];
-        uint32_t rk[kSItems];
+        uint2 pr[kItems];
+        uint32_t rk[kItems];
         uint32_t valid = 0;  // bit u: item u is kept
         {
-            int64_t sr[kSItems], tr[kSItems];
-            load_tile<kSBlock, kSItems>(src, dst, t0, m, vec, sr, tr);
+            int64_t sr[kItems], tr[kItems];
+            load_tile<kSBlock>(src, dst, t0, m, vec, sr, tr);
 #pragma unroll
-            for (int u = 0; u < kSItems; ++u) {
+            for (int u = 0; u < kItems; ++u) {
                 const int64_t e = t0 + item_off<kSBlock>(u);
                 const uint64_t s = (uint64_t)(sr[u] - L.lo), t = (uint64_t)(tr[u] - L.lo);
                 const bool ok = e < m && s < range && t < range;
@@ -304,7 +292,7 @@ __global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(4)
             }
         }
 #pragma unroll
-        for (int u = 0; u < kSItems; ++u)
+        for (int u = 0; u < kItems; ++u)
             if ((valid >> u) & 1u) rk[u] = atomicAdd(&cnt[pr[u].y >> kSliceBits], 1u);
         __syncthreads();
         scatter_tile(pr, valid, rk, nb, cursor, out, stage, base, cnt, loc, wtot, true, L.sbits);
@@ -314,7 +302,7 @@ __global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(4)
 
 // pass 2: unit u = (target slice j, replica r) -> the source cells of slice j; cursor cur2[r][j][*].
 // Global tile k belongs to unit tile_unit[k] (upre[u] <= k < upre[u + 1]).
-__global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(4))) k_scatter_s(const uint2* __restrict__ in, const int64_t* __restrict__ ustart,
+__global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(8))) k_scatter_s(const uint2* __restrict__ in, const int64_t* __restrict__ ustart,
                                                       const int64_t* __restrict__ ulen,
                                                       const int64_t* __restrict__ upre,
                                                       const int* __restrict__ tile_unit, int64_t ntiles, Layout L,
@@ -333,19 +321,19 @@ __global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(4)
         const int64_t b0 = max(tb, ustart[u]), b1 = min(tb + (int64_t)kTile, ustart[u] + ulen[u]);
         for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
         __syncthreads();
-        uint32_t rk[kSItems];
+        uint32_t rk[kItems];
         uint32_t valid = 0;
-        uint2 pr[kSItems];
-        load_pairs<kSBlock, kSItems>(in, tb, pr);
+        uint2 pr[kItems];
+        load_pairs<kSBlock, kItems>(in, tb, pr);
         const int lo = (int)(b0 - tb), hi = (int)(b1 - tb);  // 32-bit tile-relative bounds
 #pragma unroll
-        for (int k = 0; k < kSItems; ++k) {
+        for (int k = 0; k < kItems; ++k) {
             const int e = item_off<kSBlock>(k);
             valid |= (e >= lo && e < hi ? 1u : 0u) << k;
             rk[k] = 0;
         }
 #pragma unroll
-        for (int k = 0; k < kSItems; ++k)
+        for (int k = 0; k < kItems; ++k)
             if ((valid >> k) & 1u) rk[k] = atomicAdd(&cnt[pr[k].x >> L.sbits], 1u);
         __syncthreads();
         scatter_tile(pr, valid, rk, nb, cur2 + (size_t)r * L.ncells + (size_t)j * nb, out, stage, base, cnt, loc,
