@@ -49,7 +49,9 @@ def parse():
     p.add_argument("--edge-factor", type=int, default=16)
     p.add_argument("--modes", default="cold,warm", help="comma list of cold, warm, stream (first = value)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-scale", type=int, default=20)
+    p.add_argument("--cpu-scale", type=int, default=None, help="oracle sample scale (default per workload)")
+    p.add_argument("--workload", default="c3", choices=("c2", "c3", "c4", "c5"),
+                   help="c3 (default, the BASELINE metric) or the single-GPU C2/C4/C5 lines (SURVEY.md 8d)")
     return p.parse_args()
 
 
@@ -86,6 +88,10 @@ def pmc_traffic(kernel):
 
 def main():
     args = parse()
+    if args.workload != "c3":
+        return run_single(args)
+    if args.cpu_scale is None:
+        args.cpu_scale = 20
     import torch
     import torch.distributed as dist
 
@@ -270,3 +276,128 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+# ---- single-GPU lines for the other SURVEY.md 8d configs ------------------------------------------
+SINGLE = {
+    # workload: (scale, edge factor, rmat probs, description, oracle sample scale)
+    "c2": (24, 16, (57, 19, 19), "C2: MATCH (a:Person)-[r:FRIEND_OF]->(b:Person) WHERE a.age >= 18 AND a.age < 65 "
+                                 "RETURN id(a), id(b)", 22),
+    "c4": (24, 16, (57, 19, 19), "C4: MATCH (a)-[r1:FRIEND_OF]->(b)-[r2:FRIEND_OF]->(c)-[r3:FRIEND_OF]->(a) "
+                                 "RETURN count(*)", 14),
+    "c5": (20, 32, (45, 15, 15), "C5: MATCH (a:Person)-[:KNOWS*1..3]->(b:Person) RETURN id(a), count(*)", 16),
+}
+
+
+def run_single(args):
+    """C2 / C4 / C5 on one GPU: cold = the whole query from resident entity tables.
+    value = matched rows / s; matched rows = the query's bindings (C2: result rows; C4: count(*);
+    C5: sum of the per-a counts).  Roofline: the dominant timed kernel's algorithmic bytes."""
+    import numpy as np
+    import torch
+    from capsmi import Session, _lib, graph
+    from capsmi.expr import Ands, BinOp, Col, Lit
+
+    wl = args.workload
+    scale, ef, probs, desc, cpu_scale = SINGLE[wl]
+    if args.scale != 26:  # --scale given explicitly
+        scale = args.scale
+    cpu_scale = args.cpu_scale or cpu_scale
+    n, m = 1 << scale, ef << scale
+    torch.cuda.set_device(0)
+    sess = Session(0)
+    sess.set_stream(torch.cuda.current_stream().cuda_stream)
+    rels = graph.rmat_rels(sess, scale, 0, m, probs, 42)
+    kind = graph.NODES_PERSON if wl == "c2" else graph.NODES_ALL
+    nodes = graph.rmat_nodes(sess, scale, kind, 42)
+    sess.sync()
+    pred = Ands((BinOp(">=", Col("age"), Lit(18)), BinOp("<", Col("age"), Lit(65))))
+    cache = {}
+
+    def step():
+        if wl == "c2":
+            a_ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id", pred)
+            b_ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id")
+            out = graph.expand_filter(sess, rels, a_ok, b_ok, ["source", "target"], ["a", "b"])
+            return out.size, out
+        ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id")
+        if wl == "c4":
+            return graph.triangle_count(sess, [rels], ok), None
+        out = graph.var_length_count(sess, [rels], ok, ok, 1, 3)
+        return None, out
+
+    kernels = ("bitmap_add", "expand_filter", "tri_pack", "triangles", "varlen_deg", "varlen_w", "varlen_rev",
+               "varlen_t")
+    for _ in range(args.warmup):
+        step()
+    _lib.call("capsmi_session_set_profiling", sess.handle, 1)
+    for k in kernels:  # reset
+        _lib.call("capsmi_session_kernel_time", sess.handle, k.encode(), ctypes.byref(ctypes.c_int64()),
+                  ctypes.byref(ctypes.c_double()))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res, out = step()
+    torch.cuda.synchronize()
+    sec = (time.perf_counter() - t0) / args.steps
+    kt = {}
+    for k in kernels:
+        c, ms = ctypes.c_int64(), ctypes.c_double()
+        _lib.call("capsmi_session_kernel_time", sess.handle, k.encode(), ctypes.byref(c), ctypes.byref(ms))
+        if c.value:
+            kt[k] = (c.value, ms.value)
+    _lib.call("capsmi_session_set_profiling", sess.handle, 0)
+    if wl == "c5":
+        res = int(out.column("count").values.sum())  # untimed export
+    matched = res
+    # algorithmic bytes per launch of the kernels whose traffic is a plain function of the input
+    alg = {"bitmap_add": n * 8, "expand_filter": m * 16 + (2 * res * 8 if wl == "c2" else 0),
+           "tri_pack": m * 24, "varlen_deg": m * 8, "varlen_w": m * 16, "varlen_rev": m * 16, "varlen_t": m * 16}
+    dom = max(kt, key=lambda k: kt[k][1])
+    avg_ms = kt[dom][1] / kt[dom][0]
+    b_alg = {"c2": 16 * m + int(0.75 * n) * 24 + 16 * (res or 0), "c4": 3 * 24 * m + 3 * 8 * n,
+             "c5": 3 * 24 * m + 2 * 8 * n + 16 * n}[wl]  # SURVEY.md 8d worked values
+    line = {
+        "metric": f"matched rows/sec ({wl.upper()})", "value": matched / sec, "unit": "matched rows/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": sec * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic R-MAT (on-device counter-based generator, oracle/rmat.c definition)",
+        "config": {"workload": desc, "scale": scale, "nodes": n, "relationships": m,
+                   "rmat": [p / 100 for p in probs] + [round(1 - sum(probs) / 100, 2)], "seed": 42},
+        "roofline": ({"bound": "hbm", "achieved": alg[dom] / (avg_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": alg[dom] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                      "traffic": pmc_traffic("k_" + dom), "kernel": "k_" + dom, "kernel_ms": avg_ms,
+                      "alg_bytes_per_launch": alg[dom]} if dom in alg else None),
+        "query": {"result": res, "matched_rows": matched, "alg_bytes_query": b_alg,
+                  "query_frac_of_peak": b_alg / sec / 1e9 / HBM_PEAK_GBS,
+                  "kernel_ms": {k: v[1] / v[0] for k, v in kt.items()}},
+    }
+    line["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline_single(wl, cpu_scale, ef, probs)
+    print(json.dumps(line), flush=True)
+    sess.close()
+
+
+def cpu_baseline_single(wl, scale, ef, probs):
+    """The oracle on a bounded sample of the same workload (binding enumeration, OpenMP)."""
+    import numpy as np
+    from oracle import cpu
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    n = 1 << scale
+    src, dst = cpu.rmat_edges(scale, 0, ef << scale, probs, 42)
+    t0 = time.perf_counter()
+    if wl == "c2":
+        pm = cpu.person_mask(n)
+        age = cpu.ages(np.arange(n))
+        am = (pm.astype(bool) & (age >= 18) & (age < 65)).astype(np.uint8)
+        ok = (am[src] != 0) & (pm[dst] != 0)
+        rows = int(ok.sum())
+        what = "expand with node filters (numpy)"
+    elif wl == "c4":
+        rows = cpu.triangle_enumerate(n, src, dst, threads=threads)
+        what = "triangle binding enumeration (oracle/rmat.c)"
+    else:
+        rows, _per_a = cpu.var_length_count(n, src, dst, 1, 3, threads=threads)
+        what = "edge-distinct path enumeration (oracle/rmat.c)"
+    dt = time.perf_counter() - t0
+    return {"value": rows / dt, "unit": "matched rows/s", "cores": threads if wl != "c2" else 1, "kind": "port",
+            "sample": f"R-MAT scale {scale}, edge factor {ef}: {what}, {rows} rows, {dt:.2f} s"}
