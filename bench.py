@@ -274,9 +274,6 @@ def main():
         dist.destroy_process_group()
 
 
-if __name__ == "__main__":
-    main()
-
 
 # ---- single-GPU lines for the other SURVEY.md 8d configs ------------------------------------------
 SINGLE = {
@@ -401,3 +398,7 @@ def cpu_baseline_single(wl, scale, ef, probs):
     dt = time.perf_counter() - t0
     return {"value": rows / dt, "unit": "matched rows/s", "cores": threads if wl != "c2" else 1, "kind": "port",
             "sample": f"R-MAT scale {scale}, edge factor {ef}: {what}, {rows} rows, {dt:.2f} s"}
+
+
+if __name__ == "__main__":
+    main()
