@@ -1129,9 +1129,7 @@ capsmi_status capsmi_trigraph_count(capsmi_session* s, const capsmi_trigraph* g,
     need(out_rows, "out");
     REQUIRE(nparts >= 1 && part >= 0 && part < nparts, CAPSMI_ERR_ILLEGAL_ARGUMENT, "part");
     use_device(s);
-    const int64_t ne = g->g.ne;
-    const int64_t b = ne * part / nparts, e = ne * (part + 1) / nparts;
-    *out_rows = (int64_t)tri_count(s, g->g, b, e, part == 0);
+    *out_rows = (int64_t)tri_count(s, g->g, part, nparts);
     API_END
 }
 

@@ -223,11 +223,14 @@ void relpart_hop2(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* c, 
 struct TriGraph {
     int64_t lo = 0, n = 0, ne = 0;
     Buf ok, ov, off;  // oriented keys (from<<32|to), payload (m(from,to)<<32|m(to,from)), CSR offsets (n + 1)
+    Buf tg;           // uint32 targets of the oriented edges (the `to` of ok)
     Buf ek, ev, sl;   // undirected keys / payload (pair terms), self-loop counts
+    Buf small_u, big_u;  // vertices with out-degree in [2, 64] / above 64
+    int64_t nsmall = 0, nbig = 0;
 };
 void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
                const capsmi_bitmap* n_ok, TriGraph& g);
-uint64_t tri_count(capsmi_session* s, const TriGraph& g, int64_t e_begin, int64_t e_end, bool with_terms);
+uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts);
 
 // fused var-length grouped count (k_varlen.hip)
 int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,

@@ -141,35 +141,66 @@ struct OutCols {
     int n;
 };
 
-__global__ void __launch_bounds__(256) k_expand_filter(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
-                                                       int64_t m, BitView a, BitView b, OutCols oc,
-                                                       unsigned long long* __restrict__ out_count) {
-    __shared__ unsigned int wsum[4];
-    __shared__ unsigned long long block_base;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+// One 8192-relationship tile per iteration: all loads in flight (16-byte pairs when the columns
+// are aligned), bitmap tests, wave-aggregated LDS ranks of the kept rows, ONE global atomic per
+// tile for the output run, then the projected columns are gathered in tile order and written as
+// one contiguous run (coalesced).  Output order across tiles is unspecified (bag semantics).
+constexpr int kEfBlock = 1024, kEfItems = 8, kEfTile = kEfBlock * kEfItems;
+
+__global__ void __launch_bounds__(kEfBlock) k_expand_filter(const int64_t* __restrict__ src,
+                                                            const int64_t* __restrict__ dst, int64_t m, int aligned,
+                                                            BitView a, BitView b, OutCols oc,
+                                                            unsigned long long* __restrict__ out_count) {
+    __shared__ unsigned short rows[kEfTile];  // tile-relative offsets of the kept rows
+    __shared__ unsigned int nkept;
+    __shared__ unsigned long long run;
+    const int lane = threadIdx.x & 63;
     const unsigned long long lt = lane == 0 ? 0ULL : (~0ULL >> (64 - lane));
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < m; base += stride) {
-        const int64_t e = base + threadIdx.x;
-        bool keep = false;
-        if (e < m) keep = bit_ok(a, src[e]) && bit_ok(b, dst[e]);
-        const unsigned long long bal = __ballot(keep);
-        if (lane == 0) wsum[wid] = (unsigned)__popcll(bal);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const unsigned tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
-            block_base = tot ? atomicAdd(out_count, (unsigned long long)tot) : 0ULL;
-        }
-        __syncthreads();
-        if (keep) {
-            unsigned long long pos = block_base + __popcll(bal & lt);
-            for (int w = 0; w < wid; ++w) pos += wsum[w];
-            for (int c = 0; c < oc.n; ++c) {
-                oc.dst[c][pos] = oc.src[c][e];
-                if (oc.dstv[c]) oc.dstv[c][pos] = oc.srcv[c] ? oc.srcv[c][e] : 1;
+    for (int64_t t0 = (int64_t)blockIdx.x * kEfTile; t0 < m; t0 += (int64_t)gridDim.x * kEfTile) {
+        if (threadIdx.x == 0) nkept = 0;
+        int64_t s[kEfItems], t[kEfItems];
+        const bool full = t0 + kEfTile <= m;
+        if (aligned && full) {
+#pragma unroll
+            for (int k = 0; k < kEfItems / 2; ++k) {
+                const int i = k * kEfBlock + (int)threadIdx.x;
+                const longlong2 sv = reinterpret_cast<const longlong2*>(src + t0)[i];
+                const longlong2 tv = reinterpret_cast<const longlong2*>(dst + t0)[i];
+                s[2 * k] = sv.x; s[2 * k + 1] = sv.y; t[2 * k] = tv.x; t[2 * k + 1] = tv.y;
+            }
+        } else {
+            const int last = (int)(min(m - t0, (int64_t)kEfTile) - 1);
+#pragma unroll
+            for (int u = 0; u < kEfItems; ++u) {
+                const int i = min(2 * ((u >> 1) * kEfBlock + (int)threadIdx.x) + (u & 1), last);
+                s[u] = src[t0 + i];
+                t[u] = dst[t0 + i];
             }
         }
+        __syncthreads();  // nkept reset visible
+#pragma unroll
+        for (int u = 0; u < kEfItems; ++u) {
+            const int off = 2 * ((u >> 1) * kEfBlock + (int)threadIdx.x) + (u & 1);
+            const bool keep = t0 + off < m && bit_ok(a, s[u]) && bit_ok(b, t[u]);
+            const unsigned long long bal = __ballot(keep);
+            unsigned int base = 0;
+            if (lane == 0 && bal) base = atomicAdd(&nkept, (unsigned int)__popcll(bal));
+            base = __shfl(base, 0, 64);
+            if (keep) rows[base + __popcll(bal & lt)] = (unsigned short)off;
+        }
         __syncthreads();
+        const unsigned int total = nkept;
+        if (threadIdx.x == 0) run = total ? atomicAdd(out_count, (unsigned long long)total) : 0ULL;
+        __syncthreads();
+        const unsigned long long r0 = run;
+        for (unsigned int i = threadIdx.x; i < total; i += kEfBlock) {
+            const int64_t e = t0 + rows[i];
+            for (int c = 0; c < oc.n; ++c) {
+                oc.dst[c][r0 + i] = oc.src[c][e];
+                if (oc.dstv[c]) oc.dstv[c][r0 + i] = oc.srcv[c] ? oc.srcv[c][e] : 1;
+            }
+        }
+        __syncthreads();  // rows / nkept reused by the next tile
     }
 }
 
@@ -468,12 +499,13 @@ void expand_filter(capsmi_session* s, const int64_t* src, const int64_t* dst, in
         oc.dstv[c] = c < nout ? out_v[c] : nullptr;
     }
     if (m <= 0) return;
-    int64_t g = (m + 255) / 256;
-    const int64_t cap = (int64_t)s->num_cus * 8;
+    int64_t g = (m + kEfTile - 1) / kEfTile;
+    const int64_t cap = (int64_t)s->num_cus * 2;
     if (g > cap) g = cap;
+    const int al = ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) == 0;
     KernelTimer kt(s, "expand_filter");
-    hipLaunchKernelGGL(k_expand_filter, dim3((unsigned)g), dim3(256), 0, s->stream, src, dst, m, view(a), view(b), oc,
-                       (unsigned long long*)dev_count);
+    hipLaunchKernelGGL(k_expand_filter, dim3((unsigned)g), dim3(kEfBlock), 0, s->stream, src, dst, m, al, view(a),
+                       view(b), oc, (unsigned long long*)dev_count);
     HIP_CHECK(hipGetLastError());
 }
 

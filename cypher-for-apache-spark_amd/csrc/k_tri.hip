@@ -108,32 +108,234 @@ __global__ void k_offsets(const uint64_t* __restrict__ ok_, int64_t ne, int64_t 
     }
 }
 
-// one thread per oriented edge (u -> v): intersect out(u) and out(v); weight of each triangle
-__global__ void __launch_bounds__(256) k_triangles(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ ov,
-                                                   int64_t e_begin, int64_t e_end, const int64_t* __restrict__ off,
-                                                   unsigned long long* __restrict__ out) {
+// ---- triangles: vertex-centric hashing -----------------------------------------------------
+// Every triangle {u, v, w} is found once, from its lowest vertex u in (degree, id) order:
+// v, w in out(u) and w in out(v).  For each u the out-list is put in an LDS hash (w -> payload
+// m(u,w)<<32 | m(w,u)); the wedges (v, w) for v in out(u), w in out(v) are then walked as one flat
+// index range (prefix sums of the out-degrees of the v's, binary-searched in LDS) so the lanes
+// read out(v) lists contiguously whatever their lengths, and each wedge costs one 4-byte load and
+// an LDS probe (the payload of (v, w) is loaded only on a hit).  Orientation by degree bounds
+// every out-degree by O(sqrt(E)).  u with out-degree <= 64 go one per wave, larger ones one per
+// 1024-lane workgroup (their lists are taken in chunks when they exceed the LDS hash).
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+constexpr int kSmallDeg = 64;
+constexpr int kSmallSlots = 128;
+constexpr int kTriBlock = 256;  // small: 4 waves
+constexpr int kBigBlock = 1024;
+constexpr int kBigChunk = 2048;  // out-list entries per LDS chunk
+constexpr int kBigSlots = 4096;
+
+__device__ __forceinline__ uint32_t hslot(uint32_t w, int log2cap) { return (w * 0x9E3779B1u) >> (32 - log2cap); }
+
+__device__ __forceinline__ void hinsert(uint32_t* hk, uint64_t* hv, int log2cap, uint32_t w, uint64_t pv) {
+    const uint32_t mask = (1u << log2cap) - 1;
+    uint32_t sl = hslot(w, log2cap);
+    while (true) {
+        const uint32_t prev = atomicCAS(&hk[sl], kEmpty, w);
+        if (prev == kEmpty) {
+            hv[sl] = pv;
+            return;
+        }
+        sl = (sl + 1) & mask;
+    }
+}
+
+__device__ __forceinline__ int hfind(const uint32_t* hk, int log2cap, uint32_t w) {
+    const uint32_t mask = (1u << log2cap) - 1;
+    uint32_t sl = hslot(w, log2cap);
+    while (true) {
+        const uint32_t k = hk[sl];
+        if (k == w) return (int)sl;
+        if (k == kEmpty) return -1;
+        sl = (sl + 1) & mask;
+    }
+}
+
+__device__ __forceinline__ unsigned long long tri_weight(uint64_t puv, uint64_t pvw, uint64_t puw) {
+    const uint64_t m_uv = puv >> 32, m_vu = puv & 0xffffffffULL;
+    const uint64_t m_vw = pvw >> 32, m_wv = pvw & 0xffffffffULL;
+    const uint64_t m_uw = puw >> 32, m_wu = puw & 0xffffffffULL;
+    return m_uv * m_vw * m_wu + m_uw * m_wv * m_vu;
+}
+
+// last i in [0, d) with pre[i] <= f (pre[0] = 0)
+__device__ __forceinline__ int seg_of(const uint32_t* pre, int d, uint32_t f) {
+    int lo = 0, hi = d;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (pre[mid] <= f) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+struct SmallWave {
+    uint32_t hk[kSmallSlots];
+    uint64_t hv[kSmallSlots];
+    uint64_t vp[kSmallDeg];
+    int64_t voff[kSmallDeg];
+    uint32_t vl[kSmallDeg];
+    uint32_t pre[kSmallDeg];
+};
+
+__global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restrict__ tg, const int64_t* __restrict__ ov,
+                                                         const int64_t* __restrict__ off,
+                                                         const int64_t* __restrict__ us, int64_t nu,
+                                                         unsigned long long* __restrict__ out) {
+    __shared__ SmallWave sw[kTriBlock / 64];
+    SmallWave& W = sw[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
     unsigned long long acc = 0;
-    for (int64_t i = e_begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < e_end;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t u = (uint32_t)(ok_[i] >> 32), v = (uint32_t)ok_[i];
-        const uint64_t muv_p = (uint64_t)ov[i];
-        const uint64_t m_uv = muv_p >> 32, m_vu = muv_p & 0xffffffffULL;
-        int64_t a = off[u], a_end = off[u + 1], b = off[v], b_end = off[v + 1];
-        // merge intersection of two sorted lists
-        while (a < a_end && b < b_end) {
-            const uint32_t wa = (uint32_t)ok_[a], wb = (uint32_t)ok_[b];
-            if (wa < wb) { ++a; continue; }
-            if (wb < wa) { ++b; continue; }
-            const uint64_t pa = (uint64_t)ov[a], pb = (uint64_t)ov[b];
-            const uint64_t m_uw = pa >> 32, m_wu = pa & 0xffffffffULL;
-            const uint64_t m_vw = pb >> 32, m_wv = pb & 0xffffffffULL;
-            acc += m_uv * m_vw * m_wu + m_uw * m_wv * m_vu;
-            ++a;
-            ++b;
+    const int64_t nwaves = (int64_t)gridDim.x * (kTriBlock / 64);
+    for (int64_t q = (int64_t)blockIdx.x * (kTriBlock / 64) + (threadIdx.x >> 6); q < nu; q += nwaves) {
+        const int64_t u = us[q];
+        const int64_t b = off[u];
+        const int d = (int)(off[u + 1] - b);
+        W.hk[lane] = kEmpty;
+        W.hk[lane + 64] = kEmpty;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        uint32_t dv = 0;
+        if (lane < d) {
+            const uint32_t v = tg[b + lane];
+            const uint64_t pv = (uint64_t)ov[b + lane];
+            const int64_t vo = off[v];
+            dv = (uint32_t)(off[v + 1] - vo);
+            W.vl[lane] = v;
+            W.vp[lane] = pv;
+            W.voff[lane] = vo;
+            hinsert(W.hk, W.hv, 7, v, pv);
+        }
+        uint32_t x = dv;  // wave inclusive scan of the out-degrees of the v's
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane < d) W.pre[lane] = x - dv;
+        const uint32_t total = __shfl(x, 63, 64);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t f = lane; f < total; f += 64) {
+            const int i = seg_of(W.pre, d, f);
+            const int64_t pos = W.voff[i] + (f - W.pre[i]);
+            const uint32_t w = tg[pos];
+            const int sl = hfind(W.hk, 7, w);
+            if (sl >= 0) acc += tri_weight(W.vp[i], (uint64_t)ov[pos], W.hv[sl]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the wave's LDS is reused for the next u
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if (lane == 0 && acc) atomicAdd(out, acc);
+}
+
+// block-wide exclusive scan of n <= kBigChunk values (kBigBlock lanes); returns the total
+__device__ uint32_t big_scan(const uint32_t* in, uint32_t* outp, int n, uint32_t* wtot) {
+    const int per = (n + kBigBlock - 1) / kBigBlock;
+    const int b = threadIdx.x * per;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t sum = 0;
+    for (int k = 0; k < per; ++k)
+        if (b + k < n) sum += in[b + k];
+    uint32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wtot[wave] = x;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        uint32_t v = lane < kBigBlock / 64 ? wtot[lane] : 0u;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(v, o, 64);
+            if (lane >= o) v += y;
+        }
+        if (lane < kBigBlock / 64) wtot[lane] = v;
+    }
+    __syncthreads();
+    uint32_t pre = x - sum + (wave > 0 ? wtot[wave - 1] : 0u);
+    for (int k = 0; k < per; ++k)
+        if (b + k < n) {
+            const uint32_t c = in[b + k];
+            outp[b + k] = pre;
+            pre += c;
+        }
+    const uint32_t total = wtot[kBigBlock / 64 - 1];
+    __syncthreads();
+    return total;
+}
+
+struct BigLds {
+    uint32_t hk[kBigSlots];
+    uint64_t hv[kBigSlots];
+    uint64_t vp[kBigChunk];
+    int64_t voff[kBigChunk];
+    uint32_t vl[kBigChunk];
+    uint32_t dv[kBigChunk];
+    uint32_t pre[kBigChunk];
+    uint32_t wtot[kBigBlock / 64];
+};
+
+__global__ void __launch_bounds__(kBigBlock) k_tri_big(const uint32_t* __restrict__ tg, const int64_t* __restrict__ ov,
+                                                       const int64_t* __restrict__ off,
+                                                       const int64_t* __restrict__ us, int64_t nu,
+                                                       unsigned long long* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    BigLds& L = *reinterpret_cast<BigLds*>(lds_raw);
+    unsigned long long acc = 0;
+    for (int64_t q = blockIdx.x; q < nu; q += gridDim.x) {
+        const int64_t u = us[q];
+        const int64_t b = off[u];
+        const int d = (int)(off[u + 1] - b);
+        for (int h0 = 0; h0 < d; h0 += kBigChunk) {  // hash chunk of out(u)
+            const int hn = min(kBigChunk, d - h0);
+            for (int k = threadIdx.x; k < kBigSlots; k += kBigBlock) L.hk[k] = kEmpty;
+            __syncthreads();
+            for (int k = threadIdx.x; k < hn; k += kBigBlock)
+                hinsert(L.hk, L.hv, 12, tg[b + h0 + k], (uint64_t)ov[b + h0 + k]);
+            for (int v0 = 0; v0 < d; v0 += kBigChunk) {  // v chunk of out(u)
+                const int vn = min(kBigChunk, d - v0);
+                for (int k = threadIdx.x; k < vn; k += kBigBlock) {
+                    const uint32_t v = tg[b + v0 + k];
+                    const int64_t vo = off[v];
+                    L.vl[k] = v;
+                    L.vp[k] = (uint64_t)ov[b + v0 + k];
+                    L.voff[k] = vo;
+                    L.dv[k] = (uint32_t)(off[v + 1] - vo);
+                }
+                __syncthreads();
+                const uint32_t total = big_scan(L.dv, L.pre, vn, L.wtot);
+                for (uint32_t f = threadIdx.x; f < total; f += kBigBlock) {
+                    const int i = seg_of(L.pre, vn, f);
+                    const int64_t pos = L.voff[i] + (f - L.pre[i]);
+                    const uint32_t w = tg[pos];
+                    const int sl = hfind(L.hk, 12, w);
+                    if (sl >= 0) acc += tri_weight(L.vp[i], (uint64_t)ov[pos], L.hv[sl]);
+                }
+                __syncthreads();
+            }
         }
     }
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
     if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+
+// u with 2 <= out-degree: small (<= 64) and big lists; also the 4-byte target array
+__global__ void k_tri_bins(const int64_t* __restrict__ off, int64_t n, uint8_t* __restrict__ fs,
+                           uint8_t* __restrict__ fb) {
+    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < n; u += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t d = off[u + 1] - off[u];
+        fs[u] = d >= 2 && d <= kSmallDeg;
+        fb[u] = d > kSmallDeg;
+    }
+}
+
+__global__ void k_targets(const uint64_t* __restrict__ ok_, int64_t ne, uint32_t* __restrict__ tg) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x)
+        tg[i] = (uint32_t)ok_[i];
 }
 
 // pair and self terms
@@ -256,21 +458,44 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     radix_sort_pairs(s, P<uint64_t>(g.ok), P<int64_t>(g.ov), ne, 0, 32 + bits);
     g.off = dev_alloc(sizeof(int64_t) * (n + 1), st);
     hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, n, P<int64_t>(g.off));
+    g.tg = dev_alloc(sizeof(uint32_t) * (ne > 0 ? ne : 1), st);
+    if (ne > 0)
+        hipLaunchKernelGGL(k_targets, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, P<uint32_t>(g.tg));
+    Buf fsm = dev_alloc(n, st), fbg = dev_alloc(n, st);
+    hipLaunchKernelGGL(k_tri_bins, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), n, P<uint8_t>(fsm),
+                       P<uint8_t>(fbg));
+    g.nsmall = flags_to_indices(s, P<uint8_t>(fsm), n, g.small_u);
+    g.nbig = flags_to_indices(s, P<uint8_t>(fbg), n, g.big_u);
     HIP_CHECK(hipGetLastError());
 }
 
-// count over oriented edges [e_begin, e_end) (+ pair/self terms when with_terms)
-uint64_t tri_count(capsmi_session* s, const TriGraph& g, int64_t e_begin, int64_t e_end, bool with_terms) {
+// count for vertex share `part` of `nparts` (each bin sliced evenly); pair/self terms with part 0
+uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
     using namespace tri;
     hipStream_t st = s->stream;
     Buf out = dev_alloc(24, st);
     HIP_CHECK(hipMemsetAsync(P<void>(out), 0, 24, st));
-    if (e_end > e_begin) {
+    {
         KernelTimer kt(s, "triangles");
-        hipLaunchKernelGGL(k_triangles, dim3(grid(s, e_end - e_begin)), dim3(256), 0, st, P<uint64_t>(g.ok),
-                           P<int64_t>(g.ov), e_begin, e_end, P<int64_t>(g.off), P<unsigned long long>(out));
+        const int64_t sb = g.nsmall * part / nparts, se = g.nsmall * (part + 1) / nparts;
+        const int64_t bb = g.nbig * part / nparts, be = g.nbig * (part + 1) / nparts;
+        if (be > bb) {
+            const size_t lds = sizeof(BigLds);
+            HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_tri_big),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            const int64_t gb = std::min<int64_t>(be - bb, (int64_t)s->num_cus * 2);
+            hipLaunchKernelGGL(k_tri_big, dim3((unsigned)gb), dim3(kBigBlock), lds, st, P<uint32_t>(g.tg),
+                               P<int64_t>(g.ov), P<int64_t>(g.off), P<int64_t>(g.big_u) + bb, be - bb,
+                               P<unsigned long long>(out));
+        }
+        if (se > sb) {
+            const int64_t gs = std::min<int64_t>((se - sb + 3) / 4, (int64_t)s->num_cus * 16);
+            hipLaunchKernelGGL(k_tri_small, dim3((unsigned)gs), dim3(kTriBlock), 0, st, P<uint32_t>(g.tg),
+                               P<int64_t>(g.ov), P<int64_t>(g.off), P<int64_t>(g.small_u) + sb, se - sb,
+                               P<unsigned long long>(out));
+        }
     }
-    if (with_terms) {
+    if (part == 0) {
         if (g.ne > 0)
             hipLaunchKernelGGL(k_pair_terms, dim3(grid(s, g.ne)), dim3(256), 0, st, P<uint64_t>(g.ek), P<int64_t>(g.ev),
                                g.ne, P<uint32_t>(g.sl), P<unsigned long long>(out) + 1);

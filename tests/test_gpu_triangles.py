@@ -47,3 +47,32 @@ def test_node_filter_and_parts(session):
 def test_rmat(session, scale):
     src, dst = cpu.rmat_edges(scale, 0, 16 << scale)
     assert _count(session, 1 << scale, src, dst) == cpu.triangle_enumerate(1 << scale, src, dst)
+
+
+def test_dense_big_vertices(session):
+    """Out-degrees above 64 (one workgroup per vertex) on a dense random multigraph."""
+    rng = np.random.default_rng(11)
+    n, m = 300, 40000
+    src = rng.integers(0, n, m).astype(np.int64)
+    dst = rng.integers(0, n, m).astype(np.int64)
+    assert _count(session, n, src, dst) == cpu.triangle_enumerate(n, src, dst)
+
+
+@pytest.mark.parametrize("mult", [False, True])
+def test_complete_digraph_chunks(session, mult):
+    """Complete digraph on 2200 nodes: out-degrees up to 2199 exceed one LDS chunk (2048).
+    Loop-free, so count(*) = trace(M^3) for the multiplicity matrix M (exact in float64 here)."""
+    n = 2200
+    rng = np.random.default_rng(5)
+    M = np.ones((n, n), dtype=np.int64)
+    if mult:
+        M = rng.integers(1, 4, (n, n))
+    np.fill_diagonal(M, 0)
+    a, b = np.nonzero(M)
+    reps = M[a, b]
+    src = np.repeat(a, reps).astype(np.int64)
+    dst = np.repeat(b, reps).astype(np.int64)
+    Mf = M.astype(np.float64)
+    want = int(round(np.trace(Mf @ Mf @ Mf)))
+    assert _count(session, n, src, dst) == want
+    assert _count(session, n, src, dst, nparts=3) == want
