@@ -34,9 +34,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "matched rows/sec for 2-hop MATCH on R-MAT 2^30 edges; % HBM roofline @1/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-KERNELS = ("part_hist", "part_scatter_t", "part_scatter_s", "hop1", "hop2", "mid_combine", "bitmap_add")
+KERNELS = ("part_scatter1", "part_scatter2_hop1", "part_scatter2", "hop1", "hop2", "mid_combine", "bitmap_add")
 # timer name -> kernel name as rocprofv3 reports it (hop1 and hop2 are two instances of k_hop_2d)
-KERNEL_SYMBOL = {"part_hist": "k_part_hist", "part_scatter_t": "k_scatter_t", "part_scatter_s": "k_scatter_s",
+KERNEL_SYMBOL = {"part_scatter1": "k_scatter_c", "part_scatter2_hop1": "k_scatter_s2", "part_scatter2": "k_scatter_s2",
                  "hop1": "k_hop_2d", "hop2": "k_hop_2d", "mid_combine": "k_mid_combine", "bitmap_add": "k_bitmap_add"}
 
 
@@ -149,8 +149,7 @@ def main():
 
     def step_cold():
         p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")  # node scan of :Person (a, b, c)
-        rp = graph.RelPartition(sess, [rels], 0, n)
-        rp.mark_mid(p, p, mid.data_ptr(), scratch.data_ptr())
+        rp = graph.RelPartition.build_mark_mid(sess, [rels], p, p, mid.data_ptr(), scratch.data_ptr())
         r = exchange_and_finish(p, lambda q: rp.mark_dst(q, q, mid.data_ptr(), dstw.data_ptr()))
         rp.release()
         return r
@@ -221,9 +220,9 @@ def main():
         head = modes[0]
         sec, res, kt = results[head]
         # per-kernel algorithmic bytes (this rank's rels): what each kernel must touch by its function
-        alg = {"part_hist": m_local * 16,            # read source + target
-               "part_scatter_t": m_local * 24,       # read 2 x int64, write packed uint2
-               "part_scatter_s": m_local * 16,       # read + write uint2
+        alg = {"part_scatter1": m_local * 24,        # read 2 x int64, write packed uint2
+               "part_scatter2_hop1": m_local * 16 + n // 8,  # read + write uint2, write M
+               "part_scatter2": m_local * 16,        # read + write uint2
                "hop1": m_local * 8 + n // 8,         # read uint2 pairs, write M
                "hop2": m_local * 8 + n // 8 * 3,     # read uint2 pairs + X1 + X2, write C
                "mid_combine": n // 8 * 5, "bitmap_add": n * 8}

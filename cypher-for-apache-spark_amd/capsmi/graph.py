@@ -165,11 +165,24 @@ class RelPartition:
     on the cold path, or kept across queries as the Cache analogue."""
 
     def __init__(self, session: Session, rels: Sequence[GpuTable], lo: int, hi: int, src_col: str = "source",
-                 dst_col: str = "target"):
+                 dst_col: str = "target", _handle=None):
         self.session = session
-        self._h = ctypes.c_void_p()
-        _lib.call("capsmi_relpart_build", session.handle, len(rels), _handles(rels), src_col.encode(),
-                  dst_col.encode(), lo, hi, ctypes.byref(self._h))
+        self._h = ctypes.c_void_p() if _handle is None else _handle
+        if _handle is None:
+            _lib.call("capsmi_relpart_build", session.handle, len(rels), _handles(rels), src_col.encode(),
+                      dst_col.encode(), lo, hi, ctypes.byref(self._h))
+
+    @classmethod
+    def build_mark_mid(cls, session: Session, rels: Sequence[GpuTable], a_ok: "NodeBitmap", b_ok: "NodeBitmap",
+                       mid_ptr: int, scratch_ptr: int, src_col: str = "source",
+                       dst_col: str = "target") -> "RelPartition":
+        """Cold 2-hop: build the layout over b_ok's id domain and run hop 1 (RelPartition.mark_mid) in
+        the same pass when a_ok is full (include/capsmi.h capsmi_relpart_build_mark_mid)."""
+        h = ctypes.c_void_p()
+        _lib.call("capsmi_relpart_build_mark_mid", session.handle, len(rels), _handles(rels), src_col.encode(),
+                  dst_col.encode(), a_ok.handle, b_ok.handle, ctypes.c_void_p(mid_ptr), ctypes.c_void_p(scratch_ptr),
+                  ctypes.byref(h))
+        return cls(session, rels, 0, 0, _handle=h)
 
     @property
     def handle(self):

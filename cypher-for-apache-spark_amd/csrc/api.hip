@@ -934,7 +934,7 @@ static bool same_domain(const capsmi_bitmap* a, const capsmi_bitmap* b, const ca
 }
 
 static void build_part(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
-                       const char* dst_col, int64_t lo, int64_t hi, RelPart& rp) {
+                       const char* dst_col, int64_t lo, int64_t hi, RelPart& rp, const RelPartHop1* h1 = nullptr) {
     std::vector<const int64_t*> srcs, dsts;
     std::vector<int64_t> ms;
     for (int i = 0; i < nrels; ++i) {
@@ -943,7 +943,7 @@ static void build_part(capsmi_session* s, int32_t nrels, capsmi_table* const* re
         dsts.push_back(rel_col(rels[i], dst_col).d());
         ms.push_back(rels[i]->nrows);
     }
-    relpart_build(s, srcs.data(), dsts.data(), ms.data(), nrels, lo, hi, rp);
+    relpart_build(s, srcs.data(), dsts.data(), ms.data(), nrels, lo, hi, rp, h1);
 }
 
 // hop 1 on a partitioned layout into X1 (= M | S1) and X2 (= M | S2); S1 scratch
@@ -954,6 +954,19 @@ static void part_mid(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* 
     HIP_CHECK(hipMemsetAsync(X2, 0, sizeof(uint32_t) * nw, s->stream));
     HIP_CHECK(hipMemsetAsync(S1, 0, sizeof(uint32_t) * nw, s->stream));
     relpart_hop1(s, rp, a, b, X1, S1, X2);
+    graph::mid_combine(s, X1, X2, S1, nw);
+}
+
+// build + hop 1 in one go (hop 1 rides on the build's second pass when a is full)
+static void build_part_mid(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                           const char* dst_col, const capsmi_bitmap* a, const capsmi_bitmap* b, uint32_t* X1,
+                           uint32_t* X2, uint32_t* S1, RelPart& rp) {
+    const int64_t nw = b->nwords;
+    HIP_CHECK(hipMemsetAsync(X1, 0, sizeof(uint32_t) * nw, s->stream));
+    HIP_CHECK(hipMemsetAsync(X2, 0, sizeof(uint32_t) * nw, s->stream));
+    HIP_CHECK(hipMemsetAsync(S1, 0, sizeof(uint32_t) * nw, s->stream));
+    const RelPartHop1 h1{a, b, X1, S1, X2};
+    build_part(s, nrels, rels, src_col, dst_col, b->lo, b->hi, rp, &h1);
     graph::mid_combine(s, X1, X2, S1, nw);
 }
 
@@ -1002,8 +1015,7 @@ capsmi_status capsmi_two_hop_count_distinct(capsmi_session* s, int32_t nrels, ca
     if (same_domain(a_ok, b_ok, c_ok)) {
         // cold radix-partitioned path: partition + two LDS-resident hops
         RelPart rp;
-        build_part(s, nrels, rels, src_col, dst_col, b_ok->lo, b_ok->hi, rp);
-        part_mid(s, rp, a_ok, b_ok, X1, X1 + nw, X1 + 2 * nw);
+        build_part_mid(s, nrels, rels, src_col, dst_col, a_ok, b_ok, X1, X1 + nw, X1 + 2 * nw, rp);
         HIP_CHECK(hipMemsetAsync(P<void>(cw), 0, sizeof(uint32_t) * c_ok->nwords, s->stream));
         relpart_hop2(s, rp, c_ok, X1, X1 + nw, P<uint32_t>(cw));
     } else {
@@ -1034,6 +1046,29 @@ capsmi_status capsmi_relpart_build(capsmi_session* s, int32_t nrels, capsmi_tabl
     std::unique_ptr<capsmi_relpart> guard(p);
     p->sess = s;
     build_part(s, nrels, rels, src_col, dst_col, id_lo, id_hi, p->rp);
+    *out = guard.release();
+    API_END
+}
+
+capsmi_status capsmi_relpart_build_mark_mid(capsmi_session* s, int32_t nrels, capsmi_table* const* rels,
+                                            const char* src_col, const char* dst_col, const capsmi_bitmap* a_ok,
+                                            const capsmi_bitmap* b_ok, uint32_t* mid_words, uint32_t* scratch_words,
+                                            capsmi_relpart** out) {
+    API_BEGIN
+    need(s, "session");
+    need(out, "out");
+    need(mid_words, "mid_words");
+    need(scratch_words, "scratch_words");
+    check_bitmap(a_ok, "a_ok");
+    check_bitmap(b_ok, "b_ok");
+    REQUIRE(nrels >= 0 && (nrels == 0 || rels), CAPSMI_ERR_ILLEGAL_ARGUMENT, "rels");
+    REQUIRE(a_ok->lo == b_ok->lo && a_ok->hi == b_ok->hi, CAPSMI_ERR_UNSUPPORTED, "a and b scans need one id domain");
+    use_device(s);
+    auto* p = new capsmi_relpart();
+    std::unique_ptr<capsmi_relpart> guard(p);
+    p->sess = s;
+    build_part_mid(s, nrels, rels, src_col, dst_col, a_ok, b_ok, mid_words, mid_words + b_ok->nwords, scratch_words,
+                   p->rp);
     *out = guard.release();
     API_END
 }

@@ -201,7 +201,7 @@ void order_keys(capsmi_session* s, const int64_t* col, const uint8_t* valid, int
 // partitioned relationship layout (k_part.hip)
 struct PartLayout {
     int64_t lo, hi;  // id domain of both endpoints
-    int nt;          // target slices of 2^19 ids
+    int nt;          // target slices of 2^19 ids (<= 2048)
     int ns;          // source slices of 2^sbits ids
     int sbits;       // 19 while nt * ns <= 16384, coarser for larger domains
     int ncells;      // nt * ns, j-major (target slice major)
@@ -212,8 +212,15 @@ struct RelPart {
     Buf boff;   // int64 cell offsets (ncells + 1)
     int64_t kept = 0;
 };
+// hop 1 of a 2-hop run while the layout is built: M(t) |= a_ok(s) for s != t, a_ok self-loops ->
+// S1 (first) / S2 (second), target filter b_ok; outputs zeroed by the caller
+struct RelPartHop1 {
+    const capsmi_bitmap* a;
+    const capsmi_bitmap* b;
+    uint32_t *M, *S1, *S2;
+};
 void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
-                   int64_t lo, int64_t hi, RelPart& rp);
+                   int64_t lo, int64_t hi, RelPart& rp, const RelPartHop1* h1 = nullptr);
 void relpart_hop1(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* a, const capsmi_bitmap* b, uint32_t* M,
                   uint32_t* S1, uint32_t* S2);
 void relpart_hop2(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* c, const uint32_t* X1, const uint32_t* X2,

@@ -25,17 +25,17 @@ namespace part {
 
 constexpr int kSliceBits = 19;                   // 2^19 ids per slice = 64 KiB of LDS bitmap
 constexpr int kSliceWords = 1 << (kSliceBits - 5);
-constexpr int kMaxCells = 16384;                 // cell histogram = 64 KiB of LDS
-constexpr int kMaxTSlices = 4096;                // domain <= 2^31 ids
-constexpr int kBlock = 1024;                     // histogram and hop workgroups
+constexpr int kMaxCells = 16384;                 // cell histogram = 32 KiB of 16-bit LDS counters
+constexpr int kMaxTSlices = 2048;                // domain <= 2^30 ids (pass-1 LDS: 7 words per slice)
+constexpr int kBlock = 1024;                     // hop workgroups
 constexpr int kItems = 8;                        // relationships per lane per tile
-constexpr int kRepTile = kBlock * kItems;        // replica assignment unit (8192 rels, see TileWalk)
-constexpr int kSBlock = 1024;                    // scatter workgroups (512 lanes x 4096 rels measured slower)
+constexpr int kSBlock = 1024;                    // scatter workgroups
 constexpr int kTile = kSBlock * kItems;          // relationships per scatter tile (8192)
+constexpr int kCh = kTile;                       // pairs per pass-1 chunk: a tile's run spans <= 2 chunks
+constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr int kUnroll = 8;                       // loads in flight per lane in the hops
 constexpr int64_t kLoadMin = 8192;               // pull a source slice into LDS for >= this many rels
 constexpr int kPad = 2 * 8192;                   // slack pairs after every pair array (load_pairs)
-constexpr int kReps = 32;                        // cursor replicas per bucket (see TileWalk)
 
 using Layout = PartLayout;
 
@@ -82,17 +82,6 @@ __device__ uint32_t block_exclusive_scan(const uint32_t* in, uint32_t* out, int 
 __device__ __forceinline__ int cell_of(const Layout& L, uint32_t s, uint32_t t) {
     return (int)(t >> kSliceBits) * L.ns + (int)(s >> L.sbits);
 }
-
-// Input tiles are dealt to kReps replicas (tile t -> replica t % kReps).  Each replica owns a
-// contiguous share of every bucket, so a bucket's write cursor is advanced only by the tiles of
-// one replica: with one cursor per bucket every tile of the whole input would serialise on the
-// hottest bucket's atomic (R-MAT puts ~15 % of all relationships in one target slice).
-// Block b works for replica b % kReps and takes that replica's tiles round-robin.
-struct TileWalk {
-    int r, q, bpr;
-    __device__ TileWalk() : r(blockIdx.x % kReps), q(blockIdx.x / kReps), bpr(gridDim.x / kReps) {}
-    __device__ int64_t tile(int64_t k) const { return (int64_t)r + (int64_t)kReps * ((int64_t)q + k * bpr); }
-};
 
 // Tile item u of this lane is relationship t0 + item_off<B>(u): lanes read 16-byte pairs of
 // consecutive relationships (2 int64 per load, the calibrated streaming width), pair k of the
@@ -145,139 +134,66 @@ __device__ __forceinline__ void load_pairs(const uint2* __restrict__ in, int64_t
     }
 }
 
-// pass 0: per-replica cell sizes (rels with an endpoint outside [lo, hi) can never match a node
-// scan over that domain and are dropped here -- an inner join drops them the same way)
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) k_part_hist(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
-                                                      int64_t m, Layout L, unsigned int* __restrict__ counts) {
-    extern __shared__ __attribute__((aligned(16))) unsigned int h[];
-    for (int i = threadIdx.x; i < L.ncells; i += kBlock) h[i] = 0;
-    __syncthreads();
-    const uint64_t range = (uint64_t)(L.hi - L.lo);
-    const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
-    const TileWalk w;
-    for (int64_t k = 0;; ++k) {
-        const int64_t t0 = w.tile(k) * kRepTile;
-        if (t0 >= m) break;
-        int64_t sr[kItems], tr[kItems];
-        load_tile<kBlock>(src, dst, t0, m, vec, sr, tr);
-#pragma unroll
-        for (int u = 0; u < kItems; ++u) {
-            const int64_t e = t0 + item_off<kBlock>(u);
-            const uint64_t s = (uint64_t)(sr[u] - L.lo), t = (uint64_t)(tr[u] - L.lo);
-            if (e < m && s < range && t < range) atomicAdd(&h[cell_of(L, (uint32_t)s, (uint32_t)t)], 1u);
-        }
+// ---- pass 1: int64 (source, target) -> packed pairs in per-workgroup chunks of one target slice ------
+//
+// No counting pass: every workgroup keeps one open chunk (kCh pairs) per target slice and appends
+// its tiles' runs to it; a full chunk is retired and a fresh one taken from the pool, a whole
+// tile's worth of fresh chunks with one global atomic.  Chunk metadata records (slice, fill).
+// The pass also counts the 2-D cells (target slice x source slice) in a 16-bit LDS histogram,
+// so pass 2 can write the cell-grouped layout at exact offsets.
+
+__device__ __forceinline__ unsigned long long chunk_meta(int j, uint32_t fill) {
+    return (unsigned long long)(uint32_t)j | ((unsigned long long)fill << 32);
+}
+
+// 16-bit cell counter, two per LDS word; the lane that takes a counter from 0x7FFF to 0x8000
+// moves 0x8000 to the global count (a tile adds at most kTile < 0x8000 before that lands)
+__device__ __forceinline__ void hist16_inc(uint32_t* hist, unsigned long long* gcount, int c) {
+    const uint32_t sh = (uint32_t)(c & 1) * 16u;
+    const uint32_t old = atomicAdd(&hist[c >> 1], 1u << sh);
+    if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
+        atomicAdd(&gcount[c], 0x8000ULL);
+        atomicSub(&hist[c >> 1], 0x8000u << sh);
     }
-    __syncthreads();
-    unsigned int* out = counts + (size_t)w.r * L.ncells;
-    for (int i = threadIdx.x; i < L.ncells; i += kBlock)
-        if (h[i]) atomicAdd(&out[i], h[i]);
 }
 
-// offsets, one thread per cell: pre[r][c] = sum_{r' < r} cnt[r'][c], tot[c] = sum_r cnt[r][c]
-__global__ void k_cell_prefix(const unsigned int* __restrict__ cnt, int ncells, int64_t* __restrict__ pre,
-                              int64_t* __restrict__ tot) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= ncells) return;
-    int64_t run = 0;
-    for (int r = 0; r < kReps; ++r) {
-        pre[(size_t)r * ncells + c] = run;
-        run += cnt[(size_t)r * ncells + c];
-    }
-    tot[c] = run;
+__host__ __device__ constexpr size_t scatter1_lds(int nb, int ncells) {
+    return sizeof(uint2) * kTile + sizeof(uint32_t) * ((size_t)(ncells + 1) / 2 + 7 * (size_t)nb + kSBlock / 64 + 4);
 }
 
-// one thread per pass-2 unit u = j * kReps + r (the pairs replica r put in target slice j):
-// its start (= replica r's pass-1 cursor for slice j), length and tile count
-__global__ void k_units(const unsigned int* __restrict__ cnt, const int64_t* __restrict__ pre,
-                        const int64_t* __restrict__ coff, Layout L, int64_t* __restrict__ cur1,
-                        int64_t* __restrict__ ustart, int64_t* __restrict__ ulen, int64_t* __restrict__ utiles) {
-    const int u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= L.nt * kReps) return;
-    const int j = u / kReps, r = u % kReps;
-    int64_t before = 0, len = 0;
-    for (int i = 0; i < L.ns; ++i) {
-        const size_t c = (size_t)r * L.ncells + (size_t)j * L.ns + i;
-        before += pre[c];
-        len += cnt[c];
-    }
-    const int64_t st = coff[(size_t)j * L.ns] + before;
-    cur1[(size_t)r * L.nt + j] = st;
-    ustart[u] = st;
-    ulen[u] = len;
-    utiles[u] = len > 0 ? (st + len - (st & ~int64_t(1)) + kTile - 1) / kTile : 0;  // tiles on an even grid
-}
-
-// pass-2 cursors: cur2[r][c] = coff[c] + pre[r][c] (in place)
-__global__ void k_add_coff(int64_t* __restrict__ pre, const int64_t* __restrict__ coff, int ncells) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)kReps * ncells) return;
-    pre[i] += coff[i % ncells];
-}
-
-// tile -> unit map for pass 2, one thread per unit
-__global__ void k_tile_unit(const int64_t* __restrict__ upre, int nunits, int* __restrict__ tile_unit) {
-    const int u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= nunits) return;
-    for (int64_t k = upre[u]; k < upre[u + 1]; ++k) tile_unit[k] = u;
-}
-
-// LDS carve-up shared by both scatters: stage[kTile] | base[nb] (u64) | cnt[nb] | loc[nb] | wtot[kSBlock/64]
-__host__ __device__ constexpr size_t scatter_lds(int nb) {
-    return sizeof(uint2) * kTile + sizeof(unsigned long long) * nb + sizeof(uint32_t) * (2 * nb + kSBlock / 64);
-}
-
-// Tile body: items (s, t, bucket) are in registers with their rank within the bucket; reserve
-// each bucket's run with one atomic on the replica's cursor, regroup the tile in LDS, write the
-// runs out.
-__device__ __forceinline__ void scatter_tile(const uint2 (&pr)[kItems], uint32_t valid, const uint32_t (&rk)[kItems], int nb,
-                                             unsigned long long* __restrict__ cursor, uint2* __restrict__ out,
-                                             uint2* stage, unsigned long long* base, uint32_t* cnt, uint32_t* loc,
-                                             uint32_t* wtot, bool by_target, int sbits) {
-    for (int i = threadIdx.x; i < nb; i += kSBlock) {
-        const uint32_t c = cnt[i];
-        base[i] = c ? atomicAdd(&cursor[i], (unsigned long long)c) : 0ULL;
-    }
-    const uint32_t total = block_exclusive_scan<kSBlock>(cnt, loc, nb, wtot);
-#pragma unroll
-    for (int k = 0; k < kItems; ++k)
-        if ((valid >> k) & 1u) {
-            const int b = by_target ? (int)(pr[k].y >> kSliceBits) : (int)(pr[k].x >> sbits);
-            stage[loc[b] + rk[k]] = pr[k];
-        }
-    __syncthreads();
-    for (uint32_t idx = threadIdx.x; idx < total; idx += kSBlock) {
-        const uint2 p = stage[idx];
-        const int b = by_target ? (int)(p.y >> kSliceBits) : (int)(p.x >> sbits);
-        out[base[b] + (idx - loc[b])] = p;
-    }
-    __syncthreads();
-}
-
-// pass 1: int64 (source, target) -> uint32 pairs grouped by target slice, replica-major within
-// each slice; cursor = cur1[r][j]
-__global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(8))) k_scatter_t(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
-                                                      int64_t m, Layout L, unsigned long long* __restrict__ cur1,
-                                                      uint2* __restrict__ out) {
+__global__ void __launch_bounds__(kSBlock) k_scatter_c(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                       int64_t m, Layout L, unsigned int* __restrict__ pool_ctr,
+                                                       uint2* __restrict__ pool, unsigned long long* __restrict__ cmeta,
+                                                       unsigned long long* __restrict__ ccount) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
-    const int nb = L.nt;
+    const int nb = L.nt, hw = (L.ncells + 1) >> 1;
     uint2* stage = reinterpret_cast<uint2*>(smem);
-    unsigned long long* base = smem + kTile;
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(base + nb);
-    uint32_t* loc = cnt + nb;
-    uint32_t* wtot = loc + nb;
+    uint32_t* hist = reinterpret_cast<uint32_t*>(stage + kTile);
+    uint32_t* cnt = hist + hw;   // this tile's run length per slice
+    uint32_t* loc = cnt + nb;    // run start in the stage
+    uint32_t* ph = loc + nb;     // open chunk per slice (kNone: none yet)
+    uint32_t* fl = ph + nb;      // its fill
+    uint32_t* p0 = fl + nb;      // this tile's run: first part in chunk p0 from offset f0 ...
+    uint32_t* f0 = p0 + nb;
+    uint32_t* p1 = f0 + nb;      // ... the rest (if any) from the start of chunk p1
+    uint32_t* wtot = p1 + nb;
+    uint32_t* misc = wtot + kSBlock / 64;
+    for (int i = threadIdx.x; i < hw; i += kSBlock) hist[i] = 0;
+    for (int i = threadIdx.x; i < nb; i += kSBlock) {
+        ph[i] = kNone;
+        fl[i] = 0;
+    }
     const uint64_t range = (uint64_t)(L.hi - L.lo);
     const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
-    const TileWalk w;
-    unsigned long long* cursor = cur1 + (size_t)w.r * nb;
-    for (int64_t k = 0;; ++k) {
-      const int64_t r0 = w.tile(k) * kRepTile;
-      if (r0 >= m) break;  // block-uniform
-      for (int64_t t0 = r0; t0 < min(r0 + (int64_t)kRepTile, m); t0 += kTile) {
+    for (int64_t k = blockIdx.x;; k += gridDim.x) {
+        const int64_t t0 = k * kTile;
+        if (t0 >= m) break;  // block-uniform
         for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
+        if (threadIdx.x == 0) misc[0] = 0;
         __syncthreads();
         uint2 pr[kItems];
         uint32_t rk[kItems];
-        uint32_t valid = 0;  // bit u: item u is kept
+        uint32_t valid = 0;
         {
             int64_t sr[kItems], tr[kItems];
             load_tile<kSBlock>(src, dst, t0, m, vec, sr, tr);
@@ -293,52 +209,107 @@ __global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(8)
         }
 #pragma unroll
         for (int u = 0; u < kItems; ++u)
-            if ((valid >> u) & 1u) rk[u] = atomicAdd(&cnt[pr[u].y >> kSliceBits], 1u);
+            if ((valid >> u) & 1u) {
+                rk[u] = atomicAdd(&cnt[pr[u].y >> kSliceBits], 1u);
+                hist16_inc(hist, ccount, cell_of(L, pr[u].x, pr[u].y));
+            }
         __syncthreads();
-        scatter_tile(pr, valid, rk, nb, cursor, out, stage, base, cnt, loc, wtot, true, L.sbits);
-      }
+        const uint32_t total = block_exclusive_scan<kSBlock>(cnt, loc, nb, wtot);
+        for (int i = threadIdx.x; i < nb; i += kSBlock) {  // runs that fit their open chunk
+            const uint32_t c = cnt[i];
+            if (!c) continue;
+            const uint32_t p = ph[i], f = fl[i];
+            if (p != kNone && f + c <= (uint32_t)kCh) {
+                p0[i] = p;
+                f0[i] = f;
+                p1[i] = kNone;
+                fl[i] = f + c;
+            } else {
+                p1[i] = atomicAdd(&misc[0], 1u);  // index among this tile's fresh chunks
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) misc[1] = misc[0] ? atomicAdd(pool_ctr, misc[0]) : 0u;
+        __syncthreads();
+        for (int i = threadIdx.x; i < nb; i += kSBlock) {  // runs that open a chunk
+            const uint32_t c = cnt[i];
+            if (!c || p1[i] == kNone) continue;
+            const uint32_t np = misc[1] + p1[i], p = ph[i], f = fl[i];
+            if (p == kNone) {
+                p0[i] = np;
+                f0[i] = 0;
+                p1[i] = kNone;
+                fl[i] = c;
+            } else {  // fill chunk p, retire it, continue in np
+                p0[i] = p;
+                f0[i] = f;
+                p1[i] = np;
+                fl[i] = f + c - (uint32_t)kCh;
+                cmeta[p] = chunk_meta(i, (uint32_t)kCh);
+            }
+            ph[i] = np;
+        }
+#pragma unroll
+        for (int u = 0; u < kItems; ++u)
+            if ((valid >> u) & 1u) stage[loc[pr[u].y >> kSliceBits] + rk[u]] = pr[u];
+        __syncthreads();
+        for (uint32_t idx = threadIdx.x; idx < total; idx += kSBlock) {
+            const uint2 p = stage[idx];
+            const int b = (int)(p.y >> kSliceBits);
+            const uint32_t r = idx - loc[b], room = (uint32_t)kCh - f0[b];
+            const size_t o = r < room ? (size_t)p0[b] * kCh + f0[b] + r : (size_t)p1[b] * kCh + (r - room);
+            pool[o] = p;
+        }
+        __syncthreads();
+    }
+    for (int i = threadIdx.x; i < nb; i += kSBlock)
+        if (ph[i] != kNone) cmeta[ph[i]] = chunk_meta(i, fl[i]);
+    for (int i = threadIdx.x; i < hw; i += kSBlock) {
+        const uint32_t v = hist[i];
+        if (v & 0xFFFFu) atomicAdd(&ccount[2 * i], (unsigned long long)(v & 0xFFFFu));
+        if (v >> 16) atomicAdd(&ccount[2 * i + 1], (unsigned long long)(v >> 16));
     }
 }
 
-// pass 2: unit u = (target slice j, replica r) -> the source cells of slice j; cursor cur2[r][j][*].
-// Global tile k belongs to unit tile_unit[k] (upre[u] <= k < upre[u + 1]).
-__global__ void __launch_bounds__(kSBlock) __attribute__((amdgpu_waves_per_eu(8))) k_scatter_s(const uint2* __restrict__ in, const int64_t* __restrict__ ustart,
-                                                      const int64_t* __restrict__ ulen,
-                                                      const int64_t* __restrict__ upre,
-                                                      const int* __restrict__ tile_unit, int64_t ntiles, Layout L,
-                                                      unsigned long long* __restrict__ cur2,
-                                                      uint2* __restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
-    const int nb = L.ns;
-    uint2* stage = reinterpret_cast<uint2*>(smem);
-    unsigned long long* base = smem + kTile;
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(base + nb);
-    uint32_t* loc = cnt + nb;
-    uint32_t* wtot = loc + nb;
-    for (int64_t ck = blockIdx.x; ck < ntiles; ck += gridDim.x) {
-        const int u = tile_unit[ck], j = u / kReps, r = u % kReps;
-        const int64_t tb = (ustart[u] & ~int64_t(1)) + (ck - upre[u]) * kTile;  // even tile base
-        const int64_t b0 = max(tb, ustart[u]), b1 = min(tb + (int64_t)kTile, ustart[u] + ulen[u]);
-        for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
-        __syncthreads();
-        uint32_t rk[kItems];
-        uint32_t valid = 0;
-        uint2 pr[kItems];
-        load_pairs<kSBlock, kItems>(in, tb, pr);
-        const int lo = (int)(b0 - tb), hi = (int)(b1 - tb);  // 32-bit tile-relative bounds
-#pragma unroll
-        for (int k = 0; k < kItems; ++k) {
-            const int e = item_off<kSBlock>(k);
-            valid |= (e >= lo && e < hi ? 1u : 0u) << k;
-            rk[k] = 0;
-        }
-#pragma unroll
-        for (int k = 0; k < kItems; ++k)
-            if ((valid >> k) & 1u) rk[k] = atomicAdd(&cnt[pr[k].x >> L.sbits], 1u);
-        __syncthreads();
-        scatter_tile(pr, valid, rk, nb, cur2 + (size_t)r * L.ncells + (size_t)j * nb, out, stage, base, cnt, loc,
-                     wtot, false, L.sbits);
+// chunks grouped by target slice (order within a slice is arbitrary)
+__global__ void k_chunk_count(const unsigned long long* __restrict__ cmeta, int64_t nchunks,
+                              int64_t* __restrict__ jcnt) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nchunks) atomicAdd(reinterpret_cast<unsigned long long*>(&jcnt[(uint32_t)cmeta[q]]), 1ULL);
+}
+
+__global__ void k_chunk_place(const unsigned long long* __restrict__ cmeta, int64_t nchunks,
+                              unsigned long long* __restrict__ jcur, uint32_t* __restrict__ order) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nchunks) order[atomicAdd(&jcur[(uint32_t)cmeta[q]], 1ULL)] = (uint32_t)q;
+}
+
+// LDS carve-up of pass 2 (and the generic scatter_tile): stage[kTile] | base[nb] (u64) | cnt[nb] | loc[nb] | wtot
+__host__ __device__ constexpr size_t scatter_lds(int nb) {
+    return sizeof(uint2) * kTile + sizeof(unsigned long long) * nb + sizeof(uint32_t) * (2 * nb + kSBlock / 64);
+}
+
+// Tile body: items (s, t, bucket) are in registers with their rank within the bucket; reserve
+// each bucket's run with one atomic on its cursor, regroup the tile in LDS, write the runs out.
+__device__ __forceinline__ void scatter_tile(const uint2 (&pr)[kItems], uint32_t valid, const uint32_t (&rk)[kItems], int nb,
+                                             unsigned long long* __restrict__ cursor, uint2* __restrict__ out,
+                                             uint2* stage, unsigned long long* base, uint32_t* cnt, uint32_t* loc,
+                                             uint32_t* wtot, int sbits) {
+    for (int i = threadIdx.x; i < nb; i += kSBlock) {
+        const uint32_t c = cnt[i];
+        base[i] = c ? atomicAdd(&cursor[i], (unsigned long long)c) : 0ULL;
     }
+    const uint32_t total = block_exclusive_scan<kSBlock>(cnt, loc, nb, wtot);
+#pragma unroll
+    for (int k = 0; k < kItems; ++k)
+        if ((valid >> k) & 1u) stage[loc[pr[k].x >> sbits] + rk[k]] = pr[k];
+    __syncthreads();
+    for (uint32_t idx = threadIdx.x; idx < total; idx += kSBlock) {
+        const uint2 p = stage[idx];
+        const int b = (int)(p.x >> sbits);
+        out[base[b] + (idx - loc[b])] = p;
+    }
+    __syncthreads();
 }
 
 struct BitV {
@@ -363,6 +334,95 @@ __device__ __forceinline__ void flush_slice(const uint32_t* tl, uint32_t* g, int
         uint32_t v = tl[i];
         if (v && !mask.full) v &= mask.w[gw];
         if (v) atomicOr(&g[gw], v);
+    }
+}
+
+// hop-1 outputs when it runs inside pass 2 (a_ok covers the whole domain, so no source test)
+struct Hop1Out {
+    BitV tmask;  // b_ok
+    uint32_t* M;
+    uint32_t* S1;
+    uint32_t* S2;
+    int64_t gwords;
+};
+
+// ---- pass 2: each chunk (one target slice) -> the slice's source cells at exact offsets --------------
+// Block b takes chunks [b * per, (b + 1) * per) of the slice-ordered chunk list.  With HOP1 the
+// block also runs hop 1 on the pairs it moves: M(t) for s != t marked in an LDS copy of the
+// current target slice (flushed through b_ok when the slice changes), self-loops -> S1 / S2.
+template <bool HOP1>
+__global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict__ pool,
+                                                        const unsigned long long* __restrict__ cmeta,
+                                                        const uint32_t* __restrict__ order, int64_t nchunks,
+                                                        int64_t per, Layout L, unsigned long long* __restrict__ cur2,
+                                                        uint2* __restrict__ out, Hop1Out h1) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
+    const int nb = L.ns;
+    uint2* stage = reinterpret_cast<uint2*>(smem);
+    unsigned long long* base = smem + kTile;
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(base + nb);
+    uint32_t* loc = cnt + nb;
+    uint32_t* wtot = loc + nb;
+    uint32_t* tl = wtot + kSBlock / 64;  // HOP1: target slice marks
+    const int64_t q0 = (int64_t)blockIdx.x * per, q1 = min(q0 + per, nchunks);
+    int cur_j = -1;
+    for (int64_t q = q0; q < q1; ++q) {  // block-uniform
+        const uint32_t phys = order[q];
+        const unsigned long long meta = cmeta[phys];
+        const int j = (int)(uint32_t)meta;
+        const uint32_t fill = (uint32_t)(meta >> 32);
+        if (HOP1 && j != cur_j) {
+            if (cur_j >= 0) {
+                __syncthreads();
+                flush_slice(tl, h1.M, cur_j, h1.gwords, h1.tmask);
+                __syncthreads();
+            }
+            for (int k = threadIdx.x; k < kSliceWords; k += kSBlock) tl[k] = 0;
+            cur_j = j;
+        }
+        for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
+        __syncthreads();
+        // buffer loads clipped at the chunk's fill: nothing past it is fetched
+        const uint2* cb = pool + (size_t)phys * kCh;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2*>(cb), (short)0, (int)(fill * sizeof(uint2)), 0x00020000);
+        uint2 pr[kItems];
+        uint32_t rk[kItems];
+        uint32_t valid = 0;
+#pragma unroll
+        for (int k = 0; k < kItems / 2; ++k) {
+            const uint32_t off = (uint32_t)(k * kSBlock + (int)threadIdx.x) * 16u;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+            pr[2 * k] = make_uint2(v[0], v[1]);
+            pr[2 * k + 1] = make_uint2(v[2], v[3]);
+        }
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {
+            valid |= ((uint32_t)item_off<kSBlock>(k) < fill ? 1u : 0u) << k;
+            rk[k] = 0;
+        }
+        const uint32_t tbase = (uint32_t)j << kSliceBits;
+#pragma unroll
+        for (int k = 0; k < kItems; ++k)
+            if ((valid >> k) & 1u) {
+                rk[k] = atomicAdd(&cnt[pr[k].x >> L.sbits], 1u);
+                if (HOP1) {
+                    const uint32_t s = pr[k].x, t = pr[k].y;
+                    if (s != t) {
+                        lds_set(tl, t - tbase);
+                    } else if (h1.tmask.full || gbit(h1.tmask.w, t)) {  // rare: self-loops
+                        const uint32_t bit = 1u << (t & 31);
+                        const uint32_t old = atomicOr(&h1.S1[t >> 5], bit);
+                        if (old & bit) atomicOr(&h1.S2[t >> 5], bit);
+                    }
+                }
+            }
+        __syncthreads();
+        scatter_tile(pr, valid, rk, nb, cur2 + (size_t)j * nb, out, stage, base, cnt, loc, wtot, L.sbits);
+    }
+    if (HOP1 && cur_j >= 0) {
+        __syncthreads();
+        flush_slice(tl, h1.M, cur_j, h1.gwords, h1.tmask);
     }
 }
 
@@ -477,73 +537,84 @@ static void allow_lds(K kernel, size_t bytes) {
 }
 
 void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
-                   int64_t lo, int64_t hi, RelPart& rp) {
-    REQUIRE(hi > lo && (uint64_t)(hi - lo) <= (uint64_t(1) << 31), CAPSMI_ERR_UNSUPPORTED,
-            "partitioned layout needs an id domain of at most 2^31 ids");
+                   int64_t lo, int64_t hi, RelPart& rp, const RelPartHop1* h1) {
+    REQUIRE(hi > lo && (uint64_t)(hi - lo) <= (uint64_t(1) << 30), CAPSMI_ERR_UNSUPPORTED,
+            "partitioned layout needs an id domain of at most 2^30 ids");
     using namespace part;
     hipStream_t st = s->stream;
     rp.L = make_layout(lo, hi);
     const Layout& L = rp.L;
     REQUIRE(L.nt <= kMaxTSlices && L.ncells <= kMaxCells, CAPSMI_ERR_INTERNAL, "layout too large");
-    const int nunits = L.nt * kReps;
-    // blocks: a multiple of kReps, about two 1024-lane blocks per CU
-    const int grid = kReps * (int)std::max<int64_t>(1, (2 * (int64_t)s->num_cus + kReps - 1) / kReps);
+    if (h1)
+        REQUIRE(h1->a->lo == lo && h1->a->hi == hi && h1->b->lo == lo && h1->b->hi == hi, CAPSMI_ERR_UNSUPPORTED,
+                "partitioned 2-hop needs node scans over the layout's id domain");
 
-    Buf cnt = dev_alloc(sizeof(unsigned int) * kReps * L.ncells, st);
-    HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, sizeof(unsigned int) * kReps * L.ncells, st));
+    // pass 1 grid: one 1024-lane block per CU, fewer for small inputs so the open chunks
+    // (blocks x slices) stay within a few times the filled ones
+    std::vector<int> g1(nt, 0);
+    int64_t pool_chunks = 1;
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
-        KernelTimer kt(s, "part_hist");
-        hipLaunchKernelGGL(k_part_hist, dim3(grid), dim3(kBlock), sizeof(unsigned int) * L.ncells, st, srcs[i], dsts[i],
-                           ms[i], L, P<unsigned int>(cnt));
+        const int64_t full = (ms[i] + kCh - 1) / kCh;
+        int64_t g = std::min<int64_t>(s->num_cus, (ms[i] + 8 * (int64_t)kTile - 1) / (8 * (int64_t)kTile));
+        g = std::min<int64_t>(g, std::max<int64_t>(1, 8 * full / L.nt));
+        g1[i] = (int)std::max<int64_t>(1, g);
+        pool_chunks += full + (int64_t)g1[i] * L.nt;
     }
-    // offsets, all on the device: cells, pass-1 cursors per (replica, slice), pass-2 units
-    Buf pre = dev_alloc(sizeof(int64_t) * kReps * L.ncells, st);  // becomes cur2
-    Buf tot = dev_alloc(sizeof(int64_t) * L.ncells, st);
-    rp.boff = dev_alloc(sizeof(int64_t) * (L.ncells + 1), st);  // coff
-    Buf cur1 = dev_alloc(sizeof(int64_t) * nunits, st);
-    Buf units = dev_alloc(sizeof(int64_t) * (4 * (size_t)nunits + 1), st);  // ustart | ulen | utiles | upre
-    int64_t* ustart = P<int64_t>(units);
-    int64_t* ulen = ustart + nunits;
-    int64_t* utiles = ulen + nunits;
-    int64_t* upre = utiles + nunits;
-    hipLaunchKernelGGL(k_cell_prefix, dim3((L.ncells + 255) / 256), dim3(256), 0, st, P<unsigned int>(cnt), L.ncells,
-                       P<int64_t>(pre), P<int64_t>(tot));
-    exclusive_scan_i64(P<int64_t>(tot), P<int64_t>(rp.boff), L.ncells, st);
-    hipLaunchKernelGGL(k_units, dim3((nunits + 255) / 256), dim3(256), 0, st, P<unsigned int>(cnt), P<int64_t>(pre),
-                       P<int64_t>(rp.boff), L, P<int64_t>(cur1), ustart, ulen, utiles);
-    hipLaunchKernelGGL(k_add_coff, dim3((unsigned)(((int64_t)kReps * L.ncells + 255) / 256)), dim3(256), 0, st,
-                       P<int64_t>(pre), P<int64_t>(rp.boff), L.ncells);
-    exclusive_scan_i64(utiles, upre, nunits, st);
+    REQUIRE(pool_chunks < (int64_t)kNone, CAPSMI_ERR_UNSUPPORTED, "relationship table too large for the layout");
+    Buf pool = dev_alloc(sizeof(uint2) * kCh * (size_t)pool_chunks, st);
+    Buf meta = dev_alloc(sizeof(unsigned long long) * pool_chunks, st);
+    Buf ccount = dev_alloc(sizeof(unsigned long long) * (L.ncells + 1) + sizeof(unsigned int) * 2, st);
+    unsigned int* pool_ctr = reinterpret_cast<unsigned int*>(P<unsigned long long>(ccount) + L.ncells + 1);
+    HIP_CHECK(hipMemsetAsync(P<void>(ccount), 0, sizeof(unsigned long long) * (L.ncells + 1) + sizeof(unsigned int) * 2, st));
+    const size_t lds1 = scatter1_lds(L.nt, L.ncells);
+    allow_lds(k_scatter_c, lds1);
+    for (int i = 0; i < nt; ++i) {
+        if (ms[i] <= 0) continue;
+        KernelTimer kt(s, "part_scatter1");
+        hipLaunchKernelGGL(k_scatter_c, dim3(g1[i]), dim3(kSBlock), lds1, st, srcs[i], dsts[i], ms[i], L, pool_ctr,
+                           P<uint2>(pool), P<unsigned long long>(meta), P<unsigned long long>(ccount));
+    }
     HIP_CHECK(hipGetLastError());
-    int64_t kept = 0, ntiles = 0;
-    HIP_CHECK(hipMemcpyAsync(&kept, P<int64_t>(rp.boff) + L.ncells, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipMemcpyAsync(&ntiles, upre + nunits, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    rp.boff = dev_alloc(sizeof(int64_t) * (L.ncells + 1), st);  // cell offsets
+    exclusive_scan_i64(P<int64_t>(ccount), P<int64_t>(rp.boff), L.ncells, st);
+    int64_t host[2] = {0, 0};
+    HIP_CHECK(hipMemcpyAsync(&host[0], P<int64_t>(rp.boff) + L.ncells, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(&host[1], pool_ctr, sizeof(unsigned int), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    rp.kept = kept;
-    const size_t bytes = sizeof(uint2) * ((rp.kept > 0 ? rp.kept : 1) + kPad);
-    rp.pairs = dev_alloc(bytes, st);
-    if (rp.kept == 0) return;
-    Buf tmp = dev_alloc(bytes, st);
-    const size_t lds1 = scatter_lds(L.nt), lds2 = scatter_lds(L.ns);
-    allow_lds(k_scatter_t, lds1);
-    allow_lds(k_scatter_s, lds2);
-    Buf tmap = dev_alloc(sizeof(int) * (ntiles > 0 ? ntiles : 1), st);
-    hipLaunchKernelGGL(k_tile_unit, dim3((nunits + 255) / 256), dim3(256), 0, st, upre, nunits, P<int>(tmap));
-    // scatter blocks: kSBlock lanes, about two per CU, a multiple of kReps
-    const int sgrid = kReps * (int)std::max<int64_t>(1, (2 * (int64_t)s->num_cus + kReps - 1) / kReps);
-    for (int i = 0; i < nt; ++i) {
-        if (ms[i] <= 0) continue;
-        KernelTimer kt(s, "part_scatter_t");
-        hipLaunchKernelGGL(k_scatter_t, dim3(sgrid), dim3(kSBlock), lds1, st, srcs[i], dsts[i], ms[i], L,
-                           P<unsigned long long>(cur1), P<uint2>(tmp));
+    rp.kept = host[0];
+    const int64_t nchunks = host[1];
+    rp.pairs = dev_alloc(sizeof(uint2) * ((rp.kept > 0 ? rp.kept : 1) + kPad), st);
+
+    const bool fuse = h1 && h1->a->full;
+    if (rp.kept > 0) {
+        // chunks ordered by target slice, pass-2 cursors = cell offsets
+        Buf jbuf = dev_alloc(sizeof(int64_t) * (2 * (size_t)L.nt + 1) + sizeof(uint32_t) * nchunks, st);
+        int64_t* jcnt = P<int64_t>(jbuf);
+        int64_t* jcur = jcnt + L.nt;
+        uint32_t* order = reinterpret_cast<uint32_t*>(jcur + L.nt + 1);
+        HIP_CHECK(hipMemsetAsync(jcnt, 0, sizeof(int64_t) * L.nt, st));
+        const unsigned cg = (unsigned)((nchunks + 255) / 256);
+        hipLaunchKernelGGL(k_chunk_count, dim3(cg), dim3(256), 0, st, P<unsigned long long>(meta), nchunks, jcnt);
+        exclusive_scan_i64(jcnt, jcur, L.nt, st);
+        hipLaunchKernelGGL(k_chunk_place, dim3(cg), dim3(256), 0, st, P<unsigned long long>(meta), nchunks,
+                           reinterpret_cast<unsigned long long*>(jcur), order);
+        Buf cur2 = dev_alloc(sizeof(int64_t) * L.ncells, st);
+        HIP_CHECK(hipMemcpyAsync(P<void>(cur2), P<void>(rp.boff), sizeof(int64_t) * L.ncells, hipMemcpyDeviceToDevice, st));
+        Hop1Out ho{};
+        if (fuse) ho = Hop1Out{BitV{P<uint32_t>(h1->b->words), h1->b->full ? 1 : 0}, h1->M, h1->S1, h1->S2, h1->b->nwords};
+        const size_t lds2 = scatter_lds(L.ns) + (fuse ? sizeof(uint32_t) * kSliceWords : 0);
+        auto k2 = fuse ? k_scatter_s2<true> : k_scatter_s2<false>;
+        allow_lds(k2, lds2);
+        const int64_t g2 = std::min<int64_t>(nchunks, (int64_t)s->num_cus * (fuse ? 1 : 2));
+        const int64_t per = (nchunks + g2 - 1) / g2;
+        KernelTimer kt(s, fuse ? "part_scatter2_hop1" : "part_scatter2");
+        hipLaunchKernelGGL(k2, dim3((unsigned)((nchunks + per - 1) / per)), dim3(kSBlock), lds2, st, P<uint2>(pool),
+                           P<unsigned long long>(meta), order, nchunks, per, L, P<unsigned long long>(cur2),
+                           P<uint2>(rp.pairs), ho);
+        HIP_CHECK(hipGetLastError());
     }
-    {
-        KernelTimer kt(s, "part_scatter_s");
-        hipLaunchKernelGGL(k_scatter_s, dim3(sgrid), dim3(kSBlock), lds2, st, P<uint2>(tmp), ustart, ulen, upre,
-                           P<int>(tmap), ntiles, L, P<unsigned long long>(pre), P<uint2>(rp.pairs));
-    }
-    HIP_CHECK(hipGetLastError());
+    if (h1 && !fuse) relpart_hop1(s, rp, h1->a, h1->b, h1->M, h1->S1, h1->S2);
 }
 
 template <bool HOP1, bool SRC_FULL>

@@ -260,14 +260,20 @@ capsmi_status capsmi_two_hop_mark_dst(capsmi_session* s, int32_t nrels, capsmi_t
                                       const char* src_col, const char* dst_col, const capsmi_bitmap* b_ok,
                                       const capsmi_bitmap* c_ok, const uint32_t* mid_words, uint32_t* dst_words);
 /* Radix-partitioned relationship layout for the 2-hop kernels: rows of the union of `rels` with both
- * endpoints in [id_lo, id_hi) (hi - lo <= 2^32), packed to 32-bit ids and bucketed by
- * (source super-slice per XCD) x (target slice of 2^19 ids).  Building it is part of the cold query;
- * keeping it across queries is the Cache analogue (DataFrameTable.cache, SparkTable.scala:240-246). */
+ * endpoints in [id_lo, id_hi) (hi - lo <= 2^30), packed to 32-bit ids and grouped by 2-D cell
+ * (target slice of 2^19 ids) x (source slice).  Building it is part of the cold query; keeping it
+ * across queries is the Cache analogue (DataFrameTable.cache, SparkTable.scala:240-246). */
 typedef struct capsmi_relpart capsmi_relpart;
 capsmi_status capsmi_relpart_build(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
                                    const char* dst_col, int64_t id_lo, int64_t id_hi, capsmi_relpart** out);
 capsmi_status capsmi_relpart_size(const capsmi_relpart* p, int64_t* kept_rows);
 capsmi_status capsmi_relpart_release(capsmi_relpart* p);
+/* capsmi_relpart_build followed by capsmi_two_hop_mark_mid_part, with hop 1 run by the build's second
+ * pass when a_ok covers the whole id domain (the cold 2-hop: one pass fewer over the relationships) */
+capsmi_status capsmi_relpart_build_mark_mid(capsmi_session* s, int32_t nrels, capsmi_table* const* rels,
+                                            const char* src_col, const char* dst_col, const capsmi_bitmap* a_ok,
+                                            const capsmi_bitmap* b_ok, uint32_t* mid_words, uint32_t* scratch_words,
+                                            capsmi_relpart** out);
 /* the phased 2-hop over a partitioned layout (same contract as capsmi_two_hop_mark_mid/_dst) */
 capsmi_status capsmi_two_hop_mark_mid_part(capsmi_session* s, const capsmi_relpart* p, const capsmi_bitmap* a_ok,
                                            const capsmi_bitmap* b_ok, uint32_t* mid_words, uint32_t* scratch_words);

@@ -112,3 +112,85 @@ def test_several_rel_tables(session):
     assert rp.size == m
     assert rp.count_distinct(bm, bm, bm) == want
     rp.release()
+
+
+def _mid_words(session, rp_factory, n, a, b):
+    import torch
+    nw = (n + 31) // 32
+    mid = torch.zeros(2 * nw, dtype=torch.int32, device="cuda")
+    scratch = torch.zeros(nw, dtype=torch.int32, device="cuda")
+    rp = rp_factory(mid.data_ptr(), scratch.data_ptr())
+    session.sync()
+    return rp, mid.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("a_full", [True, False])
+def test_build_mark_mid_matches_phased(session, a_full):
+    """Hop 1 run inside the build's second pass (a_ok full) or after it (a_ok partial) gives the same
+    X1 / X2 frontier words as the phased build + mark_mid, and the same final count."""
+    from capsmi import graph
+    scale = 21
+    n = 1 << scale
+    rels = graph.rmat_rels(session, scale, 0, 8 << scale)
+    rng = np.random.default_rng(11)
+    a = _bitmap(session, n, np.arange(n) if a_full else np.nonzero(rng.random(n) < 0.7)[0])
+    b = _bitmap(session, n, np.nonzero(rng.random(n) < 0.8)[0])
+    rp1 = graph.RelPartition(session, [rels], 0, n)
+    _, want = _mid_words(session, lambda m, s: rp1.mark_mid(a, b, m, s), n, a, b)
+    rp2, got = _mid_words(session, lambda m, s: graph.RelPartition.build_mark_mid(session, [rels], a, b, m, s),
+                          n, a, b)
+    assert np.array_equal(got, want)
+    assert rp2.size == rp1.size == 8 << scale
+    assert rp2.count_distinct(a, b, b) == rp1.count_distinct(a, b, b)
+    rp1.release()
+    rp2.release()
+
+
+def test_skewed_slices_and_chunk_splits(session):
+    """One target slice takes most relationships (its chunks split inside tiles), the others get a
+    trickle (open chunks retired nearly empty); several input tables = several pass-1 launches."""
+    from capsmi import ColumnData, I64, graph
+    n = 1 << 23  # 16 target slices
+    rng = np.random.default_rng(21)
+    m = 3 << 20
+    hot = rng.integers(0, 1 << 19, m)
+    cold = rng.integers(0, n, m)
+    dst = np.where(rng.random(m) < 0.9, hot, cold).astype(np.int64)
+    src = rng.integers(0, n, m).astype(np.int64)
+    src[::97] = dst[::97]  # self-loops, some repeated
+    tabs = []
+    cuts = [0, 5, 70000, m // 2, m]
+    for k in range(4):
+        sl = slice(cuts[k], cuts[k + 1])
+        tabs.append(session.table([ColumnData("id", I64, np.arange(cuts[k], cuts[k + 1])),
+                                   ColumnData("source", I64, src[sl]), ColumnData("target", I64, dst[sl])]))
+    ok = np.ones(n, bool)
+    okc = rng.random(n) < 0.5
+    a, c = _bitmap(session, n, np.arange(n)), _bitmap(session, n, np.nonzero(okc)[0])
+    want = _np_count_distinct(n, src, dst, ok, ok, okc)
+    assert graph.two_hop_count_distinct(session, tabs, a, a, c) == want
+    rp = graph.RelPartition(session, tabs, 0, n)
+    assert rp.size == m
+    assert rp.count_distinct(a, a, c) == want
+    rp.release()
+
+
+def test_largest_domain(session):
+    """2^30-id domain: 2048 target slices (the pass-1 LDS limit), coarse source slices."""
+    from capsmi import ColumnData, I64, graph
+    n = 1 << 30
+    rng = np.random.default_rng(4)
+    m = 1 << 18
+    src = rng.integers(0, n, m).astype(np.int64)
+    dst = np.where(rng.random(m) < 0.5, rng.integers(0, 1 << 12, m), rng.integers(0, n, m)).astype(np.int64)
+    rels = session.table([ColumnData("id", I64, np.arange(m)), ColumnData("source", I64, src),
+                          ColumnData("target", I64, dst)])
+    ids = np.unique(np.concatenate([src, dst]))
+    bm = _bitmap(session, n, ids)
+    k = len(ids)  # the oracle on compacted ids (every endpoint is scanned)
+    ok = np.ones(k, bool)
+    want = _np_count_distinct(k, np.searchsorted(ids, src), np.searchsorted(ids, dst), ok, ok, ok)
+    rp = graph.RelPartition(session, [rels], 0, n)
+    assert rp.size == m
+    assert rp.count_distinct(bm, bm, bm) == want
+    rp.release()
