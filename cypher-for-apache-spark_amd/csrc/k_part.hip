@@ -137,10 +137,12 @@ __device__ __forceinline__ void load_pairs(const uint2* __restrict__ in, int64_t
 // ---- pass 1: int64 (source, target) -> packed pairs in per-workgroup chunks of one target slice ------
 //
 // No counting pass: every workgroup keeps one open chunk (kCh pairs) per target slice and appends
-// its tiles' runs to it; a full chunk is retired and a fresh one taken from the pool, a whole
-// tile's worth of fresh chunks with one global atomic.  Chunk metadata records (slice, fill).
-// The pass also counts the 2-D cells (target slice x source slice) in a 16-bit LDS histogram,
-// so pass 2 can write the cell-grouped layout at exact offsets.
+// its tiles' runs to it; a full chunk is retired and the next one taken from the workgroup's own
+// range of the pool (a block with T tiles fills at most T chunks and leaves at most one open per
+// slice, so T + nt chunks suffice and no global atomic sits in the tile loop).  Chunk metadata
+// records (slice, fill); fill 0 = unused.  The pass also counts the 2-D cells (target slice x
+// source slice) in a 16-bit LDS histogram, so pass 2 can write the cell-grouped layout at exact
+// offsets.  The next tile's loads are issued before this tile is regrouped and written.
 
 __device__ __forceinline__ unsigned long long chunk_meta(int j, uint32_t fill) {
     return (unsigned long long)(uint32_t)j | ((unsigned long long)fill << 32);
@@ -161,8 +163,13 @@ __host__ __device__ constexpr size_t scatter1_lds(int nb, int ncells) {
     return sizeof(uint2) * kTile + sizeof(uint32_t) * ((size_t)(ncells + 1) / 2 + 7 * (size_t)nb + kSBlock / 64 + 4);
 }
 
+// chunks per pass-1 block: tiles of the busiest block + one open chunk per slice
+__host__ __device__ inline int64_t chunks_per_block(int64_t m, int64_t grid, int nt) {
+    return ((m + kTile - 1) / kTile + grid - 1) / grid + nt;
+}
+
 __global__ void __launch_bounds__(kSBlock) k_scatter_c(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
-                                                       int64_t m, Layout L, unsigned int* __restrict__ pool_ctr,
+                                                       int64_t m, Layout L, int64_t chunk0,
                                                        uint2* __restrict__ pool, unsigned long long* __restrict__ cmeta,
                                                        unsigned long long* __restrict__ ccount) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
@@ -177,36 +184,38 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_c(const int64_t* __restrict
     uint32_t* f0 = p0 + nb;
     uint32_t* p1 = f0 + nb;      // ... the rest (if any) from the start of chunk p1
     uint32_t* wtot = p1 + nb;
-    uint32_t* misc = wtot + kSBlock / 64;
+    uint32_t* misc = wtot + kSBlock / 64;  // [0] fresh chunks this tile, [1] next free chunk
     for (int i = threadIdx.x; i < hw; i += kSBlock) hist[i] = 0;
     for (int i = threadIdx.x; i < nb; i += kSBlock) {
         ph[i] = kNone;
         fl[i] = 0;
     }
+    if (threadIdx.x == 0) {
+        misc[0] = 0;
+        misc[1] = (uint32_t)(chunk0 + (int64_t)blockIdx.x * chunks_per_block(m, gridDim.x, nb));
+    }
     const uint64_t range = (uint64_t)(L.hi - L.lo);
     const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
-    for (int64_t k = blockIdx.x;; k += gridDim.x) {
-        const int64_t t0 = k * kTile;
-        if (t0 >= m) break;  // block-uniform
+    const int64_t stride = (int64_t)gridDim.x * kTile;
+    int64_t sr[kItems], tr[kItems];
+    int64_t t0 = (int64_t)blockIdx.x * kTile;
+    if (t0 < m) load_tile<kSBlock>(src, dst, t0, m, vec, sr, tr);
+    for (; t0 < m; t0 += stride) {  // block-uniform
         for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
-        if (threadIdx.x == 0) misc[0] = 0;
         __syncthreads();
         uint2 pr[kItems];
         uint32_t rk[kItems];
         uint32_t valid = 0;
-        {
-            int64_t sr[kItems], tr[kItems];
-            load_tile<kSBlock>(src, dst, t0, m, vec, sr, tr);
 #pragma unroll
-            for (int u = 0; u < kItems; ++u) {
-                const int64_t e = t0 + item_off<kSBlock>(u);
-                const uint64_t s = (uint64_t)(sr[u] - L.lo), t = (uint64_t)(tr[u] - L.lo);
-                const bool ok = e < m && s < range && t < range;
-                pr[u] = make_uint2((uint32_t)s, (uint32_t)t);
-                valid |= (ok ? 1u : 0u) << u;
-                rk[u] = 0;
-            }
+        for (int u = 0; u < kItems; ++u) {
+            const int64_t e = t0 + item_off<kSBlock>(u);
+            const uint64_t s = (uint64_t)(sr[u] - L.lo), t = (uint64_t)(tr[u] - L.lo);
+            const bool ok = e < m && s < range && t < range;
+            pr[u] = make_uint2((uint32_t)s, (uint32_t)t);
+            valid |= (ok ? 1u : 0u) << u;
+            rk[u] = 0;
         }
+        if (t0 + stride < m) load_tile<kSBlock>(src, dst, t0 + stride, m, vec, sr, tr);  // prefetch
 #pragma unroll
         for (int u = 0; u < kItems; ++u)
             if ((valid >> u) & 1u) {
@@ -215,30 +224,21 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_c(const int64_t* __restrict
             }
         __syncthreads();
         const uint32_t total = block_exclusive_scan<kSBlock>(cnt, loc, nb, wtot);
-        for (int i = threadIdx.x; i < nb; i += kSBlock) {  // runs that fit their open chunk
+        const uint32_t nf = misc[1];
+        for (int i = threadIdx.x; i < nb; i += kSBlock) {
             const uint32_t c = cnt[i];
             if (!c) continue;
             const uint32_t p = ph[i], f = fl[i];
-            if (p != kNone && f + c <= (uint32_t)kCh) {
+            if (p != kNone && f + c <= (uint32_t)kCh) {  // fits the open chunk
                 p0[i] = p;
                 f0[i] = f;
-                p1[i] = kNone;
                 fl[i] = f + c;
-            } else {
-                p1[i] = atomicAdd(&misc[0], 1u);  // index among this tile's fresh chunks
+                continue;
             }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) misc[1] = misc[0] ? atomicAdd(pool_ctr, misc[0]) : 0u;
-        __syncthreads();
-        for (int i = threadIdx.x; i < nb; i += kSBlock) {  // runs that open a chunk
-            const uint32_t c = cnt[i];
-            if (!c || p1[i] == kNone) continue;
-            const uint32_t np = misc[1] + p1[i], p = ph[i], f = fl[i];
+            const uint32_t np = nf + atomicAdd(&misc[0], 1u);
             if (p == kNone) {
                 p0[i] = np;
                 f0[i] = 0;
-                p1[i] = kNone;
                 fl[i] = c;
             } else {  // fill chunk p, retire it, continue in np
                 p0[i] = p;
@@ -253,6 +253,10 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_c(const int64_t* __restrict
         for (int u = 0; u < kItems; ++u)
             if ((valid >> u) & 1u) stage[loc[pr[u].y >> kSliceBits] + rk[u]] = pr[u];
         __syncthreads();
+        if (threadIdx.x == 0) {
+            misc[1] += misc[0];
+            misc[0] = 0;
+        }
         for (uint32_t idx = threadIdx.x; idx < total; idx += kSBlock) {
             const uint2 p = stage[idx];
             const int b = (int)(p.y >> kSliceBits);
@@ -271,17 +275,18 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_c(const int64_t* __restrict
     }
 }
 
-// chunks grouped by target slice (order within a slice is arbitrary)
+// used chunks (fill > 0) grouped by target slice (order within a slice is arbitrary)
 __global__ void k_chunk_count(const unsigned long long* __restrict__ cmeta, int64_t nchunks,
                               int64_t* __restrict__ jcnt) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q < nchunks) atomicAdd(reinterpret_cast<unsigned long long*>(&jcnt[(uint32_t)cmeta[q]]), 1ULL);
+    if (q < nchunks && (cmeta[q] >> 32))
+        atomicAdd(reinterpret_cast<unsigned long long*>(&jcnt[(uint32_t)cmeta[q]]), 1ULL);
 }
 
 __global__ void k_chunk_place(const unsigned long long* __restrict__ cmeta, int64_t nchunks,
                               unsigned long long* __restrict__ jcur, uint32_t* __restrict__ order) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q < nchunks) order[atomicAdd(&jcur[(uint32_t)cmeta[q]], 1ULL)] = (uint32_t)q;
+    if (q < nchunks && (cmeta[q] >> 32)) order[atomicAdd(&jcur[(uint32_t)cmeta[q]], 1ULL)] = (uint32_t)q;
 }
 
 // LDS carve-up of pass 2 (and the generic scatter_tile): stage[kTile] | base[nb] (u64) | cnt[nb] | loc[nb] | wtot
@@ -552,35 +557,49 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
     // pass 1 grid: one 1024-lane block per CU, fewer for small inputs so the open chunks
     // (blocks x slices) stay within a few times the filled ones
     std::vector<int> g1(nt, 0);
-    int64_t pool_chunks = 1;
+    std::vector<int64_t> c0(nt, 0);
+    int64_t pool_chunks = 0;
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
         const int64_t full = (ms[i] + kCh - 1) / kCh;
         int64_t g = std::min<int64_t>(s->num_cus, (ms[i] + 8 * (int64_t)kTile - 1) / (8 * (int64_t)kTile));
         g = std::min<int64_t>(g, std::max<int64_t>(1, 8 * full / L.nt));
         g1[i] = (int)std::max<int64_t>(1, g);
-        pool_chunks += full + (int64_t)g1[i] * L.nt;
+        c0[i] = pool_chunks;
+        pool_chunks += (int64_t)g1[i] * chunks_per_block(ms[i], g1[i], L.nt);
     }
     REQUIRE(pool_chunks < (int64_t)kNone, CAPSMI_ERR_UNSUPPORTED, "relationship table too large for the layout");
-    Buf pool = dev_alloc(sizeof(uint2) * kCh * (size_t)pool_chunks, st);
-    Buf meta = dev_alloc(sizeof(unsigned long long) * pool_chunks, st);
-    Buf ccount = dev_alloc(sizeof(unsigned long long) * (L.ncells + 1) + sizeof(unsigned int) * 2, st);
-    unsigned int* pool_ctr = reinterpret_cast<unsigned int*>(P<unsigned long long>(ccount) + L.ncells + 1);
-    HIP_CHECK(hipMemsetAsync(P<void>(ccount), 0, sizeof(unsigned long long) * (L.ncells + 1) + sizeof(unsigned int) * 2, st));
+    const int64_t npool = pool_chunks > 0 ? pool_chunks : 1;
+    Buf pool = dev_alloc(sizeof(uint2) * kCh * (size_t)npool, st);
+    Buf meta = dev_alloc(sizeof(unsigned long long) * npool, st);
+    Buf ccount = dev_alloc(sizeof(unsigned long long) * L.ncells, st);
+    HIP_CHECK(hipMemsetAsync(P<void>(meta), 0, sizeof(unsigned long long) * npool, st));
+    HIP_CHECK(hipMemsetAsync(P<void>(ccount), 0, sizeof(unsigned long long) * L.ncells, st));
     const size_t lds1 = scatter1_lds(L.nt, L.ncells);
     allow_lds(k_scatter_c, lds1);
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
         KernelTimer kt(s, "part_scatter1");
-        hipLaunchKernelGGL(k_scatter_c, dim3(g1[i]), dim3(kSBlock), lds1, st, srcs[i], dsts[i], ms[i], L, pool_ctr,
+        hipLaunchKernelGGL(k_scatter_c, dim3(g1[i]), dim3(kSBlock), lds1, st, srcs[i], dsts[i], ms[i], L, c0[i],
                            P<uint2>(pool), P<unsigned long long>(meta), P<unsigned long long>(ccount));
     }
     HIP_CHECK(hipGetLastError());
     rp.boff = dev_alloc(sizeof(int64_t) * (L.ncells + 1), st);  // cell offsets
     exclusive_scan_i64(P<int64_t>(ccount), P<int64_t>(rp.boff), L.ncells, st);
+    // used chunks ordered by target slice
+    Buf jbuf = dev_alloc(sizeof(int64_t) * (2 * (size_t)L.nt + 1) + sizeof(uint32_t) * npool, st);
+    int64_t* jcnt = P<int64_t>(jbuf);
+    int64_t* jcur = jcnt + L.nt;
+    uint32_t* order = reinterpret_cast<uint32_t*>(jcur + L.nt + 1);
+    HIP_CHECK(hipMemsetAsync(jcnt, 0, sizeof(int64_t) * L.nt, st));
+    const unsigned cg = (unsigned)((npool + 255) / 256);
+    hipLaunchKernelGGL(k_chunk_count, dim3(cg), dim3(256), 0, st, P<unsigned long long>(meta), pool_chunks, jcnt);
+    exclusive_scan_i64(jcnt, jcur, L.nt, st);
+    hipLaunchKernelGGL(k_chunk_place, dim3(cg), dim3(256), 0, st, P<unsigned long long>(meta), pool_chunks,
+                       reinterpret_cast<unsigned long long*>(jcur), order);
     int64_t host[2] = {0, 0};
     HIP_CHECK(hipMemcpyAsync(&host[0], P<int64_t>(rp.boff) + L.ncells, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipMemcpyAsync(&host[1], pool_ctr, sizeof(unsigned int), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(&host[1], jcur + L.nt, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
     rp.kept = host[0];
     const int64_t nchunks = host[1];
@@ -588,17 +607,6 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
 
     const bool fuse = h1 && h1->a->full;
     if (rp.kept > 0) {
-        // chunks ordered by target slice, pass-2 cursors = cell offsets
-        Buf jbuf = dev_alloc(sizeof(int64_t) * (2 * (size_t)L.nt + 1) + sizeof(uint32_t) * nchunks, st);
-        int64_t* jcnt = P<int64_t>(jbuf);
-        int64_t* jcur = jcnt + L.nt;
-        uint32_t* order = reinterpret_cast<uint32_t*>(jcur + L.nt + 1);
-        HIP_CHECK(hipMemsetAsync(jcnt, 0, sizeof(int64_t) * L.nt, st));
-        const unsigned cg = (unsigned)((nchunks + 255) / 256);
-        hipLaunchKernelGGL(k_chunk_count, dim3(cg), dim3(256), 0, st, P<unsigned long long>(meta), nchunks, jcnt);
-        exclusive_scan_i64(jcnt, jcur, L.nt, st);
-        hipLaunchKernelGGL(k_chunk_place, dim3(cg), dim3(256), 0, st, P<unsigned long long>(meta), nchunks,
-                           reinterpret_cast<unsigned long long*>(jcur), order);
         Buf cur2 = dev_alloc(sizeof(int64_t) * L.ncells, st);
         HIP_CHECK(hipMemcpyAsync(P<void>(cur2), P<void>(rp.boff), sizeof(int64_t) * L.ncells, hipMemcpyDeviceToDevice, st));
         Hop1Out ho{};

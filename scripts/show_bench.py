@@ -1,0 +1,14 @@
+#!/usr/bin/env python3
+"""Print the key numbers of a bench JSON line (last JSON line of the given log)."""
+import json
+import sys
+
+for f in sys.argv[1:]:
+    line = [l for l in open(f) if l.startswith("{")][-1]
+    d = json.loads(line)
+    q = d.get("query", {})
+    print(f"{f}: {d['ms_per_step']:.3f} ms/step  value={d['value']:.4g}  kernel={d['roofline'] and d['roofline']['kernel']} "
+          f"frac={d['roofline'] and round(d['roofline']['frac'], 3)}  query_frac={q.get('query_frac_of_peak', 0):.3f}")
+    for k, v in q.get("kernel_ms", {}).items():
+        print(f"    {k:22s} {v:8.3f} ms")
+    print("    check:", q.get("check_vs_unpartitioned"))
