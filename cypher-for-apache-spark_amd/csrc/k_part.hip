@@ -140,27 +140,20 @@ __device__ __forceinline__ void load_pairs(const uint2* __restrict__ in, int64_t
 // its tiles' runs to it; a full chunk is retired and the next one taken from the workgroup's own
 // range of the pool (a block with T tiles fills at most T chunks and leaves at most one open per
 // slice, so T + nt chunks suffice and no global atomic sits in the tile loop).  Chunk metadata
-// records (slice, fill); fill 0 = unused.  The pass also counts the 2-D cells (target slice x
-// source slice) in a 16-bit LDS histogram, so pass 2 can write the cell-grouped layout at exact
-// offsets.  The next tile's loads are issued before this tile is regrouped and written.
+// records (slice, fill); fill 0 = unused.  Each open chunk also counts its pairs per source slice
+// (16-bit LDS counters, nt x ns of them = one per 2-D cell), written out as the chunk's cell
+// histogram when it is retired; pass 2 derives exact output offsets from those.  The next tile's
+// loads are issued before this tile is regrouped and written.
 
 __device__ __forceinline__ unsigned long long chunk_meta(int j, uint32_t fill) {
     return (unsigned long long)(uint32_t)j | ((unsigned long long)fill << 32);
 }
 
-// 16-bit cell counter, two per LDS word; the lane that takes a counter from 0x7FFF to 0x8000
-// moves 0x8000 to the global count (a tile adds at most kTile < 0x8000 before that lands)
-__device__ __forceinline__ void hist16_inc(uint32_t* hist, unsigned long long* gcount, int c) {
-    const uint32_t sh = (uint32_t)(c & 1) * 16u;
-    const uint32_t old = atomicAdd(&hist[c >> 1], 1u << sh);
-    if (((old >> sh) & 0xFFFFu) == 0x7FFFu) {
-        atomicAdd(&gcount[c], 0x8000ULL);
-        atomicSub(&hist[c >> 1], 0x8000u << sh);
-    }
-}
+// per-chunk histogram row: ns 16-bit counters padded to an even count (whole 32-bit words)
+__host__ __device__ constexpr int hist_words(int ns) { return (ns + 1) >> 1; }
 
-__host__ __device__ constexpr size_t scatter1_lds(int nb, int ncells) {
-    return sizeof(uint2) * kTile + sizeof(uint32_t) * ((size_t)(ncells + 1) / 2 + 7 * (size_t)nb + kSBlock / 64 + 4);
+__host__ __device__ constexpr size_t scatter1_lds(int nb, int ns) {
+    return sizeof(uint2) * kTile + sizeof(uint32_t) * ((size_t)nb * hist_words(ns) + 6 * (size_t)nb + kSBlock / 64 + 4);
 }
 
 // chunks per pass-1 block: tiles of the busiest block + one open chunk per slice
@@ -168,24 +161,27 @@ __host__ __device__ inline int64_t chunks_per_block(int64_t m, int64_t grid, int
     return ((m + kTile - 1) / kTile + grid - 1) / grid + nt;
 }
 
+__device__ __forceinline__ void hist_add(uint32_t* H, int hw, int b, uint32_t i) {
+    atomicAdd(&H[b * hw + (int)(i >> 1)], 1u << ((i & 1u) * 16u));
+}
+
 __global__ void __launch_bounds__(kSBlock) k_scatter_c(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                        int64_t m, Layout L, int64_t chunk0,
                                                        uint2* __restrict__ pool, unsigned long long* __restrict__ cmeta,
-                                                       unsigned long long* __restrict__ ccount) {
+                                                       uint32_t* __restrict__ chist) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
-    const int nb = L.nt, hw = (L.ncells + 1) >> 1;
+    const int nb = L.nt, hw = hist_words(L.ns);
     uint2* stage = reinterpret_cast<uint2*>(smem);
-    uint32_t* hist = reinterpret_cast<uint32_t*>(stage + kTile);
-    uint32_t* cnt = hist + hw;   // this tile's run length per slice
-    uint32_t* loc = cnt + nb;    // run start in the stage
-    uint32_t* ph = loc + nb;     // open chunk per slice (kNone: none yet)
-    uint32_t* fl = ph + nb;      // its fill
-    uint32_t* p0 = fl + nb;      // this tile's run: first part in chunk p0 from offset f0 ...
-    uint32_t* f0 = p0 + nb;
-    uint32_t* p1 = f0 + nb;      // ... the rest (if any) from the start of chunk p1
-    uint32_t* wtot = p1 + nb;
-    uint32_t* misc = wtot + kSBlock / 64;  // [0] fresh chunks this tile, [1] next free chunk
-    for (int i = threadIdx.x; i < hw; i += kSBlock) hist[i] = 0;
+    uint32_t* H = reinterpret_cast<uint32_t*>(stage + kTile);  // nb rows of hw words: open chunks' cell counts
+    uint32_t* cnt = H + (size_t)nb * hw;  // this tile's run length per slice
+    uint32_t* loc = cnt + nb;             // run start in the stage
+    uint32_t* ph = loc + nb;              // open chunk per slice (kNone: none yet) ...
+    uint32_t* fl = ph + nb;               // ... and its fill, both as of the start of the tile
+    uint32_t* p1 = fl + nb;               // chunk opened by this tile's run (kNone: the run fits)
+    uint32_t* opened = p1 + nb;           // slices that opened a chunk in this tile
+    uint32_t* wtot = opened + nb;
+    uint32_t* misc = wtot + kSBlock / 64;  // [0] chunks opened this tile, [1] next free chunk
+    for (int i = threadIdx.x; i < nb * hw; i += kSBlock) H[i] = 0;
     for (int i = threadIdx.x; i < nb; i += kSBlock) {
         ph[i] = kNone;
         fl[i] = 0;
@@ -218,60 +214,77 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_c(const int64_t* __restrict
         if (t0 + stride < m) load_tile<kSBlock>(src, dst, t0 + stride, m, vec, sr, tr);  // prefetch
 #pragma unroll
         for (int u = 0; u < kItems; ++u)
-            if ((valid >> u) & 1u) {
-                rk[u] = atomicAdd(&cnt[pr[u].y >> kSliceBits], 1u);
-                hist16_inc(hist, ccount, cell_of(L, pr[u].x, pr[u].y));
-            }
+            if ((valid >> u) & 1u) rk[u] = atomicAdd(&cnt[pr[u].y >> kSliceBits], 1u);
         __syncthreads();
         const uint32_t total = block_exclusive_scan<kSBlock>(cnt, loc, nb, wtot);
         const uint32_t nf = misc[1];
-        for (int i = threadIdx.x; i < nb; i += kSBlock) {
+        for (int i = threadIdx.x; i < nb; i += kSBlock) {  // a run that does not fit opens a chunk
             const uint32_t c = cnt[i];
-            if (!c) continue;
-            const uint32_t p = ph[i], f = fl[i];
-            if (p != kNone && f + c <= (uint32_t)kCh) {  // fits the open chunk
-                p0[i] = p;
-                f0[i] = f;
-                fl[i] = f + c;
-                continue;
+            uint32_t np = kNone;
+            if (c && (ph[i] == kNone || fl[i] + c > (uint32_t)kCh)) {
+                const uint32_t k = atomicAdd(&misc[0], 1u);
+                np = nf + k;
+                opened[k] = (uint32_t)i;
             }
-            const uint32_t np = nf + atomicAdd(&misc[0], 1u);
-            if (p == kNone) {
-                p0[i] = np;
-                f0[i] = 0;
-                fl[i] = c;
-            } else {  // fill chunk p, retire it, continue in np
-                p0[i] = p;
-                f0[i] = f;
-                p1[i] = np;
-                fl[i] = f + c - (uint32_t)kCh;
-                cmeta[p] = chunk_meta(i, (uint32_t)kCh);
-            }
-            ph[i] = np;
+            p1[i] = np;
         }
 #pragma unroll
         for (int u = 0; u < kItems; ++u)
             if ((valid >> u) & 1u) stage[loc[pr[u].y >> kSliceBits] + rk[u]] = pr[u];
         __syncthreads();
+        // run item r of slice b: r < room -> open chunk ph[b] at fl[b] + r, else the opened chunk p1[b]
+        for (uint32_t idx = threadIdx.x; idx < total; idx += kSBlock) {
+            const uint2 p = stage[idx];
+            const int b = (int)(p.y >> kSliceBits);
+            const uint32_t r = idx - loc[b], o = ph[b], room = o == kNone ? 0u : (uint32_t)kCh - fl[b];
+            if (r < room) {
+                pool[(size_t)o * kCh + fl[b] + r] = p;
+                hist_add(H, hw, b, p.x >> L.sbits);
+            } else {
+                pool[(size_t)p1[b] * kCh + (r - room)] = p;
+            }
+        }
+        const uint32_t nop = misc[0];
+        if (nop) {  // block-uniform: retire the filled chunks (histogram row out), count the runs' tails
+            __syncthreads();
+            for (uint32_t x = threadIdx.x; x < nop * (uint32_t)hw; x += kSBlock) {
+                const int b = (int)opened[x / hw], w = (int)(x % hw);
+                if (ph[b] != kNone) {
+                    chist[(size_t)ph[b] * hw + w] = H[b * hw + w];
+                    H[b * hw + w] = 0;
+                }
+            }
+            __syncthreads();
+            for (uint32_t k = 0; k < nop; ++k) {
+                const int b = (int)opened[k];
+                const uint32_t room = ph[b] == kNone ? 0u : (uint32_t)kCh - fl[b];
+                for (uint32_t r = room + threadIdx.x; r < cnt[b]; r += kSBlock)
+                    hist_add(H, hw, b, stage[loc[b] + r].x >> L.sbits);
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < nb; i += kSBlock) {  // advance the open chunks
+            const uint32_t c = cnt[i];
+            if (!c) continue;
+            if (p1[i] == kNone) {
+                fl[i] += c;
+            } else {
+                if (ph[i] != kNone) cmeta[ph[i]] = chunk_meta(i, (uint32_t)kCh);
+                fl[i] = ph[i] == kNone ? c : fl[i] + c - (uint32_t)kCh;
+                ph[i] = p1[i];
+            }
+        }
         if (threadIdx.x == 0) {
             misc[1] += misc[0];
             misc[0] = 0;
         }
-        for (uint32_t idx = threadIdx.x; idx < total; idx += kSBlock) {
-            const uint2 p = stage[idx];
-            const int b = (int)(p.y >> kSliceBits);
-            const uint32_t r = idx - loc[b], room = (uint32_t)kCh - f0[b];
-            const size_t o = r < room ? (size_t)p0[b] * kCh + f0[b] + r : (size_t)p1[b] * kCh + (r - room);
-            pool[o] = p;
-        }
-        __syncthreads();
     }
+    __syncthreads();
     for (int i = threadIdx.x; i < nb; i += kSBlock)
         if (ph[i] != kNone) cmeta[ph[i]] = chunk_meta(i, fl[i]);
-    for (int i = threadIdx.x; i < hw; i += kSBlock) {
-        const uint32_t v = hist[i];
-        if (v & 0xFFFFu) atomicAdd(&ccount[2 * i], (unsigned long long)(v & 0xFFFFu));
-        if (v >> 16) atomicAdd(&ccount[2 * i + 1], (unsigned long long)(v >> 16));
+    for (int x = threadIdx.x; x < nb * hw; x += kSBlock) {
+        const uint32_t p = ph[x / hw];
+        if (p != kNone) chist[(size_t)p * hw + x % hw] = H[x];
     }
 }
 
@@ -289,32 +302,118 @@ __global__ void k_chunk_place(const unsigned long long* __restrict__ cmeta, int6
     if (q < nchunks && (cmeta[q] >> 32)) order[atomicAdd(&jcur[(uint32_t)cmeta[q]], 1ULL)] = (uint32_t)q;
 }
 
-// LDS carve-up of pass 2 (and the generic scatter_tile): stage[kTile] | base[nb] (u64) | cnt[nb] | loc[nb] | wtot
-__host__ __device__ constexpr size_t scatter_lds(int nb) {
-    return sizeof(uint2) * kTile + sizeof(unsigned long long) * nb + sizeof(uint32_t) * (2 * nb + kSBlock / 64);
+// ---- pass-2 work split ------------------------------------------------------------------------------
+// Block w of pass 2 takes the used chunks [w * per, (w + 1) * per) of the slice-ordered list
+// (per = ceil(chunks / blocks), read on the device).  Its range meets slices ja(w) .. jb(w); each
+// (block, slice) intersection is a segment, numbered block-major, so the segments of one slice are
+// consecutive.  The exact output start of segment g in cell (j, i) is coff[(j, i)] + the pairs the
+// slice's earlier segments put there (prefix over the per-chunk histograms).
+
+__device__ __forceinline__ int slice_of(const int64_t* jst, int nt, int64_t q) {  // last j with jst[j] <= q
+    int lo = 0, hi = nt;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (jst[mid] <= q) lo = mid; else hi = mid;
+    }
+    return lo;
 }
 
-// Tile body: items (s, t, bucket) are in registers with their rank within the bucket; reserve
-// each bucket's run with one atomic on its cursor, regroup the tile in LDS, write the runs out.
-__device__ __forceinline__ void scatter_tile(const uint2 (&pr)[kItems], uint32_t valid, const uint32_t (&rk)[kItems], int nb,
-                                             unsigned long long* __restrict__ cursor, uint2* __restrict__ out,
-                                             uint2* stage, unsigned long long* base, uint32_t* cnt, uint32_t* loc,
-                                             uint32_t* wtot, int sbits) {
-    for (int i = threadIdx.x; i < nb; i += kSBlock) {
-        const uint32_t c = cnt[i];
-        base[i] = c ? atomicAdd(&cursor[i], (unsigned long long)c) : 0ULL;
+struct SegSplit {
+    int64_t nch, per;
+    __device__ SegSplit(const int64_t* jst, int nt, int64_t blocks) : nch(jst[nt]), per((jst[nt] + blocks - 1) / blocks) {
+        if (per < 1) per = 1;
     }
-    const uint32_t total = block_exclusive_scan<kSBlock>(cnt, loc, nb, wtot);
-#pragma unroll
-    for (int k = 0; k < kItems; ++k)
-        if ((valid >> k) & 1u) stage[loc[pr[k].x >> sbits] + rk[k]] = pr[k];
-    __syncthreads();
-    for (uint32_t idx = threadIdx.x; idx < total; idx += kSBlock) {
-        const uint2 p = stage[idx];
-        const int b = (int)(p.x >> sbits);
-        out[base[b] + (idx - loc[b])] = p;
+};
+
+// segments per block, ja(w)
+__global__ void k_seg_count(const int64_t* __restrict__ jst, int nt, int64_t blocks, int64_t* __restrict__ kseg,
+                            int* __restrict__ ja) {
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= blocks) return;
+    const SegSplit S(jst, nt, blocks);
+    const int64_t q0 = w * S.per, q1 = min(q0 + S.per, S.nch);
+    if (q0 >= q1) {
+        kseg[w] = 0;
+        ja[w] = 0;
+        return;
     }
-    __syncthreads();
+    const int a = slice_of(jst, nt, q0), b = slice_of(jst, nt, q1 - 1);
+    kseg[w] = b - a + 1;
+    ja[w] = a;
+}
+
+struct Seg {
+    int j;
+    int64_t q0, q1;  // chunk range in `order`
+};
+
+__device__ __forceinline__ Seg seg_of(const int64_t* jst, int nt, const SegSplit& S, const int* ja, int64_t w,
+                                      int64_t k) {
+    Seg g;
+    g.j = ja[w] + (int)k;
+    g.q0 = max(w * S.per, jst[g.j]);
+    g.q1 = min(min(w * S.per + S.per, S.nch), jst[g.j + 1]);
+    return g;
+}
+
+__device__ __forceinline__ int64_t block_of_seg(const int64_t* segbase, int64_t blocks, int64_t g) {
+    int64_t lo = 0, hi = blocks;  // last w with segbase[w] <= g
+    while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (segbase[mid] <= g) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// psum[g][i] = pairs of segment g in source slice i (sum of its chunks' histogram rows)
+__global__ void __launch_bounds__(256) k_seg_sum(const uint32_t* __restrict__ chist, const uint32_t* __restrict__ order,
+                                                 const int64_t* __restrict__ jst, int nt, int64_t blocks,
+                                                 const int64_t* __restrict__ segbase, const int* __restrict__ ja,
+                                                 int ns, uint32_t* __restrict__ psum) {
+    __shared__ uint32_t acc[256];
+    const int64_t g = blockIdx.x;
+    if (g >= segbase[blocks]) return;  // grid sized by an upper bound
+    const SegSplit S(jst, nt, blocks);
+    const int64_t w = block_of_seg(segbase, blocks, g);
+    const Seg sg = seg_of(jst, nt, S, ja, w, g - segbase[w]);
+    const int hw = hist_words(ns), rows = 256 / hw;  // hw <= 64
+    const int r = threadIdx.x / hw, x = threadIdx.x % hw;
+    uint32_t lo = 0, hi = 0;
+    if (r < rows)
+        for (int64_t q = sg.q0 + r; q < sg.q1; q += rows) {
+            const uint32_t v = chist[(size_t)order[q] * hw + x];
+            lo += v & 0xFFFFu;
+            hi += v >> 16;
+        }
+    for (int half = 0; half < 2; ++half) {
+        acc[threadIdx.x] = half ? hi : lo;
+        __syncthreads();
+        if (threadIdx.x < hw && 2 * (int)threadIdx.x + half < ns) {
+            uint32_t s = 0;
+            for (int k = 0; k < rows; ++k) s += acc[k * hw + threadIdx.x];
+            psum[(size_t)g * ns + 2 * threadIdx.x + half] = s;
+        }
+        __syncthreads();
+    }
+}
+
+// per cell (j, i): exclusive running sum over slice j's segments (in place) and the cell total
+__global__ void k_seg_prefix(uint32_t* __restrict__ psum, const int64_t* __restrict__ jst, int64_t blocks,
+                             const int64_t* __restrict__ segbase, const int* __restrict__ ja, Layout L,
+                             int64_t* __restrict__ tot) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= L.ncells) return;
+    const int j = c / L.ns, i = c % L.ns;
+    const SegSplit S(jst, L.nt, blocks);
+    int64_t run = 0;
+    if (jst[j + 1] > jst[j])
+        for (int64_t w = jst[j] / S.per; w <= (jst[j + 1] - 1) / S.per; ++w) {
+            const size_t at = (size_t)(segbase[w] + (j - ja[w])) * L.ns + i;
+            const uint32_t v = psum[at];
+            psum[at] = (uint32_t)run;
+            run += v;
+        }
+    tot[c] = run;
 }
 
 struct BitV {
@@ -351,79 +450,108 @@ struct Hop1Out {
     int64_t gwords;
 };
 
-// ---- pass 2: each chunk (one target slice) -> the slice's source cells at exact offsets --------------
-// Block b takes chunks [b * per, (b + 1) * per) of the slice-ordered chunk list.  With HOP1 the
-// block also runs hop 1 on the pairs it moves: M(t) for s != t marked in an LDS copy of the
-// current target slice (flushed through b_ok when the slice changes), self-loops -> S1 / S2.
+// ---- pass 2: block w's segments (chunks of one target slice each) -> the slices' source cells -----
+// Output offsets are exact and precomputed, so the reservation per tile is an LDS cursor bump and the
+// layout is deterministic.  The next chunk is loaded (buffer loads clipped at its fill) while this
+// one is regrouped.  With HOP1 the block also runs hop 1 on the pairs it moves: M(t) for s != t
+// marked in an LDS copy of the current slice (flushed through b_ok when it changes), self-loops
+// -> S1 / S2.
 template <bool HOP1>
 __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict__ pool,
                                                         const unsigned long long* __restrict__ cmeta,
-                                                        const uint32_t* __restrict__ order, int64_t nchunks,
-                                                        int64_t per, Layout L, unsigned long long* __restrict__ cur2,
+                                                        const uint32_t* __restrict__ order,
+                                                        const int64_t* __restrict__ jst,
+                                                        const int64_t* __restrict__ segbase,
+                                                        const int* __restrict__ ja, const uint32_t* __restrict__ prel,
+                                                        const int64_t* __restrict__ coff, Layout L,
                                                         uint2* __restrict__ out, Hop1Out h1) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     const int nb = L.ns;
+    const int64_t w = blockIdx.x, blocks = gridDim.x;
     uint2* stage = reinterpret_cast<uint2*>(smem);
-    unsigned long long* base = smem + kTile;
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(base + nb);
+    unsigned long long* cur = smem + kTile;  // next output index per source cell
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(cur + nb);
     uint32_t* loc = cnt + nb;
     uint32_t* wtot = loc + nb;
     uint32_t* tl = wtot + kSBlock / 64;  // HOP1: target slice marks
-    const int64_t q0 = (int64_t)blockIdx.x * per, q1 = min(q0 + per, nchunks);
-    int cur_j = -1;
-    for (int64_t q = q0; q < q1; ++q) {  // block-uniform
+    const SegSplit S(jst, L.nt, blocks);
+    auto load_chunk = [&](int64_t q, uint2 (&pr)[kItems]) -> uint32_t {
         const uint32_t phys = order[q];
-        const unsigned long long meta = cmeta[phys];
-        const int j = (int)(uint32_t)meta;
-        const uint32_t fill = (uint32_t)(meta >> 32);
-        if (HOP1 && j != cur_j) {
+        const uint32_t fill = (uint32_t)(cmeta[phys] >> 32);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint2*>(pool + (size_t)phys * kCh), (short)0, (int)(fill * sizeof(uint2)), 0x00020000);
+#pragma unroll
+        for (int k = 0; k < kItems / 2; ++k) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(k * kSBlock + (int)threadIdx.x) * 16u, 0, 0);
+            pr[2 * k] = make_uint2(v[0], v[1]);
+            pr[2 * k + 1] = make_uint2(v[2], v[3]);
+        }
+        return fill;
+    };
+    const int64_t qb = w * S.per, qe = min(qb + S.per, S.nch);
+    uint2 nx[kItems];
+    uint32_t nfill = qb < qe ? load_chunk(qb, nx) : 0u;
+    int cur_j = -1;
+    for (int64_t g = segbase[w]; g < segbase[w + 1]; ++g) {  // block-uniform
+        const Seg sg = seg_of(jst, L.nt, S, ja, w, g - segbase[w]);
+        if (sg.q0 >= sg.q1) continue;
+        if (HOP1 && sg.j != cur_j) {
             if (cur_j >= 0) {
                 __syncthreads();
                 flush_slice(tl, h1.M, cur_j, h1.gwords, h1.tmask);
                 __syncthreads();
             }
             for (int k = threadIdx.x; k < kSliceWords; k += kSBlock) tl[k] = 0;
-            cur_j = j;
         }
-        for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
-        __syncthreads();
-        // buffer loads clipped at the chunk's fill: nothing past it is fetched
-        const uint2* cb = pool + (size_t)phys * kCh;
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint2*>(cb), (short)0, (int)(fill * sizeof(uint2)), 0x00020000);
-        uint2 pr[kItems];
-        uint32_t rk[kItems];
-        uint32_t valid = 0;
+        cur_j = sg.j;
+        for (int i = threadIdx.x; i < nb; i += kSBlock)
+            cur[i] = (unsigned long long)(coff[(size_t)sg.j * nb + i] + prel[(size_t)g * nb + i]);
+        const uint32_t tbase = (uint32_t)sg.j << kSliceBits;
+        for (int64_t q = sg.q0; q < sg.q1; ++q) {
+            uint2 pr[kItems];
 #pragma unroll
-        for (int k = 0; k < kItems / 2; ++k) {
-            const uint32_t off = (uint32_t)(k * kSBlock + (int)threadIdx.x) * 16u;
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-            pr[2 * k] = make_uint2(v[0], v[1]);
-            pr[2 * k + 1] = make_uint2(v[2], v[3]);
-        }
+            for (int k = 0; k < kItems; ++k) pr[k] = nx[k];
+            const uint32_t fill = nfill;
+            if (q + 1 < qe) nfill = load_chunk(q + 1, nx);  // prefetch (may be the next segment's)
+            for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
+            __syncthreads();
+            uint32_t rk[kItems];
+            uint32_t valid = 0;
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {
-            valid |= ((uint32_t)item_off<kSBlock>(k) < fill ? 1u : 0u) << k;
-            rk[k] = 0;
-        }
-        const uint32_t tbase = (uint32_t)j << kSliceBits;
+            for (int k = 0; k < kItems; ++k) {
+                valid |= ((uint32_t)item_off<kSBlock>(k) < fill ? 1u : 0u) << k;
+                rk[k] = 0;
+            }
 #pragma unroll
-        for (int k = 0; k < kItems; ++k)
-            if ((valid >> k) & 1u) {
-                rk[k] = atomicAdd(&cnt[pr[k].x >> L.sbits], 1u);
-                if (HOP1) {
-                    const uint32_t s = pr[k].x, t = pr[k].y;
-                    if (s != t) {
-                        lds_set(tl, t - tbase);
-                    } else if (h1.tmask.full || gbit(h1.tmask.w, t)) {  // rare: self-loops
-                        const uint32_t bit = 1u << (t & 31);
-                        const uint32_t old = atomicOr(&h1.S1[t >> 5], bit);
-                        if (old & bit) atomicOr(&h1.S2[t >> 5], bit);
+            for (int k = 0; k < kItems; ++k)
+                if ((valid >> k) & 1u) {
+                    rk[k] = atomicAdd(&cnt[pr[k].x >> L.sbits], 1u);
+                    if (HOP1) {
+                        const uint32_t s = pr[k].x, t = pr[k].y;
+                        if (s != t) {
+                            lds_set(tl, t - tbase);
+                        } else if (h1.tmask.full || gbit(h1.tmask.w, t)) {  // rare: self-loops
+                            const uint32_t bit = 1u << (t & 31);
+                            const uint32_t old = atomicOr(&h1.S1[t >> 5], bit);
+                            if (old & bit) atomicOr(&h1.S2[t >> 5], bit);
+                        }
                     }
                 }
+            __syncthreads();
+            const uint32_t total = block_exclusive_scan<kSBlock>(cnt, loc, nb, wtot);
+#pragma unroll
+            for (int k = 0; k < kItems; ++k)
+                if ((valid >> k) & 1u) stage[loc[pr[k].x >> L.sbits] + rk[k]] = pr[k];
+            __syncthreads();
+            for (uint32_t idx = threadIdx.x; idx < total; idx += kSBlock) {
+                const uint2 v = stage[idx];
+                const int b = (int)(v.x >> L.sbits);
+                out[cur[b] + (idx - loc[b])] = v;
             }
-        __syncthreads();
-        scatter_tile(pr, valid, rk, nb, cur2 + (size_t)j * nb, out, stage, base, cnt, loc, wtot, L.sbits);
+            __syncthreads();
+            for (int i = threadIdx.x; i < nb; i += kSBlock) cur[i] += cnt[i];
+        }
+        __syncthreads();  // cur is re-initialised by the next segment
     }
     if (HOP1 && cur_j >= 0) {
         __syncthreads();
@@ -558,7 +686,7 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
     // (blocks x slices) stay within a few times the filled ones
     std::vector<int> g1(nt, 0);
     std::vector<int64_t> c0(nt, 0);
-    int64_t pool_chunks = 0;
+    int64_t pool_chunks = 0, mtot = 0;
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
         const int64_t full = (ms[i] + kCh - 1) / kCh;
@@ -567,61 +695,75 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
         g1[i] = (int)std::max<int64_t>(1, g);
         c0[i] = pool_chunks;
         pool_chunks += (int64_t)g1[i] * chunks_per_block(ms[i], g1[i], L.nt);
+        mtot += ms[i];
     }
-    REQUIRE(pool_chunks < (int64_t)kNone, CAPSMI_ERR_UNSUPPORTED, "relationship table too large for the layout");
+    REQUIRE(pool_chunks < (int64_t)INT32_MAX && mtot < (int64_t)UINT32_MAX, CAPSMI_ERR_UNSUPPORTED,
+            "relationship table too large for the layout");
     const int64_t npool = pool_chunks > 0 ? pool_chunks : 1;
+    const int hw = hist_words(L.ns);
     Buf pool = dev_alloc(sizeof(uint2) * kCh * (size_t)npool, st);
     Buf meta = dev_alloc(sizeof(unsigned long long) * npool, st);
-    Buf ccount = dev_alloc(sizeof(unsigned long long) * L.ncells, st);
+    Buf chist = dev_alloc(sizeof(uint32_t) * hw * (size_t)npool, st);
     HIP_CHECK(hipMemsetAsync(P<void>(meta), 0, sizeof(unsigned long long) * npool, st));
-    HIP_CHECK(hipMemsetAsync(P<void>(ccount), 0, sizeof(unsigned long long) * L.ncells, st));
-    const size_t lds1 = scatter1_lds(L.nt, L.ncells);
+    const size_t lds1 = scatter1_lds(L.nt, L.ns);
     allow_lds(k_scatter_c, lds1);
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
         KernelTimer kt(s, "part_scatter1");
         hipLaunchKernelGGL(k_scatter_c, dim3(g1[i]), dim3(kSBlock), lds1, st, srcs[i], dsts[i], ms[i], L, c0[i],
-                           P<uint2>(pool), P<unsigned long long>(meta), P<unsigned long long>(ccount));
+                           P<uint2>(pool), P<unsigned long long>(meta), P<uint32_t>(chist));
     }
     HIP_CHECK(hipGetLastError());
-    rp.boff = dev_alloc(sizeof(int64_t) * (L.ncells + 1), st);  // cell offsets
-    exclusive_scan_i64(P<int64_t>(ccount), P<int64_t>(rp.boff), L.ncells, st);
-    // used chunks ordered by target slice
-    Buf jbuf = dev_alloc(sizeof(int64_t) * (2 * (size_t)L.nt + 1) + sizeof(uint32_t) * npool, st);
+
+    // used chunks ordered by target slice; pass-2 segments and the exact output offset of every
+    // (segment, source cell); no host round trip until the layout is written
+    const bool fuse = h1 && h1->a->full;
+    const int64_t g2 = std::max<int64_t>(1, std::min<int64_t>((int64_t)s->num_cus * (fuse ? 1 : 2), npool));
+    const int64_t maxg = g2 + L.nt;  // segments <= blocks + slices
+    Buf jbuf = dev_alloc(sizeof(int64_t) * (3 * (size_t)L.nt + 2 * (size_t)g2 + 3) + sizeof(uint32_t) * npool +
+                             sizeof(int) * g2, st);
     int64_t* jcnt = P<int64_t>(jbuf);
-    int64_t* jcur = jcnt + L.nt;
-    uint32_t* order = reinterpret_cast<uint32_t*>(jcur + L.nt + 1);
+    int64_t* jst = jcnt + L.nt;        // nt + 1
+    int64_t* jcur = jst + L.nt + 1;    // nt
+    int64_t* kseg = jcur + L.nt;       // g2
+    int64_t* segbase = kseg + g2;      // g2 + 1
+    uint32_t* order = reinterpret_cast<uint32_t*>(segbase + g2 + 2);
+    int* ja = reinterpret_cast<int*>(order + npool);
+    Buf pbuf = dev_alloc(sizeof(uint32_t) * (size_t)maxg * L.ns, st);
+    uint32_t* psum = P<uint32_t>(pbuf);
+    Buf tot = dev_alloc(sizeof(int64_t) * L.ncells, st);
     HIP_CHECK(hipMemsetAsync(jcnt, 0, sizeof(int64_t) * L.nt, st));
     const unsigned cg = (unsigned)((npool + 255) / 256);
     hipLaunchKernelGGL(k_chunk_count, dim3(cg), dim3(256), 0, st, P<unsigned long long>(meta), pool_chunks, jcnt);
-    exclusive_scan_i64(jcnt, jcur, L.nt, st);
+    exclusive_scan_i64(jcnt, jst, L.nt, st);
+    HIP_CHECK(hipMemcpyAsync(jcur, jst, sizeof(int64_t) * L.nt, hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(k_chunk_place, dim3(cg), dim3(256), 0, st, P<unsigned long long>(meta), pool_chunks,
                        reinterpret_cast<unsigned long long*>(jcur), order);
-    int64_t host[2] = {0, 0};
-    HIP_CHECK(hipMemcpyAsync(&host[0], P<int64_t>(rp.boff) + L.ncells, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipMemcpyAsync(&host[1], jcur + L.nt, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
-    rp.kept = host[0];
-    const int64_t nchunks = host[1];
-    rp.pairs = dev_alloc(sizeof(uint2) * ((rp.kept > 0 ? rp.kept : 1) + kPad), st);
+    hipLaunchKernelGGL(k_seg_count, dim3((unsigned)((g2 + 255) / 256)), dim3(256), 0, st, jst, L.nt, g2, kseg, ja);
+    exclusive_scan_i64(kseg, segbase, g2, st);
+    hipLaunchKernelGGL(k_seg_sum, dim3((unsigned)maxg), dim3(256), 0, st, P<uint32_t>(chist), order, jst, L.nt, g2,
+                       segbase, ja, L.ns, psum);
+    hipLaunchKernelGGL(k_seg_prefix, dim3((L.ncells + 255) / 256), dim3(256), 0, st, psum, jst, g2, segbase, ja, L,
+                       P<int64_t>(tot));
+    rp.boff = dev_alloc(sizeof(int64_t) * (L.ncells + 1), st);  // cell offsets
+    exclusive_scan_i64(P<int64_t>(tot), P<int64_t>(rp.boff), L.ncells, st);
+    HIP_CHECK(hipGetLastError());
+    rp.pairs = dev_alloc(sizeof(uint2) * (mtot + kPad), st);  // kept <= mtot
 
-    const bool fuse = h1 && h1->a->full;
-    if (rp.kept > 0) {
-        Buf cur2 = dev_alloc(sizeof(int64_t) * L.ncells, st);
-        HIP_CHECK(hipMemcpyAsync(P<void>(cur2), P<void>(rp.boff), sizeof(int64_t) * L.ncells, hipMemcpyDeviceToDevice, st));
-        Hop1Out ho{};
-        if (fuse) ho = Hop1Out{BitV{P<uint32_t>(h1->b->words), h1->b->full ? 1 : 0}, h1->M, h1->S1, h1->S2, h1->b->nwords};
-        const size_t lds2 = scatter_lds(L.ns) + (fuse ? sizeof(uint32_t) * kSliceWords : 0);
-        auto k2 = fuse ? k_scatter_s2<true> : k_scatter_s2<false>;
-        allow_lds(k2, lds2);
-        const int64_t g2 = std::min<int64_t>(nchunks, (int64_t)s->num_cus * (fuse ? 1 : 2));
-        const int64_t per = (nchunks + g2 - 1) / g2;
+    Hop1Out ho{};
+    if (fuse) ho = Hop1Out{BitV{P<uint32_t>(h1->b->words), h1->b->full ? 1 : 0}, h1->M, h1->S1, h1->S2, h1->b->nwords};
+    const size_t lds2 = sizeof(uint2) * kTile + sizeof(unsigned long long) * L.ns +
+                        sizeof(uint32_t) * (2 * L.ns + kSBlock / 64) + (fuse ? sizeof(uint32_t) * kSliceWords : 0);
+    auto k2 = fuse ? k_scatter_s2<true> : k_scatter_s2<false>;
+    allow_lds(k2, lds2);
+    {
         KernelTimer kt(s, fuse ? "part_scatter2_hop1" : "part_scatter2");
-        hipLaunchKernelGGL(k2, dim3((unsigned)((nchunks + per - 1) / per)), dim3(kSBlock), lds2, st, P<uint2>(pool),
-                           P<unsigned long long>(meta), order, nchunks, per, L, P<unsigned long long>(cur2),
-                           P<uint2>(rp.pairs), ho);
-        HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k2, dim3((unsigned)g2), dim3(kSBlock), lds2, st, P<uint2>(pool), P<unsigned long long>(meta),
+                           order, jst, segbase, ja, psum, P<int64_t>(rp.boff), L, P<uint2>(rp.pairs), ho);
     }
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(&rp.kept, P<int64_t>(rp.boff) + L.ncells, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
     if (h1 && !fuse) relpart_hop1(s, rp, h1->a, h1->b, h1->M, h1->S1, h1->S2);
 }
 
