@@ -11,7 +11,8 @@ from ctypes import POINTER, c_char_p, c_int32, c_int64, c_size_t, c_uint32, c_ui
 
 from .expr import CapsmiExpr
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcapsmi.so")
+# CAPSMI_LIB: an alternative build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("CAPSMI_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libcapsmi.so")
 
 OK = 0
 ERR_ILLEGAL_ARGUMENT = 1

@@ -32,6 +32,9 @@ constexpr int kItems = 8;                        // relationships per lane per t
 constexpr int kSBlock = 1024;                    // scatter workgroups
 constexpr int kTile = kSBlock * kItems;          // relationships per scatter tile (8192)
 constexpr int kCh = kTile;                       // pairs per pass-1 chunk: a tile's run spans <= 2 chunks
+constexpr int kP1Block = 1024;                   // pass-1 workgroup (512 x 2 per CU measured slower)
+constexpr int kP1Tile = kP1Block * kItems;       // pass-1 tile (<= kCh)
+static_assert(kP1Tile <= kCh, "a pass-1 run must span at most two chunks");
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr int kUnroll = 8;                       // loads in flight per lane in the hops
 constexpr int64_t kLoadMin = 8192;               // pull a source slice into LDS for >= this many rels
@@ -153,26 +156,26 @@ __device__ __forceinline__ unsigned long long chunk_meta(int j, uint32_t fill) {
 __host__ __device__ constexpr int hist_words(int ns) { return (ns + 1) >> 1; }
 
 __host__ __device__ constexpr size_t scatter1_lds(int nb, int ns) {
-    return sizeof(uint2) * kTile + sizeof(uint32_t) * ((size_t)nb * hist_words(ns) + 6 * (size_t)nb + kSBlock / 64 + 4);
+    return sizeof(uint2) * kP1Tile + sizeof(uint32_t) * ((size_t)nb * hist_words(ns) + 6 * (size_t)nb + kP1Block / 64 + 4);
 }
 
 // chunks per pass-1 block: tiles of the busiest block + one open chunk per slice
 __host__ __device__ inline int64_t chunks_per_block(int64_t m, int64_t grid, int nt) {
-    return ((m + kTile - 1) / kTile + grid - 1) / grid + nt;
+    return ((m + kP1Tile - 1) / kP1Tile + grid - 1) / grid + nt;
 }
 
 __device__ __forceinline__ void hist_add(uint32_t* H, int hw, int b, uint32_t i) {
     atomicAdd(&H[b * hw + (int)(i >> 1)], 1u << ((i & 1u) * 16u));
 }
 
-__global__ void __launch_bounds__(kSBlock) k_scatter_c(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
-                                                       int64_t m, Layout L, int64_t chunk0,
+__global__ void __launch_bounds__(kP1Block) k_scatter_c(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                       int64_t m, Layout L, int64_t chunk0, size_t trash,
                                                        uint2* __restrict__ pool, unsigned long long* __restrict__ cmeta,
                                                        uint32_t* __restrict__ chist) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     const int nb = L.nt, hw = hist_words(L.ns);
     uint2* stage = reinterpret_cast<uint2*>(smem);
-    uint32_t* H = reinterpret_cast<uint32_t*>(stage + kTile);  // nb rows of hw words: open chunks' cell counts
+    uint32_t* H = reinterpret_cast<uint32_t*>(stage + kP1Tile);  // nb rows of hw words: open chunks' cell counts
     uint32_t* cnt = H + (size_t)nb * hw;  // this tile's run length per slice
     uint32_t* loc = cnt + nb;             // run start in the stage
     uint32_t* ph = loc + nb;              // open chunk per slice (kNone: none yet) ...
@@ -180,9 +183,9 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_c(const int64_t* __restrict
     uint32_t* p1 = fl + nb;               // chunk opened by this tile's run (kNone: the run fits)
     uint32_t* opened = p1 + nb;           // slices that opened a chunk in this tile
     uint32_t* wtot = opened + nb;
-    uint32_t* misc = wtot + kSBlock / 64;  // [0] chunks opened this tile, [1] next free chunk
-    for (int i = threadIdx.x; i < nb * hw; i += kSBlock) H[i] = 0;
-    for (int i = threadIdx.x; i < nb; i += kSBlock) {
+    uint32_t* misc = wtot + kP1Block / 64;  // [0] chunks opened this tile, [1] next free chunk
+    for (int i = threadIdx.x; i < nb * hw; i += kP1Block) H[i] = 0;
+    for (int i = threadIdx.x; i < nb; i += kP1Block) {
         ph[i] = kNone;
         fl[i] = 0;
     }
@@ -192,33 +195,33 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_c(const int64_t* __restrict
     }
     const uint64_t range = (uint64_t)(L.hi - L.lo);
     const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
-    const int64_t stride = (int64_t)gridDim.x * kTile;
+    const int64_t stride = (int64_t)gridDim.x * kP1Tile;
     int64_t sr[kItems], tr[kItems];
-    int64_t t0 = (int64_t)blockIdx.x * kTile;
-    if (t0 < m) load_tile<kSBlock>(src, dst, t0, m, vec, sr, tr);
+    int64_t t0 = (int64_t)blockIdx.x * kP1Tile;
+    if (t0 < m) load_tile<kP1Block>(src, dst, t0, m, vec, sr, tr);
     for (; t0 < m; t0 += stride) {  // block-uniform
-        for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
+        for (int i = threadIdx.x; i < nb; i += kP1Block) cnt[i] = 0;
         __syncthreads();
         uint2 pr[kItems];
         uint32_t rk[kItems];
         uint32_t valid = 0;
 #pragma unroll
         for (int u = 0; u < kItems; ++u) {
-            const int64_t e = t0 + item_off<kSBlock>(u);
+            const int64_t e = t0 + item_off<kP1Block>(u);
             const uint64_t s = (uint64_t)(sr[u] - L.lo), t = (uint64_t)(tr[u] - L.lo);
             const bool ok = e < m && s < range && t < range;
             pr[u] = make_uint2((uint32_t)s, (uint32_t)t);
             valid |= (ok ? 1u : 0u) << u;
             rk[u] = 0;
         }
-        if (t0 + stride < m) load_tile<kSBlock>(src, dst, t0 + stride, m, vec, sr, tr);  // prefetch
+        if (t0 + stride < m) load_tile<kP1Block>(src, dst, t0 + stride, m, vec, sr, tr);  // prefetch
 #pragma unroll
         for (int u = 0; u < kItems; ++u)
             if ((valid >> u) & 1u) rk[u] = atomicAdd(&cnt[pr[u].y >> kSliceBits], 1u);
         __syncthreads();
-        const uint32_t total = block_exclusive_scan<kSBlock>(cnt, loc, nb, wtot);
+        const uint32_t total = block_exclusive_scan<kP1Block>(cnt, loc, nb, wtot);
         const uint32_t nf = misc[1];
-        for (int i = threadIdx.x; i < nb; i += kSBlock) {  // a run that does not fit opens a chunk
+        for (int i = threadIdx.x; i < nb; i += kP1Block) {  // a run that does not fit opens a chunk
             const uint32_t c = cnt[i];
             uint32_t np = kNone;
             if (c && (ph[i] == kNone || fl[i] + c > (uint32_t)kCh)) {
@@ -233,21 +236,23 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_c(const int64_t* __restrict
             if ((valid >> u) & 1u) stage[loc[pr[u].y >> kSliceBits] + rk[u]] = pr[u];
         __syncthreads();
         // run item r of slice b: r < room -> open chunk ph[b] at fl[b] + r, else the opened chunk p1[b]
-        for (uint32_t idx = threadIdx.x; idx < total; idx += kSBlock) {
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {  // unconditional stores (idx >= total -> trash chunk)
+            const uint32_t idx = (uint32_t)(k * kP1Block + (int)threadIdx.x);
             const uint2 p = stage[idx];
-            const int b = (int)(p.y >> kSliceBits);
+            const int b = min((int)(p.y >> kSliceBits), nb - 1);  // stale stage entries past `total`
             const uint32_t r = idx - loc[b], o = ph[b], room = o == kNone ? 0u : (uint32_t)kCh - fl[b];
-            if (r < room) {
-                pool[(size_t)o * kCh + fl[b] + r] = p;
-                hist_add(H, hw, b, p.x >> L.sbits);
-            } else {
-                pool[(size_t)p1[b] * kCh + (r - room)] = p;
-            }
+            const bool first = r < room;
+            if (idx < total && first) hist_add(H, hw, b, p.x >> L.sbits);
+            const size_t at = idx >= total ? trash + threadIdx.x
+                            : first       ? (size_t)o * kCh + fl[b] + r
+                                          : (size_t)p1[b] * kCh + (r - room);
+            pool[at] = p;
         }
         const uint32_t nop = misc[0];
         if (nop) {  // block-uniform: retire the filled chunks (histogram row out), count the runs' tails
             __syncthreads();
-            for (uint32_t x = threadIdx.x; x < nop * (uint32_t)hw; x += kSBlock) {
+            for (uint32_t x = threadIdx.x; x < nop * (uint32_t)hw; x += kP1Block) {
                 const int b = (int)opened[x / hw], w = (int)(x % hw);
                 if (ph[b] != kNone) {
                     chist[(size_t)ph[b] * hw + w] = H[b * hw + w];
@@ -258,12 +263,12 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_c(const int64_t* __restrict
             for (uint32_t k = 0; k < nop; ++k) {
                 const int b = (int)opened[k];
                 const uint32_t room = ph[b] == kNone ? 0u : (uint32_t)kCh - fl[b];
-                for (uint32_t r = room + threadIdx.x; r < cnt[b]; r += kSBlock)
+                for (uint32_t r = room + threadIdx.x; r < cnt[b]; r += kP1Block)
                     hist_add(H, hw, b, stage[loc[b] + r].x >> L.sbits);
             }
         }
         __syncthreads();
-        for (int i = threadIdx.x; i < nb; i += kSBlock) {  // advance the open chunks
+        for (int i = threadIdx.x; i < nb; i += kP1Block) {  // advance the open chunks
             const uint32_t c = cnt[i];
             if (!c) continue;
             if (p1[i] == kNone) {
@@ -280,9 +285,9 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_c(const int64_t* __restrict
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < nb; i += kSBlock)
+    for (int i = threadIdx.x; i < nb; i += kP1Block)
         if (ph[i] != kNone) cmeta[ph[i]] = chunk_meta(i, fl[i]);
-    for (int x = threadIdx.x; x < nb * hw; x += kSBlock) {
+    for (int x = threadIdx.x; x < nb * hw; x += kP1Block) {
         const uint32_t p = ph[x / hw];
         if (p != kNone) chist[(size_t)p * hw + x % hw] = H[x];
     }
@@ -464,12 +469,12 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
                                                         const int64_t* __restrict__ segbase,
                                                         const int* __restrict__ ja, const uint32_t* __restrict__ prel,
                                                         const int64_t* __restrict__ coff, Layout L,
-                                                        uint2* __restrict__ out, Hop1Out h1) {
+                                                        uint2* __restrict__ out, int64_t trash, Hop1Out h1) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     const int nb = L.ns;
     const int64_t w = blockIdx.x, blocks = gridDim.x;
     uint2* stage = reinterpret_cast<uint2*>(smem);
-    unsigned long long* cur = smem + kTile;  // next output index per source cell
+    unsigned long long* cur = smem + kTile;  // next output index per source cell, minus the run start
     uint32_t* cnt = reinterpret_cast<uint32_t*>(cur + nb);
     uint32_t* loc = cnt + nb;
     uint32_t* wtot = loc + nb;
@@ -491,67 +496,78 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
     const int64_t qb = w * S.per, qe = min(qb + S.per, S.nch);
     uint2 nx[kItems];
     uint32_t nfill = qb < qe ? load_chunk(qb, nx) : 0u;
+    int64_t g = segbase[w] - 1, seg_end = qb;  // current segment and the end of its chunk range
     int cur_j = -1;
-    for (int64_t g = segbase[w]; g < segbase[w + 1]; ++g) {  // block-uniform
-        const Seg sg = seg_of(jst, L.nt, S, ja, w, g - segbase[w]);
-        if (sg.q0 >= sg.q1) continue;
-        if (HOP1 && sg.j != cur_j) {
-            if (cur_j >= 0) {
+    uint32_t tbase = 0;
+    // One flat loop over the block's chunks, so the only vector-memory operations between a
+    // chunk's prefetch and its use are the kItems stores of the tile before (unconditional, so the
+    // compiler can wait for the loads alone); segment changes are the rare branch.
+    for (int64_t q = qb; q < qe; ++q) {  // block-uniform
+        if (q == seg_end) {
+            Seg sg;
+            do {
+                ++g;
+                sg = seg_of(jst, L.nt, S, ja, w, g - segbase[w]);
+            } while (sg.q0 >= sg.q1);  // skip empty slices
+            seg_end = sg.q1;
+            if (HOP1 && sg.j != cur_j) {
+                if (cur_j >= 0) {
+                    __syncthreads();
+                    flush_slice(tl, h1.M, cur_j, h1.gwords, h1.tmask);
+                }
                 __syncthreads();
-                flush_slice(tl, h1.M, cur_j, h1.gwords, h1.tmask);
-                __syncthreads();
+                for (int k = threadIdx.x; k < kSliceWords; k += kSBlock) tl[k] = 0;
             }
-            for (int k = threadIdx.x; k < kSliceWords; k += kSBlock) tl[k] = 0;
-        }
-        cur_j = sg.j;
-        for (int i = threadIdx.x; i < nb; i += kSBlock)
-            cur[i] = (unsigned long long)(coff[(size_t)sg.j * nb + i] + prel[(size_t)g * nb + i]);
-        const uint32_t tbase = (uint32_t)sg.j << kSliceBits;
-        for (int64_t q = sg.q0; q < sg.q1; ++q) {
-            uint2 pr[kItems];
-#pragma unroll
-            for (int k = 0; k < kItems; ++k) pr[k] = nx[k];
-            const uint32_t fill = nfill;
-            if (q + 1 < qe) nfill = load_chunk(q + 1, nx);  // prefetch (may be the next segment's)
-            for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
+            cur_j = sg.j;
+            tbase = (uint32_t)sg.j << kSliceBits;
             __syncthreads();
-            uint32_t rk[kItems];
-            uint32_t valid = 0;
+            for (int i = threadIdx.x; i < nb; i += kSBlock)
+                cur[i] = (unsigned long long)(coff[(size_t)sg.j * nb + i] + prel[(size_t)g * nb + i]);
+        }
+        uint2 pr[kItems];
 #pragma unroll
-            for (int k = 0; k < kItems; ++k) {
-                valid |= ((uint32_t)item_off<kSBlock>(k) < fill ? 1u : 0u) << k;
-                rk[k] = 0;
-            }
+        for (int k = 0; k < kItems; ++k) pr[k] = nx[k];
+        const uint32_t fill = nfill;
+        if (q + 1 < qe) nfill = load_chunk(q + 1, nx);  // prefetch (may be the next segment's)
+        for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
+        __syncthreads();
+        uint32_t rk[kItems];
+        uint32_t valid = 0;
 #pragma unroll
-            for (int k = 0; k < kItems; ++k)
-                if ((valid >> k) & 1u) {
-                    rk[k] = atomicAdd(&cnt[pr[k].x >> L.sbits], 1u);
-                    if (HOP1) {
-                        const uint32_t s = pr[k].x, t = pr[k].y;
-                        if (s != t) {
-                            lds_set(tl, t - tbase);
-                        } else if (h1.tmask.full || gbit(h1.tmask.w, t)) {  // rare: self-loops
-                            const uint32_t bit = 1u << (t & 31);
-                            const uint32_t old = atomicOr(&h1.S1[t >> 5], bit);
-                            if (old & bit) atomicOr(&h1.S2[t >> 5], bit);
-                        }
+        for (int k = 0; k < kItems; ++k) {
+            valid |= ((uint32_t)item_off<kSBlock>(k) < fill ? 1u : 0u) << k;
+            rk[k] = 0;
+        }
+#pragma unroll
+        for (int k = 0; k < kItems; ++k)
+            if ((valid >> k) & 1u) {
+                rk[k] = atomicAdd(&cnt[pr[k].x >> L.sbits], 1u);
+                if (HOP1) {
+                    const uint32_t s = pr[k].x, t = pr[k].y;
+                    if (s != t) {
+                        lds_set(tl, t - tbase);
+                    } else if (h1.tmask.full || gbit(h1.tmask.w, t)) {  // rare: self-loops
+                        const uint32_t bit = 1u << (t & 31);
+                        const uint32_t old = atomicOr(&h1.S1[t >> 5], bit);
+                        if (old & bit) atomicOr(&h1.S2[t >> 5], bit);
                     }
                 }
-            __syncthreads();
-            const uint32_t total = block_exclusive_scan<kSBlock>(cnt, loc, nb, wtot);
-#pragma unroll
-            for (int k = 0; k < kItems; ++k)
-                if ((valid >> k) & 1u) stage[loc[pr[k].x >> L.sbits] + rk[k]] = pr[k];
-            __syncthreads();
-            for (uint32_t idx = threadIdx.x; idx < total; idx += kSBlock) {
-                const uint2 v = stage[idx];
-                const int b = (int)(v.x >> L.sbits);
-                out[cur[b] + (idx - loc[b])] = v;
             }
-            __syncthreads();
-            for (int i = threadIdx.x; i < nb; i += kSBlock) cur[i] += cnt[i];
+        __syncthreads();
+        const uint32_t total = block_exclusive_scan<kSBlock>(cnt, loc, nb, wtot);
+#pragma unroll
+        for (int k = 0; k < kItems; ++k)
+            if ((valid >> k) & 1u) stage[loc[pr[k].x >> L.sbits] + rk[k]] = pr[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) {  // unconditional stores; idx >= total -> trash slots
+            const uint32_t idx = (uint32_t)(k * kSBlock + (int)threadIdx.x);
+            const uint2 v = stage[idx];
+            const int b = min((int)(v.x >> L.sbits), nb - 1);  // stale stage entries past `total`
+            out[idx < total ? (int64_t)cur[b] + idx - loc[b] : trash + threadIdx.x] = v;
         }
-        __syncthreads();  // cur is re-initialised by the next segment
+        __syncthreads();
+        for (int i = threadIdx.x; i < nb; i += kSBlock) cur[i] += cnt[i];
     }
     if (HOP1 && cur_j >= 0) {
         __syncthreads();
@@ -690,7 +706,8 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
         const int64_t full = (ms[i] + kCh - 1) / kCh;
-        int64_t g = std::min<int64_t>(s->num_cus, (ms[i] + 8 * (int64_t)kTile - 1) / (8 * (int64_t)kTile));
+        int64_t g = std::min<int64_t>((int64_t)s->num_cus * (kSBlock / kP1Block),
+                                      (ms[i] + 8 * (int64_t)kP1Tile - 1) / (8 * (int64_t)kP1Tile));
         g = std::min<int64_t>(g, std::max<int64_t>(1, 8 * full / L.nt));
         g1[i] = (int)std::max<int64_t>(1, g);
         c0[i] = pool_chunks;
@@ -701,7 +718,7 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
             "relationship table too large for the layout");
     const int64_t npool = pool_chunks > 0 ? pool_chunks : 1;
     const int hw = hist_words(L.ns);
-    Buf pool = dev_alloc(sizeof(uint2) * kCh * (size_t)npool, st);
+    Buf pool = dev_alloc(sizeof(uint2) * kCh * (size_t)(npool + 1), st);  // + a trash chunk
     Buf meta = dev_alloc(sizeof(unsigned long long) * npool, st);
     Buf chist = dev_alloc(sizeof(uint32_t) * hw * (size_t)npool, st);
     HIP_CHECK(hipMemsetAsync(P<void>(meta), 0, sizeof(unsigned long long) * npool, st));
@@ -710,7 +727,8 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
         KernelTimer kt(s, "part_scatter1");
-        hipLaunchKernelGGL(k_scatter_c, dim3(g1[i]), dim3(kSBlock), lds1, st, srcs[i], dsts[i], ms[i], L, c0[i],
+        hipLaunchKernelGGL(k_scatter_c, dim3(g1[i]), dim3(kP1Block), lds1, st, srcs[i], dsts[i], ms[i], L, c0[i],
+                           (size_t)npool * kCh,
                            P<uint2>(pool), P<unsigned long long>(meta), P<uint32_t>(chist));
     }
     HIP_CHECK(hipGetLastError());
@@ -759,7 +777,7 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
     {
         KernelTimer kt(s, fuse ? "part_scatter2_hop1" : "part_scatter2");
         hipLaunchKernelGGL(k2, dim3((unsigned)g2), dim3(kSBlock), lds2, st, P<uint2>(pool), P<unsigned long long>(meta),
-                           order, jst, segbase, ja, psum, P<int64_t>(rp.boff), L, P<uint2>(rp.pairs), ho);
+                           order, jst, segbase, ja, psum, P<int64_t>(rp.boff), L, P<uint2>(rp.pairs), mtot, ho);
     }
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipMemcpyAsync(&rp.kept, P<int64_t>(rp.boff) + L.ncells, sizeof(int64_t), hipMemcpyDeviceToHost, st));

@@ -1,7 +1,7 @@
-# SQ counter pass on the partition kernels; usage: bash scripts/run_sq.sh TAG
+# SQ counter pass on the partition / hop kernels; usage: bash scripts/run_sq.sh TAG
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 T=${1:-sq}
-timeout -k 10 400 python3 bench.py --steps 5 --warmup 2 --modes cold,warm --no-cpu-baseline > gpurun_out/${T}_bench.log 2>&1 && echo bench ok > gpurun_out/${T}_status.txt && \
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VALU --kernel-include-regex "k_scatter|k_part_hist|k_hop" -T -f csv -d gpurun_out/${T}_pmc -o run -- python3 bench.py --steps 1 --warmup 0 --modes cold --no-cpu-baseline > gpurun_out/${T}_pmc.log 2>&1 && echo pmc ok >> gpurun_out/${T}_status.txt
+: > gpurun_out/${T}_status.txt
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS --kernel-include-regex "k_scatter|k_hop" -T -f csv -d gpurun_out/${T}_pmc -o run -- python3 bench.py --steps 1 --warmup 0 --modes cold --no-cpu-baseline > gpurun_out/${T}_pmc.log 2>&1 && echo pmc ok >> gpurun_out/${T}_status.txt
