@@ -204,6 +204,96 @@ __global__ void __launch_bounds__(kEfBlock) k_expand_filter(const int64_t* __res
     }
 }
 
+// Fast path when every projected column is the relationship's source or target (no nulls): the
+// kept values are written straight from registers.  Both bitmap tests are random L2/MALL reads,
+// the bound of this kernel; the target test is only issued for rows whose source passed.  Per
+// tile: wave ballots rank the kept rows, a 16-entry LDS scan orders the waves, one global atomic
+// reserves the tile's output run; item-major output order within the tile.
+constexpr int kEpBlock = 512, kEpItems = 8, kEpTile = kEpBlock * kEpItems;  // 2 blocks per CU at 85 VGPRs
+
+template <int NOUT>
+__global__ void __launch_bounds__(kEpBlock) k_expand_pairs(const int64_t* __restrict__ src,
+                                                           const int64_t* __restrict__ dst, int64_t m, int aligned,
+                                                           BitView a, BitView b, uint32_t from_dst,
+                                                           int64_t* __restrict__ o0, int64_t* __restrict__ o1,
+                                                           int64_t* __restrict__ o2, int64_t* __restrict__ o3,
+                                                           unsigned long long* __restrict__ out_count) {
+    __shared__ unsigned int woff[kEpBlock / 64 + 1];
+    __shared__ unsigned long long run;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long lt = lane == 0 ? 0ULL : (~0ULL >> (64 - lane));
+    int64_t* const outs[4] = {o0, o1, o2, o3};
+    const uint64_t ar = (uint64_t)(a.hi - a.lo), br = (uint64_t)(b.hi - b.lo);
+    for (int64_t t0 = (int64_t)blockIdx.x * kEpTile; t0 < m; t0 += (int64_t)gridDim.x * kEpTile) {
+        int64_t s[kEpItems], t[kEpItems];
+        if (aligned && t0 + kEpTile <= m) {
+#pragma unroll
+            for (int k = 0; k < kEpItems / 2; ++k) {
+                const int i = k * kEpBlock + (int)threadIdx.x;
+                const longlong2 sv = reinterpret_cast<const longlong2*>(src + t0)[i];
+                const longlong2 tv = reinterpret_cast<const longlong2*>(dst + t0)[i];
+                s[2 * k] = sv.x; s[2 * k + 1] = sv.y; t[2 * k] = tv.x; t[2 * k + 1] = tv.y;
+            }
+        } else {
+            const int last = (int)(min(m - t0, (int64_t)kEpTile) - 1);
+#pragma unroll
+            for (int u = 0; u < kEpItems; ++u) {
+                const int i = min(2 * ((u >> 1) * kEpBlock + (int)threadIdx.x) + (u & 1), last);
+                s[u] = src[t0 + i];
+                t[u] = dst[t0 + i];
+            }
+        }
+        // source test for all items (loads in flight together), then target test for the survivors
+        bool keep[kEpItems];
+        uint32_t wv[kEpItems];
+#pragma unroll
+        for (int u = 0; u < kEpItems; ++u) {
+            const int off = 2 * ((u >> 1) * kEpBlock + (int)threadIdx.x) + (u & 1);
+            const uint64_t x = (uint64_t)(s[u] - a.lo);
+            keep[u] = t0 + off < m && x < ar;
+            wv[u] = (keep[u] && !a.full) ? a.w[x >> 5] : ~0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kEpItems; ++u) {
+            const uint64_t x = (uint64_t)(s[u] - a.lo), y = (uint64_t)(t[u] - b.lo);
+            keep[u] = keep[u] && ((wv[u] >> (x & 31)) & 1u) && y < br;
+            wv[u] = (keep[u] && !b.full) ? b.w[y >> 5] : ~0u;
+        }
+        unsigned long long bal[kEpItems];
+        unsigned int wcnt = 0;
+#pragma unroll
+        for (int u = 0; u < kEpItems; ++u) {
+            const uint64_t y = (uint64_t)(t[u] - b.lo);
+            keep[u] = keep[u] && ((wv[u] >> (y & 31)) & 1u);
+            bal[u] = __ballot(keep[u]);
+            wcnt += (unsigned int)__popcll(bal[u]);
+        }
+        if (lane == 0) woff[wave] = wcnt;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned int acc = 0;
+            for (int k = 0; k < kEpBlock / 64; ++k) {
+                const unsigned int c = woff[k];
+                woff[k] = acc;
+                acc += c;
+            }
+            run = acc ? atomicAdd(out_count, (unsigned long long)acc) : 0ULL;
+        }
+        __syncthreads();
+        unsigned long long pos = run + woff[wave];
+#pragma unroll
+        for (int u = 0; u < kEpItems; ++u) {
+            if (keep[u]) {
+                const unsigned long long at = pos + __popcll(bal[u] & lt);
+#pragma unroll
+                for (int c = 0; c < NOUT; ++c) outs[c][at] = ((from_dst >> c) & 1u) ? t[u] : s[u];
+            }
+            pos += __popcll(bal[u]);
+        }
+        __syncthreads();  // woff / run reused by the next tile
+    }
+}
+
 // ---- C3: 2-hop count(DISTINCT c) ------------------------------------------------------
 // hop 1: for every rel (s -> t):
 //   s != t, a_ok(s), b_ok(t)           -> M(t)  (b has an in-edge that differs from any r2 leaving b
@@ -503,9 +593,25 @@ void expand_filter(capsmi_session* s, const int64_t* src, const int64_t* dst, in
     const int64_t cap = (int64_t)s->num_cus * 2;
     if (g > cap) g = cap;
     const int al = ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) == 0;
+    // fast path: every projected column is the source or target column, no nulls involved
+    bool pairs = true;
+    uint32_t from_dst = 0;
+    for (int c = 0; c < nout; ++c) {
+        pairs = pairs && (in_d[c] == src || in_d[c] == dst) && !in_v[c] && !out_v[c];
+        if (in_d[c] == dst) from_dst |= 1u << c;
+    }
     KernelTimer kt(s, "expand_filter");
-    hipLaunchKernelGGL(k_expand_filter, dim3((unsigned)g), dim3(kEfBlock), 0, s->stream, src, dst, m, al, view(a),
-                       view(b), oc, (unsigned long long*)dev_count);
+    if (pairs) {
+        auto k = nout == 1 ? k_expand_pairs<1> : nout == 2 ? k_expand_pairs<2> : nout == 3 ? k_expand_pairs<3>
+                                                                                     : k_expand_pairs<4>;
+        const int64_t gp = std::min<int64_t>((m + kEpTile - 1) / kEpTile, (int64_t)s->num_cus * 4);
+        hipLaunchKernelGGL(k, dim3((unsigned)gp), dim3(kEpBlock), 0, s->stream, src, dst, m, al, view(a), view(b),
+                           from_dst, out_d[0], nout > 1 ? out_d[1] : nullptr, nout > 2 ? out_d[2] : nullptr,
+                           nout > 3 ? out_d[3] : nullptr, (unsigned long long*)dev_count);
+    } else {
+        hipLaunchKernelGGL(k_expand_filter, dim3((unsigned)g), dim3(kEfBlock), 0, s->stream, src, dst, m, al, view(a),
+                           view(b), oc, (unsigned long long*)dev_count);
+    }
     HIP_CHECK(hipGetLastError());
 }
 

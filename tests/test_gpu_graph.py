@@ -208,3 +208,37 @@ def test_bitmap_add_scan_stats(session, layout):
     bits, uniq = bm.stats()
     assert bits == len(np.unique(ids))
     assert uniq == (len(np.unique(ids)) == len(ids))
+
+
+@pytest.mark.parametrize("cols", [["target"], ["source", "target"], ["target", "source", "target"],
+                                  ["source", "target", "source", "target"], ["id", "target"]])
+@pytest.mark.parametrize("skip", [0, 1])
+def test_expand_filter_projections(session, cols, skip):
+    """Register-direct fast path (projections of source/target only) and the gathering path (other
+    columns) against numpy, with rels outside the node domain and a misaligned (skipped) view."""
+    from capsmi import ColumnData, I64, graph
+    rng = np.random.default_rng(17 + skip)
+    lo, hi, m = 1000, 1000 + (1 << 16), 300_000
+    src = rng.integers(lo - 500, hi + 500, m).astype(np.int64)
+    dst = rng.integers(lo - 500, hi + 500, m).astype(np.int64)
+    rid = np.arange(m, dtype=np.int64) * 3
+    rels = session.table([ColumnData("id", I64, rid), ColumnData("source", I64, src), ColumnData("target", I64, dst)])
+    if skip:
+        rels = rels.skip(skip)
+        src, dst, rid = src[skip:], dst[skip:], rid[skip:]
+    a_ids = np.nonzero(rng.random(hi - lo) < 0.4)[0] + lo
+    b_ids = np.nonzero(rng.random(hi - lo) < 0.7)[0] + lo
+    ta = session.table([ColumnData("id", I64, a_ids)])
+    tb = session.table([ColumnData("id", I64, b_ids)])
+    a_ok = graph.NodeBitmap(session, lo, hi).add_scan(ta)
+    b_ok = graph.NodeBitmap(session, lo, hi).add_scan(tb)
+    names = [f"c{k}" for k in range(len(cols))]
+    out = graph.expand_filter(session, rels, a_ok, b_ok, cols, names)
+    keep = np.isin(src, a_ids) & np.isin(dst, b_ids)
+    full = {"id": rid, "source": src, "target": dst}
+    want = np.stack([full[c][keep] for c in cols], axis=1)
+    got = np.stack([out.column(nm).values for nm in names], axis=1)
+    assert got.shape == want.shape
+    order_w = np.lexsort(want.T[::-1])
+    order_g = np.lexsort(got.T[::-1])
+    np.testing.assert_array_equal(got[order_g], want[order_w])
