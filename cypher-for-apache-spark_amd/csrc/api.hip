@@ -861,7 +861,9 @@ capsmi_status capsmi_bitmap_add_scan(capsmi_bitmap* b, capsmi_table* nodes, cons
                 std::to_string(b->hi) + ")");
     b->rows_added += h[0];
     b->any_dup = b->any_dup || h[1] > 0;
-    b->set_bits = words_popcount(s, P<uint32_t>(b->words), 0, b->nwords);
+    // every added row either set a fresh bit or was counted as a duplicate (exact, see k_bitmap_add)
+    if (b->set_bits < 0) b->set_bits = words_popcount(s, P<uint32_t>(b->words), 0, b->nwords);
+    b->set_bits += h[0] - h[1];
     b->full = b->set_bits == b->hi - b->lo;
     API_END
 }

@@ -59,52 +59,102 @@ __device__ __forceinline__ void wave_set_bit(uint32_t* w, int64_t x, bool act) {
 }
 
 // ---- node-scan bitmaps ----------------------------------------------------------
-// One lane per scanned node row; lanes hitting the same bitmap word are combined with a
-// segmented OR (and a segmented count, for the duplicate check) so a sorted id column costs
-// one atomic per word, not per row.  Counters are reduced per wave before the atomics.
+// A wave takes 256 consecutive rows (4 per lane, two 16-B loads).  Fast path: no row filter, no
+// nulls, and the wave's ids are one ascending run id0 .. id0+255 inside [lo, hi) -- a base node
+// table -- so 9 lanes OR whole word masks.  Otherwise each of the 4 rows per lane goes through a
+// segmented OR over lanes hitting the same word (one atomic per word run, duplicates counted
+// exactly), which is cheap for clustered ids and correct for any order.  Counters are reduced
+// per block before one atomic each.
+__device__ __forceinline__ void bitmap_generic(uint32_t* w, int64_t lo, int64_t hi, int64_t id, bool act, bool valid,
+                                               unsigned long long& added, unsigned long long& dups,
+                                               unsigned long long& bad) {
+    const int lane = threadIdx.x & 63;
+    int64_t x = 0;
+    if (act) {
+        if (!valid || id < lo || id >= hi) {
+            ++bad;
+            act = false;
+        } else {
+            x = id - lo;
+        }
+    }
+    int64_t word = act ? (x >> 5) : -1;
+    uint32_t m = act ? (1u << (x & 31)) : 0u;
+    uint32_t cnt = act ? 1u : 0u;
+    // segmented suffix reduction over runs of equal `word` in adjacent lanes: `tail` marks
+    // that the lane's current window [lane, lane+o) already contains the end of its run
+    const int64_t next = __shfl_down(word, 1, 64);
+    bool tail = lane == 63 || next != word;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t mo = __shfl_down(m, o, 64);
+        const uint32_t co = __shfl_down(cnt, o, 64);
+        const bool to = __shfl_down((int)tail, o, 64) != 0;
+        if (!tail) {
+            m |= mo;
+            cnt += co;
+            tail = to;
+        }
+    }
+    const int64_t prev = __shfl_up(word, 1, 64);
+    if (act && (lane == 0 || prev != word)) {
+        const uint32_t old = atomicOr(&w[word], m);
+        added += cnt;
+        dups += (cnt - (uint32_t)__popc(m)) + (uint32_t)__popc(old & m);
+    }
+}
+
 __global__ void __launch_bounds__(256) k_bitmap_add(uint32_t* w, int64_t lo, int64_t hi, const int64_t* __restrict__ ids,
                                                     const uint8_t* __restrict__ ids_valid,
-                                                    const uint8_t* __restrict__ flags, int64_t n,
+                                                    const uint8_t* __restrict__ flags, int64_t n, int aligned,
                                                     unsigned long long* counters /* [0]=added, [1]=dups, [2]=bad */) {
-    const int lane = threadIdx.x & 63;
+    __shared__ unsigned long long red[3][4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned long long added = 0, dups = 0, bad = 0;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t base = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); base < n; base += stride) {
-        const int64_t i = base + lane;
-        bool act = i < n && (!flags || flags[i]);
-        int64_t x = 0;
-        if (act) {
-            const int64_t id = ids[i];
-            if ((ids_valid && !ids_valid[i]) || id < lo || id >= hi) {
-                ++bad;
-                act = false;
-            } else {
-                x = id - lo;
-            }
-        }
-        int64_t word = act ? (x >> 5) : -1;
-        uint32_t m = act ? (1u << (x & 31)) : 0u;
-        uint32_t cnt = act ? 1u : 0u;
-        // segmented suffix reduction over runs of equal `word` in adjacent lanes: `tail` marks
-        // that the lane's current window [lane, lane+o) already contains the end of its run
-        const int64_t next = __shfl_down(word, 1, 64);
-        bool tail = lane == 63 || next != word;
+    const int64_t stride = (int64_t)gridDim.x * 1024;
+    for (int64_t base = (int64_t)blockIdx.x * 1024 + wave * 256; base < n; base += stride) {
+        // row base + 128 * k + 2 * lane + j  (k, j in {0, 1}): two coalesced 16-B loads per lane
+        int64_t id[4];
+        const bool whole = aligned && base + 256 <= n;
+        if (whole) {
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t mo = __shfl_down(m, o, 64);
-            const uint32_t co = __shfl_down(cnt, o, 64);
-            const bool to = __shfl_down((int)tail, o, 64) != 0;
-            if (!tail) {
-                m |= mo;
-                cnt += co;
-                tail = to;
+            for (int k = 0; k < 2; ++k) {
+                const longlong2 v = reinterpret_cast<const longlong2*>(ids + base + 128 * k)[lane];
+                id[2 * k] = v.x;
+                id[2 * k + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int64_t i = base + 128 * (u >> 1) + 2 * lane + (u & 1);
+                id[u] = i < n ? ids[i] : 0;
             }
         }
-        const int64_t prev = __shfl_up(word, 1, 64);
-        if (act && (lane == 0 || prev != word)) {
-            const uint32_t old = atomicOr(&w[word], m);
-            added += cnt;
-            dups += (cnt - (uint32_t)__popc(m)) + (uint32_t)__popc(old & m);
+        const int64_t id0 = __shfl(id[0], 0, 64);
+        bool run = whole && !flags && !ids_valid && id0 >= lo && id0 + 256 <= hi;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) run = run && id[u] == id0 + 128 * (u >> 1) + 2 * lane + (u & 1);
+        if (__ballot(!run) == 0) {  // wave-uniform: one ascending run of 256 ids
+            const int64_t x0 = id0 - lo, w0 = x0 >> 5;
+            const int64_t k = lane;  // word w0 + k covers bits [32 (w0 + k), 32 (w0 + k + 1)) - x0 of the run
+            if (k <= 8) {
+                const int64_t b0 = (w0 + k) * 32 - x0;  // run offset of the word's bit 0
+                const int64_t s = b0 < 0 ? 0 : b0, t = b0 + 32 > 256 ? 256 : b0 + 32;
+                if (t > s) {
+                    const uint32_t m = (uint32_t)((((t - s) == 32) ? 0xFFFFFFFFull : ((1ull << (t - s)) - 1)) << (s - b0));
+                    const uint32_t old = atomicOr(&w[w0 + k], m);
+                    dups += (uint32_t)__popc(old & m);
+                }
+            }
+            if (lane == 0) added += 256;
+            continue;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = base + 128 * (u >> 1) + 2 * lane + (u & 1);
+            const bool act = i < n && (!flags || flags[i]);
+            const bool valid = act && (!ids_valid || ids_valid[i]);
+            bitmap_generic(w, lo, hi, id[u], act, valid, added, dups, bad);
         }
     }
 #pragma unroll
@@ -114,19 +164,45 @@ __global__ void __launch_bounds__(256) k_bitmap_add(uint32_t* w, int64_t lo, int
         bad += __shfl_down(bad, o, 64);
     }
     if (lane == 0) {
-        if (added) atomicAdd(&counters[0], added);
-        if (dups) atomicAdd(&counters[1], dups);
-        if (bad) atomicAdd(&counters[2], bad);
+        red[0][wave] = added;
+        red[1][wave] = dups;
+        red[2][wave] = bad;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const unsigned long long v = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
+        if (v) atomicAdd(&counters[threadIdx.x], v);
     }
 }
 
-__global__ void k_popcount(const uint32_t* __restrict__ w, int64_t b, int64_t e, unsigned long long* out) {
+// popcount of words [b, e): 16-B loads where aligned, block reduction, one atomic per block
+__global__ void __launch_bounds__(256) k_popcount(const uint32_t* __restrict__ w, int64_t b, int64_t e,
+                                                  unsigned long long* out) {
+    __shared__ unsigned long long red[4];
     unsigned long long c = 0;
-    for (int64_t i = b + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < e; i += (int64_t)gridDim.x * blockDim.x)
-        c += __popc(w[i]);
-    // wave reduce, one atomic per wave
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = b + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t a = (b + 3) & ~int64_t(3);  // first 16-B aligned word
+    if (a <= e) {
+        for (int64_t k = b + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a; k += stride) c += __popc(w[k]);
+        const int64_t nq = (e - a) >> 2;
+        const uint4* q = reinterpret_cast<const uint4*>(w + a);
+        for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nq; k += stride) {
+            const uint4 v = q[k];
+            c += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+        }
+        for (int64_t k = a + 4 * nq + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < e; k += stride) c += __popc(w[k]);
+    } else {
+        for (; i < e; i += stride) c += __popc(w[i]);
+    }
+#pragma unroll
     for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long t = red[0] + red[1] + red[2] + red[3];
+        if (t) atomicAdd(out, t);
+    }
 }
 
 // ---- C2: 1-hop expand with fused node filters --------------------------------------
@@ -542,8 +618,11 @@ void bitmap_add_rows(capsmi_bitmap* b, const int64_t* ids, const uint8_t* ids_va
                      int64_t* dev_counters) {
     if (n <= 0) return;
     KernelTimer kt(b->sess, "bitmap_add");
-    hipLaunchKernelGGL(k_bitmap_add, dim3(grid_cap(n, 4096)), dim3(256), 0, b->sess->stream, P<uint32_t>(b->words),
-                       b->lo, b->hi, ids, ids_valid, flags, n, (unsigned long long*)dev_counters);
+    const int aligned = (((uintptr_t)ids) & 15) == 0;
+    const int64_t g = std::min<int64_t>((n + 1023) / 1024, (int64_t)b->sess->num_cus * 8);
+    hipLaunchKernelGGL(k_bitmap_add, dim3((unsigned)std::max<int64_t>(g, 1)), dim3(256), 0, b->sess->stream,
+                       P<uint32_t>(b->words), b->lo, b->hi, ids, ids_valid, flags, n, aligned,
+                       (unsigned long long*)dev_counters);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -551,7 +630,8 @@ int64_t words_popcount(capsmi_session* s, const uint32_t* w, int64_t w_begin, in
     Buf out = dev_alloc(8, s->stream);
     HIP_CHECK(hipMemsetAsync(P<void>(out), 0, 8, s->stream));
     if (w_end > w_begin)
-        hipLaunchKernelGGL(k_popcount, dim3(grid_cap(w_end - w_begin, 2048)), dim3(256), 0, s->stream, w, w_begin, w_end,
+        hipLaunchKernelGGL(k_popcount, dim3(grid_cap((w_end - w_begin + 3) / 4, (int64_t)s->num_cus * 4)), dim3(256), 0,
+                           s->stream, w, w_begin, w_end,
                            P<unsigned long long>(out));
     HIP_CHECK(hipGetLastError());
     return read_scalar(s, P<int64_t>(out));

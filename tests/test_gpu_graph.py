@@ -242,3 +242,44 @@ def test_expand_filter_projections(session, cols, skip):
     order_w = np.lexsort(want.T[::-1])
     order_g = np.lexsort(got.T[::-1])
     np.testing.assert_array_equal(got[order_g], want[order_w])
+
+
+@pytest.mark.parametrize("case", ["runs", "runs_overlap", "mixed", "skipped_view", "unaligned_runs"])
+def test_bitmap_add_scan_bits(session, case):
+    """The ascending-run fast path (256 consecutive ids per wave) and the generic path set exactly the
+    scanned ids, across several scans into one bitmap; membership read back through expand_filter."""
+    from capsmi import ColumnData, I64, graph
+    rng = np.random.default_rng(23)
+    lo, hi = 77, 77 + 20000
+    if case == "runs":
+        scans = [np.arange(lo + 5, lo + 9000), np.arange(lo + 12001, hi)]
+    elif case == "runs_overlap":
+        scans = [np.arange(lo + 3, lo + 4000), np.arange(lo + 3900, lo + 7777), np.arange(lo + 100, lo + 400)]
+    elif case == "mixed":
+        a = np.arange(lo + 31, lo + 10000)
+        a[4000:4300] = rng.integers(lo, hi, 300)  # breaks some waves' runs
+        scans = [a, rng.integers(lo, hi, 999)]
+    elif case == "unaligned_runs":
+        scans = [np.arange(lo + 1, lo + 300), np.arange(lo + 300, lo + 301), np.arange(lo + 301, lo + 9999)]
+    else:
+        scans = [np.arange(lo, lo + 7001)]
+    bm = graph.NodeBitmap(session, lo, hi)
+    for k, ids in enumerate(scans):
+        t = session.table([ColumnData("id", I64, ids.astype(np.int64))])
+        if case == "skipped_view":
+            t = t.skip(3)  # misaligned 16-B loads -> generic loads
+            ids = ids[3:]
+        bm.add_scan(t)
+    allids = np.unique(np.concatenate([s[3:] if case == "skipped_view" else s for s in scans]))
+    total = sum(len(s) - (3 if case == "skipped_view" else 0) for s in scans)
+    bits, uniq = bm.stats()
+    assert bits == len(allids)
+    assert uniq == (len(allids) == total)
+    if not uniq:  # the fused expand refuses scans with repeated ids (ScanGraph.scala:72-76)
+        return
+    dom = np.arange(lo, hi, dtype=np.int64)
+    rels = session.table([ColumnData("id", I64, dom), ColumnData("source", I64, dom),
+                          ColumnData("target", I64, np.full(len(dom), lo, np.int64))])
+    everyone = graph.NodeBitmap(session, lo, hi).add_scan(session.table([ColumnData("id", I64, dom)]))
+    out = graph.expand_filter(session, rels, bm, everyone, ["source"], ["s"])
+    np.testing.assert_array_equal(np.sort(out.column("s").values), allids)
