@@ -371,17 +371,17 @@ __device__ __forceinline__ int64_t block_of_seg(const int64_t* segbase, int64_t 
 }
 
 // psum[g][i] = pairs of segment g in source slice i (sum of its chunks' histogram rows)
-__global__ void __launch_bounds__(256) k_seg_sum(const uint32_t* __restrict__ chist, const uint32_t* __restrict__ order,
+__global__ void __launch_bounds__(1024) k_seg_sum(const uint32_t* __restrict__ chist, const uint32_t* __restrict__ order,
                                                  const int64_t* __restrict__ jst, int nt, int64_t blocks,
                                                  const int64_t* __restrict__ segbase, const int* __restrict__ ja,
                                                  int ns, uint32_t* __restrict__ psum) {
-    __shared__ uint32_t acc[256];
+    __shared__ uint32_t acc[1024];
     const int64_t g = blockIdx.x;
     if (g >= segbase[blocks]) return;  // grid sized by an upper bound
     const SegSplit S(jst, nt, blocks);
     const int64_t w = block_of_seg(segbase, blocks, g);
     const Seg sg = seg_of(jst, nt, S, ja, w, g - segbase[w]);
-    const int hw = hist_words(ns), rows = 256 / hw;  // hw <= 64
+    const int hw = hist_words(ns), rows = 1024 / hw;  // hw <= 64
     const int r = threadIdx.x / hw, x = threadIdx.x % hw;
     uint32_t lo = 0, hi = 0;
     if (r < rows)
@@ -759,7 +759,7 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
                        reinterpret_cast<unsigned long long*>(jcur), order);
     hipLaunchKernelGGL(k_seg_count, dim3((unsigned)((g2 + 255) / 256)), dim3(256), 0, st, jst, L.nt, g2, kseg, ja);
     exclusive_scan_i64(kseg, segbase, g2, st);
-    hipLaunchKernelGGL(k_seg_sum, dim3((unsigned)maxg), dim3(256), 0, st, P<uint32_t>(chist), order, jst, L.nt, g2,
+    hipLaunchKernelGGL(k_seg_sum, dim3((unsigned)maxg), dim3(1024), 0, st, P<uint32_t>(chist), order, jst, L.nt, g2,
                        segbase, ja, L.ns, psum);
     hipLaunchKernelGGL(k_seg_prefix, dim3((L.ncells + 255) / 256), dim3(256), 0, st, psum, jst, g2, segbase, ja, L,
                        P<int64_t>(tot));
