@@ -322,7 +322,7 @@ def run_single(args):
         out = graph.var_length_count(sess, [rels], ok, ok, 1, 3)
         return None, out
 
-    kernels = ("bitmap_add", "expand_filter", "tri_pack", "triangles", "varlen_deg", "varlen_w", "varlen_rev",
+    kernels = ("bitmap_add", "expand_filter", "tri_pack", "triangles", "part_scatter1", "varlen_deg", "varlen_w", "varlen_rev",
                "varlen_t")
     for _ in range(args.warmup):
         step()
@@ -348,7 +348,7 @@ def run_single(args):
     matched = res
     # algorithmic bytes per launch of the kernels whose traffic is a plain function of the input
     alg = {"bitmap_add": n * 8, "expand_filter": m * 16 + (2 * res * 8 if wl == "c2" else 0),
-           "tri_pack": m * 24, "varlen_deg": m * 8, "varlen_w": m * 16, "varlen_rev": m * 16, "varlen_t": m * 16}
+           "tri_pack": m * 24, "part_scatter1": m * 24, "varlen_deg": m * 8, "varlen_w": m * 8, "varlen_t": m * 8}
     dom = max(kt, key=lambda k: kt[k][1])
     avg_ms = kt[dom][1] / kt[dom][0]
     b_alg = {"c2": 16 * m + int(0.75 * n) * 24 + 16 * (res or 0), "c4": 3 * 24 * m + 3 * 8 * n,

@@ -205,6 +205,7 @@ struct PartLayout {
     int ns;          // source slices of 2^sbits ids
     int sbits;       // 19 while nt * ns <= 16384, coarser for larger domains
     int ncells;      // nt * ns, j-major (target slice major)
+    int tbits;       // target slice = 2^tbits ids (19 for the 2-hop layout)
 };
 struct RelPart {
     PartLayout L;

@@ -17,125 +17,11 @@
 // target slices as packed uint32 pairs, pass 2 scatters each target slice into its source cells.
 // Both scatters stage an 8192-relationship tile in LDS grouped by bucket, so the HBM writes are
 // runs of whole cache lines rather than 8-byte scatters.
-#include "capsmi_impl.h"
+#include "part_common.h"
 
 namespace capsmi {
 
 namespace part {
-
-constexpr int kSliceBits = 19;                   // 2^19 ids per slice = 64 KiB of LDS bitmap
-constexpr int kSliceWords = 1 << (kSliceBits - 5);
-constexpr int kMaxCells = 16384;                 // cell histogram = 32 KiB of 16-bit LDS counters
-constexpr int kMaxTSlices = 2048;                // domain <= 2^30 ids (pass-1 LDS: 7 words per slice)
-constexpr int kBlock = 1024;                     // hop workgroups
-constexpr int kItems = 8;                        // relationships per lane per tile
-constexpr int kSBlock = 1024;                    // scatter workgroups
-constexpr int kTile = kSBlock * kItems;          // relationships per scatter tile (8192)
-constexpr int kCh = kTile;                       // pairs per pass-1 chunk: a tile's run spans <= 2 chunks
-constexpr int kP1Block = 1024;                   // pass-1 workgroup (512 x 2 per CU measured slower)
-constexpr int kP1Tile = kP1Block * kItems;       // pass-1 tile (<= kCh)
-static_assert(kP1Tile <= kCh, "a pass-1 run must span at most two chunks");
-constexpr uint32_t kNone = 0xFFFFFFFFu;
-constexpr int kUnroll = 8;                       // loads in flight per lane in the hops
-constexpr int64_t kLoadMin = 8192;               // pull a source slice into LDS for >= this many rels
-constexpr int kPad = 2 * 8192;                   // slack pairs after every pair array (load_pairs)
-
-using Layout = PartLayout;
-
-// Exclusive scan of in[0..n) into out[0..n) by a B-lane block; returns the total.
-// `wtot` is B/64 words of LDS scratch.  Contains barriers: call from block-uniform code.
-template <int B>
-__device__ uint32_t block_exclusive_scan(const uint32_t* in, uint32_t* out, int n, uint32_t* wtot) {
-    const int per = (n + B - 1) / B;
-    const int b = threadIdx.x * per;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t sum = 0;
-    for (int k = 0; k < per; ++k)
-        if (b + k < n) sum += in[b + k];
-    uint32_t x = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wtot[wave] = x;
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        uint32_t v = lane < B / 64 ? wtot[lane] : 0u;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(v, o, 64);
-            if (lane >= o) v += y;
-        }
-        if (lane < B / 64) wtot[lane] = v;
-    }
-    __syncthreads();
-    uint32_t pre = x - sum + (wave > 0 ? wtot[wave - 1] : 0u);
-    for (int k = 0; k < per; ++k)
-        if (b + k < n) {
-            const uint32_t c = in[b + k];
-            out[b + k] = pre;
-            pre += c;
-        }
-    const uint32_t total = wtot[B / 64 - 1];
-    __syncthreads();
-    return total;
-}
-
-__device__ __forceinline__ int cell_of(const Layout& L, uint32_t s, uint32_t t) {
-    return (int)(t >> kSliceBits) * L.ns + (int)(s >> L.sbits);
-}
-
-// Tile item u of this lane is relationship t0 + item_off<B>(u): lanes read 16-byte pairs of
-// consecutive relationships (2 int64 per load, the calibrated streaming width), pair k of the
-// tile at offset 2 * (k * B + lane).
-template <int B>
-__device__ __forceinline__ int item_off(int u) {
-    return 2 * ((u >> 1) * B + (int)threadIdx.x) + (u & 1);
-}
-
-// Issue all of a tile's loads before any test: with a branch around each load the compiler
-// waits for every load before issuing the next.  `vec` = both columns 16-byte aligned.
-template <int B>
-__device__ __forceinline__ void load_tile(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t t0,
-                                          int64_t m, bool vec, int64_t (&sr)[kItems], int64_t (&tr)[kItems]) {
-    const int64_t* __restrict__ sp = src + t0;  // wave-uniform bases, 32-bit lane offsets
-    const int64_t* __restrict__ dp = dst + t0;
-    if (vec && t0 + B * kItems <= m) {
-        const longlong2* __restrict__ sv = reinterpret_cast<const longlong2*>(sp);
-        const longlong2* __restrict__ dv = reinterpret_cast<const longlong2*>(dp);
-#pragma unroll
-        for (int k = 0; k < kItems / 2; ++k) {
-            const longlong2 a = sv[k * B + (int)threadIdx.x], b = dv[k * B + (int)threadIdx.x];
-            sr[2 * k] = a.x;
-            sr[2 * k + 1] = a.y;
-            tr[2 * k] = b.x;
-            tr[2 * k + 1] = b.y;
-        }
-    } else {
-        const int last = (int)(min(m - t0, (int64_t)B * kItems) - 1);
-#pragma unroll
-        for (int u = 0; u < kItems; ++u) {
-            const int i = min(item_off<B>(u), last);
-            sr[u] = sp[i];
-            tr[u] = dp[i];
-        }
-    }
-}
-
-// The B * N pairs of a packed uint2 array starting at the even, wave-uniform index b, as 16-byte
-// loads: this lane's item u is b + item_off<B>(u).  Pair arrays are allocated with kPad pairs of
-// slack so a tile may run past the last pair; callers mask items outside their range.
-template <int B, int N>
-__device__ __forceinline__ void load_pairs(const uint2* __restrict__ in, int64_t b, uint2 (&p)[N]) {
-    const uint4* __restrict__ v = reinterpret_cast<const uint4*>(in + b);
-#pragma unroll
-    for (int k = 0; k < N / 2; ++k) {
-        const uint4 x = v[k * B + (int)threadIdx.x];
-        p[2 * k] = make_uint2(x.x, x.y);
-        p[2 * k + 1] = make_uint2(x.z, x.w);
-    }
-}
 
 // ---- pass 1: int64 (source, target) -> packed pairs in per-workgroup chunks of one target slice ------
 //
@@ -148,12 +34,7 @@ __device__ __forceinline__ void load_pairs(const uint2* __restrict__ in, int64_t
 // histogram when it is retired; pass 2 derives exact output offsets from those.  The next tile's
 // loads are issued before this tile is regrouped and written.
 
-__device__ __forceinline__ unsigned long long chunk_meta(int j, uint32_t fill) {
-    return (unsigned long long)(uint32_t)j | ((unsigned long long)fill << 32);
-}
 
-// per-chunk histogram row: ns 16-bit counters padded to an even count (whole 32-bit words)
-__host__ __device__ constexpr int hist_words(int ns) { return (ns + 1) >> 1; }
 
 __host__ __device__ constexpr size_t scatter1_lds(int nb, int ns) {
     return sizeof(uint2) * kP1Tile + sizeof(uint32_t) * ((size_t)nb * hist_words(ns) + 6 * (size_t)nb + kP1Block / 64 + 4);
@@ -169,7 +50,7 @@ __device__ __forceinline__ void hist_add(uint32_t* H, int hw, int b, uint32_t i)
 }
 
 __global__ void __launch_bounds__(kP1Block) k_scatter_c(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
-                                                       int64_t m, Layout L, int64_t chunk0, size_t trash,
+                                                       int64_t m, Layout L, int swap, int64_t chunk0, size_t trash,
                                                        uint2* __restrict__ pool, unsigned long long* __restrict__ cmeta,
                                                        uint32_t* __restrict__ chist) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
@@ -210,14 +91,14 @@ __global__ void __launch_bounds__(kP1Block) k_scatter_c(const int64_t* __restric
             const int64_t e = t0 + item_off<kP1Block>(u);
             const uint64_t s = (uint64_t)(sr[u] - L.lo), t = (uint64_t)(tr[u] - L.lo);
             const bool ok = e < m && s < range && t < range;
-            pr[u] = make_uint2((uint32_t)s, (uint32_t)t);
+            pr[u] = swap ? make_uint2((uint32_t)t, (uint32_t)s) : make_uint2((uint32_t)s, (uint32_t)t);
             valid |= (ok ? 1u : 0u) << u;
             rk[u] = 0;
         }
         if (t0 + stride < m) load_tile<kP1Block>(src, dst, t0 + stride, m, vec, sr, tr);  // prefetch
 #pragma unroll
         for (int u = 0; u < kItems; ++u)
-            if ((valid >> u) & 1u) rk[u] = atomicAdd(&cnt[pr[u].y >> kSliceBits], 1u);
+            if ((valid >> u) & 1u) rk[u] = atomicAdd(&cnt[pr[u].y >> L.tbits], 1u);
         __syncthreads();
         const uint32_t total = block_exclusive_scan<kP1Block>(cnt, loc, nb, wtot);
         const uint32_t nf = misc[1];
@@ -233,14 +114,14 @@ __global__ void __launch_bounds__(kP1Block) k_scatter_c(const int64_t* __restric
         }
 #pragma unroll
         for (int u = 0; u < kItems; ++u)
-            if ((valid >> u) & 1u) stage[loc[pr[u].y >> kSliceBits] + rk[u]] = pr[u];
+            if ((valid >> u) & 1u) stage[loc[pr[u].y >> L.tbits] + rk[u]] = pr[u];
         __syncthreads();
         // run item r of slice b: r < room -> open chunk ph[b] at fl[b] + r, else the opened chunk p1[b]
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {  // unconditional stores (idx >= total -> trash chunk)
             const uint32_t idx = (uint32_t)(k * kP1Block + (int)threadIdx.x);
             const uint2 p = stage[idx];
-            const int b = min((int)(p.y >> kSliceBits), nb - 1);  // stale stage entries past `total`
+            const int b = min((int)(p.y >> L.tbits), nb - 1);  // stale stage entries past `total`
             const uint32_t r = idx - loc[b], o = ph[b], room = o == kNone ? 0u : (uint32_t)kCh - fl[b];
             const bool first = r < room;
             if (idx < total && first) hist_add(H, hw, b, p.x >> L.sbits);
@@ -307,29 +188,6 @@ __global__ void k_chunk_place(const unsigned long long* __restrict__ cmeta, int6
     if (q < nchunks && (cmeta[q] >> 32)) order[atomicAdd(&jcur[(uint32_t)cmeta[q]], 1ULL)] = (uint32_t)q;
 }
 
-// ---- pass-2 work split ------------------------------------------------------------------------------
-// Block w of pass 2 takes the used chunks [w * per, (w + 1) * per) of the slice-ordered list
-// (per = ceil(chunks / blocks), read on the device).  Its range meets slices ja(w) .. jb(w); each
-// (block, slice) intersection is a segment, numbered block-major, so the segments of one slice are
-// consecutive.  The exact output start of segment g in cell (j, i) is coff[(j, i)] + the pairs the
-// slice's earlier segments put there (prefix over the per-chunk histograms).
-
-__device__ __forceinline__ int slice_of(const int64_t* jst, int nt, int64_t q) {  // last j with jst[j] <= q
-    int lo = 0, hi = nt;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (jst[mid] <= q) lo = mid; else hi = mid;
-    }
-    return lo;
-}
-
-struct SegSplit {
-    int64_t nch, per;
-    __device__ SegSplit(const int64_t* jst, int nt, int64_t blocks) : nch(jst[nt]), per((jst[nt] + blocks - 1) / blocks) {
-        if (per < 1) per = 1;
-    }
-};
-
 // segments per block, ja(w)
 __global__ void k_seg_count(const int64_t* __restrict__ jst, int nt, int64_t blocks, int64_t* __restrict__ kseg,
                             int* __restrict__ ja) {
@@ -345,29 +203,6 @@ __global__ void k_seg_count(const int64_t* __restrict__ jst, int nt, int64_t blo
     const int a = slice_of(jst, nt, q0), b = slice_of(jst, nt, q1 - 1);
     kseg[w] = b - a + 1;
     ja[w] = a;
-}
-
-struct Seg {
-    int j;
-    int64_t q0, q1;  // chunk range in `order`
-};
-
-__device__ __forceinline__ Seg seg_of(const int64_t* jst, int nt, const SegSplit& S, const int* ja, int64_t w,
-                                      int64_t k) {
-    Seg g;
-    g.j = ja[w] + (int)k;
-    g.q0 = max(w * S.per, jst[g.j]);
-    g.q1 = min(min(w * S.per + S.per, S.nch), jst[g.j + 1]);
-    return g;
-}
-
-__device__ __forceinline__ int64_t block_of_seg(const int64_t* segbase, int64_t blocks, int64_t g) {
-    int64_t lo = 0, hi = blocks;  // last w with segbase[w] <= g
-    while (hi - lo > 1) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (segbase[mid] <= g) lo = mid; else hi = mid;
-    }
-    return lo;
 }
 
 // psum[g][i] = pairs of segment g in source slice i (sum of its chunks' histogram rows)
@@ -419,19 +254,6 @@ __global__ void k_seg_prefix(uint32_t* __restrict__ psum, const int64_t* __restr
             run += v;
         }
     tot[c] = run;
-}
-
-struct BitV {
-    const uint32_t* w;  // words over [lo, hi) -- same domain as the layout
-    int full;
-};
-
-__device__ __forceinline__ bool gbit(const uint32_t* w, uint32_t x) { return (w[x >> 5] >> (x & 31)) & 1u; }
-
-__device__ __forceinline__ void lds_set(uint32_t* lds, uint32_t x) {
-    const uint32_t bit = 1u << (x & 31);
-    uint32_t* p = &lds[x >> 5];
-    if (!(*p & bit)) atomicOr(p, bit);
 }
 
 // OR the block's target slice j into the global words, masked by the target-side node filter
@@ -676,6 +498,7 @@ static part::Layout make_layout(int64_t lo, int64_t hi) {
     L.ns = (int)((range + (uint64_t(1) << L.sbits) - 1) >> L.sbits);
     if (L.ns < 1) L.ns = 1;
     L.ncells = L.nt * L.ns;
+    L.tbits = part::kSliceBits;
     return L;
 }
 
@@ -685,19 +508,11 @@ static void allow_lds(K kernel, size_t bytes) {
                                   (int)bytes));
 }
 
-void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
-                   int64_t lo, int64_t hi, RelPart& rp, const RelPartHop1* h1) {
-    REQUIRE(hi > lo && (uint64_t)(hi - lo) <= (uint64_t(1) << 30), CAPSMI_ERR_UNSUPPORTED,
-            "partitioned layout needs an id domain of at most 2^30 ids");
+void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
+                     int nt, bool swap, const part::Layout& L, int64_t g2_want, ChunkPart& cp) {
     using namespace part;
     hipStream_t st = s->stream;
-    rp.L = make_layout(lo, hi);
-    const Layout& L = rp.L;
-    REQUIRE(L.nt <= kMaxTSlices && L.ncells <= kMaxCells, CAPSMI_ERR_INTERNAL, "layout too large");
-    if (h1)
-        REQUIRE(h1->a->lo == lo && h1->a->hi == hi && h1->b->lo == lo && h1->b->hi == hi, CAPSMI_ERR_UNSUPPORTED,
-                "partitioned 2-hop needs node scans over the layout's id domain");
-
+    cp.L = L;
     // pass 1 grid: one 1024-lane block per CU, fewer for small inputs so the open chunks
     // (blocks x slices) stay within a few times the filled ones
     std::vector<int> g1(nt, 0);
@@ -718,47 +533,81 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
             "relationship table too large for the layout");
     const int64_t npool = pool_chunks > 0 ? pool_chunks : 1;
     const int hw = hist_words(L.ns);
-    Buf pool = dev_alloc(sizeof(uint2) * kCh * (size_t)(npool + 1), st);  // + a trash chunk
-    Buf meta = dev_alloc(sizeof(unsigned long long) * npool, st);
-    Buf chist = dev_alloc(sizeof(uint32_t) * hw * (size_t)npool, st);
-    HIP_CHECK(hipMemsetAsync(P<void>(meta), 0, sizeof(unsigned long long) * npool, st));
+    cp.pool = dev_alloc(sizeof(uint2) * kCh * (size_t)(npool + 1), st);  // + a trash chunk
+    cp.meta = dev_alloc(sizeof(unsigned long long) * npool, st);
+    cp.chist = dev_alloc(sizeof(uint32_t) * hw * (size_t)npool, st);
+    HIP_CHECK(hipMemsetAsync(P<void>(cp.meta), 0, sizeof(unsigned long long) * npool, st));
     const size_t lds1 = scatter1_lds(L.nt, L.ns);
     allow_lds(k_scatter_c, lds1);
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
         KernelTimer kt(s, "part_scatter1");
-        hipLaunchKernelGGL(k_scatter_c, dim3(g1[i]), dim3(kP1Block), lds1, st, srcs[i], dsts[i], ms[i], L, c0[i],
+        hipLaunchKernelGGL(k_scatter_c, dim3(g1[i]), dim3(kP1Block), lds1, st, srcs[i], dsts[i], ms[i], L, swap ? 1 : 0, c0[i],
                            (size_t)npool * kCh,
-                           P<uint2>(pool), P<unsigned long long>(meta), P<uint32_t>(chist));
+                           P<uint2>(cp.pool), P<unsigned long long>(cp.meta), P<uint32_t>(cp.chist));
     }
     HIP_CHECK(hipGetLastError());
 
     // used chunks ordered by target slice; pass-2 segments and the exact output offset of every
     // (segment, source cell); no host round trip until the layout is written
-    const bool fuse = h1 && h1->a->full;
-    const int64_t g2 = std::max<int64_t>(1, std::min<int64_t>((int64_t)s->num_cus * (fuse ? 1 : 2), npool));
-    const int64_t maxg = g2 + L.nt;  // segments <= blocks + slices
-    Buf jbuf = dev_alloc(sizeof(int64_t) * (3 * (size_t)L.nt + 2 * (size_t)g2 + 3) + sizeof(uint32_t) * npool +
+    const int64_t g2 = std::max<int64_t>(1, std::min<int64_t>(g2_want, npool));
+    cp.jbuf = dev_alloc(sizeof(int64_t) * (3 * (size_t)L.nt + 2 * (size_t)g2 + 3) + sizeof(uint32_t) * npool +
                              sizeof(int) * g2, st);
-    int64_t* jcnt = P<int64_t>(jbuf);
+    int64_t* jcnt = P<int64_t>(cp.jbuf);
     int64_t* jst = jcnt + L.nt;        // nt + 1
     int64_t* jcur = jst + L.nt + 1;    // nt
     int64_t* kseg = jcur + L.nt;       // g2
     int64_t* segbase = kseg + g2;      // g2 + 1
     uint32_t* order = reinterpret_cast<uint32_t*>(segbase + g2 + 2);
     int* ja = reinterpret_cast<int*>(order + npool);
-    Buf pbuf = dev_alloc(sizeof(uint32_t) * (size_t)maxg * L.ns, st);
-    uint32_t* psum = P<uint32_t>(pbuf);
-    Buf tot = dev_alloc(sizeof(int64_t) * L.ncells, st);
     HIP_CHECK(hipMemsetAsync(jcnt, 0, sizeof(int64_t) * L.nt, st));
     const unsigned cg = (unsigned)((npool + 255) / 256);
-    hipLaunchKernelGGL(k_chunk_count, dim3(cg), dim3(256), 0, st, P<unsigned long long>(meta), pool_chunks, jcnt);
+    hipLaunchKernelGGL(k_chunk_count, dim3(cg), dim3(256), 0, st, P<unsigned long long>(cp.meta), pool_chunks, jcnt);
     exclusive_scan_i64(jcnt, jst, L.nt, st);
     HIP_CHECK(hipMemcpyAsync(jcur, jst, sizeof(int64_t) * L.nt, hipMemcpyDeviceToDevice, st));
-    hipLaunchKernelGGL(k_chunk_place, dim3(cg), dim3(256), 0, st, P<unsigned long long>(meta), pool_chunks,
+    hipLaunchKernelGGL(k_chunk_place, dim3(cg), dim3(256), 0, st, P<unsigned long long>(cp.meta), pool_chunks,
                        reinterpret_cast<unsigned long long*>(jcur), order);
     hipLaunchKernelGGL(k_seg_count, dim3((unsigned)((g2 + 255) / 256)), dim3(256), 0, st, jst, L.nt, g2, kseg, ja);
     exclusive_scan_i64(kseg, segbase, g2, st);
+    HIP_CHECK(hipGetLastError());
+    cp.pool_chunks = pool_chunks;
+    cp.npool = npool;
+    cp.mtot = mtot;
+    cp.g2 = g2;
+    cp.jst = jst;
+    cp.segbase = segbase;
+    cp.ja = ja;
+    cp.order = order;
+}
+
+void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
+                   int64_t lo, int64_t hi, RelPart& rp, const RelPartHop1* h1) {
+    REQUIRE(hi > lo && (uint64_t)(hi - lo) <= (uint64_t(1) << 30), CAPSMI_ERR_UNSUPPORTED,
+            "partitioned layout needs an id domain of at most 2^30 ids");
+    using namespace part;
+    hipStream_t st = s->stream;
+    rp.L = make_layout(lo, hi);
+    const Layout& L = rp.L;
+    REQUIRE(L.nt <= kMaxTSlices && L.ncells <= kMaxCells, CAPSMI_ERR_INTERNAL, "layout too large");
+    if (h1)
+        REQUIRE(h1->a->lo == lo && h1->a->hi == hi && h1->b->lo == lo && h1->b->hi == hi, CAPSMI_ERR_UNSUPPORTED,
+                "partitioned 2-hop needs node scans over the layout's id domain");
+
+    const bool fuse = h1 && h1->a->full;
+    ChunkPart cp;
+    chunk_partition(s, srcs, dsts, ms, nt, false, L, (int64_t)s->num_cus * (fuse ? 1 : 2), cp);
+    const int64_t g2 = cp.g2, mtot = cp.mtot;
+    const int64_t maxg = g2 + L.nt;  // segments <= blocks + slices
+    int64_t* jst = cp.jst;
+    int64_t* segbase = cp.segbase;
+    int* ja = cp.ja;
+    uint32_t* order = cp.order;
+    Buf& pool = cp.pool;
+    Buf& meta = cp.meta;
+    Buf& chist = cp.chist;
+    Buf pbuf = dev_alloc(sizeof(uint32_t) * (size_t)maxg * L.ns, st);
+    uint32_t* psum = P<uint32_t>(pbuf);
+    Buf tot = dev_alloc(sizeof(int64_t) * L.ncells, st);
     hipLaunchKernelGGL(k_seg_sum, dim3((unsigned)maxg), dim3(1024), 0, st, P<uint32_t>(chist), order, jst, L.nt, g2,
                        segbase, ja, L.ns, psum);
     hipLaunchKernelGGL(k_seg_prefix, dim3((L.ncells + 255) / 256), dim3(256), 0, st, psum, jst, g2, segbase, ja, L,

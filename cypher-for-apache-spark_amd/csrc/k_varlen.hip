@@ -12,7 +12,7 @@
 //   len 2: sum_{r: a->b} od(b) - s(a) b_ok(a)
 //   len 3: sum_{r: a->b} [W(b) - (m(b,a) + s(b)) b_ok(b)] - s(a) (od(a) - 2 b_ok(a))
 // Four streaming passes over the relationship table plus one hash probe per relationship for m(b,a).
-#include "capsmi_impl.h"
+#include "part_common.h"
 
 namespace capsmi {
 namespace varlen {
@@ -104,6 +104,265 @@ __global__ void k_final(int64_t n, Dom d, int lower, int upper, const unsigned l
     }
 }
 
+// ---- source-sliced passes (n <= 2^24 ids) ------------------------------------------------------------
+// The atomic passes above hit one global counter per relationship; R-MAT hubs make those hot
+// addresses.  Here the relationships are first grouped by source slice of 2^kVlBits ids (the
+// chunked partition of k_part.hip, buckets by source), so every per-source sum is accumulated in
+// LDS by the block that owns the slice segment and flushed once per segment.
+// The reverse multiplicity m(b, a) needs, for a in slice j, the relationships *into* slice j: a
+// second partition buckets them by target slice, and each slice gets its own open-addressing
+// table of (target, source) pair counts sized to the slice, so inserts (walking the target
+// partition) and probes (walking the source partition) both stay inside one slice's table,
+// small enough for the XCD's L2.
+constexpr int kVlBits = 13;  // 8192 ids per slice: two 64 KiB LDS accumulator arrays
+constexpr int kVlIds = 1 << kVlBits;
+constexpr int kVlBlock = 1024;
+constexpr unsigned long long kEmpty = ~0ULL;
+
+__device__ __forceinline__ unsigned long long splitmix(unsigned long long x) {
+    x += 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ unsigned long long pkey(uint32_t s, uint32_t t) { return ((unsigned long long)s << 32) | t; }
+
+// exact (source, target) pair counts, open addressing, for the candidate pairs only
+struct PairHash {
+    unsigned long long* key;
+    unsigned int* cnt;
+    unsigned long long mask;
+};
+
+__device__ __forceinline__ void pair_insert(const PairHash& h, unsigned long long k) {
+    for (unsigned long long i = splitmix(k) & h.mask;; i = (i + 1) & h.mask) {
+        unsigned long long cur = h.key[i];
+        if (cur == kEmpty) {
+            cur = atomicCAS(&h.key[i], kEmpty, k);
+            if (cur == kEmpty) cur = k;
+        }
+        if (cur == k) {
+            atomicAdd(&h.cnt[i], 1u);
+            return;
+        }
+    }
+}
+
+__device__ __forceinline__ unsigned int pair_count(const PairHash& h, unsigned long long k) {
+    for (unsigned long long i = splitmix(k) & h.mask;; i = (i + 1) & h.mask) {
+        const unsigned long long cur = h.key[i];
+        if (cur == k) return h.cnt[i];
+        if (cur == kEmpty) return 0u;
+    }
+}
+
+// One-bit filter of the directed pairs present, one region of 2^rshift bits per TARGET slice:
+// the bit of pair (s, t) lives in slice(t)'s region.  Walking the target partition sets a slice's
+// bits; the tests ask "does t -> s exist" for an s of the slice being walked in the source
+// partition, i.e. inside that slice's region -- L2-local either way.
+struct RegionBloom {
+    uint32_t* w;
+    unsigned long long rmask;  // bits per region - 1 (power of two)
+    int rshift;                // log2(bits per region)
+};
+
+__device__ __forceinline__ unsigned long long rb_bit(const RegionBloom& b, int j, unsigned long long k) {
+    return ((unsigned long long)j << b.rshift) | (splitmix(k ^ 0x5DEECE66DULL) & b.rmask);
+}
+
+struct ChunkWalk {
+    const uint2* pool;
+    const unsigned long long* meta;
+    const uint32_t* order;
+    const int64_t* jst;
+    const int64_t* segbase;
+    const int* ja;
+    int nt;
+};
+
+// Block w visits the pairs (x, y) (relative ids; the bucket follows y) of its chunk share in
+// slice order: visit(pair, j) per pair; at every slice change and at the end flush(j) runs between
+// barriers (it must also clear the block's accumulators).  The next chunk is loaded while the
+// current one is visited.
+template <class Visit, class Flush>
+__device__ void walk_chunks(const ChunkWalk& cw, Visit visit, Flush flush) {
+    using namespace part;
+    const int64_t w = blockIdx.x, blocks = gridDim.x;
+    const SegSplit S(cw.jst, cw.nt, blocks);
+    auto load_chunk = [&](int64_t q, uint2 (&pr)[kItems]) -> uint32_t {
+        const uint32_t phys = cw.order[q];
+        const uint32_t fill = (uint32_t)(cw.meta[phys] >> 32);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint2*>(cw.pool + (size_t)phys * kCh), (short)0, (int)(fill * sizeof(uint2)), 0x00020000);
+#pragma unroll
+        for (int k = 0; k < kItems / 2; ++k) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(k * kVlBlock + (int)threadIdx.x) * 16u, 0, 0);
+            pr[2 * k] = make_uint2(v[0], v[1]);
+            pr[2 * k + 1] = make_uint2(v[2], v[3]);
+        }
+        return fill;
+    };
+    const int64_t qb = w * S.per, qe = min(qb + S.per, S.nch);
+    if (qb >= qe) return;  // block-uniform
+    uint2 nx[kItems];
+    uint32_t nfill = load_chunk(qb, nx);
+    int cur_j = slice_of(cw.jst, cw.nt, qb);
+    for (int64_t q = qb; q < qe; ++q) {  // block-uniform
+        const int j = slice_of(cw.jst, cw.nt, q);
+        if (j != cur_j) {
+            __syncthreads();
+            flush(cur_j);
+            __syncthreads();
+            cur_j = j;
+        }
+        uint2 pr[kItems];
+#pragma unroll
+        for (int k = 0; k < kItems; ++k) pr[k] = nx[k];
+        const uint32_t fill = nfill;
+        if (q + 1 < qe) nfill = load_chunk(q + 1, nx);
+#pragma unroll
+        for (int k = 0; k < kItems; ++k)
+            if ((uint32_t)(2 * ((k >> 1) * kVlBlock + (int)threadIdx.x) + (k & 1)) < fill) visit(pr[k], j);
+    }
+    __syncthreads();
+    flush(cur_j);
+}
+
+__device__ __forceinline__ bool bit_of(const uint32_t* w, int full, uint32_t x) {
+    return full || ((w[x >> 5] >> (x & 31)) & 1u);
+}
+
+// flush an LDS accumulator array of slice j into the global per-node array, then clear it
+__device__ __forceinline__ void flush_acc(unsigned long long* acc, unsigned long long* g, int j, int64_t n) {
+    for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) {
+        const unsigned long long v = acc[i];
+        const int64_t x = (int64_t)j * kVlIds + i;
+        if (v && x < n) atomicAdd(&g[x], v);
+        acc[i] = 0;
+    }
+}
+
+// pass 1 (source partition, pair = (target, source)): od(v), s(v)
+__global__ void __launch_bounds__(kVlBlock) k_vl_deg(ChunkWalk cw, const uint32_t* __restrict__ bw, int b_full,
+                                                     int64_t n, unsigned long long* __restrict__ od,
+                                                     unsigned long long* __restrict__ sl) {
+    extern __shared__ unsigned long long vl_lds[];
+    unsigned long long *a_od = vl_lds, *a_s = vl_lds + kVlIds;
+    for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_od[i] = a_s[i] = 0;
+    __syncthreads();
+    walk_chunks(
+        cw,
+        [&](uint2 p, int) {
+            const uint32_t t = p.x, s = p.y, i = s & (kVlIds - 1);
+            if (bit_of(bw, b_full, t)) atomicAdd(&a_od[i], 1ULL);
+            if (s == t) atomicAdd(&a_s[i], 1ULL);
+        },
+        [&](int j) {
+            flush_acc(a_od, od, j, n);
+            flush_acc(a_s, sl, j, n);
+        });
+}
+
+// pass 2: W(v) = sum_{v -> w} od(w)
+__global__ void __launch_bounds__(kVlBlock) k_vl_w(ChunkWalk cw, int64_t n, const unsigned long long* __restrict__ od,
+                                                   unsigned long long* __restrict__ W) {
+    extern __shared__ unsigned long long vl_lds[];
+    unsigned long long* a_w = vl_lds;
+    for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_w[i] = 0;
+    __syncthreads();
+    walk_chunks(
+        cw,
+        [&](uint2 p, int) {
+            const unsigned long long x = od[p.x];
+            if (x) atomicAdd(&a_w[p.y & (kVlIds - 1)], x);
+        },
+        [&](int j) { flush_acc(a_w, W, j, n); });
+}
+
+// target partition (pair = (source, target), j = slice(t)): mark pair (s, t) in region j.  The
+// region (<= 128 KiB) is built in LDS and ORed out once per slice segment.
+__global__ void __launch_bounds__(kVlBlock) k_vl_bset(ChunkWalk cw, RegionBloom bl) {
+    extern __shared__ uint32_t rb_lds[];
+    const int rwords = 1 << (bl.rshift - 5);
+    for (int i = threadIdx.x; i < rwords; i += kVlBlock) rb_lds[i] = 0;
+    __syncthreads();
+    walk_chunks(
+        cw,
+        [&](uint2 p, int) {
+            const unsigned long long x = splitmix(pkey(p.x, p.y) ^ 0x5DEECE66DULL) & bl.rmask;
+            atomicOr(&rb_lds[x >> 5], 1u << (x & 31));
+        },
+        [&](int j) {
+            uint32_t* g = bl.w + ((size_t)j << (bl.rshift - 5));
+            for (int i = threadIdx.x; i < rwords; i += kVlBlock) {
+                const uint32_t v = rb_lds[i];
+                if (v) atomicOr(&g[i], v);
+                rb_lds[i] = 0;
+            }
+        });
+}
+
+// source partition: count (or insert) the pairs s -> t whose reverse t -> s may exist
+template <bool INSERT>
+__global__ void __launch_bounds__(kVlBlock) k_vl_cand(ChunkWalk cw, RegionBloom bl, PairHash h,
+                                                      unsigned long long* __restrict__ ncand) {
+    __shared__ unsigned int cand;
+    if (threadIdx.x == 0) cand = 0;
+    __syncthreads();
+    walk_chunks(
+        cw,
+        [&](uint2 p, int j) {  // p = (t, s), j = slice(s)
+            const unsigned long long x = rb_bit(bl, j, pkey(p.x, p.y));
+            if ((bl.w[x >> 5] >> (x & 31)) & 1u) {
+                if (INSERT) pair_insert(h, pkey(p.y, p.x));
+                else atomicAdd(&cand, 1u);
+            }
+        },
+        [&](int) {});
+    if (!INSERT && threadIdx.x == 0 && cand) atomicAdd(ncand, (unsigned long long)cand);
+}
+
+// Y(b) = W(b) - s(b) b_ok(b)
+__global__ void k_vl_y(int64_t n, const uint32_t* __restrict__ bw, int b_full, const unsigned long long* __restrict__ W,
+                       const unsigned long long* __restrict__ sl, long long* __restrict__ Y) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        Y[i] = (long long)W[i] - (bit_of(bw, b_full, (uint32_t)i) ? (long long)sl[i] : 0LL);
+}
+
+// pass 3 (source partition): per relationship a -> b with a_ok(a): T2(a) += od(b);
+// T3(a) += Y(b) - m(b, a) b_ok(b), m(b, a) from a's slice table
+__global__ void __launch_bounds__(kVlBlock) k_vl_t(ChunkWalk cw, const uint32_t* __restrict__ aw, int a_full,
+                                                   const uint32_t* __restrict__ bw, int b_full, int64_t n, RegionBloom bl,
+                                                   PairHash h,
+                                                   const unsigned long long* __restrict__ od,
+                                                   const long long* __restrict__ Y, unsigned long long* __restrict__ T2,
+                                                   unsigned long long* __restrict__ T3) {
+    extern __shared__ unsigned long long vl_lds[];
+    unsigned long long *a_t2 = vl_lds, *a_t3 = vl_lds + kVlIds;
+    for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_t2[i] = a_t3[i] = 0;
+    __syncthreads();
+    walk_chunks(
+        cw,
+        [&](uint2 p, int j) {
+            const uint32_t b = p.x, a = p.y, i = a & (kVlIds - 1);
+            if (!bit_of(aw, a_full, a)) return;
+            atomicAdd(&a_t2[i], od[b]);
+            if (Y) {
+                long long t3 = Y[b];
+                if (bit_of(bw, b_full, b)) {
+                    const unsigned long long x = rb_bit(bl, j, pkey(b, a));  // may b -> a exist?
+                    if ((bl.w[x >> 5] >> (x & 31)) & 1u) t3 -= (long long)pair_count(h, pkey(b, a));
+                }
+                atomicAdd(&a_t3[i], (unsigned long long)t3);  // two's complement sum
+            }
+        },
+        [&](int j) {
+            flush_acc(a_t2, T2, j, n);
+            flush_acc(a_t3, T3, j, n);
+        });
+}
+
 inline int grid(const capsmi_session* s, int64_t n) {
     int64_t g = (n + 255) / 256;
     const int64_t cap = (int64_t)s->num_cus * 16;
@@ -128,6 +387,81 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
         T3 = dev_alloc(nb, st);
     for (Buf* b : {&od, &sl, &W, &T2, &T3}) HIP_CHECK(hipMemsetAsync(P<void>(*b), 0, nb, st));
     const bool need3 = upper >= 3;
+    int64_t mtot = 0;
+    for (int i = 0; i < nt; ++i) mtot += ms[i] > 0 ? ms[i] : 0;
+    if (n > 0 && n <= (int64_t(1) << 24) && mtot > 0) {
+        // source-sliced passes: relationships grouped by source slice, LDS accumulators
+        part::Layout L{};
+        L.lo = d.lo;
+        L.hi = d.hi;
+        L.tbits = kVlBits;
+        L.nt = (int)((n + kVlIds - 1) / kVlIds);
+        L.ns = 1;
+        L.sbits = 31;
+        L.ncells = L.nt;
+        ChunkPart cp, ct;
+        {
+            KernelTimer kt(s, "varlen_part");
+            chunk_partition(s, srcs, dsts, ms, nt, true, L, s->num_cus, cp);
+        }
+        const ChunkWalk cw{P<uint2>(cp.pool), P<unsigned long long>(cp.meta), cp.order, cp.jst, cp.segbase, cp.ja, L.nt};
+        const unsigned g = (unsigned)cp.g2;
+        const size_t lds2 = 2 * sizeof(unsigned long long) * kVlIds;
+        for (const void* f : {reinterpret_cast<const void*>(k_vl_deg), reinterpret_cast<const void*>(k_vl_w),
+                              reinterpret_cast<const void*>(k_vl_t)})
+            HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+        {
+            KernelTimer kt(s, "varlen_deg");
+            hipLaunchKernelGGL(k_vl_deg, dim3(g), dim3(kVlBlock), lds2, st, cw, d.b, d.b_full, n, P<unsigned long long>(od),
+                               P<unsigned long long>(sl));
+        }
+        Buf Y, bw, hk, hc, cand;
+        RegionBloom bl{nullptr, 0, 0};
+        PairHash h{nullptr, nullptr, 0};
+        if (need3) {
+            {
+                KernelTimer kt(s, "varlen_w");
+                hipLaunchKernelGGL(k_vl_w, dim3(g), dim3(kVlBlock), lds2 / 2, st, cw, n, P<unsigned long long>(od),
+                                   P<unsigned long long>(W));
+            }
+            Y = dev_alloc(nb, st);
+            hipLaunchKernelGGL(k_vl_y, dim3(grid(s, n)), dim3(256), 0, st, n, d.b, d.b_full, P<unsigned long long>(W),
+                               P<unsigned long long>(sl), P<long long>(Y));
+            KernelTimer kt(s, "varlen_rev");
+            chunk_partition(s, srcs, dsts, ms, nt, false, L, s->num_cus, ct);
+            int rshift = 10;  // >= 8 bits per pair of an average slice, at most 128 KiB (LDS) per region
+            while ((int64_t(1) << rshift) < 8 * ((mtot + L.nt - 1) / L.nt) && rshift < 20) ++rshift;
+            const size_t bbytes = ((size_t)L.nt << rshift) / 8;
+            bw = dev_alloc(bbytes, st);
+            HIP_CHECK(hipMemsetAsync(P<void>(bw), 0, bbytes, st));
+            bl = RegionBloom{P<uint32_t>(bw), (unsigned long long)((int64_t(1) << rshift) - 1), rshift};
+            const ChunkWalk tw{P<uint2>(ct.pool), P<unsigned long long>(ct.meta), ct.order, ct.jst, ct.segbase, ct.ja,
+                               L.nt};
+            const size_t rlds = (size_t(1) << rshift) / 8;
+            HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_vl_bset),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds));
+            hipLaunchKernelGGL(k_vl_bset, dim3((unsigned)ct.g2), dim3(kVlBlock), rlds, st, tw, bl);
+            cand = dev_alloc(sizeof(int64_t), st);
+            HIP_CHECK(hipMemsetAsync(P<void>(cand), 0, sizeof(int64_t), st));
+            hipLaunchKernelGGL(k_vl_cand<false>, dim3(g), dim3(kVlBlock), 0, st, cw, bl, h, P<unsigned long long>(cand));
+            const int64_t nc = read_scalar(s, P<int64_t>(cand));
+            int64_t cap = 1024;
+            while (cap < 2 * nc) cap <<= 1;
+            hk = dev_alloc(sizeof(unsigned long long) * cap, st);
+            hc = dev_alloc(sizeof(unsigned int) * cap, st);
+            HIP_CHECK(hipMemsetAsync(P<void>(hk), 0xFF, sizeof(unsigned long long) * cap, st));
+            HIP_CHECK(hipMemsetAsync(P<void>(hc), 0, sizeof(unsigned int) * cap, st));
+            h = PairHash{P<unsigned long long>(hk), P<unsigned int>(hc), (unsigned long long)(cap - 1)};
+            hipLaunchKernelGGL(k_vl_cand<true>, dim3(g), dim3(kVlBlock), 0, st, cw, bl, h, P<unsigned long long>(cand));
+        }
+        {
+            KernelTimer kt(s, "varlen_t");
+            hipLaunchKernelGGL(k_vl_t, dim3(g), dim3(kVlBlock), lds2, st, cw, d.a, d.a_full, d.b, d.b_full, n, bl, h,
+                               P<unsigned long long>(od), need3 ? P<long long>(Y) : nullptr, P<unsigned long long>(T2),
+                               P<unsigned long long>(T3));
+        }
+        HIP_CHECK(hipGetLastError());
+    } else {
     {
         KernelTimer kt(s, "varlen_deg");
         for (int i = 0; i < nt; ++i)
@@ -146,8 +480,6 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
     // relationship tables (concatenated key columns)
     Buf rev, counts;
     HashTable ht;
-    int64_t mtot = 0;
-    for (int i = 0; i < nt; ++i) mtot += ms[i];
     if (need3 && mtot > 0) {
         Buf cs = dev_alloc(sizeof(int64_t) * mtot, st), cd = dev_alloc(sizeof(int64_t) * mtot, st);
         int64_t off = 0;
@@ -182,6 +514,7 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
             off += ms[i];
         }
     }
+    }  // atomic passes
     Buf cnt = dev_alloc(nb, st), flags = dev_alloc(n > 0 ? n : 1, st);
     hipLaunchKernelGGL(k_final, dim3(grid(s, n)), dim3(256), 0, st, n, d, lower, upper, P<unsigned long long>(od),
                        P<unsigned long long>(sl), P<unsigned long long>(T2), P<unsigned long long>(T3),

@@ -1,0 +1,207 @@
+// part_common.h -- shared pieces of the chunked relationship partition (k_part.hip) and its users
+// (C3 2-D layout build, C5 source-sliced var-length passes in k_varlen.hip).  Not part of the ABI.
+#pragma once
+#include "capsmi_impl.h"
+
+namespace capsmi {
+namespace part {
+
+constexpr int kSliceBits = 19;                   // 2^19 ids per slice = 64 KiB of LDS bitmap
+constexpr int kSliceWords = 1 << (kSliceBits - 5);
+constexpr int kMaxCells = 16384;                 // cell histogram = 32 KiB of 16-bit LDS counters
+constexpr int kMaxTSlices = 2048;                // domain <= 2^30 ids (pass-1 LDS: 7 words per slice)
+constexpr int kBlock = 1024;                     // hop workgroups
+constexpr int kItems = 8;                        // relationships per lane per tile
+constexpr int kSBlock = 1024;                    // scatter workgroups
+constexpr int kTile = kSBlock * kItems;          // relationships per scatter tile (8192)
+constexpr int kCh = kTile;                       // pairs per pass-1 chunk: a tile's run spans <= 2 chunks
+constexpr int kP1Block = 1024;                   // pass-1 workgroup (512 x 2 per CU measured slower)
+constexpr int kP1Tile = kP1Block * kItems;       // pass-1 tile (<= kCh)
+static_assert(kP1Tile <= kCh, "a pass-1 run must span at most two chunks");
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr int kUnroll = 8;                       // loads in flight per lane in the hops
+constexpr int64_t kLoadMin = 8192;               // pull a source slice into LDS for >= this many rels
+constexpr int kPad = 2 * 8192;                   // slack pairs after every pair array (load_pairs)
+
+using Layout = PartLayout;
+
+// Exclusive scan of in[0..n) into out[0..n) by a B-lane block; returns the total.
+// `wtot` is B/64 words of LDS scratch.  Contains barriers: call from block-uniform code.
+template <int B>
+__device__ uint32_t block_exclusive_scan(const uint32_t* in, uint32_t* out, int n, uint32_t* wtot) {
+    const int per = (n + B - 1) / B;
+    const int b = threadIdx.x * per;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t sum = 0;
+    for (int k = 0; k < per; ++k)
+        if (b + k < n) sum += in[b + k];
+    uint32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wtot[wave] = x;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        uint32_t v = lane < B / 64 ? wtot[lane] : 0u;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(v, o, 64);
+            if (lane >= o) v += y;
+        }
+        if (lane < B / 64) wtot[lane] = v;
+    }
+    __syncthreads();
+    uint32_t pre = x - sum + (wave > 0 ? wtot[wave - 1] : 0u);
+    for (int k = 0; k < per; ++k)
+        if (b + k < n) {
+            const uint32_t c = in[b + k];
+            out[b + k] = pre;
+            pre += c;
+        }
+    const uint32_t total = wtot[B / 64 - 1];
+    __syncthreads();
+    return total;
+}
+
+__device__ __forceinline__ int cell_of(const Layout& L, uint32_t s, uint32_t t) {
+    return (int)(t >> L.tbits) * L.ns + (int)(s >> L.sbits);
+}
+
+// Tile item u of this lane is relationship t0 + item_off<B>(u): lanes read 16-byte pairs of
+// consecutive relationships (2 int64 per load, the calibrated streaming width), pair k of the
+// tile at offset 2 * (k * B + lane).
+template <int B>
+__device__ __forceinline__ int item_off(int u) {
+    return 2 * ((u >> 1) * B + (int)threadIdx.x) + (u & 1);
+}
+
+// Issue all of a tile's loads before any test: with a branch around each load the compiler
+// waits for every load before issuing the next.  `vec` = both columns 16-byte aligned.
+template <int B>
+__device__ __forceinline__ void load_tile(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t t0,
+                                          int64_t m, bool vec, int64_t (&sr)[kItems], int64_t (&tr)[kItems]) {
+    const int64_t* __restrict__ sp = src + t0;  // wave-uniform bases, 32-bit lane offsets
+    const int64_t* __restrict__ dp = dst + t0;
+    if (vec && t0 + B * kItems <= m) {
+        const longlong2* __restrict__ sv = reinterpret_cast<const longlong2*>(sp);
+        const longlong2* __restrict__ dv = reinterpret_cast<const longlong2*>(dp);
+#pragma unroll
+        for (int k = 0; k < kItems / 2; ++k) {
+            const longlong2 a = sv[k * B + (int)threadIdx.x], b = dv[k * B + (int)threadIdx.x];
+            sr[2 * k] = a.x;
+            sr[2 * k + 1] = a.y;
+            tr[2 * k] = b.x;
+            tr[2 * k + 1] = b.y;
+        }
+    } else {
+        const int last = (int)(min(m - t0, (int64_t)B * kItems) - 1);
+#pragma unroll
+        for (int u = 0; u < kItems; ++u) {
+            const int i = min(item_off<B>(u), last);
+            sr[u] = sp[i];
+            tr[u] = dp[i];
+        }
+    }
+}
+
+// The B * N pairs of a packed uint2 array starting at the even, wave-uniform index b, as 16-byte
+// loads: this lane's item u is b + item_off<B>(u).  Pair arrays are allocated with kPad pairs of
+// slack so a tile may run past the last pair; callers mask items outside their range.
+template <int B, int N>
+__device__ __forceinline__ void load_pairs(const uint2* __restrict__ in, int64_t b, uint2 (&p)[N]) {
+    const uint4* __restrict__ v = reinterpret_cast<const uint4*>(in + b);
+#pragma unroll
+    for (int k = 0; k < N / 2; ++k) {
+        const uint4 x = v[k * B + (int)threadIdx.x];
+        p[2 * k] = make_uint2(x.x, x.y);
+        p[2 * k + 1] = make_uint2(x.z, x.w);
+    }
+}
+
+__device__ __forceinline__ unsigned long long chunk_meta(int j, uint32_t fill) {
+    return (unsigned long long)(uint32_t)j | ((unsigned long long)fill << 32);
+}
+
+// per-chunk histogram row: ns 16-bit counters padded to an even count (whole 32-bit words)
+__host__ __device__ constexpr int hist_words(int ns) { return (ns + 1) >> 1; }
+
+// ---- pass-2 work split ------------------------------------------------------------------------------
+// Block w of pass 2 takes the used chunks [w * per, (w + 1) * per) of the slice-ordered list
+// (per = ceil(chunks / blocks), read on the device).  Its range meets slices ja(w) .. jb(w); each
+// (block, slice) intersection is a segment, numbered block-major, so the segments of one slice are
+// consecutive.  The exact output start of segment g in cell (j, i) is coff[(j, i)] + the pairs the
+// slice's earlier segments put there (prefix over the per-chunk histograms).
+
+__device__ __forceinline__ int slice_of(const int64_t* jst, int nt, int64_t q) {  // last j with jst[j] <= q
+    int lo = 0, hi = nt;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (jst[mid] <= q) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+struct SegSplit {
+    int64_t nch, per;
+    __device__ SegSplit(const int64_t* jst, int nt, int64_t blocks) : nch(jst[nt]), per((jst[nt] + blocks - 1) / blocks) {
+        if (per < 1) per = 1;
+    }
+};
+
+struct Seg {
+    int j;
+    int64_t q0, q1;  // chunk range in `order`
+};
+
+__device__ __forceinline__ Seg seg_of(const int64_t* jst, int nt, const SegSplit& S, const int* ja, int64_t w,
+                                      int64_t k) {
+    Seg g;
+    g.j = ja[w] + (int)k;
+    g.q0 = max(w * S.per, jst[g.j]);
+    g.q1 = min(min(w * S.per + S.per, S.nch), jst[g.j + 1]);
+    return g;
+}
+
+__device__ __forceinline__ int64_t block_of_seg(const int64_t* segbase, int64_t blocks, int64_t g) {
+    int64_t lo = 0, hi = blocks;  // last w with segbase[w] <= g
+    while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (segbase[mid] <= g) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+struct BitV {
+    const uint32_t* w;  // words over [lo, hi) -- same domain as the layout
+    int full;
+};
+
+__device__ __forceinline__ bool gbit(const uint32_t* w, uint32_t x) { return (w[x >> 5] >> (x & 31)) & 1u; }
+
+__device__ __forceinline__ void lds_set(uint32_t* lds, uint32_t x) {
+    const uint32_t bit = 1u << (x & 31);
+    uint32_t* p = &lds[x >> 5];
+    if (!(*p & bit)) atomicOr(p, bit);
+}
+
+}  // namespace part
+
+// Pass 1 of the partition plus chunk ordering and the block-balanced segment split (k_part.hip):
+// relationships grouped by bucket = (y >> L.tbits) of their packed (x, y) = (source - lo, target - lo)
+// pair, in chunks of kCh pairs; with `swap` the pair is (target, source) and buckets follow the
+// source.  Blocks of a consumer kernel launched with g2 blocks walk segments via part::seg_of.
+struct ChunkPart {
+    part::Layout L;
+    Buf pool, meta, chist, jbuf;
+    int64_t pool_chunks = 0, npool = 1, mtot = 0, g2 = 1;
+    int64_t* jst = nullptr;      // nt + 1 chunk offsets per bucket in `order`
+    int64_t* segbase = nullptr;  // g2 + 1
+    int* ja = nullptr;           // first bucket per block
+    uint32_t* order = nullptr;   // used chunks grouped by bucket
+};
+void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
+                     int nt, bool swap, const part::Layout& L, int64_t g2, ChunkPart& cp);
+
+}  // namespace capsmi

@@ -61,3 +61,34 @@ def test_split_rel_tables_union(session):
     t1, t2 = _table(session, src[:700], dst[:700]), _table(session, src[700:], dst[700:])
     ones = np.ones(n, dtype=bool)
     _check(session, n, src, dst, ones, ones, 1, 3, rels=[t1, t2])
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_many_source_slices(session, seed):
+    """Domain of several 8192-id source slices (LDS accumulators flushed per slice segment),
+    reciprocal pairs and multi-edges (the (source, target) pair-count table), hub sources."""
+    rng = np.random.default_rng(100 + seed)
+    n, m = 45_000, 150_000
+    src = rng.integers(0, n, m).astype(np.int64)
+    dst = rng.integers(0, n, m).astype(np.int64)
+    hubs = rng.integers(0, n, 8)
+    src[: m // 10] = rng.choice(hubs, m // 10)
+    k = m // 5  # reciprocal copies and repeats
+    src[k:2 * k], dst[k:2 * k] = dst[:k].copy(), src[:k].copy()
+    src[2 * k:2 * k + 500], dst[2 * k:2 * k + 500] = src[:500], dst[:500]
+    src[-300:] = dst[-300:]  # self-loops
+    a_mask = rng.random(n) < 0.8
+    b_mask = rng.random(n) < 0.7
+    for lo, hi in [(1, 3), (2, 2), (3, 3)]:
+        _check(session, n, src, dst, a_mask, b_mask, lo, hi)
+
+
+def test_large_domain_atomic_path(session):
+    """n > 2^24 ids takes the atomic passes; the answer is the same."""
+    rng = np.random.default_rng(3)
+    n, m = (1 << 24) + 77, 20_000
+    nodes = rng.integers(0, n, 3000)
+    src = rng.choice(nodes, m).astype(np.int64)
+    dst = rng.choice(nodes, m).astype(np.int64)
+    ones = np.ones(n, dtype=bool)
+    _check(session, n, src, dst, ones, ones, 1, 3)
