@@ -393,8 +393,31 @@ class Planner:
         cur: Optional[_Op] = None
         varlen: Dict[str, int] = {}
         for clause in query["clauses"]:
-            cur = self._match(cur, clause["match"], clause.get("where"), varlen)
+            if "optional_match" in clause:
+                cur = self._optional(cur, clause["optional_match"], clause.get("where"), varlen)
+            else:
+                cur = self._match(cur, clause["match"], clause.get("where"), varlen)
         return self._return(cur, query["return"], varlen)
+
+    def _optional(self, cur: Optional[_Op], pattern: str, where, varlen: Dict[str, int]) -> _Op:
+        """OPTIONAL MATCH: the pattern is planned on top of the input (LogicalPlanner.scala:115-128);
+        planOptional (RelationalPlanner.scala:241-276) then left-outer-joins the input with that plan
+        on every variable they share, after dropping the right side's copies of the shared
+        variables' other columns and renaming its join columns apart."""
+        if cur is None or not (cur.node_vars or cur.rel_vars):  # `lhs.fields.isEmpty` -> rhs
+            return self._match(cur, pattern, where, varlen)
+        lhs = cur
+        rhs = self._match(_Op(cur.table, list(cur.header), set(cur.node_vars), list(cur.rel_vars)), pattern, where,
+                          varlen)
+        join_vars = [v for v in lhs.header if v in lhs.node_vars or v in lhs.rel_vars]
+        new_cols = [c for c in rhs.header if c not in lhs.header]
+        renames = [(v, self.names.fresh("opt")) for v in join_vars]
+        right = rhs.table.select(*(join_vars + new_cols))
+        for v, tmp in renames:
+            right = right.withColumnRenamed(v, tmp)
+        joined = lhs.table.join(right, "left_outer", *renames)
+        t = joined.select(*(lhs.header + new_cols))
+        return _Op(t, lhs.header + new_cols, rhs.node_vars, rhs.rel_vars)
 
     def _match(self, cur: Optional[_Op], pattern: str, where, varlen: Dict[str, int]) -> _Op:
         paths = parse_pattern(pattern, self.names)

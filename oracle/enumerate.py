@@ -110,11 +110,11 @@ def match(g: Graph, query: dict) -> List[dict]:
     rows: List[dict] = [dict()]
     bound_rels_order: List[str] = []
     for clause in query["clauses"]:
-        paths = parse_pattern(clause["match"], names)
+        optional = "optional_match" in clause
+        pattern = clause["optional_match"] if optional else clause["match"]
+        paths = parse_pattern(pattern, names)
         clause_rels: List[RelPat] = []
-        new_rows = []
-        for b in rows:
-            new_rows.extend(_clause(g, b, list(paths), clause_rels, bound_rels_order))
+        per_row = [_clause(g, b, list(paths), clause_rels, bound_rels_order) for b in rows]
         # uniqueness (single-length, overlapping types)
         singles = []
         seen = set()
@@ -122,20 +122,29 @@ def match(g: Graph, query: dict) -> List[dict]:
             if r.var_length is None and r.var not in seen:
                 seen.add(r.var)
                 singles.append(r)
-        out = []
-        for b in new_rows:
-            ok = True
+
+        def keep(b):
             for i in range(len(singles)):
                 for j in range(i + 1, len(singles)):
                     x, y = singles[i], singles[j]
                     if x.types and y.types and not (set(x.types) & set(y.types)):
                         continue
                     if b[x.var] == b[y.var]:
-                        ok = False
-            if ok and clause.get("where") is not None:
-                ok = eval_expr(clause["where"], b, g) is True
-            if ok:
-                out.append(b)
+                        return False
+            return clause.get("where") is None or eval_expr(clause["where"], b, g) is True
+
+        out = []
+        has_fields = any(k for b in rows for k in b if not k.startswith("__"))
+        pattern_vars = [e.var for p in paths for e in p]
+        for b, ext in zip(rows, per_row):
+            ext = [e for e in ext if keep(e)]
+            if optional and has_fields and not ext:  # OPTIONAL MATCH keeps the row, new variables null
+                nb = dict(b)
+                for v in pattern_vars:
+                    nb.setdefault(v, None)
+                out.append(nb)
+            else:
+                out.extend(ext)
         rows = out
         for r in clause_rels:
             if r.var not in bound_rels_order:
@@ -278,7 +287,7 @@ def project(g: Graph, rows: List[dict], ret: dict) -> List[dict]:
                     seen.add(key)
                     uniq.append(r)
             out = uniq
-        return out
+        return _order_skip_limit(out, ret)
     groups: Dict[str, list] = {}
     keys: Dict[str, dict] = {}
     for b in rows:
@@ -316,4 +325,17 @@ def project(g: Graph, rows: List[dict], ret: dict) -> List[dict]:
                 else:
                     row[a] = sum(vals) / len(vals)
         out.append(row)
+    return _order_skip_limit(out, ret)
+
+
+def _order_skip_limit(out: List[dict], ret: dict) -> List[dict]:
+    """ORDER BY (Spark asc / desc: nulls first ascending, last descending; SparkTable.scala:94-104),
+    then SKIP and LIMIT."""
+    for alias, direction in reversed(ret.get("order_by") or []):
+        desc = direction.lower().startswith("desc")
+        out = sorted(out, key=lambda r: (r[alias] is not None, r[alias] if r[alias] is not None else 0), reverse=desc)
+    if ret.get("skip"):
+        out = out[int(ret["skip"]):]
+    if ret.get("limit") is not None:
+        out = out[:int(ret["limit"])]
     return out
