@@ -392,6 +392,13 @@ class Planner:
         (table, output spec) ready for :func:`result_rows`."""
         cur: Optional[_Op] = None
         varlen: Dict[str, int] = {}
+        if query.get("driving"):  # driving table: its columns are value variables (planStartWithDrivingTable)
+            d = query["driving"]
+            cols = []
+            for name, values in d.items():
+                ty = STR if any(isinstance(v, str) for v in values) else I64
+                cols.append(_column(name, ty, values, self.g.backend.dictionary.encode))
+            cur = _Op(self.g.backend.table(cols), list(d), set(), [])
         for clause in query["clauses"]:
             if "optional_match" in clause:
                 cur = self._optional(cur, clause["optional_match"], clause.get("where"), varlen)
