@@ -323,6 +323,85 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big(const uint32_t* __restric
     if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
 }
 
+// Big u are split into work items (hash chunk of out(u), chunk of kVChunk v's of out(u)) so a hub's
+// wedges spread over many workgroups; items are taken from a global counter (dynamic balance).
+constexpr int kVChunk = 256;
+
+struct ItemLds {
+    uint32_t hk[kBigSlots];
+    uint64_t hv[kBigSlots];
+    uint64_t vp[kVChunk];
+    int64_t voff[kVChunk];
+    uint32_t vl[kVChunk];
+    uint32_t dv[kVChunk];
+    uint32_t pre[kVChunk];
+    uint32_t wtot[kBigBlock / 64];
+    unsigned long long item;
+};
+
+__global__ void k_tri_items(const int64_t* __restrict__ off, const int64_t* __restrict__ us, int64_t nu,
+                            int64_t* __restrict__ items) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nu) return;
+    const int64_t d = off[us[q] + 1] - off[us[q]];
+    items[q] = ((d + kBigChunk - 1) / kBigChunk) * ((d + kVChunk - 1) / kVChunk);
+}
+
+__global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __restrict__ tg,
+                                                             const int64_t* __restrict__ ov,
+                                                             const int64_t* __restrict__ off,
+                                                             const int64_t* __restrict__ us, int64_t nu,
+                                                             const int64_t* __restrict__ ipre,
+                                                             unsigned long long* __restrict__ ctr,
+                                                             unsigned long long* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    ItemLds& L = *reinterpret_cast<ItemLds*>(lds_raw);
+    unsigned long long& item = L.item;
+    const int64_t total = ipre[nu];
+    unsigned long long acc = 0;
+    while (true) {
+        if (threadIdx.x == 0) item = atomicAdd(ctr, 1ULL);
+        __syncthreads();
+        const int64_t it = (int64_t)item;
+        __syncthreads();  // `item` is rewritten next round
+        if (it >= total) break;  // block-uniform
+        int64_t lo = 0, hi = nu;  // last q with ipre[q] <= it
+        while (hi - lo > 1) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (ipre[mid] <= it) lo = mid; else hi = mid;
+        }
+        const int64_t u = us[lo], b = off[u];
+        const int d = (int)(off[u + 1] - b);
+        const int nvc = (d + kVChunk - 1) / kVChunk;
+        const int local = (int)(it - ipre[lo]);
+        const int h0 = (local / nvc) * kBigChunk, v0 = (local % nvc) * kVChunk;
+        const int hn = min(kBigChunk, d - h0), vn = min(kVChunk, d - v0);
+        for (int k = threadIdx.x; k < kBigSlots; k += kBigBlock) L.hk[k] = kEmpty;
+        __syncthreads();
+        for (int k = threadIdx.x; k < hn; k += kBigBlock) hinsert(L.hk, L.hv, 12, tg[b + h0 + k], (uint64_t)ov[b + h0 + k]);
+        for (int k = threadIdx.x; k < vn; k += kBigBlock) {
+            const uint32_t v = tg[b + v0 + k];
+            const int64_t vo = off[v];
+            L.vl[k] = v;
+            L.vp[k] = (uint64_t)ov[b + v0 + k];
+            L.voff[k] = vo;
+            L.dv[k] = (uint32_t)(off[v + 1] - vo);
+        }
+        __syncthreads();
+        const uint32_t tw = big_scan(L.dv, L.pre, vn, L.wtot);
+        for (uint32_t f = threadIdx.x; f < tw; f += kBigBlock) {
+            const int i = seg_of(L.pre, vn, f);
+            const int64_t pos = L.voff[i] + (f - L.pre[i]);
+            const uint32_t w = tg[pos];
+            const int sl = hfind(L.hk, 12, w);
+            if (sl >= 0) acc += tri_weight(L.vp[i], (uint64_t)ov[pos], L.hv[sl]);
+        }
+        __syncthreads();
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+
 // u with 2 <= out-degree: small (<= 64) and big lists; also the 4-byte target array
 __global__ void k_tri_bins(const int64_t* __restrict__ off, int64_t n, uint8_t* __restrict__ fs,
                            uint8_t* __restrict__ fb) {
@@ -480,13 +559,22 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
         const int64_t sb = g.nsmall * part / nparts, se = g.nsmall * (part + 1) / nparts;
         const int64_t bb = g.nbig * part / nparts, be = g.nbig * (part + 1) / nparts;
         if (be > bb) {
-            const size_t lds = sizeof(BigLds);
-            HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_tri_big),
+            const int64_t nb = be - bb;
+            const int64_t* bu = P<int64_t>(g.big_u) + bb;
+            Buf ib = dev_alloc(sizeof(int64_t) * (2 * nb + 2), st);
+            int64_t* items = P<int64_t>(ib);
+            int64_t* ipre = items + nb;
+            hipLaunchKernelGGL(k_tri_items, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, P<int64_t>(g.off), bu,
+                               nb, items);
+            exclusive_scan_i64(items, ipre, nb, st);
+            Buf ctr = dev_alloc(sizeof(unsigned long long), st);
+            HIP_CHECK(hipMemsetAsync(P<void>(ctr), 0, sizeof(unsigned long long), st));
+            const size_t lds = sizeof(ItemLds);
+            HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_tri_big_items),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            const int64_t gb = std::min<int64_t>(be - bb, (int64_t)s->num_cus * 2);
-            hipLaunchKernelGGL(k_tri_big, dim3((unsigned)gb), dim3(kBigBlock), lds, st, P<uint32_t>(g.tg),
-                               P<int64_t>(g.ov), P<int64_t>(g.off), P<int64_t>(g.big_u) + bb, be - bb,
-                               P<unsigned long long>(out));
+            hipLaunchKernelGGL(k_tri_big_items, dim3((unsigned)(s->num_cus * 4)), dim3(kBigBlock), lds, st,
+                               P<uint32_t>(g.tg), P<int64_t>(g.ov), P<int64_t>(g.off), bu, nb, ipre,
+                               P<unsigned long long>(ctr), P<unsigned long long>(out));
         }
         if (se > sb) {
             const int64_t gs = std::min<int64_t>((se - sb + 3) / 4, (int64_t)s->num_cus * 16);
