@@ -285,6 +285,11 @@ SINGLE = {
 }
 
 
+# timer name -> kernel symbol (rocprofv3 / PMC summary name) where they differ
+SINGLE_SYMBOL = {"expand_filter": "k_expand_pairs", "part_scatter1": "k_scatter_c", "varlen_deg": "k_vl_deg",
+                 "varlen_w": "k_vl_w", "varlen_t": "k_vl_t", "varlen_rev": "k_vl_cand", "triangles": "k_tri_big_items"}
+
+
 def run_single(args):
     """C2 / C4 / C5 on one GPU: cold = the whole query from resident entity tables.
     value = matched rows / s; matched rows = the query's bindings (C2: result rows; C4: count(*);
@@ -348,7 +353,8 @@ def run_single(args):
     matched = res
     # algorithmic bytes per launch of the kernels whose traffic is a plain function of the input
     alg = {"bitmap_add": n * 8, "expand_filter": m * 16 + (2 * res * 8 if wl == "c2" else 0),
-           "tri_pack": m * 24, "part_scatter1": m * 24, "varlen_deg": m * 8, "varlen_w": m * 8, "varlen_t": m * 8}
+           "tri_pack": m * 24, "part_scatter1": m * 24, "varlen_deg": m * 8, "varlen_w": m * 8, "varlen_t": m * 8,
+           "varlen_rev": m * 24 + 3 * m * 8}  # target partition + filter walk + two candidate walks
     dom = max(kt, key=lambda k: kt[k][1])
     avg_ms = kt[dom][1] / kt[dom][0]
     b_alg = {"c2": 16 * m + int(0.75 * n) * 24 + 16 * (res or 0), "c4": 3 * 24 * m + 3 * 8 * n,
@@ -362,7 +368,8 @@ def run_single(args):
                    "rmat": [p / 100 for p in probs] + [round(1 - sum(probs) / 100, 2)], "seed": 42},
         "roofline": ({"bound": "hbm", "achieved": alg[dom] / (avg_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                       "unit": "GB/s", "frac": alg[dom] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                      "traffic": pmc_traffic("k_" + dom), "kernel": "k_" + dom, "kernel_ms": avg_ms,
+                      "traffic": pmc_traffic(SINGLE_SYMBOL.get(dom, "k_" + dom)),
+                      "kernel": SINGLE_SYMBOL.get(dom, "k_" + dom), "kernel_ms": avg_ms,
                       "alg_bytes_per_launch": alg[dom]} if dom in alg else None),
         "query": {"result": res, "matched_rows": matched, "alg_bytes_query": b_alg,
                   "query_frac_of_peak": b_alg / sec / 1e9 / HBM_PEAK_GBS,

@@ -306,8 +306,10 @@ __global__ void __launch_bounds__(kEpBlock) k_expand_pairs(const int64_t* __rest
 #pragma unroll
             for (int k = 0; k < kEpItems / 2; ++k) {
                 const int i = k * kEpBlock + (int)threadIdx.x;
-                const longlong2 sv = reinterpret_cast<const longlong2*>(src + t0)[i];
-                const longlong2 tv = reinterpret_cast<const longlong2*>(dst + t0)[i];
+                // streamed once: non-temporal, so the lines do not displace the bitmaps in L2
+                typedef long long v2i64 __attribute__((ext_vector_type(2)));
+                const v2i64 sv = __builtin_nontemporal_load(reinterpret_cast<const v2i64*>(src + t0) + i);
+                const v2i64 tv = __builtin_nontemporal_load(reinterpret_cast<const v2i64*>(dst + t0) + i);
                 s[2 * k] = sv.x; s[2 * k + 1] = sv.y; t[2 * k] = tv.x; t[2 * k + 1] = tv.y;
             }
         } else {
@@ -362,7 +364,7 @@ __global__ void __launch_bounds__(kEpBlock) k_expand_pairs(const int64_t* __rest
             if (keep[u]) {
                 const unsigned long long at = pos + __popcll(bal[u] & lt);
 #pragma unroll
-                for (int c = 0; c < NOUT; ++c) outs[c][at] = ((from_dst >> c) & 1u) ? t[u] : s[u];
+                for (int c = 0; c < NOUT; ++c) __builtin_nontemporal_store(((from_dst >> c) & 1u) ? t[u] : s[u], &outs[c][at]);
             }
             pos += __popcll(bal[u]);
         }

@@ -197,7 +197,7 @@ __device__ void walk_chunks(const ChunkWalk& cw, Visit visit, Flush flush) {
             const_cast<uint2*>(cw.pool + (size_t)phys * kCh), (short)0, (int)(fill * sizeof(uint2)), 0x00020000);
 #pragma unroll
         for (int k = 0; k < kItems / 2; ++k) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(k * kVlBlock + (int)threadIdx.x) * 16u, 0, 0);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(k * kVlBlock + (int)threadIdx.x) * 16u, 0, 2);  // nt
             pr[2 * k] = make_uint2(v[0], v[1]);
             pr[2 * k + 1] = make_uint2(v[2], v[3]);
         }

@@ -111,10 +111,11 @@ __device__ __forceinline__ void load_tile(const int64_t* __restrict__ src, const
 // slack so a tile may run past the last pair; callers mask items outside their range.
 template <int B, int N>
 __device__ __forceinline__ void load_pairs(const uint2* __restrict__ in, int64_t b, uint2 (&p)[N]) {
-    const uint4* __restrict__ v = reinterpret_cast<const uint4*>(in + b);
+    typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+    const v4u32* __restrict__ v = reinterpret_cast<const v4u32*>(in + b);
 #pragma unroll
-    for (int k = 0; k < N / 2; ++k) {
-        const uint4 x = v[k * B + (int)threadIdx.x];
+    for (int k = 0; k < N / 2; ++k) {  // streamed once: non-temporal, keeps the L2 for the bitmaps
+        const v4u32 x = __builtin_nontemporal_load(v + k * B + (int)threadIdx.x);
         p[2 * k] = make_uint2(x.x, x.y);
         p[2 * k + 1] = make_uint2(x.z, x.w);
     }
