@@ -305,8 +305,17 @@ def run_single(args):
         scale = args.scale
     cpu_scale = args.cpu_scale or cpu_scale
     n, m = 1 << scale, ef << scale
-    torch.cuda.set_device(0)
-    sess = Session(0)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and wl != "c4":
+        sys.exit("the C2 / C5 lines are single-GPU (SURVEY.md 8e: C5 needs per-hop frontier exchange, next)")
+    torch.cuda.set_device(local)
+    if world > 1:  # C4: replicated oriented graph, vertex shares per rank, one all-reduce
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    sess = Session(local)
     sess.set_stream(torch.cuda.current_stream().cuda_stream)
     rels = graph.rmat_rels(sess, scale, 0, m, probs, 42)
     kind = graph.NODES_PERSON if wl == "c2" else graph.NODES_ALL
@@ -323,7 +332,13 @@ def run_single(args):
             return out.size, out
         ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id")
         if wl == "c4":
-            return graph.triangle_count(sess, [rels], ok), None
+            if world == 1:
+                return graph.triangle_count(sess, [rels], ok), None
+            g = graph.TriGraph(sess, [rels], ok)
+            t = torch.tensor([g.count(rank, world)], dtype=torch.int64, device="cuda")
+            g.release()
+            dist.all_reduce(t)
+            return int(t.item()), None
         out = graph.var_length_count(sess, [rels], ok, ok, 1, 3)
         return None, out
 
@@ -335,12 +350,20 @@ def run_single(args):
     for k in kernels:  # reset
         _lib.call("capsmi_session_kernel_time", sess.handle, k.encode(), ctypes.byref(ctypes.c_int64()),
                   ctypes.byref(ctypes.c_double()))
+    if world > 1:
+        dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res, out = step()
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     sec = (time.perf_counter() - t0) / args.steps
+    if world > 1:
+        tt = torch.tensor([sec], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        sec = float(tt.item())
     kt = {}
     for k in kernels:
         c, ms = ctypes.c_int64(), ctypes.c_double()
@@ -360,9 +383,9 @@ def run_single(args):
     b_alg = {"c2": 16 * m + int(0.75 * n) * 24 + 16 * (res or 0), "c4": 3 * 24 * m + 3 * 8 * n,
              "c5": 3 * 24 * m + 2 * 8 * n + 16 * n}[wl]  # SURVEY.md 8d worked values
     line = {
-        "metric": f"matched rows/sec ({wl.upper()})", "value": matched / sec, "unit": "matched rows/s", "n_gpus": 1,
+        "metric": f"matched rows/sec ({wl.upper()})", "value": matched / sec, "unit": "matched rows/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": sec * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "int64",
         "data": "synthetic R-MAT (on-device counter-based generator, oracle/rmat.c definition)",
         "config": {"workload": desc, "scale": scale, "nodes": n, "relationships": m,
                    "rmat": [p / 100 for p in probs] + [round(1 - sum(probs) / 100, 2)], "seed": 42},
@@ -375,9 +398,12 @@ def run_single(args):
                   "query_frac_of_peak": b_alg / sec / 1e9 / HBM_PEAK_GBS,
                   "kernel_ms": {k: v[1] / v[0] for k, v in kt.items()}},
     }
-    line["cpu_baseline"] = None if args.no_cpu_baseline else cpu_baseline_single(wl, cpu_scale, ef, probs)
-    print(json.dumps(line), flush=True)
+    line["cpu_baseline"] = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_single(wl, cpu_scale, ef, probs)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
     sess.close()
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def cpu_baseline_single(wl, scale, ef, probs):
