@@ -158,6 +158,22 @@ __device__ __forceinline__ unsigned long long tri_weight(uint64_t puv, uint64_t 
     return m_uv * m_vw * m_wu + m_uw * m_wv * m_vu;
 }
 
+// last i in [lo, d) with pre[i] <= f, given pre[lo] <= f (pre[0] = 0)
+__device__ __forceinline__ int seg_from(const uint32_t* pre, int lo, int d, uint32_t f) {
+    int hi = d;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (pre[mid] <= f) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// segment cursor for a lane's increasing wedge indices: stays put while f is still inside the
+// current v's range (long out-lists), searches only the remaining segments otherwise
+__device__ __forceinline__ int seg_next(const uint32_t* pre, int i, int d, uint32_t f) {
+    return (i + 1 < d && pre[i + 1] <= f) ? seg_from(pre, i + 1, d, f) : i;
+}
+
 // last i in [0, d) with pre[i] <= f (pre[0] = 0)
 __device__ __forceinline__ int seg_of(const uint32_t* pre, int d, uint32_t f) {
     int lo = 0, hi = d;
@@ -216,8 +232,9 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        int i = 0;
         for (uint32_t f = lane; f < total; f += 64) {
-            const int i = seg_of(W.pre, d, f);
+            i = seg_next(W.pre, i, d, f);
             const int64_t pos = W.voff[i] + (f - W.pre[i]);
             const uint32_t w = tg[pos];
             const int sl = hfind(W.hk, 7, w);
@@ -389,8 +406,9 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
         }
         __syncthreads();
         const uint32_t tw = big_scan(L.dv, L.pre, vn, L.wtot);
+        int i = 0;
         for (uint32_t f = threadIdx.x; f < tw; f += kBigBlock) {
-            const int i = seg_of(L.pre, vn, f);
+            i = seg_next(L.pre, i, vn, f);
             const int64_t pos = L.voff[i] + (f - L.pre[i]);
             const uint32_t w = tg[pos];
             const int sl = hfind(L.hk, 12, w);
