@@ -119,6 +119,7 @@ __global__ void k_offsets(const uint64_t* __restrict__ ok_, int64_t ne, int64_t 
 // 1024-lane workgroup (their lists are taken in chunks when they exceed the LDS hash).
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr int kSmallDeg = 64;
+constexpr int kWedgeUnroll = 4;  // wedges per lane with their target loads in flight together
 constexpr int kSmallSlots = 128;
 constexpr int kTriBlock = 256;  // small: 4 waves
 constexpr int kBigBlock = 1024;
@@ -233,12 +234,24 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         int i = 0;
-        for (uint32_t f = lane; f < total; f += 64) {
-            i = seg_next(W.pre, i, d, f);
-            const int64_t pos = W.voff[i] + (f - W.pre[i]);
-            const uint32_t w = tg[pos];
-            const int sl = hfind(W.hk, 7, w);
-            if (sl >= 0) acc += tri_weight(W.vp[i], (uint64_t)ov[pos], W.hv[sl]);
+        for (uint32_t f0 = lane; f0 < total; f0 += kWedgeUnroll * 64) {
+            int ii[kWedgeUnroll];
+            int64_t pos[kWedgeUnroll];
+            uint32_t w[kWedgeUnroll];
+#pragma unroll
+            for (int k = 0; k < kWedgeUnroll; ++k) {
+                const uint32_t f = f0 + k * 64;
+                if (f < total) i = seg_next(W.pre, i, d, f);
+                ii[k] = i;
+                pos[k] = W.voff[i] + (f - W.pre[i]);
+                w[k] = f < total ? tg[pos[k]] : kEmpty;
+            }
+#pragma unroll
+            for (int k = 0; k < kWedgeUnroll; ++k) {
+                if (w[k] == kEmpty) continue;
+                const int sl = hfind(W.hk, 7, w[k]);
+                if (sl >= 0) acc += tri_weight(W.vp[ii[k]], (uint64_t)ov[pos[k]], W.hv[sl]);
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();  // the wave's LDS is reused for the next u
@@ -407,12 +420,25 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
         __syncthreads();
         const uint32_t tw = big_scan(L.dv, L.pre, vn, L.wtot);
         int i = 0;
-        for (uint32_t f = threadIdx.x; f < tw; f += kBigBlock) {
-            i = seg_next(L.pre, i, vn, f);
-            const int64_t pos = L.voff[i] + (f - L.pre[i]);
-            const uint32_t w = tg[pos];
-            const int sl = hfind(L.hk, 12, w);
-            if (sl >= 0) acc += tri_weight(L.vp[i], (uint64_t)ov[pos], L.hv[sl]);
+        for (uint32_t f0 = threadIdx.x; f0 < tw; f0 += kWedgeUnroll * kBigBlock) {
+            // kWedgeUnroll wedges per lane: all their target loads in flight before the probes
+            int ii[kWedgeUnroll];
+            int64_t pos[kWedgeUnroll];
+            uint32_t w[kWedgeUnroll];
+#pragma unroll
+            for (int k = 0; k < kWedgeUnroll; ++k) {
+                const uint32_t f = f0 + k * kBigBlock;
+                if (f < tw) i = seg_next(L.pre, i, vn, f);
+                ii[k] = i;
+                pos[k] = L.voff[i] + (f - L.pre[i]);
+                w[k] = f < tw ? tg[pos[k]] : kEmpty;
+            }
+#pragma unroll
+            for (int k = 0; k < kWedgeUnroll; ++k) {
+                if (w[k] == kEmpty) continue;
+                const int sl = hfind(L.hk, 12, w[k]);
+                if (sl >= 0) acc += tri_weight(L.vp[ii[k]], (uint64_t)ov[pos[k]], L.hv[sl]);
+            }
         }
         __syncthreads();
     }
