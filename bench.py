@@ -287,7 +287,7 @@ SINGLE = {
 
 # timer name -> kernel symbol (rocprofv3 / PMC summary name) where they differ
 SINGLE_SYMBOL = {"expand_filter": "k_expand_pairs", "part_scatter1": "k_scatter_c", "varlen_deg": "k_vl_deg",
-                 "varlen_w": "k_vl_w", "varlen_t": "k_vl_t", "varlen_rev": "k_vl_cand", "triangles": "k_tri_big_items"}
+                 "varlen_w": "k_vl_w", "varlen_t": "k_vl_t", "varlen_rev": "k_vl_bset", "varlen_recip": "k_vl_recip", "triangles": "k_tri_big_items"}
 
 
 def run_single(args):
@@ -343,7 +343,7 @@ def run_single(args):
         return None, out
 
     kernels = ("bitmap_add", "expand_filter", "tri_pack", "triangles", "part_scatter1", "varlen_deg", "varlen_w", "varlen_rev",
-               "varlen_t")
+               "varlen_recip", "varlen_t")
     for _ in range(args.warmup):
         step()
     _lib.call("capsmi_session_set_profiling", sess.handle, 1)
@@ -377,7 +377,7 @@ def run_single(args):
     # algorithmic bytes per launch of the kernels whose traffic is a plain function of the input
     alg = {"bitmap_add": n * 8, "expand_filter": m * 16 + (2 * res * 8 if wl == "c2" else 0),
            "tri_pack": m * 24, "part_scatter1": m * 24, "varlen_deg": m * 8, "varlen_w": m * 8, "varlen_t": m * 8,
-           "varlen_rev": m * 24 + 3 * m * 8}  # target partition + filter walk + two candidate walks
+           "varlen_rev": m * 24 + m * 8}  # target partition + filter walk
     dom = max(kt, key=lambda k: kt[k][1])
     avg_ms = kt[dom][1] / kt[dom][0]
     b_alg = {"c2": 16 * m + int(0.75 * n) * 24 + 16 * (res or 0), "c4": 3 * 24 * m + 3 * 8 * n,

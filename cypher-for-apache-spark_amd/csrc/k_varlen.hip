@@ -12,6 +12,8 @@
 //   len 2: sum_{r: a->b} od(b) - s(a) b_ok(a)
 //   len 3: sum_{r: a->b} [W(b) - (m(b,a) + s(b)) b_ok(b)] - s(a) (od(a) - 2 b_ok(a))
 // Four streaming passes over the relationship table plus one hash probe per relationship for m(b,a).
+#include <cstdlib>
+
 #include "part_common.h"
 
 namespace capsmi {
@@ -117,7 +119,6 @@ __global__ void k_final(int64_t n, Dom d, int lower, int upper, const unsigned l
 constexpr int kVlBits = 13;  // 8192 ids per slice: two 64 KiB LDS accumulator arrays
 constexpr int kVlIds = 1 << kVlBits;
 constexpr int kVlBlock = 1024;
-constexpr unsigned long long kEmpty = ~0ULL;
 
 __device__ __forceinline__ unsigned long long splitmix(unsigned long long x) {
     x += 0x9E3779B97F4A7C15ULL;
@@ -128,47 +129,72 @@ __device__ __forceinline__ unsigned long long splitmix(unsigned long long x) {
 
 __device__ __forceinline__ unsigned long long pkey(uint32_t s, uint32_t t) { return ((unsigned long long)s << 32) | t; }
 
-// exact (source, target) pair counts, open addressing, for the candidate pairs only
+// Exact (source, target) pair counts of the candidate pairs, open addressing, one 64-bit slot per
+// pair: bits 0..47 = (s << 24 | t) + 1 (ids < 2^24 - 1, so never 0 = empty), bits 48..63 = count
+// mod 2^16; a count that wraps adds 1 to ovf[slot] (units of 2^16) and raises *any_ovf.
+constexpr unsigned long long kKeyMask = (1ULL << 48) - 1;
+constexpr unsigned long long kCnt1 = 1ULL << 48;
+
 struct PairHash {
-    unsigned long long* key;
-    unsigned int* cnt;
+    unsigned long long* slot;
+    unsigned int* ovf;
+    unsigned int* any_ovf;
     unsigned long long mask;
 };
 
+__device__ __forceinline__ unsigned long long hkey(uint32_t s, uint32_t t) {
+    return (((unsigned long long)s << 24) | t) + 1;
+}
+
 __device__ __forceinline__ void pair_insert(const PairHash& h, unsigned long long k) {
     for (unsigned long long i = splitmix(k) & h.mask;; i = (i + 1) & h.mask) {
-        unsigned long long cur = h.key[i];
-        if (cur == kEmpty) {
-            cur = atomicCAS(&h.key[i], kEmpty, k);
-            if (cur == kEmpty) cur = k;
+        unsigned long long cur = h.slot[i];
+        if (cur == 0) {
+            cur = atomicCAS(&h.slot[i], 0ULL, k | kCnt1);
+            if (cur == 0) return;
         }
-        if (cur == k) {
-            atomicAdd(&h.cnt[i], 1u);
+        if ((cur & kKeyMask) == k) {
+            if ((atomicAdd(&h.slot[i], kCnt1) >> 48) == 0xFFFFu) {
+                atomicAdd(&h.ovf[i], 1u);
+                atomicOr(h.any_ovf, 1u);
+            }
             return;
         }
     }
 }
 
-__device__ __forceinline__ unsigned int pair_count(const PairHash& h, unsigned long long k) {
+__device__ __forceinline__ unsigned long long slot_count(const PairHash& h, unsigned long long i,
+                                                         unsigned long long v, bool ovf) {
+    return (v >> 48) + (ovf ? (unsigned long long)h.ovf[i] << 16 : 0ULL);
+}
+
+__device__ __forceinline__ unsigned long long pair_count(const PairHash& h, unsigned long long k, bool ovf) {
     for (unsigned long long i = splitmix(k) & h.mask;; i = (i + 1) & h.mask) {
-        const unsigned long long cur = h.key[i];
-        if (cur == k) return h.cnt[i];
-        if (cur == kEmpty) return 0u;
+        const unsigned long long cur = h.slot[i];
+        if ((cur & kKeyMask) == k) return slot_count(h, i, cur, ovf);
+        if (cur == 0) return 0;
     }
 }
 
-// One-bit filter of the directed pairs present, one region of 2^rshift bits per TARGET slice:
-// the bit of pair (s, t) lives in slice(t)'s region.  Walking the target partition sets a slice's
-// bits; the tests ask "does t -> s exist" for an s of the slice being walked in the source
-// partition, i.e. inside that slice's region -- L2-local either way.
+// One-bit filter of the directed pairs present, one region of 2^rshift bits per 2^(kVlBits -
+// sublog) TARGET ids (2^sublog regions per slice): the bit of pair (s, t) lives in t's region.
+// Walking the target partition sets a slice's regions; the tests ask "does t -> s exist" for an s
+// of the slice being walked in the source partition, i.e. inside that slice's regions -- L2-local
+// either way.  In every walk the region follows the pair's second (bucket) id.
 struct RegionBloom {
     uint32_t* w;
     unsigned long long rmask;  // bits per region - 1 (power of two)
-    int rshift;                // log2(bits per region)
+    int rshift;                // log2(bits per region), <= 20 (128 KiB of LDS)
+    int sublog;                // log2(regions per slice)
 };
 
-__device__ __forceinline__ unsigned long long rb_bit(const RegionBloom& b, int j, unsigned long long k) {
-    return ((unsigned long long)j << b.rshift) | (splitmix(k ^ 0x5DEECE66DULL) & b.rmask);
+__device__ __forceinline__ unsigned long long rb_bit(const RegionBloom& b, uint32_t y, unsigned long long k) {
+    return ((unsigned long long)(y >> (kVlBits - b.sublog)) << b.rshift) | (splitmix(k ^ 0x5DEECE66DULL) & b.rmask);
+}
+
+__device__ __forceinline__ bool rb_test(const RegionBloom& b, uint32_t y, unsigned long long k) {
+    const unsigned long long x = rb_bit(b, y, k);
+    return (b.w[x >> 5] >> (x & 31)) & 1u;
 }
 
 struct ChunkWalk {
@@ -244,11 +270,15 @@ __device__ __forceinline__ void flush_acc(unsigned long long* acc, unsigned long
 }
 
 // pass 1 (source partition, pair = (target, source)): od(v), s(v)
+// With a filter (bl.w) it also counts the pairs s -> t whose reverse t -> s may exist.
 __global__ void __launch_bounds__(kVlBlock) k_vl_deg(ChunkWalk cw, const uint32_t* __restrict__ bw, int b_full,
                                                      int64_t n, unsigned long long* __restrict__ od,
-                                                     unsigned long long* __restrict__ sl) {
+                                                     unsigned long long* __restrict__ sl, RegionBloom bl,
+                                                     unsigned long long* __restrict__ ncand) {
     extern __shared__ unsigned long long vl_lds[];
     unsigned long long *a_od = vl_lds, *a_s = vl_lds + kVlIds;
+    __shared__ unsigned int cand;
+    if (threadIdx.x == 0) cand = 0;
     for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_od[i] = a_s[i] = 0;
     __syncthreads();
     walk_chunks(
@@ -257,86 +287,116 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_deg(ChunkWalk cw, const uint32_
             const uint32_t t = p.x, s = p.y, i = s & (kVlIds - 1);
             if (bit_of(bw, b_full, t)) atomicAdd(&a_od[i], 1ULL);
             if (s == t) atomicAdd(&a_s[i], 1ULL);
+            if (bl.w && rb_test(bl, p.y, pkey(p.x, p.y))) atomicAdd(&cand, 1u);
         },
         [&](int j) {
             flush_acc(a_od, od, j, n);
             flush_acc(a_s, sl, j, n);
         });
+    if (bl.w && threadIdx.x == 0 && cand) atomicAdd(ncand, (unsigned long long)cand);
 }
 
 // pass 2: W(v) = sum_{v -> w} od(w)
+// It also inserts the candidate pairs s -> t (those whose reverse may exist) into h.
 __global__ void __launch_bounds__(kVlBlock) k_vl_w(ChunkWalk cw, int64_t n, const unsigned long long* __restrict__ od,
-                                                   unsigned long long* __restrict__ W) {
+                                                   unsigned long long* __restrict__ W, RegionBloom bl, PairHash h) {
     extern __shared__ unsigned long long vl_lds[];
     unsigned long long* a_w = vl_lds;
     for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_w[i] = 0;
     __syncthreads();
     walk_chunks(
         cw,
-        [&](uint2 p, int) {
+        [&](uint2 p, int) {  // p = (t, s)
             const unsigned long long x = od[p.x];
             if (x) atomicAdd(&a_w[p.y & (kVlIds - 1)], x);
+            if (rb_test(bl, p.y, pkey(p.x, p.y))) pair_insert(h, hkey(p.y, p.x));
         },
         [&](int j) { flush_acc(a_w, W, j, n); });
 }
 
-// target partition (pair = (source, target), j = slice(t)): mark pair (s, t) in region j.  The
-// region (<= 128 KiB) is built in LDS and ORed out once per slice segment.
-__global__ void __launch_bounds__(kVlBlock) k_vl_bset(ChunkWalk cw, RegionBloom bl) {
+// target partition (pair = (source, target), j = slice(t)): mark pair (s, t) in t's region.  Each
+// region (<= 128 KiB) is built in LDS, one pass over the block's chunks per region of the slice,
+// and stored whole into the block's partial slot (w + j) * 2^sublog + sub: the slots of a block are
+// distinct from every other block's (a later block's slices start at or after this block's last),
+// so no atomics; k_vl_bmerge ORs a region's partials.
+__global__ void __launch_bounds__(kVlBlock) k_vl_bset(ChunkWalk cw, RegionBloom bl, uint4* __restrict__ part) {
     extern __shared__ uint32_t rb_lds[];
-    const int rwords = 1 << (bl.rshift - 5);
+    const int rwords = 1 << (bl.rshift - 5), nsub = 1 << bl.sublog, rb = kVlBits - bl.sublog;
     for (int i = threadIdx.x; i < rwords; i += kVlBlock) rb_lds[i] = 0;
     __syncthreads();
-    walk_chunks(
-        cw,
-        [&](uint2 p, int) {
-            const unsigned long long x = splitmix(pkey(p.x, p.y) ^ 0x5DEECE66DULL) & bl.rmask;
-            atomicOr(&rb_lds[x >> 5], 1u << (x & 31));
-        },
-        [&](int j) {
-            uint32_t* g = bl.w + ((size_t)j << (bl.rshift - 5));
-            for (int i = threadIdx.x; i < rwords; i += kVlBlock) {
-                const uint32_t v = rb_lds[i];
-                if (v) atomicOr(&g[i], v);
-                rb_lds[i] = 0;
-            }
-        });
+    for (int sub = 0; sub < nsub; ++sub)
+        walk_chunks(
+            cw,
+            [&](uint2 p, int) {
+                if ((int)((p.y >> rb) & (nsub - 1)) != sub) return;
+                const unsigned long long x = splitmix(pkey(p.x, p.y) ^ 0x5DEECE66DULL) & bl.rmask;
+                atomicOr(&rb_lds[x >> 5], 1u << (x & 31));
+            },
+            [&](int j) {
+                uint4* g = part + ((((size_t)blockIdx.x + j) * nsub + sub) << (bl.rshift - 7));
+                const uint4* l = reinterpret_cast<const uint4*>(rb_lds);
+                for (int i = threadIdx.x; i < rwords / 4; i += kVlBlock) g[i] = l[i];
+                __syncthreads();
+                for (int i = threadIdx.x; i < rwords; i += kVlBlock) rb_lds[i] = 0;
+                __syncthreads();  // the next pass's first visits follow the last flush directly
+            });
 }
 
-// source partition: count (or insert) the pairs s -> t whose reverse t -> s may exist
-template <bool INSERT>
-__global__ void __launch_bounds__(kVlBlock) k_vl_cand(ChunkWalk cw, RegionBloom bl, PairHash h,
-                                                      unsigned long long* __restrict__ ncand) {
-    __shared__ unsigned int cand;
-    if (threadIdx.x == 0) cand = 0;
-    __syncthreads();
-    walk_chunks(
-        cw,
-        [&](uint2 p, int j) {  // p = (t, s), j = slice(s)
-            const unsigned long long x = rb_bit(bl, j, pkey(p.x, p.y));
-            if ((bl.w[x >> 5] >> (x & 31)) & 1u) {
-                if (INSERT) pair_insert(h, pkey(p.y, p.x));
-                else atomicAdd(&cand, 1u);
+// region r = j * 2^sublog + sub = OR of the partials of the blocks whose chunk share meets slice j
+__global__ void k_vl_bmerge(const int64_t* __restrict__ jst, int nt, int64_t blocks, const uint4* __restrict__ part,
+                            RegionBloom bl) {
+    const int64_t q4 = (int64_t)1 << (bl.rshift - 7);  // uint4 per region
+    const int64_t total = ((int64_t)nt << bl.sublog) * q4;
+    const int64_t per = max((jst[nt] + blocks - 1) / blocks, (int64_t)1);
+    uint4* w = reinterpret_cast<uint4*>(bl.w);
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = x / q4, i = x - r * q4, j = r >> bl.sublog, sub = r & ((1 << bl.sublog) - 1);
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (jst[j + 1] > jst[j]) {
+            const int64_t wl = (jst[j + 1] - 1) / per;
+            for (int64_t b = jst[j] / per; b <= wl && b < blocks; ++b) {
+                const uint4 u = part[((((size_t)b + j) << bl.sublog) + sub) * q4 + i];
+                v.x |= u.x;
+                v.y |= u.y;
+                v.z |= u.z;
+                v.w |= u.w;
             }
-        },
-        [&](int) {});
-    if (!INSERT && threadIdx.x == 0 && cand) atomicAdd(ncand, (unsigned long long)cand);
+        }
+        w[x] = v;
+    }
 }
 
-// Y(b) = W(b) - s(b) b_ok(b)
-__global__ void k_vl_y(int64_t n, const uint32_t* __restrict__ bw, int b_full, const unsigned long long* __restrict__ W,
-                       const unsigned long long* __restrict__ sl, long long* __restrict__ Y) {
+// (od(b), Y(b) = W(b) - s(b) b_ok(b)) side by side: pass 3 gathers both with one access
+__global__ void k_vl_y(int64_t n, const uint32_t* __restrict__ bw, int b_full, const unsigned long long* __restrict__ od,
+                       const unsigned long long* __restrict__ W, const unsigned long long* __restrict__ sl,
+                       longlong2* __restrict__ ody) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        Y[i] = (long long)W[i] - (bit_of(bw, b_full, (uint32_t)i) ? (long long)sl[i] : 0LL);
+        ody[i] = make_longlong2((long long)od[i],
+                                (long long)W[i] - (bit_of(bw, b_full, (uint32_t)i) ? (long long)sl[i] : 0LL));
 }
 
-// pass 3 (source partition): per relationship a -> b with a_ok(a): T2(a) += od(b);
-// T3(a) += Y(b) - m(b, a) b_ok(b), m(b, a) from a's slice table
+// R(a) = sum_b m(a, b) m(b, a) b_ok(b) over the candidate table (every pair with its reverse present
+// is in it, both ways): T3(a) -= R(a) for a_ok(a)
+__global__ void k_vl_recip(PairHash h, const uint32_t* __restrict__ aw, int a_full, const uint32_t* __restrict__ bw,
+                           int b_full, unsigned long long* __restrict__ T3) {
+    const bool ovf = *h.any_ovf != 0;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i <= h.mask;
+         i += (unsigned long long)gridDim.x * blockDim.x) {
+        const unsigned long long v = h.slot[i];
+        if (!v) continue;
+        const unsigned long long key = (v & kKeyMask) - 1;
+        const uint32_t a = (uint32_t)(key >> 24), b = (uint32_t)(key & 0xFFFFFF);
+        if (!bit_of(aw, a_full, a) || !bit_of(bw, b_full, b)) continue;
+        const unsigned long long r = pair_count(h, hkey(b, a), ovf);
+        if (r) atomicAdd(&T3[a], (unsigned long long)(-(long long)(slot_count(h, i, v, ovf) * r)));
+    }
+}
+
+// pass 3 (source partition): per relationship a -> b with a_ok(a): T2(a) += od(b); T3(a) += Y(b)
+// (the - m(b, a) b_ok(b) part is k_vl_recip's)
 __global__ void __launch_bounds__(kVlBlock) k_vl_t(ChunkWalk cw, const uint32_t* __restrict__ aw, int a_full,
-                                                   const uint32_t* __restrict__ bw, int b_full, int64_t n, RegionBloom bl,
-                                                   PairHash h,
-                                                   const unsigned long long* __restrict__ od,
-                                                   const long long* __restrict__ Y, unsigned long long* __restrict__ T2,
+                                                   int64_t n, const unsigned long long* __restrict__ od,
+                                                   const longlong2* __restrict__ ody, unsigned long long* __restrict__ T2,
                                                    unsigned long long* __restrict__ T3) {
     extern __shared__ unsigned long long vl_lds[];
     unsigned long long *a_t2 = vl_lds, *a_t3 = vl_lds + kVlIds;
@@ -344,17 +404,15 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_t(ChunkWalk cw, const uint32_t*
     __syncthreads();
     walk_chunks(
         cw,
-        [&](uint2 p, int j) {
+        [&](uint2 p, int) {
             const uint32_t b = p.x, a = p.y, i = a & (kVlIds - 1);
             if (!bit_of(aw, a_full, a)) return;
-            atomicAdd(&a_t2[i], od[b]);
-            if (Y) {
-                long long t3 = Y[b];
-                if (bit_of(bw, b_full, b)) {
-                    const unsigned long long x = rb_bit(bl, j, pkey(b, a));  // may b -> a exist?
-                    if ((bl.w[x >> 5] >> (x & 31)) & 1u) t3 -= (long long)pair_count(h, pkey(b, a));
-                }
-                atomicAdd(&a_t3[i], (unsigned long long)t3);  // two's complement sum
+            if (ody) {  // T3 also wanted
+                const longlong2 v = ody[b];
+                atomicAdd(&a_t2[i], (unsigned long long)v.x);
+                atomicAdd(&a_t3[i], (unsigned long long)v.y);  // two's complement sum
+            } else {
+                atomicAdd(&a_t2[i], od[b]);
             }
         },
         [&](int j) {
@@ -389,7 +447,7 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
     const bool need3 = upper >= 3;
     int64_t mtot = 0;
     for (int i = 0; i < nt; ++i) mtot += ms[i] > 0 ? ms[i] : 0;
-    if (n > 0 && n <= (int64_t(1) << 24) && mtot > 0) {
+    if (n > 0 && n < (int64_t(1) << 24) && mtot > 0) {  // hkey: ids < 2^24 - 1
         // source-sliced passes: relationships grouped by source slice, LDS accumulators
         part::Layout L{};
         L.lo = d.lo;
@@ -410,54 +468,72 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
         for (const void* f : {reinterpret_cast<const void*>(k_vl_deg), reinterpret_cast<const void*>(k_vl_w),
                               reinterpret_cast<const void*>(k_vl_t)})
             HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+        Buf ody, bw, hk, hc, cand;
+        RegionBloom bl{nullptr, 0, 0, 0};
+        PairHash h{nullptr, nullptr, nullptr, 0};
+        if (need3) {
+            // filter of the directed pairs: 8 bits per pair of an average region where a region of
+            // at most 128 KiB (LDS) allows; a slice gets 2^sublog regions only past 4 bits per pair
+            // (each region is one more pass of k_vl_bset: on C5, 4 bits/pair and 22% false
+            // candidates beat 2 regions by ~0.1 ms and 4 by ~0.3)
+            KernelTimer kt(s, "varlen_rev");
+            chunk_partition(s, srcs, dsts, ms, nt, false, L, s->num_cus, ct);
+            const int64_t per_slice = (mtot + L.nt - 1) / L.nt;
+            int sublog = 0, rshift = 10;
+            while (sublog < 3 && (int64_t(4) * per_slice >> sublog) > (int64_t(1) << 20)) ++sublog;
+            if (const char* e = getenv("CAPSMI_VL_SUBLOG")) sublog = atoi(e) < 0 ? 0 : (atoi(e) > 5 ? 5 : atoi(e));
+            while ((int64_t(1) << rshift) < (int64_t(8) * per_slice >> sublog) && rshift < 20) ++rshift;
+            const int64_t nreg = (int64_t)L.nt << sublog;
+            const size_t rbytes = (size_t(1) << rshift) / 8;
+            bw = dev_alloc(rbytes * nreg, st);
+            bl = RegionBloom{P<uint32_t>(bw), (unsigned long long)((int64_t(1) << rshift) - 1), rshift, sublog};
+            {
+                Buf part = dev_alloc(rbytes * (((size_t)ct.g2 + L.nt) << sublog), st);
+                const ChunkWalk tw{P<uint2>(ct.pool), P<unsigned long long>(ct.meta), ct.order, ct.jst, ct.segbase,
+                                   ct.ja, L.nt};
+                HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_vl_bset),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)rbytes));
+                hipLaunchKernelGGL(k_vl_bset, dim3((unsigned)ct.g2), dim3(kVlBlock), rbytes, st, tw, bl, P<uint4>(part));
+                hipLaunchKernelGGL(k_vl_bmerge, dim3(grid(s, (int64_t)(rbytes / 16) * nreg)), dim3(256), 0, st, ct.jst,
+                                   L.nt, ct.g2, P<uint4>(part), bl);
+            }
+            cand = dev_alloc(sizeof(int64_t), st);
+            HIP_CHECK(hipMemsetAsync(P<void>(cand), 0, sizeof(int64_t), st));
+        }
         {
             KernelTimer kt(s, "varlen_deg");
             hipLaunchKernelGGL(k_vl_deg, dim3(g), dim3(kVlBlock), lds2, st, cw, d.b, d.b_full, n, P<unsigned long long>(od),
-                               P<unsigned long long>(sl));
+                               P<unsigned long long>(sl), bl, need3 ? P<unsigned long long>(cand) : nullptr);
         }
-        Buf Y, bw, hk, hc, cand;
-        RegionBloom bl{nullptr, 0, 0};
-        PairHash h{nullptr, nullptr, 0};
         if (need3) {
-            {
-                KernelTimer kt(s, "varlen_w");
-                hipLaunchKernelGGL(k_vl_w, dim3(g), dim3(kVlBlock), lds2 / 2, st, cw, n, P<unsigned long long>(od),
-                                   P<unsigned long long>(W));
-            }
-            Y = dev_alloc(nb, st);
-            hipLaunchKernelGGL(k_vl_y, dim3(grid(s, n)), dim3(256), 0, st, n, d.b, d.b_full, P<unsigned long long>(W),
-                               P<unsigned long long>(sl), P<long long>(Y));
-            KernelTimer kt(s, "varlen_rev");
-            chunk_partition(s, srcs, dsts, ms, nt, false, L, s->num_cus, ct);
-            int rshift = 10;  // >= 8 bits per pair of an average slice, at most 128 KiB (LDS) per region
-            while ((int64_t(1) << rshift) < 8 * ((mtot + L.nt - 1) / L.nt) && rshift < 20) ++rshift;
-            const size_t bbytes = ((size_t)L.nt << rshift) / 8;
-            bw = dev_alloc(bbytes, st);
-            HIP_CHECK(hipMemsetAsync(P<void>(bw), 0, bbytes, st));
-            bl = RegionBloom{P<uint32_t>(bw), (unsigned long long)((int64_t(1) << rshift) - 1), rshift};
-            const ChunkWalk tw{P<uint2>(ct.pool), P<unsigned long long>(ct.meta), ct.order, ct.jst, ct.segbase, ct.ja,
-                               L.nt};
-            const size_t rlds = (size_t(1) << rshift) / 8;
-            HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_vl_bset),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)rlds));
-            hipLaunchKernelGGL(k_vl_bset, dim3((unsigned)ct.g2), dim3(kVlBlock), rlds, st, tw, bl);
-            cand = dev_alloc(sizeof(int64_t), st);
-            HIP_CHECK(hipMemsetAsync(P<void>(cand), 0, sizeof(int64_t), st));
-            hipLaunchKernelGGL(k_vl_cand<false>, dim3(g), dim3(kVlBlock), 0, st, cw, bl, h, P<unsigned long long>(cand));
             const int64_t nc = read_scalar(s, P<int64_t>(cand));
+            if (getenv("CAPSMI_VL_DEBUG"))
+                fprintf(stderr, "varlen: pairs %lld candidates %lld regions %d x 2^%d bits\n", (long long)mtot,
+                        (long long)nc, L.nt << bl.sublog, bl.rshift);
             int64_t cap = 1024;
             while (cap < 2 * nc) cap <<= 1;
             hk = dev_alloc(sizeof(unsigned long long) * cap, st);
-            hc = dev_alloc(sizeof(unsigned int) * cap, st);
-            HIP_CHECK(hipMemsetAsync(P<void>(hk), 0xFF, sizeof(unsigned long long) * cap, st));
-            HIP_CHECK(hipMemsetAsync(P<void>(hc), 0, sizeof(unsigned int) * cap, st));
-            h = PairHash{P<unsigned long long>(hk), P<unsigned int>(hc), (unsigned long long)(cap - 1)};
-            hipLaunchKernelGGL(k_vl_cand<true>, dim3(g), dim3(kVlBlock), 0, st, cw, bl, h, P<unsigned long long>(cand));
+            hc = dev_alloc(sizeof(unsigned int) * (cap + 1), st);
+            HIP_CHECK(hipMemsetAsync(P<void>(hk), 0, sizeof(unsigned long long) * cap, st));
+            HIP_CHECK(hipMemsetAsync(P<void>(hc), 0, sizeof(unsigned int) * (cap + 1), st));
+            h = PairHash{P<unsigned long long>(hk), P<unsigned int>(hc), P<unsigned int>(hc) + cap,
+                         (unsigned long long)(cap - 1)};
+            {
+                KernelTimer kt(s, "varlen_w");
+                hipLaunchKernelGGL(k_vl_w, dim3(g), dim3(kVlBlock), lds2 / 2, st, cw, n, P<unsigned long long>(od),
+                                   P<unsigned long long>(W), bl, h);
+            }
+            ody = dev_alloc(2 * nb, st);
+            hipLaunchKernelGGL(k_vl_y, dim3(grid(s, n)), dim3(256), 0, st, n, d.b, d.b_full, P<unsigned long long>(od),
+                               P<unsigned long long>(W), P<unsigned long long>(sl), P<longlong2>(ody));
+            KernelTimer kt(s, "varlen_recip");
+            hipLaunchKernelGGL(k_vl_recip, dim3(grid(s, cap)), dim3(256), 0, st, h, d.a, d.a_full, d.b, d.b_full,
+                               P<unsigned long long>(T3));
         }
         {
             KernelTimer kt(s, "varlen_t");
-            hipLaunchKernelGGL(k_vl_t, dim3(g), dim3(kVlBlock), lds2, st, cw, d.a, d.a_full, d.b, d.b_full, n, bl, h,
-                               P<unsigned long long>(od), need3 ? P<long long>(Y) : nullptr, P<unsigned long long>(T2),
+            hipLaunchKernelGGL(k_vl_t, dim3(g), dim3(kVlBlock), lds2, st, cw, d.a, d.a_full, n, P<unsigned long long>(od),
+                               need3 ? P<longlong2>(ody) : nullptr, P<unsigned long long>(T2),
                                P<unsigned long long>(T3));
         }
         HIP_CHECK(hipGetLastError());

@@ -4,7 +4,7 @@ import pytest
 
 from oracle import cpu
 
-pytestmark = pytest.mark.gpu
+
 
 
 def _table(session, src, dst):
@@ -28,6 +28,7 @@ def _check(session, n, src, dst, a_mask, b_mask, lo, hi, rels=None):
     assert got == want
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(6))
 def test_random_multigraphs(session, seed):
     rng = np.random.default_rng(seed)
@@ -42,6 +43,7 @@ def test_random_multigraphs(session, seed):
         _check(session, n, src, dst, a_mask, b_mask, lo, hi)
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("scale", [8, 11])
 def test_ldbc_shaped_rmat(session, scale):
     """C5 generator at small scale: R-MAT (0.45, 0.15, 0.15, 0.25), edge factor 32, all Person."""
@@ -53,6 +55,7 @@ def test_ldbc_shaped_rmat(session, scale):
     _check(session, n, src, dst, ones, ones, 1, 3, rels=[rels])
 
 
+@pytest.mark.gpu
 def test_split_rel_tables_union(session):
     rng = np.random.default_rng(9)
     n, m = 100, 2000
@@ -63,6 +66,7 @@ def test_split_rel_tables_union(session):
     _check(session, n, src, dst, ones, ones, 1, 3, rels=[t1, t2])
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("seed", [0, 1])
 def test_many_source_slices(session, seed):
     """Domain of several 8192-id source slices (LDS accumulators flushed per slice segment),
@@ -83,6 +87,7 @@ def test_many_source_slices(session, seed):
         _check(session, n, src, dst, a_mask, b_mask, lo, hi)
 
 
+@pytest.mark.gpu
 def test_large_domain_atomic_path(session):
     """n > 2^24 ids takes the atomic passes; the answer is the same."""
     rng = np.random.default_rng(3)
@@ -92,3 +97,102 @@ def test_large_domain_atomic_path(session):
     dst = rng.choice(nodes, m).astype(np.int64)
     ones = np.ones(n, dtype=bool)
     _check(session, n, src, dst, ones, ones, 1, 3)
+
+
+def _pair_paths(n, src, dst, a_mask, b_mask, lo, hi):
+    """Edge-distinct path counts per start node from (pair, multiplicity): a path over node pairs
+    p1..pk counts prod over uses of (m(p) - uses so far) -- parallel edges stay countable when one
+    pair holds 10^5 relationships (the enumeration oracle would walk every path)."""
+    from collections import Counter, defaultdict
+    mult = Counter(zip(src.tolist(), dst.tolist()))
+    out = defaultdict(list)
+    for (u, v), c in mult.items():
+        out[u].append((v, c))
+    got = {}
+    for a in range(n):
+        if not a_mask[a]:
+            continue
+        total = 0
+        stack = [(a, 0, 1, ())]
+        while stack:
+            v, depth, w, used = stack.pop()
+            for x, c in out.get(v, ()):
+                k = c - sum(1 for p in used if p == (v, x))
+                if k <= 0:
+                    continue
+                ww = w * k
+                if depth + 1 >= lo and b_mask[x]:
+                    total += ww
+                if depth + 1 < hi:
+                    stack.append((x, depth + 1, ww, used + ((v, x),)))
+        if total:
+            got[a] = total
+    return got
+
+
+@pytest.mark.gpu
+def test_pair_multiplicity_over_16_bits(session):
+    """A (source, target) pair with more than 2^16 parallel relationships and its reverse: the
+    candidate pair table's packed 16-bit count wraps into its overflow word."""
+    from capsmi import ColumnData, I64, graph
+    rng = np.random.default_rng(21)
+    n = 40
+    pairs = [(3, 7, 70_000), (7, 3, 5), (9, 9, 66_000), (3, 9, 2), (9, 3, 65_537)]
+    src = [rng.integers(0, n, 400)]
+    dst = [rng.integers(0, n, 400)]
+    for u, v, c in pairs:
+        src.append(np.full(c, u))
+        dst.append(np.full(c, v))
+    src, dst = np.concatenate(src).astype(np.int64), np.concatenate(dst).astype(np.int64)
+    perm = rng.permutation(len(src))
+    src, dst = src[perm], dst[perm]
+    a_mask = np.ones(n, dtype=bool)
+    b_mask = rng.random(n) < 0.8
+    b_mask[[3, 7, 9]] = True
+    for lo, hi in [(1, 3), (3, 3)]:
+        rels = [_table(session, src, dst)]
+        a_ok = graph.NodeBitmap(session, 0, n).add_scan(session.table([ColumnData("id", I64, np.arange(n))]))
+        b_ok = graph.NodeBitmap(session, 0, n).add_scan(session.table([ColumnData("id", I64, np.nonzero(b_mask)[0])]))
+        out = graph.var_length_count(session, rels, a_ok, b_ok, lo, hi, "a", "cnt")
+        got = dict(zip(out.column("a").values.tolist(), out.column("cnt").values.tolist()))
+        assert got == _pair_paths(n, src, dst, a_mask, b_mask, lo, hi)
+
+
+def test_pair_paths_helper_matches_enumeration():
+    """The multiplicity-aware helper above agrees with the enumeration oracle on small multigraphs."""
+    rng = np.random.default_rng(5)
+    n, m = 12, 60
+    src = rng.integers(0, n, m).astype(np.int64)
+    dst = rng.integers(0, n, m).astype(np.int64)
+    src[:6] = dst[:6]
+    a_mask = rng.random(n) < 0.8
+    b_mask = rng.random(n) < 0.7
+    for lo, hi in [(1, 1), (1, 3), (2, 3), (3, 3)]:
+        _, g = cpu.var_length_count(n, src, dst, lo, hi, a_mask.astype(np.uint8), b_mask.astype(np.uint8))
+        want = {int(i): int(g[i]) for i in np.nonzero(g)[0]}
+        assert _pair_paths(n, src, dst, a_mask, b_mask, lo, hi) == want
+
+
+@pytest.mark.gpu
+def test_sliced_path_top_ids(session):
+    """Domain of 2^24 - 1 ids (the largest the sliced passes take): ids near the top of the packed
+    24-bit pair keys."""
+    rng = np.random.default_rng(4)
+    n, m = (1 << 24) - 1, 20_000
+    nodes = np.concatenate([rng.integers(0, n, 2000), np.arange(n - 40, n)])
+    src = rng.choice(nodes, m).astype(np.int64)
+    dst = rng.choice(nodes, m).astype(np.int64)
+    k = m // 4
+    src[k:2 * k], dst[k:2 * k] = dst[:k].copy(), src[:k].copy()
+    src[-50:] = dst[-50:] = n - 1
+    ones = np.ones(n, dtype=bool)
+    _check(session, n, src, dst, ones, ones, 1, 3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sublog", [1, 3])
+def test_filter_sub_regions(session, monkeypatch, sublog):
+    """Several filter regions per slice (one k_vl_bset pass each, partials ORed by k_vl_bmerge),
+    forced through CAPSMI_VL_SUBLOG: same answer."""
+    monkeypatch.setenv("CAPSMI_VL_SUBLOG", str(sublog))
+    test_many_source_slices(session, 0)
