@@ -7,7 +7,9 @@
 // Errors surface as status codes + a thread-local message, mapping the okapi exceptions.
 #include <algorithm>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <unordered_map>
 #include <unordered_set>
 
 #include "capsmi_impl.h"
@@ -43,16 +45,119 @@ static thread_local std::string g_err;
     throw Error(e == hipErrorOutOfMemory ? CAPSMI_ERR_OUT_OF_MEMORY : CAPSMI_ERR_DEVICE, msg);
 }
 
+// Device blocks are recycled per stream: a freed block goes to its stream's free list and the
+// next request of the same size class on that stream takes it back.  Stream order keeps that safe
+// (everything that used the block was queued before whatever reuses it), and it takes the
+// hipMallocAsync / hipFreeAsync calls -- 0.1-0.2 ms of host time each for the multi-GiB layout
+// buffers, during which the device idles -- out of every query after the first.  The lists are
+// trimmed when an allocation fails, when the cached bytes pass CAPSMI_CACHE_BYTES (default 1/4 of
+// the device) and when a session is destroyed.
+namespace {
+
+struct BlockCache {
+    std::mutex mu;
+    std::unordered_map<hipStream_t, std::multimap<size_t, void*>> free;
+    size_t cached = 0, cap = 0;
+};
+
+BlockCache& block_cache() {
+    static BlockCache* c = new BlockCache();  // never destroyed: DevBufs may die during exit
+    return *c;
+}
+
+size_t size_class(size_t b) {  // <= 12.5% above the request
+    if (b <= 4096) return 4096;
+    size_t p = size_t(1) << (63 - __builtin_clzll(b));
+    const size_t step = p / 8;
+    return (b + step - 1) / step * step;
+}
+
+size_t cache_cap() {
+    BlockCache& c = block_cache();
+    static std::once_flag once;
+    std::call_once(once, [&] {
+        size_t fr = 0, tot = 0;
+        if (const char* e = getenv("CAPSMI_CACHE_BYTES")) c.cap = std::max<size_t>(1, strtoull(e, nullptr, 10));
+        else c.cap = hipMemGetInfo(&fr, &tot) == hipSuccess && tot ? tot / 4 : (size_t(16) << 30);
+    });
+    return c.cap;
+}
+
+// free every cached block of stream st (all streams when st == nullptr and all == true); caller holds mu
+void trim_locked(BlockCache& c, hipStream_t st, bool all) {
+    for (auto it = c.free.begin(); it != c.free.end();) {
+        if (all || it->first == st) {
+            for (auto& kv : it->second) {
+                (void)hipFreeAsync(kv.second, it->first);
+                c.cached -= kv.first;
+            }
+            it = c.free.erase(it);
+        } else {
+            ++it;
+        }
+    }
+}
+
+}  // namespace
+
 DevBuf::~DevBuf() {
-    if (ptr) (void)hipFreeAsync(ptr, stream);
+    if (!ptr) return;
+    BlockCache& c = block_cache();
+    std::lock_guard<std::mutex> g(c.mu);
+    auto& fl = c.free[stream];
+    fl.emplace(bytes, ptr);
+    c.cached += bytes;
+    while (c.cached > cache_cap() && !fl.empty()) {  // evict this (live) stream's largest blocks
+        auto last = std::prev(fl.end());
+        (void)hipFreeAsync(last->second, stream);
+        c.cached -= last->first;
+        fl.erase(last);
+    }
 }
 
 Buf dev_alloc(size_t bytes, hipStream_t stream) {
     auto b = std::make_shared<DevBuf>();
-    b->bytes = bytes ? bytes : 8;
+    const size_t want = size_class(bytes ? bytes : 8);
     b->stream = stream;
-    HIP_CHECK(hipMallocAsync(&b->ptr, b->bytes, stream));
+    BlockCache& c = block_cache();
+    (void)cache_cap();  // sized on the first allocation, not inside a destructor
+    {
+        std::lock_guard<std::mutex> g(c.mu);
+        auto f = c.free.find(stream);
+        if (f != c.free.end()) {
+            auto it = f->second.lower_bound(want);
+            if (it != f->second.end() && it->first <= want + want / 4) {
+                b->ptr = it->second;
+                b->bytes = it->first;
+                c.cached -= it->first;
+                f->second.erase(it);
+                return b;
+            }
+        }
+    }
+    b->bytes = want;
+    hipError_t e = hipMallocAsync(&b->ptr, want, stream);
+    if (e == hipErrorOutOfMemory) {  // give the cached blocks back and try once more
+        (void)hipGetLastError();
+        (void)hipDeviceSynchronize();
+        {
+            std::lock_guard<std::mutex> g(c.mu);
+            trim_locked(c, nullptr, true);
+        }
+        (void)hipDeviceSynchronize();
+        e = hipMallocAsync(&b->ptr, want, stream);
+    }
+    if (e != hipSuccess) {
+        b->ptr = nullptr;
+        HIP_CHECK(e);
+    }
     return b;
+}
+
+void release_cached_blocks(hipStream_t st) {
+    BlockCache& c = block_cache();
+    std::lock_guard<std::mutex> g(c.mu);
+    trim_locked(c, st, false);
 }
 
 }  // namespace capsmi
@@ -285,6 +390,8 @@ capsmi_status capsmi_session_destroy(capsmi_session* s) {
     if (!s) return CAPSMI_OK;
     use_device(s);
     (void)hipStreamSynchronize(s->stream);
+    (void)hipStreamSynchronize(s->own_stream);
+    release_cached_blocks(s->own_stream);
     (void)hipStreamSynchronize(s->own_stream);
     (void)hipHostFree(s->pinned);
     (void)hipStreamDestroy(s->own_stream);
