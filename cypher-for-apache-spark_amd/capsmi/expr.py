@@ -5,8 +5,9 @@ restricted to what SparkSQLExprMapper maps for the pattern-matching path
 (spark-cypher/src/main/scala/org/opencypher/spark/impl/SparkSQLExprMapper.scala:81-312):
 column references (a Var / Property / HasLabel / HasType resolves to a physical column of the
 RecordHeader, :97-105), literals and parameters (:86-92, :111-117), Equals (:120), Not (:121),
-IsNull / IsNotNull (:122-123), Ands / Ors (:132-136), In (:138-145), < <= > >= (:147-150) and
-Add / Subtract / Multiply.
+IsNull / IsNotNull (:122-123), Ands / Ors (:132-136), In (:138-145), < <= > >= (:147-150),
+Add / Subtract / Multiply, and the id-tag vocabulary BitwiseAnd / BitwiseOr / ShiftLeft /
+ShiftRightUnsigned (:264-274) and CaseExpr (:283-298).
 
 ``compile_program`` lowers a tree to the postfix ``capsmi_expr`` program of include/capsmi.h.
 """
@@ -24,8 +25,10 @@ TYPE_NAMES = {I64: "I64", BOOL: "BOOL", F64: "F64", STR: "STR"}
 # expression opcodes (include/capsmi.h CAPSMI_X_*)
 X_COL, X_LIT, X_NULL, X_EQ, X_NEQ, X_LT, X_LE, X_GT, X_GE, X_NOT, X_AND, X_OR = range(12)
 X_ISNULL, X_ISNOTNULL, X_IN, X_ADD, X_SUB, X_MUL, X_NEG, X_COALESCE = range(12, 20)
+X_BITAND, X_BITOR, X_SHL, X_SHRU, X_CASE = range(20, 25)
 
-BIN_OPS = {"=": X_EQ, "<>": X_NEQ, "<": X_LT, "<=": X_LE, ">": X_GT, ">=": X_GE, "+": X_ADD, "-": X_SUB, "*": X_MUL}
+BIN_OPS = {"=": X_EQ, "<>": X_NEQ, "<": X_LT, "<=": X_LE, ">": X_GT, ">=": X_GE, "+": X_ADD, "-": X_SUB, "*": X_MUL,
+           "&": X_BITAND, "|": X_BITOR, "<<": X_SHL, ">>>": X_SHRU}
 
 
 class Expr:
@@ -114,6 +117,14 @@ class Coalesce(Expr):
     args: Tuple[Expr, ...]
 
 
+@dataclass(frozen=True, eq=False)
+class Case(Expr):
+    """CaseExpr (okapi-ir Expr.scala; SparkSQLExprMapper.scala:283-298): the value of the first
+    alternative whose predicate is TRUE, else ``default`` (NULL when None)."""
+    alternatives: Tuple[Tuple[Expr, Expr], ...]
+    default: object = None
+
+
 TRUE = Lit(True)
 FALSE = Lit(False)
 NULL = Lit(None)
@@ -147,6 +158,9 @@ def columns_of(e: Expr) -> set:
             for x in v:
                 if isinstance(x, Expr):
                     out |= columns_of(x)
+                elif isinstance(x, tuple):  # Case alternatives
+                    for y in x:
+                        out |= columns_of(y)
     return out
 
 
@@ -215,6 +229,15 @@ def compile_program(e: Expr, column_index: Callable[[str], int], encode_str: Cal
             for a in x.args:
                 go(a)
             out.append((X_COALESCE, len(x.args), 0, 0))
+        elif isinstance(x, Case):
+            if not x.alternatives:
+                go(x.default if x.default is not None else NULL)
+                return
+            for p, v in x.alternatives:
+                go(p)
+                go(v)
+            go(x.default if x.default is not None else NULL)
+            out.append((X_CASE, len(x.alternatives), 0, 0))
         else:
             raise NotImplementedError(f"expression {x!r}")
 

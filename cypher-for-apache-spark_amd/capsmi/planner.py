@@ -134,10 +134,14 @@ class ScanGraph:
     """Entity tables of one graph: one node table per label combination, one rel table per type
     (CAPSScanGraphFactory.scala:52-103), scanned like ScanGraph.scanOperator."""
 
-    def __init__(self, backend, nodes: List[EntityTable], rels: List[EntityTable]):
+    def __init__(self, backend, nodes: List[EntityTable], rels: List[EntityTable], tags=frozenset({0})):
         self.backend = backend
         self.nodes = nodes
         self.rels = rels
+        self.tags = frozenset(tags)  # graph tags its ids carry (RelationalCypherGraph.tags)
+
+    def entity_tables(self):
+        return self.nodes, self.rels
 
     @staticmethod
     def from_property_graph(backend, pg: PropertyGraph) -> "ScanGraph":
@@ -220,6 +224,56 @@ class ScanGraph:
     def _empty(self, schema):
         return self.backend.table([ColumnData(n, ty, np.zeros(0, dtype=np.float64 if ty == F64 else np.int64))
                                    for n, ty in schema])
+
+
+class UnionGraph:
+    """UNION ALL of graphs (okapi-relational/.../impl/graph/UnionGraph.scala:41-80): each member's
+    ids (node id; relationship id, source and target -- RecordHeader.idExpressions) are retagged by
+    its replacement map so the members' ids are disjoint, the scans are aligned and union'ed, and
+    the union is deduplicated on the scanned entity (``Distinct(..., Set(targetEntity))``, :77).
+    The retagging is a device ``withColumns`` of Tags.ExprTagging's CaseExpr, as retagVariable
+    (RelationalPlanner.scala:332-335) plans it."""
+
+    def __init__(self, backend, graphs_to_replacements):
+        if not graphs_to_replacements:
+            raise PlanningError("Union requires at least one graph")
+        self.backend = backend
+        self.members = list(graphs_to_replacements)  # [(graph, {from: to})]
+        self.tags = frozenset(t for _, rep in self.members for t in rep.values())
+
+    @staticmethod
+    def union_all(backend, *graphs) -> "UnionGraph":
+        """RelationalCypherGraphFactory.unionGraph(graphs*) (RelationalCypherGraph.scala:52-55)."""
+        from .tagging import compute_retaggings
+        keyed = {i: g.tags for i, g in enumerate(graphs)}
+        rep = compute_retaggings(keyed)
+        return UnionGraph(backend, [(g, rep[i]) for i, g in enumerate(graphs)])
+
+    def entity_tables(self):
+        from .tagging import expr_replace_tags
+        nodes, rels = [], []
+        for g, rep in self.members:
+            moves = {f: t for f, t in rep.items() if f != t}
+            gn, gr = g.entity_tables()
+            for et in gn + gr:
+                keys = [et.id_col] + ([et.src_col, et.dst_col] if et.kind == "rel" else [])
+                tab = et.table if not moves else et.table.withColumns(
+                    *[(expr_replace_tags(Col(c), rep), c) for c in keys])
+                (nodes if et.kind == "node" else rels).append(
+                    EntityTable(et.kind, et.labels, et.props, tab, et.id_col, et.src_col, et.dst_col))
+        return nodes, rels
+
+    def _flat(self) -> ScanGraph:
+        nodes, rels = self.entity_tables()
+        return ScanGraph(self.backend, nodes, rels, self.tags)
+
+    def node_scan(self, var: str, labels: Sequence[str]):
+        out, header = self._flat().node_scan(var, labels)
+        return out.distinct(*header), header
+
+    def rel_scan(self, var: str, types: Sequence[str]):
+        out, header = self._flat().rel_scan(var, types)
+        return out.distinct(*header), header
 
 
 # ---------------------------------------------------------------------------------------------

@@ -230,6 +230,36 @@ KeyCols key_cols(const capsmi_table* t, const std::vector<int>& idx) {
     return k;
 }
 
+// Grouping keys of any width (nulls compare equal, as groupBy / dropDuplicates treat them): keys
+// beyond kMaxKeys are folded 8 at a time into a dense group-id column -- rows agree on the first
+// columns iff their group ids agree -- which then joins the next columns.  `hold` keeps the
+// folded columns alive while the returned KeyCols is in use.
+KeyCols group_key_cols(capsmi_session* s, const capsmi_table* t, const std::vector<int>& idx, std::vector<Buf>& hold) {
+    if ((int)idx.size() <= kMaxKeys) return key_cols(t, idx);
+    KeyCols k;
+    size_t next = 0;
+    const int64_t* folded = nullptr;
+    while (true) {
+        k.n = 0;
+        if (folded) {
+            k.data[k.n] = folded;
+            k.valid[k.n++] = nullptr;
+        }
+        while (k.n < kMaxKeys && next < idx.size()) {
+            k.data[k.n] = t->cols[idx[next]].d();
+            k.valid[k.n++] = t->cols[idx[next++]].v();
+        }
+        for (int i = k.n; i < kMaxKeys; ++i) k.data[i] = nullptr, k.valid[i] = nullptr;
+        if (next == idx.size()) return k;
+        HashTable ht;
+        Buf sor, gid, rep;
+        hash_build(s, k, t->nrows, /*skip_null_keys=*/false, ht, sor);
+        (void)hash_group_ids(s, ht, sor, t->nrows, gid, rep);
+        hold.push_back(gid);
+        folded = P<int64_t>(gid);
+    }
+}
+
 bool types_joinable(int a, int b) {
     const bool na = a == CAPSMI_I64 || a == CAPSMI_F64, nb = b == CAPSMI_I64 || b == CAPSMI_F64;
     return a == b || (na && nb);
@@ -777,7 +807,8 @@ static capsmi_status distinct_impl(capsmi_table* t, const std::vector<int>& keys
     use_device(s);
     HashTable ht;
     Buf sor, gid, rep;
-    hash_build(s, key_cols(t, keys), t->nrows, /*skip_null_keys=*/false, ht, sor);
+    std::vector<Buf> hold;
+    hash_build(s, group_key_cols(s, t, keys, hold), t->nrows, /*skip_null_keys=*/false, ht, sor);
     const int64_t ng = hash_group_ids(s, ht, sor, t->nrows, gid, rep);
     auto* o = new_table(s, ng);
     gather_into(o, t, rep, ng, false);
@@ -789,7 +820,6 @@ capsmi_status capsmi_distinct(capsmi_table* t, capsmi_table** out) {
     if (!t || !out) { set_err("null argument"); return CAPSMI_ERR_ILLEGAL_ARGUMENT; }
     std::vector<int> keys;
     for (size_t i = 0; i < t->cols.size(); ++i) keys.push_back((int)i);
-    if (keys.size() > (size_t)kMaxKeys) { set_err("distinct over more than 8 columns"); return CAPSMI_ERR_NOT_IMPLEMENTED; }
     return distinct_impl(t, keys, out);
 }
 
@@ -819,7 +849,8 @@ capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, 
     HashTable ht;
     Buf sor;
     if (nby > 0) {
-        hash_build(s, key_cols(t, keys), n, /*skip_null_keys=*/false, ht, sor);
+        std::vector<Buf> hold;
+        hash_build(s, group_key_cols(s, t, keys, hold), n, /*skip_null_keys=*/false, ht, sor);
         ng = hash_group_ids(s, ht, sor, n, gid, rep);
     } else {
         ng = 1;  // global aggregate: exactly one row, also over empty input (Spark)

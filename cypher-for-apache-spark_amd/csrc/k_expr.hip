@@ -8,7 +8,9 @@
 //   - NOT NULL = NULL; AND: any FALSE -> FALSE, else any NULL -> NULL; OR dually;
 //   - x IN (..): TRUE on a match, else NULL if x or any element is NULL, else FALSE;
 //   - Filter keeps a row iff the value is TRUE (SparkTable.scala:65-67; pinned by
-//     PredicateBehaviour.scala:131-149).
+//     PredicateBehaviour.scala:131-149);
+//   - bitwise and shift operators on Long (the id-tag expressions of Tags.scala:101-123), NULL in ->
+//     NULL out; CASE takes the first alternative whose predicate is TRUE (a NULL predicate is not).
 #include "capsmi_impl.h"
 
 namespace capsmi {
@@ -144,6 +146,31 @@ __device__ Val eval_row(const capsmi_expr* __restrict__ prog, int nn, const ColP
                 st[sp++] = res;
                 break;
             }
+            case CAPSMI_X_BITAND: case CAPSMI_X_BITOR: case CAPSMI_X_SHL: case CAPSMI_X_SHRU: {
+                const Val b = st[--sp], a = st[--sp];
+                if (a.t != CAPSMI_I64 || b.t != CAPSMI_I64) { st[sp++] = mk_null(); break; }
+                const uint64_t ua = (uint64_t)a.b, ub = (uint64_t)b.b;
+                uint64_t r2;
+                switch (x.op) {
+                    case CAPSMI_X_BITAND: r2 = ua & ub; break;
+                    case CAPSMI_X_BITOR: r2 = ua | ub; break;
+                    case CAPSMI_X_SHL: r2 = ua << (ub & 63); break;  // Java long shift semantics
+                    default: r2 = ua >> (ub & 63); break;
+                }
+                st[sp++] = Val{(int64_t)r2, (int8_t)CAPSMI_I64};
+                break;
+            }
+            case CAPSMI_X_CASE: {
+                const int base = sp - (2 * x.arg + 1);
+                Val res = st[sp - 1];  // default
+                for (int k = x.arg - 1; k >= 0; --k) {  // the first TRUE predicate wins
+                    const Val p = st[base + 2 * k];
+                    if (p.t == CAPSMI_BOOL && p.b != 0) res = st[base + 2 * k + 1];
+                }
+                sp = base;
+                st[sp++] = res;
+                break;
+            }
             default: st[sp++] = mk_null(); break;
         }
     }
@@ -185,6 +212,18 @@ int32_t infer_type(const capsmi_table* t, int32_t nn, const capsmi_expr* prog) {
                 st.push_back((a == CAPSMI_F64 || b == CAPSMI_F64) ? CAPSMI_F64 : CAPSMI_I64);
                 break;
             }
+            case CAPSMI_X_BITAND: case CAPSMI_X_BITOR: case CAPSMI_X_SHL: case CAPSMI_X_SHRU:
+                pop(); pop(); st.push_back(CAPSMI_I64); break;
+            case CAPSMI_X_CASE: {
+                int ty = pop();  // default, then the values (predicates are BOOL)
+                for (int k = 0; k < x.arg; ++k) {
+                    const int v = pop();
+                    pop();
+                    if (v >= 0) ty = v;
+                }
+                st.push_back(ty);
+                break;
+            }
             default: pop(); pop(); st.push_back(CAPSMI_BOOL); break;
         }
     }
@@ -210,7 +249,11 @@ void validate_program(const capsmi_table* t, int32_t nn, const capsmi_expr* prog
                 pops = x.arg; break;
             case CAPSMI_X_IN: REQUIRE(x.arg >= 0, CAPSMI_ERR_ILLEGAL_ARGUMENT, "IN arity"); pops = x.arg + 1; break;
             case CAPSMI_X_EQ: case CAPSMI_X_NEQ: case CAPSMI_X_LT: case CAPSMI_X_LE: case CAPSMI_X_GT: case CAPSMI_X_GE:
-            case CAPSMI_X_ADD: case CAPSMI_X_SUB: case CAPSMI_X_MUL: pops = 2; break;
+            case CAPSMI_X_ADD: case CAPSMI_X_SUB: case CAPSMI_X_MUL:
+            case CAPSMI_X_BITAND: case CAPSMI_X_BITOR: case CAPSMI_X_SHL: case CAPSMI_X_SHRU: pops = 2; break;
+            case CAPSMI_X_CASE:
+                REQUIRE(x.arg >= 1, CAPSMI_ERR_ILLEGAL_ARGUMENT, "CASE needs >= 1 alternative");
+                pops = 2 * x.arg + 1; break;
             default: throw Error(CAPSMI_ERR_NOT_IMPLEMENTED, "unknown expression op " + std::to_string(x.op));
         }
         REQUIRE(depth >= pops, CAPSMI_ERR_ILLEGAL_ARGUMENT, "malformed expression program (stack underflow)");

@@ -94,7 +94,13 @@ enum {
     CAPSMI_X_SUB = 16,
     CAPSMI_X_MUL = 17,
     CAPSMI_X_NEG = 18,
-    CAPSMI_X_COALESCE = 19 /* pop `arg` operands, push the first non-null */
+    CAPSMI_X_COALESCE = 19, /* pop `arg` operands, push the first non-null */
+    CAPSMI_X_BITAND = 20,   /* Long a & b (SparkSQLExprMapper.scala:264-265) */
+    CAPSMI_X_BITOR = 21,    /* Long a | b (:267-268) */
+    CAPSMI_X_SHL = 22,      /* Long a << (b & 63) (:270-271, functions.shiftLeft) */
+    CAPSMI_X_SHRU = 23,     /* Long a >>> (b & 63) (:273-274, functions.shiftRightUnsigned) */
+    CAPSMI_X_CASE = 24      /* stack [p1, v1, .., p_arg, v_arg, default]: v_i of the first TRUE p_i, else
+                               default (push a NULL for none); CaseExpr, :283-298 */
 };
 
 typedef struct {

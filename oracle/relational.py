@@ -369,6 +369,13 @@ def evaluate(e, t: NumpyTable):
                 a, b = lv.astype(np.int64), rv.astype(np.int64)
                 res = a + b if e.op == "+" else (a - b if e.op == "-" else a * b)
             return I64, res, m
+        if e.op in ("&", "|", "<<", ">>>"):  # Long only (SparkSQLExprMapper.scala:264-274)
+            if lt != I64 or rt != I64:
+                return I64, np.zeros(n, np.int64), np.zeros(n, bool)
+            a, b = lv.astype(np.int64).view(np.uint64), rv.astype(np.int64).view(np.uint64)
+            sh = b & np.uint64(63)  # Java long shift count
+            res = {"&": lambda: a & b, "|": lambda: a | b, "<<": lambda: a << sh, ">>>": lambda: a >> sh}[e.op]()
+            return I64, res.view(np.int64), m
         numeric = lt in (I64, F64) and rt in (I64, F64)
         if not numeric and lt != rt:
             return BOOL, np.zeros(n, np.int64), np.zeros(n, bool)
@@ -426,6 +433,23 @@ def evaluate(e, t: NumpyTable):
             valid |= m
             if ty >= 0:
                 ty_out = ty
+        return ty_out, vals, valid
+    if name == "Case":  # first TRUE alternative, else default (SparkSQLExprMapper.scala:283-298)
+        if e.default is not None:
+            ty_out, vals, valid = evaluate(e.default, t)
+            vals, valid = vals.copy(), valid.copy()
+        else:
+            ty_out, vals, valid = -1, np.zeros(n, np.int64), np.zeros(n, dtype=bool)
+        for p, v in reversed(e.alternatives):
+            _, pv, pm = evaluate(p, t)
+            vt, vv, vm = evaluate(v, t)
+            take = pm & (pv != 0)
+            if vals.dtype != vv.dtype:
+                vals = vals.astype(vv.dtype)
+            vals = np.where(take, vv, vals)
+            valid = np.where(take, vm, valid)
+            if vt >= 0:
+                ty_out = vt
         return ty_out, vals, valid
     if name == "Neg":
         ty, v, m = evaluate(e.arg, t)

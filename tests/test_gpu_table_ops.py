@@ -144,3 +144,20 @@ def test_errors_map_to_okapi_exceptions(session):
         t.limit(1 << 40)
     with pytest.raises(IllegalArgumentException):
         t.join(t, "inner", ("a", "a"))  # columns not disjoint
+
+
+@pytest.mark.parametrize("ncols", [9, 17])
+def test_wide_distinct_and_group(session, ncols):
+    """More key columns than one hash key holds (8): the keys are folded into group ids 8 at a
+    time; nulls still compare equal (dropDuplicates / groupBy)."""
+    from capsmi import ColumnData, I64
+    from oracle.relational import NumpyBackend
+    rng = np.random.default_rng(ncols)
+    n = 4000
+    cols = [ColumnData(f"c{i}", I64, rng.integers(0, 2, n), rng.random(n) >= 0.1) for i in range(ncols)]
+    g, o = session.table(cols), NumpyBackend(session.dictionary).table(cols)
+    _same(g.distinct(), o.distinct())
+    names = [c.name for c in cols]
+    _same(g.distinct(*names[1:]), o.distinct(*names[1:]))
+    aggs = [("count_star", None, False, "n"), ("sum", "c0", False, "s")]
+    _same(g.group(names[1:], aggs), o.group(names[1:], aggs))
