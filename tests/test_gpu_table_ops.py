@@ -158,6 +158,7 @@ def test_wide_distinct_and_group(session, ncols):
     g, o = session.table(cols), NumpyBackend(session.dictionary).table(cols)
     _same(g.distinct(), o.distinct())
     names = [c.name for c in cols]
-    _same(g.distinct(*names[1:]), o.distinct(*names[1:]))
+    keys = names[1:]  # dropDuplicates keeps an arbitrary row per key: compare the keys only
+    _same(g.distinct(*keys).select(*keys), o.distinct(*keys).select(*keys))
     aggs = [("count_star", None, False, "n"), ("sum", "c0", False, "s")]
-    _same(g.group(names[1:], aggs), o.group(names[1:], aggs))
+    _same(g.group(keys, aggs), o.group(keys, aggs))
