@@ -480,7 +480,7 @@ class Planner:
         t = joined.select(*(lhs.header + new_cols))
         return _Op(t, lhs.header + new_cols, rhs.node_vars, rhs.rel_vars)
 
-    def _match(self, cur: Optional[_Op], pattern: str, where, varlen: Dict[str, int]) -> _Op:
+    def _match(self, cur: Optional[_Op], pattern: str, where, varlen: Dict[str, int], unique: bool = True) -> _Op:
         paths = parse_pattern(pattern, self.names)
         clause_rels: List[RelPat] = []
         pending = list(paths)
@@ -490,9 +490,10 @@ class Planner:
             idx = next((i for i, p in enumerate(pending) if any(isinstance(e, NodePat) and e.var in bound for e in p)), 0)
             path = pending.pop(idx)
             cur = self._path(cur, path, clause_rels, varlen)
-        # uniqueness among single-length relationships of this clause
+        # uniqueness among single-length relationships of this clause (a MATCH clause only: the
+        # front-end's rewrite does not reach pattern predicates / EXISTS)
         preds = []
-        singles = [r for r in clause_rels if r.var_length is None]
+        singles = [r for r in clause_rels if r.var_length is None] if unique else []
         for i in range(len(singles)):
             for j in range(i + 1, len(singles)):
                 a, b = singles[i], singles[j]
@@ -502,16 +503,60 @@ class Planner:
                     continue  # the front-end skips pairs that can never be equal
                 preds.append(Not(eq(Col(a.var), Col(b.var))))
         for a in singles:
-            for b in clause_rels:
+            for b in (clause_rels if unique else []):
                 if b.var_length is not None and not (a.types and b.types and not (set(a.types) & set(b.types))):
                     raise PlanningError("uniqueness between a single and a var-length relationship is "
                                         "not supported by CAPS (NotImplementedException)")
+        helper: List[str] = []
         if where is not None:
+            cur, where = self._lower_exists(cur, where, varlen, helper)
             preds.append(to_expr(where, cur.header))
         pred = ands(*preds)
         if not (isinstance(pred, Lit) and pred.value is True):
             cur.table = cur.table.filter(pred)
+        if helper:
+            cur.table = cur.table.drop(*helper)
+            cur.header = [h for h in cur.header if h not in helper]
         return cur
+
+    def _lower_exists(self, cur: _Op, spec, varlen: Dict[str, int], helper: List[str]):
+        """Replace every ``["exists", pattern, where?]`` in an expression spec by a BOOL column
+        planned as an ExistsSubQuery; returns (op, spec)."""
+        if not isinstance(spec, list) or not spec:
+            return cur, spec
+        if spec[0] == "exists":
+            cur, col = self._exists(cur, spec[1], spec[2] if len(spec) > 2 else None, varlen)
+            helper.append(col)
+            return cur, ["var", col]
+        out = [spec[0]]
+        for s in spec[1:]:
+            cur, s = self._lower_exists(cur, s, varlen, helper)
+            out.append(s)
+        return cur, out
+
+    def _exists(self, cur: Optional[_Op], pattern: str, where, varlen: Dict[str, int]):
+        """EXISTS(pattern) / a pattern predicate (RelationalPlanner.scala:181-202): the pattern is
+        planned on top of the input, its rows are reduced to the distinct bindings of the variables
+        the input already has (renamed apart), left-outer-joined back, and IsNotNull of a join
+        column is the predicate."""
+        if cur is None:
+            raise PlanningError("EXISTS needs bound variables")
+        lhs = cur
+        rhs = self._match(_Op(cur.table, list(cur.header), set(cur.node_vars), list(cur.rel_vars)), pattern, where,
+                          dict(varlen), unique=False)
+        join_vars = [h for h in lhs.header
+                     if h in lhs.node_vars or h in lhs.rel_vars or not any(c in h for c in ".:#")]
+        if not join_vars:
+            raise PlanningError("EXISTS needs bound variables")
+        renames = [(v, self.names.fresh("ex")) for v in join_vars]
+        right = rhs.table.select(*join_vars)
+        for v, tmp in renames:
+            right = right.withColumnRenamed(v, tmp)
+        right = right.distinct()
+        col = self.names.fresh("exists")
+        joined = lhs.table.join(right, "left_outer", *renames)
+        t = joined.withColumns((IsNotNull(Col(renames[0][1])), col)).select(*(lhs.header + [col]))
+        return _Op(t, lhs.header + [col], lhs.node_vars, lhs.rel_vars), col
 
     def _path(self, cur: Optional[_Op], path: List[object], clause_rels: List[RelPat],
               varlen: Dict[str, int]) -> _Op:
@@ -683,7 +728,11 @@ class Planner:
 
     # ---- RETURN ---------------------------------------------------------------------------------
     def _return(self, cur: _Op, ret: dict, varlen: Dict[str, int]):
-        items = ret["items"]
+        items = []
+        for alias, spec in ret["items"]:
+            if spec and spec[0] not in AGGS and spec[0] != "rels":
+                cur, spec = self._lower_exists(cur, spec, varlen, [])
+            items.append((alias, spec))
         t = cur.table
         plain, aggs, outs = [], [], []
         computed = []

@@ -15,6 +15,8 @@ the reference:
     from every relationship bound before the expand (VarLengthExpandPlanner.scala:83-136)
   - uniqueness: NOT(r_i = r_j) for single-length relationships of one MATCH with overlapping types
   - WHERE: three-valued logic, a row survives only if TRUE
+  - EXISTS(pattern): some extension of the row's binding matches the pattern (its var-length first
+    hop, like any, avoids the relationships already bound) (RelationalPlanner.scala:181-202)
 """
 from __future__ import annotations
 
@@ -97,6 +99,9 @@ def eval_expr(spec, b: dict, g: Graph):
         if any(h == 0 for h in hits):
             return True
         return None if any(h is None for h in hits) else False
+    if op == "exists":  # some extension of b matches the pattern (and its WHERE)
+        sub = {"clauses": [{"match": spec[1], "where": spec[2] if len(spec) > 2 else None, "unique": False}]}
+        return bool(match(g, sub, rows=[b], names=_SubNames()))
     if op in ("+", "-", "*"):
         a, c = eval_expr(spec[1], b, g), eval_expr(spec[2], b, g)
         if a is None or c is None:
@@ -105,10 +110,19 @@ def eval_expr(spec, b: dict, g: Graph):
     raise ValueError(f"expression {spec!r}")
 
 
-def match(g: Graph, query: dict) -> List[dict]:
-    names = _Names()
-    rows: List[dict] = [dict()]
-    bound_rels_order: List[str] = []
+class _SubNames(_Names):
+    """fresh names of an EXISTS pattern, apart from the outer query's"""
+    _n = 0
+
+    def fresh(self, kind: str) -> str:
+        _SubNames._n += 1
+        return f"_x{kind}{_SubNames._n}"
+
+
+def match(g: Graph, query: dict, rows: Optional[List[dict]] = None, names: Optional[_Names] = None) -> List[dict]:
+    names = names or _Names()
+    rows = rows if rows is not None else [dict()]
+    bound_rels_order: List[str] = [v for v in (rows[0] if rows else {}) if rows[0].get("__kind_" + v) == "rel"]
     for clause in query["clauses"]:
         optional = "optional_match" in clause
         pattern = clause["optional_match"] if optional else clause["match"]
@@ -118,7 +132,7 @@ def match(g: Graph, query: dict) -> List[dict]:
         # uniqueness (single-length, overlapping types)
         singles = []
         seen = set()
-        for r in clause_rels:
+        for r in (clause_rels if clause.get("unique", True) else []):  # no uniqueness inside EXISTS
             if r.var_length is None and r.var not in seen:
                 seen.add(r.var)
                 singles.append(r)

@@ -1,0 +1,78 @@
+"""The relational lowering (capsmi.planner over a Table backend) against the brute-force enumerator
+(oracle/enumerate.py) on random small multigraphs with labels, types, null properties and
+self-loops: expand, undirected expand, expand-into, var-length, OPTIONAL MATCH and EXISTS.  The
+numpy restatement of the Table operators runs on CPU; the device operators behind the GPU mark."""
+import numpy as np
+import pytest
+
+from golden_util import same_rows
+
+BACKENDS = ["numpy", pytest.param("gpu", marks=pytest.mark.gpu)]
+
+ID = lambda v: ["id", v]  # noqa: E731
+V = lambda v: ["prop", v, "v"]  # noqa: E731
+
+QUERIES = [
+    {"clauses": [{"match": "(a)-[r]->(b)"}], "return": {"items": [["a", ID("a")], ["r", ID("r")], ["b", ID("b")]]}},
+    {"clauses": [{"match": "(a:A)-[:R]->(b)-[:S]->(c)", "where": ["<", V("a"), V("c")]}],
+     "return": {"items": [["a", ID("a")], ["b", ID("b")], ["c", ID("c")]]}},
+    {"clauses": [{"match": "(a)-[r]-(b)"}], "return": {"items": [["a", ID("a")], ["r", ID("r")], ["b", ID("b")]]}},
+    {"clauses": [{"match": "(a)-->(b)-->(c)-->(a)"}], "return": {"items": [["n", ["count*"]]]}},
+    {"clauses": [{"match": "(a:A)-[*1..3]->(b)"}], "return": {"items": [["a", ID("a")], ["n", ["count*"]]]}},
+    {"clauses": [{"match": "(a:A)"}, {"optional_match": "(a)-[:R]->(b:B)"}],
+     "return": {"items": [["a", ID("a")], ["b", ID("b")]]}},
+    {"clauses": [{"match": "(a)-->(b)", "where": ["exists", "(a)-->()-->(b)"]}],
+     "return": {"items": [["a", ID("a")], ["b", ID("b")]]}},
+    {"clauses": [{"match": "(a)"}],
+     "return": {"items": [["a", ID("a")], ["e", ["exists", "(a)-[:S]->(x:B)", [">", V("x"), V("a")]]]]}},
+    {"clauses": [{"match": "(a)-[r:R]->(b)", "where": ["not", ["exists", "(b)-[*1..2]->(a)"]]}],
+     "return": {"items": [["a", ID("a")], ["r", ID("r")]]}},
+    {"clauses": [{"match": "(a)-->(b)"}, {"match": "(b)-->(c)", "where": ["<>", ID("a"), ID("c")]}],
+     "return": {"items": [["b", ID("b")], ["n", ["count*"]]]}},
+]
+
+
+def _graph(seed):
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(3, 9))
+    nodes = []
+    for i in range(n):
+        labels = [l for l in ("A", "B") if rng.random() < 0.5]
+        props = {} if rng.random() < 0.2 else {"v": int(rng.integers(0, 5))}
+        nodes.append({"id": i, "labels": labels, "props": props})
+    m = int(rng.integers(0, 3 * n))
+    rels = []
+    for j in range(m):
+        s, d = int(rng.integers(0, n)), int(rng.integers(0, n))
+        if rng.random() < 0.15:
+            d = s  # self-loop
+        rels.append({"id": n + j, "src": s, "dst": d, "type": "R" if rng.random() < 0.6 else "S", "props": {}})
+    return {"nodes": nodes, "rels": rels}
+
+
+@pytest.fixture
+def backend(request):
+    from capsmi.table import StringDictionary
+    if request.param == "numpy":
+        from oracle.relational import NumpyBackend
+        return NumpyBackend(StringDictionary())
+    s = request.getfixturevalue("session")
+    s.dictionary = StringDictionary()
+    return s
+
+
+@pytest.mark.parametrize("backend", BACKENDS, indirect=True)
+@pytest.mark.parametrize("seed", range(12))
+def test_planner_matches_enumeration(backend, seed):
+    from capsmi.planner import PGNode, PGRel, Planner, PropertyGraph, ScanGraph, result_rows
+    from oracle import enumerate as en
+    g = _graph(seed)
+    pg = PropertyGraph([PGNode(x["id"], frozenset(x["labels"]), dict(x["props"])) for x in g["nodes"]],
+                       [PGRel(r["id"], r["src"], r["dst"], r["type"], dict(r["props"])) for r in g["rels"]])
+    graph = en.Graph(g)
+    for q in QUERIES:
+        sg = ScanGraph.from_property_graph(backend, pg)
+        table, outs = Planner(sg).run(q)
+        got = result_rows(table, outs, backend.dictionary)
+        want = en.project(graph, en.match(graph, q), q["return"])
+        assert same_rows(got, want), (q, got, want)
