@@ -489,7 +489,7 @@ class Planner:
             bound = cur.node_vars if cur else set()
             idx = next((i for i, p in enumerate(pending) if any(isinstance(e, NodePat) and e.var in bound for e in p)), 0)
             path = pending.pop(idx)
-            cur = self._path(cur, path, clause_rels, varlen)
+            cur = self._path(cur, path, clause_rels, varlen, where)
         # uniqueness among single-length relationships of this clause (a MATCH clause only: the
         # front-end's rewrite does not reach pattern predicates / EXISTS)
         preds = []
@@ -559,16 +559,22 @@ class Planner:
         return _Op(t, lhs.header + [col], lhs.node_vars, lhs.rel_vars), col
 
     def _path(self, cur: Optional[_Op], path: List[object], clause_rels: List[RelPat],
-              varlen: Dict[str, int]) -> _Op:
+              varlen: Dict[str, int], where=None) -> _Op:
         first: NodePat = path[0]
         if cur is None or first.var not in cur.node_vars:
             scan, header = self.g.node_scan(first.var, first.labels)
             op = _Op(scan, header, {first.var}, [])
             if cur is None:
                 cur = op
-            else:  # disconnected component: cartesian product (RelationalPlanner.scala:56-57)
-                cur = _Op(cur.table.join(op.table, "cross"), cur.header + op.header, cur.node_vars | op.node_vars,
-                          cur.rel_vars)
+            else:  # disconnected component: cartesian product (RelationalPlanner.scala:56-57) ...
+                vj = self._value_join_keys(cur, op, where)
+                if vj is None:
+                    t = cur.table.join(op.table, "cross")
+                else:  # ... or an equi-join on a WHERE equality across it (ValueJoin)
+                    (le, lk), (re_, rk) = vj
+                    t = cur.table.withColumns((le, lk)).join(op.table.withColumns((re_, rk)), "inner", (lk, rk))
+                    t = t.drop(lk, rk)
+                cur = _Op(t, cur.header + op.header, cur.node_vars | op.node_vars, cur.rel_vars)
         else:
             cur = self._bound_labels(cur, first)
         for k in range(1, len(path), 2):
@@ -584,6 +590,35 @@ class Planner:
             else:
                 cur = self._expand(cur, left, rel, right)
         return cur
+
+    def _value_join_keys(self, lhs: _Op, rhs: _Op, where):
+        """LogicalOptimizer.replaceCartesianWithValueJoin (LogicalOptimizer.scala:58-76): a WHERE
+        conjunct ``x = y`` whose sides are each a variable or a variable's property, one solved by
+        the product's left input and one by its right, turns the product into an equi-join on the
+        two expressions.  The conjunct stays in the filter (always true on the joined rows).  Only
+        key pairs the join can compare (same type, or both numeric) are taken."""
+        if where is None:
+            return None
+        conj = where[1:] if where[0] == "and" else [where]
+
+        def side(spec, op):
+            if not isinstance(spec, list) or not spec or spec[0] not in ("prop", "var", "id"):
+                return None
+            col = f"{spec[1]}.{spec[2]}" if spec[0] == "prop" else spec[1]
+            return col if spec[1] in op.header and col in op.header else None
+
+        ltypes, rtypes = lhs.table.columnType, rhs.table.columnType
+        for c in conj:
+            if not isinstance(c, list) or not c or c[0] != "=":
+                continue
+            for a, b in ((c[1], c[2]), (c[2], c[1])):
+                lc, rc = side(a, lhs), side(b, rhs)
+                if lc is None or rc is None:
+                    continue
+                lt, rt = ltypes[lc], rtypes[rc]
+                if lt == rt or (lt in (I64, F64) and rt in (I64, F64)):
+                    return (Col(lc), self.names.fresh("vjl")), (Col(rc), self.names.fresh("vjr"))
+        return None
 
     def _bound_labels(self, cur: _Op, n: NodePat) -> _Op:
         if not n.labels:

@@ -29,6 +29,10 @@ QUERIES = [
      "return": {"items": [["a", ID("a")], ["r", ID("r")]]}},
     {"clauses": [{"match": "(a)-->(b)"}, {"match": "(b)-->(c)", "where": ["<>", ID("a"), ID("c")]}],
      "return": {"items": [["b", ID("b")], ["n", ["count*"]]]}},
+    {"clauses": [{"match": "(a:A), (b:B)", "where": ["=", V("a"), V("b")]}],  # ValueJoin
+     "return": {"items": [["a", ID("a")], ["b", ID("b")]]}},
+    {"clauses": [{"match": "(a)-[r]->(c), (b)-->(d)", "where": ["and", ["=", V("b"), V("c")], ["<", V("a"), V("d")]]}],
+     "return": {"items": [["a", ID("a")], ["r", ID("r")], ["b", ID("b")], ["d", ID("d")]]}},
 ]
 
 
