@@ -70,10 +70,14 @@ def cpu_baseline(scale, ef):
                       f"count(DISTINCT c)={dist}, {dt:.2f} s"}
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary (profiles/*pmc*.json),
-    FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B reads at 64 B), or None."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this workload
+    (profiles/*_<workload>_pmc.json, newest round first), FETCH_SIZE doubled per MI355X_MICROARCH.md
+    (gfx950 tallies 128-B reads at 64 B), or None."""
+    if "+" in kernel:  # a timer spanning several kernels: their traffic summed
+        parts = [pmc_traffic(k, workload) for k in kernel.split("+")]
+        return None if any(p is None for p in parts) else sum(parts)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}_pmc.json")))
     for f in reversed(files):
         try:
             with open(f) as fh:
@@ -230,7 +234,7 @@ def main():
         dom = max(timed, key=lambda k: timed[k][1])
         avg_ms = timed[dom][1] / timed[dom][0]
         achieved = alg[dom] / (avg_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(KERNEL_SYMBOL[dom])
+        traffic = pmc_traffic(KERNEL_SYMBOL[dom], "c3")
         query_alg = 2 * 24 * m_total + 3 * 8 * n  # SURVEY.md §8d C3 B_alg (whole query, all ranks)
         line = {
             "metric": METRIC,
@@ -287,7 +291,7 @@ SINGLE = {
 
 # timer name -> kernel symbol (rocprofv3 / PMC summary name) where they differ
 SINGLE_SYMBOL = {"expand_filter": "k_expand_pairs", "part_scatter1": "k_scatter_c", "varlen_deg": "k_vl_deg",
-                 "varlen_w": "k_vl_w", "varlen_t": "k_vl_t", "varlen_rev": "k_vl_bset", "varlen_recip": "k_vl_recip", "triangles": "k_tri_big_items"}
+                 "varlen_w": "k_vl_w", "varlen_t": "k_vl_t", "varlen_rev": "k_vl_bset", "varlen_recip": "k_vl_recip", "triangles": "k_tri_big_items+k_tri_small"}
 
 
 def run_single(args):
@@ -331,10 +335,13 @@ def run_single(args):
             out = graph.expand_filter(sess, rels, a_ok, b_ok, ["source", "target"], ["a", "b"])
             return out.size, out
         ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id")
-        if wl == "c4":
-            if world == 1:
-                return graph.triangle_count(sess, [rels], ok), None
+        if wl == "c4":  # = graph.triangle_count: build the trigraph, count, release
             g = graph.TriGraph(sess, [rels], ok)
+            cache["oriented_edges"] = g.stats()[1]
+            if world == 1:
+                c = g.count()
+                g.release()
+                return c, None
             t = torch.tensor([g.count(rank, world)], dtype=torch.int64, device="cuda")
             g.release()
             dist.all_reduce(t)
@@ -377,7 +384,10 @@ def run_single(args):
     # algorithmic bytes per launch of the kernels whose traffic is a plain function of the input
     alg = {"bitmap_add": n * 8, "expand_filter": m * 16 + (2 * res * 8 if wl == "c2" else 0),
            "tri_pack": m * 24, "part_scatter1": m * 24, "varlen_deg": m * 8, "varlen_w": m * 8, "varlen_t": m * 8,
-           "varlen_rev": m * 24 + m * 8}  # target partition + filter walk
+           "varlen_rev": m * 24 + m * 8,  # target partition + filter walk
+           # both triangle kernels together: the oriented adjacency read once (8-B offsets, 4-B
+           # targets, 8-B multiplicity payload per oriented edge)
+           "triangles": n * 8 + 12 * cache.get("oriented_edges", 0)}
     dom = max(kt, key=lambda k: kt[k][1])
     avg_ms = kt[dom][1] / kt[dom][0]
     b_alg = {"c2": 16 * m + int(0.75 * n) * 24 + 16 * (res or 0), "c4": 3 * 24 * m + 3 * 8 * n,
@@ -391,7 +401,7 @@ def run_single(args):
                    "rmat": [p / 100 for p in probs] + [round(1 - sum(probs) / 100, 2)], "seed": 42},
         "roofline": ({"bound": "hbm", "achieved": alg[dom] / (avg_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                       "unit": "GB/s", "frac": alg[dom] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                      "traffic": pmc_traffic(SINGLE_SYMBOL.get(dom, "k_" + dom)),
+                      "traffic": pmc_traffic(SINGLE_SYMBOL.get(dom, "k_" + dom), wl),
                       "kernel": SINGLE_SYMBOL.get(dom, "k_" + dom), "kernel_ms": avg_ms,
                       "alg_bytes_per_launch": alg[dom]} if dom in alg else None),
         "query": {"result": res, "matched_rows": matched, "alg_bytes_query": b_alg,

@@ -125,6 +125,7 @@ _SIGS = {
     "capsmi_trigraph_build": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, PP]),
     "capsmi_trigraph_count": (c_int32, [P, P, c_int32, c_int32, POINTER(c_int64)]),
     "capsmi_trigraph_release": (c_int32, [P]),
+    "capsmi_trigraph_stats": (c_int32, [P, POINTER(c_int64), POINTER(c_int64)]),
     "capsmi_triangle_count": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, POINTER(c_int64)]),
     "capsmi_var_length_count": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, P, c_int32, c_int32, c_char_p,
                                           c_char_p, PP]),

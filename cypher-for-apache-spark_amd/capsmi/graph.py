@@ -137,6 +137,12 @@ class TriGraph:
         _lib.call("capsmi_trigraph_count", self.session.handle, self._h, part, nparts, ctypes.byref(v))
         return v.value
 
+    def stats(self):
+        """(id-domain size, oriented simple edges)"""
+        n, ne = ctypes.c_int64(), ctypes.c_int64()
+        _lib.call("capsmi_trigraph_stats", self._h, ctypes.byref(n), ctypes.byref(ne))
+        return n.value, ne.value
+
     def release(self) -> None:
         if self._h:
             _lib.call("capsmi_trigraph_release", self._h)

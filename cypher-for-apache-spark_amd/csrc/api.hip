@@ -1308,6 +1308,14 @@ capsmi_status capsmi_trigraph_count(capsmi_session* s, const capsmi_trigraph* g,
     API_END
 }
 
+capsmi_status capsmi_trigraph_stats(const capsmi_trigraph* g, int64_t* nodes, int64_t* oriented_edges) {
+    API_BEGIN
+    need(g, "trigraph");
+    if (nodes) *nodes = g->g.n;
+    if (oriented_edges) *oriented_edges = g->g.ne;
+    API_END
+}
+
 capsmi_status capsmi_trigraph_release(capsmi_trigraph* g) {
     API_BEGIN
     if (g) {

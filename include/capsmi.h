@@ -307,6 +307,8 @@ capsmi_status capsmi_trigraph_build(capsmi_session* s, int32_t nrels, capsmi_tab
                                     const char* dst_col, const capsmi_bitmap* n_ok, capsmi_trigraph** out);
 capsmi_status capsmi_trigraph_count(capsmi_session* s, const capsmi_trigraph* g, int32_t part, int32_t nparts,
                                     int64_t* out_rows);
+/* id-domain size and number of oriented (simple, both directions folded) edges of a trigraph */
+capsmi_status capsmi_trigraph_stats(const capsmi_trigraph* g, int64_t* nodes, int64_t* oriented_edges);
 capsmi_status capsmi_trigraph_release(capsmi_trigraph* g);
 capsmi_status capsmi_triangle_count(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
                                     const char* dst_col, const capsmi_bitmap* n_ok, int64_t* out_rows);
