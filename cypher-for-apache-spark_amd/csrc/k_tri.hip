@@ -298,61 +298,6 @@ __device__ uint32_t big_scan(const uint32_t* in, uint32_t* outp, int n, uint32_t
     return total;
 }
 
-struct BigLds {
-    uint32_t hk[kBigSlots];
-    uint64_t hv[kBigSlots];
-    uint64_t vp[kBigChunk];
-    int64_t voff[kBigChunk];
-    uint32_t vl[kBigChunk];
-    uint32_t dv[kBigChunk];
-    uint32_t pre[kBigChunk];
-    uint32_t wtot[kBigBlock / 64];
-};
-
-__global__ void __launch_bounds__(kBigBlock) k_tri_big(const uint32_t* __restrict__ tg, const int64_t* __restrict__ ov,
-                                                       const int64_t* __restrict__ off,
-                                                       const int64_t* __restrict__ us, int64_t nu,
-                                                       unsigned long long* __restrict__ out) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    BigLds& L = *reinterpret_cast<BigLds*>(lds_raw);
-    unsigned long long acc = 0;
-    for (int64_t q = blockIdx.x; q < nu; q += gridDim.x) {
-        const int64_t u = us[q];
-        const int64_t b = off[u];
-        const int d = (int)(off[u + 1] - b);
-        for (int h0 = 0; h0 < d; h0 += kBigChunk) {  // hash chunk of out(u)
-            const int hn = min(kBigChunk, d - h0);
-            for (int k = threadIdx.x; k < kBigSlots; k += kBigBlock) L.hk[k] = kEmpty;
-            __syncthreads();
-            for (int k = threadIdx.x; k < hn; k += kBigBlock)
-                hinsert(L.hk, L.hv, 12, tg[b + h0 + k], (uint64_t)ov[b + h0 + k]);
-            for (int v0 = 0; v0 < d; v0 += kBigChunk) {  // v chunk of out(u)
-                const int vn = min(kBigChunk, d - v0);
-                for (int k = threadIdx.x; k < vn; k += kBigBlock) {
-                    const uint32_t v = tg[b + v0 + k];
-                    const int64_t vo = off[v];
-                    L.vl[k] = v;
-                    L.vp[k] = (uint64_t)ov[b + v0 + k];
-                    L.voff[k] = vo;
-                    L.dv[k] = (uint32_t)(off[v + 1] - vo);
-                }
-                __syncthreads();
-                const uint32_t total = big_scan(L.dv, L.pre, vn, L.wtot);
-                for (uint32_t f = threadIdx.x; f < total; f += kBigBlock) {
-                    const int i = seg_of(L.pre, vn, f);
-                    const int64_t pos = L.voff[i] + (f - L.pre[i]);
-                    const uint32_t w = tg[pos];
-                    const int sl = hfind(L.hk, 12, w);
-                    if (sl >= 0) acc += tri_weight(L.vp[i], (uint64_t)ov[pos], L.hv[sl]);
-                }
-                __syncthreads();
-            }
-        }
-    }
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
-    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
-}
-
 // Big u are split into work items (hash chunk of out(u), chunk of kVChunk v's of out(u)) so a hub's
 // wedges spread over many workgroups; items are taken from a global counter (dynamic balance).
 constexpr int kVChunk = 256;
