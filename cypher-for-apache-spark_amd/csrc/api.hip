@@ -1339,7 +1339,8 @@ capsmi_status capsmi_relpart_size(const capsmi_relpart* p, int64_t* kept_rows) {
     API_BEGIN
     need(p, "relpart");
     need(kept_rows, "out");
-    *kept_rows = p->rp.kept;
+    use_device(p->sess);
+    *kept_rows = relpart_kept(p->sess, const_cast<capsmi_relpart*>(p)->rp);
     API_END
 }
 

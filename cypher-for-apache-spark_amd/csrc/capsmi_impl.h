@@ -210,9 +210,11 @@ struct PartLayout {
 struct RelPart {
     PartLayout L;
     Buf pairs;  // uint2 (source - lo, target - lo) per kept relationship, grouped by cell
-    Buf boff;   // int64 cell offsets (ncells + 1)
-    int64_t kept = 0;
+    Buf boff;   // int64 cell offsets (ncells + 1); boff[ncells] = kept
+    int64_t kept = 0;  // -1: on the device only (relpart_kept reads it)
+    int64_t rows = 0;  // relationships offered to the build (>= kept)
 };
+int64_t relpart_kept(capsmi_session* s, RelPart& rp);
 // hop 1 of a 2-hop run while the layout is built: M(t) |= a_ok(s) for s != t, a_ok self-loops ->
 // S1 (first) / S2 (second), target filter b_ok; outputs zeroed by the caller
 struct RelPartHop1 {

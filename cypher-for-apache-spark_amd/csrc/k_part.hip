@@ -398,20 +398,24 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
 }
 
 // One hop over the 2-D layout.  Block b streams relationships [b*per, (b+1)*per) of the
-// j-major cell order.
+// j-major cell order, per = max(ceil(kept / blocks), min_per); kept = coff[ncells] is read on the
+// device, so building the layout needs no host round trip.
 //   HOP1: M(t) |= a_ok(s) for s != t; self-loops (a_ok(s) and b_ok(t)) -> S1, second one -> S2.
 //         Target filter b_ok at flush.
 //   HOP2: C(t) |= X1(s) for s != t, X2(s) for s == t.  Target filter c_ok at flush.
 // `sb` is the per-relationship source bitmap (a_ok or X1); `tmask` the target filter.
 template <bool HOP1, bool SRC_FULL>
 __global__ void __launch_bounds__(kBlock) k_hop_2d(const uint2* __restrict__ pairs, const int64_t* __restrict__ coff,
-                                                   int64_t kept, int64_t per, Layout L, BitV sb,
+                                                   int64_t min_per, Layout L, BitV sb,
                                                    const uint32_t* __restrict__ X2, BitV tmask,
                                                    uint32_t* __restrict__ out, uint32_t* __restrict__ S1,
                                                    uint32_t* __restrict__ S2, int64_t gwords) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* tl = lds;                // target slice marks
     uint32_t* sl = lds + kSliceWords;  // source slice frontier (when pulled)
+    const int64_t kept = coff[L.ncells];
+    int64_t per = (kept + gridDim.x - 1) / gridDim.x;
+    if (per < min_per) per = min_per;
     int64_t e0 = (int64_t)blockIdx.x * per;
     const int64_t e1 = min(e0 + per, kept);
     if (e0 >= e1) return;  // block-uniform
@@ -629,8 +633,8 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
                            order, jst, segbase, ja, psum, P<int64_t>(rp.boff), L, P<uint2>(rp.pairs), mtot, ho);
     }
     HIP_CHECK(hipGetLastError());
-    HIP_CHECK(hipMemcpyAsync(&rp.kept, P<int64_t>(rp.boff) + L.ncells, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipStreamSynchronize(st));
+    rp.kept = -1;  // known on the device (boff[ncells]); read only when asked (relpart_kept)
+    rp.rows = mtot;
     if (h1 && !fuse) relpart_hop1(s, rp, h1->a, h1->b, h1->M, h1->S1, h1->S2);
 }
 
@@ -641,12 +645,14 @@ static void launch_hop(capsmi_session* s, const RelPart& rp, part::BitV sb, cons
     auto k = part::k_hop_2d<HOP1, SRC_FULL>;
     allow_lds(k, lds);
     // one 128 KiB-LDS block per CU at a time; a few rounds of blocks, equal relationship shares
-    const int64_t blocks = (int64_t)s->num_cus * 4;
-    int64_t per = (rp.kept + blocks - 1) / blocks;
-    if (per < part::kBlock * part::kUnroll) per = part::kBlock * part::kUnroll;
-    const int64_t g = (rp.kept + per - 1) / per;
-    hipLaunchKernelGGL(k, dim3((unsigned)g), dim3(part::kBlock), lds, s->stream, P<uint2>(rp.pairs),
-                       P<int64_t>(rp.boff), rp.kept, per, rp.L, sb, X2, tmask, out, S1, S2, gwords);
+    // (at least kBlock * kUnroll each; blocks past the end exit at once).  Grid sized from the upper
+    // bound of the kept count (the table rows), the exact count is read by the kernel.
+    const int64_t min_per = (int64_t)part::kBlock * part::kUnroll;
+    int64_t blocks = (int64_t)s->num_cus * 4;
+    const int64_t bound = rp.kept >= 0 ? rp.kept : rp.rows;
+    blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, (bound + min_per - 1) / min_per));
+    hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(part::kBlock), lds, s->stream, P<uint2>(rp.pairs),
+                       P<int64_t>(rp.boff), min_per, rp.L, sb, X2, tmask, out, S1, S2, gwords);
     HIP_CHECK(hipGetLastError());
 }
 
@@ -654,7 +660,7 @@ void relpart_hop1(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* a, 
                   uint32_t* S1, uint32_t* S2) {
     REQUIRE(a->lo == rp.L.lo && a->hi == rp.L.hi && b->lo == rp.L.lo && b->hi == rp.L.hi, CAPSMI_ERR_UNSUPPORTED,
             "partitioned 2-hop needs node scans over the layout's id domain");
-    if (rp.kept == 0) return;
+    if (rp.rows == 0) return;
     const part::BitV av{P<uint32_t>(a->words), a->full ? 1 : 0}, bv{P<uint32_t>(b->words), b->full ? 1 : 0};
     KernelTimer kt(s, "hop1");
     if (a->full)
@@ -667,10 +673,15 @@ void relpart_hop2(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* c, 
                   uint32_t* C) {
     REQUIRE(c->lo == rp.L.lo && c->hi == rp.L.hi, CAPSMI_ERR_UNSUPPORTED,
             "partitioned 2-hop needs node scans over the layout's id domain");
-    if (rp.kept == 0) return;
+    if (rp.rows == 0) return;
     const part::BitV xv{X1, 0}, cv{P<uint32_t>(c->words), c->full ? 1 : 0};
     KernelTimer kt(s, "hop2");
     launch_hop<false, false>(s, rp, xv, X2, cv, C, nullptr, nullptr, c->nwords);
+}
+
+int64_t relpart_kept(capsmi_session* s, RelPart& rp) {
+    if (rp.kept < 0) rp.kept = rp.rows > 0 ? read_scalar(s, P<int64_t>(rp.boff) + rp.L.ncells) : 0;
+    return rp.kept;
 }
 
 }  // namespace capsmi
