@@ -70,6 +70,17 @@ def cpu_baseline(scale, ef):
                       f"count(DISTINCT c)={dist}, {dt:.2f} s"}
 
 
+def init_dist(dist, local):
+    """RCCL (backend "nccl") one rank per GPU; CAPSMI_DIST_BACKEND=gloo rehearses the same ranks and
+    collectives on fewer GPUs (RCCL refuses two ranks on one device)."""
+    import torch
+    backend = os.environ.get("CAPSMI_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+
+
 def pmc_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this workload
     (profiles/*_<workload>_pmc.json, newest round first), FETCH_SIZE doubled per MI355X_MICROARCH.md
@@ -105,10 +116,11 @@ def main():
     if world == 1 and args.gpus > 1:
         sys.exit("run with torch.distributed.run for --gpus > 1")
     distributed = world > 1
+    local = local % max(1, torch.cuda.device_count())  # rehearsal: several ranks may share one GPU (gloo)
     torch.cuda.set_device(local)
     if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        init_dist(dist, local)
 
     from capsmi import Session, _lib, graph
 
@@ -314,11 +326,12 @@ def run_single(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and wl != "c4":
         sys.exit("the C2 / C5 lines are single-GPU (SURVEY.md 8e: C5 needs per-hop frontier exchange, next)")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:  # C4: replicated oriented graph, vertex shares per rank, one all-reduce
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        init_dist(dist, local)
     sess = Session(local)
     sess.set_stream(torch.cuda.current_stream().cuda_stream)
     rels = graph.rmat_rels(sess, scale, 0, m, probs, 42)

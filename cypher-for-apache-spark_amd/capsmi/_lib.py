@@ -80,6 +80,7 @@ _SIGS = {
     "capsmi_session_create": (c_int32, [c_int32, PP]),
     "capsmi_session_destroy": (c_int32, [P]),
     "capsmi_session_set_stream": (c_int32, [P, c_void_p]),
+    "capsmi_session_use_stream": (c_int32, [P, c_void_p]),
     "capsmi_session_sync": (c_int32, [P]),
     "capsmi_session_set_profiling": (c_int32, [P, c_int32]),
     "capsmi_session_kernel_time": (c_int32, [P, c_char_p, POINTER(c_int64), POINTER(ctypes.c_double)]),

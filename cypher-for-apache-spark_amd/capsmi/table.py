@@ -81,7 +81,12 @@ class Session:
         return self._h
 
     def set_stream(self, hip_stream: Optional[int]) -> None:
-        _lib.call("capsmi_session_set_stream", self._h, ctypes.c_void_p(hip_stream or 0))
+        """Run on `hip_stream` (an int handle, e.g. ``torch.cuda.current_stream().cuda_stream``;
+        0 is the null stream, torch's default), or on the session's own stream for None."""
+        if hip_stream is None:
+            _lib.call("capsmi_session_set_stream", self._h, ctypes.c_void_p(0))
+        else:
+            _lib.call("capsmi_session_use_stream", self._h, ctypes.c_void_p(hip_stream))
 
     def sync(self) -> None:
         _lib.call("capsmi_session_sync", self._h)

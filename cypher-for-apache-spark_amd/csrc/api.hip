@@ -436,6 +436,13 @@ capsmi_status capsmi_session_set_stream(capsmi_session* s, void* hip_stream) {
     API_END
 }
 
+capsmi_status capsmi_session_use_stream(capsmi_session* s, void* hip_stream) {
+    API_BEGIN
+    need(s, "session");
+    s->stream = (hipStream_t)hip_stream;
+    API_END
+}
+
 capsmi_status capsmi_session_set_profiling(capsmi_session* s, int32_t enabled) {
     API_BEGIN
     need(s, "session");

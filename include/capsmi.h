@@ -152,6 +152,9 @@ capsmi_status capsmi_session_create(int32_t device, capsmi_session** out);
 capsmi_status capsmi_session_destroy(capsmi_session* s);
 /* run subsequent work on an external hipStream_t (e.g. torch's current stream); NULL = session stream */
 capsmi_status capsmi_session_set_stream(capsmi_session* s, void* hip_stream);
+/* run subsequent work on exactly `hip_stream`; NULL = the HIP null (legacy default) stream -- what
+ * torch's default stream is, so kernels and torch work stay ordered */
+capsmi_status capsmi_session_use_stream(capsmi_session* s, void* hip_stream);
 capsmi_status capsmi_session_sync(capsmi_session* s);
 /* per-kernel HIP-event timing of the fused graph kernels (off by default; SURVEY.md §5 tracing).
  * While enabled, each hot launch is bracketed by events on the session stream. */

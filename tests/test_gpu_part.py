@@ -194,3 +194,41 @@ def test_largest_domain(session):
     assert rp.size == m
     assert rp.count_distinct(bm, bm, bm) == want
     rp.release()
+
+
+@pytest.mark.parametrize("nparts", [1, 2, 4])
+def test_owner_partitioned_two_hop_with_torch_in_between(nparts):
+    """The multi-GPU C3 step emulated on one device: per rank the owner(target) share, build + hop
+    1, the owned frontier slices stitched by torch copies (the all-gather), hop 2 per rank, owned
+    popcounts summed.  The session runs on torch's default stream (the null stream), so the torch
+    copies between library calls are ordered after the library's kernels."""
+    import torch
+    from capsmi import Session, graph
+    scale = 16
+    n, m = 1 << scale, 16 << scale
+    nw = (n + 31) // 32
+    s = Session(0)
+    s.set_stream(torch.cuda.current_stream().cuda_stream)
+    persons = graph.rmat_nodes(s, scale, graph.NODES_ALL)
+    full = graph.rmat_rels(s, scale, 0, m, graph.RMAT_GRAPH500, 7)
+    p = graph.NodeBitmap(s, 0, n).add_scan(persons, "id")
+    ref = graph.two_hop_count_distinct(s, [full], p, p, p)
+    rels = [graph.rmat_rels(s, scale, 0, m, graph.RMAT_GRAPH500, 7, part_col=graph.PART_TARGET, part=r,
+                            nparts=nparts) for r in range(nparts)]
+    mids = [torch.zeros(2 * nw, dtype=torch.int32, device="cuda") for _ in range(nparts)]
+    scratch = torch.zeros(nw, dtype=torch.int32, device="cuda")
+    rps = [graph.RelPartition.build_mark_mid(s, [rels[r]], p, p, mids[r].data_ptr(), scratch.data_ptr())
+           for r in range(nparts)]
+    mid = torch.zeros(2 * nw, dtype=torch.int32, device="cuda")
+    for r in range(nparts):
+        wb, we = graph.owner_words(n, r, nparts)
+        mid[wb:we] = mids[r][wb:we]
+        mid[nw + wb:nw + we] = mids[r][nw + wb:nw + we]
+    total = 0
+    for r in range(nparts):
+        wb, we = graph.owner_words(n, r, nparts)
+        dst = torch.zeros(nw, dtype=torch.int32, device="cuda")
+        rps[r].mark_dst(p, p, mid.data_ptr(), dst.data_ptr())
+        total += graph.words_popcount(s, dst.data_ptr(), wb, we)
+        rps[r].release()
+    assert total == ref
