@@ -147,14 +147,17 @@ def main():
     mid = torch.zeros(2 * nw, dtype=torch.int32, device="cuda")
     scratch = torch.zeros(nw, dtype=torch.int32, device="cuda")
     dstw = torch.zeros(nw, dtype=torch.int32, device="cuda")
-    x1, x2 = mid[:nw], mid[nw:]
-    own = slice(wb, we)
     cached = {}
 
+    k_own = we - wb
+    send = torch.empty(2, k_own, dtype=torch.int32, device="cuda")
+    recv = torch.empty(world * 2, k_own, dtype=torch.int32, device="cuda")  # rank-major (rank, X1|X2) rows
+
     def exchange_and_finish(p, mark_dst):
-        if distributed:  # hop-1 frontier: every rank needs X1/X2 of every middle node
-            dist.all_gather_into_tensor(x1, x1[own].clone())
-            dist.all_gather_into_tensor(x2, x2[own].clone())
+        if distributed:  # hop-1 frontier: every rank needs X1/X2 of every middle node; one all-gather
+            send.copy_(mid.view(2, nw)[:, wb:we])
+            dist.all_gather_into_tensor(recv, send)
+            mid.view(2, world, k_own).copy_(recv.view(world, 2, k_own).transpose(0, 1))
         mark_dst(p)
         local_cnt = graph.words_popcount(sess, dstw.data_ptr(), wb, we)
         if distributed:
