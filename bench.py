@@ -306,7 +306,7 @@ SINGLE = {
 
 # timer name -> kernel symbol (rocprofv3 / PMC summary name) where they differ
 SINGLE_SYMBOL = {"expand_filter": "k_expand_pairs", "part_scatter1": "k_scatter_c", "varlen_deg": "k_vl_deg",
-                 "varlen_w": "k_vl_w", "varlen_t": "k_vl_t", "varlen_rev": "k_vl_bset", "varlen_recip": "k_vl_recip", "triangles": "k_tri_big_items+k_tri_small"}
+                 "varlen_w": "k_vl_w", "varlen_t": "k_vl_t", "varlen_rev": "k_vl_bset", "varlen_recip": "k_vl_recip", "varlen_cand": "k_vl_cand", "triangles": "k_tri_big_items+k_tri_small"}
 
 
 def run_single(args):
@@ -366,7 +366,7 @@ def run_single(args):
         return None, out
 
     kernels = ("bitmap_add", "expand_filter", "tri_pack", "triangles", "part_scatter1", "varlen_deg", "varlen_w", "varlen_rev",
-               "varlen_recip", "varlen_t")
+               "varlen_cand", "varlen_recip", "varlen_t")
     for _ in range(args.warmup):
         step()
     _lib.call("capsmi_session_set_profiling", sess.handle, 1)

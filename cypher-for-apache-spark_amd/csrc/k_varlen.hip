@@ -197,6 +197,24 @@ __device__ __forceinline__ bool rb_test(const RegionBloom& b, uint32_t y, unsign
     return (b.w[x >> 5] >> (x & 31)) & 1u;
 }
 
+// Second-level filter of the candidate pairs (those the RegionBloom passes): one region of
+// kF2Words words per source slice, two bits per key inside one word.  Built in LDS by the W walk
+// (candidates (s, t) of slice(s)), tested on the reverse key (t, s) in slice(t)'s region: a pair
+// whose reverse exists is a candidate both ways, so it always passes.
+constexpr int kF2Words = 1 << 14;  // 64 KiB per slice: ~9 bits per candidate at 22 % false positives
+
+__device__ __forceinline__ void f2_pos(unsigned long long key, uint32_t& word, uint32_t& bits) {
+    const unsigned long long h = splitmix(key ^ 0x2545F4914F6CDD1DULL);
+    word = (uint32_t)h & (kF2Words - 1);
+    bits = (1u << ((h >> 40) & 31)) | (1u << ((h >> 50) & 31));
+}
+
+__device__ __forceinline__ bool f2_test(const uint32_t* f2, uint32_t x, unsigned long long key) {
+    uint32_t word, bits;
+    f2_pos(key, word, bits);
+    return (f2[((size_t)(x >> kVlBits) * kF2Words) + word] & bits) == bits;
+}
+
 struct ChunkWalk {
     const uint2* pool;
     const unsigned long long* meta;
@@ -270,15 +288,11 @@ __device__ __forceinline__ void flush_acc(unsigned long long* acc, unsigned long
 }
 
 // pass 1 (source partition, pair = (target, source)): od(v), s(v)
-// With a filter (bl.w) it also counts the pairs s -> t whose reverse t -> s may exist.
 __global__ void __launch_bounds__(kVlBlock) k_vl_deg(ChunkWalk cw, const uint32_t* __restrict__ bw, int b_full,
                                                      int64_t n, unsigned long long* __restrict__ od,
-                                                     unsigned long long* __restrict__ sl, RegionBloom bl,
-                                                     unsigned long long* __restrict__ ncand) {
+                                                     unsigned long long* __restrict__ sl) {
     extern __shared__ unsigned long long vl_lds[];
     unsigned long long *a_od = vl_lds, *a_s = vl_lds + kVlIds;
-    __shared__ unsigned int cand;
-    if (threadIdx.x == 0) cand = 0;
     for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_od[i] = a_s[i] = 0;
     __syncthreads();
     walk_chunks(
@@ -287,31 +301,53 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_deg(ChunkWalk cw, const uint32_
             const uint32_t t = p.x, s = p.y, i = s & (kVlIds - 1);
             if (bit_of(bw, b_full, t)) atomicAdd(&a_od[i], 1ULL);
             if (s == t) atomicAdd(&a_s[i], 1ULL);
-            if (bl.w && rb_test(bl, p.y, pkey(p.x, p.y))) atomicAdd(&cand, 1u);
         },
         [&](int j) {
             flush_acc(a_od, od, j, n);
             flush_acc(a_s, sl, j, n);
         });
-    if (bl.w && threadIdx.x == 0 && cand) atomicAdd(ncand, (unsigned long long)cand);
 }
 
 // pass 2: W(v) = sum_{v -> w} od(w)
-// It also inserts the candidate pairs s -> t (those whose reverse may exist) into h.
+// It also marks the candidate pairs s -> t (those whose reverse may exist) in the block's F2 region
+// for slice(s), stored whole per slice segment into partial slot w + j (k_vl_bset's scheme), and
+// counts them.
 __global__ void __launch_bounds__(kVlBlock) k_vl_w(ChunkWalk cw, int64_t n, const unsigned long long* __restrict__ od,
-                                                   unsigned long long* __restrict__ W, RegionBloom bl, PairHash h) {
+                                                   unsigned long long* __restrict__ W, RegionBloom bl,
+                                                   uint4* __restrict__ f2part, unsigned long long* __restrict__ ncand) {
     extern __shared__ unsigned long long vl_lds[];
     unsigned long long* a_w = vl_lds;
+    uint32_t* f2 = reinterpret_cast<uint32_t*>(vl_lds + kVlIds);
+    __shared__ unsigned int cand;
+    if (threadIdx.x == 0) cand = 0;
+    unsigned int mine = 0;  // this lane's candidates (one LDS add per wave at the end)
     for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_w[i] = 0;
+    for (int i = threadIdx.x; i < kF2Words; i += kVlBlock) f2[i] = 0;
     __syncthreads();
     walk_chunks(
         cw,
         [&](uint2 p, int) {  // p = (t, s)
             const unsigned long long x = od[p.x];
             if (x) atomicAdd(&a_w[p.y & (kVlIds - 1)], x);
-            if (rb_test(bl, p.y, pkey(p.x, p.y))) pair_insert(h, hkey(p.y, p.x));
+            if (rb_test(bl, p.y, pkey(p.x, p.y))) {
+                uint32_t word, bits;
+                f2_pos(pkey(p.y, p.x), word, bits);
+                atomicOr(&f2[word], bits);
+                ++mine;
+            }
         },
-        [&](int j) { flush_acc(a_w, W, j, n); });
+        [&](int j) {
+            flush_acc(a_w, W, j, n);
+            uint4* g = f2part + (((size_t)blockIdx.x + j) * (kF2Words / 4));
+            const uint4* l = reinterpret_cast<const uint4*>(f2);
+            for (int i = threadIdx.x; i < kF2Words / 4; i += kVlBlock) g[i] = l[i];
+            __syncthreads();
+            for (int i = threadIdx.x; i < kF2Words; i += kVlBlock) f2[i] = 0;
+        });
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_down(mine, o, 64);
+    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&cand, mine);
+    __syncthreads();
+    if (threadIdx.x == 0 && cand) atomicAdd(ncand, (unsigned long long)cand);
 }
 
 // target partition (pair = (source, target), j = slice(t)): mark pair (s, t) in t's region.  Each
@@ -394,10 +430,13 @@ __global__ void k_vl_recip(PairHash h, const uint32_t* __restrict__ aw, int a_fu
 
 // pass 3 (source partition): per relationship a -> b with a_ok(a): T2(a) += od(b); T3(a) += Y(b)
 // (the - m(b, a) b_ok(b) part is k_vl_recip's)
+// With the filters (ody set) it also puts the pairs a -> b that pass both (reverse maybe present,
+// reverse itself a candidate) into the exact table for k_vl_recip.
 __global__ void __launch_bounds__(kVlBlock) k_vl_t(ChunkWalk cw, const uint32_t* __restrict__ aw, int a_full,
                                                    int64_t n, const unsigned long long* __restrict__ od,
                                                    const longlong2* __restrict__ ody, unsigned long long* __restrict__ T2,
-                                                   unsigned long long* __restrict__ T3) {
+                                                   unsigned long long* __restrict__ T3, RegionBloom bl,
+                                                   const uint32_t* __restrict__ f2, PairHash h) {
     extern __shared__ unsigned long long vl_lds[];
     unsigned long long *a_t2 = vl_lds, *a_t3 = vl_lds + kVlIds;
     for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_t2[i] = a_t3[i] = 0;
@@ -406,6 +445,7 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_t(ChunkWalk cw, const uint32_t*
         cw,
         [&](uint2 p, int) {
             const uint32_t b = p.x, a = p.y, i = a & (kVlIds - 1);
+            if (ody && rb_test(bl, a, pkey(b, a)) && f2_test(f2, b, pkey(b, a))) pair_insert(h, hkey(a, b));
             if (!bit_of(aw, a_full, a)) return;
             if (ody) {  // T3 also wanted
                 const longlong2 v = ody[b];
@@ -468,7 +508,7 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
         for (const void* f : {reinterpret_cast<const void*>(k_vl_deg), reinterpret_cast<const void*>(k_vl_w),
                               reinterpret_cast<const void*>(k_vl_t)})
             HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
-        Buf ody, bw, hk, hc, cand;
+        Buf ody, bw, hk, hc, cand, f2;
         RegionBloom bl{nullptr, 0, 0, 0};
         PairHash h{nullptr, nullptr, nullptr, 0};
         if (need3) {
@@ -503,9 +543,22 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
         {
             KernelTimer kt(s, "varlen_deg");
             hipLaunchKernelGGL(k_vl_deg, dim3(g), dim3(kVlBlock), lds2, st, cw, d.b, d.b_full, n, P<unsigned long long>(od),
-                               P<unsigned long long>(sl), bl, need3 ? P<unsigned long long>(cand) : nullptr);
+                               P<unsigned long long>(sl));
         }
         if (need3) {
+            f2 = dev_alloc(sizeof(uint32_t) * kF2Words * (size_t)L.nt, st);
+            {
+                KernelTimer kt(s, "varlen_w");
+                Buf f2part = dev_alloc(sizeof(uint32_t) * kF2Words * ((size_t)cp.g2 + L.nt), st);
+                const size_t ldsw = sizeof(unsigned long long) * kVlIds + sizeof(uint32_t) * kF2Words;
+                HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_vl_w),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsw));
+                hipLaunchKernelGGL(k_vl_w, dim3(g), dim3(kVlBlock), ldsw, st, cw, n, P<unsigned long long>(od),
+                                   P<unsigned long long>(W), bl, P<uint4>(f2part), P<unsigned long long>(cand));
+                const RegionBloom f2b{P<uint32_t>(f2), 0, 19, 0};  // kF2Words * 32 = 2^19 bits per slice
+                hipLaunchKernelGGL(k_vl_bmerge, dim3(grid(s, (int64_t)(kF2Words / 4) * L.nt)), dim3(256), 0, st, cp.jst,
+                                   L.nt, cp.g2, P<uint4>(f2part), f2b);
+            }
             const int64_t nc = read_scalar(s, P<int64_t>(cand));
             if (getenv("CAPSMI_VL_DEBUG"))
                 fprintf(stderr, "varlen: pairs %lld candidates %lld regions %d x 2^%d bits\n", (long long)mtot,
@@ -518,22 +571,19 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
             HIP_CHECK(hipMemsetAsync(P<void>(hc), 0, sizeof(unsigned int) * (cap + 1), st));
             h = PairHash{P<unsigned long long>(hk), P<unsigned int>(hc), P<unsigned int>(hc) + cap,
                          (unsigned long long)(cap - 1)};
-            {
-                KernelTimer kt(s, "varlen_w");
-                hipLaunchKernelGGL(k_vl_w, dim3(g), dim3(kVlBlock), lds2 / 2, st, cw, n, P<unsigned long long>(od),
-                                   P<unsigned long long>(W), bl, h);
-            }
             ody = dev_alloc(2 * nb, st);
             hipLaunchKernelGGL(k_vl_y, dim3(grid(s, n)), dim3(256), 0, st, n, d.b, d.b_full, P<unsigned long long>(od),
                                P<unsigned long long>(W), P<unsigned long long>(sl), P<longlong2>(ody));
-            KernelTimer kt(s, "varlen_recip");
-            hipLaunchKernelGGL(k_vl_recip, dim3(grid(s, cap)), dim3(256), 0, st, h, d.a, d.a_full, d.b, d.b_full,
-                               P<unsigned long long>(T3));
         }
         {
             KernelTimer kt(s, "varlen_t");
             hipLaunchKernelGGL(k_vl_t, dim3(g), dim3(kVlBlock), lds2, st, cw, d.a, d.a_full, n, P<unsigned long long>(od),
                                need3 ? P<longlong2>(ody) : nullptr, P<unsigned long long>(T2),
+                               P<unsigned long long>(T3), bl, P<uint32_t>(f2), h);
+        }
+        if (need3) {
+            KernelTimer kt(s, "varlen_recip");
+            hipLaunchKernelGGL(k_vl_recip, dim3(grid(s, h.mask + 1)), dim3(256), 0, st, h, d.a, d.a_full, d.b, d.b_full,
                                P<unsigned long long>(T3));
         }
         HIP_CHECK(hipGetLastError());
