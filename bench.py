@@ -316,7 +316,7 @@ def run_single(args):
     import numpy as np
     import torch
     from capsmi import Session, _lib, graph
-    from capsmi.expr import Ands, BinOp, Col, Lit
+    from capsmi.expr import Ands, BinOp, Col, Lit, Ors
 
     wl = args.workload
     scale, ef, probs, desc, cpu_scale = SINGLE[wl]
@@ -327,17 +327,28 @@ def run_single(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and wl != "c4":
-        sys.exit("the C2 / C5 lines are single-GPU (SURVEY.md 8e: C5 needs per-hop frontier exchange, next)")
+    if world > 1 and wl == "c2":
+        sys.exit("the C2 line is single-GPU (SURVEY.md 8d)")
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
-    if world > 1:  # C4: replicated oriented graph, vertex shares per rank, one all-reduce
+    if world > 1:  # C4: replicated oriented graph, vertex shares; C5: owner(source) shards
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         init_dist(dist, local)
     sess = Session(local)
     sess.set_stream(torch.cuda.current_stream().cuda_stream)
-    rels = graph.rmat_rels(sess, scale, 0, m, probs, 42)
+    shard_c5 = wl == "c5" and world > 1
+    if shard_c5:  # ingest (untimed): out-relationships of owned sources + in-relationships from other ranks
+        wb, we = graph.owner_words(n, rank, world)
+        own_lo, own_hi = min(32 * wb, n), min(32 * we, n)
+        rels = graph.rmat_rels(sess, scale, 0, m, probs, 42, part_col=graph.PART_SOURCE, part=rank, nparts=world)
+        into = graph.rmat_rels(sess, scale, 0, m, probs, 42, part_col=graph.PART_TARGET, part=rank, nparts=world)
+        rels_in = into.filter(Ors((BinOp("<", Col("source"), Lit(own_lo)), BinOp(">=", Col("source"), Lit(own_hi)))))
+        del into
+        od_buf = torch.zeros(n, dtype=torch.int64, device="cuda")
+        y_buf = torch.zeros(n, dtype=torch.int64, device="cuda")
+    else:
+        rels = graph.rmat_rels(sess, scale, 0, m, probs, 42)
     kind = graph.NODES_PERSON if wl == "c2" else graph.NODES_ALL
     nodes = graph.rmat_nodes(sess, scale, kind, 42)
     sess.sync()
@@ -362,6 +373,14 @@ def run_single(args):
             g.release()
             dist.all_reduce(t)
             return int(t.item()), None
+        if shard_c5:  # begin -> all-reduce od -> mid -> all-reduce Y -> finish (rows of owned a)
+            sh = graph.VarlenShard(sess, [rels], [rels_in], ok, ok, 1, 3, own_lo, own_hi, od_buf.data_ptr())
+            dist.all_reduce(od_buf)
+            sh.mid(y_buf.data_ptr())
+            dist.all_reduce(y_buf)
+            out = sh.finish()
+            sh.release()
+            return None, out
         out = graph.var_length_count(sess, [rels], ok, ok, 1, 3)
         return None, out
 
@@ -394,13 +413,25 @@ def run_single(args):
         if c.value:
             kt[k] = (c.value, ms.value)
     _lib.call("capsmi_session_set_profiling", sess.handle, 0)
+    check = None
     if wl == "c5":
         res = int(out.column("count").values.sum())  # untimed export
+        if shard_c5:  # the ranks' rows are disjoint: total = sum; rank 0 checks the unsharded answer
+            t = torch.tensor([res], dtype=torch.int64, device="cuda")
+            dist.all_reduce(t)
+            res = int(t.item())
+            if rank == 0:
+                full = graph.rmat_rels(sess, scale, 0, m, probs, 42)
+                ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id")
+                ref = int(graph.var_length_count(sess, [full], ok, ok, 1, 3).column("count").values.sum())
+                check = "ok" if ref == res else f"MISMATCH {res} vs unsharded {ref}"
+                del full
     matched = res
+    m_kern = rels.size if shard_c5 else m  # relationships behind one launch of this rank's kernels
     # algorithmic bytes per launch of the kernels whose traffic is a plain function of the input
     alg = {"bitmap_add": n * 8, "expand_filter": m * 16 + (2 * res * 8 if wl == "c2" else 0),
-           "tri_pack": m * 24, "part_scatter1": m * 24, "varlen_deg": m * 8, "varlen_w": m * 8, "varlen_t": m * 8,
-           "varlen_rev": m * 24 + m * 8,  # target partition + filter walk
+           "tri_pack": m * 24, "part_scatter1": m_kern * 24, "varlen_deg": m_kern * 8, "varlen_w": m_kern * 8,
+           "varlen_t": m_kern * 8, "varlen_rev": m * 24 + m * 8,  # target partition + filter walk
            # both triangle kernels together: the oriented adjacency read once (8-B offsets, 4-B
            # targets, 8-B multiplicity payload per oriented edge)
            "triangles": n * 8 + 12 * cache.get("oriented_edges", 0)}
@@ -424,6 +455,10 @@ def run_single(args):
                   "query_frac_of_peak": b_alg / sec / 1e9 / HBM_PEAK_GBS,
                   "kernel_ms": {k: v[1] / v[0] for k, v in kt.items()}},
     }
+    if shard_c5:
+        line["config"]["parallelism"] = (f"owner(source) shards over {world} GPU(s); od and Y all-reduced between "
+                                         f"phases; in-relationships exchanged at ingest")
+        line["query"]["check_vs_unsharded"] = check
     line["cpu_baseline"] = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_single(wl, cpu_scale, ef, probs)
     if rank == 0:
         print(json.dumps(line), flush=True)

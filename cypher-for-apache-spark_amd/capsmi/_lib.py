@@ -130,6 +130,11 @@ _SIGS = {
     "capsmi_triangle_count": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, POINTER(c_int64)]),
     "capsmi_var_length_count": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, P, c_int32, c_int32, c_char_p,
                                           c_char_p, PP]),
+    "capsmi_varlen_shard_begin": (c_int32, [P, c_int32, PP, c_int32, PP, c_char_p, c_char_p, P, P, c_int32, c_int32,
+                                            c_int64, c_int64, c_void_p, PP]),
+    "capsmi_varlen_shard_mid": (c_int32, [P, c_void_p]),
+    "capsmi_varlen_shard_finish": (c_int32, [P, c_char_p, c_char_p, PP]),
+    "capsmi_varlen_shard_release": (c_int32, [P]),
     "capsmi_relpart_release": (c_int32, [P]),
     "capsmi_two_hop_mark_mid_part": (c_int32, [P, P, P, P, c_void_p, c_void_p]),
     "capsmi_two_hop_mark_dst_part": (c_int32, [P, P, P, P, c_void_p, c_void_p]),

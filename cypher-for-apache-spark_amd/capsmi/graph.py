@@ -122,6 +122,45 @@ def var_length_count(session: Session, rels: Sequence[GpuTable], a_ok: NodeBitma
     return GpuTable(session, out)
 
 
+class VarlenShard:
+    """One rank's share of the var-length grouped count (multi-GPU C5; include/capsmi.h
+    capsmi_varlen_shard_*).  The rank owns source ids [own_lo, own_hi); `out_rels` are the
+    relationships it owns by source, `in_rels` those from other ranks into its owned ids.  `od_ptr`
+    and (in mid) `y_ptr` are device int64 buffers over the id domain that the caller sums over
+    ranks between the phases:  begin -> sum od -> mid -> sum y -> finish."""
+
+    def __init__(self, session: Session, out_rels: Sequence[GpuTable], in_rels: Sequence[GpuTable], a_ok: NodeBitmap,
+                 b_ok: NodeBitmap, lower: int, upper: int, own_lo: int, own_hi: int, od_ptr: int,
+                 src_col: str = "source", dst_col: str = "target"):
+        self.session = session
+        self._h = ctypes.c_void_p()
+        self._keep = (list(out_rels), list(in_rels), a_ok, b_ok)  # inputs stay alive until finish
+        _lib.call("capsmi_varlen_shard_begin", session.handle, len(out_rels), _handles(out_rels), len(in_rels),
+                  _handles(in_rels), src_col.encode(), dst_col.encode(), a_ok.handle, b_ok.handle, lower, upper,
+                  own_lo, own_hi, ctypes.c_void_p(od_ptr), ctypes.byref(self._h))
+
+    def mid(self, y_ptr: int) -> None:
+        _lib.call("capsmi_varlen_shard_mid", self._h, ctypes.c_void_p(y_ptr))
+
+    def finish(self, id_name: str = "id", count_name: str = "count") -> GpuTable:
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_varlen_shard_finish", self._h, id_name.encode(), count_name.encode(), ctypes.byref(out))
+        return GpuTable(self.session, out)
+
+    def release(self) -> None:
+        if self._h:
+            _lib.call("capsmi_varlen_shard_release", self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            if self._h and _lib._lib is not None:
+                _lib._lib.capsmi_varlen_shard_release(self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+
 class TriGraph:
     """Oriented simple graph with directed multiplicities for the cyclic triangle count (C4)."""
 

@@ -1264,6 +1264,96 @@ capsmi_status capsmi_var_length_count(capsmi_session* s, int32_t nrels, capsmi_t
     API_END
 }
 
+struct capsmi_varlen_shard {
+    capsmi_session* sess = nullptr;
+    capsmi::VarlenShard* v = nullptr;
+    ~capsmi_varlen_shard() { capsmi::varlen_shard_free(v); }
+};
+
+capsmi_status capsmi_varlen_shard_begin(capsmi_session* s, int32_t nout, capsmi_table* const* out_rels, int32_t nin,
+                                        capsmi_table* const* in_rels, const char* src_col, const char* dst_col,
+                                        const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, int32_t lower,
+                                        int32_t upper, int64_t own_lo, int64_t own_hi, int64_t* od,
+                                        capsmi_varlen_shard** out) {
+    API_BEGIN
+    need(s, "session");
+    need(out, "out");
+    need(od, "od");
+    check_bitmap(a_ok, "a_ok");
+    check_bitmap(b_ok, "b_ok");
+    REQUIRE(nout >= 0 && (nout == 0 || out_rels) && nin >= 0 && (nin == 0 || in_rels), CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            "rels");
+    REQUIRE(lower >= 1 && lower <= upper && upper <= 3, CAPSMI_ERR_NOT_IMPLEMENTED,
+            "fused var-length count supports 1 <= lower <= upper <= 3 (use the join plan otherwise)");
+    REQUIRE(a_ok->lo == b_ok->lo && a_ok->hi == b_ok->hi, CAPSMI_ERR_UNSUPPORTED, "a and b scans need one id domain");
+    REQUIRE(!a_ok->any_dup && !b_ok->any_dup, CAPSMI_ERR_UNSUPPORTED,
+            "fused count(*) needs each node id in one scanned row");
+    use_device(s);
+    std::vector<const int64_t*> srcs, dsts, isrcs, idsts;
+    std::vector<int64_t> ms, ims;
+    for (int i = 0; i < nout; ++i) {
+        need(out_rels[i], "out_rels[i]");
+        srcs.push_back(rel_col(out_rels[i], src_col).d());
+        dsts.push_back(rel_col(out_rels[i], dst_col).d());
+        ms.push_back(out_rels[i]->nrows);
+    }
+    for (int i = 0; i < nin; ++i) {
+        need(in_rels[i], "in_rels[i]");
+        isrcs.push_back(rel_col(in_rels[i], src_col).d());
+        idsts.push_back(rel_col(in_rels[i], dst_col).d());
+        ims.push_back(in_rels[i]->nrows);
+    }
+    auto h = std::make_unique<capsmi_varlen_shard>();
+    h->sess = s;
+    h->v = varlen_shard_begin(s, srcs.data(), dsts.data(), ms.data(), nout, isrcs.data(), idsts.data(), ims.data(),
+                              nin, a_ok, b_ok, lower, upper, own_lo, own_hi, od);
+    *out = h.release();
+    API_END
+}
+
+capsmi_status capsmi_varlen_shard_mid(capsmi_varlen_shard* v, int64_t* y) {
+    API_BEGIN
+    need(v, "shard");
+    need(y, "y");
+    use_device(v->sess);
+    varlen_shard_mid(v->v, y);
+    API_END
+}
+
+capsmi_status capsmi_varlen_shard_finish(capsmi_varlen_shard* v, const char* id_name, const char* count_name,
+                                         capsmi_table** out) {
+    API_BEGIN
+    need(v, "shard");
+    need(out, "out");
+    need(id_name, "id_name");
+    need(count_name, "count_name");
+    REQUIRE(std::string(id_name) != count_name, CAPSMI_ERR_ILLEGAL_ARGUMENT, "output names must differ");
+    use_device(v->sess);
+    Buf ids, cnt;
+    const int64_t rows = varlen_shard_finish(v->v, ids, cnt);
+    auto* o = new_table(v->sess, rows);
+    Column a, c;
+    a.name = id_name;
+    a.type = CAPSMI_I64;
+    a.data = ids;
+    c.name = count_name;
+    c.type = CAPSMI_I64;
+    c.data = cnt;
+    o->cols.push_back(std::move(a));
+    o->cols.push_back(std::move(c));
+    *out = o;
+    API_END
+}
+
+capsmi_status capsmi_varlen_shard_release(capsmi_varlen_shard* v) {
+    API_BEGIN
+    if (v) {
+        use_device(v->sess);
+        delete v;
+    }
+    API_END
+}
+
 }  // extern "C"
 
 struct capsmi_trigraph {

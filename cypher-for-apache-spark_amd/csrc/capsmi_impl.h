@@ -247,6 +247,17 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
                          int nt, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, int lower, int upper,
                          Buf& out_ids, Buf& out_cnt);
 
+// sharded var-length grouped count (multi-GPU C5; k_varlen.hip): begin -> caller sums od over ranks
+// -> mid -> caller sums Y -> finish (rows of owned ids)
+struct VarlenShard;
+VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts,
+                                const int64_t* ms, int nt, const int64_t* const* isrcs, const int64_t* const* idsts,
+                                const int64_t* ims, int nin, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok,
+                                int lower, int upper, int64_t own_lo, int64_t own_hi, int64_t* od);
+void varlen_shard_mid(VarlenShard* v, int64_t* y);
+int64_t varlen_shard_finish(VarlenShard* v, Buf& out_ids, Buf& out_cnt);
+void varlen_shard_free(VarlenShard* v);
+
 // graph (k_graph.hip)
 void bitmap_add_rows(capsmi_bitmap* b, const int64_t* ids, const uint8_t* ids_valid,
                      const uint8_t* flags, int64_t n, int64_t* dev_counters);

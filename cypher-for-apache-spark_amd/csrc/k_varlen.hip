@@ -327,9 +327,11 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_w(ChunkWalk cw, int64_t n, cons
     walk_chunks(
         cw,
         [&](uint2 p, int) {  // p = (t, s)
-            const unsigned long long x = od[p.x];
-            if (x) atomicAdd(&a_w[p.y & (kVlIds - 1)], x);
-            if (rb_test(bl, p.y, pkey(p.x, p.y))) {
+            if (W) {
+                const unsigned long long x = od[p.x];
+                if (x) atomicAdd(&a_w[p.y & (kVlIds - 1)], x);
+            }
+            if (f2part && rb_test(bl, p.y, pkey(p.x, p.y))) {
                 uint32_t word, bits;
                 f2_pos(pkey(p.y, p.x), word, bits);
                 atomicOr(&f2[word], bits);
@@ -337,17 +339,30 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_w(ChunkWalk cw, int64_t n, cons
             }
         },
         [&](int j) {
-            flush_acc(a_w, W, j, n);
-            uint4* g = f2part + (((size_t)blockIdx.x + j) * (kF2Words / 4));
-            const uint4* l = reinterpret_cast<const uint4*>(f2);
-            for (int i = threadIdx.x; i < kF2Words / 4; i += kVlBlock) g[i] = l[i];
-            __syncthreads();
-            for (int i = threadIdx.x; i < kF2Words; i += kVlBlock) f2[i] = 0;
+            if (W) flush_acc(a_w, W, j, n);
+            if (f2part) {
+                uint4* g = f2part + (((size_t)blockIdx.x + j) * (kF2Words / 4));
+                const uint4* l = reinterpret_cast<const uint4*>(f2);
+                for (int i = threadIdx.x; i < kF2Words / 4; i += kVlBlock) g[i] = l[i];
+                __syncthreads();
+                for (int i = threadIdx.x; i < kF2Words; i += kVlBlock) f2[i] = 0;
+            }
         });
     for (int o = 32; o > 0; o >>= 1) mine += __shfl_down(mine, o, 64);
     if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&cand, mine);
     __syncthreads();
     if (threadIdx.x == 0 && cand) atomicAdd(ncand, (unsigned long long)cand);
+}
+
+// pairs a -> b passing both filters into the exact table (the sharded form's separate walk)
+__global__ void __launch_bounds__(kVlBlock) k_vl_ins(ChunkWalk cw, RegionBloom bl, const uint32_t* __restrict__ f2,
+                                                     PairHash h) {
+    walk_chunks(
+        cw,
+        [&](uint2 p, int) {  // p = (b, a)
+            if (rb_test(bl, p.y, pkey(p.x, p.y)) && f2_test(f2, p.x, pkey(p.x, p.y))) pair_insert(h, hkey(p.y, p.x));
+        },
+        [&](int) {});
 }
 
 // target partition (pair = (source, target), j = slice(t)): mark pair (s, t) in t's region.  Each
@@ -411,10 +426,24 @@ __global__ void k_vl_y(int64_t n, const uint32_t* __restrict__ bw, int b_full, c
                                 (long long)W[i] - (bit_of(bw, b_full, (uint32_t)i) ? (long long)sl[i] : 0LL));
 }
 
+// sharded form: Y(b) alone (partial: the owner's W), then (od, Y) packed once both are reduced
+__global__ void k_vl_yonly(int64_t n, const uint32_t* __restrict__ bw, int b_full,
+                           const unsigned long long* __restrict__ W, const unsigned long long* __restrict__ sl,
+                           long long* __restrict__ Y) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        Y[i] = (long long)W[i] - (bit_of(bw, b_full, (uint32_t)i) ? (long long)sl[i] : 0LL);
+}
+
+__global__ void k_vl_pack(int64_t n, const long long* __restrict__ od, const long long* __restrict__ Y,
+                          longlong2* __restrict__ ody) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        ody[i] = make_longlong2(od[i], Y[i]);
+}
+
 // R(a) = sum_b m(a, b) m(b, a) b_ok(b) over the candidate table (every pair with its reverse present
 // is in it, both ways): T3(a) -= R(a) for a_ok(a)
 __global__ void k_vl_recip(PairHash h, const uint32_t* __restrict__ aw, int a_full, const uint32_t* __restrict__ bw,
-                           int b_full, unsigned long long* __restrict__ T3) {
+                           int b_full, unsigned long long* __restrict__ T3, uint32_t own_lo, uint32_t own_hi) {
     const bool ovf = *h.any_ovf != 0;
     for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i <= h.mask;
          i += (unsigned long long)gridDim.x * blockDim.x) {
@@ -422,7 +451,7 @@ __global__ void k_vl_recip(PairHash h, const uint32_t* __restrict__ aw, int a_fu
         if (!v) continue;
         const unsigned long long key = (v & kKeyMask) - 1;
         const uint32_t a = (uint32_t)(key >> 24), b = (uint32_t)(key & 0xFFFFFF);
-        if (!bit_of(aw, a_full, a) || !bit_of(bw, b_full, b)) continue;
+        if (a < own_lo || a >= own_hi || !bit_of(aw, a_full, a) || !bit_of(bw, b_full, b)) continue;
         const unsigned long long r = pair_count(h, hkey(b, a), ovf);
         if (r) atomicAdd(&T3[a], (unsigned long long)(-(long long)(slot_count(h, i, v, ovf) * r)));
     }
@@ -445,7 +474,7 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_t(ChunkWalk cw, const uint32_t*
         cw,
         [&](uint2 p, int) {
             const uint32_t b = p.x, a = p.y, i = a & (kVlIds - 1);
-            if (ody && rb_test(bl, a, pkey(b, a)) && f2_test(f2, b, pkey(b, a))) pair_insert(h, hkey(a, b));
+            if (h.slot && rb_test(bl, a, pkey(b, a)) && f2_test(f2, b, pkey(b, a))) pair_insert(h, hkey(a, b));
             if (!bit_of(aw, a_full, a)) return;
             if (ody) {  // T3 also wanted
                 const longlong2 v = ody[b];
@@ -584,7 +613,7 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
         if (need3) {
             KernelTimer kt(s, "varlen_recip");
             hipLaunchKernelGGL(k_vl_recip, dim3(grid(s, h.mask + 1)), dim3(256), 0, st, h, d.a, d.a_full, d.b, d.b_full,
-                               P<unsigned long long>(T3));
+                               P<unsigned long long>(T3), 0u, (uint32_t)n);
         }
         HIP_CHECK(hipGetLastError());
     } else {
@@ -658,5 +687,205 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
     }
     return rows;
 }
+
+}  // namespace capsmi
+
+namespace capsmi {
+
+// ---- sharded form (multi-GPU C5) ------------------------------------------------------
+// Rank r owns the sources in [own_lo, own_hi) and holds their out-relationships ("out") plus the
+// relationships into its owned ids from other ranks' sources ("in", exchanged once at ingest).
+//   begin : out by source slice -> od, s of owned ids (0 elsewhere: the caller sums od over ranks);
+//           R(a) for owned a from out + in (every reciprocal pair of an owned a is there both ways):
+//           first-level filter by target, second level by source, exact table, k_vl_recip
+//   mid   : W(v) of owned v from the summed od -> Y of owned v (0 elsewhere: the caller sums Y)
+//   finish: T2, T3 of owned a from the summed od and Y -> rows of owned a
+struct VarlenShard {
+    capsmi_session* s = nullptr;
+    varlen::Dom d{};
+    int64_t n = 0, own_lo = 0, own_hi = 0;  // own range relative to d.lo
+    int lower = 1, upper = 1;
+    bool need3 = false;
+    part::Layout L{};
+    ChunkPart cp;  // out, by source slice
+    Buf sl, W, T2, T3, ody, bw, f2, hk, hc;
+    int64_t* od = nullptr;  // caller buffers (n int64 each), summed over ranks by the caller
+    int64_t* y = nullptr;
+};
+
+VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts,
+                                const int64_t* ms, int nt, const int64_t* const* isrcs, const int64_t* const* idsts,
+                                const int64_t* ims, int nin, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok,
+                                int lower, int upper, int64_t own_lo, int64_t own_hi, int64_t* od) {
+    using namespace varlen;
+    using namespace part;
+    hipStream_t st = s->stream;
+    const int64_t n = b_ok->hi - b_ok->lo;
+    REQUIRE(n > 0 && n < (int64_t(1) << 24), CAPSMI_ERR_UNSUPPORTED, "sharded var-length count needs < 2^24 ids");
+    REQUIRE(own_lo >= b_ok->lo && own_lo <= own_hi && own_hi <= b_ok->hi, CAPSMI_ERR_ILLEGAL_ARGUMENT, "own range");
+    auto v = std::make_unique<VarlenShard>();
+    v->s = s;
+    v->d = Dom{P<uint32_t>(a_ok->words), P<uint32_t>(b_ok->words), b_ok->lo, b_ok->hi, a_ok->full ? 1 : 0,
+               b_ok->full ? 1 : 0};
+    v->n = n;
+    v->own_lo = own_lo - b_ok->lo;
+    v->own_hi = own_hi - b_ok->lo;
+    v->lower = lower;
+    v->upper = upper;
+    v->need3 = upper >= 3;
+    v->od = od;
+    const size_t nb = sizeof(uint64_t) * n;
+    HIP_CHECK(hipMemsetAsync(od, 0, nb, st));
+    v->sl = dev_alloc(nb, st);
+    v->W = dev_alloc(nb, st);
+    v->T2 = dev_alloc(nb, st);
+    v->T3 = dev_alloc(nb, st);
+    for (Buf* b : {&v->sl, &v->W, &v->T2, &v->T3}) HIP_CHECK(hipMemsetAsync(P<void>(*b), 0, nb, st));
+    Layout& L = v->L;
+    L.lo = v->d.lo;
+    L.hi = v->d.hi;
+    L.tbits = kVlBits;
+    L.nt = (int)((n + kVlIds - 1) / kVlIds);
+    L.ns = 1;
+    L.sbits = 31;
+    L.ncells = L.nt;
+    int64_t mout = 0, min_ = 0;
+    for (int i = 0; i < nt; ++i) mout += ms[i] > 0 ? ms[i] : 0;
+    for (int i = 0; i < nin; ++i) min_ += ims[i] > 0 ? ims[i] : 0;
+    const size_t lds2 = 2 * sizeof(unsigned long long) * kVlIds;
+    for (const void* f : {reinterpret_cast<const void*>(k_vl_deg), reinterpret_cast<const void*>(k_vl_w),
+                          reinterpret_cast<const void*>(k_vl_t)})
+        HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+    if (mout > 0) {
+        {
+            KernelTimer kt(s, "varlen_part");
+            chunk_partition(s, srcs, dsts, ms, nt, true, L, s->num_cus, v->cp);
+        }
+        const ChunkWalk cw{P<uint2>(v->cp.pool), P<unsigned long long>(v->cp.meta), v->cp.order, v->cp.jst,
+                           v->cp.segbase, v->cp.ja, L.nt};
+        KernelTimer kt(s, "varlen_deg");
+        hipLaunchKernelGGL(k_vl_deg, dim3((unsigned)v->cp.g2), dim3(kVlBlock), lds2, st, cw, v->d.b, v->d.b_full, n,
+                           reinterpret_cast<unsigned long long*>(od), P<unsigned long long>(v->sl));
+    }
+    const int64_t mall = mout + min_;
+    if (v->need3 && mall > 0) {
+        std::vector<const int64_t*> as(srcs, srcs + nt), ad(dsts, dsts + nt);
+        std::vector<int64_t> am(ms, ms + nt);
+        for (int i = 0; i < nin; ++i) {
+            as.push_back(isrcs[i]);
+            ad.push_back(idsts[i]);
+            am.push_back(ims[i]);
+        }
+        const int na = (int)as.size();
+        ChunkPart ct, ca;
+        KernelTimer kt(s, "varlen_rev");
+        chunk_partition(s, as.data(), ad.data(), am.data(), na, false, L, s->num_cus, ct);
+        const int64_t per_slice = (mall + L.nt - 1) / L.nt;
+        int rshift = 10;
+        while ((int64_t(1) << rshift) < int64_t(8) * per_slice && rshift < 20) ++rshift;
+        const size_t rbytes = (size_t(1) << rshift) / 8;
+        v->bw = dev_alloc(rbytes * L.nt, st);
+        const RegionBloom bl{P<uint32_t>(v->bw), (unsigned long long)((int64_t(1) << rshift) - 1), rshift, 0};
+        {
+            Buf part = dev_alloc(rbytes * ((size_t)ct.g2 + L.nt), st);
+            const ChunkWalk tw{P<uint2>(ct.pool), P<unsigned long long>(ct.meta), ct.order, ct.jst, ct.segbase, ct.ja,
+                               L.nt};
+            HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_vl_bset),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)rbytes));
+            hipLaunchKernelGGL(k_vl_bset, dim3((unsigned)ct.g2), dim3(kVlBlock), rbytes, st, tw, bl, P<uint4>(part));
+            hipLaunchKernelGGL(k_vl_bmerge, dim3(grid(s, (int64_t)(rbytes / 16) * L.nt)), dim3(256), 0, st, ct.jst, L.nt,
+                               ct.g2, P<uint4>(part), bl);
+        }
+        chunk_partition(s, as.data(), ad.data(), am.data(), na, true, L, s->num_cus, ca);
+        const ChunkWalk aw{P<uint2>(ca.pool), P<unsigned long long>(ca.meta), ca.order, ca.jst, ca.segbase, ca.ja, L.nt};
+        v->f2 = dev_alloc(sizeof(uint32_t) * kF2Words * (size_t)L.nt, st);
+        Buf cand = dev_alloc(sizeof(int64_t), st);
+        HIP_CHECK(hipMemsetAsync(P<void>(cand), 0, sizeof(int64_t), st));
+        {
+            Buf f2part = dev_alloc(sizeof(uint32_t) * kF2Words * ((size_t)ca.g2 + L.nt), st);
+            hipLaunchKernelGGL(k_vl_w, dim3((unsigned)ca.g2), dim3(kVlBlock), lds2, st, aw, n, nullptr, nullptr, bl,
+                               P<uint4>(f2part), P<unsigned long long>(cand));
+            const RegionBloom f2b{P<uint32_t>(v->f2), 0, 19, 0};
+            hipLaunchKernelGGL(k_vl_bmerge, dim3(grid(s, (int64_t)(kF2Words / 4) * L.nt)), dim3(256), 0, st, ca.jst,
+                               L.nt, ca.g2, P<uint4>(f2part), f2b);
+        }
+        const int64_t nc = read_scalar(s, P<int64_t>(cand));
+        int64_t cap = 1024;
+        while (cap < 2 * nc) cap <<= 1;
+        v->hk = dev_alloc(sizeof(unsigned long long) * cap, st);
+        v->hc = dev_alloc(sizeof(unsigned int) * (cap + 1), st);
+        HIP_CHECK(hipMemsetAsync(P<void>(v->hk), 0, sizeof(unsigned long long) * cap, st));
+        HIP_CHECK(hipMemsetAsync(P<void>(v->hc), 0, sizeof(unsigned int) * (cap + 1), st));
+        const PairHash h{P<unsigned long long>(v->hk), P<unsigned int>(v->hc), P<unsigned int>(v->hc) + cap,
+                         (unsigned long long)(cap - 1)};
+        hipLaunchKernelGGL(k_vl_ins, dim3((unsigned)ca.g2), dim3(kVlBlock), 0, st, aw, bl, P<uint32_t>(v->f2), h);
+        hipLaunchKernelGGL(k_vl_recip, dim3(grid(s, cap)), dim3(256), 0, st, h, v->d.a, v->d.a_full, v->d.b,
+                           v->d.b_full, P<unsigned long long>(v->T3), (uint32_t)v->own_lo, (uint32_t)v->own_hi);
+    }
+    HIP_CHECK(hipGetLastError());
+    return v.release();
+}
+
+void varlen_shard_mid(VarlenShard* v, int64_t* y) {
+    using namespace varlen;
+    capsmi_session* s = v->s;
+    hipStream_t st = s->stream;
+    v->y = y;
+    HIP_CHECK(hipMemsetAsync(y, 0, sizeof(int64_t) * v->n, st));
+    if (!v->need3) return;
+    if (v->cp.pool) {
+        const ChunkWalk cw{P<uint2>(v->cp.pool), P<unsigned long long>(v->cp.meta), v->cp.order, v->cp.jst,
+                           v->cp.segbase, v->cp.ja, v->L.nt};
+        KernelTimer kt(s, "varlen_w");
+        hipLaunchKernelGGL(k_vl_w, dim3((unsigned)v->cp.g2), dim3(kVlBlock), 2 * sizeof(unsigned long long) * kVlIds, st,
+                           cw, v->n, reinterpret_cast<const unsigned long long*>(v->od), P<unsigned long long>(v->W),
+                           RegionBloom{nullptr, 0, 0, 0}, nullptr, nullptr);
+    }
+    hipLaunchKernelGGL(k_vl_yonly, dim3(grid(s, v->n)), dim3(256), 0, st, v->n, v->d.b, v->d.b_full,
+                       P<unsigned long long>(v->W), P<unsigned long long>(v->sl), reinterpret_cast<long long*>(y));
+    HIP_CHECK(hipGetLastError());
+}
+
+int64_t varlen_shard_finish(VarlenShard* v, Buf& out_ids, Buf& out_cnt) {
+    using namespace varlen;
+    capsmi_session* s = v->s;
+    hipStream_t st = s->stream;
+    const int64_t n = v->n;
+    if (v->need3) {
+        REQUIRE(v->y != nullptr, CAPSMI_ERR_ILLEGAL_ARGUMENT, "varlen shard: mid() before finish()");
+        v->ody = dev_alloc(2 * sizeof(int64_t) * n, st);
+        hipLaunchKernelGGL(k_vl_pack, dim3(grid(s, n)), dim3(256), 0, st, n, reinterpret_cast<const long long*>(v->od),
+                           reinterpret_cast<const long long*>(v->y), P<longlong2>(v->ody));
+    }
+    if (v->cp.pool) {
+        const ChunkWalk cw{P<uint2>(v->cp.pool), P<unsigned long long>(v->cp.meta), v->cp.order, v->cp.jst,
+                           v->cp.segbase, v->cp.ja, v->L.nt};
+        KernelTimer kt(s, "varlen_t");
+        hipLaunchKernelGGL(k_vl_t, dim3((unsigned)v->cp.g2), dim3(kVlBlock), 2 * sizeof(unsigned long long) * kVlIds, st,
+                           cw, v->d.a, v->d.a_full, n, reinterpret_cast<const unsigned long long*>(v->od),
+                           v->need3 ? P<longlong2>(v->ody) : nullptr, P<unsigned long long>(v->T2),
+                           P<unsigned long long>(v->T3), RegionBloom{nullptr, 0, 0, 0}, nullptr,
+                           PairHash{nullptr, nullptr, nullptr, 0});
+    }
+    Buf cnt = dev_alloc(sizeof(int64_t) * n, st), flags = dev_alloc(n, st);
+    hipLaunchKernelGGL(k_final, dim3(grid(s, n)), dim3(256), 0, st, n, v->d, v->lower, v->upper,
+                       reinterpret_cast<const unsigned long long*>(v->od), P<unsigned long long>(v->sl),
+                       P<unsigned long long>(v->T2), P<unsigned long long>(v->T3), P<int64_t>(cnt), P<uint8_t>(flags));
+    if (v->own_lo > 0) HIP_CHECK(hipMemsetAsync(P<uint8_t>(flags), 0, v->own_lo, st));  // rows of owned a only
+    if (v->own_hi < n) HIP_CHECK(hipMemsetAsync(P<uint8_t>(flags) + v->own_hi, 0, n - v->own_hi, st));
+    HIP_CHECK(hipGetLastError());
+    Buf idx;
+    const int64_t rows = flags_to_indices(s, P<uint8_t>(flags), n, idx);
+    out_ids = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), st);
+    out_cnt = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), st);
+    gather_col(P<int64_t>(cnt), nullptr, P<int64_t>(idx), rows, P<int64_t>(out_cnt), nullptr, st);
+    if (rows > 0) {
+        HIP_CHECK(hipMemcpyAsync(P<void>(out_ids), P<void>(idx), sizeof(int64_t) * rows, hipMemcpyDeviceToDevice, st));
+        add_i64(P<int64_t>(out_ids), v->d.lo, rows, st);
+    }
+    return rows;
+}
+
+void varlen_shard_free(VarlenShard* v) { delete v; }
 
 }  // namespace capsmi

@@ -300,6 +300,23 @@ capsmi_status capsmi_var_length_count(capsmi_session* s, int32_t nrels, capsmi_t
                                       const char* src_col, const char* dst_col, const capsmi_bitmap* a_ok,
                                       const capsmi_bitmap* b_ok, int32_t lower, int32_t upper, const char* id_name,
                                       const char* count_name, capsmi_table** out);
+/* Sharded form of capsmi_var_length_count for one rank of a multi-GPU run.  The
+ * rank owns the source ids [own_lo, own_hi); `out_rels` hold the relationships whose source it
+ * owns, `in_rels` those from other ranks' sources into its owned ids.  `od` and `y` are caller
+ * device buffers of (b_ok->hi - b_ok->lo) int64 each:
+ *   begin  writes the rank's partial out-degrees into od -> the caller sums od over ranks in place;
+ *   mid    writes the rank's partial Y into y            -> the caller sums y over ranks in place;
+ *   finish returns the (id, count) rows of the owned ids.  od / y must stay valid until finish. */
+typedef struct capsmi_varlen_shard capsmi_varlen_shard;
+capsmi_status capsmi_varlen_shard_begin(capsmi_session* s, int32_t nout, capsmi_table* const* out_rels, int32_t nin,
+                                        capsmi_table* const* in_rels, const char* src_col, const char* dst_col,
+                                        const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, int32_t lower,
+                                        int32_t upper, int64_t own_lo, int64_t own_hi, int64_t* od,
+                                        capsmi_varlen_shard** out);
+capsmi_status capsmi_varlen_shard_mid(capsmi_varlen_shard* v, int64_t* y);
+capsmi_status capsmi_varlen_shard_finish(capsmi_varlen_shard* v, const char* id_name, const char* count_name,
+                                         capsmi_table** out);
+capsmi_status capsmi_varlen_shard_release(capsmi_varlen_shard* v);
 /* Cyclic triangle count (C4), fused:
  *   MATCH (a)-[r1]->(b)-[r2]->(c)-[r3]->(a) WHERE n_ok(a) AND n_ok(b) AND n_ok(c) RETURN count(*)
  * (two Expands + ExpandInto on (c, a), RelationalPlanner.scala:113-154, plus pairwise uniqueness).

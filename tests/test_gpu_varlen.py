@@ -196,3 +196,58 @@ def test_filter_sub_regions(session, monkeypatch, sublog):
     forced through CAPSMI_VL_SUBLOG: same answer."""
     monkeypatch.setenv("CAPSMI_VL_SUBLOG", str(sublog))
     test_many_source_slices(session, 0)
+
+
+def _sharded(session, n, src, dst, a_mask, b_mask, lo, hi, nparts):
+    """The multi-GPU C5 protocol emulated on one device: per rank the relationships it owns by
+    source plus those into its owned ids from other ranks; od and Y summed over ranks by torch
+    between the phases (the all-reduces); the ranks' rows concatenated."""
+    import torch
+    from capsmi import ColumnData, I64, Session, graph
+    session = Session(0)  # on torch's stream: the torch sums between the phases are ordered with the kernels
+    session.set_stream(torch.cuda.current_stream().cuda_stream)
+    a_ok = graph.NodeBitmap(session, 0, n).add_scan(session.table([ColumnData("id", I64, np.nonzero(a_mask)[0])]))
+    b_ok = graph.NodeBitmap(session, 0, n).add_scan(session.table([ColumnData("id", I64, np.nonzero(b_mask)[0])]))
+    nw = (n + 31) // 32
+    bounds = [(min(32 * (r * nw // nparts), n), min(32 * ((r + 1) * nw // nparts), n)) for r in range(nparts)]
+    ods = [torch.zeros(n, dtype=torch.int64, device="cuda") for _ in range(nparts)]
+    ys = [torch.zeros(n, dtype=torch.int64, device="cuda") for _ in range(nparts)]
+    shards = []
+    for r, (ol, oh) in enumerate(bounds):
+        own_s = (src >= ol) & (src < oh)
+        own_t = (dst >= ol) & (dst < oh)
+        out_t = _table(session, src[own_s], dst[own_s])
+        in_t = _table(session, src[own_t & ~own_s], dst[own_t & ~own_s])
+        shards.append(graph.VarlenShard(session, [out_t], [in_t], a_ok, b_ok, lo, hi, ol, oh, ods[r].data_ptr()))
+    od = sum(ods)
+    for r in range(nparts):
+        ods[r].copy_(od)
+        shards[r].mid(ys[r].data_ptr())
+    y = sum(ys)
+    got = {}
+    for r in range(nparts):
+        ys[r].copy_(y)
+        out = shards[r].finish("a", "cnt")
+        got.update(zip(out.column("a").values.tolist(), out.column("cnt").values.tolist()))
+        shards[r].release()
+    return got
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nparts", [1, 2, 3, 4])
+def test_sharded_matches_enumeration(session, nparts):
+    """Owner-partitioned C5 (rows of each rank's own ids; reciprocal pairs across ranks; self-loops;
+    multi-edges) against edge-distinct path enumeration."""
+    rng = np.random.default_rng(40 + nparts)
+    n, m = 3000, 30_000
+    src = rng.integers(0, n, m).astype(np.int64)
+    dst = rng.integers(0, n, m).astype(np.int64)
+    k = m // 5
+    src[k:2 * k], dst[k:2 * k] = dst[:k].copy(), src[:k].copy()
+    src[-200:] = dst[-200:]
+    a_mask = rng.random(n) < 0.8
+    b_mask = rng.random(n) < 0.7
+    for lo, hi in [(1, 3), (2, 3), (1, 2)]:
+        got = _sharded(session, n, src, dst, a_mask, b_mask, lo, hi, nparts)
+        _, g = cpu.var_length_count(n, src, dst, lo, hi, a_mask.astype(np.uint8), b_mask.astype(np.uint8))
+        assert got == {int(i): int(g[i]) for i in np.nonzero(g)[0]}
