@@ -327,11 +327,10 @@ def run_single(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and wl == "c2":
-        sys.exit("the C2 line is single-GPU (SURVEY.md 8d)")
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
-    if world > 1:  # C4: replicated oriented graph, vertex shares; C5: owner(source) shards
+    if world > 1:  # C2: rels by owner(source), local expand; C4: replicated oriented graph, vertex shares;
+        # C5: owner(source) shards
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         init_dist(dist, local)
@@ -347,6 +346,8 @@ def run_single(args):
         del into
         od_buf = torch.zeros(n, dtype=torch.int64, device="cuda")
         y_buf = torch.zeros(n, dtype=torch.int64, device="cuda")
+    elif wl == "c2" and world > 1:  # each rank expands its own sources; output stays partitioned
+        rels = graph.rmat_rels(sess, scale, 0, m, probs, 42, part_col=graph.PART_SOURCE, part=rank, nparts=world)
     else:
         rels = graph.rmat_rels(sess, scale, 0, m, probs, 42)
     kind = graph.NODES_PERSON if wl == "c2" else graph.NODES_ALL
@@ -360,6 +361,10 @@ def run_single(args):
             a_ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id", pred)
             b_ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id")
             out = graph.expand_filter(sess, rels, a_ok, b_ok, ["source", "target"], ["a", "b"])
+            if world > 1:
+                t = torch.tensor([out.size], dtype=torch.int64, device="cuda")
+                dist.all_reduce(t)
+                return int(t.item()), out
             return out.size, out
         ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id")
         if wl == "c4":  # = graph.triangle_count: build the trigraph, count, release
@@ -426,10 +431,17 @@ def run_single(args):
                 ref = int(graph.var_length_count(sess, [full], ok, ok, 1, 3).column("count").values.sum())
                 check = "ok" if ref == res else f"MISMATCH {res} vs unsharded {ref}"
                 del full
+    if wl == "c2" and world > 1 and rank == 0:  # the whole table on one device gives the same row count
+        full = graph.rmat_rels(sess, scale, 0, m, probs, 42)
+        a_ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id", pred)
+        b_ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id")
+        ref = graph.expand_filter(sess, full, a_ok, b_ok, ["source", "target"], ["a", "b"]).size
+        check = "ok" if ref == res else f"MISMATCH {res} vs unsharded {ref}"
+        del full
     matched = res
-    m_kern = rels.size if shard_c5 else m  # relationships behind one launch of this rank's kernels
+    m_kern = rels.size if world > 1 and wl in ("c2", "c5") else m  # relationships behind one launch here
     # algorithmic bytes per launch of the kernels whose traffic is a plain function of the input
-    alg = {"bitmap_add": n * 8, "expand_filter": m * 16 + (2 * res * 8 if wl == "c2" else 0),
+    alg = {"bitmap_add": n * 8, "expand_filter": m_kern * 16 + (2 * out.size * 8 if wl == "c2" else 0),
            "tri_pack": m * 24, "part_scatter1": m_kern * 24, "varlen_deg": m_kern * 8, "varlen_w": m_kern * 8,
            "varlen_t": m_kern * 8, "varlen_rev": m * 24 + m * 8,  # target partition + filter walk
            # both triangle kernels together: the oriented adjacency read once (8-B offsets, 4-B
@@ -458,6 +470,9 @@ def run_single(args):
     if shard_c5:
         line["config"]["parallelism"] = (f"owner(source) shards over {world} GPU(s); od and Y all-reduced between "
                                          f"phases; in-relationships exchanged at ingest")
+    elif wl == "c2" and world > 1:
+        line["config"]["parallelism"] = f"relationships by owner(source) over {world} GPU(s); row count all-reduced"
+    if check is not None or (world > 1 and wl in ("c2", "c5")):
         line["query"]["check_vs_unsharded"] = check
     line["cpu_baseline"] = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_single(wl, cpu_scale, ef, probs)
     if rank == 0:
