@@ -288,58 +288,41 @@ __device__ __forceinline__ void flush_acc(unsigned long long* acc, unsigned long
 }
 
 // pass 1 (source partition, pair = (target, source)): od(v), s(v)
+// With od: od(s) (LDS) and self-loop counts s(v) (global atomics: rare).  With f2part: the
+// candidate pairs s -> t (those the first-level filter passes) marked in the block's F2 region for
+// slice(s), stored whole per slice segment into partial slot w + j (k_vl_bset's scheme), and
+// counted.  One 1024-lane block per CU either way (64 KiB accumulators + 64 KiB F2 region).
 __global__ void __launch_bounds__(kVlBlock) k_vl_deg(ChunkWalk cw, const uint32_t* __restrict__ bw, int b_full,
                                                      int64_t n, unsigned long long* __restrict__ od,
-                                                     unsigned long long* __restrict__ sl) {
+                                                     unsigned long long* __restrict__ sl, RegionBloom bl,
+                                                     uint4* __restrict__ f2part, unsigned long long* __restrict__ ncand) {
     extern __shared__ unsigned long long vl_lds[];
-    unsigned long long *a_od = vl_lds, *a_s = vl_lds + kVlIds;
-    for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_od[i] = a_s[i] = 0;
-    __syncthreads();
-    walk_chunks(
-        cw,
-        [&](uint2 p, int) {
-            const uint32_t t = p.x, s = p.y, i = s & (kVlIds - 1);
-            if (bit_of(bw, b_full, t)) atomicAdd(&a_od[i], 1ULL);
-            if (s == t) atomicAdd(&a_s[i], 1ULL);
-        },
-        [&](int j) {
-            flush_acc(a_od, od, j, n);
-            flush_acc(a_s, sl, j, n);
-        });
-}
-
-// pass 2: W(v) = sum_{v -> w} od(w)
-// It also marks the candidate pairs s -> t (those whose reverse may exist) in the block's F2 region
-// for slice(s), stored whole per slice segment into partial slot w + j (k_vl_bset's scheme), and
-// counts them.
-__global__ void __launch_bounds__(kVlBlock) k_vl_w(ChunkWalk cw, int64_t n, const unsigned long long* __restrict__ od,
-                                                   unsigned long long* __restrict__ W, RegionBloom bl,
-                                                   uint4* __restrict__ f2part, unsigned long long* __restrict__ ncand) {
-    extern __shared__ unsigned long long vl_lds[];
-    unsigned long long* a_w = vl_lds;
+    unsigned long long* a_od = vl_lds;
     uint32_t* f2 = reinterpret_cast<uint32_t*>(vl_lds + kVlIds);
     __shared__ unsigned int cand;
     if (threadIdx.x == 0) cand = 0;
     unsigned int mine = 0;  // this lane's candidates (one LDS add per wave at the end)
-    for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_w[i] = 0;
-    for (int i = threadIdx.x; i < kF2Words; i += kVlBlock) f2[i] = 0;
+    for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_od[i] = 0;
+    if (f2part)
+        for (int i = threadIdx.x; i < kF2Words; i += kVlBlock) f2[i] = 0;
     __syncthreads();
     walk_chunks(
         cw,
         [&](uint2 p, int) {  // p = (t, s)
-            if (W) {
-                const unsigned long long x = od[p.x];
-                if (x) atomicAdd(&a_w[p.y & (kVlIds - 1)], x);
+            const uint32_t t = p.x, s = p.y;
+            if (od) {
+                if (bit_of(bw, b_full, t)) atomicAdd(&a_od[s & (kVlIds - 1)], 1ULL);
+                if (s == t) atomicAdd(&sl[s], 1ULL);
             }
-            if (f2part && rb_test(bl, p.y, pkey(p.x, p.y))) {
+            if (f2part && rb_test(bl, s, pkey(t, s))) {
                 uint32_t word, bits;
-                f2_pos(pkey(p.y, p.x), word, bits);
+                f2_pos(pkey(s, t), word, bits);
                 atomicOr(&f2[word], bits);
                 ++mine;
             }
         },
         [&](int j) {
-            if (W) flush_acc(a_w, W, j, n);
+            if (od) flush_acc(a_od, od, j, n);
             if (f2part) {
                 uint4* g = f2part + (((size_t)blockIdx.x + j) * (kF2Words / 4));
                 const uint4* l = reinterpret_cast<const uint4*>(f2);
@@ -348,10 +331,28 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_w(ChunkWalk cw, int64_t n, cons
                 for (int i = threadIdx.x; i < kF2Words; i += kVlBlock) f2[i] = 0;
             }
         });
-    for (int o = 32; o > 0; o >>= 1) mine += __shfl_down(mine, o, 64);
-    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&cand, mine);
+    if (f2part) {
+        for (int o = 32; o > 0; o >>= 1) mine += __shfl_down(mine, o, 64);
+        if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&cand, mine);
+        __syncthreads();
+        if (threadIdx.x == 0 && cand) atomicAdd(ncand, (unsigned long long)cand);
+    }
+}
+
+// pass 2: W(v) = sum_{v -> w} od(w); 64 KiB of LDS, two blocks per CU for the random od gathers
+__global__ void __launch_bounds__(kVlBlock) k_vl_w(ChunkWalk cw, int64_t n, const unsigned long long* __restrict__ od,
+                                                   unsigned long long* __restrict__ W) {
+    extern __shared__ unsigned long long vl_lds[];
+    unsigned long long* a_w = vl_lds;
+    for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_w[i] = 0;
     __syncthreads();
-    if (threadIdx.x == 0 && cand) atomicAdd(ncand, (unsigned long long)cand);
+    walk_chunks(
+        cw,
+        [&](uint2 p, int) {  // p = (t, s)
+            const unsigned long long x = od[p.x];
+            if (x) atomicAdd(&a_w[p.y & (kVlIds - 1)], x);
+        },
+        [&](int j) { flush_acc(a_w, W, j, n); });
 }
 
 // pairs a -> b passing both filters into the exact table (the sharded form's separate walk)
@@ -571,22 +572,24 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
         }
         {
             KernelTimer kt(s, "varlen_deg");
+            Buf f2part;
+            if (need3) {
+                f2 = dev_alloc(sizeof(uint32_t) * kF2Words * (size_t)L.nt, st);
+                f2part = dev_alloc(sizeof(uint32_t) * kF2Words * ((size_t)cp.g2 + L.nt), st);
+            }
             hipLaunchKernelGGL(k_vl_deg, dim3(g), dim3(kVlBlock), lds2, st, cw, d.b, d.b_full, n, P<unsigned long long>(od),
-                               P<unsigned long long>(sl));
-        }
-        if (need3) {
-            f2 = dev_alloc(sizeof(uint32_t) * kF2Words * (size_t)L.nt, st);
-            {
-                KernelTimer kt(s, "varlen_w");
-                Buf f2part = dev_alloc(sizeof(uint32_t) * kF2Words * ((size_t)cp.g2 + L.nt), st);
-                const size_t ldsw = sizeof(unsigned long long) * kVlIds + sizeof(uint32_t) * kF2Words;
-                HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_vl_w),
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)ldsw));
-                hipLaunchKernelGGL(k_vl_w, dim3(g), dim3(kVlBlock), ldsw, st, cw, n, P<unsigned long long>(od),
-                                   P<unsigned long long>(W), bl, P<uint4>(f2part), P<unsigned long long>(cand));
+                               P<unsigned long long>(sl), bl, P<uint4>(f2part), P<unsigned long long>(cand));
+            if (need3) {
                 const RegionBloom f2b{P<uint32_t>(f2), 0, 19, 0};  // kF2Words * 32 = 2^19 bits per slice
                 hipLaunchKernelGGL(k_vl_bmerge, dim3(grid(s, (int64_t)(kF2Words / 4) * L.nt)), dim3(256), 0, st, cp.jst,
                                    L.nt, cp.g2, P<uint4>(f2part), f2b);
+            }
+        }
+        if (need3) {
+            {
+                KernelTimer kt(s, "varlen_w");
+                hipLaunchKernelGGL(k_vl_w, dim3(g), dim3(kVlBlock), lds2 / 2, st, cw, n, P<unsigned long long>(od),
+                                   P<unsigned long long>(W));
             }
             const int64_t nc = read_scalar(s, P<int64_t>(cand));
             if (getenv("CAPSMI_VL_DEBUG"))
@@ -765,7 +768,8 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
                            v->cp.segbase, v->cp.ja, L.nt};
         KernelTimer kt(s, "varlen_deg");
         hipLaunchKernelGGL(k_vl_deg, dim3((unsigned)v->cp.g2), dim3(kVlBlock), lds2, st, cw, v->d.b, v->d.b_full, n,
-                           reinterpret_cast<unsigned long long*>(od), P<unsigned long long>(v->sl));
+                           reinterpret_cast<unsigned long long*>(od), P<unsigned long long>(v->sl),
+                           RegionBloom{nullptr, 0, 0, 0}, nullptr, nullptr);
     }
     const int64_t mall = mout + min_;
     if (v->need3 && mall > 0) {
@@ -803,8 +807,8 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
         HIP_CHECK(hipMemsetAsync(P<void>(cand), 0, sizeof(int64_t), st));
         {
             Buf f2part = dev_alloc(sizeof(uint32_t) * kF2Words * ((size_t)ca.g2 + L.nt), st);
-            hipLaunchKernelGGL(k_vl_w, dim3((unsigned)ca.g2), dim3(kVlBlock), lds2, st, aw, n, nullptr, nullptr, bl,
-                               P<uint4>(f2part), P<unsigned long long>(cand));
+            hipLaunchKernelGGL(k_vl_deg, dim3((unsigned)ca.g2), dim3(kVlBlock), lds2, st, aw, v->d.b, v->d.b_full, n,
+                               nullptr, nullptr, bl, P<uint4>(f2part), P<unsigned long long>(cand));
             const RegionBloom f2b{P<uint32_t>(v->f2), 0, 19, 0};
             hipLaunchKernelGGL(k_vl_bmerge, dim3(grid(s, (int64_t)(kF2Words / 4) * L.nt)), dim3(256), 0, st, ca.jst,
                                L.nt, ca.g2, P<uint4>(f2part), f2b);
@@ -837,9 +841,8 @@ void varlen_shard_mid(VarlenShard* v, int64_t* y) {
         const ChunkWalk cw{P<uint2>(v->cp.pool), P<unsigned long long>(v->cp.meta), v->cp.order, v->cp.jst,
                            v->cp.segbase, v->cp.ja, v->L.nt};
         KernelTimer kt(s, "varlen_w");
-        hipLaunchKernelGGL(k_vl_w, dim3((unsigned)v->cp.g2), dim3(kVlBlock), 2 * sizeof(unsigned long long) * kVlIds, st,
-                           cw, v->n, reinterpret_cast<const unsigned long long*>(v->od), P<unsigned long long>(v->W),
-                           RegionBloom{nullptr, 0, 0, 0}, nullptr, nullptr);
+        hipLaunchKernelGGL(k_vl_w, dim3((unsigned)v->cp.g2), dim3(kVlBlock), sizeof(unsigned long long) * kVlIds, st,
+                           cw, v->n, reinterpret_cast<const unsigned long long*>(v->od), P<unsigned long long>(v->W));
     }
     hipLaunchKernelGGL(k_vl_yonly, dim3(grid(s, v->n)), dim3(256), 0, st, v->n, v->d.b, v->d.b_full,
                        P<unsigned long long>(v->W), P<unsigned long long>(v->sl), reinterpret_cast<long long*>(y));
