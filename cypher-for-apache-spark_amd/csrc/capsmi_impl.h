@@ -195,6 +195,9 @@ void eval_predicate(capsmi_session* s, const capsmi_table* t, int32_t nnodes, co
 // sort (k_sort.hip): stable ascending permutation of row indices by a 64-bit key
 void radix_sort_pairs(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, int begin_bit,
                       int end_bit);
+// the same over an explicit list of 8-bit digit positions (LSD order; digits no key uses skipped);
+// vals may be null (keys only)
+void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, const std::vector<int>& shifts);
 void order_keys(capsmi_session* s, const int64_t* col, const uint8_t* valid, int type, bool desc, bool null_pass,
                 const int64_t* perm, int64_t n, uint64_t* key);
 

@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(kBlock) k_scatter(const uint64_t* __restrict__
         int d = 0;
         if (act) {
             k = keys[i];
-            v = vals[i];
+            if (vals) v = vals[i];
             d = (int)((k >> shift) & 255);
         }
         unsigned long long peers = __ballot(act);
@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(kBlock) k_scatter(const uint64_t* __restrict__
             int64_t pos = base_d[d] + rank;
             for (int w = 0; w < wid; ++w) pos += wcnt[w][d];
             okeys[pos] = k;
-            ovals[pos] = v;
+            if (vals) ovals[pos] = v;
         }
         __syncthreads();
         base_d[threadIdx.x] += wcnt[0][threadIdx.x] + wcnt[1][threadIdx.x] + wcnt[2][threadIdx.x] + wcnt[3][threadIdx.x];
@@ -78,17 +78,23 @@ __global__ void __launch_bounds__(kBlock) k_scatter(const uint64_t* __restrict__
 }  // namespace
 
 void radix_sort_pairs(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, int begin_bit, int end_bit) {
-    if (n <= 1 || end_bit <= begin_bit) return;
+    std::vector<int> shifts;
+    for (int shift = begin_bit; shift < end_bit; shift += 8) shifts.push_back(shift);
+    radix_sort_digits(s, keys, vals, n, shifts);
+}
+
+void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, const std::vector<int>& shifts) {
+    if (n <= 1 || shifts.empty()) return;
     hipStream_t st = s->stream;
     const int64_t ntiles = (n + kTile - 1) / kTile;
     Buf hist = dev_alloc(sizeof(int64_t) * 256 * ntiles, st);
     Buf offs = dev_alloc(sizeof(int64_t) * (256 * ntiles + 1), st);
     Buf k2 = dev_alloc(sizeof(uint64_t) * n, st);
-    Buf v2 = dev_alloc(sizeof(int64_t) * n, st);
+    Buf v2 = vals ? dev_alloc(sizeof(int64_t) * n, st) : Buf();
     uint64_t *ki = keys, *ko = P<uint64_t>(k2);
     int64_t *vi = vals, *vo = P<int64_t>(v2);
     int passes = 0;
-    for (int shift = begin_bit; shift < end_bit; shift += 8) {
+    for (const int shift : shifts) {
         hipLaunchKernelGGL(k_hist, dim3((unsigned)ntiles), dim3(kBlock), 0, st, ki, n, shift, ntiles, P<int64_t>(hist));
         exclusive_scan_i64(P<int64_t>(hist), P<int64_t>(offs), 256 * ntiles, st);
         hipLaunchKernelGGL(k_scatter, dim3((unsigned)ntiles), dim3(kBlock), 0, st, ki, vi, n, shift, ntiles,
@@ -100,7 +106,7 @@ void radix_sort_pairs(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t 
     }
     if (passes & 1) {
         HIP_CHECK(hipMemcpyAsync(keys, ki, sizeof(uint64_t) * n, hipMemcpyDeviceToDevice, st));
-        HIP_CHECK(hipMemcpyAsync(vals, vi, sizeof(int64_t) * n, hipMemcpyDeviceToDevice, st));
+        if (vals) HIP_CHECK(hipMemcpyAsync(vals, vi, sizeof(int64_t) * n, hipMemcpyDeviceToDevice, st));
     }
 }
 

@@ -62,18 +62,36 @@ __global__ void k_dir_runs(const uint64_t* __restrict__ k, const int64_t* __rest
     }
 }
 
-// undirected runs (<= 2 records each) -> combined multiplicities, degrees
+// undirected runs (<= 2 records each) -> combined multiplicities, degrees.  The runs are sorted
+// by their lower end, so a wave's lanes with the same lower end are contiguous: one atomic per
+// such segment (hubs would otherwise serialise hundreds of thousands of adds on one counter).
 __global__ void k_und_runs(const uint64_t* __restrict__ uk, const int64_t* __restrict__ uv,
                            const int64_t* __restrict__ heads, int64_t nruns, int64_t nvalid,
                            uint64_t* __restrict__ ek, int64_t* __restrict__ ev, uint32_t* __restrict__ deg) {
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nruns; r += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t h = heads[r], h2 = r + 1 < nruns ? heads[r + 1] : nvalid;
-        int64_t v = 0;
-        for (int64_t i = h; i < h2; ++i) v += uv[i];
-        ek[r] = uk[h];
-        ev[r] = v;
-        atomicAdd(&deg[(uint32_t)(uk[h] >> 32)], 1u);
-        atomicAdd(&deg[(uint32_t)uk[h]], 1u);
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); r0 < nruns; r0 += stride) {  // wave-uniform
+        const int64_t r = r0 + lane;
+        const bool act = r < nruns;  // the active lanes are a prefix of the wave
+        uint32_t mn = 0;
+        if (act) {
+            const int64_t h = heads[r], h2 = r + 1 < nruns ? heads[r + 1] : nvalid;
+            int64_t v = 0;
+            for (int64_t i = h; i < h2; ++i) v += uv[i];
+            const uint64_t key = uk[h];
+            ek[r] = key;
+            ev[r] = v;
+            mn = (uint32_t)(key >> 32);
+            atomicAdd(&deg[(uint32_t)key], 1u);
+        }
+        const uint32_t prev = __shfl_up(mn, 1, 64);
+        const bool head = act && (lane == 0 || prev != mn);
+        const unsigned long long hb = __ballot(head), am = __ballot(act);
+        if (head) {
+            const unsigned long long later = lane == 63 ? 0ULL : hb >> (lane + 1);
+            const int next = later ? lane + 1 + __builtin_ctzll(later) : __popcll(am);
+            atomicAdd(&deg[mn], (uint32_t)(next - lane));
+        }
     }
 }
 
@@ -456,7 +474,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     int64_t m = 0;
     for (int i = 0; i < nt; ++i) m += ms[i];
     const int bits = bits_for((uint64_t)n);
-    Buf key = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), st), val = dev_alloc(sizeof(int64_t) * (m > 0 ? m : 1), st);
+    Buf key = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), st);
     {
         KernelTimer kt(s, "tri_pack");
         int64_t off = 0;
@@ -467,8 +485,14 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
             off += ms[i];
         }
     }
-    iota_i64(P<int64_t>(val), 0, m, st);
-    radix_sort_pairs(s, P<uint64_t>(key), P<int64_t>(val), m, 0, 64);  // kNone (all ones) sorts last
+    // keys (s << 32 | t) use the digits of s and t only, plus the top digit that makes kNone (all
+    // ones) sort last; the directed runs need the keys alone
+    std::vector<int> kd;
+    for (int sh = 0; sh < bits; sh += 8) kd.push_back(sh);
+    for (int sh = 32; sh < 32 + bits; sh += 8) kd.push_back(sh);
+    const std::vector<int> od = kd;
+    if (kd.back() < 56) kd.push_back(56);
+    radix_sort_digits(s, P<uint64_t>(key), nullptr, m, kd);
     // directed runs
     Buf f = dev_alloc(m > 0 ? m : 1, st), heads;
     hipLaunchKernelGGL(k_heads, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, P<uint8_t>(f));
@@ -493,8 +517,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         hipLaunchKernelGGL(k_dir_runs, dim3(grid(s, nruns)), dim3(256), 0, st, P<uint64_t>(key), P<int64_t>(heads),
                            nruns, nvalid, P<uint32_t>(g.sl), P<uint64_t>(uk), P<int64_t>(uv));
     key.reset();
-    val.reset();
-    radix_sort_pairs(s, P<uint64_t>(uk), P<int64_t>(uv), nruns, 0, 64);
+    radix_sort_digits(s, P<uint64_t>(uk), P<int64_t>(uv), nruns, kd);
     Buf f2 = dev_alloc(nruns > 0 ? nruns : 1, st), heads2;
     hipLaunchKernelGGL(k_heads, dim3(grid(s, nruns)), dim3(256), 0, st, P<uint64_t>(uk), nruns, P<uint8_t>(f2));
     const int64_t ne = flags_to_indices(s, P<uint8_t>(f2), nruns, heads2);
@@ -523,7 +546,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     if (ne > 0)
         hipLaunchKernelGGL(k_orient, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ek), P<int64_t>(g.ev), ne,
                            P<uint32_t>(deg), P<uint64_t>(g.ok), P<int64_t>(g.ov));
-    radix_sort_pairs(s, P<uint64_t>(g.ok), P<int64_t>(g.ov), ne, 0, 32 + bits);
+    radix_sort_digits(s, P<uint64_t>(g.ok), P<int64_t>(g.ov), ne, od);  // no kNone among the oriented keys
     g.off = dev_alloc(sizeof(int64_t) * (n + 1), st);
     hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, n, P<int64_t>(g.off));
     g.tg = dev_alloc(sizeof(uint32_t) * (ne > 0 ? ne : 1), st);
