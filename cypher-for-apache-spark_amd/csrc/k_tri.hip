@@ -138,21 +138,23 @@ __global__ void k_offsets(const uint64_t* __restrict__ ok_, int64_t ne, int64_t 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr int kSmallDeg = 64;
 constexpr int kWedgeUnroll = 4;  // wedges per lane with their target loads in flight together
-constexpr int kSmallSlots = 128;
+constexpr int kSmallSlots = 256;  // load <= 1/4: a miss (most wedges) ends after ~1.4 probes
 constexpr int kTriBlock = 256;  // small: 4 waves
 constexpr int kBigBlock = 1024;
 constexpr int kBigChunk = 2048;  // out-list entries per LDS chunk
-constexpr int kBigSlots = 4096;
+constexpr int kBigSlots = 8192;  // load <= 1/4
 
 __device__ __forceinline__ uint32_t hslot(uint32_t w, int log2cap) { return (w * 0x9E3779B1u) >> (32 - log2cap); }
 
-__device__ __forceinline__ void hinsert(uint32_t* hk, uint64_t* hv, int log2cap, uint32_t w, uint64_t pv) {
+// key w, and the index of its entry in the hashed list (the payload is read through it, on hits)
+template <class Idx>
+__device__ __forceinline__ void hinsert(uint32_t* hk, Idx* hi, int log2cap, uint32_t w, uint32_t idx) {
     const uint32_t mask = (1u << log2cap) - 1;
     uint32_t sl = hslot(w, log2cap);
     while (true) {
         const uint32_t prev = atomicCAS(&hk[sl], kEmpty, w);
         if (prev == kEmpty) {
-            hv[sl] = pv;
+            hi[sl] = (Idx)idx;
             return;
         }
         sl = (sl + 1) & mask;
@@ -205,7 +207,7 @@ __device__ __forceinline__ int seg_of(const uint32_t* pre, int d, uint32_t f) {
 
 struct SmallWave {
     uint32_t hk[kSmallSlots];
-    uint64_t hv[kSmallSlots];
+    uint8_t hi[kSmallSlots];  // lane of the key's entry: payload = vp[hi]
     uint64_t vp[kSmallDeg];
     int64_t voff[kSmallDeg];
     uint32_t vl[kSmallDeg];
@@ -225,8 +227,8 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
         const int64_t u = us[q];
         const int64_t b = off[u];
         const int d = (int)(off[u + 1] - b);
-        W.hk[lane] = kEmpty;
-        W.hk[lane + 64] = kEmpty;
+#pragma unroll
+        for (int k = 0; k < kSmallSlots / 64; ++k) W.hk[lane + 64 * k] = kEmpty;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         uint32_t dv = 0;
@@ -238,7 +240,7 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
             W.vl[lane] = v;
             W.vp[lane] = pv;
             W.voff[lane] = vo;
-            hinsert(W.hk, W.hv, 7, v, pv);
+            hinsert(W.hk, W.hi, 8, v, (uint32_t)lane);
         }
         uint32_t x = dv;  // wave inclusive scan of the out-degrees of the v's
 #pragma unroll
@@ -267,8 +269,8 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
 #pragma unroll
             for (int k = 0; k < kWedgeUnroll; ++k) {
                 if (w[k] == kEmpty) continue;
-                const int sl = hfind(W.hk, 7, w[k]);
-                if (sl >= 0) acc += tri_weight(W.vp[ii[k]], (uint64_t)ov[pos[k]], W.hv[sl]);
+                const int sl = hfind(W.hk, 8, w[k]);
+                if (sl >= 0) acc += tri_weight(W.vp[ii[k]], (uint64_t)ov[pos[k]], W.vp[W.hi[sl]]);
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -322,7 +324,7 @@ constexpr int kVChunk = 256;
 
 struct ItemLds {
     uint32_t hk[kBigSlots];
-    uint64_t hv[kBigSlots];
+    uint16_t hi[kBigSlots];  // position of the key in out(u)'s hash chunk: payload = ov[b + h0 + hi]
     uint64_t vp[kVChunk];
     int64_t voff[kVChunk];
     uint32_t vl[kVChunk];
@@ -371,7 +373,7 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
         const int hn = min(kBigChunk, d - h0), vn = min(kVChunk, d - v0);
         for (int k = threadIdx.x; k < kBigSlots; k += kBigBlock) L.hk[k] = kEmpty;
         __syncthreads();
-        for (int k = threadIdx.x; k < hn; k += kBigBlock) hinsert(L.hk, L.hv, 12, tg[b + h0 + k], (uint64_t)ov[b + h0 + k]);
+        for (int k = threadIdx.x; k < hn; k += kBigBlock) hinsert(L.hk, L.hi, 13, tg[b + h0 + k], (uint32_t)k);
         for (int k = threadIdx.x; k < vn; k += kBigBlock) {
             const uint32_t v = tg[b + v0 + k];
             const int64_t vo = off[v];
@@ -399,8 +401,8 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
 #pragma unroll
             for (int k = 0; k < kWedgeUnroll; ++k) {
                 if (w[k] == kEmpty) continue;
-                const int sl = hfind(L.hk, 12, w[k]);
-                if (sl >= 0) acc += tri_weight(L.vp[ii[k]], (uint64_t)ov[pos[k]], L.hv[sl]);
+                const int sl = hfind(L.hk, 13, w[k]);
+                if (sl >= 0) acc += tri_weight(L.vp[ii[k]], (uint64_t)ov[pos[k]], (uint64_t)ov[b + h0 + L.hi[sl]]);
             }
         }
         __syncthreads();
