@@ -138,7 +138,7 @@ __global__ void k_offsets(const uint64_t* __restrict__ ok_, int64_t ne, int64_t 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr int kSmallDeg = 64;
 constexpr int kWedgeUnroll = 4;  // wedges per lane with their target loads in flight together
-constexpr int kSmallSlots = 256;  // load <= 1/4: a miss (most wedges) ends after ~1.4 probes
+constexpr int kSmallSlots = 512;  // load <= 1/8: a miss (most wedges) ends after ~1.2 probes
 constexpr int kTriBlock = 256;  // small: 4 waves
 constexpr int kBigBlock = 1024;
 constexpr int kBigChunk = 2048;  // out-list entries per LDS chunk
@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
             W.vl[lane] = v;
             W.vp[lane] = pv;
             W.voff[lane] = vo;
-            hinsert(W.hk, W.hi, 8, v, (uint32_t)lane);
+            hinsert(W.hk, W.hi, 9, v, (uint32_t)lane);
         }
         uint32_t x = dv;  // wave inclusive scan of the out-degrees of the v's
 #pragma unroll
@@ -269,7 +269,7 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
 #pragma unroll
             for (int k = 0; k < kWedgeUnroll; ++k) {
                 if (w[k] == kEmpty) continue;
-                const int sl = hfind(W.hk, 8, w[k]);
+                const int sl = hfind(W.hk, 9, w[k]);
                 if (sl >= 0) acc += tri_weight(W.vp[ii[k]], (uint64_t)ov[pos[k]], W.vp[W.hi[sl]]);
             }
         }
