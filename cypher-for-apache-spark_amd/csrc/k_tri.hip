@@ -146,6 +146,22 @@ constexpr int kBigSlots = 8192;  // load <= 1/4
 
 __device__ __forceinline__ uint32_t hslot(uint32_t w, int log2cap) { return (w * 0x9E3779B1u) >> (32 - log2cap); }
 
+// One-bit pre-filter in front of each hash: a wave's probe loop runs as long as its longest
+// chain, so most wedges (misses) are rejected with one LDS read instead.
+constexpr int kSmallBloomBits = 10, kBigBloomBits = 16;
+
+__device__ __forceinline__ uint32_t bbit(uint32_t w, int bits) { return (w * 0x85EBCA6Bu) >> (32 - bits); }
+
+__device__ __forceinline__ void bset(uint32_t* bf, int bits, uint32_t w) {
+    const uint32_t x = bbit(w, bits);
+    atomicOr(&bf[x >> 5], 1u << (x & 31));
+}
+
+__device__ __forceinline__ bool btest(const uint32_t* bf, int bits, uint32_t w) {
+    const uint32_t x = bbit(w, bits);
+    return (bf[x >> 5] >> (x & 31)) & 1u;
+}
+
 // key w, and the index of its entry in the hashed list (the payload is read through it, on hits)
 template <class Idx>
 __device__ __forceinline__ void hinsert(uint32_t* hk, Idx* hi, int log2cap, uint32_t w, uint32_t idx) {
@@ -206,6 +222,7 @@ __device__ __forceinline__ int seg_of(const uint32_t* pre, int d, uint32_t f) {
 }
 
 struct SmallWave {
+    uint32_t bf[(1 << kSmallBloomBits) / 32];
     uint32_t hk[kSmallSlots];
     uint8_t hi[kSmallSlots];  // lane of the key's entry: payload = vp[hi]
     uint64_t vp[kSmallDeg];
@@ -229,6 +246,7 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
         const int d = (int)(off[u + 1] - b);
 #pragma unroll
         for (int k = 0; k < kSmallSlots / 64; ++k) W.hk[lane + 64 * k] = kEmpty;
+        if (lane < (1 << kSmallBloomBits) / 32) W.bf[lane] = 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         uint32_t dv = 0;
@@ -241,6 +259,7 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
             W.vp[lane] = pv;
             W.voff[lane] = vo;
             hinsert(W.hk, W.hi, 9, v, (uint32_t)lane);
+            bset(W.bf, kSmallBloomBits, v);
         }
         uint32_t x = dv;  // wave inclusive scan of the out-degrees of the v's
 #pragma unroll
@@ -268,7 +287,7 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
             }
 #pragma unroll
             for (int k = 0; k < kWedgeUnroll; ++k) {
-                if (w[k] == kEmpty) continue;
+                if (w[k] == kEmpty || !btest(W.bf, kSmallBloomBits, w[k])) continue;
                 const int sl = hfind(W.hk, 9, w[k]);
                 if (sl >= 0) acc += tri_weight(W.vp[ii[k]], (uint64_t)ov[pos[k]], W.vp[W.hi[sl]]);
             }
@@ -323,6 +342,7 @@ __device__ uint32_t big_scan(const uint32_t* in, uint32_t* outp, int n, uint32_t
 constexpr int kVChunk = 256;
 
 struct ItemLds {
+    uint32_t bf[(1 << kBigBloomBits) / 32];
     uint32_t hk[kBigSlots];
     uint16_t hi[kBigSlots];  // position of the key in out(u)'s hash chunk: payload = ov[b + h0 + hi]
     uint64_t vp[kVChunk];
@@ -372,8 +392,13 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
         const int h0 = (local / nvc) * kBigChunk, v0 = (local % nvc) * kVChunk;
         const int hn = min(kBigChunk, d - h0), vn = min(kVChunk, d - v0);
         for (int k = threadIdx.x; k < kBigSlots; k += kBigBlock) L.hk[k] = kEmpty;
+        for (int k = threadIdx.x; k < (1 << kBigBloomBits) / 32; k += kBigBlock) L.bf[k] = 0;
         __syncthreads();
-        for (int k = threadIdx.x; k < hn; k += kBigBlock) hinsert(L.hk, L.hi, 13, tg[b + h0 + k], (uint32_t)k);
+        for (int k = threadIdx.x; k < hn; k += kBigBlock) {
+            const uint32_t w = tg[b + h0 + k];
+            hinsert(L.hk, L.hi, 13, w, (uint32_t)k);
+            bset(L.bf, kBigBloomBits, w);
+        }
         for (int k = threadIdx.x; k < vn; k += kBigBlock) {
             const uint32_t v = tg[b + v0 + k];
             const int64_t vo = off[v];
@@ -400,7 +425,7 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
             }
 #pragma unroll
             for (int k = 0; k < kWedgeUnroll; ++k) {
-                if (w[k] == kEmpty) continue;
+                if (w[k] == kEmpty || !btest(L.bf, kBigBloomBits, w[k])) continue;
                 const int sl = hfind(L.hk, 13, w[k]);
                 if (sl >= 0) acc += tri_weight(L.vp[ii[k]], (uint64_t)ov[pos[k]], (uint64_t)ov[b + h0 + L.hi[sl]]);
             }
