@@ -205,22 +205,6 @@ __device__ __forceinline__ int seg_from(const uint32_t* pre, int lo, int d, uint
     return lo;
 }
 
-// segment cursor for a lane's increasing wedge indices: stays put while f is still inside the
-// current v's range (long out-lists), searches only the remaining segments otherwise
-__device__ __forceinline__ int seg_next(const uint32_t* pre, int i, int d, uint32_t f) {
-    return (i + 1 < d && pre[i + 1] <= f) ? seg_from(pre, i + 1, d, f) : i;
-}
-
-// last i in [0, d) with pre[i] <= f (pre[0] = 0)
-__device__ __forceinline__ int seg_of(const uint32_t* pre, int d, uint32_t f) {
-    int lo = 0, hi = d;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (pre[mid] <= f) lo = mid; else hi = mid;
-    }
-    return lo;
-}
-
 struct SmallWave {
     uint32_t bf[(1 << kSmallBloomBits) / 32];
     uint32_t hk[kSmallSlots];
@@ -272,7 +256,11 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the lane's current v: index, list base (voff - pre) and the next v's first wedge, in
+        // registers; LDS is read only when the lane moves to another v
         int i = 0;
+        int64_t base = W.voff[0];
+        uint32_t nxt = d > 1 ? W.pre[1] : 0xFFFFFFFFu;
         for (uint32_t f0 = lane; f0 < total; f0 += kWedgeUnroll * 64) {
             int ii[kWedgeUnroll];
             int64_t pos[kWedgeUnroll];
@@ -280,9 +268,13 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
 #pragma unroll
             for (int k = 0; k < kWedgeUnroll; ++k) {
                 const uint32_t f = f0 + k * 64;
-                if (f < total) i = seg_next(W.pre, i, d, f);
+                if (f < total && f >= nxt) {
+                    i = seg_from(W.pre, i + 1, d, f);
+                    base = W.voff[i] - (int64_t)W.pre[i];
+                    nxt = i + 1 < d ? W.pre[i + 1] : 0xFFFFFFFFu;
+                }
                 ii[k] = i;
-                pos[k] = W.voff[i] + (f - W.pre[i]);
+                pos[k] = base + f;
                 w[k] = f < total ? tg[pos[k]] : kEmpty;
             }
 #pragma unroll
@@ -362,11 +354,19 @@ __global__ void k_tri_items(const int64_t* __restrict__ off, const int64_t* __re
     items[q] = ((d + kBigChunk - 1) / kBigChunk) * ((d + kVChunk - 1) / kVChunk);
 }
 
+// item -> its u's index q (items of q are [ipre[q], ipre[q+1])): one load per item instead of a
+// ~20-step dependent binary search over ipre at the start of every item
+__global__ void k_tri_item_map(const int64_t* __restrict__ ipre, int64_t nu, uint32_t* __restrict__ item_q) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nu; q += (int64_t)gridDim.x * blockDim.x)
+        for (int64_t it = ipre[q]; it < ipre[q + 1]; ++it) item_q[it] = (uint32_t)q;
+}
+
 __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __restrict__ tg,
                                                              const int64_t* __restrict__ ov,
                                                              const int64_t* __restrict__ off,
                                                              const int64_t* __restrict__ us, int64_t nu,
                                                              const int64_t* __restrict__ ipre,
+                                                             const uint32_t* __restrict__ item_q,
                                                              unsigned long long* __restrict__ ctr,
                                                              unsigned long long* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -380,11 +380,7 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
         const int64_t it = (int64_t)item;
         __syncthreads();  // `item` is rewritten next round
         if (it >= total) break;  // block-uniform
-        int64_t lo = 0, hi = nu;  // last q with ipre[q] <= it
-        while (hi - lo > 1) {
-            const int64_t mid = (lo + hi) >> 1;
-            if (ipre[mid] <= it) lo = mid; else hi = mid;
-        }
+        const int64_t lo = item_q[it];
         const int64_t u = us[lo], b = off[u];
         const int d = (int)(off[u + 1] - b);
         const int nvc = (d + kVChunk - 1) / kVChunk;
@@ -409,7 +405,9 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
         }
         __syncthreads();
         const uint32_t tw = big_scan(L.dv, L.pre, vn, L.wtot);
-        int i = 0;
+        int i = 0;  // the lane's current v, as in k_tri_small
+        int64_t base = L.voff[0];
+        uint32_t nxt = vn > 1 ? L.pre[1] : 0xFFFFFFFFu;
         for (uint32_t f0 = threadIdx.x; f0 < tw; f0 += kWedgeUnroll * kBigBlock) {
             // kWedgeUnroll wedges per lane: all their target loads in flight before the probes
             int ii[kWedgeUnroll];
@@ -418,9 +416,13 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
 #pragma unroll
             for (int k = 0; k < kWedgeUnroll; ++k) {
                 const uint32_t f = f0 + k * kBigBlock;
-                if (f < tw) i = seg_next(L.pre, i, vn, f);
+                if (f < tw && f >= nxt) {
+                    i = seg_from(L.pre, i + 1, vn, f);
+                    base = L.voff[i] - (int64_t)L.pre[i];
+                    nxt = i + 1 < vn ? L.pre[i + 1] : 0xFFFFFFFFu;
+                }
                 ii[k] = i;
-                pos[k] = L.voff[i] + (f - L.pre[i]);
+                pos[k] = base + f;
                 w[k] = f < tw ? tg[pos[k]] : kEmpty;
             }
 #pragma unroll
@@ -606,13 +608,16 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
             hipLaunchKernelGGL(k_tri_items, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, P<int64_t>(g.off), bu,
                                nb, items);
             exclusive_scan_i64(items, ipre, nb, st);
+            const int64_t nitems = read_scalar(s, ipre + nb);
+            Buf iq = dev_alloc(sizeof(uint32_t) * (nitems > 0 ? nitems : 1), st);
+            hipLaunchKernelGGL(k_tri_item_map, dim3(grid(s, nb)), dim3(256), 0, st, ipre, nb, P<uint32_t>(iq));
             Buf ctr = dev_alloc(sizeof(unsigned long long), st);
             HIP_CHECK(hipMemsetAsync(P<void>(ctr), 0, sizeof(unsigned long long), st));
             const size_t lds = sizeof(ItemLds);
             HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_tri_big_items),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             hipLaunchKernelGGL(k_tri_big_items, dim3((unsigned)(s->num_cus * 4)), dim3(kBigBlock), lds, st,
-                               P<uint32_t>(g.tg), P<int64_t>(g.ov), P<int64_t>(g.off), bu, nb, ipre,
+                               P<uint32_t>(g.tg), P<int64_t>(g.ov), P<int64_t>(g.off), bu, nb, ipre, P<uint32_t>(iq),
                                P<unsigned long long>(ctr), P<unsigned long long>(out));
         }
         if (se > sb) {
