@@ -36,7 +36,7 @@ METRIC = "matched rows/sec for 2-hop MATCH on R-MAT 2^30 edges; % HBM roofline @
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 KERNELS = ("part_scatter1", "part_scatter2_hop1", "part_scatter2", "hop1", "hop2", "mid_combine", "bitmap_add")
 # timer name -> kernel name as rocprofv3 reports it (hop1 and hop2 are two instances of k_hop_2d)
-KERNEL_SYMBOL = {"part_scatter1": "k_scatter_c", "part_scatter2_hop1": "k_scatter_s2", "part_scatter2": "k_scatter_s2",
+KERNEL_SYMBOL = {"part_scatter1": "k_scatter_l", "part_scatter2_hop1": "k_scatter_s2", "part_scatter2": "k_scatter_s2",
                  "hop1": "k_hop_2d", "hop2": "k_hop_2d", "mid_combine": "k_mid_combine", "bitmap_add": "k_bitmap_add"}
 
 
@@ -305,7 +305,7 @@ SINGLE = {
 
 
 # timer name -> kernel symbol (rocprofv3 / PMC summary name) where they differ
-SINGLE_SYMBOL = {"expand_filter": "k_expand_pairs", "part_scatter1": "k_scatter_c", "varlen_deg": "k_vl_deg",
+SINGLE_SYMBOL = {"expand_filter": "k_expand_pairs", "part_scatter1": "k_scatter_l", "varlen_deg": "k_vl_deg",
                  "varlen_w": "k_vl_w", "varlen_t": "k_vl_t", "varlen_rev": "k_vl_bset", "varlen_recip": "k_vl_recip", "varlen_cand": "k_vl_cand", "triangles": "k_tri_big_items+k_tri_small"}
 
 

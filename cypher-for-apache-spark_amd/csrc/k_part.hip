@@ -36,27 +36,30 @@ namespace part {
 
 
 
-__host__ __device__ constexpr size_t scatter1_lds(int nb, int ns) {
-    return sizeof(uint2) * kP1Tile + sizeof(uint32_t) * ((size_t)nb * hist_words(ns) + 6 * (size_t)nb + kP1Block / 64 + 4);
+__host__ __device__ constexpr size_t scatter1_lds(int nb, int ns, int block = kP1Block, int tile = kP1Tile) {
+    return sizeof(uint2) * tile + sizeof(uint32_t) * ((size_t)nb * hist_words(ns) + 7 * (size_t)nb + block / 64 + 4);
 }
 
 // chunks per pass-1 block: tiles of the busiest block + one open chunk per slice
-__host__ __device__ inline int64_t chunks_per_block(int64_t m, int64_t grid, int nt) {
-    return ((m + kP1Tile - 1) / kP1Tile + grid - 1) / grid + nt;
+__host__ __device__ inline int64_t chunks_per_block(int64_t m, int64_t grid, int nt, int64_t tile = kP1Tile) {
+    return ((m + tile - 1) / tile + grid - 1) / grid + nt;
 }
 
 __device__ __forceinline__ void hist_add(uint32_t* H, int hw, int b, uint32_t i) {
     atomicAdd(&H[b * hw + (int)(i >> 1)], 1u << ((i & 1u) * 16u));
 }
 
-__global__ void __launch_bounds__(kP1Block) k_scatter_c(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+template <int B, int IT, int MINW, bool NTS>  // MINW: waves per SIMD to fit
+__global__ void __launch_bounds__(B, MINW) k_scatter_c(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                        int64_t m, Layout L, int swap, int64_t chunk0, size_t trash,
                                                        uint2* __restrict__ pool, unsigned long long* __restrict__ cmeta,
                                                        uint32_t* __restrict__ chist) {
+    constexpr int T = B * IT;
+    static_assert(T <= kCh, "a pass-1 run must span at most two chunks");
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     const int nb = L.nt, hw = hist_words(L.ns);
     uint2* stage = reinterpret_cast<uint2*>(smem);
-    uint32_t* H = reinterpret_cast<uint32_t*>(stage + kP1Tile);  // nb rows of hw words: open chunks' cell counts
+    uint32_t* H = reinterpret_cast<uint32_t*>(stage + T);  // nb rows of hw words: open chunks' cell counts
     uint32_t* cnt = H + (size_t)nb * hw;  // this tile's run length per slice
     uint32_t* loc = cnt + nb;             // run start in the stage
     uint32_t* ph = loc + nb;              // open chunk per slice (kNone: none yet) ...
@@ -64,45 +67,45 @@ __global__ void __launch_bounds__(kP1Block) k_scatter_c(const int64_t* __restric
     uint32_t* p1 = fl + nb;               // chunk opened by this tile's run (kNone: the run fits)
     uint32_t* opened = p1 + nb;           // slices that opened a chunk in this tile
     uint32_t* wtot = opened + nb;
-    uint32_t* misc = wtot + kP1Block / 64;  // [0] chunks opened this tile, [1] next free chunk
-    for (int i = threadIdx.x; i < nb * hw; i += kP1Block) H[i] = 0;
-    for (int i = threadIdx.x; i < nb; i += kP1Block) {
+    uint32_t* misc = wtot + B / 64;  // [0] chunks opened this tile, [1] next free chunk
+    for (int i = threadIdx.x; i < nb * hw; i += B) H[i] = 0;
+    for (int i = threadIdx.x; i < nb; i += B) {
         ph[i] = kNone;
         fl[i] = 0;
     }
     if (threadIdx.x == 0) {
         misc[0] = 0;
-        misc[1] = (uint32_t)(chunk0 + (int64_t)blockIdx.x * chunks_per_block(m, gridDim.x, nb));
+        misc[1] = (uint32_t)(chunk0 + (int64_t)blockIdx.x * chunks_per_block(m, gridDim.x, nb, T));
     }
     const uint64_t range = (uint64_t)(L.hi - L.lo);
     const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
-    const int64_t stride = (int64_t)gridDim.x * kP1Tile;
-    int64_t sr[kItems], tr[kItems];
-    int64_t t0 = (int64_t)blockIdx.x * kP1Tile;
-    if (t0 < m) load_tile<kP1Block>(src, dst, t0, m, vec, sr, tr);
+    const int64_t stride = (int64_t)gridDim.x * T;
+    int64_t sr[IT], tr[IT];
+    int64_t t0 = (int64_t)blockIdx.x * T;
+    if (t0 < m) load_tile<B>(src, dst, t0, m, vec, sr, tr);
     for (; t0 < m; t0 += stride) {  // block-uniform
-        for (int i = threadIdx.x; i < nb; i += kP1Block) cnt[i] = 0;
+        for (int i = threadIdx.x; i < nb; i += B) cnt[i] = 0;
         __syncthreads();
-        uint2 pr[kItems];
-        uint32_t rk[kItems];
+        uint2 pr[IT];
+        uint32_t rk[IT];
         uint32_t valid = 0;
 #pragma unroll
-        for (int u = 0; u < kItems; ++u) {
-            const int64_t e = t0 + item_off<kP1Block>(u);
+        for (int u = 0; u < IT; ++u) {
+            const int64_t e = t0 + item_off<B>(u);
             const uint64_t s = (uint64_t)(sr[u] - L.lo), t = (uint64_t)(tr[u] - L.lo);
             const bool ok = e < m && s < range && t < range;
             pr[u] = swap ? make_uint2((uint32_t)t, (uint32_t)s) : make_uint2((uint32_t)s, (uint32_t)t);
             valid |= (ok ? 1u : 0u) << u;
             rk[u] = 0;
         }
-        if (t0 + stride < m) load_tile<kP1Block>(src, dst, t0 + stride, m, vec, sr, tr);  // prefetch
+        if (t0 + stride < m) load_tile<B>(src, dst, t0 + stride, m, vec, sr, tr);  // prefetch
 #pragma unroll
-        for (int u = 0; u < kItems; ++u)
+        for (int u = 0; u < IT; ++u)
             if ((valid >> u) & 1u) rk[u] = atomicAdd(&cnt[pr[u].y >> L.tbits], 1u);
         __syncthreads();
-        const uint32_t total = block_exclusive_scan<kP1Block>(cnt, loc, nb, wtot);
+        const uint32_t total = block_exclusive_scan<B>(cnt, loc, nb, wtot);
         const uint32_t nf = misc[1];
-        for (int i = threadIdx.x; i < nb; i += kP1Block) {  // a run that does not fit opens a chunk
+        for (int i = threadIdx.x; i < nb; i += B) {  // a run that does not fit opens a chunk
             const uint32_t c = cnt[i];
             uint32_t np = kNone;
             if (c && (ph[i] == kNone || fl[i] + c > (uint32_t)kCh)) {
@@ -113,13 +116,13 @@ __global__ void __launch_bounds__(kP1Block) k_scatter_c(const int64_t* __restric
             p1[i] = np;
         }
 #pragma unroll
-        for (int u = 0; u < kItems; ++u)
+        for (int u = 0; u < IT; ++u)
             if ((valid >> u) & 1u) stage[loc[pr[u].y >> L.tbits] + rk[u]] = pr[u];
         __syncthreads();
         // run item r of slice b: r < room -> open chunk ph[b] at fl[b] + r, else the opened chunk p1[b]
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {  // unconditional stores (idx >= total -> trash chunk)
-            const uint32_t idx = (uint32_t)(k * kP1Block + (int)threadIdx.x);
+        for (int k = 0; k < IT; ++k) {  // unconditional stores (idx >= total -> trash chunk)
+            const uint32_t idx = (uint32_t)(k * B + (int)threadIdx.x);
             const uint2 p = stage[idx];
             const int b = min((int)(p.y >> L.tbits), nb - 1);  // stale stage entries past `total`
             const uint32_t r = idx - loc[b], o = ph[b], room = o == kNone ? 0u : (uint32_t)kCh - fl[b];
@@ -128,12 +131,16 @@ __global__ void __launch_bounds__(kP1Block) k_scatter_c(const int64_t* __restric
             const size_t at = idx >= total ? trash + threadIdx.x
                             : first       ? (size_t)o * kCh + fl[b] + r
                                           : (size_t)p1[b] * kCh + (r - room);
-            pool[at] = p;
+            if (NTS)
+                __builtin_nontemporal_store(*reinterpret_cast<const unsigned long long*>(&p),
+                                            reinterpret_cast<unsigned long long*>(pool + at));
+            else
+                pool[at] = p;
         }
         const uint32_t nop = misc[0];
         if (nop) {  // block-uniform: retire the filled chunks (histogram row out), count the runs' tails
             __syncthreads();
-            for (uint32_t x = threadIdx.x; x < nop * (uint32_t)hw; x += kP1Block) {
+            for (uint32_t x = threadIdx.x; x < nop * (uint32_t)hw; x += B) {
                 const int b = (int)opened[x / hw], w = (int)(x % hw);
                 if (ph[b] != kNone) {
                     chist[(size_t)ph[b] * hw + w] = H[b * hw + w];
@@ -144,12 +151,12 @@ __global__ void __launch_bounds__(kP1Block) k_scatter_c(const int64_t* __restric
             for (uint32_t k = 0; k < nop; ++k) {
                 const int b = (int)opened[k];
                 const uint32_t room = ph[b] == kNone ? 0u : (uint32_t)kCh - fl[b];
-                for (uint32_t r = room + threadIdx.x; r < cnt[b]; r += kP1Block)
+                for (uint32_t r = room + threadIdx.x; r < cnt[b]; r += B)
                     hist_add(H, hw, b, stage[loc[b] + r].x >> L.sbits);
             }
         }
         __syncthreads();
-        for (int i = threadIdx.x; i < nb; i += kP1Block) {  // advance the open chunks
+        for (int i = threadIdx.x; i < nb; i += B) {  // advance the open chunks
             const uint32_t c = cnt[i];
             if (!c) continue;
             if (p1[i] == kNone) {
@@ -166,9 +173,235 @@ __global__ void __launch_bounds__(kP1Block) k_scatter_c(const int64_t* __restric
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < nb; i += kP1Block)
+    for (int i = threadIdx.x; i < nb; i += B)
         if (ph[i] != kNone) cmeta[ph[i]] = chunk_meta(i, fl[i]);
-    for (int x = threadIdx.x; x < nb * hw; x += kP1Block) {
+    for (int x = threadIdx.x; x < nb * hw; x += B) {
+        const uint32_t p = ph[x / hw];
+        if (p != kNone) chist[(size_t)p * hw + x % hw] = H[x];
+    }
+}
+
+// ---- pass 1, whole-line variant (used when its LDS fits: <= 128 target slices at 2^19 ids) -------
+// The chunk bookkeeping of a tile (scan of the run lengths, chunks opened) and the deferred part of
+// the previous tile (retiring the chunks it filled, the histogram counts of its runs' tails,
+// advancing the open chunks) run in wave 0 between the ranking and the regroup; run lengths are
+// double-buffered by tile parity, so a tile takes three barriers.
+
+// orders one wave's LDS accesses (wave 0 runs the bookkeeping alone)
+__device__ __forceinline__ void wave_lds_order() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x;
+}
+
+// Pass 1 writing whole 128-byte lines only.  A slice's run is appended behind the items its open
+// chunk still holds back (fewer than kLine, kept in LDS): the combined sequence is staged, every
+// complete line of it is stored, and the tail is held back again.  A line is then written once,
+// by one wave, instead of in two pieces by two tiles, which the L2 may write back separately.
+// The chunk contents and histograms equal k_scatter_c's up to the order within a chunk.
+constexpr int kLine = 16;  // pairs per 128-byte line
+
+__device__ __forceinline__ uint32_t held(uint32_t o, uint32_t f) { return o == kNone ? 0u : (f & (kLine - 1)); }
+
+// wave 0: retire the chunks the previous tile filled, add its runs' tails to the opened chunks'
+// histogram rows, advance the open chunks and clear the previous run lengths `cp`
+__device__ __forceinline__ void p1l_settle(const Layout& L, int hw, const uint2* stage, uint32_t* H, uint32_t* cp,
+                                           const uint32_t* loc, uint32_t* ph, uint32_t* fl, const uint32_t* p1,
+                                           const uint32_t* opened, uint32_t* misc, unsigned long long* cmeta,
+                                           uint32_t* chist) {
+    const int nb = L.nt, lane = threadIdx.x & 63;
+    const uint32_t nop = misc[0];
+    for (uint32_t x = lane; x < nop * (uint32_t)hw; x += 64) {
+        const int b = (int)opened[x / hw], w = (int)(x % hw);
+        if (ph[b] != kNone) {
+            chist[(size_t)ph[b] * hw + w] = H[b * hw + w];
+            H[b * hw + w] = 0;
+        }
+    }
+    wave_lds_order();
+    for (uint32_t k = 0; k < nop; ++k) {  // items past the old chunk's room belong to the opened one
+        const int b = (int)opened[k];
+        const uint32_t h = held(ph[b], fl[b]);
+        const uint32_t room = ph[b] == kNone ? 0u : (uint32_t)kCh - (fl[b] - h);
+        for (uint32_t r = room + lane; r < h + cp[b]; r += 64) hist_add(H, hw, b, stage[loc[b] + r].x >> L.sbits);
+    }
+    wave_lds_order();
+    for (int i = lane; i < nb; i += 64) {
+        const uint32_t c = cp[i];
+        if (!c) continue;
+        if (p1[i] == kNone) {
+            fl[i] += c;
+        } else {
+            if (ph[i] != kNone) cmeta[ph[i]] = chunk_meta(i, (uint32_t)kCh);
+            fl[i] = ph[i] == kNone ? c : fl[i] + c - (uint32_t)kCh;
+            ph[i] = p1[i];
+        }
+        cp[i] = 0;
+    }
+    if (lane == 0) {
+        misc[1] += nop;
+        misc[0] = 0;
+    }
+    wave_lds_order();
+}
+
+// wave 0: run starts `loc` of this tile (exclusive scan over each slice's staged sequence = held
+// items + run), the chunks its runs open (p1, opened, misc[0]) and the staged total (misc[2])
+__device__ __forceinline__ void p1l_plan(int nb, const uint32_t* cn, uint32_t* loc, const uint32_t* ph,
+                                         const uint32_t* fl, uint32_t* p1, uint32_t* opened, uint32_t* misc) {
+    const int lane = threadIdx.x & 63;
+    const int per = (nb + 63) / 64, b0 = lane * per, b1 = min(b0 + per, nb);
+    uint32_t sum = 0, need = 0;
+    for (int i = b0; i < b1; ++i) {
+        const uint32_t c = cn[i];
+        sum += c + held(ph[i], fl[i]);
+        need += (c && (ph[i] == kNone || fl[i] + c > (uint32_t)kCh)) ? 1u : 0u;
+    }
+    const uint32_t is = wave_incl_scan(sum), in = wave_incl_scan(need);
+    uint32_t pre = is - sum, k = in - need;
+    const uint32_t nf = misc[1];
+    for (int i = b0; i < b1; ++i) {
+        const uint32_t c = cn[i];
+        loc[i] = pre;
+        pre += c + held(ph[i], fl[i]);
+        uint32_t np = kNone;
+        if (c && (ph[i] == kNone || fl[i] + c > (uint32_t)kCh)) {
+            np = nf + k;
+            opened[k++] = (uint32_t)i;
+        }
+        p1[i] = np;
+    }
+    if (lane == 63) {
+        misc[0] = in;
+        misc[2] = is;
+    }
+    wave_lds_order();
+}
+
+__host__ __device__ constexpr size_t scatter1l_lds(int nb, int ns, int block, int tile) {
+    return sizeof(uint2) * ((size_t)tile + (size_t)nb * (2 * kLine)) +
+           sizeof(uint32_t) * ((size_t)nb * hist_words(ns) + 7 * (size_t)nb + block / 64 + 4);
+}
+
+template <int B, int IT, int MINW>
+__global__ void __launch_bounds__(B, MINW) k_scatter_l(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                      int64_t m, Layout L, int swap, int64_t chunk0, size_t trash,
+                                                      uint2* __restrict__ pool, unsigned long long* __restrict__ cmeta,
+                                                      uint32_t* __restrict__ chist) {
+    constexpr int T = B * IT;
+    static_assert(T <= kCh && kCh % kLine == 0, "a pass-1 run must span at most two chunks");
+    extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
+    const int nb = L.nt, hw = hist_words(L.ns);
+    uint2* stage = reinterpret_cast<uint2*>(smem);    // T + nb * kLine: runs behind their held items
+    uint2* hold = stage + T + (size_t)nb * kLine;      // nb x kLine held items
+    uint32_t* H = reinterpret_cast<uint32_t*>(hold + (size_t)nb * kLine);
+    uint32_t* cnt = H + (size_t)nb * hw;
+    uint32_t* loc = cnt + 2 * nb;
+    uint32_t* ph = loc + nb;
+    uint32_t* fl = ph + nb;  // logical fill of the open chunk (held items included)
+    uint32_t* p1 = fl + nb;
+    uint32_t* opened = p1 + nb;
+    uint32_t* misc = opened + nb;
+    for (int i = threadIdx.x; i < nb * hw; i += B) H[i] = 0;
+    for (int i = threadIdx.x; i < nb; i += B) {
+        cnt[i] = 0;
+        cnt[nb + i] = 0;
+        ph[i] = kNone;
+        fl[i] = 0;
+    }
+    if (threadIdx.x == 0) {
+        misc[0] = 0;
+        misc[1] = (uint32_t)(chunk0 + (int64_t)blockIdx.x * chunks_per_block(m, gridDim.x, nb, T));
+    }
+    __syncthreads();
+    const uint64_t range = (uint64_t)(L.hi - L.lo);
+    const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
+    const int64_t stride = (int64_t)gridDim.x * T;
+    int64_t sr[IT], tr[IT];
+    int64_t t0 = (int64_t)blockIdx.x * T;
+    if (t0 < m) load_tile<B>(src, dst, t0, m, vec, sr, tr);
+    int par = 0;
+    bool pending = false;
+    for (; t0 < m; t0 += stride, par ^= 1) {
+        uint32_t* cn = cnt + par * nb;
+        uint2 pr[IT];
+        uint32_t rk[IT];
+        uint32_t valid = 0;
+#pragma unroll
+        for (int u = 0; u < IT; ++u) {
+            const int64_t e = t0 + item_off<B>(u);
+            const uint64_t s = (uint64_t)(sr[u] - L.lo), t = (uint64_t)(tr[u] - L.lo);
+            const bool ok = e < m && s < range && t < range;
+            pr[u] = swap ? make_uint2((uint32_t)t, (uint32_t)s) : make_uint2((uint32_t)s, (uint32_t)t);
+            valid |= (ok ? 1u : 0u) << u;
+            rk[u] = 0;
+        }
+        if (t0 + stride < m) load_tile<B>(src, dst, t0 + stride, m, vec, sr, tr);  // prefetch
+#pragma unroll
+        for (int u = 0; u < IT; ++u)
+            if ((valid >> u) & 1u) rk[u] = atomicAdd(&cn[pr[u].y >> L.tbits], 1u);
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            if (pending) p1l_settle(L, hw, stage, H, cnt + (par ^ 1) * nb, loc, ph, fl, p1, opened, misc, cmeta, chist);
+            p1l_plan(nb, cn, loc, ph, fl, p1, opened, misc);
+        }
+        __syncthreads();
+        pending = true;
+        const uint32_t total = misc[2];
+        for (int x = threadIdx.x; x < nb * kLine; x += B) {  // held items first
+            const int b = x / kLine, k = x % kLine;
+            if ((uint32_t)k < held(ph[b], fl[b])) stage[loc[b] + k] = hold[x];
+        }
+#pragma unroll
+        for (int u = 0; u < IT; ++u)
+            if ((valid >> u) & 1u) {
+                const int b = pr[u].y >> L.tbits;
+                stage[loc[b] + held(ph[b], fl[b]) + rk[u]] = pr[u];
+            }
+        __syncthreads();
+        // staged item r of slice b: logical position w + r of chunk ph[b] (w = written prefix) while
+        // it fits, else position r - room of the opened chunk p1[b]; positions below the chunk's
+        // last complete line are stored, the rest held back
+        for (uint32_t idx = threadIdx.x; idx < (uint32_t)(T + nb * kLine); idx += B) {
+            const uint2 p = stage[idx];
+            const int b = min((int)(p.y >> L.tbits), nb - 1);
+            const uint32_t r = idx - loc[b], o = ph[b], f = fl[b], h = held(o, f), c = cn[b];
+            const uint32_t w = f - h, room = o == kNone ? 0u : (uint32_t)kCh - w;
+            const bool first = r < room;
+            if (idx < total && first && r >= h) hist_add(H, hw, b, p.x >> L.sbits);
+            // end of the sequence in the chunk it lands in, and that chunk's stored prefix
+            const uint32_t end = first ? min(w + h + c, (uint32_t)kCh) : h + c - room;
+            const uint32_t pos = first ? w + r : r - room;
+            const uint32_t cut = end & ~(uint32_t)(kLine - 1);
+            if (idx >= total) {
+                break;  // idx only grows
+            } else if (pos < cut) {
+                pool[(size_t)(first ? o : p1[b]) * kCh + pos] = p;
+            } else {
+                hold[b * kLine + (pos - cut)] = p;
+            }
+        }
+    }
+    __syncthreads();
+    if (pending && threadIdx.x < 64)
+        p1l_settle(L, hw, stage, H, cnt + (par ^ 1) * nb, loc, ph, fl, p1, opened, misc, cmeta, chist);
+    __syncthreads();
+    for (int x = threadIdx.x; x < nb * kLine; x += B) {  // held tails
+        const int b = x / kLine, k = x % kLine;
+        if ((uint32_t)k < held(ph[b], fl[b])) pool[(size_t)ph[b] * kCh + (fl[b] - held(ph[b], fl[b])) + k] = hold[x];
+    }
+    for (int i = threadIdx.x; i < nb; i += B)
+        if (ph[i] != kNone) cmeta[ph[i]] = chunk_meta(i, fl[i]);
+    for (int x = threadIdx.x; x < nb * hw; x += B) {
         const uint32_t p = ph[x / hw];
         if (p != kNone) chist[(size_t)p * hw + x % hw] = H[x];
     }
@@ -296,12 +529,24 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
     const int nb = L.ns;
     const int64_t w = blockIdx.x, blocks = gridDim.x;
     uint2* stage = reinterpret_cast<uint2*>(smem);
-    unsigned long long* cur = smem + kTile;  // next output index per source cell, minus the run start
+    uint2* hold = stage + kTile;  // per source cell: the items of its unfinished output line, slot = index & 15
+    unsigned long long* cur = reinterpret_cast<unsigned long long*>(hold + (size_t)nb * kLine);  // next output index per cell
     uint32_t* cnt = reinterpret_cast<uint32_t*>(cur + nb);
     uint32_t* loc = cnt + nb;
-    uint32_t* wtot = loc + nb;
+    uint32_t* hc = loc + nb;  // items held per cell (all in the line of cur)
+    uint32_t* wtot = hc + nb;
     uint32_t* tl = wtot + kSBlock / 64;  // HOP1: target slice marks
     const SegSplit S(jst, L.nt, blocks);
+    for (int i = threadIdx.x; i < nb; i += kSBlock) hc[i] = 0;
+    auto flush_held = [&]() {  // the segment's unfinished lines (shared with a neighbouring segment)
+        for (int x = threadIdx.x; x < nb * kLine; x += kSBlock) {
+            const int b = x / kLine, k = x % kLine;
+            if ((uint32_t)k < hc[b]) {
+                const unsigned long long pos = cur[b] - hc[b] + (unsigned long long)k;
+                out[pos] = hold[b * kLine + (int)(pos & (kLine - 1))];
+            }
+        }
+    };
     auto load_chunk = [&](int64_t q, uint2 (&pr)[kItems]) -> uint32_t {
         const uint32_t phys = order[q];
         const uint32_t fill = (uint32_t)(cmeta[phys] >> 32);
@@ -326,6 +571,10 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
     // compiler can wait for the loads alone); segment changes are the rare branch.
     for (int64_t q = qb; q < qe; ++q) {  // block-uniform
         if (q == seg_end) {
+            __syncthreads();
+            flush_held();
+            __syncthreads();
+            for (int i = threadIdx.x; i < nb; i += kSBlock) hc[i] = 0;
             Seg sg;
             do {
                 ++g;
@@ -377,24 +626,46 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
             }
         __syncthreads();
         const uint32_t total = block_exclusive_scan<kSBlock>(cnt, loc, nb, wtot);
+        // Whole output lines: a cell's run is stored up to the last line boundary it reaches, the
+        // rest held in LDS; held items go out when their line completes, together with the run
+        // items that complete it (so a line is written within one tile, not in pieces by two).
+        for (int x = threadIdx.x; x < nb * kLine; x += kSBlock) {
+            const int b = x / kLine, k = x % kLine;
+            if ((uint32_t)k < hc[b]) {
+                const unsigned long long c = cur[b], pos = c - hc[b] + (unsigned long long)k;
+                if (((c + cnt[b]) & ~(unsigned long long)(kLine - 1)) > (c & ~(unsigned long long)(kLine - 1)))
+                    out[pos] = hold[b * kLine + (int)(pos & (kLine - 1))];
+            }
+        }
 #pragma unroll
         for (int k = 0; k < kItems; ++k)
             if ((valid >> k) & 1u) stage[loc[pr[k].x >> L.sbits] + rk[k]] = pr[k];
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {  // unconditional stores; idx >= total -> trash slots
+        for (int k = 0; k < kItems; ++k) {
             const uint32_t idx = (uint32_t)(k * kSBlock + (int)threadIdx.x);
             const uint2 v = stage[idx];
             const int b = min((int)(v.x >> L.sbits), nb - 1);  // stale stage entries past `total`
-            out[idx < total ? (int64_t)cur[b] + idx - loc[b] : trash + threadIdx.x] = v;
+            const unsigned long long pos = cur[b] + idx - loc[b];
+            const unsigned long long cut = (cur[b] + cnt[b]) & ~(unsigned long long)(kLine - 1);
+            if (idx >= total)
+                out[trash + threadIdx.x] = v;
+            else if (pos < cut)
+                out[pos] = v;
+            else
+                hold[b * kLine + (int)(pos & (kLine - 1))] = v;
         }
         __syncthreads();
-        for (int i = threadIdx.x; i < nb; i += kSBlock) cur[i] += cnt[i];
+        for (int i = threadIdx.x; i < nb; i += kSBlock) {
+            const unsigned long long c = cur[i], n = cnt[i];
+            const unsigned long long cut = (c + n) & ~(unsigned long long)(kLine - 1);
+            hc[i] = cut > (c & ~(unsigned long long)(kLine - 1)) ? (uint32_t)(c + n - cut) : hc[i] + (uint32_t)n;
+            cur[i] = c + n;
+        }
     }
-    if (HOP1 && cur_j >= 0) {
-        __syncthreads();
-        flush_slice(tl, h1.M, cur_j, h1.gwords, h1.tmask);
-    }
+    __syncthreads();
+    flush_held();
+    if (HOP1 && cur_j >= 0) flush_slice(tl, h1.M, cur_j, h1.gwords, h1.tmask);
 }
 
 // One hop over the 2-D layout.  Block b streams relationships [b*per, (b+1)*per) of the
@@ -541,14 +812,24 @@ void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_
     cp.meta = dev_alloc(sizeof(unsigned long long) * npool, st);
     cp.chist = dev_alloc(sizeof(uint32_t) * hw * (size_t)npool, st);
     HIP_CHECK(hipMemsetAsync(P<void>(cp.meta), 0, sizeof(unsigned long long) * npool, st));
-    const size_t lds1 = scatter1_lds(L.nt, L.ns);
-    allow_lds(k_scatter_c, lds1);
+    const size_t lds1l = scatter1l_lds(L.nt, L.ns, kP1Block, kP1Tile);
+    const bool lines = lds1l <= (size_t)160 * 1024;
+    const size_t lds1 = lines ? lds1l : scatter1_lds(L.nt, L.ns);
+    if (lines)
+        allow_lds(k_scatter_l<kP1Block, kItems, 4>, lds1);
+    else
+        allow_lds(k_scatter_c<kP1Block, kItems, 4, kP1NT>, lds1);
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
         KernelTimer kt(s, "part_scatter1");
-        hipLaunchKernelGGL(k_scatter_c, dim3(g1[i]), dim3(kP1Block), lds1, st, srcs[i], dsts[i], ms[i], L, swap ? 1 : 0, c0[i],
-                           (size_t)npool * kCh,
-                           P<uint2>(cp.pool), P<unsigned long long>(cp.meta), P<uint32_t>(cp.chist));
+        if (lines)
+            hipLaunchKernelGGL((k_scatter_l<kP1Block, kItems, 4>), dim3(g1[i]), dim3(kP1Block), lds1, st, srcs[i], dsts[i],
+                               ms[i], L, swap ? 1 : 0, c0[i], (size_t)npool * kCh, P<uint2>(cp.pool),
+                               P<unsigned long long>(cp.meta), P<uint32_t>(cp.chist));
+        else
+            hipLaunchKernelGGL((k_scatter_c<kP1Block, kItems, 4, kP1NT>), dim3(g1[i]), dim3(kP1Block), lds1, st, srcs[i],
+                               dsts[i], ms[i], L, swap ? 1 : 0, c0[i], (size_t)npool * kCh, P<uint2>(cp.pool),
+                               P<unsigned long long>(cp.meta), P<uint32_t>(cp.chist));
     }
     HIP_CHECK(hipGetLastError());
 
@@ -623,8 +904,8 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
 
     Hop1Out ho{};
     if (fuse) ho = Hop1Out{BitV{P<uint32_t>(h1->b->words), h1->b->full ? 1 : 0}, h1->M, h1->S1, h1->S2, h1->b->nwords};
-    const size_t lds2 = sizeof(uint2) * kTile + sizeof(unsigned long long) * L.ns +
-                        sizeof(uint32_t) * (2 * L.ns + kSBlock / 64) + (fuse ? sizeof(uint32_t) * kSliceWords : 0);
+    const size_t lds2 = sizeof(uint2) * ((size_t)kTile + (size_t)L.ns * kLine) + sizeof(unsigned long long) * L.ns +
+                        sizeof(uint32_t) * (3 * L.ns + kSBlock / 64) + (fuse ? sizeof(uint32_t) * kSliceWords : 0);
     auto k2 = fuse ? k_scatter_s2<true> : k_scatter_s2<false>;
     allow_lds(k2, lds2);
     {

@@ -18,6 +18,7 @@ constexpr int kCh = kTile;                       // pairs per pass-1 chunk: a ti
 constexpr int kP1Block = 1024;                   // pass-1 workgroup (512 x 2 per CU measured slower)
 constexpr int kP1Tile = kP1Block * kItems;       // pass-1 tile (<= kCh)
 static_assert(kP1Tile <= kCh, "a pass-1 run must span at most two chunks");
+constexpr bool kP1NT = false;                    // pass-1 pool stores non-temporal
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 constexpr int kUnroll = 8;                       // loads in flight per lane in the hops
 constexpr int64_t kLoadMin = 8192;               // pull a source slice into LDS for >= this many rels
@@ -79,26 +80,38 @@ __device__ __forceinline__ int item_off(int u) {
 
 // Issue all of a tile's loads before any test: with a branch around each load the compiler
 // waits for every load before issuing the next.  `vec` = both columns 16-byte aligned.
-template <int B>
+template <int B, bool NTL = false, int N>
 __device__ __forceinline__ void load_tile(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t t0,
-                                          int64_t m, bool vec, int64_t (&sr)[kItems], int64_t (&tr)[kItems]) {
+                                          int64_t m, bool vec, int64_t (&sr)[N], int64_t (&tr)[N]) {
     const int64_t* __restrict__ sp = src + t0;  // wave-uniform bases, 32-bit lane offsets
     const int64_t* __restrict__ dp = dst + t0;
-    if (vec && t0 + B * kItems <= m) {
+    if (vec && t0 + B * N <= m) {
         const longlong2* __restrict__ sv = reinterpret_cast<const longlong2*>(sp);
         const longlong2* __restrict__ dv = reinterpret_cast<const longlong2*>(dp);
 #pragma unroll
-        for (int k = 0; k < kItems / 2; ++k) {
-            const longlong2 a = sv[k * B + (int)threadIdx.x], b = dv[k * B + (int)threadIdx.x];
+        for (int k = 0; k < N / 2; ++k) {
+            typedef long long v2i64 __attribute__((ext_vector_type(2)));
+            longlong2 a, b;
+            if (NTL) {  // streamed once: keep the L2 for lines still being written
+                const v2i64 x = __builtin_nontemporal_load(reinterpret_cast<const v2i64*>(sv) + k * B + (int)threadIdx.x);
+                const v2i64 y = __builtin_nontemporal_load(reinterpret_cast<const v2i64*>(dv) + k * B + (int)threadIdx.x);
+                a.x = x.x;
+                a.y = x.y;
+                b.x = y.x;
+                b.y = y.y;
+            } else {
+                a = sv[k * B + (int)threadIdx.x];
+                b = dv[k * B + (int)threadIdx.x];
+            }
             sr[2 * k] = a.x;
             sr[2 * k + 1] = a.y;
             tr[2 * k] = b.x;
             tr[2 * k + 1] = b.y;
         }
     } else {
-        const int last = (int)(min(m - t0, (int64_t)B * kItems) - 1);
+        const int last = (int)(min(m - t0, (int64_t)B * N) - 1);
 #pragma unroll
-        for (int u = 0; u < kItems; ++u) {
+        for (int u = 0; u < N; ++u) {
             const int i = min(item_off<B>(u), last);
             sr[u] = sp[i];
             tr[u] = dp[i];
