@@ -292,7 +292,7 @@ __host__ __device__ constexpr size_t scatter1l_lds(int nb, int ns, int block, in
            sizeof(uint32_t) * ((size_t)nb * hist_words(ns) + 7 * (size_t)nb + block / 64 + 4);
 }
 
-template <int B, int IT, int MINW>
+template <int B, int IT, int MINW, bool NTL = false, bool NTS = false>
 __global__ void __launch_bounds__(B, MINW) k_scatter_l(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                       int64_t m, Layout L, int swap, int64_t chunk0, size_t trash,
                                                       uint2* __restrict__ pool, unsigned long long* __restrict__ cmeta,
@@ -328,7 +328,7 @@ __global__ void __launch_bounds__(B, MINW) k_scatter_l(const int64_t* __restrict
     const int64_t stride = (int64_t)gridDim.x * T;
     int64_t sr[IT], tr[IT];
     int64_t t0 = (int64_t)blockIdx.x * T;
-    if (t0 < m) load_tile<B>(src, dst, t0, m, vec, sr, tr);
+    if (t0 < m) load_tile<B, NTL>(src, dst, t0, m, vec, sr, tr);
     int par = 0;
     bool pending = false;
     for (; t0 < m; t0 += stride, par ^= 1) {
@@ -345,7 +345,7 @@ __global__ void __launch_bounds__(B, MINW) k_scatter_l(const int64_t* __restrict
             valid |= (ok ? 1u : 0u) << u;
             rk[u] = 0;
         }
-        if (t0 + stride < m) load_tile<B>(src, dst, t0 + stride, m, vec, sr, tr);  // prefetch
+        if (t0 + stride < m) load_tile<B, NTL>(src, dst, t0 + stride, m, vec, sr, tr);  // prefetch
 #pragma unroll
         for (int u = 0; u < IT; ++u)
             if ((valid >> u) & 1u) rk[u] = atomicAdd(&cn[pr[u].y >> L.tbits], 1u);
@@ -385,7 +385,12 @@ __global__ void __launch_bounds__(B, MINW) k_scatter_l(const int64_t* __restrict
             if (idx >= total) {
                 break;  // idx only grows
             } else if (pos < cut) {
-                pool[(size_t)(first ? o : p1[b]) * kCh + pos] = p;
+                uint2* d = pool + (size_t)(first ? o : p1[b]) * kCh + pos;
+                if (NTS)
+                    __builtin_nontemporal_store(*reinterpret_cast<const unsigned long long*>(&p),
+                                                reinterpret_cast<unsigned long long*>(d));
+                else
+                    *d = p;
             } else {
                 hold[b * kLine + (pos - cut)] = p;
             }

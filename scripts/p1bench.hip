@@ -130,7 +130,9 @@ int main(int argc, char** argv) {
     const V vs[] = {
         {"sc_1024x8", (const void*)k_scatter_c<1024, 8, 4, false>, 1024, 8192, 1, 0},
         {"sl_1024x8", (const void*)k_scatter_l<1024, 8, 4>, 1024, 8192, 1, 2},
-        {"sl_1024x6", (const void*)k_scatter_l<1024, 6, 4>, 1024, 6144, 1, 2},
+        {"sl_ntl", (const void*)k_scatter_l<1024, 8, 4, true, false>, 1024, 8192, 1, 2},
+        {"sl_nts", (const void*)k_scatter_l<1024, 8, 4, false, true>, 1024, 8192, 1, 2},
+        {"sl_ntl_nts", (const void*)k_scatter_l<1024, 8, 4, true, true>, 1024, 8192, 1, 2},
         {"floor", (const void*)k_floor<false, false>, 1024, 8192, 1, 1},
         {"floor_ntls", (const void*)k_floor<true, true>, 1024, 8192, 1, 1},
     };
