@@ -194,11 +194,8 @@ struct BitV {
 
 __device__ __forceinline__ bool gbit(const uint32_t* w, uint32_t x) { return (w[x >> 5] >> (x & 31)) & 1u; }
 
-__device__ __forceinline__ void lds_set(uint32_t* lds, uint32_t x) {
-    const uint32_t bit = 1u << (x & 31);
-    uint32_t* p = &lds[x >> 5];
-    if (!(*p & bit)) atomicOr(p, bit);
-}
+// set bit x of an LDS bitmap: a no-return ds_or (a read-then-or measured 0.1 ms slower at C3)
+__device__ __forceinline__ void lds_set(uint32_t* lds, uint32_t x) { atomicOr(&lds[x >> 5], 1u << (x & 31)); }
 
 }  // namespace part
 
