@@ -412,18 +412,46 @@ __global__ void __launch_bounds__(B, MINW) k_scatter_l(const int64_t* __restrict
     }
 }
 
-// used chunks (fill > 0) grouped by target slice (order within a slice is arbitrary)
-__global__ void k_chunk_count(const unsigned long long* __restrict__ cmeta, int64_t nchunks,
-                              int64_t* __restrict__ jcnt) {
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q < nchunks && (cmeta[q] >> 32))
-        atomicAdd(reinterpret_cast<unsigned long long*>(&jcnt[(uint32_t)cmeta[q]]), 1ULL);
+// used chunks (fill > 0) grouped by target slice (order within a slice is arbitrary).  Each block
+// takes kChunkPer chunks and aggregates per slice in LDS, so a slice counter sees one global atomic
+// per block instead of one per chunk (≈10^5 chunks on ≈10^2 counters at C3).
+constexpr int kChunkBlock = 1024, kChunkPer = 8192;
+
+__global__ void __launch_bounds__(kChunkBlock) k_chunk_count(const unsigned long long* __restrict__ cmeta,
+                                                             int64_t nchunks, int nt, int64_t* __restrict__ jcnt) {
+    extern __shared__ uint32_t h[];  // nt
+    for (int i = threadIdx.x; i < nt; i += kChunkBlock) h[i] = 0;
+    __syncthreads();
+    const int64_t q0 = (int64_t)blockIdx.x * kChunkPer, q1 = min(q0 + kChunkPer, nchunks);
+    for (int64_t q = q0 + threadIdx.x; q < q1; q += kChunkBlock)
+        if (cmeta[q] >> 32) atomicAdd(&h[(uint32_t)cmeta[q]], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nt; i += kChunkBlock)
+        if (h[i]) atomicAdd(reinterpret_cast<unsigned long long*>(&jcnt[i]), (unsigned long long)h[i]);
 }
 
-__global__ void k_chunk_place(const unsigned long long* __restrict__ cmeta, int64_t nchunks,
-                              unsigned long long* __restrict__ jcur, uint32_t* __restrict__ order) {
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q < nchunks && (cmeta[q] >> 32)) order[atomicAdd(&jcur[(uint32_t)cmeta[q]], 1ULL)] = (uint32_t)q;
+__global__ void __launch_bounds__(kChunkBlock) k_chunk_place(const unsigned long long* __restrict__ cmeta,
+                                                             int64_t nchunks, int nt,
+                                                             unsigned long long* __restrict__ jcur,
+                                                             uint32_t* __restrict__ order) {
+    extern __shared__ uint32_t h[];  // nt counts, then nt bases (low 32 bits of the global cursor)
+    uint32_t* base = h + nt;
+    for (int i = threadIdx.x; i < nt; i += kChunkBlock) h[i] = 0;
+    __syncthreads();
+    const int64_t q0 = (int64_t)blockIdx.x * kChunkPer, q1 = min(q0 + kChunkPer, nchunks);
+    for (int64_t q = q0 + threadIdx.x; q < q1; q += kChunkBlock)
+        if (cmeta[q] >> 32) atomicAdd(&h[(uint32_t)cmeta[q]], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nt; i += kChunkBlock) {
+        base[i] = h[i] ? (uint32_t)atomicAdd(&jcur[i], (unsigned long long)h[i]) : 0u;  // order has < 2^32 entries
+        h[i] = 0;
+    }
+    __syncthreads();
+    for (int64_t q = q0 + threadIdx.x; q < q1; q += kChunkBlock)
+        if (cmeta[q] >> 32) {
+            const uint32_t j = (uint32_t)cmeta[q];
+            order[base[j] + atomicAdd(&h[j], 1u)] = (uint32_t)q;
+        }
 }
 
 // segments per block, ja(w)
@@ -851,11 +879,13 @@ void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_
     uint32_t* order = reinterpret_cast<uint32_t*>(segbase + g2 + 2);
     int* ja = reinterpret_cast<int*>(order + npool);
     HIP_CHECK(hipMemsetAsync(jcnt, 0, sizeof(int64_t) * L.nt, st));
-    const unsigned cg = (unsigned)((npool + 255) / 256);
-    hipLaunchKernelGGL(k_chunk_count, dim3(cg), dim3(256), 0, st, P<unsigned long long>(cp.meta), pool_chunks, jcnt);
+    const unsigned cg = (unsigned)((npool + kChunkPer - 1) / kChunkPer);
+    hipLaunchKernelGGL(k_chunk_count, dim3(cg), dim3(kChunkBlock), sizeof(uint32_t) * L.nt, st,
+                       P<unsigned long long>(cp.meta), pool_chunks, L.nt, jcnt);
     exclusive_scan_i64(jcnt, jst, L.nt, st);
     HIP_CHECK(hipMemcpyAsync(jcur, jst, sizeof(int64_t) * L.nt, hipMemcpyDeviceToDevice, st));
-    hipLaunchKernelGGL(k_chunk_place, dim3(cg), dim3(256), 0, st, P<unsigned long long>(cp.meta), pool_chunks,
+    hipLaunchKernelGGL(k_chunk_place, dim3(cg), dim3(kChunkBlock), sizeof(uint32_t) * 2 * L.nt, st,
+                       P<unsigned long long>(cp.meta), pool_chunks, L.nt,
                        reinterpret_cast<unsigned long long*>(jcur), order);
     hipLaunchKernelGGL(k_seg_count, dim3((unsigned)((g2 + 255) / 256)), dim3(256), 0, st, jst, L.nt, g2, kseg, ja);
     exclusive_scan_i64(kseg, segbase, g2, st);
