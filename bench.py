@@ -50,6 +50,9 @@ def parse():
     p.add_argument("--modes", default="cold,warm", help="comma list of cold, warm, stream (first = value)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-scale", type=int, default=None, help="oracle sample scale (default per workload)")
+    p.add_argument("--shard-of", type=int, default=0,
+                   help="diagnostic (C3): time rank 0's shard of an N-way owner(target) partition on one GPU, "
+                        "no exchange; the line is not the metric")
     p.add_argument("--workload", default="c3", choices=("c2", "c3", "c4", "c5"),
                    help="c3 (default, the BASELINE metric) or the single-GPU C2/C4/C5 lines (SURVEY.md 8d)")
     return p.parse_args()
@@ -131,14 +134,15 @@ def main():
     n = 1 << scale
     m_total = ef << scale
     nw = (n + 31) // 32
-    assert nw % world == 0, "owner slices must be equal for the all-gather"
-    wb, we = graph.owner_words(n, rank, world)
+    shards = args.shard_of if (args.shard_of and not distributed) else world
+    assert nw % shards == 0, "owner slices must be equal for the all-gather"
+    wb, we = graph.owner_words(n, rank, shards)
     modes = [m.strip() for m in args.modes.split(",") if m.strip()]
 
     # ---- ingest (untimed): partitioned relationship table + Person node table --------------------
     t0 = time.perf_counter()
     rels = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42,
-                           part_col=graph.PART_TARGET if distributed else graph.PART_NONE, part=rank, nparts=world)
+                           part_col=graph.PART_TARGET if shards > 1 else graph.PART_NONE, part=rank, nparts=shards)
     persons = graph.rmat_nodes(sess, scale, graph.NODES_ALL)
     m_local = rels.size
     sess.sync()
@@ -233,6 +237,8 @@ def main():
         ref = graph.two_hop_count_distinct(sess, [full], p, p, p)
         answers = {m: r[1] for m, r in results.items()}
         check = "ok" if all(v == ref for v in answers.values()) else f"MISMATCH {answers} vs unpartitioned {ref}"
+        if shards != world:
+            check = f"not applicable (--shard-of {shards}: rank 0's shard alone)"
         del full
 
     if rank == 0:
@@ -280,6 +286,8 @@ def main():
                       "kernel_ms": {k: v[1] / v[0] for k, v in timed.items()},
                       "rels_local_rank0": m_local, "ingest_s": ingest_s},
         }
+        if shards != world:
+            line["config"]["diagnostic"] = f"rank 0's shard of {shards} on one GPU, no exchange (not the metric)"
         for mode in modes[1:]:
             s2, r2, kt2 = results[mode]
             line["query"][mode] = {"ms_per_step": s2 * 1e3, "value": matched / s2, "count_distinct_c": r2,
