@@ -123,6 +123,8 @@ _SIGS = {
     "capsmi_relpart_build": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, c_int64, c_int64, PP]),
     "capsmi_relpart_build_mark_mid": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, P, P, P, PP]),
     "capsmi_relpart_size": (c_int32, [P, POINTER(c_int64)]),
+    "capsmi_relpart_digest": (c_int32, [P, POINTER(c_int64), POINTER(c_int64), POINTER(c_int32), POINTER(c_int32), P, P,
+                                        POINTER(c_int64)]),
     "capsmi_trigraph_build": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, PP]),
     "capsmi_trigraph_count": (c_int32, [P, P, c_int32, c_int32, POINTER(c_int64)]),
     "capsmi_trigraph_release": (c_int32, [P]),

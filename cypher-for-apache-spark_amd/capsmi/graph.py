@@ -239,6 +239,22 @@ class RelPartition:
         _lib.call("capsmi_relpart_size", self._h, ctypes.byref(v))
         return v.value
 
+    def digest(self):
+        """Layout check (include/capsmi.h capsmi_relpart_digest): per-cell pair counts, per-cell wrapping
+        sums of mix64(source << 32 | target) (ids relative to the domain), the number of misplaced pairs,
+        and the geometry (ns, sbits, tbits)."""
+        import numpy as np
+        nc, ns, sb, tb = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int32()
+        _lib.call("capsmi_relpart_digest", self._h, ctypes.byref(nc), ctypes.byref(ns), ctypes.byref(sb),
+                  ctypes.byref(tb), None, None, None)
+        counts = np.zeros(nc.value, np.int64)
+        sums = np.zeros(nc.value, np.uint64)
+        bad = ctypes.c_int64()
+        _lib.call("capsmi_relpart_digest", self._h, ctypes.byref(nc), ctypes.byref(ns), ctypes.byref(sb),
+                  ctypes.byref(tb), ctypes.c_void_p(counts.ctypes.data), ctypes.c_void_p(sums.ctypes.data),
+                  ctypes.byref(bad))
+        return counts, sums, bad.value, (ns.value, sb.value, tb.value)
+
     def release(self) -> None:
         if self._h:
             _lib.call("capsmi_relpart_release", self._h)

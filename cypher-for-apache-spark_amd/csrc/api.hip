@@ -1441,6 +1441,29 @@ capsmi_status capsmi_relpart_size(const capsmi_relpart* p, int64_t* kept_rows) {
     API_END
 }
 
+capsmi_status capsmi_relpart_digest(const capsmi_relpart* p, int64_t* ncells, int64_t* ns, int32_t* sbits,
+                                    int32_t* tbits, int64_t* counts, uint64_t* sums, int64_t* misplaced) {
+    API_BEGIN
+    need(p, "relpart");
+    need(ncells, "ncells");
+    need(ns, "ns");
+    need(sbits, "sbits");
+    need(tbits, "tbits");
+    const PartLayout& L = p->rp.L;
+    *ncells = L.ncells;
+    *ns = L.ns;
+    *sbits = L.sbits;
+    *tbits = L.tbits;
+    if (counts || sums) {
+        need(counts, "counts");
+        need(sums, "sums");
+        need(misplaced, "misplaced");
+        use_device(p->sess);
+        relpart_digest(p->sess, p->rp, counts, sums, misplaced);
+    }
+    API_END
+}
+
 capsmi_status capsmi_relpart_release(capsmi_relpart* p) {
     API_BEGIN
     if (p) {

@@ -218,6 +218,7 @@ struct RelPart {
     int64_t rows = 0;  // relationships offered to the build (>= kept)
 };
 int64_t relpart_kept(capsmi_session* s, RelPart& rp);
+void relpart_digest(capsmi_session* s, const RelPart& rp, int64_t* counts, uint64_t* sums, int64_t* misplaced);
 // hop 1 of a 2-hop run while the layout is built: M(t) |= a_ok(s) for s != t, a_ok self-loops ->
 // S1 (first) / S2 (second), target filter b_ok; outputs zeroed by the caller
 struct RelPartHop1 {

@@ -995,6 +995,50 @@ void relpart_hop2(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* c, 
     launch_hop<false, false>(s, rp, xv, X2, cv, C, nullptr, nullptr, c->nwords);
 }
 
+// ---- layout digest (test support): per cell, pair count and wrapping sum of a 64-bit mix ----------------
+__device__ __forceinline__ uint64_t pair_mix(uint2 p) {
+    uint64_t z = ((uint64_t)p.x << 32 | p.y) + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256) k_cell_digest(const uint2* __restrict__ pairs, const int64_t* __restrict__ boff,
+                                                    part::Layout L, unsigned long long* __restrict__ sums,
+                                                    unsigned long long* __restrict__ bad) {
+    const int c = blockIdx.x;
+    unsigned long long acc = 0, nb = 0;
+    for (int64_t i = boff[c] + threadIdx.x; i < boff[c + 1]; i += 256) {
+        const uint2 p = pairs[i];
+        acc += pair_mix(p);
+        if (part::cell_of(L, p.x, p.y) != c) ++nb;
+    }
+    atomicAdd(&sums[c], acc);
+    if (nb) atomicAdd(bad, nb);
+}
+
+void relpart_digest(capsmi_session* s, const RelPart& rp, int64_t* counts, uint64_t* sums, int64_t* misplaced) {
+    hipStream_t st = s->stream;
+    const int nc = rp.L.ncells;
+    std::vector<int64_t> off(nc + 1, 0);
+    Buf d = dev_alloc(sizeof(unsigned long long) * (nc + 1), st);
+    HIP_CHECK(hipMemsetAsync(P<void>(d), 0, sizeof(unsigned long long) * (nc + 1), st));
+    if (rp.rows > 0) {
+        hipLaunchKernelGGL(k_cell_digest, dim3(nc), dim3(256), 0, st, P<uint2>(rp.pairs), P<int64_t>(rp.boff), rp.L,
+                           P<unsigned long long>(d), P<unsigned long long>(d) + nc);
+        HIP_CHECK(hipGetLastError());
+        HIP_CHECK(hipMemcpyAsync(off.data(), P<void>(rp.boff), sizeof(int64_t) * (nc + 1), hipMemcpyDeviceToHost, st));
+    }
+    std::vector<unsigned long long> h(nc + 1);
+    HIP_CHECK(hipMemcpyAsync(h.data(), P<void>(d), sizeof(unsigned long long) * (nc + 1), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    for (int c = 0; c < nc; ++c) {
+        counts[c] = off[c + 1] - off[c];
+        sums[c] = h[c];
+    }
+    *misplaced = (int64_t)h[nc];
+}
+
 int64_t relpart_kept(capsmi_session* s, RelPart& rp) {
     if (rp.kept < 0) rp.kept = rp.rows > 0 ? read_scalar(s, P<int64_t>(rp.boff) + rp.L.ncells) : 0;
     return rp.kept;

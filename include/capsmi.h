@@ -277,6 +277,12 @@ capsmi_status capsmi_relpart_build(capsmi_session* s, int32_t nrels, capsmi_tabl
                                    const char* dst_col, int64_t id_lo, int64_t id_hi, capsmi_relpart** out);
 capsmi_status capsmi_relpart_size(const capsmi_relpart* p, int64_t* kept_rows);
 capsmi_status capsmi_relpart_release(capsmi_relpart* p);
+/* Layout check (test support, synchronous): per 2-D cell c (target slice major) the number of pairs and
+   the wrapping sum of mix64((source - lo) << 32 | (target - lo)) over them; pairs stored outside their
+   own cell are counted in *misplaced.  counts/sums hold *ncells entries each; pass NULL arrays to read
+   the cell geometry only (*ncells, *ns = source slices per target slice, *sbits, *tbits). */
+capsmi_status capsmi_relpart_digest(const capsmi_relpart* p, int64_t* ncells, int64_t* ns, int32_t* sbits,
+                                    int32_t* tbits, int64_t* counts, uint64_t* sums, int64_t* misplaced);
 /* capsmi_relpart_build followed by capsmi_two_hop_mark_mid_part, with hop 1 run by the build's second
  * pass when a_ok covers the whole id domain (the cold 2-hop: one pass fewer over the relationships) */
 capsmi_status capsmi_relpart_build_mark_mid(capsmi_session* s, int32_t nrels, capsmi_table* const* rels,

@@ -24,6 +24,29 @@ def _np_count_distinct(n, src, dst, a_ok, b_ok, c_ok):
     return int(C.sum())
 
 
+def _mix64(x):
+    z = x + np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def _check_layout(rp, lo, hi, src, dst):
+    """Every relationship with both endpoints in [lo, hi) is stored exactly once, in its own cell:
+    per-cell counts and wrapping sums of a 64-bit mix of the packed pair match a numpy grouping."""
+    counts, sums, bad, (ns, sbits, tbits) = rp.digest()
+    keep = (src >= lo) & (src < hi) & (dst >= lo) & (dst < hi)
+    x, y = (src[keep] - lo).astype(np.uint64), (dst[keep] - lo).astype(np.uint64)
+    cell = (y >> np.uint64(tbits)).astype(np.int64) * ns + (x >> np.uint64(sbits)).astype(np.int64)
+    want_n = np.bincount(cell, minlength=len(counts))
+    want_s = np.zeros(len(counts), np.uint64)
+    with np.errstate(over="ignore"):
+        np.add.at(want_s, cell, _mix64((x << np.uint64(32)) | y))
+    assert bad == 0
+    np.testing.assert_array_equal(counts, want_n)
+    np.testing.assert_array_equal(sums, want_s)
+
+
 def _bitmap(session, n, ids):
     from capsmi import ColumnData, I64, graph
     t = session.table([ColumnData("id", I64, np.asarray(ids, dtype=np.int64))])
@@ -124,6 +147,36 @@ def _mid_words(session, rp_factory, n, a, b):
     return rp, mid.cpu().numpy().view(np.uint32)
 
 
+@pytest.mark.parametrize("fused", [False, True])
+def test_layout_digest_full_domain(session, fused):
+    """2^26 ids = 128 x 128 cells (the whole-line pass-1 kernel and pass 2 with many segments per
+    slice), uniform ids plus hub targets and sources: every pair stored once, in its own cell; with
+    `fused` the layout comes from the build that runs hop 1 in pass 2."""
+    import torch
+    from capsmi import ColumnData, I64, graph
+    n = 1 << 26
+    rng = np.random.default_rng(31)
+    m = 6 << 20
+    hubs = rng.integers(0, n, 64)
+    src = np.where(rng.random(m) < 0.2, rng.choice(hubs, m), rng.integers(0, n, m)).astype(np.int64)
+    dst = np.where(rng.random(m) < 0.3, rng.choice(hubs, m), rng.integers(0, n, m)).astype(np.int64)
+    src[::1001] = dst[::1001]  # self-loops
+    rels = session.table([ColumnData("id", I64, np.arange(m)), ColumnData("source", I64, src),
+                          ColumnData("target", I64, dst)])
+    if fused:
+        a = _bitmap(session, n, np.arange(n))
+        nw = n // 32
+        mid = torch.zeros(2 * nw, dtype=torch.int32, device="cuda")
+        scratch = torch.zeros(nw, dtype=torch.int32, device="cuda")
+        rp = graph.RelPartition.build_mark_mid(session, [rels], a, a, mid.data_ptr(), scratch.data_ptr())
+        session.sync()
+    else:
+        rp = graph.RelPartition(session, [rels], 0, n)
+    assert rp.size == m
+    _check_layout(rp, 0, n, src, dst)
+    rp.release()
+
+
 @pytest.mark.parametrize("a_full", [True, False])
 def test_build_mark_mid_matches_phased(session, a_full):
     """Hop 1 run inside the build's second pass (a_ok full) or after it (a_ok partial) gives the same
@@ -171,6 +224,7 @@ def test_skewed_slices_and_chunk_splits(session):
     assert graph.two_hop_count_distinct(session, tabs, a, a, c) == want
     rp = graph.RelPartition(session, tabs, 0, n)
     assert rp.size == m
+    _check_layout(rp, 0, n, src, dst)
     assert rp.count_distinct(a, a, c) == want
     rp.release()
 
@@ -192,6 +246,7 @@ def test_largest_domain(session):
     want = _np_count_distinct(k, np.searchsorted(ids, src), np.searchsorted(ids, dst), ok, ok, ok)
     rp = graph.RelPartition(session, [rels], 0, n)
     assert rp.size == m
+    _check_layout(rp, 0, n, src, dst)
     assert rp.count_distinct(bm, bm, bm) == want
     rp.release()
 
