@@ -563,8 +563,8 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
     const int64_t w = blockIdx.x, blocks = gridDim.x;
     uint2* stage = reinterpret_cast<uint2*>(smem);
     uint2* hold = stage + kTile;  // per source cell: the items of its unfinished output line, slot = index & 15
-    unsigned long long* cur = reinterpret_cast<unsigned long long*>(hold + (size_t)nb * kLine);  // next output index per cell
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(cur + nb);
+    uint32_t* cur = reinterpret_cast<uint32_t*>(hold + (size_t)nb * kLine);  // next output index per cell (< 2^32)
+    uint32_t* cnt = cur + nb;
     uint32_t* loc = cnt + nb;
     uint32_t* hc = loc + nb;  // items held per cell (all in the line of cur)
     uint32_t* wtot = hc + nb;
@@ -575,7 +575,7 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
         for (int x = threadIdx.x; x < nb * kLine; x += kSBlock) {
             const int b = x / kLine, k = x % kLine;
             if ((uint32_t)k < hc[b]) {
-                const unsigned long long pos = cur[b] - hc[b] + (unsigned long long)k;
+                const uint32_t pos = cur[b] - hc[b] + (uint32_t)k;
                 out[pos] = hold[b * kLine + (int)(pos & (kLine - 1))];
             }
         }
@@ -626,7 +626,7 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
             tbase = (uint32_t)sg.j << kSliceBits;
             __syncthreads();
             for (int i = threadIdx.x; i < nb; i += kSBlock)
-                cur[i] = (unsigned long long)(coff[(size_t)sg.j * nb + i] + prel[(size_t)g * nb + i]);
+                cur[i] = (uint32_t)(coff[(size_t)sg.j * nb + i] + prel[(size_t)g * nb + i]);
         }
         uint2 pr[kItems];
 #pragma unroll
@@ -665,8 +665,8 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
         for (int x = threadIdx.x; x < nb * kLine; x += kSBlock) {
             const int b = x / kLine, k = x % kLine;
             if ((uint32_t)k < hc[b]) {
-                const unsigned long long c = cur[b], pos = c - hc[b] + (unsigned long long)k;
-                if (((c + cnt[b]) & ~(unsigned long long)(kLine - 1)) > (c & ~(unsigned long long)(kLine - 1)))
+                const uint32_t c = cur[b], pos = c - hc[b] + (uint32_t)k;
+                if (((c + cnt[b]) & ~(uint32_t)(kLine - 1)) > (c & ~(uint32_t)(kLine - 1)))
                     out[pos] = hold[b * kLine + (int)(pos & (kLine - 1))];
             }
         }
@@ -679,8 +679,8 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
             const uint32_t idx = (uint32_t)(k * kSBlock + (int)threadIdx.x);
             const uint2 v = stage[idx];
             const int b = min((int)(v.x >> L.sbits), nb - 1);  // stale stage entries past `total`
-            const unsigned long long pos = cur[b] + idx - loc[b];
-            const unsigned long long cut = (cur[b] + cnt[b]) & ~(unsigned long long)(kLine - 1);
+            const uint32_t pos = cur[b] + idx - loc[b];
+            const uint32_t cut = (cur[b] + cnt[b]) & ~(uint32_t)(kLine - 1);
             if (idx >= total)
                 out[trash + threadIdx.x] = v;
             else if (pos < cut)
@@ -690,9 +690,9 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
         }
         __syncthreads();
         for (int i = threadIdx.x; i < nb; i += kSBlock) {
-            const unsigned long long c = cur[i], n = cnt[i];
-            const unsigned long long cut = (c + n) & ~(unsigned long long)(kLine - 1);
-            hc[i] = cut > (c & ~(unsigned long long)(kLine - 1)) ? (uint32_t)(c + n - cut) : hc[i] + (uint32_t)n;
+            const uint32_t c = cur[i], n = cnt[i];
+            const uint32_t cut = (c + n) & ~(uint32_t)(kLine - 1);
+            hc[i] = cut > (c & ~(uint32_t)(kLine - 1)) ? c + n - cut : hc[i] + n;
             cur[i] = c + n;
         }
     }
@@ -837,7 +837,7 @@ void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_
         pool_chunks += (int64_t)g1[i] * chunks_per_block(ms[i], g1[i], L.nt);
         mtot += ms[i];
     }
-    REQUIRE(pool_chunks < (int64_t)INT32_MAX && mtot < (int64_t)UINT32_MAX, CAPSMI_ERR_UNSUPPORTED,
+    REQUIRE(pool_chunks < (int64_t)INT32_MAX && mtot + 2 * kPad < (int64_t)UINT32_MAX, CAPSMI_ERR_UNSUPPORTED,
             "relationship table too large for the layout");
     const int64_t npool = pool_chunks > 0 ? pool_chunks : 1;
     const int hw = hist_words(L.ns);
@@ -939,8 +939,8 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
 
     Hop1Out ho{};
     if (fuse) ho = Hop1Out{BitV{P<uint32_t>(h1->b->words), h1->b->full ? 1 : 0}, h1->M, h1->S1, h1->S2, h1->b->nwords};
-    const size_t lds2 = sizeof(uint2) * ((size_t)kTile + (size_t)L.ns * kLine) + sizeof(unsigned long long) * L.ns +
-                        sizeof(uint32_t) * (3 * L.ns + kSBlock / 64) + (fuse ? sizeof(uint32_t) * kSliceWords : 0);
+    const size_t lds2 = sizeof(uint2) * ((size_t)kTile + (size_t)L.ns * kLine) +
+                        sizeof(uint32_t) * (4 * L.ns + kSBlock / 64) + (fuse ? sizeof(uint32_t) * kSliceWords : 0);
     auto k2 = fuse ? k_scatter_s2<true> : k_scatter_s2<false>;
     allow_lds(k2, lds2);
     {
