@@ -76,7 +76,8 @@ __global__ void __launch_bounds__(kBlock) k_tile_scan(const int64_t* __restrict_
         s += v[j];
     }
     int64_t tot;
-    int64_t pre = block_excl_scan(s, lds, &tot) + tile_off[blockIdx.x];
+    const int64_t toff = tile_off ? tile_off[blockIdx.x] : 0;  // null: a single tile
+    int64_t pre = block_excl_scan(s, lds, &tot) + toff;
 #pragma unroll
     for (int j = 0; j < kItems; ++j) {
         tile[threadIdx.x * kItems + j] = pre;
@@ -88,7 +89,7 @@ __global__ void __launch_bounds__(kBlock) k_tile_scan(const int64_t* __restrict_
         const int64_t i = base + j * kBlock + threadIdx.x;
         if (i < n) out[i] = tile[j * kBlock + threadIdx.x];
     }
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kBlock - 1) out[n] = tile_off[blockIdx.x] + tot;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kBlock - 1) out[n] = toff + tot;
 }
 
 __global__ void k_fill_i64(int64_t* p, int64_t v, int64_t n) {
@@ -162,14 +163,15 @@ void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t 
         HIP_CHECK(hipMemsetAsync(out, 0, sizeof(int64_t), st));
         return;
     }
+    if (ntiles == 1) {  // one launch
+        hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(kBlock), 0, st, in, n, (const int64_t*)nullptr, out);
+        HIP_CHECK(hipGetLastError());
+        return;
+    }
     Buf sums = dev_alloc(sizeof(int64_t) * ntiles, st);
     Buf offs = dev_alloc(sizeof(int64_t) * (ntiles + 1), st);
     hipLaunchKernelGGL(k_tile_sum, dim3((unsigned)ntiles), dim3(kBlock), 0, st, in, n, P<int64_t>(sums));
-    if (ntiles == 1) {
-        HIP_CHECK(hipMemsetAsync(P<int64_t>(offs), 0, sizeof(int64_t), st));
-    } else {
-        exclusive_scan_i64(P<int64_t>(sums), P<int64_t>(offs), ntiles, st);
-    }
+    exclusive_scan_i64(P<int64_t>(sums), P<int64_t>(offs), ntiles, st);
     hipLaunchKernelGGL(k_tile_scan, dim3((unsigned)ntiles), dim3(kBlock), 0, st, in, n, P<int64_t>(offs), out);
     HIP_CHECK(hipGetLastError());
 }
