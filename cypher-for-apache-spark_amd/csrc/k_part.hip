@@ -485,12 +485,24 @@ __global__ void __launch_bounds__(1024) k_seg_sum(const uint32_t* __restrict__ c
     const int hw = hist_words(ns), rows = 1024 / hw;  // hw <= 64
     const int r = threadIdx.x / hw, x = threadIdx.x % hw;
     uint32_t lo = 0, hi = 0;
-    if (r < rows)
-        for (int64_t q = sg.q0 + r; q < sg.q1; q += rows) {
+    if (r < rows) {
+        int64_t q = sg.q0 + r;
+        for (; q + 3 * rows < sg.q1; q += 4 * rows) {  // four rows' loads in flight per lane
+            uint32_t v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[k] = chist[(size_t)order[q + k * rows] * hw + x];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                lo += v[k] & 0xFFFFu;
+                hi += v[k] >> 16;
+            }
+        }
+        for (; q < sg.q1; q += rows) {
             const uint32_t v = chist[(size_t)order[q] * hw + x];
             lo += v & 0xFFFFu;
             hi += v >> 16;
         }
+    }
     for (int half = 0; half < 2; ++half) {
         acc[threadIdx.x] = half ? hi : lo;
         __syncthreads();
