@@ -59,18 +59,44 @@ def parse():
 
 
 def cpu_baseline(scale, ef):
-    """The oracle (CPU restatement) on a bounded sample: the same query on R-MAT scale `scale`,
-    computed the way CAPS's joins compute it -- every (a, r1, b, r2, c) binding enumerated."""
+    """The oracle on the host cores: (1) the SAME algorithm as the device path -- the closed form /
+    frontier bitmaps of oracle/closed.c orc_two_hop_closed_form_mt -- on the SAME full workload
+    (R-MAT `scale`, seed 42), OpenMP over `cores` threads; (2) a second, clearly labelled line: the
+    join semantics CAPS runs (every (a, r1, b, r2, c) binding enumerated, oracle/rmat.c) on R-MAT
+    scale 20.  Both are CPU restatements, not CAPS-on-Spark (no JVM on the box).  Edge generation is
+    ingest and untimed."""
     from oracle import cpu
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    n = 1 << scale
     src, dst = cpu.rmat_edges(scale, 0, ef << scale)
     t0 = time.perf_counter()
-    rows, dist = cpu.two_hop_enumerate(1 << scale, src, dst, threads=threads)
+    rows, dist = cpu.two_hop_closed_form_mt(n, src, dst, threads=threads)
     dt = time.perf_counter() - t0
+    del src, dst
+    es = 20
+    s2, d2 = cpu.rmat_edges(es, 0, ef << es)
+    t1 = time.perf_counter()
+    erows, edist = cpu.two_hop_enumerate(1 << es, s2, d2, threads=threads)
+    edt = time.perf_counter() - t1
     return {"value": rows / dt, "unit": "matched rows/s", "cores": threads, "kind": "port",
-            "sample": f"R-MAT scale {scale} (2^{scale} nodes, {ef << scale} rels), full C3 query by binding "
-                      f"enumeration (oracle/rmat.c orc_two_hop_enumerate): {rows} bindings, "
-                      f"count(DISTINCT c)={dist}, {dt:.2f} s"}
+            "sample": f"CPU restatement, not CAPS: the device algorithm (closed form + frontier bitmaps, "
+                      f"oracle/closed.c orc_two_hop_closed_form_mt) on the same workload, R-MAT scale {scale} "
+                      f"({ef << scale} rels, seed 42), {threads} OpenMP threads: count(*)={rows}, "
+                      f"count(DISTINCT c)={dist}, {dt:.2f} s",
+            "enumeration": {"value": erows / edt, "unit": "matched rows/s", "cores": threads,
+                            "sample": f"CAPS join semantics (every binding enumerated, oracle/rmat.c "
+                                      f"orc_two_hop_enumerate) on R-MAT scale {es}: {erows} bindings, "
+                                      f"count(DISTINCT c)={edist}, {edt:.2f} s"}}
+
+
+def fixture(key):
+    """Exact full-size answer from tests/golden/rmat_full.json (oracle closed forms, committed with
+    the script that made them: tests/golden/make_rmat_full.py), or None."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "rmat_full.json")) as f:
+            return json.load(f)["cases"].get(key)
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def init_dist(dist, local):
@@ -108,8 +134,6 @@ def main():
     args = parse()
     if args.workload != "c3":
         return run_single(args)
-    if args.cpu_scale is None:
-        args.cpu_scale = 20
     import torch
     import torch.distributed as dist
 
@@ -228,17 +252,23 @@ def main():
     if "rp" in cached:
         cached["rp"].release()
 
-    # ---- untimed checks: matched rows (closed form) and the unpartitioned answer on rank 0 -----------
+    # ---- untimed checks: matched rows (closed form) and every mode's answer vs the committed fixture -
     matched = check = None
+    fx = fixture(f"c3_s{scale}") if ef == 16 else None
     if rank == 0:
         full = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42) if distributed else rels
         p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")
         matched = graph.two_hop_count(sess, [full], p, p, p)
-        ref = graph.two_hop_count_distinct(sess, [full], p, p, p)
         answers = {m: r[1] for m, r in results.items()}
-        check = "ok" if all(v == ref for v in answers.values()) else f"MISMATCH {answers} vs unpartitioned {ref}"
         if shards != world:
             check = f"not applicable (--shard-of {shards}: rank 0's shard alone)"
+        elif fx is None:
+            check = "no fixture for this scale"
+        else:
+            bad = {m: v for m, v in answers.items() if v != fx["count_distinct_c"]}
+            if matched != fx["count_star"]:
+                bad["count_star"] = matched
+            check = "ok" if not bad else f"MISMATCH {bad} vs fixture {fx['count_distinct_c']} / {fx['count_star']}"
         del full
 
     if rank == 0:
@@ -279,7 +309,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": KERNEL_SYMBOL[dom],
                          "kernel_ms": avg_ms, "alg_bytes_per_launch": alg[dom]},
-            "query": {"count_distinct_c": res, "matched_rows": matched, "check_vs_unpartitioned": check,
+            "query": {"count_distinct_c": res, "matched_rows": matched,
+                      "check_vs_fixture": check,  # tests/golden/rmat_full.json (oracle closed form)
                       "alg_bytes_query": query_alg,
                       "query_alg_GBs": query_alg / sec / 1e9,
                       "query_frac_of_peak": query_alg / sec / 1e9 / (HBM_PEAK_GBS * world),
@@ -288,13 +319,19 @@ def main():
         }
         if shards != world:
             line["config"]["diagnostic"] = f"rank 0's shard of {shards} on one GPU, no exchange (not the metric)"
+        # warm (layout cached): the query reads the cached 8-B packed layout once per hop instead of the
+        # int64 (source, target) scans, plus the three node scans -- its own algorithmic bytes
+        warm_alg = 2 * 8 * m_total + 3 * 8 * n
         for mode in modes[1:]:
             s2, r2, kt2 = results[mode]
+            b2 = warm_alg if mode == "warm" else query_alg
             line["query"][mode] = {"ms_per_step": s2 * 1e3, "value": matched / s2, "count_distinct_c": r2,
-                                   "query_frac_of_peak": query_alg / s2 / 1e9 / (HBM_PEAK_GBS * world),
+                                   "alg_bytes_query": b2, "query_frac_of_peak": b2 / s2 / 1e9 / (HBM_PEAK_GBS * world),
                                    "kernel_ms": {k: v[1] / v[0] for k, v in kt2.items() if v[0] > 0}}
-        line["cpu_baseline"] = cpu_baseline(args.cpu_scale, ef) if (not args.no_cpu_baseline and world == 1) else None
+        line["cpu_baseline"] = cpu_baseline(scale, ef) if (not args.no_cpu_baseline and world == 1) else None
         print(json.dumps(line), flush=True)
+        if check is not None and check.startswith("MISMATCH"):
+            sys.exit(f"bench: result differs from the oracle fixture: {check}")
     sess.close()
     if distributed:
         dist.destroy_process_group()
@@ -446,6 +483,24 @@ def run_single(args):
         ref = graph.expand_filter(sess, full, a_ok, b_ok, ["source", "target"], ["a", "b"]).size
         check = "ok" if ref == res else f"MISMATCH {res} vs unsharded {ref}"
         del full
+    # every line checks its answer against the committed oracle fixture (tests/golden/rmat_full.json)
+    fx = fixture(f"{wl}_s{scale}")
+    if fx is None or (world > 1 and wl == "c2"):
+        fcheck = "no fixture for this scale" if fx is None else "rows only (output stays partitioned)"
+        if fx is not None and wl == "c2":
+            fcheck = "ok" if res == fx["rows"] else f"MISMATCH rows {res} vs fixture {fx['rows']}"
+    elif wl == "c2":
+        fp = list(out.fingerprint(["a", "b"]))
+        want = [fx["fingerprint"][0], int(fx["fingerprint"][1]), int(fx["fingerprint"][2])]
+        fcheck = "ok" if fp == want else f"MISMATCH fingerprint {fp} vs fixture {want}"
+    elif wl == "c4":
+        fcheck = "ok" if res == fx["count_star"] else f"MISMATCH {res} vs fixture {fx['count_star']}"
+    else:
+        fcheck = "ok" if res == fx["sum_count"] else f"MISMATCH sum {res} vs fixture {fx['sum_count']}"
+        if world == 1 and fcheck == "ok":
+            fp = list(out.fingerprint(["id", "count"]))
+            want = [fx["fingerprint"][0], int(fx["fingerprint"][1]), int(fx["fingerprint"][2])]
+            fcheck = "ok" if fp == want else f"MISMATCH fingerprint {fp} vs fixture {want}"
     matched = res
     m_kern = rels.size if world > 1 and wl in ("c2", "c5") else m  # relationships behind one launch here
     # algorithmic bytes per launch of the kernels whose traffic is a plain function of the input
@@ -480,6 +535,7 @@ def run_single(args):
                                          f"phases; in-relationships exchanged at ingest")
     elif wl == "c2" and world > 1:
         line["config"]["parallelism"] = f"relationships by owner(source) over {world} GPU(s); row count all-reduced"
+    line["query"]["check_vs_fixture"] = fcheck
     if check is not None or (world > 1 and wl in ("c2", "c5")):
         line["query"]["check_vs_unsharded"] = check
     line["cpu_baseline"] = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_single(wl, cpu_scale, ef, probs)
@@ -488,6 +544,8 @@ def run_single(args):
     sess.close()
     if world > 1:
         dist.destroy_process_group()
+    if fcheck.startswith("MISMATCH"):
+        sys.exit(f"bench: result differs from the oracle fixture: {fcheck}")
 
 
 def cpu_baseline_single(wl, scale, ef, probs):

@@ -73,8 +73,7 @@ def read_schema(graph_dir: str) -> Tuple[List[Tuple[frozenset, Dict[str, int]]],
 
 def fs_graph(backend, graph_dir: str, extra_strings=()) -> ScanGraph:
     """ScanGraph of a CSV graph directory; `backend` is a capsmi Session (GPU) or the oracle's backend.
-    `extra_strings`: strings of other inputs (e.g. a driving table) that must share the order-preserving
-    dictionary, which is fixed once the entity tables are encoded."""
+    `extra_strings`: strings to register up front (codes are stable, so later strings may also be added)."""
     node_schemas, rel_schemas = read_schema(graph_dir)
     parsed = []
     strings = set()

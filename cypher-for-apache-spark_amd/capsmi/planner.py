@@ -744,7 +744,6 @@ class Planner:
                 if src_col in cur.header:
                     cols.append((Col(src_col), c))
                 else:
-                    ty = STR if False else (BOOL if suffix.startswith(":") else None)
                     cols.append((Lit(False) if suffix.startswith(":") else self._null_like(ns, c), c))
             cols += [(Lit(None, I64), c) for i in range(1, upper + 1) for c in seg_cols(i)[:3]]
             cols += [(Lit(None, STR), seg_cols(i)[3]) for i in range(1, upper + 1)]

@@ -41,27 +41,59 @@ class ColumnData:
 class StringDictionary:
     """Order-preserving dictionary for CTString values (include/capsmi.h: STR columns are codes).
 
-    Known strings get even codes 2*rank; an unknown literal gets the odd code between its sorted
-    neighbours, so equality and ordering on codes equal equality and ordering on strings."""
+    Codes are stable: once a string has a code it keeps it for the life of the dictionary, so device
+    columns encoded earlier (a first graph, a driving table) stay valid when later graphs or
+    literals bring new strings.  Order is preserved by allocating codes from gaps: a batch of new
+    strings that falls between two known neighbours is spread evenly over the open interval between
+    their codes (the first batch over [-2^62, 2^62]).  Equality and ordering on codes therefore equal
+    equality and ordering on strings.  Every string that is encoded -- query literals included --
+    is inserted, so two distinct strings never share a code.  A gap only runs out after ~60 nested
+    insertions at one spot; that raises instead of renumbering codes already on the device."""
+
+    LO, HI = -(1 << 62), 1 << 62
 
     def __init__(self, strings: Iterable[str] = ()):
-        self._sorted: List[str] = sorted(set(strings))
+        self._sorted: List[str] = []
+        self._codes: List[int] = []
+        self._by_code = {}
+        self.extend(strings)
 
     def extend(self, strings: Iterable[str]) -> None:
-        new = set(strings) - set(self._sorted)
-        if new:
-            self._sorted = sorted(set(self._sorted) | new)
+        new = sorted(set(strings) - set(self._by_code.values()))
+        if not new:
+            return
+        # group the new strings by the gap (insertion point) they fall into
+        groups = {}
+        for x in new:
+            groups.setdefault(bisect.bisect_left(self._sorted, x), []).append(x)
+        placed = []
+        for i, xs in groups.items():
+            lo = self._codes[i - 1] if i > 0 else self.LO
+            hi = self._codes[i] if i < len(self._codes) else self.HI
+            step = (hi - lo) // (len(xs) + 1)
+            if step < 1:
+                raise OverflowError("string dictionary: no code left between "
+                                    f"{self._sorted[i - 1] if i > 0 else None!r} and "
+                                    f"{self._sorted[i] if i < len(self._sorted) else None!r}")
+            placed += [(lo + (k + 1) * step, x) for k, x in enumerate(xs)]
+        for c, x in placed:
+            self._by_code[c] = x
+        merged = sorted(list(zip(self._codes, self._sorted)) + placed)
+        self._codes = [c for c, _ in merged]
+        self._sorted = [x for _, x in merged]
 
     def encode(self, s: str) -> int:
         i = bisect.bisect_left(self._sorted, s)
         if i < len(self._sorted) and self._sorted[i] == s:
-            return 2 * i
-        return 2 * i - 1
+            return self._codes[i]
+        self.extend([s])
+        return self._codes[bisect.bisect_left(self._sorted, s)]
 
     def decode(self, code: int) -> str:
-        if code % 2:
-            raise KeyError(f"code {code} is not a dictionary string")
-        return self._sorted[code // 2]
+        try:
+            return self._by_code[int(code)]
+        except KeyError:
+            raise KeyError(f"code {code} is not a dictionary string") from None
 
     def __len__(self) -> int:
         return len(self._sorted)

@@ -45,18 +45,28 @@ static thread_local std::string g_err;
     throw Error(e == hipErrorOutOfMemory ? CAPSMI_ERR_OUT_OF_MEMORY : CAPSMI_ERR_DEVICE, msg);
 }
 
-// Device blocks are recycled per stream: a freed block goes to its stream's free list and the
-// next request of the same size class on that stream takes it back.  Stream order keeps that safe
-// (everything that used the block was queued before whatever reuses it), and it takes the
-// hipMallocAsync / hipFreeAsync calls -- 0.1-0.2 ms of host time each for the multi-GiB layout
-// buffers, during which the device idles -- out of every query after the first.  The lists are
-// trimmed when an allocation fails, when the cached bytes pass CAPSMI_CACHE_BYTES (default 1/4 of
-// the device) and when a session is destroyed.
+// Device blocks are recycled per session: a freed block goes to its session's free list and the
+// next request of the same size class in that session takes it back.  Every block of a session is
+// used on the session's current stream, so stream order keeps reuse safe (everything that used the
+// block was queued before whatever reuses it); a stream switch first drains the old stream
+// (capsmi_session_set_stream / _use_stream), after which every cached block is idle.  This takes
+// the hipMallocAsync / hipFreeAsync calls -- 0.1-0.2 ms of host time each for the multi-GiB
+// layout buffers, during which the device idles -- out of every query after the first.  The lists
+// are trimmed when an allocation fails (every session's), when the cached bytes of all sessions
+// pass CAPSMI_CACHE_BYTES (default 1/4 of the device) and when the session is destroyed; a block
+// freed after its session is gone goes straight back to the device.
+struct AllocCtx {
+    int device = 0;
+    hipStream_t stream = nullptr;  // the owning session's current stream
+    bool alive = true;
+    std::multimap<size_t, void*> free;
+};
+
 namespace {
 
 struct BlockCache {
     std::mutex mu;
-    std::unordered_map<hipStream_t, std::multimap<size_t, void*>> free;
+    std::vector<std::weak_ptr<AllocCtx>> ctxs;  // every live session context (trim on OOM)
     size_t cached = 0, cap = 0;
 };
 
@@ -83,19 +93,13 @@ size_t cache_cap() {
     return c.cap;
 }
 
-// free every cached block of stream st (all streams when st == nullptr and all == true); caller holds mu
-void trim_locked(BlockCache& c, hipStream_t st, bool all) {
-    for (auto it = c.free.begin(); it != c.free.end();) {
-        if (all || it->first == st) {
-            for (auto& kv : it->second) {
-                (void)hipFreeAsync(kv.second, it->first);
-                c.cached -= kv.first;
-            }
-            it = c.free.erase(it);
-        } else {
-            ++it;
-        }
+// free every cached block of one context; caller holds mu
+void trim_ctx_locked(BlockCache& c, AllocCtx& x) {
+    for (auto& kv : x.free) {
+        (void)hipFreeAsync(kv.second, x.stream);
+        c.cached -= kv.first;
     }
+    x.free.clear();
 }
 
 }  // namespace
@@ -104,48 +108,54 @@ DevBuf::~DevBuf() {
     if (!ptr) return;
     BlockCache& c = block_cache();
     std::lock_guard<std::mutex> g(c.mu);
-    auto& fl = c.free[stream];
-    fl.emplace(bytes, ptr);
+    if (!ctx || !ctx->alive) {  // the session is gone (its stream may be too): back to the device
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (ctx) (void)hipSetDevice(ctx->device);
+        (void)hipFree(ptr);
+        if (ctx) (void)hipSetDevice(dev);
+        return;
+    }
+    ctx->free.emplace(bytes, ptr);
     c.cached += bytes;
-    while (c.cached > cache_cap() && !fl.empty()) {  // evict this (live) stream's largest blocks
-        auto last = std::prev(fl.end());
-        (void)hipFreeAsync(last->second, stream);
+    while (c.cached > cache_cap() && !ctx->free.empty()) {  // evict this session's largest blocks
+        auto last = std::prev(ctx->free.end());
+        (void)hipFreeAsync(last->second, ctx->stream);
         c.cached -= last->first;
-        fl.erase(last);
+        ctx->free.erase(last);
     }
 }
 
-Buf dev_alloc(size_t bytes, hipStream_t stream) {
+Buf dev_alloc(size_t bytes, capsmi_session* s) {
     auto b = std::make_shared<DevBuf>();
     const size_t want = size_class(bytes ? bytes : 8);
-    b->stream = stream;
+    AllocCtx& x = *s->alloc;
+    b->ctx = s->alloc;
     BlockCache& c = block_cache();
     (void)cache_cap();  // sized on the first allocation, not inside a destructor
     {
         std::lock_guard<std::mutex> g(c.mu);
-        auto f = c.free.find(stream);
-        if (f != c.free.end()) {
-            auto it = f->second.lower_bound(want);
-            if (it != f->second.end() && it->first <= want + want / 4) {
-                b->ptr = it->second;
-                b->bytes = it->first;
-                c.cached -= it->first;
-                f->second.erase(it);
-                return b;
-            }
+        auto it = x.free.lower_bound(want);
+        if (it != x.free.end() && it->first <= want + want / 4) {
+            b->ptr = it->second;
+            b->bytes = it->first;
+            c.cached -= it->first;
+            x.free.erase(it);
+            return b;
         }
     }
     b->bytes = want;
-    hipError_t e = hipMallocAsync(&b->ptr, want, stream);
-    if (e == hipErrorOutOfMemory) {  // give the cached blocks back and try once more
+    hipError_t e = hipMallocAsync(&b->ptr, want, s->stream);
+    if (e == hipErrorOutOfMemory) {  // give every session's cached blocks back and try once more
         (void)hipGetLastError();
         (void)hipDeviceSynchronize();
         {
             std::lock_guard<std::mutex> g(c.mu);
-            trim_locked(c, nullptr, true);
+            for (auto& w : c.ctxs)
+                if (auto p = w.lock()) trim_ctx_locked(c, *p);
         }
         (void)hipDeviceSynchronize();
-        e = hipMallocAsync(&b->ptr, want, stream);
+        e = hipMallocAsync(&b->ptr, want, s->stream);
     }
     if (e != hipSuccess) {
         b->ptr = nullptr;
@@ -154,10 +164,33 @@ Buf dev_alloc(size_t bytes, hipStream_t stream) {
     return b;
 }
 
-void release_cached_blocks(hipStream_t st) {
+void alloc_ctx_open(capsmi_session* s) {
+    s->alloc = std::make_shared<AllocCtx>();
+    s->alloc->device = s->device;
+    s->alloc->stream = s->stream;
     BlockCache& c = block_cache();
     std::lock_guard<std::mutex> g(c.mu);
-    trim_locked(c, st, false);
+    c.ctxs.erase(std::remove_if(c.ctxs.begin(), c.ctxs.end(), [](const std::weak_ptr<AllocCtx>& w) { return w.expired(); }),
+                 c.ctxs.end());
+    c.ctxs.push_back(s->alloc);
+}
+
+// drain the old stream, then run the session (and its cache) on `st`
+void alloc_ctx_switch(capsmi_session* s, hipStream_t st) {
+    if (st == s->stream) return;
+    HIP_CHECK(hipStreamSynchronize(s->stream));
+    BlockCache& c = block_cache();
+    std::lock_guard<std::mutex> g(c.mu);
+    s->stream = st;
+    s->alloc->stream = st;
+}
+
+// session destroy: the stream is drained by the caller; every cached block goes back to the device
+void alloc_ctx_close(capsmi_session* s) {
+    BlockCache& c = block_cache();
+    std::lock_guard<std::mutex> g(c.mu);
+    trim_ctx_locked(c, *s->alloc);
+    s->alloc->alive = false;
 }
 
 }  // namespace capsmi
@@ -212,8 +245,8 @@ void gather_into(capsmi_table* out, const capsmi_table* t, const Buf& idx, int64
         Column o;
         o.name = c.name;
         o.type = c.type;
-        o.data = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s->stream);
-        if (c.valid || may_miss) o.valid = dev_alloc(n > 0 ? n : 1, s->stream);
+        o.data = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
+        if (c.valid || may_miss) o.valid = dev_alloc(n > 0 ? n : 1, s);
         gather_col(c.d(), c.v(), P<int64_t>(idx), n, P<int64_t>(o.data), P<uint8_t>(o.valid), s->stream);
         out->cols.push_back(std::move(o));
     }
@@ -278,8 +311,8 @@ capsmi_table* join_impl(capsmi_table* l, capsmi_table* r, int jt, const std::vec
     bool lmiss = false, rmiss = false;
     if (jt == CAPSMI_JOIN_CROSS) {
         total = l->nrows * r->nrows;
-        li = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), st);
-        ri = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), st);
+        li = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), s);
+        ri = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), s);
         cross_pairs(l->nrows, r->nrows, P<int64_t>(li), P<int64_t>(ri), st);
     } else {
         for (size_t i = 0; i < lk.size(); ++i)
@@ -291,8 +324,23 @@ capsmi_table* join_impl(capsmi_table* l, capsmi_table* r, int jt, const std::vec
         else if (jt == CAPSMI_JOIN_RIGHT_OUTER) build_left = true;
         capsmi_table* B = build_left ? l : r;
         capsmi_table* Pr = build_left ? r : l;
-        const KeyCols bk = key_cols(B, build_left ? lk : rk);
-        const KeyCols pk = key_cols(Pr, build_left ? rk : lk);
+        KeyCols bk = key_cols(B, build_left ? lk : rk);
+        KeyCols pk = key_cols(Pr, build_left ? rk : lk);
+        // A Long key compared with a Double key: Spark's analyser casts the Long side to Double
+        // (1 = 1.0 matches).  Equal-typed keys compare by their 64-bit words; Spark 2.2.1 does not
+        // normalise -0.0 / NaN in join keys either (SPARK-26021 changed that only in 3.0).
+        std::vector<Buf> widened;
+        for (size_t i = 0; i < lk.size(); ++i) {
+            const int bt = B->cols[(build_left ? lk : rk)[i]].type, pt = Pr->cols[(build_left ? rk : lk)[i]].type;
+            if (bt == pt) continue;
+            const bool widen_build = bt == CAPSMI_I64;
+            KeyCols& kc = widen_build ? bk : pk;
+            const int64_t rows = widen_build ? B->nrows : Pr->nrows;
+            Buf w = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), s);
+            i64_to_f64(kc.data[i], P<int64_t>(w), rows, st);
+            kc.data[i] = P<int64_t>(w);
+            widened.push_back(w);
+        }
         HashTable ht;
         Buf slot_of_row, slot_of_probe, offsets, rows;
         hash_build(s, bk, B->nrows, /*skip_null_keys=*/true, ht, slot_of_row);
@@ -305,12 +353,12 @@ capsmi_table* join_impl(capsmi_table* l, capsmi_table* r, int jt, const std::vec
         if (outer) (build_left ? lmiss : rmiss) = true;
         if (jt == CAPSMI_JOIN_FULL_OUTER) {
             // append build (right) rows that never matched, left side NULL
-            Buf unm_flags = dev_alloc(B->nrows > 0 ? B->nrows : 1, st);
+            Buf unm_flags = dev_alloc(B->nrows > 0 ? B->nrows : 1, s);
             invert_u8(P<uint8_t>(matched), P<uint8_t>(unm_flags), B->nrows, st);
             Buf unm_idx;
             const int64_t nu = flags_to_indices(s, P<uint8_t>(unm_flags), B->nrows, unm_idx);
-            Buf pi2 = dev_alloc(sizeof(int64_t) * (total + nu > 0 ? total + nu : 1), st);
-            Buf bi2 = dev_alloc(sizeof(int64_t) * (total + nu > 0 ? total + nu : 1), st);
+            Buf pi2 = dev_alloc(sizeof(int64_t) * (total + nu > 0 ? total + nu : 1), s);
+            Buf bi2 = dev_alloc(sizeof(int64_t) * (total + nu > 0 ? total + nu : 1), s);
             if (total) {
                 HIP_CHECK(hipMemcpyAsync(P<void>(pi2), P<void>(pi), sizeof(int64_t) * total, hipMemcpyDeviceToDevice, st));
                 HIP_CHECK(hipMemcpyAsync(P<void>(bi2), P<void>(bi), sizeof(int64_t) * total, hipMemcpyDeviceToDevice, st));
@@ -341,10 +389,10 @@ Buf order_perm(capsmi_table* t, const std::vector<int>& keys, const std::vector<
     capsmi_session* s = t->sess;
     hipStream_t st = s->stream;
     const int64_t n = t->nrows;
-    Buf perm = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), st);
+    Buf perm = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
     iota_i64(P<int64_t>(perm), 0, n, st);
     if (n <= 1) return perm;
-    Buf kbuf = dev_alloc(sizeof(uint64_t) * n, st);
+    Buf kbuf = dev_alloc(sizeof(uint64_t) * n, s);
     for (int k = (int)keys.size() - 1; k >= 0; --k) {
         const Column& c = t->cols[keys[k]];
         order_keys(s, c.d(), c.v(), c.type, desc[k] != 0, false, P<int64_t>(perm), n, P<uint64_t>(kbuf));
@@ -402,6 +450,7 @@ capsmi_status capsmi_session_create(int32_t device, capsmi_session** out) {
     s->device = device;
     HIP_CHECK(hipStreamCreateWithFlags(&s->own_stream, hipStreamNonBlocking));
     s->stream = s->own_stream;
+    alloc_ctx_open(s);
     hipDeviceProp_t prop;
     HIP_CHECK(hipGetDeviceProperties(&prop, device));
     s->num_cus = prop.multiProcessorCount;
@@ -421,7 +470,8 @@ capsmi_status capsmi_session_destroy(capsmi_session* s) {
     use_device(s);
     (void)hipStreamSynchronize(s->stream);
     (void)hipStreamSynchronize(s->own_stream);
-    release_cached_blocks(s->own_stream);
+    alloc_ctx_close(s);
+    (void)hipStreamSynchronize(s->stream);
     (void)hipStreamSynchronize(s->own_stream);
     (void)hipHostFree(s->pinned);
     (void)hipStreamDestroy(s->own_stream);
@@ -432,14 +482,16 @@ capsmi_status capsmi_session_destroy(capsmi_session* s) {
 capsmi_status capsmi_session_set_stream(capsmi_session* s, void* hip_stream) {
     API_BEGIN
     need(s, "session");
-    s->stream = hip_stream ? (hipStream_t)hip_stream : s->own_stream;
+    use_device(s);
+    alloc_ctx_switch(s, hip_stream ? (hipStream_t)hip_stream : s->own_stream);
     API_END
 }
 
 capsmi_status capsmi_session_use_stream(capsmi_session* s, void* hip_stream) {
     API_BEGIN
     need(s, "session");
-    s->stream = (hipStream_t)hip_stream;
+    use_device(s);
+    alloc_ctx_switch(s, (hipStream_t)hip_stream);
     API_END
 }
 
@@ -500,10 +552,10 @@ static capsmi_status table_from(capsmi_session* s, int32_t ncols, const capsmi_c
         Column c;
         c.name = cols[i].name;
         c.type = cols[i].type;
-        c.data = dev_alloc(sizeof(int64_t) * (nrows > 0 ? nrows : 1), s->stream);
+        c.data = dev_alloc(sizeof(int64_t) * (nrows > 0 ? nrows : 1), s);
         if (nrows) HIP_CHECK(hipMemcpyAsync(P<void>(c.data), cols[i].data, sizeof(int64_t) * nrows, kind, s->stream));
         if (cols[i].valid) {
-            c.valid = dev_alloc(nrows > 0 ? nrows : 1, s->stream);
+            c.valid = dev_alloc(nrows > 0 ? nrows : 1, s);
             if (nrows) HIP_CHECK(hipMemcpyAsync(P<void>(c.valid), cols[i].valid, nrows, kind, s->stream));
         }
         t->cols.push_back(std::move(c));
@@ -680,7 +732,7 @@ capsmi_status capsmi_filter(capsmi_table* t, int32_t nnodes, const capsmi_expr* 
     REQUIRE(nnodes == 0 || prog, CAPSMI_ERR_ILLEGAL_ARGUMENT, "null program");
     capsmi_session* s = t->sess;
     use_device(s);
-    Buf flags = dev_alloc(t->nrows > 0 ? t->nrows : 1, s->stream);
+    Buf flags = dev_alloc(t->nrows > 0 ? t->nrows : 1, s);
     eval_predicate(s, t, nnodes, prog, P<uint8_t>(flags));
     Buf idx;
     const int64_t n = flags_to_indices(s, P<uint8_t>(flags), t->nrows, idx);
@@ -702,8 +754,8 @@ capsmi_status capsmi_with_columns(capsmi_table* t, int32_t ncols, const capsmi_e
         need(cols[i].name, "column name");
         Column c;
         c.name = cols[i].name;
-        c.data = dev_alloc(sizeof(int64_t) * (t->nrows > 0 ? t->nrows : 1), s->stream);
-        c.valid = dev_alloc(t->nrows > 0 ? t->nrows : 1, s->stream);
+        c.data = dev_alloc(sizeof(int64_t) * (t->nrows > 0 ? t->nrows : 1), s);
+        c.valid = dev_alloc(t->nrows > 0 ? t->nrows : 1, s);
         eval_expr(s, t, cols[i].nnodes, cols[i].prog, P<int64_t>(c.data), P<uint8_t>(c.valid), &c.type);
         const int j = o->find(c.name);
         if (j >= 0) o->cols[j] = std::move(c);  // replaced in place (SparkTable.scala:82-87)
@@ -748,14 +800,14 @@ capsmi_status capsmi_union_all(capsmi_table* a, capsmi_table* b, capsmi_table** 
         Column c;
         c.name = x.name;  // positional union, left names (Dataset.union)
         c.type = x.type;
-        c.data = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s->stream);
+        c.data = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
         if (a->nrows)
             HIP_CHECK(hipMemcpyAsync(P<int64_t>(c.data), x.d(), sizeof(int64_t) * a->nrows, hipMemcpyDeviceToDevice, s->stream));
         if (b->nrows)
             HIP_CHECK(hipMemcpyAsync(P<int64_t>(c.data) + a->nrows, y.d(), sizeof(int64_t) * b->nrows,
                                      hipMemcpyDeviceToDevice, s->stream));
         if (x.valid || y.valid) {
-            c.valid = dev_alloc(n > 0 ? n : 1, s->stream);
+            c.valid = dev_alloc(n > 0 ? n : 1, s);
             if (x.valid) { if (a->nrows) HIP_CHECK(hipMemcpyAsync(P<uint8_t>(c.valid), x.v(), a->nrows, hipMemcpyDeviceToDevice, s->stream)); }
             else fill_u8(P<uint8_t>(c.valid), 1, a->nrows, s->stream);
             if (y.valid) { if (b->nrows) HIP_CHECK(hipMemcpyAsync(P<uint8_t>(c.valid) + a->nrows, y.v(), b->nrows, hipMemcpyDeviceToDevice, s->stream)); }
@@ -861,7 +913,7 @@ capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, 
         ng = hash_group_ids(s, ht, sor, n, gid, rep);
     } else {
         ng = 1;  // global aggregate: exactly one row, also over empty input (Spark)
-        gid = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), st);
+        gid = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
         fill_i64(P<int64_t>(gid), 0, n, st);
     }
     auto* o = new_table(s, ng);
@@ -878,7 +930,7 @@ capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, 
         need(ag.output, "aggregate output name");
         Column c;
         c.name = ag.output;
-        c.data = dev_alloc(sizeof(int64_t) * ng, st);
+        c.data = dev_alloc(sizeof(int64_t) * ng, s);
         const Column* in = nullptr;
         if (ag.kind != CAPSMI_AGG_COUNT_STAR) in = &t->cols[col_index(t, ag.input)];
         switch (ag.kind) {
@@ -904,7 +956,7 @@ capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, 
                     Buf sor2, gid2, rep2;
                     hash_build(s, k, n, /*skip_null_keys=*/true, h2, sor2);
                     const int64_t np = hash_group_ids(s, h2, sor2, n, gid2, rep2);
-                    Buf pg = dev_alloc(sizeof(int64_t) * (np > 0 ? np : 1), st);
+                    Buf pg = dev_alloc(sizeof(int64_t) * (np > 0 ? np : 1), s);
                     gather_col(P<int64_t>(gid), nullptr, P<int64_t>(rep2), np, P<int64_t>(pg), nullptr, st);
                     agg_count(P<int64_t>(pg), nullptr, np, P<int64_t>(c.data), st);
                 }
@@ -913,7 +965,7 @@ capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, 
             case CAPSMI_AGG_SUM: {
                 REQUIRE(in->type == CAPSMI_I64 || in->type == CAPSMI_F64, CAPSMI_ERR_ILLEGAL_ARGUMENT, "sum of non-number");
                 c.type = in->type;
-                c.valid = dev_alloc(ng, st);
+                c.valid = dev_alloc(ng, s);
                 HIP_CHECK(hipMemsetAsync(P<void>(c.data), 0, sizeof(int64_t) * ng, st));
                 HIP_CHECK(hipMemsetAsync(P<void>(c.valid), 0, ng, st));
                 if (in->type == CAPSMI_I64) agg_sum_i64(P<int64_t>(gid), in->d(), in->v(), n, P<int64_t>(c.data), P<uint8_t>(c.valid), st);
@@ -924,7 +976,7 @@ capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, 
             case CAPSMI_AGG_MAX: {
                 const bool mx = ag.kind == CAPSMI_AGG_MAX;
                 c.type = in->type;
-                c.valid = dev_alloc(ng, st);
+                c.valid = dev_alloc(ng, s);
                 fill_i64(P<int64_t>(c.data), mx ? INT64_MIN : INT64_MAX, ng, st);
                 HIP_CHECK(hipMemsetAsync(P<void>(c.valid), 0, ng, st));
                 agg_minmax(P<int64_t>(gid), in->d(), in->v(), n, in->type, mx, P<int64_t>(c.data), P<uint8_t>(c.valid), st);
@@ -934,13 +986,13 @@ capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, 
             case CAPSMI_AGG_AVG: {
                 REQUIRE(in->type == CAPSMI_I64 || in->type == CAPSMI_F64, CAPSMI_ERR_ILLEGAL_ARGUMENT, "avg of non-number");
                 c.type = in->type;  // avg(..).cast(cypherType): integer averages come back as Long
-                c.valid = dev_alloc(ng, st);
-                Buf sum = dev_alloc(sizeof(double) * ng, st), cnt = dev_alloc(sizeof(int64_t) * ng, st), seen = dev_alloc(ng, st);
+                c.valid = dev_alloc(ng, s);
+                Buf sum = dev_alloc(sizeof(double) * ng, s), cnt = dev_alloc(sizeof(int64_t) * ng, s), seen = dev_alloc(ng, s);
                 HIP_CHECK(hipMemsetAsync(P<void>(sum), 0, sizeof(double) * ng, st));
                 HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, sizeof(int64_t) * ng, st));
                 if (in->type == CAPSMI_I64) {
                     // Spark casts Long input to Double before summing
-                    Buf dv = dev_alloc(sizeof(double) * (n > 0 ? n : 1), st);
+                    Buf dv = dev_alloc(sizeof(double) * (n > 0 ? n : 1), s);
                     i64_to_f64(in->d(), P<int64_t>(dv), n, st);
                     agg_sum_f64(P<int64_t>(gid), P<int64_t>(dv), in->v(), n, P<double>(sum), P<uint8_t>(seen), st);
                 } else {
@@ -973,7 +1025,7 @@ capsmi_status capsmi_bitmap_create(capsmi_session* s, int64_t id_lo, int64_t id_
     b->lo = id_lo;
     b->hi = id_hi;
     b->nwords = (id_hi - id_lo + 31) / 32;
-    b->words = dev_alloc(sizeof(uint32_t) * (b->nwords > 0 ? b->nwords : 1), s->stream);
+    b->words = dev_alloc(sizeof(uint32_t) * (b->nwords > 0 ? b->nwords : 1), s);
     HIP_CHECK(hipMemsetAsync(P<void>(b->words), 0, sizeof(uint32_t) * (b->nwords > 0 ? b->nwords : 1), s->stream));
     b->set_bits = 0;
     b->full = id_hi == id_lo;
@@ -992,10 +1044,10 @@ capsmi_status capsmi_bitmap_add_scan(capsmi_bitmap* b, capsmi_table* nodes, cons
     REQUIRE(idc.type == CAPSMI_I64, CAPSMI_ERR_ILLEGAL_ARGUMENT, "node id column must be Long");
     Buf flags;
     if (nnodes > 0) {
-        flags = dev_alloc(nodes->nrows > 0 ? nodes->nrows : 1, s->stream);
+        flags = dev_alloc(nodes->nrows > 0 ? nodes->nrows : 1, s);
         eval_predicate(s, nodes, nnodes, pred, P<uint8_t>(flags));
     }
-    Buf cnt = dev_alloc(3 * sizeof(int64_t), s->stream);
+    Buf cnt = dev_alloc(3 * sizeof(int64_t), s);
     HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, 3 * sizeof(int64_t), s->stream));
     bitmap_add_rows(b, idc.d(), idc.v(), P<uint8_t>(flags), nodes->nrows, P<int64_t>(cnt));
     int64_t h[3];
@@ -1059,15 +1111,15 @@ capsmi_status capsmi_expand_filter(capsmi_session* s, capsmi_table* rels, const 
         oc.name = out_names && out_names[i] ? out_names[i] : c.name;
         REQUIRE(names.insert(oc.name).second, CAPSMI_ERR_ILLEGAL_ARGUMENT, "duplicate output column " + oc.name);
         oc.type = c.type;
-        oc.data = dev_alloc(sizeof(int64_t) * (m > 0 ? m : 1), s->stream);
-        if (c.valid) oc.valid = dev_alloc(m > 0 ? m : 1, s->stream);
+        oc.data = dev_alloc(sizeof(int64_t) * (m > 0 ? m : 1), s);
+        if (c.valid) oc.valid = dev_alloc(m > 0 ? m : 1, s);
         in_d[i] = c.d();
         in_v[i] = c.v();
         out_d[i] = P<int64_t>(oc.data);
         out_v[i] = P<uint8_t>(oc.valid);
         o->cols.push_back(std::move(oc));
     }
-    Buf cnt = dev_alloc(8, s->stream);
+    Buf cnt = dev_alloc(8, s);
     HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, 8, s->stream));
     graph::expand_filter(s, sc.d(), dc.d(), m, src_ok, dst_ok, nout, in_d, in_v, out_d, out_v, P<int64_t>(cnt));
     o->nrows = read_scalar(s, P<int64_t>(cnt));
@@ -1156,8 +1208,8 @@ capsmi_status capsmi_two_hop_count_distinct(capsmi_session* s, int32_t nrels, ca
     check_bitmap(c_ok, "c_ok");
     use_device(s);
     const int64_t nw = b_ok->nwords > 0 ? b_ok->nwords : 1;
-    Buf x = dev_alloc(sizeof(uint32_t) * nw * 3, s->stream);
-    Buf cw = dev_alloc(sizeof(uint32_t) * (c_ok->nwords > 0 ? c_ok->nwords : 1), s->stream);
+    Buf x = dev_alloc(sizeof(uint32_t) * nw * 3, s);
+    Buf cw = dev_alloc(sizeof(uint32_t) * (c_ok->nwords > 0 ? c_ok->nwords : 1), s);
     uint32_t* X1 = P<uint32_t>(x);
     if (same_domain(a_ok, b_ok, c_ok)) {
         // cold radix-partitioned path: partition + two LDS-resident hops
@@ -1516,7 +1568,7 @@ capsmi_status capsmi_two_hop_count_distinct_part(capsmi_session* s, const capsmi
     REQUIRE(same_domain(a_ok, b_ok, c_ok), CAPSMI_ERR_UNSUPPORTED, "a, b, c scans need one id domain");
     use_device(s);
     const int64_t nw = b_ok->nwords > 0 ? b_ok->nwords : 1;
-    Buf x = dev_alloc(sizeof(uint32_t) * nw * 4, s->stream);
+    Buf x = dev_alloc(sizeof(uint32_t) * nw * 4, s);
     uint32_t* X1 = P<uint32_t>(x);
     part_mid(s, p->rp, a_ok, b_ok, X1, X1 + nw, X1 + 2 * nw);
     HIP_CHECK(hipMemsetAsync(X1 + 3 * nw, 0, sizeof(uint32_t) * nw, s->stream));
@@ -1577,9 +1629,9 @@ capsmi_status capsmi_two_hop_count(capsmi_session* s, int32_t nrels, capsmi_tabl
             "closed-form count(*) needs each node id in one scanned row");
     use_device(s);
     const int64_t n = b_ok->hi - b_ok->lo;
-    Buf inA = dev_alloc(sizeof(uint32_t) * (n > 0 ? n : 1), s->stream);
-    Buf outC = dev_alloc(sizeof(uint32_t) * (n > 0 ? n : 1), s->stream);
-    Buf acc = dev_alloc(16, s->stream);  // [0] = loops, [1] = sum of products
+    Buf inA = dev_alloc(sizeof(uint32_t) * (n > 0 ? n : 1), s);
+    Buf outC = dev_alloc(sizeof(uint32_t) * (n > 0 ? n : 1), s);
+    Buf acc = dev_alloc(16, s);  // [0] = loops, [1] = sum of products
     HIP_CHECK(hipMemsetAsync(P<void>(inA), 0, sizeof(uint32_t) * (n > 0 ? n : 1), s->stream));
     HIP_CHECK(hipMemsetAsync(P<void>(outC), 0, sizeof(uint32_t) * (n > 0 ? n : 1), s->stream));
     HIP_CHECK(hipMemsetAsync(P<void>(acc), 0, 16, s->stream));
@@ -1610,8 +1662,8 @@ capsmi_status capsmi_cluster_by(capsmi_table* rels, const char* key_col, int64_t
     // [lo, hi) would break the bit budget, so the sort covers all 64 bits when the range is unknown
     int bits = 1;
     while (bits < 64 && (int64_t(1) << bits) < (id_hi - id_lo)) ++bits;
-    Buf keys = dev_alloc(sizeof(uint64_t) * (n > 0 ? n : 1), s->stream);
-    Buf perm = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s->stream);
+    Buf keys = dev_alloc(sizeof(uint64_t) * (n > 0 ? n : 1), s);
+    Buf perm = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
     HIP_CHECK(hipMemcpyAsync(P<void>(keys), kc.d(), sizeof(int64_t) * n, hipMemcpyDeviceToDevice, s->stream));
     iota_i64(P<int64_t>(perm), 0, n, s->stream);
     // validate range on device via a bitmap scan of the key column
@@ -1621,9 +1673,9 @@ capsmi_status capsmi_cluster_by(capsmi_table* rels, const char* key_col, int64_t
         tmp.lo = id_lo;
         tmp.hi = id_hi;
         tmp.nwords = (id_hi - id_lo + 31) / 32;
-        tmp.words = dev_alloc(sizeof(uint32_t) * (tmp.nwords > 0 ? tmp.nwords : 1), s->stream);
+        tmp.words = dev_alloc(sizeof(uint32_t) * (tmp.nwords > 0 ? tmp.nwords : 1), s);
         HIP_CHECK(hipMemsetAsync(P<void>(tmp.words), 0, sizeof(uint32_t) * (tmp.nwords > 0 ? tmp.nwords : 1), s->stream));
-        Buf cnt = dev_alloc(24, s->stream);
+        Buf cnt = dev_alloc(24, s);
         HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, 24, s->stream));
         bitmap_add_rows(&tmp, kc.d(), nullptr, nullptr, n, P<int64_t>(cnt));
         int64_t h[3];
@@ -1693,10 +1745,10 @@ capsmi_status capsmi_rmat_nodes(capsmi_session* s, int32_t scale, int32_t kind, 
     Buf ids;
     int64_t rows = n;
     if (kind == 0) {
-        ids = dev_alloc(sizeof(int64_t) * n, s->stream);
+        ids = dev_alloc(sizeof(int64_t) * n, s);
         iota_i64(P<int64_t>(ids), 0, n, s->stream);
     } else {
-        Buf f = dev_alloc(n, s->stream);
+        Buf f = dev_alloc(n, s);
         graph::person_flags(s, n, kind == 1, P<uint8_t>(f));
         rows = flags_to_indices(s, P<uint8_t>(f), n, ids);  // id == row index of the full range
     }
@@ -1710,7 +1762,7 @@ capsmi_status capsmi_rmat_nodes(capsmi_session* s, int32_t scale, int32_t kind, 
         Column a;
         a.name = "age";
         a.type = CAPSMI_I64;
-        a.data = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), s->stream);
+        a.data = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), s);
         graph::ages(s, P<int64_t>(ids), rows, seed, P<int64_t>(a.data));
         o->cols.push_back(std::move(a));
     }

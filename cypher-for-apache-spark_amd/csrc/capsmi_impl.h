@@ -40,14 +40,18 @@ struct Error : std::runtime_error {
 // ---- device memory --------------------------------------------------------------
 // Stream-ordered allocations from the device's default pool (release threshold
 // raised at session create, so freed blocks are recycled instead of unmapped).
+// Per-session allocation context: the device, the stream the session currently runs on, and the
+// session's cache of freed device blocks (api.hip).  Blocks hold it, so a block that outlives its
+// session is returned to the device instead of to a dead cache.
+struct AllocCtx;
 struct DevBuf {
     void* ptr = nullptr;
     size_t bytes = 0;
-    hipStream_t stream = nullptr;
+    std::shared_ptr<AllocCtx> ctx;
     ~DevBuf();
 };
 using Buf = std::shared_ptr<DevBuf>;
-Buf dev_alloc(size_t bytes, hipStream_t stream);
+Buf dev_alloc(size_t bytes, capsmi_session* s);
 
 template <class T>
 inline T* P(const Buf& b) { return b ? static_cast<T*>(b->ptr) : nullptr; }
@@ -65,6 +69,7 @@ struct Column {
 }  // namespace capsmi
 
 struct capsmi_session {
+    std::shared_ptr<capsmi::AllocCtx> alloc;  // block cache of this session (api.hip)
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;  // current (own or external)
@@ -127,7 +132,7 @@ namespace capsmi {
 
 // ---- kernel launchers (k_*.hip) ------------------------------------------------
 // scan / compaction / gather (k_basic.hip)
-void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t st);  // out has n+1 entries
+void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, capsmi_session* s);  // out has n+1 entries
 void fill_i64(int64_t* p, int64_t v, int64_t n, hipStream_t st);
 void fill_u8(uint8_t* p, uint8_t v, int64_t n, hipStream_t st);
 void iota_i64(int64_t* p, int64_t start, int64_t n, hipStream_t st);

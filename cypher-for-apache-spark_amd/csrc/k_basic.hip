@@ -157,7 +157,8 @@ inline int grid_for(int64_t n, int block = 256) {
 
 }  // namespace
 
-void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t st) {
+void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, capsmi_session* s) {
+    hipStream_t st = s->stream;
     const int64_t ntiles = (n + kTile - 1) / kTile;
     if (n == 0) {
         HIP_CHECK(hipMemsetAsync(out, 0, sizeof(int64_t), st));
@@ -168,10 +169,10 @@ void exclusive_scan_i64(const int64_t* in, int64_t* out, int64_t n, hipStream_t 
         HIP_CHECK(hipGetLastError());
         return;
     }
-    Buf sums = dev_alloc(sizeof(int64_t) * ntiles, st);
-    Buf offs = dev_alloc(sizeof(int64_t) * (ntiles + 1), st);
+    Buf sums = dev_alloc(sizeof(int64_t) * ntiles, s);
+    Buf offs = dev_alloc(sizeof(int64_t) * (ntiles + 1), s);
     hipLaunchKernelGGL(k_tile_sum, dim3((unsigned)ntiles), dim3(kBlock), 0, st, in, n, P<int64_t>(sums));
-    exclusive_scan_i64(P<int64_t>(sums), P<int64_t>(offs), ntiles, st);
+    exclusive_scan_i64(P<int64_t>(sums), P<int64_t>(offs), ntiles, s);
     hipLaunchKernelGGL(k_tile_scan, dim3((unsigned)ntiles), dim3(kBlock), 0, st, in, n, P<int64_t>(offs), out);
     HIP_CHECK(hipGetLastError());
 }
@@ -198,16 +199,16 @@ int64_t read_scalar(capsmi_session* s, const int64_t* dev) {
 int64_t flags_to_indices(capsmi_session* s, const uint8_t* flags, int64_t n, Buf& out_idx) {
     hipStream_t st = s->stream;
     if (n == 0) {
-        out_idx = dev_alloc(8, st);
+        out_idx = dev_alloc(8, s);
         return 0;
     }
     const int64_t ntiles = (n + kTile - 1) / kTile;
-    Buf cnt = dev_alloc(sizeof(int64_t) * ntiles, st);
-    Buf off = dev_alloc(sizeof(int64_t) * (ntiles + 1), st);
+    Buf cnt = dev_alloc(sizeof(int64_t) * ntiles, s);
+    Buf off = dev_alloc(sizeof(int64_t) * (ntiles + 1), s);
     hipLaunchKernelGGL(k_flag_count, dim3((unsigned)ntiles), dim3(kBlock), 0, st, flags, n, P<int64_t>(cnt));
-    exclusive_scan_i64(P<int64_t>(cnt), P<int64_t>(off), ntiles, st);
+    exclusive_scan_i64(P<int64_t>(cnt), P<int64_t>(off), ntiles, s);
     const int64_t total = read_scalar(s, P<int64_t>(off) + ntiles);
-    out_idx = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), st);
+    out_idx = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), s);
     hipLaunchKernelGGL(k_flag_write, dim3((unsigned)ntiles), dim3(kBlock), 0, st, flags, n, P<int64_t>(off),
                        P<int64_t>(out_idx));
     HIP_CHECK(hipGetLastError());

@@ -276,7 +276,7 @@ void launch_eval(capsmi_session* s, const capsmi_table* t, int32_t nn, const cap
         cp.valid[c] = t->cols[c].v();
         cp.type[c] = (int8_t)t->cols[c].type;
     }
-    Buf dprog = dev_alloc(sizeof(capsmi_expr) * (nn > 0 ? nn : 1), s->stream);
+    Buf dprog = dev_alloc(sizeof(capsmi_expr) * (nn > 0 ? nn : 1), s);
     if (nn > 0)
         HIP_CHECK(hipMemcpyAsync(P<void>(dprog), prog, sizeof(capsmi_expr) * nn, hipMemcpyHostToDevice, s->stream));
     int64_t g = (n + 255) / 256;

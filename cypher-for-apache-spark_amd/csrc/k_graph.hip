@@ -629,7 +629,7 @@ void bitmap_add_rows(capsmi_bitmap* b, const int64_t* ids, const uint8_t* ids_va
 }
 
 int64_t words_popcount(capsmi_session* s, const uint32_t* w, int64_t w_begin, int64_t w_end) {
-    Buf out = dev_alloc(8, s->stream);
+    Buf out = dev_alloc(8, s);
     HIP_CHECK(hipMemsetAsync(P<void>(out), 0, 8, s->stream));
     if (w_end > w_begin)
         hipLaunchKernelGGL(k_popcount, dim3(grid_cap((w_end - w_begin + 3) / 4, (int64_t)s->num_cus * 4)), dim3(256), 0,
@@ -763,14 +763,14 @@ int64_t rmat(capsmi_session* s, int scale, int64_t e_begin, int64_t e_end, int p
     const int64_t m = e_end - e_begin;
     const int64_t nb = (m + 255) / 256;
     hipStream_t st = s->stream;
-    Buf cnt = dev_alloc(sizeof(int64_t) * (nb > 0 ? nb : 1), st);
-    Buf off = dev_alloc(sizeof(int64_t) * (nb + 1), st);
+    Buf cnt = dev_alloc(sizeof(int64_t) * (nb > 0 ? nb : 1), s);
+    Buf off = dev_alloc(sizeof(int64_t) * (nb + 1), s);
     if (nb > 0) hipLaunchKernelGGL(k_rmat_count, dim3((unsigned)nb), dim3(256), 0, st, g, P<unsigned long long>(cnt));
-    exclusive_scan_i64(P<int64_t>(cnt), P<int64_t>(off), nb, st);
+    exclusive_scan_i64(P<int64_t>(cnt), P<int64_t>(off), nb, s);
     const int64_t total = read_scalar(s, P<int64_t>(off) + nb);
-    id = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), st);
-    so = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), st);
-    dout = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), st);
+    id = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), s);
+    so = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), s);
+    dout = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), s);
     if (nb > 0)
         hipLaunchKernelGGL(k_rmat_write, dim3((unsigned)nb), dim3(256), 0, st, g, P<int64_t>(off), P<int64_t>(id),
                            P<int64_t>(so), P<int64_t>(dout));
@@ -798,7 +798,7 @@ void fingerprint(capsmi_session* s, int ncols, const int64_t* const* d, const ui
         fc.d[c] = c < ncols ? d[c] : nullptr;
         fc.v[c] = c < ncols ? v[c] : nullptr;
     }
-    Buf out = dev_alloc(16, s->stream);
+    Buf out = dev_alloc(16, s);
     HIP_CHECK(hipMemsetAsync(P<void>(out), 0, 16, s->stream));
     if (n > 0)
         hipLaunchKernelGGL(k_fingerprint, dim3(grid_cap(n, 4096)), dim3(256), 0, s->stream, fc, n,

@@ -243,11 +243,11 @@ void hash_build(capsmi_session* s, const KeyCols& k, int64_t n, bool skip_null_k
     int64_t cap = 64;
     while (cap < 2 * n) cap <<= 1;
     ht.cap = cap;
-    ht.slot_row = dev_alloc(sizeof(int64_t) * cap, st);
-    ht.slot_count = dev_alloc(sizeof(int64_t) * cap, st);
+    ht.slot_row = dev_alloc(sizeof(int64_t) * cap, s);
+    ht.slot_count = dev_alloc(sizeof(int64_t) * cap, s);
     fill_i64(P<int64_t>(ht.slot_row), -1, cap, st);
     HIP_CHECK(hipMemsetAsync(P<void>(ht.slot_count), 0, sizeof(int64_t) * cap, st));
-    slot_of_row = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), st);
+    slot_of_row = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
     if (n > 0)
         hipLaunchKernelGGL(k_hash_build, dim3(grid_for(n)), dim3(256), 0, st, k, n, skip_null_keys ? 1 : 0,
                            P<unsigned long long>(ht.slot_row), P<unsigned long long>(ht.slot_count), cap - 1,
@@ -258,7 +258,7 @@ void hash_build(capsmi_session* s, const KeyCols& k, int64_t n, bool skip_null_k
 void hash_probe(capsmi_session* s, const KeyCols& probe, const KeyCols& build, int64_t n, const HashTable& ht,
                 Buf& slot_of_probe) {
     hipStream_t st = s->stream;
-    slot_of_probe = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), st);
+    slot_of_probe = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
     if (n > 0)
         hipLaunchKernelGGL(k_hash_probe, dim3(grid_for(n)), dim3(256), 0, st, probe, build, n,
                            P<int64_t>(ht.slot_row), ht.cap - 1, P<int64_t>(slot_of_probe));
@@ -268,17 +268,17 @@ void hash_probe(capsmi_session* s, const KeyCols& probe, const KeyCols& build, i
 int64_t hash_group_ids(capsmi_session* s, const HashTable& ht, const Buf& slot_of_row, int64_t n, Buf& gid_of_row,
                        Buf& rep_row_of_gid) {
     hipStream_t st = s->stream;
-    Buf occ = dev_alloc(ht.cap, st);
+    Buf occ = dev_alloc(ht.cap, s);
     hipLaunchKernelGGL(k_occupied, dim3(grid_for(ht.cap)), dim3(256), 0, st, P<int64_t>(ht.slot_row), ht.cap,
                        P<uint8_t>(occ));
     Buf slots;
     const int64_t ng = flags_to_indices(s, P<uint8_t>(occ), ht.cap, slots);
-    Buf slot_gid = dev_alloc(sizeof(int64_t) * ht.cap, st);
-    rep_row_of_gid = dev_alloc(sizeof(int64_t) * (ng > 0 ? ng : 1), st);
+    Buf slot_gid = dev_alloc(sizeof(int64_t) * ht.cap, s);
+    rep_row_of_gid = dev_alloc(sizeof(int64_t) * (ng > 0 ? ng : 1), s);
     if (ng > 0)
         hipLaunchKernelGGL(k_slot_gid, dim3(grid_for(ng)), dim3(256), 0, st, P<int64_t>(slots), ng,
                            P<int64_t>(ht.slot_row), P<int64_t>(slot_gid), P<int64_t>(rep_row_of_gid));
-    gid_of_row = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), st);
+    gid_of_row = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
     if (n > 0)
         hipLaunchKernelGGL(k_row_gid, dim3(grid_for(n)), dim3(256), 0, st, P<int64_t>(slot_of_row), n,
                            P<int64_t>(slot_gid), P<int64_t>(gid_of_row));
@@ -289,11 +289,11 @@ int64_t hash_group_ids(capsmi_session* s, const HashTable& ht, const Buf& slot_o
 void hash_group_rows(capsmi_session* s, const HashTable& ht, const Buf& slot_of_row, int64_t n, Buf& offsets,
                      Buf& rows) {
     hipStream_t st = s->stream;
-    offsets = dev_alloc(sizeof(int64_t) * (ht.cap + 1), st);
-    exclusive_scan_i64(P<int64_t>(ht.slot_count), P<int64_t>(offsets), ht.cap, st);
-    Buf cursor = dev_alloc(sizeof(int64_t) * ht.cap, st);
+    offsets = dev_alloc(sizeof(int64_t) * (ht.cap + 1), s);
+    exclusive_scan_i64(P<int64_t>(ht.slot_count), P<int64_t>(offsets), ht.cap, s);
+    Buf cursor = dev_alloc(sizeof(int64_t) * ht.cap, s);
     HIP_CHECK(hipMemcpyAsync(P<void>(cursor), P<void>(offsets), sizeof(int64_t) * ht.cap, hipMemcpyDeviceToDevice, st));
-    rows = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), st);
+    rows = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
     if (n > 0)
         hipLaunchKernelGGL(k_scatter_rows, dim3(grid_for(n)), dim3(256), 0, st, P<int64_t>(slot_of_row), n,
                            P<unsigned long long>(cursor), P<int64_t>(rows));
@@ -304,18 +304,18 @@ int64_t join_expand(capsmi_session* s, const Buf& slot_of_probe, int64_t nprobe,
                     const Buf& offsets, const Buf& rows, bool left_outer, Buf& out_l, Buf& out_r,
                     Buf* matched_build, int64_t nbuild) {
     hipStream_t st = s->stream;
-    Buf cnt = dev_alloc(sizeof(int64_t) * (nprobe > 0 ? nprobe : 1), st);
-    Buf prefix = dev_alloc(sizeof(int64_t) * (nprobe + 1), st);
+    Buf cnt = dev_alloc(sizeof(int64_t) * (nprobe > 0 ? nprobe : 1), s);
+    Buf prefix = dev_alloc(sizeof(int64_t) * (nprobe + 1), s);
     if (nprobe > 0)
         hipLaunchKernelGGL(k_probe_counts, dim3(grid_for(nprobe)), dim3(256), 0, st, P<int64_t>(slot_of_probe),
                            nprobe, P<int64_t>(ht.slot_count), left_outer ? 1 : 0, P<int64_t>(cnt));
-    exclusive_scan_i64(P<int64_t>(cnt), P<int64_t>(prefix), nprobe, st);
+    exclusive_scan_i64(P<int64_t>(cnt), P<int64_t>(prefix), nprobe, s);
     const int64_t total = read_scalar(s, P<int64_t>(prefix) + nprobe);
-    out_l = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), st);
-    out_r = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), st);
+    out_l = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), s);
+    out_r = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), s);
     uint8_t* matched = nullptr;
     if (matched_build) {
-        *matched_build = dev_alloc(nbuild > 0 ? nbuild : 1, st);
+        *matched_build = dev_alloc(nbuild > 0 ? nbuild : 1, s);
         matched = P<uint8_t>(*matched_build);
         HIP_CHECK(hipMemsetAsync(matched, 0, nbuild > 0 ? nbuild : 1, st));
     }

@@ -853,9 +853,9 @@ void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_
             "relationship table too large for the layout");
     const int64_t npool = pool_chunks > 0 ? pool_chunks : 1;
     const int hw = hist_words(L.ns);
-    cp.pool = dev_alloc(sizeof(uint2) * kCh * (size_t)(npool + 1), st);  // + a trash chunk
-    cp.meta = dev_alloc(sizeof(unsigned long long) * npool, st);
-    cp.chist = dev_alloc(sizeof(uint32_t) * hw * (size_t)npool, st);
+    cp.pool = dev_alloc(sizeof(uint2) * kCh * (size_t)(npool + 1), s);  // + a trash chunk
+    cp.meta = dev_alloc(sizeof(unsigned long long) * npool, s);
+    cp.chist = dev_alloc(sizeof(uint32_t) * hw * (size_t)npool, s);
     HIP_CHECK(hipMemsetAsync(P<void>(cp.meta), 0, sizeof(unsigned long long) * npool, st));
     const size_t lds1l = scatter1l_lds(L.nt, L.ns, kP1Block, kP1Tile);
     const bool lines = lds1l <= (size_t)160 * 1024;
@@ -882,7 +882,7 @@ void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_
     // (segment, source cell); no host round trip until the layout is written
     const int64_t g2 = std::max<int64_t>(1, std::min<int64_t>(g2_want, npool));
     cp.jbuf = dev_alloc(sizeof(int64_t) * (3 * (size_t)L.nt + 2 * (size_t)g2 + 3) + sizeof(uint32_t) * npool +
-                             sizeof(int) * g2, st);
+                             sizeof(int) * g2, s);
     int64_t* jcnt = P<int64_t>(cp.jbuf);
     int64_t* jst = jcnt + L.nt;        // nt + 1
     int64_t* jcur = jst + L.nt + 1;    // nt
@@ -894,13 +894,13 @@ void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_
     const unsigned cg = (unsigned)((npool + kChunkPer - 1) / kChunkPer);
     hipLaunchKernelGGL(k_chunk_count, dim3(cg), dim3(kChunkBlock), sizeof(uint32_t) * L.nt, st,
                        P<unsigned long long>(cp.meta), pool_chunks, L.nt, jcnt);
-    exclusive_scan_i64(jcnt, jst, L.nt, st);
+    exclusive_scan_i64(jcnt, jst, L.nt, s);
     HIP_CHECK(hipMemcpyAsync(jcur, jst, sizeof(int64_t) * L.nt, hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(k_chunk_place, dim3(cg), dim3(kChunkBlock), sizeof(uint32_t) * 2 * L.nt, st,
                        P<unsigned long long>(cp.meta), pool_chunks, L.nt,
                        reinterpret_cast<unsigned long long*>(jcur), order);
     hipLaunchKernelGGL(k_seg_count, dim3((unsigned)((g2 + 255) / 256)), dim3(256), 0, st, jst, L.nt, g2, kseg, ja);
-    exclusive_scan_i64(kseg, segbase, g2, st);
+    exclusive_scan_i64(kseg, segbase, g2, s);
     HIP_CHECK(hipGetLastError());
     cp.pool_chunks = pool_chunks;
     cp.npool = npool;
@@ -937,17 +937,17 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
     Buf& pool = cp.pool;
     Buf& meta = cp.meta;
     Buf& chist = cp.chist;
-    Buf pbuf = dev_alloc(sizeof(uint32_t) * (size_t)maxg * L.ns, st);
+    Buf pbuf = dev_alloc(sizeof(uint32_t) * (size_t)maxg * L.ns, s);
     uint32_t* psum = P<uint32_t>(pbuf);
-    Buf tot = dev_alloc(sizeof(int64_t) * L.ncells, st);
+    Buf tot = dev_alloc(sizeof(int64_t) * L.ncells, s);
     hipLaunchKernelGGL(k_seg_sum, dim3((unsigned)maxg), dim3(1024), 0, st, P<uint32_t>(chist), order, jst, L.nt, g2,
                        segbase, ja, L.ns, psum);
     hipLaunchKernelGGL(k_seg_prefix, dim3((L.ncells + 255) / 256), dim3(256), 0, st, psum, jst, g2, segbase, ja, L,
                        P<int64_t>(tot));
-    rp.boff = dev_alloc(sizeof(int64_t) * (L.ncells + 1), st);  // cell offsets
-    exclusive_scan_i64(P<int64_t>(tot), P<int64_t>(rp.boff), L.ncells, st);
+    rp.boff = dev_alloc(sizeof(int64_t) * (L.ncells + 1), s);  // cell offsets
+    exclusive_scan_i64(P<int64_t>(tot), P<int64_t>(rp.boff), L.ncells, s);
     HIP_CHECK(hipGetLastError());
-    rp.pairs = dev_alloc(sizeof(uint2) * (mtot + kPad), st);  // kept <= mtot
+    rp.pairs = dev_alloc(sizeof(uint2) * (mtot + kPad), s);  // kept <= mtot
 
     Hop1Out ho{};
     if (fuse) ho = Hop1Out{BitV{P<uint32_t>(h1->b->words), h1->b->full ? 1 : 0}, h1->M, h1->S1, h1->S2, h1->b->nwords};
@@ -1033,7 +1033,7 @@ void relpart_digest(capsmi_session* s, const RelPart& rp, int64_t* counts, uint6
     hipStream_t st = s->stream;
     const int nc = rp.L.ncells;
     std::vector<int64_t> off(nc + 1, 0);
-    Buf d = dev_alloc(sizeof(unsigned long long) * (nc + 1), st);
+    Buf d = dev_alloc(sizeof(unsigned long long) * (nc + 1), s);
     HIP_CHECK(hipMemsetAsync(P<void>(d), 0, sizeof(unsigned long long) * (nc + 1), st));
     if (rp.rows > 0) {
         hipLaunchKernelGGL(k_cell_digest, dim3(nc), dim3(256), 0, st, P<uint2>(rp.pairs), P<int64_t>(rp.boff), rp.L,

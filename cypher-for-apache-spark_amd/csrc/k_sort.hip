@@ -87,16 +87,16 @@ void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t
     if (n <= 1 || shifts.empty()) return;
     hipStream_t st = s->stream;
     const int64_t ntiles = (n + kTile - 1) / kTile;
-    Buf hist = dev_alloc(sizeof(int64_t) * 256 * ntiles, st);
-    Buf offs = dev_alloc(sizeof(int64_t) * (256 * ntiles + 1), st);
-    Buf k2 = dev_alloc(sizeof(uint64_t) * n, st);
-    Buf v2 = vals ? dev_alloc(sizeof(int64_t) * n, st) : Buf();
+    Buf hist = dev_alloc(sizeof(int64_t) * 256 * ntiles, s);
+    Buf offs = dev_alloc(sizeof(int64_t) * (256 * ntiles + 1), s);
+    Buf k2 = dev_alloc(sizeof(uint64_t) * n, s);
+    Buf v2 = vals ? dev_alloc(sizeof(int64_t) * n, s) : Buf();
     uint64_t *ki = keys, *ko = P<uint64_t>(k2);
     int64_t *vi = vals, *vo = P<int64_t>(v2);
     int passes = 0;
     for (const int shift : shifts) {
         hipLaunchKernelGGL(k_hist, dim3((unsigned)ntiles), dim3(kBlock), 0, st, ki, n, shift, ntiles, P<int64_t>(hist));
-        exclusive_scan_i64(P<int64_t>(hist), P<int64_t>(offs), 256 * ntiles, st);
+        exclusive_scan_i64(P<int64_t>(hist), P<int64_t>(offs), 256 * ntiles, s);
         hipLaunchKernelGGL(k_scatter, dim3((unsigned)ntiles), dim3(kBlock), 0, st, ki, vi, n, shift, ntiles,
                            P<int64_t>(offs), ko, vo);
         HIP_CHECK(hipGetLastError());

@@ -503,7 +503,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     int64_t m = 0;
     for (int i = 0; i < nt; ++i) m += ms[i];
     const int bits = bits_for((uint64_t)n);
-    Buf key = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), st);
+    Buf key = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s);
     {
         KernelTimer kt(s, "tri_pack");
         int64_t off = 0;
@@ -523,7 +523,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     if (kd.back() < 56) kd.push_back(56);
     radix_sort_digits(s, P<uint64_t>(key), nullptr, m, kd);
     // directed runs
-    Buf f = dev_alloc(m > 0 ? m : 1, st), heads;
+    Buf f = dev_alloc(m > 0 ? m : 1, s), heads;
     hipLaunchKernelGGL(k_heads, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, P<uint8_t>(f));
     const int64_t nruns = flags_to_indices(s, P<uint8_t>(f), m, heads);
     int64_t nvalid = 0;
@@ -539,15 +539,15 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         }
         nvalid = a;
     }
-    g.sl = dev_alloc(sizeof(uint32_t) * n, st);
+    g.sl = dev_alloc(sizeof(uint32_t) * n, s);
     HIP_CHECK(hipMemsetAsync(P<void>(g.sl), 0, sizeof(uint32_t) * n, st));
-    Buf uk = dev_alloc(sizeof(uint64_t) * (nruns > 0 ? nruns : 1), st), uv = dev_alloc(sizeof(int64_t) * (nruns > 0 ? nruns : 1), st);
+    Buf uk = dev_alloc(sizeof(uint64_t) * (nruns > 0 ? nruns : 1), s), uv = dev_alloc(sizeof(int64_t) * (nruns > 0 ? nruns : 1), s);
     if (nruns > 0)
         hipLaunchKernelGGL(k_dir_runs, dim3(grid(s, nruns)), dim3(256), 0, st, P<uint64_t>(key), P<int64_t>(heads),
                            nruns, nvalid, P<uint32_t>(g.sl), P<uint64_t>(uk), P<int64_t>(uv));
     key.reset();
     radix_sort_digits(s, P<uint64_t>(uk), P<int64_t>(uv), nruns, kd);
-    Buf f2 = dev_alloc(nruns > 0 ? nruns : 1, st), heads2;
+    Buf f2 = dev_alloc(nruns > 0 ? nruns : 1, s), heads2;
     hipLaunchKernelGGL(k_heads, dim3(grid(s, nruns)), dim3(256), 0, st, P<uint64_t>(uk), nruns, P<uint8_t>(f2));
     const int64_t ne = flags_to_indices(s, P<uint8_t>(f2), nruns, heads2);
     int64_t nuvalid = 0;
@@ -563,25 +563,25 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         nuvalid = a;
     }
     g.ne = ne;
-    g.ek = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), st);
-    g.ev = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), st);
-    Buf deg = dev_alloc(sizeof(uint32_t) * n, st);
+    g.ek = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), s);
+    g.ev = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);
+    Buf deg = dev_alloc(sizeof(uint32_t) * n, s);
     HIP_CHECK(hipMemsetAsync(P<void>(deg), 0, sizeof(uint32_t) * n, st));
     if (ne > 0)
         hipLaunchKernelGGL(k_und_runs, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(uk), P<int64_t>(uv),
                            P<int64_t>(heads2), ne, nuvalid, P<uint64_t>(g.ek), P<int64_t>(g.ev), P<uint32_t>(deg));
-    g.ok = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), st);
-    g.ov = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), st);
+    g.ok = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), s);
+    g.ov = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);
     if (ne > 0)
         hipLaunchKernelGGL(k_orient, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ek), P<int64_t>(g.ev), ne,
                            P<uint32_t>(deg), P<uint64_t>(g.ok), P<int64_t>(g.ov));
     radix_sort_digits(s, P<uint64_t>(g.ok), P<int64_t>(g.ov), ne, od);  // no kNone among the oriented keys
-    g.off = dev_alloc(sizeof(int64_t) * (n + 1), st);
+    g.off = dev_alloc(sizeof(int64_t) * (n + 1), s);
     hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, n, P<int64_t>(g.off));
-    g.tg = dev_alloc(sizeof(uint32_t) * (ne > 0 ? ne : 1), st);
+    g.tg = dev_alloc(sizeof(uint32_t) * (ne > 0 ? ne : 1), s);
     if (ne > 0)
         hipLaunchKernelGGL(k_targets, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, P<uint32_t>(g.tg));
-    Buf fsm = dev_alloc(n, st), fbg = dev_alloc(n, st);
+    Buf fsm = dev_alloc(n, s), fbg = dev_alloc(n, s);
     hipLaunchKernelGGL(k_tri_bins, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), n, P<uint8_t>(fsm),
                        P<uint8_t>(fbg));
     g.nsmall = flags_to_indices(s, P<uint8_t>(fsm), n, g.small_u);
@@ -593,7 +593,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
 uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
     using namespace tri;
     hipStream_t st = s->stream;
-    Buf out = dev_alloc(24, st);
+    Buf out = dev_alloc(24, s);
     HIP_CHECK(hipMemsetAsync(P<void>(out), 0, 24, st));
     {
         KernelTimer kt(s, "triangles");
@@ -602,16 +602,16 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
         if (be > bb) {
             const int64_t nb = be - bb;
             const int64_t* bu = P<int64_t>(g.big_u) + bb;
-            Buf ib = dev_alloc(sizeof(int64_t) * (2 * nb + 2), st);
+            Buf ib = dev_alloc(sizeof(int64_t) * (2 * nb + 2), s);
             int64_t* items = P<int64_t>(ib);
             int64_t* ipre = items + nb;
             hipLaunchKernelGGL(k_tri_items, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, P<int64_t>(g.off), bu,
                                nb, items);
-            exclusive_scan_i64(items, ipre, nb, st);
+            exclusive_scan_i64(items, ipre, nb, s);
             const int64_t nitems = read_scalar(s, ipre + nb);
-            Buf iq = dev_alloc(sizeof(uint32_t) * (nitems > 0 ? nitems : 1), st);
+            Buf iq = dev_alloc(sizeof(uint32_t) * (nitems > 0 ? nitems : 1), s);
             hipLaunchKernelGGL(k_tri_item_map, dim3(grid(s, nb)), dim3(256), 0, st, ipre, nb, P<uint32_t>(iq));
-            Buf ctr = dev_alloc(sizeof(unsigned long long), st);
+            Buf ctr = dev_alloc(sizeof(unsigned long long), s);
             HIP_CHECK(hipMemsetAsync(P<void>(ctr), 0, sizeof(unsigned long long), st));
             const size_t lds = sizeof(ItemLds);
             HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_tri_big_items),

@@ -511,8 +511,8 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
     Dom d{P<uint32_t>(a_ok->words), P<uint32_t>(b_ok->words), b_ok->lo, b_ok->hi, a_ok->full ? 1 : 0,
           b_ok->full ? 1 : 0};
     const size_t nb = sizeof(uint64_t) * (n > 0 ? n : 1);
-    Buf od = dev_alloc(nb, st), sl = dev_alloc(nb, st), W = dev_alloc(nb, st), T2 = dev_alloc(nb, st),
-        T3 = dev_alloc(nb, st);
+    Buf od = dev_alloc(nb, s), sl = dev_alloc(nb, s), W = dev_alloc(nb, s), T2 = dev_alloc(nb, s),
+        T3 = dev_alloc(nb, s);
     for (Buf* b : {&od, &sl, &W, &T2, &T3}) HIP_CHECK(hipMemsetAsync(P<void>(*b), 0, nb, st));
     const bool need3 = upper >= 3;
     int64_t mtot = 0;
@@ -555,10 +555,10 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
             while ((int64_t(1) << rshift) < (int64_t(8) * per_slice >> sublog) && rshift < 20) ++rshift;
             const int64_t nreg = (int64_t)L.nt << sublog;
             const size_t rbytes = (size_t(1) << rshift) / 8;
-            bw = dev_alloc(rbytes * nreg, st);
+            bw = dev_alloc(rbytes * nreg, s);
             bl = RegionBloom{P<uint32_t>(bw), (unsigned long long)((int64_t(1) << rshift) - 1), rshift, sublog};
             {
-                Buf part = dev_alloc(rbytes * (((size_t)ct.g2 + L.nt) << sublog), st);
+                Buf part = dev_alloc(rbytes * (((size_t)ct.g2 + L.nt) << sublog), s);
                 const ChunkWalk tw{P<uint2>(ct.pool), P<unsigned long long>(ct.meta), ct.order, ct.jst, ct.segbase,
                                    ct.ja, L.nt};
                 HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_vl_bset),
@@ -567,15 +567,15 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
                 hipLaunchKernelGGL(k_vl_bmerge, dim3(grid(s, (int64_t)(rbytes / 16) * nreg)), dim3(256), 0, st, ct.jst,
                                    L.nt, ct.g2, P<uint4>(part), bl);
             }
-            cand = dev_alloc(sizeof(int64_t), st);
+            cand = dev_alloc(sizeof(int64_t), s);
             HIP_CHECK(hipMemsetAsync(P<void>(cand), 0, sizeof(int64_t), st));
         }
         {
             KernelTimer kt(s, "varlen_deg");
             Buf f2part;
             if (need3) {
-                f2 = dev_alloc(sizeof(uint32_t) * kF2Words * (size_t)L.nt, st);
-                f2part = dev_alloc(sizeof(uint32_t) * kF2Words * ((size_t)cp.g2 + L.nt), st);
+                f2 = dev_alloc(sizeof(uint32_t) * kF2Words * (size_t)L.nt, s);
+                f2part = dev_alloc(sizeof(uint32_t) * kF2Words * ((size_t)cp.g2 + L.nt), s);
             }
             hipLaunchKernelGGL(k_vl_deg, dim3(g), dim3(kVlBlock), lds2, st, cw, d.b, d.b_full, n, P<unsigned long long>(od),
                                P<unsigned long long>(sl), bl, P<uint4>(f2part), P<unsigned long long>(cand));
@@ -597,13 +597,13 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
                         (long long)nc, L.nt << bl.sublog, bl.rshift);
             int64_t cap = 1024;
             while (cap < 2 * nc) cap <<= 1;
-            hk = dev_alloc(sizeof(unsigned long long) * cap, st);
-            hc = dev_alloc(sizeof(unsigned int) * (cap + 1), st);
+            hk = dev_alloc(sizeof(unsigned long long) * cap, s);
+            hc = dev_alloc(sizeof(unsigned int) * (cap + 1), s);
             HIP_CHECK(hipMemsetAsync(P<void>(hk), 0, sizeof(unsigned long long) * cap, st));
             HIP_CHECK(hipMemsetAsync(P<void>(hc), 0, sizeof(unsigned int) * (cap + 1), st));
             h = PairHash{P<unsigned long long>(hk), P<unsigned int>(hc), P<unsigned int>(hc) + cap,
                          (unsigned long long)(cap - 1)};
-            ody = dev_alloc(2 * nb, st);
+            ody = dev_alloc(2 * nb, s);
             hipLaunchKernelGGL(k_vl_y, dim3(grid(s, n)), dim3(256), 0, st, n, d.b, d.b_full, P<unsigned long long>(od),
                                P<unsigned long long>(W), P<unsigned long long>(sl), P<longlong2>(ody));
         }
@@ -639,7 +639,7 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
     Buf rev, counts;
     HashTable ht;
     if (need3 && mtot > 0) {
-        Buf cs = dev_alloc(sizeof(int64_t) * mtot, st), cd = dev_alloc(sizeof(int64_t) * mtot, st);
+        Buf cs = dev_alloc(sizeof(int64_t) * mtot, s), cd = dev_alloc(sizeof(int64_t) * mtot, s);
         int64_t off = 0;
         for (int i = 0; i < nt; ++i) {
             if (ms[i] <= 0) continue;
@@ -673,15 +673,15 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
         }
     }
     }  // atomic passes
-    Buf cnt = dev_alloc(nb, st), flags = dev_alloc(n > 0 ? n : 1, st);
+    Buf cnt = dev_alloc(nb, s), flags = dev_alloc(n > 0 ? n : 1, s);
     hipLaunchKernelGGL(k_final, dim3(grid(s, n)), dim3(256), 0, st, n, d, lower, upper, P<unsigned long long>(od),
                        P<unsigned long long>(sl), P<unsigned long long>(T2), P<unsigned long long>(T3),
                        P<int64_t>(cnt), P<uint8_t>(flags));
     HIP_CHECK(hipGetLastError());
     Buf idx;
     const int64_t rows = flags_to_indices(s, P<uint8_t>(flags), n, idx);
-    out_ids = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), st);
-    out_cnt = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), st);
+    out_ids = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), s);
+    out_cnt = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), s);
     // ids = lo + idx; counts = cnt[idx]
     gather_col(P<int64_t>(cnt), nullptr, P<int64_t>(idx), rows, P<int64_t>(out_cnt), nullptr, st);
     if (rows > 0) {
@@ -739,10 +739,10 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
     v->od = od;
     const size_t nb = sizeof(uint64_t) * n;
     HIP_CHECK(hipMemsetAsync(od, 0, nb, st));
-    v->sl = dev_alloc(nb, st);
-    v->W = dev_alloc(nb, st);
-    v->T2 = dev_alloc(nb, st);
-    v->T3 = dev_alloc(nb, st);
+    v->sl = dev_alloc(nb, s);
+    v->W = dev_alloc(nb, s);
+    v->T2 = dev_alloc(nb, s);
+    v->T3 = dev_alloc(nb, s);
     for (Buf* b : {&v->sl, &v->W, &v->T2, &v->T3}) HIP_CHECK(hipMemsetAsync(P<void>(*b), 0, nb, st));
     Layout& L = v->L;
     L.lo = v->d.lo;
@@ -788,10 +788,10 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
         int rshift = 10;
         while ((int64_t(1) << rshift) < int64_t(8) * per_slice && rshift < 20) ++rshift;
         const size_t rbytes = (size_t(1) << rshift) / 8;
-        v->bw = dev_alloc(rbytes * L.nt, st);
+        v->bw = dev_alloc(rbytes * L.nt, s);
         const RegionBloom bl{P<uint32_t>(v->bw), (unsigned long long)((int64_t(1) << rshift) - 1), rshift, 0};
         {
-            Buf part = dev_alloc(rbytes * ((size_t)ct.g2 + L.nt), st);
+            Buf part = dev_alloc(rbytes * ((size_t)ct.g2 + L.nt), s);
             const ChunkWalk tw{P<uint2>(ct.pool), P<unsigned long long>(ct.meta), ct.order, ct.jst, ct.segbase, ct.ja,
                                L.nt};
             HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_vl_bset),
@@ -802,11 +802,11 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
         }
         chunk_partition(s, as.data(), ad.data(), am.data(), na, true, L, s->num_cus, ca);
         const ChunkWalk aw{P<uint2>(ca.pool), P<unsigned long long>(ca.meta), ca.order, ca.jst, ca.segbase, ca.ja, L.nt};
-        v->f2 = dev_alloc(sizeof(uint32_t) * kF2Words * (size_t)L.nt, st);
-        Buf cand = dev_alloc(sizeof(int64_t), st);
+        v->f2 = dev_alloc(sizeof(uint32_t) * kF2Words * (size_t)L.nt, s);
+        Buf cand = dev_alloc(sizeof(int64_t), s);
         HIP_CHECK(hipMemsetAsync(P<void>(cand), 0, sizeof(int64_t), st));
         {
-            Buf f2part = dev_alloc(sizeof(uint32_t) * kF2Words * ((size_t)ca.g2 + L.nt), st);
+            Buf f2part = dev_alloc(sizeof(uint32_t) * kF2Words * ((size_t)ca.g2 + L.nt), s);
             hipLaunchKernelGGL(k_vl_deg, dim3((unsigned)ca.g2), dim3(kVlBlock), lds2, st, aw, v->d.b, v->d.b_full, n,
                                nullptr, nullptr, bl, P<uint4>(f2part), P<unsigned long long>(cand));
             const RegionBloom f2b{P<uint32_t>(v->f2), 0, 19, 0};
@@ -816,8 +816,8 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
         const int64_t nc = read_scalar(s, P<int64_t>(cand));
         int64_t cap = 1024;
         while (cap < 2 * nc) cap <<= 1;
-        v->hk = dev_alloc(sizeof(unsigned long long) * cap, st);
-        v->hc = dev_alloc(sizeof(unsigned int) * (cap + 1), st);
+        v->hk = dev_alloc(sizeof(unsigned long long) * cap, s);
+        v->hc = dev_alloc(sizeof(unsigned int) * (cap + 1), s);
         HIP_CHECK(hipMemsetAsync(P<void>(v->hk), 0, sizeof(unsigned long long) * cap, st));
         HIP_CHECK(hipMemsetAsync(P<void>(v->hc), 0, sizeof(unsigned int) * (cap + 1), st));
         const PairHash h{P<unsigned long long>(v->hk), P<unsigned int>(v->hc), P<unsigned int>(v->hc) + cap,
@@ -856,7 +856,7 @@ int64_t varlen_shard_finish(VarlenShard* v, Buf& out_ids, Buf& out_cnt) {
     const int64_t n = v->n;
     if (v->need3) {
         REQUIRE(v->y != nullptr, CAPSMI_ERR_ILLEGAL_ARGUMENT, "varlen shard: mid() before finish()");
-        v->ody = dev_alloc(2 * sizeof(int64_t) * n, st);
+        v->ody = dev_alloc(2 * sizeof(int64_t) * n, s);
         hipLaunchKernelGGL(k_vl_pack, dim3(grid(s, n)), dim3(256), 0, st, n, reinterpret_cast<const long long*>(v->od),
                            reinterpret_cast<const long long*>(v->y), P<longlong2>(v->ody));
     }
@@ -870,7 +870,7 @@ int64_t varlen_shard_finish(VarlenShard* v, Buf& out_ids, Buf& out_cnt) {
                            P<unsigned long long>(v->T3), RegionBloom{nullptr, 0, 0, 0}, nullptr,
                            PairHash{nullptr, nullptr, nullptr, 0});
     }
-    Buf cnt = dev_alloc(sizeof(int64_t) * n, st), flags = dev_alloc(n, st);
+    Buf cnt = dev_alloc(sizeof(int64_t) * n, s), flags = dev_alloc(n, s);
     hipLaunchKernelGGL(k_final, dim3(grid(s, n)), dim3(256), 0, st, n, v->d, v->lower, v->upper,
                        reinterpret_cast<const unsigned long long*>(v->od), P<unsigned long long>(v->sl),
                        P<unsigned long long>(v->T2), P<unsigned long long>(v->T3), P<int64_t>(cnt), P<uint8_t>(flags));
@@ -879,8 +879,8 @@ int64_t varlen_shard_finish(VarlenShard* v, Buf& out_ids, Buf& out_cnt) {
     HIP_CHECK(hipGetLastError());
     Buf idx;
     const int64_t rows = flags_to_indices(s, P<uint8_t>(flags), n, idx);
-    out_ids = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), st);
-    out_cnt = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), st);
+    out_ids = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), s);
+    out_cnt = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), s);
     gather_col(P<int64_t>(cnt), nullptr, P<int64_t>(idx), rows, P<int64_t>(out_cnt), nullptr, st);
     if (rows > 0) {
         HIP_CHECK(hipMemcpyAsync(P<void>(out_ids), P<void>(idx), sizeof(int64_t) * rows, hipMemcpyDeviceToDevice, st));

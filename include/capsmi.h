@@ -150,7 +150,9 @@ const char* capsmi_version(void);
 /* CAPSSession.local()/create (spark-cypher/.../api/CAPSSession.scala:110-131): one device, one stream */
 capsmi_status capsmi_session_create(int32_t device, capsmi_session** out);
 capsmi_status capsmi_session_destroy(capsmi_session* s);
-/* run subsequent work on an external hipStream_t (e.g. torch's current stream); NULL = session stream */
+/* run subsequent work on an external hipStream_t (e.g. torch's current stream); NULL = session stream.
+ * The previous stream is drained first (the session's cached device blocks then move with it); an
+ * external stream must outlive the session or the next switch away from it. */
 capsmi_status capsmi_session_set_stream(capsmi_session* s, void* hip_stream);
 /* run subsequent work on exactly `hip_stream`; NULL = the HIP null (legacy default) stream -- what
  * torch's default stream is, so kernels and torch work stay ordered */

@@ -50,6 +50,17 @@ def load():
         lib.orc_var_length_count.restype = ctypes.c_int
         lib.orc_var_length_count.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, U8P, U8P, ctypes.c_int,
                                              ctypes.c_int, I64P, I64P, ctypes.c_int]
+        # closed.c
+        lib.orc_c2_masks.restype = None
+        lib.orc_c2_masks.argtypes = [ctypes.c_int64, ctypes.c_uint64, U8P, U8P]
+        lib.orc_two_hop_closed_form_mt.restype = ctypes.c_int
+        lib.orc_two_hop_closed_form_mt.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, U8P, U8P, U8P, I64P,
+                                                   I64P, ctypes.c_int]
+        lib.orc_var_length_closed_form.restype = ctypes.c_int
+        lib.orc_var_length_closed_form.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, U8P, U8P, ctypes.c_int,
+                                                   ctypes.c_int, I64P, I64P, ctypes.c_int]
+        lib.orc_triangle_closed_form.restype = ctypes.c_int
+        lib.orc_triangle_closed_form.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, U8P, I64P, ctypes.c_int]
         _lib = lib
     return _lib
 
@@ -152,3 +163,37 @@ def var_length_count(n, src, dst, lo, hi, a_ok=None, b_ok=None, threads=0):
     if rc:
         raise ValueError(f"orc_var_length_count rc={rc}")
     return rows.value, g
+
+
+def c2_masks(n: int, seed: int = 42):
+    """(person, adult) uint8 masks of the C2 node tables (closed.c orc_c2_masks)."""
+    person = np.empty(n, dtype=np.uint8)
+    adult = np.empty(n, dtype=np.uint8)
+    load().orc_c2_masks(n, seed, _p8(person), _p8(adult))
+    return person, adult
+
+
+def two_hop_closed_form_mt(n, src, dst, a_ok=None, b_ok=None, c_ok=None, threads=0):
+    rows, dist = ctypes.c_int64(), ctypes.c_int64()
+    if load().orc_two_hop_closed_form_mt(n, len(src), _p64(src), _p64(dst), _p8(a_ok), _p8(b_ok), _p8(c_ok),
+                                         ctypes.byref(rows), ctypes.byref(dist), threads):
+        raise MemoryError("orc_two_hop_closed_form_mt")
+    return rows.value, dist.value
+
+
+def var_length_closed_form(n, src, dst, lo, hi, a_ok=None, b_ok=None, threads=0):
+    rows = ctypes.c_int64()
+    g = np.zeros(n, dtype=np.int64)
+    rc = load().orc_var_length_closed_form(n, len(src), _p64(src), _p64(dst), _p8(a_ok), _p8(b_ok), lo, hi, _p64(g),
+                                           ctypes.byref(rows), threads)
+    if rc:
+        raise ValueError(f"orc_var_length_closed_form rc={rc}")
+    return rows.value, g
+
+
+def triangle_closed_form(n, src, dst, n_ok=None, threads=0):
+    rows = ctypes.c_int64()
+    rc = load().orc_triangle_closed_form(n, len(src), _p64(src), _p64(dst), _p8(n_ok), ctypes.byref(rows), threads)
+    if rc:
+        raise ValueError(f"orc_triangle_closed_form rc={rc}")
+    return rows.value

@@ -10,7 +10,9 @@ def _tables(session, rng, n, null_frac=0.2, key_range=20):
     from capsmi import ColumnData
     from capsmi.expr import BOOL, F64, I64, STR
     from oracle.relational import NumpyBackend
-    session.dictionary.extend([f"s{i:03d}" for i in range(50)])
+    strings = [f"s{i:03d}" for i in range(50)]
+    session.dictionary.extend(strings)
+    codes = np.array([session.dictionary.encode(x) for x in strings], dtype=np.int64)
 
     def col(name, ty):
         if ty == F64:
@@ -18,7 +20,7 @@ def _tables(session, rng, n, null_frac=0.2, key_range=20):
         elif ty == BOOL:
             v = rng.integers(0, 2, n)
         elif ty == STR:
-            v = rng.integers(0, 50, n) * 2  # even codes = dictionary strings
+            v = codes[rng.integers(0, 50, n)]  # dictionary strings
         else:
             v = rng.integers(-key_range, key_range, n)
         valid = rng.random(n) >= null_frac
@@ -162,3 +164,22 @@ def test_wide_distinct_and_group(session, ncols):
     _same(g.distinct(*keys).select(*keys), o.distinct(*keys).select(*keys))
     aggs = [("count_star", None, False, "n"), ("sum", "c0", False, "s")]
     _same(g.group(keys, aggs), o.group(keys, aggs))
+
+
+@pytest.mark.parametrize("jt", ["inner", "left_outer", "full_outer"])
+def test_join_long_with_double_keys(session, jt):
+    """ValueJoin on Int = Float (ADVICE r1): Spark casts the Long key to Double, so 1 matches 1.0;
+    -0.0 and 0.0 stay distinct keys as in Spark 2.2.1."""
+    from capsmi import ColumnData
+    from capsmi.expr import F64, I64
+    from oracle.relational import NumpyBackend
+    rng = np.random.default_rng(29)
+    li = rng.integers(-5, 6, 400)
+    rf = np.concatenate([rng.integers(-5, 6, 300).astype(np.float64), [0.5, -0.0, 0.0, 2.0, 1e300]])
+    lcols = [ColumnData("l", I64, li, rng.random(400) >= 0.1), ColumnData("x", I64, np.arange(400))]
+    rcols = [ColumnData("r", F64, rf, rng.random(len(rf)) >= 0.1), ColumnData("y", I64, np.arange(len(rf)))]
+    nb = NumpyBackend(session.dictionary)
+    g = session.table(lcols).join(session.table(rcols), jt, ("l", "r"))
+    o = nb.table(lcols).join(nb.table(rcols), jt, ("l", "r"))
+    _same(g, o)
+    assert g.size > 0

@@ -128,7 +128,7 @@ def _rows(backend, table, header):
 def test_union_all_scans(backend):
     """ScanGraphTest "executes union": graph2's ids move to tag 1; labels and properties aligned."""
     p1, p2 = _pg(PERSONS, KNOWS), _pg(PROGRAMMERS + BOOKS, READS)
-    backend.dictionary.extend(p1.strings() + p2.strings())  # order-preserving codes: one extend
+    # graphs loaded one after the other: graph 2's strings interleave graph 1's (stable codes)
     g1 = ScanGraph.from_property_graph(backend, p1)
     g2 = ScanGraph.from_property_graph(backend, p2)
     u = UnionGraph.union_all(backend, g1, g2)
