@@ -147,6 +147,12 @@ _SIGS = {
     "capsmi_owner_words": (c_int32, [c_int64, c_int32, c_int32, POINTER(c_int64), POINTER(c_int64)]),
     "capsmi_rmat_nodes": (c_int32, [P, c_int32, c_int32, c_uint64, PP]),
     "capsmi_table_fingerprint": (c_int32, [P, c_int32, STRS, POINTER(c_int64), POINTER(c_uint64), POINTER(c_uint64)]),
+    "capsmi_node_table": (c_int32, [P, c_char_p, c_int32, STRS, PP]),
+    "capsmi_rel_table": (c_int32, [P, c_char_p, c_char_p, c_char_p, c_int32, STRS, PP]),
+    "capsmi_table_entity": (c_int32, [P, POINTER(c_int32), POINTER(c_int64), POINTER(c_int64)]),
+    "capsmi_flatten_rel_types": (c_int32, [P, c_char_p, c_int32, POINTER(c_int64), STRS, PP]),
+    "capsmi_session_set_fused": (c_int32, [P, c_int32]),
+    "capsmi_session_route_count": (c_int32, [P, c_char_p, POINTER(c_int64)]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -105,6 +105,8 @@ def fs_graph(backend, graph_dir: str, extra_strings=()) -> ScanGraph:
     for kind, labels, props, keys, cols in parsed:
         ids = [ID] if kind == "node" else [ID, SRC, DST]
         data = [_column(c, I64, cols[c], enc) for c in ids] + [_column(k, props[k], cols[k], enc) for k in keys]
-        et = EntityTable(kind, labels, dict(props), backend.table(data))
+        t = backend.table(data)
+        t = t.as_node_table(ID) if kind == "node" else t.as_rel_table(ID, SRC, DST)
+        et = EntityTable(kind, labels, dict(props), t)
         (nodes if kind == "node" else rels).append(et)
     return ScanGraph(backend, nodes, rels)

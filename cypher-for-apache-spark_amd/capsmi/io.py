@@ -45,7 +45,7 @@ def edge_list_tables(session: Session, src: np.ndarray, dst: np.ndarray) -> Tupl
     s = rels.select("source").withColumnRenamed("source", "id")
     t = rels.select("target").withColumnRenamed("target", "id")
     nodes = s.unionAll(t).distinct()
-    return nodes, rels
+    return nodes.as_node_table("id"), rels.as_rel_table("id", "source", "target")
 
 
 def edge_list_graph(session: Session, path: str, delimiter: str = " ") -> Tuple[GpuTable, GpuTable]:

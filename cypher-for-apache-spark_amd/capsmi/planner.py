@@ -157,7 +157,7 @@ class ScanGraph:
             cols = [_column(ID, I64, [n.id for n in ns], enc)]
             for k in sorted(pt):
                 cols.append(_column(k, pt[k], [n.props.get(k) for n in ns], enc))
-            nodes.append(EntityTable("node", labels, pt, backend.table(cols)))
+            nodes.append(EntityTable("node", labels, pt, backend.table(cols).as_node_table(ID)))
         types: Dict[str, List[PGRel]] = {}
         for r in pg.rels:
             types.setdefault(r.type, []).append(r)
@@ -169,7 +169,7 @@ class ScanGraph:
                     _column(DST, I64, [r.dst for r in rs], enc)]
             for k in sorted(pt):
                 cols.append(_column(k, pt[k], [r.props.get(k) for r in rs], enc))
-            rels.append(EntityTable("rel", frozenset([t]), pt, backend.table(cols)))
+            rels.append(EntityTable("rel", frozenset([t]), pt, backend.table(cols).as_rel_table(ID, SRC, DST)))
         return ScanGraph(backend, nodes, rels)
 
     # ---- scans --------------------------------------------------------------------------

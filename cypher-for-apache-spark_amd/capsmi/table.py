@@ -154,6 +154,18 @@ class Session:
     def encode_str(self, s: str) -> int:
         return self.dictionary.encode(s)
 
+    def set_fused(self, enabled: bool) -> None:
+        """Route lazy plans of the Expand shapes to the fused kernels (default) or run them operator
+        by operator (include/capsmi.h capsmi_session_set_fused)."""
+        _lib.call("capsmi_session_set_fused", self._h, 1 if enabled else 0)
+
+    def route_count(self, name: str) -> int:
+        """Plans routed to fused entry point `name` ("expand", "expand_count", "two_hop", "triangle",
+        "var_length") so far."""
+        v = ctypes.c_int64()
+        _lib.call("capsmi_session_route_count", self._h, name.encode(), ctypes.byref(v))
+        return v.value
+
 
 class GpuTable:
     """A device-resident, immutable table; each operator returns a new GpuTable."""
@@ -161,6 +173,7 @@ class GpuTable:
     def __init__(self, session: Session, handle: ctypes.c_void_p):
         self.session = session
         self._h = handle
+        self._schema = None  # (names, types): tables are immutable, so the schema is read once
 
     # ---- lifetime ------------------------------------------------------------------------
     @property
@@ -190,25 +203,58 @@ class GpuTable:
         _lib.call("capsmi_table_size", self._h, ctypes.byref(v))
         return v.value
 
+    def _read_schema(self):
+        if self._schema is None:
+            n = ctypes.c_int32()
+            _lib.call("capsmi_table_num_columns", self._h, ctypes.byref(n))
+            buf = ctypes.create_string_buffer(1024)
+            t = ctypes.c_int32()
+            names, types = [], []
+            for i in range(n.value):
+                _lib.call("capsmi_table_column_name", self._h, i, buf, 1024)
+                _lib.call("capsmi_table_column_type", self._h, i, ctypes.byref(t))
+                names.append(buf.value.decode())
+                types.append(t.value)
+            self._schema = (names, types)
+        return self._schema
+
     @property
     def physicalColumns(self) -> List[str]:
-        n = ctypes.c_int32()
-        _lib.call("capsmi_table_num_columns", self._h, ctypes.byref(n))
-        buf = ctypes.create_string_buffer(1024)
-        out = []
-        for i in range(n.value):
-            _lib.call("capsmi_table_column_name", self._h, i, buf, 1024)
-            out.append(buf.value.decode())
-        return out
+        return list(self._read_schema()[0])
 
     @property
     def columnType(self) -> dict:
-        out = {}
-        t = ctypes.c_int32()
-        for i, name in enumerate(self.physicalColumns):
-            _lib.call("capsmi_table_column_type", self._h, i, ctypes.byref(t))
-            out[name] = t.value
-        return out
+        names, types = self._read_schema()
+        return dict(zip(names, types))
+
+    # ---- entity tables (include/capsmi.h capsmi_node_table / capsmi_rel_table) -----------------
+    def as_node_table(self, id_col: str, label_cols: Sequence[str] = ()) -> "GpuTable":
+        """CAPSNodeTable + EntityTable.verify (EntityTable.scala:59-65, 105-131)."""
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_node_table", self._h, id_col.encode(), len(label_cols), _lib.strs(label_cols),
+                  ctypes.byref(out))
+        return self._wrap(out)
+
+    def as_rel_table(self, id_col: str, src_col: str, dst_col: str, type_cols: Sequence[str] = ()) -> "GpuTable":
+        """CAPSRelationshipTable + EntityTable.verify (EntityTable.scala:59-65, 137-164)."""
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_rel_table", self._h, id_col.encode(), src_col.encode(), dst_col.encode(), len(type_cols),
+                  _lib.strs(type_cols), ctypes.byref(out))
+        return self._wrap(out)
+
+    def entity(self) -> Tuple[int, int, int]:
+        """(kind: 0 plain / 1 node / 2 relationship, id_lo, id_hi)"""
+        k, lo, hi = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64()
+        _lib.call("capsmi_table_entity", self._h, ctypes.byref(k), ctypes.byref(lo), ctypes.byref(hi))
+        return k.value, lo.value, hi.value
+
+    def flatten_rel_types(self, type_col: str, types: Sequence[str], out_cols: Sequence[str]) -> "GpuTable":
+        """CAPSRelationshipTable.fromMapping's String type column -> Boolean flags (CAPSTable.scala:189-204)."""
+        codes = (ctypes.c_int64 * max(1, len(types)))(*[self.session.encode_str(t) for t in types])
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_flatten_rel_types", self._h, type_col.encode(), len(types), codes, _lib.strs(out_cols),
+                  ctypes.byref(out))
+        return self._wrap(out)
 
     def column_index(self, name: str) -> int:
         v = ctypes.c_int32()

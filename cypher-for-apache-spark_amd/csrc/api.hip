@@ -39,6 +39,9 @@ void fingerprint(capsmi_session* s, int ncols, const int64_t* const* d, const ui
 
 static thread_local std::string g_err;
 
+void set_last_error(const std::string& m) { g_err = m; }
+std::string last_error_string() { return g_err; }
+
 [[noreturn]] void throw_hip(hipError_t e, const char* what, const char* file, int line) {
     const std::string msg = std::string("HIP error ") + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ") at " +
                             file + ":" + std::to_string(line) + ": " + what;
@@ -547,13 +550,27 @@ static capsmi_status table_from(capsmi_session* s, int32_t ncols, const capsmi_c
         need(cols[i].name, "column name");
         REQUIRE(seen.insert(cols[i].name).second, CAPSMI_ERR_ILLEGAL_ARGUMENT,
                 std::string("duplicate column '") + cols[i].name + "'");
-        REQUIRE(cols[i].type >= CAPSMI_I64 && cols[i].type <= CAPSMI_STR, CAPSMI_ERR_ILLEGAL_ARGUMENT, "bad column type");
+        const int32_t ty = cols[i].type;
+        const bool narrow = ty >= CAPSMI_IN_I32 && ty <= CAPSMI_IN_BOOL8;
+        REQUIRE((ty >= CAPSMI_I64 && ty <= CAPSMI_STR) || narrow, CAPSMI_ERR_ILLEGAL_ARGUMENT, "bad column type");
         REQUIRE(nrows == 0 || cols[i].data, CAPSMI_ERR_ILLEGAL_ARGUMENT, "null column data");
         Column c;
         c.name = cols[i].name;
-        c.type = cols[i].type;
+        c.type = ty;
         c.data = dev_alloc(sizeof(int64_t) * (nrows > 0 ? nrows : 1), s);
-        if (nrows) HIP_CHECK(hipMemcpyAsync(P<void>(c.data), cols[i].data, sizeof(int64_t) * nrows, kind, s->stream));
+        if (narrow) {
+            // Byte/Short/Integer -> Long, Float -> Double (DataFrameOps.withCypherCompatibleTypes)
+            const size_t w = ty == CAPSMI_IN_I32 || ty == CAPSMI_IN_F32 ? 4 : (ty == CAPSMI_IN_I16 ? 2 : 1);
+            c.type = ty == CAPSMI_IN_F32 ? CAPSMI_F64 : (ty == CAPSMI_IN_BOOL8 ? CAPSMI_BOOL : CAPSMI_I64);
+            if (nrows) {
+                Buf raw = dev_alloc(w * nrows, s);
+                HIP_CHECK(hipMemcpyAsync(P<void>(raw), cols[i].data, w * nrows, kind, s->stream));
+                widen_words(P<void>(raw), ty, P<int64_t>(c.data), nrows, s->stream);
+                if (kind == hipMemcpyHostToDevice) HIP_CHECK(hipStreamSynchronize(s->stream));
+            }
+        } else if (nrows) {
+            HIP_CHECK(hipMemcpyAsync(P<void>(c.data), cols[i].data, sizeof(int64_t) * nrows, kind, s->stream));
+        }
         if (cols[i].valid) {
             c.valid = dev_alloc(nrows > 0 ? nrows : 1, s);
             if (nrows) HIP_CHECK(hipMemcpyAsync(P<void>(c.valid), cols[i].valid, nrows, kind, s->stream));
@@ -596,6 +613,7 @@ capsmi_status capsmi_table_size(const capsmi_table* t, int64_t* out) {
     API_BEGIN
     need(t, "table");
     need(out, "out");
+    M(t);
     *out = t->nrows;
     API_END
 }
@@ -649,6 +667,7 @@ capsmi_status capsmi_table_export(const capsmi_table* t, int32_t col, void* host
                                   int64_t offset, int64_t n) {
     API_BEGIN
     need(t, "table");
+    M(t);
     REQUIRE(col >= 0 && col < (int)t->cols.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT, "column index out of range");
     REQUIRE(offset >= 0 && n >= 0 && offset + n <= t->nrows, CAPSMI_ERR_ILLEGAL_ARGUMENT, "export range out of bounds");
     use_device(t->sess);
@@ -668,24 +687,21 @@ capsmi_status capsmi_table_column_device_ptr(const capsmi_table* t, int32_t col,
                                              const uint8_t** valid) {
     API_BEGIN
     need(t, "table");
+    M(t);
     REQUIRE(col >= 0 && col < (int)t->cols.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT, "column index out of range");
     if (data) *data = t->cols[col].d();
     if (valid) *valid = t->cols[col].v();
     API_END
 }
 
-// ---- Table[T] operators ---------------------------------------------------------------------
-capsmi_status capsmi_cache(capsmi_table* t, capsmi_table** out) {
-    // device tables are already materialised (DataFrameTable.cache, SparkTable.scala:240-246)
-    API_BEGIN
-    need(t, "table");
-    need(out, "out");
-    t->refs.fetch_add(1);
-    *out = t;
-    API_END
-}
+}  // extern "C"
 
-capsmi_status capsmi_select(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out) {
+// Eager Table[T] operators over materialised inputs.  The public entry points (plan.hip) build lazy
+// plan nodes; materialisation runs these (or a fused kernel the recogniser picked).
+namespace capsmi {
+
+// ---- Table[T] operators ---------------------------------------------------------------------
+capsmi_status eager_select(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out) {
     API_BEGIN
     need(t, "table");
     need(out, "out");
@@ -696,7 +712,7 @@ capsmi_status capsmi_select(capsmi_table* t, int32_t ncols, const char* const* c
     API_END
 }
 
-capsmi_status capsmi_drop(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out) {
+capsmi_status eager_drop(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out) {
     API_BEGIN
     need(t, "table");
     need(out, "out");
@@ -709,7 +725,7 @@ capsmi_status capsmi_drop(capsmi_table* t, int32_t ncols, const char* const* col
     API_END
 }
 
-capsmi_status capsmi_with_column_renamed(capsmi_table* t, const char* old_name, const char* new_name,
+capsmi_status eager_with_column_renamed(capsmi_table* t, const char* old_name, const char* new_name,
                                          capsmi_table** out) {
     API_BEGIN
     need(t, "table");
@@ -725,7 +741,7 @@ capsmi_status capsmi_with_column_renamed(capsmi_table* t, const char* old_name, 
     API_END
 }
 
-capsmi_status capsmi_filter(capsmi_table* t, int32_t nnodes, const capsmi_expr* prog, capsmi_table** out) {
+capsmi_status eager_filter(capsmi_table* t, int32_t nnodes, const capsmi_expr* prog, capsmi_table** out) {
     API_BEGIN
     need(t, "table");
     need(out, "out");
@@ -742,7 +758,7 @@ capsmi_status capsmi_filter(capsmi_table* t, int32_t nnodes, const capsmi_expr* 
     API_END
 }
 
-capsmi_status capsmi_with_columns(capsmi_table* t, int32_t ncols, const capsmi_expr_column* cols, capsmi_table** out) {
+capsmi_status eager_with_columns(capsmi_table* t, int32_t ncols, const capsmi_expr_column* cols, capsmi_table** out) {
     API_BEGIN
     need(t, "table");
     need(out, "out");
@@ -765,7 +781,7 @@ capsmi_status capsmi_with_columns(capsmi_table* t, int32_t ncols, const capsmi_e
     API_END
 }
 
-capsmi_status capsmi_join(capsmi_table* l, capsmi_table* r, int32_t join_type, int32_t npairs,
+capsmi_status eager_join(capsmi_table* l, capsmi_table* r, int32_t join_type, int32_t npairs,
                           const char* const* lcols, const char* const* rcols, capsmi_table** out) {
     API_BEGIN
     need(l, "left");
@@ -781,7 +797,7 @@ capsmi_status capsmi_join(capsmi_table* l, capsmi_table* r, int32_t join_type, i
     API_END
 }
 
-capsmi_status capsmi_union_all(capsmi_table* a, capsmi_table* b, capsmi_table** out) {
+capsmi_status eager_union_all(capsmi_table* a, capsmi_table* b, capsmi_table** out) {
     API_BEGIN
     need(a, "left");
     need(b, "right");
@@ -819,7 +835,7 @@ capsmi_status capsmi_union_all(capsmi_table* a, capsmi_table* b, capsmi_table** 
     API_END
 }
 
-capsmi_status capsmi_order_by(capsmi_table* t, int32_t nkeys, const char* const* cols, const int32_t* descending,
+capsmi_status eager_order_by(capsmi_table* t, int32_t nkeys, const char* const* cols, const int32_t* descending,
                               capsmi_table** out) {
     API_BEGIN
     need(t, "table");
@@ -835,7 +851,7 @@ capsmi_status capsmi_order_by(capsmi_table* t, int32_t nkeys, const char* const*
     API_END
 }
 
-capsmi_status capsmi_skip(capsmi_table* t, int64_t n, capsmi_table** out) {
+capsmi_status eager_skip(capsmi_table* t, int64_t n, capsmi_table** out) {
     API_BEGIN
     need(t, "table");
     need(out, "out");
@@ -848,7 +864,7 @@ capsmi_status capsmi_skip(capsmi_table* t, int64_t n, capsmi_table** out) {
     API_END
 }
 
-capsmi_status capsmi_limit(capsmi_table* t, int64_t n, capsmi_table** out) {
+capsmi_status eager_limit(capsmi_table* t, int64_t n, capsmi_table** out) {
     API_BEGIN
     need(t, "table");
     need(out, "out");
@@ -875,14 +891,14 @@ static capsmi_status distinct_impl(capsmi_table* t, const std::vector<int>& keys
     API_END
 }
 
-capsmi_status capsmi_distinct(capsmi_table* t, capsmi_table** out) {
+capsmi_status eager_distinct(capsmi_table* t, capsmi_table** out) {
     if (!t || !out) { set_err("null argument"); return CAPSMI_ERR_ILLEGAL_ARGUMENT; }
     std::vector<int> keys;
     for (size_t i = 0; i < t->cols.size(); ++i) keys.push_back((int)i);
     return distinct_impl(t, keys, out);
 }
 
-capsmi_status capsmi_distinct_on(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out) {
+capsmi_status eager_distinct_on(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out) {
     API_BEGIN
     need(t, "table");
     need(out, "out");
@@ -892,7 +908,7 @@ capsmi_status capsmi_distinct_on(capsmi_table* t, int32_t ncols, const char* con
     API_END
 }
 
-capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, int32_t naggs, const capsmi_agg* aggs,
+capsmi_status eager_group(capsmi_table* t, int32_t nby, const char* const* by, int32_t naggs, const capsmi_agg* aggs,
                            capsmi_table** out) {
     API_BEGIN
     need(t, "table");
@@ -1012,6 +1028,10 @@ capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, 
     API_END
 }
 
+}  // namespace capsmi
+
+extern "C" {
+
 // ---- graph fast path ------------------------------------------------------------------------------
 capsmi_status capsmi_bitmap_create(capsmi_session* s, int64_t id_lo, int64_t id_hi, capsmi_bitmap** out) {
     API_BEGIN
@@ -1038,6 +1058,7 @@ capsmi_status capsmi_bitmap_add_scan(capsmi_bitmap* b, capsmi_table* nodes, cons
     API_BEGIN
     need(b, "bitmap");
     need(nodes, "nodes");
+    M(nodes);
     capsmi_session* s = b->sess;
     use_device(s);
     const Column& idc = nodes->cols[col_index(nodes, id_col)];
@@ -1088,6 +1109,7 @@ capsmi_status capsmi_expand_filter(capsmi_session* s, capsmi_table* rels, const 
     API_BEGIN
     need(s, "session");
     need(rels, "rels");
+    M(rels);
     need(out, "out");
     check_bitmap(src_ok, "src_ok");
     check_bitmap(dst_ok, "dst_ok");
@@ -1138,6 +1160,7 @@ static void build_part(capsmi_session* s, int32_t nrels, capsmi_table* const* re
     std::vector<int64_t> ms;
     for (int i = 0; i < nrels; ++i) {
         need(rels[i], "rels[i]");
+        M(rels[i]);
         srcs.push_back(rel_col(rels[i], src_col).d());
         dsts.push_back(rel_col(rels[i], dst_col).d());
         ms.push_back(rels[i]->nrows);
@@ -1178,6 +1201,7 @@ static void two_hop_mid(capsmi_session* s, int32_t nrels, capsmi_table* const* r
     HIP_CHECK(hipMemsetAsync(S1, 0, sizeof(uint32_t) * nw, s->stream));
     for (int i = 0; i < nrels; ++i) {
         need(rels[i], "rels[i]");
+        M(rels[i]);
         const Column& sc = rel_col(rels[i], src_col);
         const Column& dc = rel_col(rels[i], dst_col);
         graph::hop1(s, sc.d(), dc.d(), rels[i]->nrows, a, b, X1, S1, X2);
@@ -1190,6 +1214,7 @@ static void two_hop_dst(capsmi_session* s, int32_t nrels, capsmi_table* const* r
                         const uint32_t* X2, uint32_t* C) {
     HIP_CHECK(hipMemsetAsync(C, 0, sizeof(uint32_t) * c->nwords, s->stream));
     for (int i = 0; i < nrels; ++i) {
+        M(rels[i]);
         const Column& sc = rel_col(rels[i], src_col);
         const Column& dc = rel_col(rels[i], dst_col);
         graph::hop2(s, sc.d(), dc.d(), rels[i]->nrows, c, X1, X2, b->lo, b->hi, C);
@@ -1295,6 +1320,7 @@ capsmi_status capsmi_var_length_count(capsmi_session* s, int32_t nrels, capsmi_t
     std::vector<int64_t> ms;
     for (int i = 0; i < nrels; ++i) {
         need(rels[i], "rels[i]");
+        M(rels[i]);
         srcs.push_back(rel_col(rels[i], src_col).d());
         dsts.push_back(rel_col(rels[i], dst_col).d());
         ms.push_back(rels[i]->nrows);
@@ -1345,12 +1371,14 @@ capsmi_status capsmi_varlen_shard_begin(capsmi_session* s, int32_t nout, capsmi_
     std::vector<int64_t> ms, ims;
     for (int i = 0; i < nout; ++i) {
         need(out_rels[i], "out_rels[i]");
+        M(out_rels[i]);
         srcs.push_back(rel_col(out_rels[i], src_col).d());
         dsts.push_back(rel_col(out_rels[i], dst_col).d());
         ms.push_back(out_rels[i]->nrows);
     }
     for (int i = 0; i < nin; ++i) {
         need(in_rels[i], "in_rels[i]");
+        M(in_rels[i]);
         isrcs.push_back(rel_col(in_rels[i], src_col).d());
         idsts.push_back(rel_col(in_rels[i], dst_col).d());
         ims.push_back(in_rels[i]->nrows);
@@ -1417,6 +1445,7 @@ static void rel_cols(int32_t nrels, capsmi_table* const* rels, const char* src_c
                      std::vector<const int64_t*>& srcs, std::vector<const int64_t*>& dsts, std::vector<int64_t>& ms) {
     for (int i = 0; i < nrels; ++i) {
         need(rels[i], "rels[i]");
+        M(rels[i]);
         srcs.push_back(rel_col(rels[i], src_col).d());
         dsts.push_back(rel_col(rels[i], dst_col).d());
         ms.push_back(rels[i]->nrows);
@@ -1636,6 +1665,8 @@ capsmi_status capsmi_two_hop_count(capsmi_session* s, int32_t nrels, capsmi_tabl
     HIP_CHECK(hipMemsetAsync(P<void>(outC), 0, sizeof(uint32_t) * (n > 0 ? n : 1), s->stream));
     HIP_CHECK(hipMemsetAsync(P<void>(acc), 0, 16, s->stream));
     for (int i = 0; i < nrels; ++i) {
+        need(rels[i], "rels[i]");
+        M(rels[i]);
         const Column& sc = rel_col(rels[i], src_col);
         const Column& dc = rel_col(rels[i], dst_col);
         graph::degrees(s, sc.d(), dc.d(), rels[i]->nrows, a_ok, b_ok, c_ok, P<uint32_t>(inA), P<uint32_t>(outC),
@@ -1653,6 +1684,7 @@ capsmi_status capsmi_cluster_by(capsmi_table* rels, const char* key_col, int64_t
                                 capsmi_table** out) {
     API_BEGIN
     need(rels, "rels");
+    M(rels);
     need(out, "out");
     capsmi_session* s = rels->sess;
     use_device(s);
@@ -1730,6 +1762,7 @@ capsmi_status capsmi_rmat_rels(capsmi_session* s, int32_t scale, int64_t e_begin
         c.data = bufs[i];
         o->cols.push_back(std::move(c));
     }
+    attach_entity(o, 2, 0, int64_t(1) << scale);  // [id, source, target]: a registered relationship table
     *out = o;
     API_END
 }
@@ -1766,6 +1799,7 @@ capsmi_status capsmi_rmat_nodes(capsmi_session* s, int32_t scale, int32_t kind, 
         graph::ages(s, P<int64_t>(ids), rows, seed, P<int64_t>(a.data));
         o->cols.push_back(std::move(a));
     }
+    attach_entity(o, 1, 0, n);  // [id] / [id, age]: a registered node table
     *out = o;
     API_END
 }
@@ -1774,6 +1808,7 @@ capsmi_status capsmi_table_fingerprint(capsmi_table* t, int32_t ncols, const cha
                                        uint64_t* sum, uint64_t* xr) {
     API_BEGIN
     need(t, "table");
+    M(t);
     use_device(t->sess);
     auto idx = names_to_idx(t, ncols, cols);
     std::vector<const int64_t*> d;

@@ -62,9 +62,21 @@ struct Column {
     Buf data;              // int64 words
     Buf valid;             // uint8 per row, may be null (no nulls)
     int64_t offset = 0;    // row offset into data/valid (zero-copy skip)
+    bool lazy_nullable = false;  // schema of a lazy table's column (no data yet): may hold nulls
     const int64_t* d() const { return P<int64_t>(data) + offset; }
     const uint8_t* v() const { return valid ? P<uint8_t>(valid) + offset : nullptr; }
+    bool nullable() const { return valid != nullptr || lazy_nullable; }
 };
+
+// Entity-table contract of a registered node / relationship table (capsmi_node_table /
+// capsmi_rel_table; EntityTable.verify, okapi-relational/.../api/io/EntityTable.scala:59-65,155-164).
+struct EntityInfo {
+    int kind = 0;                 // 1 node, 2 relationship
+    int id = -1, src = -1, dst = -1;  // column indices of the key columns
+    int64_t lo = 0, hi = 0;       // [min, max + 1) of the ids (node) or of both endpoints (relationship)
+    int64_t rows = 0;
+};
+struct PlanNode;  // lazy Table[T] operator (plan.hip)
 
 }  // namespace capsmi
 
@@ -84,6 +96,9 @@ struct capsmi_session {
     };
     std::vector<Pending> pending;
     std::map<std::string, std::pair<int64_t, double>> totals;
+    // fused-path routing of lazy plans (plan.hip): enabled flag and per-route counters
+    bool fused = true;
+    std::map<std::string, int64_t> routes;
 };
 
 namespace capsmi {
@@ -108,8 +123,11 @@ struct KernelTimer {
 struct capsmi_table {
     std::atomic<int> refs{1};
     capsmi_session* sess = nullptr;
-    int64_t nrows = 0;
-    std::vector<capsmi::Column> cols;
+    int64_t nrows = 0;               // valid once materialised (plan == null)
+    std::vector<capsmi::Column> cols;  // lazy: the schema only (name, type, lazy_nullable)
+    std::shared_ptr<capsmi::PlanNode> plan;            // non-null until materialised (plan.hip)
+    std::shared_ptr<const capsmi::EntityInfo> entity;  // registered entity table
+    bool lazy() const { return (bool)plan; }
     int find(const std::string& n) const {
         for (size_t i = 0; i < cols.size(); ++i)
             if (cols[i].name == n) return (int)i;
@@ -266,6 +284,43 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
 void varlen_shard_mid(VarlenShard* v, int64_t* y);
 int64_t varlen_shard_finish(VarlenShard* v, Buf& out_ids, Buf& out_cnt);
 void varlen_shard_free(VarlenShard* v);
+
+// [min, max] over `ncols` int64 columns of n rows into out[0], out[1] (synchronises); n > 0
+void minmax_i64(capsmi_session* s, const int64_t* const* cols, int ncols, int64_t n, int64_t* out);
+// widen n input values of width `code` (CAPSMI_IN_* of include/capsmi.h) to 8-byte words
+void widen_words(const void* in, int code, int64_t* out, int64_t n, hipStream_t st);
+
+// expressions: static result type and validation of a postfix program over a table's schema (k_expr.hip)
+int32_t infer_type(const capsmi_table* t, int32_t nn, const capsmi_expr* prog);
+void validate_program(const capsmi_table* t, int32_t nn, const capsmi_expr* prog);
+
+// lazy plans (plan.hip): run the plan (a fused kernel when the recogniser matches) and keep the result
+void materialize(capsmi_table* t);
+// mark a materialised table in canonical entity layout (ids first) as a node (1) / relationship (2)
+// table whose ids (endpoints) lie in [lo, hi)
+void attach_entity(capsmi_table* t, int kind, int64_t lo, int64_t hi);
+inline capsmi_table* M(const capsmi_table* t) {
+    materialize(const_cast<capsmi_table*>(t));
+    return const_cast<capsmi_table*>(t);
+}
+
+// eager Table[T] operators over materialised inputs (api.hip)
+capsmi_status eager_select(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out);
+capsmi_status eager_drop(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out);
+capsmi_status eager_with_column_renamed(capsmi_table* t, const char* old_name, const char* new_name, capsmi_table** out);
+capsmi_status eager_filter(capsmi_table* t, int32_t nnodes, const capsmi_expr* prog, capsmi_table** out);
+capsmi_status eager_with_columns(capsmi_table* t, int32_t ncols, const capsmi_expr_column* cols, capsmi_table** out);
+capsmi_status eager_join(capsmi_table* l, capsmi_table* r, int32_t join_type, int32_t npairs, const char* const* lcols,
+                         const char* const* rcols, capsmi_table** out);
+capsmi_status eager_union_all(capsmi_table* a, capsmi_table* b, capsmi_table** out);
+capsmi_status eager_order_by(capsmi_table* t, int32_t nkeys, const char* const* cols, const int32_t* descending,
+                             capsmi_table** out);
+capsmi_status eager_skip(capsmi_table* t, int64_t n, capsmi_table** out);
+capsmi_status eager_limit(capsmi_table* t, int64_t n, capsmi_table** out);
+capsmi_status eager_distinct(capsmi_table* t, capsmi_table** out);
+capsmi_status eager_distinct_on(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out);
+capsmi_status eager_group(capsmi_table* t, int32_t nby, const char* const* by, int32_t naggs, const capsmi_agg* aggs,
+                          capsmi_table** out);
 
 // graph (k_graph.hip)
 void bitmap_add_rows(capsmi_bitmap* b, const int64_t* ids, const uint8_t* ids_valid,

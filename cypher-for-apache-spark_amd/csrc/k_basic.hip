@@ -2,6 +2,8 @@
 // Table operator uses (filter = predicate + compaction + gather; join/group =
 // hash + scan + gather).  Wave64 throughout: __ballot is 64-bit and the
 // per-wave scans run over 64 lanes.
+#include <climits>
+
 #include "capsmi_impl.h"
 
 namespace capsmi {
@@ -241,6 +243,74 @@ void invert_u8(const uint8_t* a, uint8_t* b, int64_t n, hipStream_t st) {
     hipLaunchKernelGGL(k_invert_u8, dim3(grid_for(n)), dim3(256), 0, st, a, b, n);
     HIP_CHECK(hipGetLastError());
 }
+namespace {
+
+// block min/max over up to 3 columns, one atomic pair per block
+__global__ void k_minmax(const int64_t* __restrict__ c0, const int64_t* __restrict__ c1, const int64_t* __restrict__ c2,
+                         int64_t n, long long* out) {
+    long long lo = LLONG_MAX, hi = LLONG_MIN;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const long long a = c0[i];
+        lo = min(lo, a);
+        hi = max(hi, a);
+        if (c1) { const long long b = c1[i]; lo = min(lo, b); hi = max(hi, b); }
+        if (c2) { const long long c = c2[i]; lo = min(lo, c); hi = max(hi, c); }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, (long long)__shfl_xor(lo, o));
+        hi = max(hi, (long long)__shfl_xor(hi, o));
+    }
+    __shared__ long long slo[4], shi[4];
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { slo[w] = lo; shi[w] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < (int)(blockDim.x >> 6); ++k) { lo = min(lo, slo[k]); hi = max(hi, shi[k]); }
+        atomicMin(&out[0], lo);
+        atomicMax(&out[1], hi);
+    }
+}
+
+// DataFrameOps.withCypherCompatibleTypes (spark-cypher/.../impl/DataFrameOps.scala:185-198):
+// Byte/Short/Integer -> Long, Float -> Double; Boolean bytes -> 0/1 words
+__global__ void k_widen(const void* __restrict__ in, int code, int64_t* __restrict__ out, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t v;
+        switch (code) {
+            case CAPSMI_IN_I32: v = ((const int32_t*)in)[i]; break;
+            case CAPSMI_IN_I16: v = ((const int16_t*)in)[i]; break;
+            case CAPSMI_IN_I8: v = ((const int8_t*)in)[i]; break;
+            case CAPSMI_IN_F32: v = __double_as_longlong((double)((const float*)in)[i]); break;
+            default: v = ((const uint8_t*)in)[i] != 0; break;  // CAPSMI_IN_BOOL8
+        }
+        out[i] = v;
+    }
+}
+
+}  // namespace
+
+void minmax_i64(capsmi_session* s, const int64_t* const* cols, int ncols, int64_t n, int64_t* out) {
+    Buf d = dev_alloc(2 * sizeof(long long), s);
+    const long long init[2] = {LLONG_MAX, LLONG_MIN};
+    HIP_CHECK(hipMemcpyAsync(P<void>(d), init, sizeof(init), hipMemcpyHostToDevice, s->stream));
+    if (n > 0) {
+        hipLaunchKernelGGL(k_minmax, dim3(grid_for(n)), dim3(256), 0, s->stream, cols[0], ncols > 1 ? cols[1] : nullptr,
+                           ncols > 2 ? cols[2] : nullptr, n, P<long long>(d));
+        HIP_CHECK(hipGetLastError());
+    }
+    long long h[2];
+    HIP_CHECK(hipMemcpyAsync(h, P<void>(d), sizeof(h), hipMemcpyDeviceToHost, s->stream));
+    HIP_CHECK(hipStreamSynchronize(s->stream));
+    out[0] = h[0];
+    out[1] = h[1];
+}
+
+void widen_words(const void* in, int code, int64_t* out, int64_t n, hipStream_t st) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_widen, dim3(grid_for(n)), dim3(256), 0, st, in, code, out, n);
+    HIP_CHECK(hipGetLastError());
+}
+
 void i64_to_f64(const int64_t* a, int64_t* b, int64_t n, hipStream_t st) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_i64_to_f64, dim3(grid_for(n)), dim3(256), 0, st, a, b, n);

@@ -187,6 +187,8 @@ __global__ void k_eval(const capsmi_expr* __restrict__ prog, int nn, ColPtrs cp,
     }
 }
 
+}  // namespace
+
 // static type of a program (host): literal / column types propagate, comparisons -> BOOL
 int32_t infer_type(const capsmi_table* t, int32_t nn, const capsmi_expr* prog) {
     std::vector<int> st;
@@ -263,6 +265,8 @@ void validate_program(const capsmi_table* t, int32_t nn, const capsmi_expr* prog
     REQUIRE(nn == 0 || depth == 1, CAPSMI_ERR_ILLEGAL_ARGUMENT, "expression program must leave one value");
     REQUIRE(maxd <= kMaxStack, CAPSMI_ERR_NOT_IMPLEMENTED, "expression too deep");
 }
+
+namespace {
 
 void launch_eval(capsmi_session* s, const capsmi_table* t, int32_t nn, const capsmi_expr* prog, int64_t* out,
                  uint8_t* out_valid, uint8_t* flags) {

@@ -1,0 +1,1497 @@
+// plan.hip -- lazy Table[T] plans, materialisation and the fused-path recogniser.
+//
+// CAPS's backend sees a MATCH only as the Table[T] calls RelationalPlanner emits
+// (okapi-relational/.../planning/RelationalPlanner.scala:113-177): an Expand is
+//   join(nodeScan, relScan, (src.id, r.source)) then join(.., nodeScan, (r.target, dst.id)),
+// an ExpandInto a 2-key join, a BoundedVarLengthExpand a union of unrolled join chains with
+// isomorphism filters (VarLengthExpandPlanner.scala:46-310), followed by Filter (uniqueness
+// NOT(r_i = r_j), node predicates) and Aggregate (RelationalOperator.scala:293-351).  DataFrameTable
+// builds a lazy Spark plan from those calls and runs it at the first action (SparkTable.scala:59).
+// libcapsmi does the same: every Table operator returns a lazy table (schema known, rows not yet
+// computed); materialisation first matches the plan against the shapes the fused kernels compute
+//   Expand + node filters, projected ........................ capsmi_expand_filter     ("expand")
+//   Expand + node filters, count(*) ......................... expand count              ("expand_count")
+//   2 x Expand + uniqueness, count(*) / count(DISTINCT end) . two-hop kernels           ("two_hop")
+//   2 x Expand + ExpandInto closing a cycle, count(*) ....... triangle count            ("triangle")
+//   var-length 1 <= l <= u <= 3, grouped count(*) by start .. var-length count          ("var_length")
+// over registered entity tables (capsmi_node_table / capsmi_rel_table), and otherwise runs the
+// operators one by one (api.hip eager_*).  Node predicates become node-scan bitmaps; ids must be
+// unique per scan and inside one window of at most 2^30 ids, else the plan runs unfused.
+#include <algorithm>
+#include <cstring>
+#include <functional>
+#include <set>
+
+#include "capsmi_impl.h"
+
+namespace capsmi {
+
+void set_last_error(const std::string& m);
+std::string last_error_string();
+
+struct AggSpec {
+    int32_t kind = 0, distinct = 0;
+    std::string input, output;
+};
+
+struct PlanNode {
+    enum Kind { SELECT, DROP, RENAME, FILTER, WITH_COLUMNS, JOIN, UNION, DISTINCT, DISTINCT_ON, GROUP, ORDER, SKIP, LIMIT };
+    Kind kind = SELECT;
+    std::vector<capsmi_table*> in;            // retained inputs
+    std::vector<std::string> a, b;            // column names (see builders)
+    std::vector<std::vector<capsmi_expr>> progs;
+    std::vector<int32_t> flags;               // ORDER: descending
+    std::vector<AggSpec> aggs;
+    int32_t jt = 0;
+    int64_t n = 0;
+    ~PlanNode() {
+        for (capsmi_table* t : in) capsmi_table_release(t);
+    }
+};
+
+namespace {
+
+#define P_BEGIN try {
+#define P_END                                                   \
+    }                                                           \
+    catch (const capsmi::Error& e) {                            \
+        set_last_error(e.what());                               \
+        return e.code;                                          \
+    }                                                           \
+    catch (const std::bad_alloc&) {                             \
+        set_last_error("host allocation failed");               \
+        return CAPSMI_ERR_OUT_OF_MEMORY;                        \
+    }                                                           \
+    catch (const std::exception& e) {                           \
+        set_last_error(e.what());                               \
+        return CAPSMI_ERR_INTERNAL;                             \
+    }                                                           \
+    return CAPSMI_OK;
+
+void need(const void* p, const char* what) {
+    REQUIRE(p != nullptr, CAPSMI_ERR_ILLEGAL_ARGUMENT, std::string("null argument: ") + what);
+}
+
+void check(capsmi_status st) {
+    if (st != CAPSMI_OK) throw Error(st, last_error_string());
+}
+
+int find_col(const capsmi_table* t, const std::string& name) {
+    for (size_t i = 0; i < t->cols.size(); ++i)
+        if (t->cols[i].name == name) return (int)i;
+    return -1;
+}
+
+int col_of(const capsmi_table* t, const char* name) {
+    need(name, "column name");
+    const int i = find_col(t, name);
+    REQUIRE(i >= 0, CAPSMI_ERR_ILLEGAL_ARGUMENT, std::string("no column named '") + name + "'");
+    return i;
+}
+
+Column schema_col(const std::string& name, int32_t type, bool nullable) {
+    Column c;
+    c.name = name;
+    c.type = type;
+    c.lazy_nullable = nullable;
+    return c;
+}
+
+Column schema_of(const Column& c) { return schema_col(c.name, c.type, c.nullable()); }
+
+// an input of a plan node: retained here, released by ~PlanNode (also when the builder throws)
+void hold(PlanNode& p, capsmi_table* t) {
+    t->refs.fetch_add(1);
+    p.in.push_back(t);
+}
+
+// a lazy table over node `p` (inputs already held)
+capsmi_table* lazy_table(capsmi_session* s, std::shared_ptr<PlanNode> p, std::vector<Column> schema) {
+    auto* t = new capsmi_table();
+    t->sess = s;
+    t->nrows = -1;
+    t->cols = std::move(schema);
+    t->plan = std::move(p);
+    return t;
+}
+
+std::vector<const char*> cstrs(const std::vector<std::string>& v) {
+    std::vector<const char*> o;
+    for (auto& x : v) o.push_back(x.c_str());
+    return o;
+}
+
+int arity(const capsmi_expr& x) {
+    switch (x.op) {
+        case CAPSMI_X_COL: case CAPSMI_X_LIT: case CAPSMI_X_NULL: return 0;
+        case CAPSMI_X_NOT: case CAPSMI_X_ISNULL: case CAPSMI_X_ISNOTNULL: case CAPSMI_X_NEG: return 1;
+        case CAPSMI_X_AND: case CAPSMI_X_OR: case CAPSMI_X_COALESCE: return x.arg;
+        case CAPSMI_X_IN: return x.arg + 1;
+        case CAPSMI_X_CASE: return 2 * x.arg + 1;
+        default: return 2;
+    }
+}
+
+// ============================ operator-by-operator execution ===============================
+capsmi_table* exec_node(const PlanNode& p) {
+    capsmi_table* r = nullptr;
+    capsmi_table* x = p.in.empty() ? nullptr : p.in[0];
+    switch (p.kind) {
+        case PlanNode::SELECT: { auto c = cstrs(p.a); check(eager_select(x, (int)c.size(), c.data(), &r)); break; }
+        case PlanNode::DROP: { auto c = cstrs(p.a); check(eager_drop(x, (int)c.size(), c.data(), &r)); break; }
+        case PlanNode::RENAME: check(eager_with_column_renamed(x, p.a[0].c_str(), p.b[0].c_str(), &r)); break;
+        case PlanNode::FILTER: check(eager_filter(x, (int)p.progs[0].size(), p.progs[0].data(), &r)); break;
+        case PlanNode::WITH_COLUMNS: {
+            std::vector<capsmi_expr_column> cols(p.a.size());
+            for (size_t i = 0; i < p.a.size(); ++i) {
+                cols[i].name = p.a[i].c_str();
+                cols[i].nnodes = (int32_t)p.progs[i].size();
+                cols[i].prog = p.progs[i].data();
+            }
+            check(eager_with_columns(x, (int)cols.size(), cols.data(), &r));
+            break;
+        }
+        case PlanNode::JOIN: {
+            auto l = cstrs(p.a), rr = cstrs(p.b);
+            check(eager_join(x, p.in[1], p.jt, (int)l.size(), l.data(), rr.data(), &r));
+            break;
+        }
+        case PlanNode::UNION: check(eager_union_all(x, p.in[1], &r)); break;
+        case PlanNode::DISTINCT: check(eager_distinct(x, &r)); break;
+        case PlanNode::DISTINCT_ON: { auto c = cstrs(p.a); check(eager_distinct_on(x, (int)c.size(), c.data(), &r)); break; }
+        case PlanNode::GROUP: {
+            auto by = cstrs(p.a);
+            std::vector<capsmi_agg> ag(p.aggs.size());
+            for (size_t i = 0; i < p.aggs.size(); ++i) {
+                ag[i].kind = p.aggs[i].kind;
+                ag[i].distinct = p.aggs[i].distinct;
+                ag[i].input = p.aggs[i].input.empty() ? nullptr : p.aggs[i].input.c_str();
+                ag[i].output = p.aggs[i].output.c_str();
+            }
+            check(eager_group(x, (int)by.size(), by.data(), (int)ag.size(), ag.data(), &r));
+            break;
+        }
+        case PlanNode::ORDER: { auto c = cstrs(p.a); check(eager_order_by(x, (int)c.size(), c.data(), p.flags.data(), &r)); break; }
+        case PlanNode::SKIP: check(eager_skip(x, p.n, &r)); break;
+        case PlanNode::LIMIT: check(eager_limit(x, p.n, &r)); break;
+    }
+    return r;
+}
+
+// move a materialised result into the lazy table `t` (names from t's schema)
+void adopt(capsmi_table* t, capsmi_table* r) {
+    std::unique_ptr<capsmi_table> g(r);
+    REQUIRE(r->cols.size() == t->cols.size(), CAPSMI_ERR_INTERNAL, "materialised schema differs from the plan's");
+    for (size_t i = 0; i < r->cols.size(); ++i) r->cols[i].name = t->cols[i].name;
+    t->cols = std::move(r->cols);
+    t->nrows = r->nrows;
+}
+
+// ================================ the recogniser ===========================================
+enum { ROLE_NONE = 0, ROLE_ID = 1, ROLE_SRC = 2, ROLE_DST = 3 };
+
+// A scan: union of registered entity tables, each column a base column or a per-table constant
+// (ScanGraph.scanOperator's aligned entity tables, ScanGraph.scala:61-96).
+struct Member {
+    capsmi_table* base = nullptr;
+    std::vector<int> src;            // per scan column: base column, or -1 (constant)
+    std::vector<capsmi_expr> cst;    // the constant as a one-node program (LIT / NULL)
+};
+struct Scan {
+    int kind = 0;  // 1 node, 2 relationship
+    std::vector<Member> m;
+    std::vector<int> role;  // per scan column: ROLE_* in every member, else ROLE_NONE
+};
+
+void scan_roles(Scan& sc, size_t ncols) {
+    sc.role.assign(ncols, ROLE_NONE);
+    for (size_t k = 0; k < ncols; ++k) {
+        for (int r : {ROLE_ID, ROLE_SRC, ROLE_DST}) {
+            bool all = !sc.m.empty();
+            for (const Member& m : sc.m) {
+                const EntityInfo& e = *m.base->entity;
+                const int want = r == ROLE_ID ? e.id : (r == ROLE_SRC ? e.src : e.dst);
+                if (want < 0 || m.src[k] != want) { all = false; break; }
+            }
+            if (all) { sc.role[k] = r; break; }
+        }
+    }
+}
+
+bool as_scan(const capsmi_table* t, Scan& sc) {
+    if (!t->lazy()) {
+        if (!t->entity) return false;
+        sc = Scan();
+        sc.kind = t->entity->kind;
+        Member m;
+        m.base = const_cast<capsmi_table*>(t);
+        for (size_t k = 0; k < t->cols.size(); ++k) m.src.push_back((int)k);
+        m.cst.resize(t->cols.size());
+        sc.m.push_back(std::move(m));
+        scan_roles(sc, t->cols.size());
+        return true;
+    }
+    const PlanNode& p = *t->plan;
+    const capsmi_table* in = p.in.empty() ? nullptr : p.in[0];
+    switch (p.kind) {
+        case PlanNode::WITH_COLUMNS: {
+            if (!as_scan(in, sc)) return false;
+            std::vector<std::string> names;
+            for (auto& c : in->cols) names.push_back(c.name);
+            const std::vector<Member> before = sc.m;  // expressions read the input columns
+            for (size_t i = 0; i < p.a.size(); ++i) {
+                if (p.progs[i].size() != 1) return false;
+                const capsmi_expr& x = p.progs[i][0];
+                if (x.op != CAPSMI_X_COL && x.op != CAPSMI_X_LIT && x.op != CAPSMI_X_NULL) return false;
+                int j = -1;
+                for (size_t q = 0; q < names.size(); ++q) if (names[q] == p.a[i]) j = (int)q;
+                if (j < 0) {
+                    j = (int)names.size();
+                    names.push_back(p.a[i]);
+                    for (Member& m : sc.m) { m.src.push_back(-1); m.cst.push_back(capsmi_expr{}); }
+                }
+                for (size_t q = 0; q < sc.m.size(); ++q) {
+                    Member& m = sc.m[q];
+                    if (x.op == CAPSMI_X_COL) {
+                        m.src[j] = before[q].src[x.arg];
+                        m.cst[j] = before[q].cst[x.arg];
+                    } else {
+                        m.src[j] = -1;
+                        m.cst[j] = x;
+                    }
+                }
+            }
+            break;
+        }
+        case PlanNode::SELECT:
+        case PlanNode::DROP:
+        case PlanNode::RENAME: {
+            if (!as_scan(in, sc)) return false;
+            std::vector<int> pick;
+            if (p.kind == PlanNode::SELECT) {
+                for (auto& nm : p.a) pick.push_back(find_col(in, nm));
+            } else if (p.kind == PlanNode::DROP) {
+                std::set<std::string> d(p.a.begin(), p.a.end());
+                for (size_t k = 0; k < in->cols.size(); ++k) if (!d.count(in->cols[k].name)) pick.push_back((int)k);
+            } else {
+                for (size_t k = 0; k < in->cols.size(); ++k) pick.push_back((int)k);
+            }
+            for (Member& m : sc.m) {
+                Member o;
+                o.base = m.base;
+                for (int k : pick) { o.src.push_back(m.src[k]); o.cst.push_back(m.cst[k]); }
+                m = std::move(o);
+            }
+            break;
+        }
+        case PlanNode::UNION: {
+            Scan r;
+            if (!as_scan(in, sc) || !as_scan(p.in[1], r) || sc.kind != r.kind) return false;
+            for (Member& m : r.m) sc.m.push_back(std::move(m));
+            break;
+        }
+        default: return false;
+    }
+    scan_roles(sc, t->cols.size());
+    return true;
+}
+
+enum RK : int8_t { RK_EXPR, RK_CONST, RK_NODE, RK_REL };
+struct Role {
+    RK k = RK_EXPR;
+    int inst = -1, scol = -1;
+    capsmi_expr cst{};
+};
+
+struct ENode {
+    capsmi_expr x{};
+    Role role;  // CAPSMI_X_COL leaves
+    std::vector<ENode> kids;
+};
+
+struct Hop {
+    int rel = -1;          // instance of the relationship scan
+    int from = -1, to = -1;  // positions
+    int from_role = ROLE_SRC, to_role = ROLE_DST;
+};
+
+// A join chain over scans: positions (pattern nodes) joined by hops (relationships)
+struct Path {
+    std::vector<Scan> inst;
+    std::vector<int> pos_node;  // per position: node-scan instance, or -1
+    std::vector<Hop> hops;
+    std::vector<Role> cols;     // per output column
+    std::vector<ENode> conj;    // filter conjuncts
+};
+
+bool parse_prog(const std::vector<capsmi_expr>& prog, const std::vector<Role>& cols, ENode& out) {
+    std::vector<ENode> st;
+    for (const capsmi_expr& x : prog) {
+        const int k = arity(x);
+        if (k < 0 || (int)st.size() < k) return false;
+        ENode n;
+        n.x = x;
+        n.kids.assign(st.end() - k, st.end());
+        st.resize(st.size() - k);
+        if (x.op == CAPSMI_X_COL) {
+            if (x.arg < 0 || x.arg >= (int)cols.size()) return false;
+            n.role = cols[x.arg];
+        }
+        st.push_back(std::move(n));
+    }
+    if (st.size() != 1) return false;
+    out = std::move(st[0]);
+    return true;
+}
+
+void flatten_and(const ENode& n, std::vector<ENode>& out) {
+    if (n.x.op == CAPSMI_X_AND) {
+        for (const ENode& k : n.kids) flatten_and(k, out);
+    } else {
+        out.push_back(n);
+    }
+}
+
+// position a join column denotes: a node scan's id, or one end of a relationship hop
+int position_of(const Path& P, const Role& r) {
+    if (r.k == RK_NODE) {
+        if (P.inst[r.inst].role[r.scol] != ROLE_ID) return -1;
+        for (size_t p = 0; p < P.pos_node.size(); ++p)
+            if (P.pos_node[p] == r.inst) return (int)p;
+        return -1;
+    }
+    if (r.k == RK_REL) {
+        const int role = P.inst[r.inst].role[r.scol];
+        for (const Hop& h : P.hops) {
+            if (h.rel != r.inst) continue;
+            if (role == h.from_role) return h.from;
+            if (role == h.to_role) return h.to;
+        }
+    }
+    return -1;
+}
+
+bool as_paths(const capsmi_table* t, std::vector<Path>& out);
+
+bool as_paths_node(const capsmi_table* t, std::vector<Path>& out) {
+    const PlanNode& p = *t->plan;
+    const capsmi_table* in = p.in[0];
+    switch (p.kind) {
+        case PlanNode::JOIN: {
+            if (p.jt != CAPSMI_JOIN_INNER) return false;
+            std::vector<Path> L;
+            Scan R;
+            if (!as_paths(in, L) || L.size() != 1 || !as_scan(p.in[1], R)) return false;
+            Path P = std::move(L[0]);
+            const int ri = (int)P.inst.size();
+            std::vector<int> lk, rk;
+            for (size_t i = 0; i < p.a.size(); ++i) {
+                lk.push_back(find_col(in, p.a[i]));
+                rk.push_back(find_col(p.in[1], p.b[i]));
+                if (lk.back() < 0 || rk.back() < 0) return false;
+            }
+            P.inst.push_back(R);
+            if (R.kind == 1) {
+                if (lk.size() != 1 || R.role[rk[0]] != ROLE_ID) return false;
+                const int pos = position_of(P, P.cols[lk[0]]);
+                if (pos < 0 || P.pos_node[pos] >= 0) return false;
+                P.pos_node[pos] = ri;
+            } else {
+                if (lk.size() == 1) {  // Expand: a new position
+                    const int pos = position_of(P, P.cols[lk[0]]);
+                    const int rr = R.role[rk[0]];
+                    if (pos < 0 || (rr != ROLE_SRC && rr != ROLE_DST)) return false;
+                    Hop h;
+                    h.rel = ri;
+                    h.from = pos;
+                    h.to = (int)P.pos_node.size();
+                    h.from_role = rr;
+                    h.to_role = rr == ROLE_SRC ? ROLE_DST : ROLE_SRC;
+                    P.pos_node.push_back(-1);
+                    P.hops.push_back(h);
+                } else if (lk.size() == 2) {  // ExpandInto: both ends bound
+                    const int p1 = position_of(P, P.cols[lk[0]]), p2 = position_of(P, P.cols[lk[1]]);
+                    const int r1 = R.role[rk[0]], r2 = R.role[rk[1]];
+                    if (p1 < 0 || p2 < 0 || !((r1 == ROLE_SRC && r2 == ROLE_DST) || (r1 == ROLE_DST && r2 == ROLE_SRC)))
+                        return false;
+                    Hop h;
+                    h.rel = ri;
+                    h.from = r1 == ROLE_SRC ? p1 : p2;
+                    h.to = r1 == ROLE_SRC ? p2 : p1;
+                    P.hops.push_back(h);
+                } else {
+                    return false;
+                }
+            }
+            const capsmi_table* rt = p.in[1];
+            for (size_t k = 0; k < rt->cols.size(); ++k) {
+                Role r;
+                r.k = R.kind == 1 ? RK_NODE : RK_REL;
+                r.inst = ri;
+                r.scol = (int)k;
+                P.cols.push_back(r);
+            }
+            out.push_back(std::move(P));
+            return true;
+        }
+        case PlanNode::FILTER: {
+            if (!as_paths(in, out)) return false;
+            for (Path& P : out) {
+                ENode e;
+                if (!parse_prog(p.progs[0], P.cols, e)) return false;
+                flatten_and(e, P.conj);
+            }
+            return true;
+        }
+        case PlanNode::WITH_COLUMNS: {
+            if (!as_paths(in, out)) return false;
+            for (Path& P : out) {
+                std::vector<Role> cols = P.cols;
+                std::vector<std::string> names;
+                for (auto& c : in->cols) names.push_back(c.name);
+                for (size_t i = 0; i < p.a.size(); ++i) {
+                    Role r;
+                    const auto& prog = p.progs[i];
+                    if (prog.size() == 1 && prog[0].op == CAPSMI_X_COL) r = P.cols[prog[0].arg];
+                    else if (prog.size() == 1 && (prog[0].op == CAPSMI_X_LIT || prog[0].op == CAPSMI_X_NULL)) {
+                        r.k = RK_CONST;
+                        r.cst = prog[0];
+                    }
+                    int j = -1;
+                    for (size_t q = 0; q < names.size(); ++q) if (names[q] == p.a[i]) j = (int)q;
+                    if (j < 0) { names.push_back(p.a[i]); cols.push_back(r); }
+                    else cols[j] = r;
+                }
+                P.cols = std::move(cols);
+            }
+            return true;
+        }
+        case PlanNode::SELECT:
+        case PlanNode::DROP:
+        case PlanNode::RENAME: {
+            if (!as_paths(in, out)) return false;
+            std::vector<int> pick;
+            if (p.kind == PlanNode::SELECT) {
+                for (auto& nm : p.a) pick.push_back(find_col(in, nm));
+            } else if (p.kind == PlanNode::DROP) {
+                std::set<std::string> d(p.a.begin(), p.a.end());
+                for (size_t k = 0; k < in->cols.size(); ++k) if (!d.count(in->cols[k].name)) pick.push_back((int)k);
+            } else {
+                for (size_t k = 0; k < in->cols.size(); ++k) pick.push_back((int)k);
+            }
+            for (Path& P : out) {
+                std::vector<Role> c;
+                for (int k : pick) c.push_back(P.cols[k]);
+                P.cols = std::move(c);
+            }
+            return true;
+        }
+        case PlanNode::UNION: {
+            std::vector<Path> r;
+            if (!as_paths(in, out) || !as_paths(p.in[1], r)) return false;
+            for (Path& x : r) out.push_back(std::move(x));
+            return true;
+        }
+        default: return false;
+    }
+}
+
+bool as_paths(const capsmi_table* t, std::vector<Path>& out) {
+    Scan sc;
+    if (as_scan(t, sc)) {  // a node scan starts a pattern
+        if (sc.kind != 1) return false;
+        Path P;
+        P.inst.push_back(sc);
+        P.pos_node.push_back(0);
+        for (size_t k = 0; k < t->cols.size(); ++k) {
+            Role r;
+            r.k = RK_NODE;
+            r.inst = 0;
+            r.scol = (int)k;
+            P.cols.push_back(r);
+        }
+        out.push_back(std::move(P));
+        return true;
+    }
+    if (!t->lazy()) return false;
+    return as_paths_node(t, out);
+}
+
+// ---- conjunct classification ----------------------------------------------------------------
+int hop_of_rel_id(const Path& P, const ENode& n) {
+    if (n.x.op != CAPSMI_X_COL || n.role.k != RK_REL) return -1;
+    if (P.inst[n.role.inst].role[n.role.scol] != ROLE_ID) return -1;
+    for (size_t h = 0; h < P.hops.size(); ++h)
+        if (P.hops[h].rel == n.role.inst) return (int)h;
+    return -1;
+}
+
+// NOT(r_i = r_j) / r_i <> r_j over two hops' relationship ids
+bool uniqueness(const Path& P, const ENode& c, int* i, int* j) {
+    const ENode* eq = nullptr;
+    if (c.x.op == CAPSMI_X_NOT && c.kids[0].x.op == CAPSMI_X_EQ) eq = &c.kids[0];
+    else if (c.x.op == CAPSMI_X_NEQ) eq = &c;
+    if (!eq) return false;
+    *i = hop_of_rel_id(P, eq->kids[0]);
+    *j = hop_of_rel_id(P, eq->kids[1]);
+    return *i >= 0 && *j >= 0 && *i != *j;
+}
+
+// leaves of a node predicate: one node instance's columns and constants; returns the instance or -1
+bool node_leaves(const ENode& n, int* inst) {
+    if (n.x.op == CAPSMI_X_COL) {
+        if (n.role.k == RK_CONST) return true;
+        if (n.role.k != RK_NODE) return false;
+        if (*inst >= 0 && *inst != n.role.inst) return false;
+        *inst = n.role.inst;
+        return true;
+    }
+    for (const ENode& k : n.kids)
+        if (!node_leaves(k, inst)) return false;
+    return true;
+}
+
+// postfix program of a node predicate over one member's base table
+void emit_pred(const ENode& n, const Member& m, std::vector<capsmi_expr>& out) {
+    for (const ENode& k : n.kids) emit_pred(k, m, out);
+    if (n.x.op == CAPSMI_X_COL) {
+        if (n.role.k == RK_CONST) {
+            out.push_back(n.role.cst);
+        } else if (m.src[n.role.scol] >= 0) {
+            capsmi_expr x{};
+            x.op = CAPSMI_X_COL;
+            x.arg = m.src[n.role.scol];
+            out.push_back(x);
+        } else {
+            out.push_back(m.cst[n.role.scol]);
+        }
+    } else {
+        out.push_back(n.x);
+    }
+}
+
+struct Classified {
+    std::set<std::pair<int, int>> uniq;         // hop pairs (i < j) with NOT(r_i = r_j)
+    std::vector<std::vector<const ENode*>> pred; // per instance: node predicate conjuncts
+};
+
+bool classify(const Path& P, Classified& c) {
+    c.pred.assign(P.inst.size(), {});
+    for (const ENode& e : P.conj) {
+        int i, j;
+        if (uniqueness(P, e, &i, &j)) {
+            c.uniq.insert({std::min(i, j), std::max(i, j)});
+            continue;
+        }
+        int inst = -1;
+        if (!node_leaves(e, &inst)) return false;
+        if (inst < 0) {  // constant conjunct: only TRUE is harmless
+            if (e.x.op == CAPSMI_X_LIT && e.x.type == CAPSMI_BOOL && e.x.ival != 0) continue;
+            return false;
+        }
+        c.pred[inst].push_back(&e);
+    }
+    return true;
+}
+
+// ---- bitmaps of node scans (+ predicates) ------------------------------------------------------
+struct BitmapSet {
+    std::vector<std::pair<std::string, capsmi_bitmap*>> made;
+    ~BitmapSet() {
+        for (auto& x : made) capsmi_bitmap_release(x.second);
+    }
+};
+
+std::string member_prog_key(const capsmi_table* base, const std::vector<capsmi_expr>& prog) {
+    std::string k(reinterpret_cast<const char*>(&base), sizeof(base));
+    k.append(reinterpret_cast<const char*>(prog.data()), prog.size() * sizeof(capsmi_expr));
+    return k + "|";
+}
+
+// bitmap of node instance `inst` with its predicate conjuncts over [lo, hi); identical scans share one.
+// Returns null when an id occurs in two scanned rows (CAPS would bind it twice, ScanGraph.scala:72-76).
+capsmi_bitmap* node_bitmap(capsmi_session* s, const Path& P, const Classified& c, int inst, int64_t lo, int64_t hi,
+                           BitmapSet& bs, std::string* key_out = nullptr) {
+    const Scan& sc = P.inst[inst];
+    std::vector<std::vector<capsmi_expr>> progs;
+    std::string key;
+    for (const Member& m : sc.m) {
+        std::vector<capsmi_expr> prog;
+        for (const ENode* e : c.pred[inst]) emit_pred(*e, m, prog);
+        if (c.pred[inst].size() > 1) {
+            capsmi_expr a{};
+            a.op = CAPSMI_X_AND;
+            a.arg = (int32_t)c.pred[inst].size();
+            prog.push_back(a);
+        }
+        key += member_prog_key(m.base, prog);
+        progs.push_back(std::move(prog));
+    }
+    if (key_out) *key_out = key;
+    for (auto& x : bs.made)
+        if (x.first == key) return x.second;
+    capsmi_bitmap* b = nullptr;
+    check(capsmi_bitmap_create(s, lo, hi, &b));
+    bs.made.push_back({key, b});
+    for (size_t i = 0; i < sc.m.size(); ++i) {
+        const Member& m = sc.m[i];
+        const char* idn = m.base->cols[m.base->entity->id].name.c_str();
+        check(capsmi_bitmap_add_scan(b, m.base, idn, (int32_t)progs[i].size(), progs[i].empty() ? nullptr : progs[i].data()));
+    }
+    return b->any_dup ? nullptr : b;
+}
+
+// the relationship tables of a hop as (source-side, target-side) column views, zero-copy
+struct RelViews {
+    std::vector<capsmi_table*> t;
+    std::string sig;  // identity of the tables and oriented columns (hops over equal sets share kernels)
+    ~RelViews() {
+        for (auto* x : t) capsmi_table_release(x);
+    }
+};
+
+void rel_views(const Path& P, const Hop& h, RelViews& v) {
+    std::vector<std::string> sig;
+    for (const Member& m : P.inst[h.rel].m) {
+        const EntityInfo& e = *m.base->entity;
+        const int fc = h.from_role == ROLE_SRC ? e.src : e.dst, tc = h.to_role == ROLE_SRC ? e.src : e.dst;
+        auto* x = new capsmi_table();
+        x->sess = m.base->sess;
+        x->nrows = m.base->nrows;
+        Column a = m.base->cols[fc], b = m.base->cols[tc];
+        a.name = "s";
+        b.name = "t";
+        x->cols = {a, b};
+        v.t.push_back(x);
+        std::string k(reinterpret_cast<const char*>(&m.base), sizeof(m.base));
+        k += char(fc);
+        k += char(tc);
+        sig.push_back(k);
+    }
+    std::sort(sig.begin(), sig.end());
+    for (auto& k : sig) v.sig += k;
+}
+
+// id window covering every scanned node and relationship endpoint of the path(s)
+bool id_window(const std::vector<Path>& B, int64_t* lo, int64_t* hi) {
+    int64_t l = INT64_MAX, h = INT64_MIN;
+    for (const Path& P : B)
+        for (const Scan& sc : P.inst)
+            for (const Member& m : sc.m) {
+                if (m.base->entity->rows == 0) continue;
+                l = std::min(l, m.base->entity->lo);
+                h = std::max(h, m.base->entity->hi);
+            }
+    if (l >= h) return false;
+    if ((uint64_t)(h - l) > (uint64_t(1) << 30)) return false;
+    *lo = l;
+    *hi = h;
+    return true;
+}
+
+bool id_like(const Path& P, const Role& r) {  // a non-null id / endpoint column
+    if (r.k == RK_NODE) return P.inst[r.inst].role[r.scol] == ROLE_ID;
+    if (r.k == RK_REL) return P.inst[r.inst].role[r.scol] != ROLE_NONE;
+    return false;
+}
+
+capsmi_table* result_table(capsmi_session* s, int64_t rows) {
+    auto* r = new capsmi_table();
+    r->sess = s;
+    r->nrows = rows;
+    return r;
+}
+
+Column i64_column(capsmi_session* s, const std::vector<int64_t>& v) {
+    Column c;
+    c.type = CAPSMI_I64;
+    c.data = dev_alloc(sizeof(int64_t) * (v.empty() ? 1 : v.size()), s);
+    if (!v.empty())
+        HIP_CHECK(hipMemcpyAsync(P<void>(c.data), v.data(), sizeof(int64_t) * v.size(), hipMemcpyHostToDevice, s->stream));
+    HIP_CHECK(hipStreamSynchronize(s->stream));
+    return c;
+}
+
+// ---- the shapes ---------------------------------------------------------------------------------
+enum Agg1 { A_COUNT, A_DISTINCT_END, A_DISTINCT_START };
+
+// count-like aggregates of a group over one branch
+bool agg_kinds(const capsmi_table* in, const PlanNode& g, const Path& P, int start, int end, std::vector<int>& kinds) {
+    for (const AggSpec& a : g.aggs) {
+        if (a.kind == CAPSMI_AGG_COUNT_STAR) { kinds.push_back(A_COUNT); continue; }
+        if (a.kind != CAPSMI_AGG_COUNT) return false;
+        const int c = find_col(in, a.input);
+        if (c < 0) return false;
+        const Role& r = P.cols[c];
+        if (!a.distinct) {
+            if (!id_like(P, r)) return false;
+            kinds.push_back(A_COUNT);
+            continue;
+        }
+        const int pos = position_of(P, r);
+        if (pos >= 0 && pos == end && end != start) kinds.push_back(A_DISTINCT_END);
+        else if (pos >= 0 && pos == start && end != start) kinds.push_back(A_DISTINCT_START);
+        else return false;
+    }
+    return true;
+}
+
+// chain P0 -h0-> P1 -h1-> ... with hop i from position i to i + 1; true if the hops form that chain
+bool is_chain(const Path& P) {
+    for (size_t i = 0; i < P.hops.size(); ++i)
+        if (P.hops[i].from != (int)i || P.hops[i].to != (int)i + 1) return false;
+    return P.pos_node.size() == P.hops.size() + 1;
+}
+
+bool same_orientation(const Path& P) {
+    for (const Hop& h : P.hops)
+        if (h.from_role != P.hops[0].from_role) return false;
+    return true;
+}
+
+bool all_pairs_unique(const Classified& c, int nh) {
+    for (int i = 0; i < nh; ++i)
+        for (int j = i + 1; j < nh; ++j)
+            if (!c.uniq.count({i, j})) return false;
+    return (int)c.uniq.size() == nh * (nh - 1) / 2;
+}
+
+void route(capsmi_session* s, const char* name) { s->routes[name] += 1; }
+
+// count(*) / count(DISTINCT end | start) of one branch: 1 hop, a 2-hop chain, or the closed triangle.
+// Returns false when the shape or a precondition does not hold.
+bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kinds, std::vector<int64_t>& vals) {
+    Classified c;
+    if (!classify(P, c)) return false;
+    for (int x : P.pos_node) if (x < 0) return false;
+    const size_t nh = P.hops.size();
+    if (nh < 1 || nh > 3) return false;
+    std::vector<Path> one{P};
+    int64_t lo, hi;
+    if (!id_window(one, &lo, &hi)) return false;
+    BitmapSet bs;
+    RelViews v0;
+    rel_views(P, P.hops[0], v0);
+    const int64_t nt = (int64_t)v0.t.size();
+    if (nh == 1 && is_chain(P) && c.uniq.empty()) {
+        for (int k : kinds) if (k != A_COUNT) return false;
+        capsmi_bitmap* a = node_bitmap(s, P, c, P.pos_node[0], lo, hi, bs);
+        capsmi_bitmap* b = node_bitmap(s, P, c, P.pos_node[1], lo, hi, bs);
+        if (!a || !b) return false;
+        int64_t total = 0;
+        for (capsmi_table* t : v0.t) {
+            const char* sc[1] = {"s"};
+            capsmi_table* o = nullptr;
+            check(capsmi_expand_filter(s, t, "s", "t", a, b, 1, sc, nullptr, &o));
+            total += o->nrows;
+            capsmi_table_release(o);
+        }
+        vals.assign(kinds.size(), total);
+        route(s, "expand_count");
+        return true;
+    }
+    if (nh == 2 && is_chain(P) && same_orientation(P)) {
+        RelViews v1;
+        rel_views(P, P.hops[1], v1);
+        if (v1.sig != v0.sig || !all_pairs_unique(c, 2)) return false;
+        capsmi_bitmap* a = node_bitmap(s, P, c, P.pos_node[0], lo, hi, bs);
+        capsmi_bitmap* b = node_bitmap(s, P, c, P.pos_node[1], lo, hi, bs);
+        capsmi_bitmap* cc = node_bitmap(s, P, c, P.pos_node[2], lo, hi, bs);
+        if (!a || !b || !cc) return false;
+        for (int k : kinds) {
+            int64_t x = 0;
+            if (k == A_COUNT) {
+                check(capsmi_two_hop_count(s, (int32_t)nt, v0.t.data(), "s", "t", a, b, cc, &x));
+            } else if (k == A_DISTINCT_END) {
+                check(capsmi_two_hop_count_distinct(s, (int32_t)nt, v0.t.data(), "s", "t", a, b, cc, &x));
+            } else {  // distinct start: the same walk over the reversed relationships
+                check(capsmi_two_hop_count_distinct(s, (int32_t)nt, v0.t.data(), "t", "s", cc, b, a, &x));
+            }
+            vals.push_back(x);
+        }
+        route(s, "two_hop");
+        return true;
+    }
+    if (nh == 3 && P.pos_node.size() == 3 && same_orientation(P)) {
+        // P0 -h0-> P1 -h1-> P2 -h2-> P0 (the closing hop is the ExpandInto)
+        const Hop &h0 = P.hops[0], &h1 = P.hops[1], &h2 = P.hops[2];
+        if (!(h0.from == 0 && h0.to == 1 && h1.from == 1 && h1.to == 2 && h2.from == 2 && h2.to == 0)) return false;
+        RelViews v1, v2;
+        rel_views(P, h1, v1);
+        rel_views(P, h2, v2);
+        if (v1.sig != v0.sig || v2.sig != v0.sig || !all_pairs_unique(c, 3)) return false;
+        for (int k : kinds) if (k != A_COUNT) return false;
+        std::string k0, k1, k2;
+        capsmi_bitmap* a = node_bitmap(s, P, c, P.pos_node[0], lo, hi, bs, &k0);
+        capsmi_bitmap* b = node_bitmap(s, P, c, P.pos_node[1], lo, hi, bs, &k1);
+        capsmi_bitmap* cc = node_bitmap(s, P, c, P.pos_node[2], lo, hi, bs, &k2);
+        if (!a || !b || !cc || k0 != k1 || k1 != k2) return false;  // one node filter for all three
+        int64_t x = 0;
+        check(capsmi_triangle_count(s, (int32_t)nt, v0.t.data(), "s", "t", a, &x));
+        vals.assign(kinds.size(), x);
+        route(s, "triangle");
+        return true;
+    }
+    return false;
+}
+
+// group by the start node, count(*), over the branches of a bounded var-length expand
+bool fused_var_length(capsmi_session* s, const capsmi_table* in, const PlanNode& g, const std::vector<Path>& B,
+                      capsmi_table** out) {
+    if (g.a.size() != 1 || g.aggs.size() != 1) return false;
+    const AggSpec& ag = g.aggs[0];
+    const int gc = find_col(in, g.a[0]);
+    if (gc < 0) return false;
+    std::set<int> lens;
+    std::string akey, bkey, rsig;
+    int64_t lo, hi;
+    if (!id_window(B, &lo, &hi)) return false;
+    BitmapSet bs;
+    capsmi_bitmap *abm = nullptr, *bbm = nullptr;
+    RelViews views;
+    for (size_t bi = 0; bi < B.size(); ++bi) {
+        const Path& P = B[bi];
+        const int k = (int)P.hops.size();
+        if (k < 1 || !is_chain(P) || !same_orientation(P) || lens.count(k)) return false;
+        lens.insert(k);
+        for (int q = 1; q < k; ++q) if (P.pos_node[q] >= 0) return false;  // hops are not node-scanned
+        if (P.pos_node[0] < 0 || P.pos_node[k] < 0) return false;
+        if (position_of(P, P.cols[gc]) != 0 || !id_like(P, P.cols[gc])) return false;
+        if (ag.kind == CAPSMI_AGG_COUNT) {
+            const int c = find_col(in, ag.input);
+            if (ag.distinct || c < 0 || !id_like(P, P.cols[c])) return false;
+        } else if (ag.kind != CAPSMI_AGG_COUNT_STAR) {
+            return false;
+        }
+        Classified c;
+        if (!classify(P, c) || !all_pairs_unique(c, k)) return false;
+        for (size_t q = 0; q < P.inst.size(); ++q)
+            if (!c.pred[q].empty() && (int)q != P.pos_node[0] && (int)q != P.pos_node[k]) return false;
+        std::string ka, kb;
+        capsmi_bitmap* a = node_bitmap(s, P, c, P.pos_node[0], lo, hi, bs, &ka);
+        capsmi_bitmap* b = node_bitmap(s, P, c, P.pos_node[k], lo, hi, bs, &kb);
+        if (!a || !b) return false;
+        for (int h = 0; h < k; ++h) {
+            RelViews v;
+            rel_views(P, P.hops[h], v);
+            if (bi == 0 && h == 0) { rsig = v.sig; views.t.swap(v.t); }
+            else if (v.sig != rsig) return false;
+        }
+        if (bi == 0) { akey = ka; bkey = kb; abm = a; bbm = b; }
+        else if (ka != akey || kb != bkey) return false;
+    }
+    const int l = *lens.begin(), u = *lens.rbegin();
+    if (l < 1 || u > 3 || u - l + 1 != (int)lens.size()) return false;
+    check(capsmi_var_length_count(s, (int32_t)views.t.size(), views.t.data(), "s", "t", abm, bbm, l, u, g.a[0].c_str(),
+                                  ag.output.c_str(), out));
+    route(s, "var_length");
+    return true;
+}
+
+// Expand + node filters projected on relationship / endpoint columns (C2)
+bool fused_projection(capsmi_session* s, const capsmi_table* t, const std::vector<Path>& B, capsmi_table** out) {
+    if (B.size() != 1) return false;
+    const Path& P = B[0];
+    if (P.hops.size() != 1 || !is_chain(P) || P.pos_node[0] < 0 || P.pos_node[1] < 0) return false;
+    Classified c;
+    if (!classify(P, c) || !c.uniq.empty()) return false;
+    const Hop& h = P.hops[0];
+    const Scan& R = P.inst[h.rel];
+    // output column -> (relationship scan column | endpoint role | constant)
+    std::vector<int> rcol(P.cols.size(), -1), endp(P.cols.size(), ROLE_NONE);
+    int ndata = 0;
+    for (size_t i = 0; i < P.cols.size(); ++i) {
+        const Role& r = P.cols[i];
+        if (r.k == RK_CONST) continue;
+        if (r.k == RK_REL && r.inst == h.rel) { rcol[i] = r.scol; ++ndata; continue; }
+        const int pos = position_of(P, r);
+        if (r.k == RK_NODE && pos == 0) { endp[i] = h.from_role; ++ndata; continue; }
+        if (r.k == RK_NODE && pos == 1) { endp[i] = h.to_role; ++ndata; continue; }
+        return false;  // node properties / labels: joined in the generic plan
+    }
+    if (ndata > 4) return false;
+    std::vector<Path> one{P};
+    int64_t lo, hi;
+    if (!id_window(one, &lo, &hi)) return false;
+    BitmapSet bs;
+    capsmi_bitmap* a = node_bitmap(s, P, c, P.pos_node[0], lo, hi, bs);
+    capsmi_bitmap* b = node_bitmap(s, P, c, P.pos_node[1], lo, hi, bs);
+    if (!a || !b) return false;
+    std::vector<capsmi_table*> parts;
+    struct Release { std::vector<capsmi_table*>& v; ~Release() { for (auto* x : v) capsmi_table_release(x); } } rel{parts};
+    for (const Member& m : R.m) {
+        const EntityInfo& e = *m.base->entity;
+        const int fc = h.from_role == ROLE_SRC ? e.src : e.dst, tc = h.to_role == ROLE_SRC ? e.src : e.dst;
+        std::vector<const char*> ocols, onames;
+        std::vector<std::string> tmpn;
+        for (size_t i = 0; i < P.cols.size(); ++i) tmpn.push_back("c" + std::to_string(i));
+        bool const_member = false;
+        for (size_t i = 0; i < P.cols.size(); ++i) {
+            int bc = -1;
+            if (rcol[i] >= 0) bc = m.src[rcol[i]];
+            else if (endp[i] != ROLE_NONE) bc = endp[i] == ROLE_SRC ? e.src : e.dst;
+            else continue;
+            if (bc < 0) { const_member = true; break; }  // a per-table constant in a relationship column
+            ocols.push_back(m.base->cols[bc].name.c_str());
+            onames.push_back(tmpn[i].c_str());
+        }
+        if (const_member) return false;
+        const char* any[1] = {m.base->cols[fc].name.c_str()};
+        const char* anyn[1] = {"c_"};
+        capsmi_table* o = nullptr;
+        if (ocols.empty()) check(capsmi_expand_filter(s, m.base, m.base->cols[fc].name.c_str(), m.base->cols[tc].name.c_str(),
+                                                      a, b, 1, any, anyn, &o));
+        else check(capsmi_expand_filter(s, m.base, m.base->cols[fc].name.c_str(), m.base->cols[tc].name.c_str(), a, b,
+                                        (int32_t)ocols.size(), ocols.data(), onames.data(), &o));
+        parts.push_back(o);
+    }
+    // assemble the output schema: data columns from the kernel, constants filled
+    capsmi_table* acc = nullptr;
+    for (capsmi_table* part : parts) {
+        auto* r = result_table(s, part->nrows);
+        for (size_t i = 0; i < P.cols.size(); ++i) {
+            Column col;
+            const int j = find_col(part, "c" + std::to_string(i));
+            if (j >= 0) {
+                col = part->cols[j];
+            } else {
+                const capsmi_expr& x = P.cols[i].cst;
+                col.type = t->cols[i].type;
+                col.data = dev_alloc(sizeof(int64_t) * (part->nrows > 0 ? part->nrows : 1), s);
+                fill_i64(::capsmi::P<int64_t>(col.data), x.op == CAPSMI_X_LIT ? x.ival : 0, part->nrows, s->stream);
+                if (x.op == CAPSMI_X_NULL || t->cols[i].nullable()) {
+                    col.valid = dev_alloc(part->nrows > 0 ? part->nrows : 1, s);
+                    fill_u8(::capsmi::P<uint8_t>(col.valid), x.op == CAPSMI_X_NULL ? 0 : 1, part->nrows, s->stream);
+                }
+            }
+            col.name = t->cols[i].name;
+            r->cols.push_back(col);
+        }
+        if (!acc) {
+            acc = r;
+        } else {
+            capsmi_table* u = nullptr;
+            const capsmi_status st = eager_union_all(acc, r, &u);
+            capsmi_table_release(acc);
+            capsmi_table_release(r);
+            check(st);
+            acc = u;
+        }
+    }
+    *out = acc;
+    route(s, "expand");
+    return true;
+}
+
+// try the fused shapes for lazy table `t`; on success *out is its materialised content
+bool try_fused(capsmi_table* t, capsmi_table** out) {
+    capsmi_session* s = t->sess;
+    if (!s->fused) return false;
+    const PlanNode& p = *t->plan;
+    if (p.kind == PlanNode::GROUP) {
+        const capsmi_table* in = p.in[0];
+        std::vector<Path> B;
+        if (!as_paths(in, B) || B.empty()) return false;
+        if (p.a.empty()) {
+            if (B.size() != 1) return false;
+            std::vector<int> kinds;
+            const int end = (int)B[0].pos_node.size() - 1;
+            if (!agg_kinds(in, p, B[0], 0, B[0].hops.size() == 3 ? 0 : end, kinds)) return false;
+            std::vector<int64_t> vals;
+            if (!fused_counts(s, B[0], kinds, vals)) return false;
+            auto* r = result_table(s, 1);
+            for (size_t i = 0; i < vals.size(); ++i) {
+                Column c = i64_column(s, {vals[i]});
+                c.name = p.aggs[i].output;
+                r->cols.push_back(std::move(c));
+            }
+            *out = r;
+            return true;
+        }
+        return fused_var_length(s, in, p, B, out);
+    }
+    std::vector<Path> B;
+    if (!as_paths(t, B)) return false;
+    return fused_projection(s, t, B, out);
+}
+
+}  // namespace
+
+void attach_entity(capsmi_table* t, int kind, int64_t lo, int64_t hi) {
+    auto e = std::make_shared<EntityInfo>();
+    e->kind = kind;
+    e->id = 0;
+    if (kind == 2) {
+        e->src = 1;
+        e->dst = 2;
+    }
+    e->rows = t->nrows;
+    e->lo = lo;
+    e->hi = hi;
+    t->entity = e;
+}
+
+// ================================ materialisation ===========================================
+void materialize(capsmi_table* t) {
+    if (!t || !t->plan) return;
+    std::shared_ptr<PlanNode> p = t->plan;  // inputs stay alive while this runs
+    capsmi_table* r = nullptr;
+    if (!try_fused(t, &r)) {
+        for (capsmi_table* x : p->in) materialize(x);
+        r = exec_node(*p);
+    }
+    adopt(t, r);
+    t->plan.reset();  // the inputs are released unless shared elsewhere
+}
+
+}  // namespace capsmi
+
+using namespace capsmi;
+
+// ===================================== C ABI ====================================================
+extern "C" {
+
+static capsmi_status build(capsmi_table* t, capsmi_table** out, const std::function<capsmi_table*()>& f) {
+    P_BEGIN
+    need(t, "table");
+    need(out, "out");
+    *out = f();
+    P_END
+}
+
+capsmi_status capsmi_cache(capsmi_table* t, capsmi_table** out) {
+    // a table keeps its rows once computed (DataFrameTable.cache, SparkTable.scala:240-246): same handle
+    return build(t, out, [&] {
+        t->refs.fetch_add(1);
+        return t;
+    });
+}
+
+capsmi_status capsmi_select(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out) {
+    return build(t, out, [&] {
+        auto p = std::make_shared<PlanNode>();
+        p->kind = PlanNode::SELECT;
+        hold(*p, t);
+        std::vector<Column> sch;
+        for (int i = 0; i < ncols; ++i) {
+            sch.push_back(schema_of(t->cols[col_of(t, cols[i])]));
+            p->a.push_back(cols[i]);
+        }
+        return lazy_table(t->sess, p, sch);
+    });
+}
+
+capsmi_status capsmi_drop(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out) {
+    return build(t, out, [&] {
+        auto p = std::make_shared<PlanNode>();
+        p->kind = PlanNode::DROP;
+        hold(*p, t);
+        std::set<std::string> d;
+        for (int i = 0; i < ncols; ++i) {
+            need(cols[i], "column name");
+            d.insert(cols[i]);  // Spark drop ignores unknown names
+            p->a.push_back(cols[i]);
+        }
+        std::vector<Column> sch;
+        for (auto& c : t->cols) if (!d.count(c.name)) sch.push_back(schema_of(c));
+        return lazy_table(t->sess, p, sch);
+    });
+}
+
+capsmi_status capsmi_with_column_renamed(capsmi_table* t, const char* old_name, const char* new_name, capsmi_table** out) {
+    return build(t, out, [&] {
+        need(new_name, "new name");
+        const int i = col_of(t, old_name);
+        const int j = find_col(t, new_name);
+        REQUIRE(j < 0 || j == i, CAPSMI_ERR_ILLEGAL_ARGUMENT, std::string("column '") + new_name + "' already exists");
+        auto p = std::make_shared<PlanNode>();
+        p->kind = PlanNode::RENAME;
+        hold(*p, t);
+        p->a = {old_name};
+        p->b = {new_name};
+        std::vector<Column> sch;
+        for (auto& c : t->cols) sch.push_back(schema_of(c));
+        sch[i].name = new_name;
+        return lazy_table(t->sess, p, sch);
+    });
+}
+
+capsmi_status capsmi_filter(capsmi_table* t, int32_t nnodes, const capsmi_expr* prog, capsmi_table** out) {
+    return build(t, out, [&] {
+        REQUIRE(nnodes == 0 || prog, CAPSMI_ERR_ILLEGAL_ARGUMENT, "null program");
+        validate_program(t, nnodes, prog);
+        auto p = std::make_shared<PlanNode>();
+        p->kind = PlanNode::FILTER;
+        hold(*p, t);
+        p->progs.emplace_back(prog, prog + nnodes);
+        std::vector<Column> sch;
+        for (auto& c : t->cols) sch.push_back(schema_of(c));
+        return lazy_table(t->sess, p, sch);
+    });
+}
+
+capsmi_status capsmi_with_columns(capsmi_table* t, int32_t ncols, const capsmi_expr_column* cols, capsmi_table** out) {
+    return build(t, out, [&] {
+        REQUIRE(ncols == 0 || cols, CAPSMI_ERR_ILLEGAL_ARGUMENT, "null columns");
+        auto p = std::make_shared<PlanNode>();
+        p->kind = PlanNode::WITH_COLUMNS;
+        hold(*p, t);
+        std::vector<Column> sch;
+        for (auto& c : t->cols) sch.push_back(schema_of(c));
+        for (int i = 0; i < ncols; ++i) {
+            need(cols[i].name, "column name");
+            REQUIRE(cols[i].nnodes == 0 || cols[i].prog, CAPSMI_ERR_ILLEGAL_ARGUMENT, "null program");
+            validate_program(t, cols[i].nnodes, cols[i].prog);
+            p->a.push_back(cols[i].name);
+            p->progs.emplace_back(cols[i].prog, cols[i].prog + cols[i].nnodes);
+            Column c = schema_col(cols[i].name, infer_type(t, cols[i].nnodes, cols[i].prog), true);
+            int j = -1;
+            for (size_t q = 0; q < sch.size(); ++q) if (sch[q].name == c.name) j = (int)q;
+            if (j >= 0) sch[j] = c;  // replaced in place (SparkTable.scala:82-87)
+            else sch.push_back(c);
+        }
+        return lazy_table(t->sess, p, sch);
+    });
+}
+
+capsmi_status capsmi_join(capsmi_table* l, capsmi_table* r, int32_t join_type, int32_t npairs, const char* const* lcols,
+                          const char* const* rcols, capsmi_table** out) {
+    return build(l, out, [&] {
+        need(r, "right");
+        REQUIRE(l->sess == r->sess, CAPSMI_ERR_ILLEGAL_ARGUMENT, "tables belong to different sessions");
+        REQUIRE(join_type >= CAPSMI_JOIN_INNER && join_type <= CAPSMI_JOIN_CROSS, CAPSMI_ERR_ILLEGAL_ARGUMENT, "join type");
+        REQUIRE(join_type == CAPSMI_JOIN_CROSS || npairs > 0, CAPSMI_ERR_ILLEGAL_ARGUMENT, "equi-join needs key pairs");
+        for (const Column& a : l->cols)
+            for (const Column& b : r->cols)
+                REQUIRE(a.name != b.name, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                        "join inputs share column '" + a.name + "' (RelationalPlanner renames to disjoint columns)");
+        auto p = std::make_shared<PlanNode>();
+        p->kind = PlanNode::JOIN;
+        hold(*p, l);
+        hold(*p, r);
+        p->jt = join_type;
+        if (join_type != CAPSMI_JOIN_CROSS) {
+            REQUIRE(npairs <= 8, CAPSMI_ERR_NOT_IMPLEMENTED, "more than 8 key columns");
+            for (int i = 0; i < npairs; ++i) {
+                const int a = col_of(l, lcols[i]), b = col_of(r, rcols[i]);
+                const int ta = l->cols[a].type, tb = r->cols[b].type;
+                const bool na = ta == CAPSMI_I64 || ta == CAPSMI_F64, nb = tb == CAPSMI_I64 || tb == CAPSMI_F64;
+                REQUIRE(ta == tb || (na && nb), CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                        "join key types differ: " + l->cols[a].name + " vs " + r->cols[b].name);
+                p->a.push_back(lcols[i]);
+                p->b.push_back(rcols[i]);
+            }
+        }
+        const bool lmiss = join_type == CAPSMI_JOIN_RIGHT_OUTER || join_type == CAPSMI_JOIN_FULL_OUTER;
+        const bool rmiss = join_type == CAPSMI_JOIN_LEFT_OUTER || join_type == CAPSMI_JOIN_FULL_OUTER;
+        std::vector<Column> sch;
+        for (auto& c : l->cols) sch.push_back(schema_col(c.name, c.type, c.nullable() || lmiss));
+        for (auto& c : r->cols) sch.push_back(schema_col(c.name, c.type, c.nullable() || rmiss));
+        return lazy_table(l->sess, p, sch);
+    });
+}
+
+capsmi_status capsmi_union_all(capsmi_table* a, capsmi_table* b, capsmi_table** out) {
+    return build(a, out, [&] {
+        need(b, "right");
+        REQUIRE(a->cols.size() == b->cols.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT, "union all: column counts differ");
+        std::vector<Column> sch;
+        for (size_t i = 0; i < a->cols.size(); ++i) {
+            REQUIRE(a->cols[i].type == b->cols[i].type, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                    "Equal column data types for union all (differing nullability is OK): " + a->cols[i].name + " vs " +
+                        b->cols[i].name);
+            sch.push_back(schema_col(a->cols[i].name, a->cols[i].type, a->cols[i].nullable() || b->cols[i].nullable()));
+        }
+        auto p = std::make_shared<PlanNode>();
+        p->kind = PlanNode::UNION;
+        hold(*p, a);
+        hold(*p, b);
+        return lazy_table(a->sess, p, sch);
+    });
+}
+
+capsmi_status capsmi_order_by(capsmi_table* t, int32_t nkeys, const char* const* cols, const int32_t* descending,
+                              capsmi_table** out) {
+    return build(t, out, [&] {
+        auto p = std::make_shared<PlanNode>();
+        p->kind = PlanNode::ORDER;
+        hold(*p, t);
+        for (int i = 0; i < nkeys; ++i) {
+            (void)col_of(t, cols[i]);
+            p->a.push_back(cols[i]);
+            p->flags.push_back(descending ? descending[i] : 0);
+        }
+        std::vector<Column> sch;
+        for (auto& c : t->cols) sch.push_back(schema_of(c));
+        return lazy_table(t->sess, p, sch);
+    });
+}
+
+capsmi_status capsmi_skip(capsmi_table* t, int64_t n, capsmi_table** out) {
+    return build(t, out, [&] {
+        REQUIRE(n >= 0, CAPSMI_ERR_ILLEGAL_ARGUMENT, "negative skip");
+        auto p = std::make_shared<PlanNode>();
+        p->kind = PlanNode::SKIP;
+        hold(*p, t);
+        p->n = n;
+        std::vector<Column> sch;
+        for (auto& c : t->cols) sch.push_back(schema_of(c));
+        return lazy_table(t->sess, p, sch);
+    });
+}
+
+capsmi_status capsmi_limit(capsmi_table* t, int64_t n, capsmi_table** out) {
+    return build(t, out, [&] {
+        REQUIRE(n >= 0 && n <= 2147483647LL, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                "an integer: limit must fit an Int (SparkTable.scala:117)");
+        auto p = std::make_shared<PlanNode>();
+        p->kind = PlanNode::LIMIT;
+        hold(*p, t);
+        p->n = n;
+        std::vector<Column> sch;
+        for (auto& c : t->cols) sch.push_back(schema_of(c));
+        return lazy_table(t->sess, p, sch);
+    });
+}
+
+capsmi_status capsmi_distinct(capsmi_table* t, capsmi_table** out) {
+    return build(t, out, [&] {
+        auto p = std::make_shared<PlanNode>();
+        p->kind = PlanNode::DISTINCT;
+        hold(*p, t);
+        std::vector<Column> sch;
+        for (auto& c : t->cols) sch.push_back(schema_of(c));
+        return lazy_table(t->sess, p, sch);
+    });
+}
+
+capsmi_status capsmi_distinct_on(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out) {
+    return build(t, out, [&] {
+        auto p = std::make_shared<PlanNode>();
+        p->kind = PlanNode::DISTINCT_ON;
+        hold(*p, t);
+        for (int i = 0; i < ncols; ++i) {
+            (void)col_of(t, cols[i]);
+            p->a.push_back(cols[i]);
+        }
+        std::vector<Column> sch;
+        for (auto& c : t->cols) sch.push_back(schema_of(c));
+        return lazy_table(t->sess, p, sch);
+    });
+}
+
+capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, int32_t naggs, const capsmi_agg* aggs,
+                           capsmi_table** out) {
+    return build(t, out, [&] {
+        REQUIRE(naggs == 0 || aggs, CAPSMI_ERR_ILLEGAL_ARGUMENT, "null aggregations");
+        auto p = std::make_shared<PlanNode>();
+        p->kind = PlanNode::GROUP;
+        hold(*p, t);
+        std::vector<Column> sch;
+        for (int i = 0; i < nby; ++i) {
+            const int c = col_of(t, by[i]);
+            p->a.push_back(by[i]);
+            sch.push_back(schema_of(t->cols[c]));
+        }
+        for (int i = 0; i < naggs; ++i) {
+            const capsmi_agg& ag = aggs[i];
+            need(ag.output, "aggregate output name");
+            AggSpec sp;
+            sp.kind = ag.kind;
+            sp.distinct = ag.distinct;
+            sp.output = ag.output;
+            int32_t ty = CAPSMI_I64;
+            bool nullable = false;
+            switch (ag.kind) {
+                case CAPSMI_AGG_COUNT_STAR: break;
+                case CAPSMI_AGG_COUNT: sp.input = t->cols[col_of(t, ag.input)].name; break;
+                case CAPSMI_AGG_SUM: case CAPSMI_AGG_AVG: {
+                    const Column& c = t->cols[col_of(t, ag.input)];
+                    REQUIRE(c.type == CAPSMI_I64 || c.type == CAPSMI_F64, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                            ag.kind == CAPSMI_AGG_SUM ? "sum of non-number" : "avg of non-number");
+                    sp.input = c.name;
+                    ty = c.type;
+                    nullable = true;
+                    break;
+                }
+                case CAPSMI_AGG_MIN: case CAPSMI_AGG_MAX: {
+                    const Column& c = t->cols[col_of(t, ag.input)];
+                    sp.input = c.name;
+                    ty = c.type;
+                    nullable = true;
+                    break;
+                }
+                default: throw Error(CAPSMI_ERR_NOT_IMPLEMENTED, "Aggregation function " + std::to_string(ag.kind));
+            }
+            p->aggs.push_back(sp);
+            sch.push_back(schema_col(ag.output, ty, nullable));
+        }
+        return lazy_table(t->sess, p, sch);
+    });
+}
+
+capsmi_status capsmi_session_set_fused(capsmi_session* s, int32_t enabled) {
+    P_BEGIN
+    need(s, "session");
+    s->fused = enabled != 0;
+    P_END
+}
+
+capsmi_status capsmi_session_route_count(capsmi_session* s, const char* name, int64_t* count) {
+    P_BEGIN
+    need(s, "session");
+    need(name, "name");
+    need(count, "count");
+    auto it = s->routes.find(name);
+    *count = it == s->routes.end() ? 0 : it->second;
+    P_END
+}
+
+// ---- entity tables ------------------------------------------------------------------------------
+static void verify_key(const capsmi_table* t, const char* name, const char* what, int32_t type) {
+    need(name, what);
+    const int i = find_col(t, name);
+    REQUIRE(i >= 0, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            std::string("table with column key ") + name + " (EntityTable.verify: no such column)");
+    const Column& c = t->cols[i];
+    const char* tn = type == CAPSMI_I64 ? "CTInteger" : "CTBoolean";
+    REQUIRE(c.type == type, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            std::string(what) + " column `" + name + "` of type " + tn + " (incompatible column type)");
+    REQUIRE(!c.nullable(), CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            std::string("non-nullable type for ") + what + " column `" + name + "` (nullable type)");
+}
+
+static capsmi_table* register_entity(capsmi_table* t, int kind, const std::vector<const char*>& keys,
+                                     const std::vector<const char*>& flags) {
+    // canonical order: keys ++ flags ++ properties sorted (EntityMapping.allSourceKeys, EntityMapping.scala:50)
+    std::vector<std::string> want(keys.begin(), keys.end());
+    want.insert(want.end(), flags.begin(), flags.end());
+    std::set<std::string> fixed(want.begin(), want.end());
+    REQUIRE(fixed.size() == want.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT, "One-to-one mapping from entity elements to source keys");
+    std::vector<std::string> props;
+    for (auto& c : t->cols) if (!fixed.count(c.name)) props.push_back(c.name);
+    std::sort(props.begin(), props.end());
+    want.insert(want.end(), props.begin(), props.end());
+    bool ok = want.size() == t->cols.size();
+    for (size_t i = 0; ok && i < want.size(); ++i) ok = t->cols[i].name == want[i];
+    if (!ok) {
+        std::string exp, got;
+        for (auto& w : want) exp += (exp.empty() ? "" : ", ") + w;
+        for (auto& c : t->cols) got += (got.empty() ? "" : ", ") + c.name;
+        throw Error(CAPSMI_ERR_ILLEGAL_ARGUMENT, "Columns: " + exp + " expected, got Columns: " + got +
+                                                     " (use CAPS[Node|Relationship]Table#fromMapping to create a valid "
+                                                     "EntityTable)");
+    }
+    materialize(t);
+    auto e = std::make_shared<EntityInfo>();
+    e->kind = kind;
+    e->id = 0;
+    if (kind == 2) {
+        e->src = 1;
+        e->dst = 2;
+    }
+    e->rows = t->nrows;
+    if (t->nrows > 0) {
+        capsmi_session* s = t->sess;
+        HIP_CHECK(hipSetDevice(s->device));
+        int64_t mm[2];
+        if (kind == 1) {
+            const int64_t* c[1] = {t->cols[0].d()};
+            minmax_i64(s, c, 1, t->nrows, mm);
+        } else {
+            const int64_t* c[2] = {t->cols[1].d(), t->cols[2].d()};
+            minmax_i64(s, c, 2, t->nrows, mm);
+        }
+        e->lo = mm[0];
+        e->hi = mm[1] == INT64_MAX ? INT64_MAX : mm[1] + 1;
+    }
+    auto* o = new capsmi_table();
+    o->sess = t->sess;
+    o->nrows = t->nrows;
+    o->cols = t->cols;
+    o->entity = e;
+    return o;
+}
+
+capsmi_status capsmi_node_table(capsmi_table* t, const char* id_col, int32_t nlabels, const char* const* label_cols,
+                                capsmi_table** out) {
+    return build(t, out, [&] {
+        verify_key(t, id_col, "id key", CAPSMI_I64);
+        std::vector<const char*> flags;
+        for (int i = 0; i < nlabels; ++i) {
+            verify_key(t, label_cols[i], "optional label", CAPSMI_BOOL);
+            flags.push_back(label_cols[i]);
+        }
+        return register_entity(t, 1, {id_col}, flags);
+    });
+}
+
+capsmi_status capsmi_rel_table(capsmi_table* t, const char* id_col, const char* src_col, const char* dst_col,
+                               int32_t ntypes, const char* const* type_cols, capsmi_table** out) {
+    return build(t, out, [&] {
+        verify_key(t, id_col, "id key", CAPSMI_I64);
+        verify_key(t, src_col, "start node", CAPSMI_I64);
+        verify_key(t, dst_col, "end node", CAPSMI_I64);
+        std::vector<const char*> flags;
+        for (int i = 0; i < ntypes; ++i) {
+            verify_key(t, type_cols[i], "relationship type", CAPSMI_BOOL);
+            flags.push_back(type_cols[i]);
+        }
+        return register_entity(t, 2, {id_col, src_col, dst_col}, flags);
+    });
+}
+
+capsmi_status capsmi_table_entity(const capsmi_table* t, int32_t* kind, int64_t* id_lo, int64_t* id_hi) {
+    P_BEGIN
+    need(t, "table");
+    if (kind) *kind = t->entity ? t->entity->kind : 0;
+    if (id_lo) *id_lo = t->entity ? t->entity->lo : 0;
+    if (id_hi) *id_hi = t->entity ? t->entity->hi : 0;
+    P_END
+}
+
+capsmi_status capsmi_flatten_rel_types(capsmi_table* t, const char* type_col, int32_t ntypes, const int64_t* type_codes,
+                                       const char* const* out_cols, capsmi_table** out) {
+    return build(t, out, [&] {
+        const int tc = col_of(t, type_col);
+        REQUIRE(t->cols[tc].type == CAPSMI_STR, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                std::string("relationship type column `") + type_col + "` of type CTString");
+        REQUIRE(ntypes >= 0 && (ntypes == 0 || (type_codes && out_cols)), CAPSMI_ERR_ILLEGAL_ARGUMENT, "types");
+        materialize(t);
+        capsmi_session* s = t->sess;
+        HIP_CHECK(hipSetDevice(s->device));
+        auto* o = new capsmi_table();
+        std::unique_ptr<capsmi_table> g(o);
+        o->sess = s;
+        o->nrows = t->nrows;
+        for (size_t i = 0; i < t->cols.size(); ++i)
+            if ((int)i != tc) o->cols.push_back(t->cols[i]);
+        for (int k = 0; k < ntypes; ++k) {
+            need(out_cols[k], "type column name");
+            REQUIRE(find_col(o, out_cols[k]) < 0, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                    std::string("column '") + out_cols[k] + "' already exists");
+            // coalesce(type = code, false): a non-nullable flag (setNonNullable, CAPSTable.scala:198-200)
+            capsmi_expr prog[5] = {};
+            prog[0].op = CAPSMI_X_COL;
+            prog[0].arg = tc;
+            prog[1].op = CAPSMI_X_LIT;
+            prog[1].type = CAPSMI_STR;
+            prog[1].ival = type_codes[k];
+            prog[2].op = CAPSMI_X_EQ;
+            prog[3].op = CAPSMI_X_LIT;
+            prog[3].type = CAPSMI_BOOL;
+            prog[3].ival = 0;
+            prog[4].op = CAPSMI_X_COALESCE;
+            prog[4].arg = 2;
+            Column c;
+            c.name = out_cols[k];
+            c.data = dev_alloc(sizeof(int64_t) * (t->nrows > 0 ? t->nrows : 1), s);
+            eval_expr(s, t, 5, prog, P<int64_t>(c.data), nullptr, &c.type);
+            c.type = CAPSMI_BOOL;
+            o->cols.push_back(std::move(c));
+        }
+        return g.release();
+    });
+}
+
+}  // extern "C"

@@ -61,10 +61,21 @@ enum {
     CAPSMI_STR = 3   /* CTString, dictionary code */
 };
 
+/* Input-only value widths of capsmi_col_desc.type: widened at ingest the way
+ * DataFrameOps.withCypherCompatibleTypes lifts Spark columns (spark-cypher/.../impl/DataFrameOps.scala:185-198,
+ * SparkConversions.scala:162-168): Byte/Short/Integer -> Long, Float -> Double; a Boolean byte -> BOOL. */
+enum {
+    CAPSMI_IN_I32 = 16,  /* int32  -> CAPSMI_I64 */
+    CAPSMI_IN_I16 = 17,  /* int16  -> CAPSMI_I64 */
+    CAPSMI_IN_I8 = 18,   /* int8   -> CAPSMI_I64 */
+    CAPSMI_IN_F32 = 19,  /* float  -> CAPSMI_F64 */
+    CAPSMI_IN_BOOL8 = 20 /* uint8 0/1 -> CAPSMI_BOOL */
+};
+
 typedef struct {
     const char* name;
-    int32_t type;         /* CAPSMI_I64 ... CAPSMI_STR */
-    const void* data;     /* nrows x 8 bytes */
+    int32_t type;         /* CAPSMI_I64 ... CAPSMI_STR, or a CAPSMI_IN_* width */
+    const void* data;     /* nrows x 8 bytes (nrows x the CAPSMI_IN_* width) */
     const uint8_t* valid; /* nrows bytes (1 = non-null) or NULL (no nulls) */
 } capsmi_col_desc;
 
@@ -164,6 +175,11 @@ capsmi_status capsmi_session_set_profiling(capsmi_session* s, int32_t enabled);
 /* resolve pending events (synchronises) and report totals for kernel `name` ("hop1", "hop2",
  * "expand_filter", "bitmap_add", ...): launches and summed milliseconds; then the counters reset. */
 capsmi_status capsmi_session_kernel_time(capsmi_session* s, const char* name, int64_t* launches, double* total_ms);
+/* fused-path routing of lazy plans: enable / disable (default on; off = operator by operator, for
+ * A/B checks), and the number of plans routed to fused entry point `name` ("expand", "expand_count",
+ * "two_hop", "triangle", "var_length") since the session started */
+capsmi_status capsmi_session_set_fused(capsmi_session* s, int32_t enabled);
+capsmi_status capsmi_session_route_count(capsmi_session* s, const char* name, int64_t* count);
 
 /* ---- tables (CypherTable: okapi-api/.../api/table/CypherTable.scala:41-68) -------- */
 /* CAPSNodeTable/CAPSRelationshipTable ingest (spark-cypher/.../api/io/CAPSTable.scala:47-214): copies */
@@ -190,7 +206,39 @@ capsmi_status capsmi_table_export(const capsmi_table* t, int32_t col, void* host
 capsmi_status capsmi_table_column_device_ptr(const capsmi_table* t, int32_t col, const void** data,
                                              const uint8_t** valid);
 
-/* ---- Table[T] operators ------------------------------------------------------------- */
+/* ---- entity tables (the input contract) ------------------------------------------------
+ * CAPSNodeTable / CAPSRelationshipTable construction with EntityTable.verify
+ * (okapi-relational/.../api/io/EntityTable.scala:59-65, 105-131, 155-164): the id keys must be
+ * non-nullable Long columns ("id key", "start node", "end node"), optional-label and relationship-type
+ * flag columns non-nullable Boolean, and the columns in canonical order
+ *   node: [id, label flags..., properties sorted by name]
+ *   rel:  [id, source, target, type flags..., properties sorted by name]     (EntityMapping.scala:50)
+ * else CAPSMI_ERR_ILLEGAL_ARGUMENT.  The result shares the input's columns and is what the fused-path
+ * recogniser (below) treats as a scanned entity table; registration records the id range. */
+capsmi_status capsmi_node_table(capsmi_table* t, const char* id_col, int32_t nlabels, const char* const* label_cols,
+                                capsmi_table** out);
+capsmi_status capsmi_rel_table(capsmi_table* t, const char* id_col, const char* src_col, const char* dst_col,
+                               int32_t ntypes, const char* const* type_cols, capsmi_table** out);
+/* kind 0 = plain table, 1 = node table, 2 = relationship table; [*id_lo, *id_hi) = range of the ids
+ * (node) or of both endpoints (relationship) */
+capsmi_status capsmi_table_entity(const capsmi_table* t, int32_t* kind, int64_t* id_lo, int64_t* id_hi);
+/* CAPSRelationshipTable.fromMapping's relationship-type flattening (spark-cypher/.../api/io/CAPSTable.scala:189-204):
+ * the String column `type_col` (dictionary codes) becomes one non-nullable Boolean column per type,
+ * out_cols[i] = (type_col = type_codes[i]), and type_col is dropped. */
+capsmi_status capsmi_flatten_rel_types(capsmi_table* t, const char* type_col, int32_t ntypes, const int64_t* type_codes,
+                                       const char* const* out_cols, capsmi_table** out);
+
+/* ---- Table[T] operators -------------------------------------------------------------
+ * Operators are lazy, like DataFrameTable's Spark plans: each returns a table whose schema is known
+ * at once (name / type / nullability queries, errors for unknown columns or bad programs) and whose
+ * rows are computed when first needed -- capsmi_table_size, _export, _column_device_ptr,
+ * _fingerprint, or a graph entry point consuming it (RelationalCypherRecords.size -> df.count(),
+ * SparkTable.scala:59).  At that point the plan is matched against the fused graph kernels: joins of
+ * registered node / relationship tables in the Expand / ExpandInto / BoundedVarLengthExpand shapes
+ * RelationalPlanner emits (RelationalPlanner.scala:113-177, VarLengthExpandPlanner.scala:46-310),
+ * their uniqueness and node filters, and the aggregate or projection on top run as one fused call;
+ * anything else runs operator by operator.  A materialised table keeps its rows (shared sub-plans
+ * run once: the Cache analogue). */
 capsmi_status capsmi_cache(capsmi_table* t, capsmi_table** out);                         /* Table.scala:52  */
 capsmi_status capsmi_select(capsmi_table* t, int32_t ncols, const char* const* cols,
                             capsmi_table** out);                                        /* Table.scala:60  */

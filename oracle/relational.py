@@ -112,6 +112,27 @@ class NumpyTable:
             out[k] = Col_(c.type, vals, valid)
         return out
 
+    # ---- entity tables: EntityTable.verify (okapi-relational/.../api/io/EntityTable.scala:59-65, 105-164) --
+    def as_node_table(self, id_col, label_cols=()):
+        _verify_entity(self, [(id_col, "id key", I64)], [(c, "optional label", BOOL) for c in label_cols])
+        return self
+
+    def as_rel_table(self, id_col, src_col, dst_col, type_cols=()):
+        _verify_entity(self, [(id_col, "id key", I64), (src_col, "start node", I64), (dst_col, "end node", I64)],
+                       [(c, "relationship type", BOOL) for c in type_cols])
+        return self
+
+    def flatten_rel_types(self, type_col, types, out_cols):
+        """CAPSRelationshipTable.fromMapping's type flattening (CAPSTable.scala:189-204)."""
+        c = self.cols[type_col]
+        if c.type != STR:
+            raise OracleError(f"relationship type column `{type_col}` of type CTString")
+        out = OrderedDict((k, v) for k, v in self.cols.items() if k != type_col)
+        for t, name in zip(types, out_cols):
+            code = self.backend.dictionary.encode(t)
+            out[name] = Col_(BOOL, (c.valid & (c.values == code)).astype(np.int64), np.ones(self.n, dtype=bool))
+        return self._new(out, self.n)
+
     # ---- operators -------------------------------------------------------------------------
     def cache(self):
         return self
@@ -258,6 +279,23 @@ class NumpyTable:
 
 
 # ---- helpers ---------------------------------------------------------------------------------
+def _verify_entity(t: NumpyTable, keys, flags):
+    """EntityTable.verify: key columns non-nullable of the stated type, canonical column order
+    keys ++ flags ++ sorted properties (EntityMapping.allSourceKeys, EntityMapping.scala:50)."""
+    for name, what, ty in keys + flags:
+        if name not in t.cols:
+            raise OracleError(f"table with column key {name}")
+        c = t.cols[name]
+        if c.type != ty:
+            raise OracleError(f"{what} column `{name}` of type {'CTInteger' if ty == I64 else 'CTBoolean'}")
+        if not c.valid.all():
+            raise OracleError(f"non-nullable type for {what} column `{name}`")
+    fixed = [n for n, _, _ in keys + flags]
+    want = fixed + sorted(k for k in t.cols if k not in fixed)
+    if list(t.cols) != want:
+        raise OracleError(f"Columns: {', '.join(want)} expected, got Columns: {', '.join(t.cols)}")
+
+
 def _key_matrix(cols: Sequence[Col_], n: int, with_nulls: bool) -> np.ndarray:
     parts = []
     for c in cols:
