@@ -94,6 +94,8 @@ _SIGS = {
     "capsmi_table_column_type": (c_int32, [P, c_int32, POINTER(c_int32)]),
     "capsmi_table_column_index": (c_int32, [P, c_char_p, POINTER(c_int32)]),
     "capsmi_table_column_nullable": (c_int32, [P, c_int32, POINTER(c_int32)]),
+    "capsmi_table_schema": (c_int32, [P, POINTER(c_int32), c_char_p, c_size_t, POINTER(c_int32), POINTER(c_int32),
+                                      c_int32]),
     "capsmi_table_export": (c_int32, [P, c_int32, c_void_p, c_void_p, c_int64, c_int64]),
     "capsmi_table_column_device_ptr": (c_int32, [P, c_int32, PP, PP]),
     "capsmi_cache": (c_int32, [P, PP]),

@@ -203,19 +203,18 @@ class GpuTable:
         _lib.call("capsmi_table_size", self._h, ctypes.byref(v))
         return v.value
 
+    _MAXC = 256
+
     def _read_schema(self):
-        if self._schema is None:
+        if self._schema is None:  # one call for names and types (include/capsmi.h capsmi_table_schema)
             n = ctypes.c_int32()
-            _lib.call("capsmi_table_num_columns", self._h, ctypes.byref(n))
-            buf = ctypes.create_string_buffer(1024)
-            t = ctypes.c_int32()
-            names, types = [], []
-            for i in range(n.value):
-                _lib.call("capsmi_table_column_name", self._h, i, buf, 1024)
-                _lib.call("capsmi_table_column_type", self._h, i, ctypes.byref(t))
-                names.append(buf.value.decode())
-                types.append(t.value)
-            self._schema = (names, types)
+            buf = ctypes.create_string_buffer(16384)
+            types = (ctypes.c_int32 * self._MAXC)()
+            _lib.call("capsmi_table_schema", self._h, ctypes.byref(n), buf, len(buf), types, None, self._MAXC)
+            if n.value > self._MAXC:
+                raise _lib.NotImplementedException(f"table with {n.value} columns")
+            names = [x.decode() for x in buf.raw.split(b"\0")[:n.value]]
+            self._schema = (names, list(types[:n.value]))
         return self._schema
 
     @property

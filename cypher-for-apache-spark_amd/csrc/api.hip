@@ -659,7 +659,27 @@ capsmi_status capsmi_table_column_nullable(const capsmi_table* t, int32_t col, i
     need(t, "table");
     need(out, "out");
     REQUIRE(col >= 0 && col < (int)t->cols.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT, "column index out of range");
-    *out = t->cols[col].valid ? 1 : 0;
+    *out = t->cols[col].nullable() ? 1 : 0;
+    API_END
+}
+
+capsmi_status capsmi_table_schema(const capsmi_table* t, int32_t* ncols, char* names, size_t names_len, int32_t* types,
+                                  int32_t* nullable, int32_t max_cols) {
+    API_BEGIN
+    need(t, "table");
+    need(ncols, "ncols");
+    *ncols = (int32_t)t->cols.size();
+    size_t pos = 0;
+    for (size_t i = 0; i < t->cols.size() && (int32_t)i < max_cols; ++i) {
+        const std::string& nm = t->cols[i].name;
+        if (names) {
+            REQUIRE(pos + nm.size() + 1 <= names_len, CAPSMI_ERR_ILLEGAL_ARGUMENT, "name buffer too small");
+            std::memcpy(names + pos, nm.c_str(), nm.size() + 1);
+        }
+        pos += nm.size() + 1;
+        if (types) types[i] = t->cols[i].type;
+        if (nullable) nullable[i] = t->cols[i].nullable() ? 1 : 0;
+    }
     API_END
 }
 

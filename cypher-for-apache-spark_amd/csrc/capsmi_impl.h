@@ -127,6 +127,10 @@ struct capsmi_table {
     std::vector<capsmi::Column> cols;  // lazy: the schema only (name, type, lazy_nullable)
     std::shared_ptr<capsmi::PlanNode> plan;            // non-null until materialised (plan.hip)
     std::shared_ptr<const capsmi::EntityInfo> entity;  // registered entity table
+    // Table.cache on a relationship table (SparkTable.scala:240-246): fused routes keep the layouts
+    // they build from it (partitioned 2-hop layout per orientation and id window), freed with the table
+    bool keep_layouts = false;
+    std::map<std::string, std::shared_ptr<capsmi_relpart>> layouts;
     bool lazy() const { return (bool)plan; }
     int find(const std::string& n) const {
         for (size_t i = 0; i < cols.size(); ++i)

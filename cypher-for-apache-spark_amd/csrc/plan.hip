@@ -798,10 +798,27 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
         capsmi_bitmap* b = node_bitmap(s, P, c, P.pos_node[1], lo, hi, bs);
         capsmi_bitmap* cc = node_bitmap(s, P, c, P.pos_node[2], lo, hi, bs);
         if (!a || !b || !cc) return false;
+        // Cache analogue: relationship tables marked cache() keep the partitioned layout of the walk
+        const Scan& R = P.inst[P.hops[0].rel];
+        bool keep = !R.m.empty();
+        for (const Member& m : R.m) keep = keep && m.base->keep_layouts;
         for (int k : kinds) {
             int64_t x = 0;
             if (k == A_COUNT) {
                 check(capsmi_two_hop_count(s, (int32_t)nt, v0.t.data(), "s", "t", a, b, cc, &x));
+            } else if (keep) {
+                const bool rev = k == A_DISTINCT_START;  // distinct start = distinct end of the reversed walk
+                const std::string key = v0.sig + (rev ? "<" : ">") + std::to_string(lo) + ":" + std::to_string(hi);
+                auto& cache = R.m[0].base->layouts;
+                auto it = cache.find(key);
+                if (it == cache.end()) {
+                    capsmi_relpart* rp = nullptr;
+                    check(capsmi_relpart_build(s, (int32_t)nt, v0.t.data(), rev ? "t" : "s", rev ? "s" : "t", lo, hi, &rp));
+                    it = cache.emplace(key, std::shared_ptr<capsmi_relpart>(rp, [](capsmi_relpart* q) {
+                                           capsmi_relpart_release(q);
+                                       })).first;
+                }
+                check(capsmi_two_hop_count_distinct_part(s, it->second.get(), rev ? cc : a, b, rev ? a : cc, &x));
             } else if (k == A_DISTINCT_END) {
                 check(capsmi_two_hop_count_distinct(s, (int32_t)nt, v0.t.data(), "s", "t", a, b, cc, &x));
             } else {  // distinct start: the same walk over the reversed relationships
@@ -1060,8 +1077,10 @@ static capsmi_status build(capsmi_table* t, capsmi_table** out, const std::funct
 }
 
 capsmi_status capsmi_cache(capsmi_table* t, capsmi_table** out) {
-    // a table keeps its rows once computed (DataFrameTable.cache, SparkTable.scala:240-246): same handle
+    // a table keeps its rows once computed (DataFrameTable.cache, SparkTable.scala:240-246): same handle;
+    // a cached relationship table also keeps the fused layouts built from it
     return build(t, out, [&] {
+        t->keep_layouts = true;
         t->refs.fetch_add(1);
         return t;
     });

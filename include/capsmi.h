@@ -198,6 +198,11 @@ capsmi_status capsmi_table_column_name(const capsmi_table* t, int32_t col, char*
 capsmi_status capsmi_table_column_type(const capsmi_table* t, int32_t col, int32_t* out);
 capsmi_status capsmi_table_column_index(const capsmi_table* t, const char* name, int32_t* out);
 capsmi_status capsmi_table_column_nullable(const capsmi_table* t, int32_t col, int32_t* out);
+/* the whole schema in one call (no materialisation): *ncols columns; names NUL-separated into
+ * `names` (names_len bytes), types[i] and nullable[i] for i < min(*ncols, max_cols); ILLEGAL_ARGUMENT
+ * if the names do not fit */
+capsmi_status capsmi_table_schema(const capsmi_table* t, int32_t* ncols, char* names, size_t names_len, int32_t* types,
+                                  int32_t* nullable, int32_t max_cols);
 /* CypherTable.rows / CAPSRecords.collect (SparkTable.scala:55-57, CAPSRecords.scala:136-143):
  * copies rows [offset, offset+n) of one column to the host; host_valid may be NULL */
 capsmi_status capsmi_table_export(const capsmi_table* t, int32_t col, void* host_data, uint8_t* host_valid,
