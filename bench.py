@@ -134,10 +134,60 @@ def pmc_traffic(kernel, workload):
     return None
 
 
+def shard_diagnostic(args):
+    """--shard-of N on one GPU: every rank's owner(target) shard of the C3 cold step, timed one after
+    the other (kernels only: the frontier exchange and the count all-reduce are not run, the node scan
+    is the whole table).  Reports per-rank times and the max -- the projected N-GPU step before the
+    collectives.  Not the metric."""
+    import torch
+    from capsmi import Session, graph
+    N = args.shard_of
+    torch.cuda.set_device(0)
+    sess = Session(0)
+    sess.set_stream(torch.cuda.current_stream().cuda_stream)
+    scale, ef = args.scale, args.edge_factor
+    n, m_total = 1 << scale, ef << scale
+    nw = (n + 31) // 32
+    persons = graph.rmat_nodes(sess, scale, graph.NODES_ALL)
+    mid = torch.zeros(2 * nw, dtype=torch.int32, device="cuda")
+    scratch = torch.zeros(nw, dtype=torch.int32, device="cuda")
+    dstw = torch.zeros(nw, dtype=torch.int32, device="cuda")
+    per_rank, rows = [], []
+    for r in range(N):
+        rels = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42, part_col=graph.PART_TARGET, part=r,
+                               nparts=N)
+        wb, we = graph.owner_words(n, r, N)
+
+        def step():
+            p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")
+            rp = graph.RelPartition.build_mark_mid(sess, [rels], p, p, mid.data_ptr(), scratch.data_ptr())
+            rp.mark_dst(p, p, mid.data_ptr(), dstw.data_ptr())
+            rp.release()
+            return graph.words_popcount(sess, dstw.data_ptr(), wb, we)
+
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
+        rows.append(rels.size)
+        del rels
+    mean = sum(per_rank) / N
+    print(json.dumps({"diagnostic": f"C3 cold step, every rank's owner(target) shard of {N} on one GPU, no exchange",
+                      "scale": scale, "per_rank_ms": per_rank, "max_ms": max(per_rank), "mean_ms": mean,
+                      "imbalance_max_over_mean": max(per_rank) / mean, "rels_per_rank": rows}), flush=True)
+    sess.close()
+
+
 def main():
     args = parse()
     if args.workload != "c3":
         return run_single(args)
+    if args.shard_of and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        return shard_diagnostic(args)
     import torch
     import torch.distributed as dist
 
@@ -172,6 +222,11 @@ def main():
     rels = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42,
                            part_col=graph.PART_TARGET if shards > 1 else graph.PART_NONE, part=rank, nparts=shards)
     persons = graph.rmat_nodes(sess, scale, graph.NODES_ALL)
+    if distributed:  # each rank holds (and scans) the :Person rows of the ids it owns
+        from capsmi.expr import Ands, BinOp, Col, Lit
+        own_lo, own_hi = 32 * wb, min(32 * we, n)
+        persons = persons.filter(Ands((BinOp(">=", Col("id"), Lit(own_lo)), BinOp("<", Col("id"), Lit(own_hi))))) \
+            .as_node_table("id")
     m_local = rels.size
     sess.sync()
     ingest_s = time.perf_counter() - t0
@@ -184,6 +239,22 @@ def main():
     k_own = we - wb
     send = torch.empty(2, k_own, dtype=torch.int32, device="cuda")
     recv = torch.empty(world * 2, k_own, dtype=torch.int32, device="cuda")  # rank-major (rank, X1|X2) rows
+    nsend = torch.empty(k_own, dtype=torch.int32, device="cuda")
+    nrecv = torch.empty(world * k_own, dtype=torch.int32, device="cuda")
+    flag = torch.ones(1, dtype=torch.int32, device="cuda")
+
+    def node_scan():
+        """The :Person scan (a, b, c).  N > 1: every rank scans its owned rows into its slice of the
+        bitmap, then one all-gather of the owned word slices (2^26 ids: 8 MiB in all) completes it."""
+        p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")
+        if not distributed:
+            return p
+        p.copy_words(wb, we, nsend.data_ptr(), to_bitmap=False)
+        dist.all_gather_into_tensor(nrecv, nsend)
+        p.copy_words(0, nw, nrecv.data_ptr(), to_bitmap=True)
+        flag.fill_(1 if p.stats()[1] else 0)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return p.refresh(bool(flag.item()))
 
     def exchange_and_finish(p, mark_dst):
         if distributed:  # hop-1 frontier: every rank needs X1/X2 of every middle node; one all-gather
@@ -199,7 +270,7 @@ def main():
         return local_cnt
 
     def step_cold():
-        p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")  # node scan of :Person (a, b, c)
+        p = node_scan()  # node scan of :Person (a, b, c)
         rp = graph.RelPartition.build_mark_mid(sess, [rels], p, p, mid.data_ptr(), scratch.data_ptr())
         r = exchange_and_finish(p, lambda q: rp.mark_dst(q, q, mid.data_ptr(), dstw.data_ptr()))
         rp.release()
@@ -209,12 +280,12 @@ def main():
         if "rp" not in cached:
             cached["rp"] = graph.RelPartition(sess, [rels], 0, n)
         rp = cached["rp"]
-        p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")
+        p = node_scan()
         rp.mark_mid(p, p, mid.data_ptr(), scratch.data_ptr())
         return exchange_and_finish(p, lambda q: rp.mark_dst(q, q, mid.data_ptr(), dstw.data_ptr()))
 
     def step_stream():
-        p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")
+        p = node_scan()
         graph.two_hop_mark_mid(sess, [rels], p, p, mid.data_ptr(), scratch.data_ptr())
         return exchange_and_finish(p, lambda q: graph.two_hop_mark_dst(sess, [rels], q, q, mid.data_ptr(),
                                                                           dstw.data_ptr()))
@@ -286,7 +357,8 @@ def main():
     fx = fixture(f"c3_s{scale}") if ef == 16 else None
     if rank == 0:
         full = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42) if distributed else rels
-        p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")
+        all_persons = graph.rmat_nodes(sess, scale, graph.NODES_ALL) if distributed else persons
+        p = graph.NodeBitmap(sess, 0, n).add_scan(all_persons, "id")
         matched = graph.two_hop_count(sess, [full], p, p, p)
         answers = {m: r[1] for m, r in results.items()}
         if shards != world:

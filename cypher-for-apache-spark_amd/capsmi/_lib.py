@@ -116,6 +116,9 @@ _SIGS = {
     "capsmi_bitmap_add_scan": (c_int32, [P, P, c_char_p, c_int32, POINTER(CapsmiExpr)]),
     "capsmi_bitmap_stats": (c_int32, [P, POINTER(c_int64), POINTER(c_int32)]),
     "capsmi_bitmap_release": (c_int32, [P]),
+    "capsmi_bitmap_words": (c_int32, [P, PP, POINTER(c_int64)]),
+    "capsmi_bitmap_refresh": (c_int32, [P, c_int32]),
+    "capsmi_bitmap_copy_words": (c_int32, [P, c_int64, c_int64, c_void_p, c_int32]),
     "capsmi_expand_filter": (c_int32, [P, P, c_char_p, c_char_p, P, P, c_int32, STRS, STRS, PP]),
     "capsmi_two_hop_count_distinct": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, P, P, POINTER(c_int64)]),
     "capsmi_two_hop_count": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, P, P, POINTER(c_int64)]),

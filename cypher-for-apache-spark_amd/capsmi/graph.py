@@ -50,6 +50,22 @@ class NodeBitmap:
         _lib.call("capsmi_bitmap_stats", self._h, ctypes.byref(bits), ctypes.byref(uniq))
         return bits.value, bool(uniq.value)
 
+    def words_ptr(self) -> int:
+        """Device address of the bitmap's uint32 words (include/capsmi.h capsmi_bitmap_words)."""
+        p, n = ctypes.c_void_p(), ctypes.c_int64()
+        _lib.call("capsmi_bitmap_words", self._h, ctypes.byref(p), ctypes.byref(n))
+        return p.value or 0
+
+    def copy_words(self, w_begin: int, w_end: int, ext_ptr: int, to_bitmap: bool) -> None:
+        """Device copy of words [w_begin, w_end) between the bitmap and a caller buffer (e.g. a torch
+        tensor's data_ptr), ordered on the session stream."""
+        _lib.call("capsmi_bitmap_copy_words", self._h, w_begin, w_end, ctypes.c_void_p(ext_ptr), 1 if to_bitmap else 0)
+
+    def refresh(self, unique_rows: bool = True) -> "NodeBitmap":
+        """Re-derive the set-bit count after the words were written (e.g. all-gathered)."""
+        _lib.call("capsmi_bitmap_refresh", self._h, 1 if unique_rows else 0)
+        return self
+
     def release(self) -> None:
         if self._h:
             _lib.call("capsmi_bitmap_release", self._h)

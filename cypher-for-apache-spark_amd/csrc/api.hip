@@ -1114,6 +1114,41 @@ capsmi_status capsmi_bitmap_stats(capsmi_bitmap* b, int64_t* set_bits, int32_t* 
     API_END
 }
 
+capsmi_status capsmi_bitmap_words(capsmi_bitmap* b, uint32_t** words, int64_t* nwords) {
+    API_BEGIN
+    need(b, "bitmap");
+    if (words) *words = P<uint32_t>(b->words);
+    if (nwords) *nwords = b->nwords;
+    b->set_bits = -1;  // the caller may rewrite the words
+    API_END
+}
+
+capsmi_status capsmi_bitmap_refresh(capsmi_bitmap* b, int32_t unique_rows) {
+    API_BEGIN
+    need(b, "bitmap");
+    use_device(b->sess);
+    b->set_bits = words_popcount(b->sess, P<uint32_t>(b->words), 0, b->nwords);
+    b->full = b->set_bits == b->hi - b->lo;
+    b->any_dup = unique_rows == 0;
+    API_END
+}
+
+capsmi_status capsmi_bitmap_copy_words(capsmi_bitmap* b, int64_t w_begin, int64_t w_end, uint32_t* ext,
+                                       int32_t to_bitmap) {
+    API_BEGIN
+    need(b, "bitmap");
+    need(ext, "ext");
+    REQUIRE(w_begin >= 0 && w_begin <= w_end && w_end <= b->nwords, CAPSMI_ERR_ILLEGAL_ARGUMENT, "word range");
+    use_device(b->sess);
+    uint32_t* w = P<uint32_t>(b->words) + w_begin;
+    const size_t bytes = sizeof(uint32_t) * (size_t)(w_end - w_begin);
+    if (bytes)
+        HIP_CHECK(hipMemcpyAsync(to_bitmap ? (void*)w : (void*)ext, to_bitmap ? (const void*)ext : (const void*)w, bytes,
+                                 hipMemcpyDeviceToDevice, b->sess->stream));
+    if (to_bitmap) b->set_bits = -1;
+    API_END
+}
+
 capsmi_status capsmi_bitmap_release(capsmi_bitmap* b) {
     API_BEGIN
     if (b) {

@@ -287,6 +287,16 @@ capsmi_status capsmi_bitmap_add_scan(capsmi_bitmap* b, capsmi_table* nodes, cons
  * ScanGraph.scala:72-76) */
 capsmi_status capsmi_bitmap_stats(capsmi_bitmap* b, int64_t* set_bits, int32_t* unique_rows);
 capsmi_status capsmi_bitmap_release(capsmi_bitmap* b);
+/* the bitmap's device words (uint32, bit i of word w <-> id lo + 32w + i) for collectives: a rank
+ * scans its owned node rows, the ranks all-gather their owned word slices into these words, then
+ * capsmi_bitmap_refresh re-derives the set-bit count (synchronises); `unique_rows` states whether
+ * every rank's scan was duplicate-free (the all-reduced AND of capsmi_bitmap_stats) */
+capsmi_status capsmi_bitmap_words(capsmi_bitmap* b, uint32_t** words, int64_t* nwords);
+capsmi_status capsmi_bitmap_refresh(capsmi_bitmap* b, int32_t unique_rows);
+/* stream-ordered device copy of words [w_begin, w_end): to_bitmap = 0 copies bitmap -> ext,
+ * 1 copies ext -> bitmap (ext: a caller device buffer of w_end - w_begin words) */
+capsmi_status capsmi_bitmap_copy_words(capsmi_bitmap* b, int64_t w_begin, int64_t w_end, uint32_t* ext,
+                                       int32_t to_bitmap);
 
 /* 1-hop Expand + node filters, fused (C2):
  *   MATCH (a)-[r]->(b) WHERE src_ok(a) AND dst_ok(b)

@@ -11,4 +11,4 @@ for f in sys.argv[1:]:
           f"frac={d['roofline'] and round(d['roofline']['frac'], 3)}  query_frac={q.get('query_frac_of_peak', 0):.3f}")
     for k, v in q.get("kernel_ms", {}).items():
         print(f"    {k:22s} {v:8.3f} ms")
-    print("    check:", q.get("check_vs_unpartitioned"))
+    print("    check:", q.get("check_vs_fixture"))
