@@ -157,6 +157,7 @@ _SIGS = {
     "capsmi_table_entity": (c_int32, [P, POINTER(c_int32), POINTER(c_int64), POINTER(c_int64)]),
     "capsmi_flatten_rel_types": (c_int32, [P, c_char_p, c_int32, POINTER(c_int64), STRS, PP]),
     "capsmi_session_set_fused": (c_int32, [P, c_int32]),
+    "capsmi_graph_compact": (c_int32, [P, c_int32, PP, c_int32, PP, POINTER(c_int64)]),
     "capsmi_session_route_count": (c_int32, [P, c_char_p, POINTER(c_int64)]),
 }
 

@@ -109,4 +109,5 @@ def fs_graph(backend, graph_dir: str, extra_strings=()) -> ScanGraph:
         t = t.as_node_table(ID) if kind == "node" else t.as_rel_table(ID, SRC, DST)
         et = EntityTable(kind, labels, dict(props), t)
         (nodes if kind == "node" else rels).append(et)
+    backend.compact_if_sparse([e.table for e in nodes], [e.table for e in rels])
     return ScanGraph(backend, nodes, rels)

@@ -44,8 +44,10 @@ def edge_list_tables(session: Session, src: np.ndarray, dst: np.ndarray) -> Tupl
                           ColumnData("target", I64, dst)])
     s = rels.select("source").withColumnRenamed("source", "id")
     t = rels.select("target").withColumnRenamed("target", "id")
-    nodes = s.unionAll(t).distinct()
-    return nodes.as_node_table("id"), rels.as_rel_table("id", "source", "target")
+    nodes = s.unionAll(t).distinct().as_node_table("id")
+    rels = rels.as_rel_table("id", "source", "target")
+    session.compact_if_sparse([nodes], [rels])  # edge-list ids are arbitrary Longs
+    return nodes, rels
 
 
 def edge_list_graph(session: Session, path: str, delimiter: str = " ") -> Tuple[GpuTable, GpuTable]:

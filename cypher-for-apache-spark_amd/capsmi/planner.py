@@ -170,6 +170,7 @@ class ScanGraph:
             for k in sorted(pt):
                 cols.append(_column(k, pt[k], [r.props.get(k) for r in rs], enc))
             rels.append(EntityTable("rel", frozenset([t]), pt, backend.table(cols).as_rel_table(ID, SRC, DST)))
+        backend.compact_if_sparse([e.table for e in nodes], [e.table for e in rels])
         return ScanGraph(backend, nodes, rels)
 
     # ---- scans --------------------------------------------------------------------------

@@ -154,6 +154,24 @@ class Session:
     def encode_str(self, s: str) -> int:
         return self.dictionary.encode(s)
 
+    def compact_graph(self, nodes: Sequence["GpuTable"], rels: Sequence["GpuTable"]) -> int:
+        """Dense ids for one graph's registered node / relationship tables (include/capsmi.h
+        capsmi_graph_compact); returns the number of dense ids."""
+        na = (ctypes.c_void_p * max(1, len(nodes)))(*[t.handle for t in nodes])
+        ra = (ctypes.c_void_p * max(1, len(rels)))(*[t.handle for t in rels])
+        n = ctypes.c_int64()
+        _lib.call("capsmi_graph_compact", self._h, len(nodes), na, len(rels), ra, ctypes.byref(n))
+        return n.value
+
+    def compact_if_sparse(self, nodes: Sequence["GpuTable"], rels: Sequence["GpuTable"]) -> bool:
+        """Compact when the tables' ids do not fit the fused kernels' window of 2^30 ids."""
+        spans = [t.entity() for t in list(nodes) + list(rels)]
+        spans = [(lo, hi) for k, lo, hi in spans if k and hi > lo]
+        if not spans or max(h for _, h in spans) - min(l for l, _ in spans) <= (1 << 30):
+            return False
+        self.compact_graph(nodes, rels)
+        return True
+
     def set_fused(self, enabled: bool) -> None:
         """Route lazy plans of the Expand shapes to the fused kernels (default) or run them operator
         by operator (include/capsmi.h capsmi_session_set_fused)."""

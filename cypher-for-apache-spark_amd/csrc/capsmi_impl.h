@@ -78,6 +78,14 @@ struct EntityInfo {
 };
 struct PlanNode;  // lazy Table[T] operator (plan.hip)
 
+// Dense id space of one graph (capsmi_graph_compact): every node id and relationship endpoint of
+// the graph's entity tables numbered 0..n-1; orig[d] is the Long id of dense id d.  The fused
+// routes run on dense ids when the Long ids do not fit one window of 2^30 ids.
+struct DenseIds {
+    int64_t n = 0;
+    Buf orig;
+};
+
 }  // namespace capsmi
 
 struct capsmi_session {
@@ -130,6 +138,9 @@ struct capsmi_table {
     // Table.cache on a relationship table (SparkTable.scala:240-246): fused routes keep the layouts
     // they build from it (partitioned 2-hop layout per orientation and id window), freed with the table
     bool keep_layouts = false;
+    // dense ids of a compacted graph: node tables `did`, relationship tables `dsrc` / `ddst` (int64 per row)
+    std::shared_ptr<capsmi::DenseIds> dense;
+    capsmi::Column did, dsrc, ddst;
     std::map<std::string, std::shared_ptr<capsmi_relpart>> layouts;
     bool lazy() const { return (bool)plan; }
     int find(const std::string& n) const {

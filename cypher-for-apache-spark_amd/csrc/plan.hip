@@ -594,6 +594,53 @@ bool classify(const Path& P, Classified& c) {
     return true;
 }
 
+// The id domain the fused kernels run on: the Long ids' window when it holds at most 2^30 ids,
+// else the dense ids of a compacted graph (capsmi_graph_compact) shared by every scanned table.
+thread_local const DenseIds* g_dense = nullptr;  // domain of the route being planned (one at a time)
+
+bool id_window(const std::vector<Path>& B, int64_t* lo, int64_t* hi) {
+    int64_t l = INT64_MAX, h = INT64_MIN;
+    const DenseIds* d = nullptr;
+    bool all_dense = true;
+    for (const Path& P : B)
+        for (const Scan& sc : P.inst)
+            for (const Member& m : sc.m) {
+                if (!m.base->dense || (d && m.base->dense.get() != d)) all_dense = false;
+                else d = m.base->dense.get();
+                if (m.base->entity->rows == 0) continue;
+                l = std::min(l, m.base->entity->lo);
+                h = std::max(h, m.base->entity->hi);
+            }
+    g_dense = nullptr;
+    if (l < h && (uint64_t)(h - l) <= (uint64_t(1) << 30)) {
+        *lo = l;
+        *hi = h;
+        return true;
+    }
+    if (all_dense && d && d->n > 0 && (uint64_t)d->n <= (uint64_t(1) << 30)) {
+        g_dense = d;
+        *lo = 0;
+        *hi = d->n;
+        return true;
+    }
+    return false;
+}
+
+// a zero-copy view of a base table with its dense key columns appended (dense domain only)
+capsmi_table* dense_view(const capsmi_table* base) {
+    auto* x = new capsmi_table();
+    x->sess = base->sess;
+    x->nrows = base->nrows;
+    x->cols = base->cols;
+    Column a = base->did, b = base->dsrc, c = base->ddst;
+    a.name = "__dense_id";
+    b.name = "__dense_src";
+    c.name = "__dense_dst";
+    if (base->entity->kind == 1) x->cols.push_back(a);
+    else { x->cols.push_back(b); x->cols.push_back(c); }
+    return x;
+}
+
 // ---- bitmaps of node scans (+ predicates) ------------------------------------------------------
 struct BitmapSet {
     std::vector<std::pair<std::string, capsmi_bitmap*>> made;
@@ -635,8 +682,16 @@ capsmi_bitmap* node_bitmap(capsmi_session* s, const Path& P, const Classified& c
     bs.made.push_back({key, b});
     for (size_t i = 0; i < sc.m.size(); ++i) {
         const Member& m = sc.m[i];
-        const char* idn = m.base->cols[m.base->entity->id].name.c_str();
-        check(capsmi_bitmap_add_scan(b, m.base, idn, (int32_t)progs[i].size(), progs[i].empty() ? nullptr : progs[i].data()));
+        const capsmi_expr* pr = progs[i].empty() ? nullptr : progs[i].data();
+        if (g_dense) {  // predicate columns keep their indices: the dense id is appended
+            capsmi_table* v = dense_view(m.base);
+            const capsmi_status st = capsmi_bitmap_add_scan(b, v, "__dense_id", (int32_t)progs[i].size(), pr);
+            capsmi_table_release(v);
+            check(st);
+        } else {
+            check(capsmi_bitmap_add_scan(b, m.base, m.base->cols[m.base->entity->id].name.c_str(),
+                                         (int32_t)progs[i].size(), pr));
+        }
     }
     return b->any_dup ? nullptr : b;
 }
@@ -659,6 +714,10 @@ void rel_views(const Path& P, const Hop& h, RelViews& v) {
         x->sess = m.base->sess;
         x->nrows = m.base->nrows;
         Column a = m.base->cols[fc], b = m.base->cols[tc];
+        if (g_dense) {
+            a = h.from_role == ROLE_SRC ? m.base->dsrc : m.base->ddst;
+            b = h.to_role == ROLE_SRC ? m.base->dsrc : m.base->ddst;
+        }
         a.name = "s";
         b.name = "t";
         x->cols = {a, b};
@@ -666,27 +725,11 @@ void rel_views(const Path& P, const Hop& h, RelViews& v) {
         std::string k(reinterpret_cast<const char*>(&m.base), sizeof(m.base));
         k += char(fc);
         k += char(tc);
+        k += g_dense ? 'D' : 'L';
         sig.push_back(k);
     }
     std::sort(sig.begin(), sig.end());
     for (auto& k : sig) v.sig += k;
-}
-
-// id window covering every scanned node and relationship endpoint of the path(s)
-bool id_window(const std::vector<Path>& B, int64_t* lo, int64_t* hi) {
-    int64_t l = INT64_MAX, h = INT64_MIN;
-    for (const Path& P : B)
-        for (const Scan& sc : P.inst)
-            for (const Member& m : sc.m) {
-                if (m.base->entity->rows == 0) continue;
-                l = std::min(l, m.base->entity->lo);
-                h = std::max(h, m.base->entity->hi);
-            }
-    if (l >= h) return false;
-    if ((uint64_t)(h - l) > (uint64_t(1) << 30)) return false;
-    *lo = l;
-    *hi = h;
-    return true;
 }
 
 bool id_like(const Path& P, const Role& r) {  // a non-null id / endpoint column
@@ -901,6 +944,14 @@ bool fused_var_length(capsmi_session* s, const capsmi_table* in, const PlanNode&
     if (l < 1 || u > 3 || u - l + 1 != (int)lens.size()) return false;
     check(capsmi_var_length_count(s, (int32_t)views.t.size(), views.t.data(), "s", "t", abm, bbm, l, u, g.a[0].c_str(),
                                   ag.output.c_str(), out));
+    if (g_dense) {  // start ids back to the graph's Long ids
+        capsmi_table* r = *out;
+        Column& c = r->cols[0];
+        Buf ids = dev_alloc(sizeof(int64_t) * (r->nrows > 0 ? r->nrows : 1), s);
+        gather_col(P<int64_t>(g_dense->orig), nullptr, c.d(), r->nrows, ::capsmi::P<int64_t>(ids), nullptr, s->stream);
+        c.data = ids;
+        c.offset = 0;
+    }
     route(s, "var_length");
     return true;
 }
@@ -956,10 +1007,15 @@ bool fused_projection(capsmi_session* s, const capsmi_table* t, const std::vecto
         const char* any[1] = {m.base->cols[fc].name.c_str()};
         const char* anyn[1] = {"c_"};
         capsmi_table* o = nullptr;
-        if (ocols.empty()) check(capsmi_expand_filter(s, m.base, m.base->cols[fc].name.c_str(), m.base->cols[tc].name.c_str(),
-                                                      a, b, 1, any, anyn, &o));
-        else check(capsmi_expand_filter(s, m.base, m.base->cols[fc].name.c_str(), m.base->cols[tc].name.c_str(), a, b,
-                                        (int32_t)ocols.size(), ocols.data(), onames.data(), &o));
+        // node tests on the (dense) endpoint columns, projections of the original columns
+        capsmi_table* tab = g_dense ? dense_view(m.base) : m.base;
+        const char* tf = g_dense ? (h.from_role == ROLE_SRC ? "__dense_src" : "__dense_dst") : m.base->cols[fc].name.c_str();
+        const char* tt = g_dense ? (h.to_role == ROLE_SRC ? "__dense_src" : "__dense_dst") : m.base->cols[tc].name.c_str();
+        capsmi_status st;
+        if (ocols.empty()) st = capsmi_expand_filter(s, tab, tf, tt, a, b, 1, any, anyn, &o);
+        else st = capsmi_expand_filter(s, tab, tf, tt, a, b, (int32_t)ocols.size(), ocols.data(), onames.data(), &o);
+        if (g_dense) capsmi_table_release(tab);
+        check(st);
         parts.push_back(o);
     }
     // assemble the output schema: data columns from the kernel, constants filled
@@ -1458,6 +1514,171 @@ capsmi_status capsmi_rel_table(capsmi_table* t, const char* id_col, const char* 
         }
         return register_entity(t, 2, {id_col, src_col, dst_col}, flags);
     });
+}
+
+}  // extern "C"
+
+namespace capsmi {
+namespace {
+
+__global__ void k_dense_of(const int64_t* __restrict__ slot_of_probe, const int64_t* __restrict__ slot_row,
+                           const int64_t* __restrict__ gid_of_row, int64_t n, int64_t* __restrict__ out,
+                           uint8_t* __restrict__ miss) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t sl = slot_of_probe[i];
+        out[i] = sl >= 0 ? gid_of_row[slot_row[sl]] : -1;
+        miss[i] = sl < 0;
+    }
+}
+
+__global__ void k_place_dense(const int64_t* __restrict__ idx, const int64_t* __restrict__ gid, int64_t n, int64_t base,
+                              int64_t* __restrict__ out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[idx[i]] = base + gid[i];
+}
+
+unsigned grid_of(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 65536)); }
+
+KeyCols one_key(const int64_t* d) {
+    KeyCols k;
+    k.n = 1;
+    for (int i = 0; i < kMaxKeys; ++i) { k.data[i] = nullptr; k.valid[i] = nullptr; }
+    k.data[0] = d;
+    return k;
+}
+
+}  // namespace
+
+void graph_compact(capsmi_session* s, const std::vector<capsmi_table*>& nodes, const std::vector<capsmi_table*>& rels,
+                   int64_t* n_out) {
+    hipStream_t st = s->stream;
+    int64_t nn = 0;
+    for (auto* t : nodes) nn += t->nrows;
+    // node ids of every node table, one key column
+    Buf keys = dev_alloc(sizeof(int64_t) * (nn > 0 ? nn : 1), s);
+    int64_t off = 0;
+    for (auto* t : nodes) {
+        if (t->nrows) HIP_CHECK(hipMemcpyAsync(::capsmi::P<int64_t>(keys) + off, t->cols[t->entity->id].d(),
+                                               sizeof(int64_t) * t->nrows, hipMemcpyDeviceToDevice, st));
+        off += t->nrows;
+    }
+    const KeyCols kc = one_key(::capsmi::P<int64_t>(keys));
+    HashTable ht;
+    Buf sor, gid, rep;
+    hash_build(s, kc, nn, false, ht, sor);
+    const int64_t ng = nn > 0 ? hash_group_ids(s, ht, sor, nn, gid, rep) : 0;
+    // endpoints: probe the node ids; endpoints of no node table (dangling) are numbered after them
+    struct Miss { Buf idx; int64_t n; Buf dense; };
+    std::vector<Miss> miss;
+    std::vector<std::pair<Buf, Buf>> rel_dense;
+    for (auto* t : rels) {
+        const int64_t m = t->nrows;
+        Buf d[2];
+        for (int k = 0; k < 2; ++k) {
+            const Column& c = t->cols[k == 0 ? t->entity->src : t->entity->dst];
+            d[k] = dev_alloc(sizeof(int64_t) * (m > 0 ? m : 1), s);
+            if (m == 0) continue;
+            Buf sop, fl = dev_alloc(m, s);
+            hash_probe(s, one_key(c.d()), kc, m, ht, sop);
+            hipLaunchKernelGGL(k_dense_of, dim3(grid_of(m)), dim3(256), 0, st, ::capsmi::P<int64_t>(sop),
+                               ::capsmi::P<int64_t>(ht.slot_row), ::capsmi::P<int64_t>(gid), m,
+                               ::capsmi::P<int64_t>(d[k]), ::capsmi::P<uint8_t>(fl));
+            HIP_CHECK(hipGetLastError());
+            Miss x;
+            x.n = flags_to_indices(s, ::capsmi::P<uint8_t>(fl), m, x.idx);
+            x.dense = d[k];
+            if (x.n > 0) {
+                // remember the missing keys next to their row indices
+                Buf mk = dev_alloc(sizeof(int64_t) * x.n, s);
+                gather_col(c.d(), nullptr, ::capsmi::P<int64_t>(x.idx), x.n, ::capsmi::P<int64_t>(mk), nullptr, st);
+                miss.push_back(x);
+                miss.push_back(Miss{mk, -1, Buf()});  // keys of the entry before
+            }
+        }
+        rel_dense.push_back({d[0], d[1]});
+    }
+    int64_t nm = 0;
+    for (size_t i = 0; i < miss.size(); i += 2) nm += miss[i].n;
+    Buf mkeys = dev_alloc(sizeof(int64_t) * (nm > 0 ? nm : 1), s);
+    off = 0;
+    for (size_t i = 0; i < miss.size(); i += 2) {
+        HIP_CHECK(hipMemcpyAsync(::capsmi::P<int64_t>(mkeys) + off, ::capsmi::P<int64_t>(miss[i + 1].idx),
+                                 sizeof(int64_t) * miss[i].n, hipMemcpyDeviceToDevice, st));
+        off += miss[i].n;
+    }
+    int64_t ng2 = 0;
+    Buf gid2, rep2;
+    if (nm > 0) {
+        HashTable h2;
+        Buf sor2;
+        hash_build(s, one_key(::capsmi::P<int64_t>(mkeys)), nm, false, h2, sor2);
+        ng2 = hash_group_ids(s, h2, sor2, nm, gid2, rep2);
+        off = 0;
+        for (size_t i = 0; i < miss.size(); i += 2) {
+            hipLaunchKernelGGL(k_place_dense, dim3(grid_of(miss[i].n)), dim3(256), 0, st, ::capsmi::P<int64_t>(miss[i].idx),
+                               ::capsmi::P<int64_t>(gid2) + off, miss[i].n, ng, ::capsmi::P<int64_t>(miss[i].dense));
+            off += miss[i].n;
+        }
+        HIP_CHECK(hipGetLastError());
+    }
+    auto D = std::make_shared<DenseIds>();
+    D->n = ng + ng2;
+    D->orig = dev_alloc(sizeof(int64_t) * (D->n > 0 ? D->n : 1), s);
+    if (ng) gather_col(::capsmi::P<int64_t>(keys), nullptr, ::capsmi::P<int64_t>(rep), ng, ::capsmi::P<int64_t>(D->orig),
+                       nullptr, st);
+    if (ng2) gather_col(::capsmi::P<int64_t>(mkeys), nullptr, ::capsmi::P<int64_t>(rep2), ng2,
+                        ::capsmi::P<int64_t>(D->orig) + ng, nullptr, st);
+    off = 0;
+    for (auto* t : nodes) {
+        t->dense = D;
+        t->did = Column();
+        t->did.type = CAPSMI_I64;
+        t->did.data = gid;
+        t->did.offset = off;
+        off += t->nrows;
+    }
+    for (size_t i = 0; i < rels.size(); ++i) {
+        auto* t = rels[i];
+        t->dense = D;
+        t->dsrc = Column();
+        t->dsrc.type = CAPSMI_I64;
+        t->dsrc.data = rel_dense[i].first;
+        t->ddst = Column();
+        t->ddst.type = CAPSMI_I64;
+        t->ddst.data = rel_dense[i].second;
+    }
+    HIP_CHECK(hipStreamSynchronize(st));
+    *n_out = D->n;
+}
+
+}  // namespace capsmi
+
+extern "C" {
+
+capsmi_status capsmi_graph_compact(capsmi_session* s, int32_t nnodes, capsmi_table* const* nodes, int32_t nrels,
+                                   capsmi_table* const* rels, int64_t* dense_ids) {
+    P_BEGIN
+    need(s, "session");
+    REQUIRE(nnodes >= 0 && nrels >= 0 && (nnodes == 0 || nodes) && (nrels == 0 || rels), CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            "tables");
+    HIP_CHECK(hipSetDevice(s->device));
+    std::vector<capsmi_table*> nv, rv;
+    for (int i = 0; i < nnodes; ++i) {
+        need(nodes[i], "nodes[i]");
+        REQUIRE(nodes[i]->entity && nodes[i]->entity->kind == 1 && nodes[i]->sess == s, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                "graph_compact: nodes[i] is not a node table of this session (capsmi_node_table)");
+        nv.push_back(nodes[i]);
+    }
+    for (int i = 0; i < nrels; ++i) {
+        need(rels[i], "rels[i]");
+        REQUIRE(rels[i]->entity && rels[i]->entity->kind == 2 && rels[i]->sess == s, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                "graph_compact: rels[i] is not a relationship table of this session (capsmi_rel_table)");
+        rv.push_back(rels[i]);
+    }
+    int64_t n = 0;
+    graph_compact(s, nv, rv, &n);
+    if (dense_ids) *dense_ids = n;
+    P_END
 }
 
 capsmi_status capsmi_table_entity(const capsmi_table* t, int32_t* kind, int64_t* id_lo, int64_t* id_hi) {

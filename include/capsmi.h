@@ -224,6 +224,12 @@ capsmi_status capsmi_node_table(capsmi_table* t, const char* id_col, int32_t nla
                                 capsmi_table** out);
 capsmi_status capsmi_rel_table(capsmi_table* t, const char* id_col, const char* src_col, const char* dst_col,
                                int32_t ntypes, const char* const* type_cols, capsmi_table** out);
+/* Graph-level id compaction (the analogue of caching a graph at creation, CAPSGraphFactory.create /
+ * CachedDataSource): numbers every node id of `nodes` and every endpoint of `rels` densely and keeps
+ * the dense columns with the tables, so graphs whose Long ids are sparse, large or carry tag bits
+ * (Tags.scala:36-55) reach the fused kernels.  Results keep the original ids. */
+capsmi_status capsmi_graph_compact(capsmi_session* s, int32_t nnodes, capsmi_table* const* nodes, int32_t nrels,
+                                   capsmi_table* const* rels, int64_t* dense_ids);
 /* kind 0 = plain table, 1 = node table, 2 = relationship table; [*id_lo, *id_hi) = range of the ids
  * (node) or of both endpoints (relationship) */
 capsmi_status capsmi_table_entity(const capsmi_table* t, int32_t* kind, int64_t* id_lo, int64_t* id_hi);

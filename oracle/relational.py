@@ -57,6 +57,9 @@ class NumpyBackend:
     def __init__(self, dictionary):
         self.dictionary = dictionary
 
+    def compact_if_sparse(self, nodes, rels):  # dense-id compaction is a device-path concern
+        return False
+
     def table(self, columns) -> "NumpyTable":
         cols = OrderedDict()
         n = None
