@@ -73,6 +73,8 @@ P = c_void_p  # opaque handles
 PP = POINTER(c_void_p)
 STRS = POINTER(c_char_p)
 
+INTERN_FN = ctypes.CFUNCTYPE(c_int64, c_void_p, ctypes.POINTER(ctypes.c_char), c_size_t)
+
 # name -> (restype-is-status, argtypes)
 _SIGS = {
     "capsmi_last_error": (c_size_t, [c_char_p, c_size_t]),
@@ -158,6 +160,8 @@ _SIGS = {
     "capsmi_flatten_rel_types": (c_int32, [P, c_char_p, c_int32, POINTER(c_int64), STRS, PP]),
     "capsmi_session_set_fused": (c_int32, [P, c_int32]),
     "capsmi_graph_compact": (c_int32, [P, c_int32, PP, c_int32, PP, POINTER(c_int64)]),
+    "capsmi_read_csv": (c_int32, [P, c_int32, STRS, ctypes.c_char, ctypes.c_char, c_int32, STRS, POINTER(c_int32),
+                                  INTERN_FN, c_void_p, c_char_p, PP]),
     "capsmi_session_route_count": (c_int32, [P, c_char_p, POINTER(c_int64)]),
 }
 

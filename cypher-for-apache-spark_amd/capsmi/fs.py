@@ -11,7 +11,8 @@ Restates the reference's FS layout and table schemas:
     table per label combination of the schema, one relationship table per type
   - Spark's CSV reader with an explicit schema: no header line, ',' separated, '"' quoted, an
     empty field is null.
-Parsing is host work (file IO); columns go to the device as entity tables of a ScanGraph.
+On a device session the tables are parsed by libcapsmi's native CSV reader (host threads) straight
+into device entity tables; the CPU oracle backend parses them in Python.
 """
 from __future__ import annotations
 
@@ -71,10 +72,32 @@ def read_schema(graph_dir: str) -> Tuple[List[Tuple[frozenset, Dict[str, int]]],
     return nodes, rels
 
 
+def _native_tables(session, graph_dir, node_schemas, rel_schemas):
+    """Device path: every table directory parsed by libcapsmi's native CSV reader (capsmi_read_csv)."""
+    nodes, rels = [], []
+    for labels, props in node_schemas:
+        d = os.path.join(graph_dir, "nodes", "_".join(sorted(labels)))
+        keys = sorted(props)
+        t = session.read_csv(sorted(glob.glob(os.path.join(d, "*.csv"))), [ID] + keys, [I64] + [props[k] for k in keys])
+        nodes.append(EntityTable("node", labels, dict(props), t.as_node_table(ID)))
+    for rtype, props in rel_schemas:
+        d = os.path.join(graph_dir, "relationships", rtype)
+        keys = sorted(props)
+        t = session.read_csv(sorted(glob.glob(os.path.join(d, "*.csv"))), [ID, SRC, DST] + keys,
+                             [I64, I64, I64] + [props[k] for k in keys])
+        rels.append(EntityTable("rel", frozenset([rtype]), dict(props), t.as_rel_table(ID, SRC, DST)))
+    return nodes, rels
+
+
 def fs_graph(backend, graph_dir: str, extra_strings=()) -> ScanGraph:
     """ScanGraph of a CSV graph directory; `backend` is a capsmi Session (GPU) or the oracle's backend.
     `extra_strings`: strings to register up front (codes are stable, so later strings may also be added)."""
     node_schemas, rel_schemas = read_schema(graph_dir)
+    if hasattr(backend, "read_csv"):  # a device session
+        backend.dictionary.extend(extra_strings)
+        nodes, rels = _native_tables(backend, graph_dir, node_schemas, rel_schemas)
+        backend.compact_if_sparse([e.table for e in nodes], [e.table for e in rels])
+        return ScanGraph(backend, nodes, rels)
     parsed = []
     strings = set()
     for labels, props in node_schemas:

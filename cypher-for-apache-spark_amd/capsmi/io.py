@@ -7,7 +7,8 @@ Restates EdgeListDataSource.graph
   - relationships get `id = monotonically_increasing_id()`, which for a single input partition is
     the row number 0, 1, 2, ...;
   - nodes = distinct(source UNION target), label "V"; relationship type "E" (:45-53).
-Parsing is host work (file IO); the node table's distinct runs on the device.
+Parsing runs in libcapsmi's native CSV reader (host threads); the node table's distinct runs on the
+device.
 """
 from __future__ import annotations
 
@@ -23,18 +24,12 @@ REL_TYPE = "E"
 
 
 def read_edge_list(path: str, delimiter: str = " ", comment: str = "#") -> Tuple[np.ndarray, np.ndarray]:
-    src, dst = [], []
-    with open(path) as f:
-        for line in f:
-            line = line.strip()
-            if not line or (comment and line.startswith(comment)):
-                continue
-            parts = [p for p in line.split(delimiter) if p != ""] if delimiter != " " else line.split()
-            if len(parts) < 2:
-                raise ValueError(f"malformed edge-list line: {line!r}")
-            src.append(int(parts[0]))
-            dst.append(int(parts[1]))
-    return np.asarray(src, dtype=np.int64), np.asarray(dst, dtype=np.int64)
+    """Host arrays of an edge-list file (vectorised C parser; the device path is edge_list_graph)."""
+    import pandas as pd
+    sep = r"\s+" if delimiter == " " else delimiter
+    df = pd.read_csv(path, sep=sep, comment=comment or None, header=None, usecols=[0, 1], dtype=np.int64,
+                     engine="c")
+    return df[0].to_numpy(np.int64), df[1].to_numpy(np.int64)
 
 
 def edge_list_tables(session: Session, src: np.ndarray, dst: np.ndarray) -> Tuple[GpuTable, GpuTable]:
@@ -42,6 +37,10 @@ def edge_list_tables(session: Session, src: np.ndarray, dst: np.ndarray) -> Tupl
     m = len(src)
     rels = session.table([ColumnData("id", I64, np.arange(m, dtype=np.int64)), ColumnData("source", I64, src),
                           ColumnData("target", I64, dst)])
+    return _graph_of(session, rels)
+
+
+def _graph_of(session: Session, rels: GpuTable) -> Tuple[GpuTable, GpuTable]:
     s = rels.select("source").withColumnRenamed("source", "id")
     t = rels.select("target").withColumnRenamed("target", "id")
     nodes = s.unionAll(t).distinct().as_node_table("id")
@@ -50,6 +49,8 @@ def edge_list_tables(session: Session, src: np.ndarray, dst: np.ndarray) -> Tupl
     return nodes, rels
 
 
-def edge_list_graph(session: Session, path: str, delimiter: str = " ") -> Tuple[GpuTable, GpuTable]:
-    src, dst = read_edge_list(path, delimiter)
-    return edge_list_tables(session, src, dst)
+def edge_list_graph(session: Session, path: str, delimiter: str = " ", comment: str = "#") -> Tuple[GpuTable, GpuTable]:
+    """EdgeListDataSource.graph: the file parsed by libcapsmi's native CSV reader (host threads), rel ids
+    = row numbers, nodes = distinct endpoints on the device."""
+    rels = session.read_csv([path], ["source", "target"], [I64, I64], delimiter, comment, row_id_col="id")
+    return _graph_of(session, rels)

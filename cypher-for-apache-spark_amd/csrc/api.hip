@@ -1859,6 +1859,34 @@ capsmi_status capsmi_rmat_nodes(capsmi_session* s, int32_t scale, int32_t kind, 
     API_END
 }
 
+capsmi_status capsmi_read_csv(capsmi_session* s, int32_t nfiles, const char* const* paths, char delimiter, char comment,
+                              int32_t ncols, const char* const* names, const int32_t* types, capsmi_intern_fn intern,
+                              void* intern_ctx, const char* row_id_col, capsmi_table** out) {
+    API_BEGIN
+    need(s, "session");
+    need(out, "out");
+    REQUIRE(nfiles >= 0 && (nfiles == 0 || paths) && ncols >= 1 && names && types, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            "read_csv arguments");
+    use_device(s);
+    std::vector<std::string> ps, ns;
+    std::vector<int32_t> ts;
+    std::unordered_set<std::string> seen;
+    if (row_id_col) seen.insert(row_id_col);
+    for (int i = 0; i < nfiles; ++i) {
+        need(paths[i], "path");
+        ps.push_back(paths[i]);
+    }
+    for (int k = 0; k < ncols; ++k) {
+        need(names[k], "column name");
+        REQUIRE(seen.insert(names[k]).second, CAPSMI_ERR_ILLEGAL_ARGUMENT, std::string("duplicate column '") + names[k] + "'");
+        REQUIRE(types[k] >= CAPSMI_I64 && types[k] <= CAPSMI_STR, CAPSMI_ERR_ILLEGAL_ARGUMENT, "bad column type");
+        ns.push_back(names[k]);
+        ts.push_back(types[k]);
+    }
+    *out = read_csv(s, ps, delimiter, comment, ns, ts, intern, intern_ctx, row_id_col);
+    API_END
+}
+
 capsmi_status capsmi_table_fingerprint(capsmi_table* t, int32_t ncols, const char* const* cols, int64_t* count,
                                        uint64_t* sum, uint64_t* xr) {
     API_BEGIN

@@ -337,6 +337,11 @@ capsmi_status eager_distinct_on(capsmi_table* t, int32_t ncols, const char* cons
 capsmi_status eager_group(capsmi_table* t, int32_t nby, const char* const* by, int32_t naggs, const capsmi_agg* aggs,
                           capsmi_table** out);
 
+// CSV ingest (ingest.hip)
+capsmi_table* read_csv(capsmi_session* s, const std::vector<std::string>& paths, char delim, char comment,
+                       const std::vector<std::string>& names, const std::vector<int32_t>& types, capsmi_intern_fn intern,
+                       void* ctx, const char* row_id_col);
+
 // graph (k_graph.hip)
 void bitmap_add_rows(capsmi_bitmap* b, const int64_t* ids, const uint8_t* ids_valid,
                      const uint8_t* flags, int64_t n, int64_t* dev_counters);

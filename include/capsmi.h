@@ -429,6 +429,21 @@ capsmi_status capsmi_rmat_rels(capsmi_session* s, int32_t scale, int64_t e_begin
 /* word range [w_begin, w_end) of part `part` of `nparts` for ids in [0, 2^scale) */
 capsmi_status capsmi_owner_words(int64_t nbits, int32_t part, int32_t nparts, int64_t* w_begin,
                                  int64_t* w_end);
+/* ---- ingest ----------------------------------------------------
+ * DataFrameReader.csv with an explicit schema, as EdgeListDataSource (EdgeListDataSource.scala:76-97)
+ * and the FS graph source read their tables: files in order, no header, `delimiter` (' ' = runs of
+ * blanks), '"' quotes, an empty unquoted field is null, lines starting with `comment` (0 = none)
+ * skipped; Spark's PERMISSIVE token counts (missing trailing fields null, extra tokens dropped);
+ * a token that does not parse as its column type is ILLEGAL_ARGUMENT.  Parsed by host threads
+ * (CAPSMI_INGEST_THREADS, default OMP_NUM_THREADS), copied to the device.  types: CAPSMI_I64 /
+ * F64 / BOOL / STR; STR fields go through `intern` (the caller's dictionary), in row order.
+ * row_id_col != NULL prepends a Long column of row numbers (monotonically_increasing_id of one
+ * partition). */
+typedef int64_t (*capsmi_intern_fn)(void* ctx, const char* s, size_t len);
+capsmi_status capsmi_read_csv(capsmi_session* s, int32_t nfiles, const char* const* paths, char delimiter, char comment,
+                              int32_t ncols, const char* const* names, const int32_t* types, capsmi_intern_fn intern,
+                              void* intern_ctx, const char* row_id_col, capsmi_table** out);
+
 /* R-MAT node table(s): kind 0 -> one table [id] with every id 0..2^scale-1 (all Person);
  * kind 1 -> Person ids (splitmix64(id) & 3 != 0) with [id, age], age = splitmix64(seed ^ id) % 100;
  * kind 2 -> Company ids (the complement) with [id] */
