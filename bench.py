@@ -33,6 +33,10 @@ sys.path.insert(0, os.path.join(ROOT, "cypher-for-apache-spark_amd"))
 sys.path.insert(0, ROOT)
 
 METRIC = "matched rows/sec for 2-hop MATCH on R-MAT 2^30 edges; % HBM roofline @1/8 GPU"
+C2_QUERY = {"clauses": [{"match": "(a:Person)-[r:FRIEND_OF]->(b:Person)",
+                          "where": ["and", [">=", ["prop", "a", "age"], ["lit", 18]],
+                                    ["<", ["prop", "a", "age"], ["lit", 65]]]}],
+            "return": {"items": [["a", ["id", "a"]], ["b", ["id", "b"]]]}}
 C3_QUERY = {"clauses": [{"match": "(a:Person)-[:FRIEND_OF]->(b:Person)-[:FRIEND_OF]->(c:Person)"}],
             "return": {"items": [["count(DISTINCT c)", ["count_distinct", ["id", "c"]]]]}}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -57,6 +61,9 @@ def parse():
     p.add_argument("--shard-of", type=int, default=0,
                    help="diagnostic (C3): time rank 0's shard of an N-way owner(target) partition on one GPU, "
                         "no exchange; the line is not the metric")
+    p.add_argument("--c2-route", default="direct", choices=("direct", "planner", "joins"),
+                   help="C2: explicit expand kernels (direct), Planner(sg).run routed to the fused expand "
+                        "(planner), or the same plan operator by operator through the generic radix joins (joins)")
     p.add_argument("--workload", default="c3", choices=("c2", "c3", "c4", "c5"),
                    help="c3 (default, the BASELINE metric) or the single-GPU C2/C4/C5 lines (SURVEY.md 8d)")
     return p.parse_args()
@@ -454,7 +461,8 @@ SINGLE = {
 
 
 # timer name -> kernel symbol (rocprofv3 / PMC summary name) where they differ
-SINGLE_SYMBOL = {"expand_filter": "k_expand_pairs", "part_scatter1": "k_scatter_l", "varlen_deg": "k_vl_deg",
+SINGLE_SYMBOL = {"direct_join_probe": "k_direct_probe", "radix_join_count": "k_join", "radix_join_write": "k_join",
+                 "expand_filter": "k_expand_pairs", "part_scatter1": "k_scatter_l", "varlen_deg": "k_vl_deg",
                  "varlen_w": "k_vl_w", "varlen_t": "k_vl_t", "varlen_rev": "k_vl_bset", "varlen_recip": "k_vl_recip", "varlen_cand": "k_vl_cand", "triangles": "k_tri_big_items+k_tri_small"}
 
 
@@ -504,8 +512,19 @@ def run_single(args):
     sess.sync()
     pred = Ands((BinOp(">=", Col("age"), Lit(18)), BinOp("<", Col("age"), Lit(65))))
     cache = {}
+    route = args.c2_route if wl == "c2" and world == 1 else "direct"
+    if route != "direct":
+        from capsmi.planner import EntityTable, Planner, ScanGraph
+        sg = ScanGraph(sess, [EntityTable("node", frozenset({"Person"}), {"age": 0}, nodes, id_col="id")],
+                       [EntityTable("rel", frozenset({"FRIEND_OF"}), {}, rels, id_col="id", src_col="source",
+                                    dst_col="target")])
+        sess.set_fused(route == "planner")
 
     def step():
+        if route != "direct":  # the Cypher query through the planner mirror
+            t, outs = Planner(sg).run(C2_QUERY)
+            cache["outs"] = [outs[0][2], outs[1][2]]
+            return t.size, t
         if wl == "c2":
             a_ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id", pred)
             b_ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id")
@@ -538,7 +557,7 @@ def run_single(args):
         out = graph.var_length_count(sess, [rels], ok, ok, 1, 3)
         return None, out
 
-    kernels = ("bitmap_add", "expand_filter", "tri_pack", "triangles", "part_scatter1", "varlen_deg", "varlen_w", "varlen_rev",
+    kernels = ("direct_join_probe", "radix_join_count", "radix_join_write", "bitmap_add", "expand_filter", "tri_pack", "triangles", "part_scatter1", "varlen_deg", "varlen_w", "varlen_rev",
                "varlen_cand", "varlen_recip", "varlen_t")
     for _ in range(args.warmup):
         step()
@@ -546,6 +565,7 @@ def run_single(args):
     for k in kernels:  # reset
         _lib.call("capsmi_session_kernel_time", sess.handle, k.encode(), ctypes.byref(ctypes.c_int64()),
                   ctypes.byref(ctypes.c_double()))
+        _lib.call("capsmi_session_kernel_bytes", sess.handle, k.encode(), ctypes.byref(ctypes.c_double()))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -560,12 +580,15 @@ def run_single(args):
         tt = torch.tensor([sec], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         sec = float(tt.item())
-    kt = {}
+    kt, kbytes = {}, {}
     for k in kernels:
-        c, ms = ctypes.c_int64(), ctypes.c_double()
+        c, ms, b = ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
         _lib.call("capsmi_session_kernel_time", sess.handle, k.encode(), ctypes.byref(c), ctypes.byref(ms))
+        _lib.call("capsmi_session_kernel_bytes", sess.handle, k.encode(), ctypes.byref(b))
         if c.value:
             kt[k] = (c.value, ms.value)
+            if b.value:
+                kbytes[k] = b.value / c.value  # per launch
     _lib.call("capsmi_session_set_profiling", sess.handle, 0)
     check = None
     if wl == "c5":
@@ -594,7 +617,7 @@ def run_single(args):
         if fx is not None and wl == "c2":
             fcheck = "ok" if res == fx["rows"] else f"MISMATCH rows {res} vs fixture {fx['rows']}"
     elif wl == "c2":
-        fp = list(out.fingerprint(["a", "b"]))
+        fp = list(out.fingerprint(cache.get("outs", ["a", "b"])))
         want = [fx["fingerprint"][0], int(fx["fingerprint"][1]), int(fx["fingerprint"][2])]
         fcheck = "ok" if fp == want else f"MISMATCH fingerprint {fp} vs fixture {want}"
     elif wl == "c4":
@@ -614,8 +637,9 @@ def run_single(args):
            # both triangle kernels together: the oriented adjacency read once (8-B offsets, 4-B
            # targets, 8-B multiplicity payload per oriented edge)
            "triangles": n * 8 + 12 * cache.get("oriented_edges", 0)}
-    dom = max(kt, key=lambda k: kt[k][1])
-    avg_ms = kt[dom][1] / kt[dom][0]
+    alg.update(kbytes)  # kernels that declare their bytes (generic joins)
+    dom = max(kt, key=lambda k: kt[k][1]) if kt else None
+    avg_ms = kt[dom][1] / kt[dom][0] if kt else None
     b_alg = {"c2": 16 * m + int(0.75 * n) * 24 + 16 * (res or 0), "c4": 3 * 24 * m + 3 * 8 * n,
              "c5": 3 * 24 * m + 2 * 8 * n + 16 * n}[wl]  # SURVEY.md 8d worked values
     line = {
@@ -639,6 +663,11 @@ def run_single(args):
                                          f"phases; in-relationships exchanged at ingest")
     elif wl == "c2" and world > 1:
         line["config"]["parallelism"] = f"relationships by owner(source) over {world} GPU(s); row count all-reduced"
+    if wl == "c2":
+        line["config"]["route"] = {"direct": "explicit bitmap + expand_filter calls",
+                                   "planner": "Planner(sg).run, recognised and routed to the fused expand",
+                                   "joins": "Planner(sg).run operator by operator: node scans, two generic "
+                                            "radix joins, filter, select (fused routing off)"}[route]
     line["query"]["check_vs_fixture"] = fcheck
     if check is not None or (world > 1 and wl in ("c2", "c5")):
         line["query"]["check_vs_unsharded"] = check

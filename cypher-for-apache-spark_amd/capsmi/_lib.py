@@ -86,6 +86,7 @@ _SIGS = {
     "capsmi_session_sync": (c_int32, [P]),
     "capsmi_session_set_profiling": (c_int32, [P, c_int32]),
     "capsmi_session_kernel_time": (c_int32, [P, c_char_p, POINTER(c_int64), POINTER(ctypes.c_double)]),
+    "capsmi_session_kernel_bytes": (c_int32, [P, c_char_p, POINTER(ctypes.c_double)]),
     "capsmi_table_from_host": (c_int32, [P, c_int32, POINTER(ColDesc), c_int64, PP]),
     "capsmi_table_from_device": (c_int32, [P, c_int32, POINTER(ColDesc), c_int64, PP]),
     "capsmi_table_retain": (c_int32, [P]),

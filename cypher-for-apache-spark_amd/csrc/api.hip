@@ -301,6 +301,20 @@ bool types_joinable(int a, int b) {
     return a == b || (na && nb);
 }
 
+// Join strategy (Spark picks broadcast-hash vs shuffled joins by size; this picks by key shape and
+// build size): "direct" -- unique Long build keys in a dense range, a direct-address table; "hash"
+// -- one global hash table, for builds whose table stays cache-resident; "radix" -- both sides
+// radix-partitioned to LDS tables, for larger builds.  CAPSMI_JOIN=direct|hash|radix forces one for
+// A/B runs (direct still falls back when the keys are not eligible).
+enum JoinStrategy { JS_AUTO, JS_DIRECT, JS_HASH, JS_RADIX };
+JoinStrategy forced_join_strategy() {
+    const char* e = getenv("CAPSMI_JOIN");
+    if (!e) return JS_AUTO;
+    const std::string v(e);
+    return v == "direct" ? JS_DIRECT : v == "hash" ? JS_HASH : v == "radix" ? JS_RADIX : JS_AUTO;
+}
+constexpr int64_t kRadixBuildRows = int64_t(1) << 25;  // above: the hash table outgrows the MALL
+
 capsmi_table* join_impl(capsmi_table* l, capsmi_table* r, int jt, const std::vector<int>& lk,
                         const std::vector<int>& rk) {
     capsmi_session* s = l->sess;
@@ -344,15 +358,26 @@ capsmi_table* join_impl(capsmi_table* l, capsmi_table* r, int jt, const std::vec
             kc.data[i] = P<int64_t>(w);
             widened.push_back(w);
         }
-        HashTable ht;
-        Buf slot_of_row, slot_of_probe, offsets, rows;
-        hash_build(s, bk, B->nrows, /*skip_null_keys=*/true, ht, slot_of_row);
-        hash_group_rows(s, ht, slot_of_row, B->nrows, offsets, rows);
-        hash_probe(s, pk, bk, Pr->nrows, ht, slot_of_probe);
         const bool outer = jt != CAPSMI_JOIN_INNER;
         Buf pi, bi, matched;
-        total = join_expand(s, slot_of_probe, Pr->nrows, ht, offsets, rows, outer, pi, bi,
-                            jt == CAPSMI_JOIN_FULL_OUTER ? &matched : nullptr, B->nrows);
+        const JoinStrategy js = forced_join_strategy();
+        bool done = false;
+        if (jt != CAPSMI_JOIN_FULL_OUTER && (js == JS_AUTO || js == JS_DIRECT) && bk.n == 1 &&
+            B->cols[(build_left ? lk : rk)[0]].type == CAPSMI_I64 && Pr->cols[(build_left ? rk : lk)[0]].type == CAPSMI_I64)
+            done = direct_join(s, bk, B->nrows, pk, Pr->nrows, outer, pi, bi, &total);
+        if (done) {
+        } else if (jt != CAPSMI_JOIN_FULL_OUTER && (js == JS_RADIX || (js == JS_AUTO && B->nrows > kRadixBuildRows))) {
+            // radix-partitioned build / probe with LDS partition tables (k_rjoin.hip)
+            total = radix_join(s, bk, B->nrows, pk, Pr->nrows, outer, pi, bi);
+        } else {
+            HashTable ht;
+            Buf slot_of_row, slot_of_probe, offsets, rows;
+            hash_build(s, bk, B->nrows, /*skip_null_keys=*/true, ht, slot_of_row);
+            hash_group_rows(s, ht, slot_of_row, B->nrows, offsets, rows);
+            hash_probe(s, pk, bk, Pr->nrows, ht, slot_of_probe);
+            total = join_expand(s, slot_of_probe, Pr->nrows, ht, offsets, rows, outer, pi, bi,
+                                jt == CAPSMI_JOIN_FULL_OUTER ? &matched : nullptr, B->nrows);
+        }
         if (outer) (build_left ? lmiss : rmiss) = true;
         if (jt == CAPSMI_JOIN_FULL_OUTER) {
             // append build (right) rows that never matched, left side NULL
@@ -502,6 +527,17 @@ capsmi_status capsmi_session_set_profiling(capsmi_session* s, int32_t enabled) {
     API_BEGIN
     need(s, "session");
     s->prof = enabled != 0;
+    API_END
+}
+
+capsmi_status capsmi_session_kernel_bytes(capsmi_session* s, const char* name, double* bytes) {
+    API_BEGIN
+    need(s, "session");
+    need(name, "name");
+    need(bytes, "bytes");
+    auto it = s->alg_bytes.find(name);
+    *bytes = it == s->alg_bytes.end() ? 0.0 : it->second;
+    if (it != s->alg_bytes.end()) s->alg_bytes.erase(it);
     API_END
 }
 
@@ -778,6 +814,28 @@ capsmi_status eager_filter(capsmi_table* t, int32_t nnodes, const capsmi_expr* p
     API_END
 }
 
+// Filter followed by a projection: only the `keep` columns of the surviving rows are gathered
+capsmi_status eager_filter_keep(capsmi_table* t, int32_t nnodes, const capsmi_expr* prog,
+                                const std::vector<std::string>& keep, capsmi_table** out) {
+    API_BEGIN
+    need(t, "table");
+    need(out, "out");
+    capsmi_session* s = t->sess;
+    use_device(s);
+    Buf flags = dev_alloc(t->nrows > 0 ? t->nrows : 1, s);
+    eval_predicate(s, t, nnodes, prog, P<uint8_t>(flags));
+    Buf idx;
+    const int64_t n = flags_to_indices(s, P<uint8_t>(flags), t->nrows, idx);
+    capsmi_table kept;
+    kept.sess = s;
+    kept.nrows = t->nrows;
+    for (const std::string& k : keep) kept.cols.push_back(t->cols[col_index(t, k.c_str())]);
+    auto* o = new_table(s, n);
+    gather_into(o, &kept, idx, n, false);
+    *out = o;
+    API_END
+}
+
 capsmi_status eager_with_columns(capsmi_table* t, int32_t ncols, const capsmi_expr_column* cols, capsmi_table** out) {
     API_BEGIN
     need(t, "table");
@@ -789,6 +847,16 @@ capsmi_status eager_with_columns(capsmi_table* t, int32_t ncols, const capsmi_ex
     for (int i = 0; i < ncols; ++i) {
         need(cols[i].name, "column name");
         Column c;
+        if (cols[i].nnodes == 1 && cols[i].prog[0].op == CAPSMI_X_COL) {  // an alias: shares the buffers
+            REQUIRE(cols[i].prog[0].arg >= 0 && cols[i].prog[0].arg < (int)t->cols.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                    "column index out of range");
+            c = t->cols[cols[i].prog[0].arg];
+            c.name = cols[i].name;
+            const int j = o->find(c.name);
+            if (j >= 0) o->cols[j] = std::move(c);
+            else o->cols.push_back(std::move(c));
+            continue;
+        }
         c.name = cols[i].name;
         c.data = dev_alloc(sizeof(int64_t) * (t->nrows > 0 ? t->nrows : 1), s);
         c.valid = dev_alloc(t->nrows > 0 ? t->nrows : 1, s);

@@ -104,6 +104,7 @@ struct capsmi_session {
     };
     std::vector<Pending> pending;
     std::map<std::string, std::pair<int64_t, double>> totals;
+    std::map<std::string, double> alg_bytes;  // algorithmic bytes of the timed launches, per name
     // fused-path routing of lazy plans (plan.hip): enabled flag and per-route counters
     bool fused = true;
     std::map<std::string, int64_t> routes;
@@ -115,9 +116,12 @@ struct KernelTimer {
     capsmi_session* s;
     const char* name;
     hipEvent_t a = nullptr, b = nullptr;
-    KernelTimer(capsmi_session* s_, const char* n) : s(s_), name(n) {
-        if (s->prof && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess)
+    // bytes: the launch's algorithmic bytes (inputs read once, outputs written once), if known
+    KernelTimer(capsmi_session* s_, const char* n, double bytes = 0) : s(s_), name(n) {
+        if (s->prof && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess) {
             (void)hipEventRecord(a, s->stream);
+            if (bytes > 0) s->alg_bytes[name] += bytes;
+        }
     }
     ~KernelTimer() {
         if (a && b) {
@@ -220,6 +224,14 @@ void agg_minmax(const int64_t* gid, const int64_t* v, const uint8_t* valid, int6
 void avg_finish(const double* sum, const int64_t* cnt, int64_t ng, bool to_i64, int64_t* out, uint8_t* valid,
                 hipStream_t st);
 void minmax_finish(int64_t* v, int type, bool is_max, int64_t ng, hipStream_t st);
+// radix-partitioned equi-join (k_rjoin.hip): (probe row, build row) pairs grouped by key-hash
+// partition; build row -1 for an unmatched or null-key probe row when `outer`.  Returns #pairs.
+int64_t radix_join(capsmi_session* s, const KeyCols& bk, int64_t nb, const KeyCols& pk, int64_t np, bool outer,
+                   Buf& out_p, Buf& out_b);
+// direct-address join (k_rjoin.hip): single Long key, unique build keys in a dense range; false if
+// not eligible (then nothing was produced)
+bool direct_join(capsmi_session* s, const KeyCols& bk, int64_t nb, const KeyCols& pk, int64_t np, bool outer,
+                 Buf& out_p, Buf& out_b, int64_t* total);
 void cross_pairs(int64_t nl, int64_t nr, int64_t* out_l, int64_t* out_r, hipStream_t st);
 
 // expressions (k_expr.hip)
@@ -324,6 +336,8 @@ capsmi_status eager_select(capsmi_table* t, int32_t ncols, const char* const* co
 capsmi_status eager_drop(capsmi_table* t, int32_t ncols, const char* const* cols, capsmi_table** out);
 capsmi_status eager_with_column_renamed(capsmi_table* t, const char* old_name, const char* new_name, capsmi_table** out);
 capsmi_status eager_filter(capsmi_table* t, int32_t nnodes, const capsmi_expr* prog, capsmi_table** out);
+capsmi_status eager_filter_keep(capsmi_table* t, int32_t nnodes, const capsmi_expr* prog,
+                                const std::vector<std::string>& keep, capsmi_table** out);
 capsmi_status eager_with_columns(capsmi_table* t, int32_t ncols, const capsmi_expr_column* cols, capsmi_table** out);
 capsmi_status eager_join(capsmi_table* l, capsmi_table* r, int32_t join_type, int32_t npairs, const char* const* lcols,
                          const char* const* rcols, capsmi_table** out);

@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <set>
 
 #include "capsmi_impl.h"
@@ -1104,14 +1105,309 @@ void attach_entity(capsmi_table* t, int kind, int64_t lo, int64_t hi) {
     t->entity = e;
 }
 
+// ============================ operator-by-operator execution, pruned ========================
+// What Catalyst does to the DataFrame plan DataFrameTable builds before Spark runs it (the optimiser
+// rules ColumnPruning and PushDownPredicate / PushPredicateThroughJoin): a plan that is not routed
+// to a fused kernel executes with
+//   - every Filter split into its conjuncts, each pushed below Select / Drop / WithColumnRenamed /
+//     WithColumns (when it does not read a column they add) and into the side of a Join whose columns
+//     it reads (inner and cross: either side; one-sided outer: the preserved side only), and applied
+//     where it stops -- with the rows of only the columns still needed gathered;
+//   - only the columns some operator above still reads computed and gathered (join outputs, filters,
+//     WithColumns expressions nobody reads are skipped).
+// Results are the same rows (conjunct order does not change a TRUE / not-TRUE filter under 3VL);
+// columns are matched by name, and put back in schema order where position matters (union inputs,
+// the materialised table).
+// A sub-plan with two parents in the plan DAG is materialised once in place and shared.
+namespace {
+
+using Names = std::vector<std::string>;  // ordered, unique column names
+
+bool has(const Names& v, const std::string& x) { return std::find(v.begin(), v.end(), x) != v.end(); }
+void add(Names& v, const std::string& x) {
+    if (!has(v, x)) v.push_back(x);
+}
+
+struct Pred {                     // one conjunct; COL args index `names`
+    std::vector<capsmi_expr> prog;
+    Names names;
+};
+
+// first node of the complete sub-expression that ends at prog[end] (postfix)
+int subtree_start(const std::vector<capsmi_expr>& prog, int end) {
+    int want = 1;
+    for (int i = end; i >= 0; --i) {
+        want += arity(prog[i]) - 1;
+        if (want == 0) return i;
+    }
+    throw Error(CAPSMI_ERR_INTERNAL, "malformed expression program");
+}
+
+void conjuncts(const std::vector<capsmi_expr>& prog, int lo, int hi, std::vector<std::vector<capsmi_expr>>& out) {
+    if (prog[hi].op == CAPSMI_X_AND) {
+        std::vector<std::pair<int, int>> kids;
+        int end = hi - 1;
+        for (int k = 0; k < prog[hi].arg; ++k) {
+            const int st = subtree_start(prog, end);
+            kids.push_back({st, end});
+            end = st - 1;
+        }
+        for (auto it = kids.rbegin(); it != kids.rend(); ++it) conjuncts(prog, it->first, it->second, out);
+    } else {
+        out.emplace_back(prog.begin() + lo, prog.begin() + hi + 1);
+    }
+}
+
+Pred to_pred(const std::vector<capsmi_expr>& prog, const capsmi_table* schema) {
+    Pred p;
+    p.prog = prog;
+    for (capsmi_expr& x : p.prog)
+        if (x.op == CAPSMI_X_COL) {
+            const std::string& n = schema->cols.at(x.arg).name;
+            add(p.names, n);
+            x.arg = (int32_t)(std::find(p.names.begin(), p.names.end(), n) - p.names.begin());
+        }
+    return p;
+}
+
+// a program over `from`'s columns re-indexed against `to` (by name)
+std::vector<capsmi_expr> remap(std::vector<capsmi_expr> prog, const capsmi_table* from, const capsmi_table* to) {
+    for (capsmi_expr& x : prog)
+        if (x.op == CAPSMI_X_COL) x.arg = col_of(to, from->cols.at(x.arg).name.c_str());
+    return prog;
+}
+
+struct Res {  // an operator's result: a table this executor owns, or a borrowed materialised input
+    capsmi_table* t = nullptr;
+    bool owned = false;
+    Res() = default;
+    Res(capsmi_table* x, bool o) : t(x), owned(o) {}
+    Res(Res&& o) noexcept : t(o.t), owned(o.owned) { o.t = nullptr; }
+    Res& operator=(Res&& o) noexcept {
+        if (this != &o) {
+            reset();
+            t = o.t;
+            owned = o.owned;
+            o.t = nullptr;
+        }
+        return *this;
+    }
+    ~Res() { reset(); }
+    void reset() {
+        if (t && owned) capsmi_table_release(t);
+        t = nullptr;
+    }
+};
+
+Res owned(capsmi_table* t) { return Res(t, true); }
+
+// apply the pending conjuncts, keep exactly `need` (in the table's order)
+Res finish(Res r, const Names& need, const std::vector<Pred>& preds) {
+    Names keep;
+    for (const Column& c : r.t->cols)
+        if (has(need, c.name)) keep.push_back(c.name);
+    REQUIRE(keep.size() == need.size(), CAPSMI_ERR_INTERNAL, "pruned plan lost a column");
+    capsmi_table* o = nullptr;
+    if (!preds.empty()) {
+        std::vector<capsmi_expr> prog;
+        for (const Pred& p : preds)
+            for (capsmi_expr x : p.prog) {
+                if (x.op == CAPSMI_X_COL) x.arg = col_of(r.t, p.names.at(x.arg).c_str());
+                prog.push_back(x);
+            }
+        if (preds.size() > 1) {
+            capsmi_expr a{};
+            a.op = CAPSMI_X_AND;
+            a.arg = (int32_t)preds.size();
+            prog.push_back(a);
+        }
+        check(eager_filter_keep(r.t, (int32_t)prog.size(), prog.data(), keep, &o));
+        return owned(o);
+    }
+    if (keep.size() == r.t->cols.size()) return r;
+    auto c = cstrs(keep);
+    check(eager_select(r.t, (int32_t)c.size(), c.data(), &o));
+    return owned(o);
+}
+
+using Parents = std::map<const capsmi_table*, int>;
+
+void count_parents(const capsmi_table* t, Parents& par) {
+    if (!t->lazy()) return;
+    for (const capsmi_table* x : t->plan->in)
+        if (++par[x] == 1) count_parents(x, par);
+}
+
+Names all_names(const capsmi_table* t) {
+    Names v;
+    for (const Column& c : t->cols) v.push_back(c.name);
+    return v;
+}
+
+Res exec(capsmi_table* t, const Names& need, std::vector<Pred> preds, const Parents& par) {
+    if (t->lazy()) {
+        auto it = par.find(t);
+        if (it != par.end() && it->second > 1) materialize(t);  // shared sub-plan: once, in place
+    }
+    if (!t->lazy()) return finish(Res(t, false), need, preds);
+    capsmi_table* fr = nullptr;
+    if (try_fused(t, &fr)) {
+        REQUIRE(fr->cols.size() == t->cols.size(), CAPSMI_ERR_INTERNAL, "fused result schema differs from the plan's");
+        for (size_t i = 0; i < fr->cols.size(); ++i) fr->cols[i].name = t->cols[i].name;
+        return finish(owned(fr), need, preds);
+    }
+    std::shared_ptr<PlanNode> keep_alive = t->plan;
+    const PlanNode& p = *keep_alive;
+    capsmi_table* x = p.in.empty() ? nullptr : p.in[0];
+    switch (p.kind) {
+        case PlanNode::FILTER: {
+            std::vector<std::vector<capsmi_expr>> cs;
+            if (!p.progs[0].empty()) conjuncts(p.progs[0], 0, (int)p.progs[0].size() - 1, cs);
+            for (auto& c : cs) preds.push_back(to_pred(c, x));
+            return exec(x, need, std::move(preds), par);
+        }
+        case PlanNode::SELECT:
+        case PlanNode::DROP:
+            return exec(x, need, std::move(preds), par);
+        case PlanNode::RENAME: {
+            const std::string &a = p.a[0], &b = p.b[0];
+            if (a == b) return exec(x, need, std::move(preds), par);
+            Names nin;
+            for (const std::string& n : need) nin.push_back(n == b ? a : n);
+            for (Pred& pr : preds)
+                for (std::string& n : pr.names)
+                    if (n == b) n = a;
+            Res r = exec(x, nin, std::move(preds), par);
+            if (r.t->find(a) < 0) return r;
+            capsmi_table* o = nullptr;
+            check(eager_with_column_renamed(r.t, a.c_str(), b.c_str(), &o));
+            return owned(o);
+        }
+        case PlanNode::WITH_COLUMNS: {
+            std::vector<Pred> down, stay;
+            for (Pred& pr : preds) {
+                bool reads_new = false;
+                for (const std::string& n : pr.names) reads_new |= has(p.a, n);
+                (reads_new ? stay : down).push_back(std::move(pr));
+            }
+            Names out = need;
+            for (const Pred& pr : stay)
+                for (const std::string& n : pr.names) add(out, n);
+            Names nin;
+            std::vector<size_t> comp;
+            for (const std::string& n : out)
+                if (!has(p.a, n)) add(nin, n);
+            for (size_t i = 0; i < p.a.size(); ++i) {
+                if (!has(out, p.a[i])) continue;  // nobody reads it
+                comp.push_back(i);
+                for (const capsmi_expr& e : p.progs[i])
+                    if (e.op == CAPSMI_X_COL) add(nin, x->cols.at(e.arg).name);
+            }
+            Res r = exec(x, nin, std::move(down), par);
+            if (!comp.empty()) {
+                std::vector<std::vector<capsmi_expr>> progs;
+                for (size_t i : comp) progs.push_back(remap(p.progs[i], x, r.t));
+                std::vector<capsmi_expr_column> cols(comp.size());
+                for (size_t k = 0; k < comp.size(); ++k) {
+                    cols[k].name = p.a[comp[k]].c_str();
+                    cols[k].nnodes = (int32_t)progs[k].size();
+                    cols[k].prog = progs[k].data();
+                }
+                capsmi_table* o = nullptr;
+                check(eager_with_columns(r.t, (int32_t)cols.size(), cols.data(), &o));
+                r = owned(o);
+            }
+            return finish(std::move(r), need, stay);
+        }
+        case PlanNode::JOIN: {
+            capsmi_table* y = p.in[1];
+            const Names L = all_names(x), R = all_names(y);
+            const bool cross = p.jt == CAPSMI_JOIN_CROSS;
+            const bool to_l = p.jt == CAPSMI_JOIN_INNER || cross || p.jt == CAPSMI_JOIN_LEFT_OUTER;
+            const bool to_r = p.jt == CAPSMI_JOIN_INNER || cross || p.jt == CAPSMI_JOIN_RIGHT_OUTER;
+            std::vector<Pred> pl, pr, stay;
+            for (Pred& q : preds) {
+                bool in_l = true, in_r = true;
+                for (const std::string& n : q.names) {
+                    in_l &= has(L, n);
+                    in_r &= has(R, n);
+                }
+                if (to_l && in_l) pl.push_back(std::move(q));
+                else if (to_r && in_r) pr.push_back(std::move(q));
+                else stay.push_back(std::move(q));
+            }
+            Names out = need;
+            for (const Pred& q : stay)
+                for (const std::string& n : q.names) add(out, n);
+            Names nl, nr;
+            for (const std::string& n : out) add(has(L, n) ? nl : nr, n);
+            for (const std::string& n : p.a) add(nl, n);
+            for (const std::string& n : p.b) add(nr, n);
+            Res a = exec(x, nl, std::move(pl), par);
+            Res b = exec(y, nr, std::move(pr), par);
+            auto lk = cstrs(p.a), rk = cstrs(p.b);
+            capsmi_table* o = nullptr;
+            check(eager_join(a.t, b.t, p.jt, (int32_t)lk.size(), lk.data(), rk.data(), &o));
+            a.reset();
+            b.reset();
+            return finish(owned(o), need, stay);
+        }
+        default: {  // union, distinct, grouping, ordering, skip / limit: conjuncts stay above
+            std::vector<Names> nin(p.in.size());
+            for (size_t i = 0; i < p.in.size(); ++i) nin[i] = all_names(p.in[i]);
+            if (p.kind == PlanNode::GROUP) {
+                Names v = p.a;
+                for (const AggSpec& ag : p.aggs)
+                    if (!ag.input.empty()) add(v, ag.input);
+                nin[0] = v;
+            } else if (p.kind == PlanNode::ORDER || p.kind == PlanNode::SKIP || p.kind == PlanNode::LIMIT) {
+                Names v = need;
+                for (const std::string& n : p.a) add(v, n);
+                for (const Pred& q : preds)
+                    for (const std::string& n : q.names) add(v, n);
+                nin[0] = v;
+            }
+            PlanNode run;  // the same operator over the pruned inputs
+            run.kind = p.kind;
+            run.a = p.a;
+            run.b = p.b;
+            run.progs = p.progs;
+            run.flags = p.flags;
+            run.aggs = p.aggs;
+            run.jt = p.jt;
+            run.n = p.n;
+            for (size_t i = 0; i < p.in.size(); ++i) {
+                Res r = exec(p.in[i], nin[i], {}, par);
+                if (p.kind == PlanNode::UNION) {  // positional: the input's schema order
+                    capsmi_table* o = nullptr;
+                    auto c = cstrs(nin[i]);
+                    check(eager_select(r.t, (int32_t)c.size(), c.data(), &o));
+                    r = owned(o);
+                }
+                hold(run, r.t);
+            }
+            return finish(owned(exec_node(run)), need, preds);
+        }
+    }
+    return Res();
+}
+
+}  // namespace
+
 // ================================ materialisation ===========================================
 void materialize(capsmi_table* t) {
     if (!t || !t->plan) return;
     std::shared_ptr<PlanNode> p = t->plan;  // inputs stay alive while this runs
+    Parents par;
+    count_parents(t, par);
+    const Names all = all_names(t);
+    Names uniq;
+    for (const std::string& n : all) add(uniq, n);
     capsmi_table* r = nullptr;
-    if (!try_fused(t, &r)) {
-        for (capsmi_table* x : p->in) materialize(x);
-        r = exec_node(*p);
+    {
+        Res e = exec(t, uniq, {}, par);
+        auto c = cstrs(all);
+        check(eager_select(e.t, (int32_t)c.size(), c.data(), &r));  // schema order, an owned table
     }
     adopt(t, r);
     t->plan.reset();  // the inputs are released unless shared elsewhere

@@ -175,6 +175,10 @@ capsmi_status capsmi_session_set_profiling(capsmi_session* s, int32_t enabled);
 /* resolve pending events (synchronises) and report totals for kernel `name` ("hop1", "hop2",
  * "expand_filter", "bitmap_add", ...): launches and summed milliseconds; then the counters reset. */
 capsmi_status capsmi_session_kernel_time(capsmi_session* s, const char* name, int64_t* launches, double* total_ms);
+/* summed algorithmic bytes (inputs read once, outputs written once) of the timed launches of `name`,
+ * for kernels that declare them (the join kernels: "direct_join_probe", "radix_join_count",
+ * "radix_join_write"); 0 otherwise; then the counter resets. */
+capsmi_status capsmi_session_kernel_bytes(capsmi_session* s, const char* name, double* bytes);
 /* fused-path routing of lazy plans: enable / disable (default on; off = operator by operator, for
  * A/B checks), and the number of plans routed to fused entry point `name` ("expand", "expand_count",
  * "two_hop", "triangle", "var_length") since the session started */
