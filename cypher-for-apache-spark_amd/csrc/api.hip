@@ -313,7 +313,9 @@ JoinStrategy forced_join_strategy() {
     const std::string v(e);
     return v == "direct" ? JS_DIRECT : v == "hash" ? JS_HASH : v == "radix" ? JS_RADIX : JS_AUTO;
 }
-constexpr int64_t kRadixBuildRows = int64_t(1) << 25;  // above: the hash table outgrows the MALL
+// from 2^22 build rows (a global table of ~128 MB, half the MALL) the radix join measured faster:
+// 3.4 vs 3.9 ms at 2^22, 14.3 vs 16.2 at 2^24, 62.6 vs 70.1 at 2^26 (scripts/join_bench.py)
+constexpr int64_t kRadixBuildRows = int64_t(1) << 22;
 
 capsmi_table* join_impl(capsmi_table* l, capsmi_table* r, int jt, const std::vector<int>& lk,
                         const std::vector<int>& rk) {
@@ -366,7 +368,7 @@ capsmi_table* join_impl(capsmi_table* l, capsmi_table* r, int jt, const std::vec
             B->cols[(build_left ? lk : rk)[0]].type == CAPSMI_I64 && Pr->cols[(build_left ? rk : lk)[0]].type == CAPSMI_I64)
             done = direct_join(s, bk, B->nrows, pk, Pr->nrows, outer, pi, bi, &total);
         if (done) {
-        } else if (jt != CAPSMI_JOIN_FULL_OUTER && (js == JS_RADIX || (js == JS_AUTO && B->nrows > kRadixBuildRows))) {
+        } else if (jt != CAPSMI_JOIN_FULL_OUTER && (js == JS_RADIX || (js == JS_AUTO && B->nrows >= kRadixBuildRows))) {
             // radix-partitioned build / probe with LDS partition tables (k_rjoin.hip)
             total = radix_join(s, bk, B->nrows, pk, Pr->nrows, outer, pi, bi);
         } else {

@@ -55,23 +55,27 @@ def _pairs(t):
 
 
 def _join(session, L, R, jt, nkeys, mode):
-    old = os.environ.get("CAPSMI_JOIN")
-    os.environ["CAPSMI_JOIN"] = mode
+    """mode: a CAPSMI_JOIN strategy, "radix:probe" = the radix join emitting in probe-row order"""
+    strategy, _, order = mode.partition(":")
+    saved = {k: os.environ.get(k) for k in ("CAPSMI_JOIN", "CAPSMI_RADIX_ORDER")}
+    os.environ["CAPSMI_JOIN"] = strategy
+    os.environ["CAPSMI_RADIX_ORDER"] = order or "partition"
     try:
         t = L.join(R, jt, *[(f"l_k{i}", f"r_k{i}") for i in range(nkeys)])
         return _pairs(t)
     finally:
-        if old is None:
-            del os.environ["CAPSMI_JOIN"]
-        else:
-            os.environ["CAPSMI_JOIN"] = old
+        for k, v in saved.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
 def _check(session, lk, rk, jt, lv=None, rv=None, types=None):
     L = _table(session, "l", lk, lv, types)
     R = _table(session, "r", rk, rv, types)
     want = _expected(lk, lv, rk, rv, jt)
-    for mode in ("radix", "hash", "direct", "auto"):
+    for mode in ("radix", "radix:probe", "hash", "direct", "auto"):
         got = _join(session, L, R, jt, len(lk), mode)
         assert got.shape == want.shape, mode
         np.testing.assert_array_equal(got, want, err_msg=mode)
@@ -116,10 +120,11 @@ def test_skewed_duplicate_keys(session, jt):
     """Zipf keys on both sides: hub keys put more than one LDS table of build rows in a partition
     and more than one tile of probe rows."""
     rng = np.random.default_rng(2)
-    lk = (rng.zipf(1.3, 120_000) % 5000).astype(np.int64)
-    rk = (rng.zipf(1.3, 60_000) % 5000).astype(np.int64)
-    lk[lk == 1] = 10_001  # cap the output: drop the heaviest key on the probe side
-    _check(session, [lk], [rk], jt)
+    rk = (rng.zipf(1.3, 60_000) % 5000).astype(np.int64)      # build: key 1 ~ 18k rows (9 LDS chunks)
+    lk = rng.integers(0, 6000, 120_000).astype(np.int64)      # probe: uniform (some keys unmatched) ...
+    lk[:50], lk[50:150], lk[150:3150] = 1, 2, 7               # ... plus hubs: key 7 spans two probe tiles
+    rng.shuffle(lk)
+    assert _check(session, [lk], [rk], jt) < 8_000_000
 
 
 @pytest.mark.parametrize("jt", ["inner", "left_outer", "right_outer"])
