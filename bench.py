@@ -37,13 +37,18 @@ C2_QUERY = {"clauses": [{"match": "(a:Person)-[r:FRIEND_OF]->(b:Person)",
                           "where": ["and", [">=", ["prop", "a", "age"], ["lit", 18]],
                                     ["<", ["prop", "a", "age"], ["lit", 65]]]}],
             "return": {"items": [["a", ["id", "a"]], ["b", ["id", "b"]]]}}
+C3_COUNT_QUERY = {"clauses": [{"match": "(a:Person)-[:FRIEND_OF]->(b:Person)-[:FRIEND_OF]->(c:Person)"}],
+                  "return": {"items": [["n", ["count*"]]]}}
 C3_QUERY = {"clauses": [{"match": "(a:Person)-[:FRIEND_OF]->(b:Person)-[:FRIEND_OF]->(c:Person)"}],
             "return": {"items": [["count(DISTINCT c)", ["count_distinct", ["id", "c"]]]]}}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-KERNELS = ("part_scatter1", "part_scatter2_hop1", "part_scatter2", "hop1", "hop2", "mid_combine", "bitmap_add")
+KERNELS = ("part_scatter1", "part_scatter2_hop1", "part_scatter2", "hop1", "hop2", "mid_combine", "bitmap_add",
+           "count_part_in", "count_in", "count_part_out", "count_out", "degrees")
 # timer name -> kernel name as rocprofv3 reports it (hop1 and hop2 are two instances of k_hop_2d)
 KERNEL_SYMBOL = {"part_scatter1": "k_scatter_l", "part_scatter2_hop1": "k_scatter_s2", "part_scatter2": "k_scatter_s2",
-                 "hop1": "k_hop_2d", "hop2": "k_hop_2d", "mid_combine": "k_mid_combine", "bitmap_add": "k_bitmap_add"}
+                 "hop1": "k_hop_2d", "hop2": "k_hop_2d", "mid_combine": "k_mid_combine", "bitmap_add": "k_bitmap_add",
+                 "count_part_in": "k_scatter_c", "count_part_out": "k_scatter_c", "count_in": "k_cnt_in",
+                 "count_out": "k_cnt_out", "degrees": "k_degrees"}
 
 
 def parse():
@@ -53,9 +58,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--scale", type=int, default=26)
     p.add_argument("--edge-factor", type=int, default=16)
-    p.add_argument("--modes", default="cold,warm,direct",
+    p.add_argument("--modes", default="cold,warm,direct,count",
                    help="comma list of cold, warm (the planner route, N=1), direct, direct_warm (explicit kernel "
-                        "calls), stream (first = value)")
+                        "calls), stream, count / count_atomic (count(*) of the same match through the route, "
+                        "partitioned / per-relationship atomic degrees) (first = value)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-scale", type=int, default=None, help="oracle sample scale (default per workload)")
     p.add_argument("--shard-of", type=int, default=0,
@@ -318,17 +324,32 @@ def main():
         t, outs = Planner(sg).run(C3_QUERY)
         return int(t.column(outs[0][2]).values[0])
 
+    def run_count(atomic=False):  # count(*) of the same match through the route
+        if atomic:
+            os.environ["CAPSMI_COUNT"] = "atomic"
+        try:
+            t, outs = Planner(sg_cold).run(C3_COUNT_QUERY)
+            return int(t.column(outs[0][2]).values[0])
+        finally:
+            os.environ.pop("CAPSMI_COUNT", None)
+
     steps = {"cold": lambda: run_planner(sg_cold), "warm": lambda: run_planner(sg_warm),
-             "direct": step_cold, "direct_warm": step_warm, "stream": step_stream}
+             "direct": step_cold, "direct_warm": step_warm, "stream": step_stream,
+             "count": run_count, "count_atomic": lambda: run_count(True)}
     if distributed or shards != world:  # the recogniser plans one device: ranks run the phased kernels
         steps["cold"], steps["warm"] = step_cold, step_warm
+
+    kbytes = {}  # per-launch algorithmic bytes the library declares for a timer (count(*) walks)
 
     def kernel_times():
         out = {}
         for k in KERNELS:
-            cnt, ms = ctypes.c_int64(), ctypes.c_double()
+            cnt, ms, b = ctypes.c_int64(), ctypes.c_double(), ctypes.c_double()
             _lib.call("capsmi_session_kernel_time", sess.handle, k.encode(), ctypes.byref(cnt), ctypes.byref(ms))
+            _lib.call("capsmi_session_kernel_bytes", sess.handle, k.encode(), ctypes.byref(b))
             out[k] = (cnt.value, ms.value)
+            if cnt.value and b.value:
+                kbytes[k] = b.value / cnt.value
         return out
 
     results = {}
@@ -373,7 +394,8 @@ def main():
         elif fx is None:
             check = "no fixture for this scale"
         else:
-            bad = {m: v for m, v in answers.items() if v != fx["count_distinct_c"]}
+            bad = {m: v for m, v in answers.items()
+                   if v != (fx["count_star"] if m.startswith("count") else fx["count_distinct_c"])}
             if matched != fx["count_star"]:
                 bad["count_star"] = matched
             check = "ok" if not bad else f"MISMATCH {bad} vs fixture {fx['count_distinct_c']} / {fx['count_star']}"
@@ -388,7 +410,10 @@ def main():
                "part_scatter2": m_local * 16,        # read + write uint2
                "hop1": m_local * 8 + n // 8,         # read uint2 pairs, write M
                "hop2": m_local * 8 + n // 8 * 3,     # read uint2 pairs + X1 + X2, write C
-               "mid_combine": n // 8 * 5, "bitmap_add": n * 8}
+               "mid_combine": n // 8 * 5, "bitmap_add": n * 8,
+               "count_part_in": m_local * 24, "count_part_out": m_local * 24,  # chunked partition pass 1
+               "degrees": m_local * 16 + n * 8}                  # read int64 pairs, inA + outC
+        alg.update(kbytes)
         timed = {k: (c, ms) for k, (c, ms) in kt.items() if c > 0}
         dom = max(timed, key=lambda k: timed[k][1])
         avg_ms = timed[dom][1] / timed[dom][0]
@@ -436,7 +461,8 @@ def main():
         for mode in modes[1:]:
             s2, r2, kt2 = results[mode]
             b2 = warm_alg if mode in ("warm", "direct_warm") else query_alg
-            line["query"][mode] = {"ms_per_step": s2 * 1e3, "value": matched / s2, "count_distinct_c": r2,
+            line["query"][mode] = {"ms_per_step": s2 * 1e3, "value": matched / s2,
+                                   ("count_star" if mode.startswith("count") else "count_distinct_c"): r2,
                                    "alg_bytes_query": b2, "query_frac_of_peak": b2 / s2 / 1e9 / (HBM_PEAK_GBS * world),
                                    "kernel_ms": {k: v[1] / v[0] for k, v in kt2.items() if v[0] > 0}}
         line["cpu_baseline"] = cpu_baseline(scale, ef) if (not args.no_cpu_baseline and world == 1) else None

@@ -1783,6 +1783,21 @@ capsmi_status capsmi_two_hop_count(capsmi_session* s, int32_t nrels, capsmi_tabl
             "closed-form count(*) needs each node id in one scanned row");
     use_device(s);
     const int64_t n = b_ok->hi - b_ok->lo;
+    const bool same_domain = a_ok->lo == b_ok->lo && a_ok->hi == b_ok->hi && c_ok->lo == b_ok->lo && c_ok->hi == b_ok->hi;
+    const char* mode = getenv("CAPSMI_COUNT");  // "atomic": the per-relationship atomic form (A/B runs)
+    if (same_domain && n > 0 && n <= (int64_t(1) << 26) && !(mode && std::string(mode) == "atomic")) {
+        std::vector<const int64_t*> srcs, dsts;
+        std::vector<int64_t> ms;
+        for (int i = 0; i < nrels; ++i) {
+            need(rels[i], "rels[i]");
+            M(rels[i]);
+            srcs.push_back(rel_col(rels[i], src_col).d());
+            dsts.push_back(rel_col(rels[i], dst_col).d());
+            ms.push_back(rels[i]->nrows);
+        }
+        *out_rows = two_hop_count_part(s, srcs.data(), dsts.data(), ms.data(), nrels, a_ok, b_ok, c_ok);
+        return CAPSMI_OK;
+    }
     Buf inA = dev_alloc(sizeof(uint32_t) * (n > 0 ? n : 1), s);
     Buf outC = dev_alloc(sizeof(uint32_t) * (n > 0 ? n : 1), s);
     Buf acc = dev_alloc(16, s);  // [0] = loops, [1] = sum of products

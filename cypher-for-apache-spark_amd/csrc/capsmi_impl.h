@@ -232,6 +232,10 @@ int64_t radix_join(capsmi_session* s, const KeyCols& bk, int64_t nb, const KeyCo
 // not eligible (then nothing was produced)
 bool direct_join(capsmi_session* s, const KeyCols& bk, int64_t nb, const KeyCols& pk, int64_t np, bool outer,
                  Buf& out_p, Buf& out_b, int64_t* total);
+// 2-hop count(*) from two chunked partitions with LDS counts (k_count.hip); bitmaps over one domain of
+// at most 2^26 ids
+int64_t two_hop_count_part(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
+                           int nt, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok);
 void cross_pairs(int64_t nl, int64_t nr, int64_t* out_l, int64_t* out_r, hipStream_t st);
 
 // expressions (k_expr.hip)

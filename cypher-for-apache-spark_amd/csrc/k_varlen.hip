@@ -215,62 +215,11 @@ __device__ __forceinline__ bool f2_test(const uint32_t* f2, uint32_t x, unsigned
     return (f2[((size_t)(x >> kVlBits) * kF2Words) + word] & bits) == bits;
 }
 
-struct ChunkWalk {
-    const uint2* pool;
-    const unsigned long long* meta;
-    const uint32_t* order;
-    const int64_t* jst;
-    const int64_t* segbase;
-    const int* ja;
-    int nt;
-};
+using part::ChunkWalk;
 
-// Block w visits the pairs (x, y) (relative ids; the bucket follows y) of its chunk share in
-// slice order: visit(pair, j) per pair; at every slice change and at the end flush(j) runs between
-// barriers (it must also clear the block's accumulators).  The next chunk is loaded while the
-// current one is visited.
 template <class Visit, class Flush>
 __device__ void walk_chunks(const ChunkWalk& cw, Visit visit, Flush flush) {
-    using namespace part;
-    const int64_t w = blockIdx.x, blocks = gridDim.x;
-    const SegSplit S(cw.jst, cw.nt, blocks);
-    auto load_chunk = [&](int64_t q, uint2 (&pr)[kItems]) -> uint32_t {
-        const uint32_t phys = cw.order[q];
-        const uint32_t fill = (uint32_t)(cw.meta[phys] >> 32);
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint2*>(cw.pool + (size_t)phys * kCh), (short)0, (int)(fill * sizeof(uint2)), 0x00020000);
-#pragma unroll
-        for (int k = 0; k < kItems / 2; ++k) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(k * kVlBlock + (int)threadIdx.x) * 16u, 0, 2);  // nt
-            pr[2 * k] = make_uint2(v[0], v[1]);
-            pr[2 * k + 1] = make_uint2(v[2], v[3]);
-        }
-        return fill;
-    };
-    const int64_t qb = w * S.per, qe = min(qb + S.per, S.nch);
-    if (qb >= qe) return;  // block-uniform
-    uint2 nx[kItems];
-    uint32_t nfill = load_chunk(qb, nx);
-    int cur_j = slice_of(cw.jst, cw.nt, qb);
-    for (int64_t q = qb; q < qe; ++q) {  // block-uniform
-        const int j = slice_of(cw.jst, cw.nt, q);
-        if (j != cur_j) {
-            __syncthreads();
-            flush(cur_j);
-            __syncthreads();
-            cur_j = j;
-        }
-        uint2 pr[kItems];
-#pragma unroll
-        for (int k = 0; k < kItems; ++k) pr[k] = nx[k];
-        const uint32_t fill = nfill;
-        if (q + 1 < qe) nfill = load_chunk(q + 1, nx);
-#pragma unroll
-        for (int k = 0; k < kItems; ++k)
-            if ((uint32_t)(2 * ((k >> 1) * kVlBlock + (int)threadIdx.x) + (k & 1)) < fill) visit(pr[k], j);
-    }
-    __syncthreads();
-    flush(cur_j);
+    part::walk_chunks<kVlBlock>(cw, visit, flush);
 }
 
 __device__ __forceinline__ bool bit_of(const uint32_t* w, int full, uint32_t x) {

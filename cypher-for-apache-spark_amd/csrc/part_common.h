@@ -197,6 +197,98 @@ __device__ __forceinline__ bool gbit(const uint32_t* w, uint32_t x) { return (w[
 // set bit x of an LDS bitmap: a no-return ds_or (a read-then-or measured 0.1 ms slower at C3)
 __device__ __forceinline__ void lds_set(uint32_t* lds, uint32_t x) { atomicOr(&lds[x >> 5], 1u << (x & 31)); }
 
+struct ChunkWalk {
+    const uint2* pool;
+    const unsigned long long* meta;
+    const uint32_t* order;
+    const int64_t* jst;
+    const int64_t* segbase;
+    const int* ja;
+    int nt;
+};
+
+// A chunked partition (chunk_partition below) as its consumers walk it.
+// Block w visits the pairs (x, y) (relative ids; the bucket follows y) of its chunk share in
+// slice order: visit(pair, j) per pair; at every slice change and at the end flush(j) runs between
+// barriers (it must also clear the block's accumulators).  The next chunk is loaded while the
+// current one is visited.
+struct NoBegin {
+    __device__ void operator()(int) const {}
+};
+
+// begin(j) runs (between barriers) before the first pair of each slice the block visits.
+// G chunks are loaded per step (the next group while the current one is visited): with many
+// buckets the chunks are only partly filled, and one chunk in flight per block left the walk
+// latency-bound.
+template <int BLK, int G = 1, class Visit, class Flush, class Begin = NoBegin>
+__device__ void walk_chunks(const ChunkWalk& cw, Visit visit, Flush flush, Begin begin = Begin()) {
+    static_assert(BLK * kItems == kCh, "a block loads one chunk per step");
+    const int64_t w = blockIdx.x, blocks = gridDim.x;
+    const SegSplit S(cw.jst, cw.nt, blocks);
+    const int64_t qb = w * S.per, qe = min(qb + S.per, S.nch);
+    auto load_chunk = [&](int64_t q, uint2 (&pr)[kItems]) -> uint32_t {
+        if (q >= qe) return 0;
+        const uint32_t phys = cw.order[q];
+        const uint32_t fill = (uint32_t)(cw.meta[phys] >> 32);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint2*>(cw.pool + (size_t)phys * kCh), (short)0, (int)(fill * sizeof(uint2)), 0x00020000);
+#pragma unroll
+        for (int k = 0; k < kItems / 2; ++k) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(k * BLK + (int)threadIdx.x) * 16u, 0, 2);  // nt
+            pr[2 * k] = make_uint2(v[0], v[1]);
+            pr[2 * k + 1] = make_uint2(v[2], v[3]);
+        }
+        return fill;
+    };
+    if (qb >= qe) return;  // block-uniform
+    uint2 nx[G][kItems];
+    uint32_t nfill[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) nfill[g] = load_chunk(qb + g, nx[g]);
+    int cur_j = slice_of(cw.jst, cw.nt, qb);
+    int64_t j_end = cw.jst[cur_j + 1];  // chunk q belongs to a later slice once q >= j_end
+    begin(cur_j);
+    __syncthreads();
+    for (int64_t q0 = qb; q0 < qe; q0 += G) {  // block-uniform
+        uint2 pr[G][kItems];
+        uint32_t fill[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            fill[g] = nfill[g];
+#pragma unroll
+            for (int k = 0; k < kItems; ++k) pr[g][k] = nx[g][k];
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) nfill[g] = load_chunk(q0 + G + g, nx[g]);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int64_t q = q0 + g;
+            if (q >= qe) break;
+            int j = cur_j;
+            while (q >= j_end) j_end = cw.jst[++j + 1];  // empty slices are skipped
+            if (j != cur_j) {
+                __syncthreads();
+                flush(cur_j);
+                begin(j);
+                __syncthreads();
+                cur_j = j;
+            }
+#pragma unroll
+            for (int k = 0; k < kItems; ++k)
+                if ((uint32_t)(2 * ((k >> 1) * BLK + (int)threadIdx.x) + (k & 1)) < fill[g]) visit(pr[g][k], j);
+        }
+    }
+    __syncthreads();
+    flush(cur_j);
+}
+
+// whether block w's chunk share holds all of slice j's chunks (then its flush owns the slice)
+__device__ __forceinline__ bool owns_slice(const ChunkWalk& cw, int j) {
+    const SegSplit S(cw.jst, cw.nt, gridDim.x);
+    const int64_t qb = (int64_t)blockIdx.x * S.per, qe = min(qb + S.per, S.nch);
+    return qb <= cw.jst[j] && qe >= cw.jst[j + 1];
+}
+
 }  // namespace part
 
 // Pass 1 of the partition plus chunk ordering and the block-balanced segment split (k_part.hip):

@@ -70,6 +70,28 @@ def test_c3_count_distinct_routed(session, scale):
     assert got == [{"n": rows, "m": rows, "d": dist_a}]
 
 
+@pytest.mark.parametrize("scale,kind", [(13, "all"), (16, "person")])
+def test_c3_count_star_partitioned(session, scale, kind):
+    """count(*) of C3 from the two chunked partitions with LDS counts (k_count.hip) equals the
+    per-relationship atomic form and the oracle's closed form; at scale 16 a slice of 2^15 ids is
+    shared by several blocks' chunk shares (flushed with atomics)."""
+    import os
+    from oracle import cpu
+    sg = _graph(session, scale, kind=kind)
+    q = {"clauses": C3["clauses"], "return": {"items": [["n", ["count*"]]]}}
+    got = _routed(session, "two_hop", lambda: _run(session, sg, q))
+    os.environ["CAPSMI_COUNT"] = "atomic"
+    try:
+        atomic = _run(session, sg, q)
+    finally:
+        del os.environ["CAPSMI_COUNT"]
+    n = 1 << scale
+    src, dst = cpu.rmat_edges(scale, 0, 16 << scale)
+    pm = cpu.person_mask(n) if kind == "person" else np.ones(n, np.uint8)
+    rows, _ = cpu.two_hop_closed_form_mt(n, src, dst, pm, pm, pm)
+    assert got == atomic == [{"n": rows}]
+
+
 def test_c3_unfused_equals_fused(session):
     sg = _graph(session, 8)
     assert _run(session, sg, C3, fused=False) == _run(session, sg, C3)
