@@ -61,6 +61,15 @@ class ColDesc(ctypes.Structure):
     _fields_ = [("name", c_char_p), ("type", c_int32), ("data", c_void_p), ("valid", c_void_p)]
 
 
+class Value(ctypes.Structure):  # capsmi_value
+    _fields_ = [("ival", ctypes.c_int64), ("is_null", c_int32), ("reserved", c_int32)]
+
+
+class Param(ctypes.Structure):  # capsmi_param
+    _fields_ = [("type", c_int32), ("is_list", c_int32), ("count", c_int32), ("reserved", c_int32),
+                ("values", c_void_p)]
+
+
 class ExprColumn(ctypes.Structure):
     _fields_ = [("name", c_char_p), ("nnodes", c_int32), ("prog", POINTER(CapsmiExpr))]
 
@@ -87,6 +96,7 @@ _SIGS = {
     "capsmi_session_set_profiling": (c_int32, [P, c_int32]),
     "capsmi_session_kernel_time": (c_int32, [P, c_char_p, POINTER(c_int64), POINTER(ctypes.c_double)]),
     "capsmi_session_kernel_bytes": (c_int32, [P, c_char_p, POINTER(ctypes.c_double)]),
+    "capsmi_session_set_params": (c_int32, [P, c_int32, P]),
     "capsmi_table_from_host": (c_int32, [P, c_int32, POINTER(ColDesc), c_int64, PP]),
     "capsmi_table_from_device": (c_int32, [P, c_int32, POINTER(ColDesc), c_int64, PP]),
     "capsmi_table_retain": (c_int32, [P]),

@@ -25,7 +25,7 @@ TYPE_NAMES = {I64: "I64", BOOL: "BOOL", F64: "F64", STR: "STR"}
 # expression opcodes (include/capsmi.h CAPSMI_X_*)
 X_COL, X_LIT, X_NULL, X_EQ, X_NEQ, X_LT, X_LE, X_GT, X_GE, X_NOT, X_AND, X_OR = range(12)
 X_ISNULL, X_ISNOTNULL, X_IN, X_ADD, X_SUB, X_MUL, X_NEG, X_COALESCE = range(12, 20)
-X_BITAND, X_BITOR, X_SHL, X_SHRU, X_CASE = range(20, 25)
+X_BITAND, X_BITOR, X_SHL, X_SHRU, X_CASE, X_PARAM = range(20, 26)
 
 BIN_OPS = {"=": X_EQ, "<>": X_NEQ, "<": X_LT, "<=": X_LE, ">": X_GT, ">=": X_GE, "+": X_ADD, "-": X_SUB, "*": X_MUL,
            "&": X_BITAND, "|": X_BITOR, "<<": X_SHL, ">>>": X_SHRU}
@@ -125,6 +125,15 @@ class Case(Expr):
     default: object = None
 
 
+@dataclass(frozen=True, eq=False)
+class Param(Expr):
+    """Param(name) (okapi-ir Expr.scala): query parameter ``index`` of the session's parameter table
+    (``Session.set_params``), bound to a literal by the library when the program is handed over, as
+    SparkSQLExprMapper.scala:86-92 turns it into ``functions.lit``.  A list parameter may only be an
+    element of ``In``, where it stands for its values."""
+    index: int
+
+
 TRUE = Lit(True)
 FALSE = Lit(False)
 NULL = Lit(None)
@@ -197,6 +206,8 @@ def compile_program(e: Expr, column_index: Callable[[str], int], encode_str: Cal
                 out.append((X_NULL, x.type + 1 if x.type >= 0 else 0, 0, 0))
             else:
                 out.append((X_LIT, 0, ty, _lit_bits(x.value, ty, encode_str)))
+        elif isinstance(x, Param):
+            out.append((X_PARAM, x.index, 0, 0))
         elif isinstance(x, BinOp):
             go(x.left)
             go(x.right)

@@ -188,6 +188,34 @@ class Session:
         self.compact_graph(nodes, rels)
         return True
 
+    def set_params(self, values: Sequence[object]) -> None:
+        """Query parameters for ``expr.Param(i)`` (the CypherMap of SparkSQLExprMapper.scala:86-92):
+        ``values[i]`` is a Python scalar (int, float, bool, str, None) or a list of them (usable as the
+        element list of ``In``).  Strings are dictionary-encoded; an int list with a float is Double."""
+        from .expr import BOOL, F64, I64, STR, _lit_bits
+
+        def type_of(v):
+            return BOOL if isinstance(v, bool) else I64 if isinstance(v, int) else F64 if isinstance(v, float) \
+                else STR if isinstance(v, str) else None
+
+        keep, arr = [], (_lib.Param * max(1, len(values)))()
+        for i, v in enumerate(values):
+            items = list(v) if isinstance(v, (list, tuple)) else [v]
+            tys = {type_of(x) for x in items} - {None}
+            if tys == {I64, F64}:
+                tys = {F64}
+            if len(tys) > 1:
+                raise _lib.IllegalArgumentException(f"parameter {i}: mixed value types")
+            ty = tys.pop() if tys else I64
+            vals = (_lib.Value * max(1, len(items)))()
+            for k, x in enumerate(items):
+                vals[k].is_null = 1 if x is None else 0
+                vals[k].ival = 0 if x is None else _lit_bits(x, ty, self.encode_str)
+            keep.append(vals)
+            arr[i].type, arr[i].is_list, arr[i].count, arr[i].values = ty, int(isinstance(v, (list, tuple))), \
+                len(items), ctypes.cast(vals, ctypes.c_void_p)
+        _lib.call("capsmi_session_set_params", self._h, len(values), arr)
+
     def set_fused(self, enabled: bool) -> None:
         """Route lazy plans of the Expand shapes to the fused kernels (default) or run them operator
         by operator (include/capsmi.h capsmi_session_set_fused)."""

@@ -532,6 +532,25 @@ capsmi_status capsmi_session_set_profiling(capsmi_session* s, int32_t enabled) {
     API_END
 }
 
+capsmi_status capsmi_session_set_params(capsmi_session* s, int32_t nparams, const capsmi_param* params) {
+    API_BEGIN
+    need(s, "session");
+    REQUIRE(nparams >= 0 && (nparams == 0 || params), CAPSMI_ERR_ILLEGAL_ARGUMENT, "parameters");
+    std::vector<capsmi_session::Param> ps(nparams);
+    for (int i = 0; i < nparams; ++i) {
+        const capsmi_param& p = params[i];
+        REQUIRE(p.type >= CAPSMI_I64 && p.type <= CAPSMI_STR, CAPSMI_ERR_ILLEGAL_ARGUMENT, "parameter type");
+        REQUIRE(p.is_list ? p.count >= 0 : p.count == 1, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                "a scalar parameter has one value, a list zero or more");
+        REQUIRE(p.count == 0 || p.values, CAPSMI_ERR_ILLEGAL_ARGUMENT, "parameter values");
+        ps[i].type = p.type;
+        ps[i].list = p.is_list != 0;
+        ps[i].values.assign(p.values, p.values + p.count);
+    }
+    s->params = std::move(ps);
+    API_END
+}
+
 capsmi_status capsmi_session_kernel_bytes(capsmi_session* s, const char* name, double* bytes) {
     API_BEGIN
     need(s, "session");
@@ -1154,13 +1173,23 @@ capsmi_status capsmi_bitmap_add_scan(capsmi_bitmap* b, capsmi_table* nodes, cons
     const Column& idc = nodes->cols[col_index(nodes, id_col)];
     REQUIRE(idc.type == CAPSMI_I64, CAPSMI_ERR_ILLEGAL_ARGUMENT, "node id column must be Long");
     Buf flags;
+    RangePred rp;
+    std::vector<capsmi_expr> bound;
+    if (nnodes > 0 && has_params(nnodes, pred)) {
+        bound = bind_params(s, nnodes, pred);
+        pred = bound.data();
+        nnodes = (int32_t)bound.size();
+    }
     if (nnodes > 0) {
-        flags = dev_alloc(nodes->nrows > 0 ? nodes->nrows : 1, s);
-        eval_predicate(s, nodes, nnodes, pred, P<uint8_t>(flags));
+        validate_program(nodes, nnodes, pred);
+        if (!compile_range_pred(nodes, nnodes, pred, rp)) {  // general predicates: a flag column first
+            flags = dev_alloc(nodes->nrows > 0 ? nodes->nrows : 1, s);
+            eval_predicate(s, nodes, nnodes, pred, P<uint8_t>(flags));
+        }
     }
     Buf cnt = dev_alloc(3 * sizeof(int64_t), s);
     HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, 3 * sizeof(int64_t), s->stream));
-    bitmap_add_rows(b, idc.d(), idc.v(), P<uint8_t>(flags), nodes->nrows, P<int64_t>(cnt));
+    bitmap_add_rows(b, idc.d(), idc.v(), P<uint8_t>(flags), nodes->nrows, P<int64_t>(cnt), &rp);
     int64_t h[3];
     HIP_CHECK(hipMemcpyAsync(h, P<void>(cnt), sizeof(h), hipMemcpyDeviceToHost, s->stream));
     HIP_CHECK(hipStreamSynchronize(s->stream));

@@ -90,6 +90,12 @@ struct DenseIds {
 
 struct capsmi_session {
     std::shared_ptr<capsmi::AllocCtx> alloc;  // block cache of this session (api.hip)
+    struct Param {
+        int32_t type = 0;
+        bool list = false;
+        std::vector<capsmi_value> values;
+    };
+    std::vector<Param> params;  // query parameters (capsmi_session_set_params)
     int device = 0;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;  // current (own or external)
@@ -323,6 +329,9 @@ void widen_words(const void* in, int code, int64_t* out, int64_t n, hipStream_t 
 
 // expressions: static result type and validation of a postfix program over a table's schema (k_expr.hip)
 int32_t infer_type(const capsmi_table* t, int32_t nn, const capsmi_expr* prog);
+// a program with every CAPSMI_X_PARAM replaced by its literal(s) from the session's parameters
+std::vector<capsmi_expr> bind_params(const capsmi_session* s, int32_t nn, const capsmi_expr* prog);
+bool has_params(int32_t nn, const capsmi_expr* prog);
 void validate_program(const capsmi_table* t, int32_t nn, const capsmi_expr* prog);
 
 // lazy plans (plan.hip): run the plan (a fused kernel when the recogniser matches) and keep the result
@@ -361,8 +370,18 @@ capsmi_table* read_csv(capsmi_session* s, const std::vector<std::string>& paths,
                        void* ctx, const char* row_id_col);
 
 // graph (k_graph.hip)
-void bitmap_add_rows(capsmi_bitmap* b, const int64_t* ids, const uint8_t* ids_valid,
-                     const uint8_t* flags, int64_t n, int64_t* dev_counters);
+// node predicate compiled for the bitmap scan: AND of range tests on Long columns (k_graph.hip)
+constexpr int kMaxRangeTerms = 4;
+struct RangePred {
+    int n = 0;
+    const int64_t* col[kMaxRangeTerms];
+    const uint8_t* valid[kMaxRangeTerms];
+    int64_t lo[kMaxRangeTerms], hi[kMaxRangeTerms];  // inclusive
+};
+// compile `prog` over table t (AND of comparisons Long column <op> Long literal); false if not of that form
+bool compile_range_pred(const capsmi_table* t, int32_t nn, const capsmi_expr* prog, RangePred& rp);
+void bitmap_add_rows(capsmi_bitmap* b, const int64_t* ids, const uint8_t* ids_valid, const uint8_t* flags, int64_t n,
+                     int64_t* dev_counters, const RangePred* rp = nullptr);
 int64_t words_popcount(capsmi_session* s, const uint32_t* w, int64_t w_begin, int64_t w_end);
 
 }  // namespace capsmi

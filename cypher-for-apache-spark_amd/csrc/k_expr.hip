@@ -233,6 +233,74 @@ int32_t infer_type(const capsmi_table* t, int32_t nn, const capsmi_expr* prog) {
     return ty < 0 ? CAPSMI_I64 : ty;
 }
 
+bool has_params(int32_t nn, const capsmi_expr* prog) {
+    for (int i = 0; i < nn; ++i)
+        if (prog[i].op == CAPSMI_X_PARAM) return true;
+    return false;
+}
+
+// Param(name) -> functions.lit(parameters(name)) (SparkSQLExprMapper.scala:86-92).  Each stack entry
+// of the postfix program is tracked with the number of values it stands for: 1, or a list
+// parameter's length, which only IN may consume (its element count grows by the list's values).
+std::vector<capsmi_expr> bind_params(const capsmi_session* s, int32_t nn, const capsmi_expr* prog) {
+    std::vector<capsmi_expr> out;
+    std::vector<int> width;  // per stack entry: values it contributes (-1 - k: a list of k values)
+    auto lit = [](int32_t type, const capsmi_value& v) {
+        capsmi_expr x{};
+        if (v.is_null) {
+            x.op = CAPSMI_X_NULL;
+            x.arg = type + 1;
+        } else {
+            x.op = CAPSMI_X_LIT;
+            x.type = type;
+            x.ival = v.ival;
+        }
+        return x;
+    };
+    for (int i = 0; i < nn; ++i) {
+        const capsmi_expr& x = prog[i];
+        if (x.op == CAPSMI_X_PARAM) {
+            REQUIRE(x.arg >= 0 && x.arg < (int)s->params.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                    "expression parameter " + std::to_string(x.arg) + " is not set (capsmi_session_set_params)");
+            const capsmi_session::Param& p = s->params[x.arg];
+            if (!p.list) {
+                out.push_back(lit(p.type, p.values[0]));
+                width.push_back(1);
+            } else {
+                for (const capsmi_value& v : p.values) out.push_back(lit(p.type, v));
+                width.push_back(-1 - (int)p.values.size());
+            }
+            continue;
+        }
+        int pops = 0;
+        switch (x.op) {
+            case CAPSMI_X_COL: case CAPSMI_X_LIT: case CAPSMI_X_NULL: pops = 0; break;
+            case CAPSMI_X_NOT: case CAPSMI_X_ISNULL: case CAPSMI_X_ISNOTNULL: case CAPSMI_X_NEG: pops = 1; break;
+            case CAPSMI_X_AND: case CAPSMI_X_OR: case CAPSMI_X_COALESCE: pops = x.arg; break;
+            case CAPSMI_X_IN: pops = x.arg + 1; break;
+            case CAPSMI_X_CASE: pops = 2 * x.arg + 1; break;
+            default: pops = 2; break;
+        }
+        REQUIRE(pops >= 0 && (int)width.size() >= pops, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                "malformed expression program (stack underflow)");
+        capsmi_expr y = x;
+        if (x.op == CAPSMI_X_IN) {
+            const size_t first = width.size() - pops;  // the tested value, then the elements
+            REQUIRE(width[first] == 1, CAPSMI_ERR_ILLEGAL_ARGUMENT, "a list parameter is not a single value");
+            int n = 0;
+            for (size_t k = first + 1; k < width.size(); ++k) n += width[k] >= 0 ? width[k] : -1 - width[k];
+            y.arg = n;
+        } else {
+            for (size_t k = width.size() - pops; k < width.size(); ++k)
+                REQUIRE(width[k] == 1, CAPSMI_ERR_ILLEGAL_ARGUMENT, "a list parameter may only be an element of IN");
+        }
+        width.resize(width.size() - pops);
+        width.push_back(1);
+        out.push_back(y);
+    }
+    return out;
+}
+
 void validate_program(const capsmi_table* t, int32_t nn, const capsmi_expr* prog) {
     int depth = 0, maxd = 0;
     for (int i = 0; i < nn; ++i) {

@@ -104,10 +104,20 @@ __device__ __forceinline__ void bitmap_generic(uint32_t* w, int64_t lo, int64_t 
     }
 }
 
+__device__ __forceinline__ bool range_ok(const RangePred& rp, int64_t i) {
+    bool ok = true;
+    for (int k = 0; k < rp.n; ++k) {
+        const int64_t v = rp.col[k][i];
+        ok = ok && (!rp.valid[k] || rp.valid[k][i]) && v >= rp.lo[k] && v <= rp.hi[k];
+    }
+    return ok;
+}
+
 __global__ void __launch_bounds__(256) k_bitmap_add(uint32_t* w, int64_t lo, int64_t hi, const int64_t* __restrict__ ids,
                                                     const uint8_t* __restrict__ ids_valid,
                                                     const uint8_t* __restrict__ flags, int64_t n, int aligned,
-                                                    unsigned long long* counters /* [0]=added, [1]=dups, [2]=bad */) {
+                                                    unsigned long long* counters /* [0]=added, [1]=dups, [2]=bad */,
+                                                    RangePred rp) {
     __shared__ unsigned long long red[3][4];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned long long added = 0, dups = 0, bad = 0;
@@ -131,7 +141,7 @@ __global__ void __launch_bounds__(256) k_bitmap_add(uint32_t* w, int64_t lo, int
             }
         }
         const int64_t id0 = __shfl(id[0], 0, 64);
-        bool run = whole && !flags && !ids_valid && id0 >= lo && id0 + 256 <= hi;
+        bool run = whole && !flags && !ids_valid && rp.n == 0 && id0 >= lo && id0 + 256 <= hi;
 #pragma unroll
         for (int u = 0; u < 4; ++u) run = run && id[u] == id0 + 128 * (u >> 1) + 2 * lane + (u & 1);
         if (__ballot(!run) == 0) {  // wave-uniform: one ascending run of 256 ids
@@ -152,7 +162,7 @@ __global__ void __launch_bounds__(256) k_bitmap_add(uint32_t* w, int64_t lo, int
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int64_t i = base + 128 * (u >> 1) + 2 * lane + (u & 1);
-            const bool act = i < n && (!flags || flags[i]);
+            const bool act = i < n && (!flags || flags[i]) && range_ok(rp, i);
             const bool valid = act && (!ids_valid || ids_valid[i]);
             bitmap_generic(w, lo, hi, id[u], act, valid, added, dups, bad);
         }
@@ -300,14 +310,15 @@ __global__ void __launch_bounds__(kEpBlock) k_expand_pairs(const int64_t* __rest
     const unsigned long long lt = lane == 0 ? 0ULL : (~0ULL >> (64 - lane));
     int64_t* const outs[4] = {o0, o1, o2, o3};
     const uint64_t ar = (uint64_t)(a.hi - a.lo), br = (uint64_t)(b.hi - b.lo);
-    for (int64_t t0 = (int64_t)blockIdx.x * kEpTile; t0 < m; t0 += (int64_t)gridDim.x * kEpTile) {
-        int64_t s[kEpItems], t[kEpItems];
+    typedef long long v2i64 __attribute__((ext_vector_type(2)));
+    // tile loads; the next tile's are issued while the current tile's bitmap tests are in flight
+    auto load = [&](int64_t t0, int64_t (&s)[kEpItems], int64_t (&t)[kEpItems]) {
+        if (t0 >= m) return;
         if (aligned && t0 + kEpTile <= m) {
 #pragma unroll
             for (int k = 0; k < kEpItems / 2; ++k) {
                 const int i = k * kEpBlock + (int)threadIdx.x;
                 // streamed once: non-temporal, so the lines do not displace the bitmaps in L2
-                typedef long long v2i64 __attribute__((ext_vector_type(2)));
                 const v2i64 sv = __builtin_nontemporal_load(reinterpret_cast<const v2i64*>(src + t0) + i);
                 const v2i64 tv = __builtin_nontemporal_load(reinterpret_cast<const v2i64*>(dst + t0) + i);
                 s[2 * k] = sv.x; s[2 * k + 1] = sv.y; t[2 * k] = tv.x; t[2 * k + 1] = tv.y;
@@ -321,6 +332,11 @@ __global__ void __launch_bounds__(kEpBlock) k_expand_pairs(const int64_t* __rest
                 t[u] = dst[t0 + i];
             }
         }
+    };
+    const int64_t stride = (int64_t)gridDim.x * kEpTile;
+    int64_t s[kEpItems], t[kEpItems], ns[kEpItems], nt[kEpItems];
+    load((int64_t)blockIdx.x * kEpTile, s, t);
+    for (int64_t t0 = (int64_t)blockIdx.x * kEpTile; t0 < m; t0 += stride) {
         // source test for all items (loads in flight together), then target test for the survivors
         bool keep[kEpItems];
         uint32_t wv[kEpItems];
@@ -331,6 +347,7 @@ __global__ void __launch_bounds__(kEpBlock) k_expand_pairs(const int64_t* __rest
             keep[u] = t0 + off < m && x < ar;
             wv[u] = (keep[u] && !a.full) ? a.w[x >> 5] : ~0u;
         }
+        load(t0 + stride, ns, nt);
 #pragma unroll
         for (int u = 0; u < kEpItems; ++u) {
             const uint64_t x = (uint64_t)(s[u] - a.lo), y = (uint64_t)(t[u] - b.lo);
@@ -367,6 +384,11 @@ __global__ void __launch_bounds__(kEpBlock) k_expand_pairs(const int64_t* __rest
                 for (int c = 0; c < NOUT; ++c) __builtin_nontemporal_store(((from_dst >> c) & 1u) ? t[u] : s[u], &outs[c][at]);
             }
             pos += __popcll(bal[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kEpItems; ++u) {
+            s[u] = ns[u];
+            t[u] = nt[u];
         }
         __syncthreads();  // woff / run reused by the next tile
     }
@@ -617,15 +639,94 @@ inline int grid_cap(int64_t n, int64_t cap) {
 // ================================ host side =================================================
 
 void bitmap_add_rows(capsmi_bitmap* b, const int64_t* ids, const uint8_t* ids_valid, const uint8_t* flags, int64_t n,
-                     int64_t* dev_counters) {
+                     int64_t* dev_counters, const RangePred* rp) {
     if (n <= 0) return;
     KernelTimer kt(b->sess, "bitmap_add");
     const int aligned = (((uintptr_t)ids) & 15) == 0;
     const int64_t g = std::min<int64_t>((n + 1023) / 1024, (int64_t)b->sess->num_cus * 8);
     hipLaunchKernelGGL(k_bitmap_add, dim3((unsigned)std::max<int64_t>(g, 1)), dim3(256), 0, b->sess->stream,
                        P<uint32_t>(b->words), b->lo, b->hi, ids, ids_valid, flags, n, aligned,
-                       (unsigned long long*)dev_counters);
+                       (unsigned long long*)dev_counters, rp ? *rp : RangePred());
     HIP_CHECK(hipGetLastError());
+}
+
+// Node predicates of the form the bitmap scan evaluates inline: a conjunction of comparisons between
+// a Long column and a Long literal (C2's `a.age >= 18 AND a.age < 65`).  3VL: a null column value
+// makes its comparison NULL, so the row is not kept (Filter keeps TRUE rows only).
+bool compile_range_pred(const capsmi_table* t, int32_t nn, const capsmi_expr* prog, RangePred& rp) {
+    rp = RangePred();
+    if (nn <= 0) return false;
+    auto arity = [](const capsmi_expr& x) {
+        switch (x.op) {
+            case CAPSMI_X_COL: case CAPSMI_X_LIT: case CAPSMI_X_NULL: return 0;
+            case CAPSMI_X_NOT: case CAPSMI_X_ISNULL: case CAPSMI_X_ISNOTNULL: case CAPSMI_X_NEG: return 1;
+            case CAPSMI_X_AND: case CAPSMI_X_OR: case CAPSMI_X_COALESCE: return (int)x.arg;
+            case CAPSMI_X_IN: return (int)x.arg + 1;
+            case CAPSMI_X_CASE: return 2 * (int)x.arg + 1;
+            default: return 2;
+        }
+    };
+    // conjunct spans [lo, hi] of the root AND (or the root itself)
+    std::vector<std::pair<int, int>> spans;
+    const capsmi_expr& root = prog[nn - 1];
+    if (root.op == CAPSMI_X_AND) {
+        int end = nn - 2;
+        for (int k = 0; k < root.arg; ++k) {
+            int want = 1, i = end;
+            for (; i >= 0; --i) {
+                want += arity(prog[i]) - 1;
+                if (want == 0) break;
+            }
+            if (i < 0) return false;
+            spans.push_back({i, end});
+            end = i - 1;
+        }
+        if (end != -1) return false;
+    } else {
+        spans.push_back({0, nn - 1});
+    }
+    for (const auto& sp : spans) {
+        if (sp.second - sp.first != 2) return false;
+        const capsmi_expr &a = prog[sp.first], &b = prog[sp.first + 1], &op = prog[sp.second];
+        const bool col_first = a.op == CAPSMI_X_COL && b.op == CAPSMI_X_LIT;
+        const bool lit_first = a.op == CAPSMI_X_LIT && b.op == CAPSMI_X_COL;
+        if (!col_first && !lit_first) return false;
+        const capsmi_expr& c = col_first ? a : b;
+        const capsmi_expr& l = col_first ? b : a;
+        if (c.arg < 0 || c.arg >= (int)t->cols.size() || t->cols[c.arg].type != CAPSMI_I64 || l.type != CAPSMI_I64)
+            return false;
+        int o = op.op;
+        if (lit_first) {  // v op col  ==  col op' v
+            if (o == CAPSMI_X_LT) o = CAPSMI_X_GT;
+            else if (o == CAPSMI_X_LE) o = CAPSMI_X_GE;
+            else if (o == CAPSMI_X_GT) o = CAPSMI_X_LT;
+            else if (o == CAPSMI_X_GE) o = CAPSMI_X_LE;
+        }
+        const int64_t v = l.ival;
+        int64_t lo = INT64_MIN, hi = INT64_MAX;
+        switch (o) {
+            case CAPSMI_X_EQ: lo = hi = v; break;
+            case CAPSMI_X_LT: if (v == INT64_MIN) { lo = 1; hi = 0; } else hi = v - 1; break;
+            case CAPSMI_X_LE: hi = v; break;
+            case CAPSMI_X_GT: if (v == INT64_MAX) { lo = 1; hi = 0; } else lo = v + 1; break;
+            case CAPSMI_X_GE: lo = v; break;
+            default: return false;
+        }
+        const Column& col = t->cols[c.arg];
+        int k = 0;
+        while (k < rp.n && rp.col[k] != col.d()) ++k;
+        if (k == rp.n) {
+            if (rp.n == kMaxRangeTerms) return false;
+            rp.col[k] = col.d();
+            rp.valid[k] = col.v();
+            rp.lo[k] = INT64_MIN;
+            rp.hi[k] = INT64_MAX;
+            ++rp.n;
+        }
+        rp.lo[k] = std::max(rp.lo[k], lo);
+        rp.hi[k] = std::min(rp.hi[k], hi);
+    }
+    return true;
 }
 
 int64_t words_popcount(capsmi_session* s, const uint32_t* w, int64_t w_begin, int64_t w_end) {

@@ -1490,6 +1490,12 @@ capsmi_status capsmi_with_column_renamed(capsmi_table* t, const char* old_name, 
 capsmi_status capsmi_filter(capsmi_table* t, int32_t nnodes, const capsmi_expr* prog, capsmi_table** out) {
     return build(t, out, [&] {
         REQUIRE(nnodes == 0 || prog, CAPSMI_ERR_ILLEGAL_ARGUMENT, "null program");
+        std::vector<capsmi_expr> bound;
+        if (has_params(nnodes, prog)) {  // parameters become literals now, as in the Spark plan
+            bound = bind_params(t->sess, nnodes, prog);
+            prog = bound.data();
+            nnodes = (int32_t)bound.size();
+        }
         validate_program(t, nnodes, prog);
         auto p = std::make_shared<PlanNode>();
         p->kind = PlanNode::FILTER;
@@ -1512,10 +1518,12 @@ capsmi_status capsmi_with_columns(capsmi_table* t, int32_t ncols, const capsmi_e
         for (int i = 0; i < ncols; ++i) {
             need(cols[i].name, "column name");
             REQUIRE(cols[i].nnodes == 0 || cols[i].prog, CAPSMI_ERR_ILLEGAL_ARGUMENT, "null program");
-            validate_program(t, cols[i].nnodes, cols[i].prog);
+            std::vector<capsmi_expr> prog(cols[i].prog, cols[i].prog + cols[i].nnodes);
+            if (has_params(cols[i].nnodes, cols[i].prog)) prog = bind_params(t->sess, cols[i].nnodes, cols[i].prog);
+            validate_program(t, (int32_t)prog.size(), prog.data());
             p->a.push_back(cols[i].name);
-            p->progs.emplace_back(cols[i].prog, cols[i].prog + cols[i].nnodes);
-            Column c = schema_col(cols[i].name, infer_type(t, cols[i].nnodes, cols[i].prog), true);
+            Column c = schema_col(cols[i].name, infer_type(t, (int32_t)prog.size(), prog.data()), true);
+            p->progs.push_back(std::move(prog));
             int j = -1;
             for (size_t q = 0; q < sch.size(); ++q) if (sch[q].name == c.name) j = (int)q;
             if (j >= 0) sch[j] = c;  // replaced in place (SparkTable.scala:82-87)

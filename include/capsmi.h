@@ -110,8 +110,12 @@ enum {
     CAPSMI_X_BITOR = 21,    /* Long a | b (:267-268) */
     CAPSMI_X_SHL = 22,      /* Long a << (b & 63) (:270-271, functions.shiftLeft) */
     CAPSMI_X_SHRU = 23,     /* Long a >>> (b & 63) (:273-274, functions.shiftRightUnsigned) */
-    CAPSMI_X_CASE = 24      /* stack [p1, v1, .., p_arg, v_arg, default]: v_i of the first TRUE p_i, else
+    CAPSMI_X_CASE = 24,     /* stack [p1, v1, .., p_arg, v_arg, default]: v_i of the first TRUE p_i, else
                                default (push a NULL for none); CaseExpr, :283-298 */
+    CAPSMI_X_PARAM = 25     /* push query parameter `arg` of the session's table (capsmi_session_set_params);
+                               bound to a literal when the program enters the library, as Param(name) ->
+                               functions.lit (:86-92).  A list parameter may only be an element operand of
+                               IN, where it expands to its values (:86-89, functions.array) */
 };
 
 typedef struct {
@@ -183,6 +187,22 @@ capsmi_status capsmi_session_kernel_bytes(capsmi_session* s, const char* name, d
  * A/B checks), and the number of plans routed to fused entry point `name` ("expand", "expand_count",
  * "two_hop", "triangle", "var_length") since the session started */
 capsmi_status capsmi_session_set_fused(capsmi_session* s, int32_t enabled);
+/* query parameters (the CypherMap handed to asSparkSQLExpr): CAPSMI_X_PARAM `arg` = index into
+ * `params`.  A scalar has count 1 (is_list 0); a list has is_list 1 and `count` values.  Values are
+ * copied; programs built after the call see them. */
+typedef struct {
+    int64_t ival;     /* literal payload, as capsmi_expr.ival */
+    int32_t is_null;
+    int32_t reserved;
+} capsmi_value;
+typedef struct {
+    int32_t type;     /* CAPSMI_I64 / F64 / BOOL / STR (dictionary code) */
+    int32_t is_list;
+    int32_t count;
+    int32_t reserved;
+    const capsmi_value* values;
+} capsmi_param;
+capsmi_status capsmi_session_set_params(capsmi_session* s, int32_t nparams, const capsmi_param* params);
 capsmi_status capsmi_session_route_count(capsmi_session* s, const char* name, int64_t* count);
 
 /* ---- tables (CypherTable: okapi-api/.../api/table/CypherTable.scala:41-68) -------- */

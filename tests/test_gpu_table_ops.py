@@ -183,3 +183,30 @@ def test_join_long_with_double_keys(session, jt):
     o = nb.table(lcols).join(nb.table(rcols), jt, ("l", "r"))
     _same(g, o)
     assert g.size > 0
+
+
+def test_query_parameters(session):
+    """Param(name) -> literal (SparkSQLExprMapper.scala:86-92): filters and projections with
+    parameters equal the same programs with the values inlined; a list parameter expands inside IN."""
+    from capsmi import _lib
+    from capsmi.expr import BinOp, Col, In, IsNull, Lit, Param
+    rng = np.random.default_rng(11)
+    g, o = _tables(session, rng, 3000)
+    session.set_params([3, 0.25, [1, 2, None, 7], "s010", None, []])
+    pairs = [
+        (BinOp("=", Col("k"), Param(0)), BinOp("=", Col("k"), Lit(3))),
+        (BinOp(">=", Col("f"), Param(1)), BinOp(">=", Col("f"), Lit(0.25))),
+        (In(Col("v"), (Param(2),)), In(Col("v"), (Lit(1), Lit(2), Lit(None), Lit(7)))),
+        (In(Col("v"), (Lit(5), Param(2), Param(0))), In(Col("v"), (Lit(5), Lit(1), Lit(2), Lit(None), Lit(7), Lit(3)))),
+        (BinOp("<>", Col("s"), Param(3)), BinOp("<>", Col("s"), Lit("s010"))),
+        (IsNull(Param(4)), IsNull(Lit(None))),
+        (In(Col("k"), (Param(5),)), In(Col("k"), ())),
+    ]
+    for with_param, inlined in pairs:
+        _same(g.filter(with_param), o.filter(inlined))
+    _same(g.withColumns((BinOp("+", Col("k"), Param(0)), "k3")), o.withColumns((BinOp("+", Col("k"), Lit(3)), "k3")))
+    with pytest.raises(_lib.IllegalArgumentException, match="not set"):
+        g.filter(BinOp("=", Col("k"), Param(9)))
+    with pytest.raises(_lib.IllegalArgumentException, match="element of IN"):
+        g.filter(BinOp("=", Col("k"), Param(2)))
+    session.set_params([])
