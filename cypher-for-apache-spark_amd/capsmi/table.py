@@ -275,7 +275,11 @@ class GpuTable:
             _lib.call("capsmi_table_schema", self._h, ctypes.byref(n), buf, len(buf), types, None, self._MAXC)
             if n.value > self._MAXC:
                 raise _lib.NotImplementedException(f"table with {n.value} columns")
-            names = [x.decode() for x in buf.raw.split(b"\0")[:n.value]]
+            raw, names, pos = buf.raw, [], 0  # n NUL-terminated names (not a split of the whole buffer)
+            for _ in range(n.value):
+                end = raw.index(b"\0", pos)
+                names.append(raw[pos:end].decode())
+                pos = end + 1
             self._schema = (names, list(types[:n.value]))
         return self._schema
 
