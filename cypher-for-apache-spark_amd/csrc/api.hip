@@ -1463,8 +1463,8 @@ capsmi_status capsmi_var_length_count(capsmi_session* s, int32_t nrels, capsmi_t
     check_bitmap(a_ok, "a_ok");
     check_bitmap(b_ok, "b_ok");
     REQUIRE(nrels >= 0 && (nrels == 0 || rels), CAPSMI_ERR_ILLEGAL_ARGUMENT, "rels");
-    REQUIRE(lower >= 1 && lower <= upper && upper <= 3, CAPSMI_ERR_NOT_IMPLEMENTED,
-            "fused var-length count supports 1 <= lower <= upper <= 3 (use the join plan otherwise)");
+    REQUIRE(lower >= 0 && lower <= upper && upper >= 1 && upper <= 3, CAPSMI_ERR_NOT_IMPLEMENTED,
+            "fused var-length count supports 0 <= lower <= upper <= 3, upper >= 1 (use the join plan otherwise)");
     REQUIRE(a_ok->lo == b_ok->lo && a_ok->hi == b_ok->hi, CAPSMI_ERR_UNSUPPORTED, "a and b scans need one id domain");
     REQUIRE(!a_ok->any_dup && !b_ok->any_dup, CAPSMI_ERR_UNSUPPORTED,
             "fused count(*) needs each node id in one scanned row");
@@ -1515,8 +1515,8 @@ capsmi_status capsmi_varlen_shard_begin(capsmi_session* s, int32_t nout, capsmi_
     check_bitmap(b_ok, "b_ok");
     REQUIRE(nout >= 0 && (nout == 0 || out_rels) && nin >= 0 && (nin == 0 || in_rels), CAPSMI_ERR_ILLEGAL_ARGUMENT,
             "rels");
-    REQUIRE(lower >= 1 && lower <= upper && upper <= 3, CAPSMI_ERR_NOT_IMPLEMENTED,
-            "fused var-length count supports 1 <= lower <= upper <= 3 (use the join plan otherwise)");
+    REQUIRE(lower >= 0 && lower <= upper && upper >= 1 && upper <= 3, CAPSMI_ERR_NOT_IMPLEMENTED,
+            "fused var-length count supports 0 <= lower <= upper <= 3, upper >= 1 (use the join plan otherwise)");
     REQUIRE(a_ok->lo == b_ok->lo && a_ok->hi == b_ok->hi, CAPSMI_ERR_UNSUPPORTED, "a and b scans need one id domain");
     REQUIRE(!a_ok->any_dup && !b_ok->any_dup, CAPSMI_ERR_UNSUPPORTED,
             "fused count(*) needs each node id in one scanned row");

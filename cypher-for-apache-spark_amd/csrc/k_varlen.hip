@@ -1,6 +1,7 @@
 // k_varlen.hip -- fused BoundedVarLengthExpand + grouped count (C5), never materialising paths.
 //
-//   MATCH (a)-[r*lower..upper]->(b) WHERE a_ok(a) AND b_ok(b) RETURN id(a), count(*)   (1 <= lower <= upper <= 3)
+//   MATCH (a)-[r*lower..upper]->(b) WHERE a_ok(a) AND b_ok(b) RETURN id(a), count(*)   (0 <= lower <= upper <= 3,
+//   upper >= 1; lower = 0 adds the zero-length path, whose b is a copy of a without b's node scan)
 //
 // CAPS plans this as `upper` chained joins with an isomorphism filter per hop and a union over the
 // lengths (VarLengthExpandPlanner.scala:83-136, 146-171, 247-260): one row per edge-distinct path.
@@ -97,6 +98,7 @@ __global__ void k_final(int64_t n, Dom d, int lower, int upper, const unsigned l
             const int64_t c1 = o;
             const int64_t c2 = (int64_t)T2[i] - sl * ba;
             const int64_t c3 = (int64_t)T3[i] - sl * (o - 2 * ba);
+            if (lower == 0) total += 1;  // the zero-length path: b is a copy of a (VarLengthExpandPlanner.scala:146-153)
             if (lower <= 1 && upper >= 1) total += c1;
             if (lower <= 2 && upper >= 2) total += c2;
             if (lower <= 3 && upper >= 3) total += c3;

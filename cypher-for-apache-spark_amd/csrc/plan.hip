@@ -910,9 +910,24 @@ bool fused_var_length(capsmi_session* s, const capsmi_table* in, const PlanNode&
     BitmapSet bs;
     capsmi_bitmap *abm = nullptr, *bbm = nullptr;
     RelViews views;
+    std::string zero_key;  // the zero-length branch's start scan (lower = 0)
+    bool first = true;
     for (size_t bi = 0; bi < B.size(); ++bi) {
         const Path& P = B[bi];
         const int k = (int)P.hops.size();
+        if (k == 0) {
+            // lower = 0: copyEntity(source -> target) of the start scan (VarLengthExpandPlanner.scala:146-153,
+            // 190-210) -- one row per scanned start node, whatever the target's labels; count(*) only
+            if (lens.count(0) || ag.kind != CAPSMI_AGG_COUNT_STAR || P.pos_node.empty() || P.pos_node[0] < 0) return false;
+            if (position_of(P, P.cols[gc]) != 0 || !id_like(P, P.cols[gc])) return false;
+            Classified c;
+            if (!classify(P, c) || !c.uniq.empty()) return false;
+            for (size_t q = 0; q < P.inst.size(); ++q)
+                if (!c.pred[q].empty() && (int)q != P.pos_node[0]) return false;
+            if (!node_bitmap(s, P, c, P.pos_node[0], lo, hi, bs, &zero_key)) return false;
+            lens.insert(0);
+            continue;
+        }
         if (k < 1 || !is_chain(P) || !same_orientation(P) || lens.count(k)) return false;
         lens.insert(k);
         for (int q = 1; q < k; ++q) if (P.pos_node[q] >= 0) return false;  // hops are not node-scanned
@@ -935,14 +950,15 @@ bool fused_var_length(capsmi_session* s, const capsmi_table* in, const PlanNode&
         for (int h = 0; h < k; ++h) {
             RelViews v;
             rel_views(P, P.hops[h], v);
-            if (bi == 0 && h == 0) { rsig = v.sig; views.t.swap(v.t); }
+            if (first && h == 0) { rsig = v.sig; views.t.swap(v.t); }
             else if (v.sig != rsig) return false;
         }
-        if (bi == 0) { akey = ka; bkey = kb; abm = a; bbm = b; }
+        if (first) { akey = ka; bkey = kb; abm = a; bbm = b; first = false; }
         else if (ka != akey || kb != bkey) return false;
     }
+    if (first || (lens.count(0) && zero_key != akey)) return false;  // a path of >= 1 hop; one start scan
     const int l = *lens.begin(), u = *lens.rbegin();
-    if (l < 1 || u > 3 || u - l + 1 != (int)lens.size()) return false;
+    if (l < 0 || u > 3 || u - l + 1 != (int)lens.size()) return false;
     check(capsmi_var_length_count(s, (int32_t)views.t.size(), views.t.data(), "s", "t", abm, bbm, l, u, g.a[0].c_str(),
                                   ag.output.c_str(), out));
     if (g_dense) {  // start ids back to the graph's Long ids

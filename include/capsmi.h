@@ -395,8 +395,10 @@ capsmi_status capsmi_two_hop_count_distinct_part(capsmi_session* s, const capsmi
                                                  int64_t* out_distinct);
 /* BoundedVarLengthExpand + grouped count, fused (C5):
  *   MATCH (a)-[r*lower..upper]->(b) WHERE a_ok(a) AND b_ok(b) RETURN id(a) AS <id_name>, count(*) AS <count_name>
- * with edge-distinct paths (VarLengthExpandPlanner.scala:83-136, 179-180), 1 <= lower <= upper <= 3.
- * One output row per a with at least one path.  a_ok and b_ok must share one id domain. */
+ * with edge-distinct paths (VarLengthExpandPlanner.scala:83-136, 179-180), 0 <= lower <= upper <= 3,
+ * upper >= 1.  lower = 0 adds the zero-length path of every a_ok node (copyEntity, :146-153, 190-210:
+ * b is a copy of a, without b's node scan).  One output row per a with at least one path.  a_ok and
+ * b_ok must share one id domain. */
 capsmi_status capsmi_var_length_count(capsmi_session* s, int32_t nrels, capsmi_table* const* rels,
                                       const char* src_col, const char* dst_col, const capsmi_bitmap* a_ok,
                                       const capsmi_bitmap* b_ok, int32_t lower, int32_t upper, const char* id_name,

@@ -145,8 +145,9 @@ def test_c4_triangle_routed(session):
     assert got == [{"n": cpu.triangle_enumerate(1 << scale, src, dst)}]
 
 
-@pytest.mark.parametrize("lo,hi", [(1, 3), (1, 1), (2, 3)])
+@pytest.mark.parametrize("lo,hi", [(1, 3), (1, 1), (2, 3), (0, 3), (0, 1)])
 def test_c5_var_length_routed(session, lo, hi):
+    """lower = 0 adds the zero-length path of every start node (VarLengthExpandPlanner.scala:146-153)."""
     from oracle import cpu
     scale = 8
     sg = _graph(session, scale, ef=32, probs=(45, 15, 15), rtype="KNOWS")
@@ -154,10 +155,12 @@ def test_c5_var_length_routed(session, lo, hi):
          "return": {"items": [["a", ["id", "a"]], ["n", ["count*"]]]}}
     got = _routed(session, "var_length", lambda: _run(session, sg, q))
     src, dst = cpu.rmat_edges(scale, 0, 32 << scale, (45, 15, 15), 42)
-    _, per_a = cpu.var_length_count(1 << scale, src, dst, lo, hi)
+    _, per_a = cpu.var_length_count(1 << scale, src, dst, max(lo, 1), hi)
+    if lo == 0:
+        per_a = per_a + 1
     want = [{"a": int(i), "n": int(per_a[i])} for i in np.nonzero(per_a)[0]]
     assert same_rows(got, want)
-    if (lo, hi) == (1, 3) and scale <= 8:
+    if (lo, hi) in ((1, 3), (0, 3)) and scale <= 8:
         assert same_rows(_run(session, sg, q, fused=False), want)
 
 
