@@ -229,6 +229,8 @@ def main():
     assert nw % shards == 0, "owner slices must be equal for the all-gather"
     wb, we = graph.owner_words(n, rank, shards)
     modes = [m.strip() for m in args.modes.split(",") if m.strip()]
+    if world > 1 or args.shard_of:  # count(*) needs every middle node's in- and out-degree: one device
+        modes = [m for m in modes if not m.startswith("count")] or ["cold"]
 
     # ---- ingest (untimed): partitioned relationship table + Person node table --------------------
     t0 = time.perf_counter()
