@@ -298,6 +298,12 @@ struct TriGraph {
     int64_t lo = 0, n = 0, ne = 0;
     Buf ok, ov, off;  // oriented keys (from<<32|to), payload (m(from,to)<<32|m(to,from)), CSR offsets (n + 1)
     Buf tg;           // uint32 targets of the oriented edges (the `to` of ok)
+    // Ids are the degree order (0 = highest (degree, id)), so the hub vertices' out-lists -- the ones
+    // the wedge walk re-reads -- are the prefix [0, hot_end) of tg, and their targets are hubs too:
+    // that prefix is also kept as uint16 (vertices 0 .. 2^16 - 1)
+    Buf tg16;
+    int64_t hot_end = 0;
+    Buf orig;         // int64 per vertex: relative id of the degree-order id (unused by the count)
     Buf ek, ev, sl;   // undirected keys / payload (pair terms), self-loop counts
     Buf small_u, big_u;  // vertices with out-degree in [2, 64] / above 64
     int64_t nsmall = 0, nbig = 0;

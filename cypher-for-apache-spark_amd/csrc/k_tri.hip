@@ -95,22 +95,47 @@ __global__ void k_und_runs(const uint64_t* __restrict__ uk, const int64_t* __res
     }
 }
 
-// orient each undirected edge from the lower (degree, id) end; payload = m(from,to)<<32 | m(to,from)
+// (degree, id) sort keys of the vertices
+__global__ void k_deg_keys(const uint32_t* __restrict__ deg, int64_t n, uint64_t* __restrict__ key,
+                           int64_t* __restrict__ val) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        key[i] = ((uint64_t)deg[i] << 32) | (uint64_t)i;
+        val[i] = i;
+    }
+}
+
+// degree-order ids: the vertex at position p of the ascending (degree, id) order gets n - 1 - p
+__global__ void k_rank_ids(const int64_t* __restrict__ by_order, int64_t n, uint32_t* __restrict__ rid,
+                           int64_t* __restrict__ orig) {
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t v = by_order[p], r = n - 1 - p;
+        rid[v] = (uint32_t)r;
+        orig[r] = v;
+    }
+}
+
+// orient each undirected edge from the lower (degree, id) end -- towards the smaller degree-order id;
+// key = rid(from)<<32 | rid(to), payload = m(from,to)<<32 | m(to,from)
 __global__ void k_orient(const uint64_t* __restrict__ ek, const int64_t* __restrict__ ev, int64_t ne,
-                         const uint32_t* __restrict__ deg, uint64_t* __restrict__ ok_, int64_t* __restrict__ ov) {
+                         const uint32_t* __restrict__ rid, uint64_t* __restrict__ ok_, int64_t* __restrict__ ov) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t x = (uint32_t)(ek[i] >> 32), y = (uint32_t)ek[i];
         const uint64_t v = (uint64_t)ev[i];
         const uint32_t mxy = (uint32_t)(v >> 32), myx = (uint32_t)v;
-        const bool x_first = deg[x] < deg[y] || (deg[x] == deg[y] && x < y);
-        if (x_first) {
-            ok_[i] = ((uint64_t)x << 32) | y;
+        const uint32_t rx = rid[x], ry = rid[y];
+        if (rx > ry) {  // x is lower in (degree, id)
+            ok_[i] = ((uint64_t)rx << 32) | ry;
             ov[i] = (int64_t)(((uint64_t)mxy << 32) | myx);
         } else {
-            ok_[i] = ((uint64_t)y << 32) | x;
+            ok_[i] = ((uint64_t)ry << 32) | rx;
             ov[i] = (int64_t)(((uint64_t)myx << 32) | mxy);
         }
     }
+}
+
+__global__ void k_targets16(const uint32_t* __restrict__ tg, int64_t n, uint16_t* __restrict__ tg16) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        tg16[i] = (uint16_t)tg[i];
 }
 
 // CSR offsets of the oriented (sorted) edges: off[v] = first edge with source >= v
@@ -213,9 +238,19 @@ struct SmallWave {
     int64_t voff[kSmallDeg];
     uint32_t vl[kSmallDeg];
     uint32_t pre[kSmallDeg];
+    uint32_t dv[kSmallDeg];
 };
 
-__global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restrict__ tg, const int64_t* __restrict__ ov,
+// target of oriented edge `pos`: 2 bytes inside the hub prefix, 4 beyond it
+__device__ __forceinline__ uint32_t target(const uint32_t* __restrict__ tg, const uint16_t* __restrict__ tg16,
+                                          int64_t hot_end, int64_t pos) {
+    return pos < hot_end ? (uint32_t)tg16[pos] : tg[pos];
+}
+
+template <bool LISTS>  // LISTS: the wave walks each out(v) with all lanes (as k_tri_big_items<true>)
+__global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restrict__ tg,
+                                                         const uint16_t* __restrict__ tg16, int64_t hot_end,
+                                                         const int64_t* __restrict__ ov,
                                                          const int64_t* __restrict__ off,
                                                          const int64_t* __restrict__ us, int64_t nu,
                                                          unsigned long long* __restrict__ out) {
@@ -242,6 +277,7 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
             W.vl[lane] = v;
             W.vp[lane] = pv;
             W.voff[lane] = vo;
+            W.dv[lane] = dv;
             hinsert(W.hk, W.hi, 9, v, (uint32_t)lane);
             bset(W.bf, kSmallBloomBits, v);
         }
@@ -256,6 +292,32 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (LISTS) {
+            for (int k = 0; k < d; ++k) {
+                const int64_t vo = W.voff[k];
+                const uint32_t dvk = W.dv[k];
+                const uint64_t puv = W.vp[k];
+                for (uint32_t j0 = lane; j0 < dvk; j0 += kWedgeUnroll * 64) {
+                    int64_t pos[kWedgeUnroll];
+                    uint32_t w[kWedgeUnroll];
+#pragma unroll
+                    for (int r = 0; r < kWedgeUnroll; ++r) {
+                        const uint32_t j = j0 + r * 64;
+                        pos[r] = vo + j;
+                        w[r] = j < dvk ? target(tg, tg16, hot_end, pos[r]) : kEmpty;
+                    }
+#pragma unroll
+                    for (int r = 0; r < kWedgeUnroll; ++r) {
+                        if (w[r] == kEmpty || !btest(W.bf, kSmallBloomBits, w[r])) continue;
+                        const int sl = hfind(W.hk, 9, w[r]);
+                        if (sl >= 0) acc += tri_weight(puv, (uint64_t)ov[pos[r]], W.vp[W.hi[sl]]);
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();  // the wave's LDS is reused for the next u
+            continue;
+        }
         // the lane's current v: index, list base (voff - pre) and the next v's first wedge, in
         // registers; LDS is read only when the lane moves to another v
         int i = 0;
@@ -275,7 +337,7 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
                 }
                 ii[k] = i;
                 pos[k] = base + f;
-                w[k] = f < total ? tg[pos[k]] : kEmpty;
+                w[k] = f < total ? target(tg, tg16, hot_end, pos[k]) : kEmpty;
             }
 #pragma unroll
             for (int k = 0; k < kWedgeUnroll; ++k) {
@@ -361,7 +423,14 @@ __global__ void k_tri_item_map(const int64_t* __restrict__ ipre, int64_t nu, uin
         for (int64_t it = ipre[q]; it < ipre[q + 1]; ++it) item_q[it] = (uint32_t)q;
 }
 
+// LISTS (default): each wave walks whole out(v) lists of the item's v chunk (wave q takes v = q, q + 16,
+// ...), its lanes striding the list -- coalesced loads, no per-wedge segment search.  The wedges of
+// big u lie in long lists (wedge-weighted mean ≈600 at R-MAT s = 22; 99.8 % in lists of ≥ 64), so the
+// lanes stay busy; the flat form below (one prefix-sum index range over the chunk's wedges) spent
+// ≈70 VALU instructions per wedge on the cursor and the segment search and was issue-bound.
+template <bool LISTS>
 __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __restrict__ tg,
+                                                             const uint16_t* __restrict__ tg16, int64_t hot_end,
                                                              const int64_t* __restrict__ ov,
                                                              const int64_t* __restrict__ off,
                                                              const int64_t* __restrict__ us, int64_t nu,
@@ -404,6 +473,32 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
             L.dv[k] = (uint32_t)(off[v + 1] - vo);
         }
         __syncthreads();
+        if (LISTS) {
+            const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+            for (int k = wave; k < vn; k += kBigBlock / 64) {
+                const int64_t vo = L.voff[k];
+                const int64_t dv = (int64_t)L.dv[k];
+                const uint64_t puv = L.vp[k];
+                for (int64_t j0 = lane; j0 < dv; j0 += kWedgeUnroll * 64) {
+                    int64_t pos[kWedgeUnroll];
+                    uint32_t w[kWedgeUnroll];
+#pragma unroll
+                    for (int r = 0; r < kWedgeUnroll; ++r) {
+                        const int64_t j = j0 + r * 64;
+                        pos[r] = vo + j;
+                        w[r] = j < dv ? target(tg, tg16, hot_end, pos[r]) : kEmpty;
+                    }
+#pragma unroll
+                    for (int r = 0; r < kWedgeUnroll; ++r) {
+                        if (w[r] == kEmpty || !btest(L.bf, kBigBloomBits, w[r])) continue;
+                        const int sl = hfind(L.hk, 13, w[r]);
+                        if (sl >= 0) acc += tri_weight(puv, (uint64_t)ov[pos[r]], (uint64_t)ov[b + h0 + L.hi[sl]]);
+                    }
+                }
+            }
+            __syncthreads();
+            continue;
+        }
         const uint32_t tw = big_scan(L.dv, L.pre, vn, L.wtot);
         int i = 0;  // the lane's current v, as in k_tri_small
         int64_t base = L.voff[0];
@@ -423,7 +518,7 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
                 }
                 ii[k] = i;
                 pos[k] = base + f;
-                w[k] = f < tw ? tg[pos[k]] : kEmpty;
+                w[k] = f < tw ? target(tg, tg16, hot_end, pos[k]) : kEmpty;
             }
 #pragma unroll
             for (int k = 0; k < kWedgeUnroll; ++k) {
@@ -570,17 +665,38 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     if (ne > 0)
         hipLaunchKernelGGL(k_und_runs, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(uk), P<int64_t>(uv),
                            P<int64_t>(heads2), ne, nuvalid, P<uint64_t>(g.ek), P<int64_t>(g.ev), P<uint32_t>(deg));
+    // degree-order ids (hubs first): sort the vertices by (degree, id)
+    Buf rid = dev_alloc(sizeof(uint32_t) * n, s);
+    g.orig = dev_alloc(sizeof(int64_t) * n, s);
+    {
+        Buf dk = dev_alloc(sizeof(uint64_t) * n, s), dv = dev_alloc(sizeof(int64_t) * n, s);
+        hipLaunchKernelGGL(k_deg_keys, dim3(grid(s, n)), dim3(256), 0, st, P<uint32_t>(deg), n, P<uint64_t>(dk),
+                           P<int64_t>(dv));
+        std::vector<int> dd;
+        for (int sh = 0; sh < bits; sh += 8) dd.push_back(sh);
+        for (int sh = 32; sh < 64; sh += 8) dd.push_back(sh);
+        radix_sort_digits(s, P<uint64_t>(dk), P<int64_t>(dv), n, dd);
+        hipLaunchKernelGGL(k_rank_ids, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(dv), n, P<uint32_t>(rid),
+                           P<int64_t>(g.orig));
+    }
     g.ok = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), s);
     g.ov = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);
     if (ne > 0)
         hipLaunchKernelGGL(k_orient, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ek), P<int64_t>(g.ev), ne,
-                           P<uint32_t>(deg), P<uint64_t>(g.ok), P<int64_t>(g.ov));
+                           P<uint32_t>(rid), P<uint64_t>(g.ok), P<int64_t>(g.ov));
     radix_sort_digits(s, P<uint64_t>(g.ok), P<int64_t>(g.ov), ne, od);  // no kNone among the oriented keys
     g.off = dev_alloc(sizeof(int64_t) * (n + 1), s);
     hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, n, P<int64_t>(g.off));
     g.tg = dev_alloc(sizeof(uint32_t) * (ne > 0 ? ne : 1), s);
     if (ne > 0)
         hipLaunchKernelGGL(k_targets, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, P<uint32_t>(g.tg));
+    // the hub prefix: out-lists of vertices 0 .. 2^16 - 1, whose targets are smaller ids, as uint16
+    const int64_t nhub = std::min<int64_t>(n, int64_t(1) << 16);
+    g.hot_end = read_scalar(s, P<int64_t>(g.off) + nhub);
+    g.tg16 = dev_alloc(sizeof(uint16_t) * (g.hot_end > 0 ? g.hot_end : 1), s);
+    if (g.hot_end > 0)
+        hipLaunchKernelGGL(k_targets16, dim3(grid(s, g.hot_end)), dim3(256), 0, st, P<uint32_t>(g.tg), g.hot_end,
+                           P<uint16_t>(g.tg16));
     Buf fsm = dev_alloc(n, s), fbg = dev_alloc(n, s);
     hipLaunchKernelGGL(k_tri_bins, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), n, P<uint8_t>(fsm),
                        P<uint8_t>(fbg));
@@ -614,16 +730,24 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
             Buf ctr = dev_alloc(sizeof(unsigned long long), s);
             HIP_CHECK(hipMemsetAsync(P<void>(ctr), 0, sizeof(unsigned long long), st));
             const size_t lds = sizeof(ItemLds);
-            HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_tri_big_items),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            hipLaunchKernelGGL(k_tri_big_items, dim3((unsigned)(s->num_cus * 4)), dim3(kBigBlock), lds, st,
-                               P<uint32_t>(g.tg), P<int64_t>(g.ov), P<int64_t>(g.off), bu, nb, ipre, P<uint32_t>(iq),
+            const char* walk = getenv("CAPSMI_TRI_WALK");  // "flat": the prefix-sum walk (A/B runs)
+            const bool lists = !(walk && std::string(walk) == "flat");
+            const void* kf = lists ? reinterpret_cast<const void*>(k_tri_big_items<true>)
+                                   : reinterpret_cast<const void*>(k_tri_big_items<false>);
+            HIP_CHECK(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            hipLaunchKernelGGL(lists ? k_tri_big_items<true> : k_tri_big_items<false>, dim3((unsigned)(s->num_cus * 4)),
+                               dim3(kBigBlock), lds, st,
+                               P<uint32_t>(g.tg), P<uint16_t>(g.tg16), g.hot_end, P<int64_t>(g.ov), P<int64_t>(g.off),
+                               bu, nb, ipre, P<uint32_t>(iq),
                                P<unsigned long long>(ctr), P<unsigned long long>(out));
         }
         if (se > sb) {
             const int64_t gs = std::min<int64_t>((se - sb + 3) / 4, (int64_t)s->num_cus * 16);
-            hipLaunchKernelGGL(k_tri_small, dim3((unsigned)gs), dim3(kTriBlock), 0, st, P<uint32_t>(g.tg),
-                               P<int64_t>(g.ov), P<int64_t>(g.off), P<int64_t>(g.small_u) + sb, se - sb,
+            const char* sw = getenv("CAPSMI_TRI_WALK");  // "flat": the prefix-sum walk (A/B runs)
+            const bool slists = !(sw && std::string(sw) == "flat");
+            hipLaunchKernelGGL(slists ? k_tri_small<true> : k_tri_small<false>, dim3((unsigned)gs), dim3(kTriBlock), 0, st,
+                               P<uint32_t>(g.tg),
+                               P<uint16_t>(g.tg16), g.hot_end, P<int64_t>(g.ov), P<int64_t>(g.off), P<int64_t>(g.small_u) + sb, se - sb,
                                P<unsigned long long>(out));
         }
     }

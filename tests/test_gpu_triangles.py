@@ -43,14 +43,21 @@ def test_node_filter_and_parts(session):
     assert _count(session, n, src, dst, mask, nparts=4) == want
 
 
+@pytest.mark.parametrize("walk", ["lists", "flat"])
 @pytest.mark.parametrize("scale", [9, 12])
-def test_rmat(session, scale):
+def test_rmat(session, monkeypatch, scale, walk):
+    if walk == "flat":
+        monkeypatch.setenv("CAPSMI_TRI_WALK", "flat")
     src, dst = cpu.rmat_edges(scale, 0, 16 << scale)
     assert _count(session, 1 << scale, src, dst) == cpu.triangle_enumerate(1 << scale, src, dst)
 
 
-def test_dense_big_vertices(session):
-    """Out-degrees above 64 (one workgroup per vertex) on a dense random multigraph."""
+@pytest.mark.parametrize("walk", ["lists", "flat"])
+def test_dense_big_vertices(session, monkeypatch, walk):
+    """Out-degrees above 64 (one workgroup per vertex) on a dense random multigraph; both wedge
+    walks (wave-per-list default, CAPSMI_TRI_WALK=flat prefix-sum walk)."""
+    if walk == "flat":
+        monkeypatch.setenv("CAPSMI_TRI_WALK", "flat")
     rng = np.random.default_rng(11)
     n, m = 300, 40000
     src = rng.integers(0, n, m).astype(np.int64)
