@@ -20,8 +20,13 @@ namespace tri {
 
 constexpr uint64_t kNone = ~0ULL;
 
+// Undirected keys of the kept, non-loop relationships: min << 32 | max in the low word with the
+// direction bit beside it (bit 31 when the sorted digits of max end below it, else bit 0 with max
+// shifted up: `msh` = 0 / 1).  Self-loops are counted directly.  Dropped relationships get kNone,
+// which sorts last: a valid key's min is at most n - 2, below the all-ones digits of kNone.
 __global__ void k_pack(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, int64_t lo,
-                       int64_t hi, const uint32_t* __restrict__ okw, int full, uint64_t* __restrict__ key) {
+                       int64_t hi, const uint32_t* __restrict__ okw, int full, int msh, uint64_t* __restrict__ key,
+                       uint32_t* __restrict__ sl) {
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t s = src[e], t = dst[e];
         bool ok = s >= lo && s < hi && t >= lo && t < hi;
@@ -29,45 +34,32 @@ __global__ void k_pack(const int64_t* __restrict__ src, const int64_t* __restric
             const uint64_t xs = (uint64_t)(s - lo), xt = (uint64_t)(t - lo);
             ok = ((okw[xs >> 5] >> (xs & 31)) & 1u) && ((okw[xt >> 5] >> (xt & 31)) & 1u);
         }
-        key[e] = ok ? (((uint64_t)(s - lo) << 32) | (uint64_t)(t - lo)) : kNone;
-    }
-}
-
-// run heads of a sorted key array (valid keys only)
-__global__ void k_heads(const uint64_t* __restrict__ k, int64_t n, uint8_t* __restrict__ f) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        f[i] = (k[i] != kNone && (i == 0 || k[i] != k[i - 1])) ? 1 : 0;
-}
-
-// directed runs -> self-loop counts, and undirected records (key = min<<32|max, val = m(min,max)<<32 | m(max,min))
-__global__ void k_dir_runs(const uint64_t* __restrict__ k, const int64_t* __restrict__ heads, int64_t nruns,
-                           int64_t nvalid, uint32_t* __restrict__ sl, uint64_t* __restrict__ ukey,
-                           int64_t* __restrict__ uval) {
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < nruns; r += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t h = heads[r], h2 = r + 1 < nruns ? heads[r + 1] : nvalid;
-        const uint64_t c = (uint64_t)(h2 - h);
-        const uint64_t key = k[h];
-        const uint32_t s = (uint32_t)(key >> 32), t = (uint32_t)key;
-        if (s == t) {
-            sl[s] = (uint32_t)c;
-            ukey[r] = kNone;
-            uval[r] = 0;
-        } else if (s < t) {
-            ukey[r] = ((uint64_t)s << 32) | t;
-            uval[r] = (int64_t)(c << 32);
-        } else {
-            ukey[r] = ((uint64_t)t << 32) | s;
-            uval[r] = (int64_t)c;
+        uint64_t k = kNone;
+        if (ok) {
+            const uint64_t xs = (uint64_t)(s - lo), xt = (uint64_t)(t - lo);
+            if (xs == xt) {
+                atomicAdd(&sl[xs], 1u);
+            } else {
+                const uint64_t mn = xs < xt ? xs : xt, mx = xs < xt ? xt : xs, dir = xs > xt;
+                k = (mn << 32) | (msh ? (mx << 1) | dir : (dir << 31) | mx);
+            }
         }
+        key[e] = k;
     }
 }
 
-// undirected runs (<= 2 records each) -> combined multiplicities, degrees.  The runs are sorted
-// by their lower end, so a wave's lanes with the same lower end are contiguous: one atomic per
-// such segment (hubs would otherwise serialise hundreds of thousands of adds on one counter).
-__global__ void k_und_runs(const uint64_t* __restrict__ uk, const int64_t* __restrict__ uv,
-                           const int64_t* __restrict__ heads, int64_t nruns, int64_t nvalid,
-                           uint64_t* __restrict__ ek, int64_t* __restrict__ ev, uint32_t* __restrict__ deg) {
+// run heads of the sorted undirected keys (direction bit masked off; valid keys only)
+__global__ void k_heads(const uint64_t* __restrict__ k, int64_t n, uint64_t mask, uint8_t* __restrict__ f) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        f[i] = (k[i] != kNone && (i == 0 || (k[i] & mask) != (k[i - 1] & mask))) ? 1 : 0;
+}
+
+// undirected runs -> (key min<<32|max, payload m(min,max)<<32 | m(max,min)), degrees.  The runs are
+// sorted by their lower end, so a wave's lanes with the same lower end are contiguous: one atomic
+// per such segment (hubs would otherwise serialise hundreds of thousands of adds on one counter).
+__global__ void k_und_runs(const uint64_t* __restrict__ k, const int64_t* __restrict__ heads, int64_t nruns,
+                           int64_t nvalid, int msh, uint64_t* __restrict__ ek, int64_t* __restrict__ ev,
+                           uint32_t* __restrict__ deg) {
     const int lane = threadIdx.x & 63;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); r0 < nruns; r0 += stride) {  // wave-uniform
@@ -76,13 +68,14 @@ __global__ void k_und_runs(const uint64_t* __restrict__ uk, const int64_t* __res
         uint32_t mn = 0;
         if (act) {
             const int64_t h = heads[r], h2 = r + 1 < nruns ? heads[r + 1] : nvalid;
-            int64_t v = 0;
-            for (int64_t i = h; i < h2; ++i) v += uv[i];
-            const uint64_t key = uk[h];
-            ek[r] = key;
-            ev[r] = v;
+            uint64_t back = 0;  // relationships max -> min
+            for (int64_t i = h; i < h2; ++i) back += msh ? (k[i] & 1u) : ((k[i] >> 31) & 1u);
+            const uint64_t key = k[h];
             mn = (uint32_t)(key >> 32);
-            atomicAdd(&deg[(uint32_t)key], 1u);
+            const uint32_t mx = msh ? ((uint32_t)key >> 1) : ((uint32_t)key & 0x7FFFFFFFu);
+            ek[r] = ((uint64_t)mn << 32) | mx;
+            ev[r] = (int64_t)((((uint64_t)(h2 - h) - back) << 32) | back);
+            atomicAdd(&deg[mx], 1u);
         }
         const uint32_t prev = __shfl_up(mn, 1, 64);
         const bool head = act && (lane == 0 || prev != mn);
@@ -553,8 +546,9 @@ __global__ void k_pair_terms(const uint64_t* __restrict__ ek, const int64_t* __r
                              const uint32_t* __restrict__ sl, unsigned long long* __restrict__ out) {
     unsigned long long acc = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t x = (uint32_t)(ek[i] >> 32), y = (uint32_t)ek[i];
         const uint64_t v = (uint64_t)ev[i];
+        if ((v >> 32) == 0 || (v & 0xffffffffULL) == 0) continue;  // one direction only: no term, no gathers
+        const uint32_t x = (uint32_t)(ek[i] >> 32), y = (uint32_t)ek[i];
         acc += 3ULL * ((uint64_t)sl[x] + sl[y]) * (v >> 32) * (v & 0xffffffffULL);
     }
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
@@ -592,12 +586,16 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     using namespace tri;
     hipStream_t st = s->stream;
     const int64_t lo = n_ok->lo, hi = n_ok->hi, n = hi - lo;
-    REQUIRE(n > 0 && (uint64_t)n <= (uint64_t(1) << 32), CAPSMI_ERR_UNSUPPORTED, "triangle count needs <= 2^32 ids");
+    REQUIRE(n > 0 && (uint64_t)n <= (uint64_t(1) << 31), CAPSMI_ERR_UNSUPPORTED, "triangle count needs <= 2^31 ids");
     g.lo = lo;
     g.n = n;
     int64_t m = 0;
     for (int i = 0; i < nt; ++i) m += ms[i];
     const int bits = bits_for((uint64_t)n);
+    // the direction bit rides unsorted at bit 31 when max's digits end at or below bit 24
+    const int msh = bits > 24 ? 1 : 0;
+    g.sl = dev_alloc(sizeof(uint32_t) * n, s);
+    HIP_CHECK(hipMemsetAsync(P<void>(g.sl), 0, sizeof(uint32_t) * n, st));
     Buf key = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s);
     {
         KernelTimer kt(s, "tri_pack");
@@ -605,22 +603,20 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         for (int i = 0; i < nt; ++i) {
             if (ms[i] > 0)
                 hipLaunchKernelGGL(k_pack, dim3(grid(s, ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], lo, hi,
-                                   P<uint32_t>(n_ok->words), n_ok->full ? 1 : 0, P<uint64_t>(key) + off);
+                                   P<uint32_t>(n_ok->words), n_ok->full ? 1 : 0, msh, P<uint64_t>(key) + off,
+                                   P<uint32_t>(g.sl));
             off += ms[i];
         }
     }
-    // keys (s << 32 | t) use the digits of s and t only, plus the top digit that makes kNone (all
-    // ones) sort last; the directed runs need the keys alone
+    // one sort of the undirected keys: digits of max (and the direction bit when msh) then of min
     std::vector<int> kd;
-    for (int sh = 0; sh < bits; sh += 8) kd.push_back(sh);
+    for (int sh = 0; sh < bits + msh; sh += 8) kd.push_back(sh);
     for (int sh = 32; sh < 32 + bits; sh += 8) kd.push_back(sh);
-    const std::vector<int> od = kd;
-    if (kd.back() < 56) kd.push_back(56);
     radix_sort_digits(s, P<uint64_t>(key), nullptr, m, kd);
-    // directed runs
+    const uint64_t dmask = msh ? ~1ULL : ~(1ULL << 31);
     Buf f = dev_alloc(m > 0 ? m : 1, s), heads;
-    hipLaunchKernelGGL(k_heads, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, P<uint8_t>(f));
-    const int64_t nruns = flags_to_indices(s, P<uint8_t>(f), m, heads);
+    hipLaunchKernelGGL(k_heads, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, dmask, P<uint8_t>(f));
+    const int64_t ne = flags_to_indices(s, P<uint8_t>(f), m, heads);
     int64_t nvalid = 0;
     {
         // nvalid: binary search for the first kNone in the sorted keys (host-side bisection, O(log m) reads)
@@ -634,37 +630,17 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         }
         nvalid = a;
     }
-    g.sl = dev_alloc(sizeof(uint32_t) * n, s);
-    HIP_CHECK(hipMemsetAsync(P<void>(g.sl), 0, sizeof(uint32_t) * n, st));
-    Buf uk = dev_alloc(sizeof(uint64_t) * (nruns > 0 ? nruns : 1), s), uv = dev_alloc(sizeof(int64_t) * (nruns > 0 ? nruns : 1), s);
-    if (nruns > 0)
-        hipLaunchKernelGGL(k_dir_runs, dim3(grid(s, nruns)), dim3(256), 0, st, P<uint64_t>(key), P<int64_t>(heads),
-                           nruns, nvalid, P<uint32_t>(g.sl), P<uint64_t>(uk), P<int64_t>(uv));
-    key.reset();
-    radix_sort_digits(s, P<uint64_t>(uk), P<int64_t>(uv), nruns, kd);
-    Buf f2 = dev_alloc(nruns > 0 ? nruns : 1, s), heads2;
-    hipLaunchKernelGGL(k_heads, dim3(grid(s, nruns)), dim3(256), 0, st, P<uint64_t>(uk), nruns, P<uint8_t>(f2));
-    const int64_t ne = flags_to_indices(s, P<uint8_t>(f2), nruns, heads2);
-    int64_t nuvalid = 0;
-    {
-        int64_t a = 0, b = nruns;
-        while (a < b) {
-            const int64_t mid = (a + b) / 2;
-            uint64_t kv;
-            HIP_CHECK(hipMemcpyAsync(&kv, P<uint64_t>(uk) + mid, 8, hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
-            if (kv == kNone) b = mid; else a = mid + 1;
-        }
-        nuvalid = a;
-    }
     g.ne = ne;
     g.ek = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), s);
     g.ev = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);
     Buf deg = dev_alloc(sizeof(uint32_t) * n, s);
     HIP_CHECK(hipMemsetAsync(P<void>(deg), 0, sizeof(uint32_t) * n, st));
     if (ne > 0)
-        hipLaunchKernelGGL(k_und_runs, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(uk), P<int64_t>(uv),
-                           P<int64_t>(heads2), ne, nuvalid, P<uint64_t>(g.ek), P<int64_t>(g.ev), P<uint32_t>(deg));
+        hipLaunchKernelGGL(k_und_runs, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(key), P<int64_t>(heads), ne,
+                           nvalid, msh, P<uint64_t>(g.ek), P<int64_t>(g.ev), P<uint32_t>(deg));
+    key.reset();
+    f.reset();
+    heads.reset();
     // degree-order ids (hubs first): sort the vertices by (degree, id)
     Buf rid = dev_alloc(sizeof(uint32_t) * n, s);
     g.orig = dev_alloc(sizeof(int64_t) * n, s);
@@ -684,6 +660,9 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     if (ne > 0)
         hipLaunchKernelGGL(k_orient, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ek), P<int64_t>(g.ev), ne,
                            P<uint32_t>(rid), P<uint64_t>(g.ok), P<int64_t>(g.ov));
+    std::vector<int> od;  // (source, target): grouped and target-sorted lists
+    for (int sh = 0; sh < bits; sh += 8) od.push_back(sh);
+    for (int sh = 32; sh < 32 + bits; sh += 8) od.push_back(sh);
     radix_sort_digits(s, P<uint64_t>(g.ok), P<int64_t>(g.ov), ne, od);  // no kNone among the oriented keys
     g.off = dev_alloc(sizeof(int64_t) * (n + 1), s);
     hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, n, P<int64_t>(g.off));

@@ -83,3 +83,24 @@ def test_complete_digraph_chunks(session, mult):
     want = int(round(np.trace(Mf @ Mf @ Mf)))
     assert _count(session, n, src, dst) == want
     assert _count(session, n, src, dst, nparts=3) == want
+
+
+def test_wide_id_range(session):
+    """Ids spread over [0, 2^25 + 3): the undirected sort keys carry the direction bit below the
+    target (bits > 24) instead of in the unsorted bit 31.  The count is label-invariant, so the
+    oracle enumerates the compacted ids."""
+    from capsmi import ColumnData, I64, graph
+    rng = np.random.default_rng(21)
+    n = (1 << 25) + 3
+    ids = np.unique(rng.integers(0, n, 700)).astype(np.int64)
+    ids[-1] = n - 1
+    k = len(ids)
+    a = rng.integers(0, k, 9000)
+    b = rng.integers(0, k, 9000)
+    b[:300] = a[:300]  # self-loops
+    src, dst = ids[a], ids[b]
+    rels = session.table([ColumnData("id", I64, np.arange(len(src))), ColumnData("source", I64, src),
+                          ColumnData("target", I64, dst)])
+    nodes = session.table([ColumnData("id", I64, ids)])
+    ok = graph.NodeBitmap(session, 0, n).add_scan(nodes)
+    assert graph.triangle_count(session, [rels], ok) == cpu.triangle_enumerate(k, a.astype(np.int64), b.astype(np.int64))
