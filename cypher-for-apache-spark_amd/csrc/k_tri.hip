@@ -155,7 +155,9 @@ __global__ void k_offsets(const uint64_t* __restrict__ ok_, int64_t ne, int64_t 
 // 1024-lane workgroup (their lists are taken in chunks when they exceed the LDS hash).
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr int kSmallDeg = 64;
-constexpr int kWedgeUnroll = 4;  // wedges per lane with their target loads in flight together
+constexpr int kWedgeUnroll = 4;  // flat walks: wedges per lane with their target loads in flight together
+// (the list walks take it as a template parameter, 8 by default: 252.9 -> 240.8 ms at s = 24 over 4;
+// 16 gains nothing more, since most lists end within one 512-entry pass)
 constexpr int kSmallSlots = 512;  // load <= 1/8: a miss (most wedges) ends after ~1.2 probes
 constexpr int kTriBlock = 256;  // small: 4 waves
 constexpr int kBigBlock = 1024;
@@ -240,7 +242,7 @@ __device__ __forceinline__ uint32_t target(const uint32_t* __restrict__ tg, cons
     return pos < hot_end ? (uint32_t)tg16[pos] : tg[pos];
 }
 
-template <bool LISTS>  // LISTS: the wave walks each out(v) with all lanes (as k_tri_big_items<true>)
+template <bool LISTS, int U>  // LISTS: the wave walks each out(v) with all lanes (as k_tri_big_items<true>)
 __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restrict__ tg,
                                                          const uint16_t* __restrict__ tg16, int64_t hot_end,
                                                          const int64_t* __restrict__ ov,
@@ -290,20 +292,18 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
                 const int64_t vo = W.voff[k];
                 const uint32_t dvk = W.dv[k];
                 const uint64_t puv = W.vp[k];
-                for (uint32_t j0 = lane; j0 < dvk; j0 += kWedgeUnroll * 64) {
-                    int64_t pos[kWedgeUnroll];
-                    uint32_t w[kWedgeUnroll];
+                for (uint32_t j0 = lane; j0 < dvk; j0 += U * 64) {
+                    uint32_t w[U];  // U target loads in flight per lane
 #pragma unroll
-                    for (int r = 0; r < kWedgeUnroll; ++r) {
+                    for (int r = 0; r < U; ++r) {
                         const uint32_t j = j0 + r * 64;
-                        pos[r] = vo + j;
-                        w[r] = j < dvk ? target(tg, tg16, hot_end, pos[r]) : kEmpty;
+                        w[r] = j < dvk ? target(tg, tg16, hot_end, vo + j) : kEmpty;
                     }
 #pragma unroll
-                    for (int r = 0; r < kWedgeUnroll; ++r) {
+                    for (int r = 0; r < U; ++r) {
                         if (w[r] == kEmpty || !btest(W.bf, kSmallBloomBits, w[r])) continue;
                         const int sl = hfind(W.hk, 9, w[r]);
-                        if (sl >= 0) acc += tri_weight(puv, (uint64_t)ov[pos[r]], W.vp[W.hi[sl]]);
+                        if (sl >= 0) acc += tri_weight(puv, (uint64_t)ov[vo + j0 + r * 64], W.vp[W.hi[sl]]);
                     }
                 }
             }
@@ -421,7 +421,7 @@ __global__ void k_tri_item_map(const int64_t* __restrict__ ipre, int64_t nu, uin
 // big u lie in long lists (wedge-weighted mean ≈600 at R-MAT s = 22; 99.8 % in lists of ≥ 64), so the
 // lanes stay busy; the flat form below (one prefix-sum index range over the chunk's wedges) spent
 // ≈70 VALU instructions per wedge on the cursor and the segment search and was issue-bound.
-template <bool LISTS>
+template <bool LISTS, int U>
 __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __restrict__ tg,
                                                              const uint16_t* __restrict__ tg16, int64_t hot_end,
                                                              const int64_t* __restrict__ ov,
@@ -472,20 +472,19 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
                 const int64_t vo = L.voff[k];
                 const int64_t dv = (int64_t)L.dv[k];
                 const uint64_t puv = L.vp[k];
-                for (int64_t j0 = lane; j0 < dv; j0 += kWedgeUnroll * 64) {
-                    int64_t pos[kWedgeUnroll];
-                    uint32_t w[kWedgeUnroll];
+                for (int j0 = lane; j0 < (int)dv; j0 += U * 64) {
+                    uint32_t w[U];  // U target loads in flight per lane
 #pragma unroll
-                    for (int r = 0; r < kWedgeUnroll; ++r) {
-                        const int64_t j = j0 + r * 64;
-                        pos[r] = vo + j;
-                        w[r] = j < dv ? target(tg, tg16, hot_end, pos[r]) : kEmpty;
+                    for (int r = 0; r < U; ++r) {
+                        const int j = j0 + r * 64;
+                        w[r] = j < (int)dv ? target(tg, tg16, hot_end, vo + j) : kEmpty;
                     }
 #pragma unroll
-                    for (int r = 0; r < kWedgeUnroll; ++r) {
+                    for (int r = 0; r < U; ++r) {
                         if (w[r] == kEmpty || !btest(L.bf, kBigBloomBits, w[r])) continue;
                         const int sl = hfind(L.hk, 13, w[r]);
-                        if (sl >= 0) acc += tri_weight(puv, (uint64_t)ov[pos[r]], (uint64_t)ov[b + h0 + L.hi[sl]]);
+                        if (sl >= 0)
+                            acc += tri_weight(puv, (uint64_t)ov[vo + j0 + r * 64], (uint64_t)ov[b + h0 + L.hi[sl]]);
                     }
                 }
             }
@@ -711,11 +710,14 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
             const size_t lds = sizeof(ItemLds);
             const char* walk = getenv("CAPSMI_TRI_WALK");  // "flat": the prefix-sum walk (A/B runs)
             const bool lists = !(walk && std::string(walk) == "flat");
-            const void* kf = lists ? reinterpret_cast<const void*>(k_tri_big_items<true>)
-                                   : reinterpret_cast<const void*>(k_tri_big_items<false>);
-            HIP_CHECK(hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            hipLaunchKernelGGL(lists ? k_tri_big_items<true> : k_tri_big_items<false>, dim3((unsigned)(s->num_cus * 4)),
-                               dim3(kBigBlock), lds, st,
+            const char* ue = getenv("CAPSMI_TRI_UNROLL");  // target loads in flight per lane: 4, 8 or 16
+            const int un = ue ? atoi(ue) : 8;
+            auto kf = !lists ? k_tri_big_items<false, 4>
+                      : un == 16 ? k_tri_big_items<true, 16>
+                      : un == 8 ? k_tri_big_items<true, 8> : k_tri_big_items<true, 4>;
+            HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kf), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)lds));
+            hipLaunchKernelGGL(kf, dim3((unsigned)(s->num_cus * 4)), dim3(kBigBlock), lds, st,
                                P<uint32_t>(g.tg), P<uint16_t>(g.tg16), g.hot_end, P<int64_t>(g.ov), P<int64_t>(g.off),
                                bu, nb, ipre, P<uint32_t>(iq),
                                P<unsigned long long>(ctr), P<unsigned long long>(out));
@@ -724,7 +726,12 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
             const int64_t gs = std::min<int64_t>((se - sb + 3) / 4, (int64_t)s->num_cus * 16);
             const char* sw = getenv("CAPSMI_TRI_WALK");  // "flat": the prefix-sum walk (A/B runs)
             const bool slists = !(sw && std::string(sw) == "flat");
-            hipLaunchKernelGGL(slists ? k_tri_small<true> : k_tri_small<false>, dim3((unsigned)gs), dim3(kTriBlock), 0, st,
+            const char* ue = getenv("CAPSMI_TRI_UNROLL");
+            const int un = ue ? atoi(ue) : 8;
+            auto kfs = !slists ? k_tri_small<false, 4>
+                       : un == 16 ? k_tri_small<true, 16>
+                       : un == 8 ? k_tri_small<true, 8> : k_tri_small<true, 4>;
+            hipLaunchKernelGGL(kfs, dim3((unsigned)gs), dim3(kTriBlock), 0, st,
                                P<uint32_t>(g.tg),
                                P<uint16_t>(g.tg16), g.hot_end, P<int64_t>(g.ov), P<int64_t>(g.off), P<int64_t>(g.small_u) + sb, se - sb,
                                P<unsigned long long>(out));
