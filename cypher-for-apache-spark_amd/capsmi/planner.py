@@ -450,9 +450,15 @@ class Planner:
         if query.get("driving"):  # driving table: its columns are value variables (planStartWithDrivingTable)
             d = query["driving"]
             cols = []
+            dictionary = self.g.backend.dictionary
             for name, values in d.items():
-                ty = STR if any(isinstance(v, str) for v in values) else I64
-                cols.append(_column(name, ty, values, self.g.backend.dictionary.encode))
+                if any(isinstance(v, str) for v in values):
+                    ty = STR
+                    # codes are stable under insertion, so new strings are added, never guessed at
+                    dictionary.extend(v for v in values if v is not None)
+                else:
+                    ty = F64 if any(isinstance(v, float) for v in values) else I64
+                cols.append(_column(name, ty, values, dictionary.encode))
             cur = _Op(self.g.backend.table(cols), list(d), set(), [])
         for clause in query["clauses"]:
             if "optional_match" in clause:

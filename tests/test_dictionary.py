@@ -74,3 +74,16 @@ def test_driving_table_strings_are_registered():
          "return": {"items": [["x", ["var", "x"]]]}}
     t, outs = Planner(sg).run(q)
     assert result_rows(t, outs, be.dictionary) == [{"x": "Bo"}]
+
+
+def test_driving_table_floats_keep_their_type():
+    """A driving-table column with a float is Double, not truncated to Long."""
+    from capsmi.planner import PGNode, Planner, PropertyGraph, ScanGraph, result_rows
+    from capsmi.table import StringDictionary
+    from oracle.relational import NumpyBackend
+    be = NumpyBackend(StringDictionary())
+    sg = ScanGraph.from_property_graph(be, PropertyGraph([PGNode(0, frozenset({"P"}), {"v": 2})], []))
+    q = {"driving": {"x": [1.5, 2]}, "clauses": [{"match": "(a:P)", "where": ["<", ["var", "x"], ["prop", "a", "v"]]}],
+         "return": {"items": [["x", ["var", "x"]]]}}
+    t, outs = Planner(sg).run(q)
+    assert result_rows(t, outs, be.dictionary) == [{"x": 1.5}]
