@@ -327,13 +327,17 @@ def main():
         return int(t.column(outs[0][2]).values[0])
 
     def run_count(atomic=False):  # count(*) of the same match through the route
+        prev = os.environ.get("CAPSMI_COUNT")  # a caller's A/B choice (scripts/ab.sh) stays in force
         if atomic:
             os.environ["CAPSMI_COUNT"] = "atomic"
         try:
             t, outs = Planner(sg_cold).run(C3_COUNT_QUERY)
             return int(t.column(outs[0][2]).values[0])
         finally:
-            os.environ.pop("CAPSMI_COUNT", None)
+            if prev is None:
+                os.environ.pop("CAPSMI_COUNT", None)
+            else:
+                os.environ["CAPSMI_COUNT"] = prev
 
     steps = {"cold": lambda: run_planner(sg_cold), "warm": lambda: run_planner(sg_warm),
              "direct": step_cold, "direct_warm": step_warm, "stream": step_stream,

@@ -1,0 +1,86 @@
+"""2-hop count(*) (capsmi_two_hop_count) in both forms against the closed form of oracle/closed.c:
+the two chunked partitions with LDS slice counts (default) and the per-relationship atomics
+(CAPSMI_COUNT=atomic).  The closed form itself is pinned against binding enumeration in
+tests/test_oracle*.py."""
+import numpy as np
+import pytest
+
+from oracle import cpu
+
+pytestmark = pytest.mark.gpu
+
+MODES = ["part", "atomic"]
+
+
+def _mode(monkeypatch, mode):
+    if mode != "part":
+        monkeypatch.setenv("CAPSMI_COUNT", mode)
+
+
+def _bm(session, n, mask):
+    from capsmi import ColumnData, I64, graph
+    nodes = session.table([ColumnData("id", I64, np.nonzero(mask)[0].astype(np.int64))])
+    return graph.NodeBitmap(session, 0, n).add_scan(nodes)
+
+
+def _rels(session, src, dst):
+    from capsmi import ColumnData, I64
+    return session.table([ColumnData("id", I64, np.arange(len(src))), ColumnData("source", I64, src),
+                          ColumnData("target", I64, dst)])
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_self_loops_and_distinct_masks(session, monkeypatch, mode):
+    from capsmi import graph
+    _mode(monkeypatch, mode)
+    edges = [(0, 0), (1, 1), (1, 1), (3, 2), (2, 2), (4, 5), (5, 5), (5, 6), (2, 5), (6, 2), (3, 3)]
+    src = np.array([e[0] for e in edges], dtype=np.int64)
+    dst = np.array([e[1] for e in edges], dtype=np.int64)
+    n = 8
+    for am, bm_, cm in [([1] * 8, [1] * 8, [1] * 8), ([1, 1, 0, 1, 1, 1, 1, 1], [1, 1, 1, 0, 1, 1, 1, 1],
+                                                      [0, 1, 1, 1, 1, 1, 1, 1])]:
+        a, b, c = (np.array(x, dtype=np.uint8) for x in (am, bm_, cm))
+        rows, _ = cpu.two_hop_closed_form(n, src, dst, a, b, c)
+        assert graph.two_hop_count(session, [_rels(session, src, dst)], _bm(session, n, a), _bm(session, n, b),
+                                   _bm(session, n, c)) == rows
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_hub_slices_and_split_walks(session, monkeypatch, mode):
+    """2^21 ids (64 slices of 2^15): hub slices far longer than one chunk, slices split between walk
+    blocks, ids outside the domain, self-loops, two tables, distinct a/b/c filters."""
+    from capsmi import graph
+    _mode(monkeypatch, mode)
+    rng = np.random.default_rng(17)
+    n = 1 << 21
+    m = 400000
+    src = rng.integers(0, n, m)
+    dst = rng.integers(0, n, m)
+    hubs = rng.integers(0, 1 << 14, 40)  # all in slice 0
+    src[: m // 3] = hubs[rng.integers(0, 40, m // 3)]
+    dst[m // 3: 2 * m // 3] = hubs[rng.integers(0, 40, m // 3)]
+    src[:50] = dst[:50]
+    outside = np.array([n + 5, -3, 7], dtype=np.int64)
+    s_all = np.concatenate([src, outside]).astype(np.int64)
+    d_all = np.concatenate([dst, [4, 5, n + 1]]).astype(np.int64)
+    a = (rng.random(n) < 0.9).astype(np.uint8)
+    b = (rng.random(n) < 0.8).astype(np.uint8)
+    c = (rng.random(n) < 0.7).astype(np.uint8)
+    keep = (s_all >= 0) & (s_all < n) & (d_all >= 0) & (d_all < n)
+    rows, _ = cpu.two_hop_closed_form(n, s_all[keep], d_all[keep], a, b, c)
+    h = len(s_all) // 2
+    t1, t2 = _rels(session, s_all[:h], d_all[:h]), _rels(session, s_all[h:], d_all[h:])
+    assert graph.two_hop_count(session, [t1, t2], _bm(session, n, a), _bm(session, n, b), _bm(session, n, c)) == rows
+
+
+@pytest.mark.parametrize("mode", ["part"])
+@pytest.mark.parametrize("scale,kind", [(12, "person"), (16, "all"), (17, "person")])
+def test_rmat(session, monkeypatch, mode, scale, kind):
+    from capsmi import graph
+    _mode(monkeypatch, mode)
+    n = 1 << scale
+    src, dst = cpu.rmat_edges(scale, 0, 16 << scale)
+    mask = np.ones(n, np.uint8) if kind == "all" else cpu.person_mask(n).astype(np.uint8)
+    rows, _ = cpu.two_hop_closed_form(n, src, dst, mask, mask, mask)
+    bm = _bm(session, n, mask)
+    assert graph.two_hop_count(session, [_rels(session, src, dst)], bm, bm, bm) == rows
