@@ -242,6 +242,37 @@ __device__ __forceinline__ uint32_t target(const uint32_t* __restrict__ tg, cons
     return pos < hot_end ? (uint32_t)tg16[pos] : tg[pos];
 }
 
+// One pass of a wave over U x 64 consecutive entries of a list (this lane: entries j0 + r * 64):
+// the list lies wholly inside or wholly outside the 16-bit hub prefix, so the choice is made once,
+// and the loads are unconditional at clamped indexes (entries past the end become kEmpty), which
+// keeps them free of per-load branches.  Then the U pre-filter words are read together before any
+// is tested; `keep` marks the entries that pass.
+template <int U>
+__device__ __forceinline__ void list_pass(const uint32_t* __restrict__ tg, const uint16_t* __restrict__ tg16,
+                                          int64_t hot_end, int64_t vo, int dv, int j0, const uint32_t* bf, int bits,
+                                          uint32_t (&w)[U], uint32_t& keep) {
+    const int last = dv - 1;
+    if (vo + dv <= hot_end) {  // wave-uniform
+        const uint16_t* __restrict__ p = tg16 + vo;
+#pragma unroll
+        for (int r = 0; r < U; ++r) w[r] = p[min(j0 + r * 64, last)];
+    } else {
+        const uint32_t* __restrict__ p = tg + vo;
+#pragma unroll
+        for (int r = 0; r < U; ++r) w[r] = p[min(j0 + r * 64, last)];
+    }
+    uint32_t word[U], bit[U];
+#pragma unroll
+    for (int r = 0; r < U; ++r) {
+        bit[r] = bbit(w[r], bits);
+        word[r] = bf[bit[r] >> 5];
+    }
+    keep = 0;
+#pragma unroll
+    for (int r = 0; r < U; ++r)
+        if (j0 + r * 64 < dv && ((word[r] >> (bit[r] & 31)) & 1u)) keep |= 1u << r;
+}
+
 template <bool LISTS, int U>  // LISTS: the wave walks each out(v) with all lanes (as k_tri_big_items<true>)
 __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restrict__ tg,
                                                          const uint16_t* __restrict__ tg16, int64_t hot_end,
@@ -292,16 +323,12 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
                 const int64_t vo = W.voff[k];
                 const uint32_t dvk = W.dv[k];
                 const uint64_t puv = W.vp[k];
-                for (uint32_t j0 = lane; j0 < dvk; j0 += U * 64) {
-                    uint32_t w[U];  // U target loads in flight per lane
+                for (int j0 = lane; j0 < (int)dvk; j0 += U * 64) {
+                    uint32_t w[U], keep;  // U target loads in flight per lane
+                    list_pass<U>(tg, tg16, hot_end, vo, (int)dvk, j0, W.bf, kSmallBloomBits, w, keep);
 #pragma unroll
                     for (int r = 0; r < U; ++r) {
-                        const uint32_t j = j0 + r * 64;
-                        w[r] = j < dvk ? target(tg, tg16, hot_end, vo + j) : kEmpty;
-                    }
-#pragma unroll
-                    for (int r = 0; r < U; ++r) {
-                        if (w[r] == kEmpty || !btest(W.bf, kSmallBloomBits, w[r])) continue;
+                        if (!((keep >> r) & 1u)) continue;
                         const int sl = hfind(W.hk, 9, w[r]);
                         if (sl >= 0) acc += tri_weight(puv, (uint64_t)ov[vo + j0 + r * 64], W.vp[W.hi[sl]]);
                     }
@@ -473,15 +500,11 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
                 const int64_t dv = (int64_t)L.dv[k];
                 const uint64_t puv = L.vp[k];
                 for (int j0 = lane; j0 < (int)dv; j0 += U * 64) {
-                    uint32_t w[U];  // U target loads in flight per lane
+                    uint32_t w[U], keep;  // U target loads in flight per lane
+                    list_pass<U>(tg, tg16, hot_end, vo, (int)dv, j0, L.bf, kBigBloomBits, w, keep);
 #pragma unroll
                     for (int r = 0; r < U; ++r) {
-                        const int j = j0 + r * 64;
-                        w[r] = j < (int)dv ? target(tg, tg16, hot_end, vo + j) : kEmpty;
-                    }
-#pragma unroll
-                    for (int r = 0; r < U; ++r) {
-                        if (w[r] == kEmpty || !btest(L.bf, kBigBloomBits, w[r])) continue;
+                        if (!((keep >> r) & 1u)) continue;
                         const int sl = hfind(L.hk, 13, w[r]);
                         if (sl >= 0)
                             acc += tri_weight(puv, (uint64_t)ov[vo + j0 + r * 64], (uint64_t)ov[b + h0 + L.hi[sl]]);
