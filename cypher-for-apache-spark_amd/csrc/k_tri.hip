@@ -164,13 +164,18 @@ constexpr int kBigBlock = 1024;
 constexpr int kBigChunk = 2048;  // out-list entries per LDS chunk
 constexpr int kBigSlots = 8192;  // load <= 1/4
 
-__device__ __forceinline__ uint32_t hslot(uint32_t w, int log2cap) { return (w * 0x9E3779B1u) >> (32 - log2cap); }
+// Multiplicative hashes on the full-rate 24-bit multiplier (a 32-bit v_mul_lo is quarter rate, and
+// the walks are VALU-bound): the id's bits above 24 are folded in first, so every bit counts
+// (both operands masked to 24 bits, so the compiler selects v_mul_u32_u24 for the low 32 bits)
+__device__ __forceinline__ uint32_t fold24(uint32_t w) { return (w ^ (w >> 24)) & 0xFFFFFFu; }
+__device__ __forceinline__ uint32_t mul24(uint32_t a, uint32_t b) { return a * b; }
+__device__ __forceinline__ uint32_t hslot(uint32_t w, int log2cap) { return mul24(fold24(w), 0x9E3779u) >> (32 - log2cap); }
 
 // One-bit pre-filter in front of each hash: a wave's probe loop runs as long as its longest
 // chain, so most wedges (misses) are rejected with one LDS read instead.
 constexpr int kSmallBloomBits = 10, kBigBloomBits = 16;
 
-__device__ __forceinline__ uint32_t bbit(uint32_t w, int bits) { return (w * 0x85EBCA6Bu) >> (32 - bits); }
+__device__ __forceinline__ uint32_t bbit(uint32_t w, int bits) { return mul24(fold24(w), 0xC2B2AFu) >> (32 - bits); }
 
 __device__ __forceinline__ void bset(uint32_t* bf, int bits, uint32_t w) {
     const uint32_t x = bbit(w, bits);
@@ -240,6 +245,13 @@ struct SmallWave {
 __device__ __forceinline__ uint32_t target(const uint32_t* __restrict__ tg, const uint16_t* __restrict__ tg16,
                                           int64_t hot_end, int64_t pos) {
     return pos < hot_end ? (uint32_t)tg16[pos] : tg[pos];
+}
+
+// a wave-uniform 64-bit value into scalar registers, so addresses built on it take the scalar base +
+// 32-bit lane offset form instead of 64-bit vector arithmetic per load
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
 // One pass of a wave over U x 64 consecutive entries of a list (this lane: entries j0 + r * 64):
@@ -320,8 +332,8 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (LISTS) {
             for (int k = 0; k < d; ++k) {
-                const int64_t vo = W.voff[k];
-                const uint32_t dvk = W.dv[k];
+                const int64_t vo = uniform64(W.voff[k]);
+                const uint32_t dvk = __builtin_amdgcn_readfirstlane(W.dv[k]);
                 const uint64_t puv = W.vp[k];
                 for (int j0 = lane; j0 < (int)dvk; j0 += U * 64) {
                     uint32_t w[U], keep;  // U target loads in flight per lane
@@ -470,7 +482,7 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
         __syncthreads();  // `item` is rewritten next round
         if (it >= total) break;  // block-uniform
         const int64_t lo = item_q[it];
-        const int64_t u = us[lo], b = off[u];
+        const int64_t u = us[lo], b = uniform64(off[u]);
         const int d = (int)(off[u + 1] - b);
         const int nvc = (d + kVChunk - 1) / kVChunk;
         const int local = (int)(it - ipre[lo]);
@@ -496,8 +508,8 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
         if (LISTS) {
             const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
             for (int k = wave; k < vn; k += kBigBlock / 64) {
-                const int64_t vo = L.voff[k];
-                const int64_t dv = (int64_t)L.dv[k];
+                const int64_t vo = uniform64(L.voff[k]);
+                const int64_t dv = (int64_t)__builtin_amdgcn_readfirstlane(L.dv[k]);
                 const uint64_t puv = L.vp[k];
                 for (int j0 = lane; j0 < (int)dv; j0 += U * 64) {
                     uint32_t w[U], keep;  // U target loads in flight per lane
