@@ -263,15 +263,16 @@ template <int U>
 __device__ __forceinline__ void list_pass(const uint32_t* __restrict__ tg, const uint16_t* __restrict__ tg16,
                                           int64_t hot_end, int64_t vo, int dv, int j0, const uint32_t* bf, int bits,
                                           uint32_t (&w)[U], uint32_t& keep) {
-    const int last = dv - 1;
+    // unsigned 32-bit indexes off a scalar base: the loads take the scalar-base + lane-offset form
+    const uint32_t last = (uint32_t)dv - 1u, j = (uint32_t)j0;
     if (vo + dv <= hot_end) {  // wave-uniform
-        const uint16_t* __restrict__ p = tg16 + vo;
+        const char* __restrict__ p = reinterpret_cast<const char*>(tg16 + vo);
 #pragma unroll
-        for (int r = 0; r < U; ++r) w[r] = p[min(j0 + r * 64, last)];
+        for (int r = 0; r < U; ++r) w[r] = *reinterpret_cast<const uint16_t*>(p + (min(j + (uint32_t)r * 64u, last) << 1));
     } else {
-        const uint32_t* __restrict__ p = tg + vo;
+        const char* __restrict__ p = reinterpret_cast<const char*>(tg + vo);
 #pragma unroll
-        for (int r = 0; r < U; ++r) w[r] = p[min(j0 + r * 64, last)];
+        for (int r = 0; r < U; ++r) w[r] = *reinterpret_cast<const uint32_t*>(p + (min(j + (uint32_t)r * 64u, last) << 2));
     }
     uint32_t word[U], bit[U];
 #pragma unroll
@@ -279,10 +280,10 @@ __device__ __forceinline__ void list_pass(const uint32_t* __restrict__ tg, const
         bit[r] = bbit(w[r], bits);
         word[r] = bf[bit[r] >> 5];
     }
-    keep = 0;
+    keep = 0;  // branch-free: in range and pre-filter bit set
 #pragma unroll
     for (int r = 0; r < U; ++r)
-        if (j0 + r * 64 < dv && ((word[r] >> (bit[r] & 31)) & 1u)) keep |= 1u << r;
+        keep |= ((uint32_t)(j + (uint32_t)r * 64u <= last) & (word[r] >> (bit[r] & 31))) << r;
 }
 
 template <bool LISTS, int U>  // LISTS: the wave walks each out(v) with all lanes (as k_tri_big_items<true>)
