@@ -307,6 +307,13 @@ struct TriGraph {
     Buf ek, ev, sl;   // undirected keys / payload (pair terms), self-loop counts
     Buf small_u, big_u;  // vertices with out-degree in [2, 64] / above 64
     int64_t nsmall = 0, nbig = 0;
+    // Direction choice per oriented edge u -> v (the wedges through it cost od(v) probes walking
+    // out(v) from u, or od(u) walking out(u) from v): with vmt > 0 the edges with od(v) >= vmt and
+    // od(u) <= od(v) are taken from v ("v-mode"), over the in-lists (ioff, itg, iov: sources and
+    // payloads of the oriented edges grouped by target); vm_c = the v-mode centers.
+    int vmt = 0;
+    Buf ioff, itg, iov, vm_c;
+    int64_t nvm = 0;
 };
 void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
                const capsmi_bitmap* n_ok, TriGraph& g);

@@ -126,6 +126,23 @@ __global__ void k_orient(const uint64_t* __restrict__ ek, const int64_t* __restr
     }
 }
 
+// in-lists: oriented keys (from << 32 | to) swapped to (to << 32 | from), payloads alongside
+__global__ void k_swap_keys(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ ov, int64_t ne,
+                            uint64_t* __restrict__ ik, int64_t* __restrict__ iv) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = ok_[i];
+        ik[i] = (k << 32) | (k >> 32);
+        iv[i] = ov[i];
+    }
+}
+
+// v-mode centers: od(v) >= vmt with at least one in-edge
+__global__ void k_tri_vm_bins(const int64_t* __restrict__ off, const int64_t* __restrict__ ioff, int64_t n, int vmt,
+                              uint8_t* __restrict__ f) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+        f[v] = off[v + 1] - off[v] >= vmt && ioff[v + 1] > ioff[v];
+}
+
 __global__ void k_targets16(const uint32_t* __restrict__ tg, int64_t n, uint16_t* __restrict__ tg16) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         tg16[i] = (uint16_t)tg[i];
@@ -290,7 +307,7 @@ template <bool LISTS, int U>  // LISTS: the wave walks each out(v) with all lane
 __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restrict__ tg,
                                                          const uint16_t* __restrict__ tg16, int64_t hot_end,
                                                          const int64_t* __restrict__ ov,
-                                                         const int64_t* __restrict__ off,
+                                                         const int64_t* __restrict__ off, int vmt,
                                                          const int64_t* __restrict__ us, int64_t nu,
                                                          unsigned long long* __restrict__ out) {
     __shared__ SmallWave sw[kTriBlock / 64];
@@ -313,6 +330,7 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
             const uint64_t pv = (uint64_t)ov[b + lane];
             const int64_t vo = off[v];
             dv = (uint32_t)(off[v + 1] - vo);
+            if (vmt > 0 && dv >= (uint32_t)vmt && (uint32_t)d <= dv) dv = 0;  // v-mode takes u -> v
             W.vl[lane] = v;
             W.vp[lane] = pv;
             W.voff[lane] = vo;
@@ -441,12 +459,14 @@ struct ItemLds {
     unsigned long long item;
 };
 
-__global__ void k_tri_items(const int64_t* __restrict__ off, const int64_t* __restrict__ us, int64_t nu,
-                            int64_t* __restrict__ items) {
+// items of center q: hash chunks of out(c) x chunks of its neighbour list (out(c), or in(c) when
+// ioff is set: v-mode)
+__global__ void k_tri_items(const int64_t* __restrict__ off, const int64_t* __restrict__ ioff,
+                            const int64_t* __restrict__ us, int64_t nu, int64_t* __restrict__ items) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nu) return;
-    const int64_t d = off[us[q] + 1] - off[us[q]];
-    items[q] = ((d + kBigChunk - 1) / kBigChunk) * ((d + kVChunk - 1) / kVChunk);
+    const int64_t c = us[q], d = off[c + 1] - off[c], nd = ioff ? ioff[c + 1] - ioff[c] : d;
+    items[q] = ((d + kBigChunk - 1) / kBigChunk) * ((nd + kVChunk - 1) / kVChunk);
 }
 
 // item -> its u's index q (items of q are [ipre[q], ipre[q+1])): one load per item instead of a
@@ -461,11 +481,17 @@ __global__ void k_tri_item_map(const int64_t* __restrict__ ipre, int64_t nu, uin
 // big u lie in long lists (wedge-weighted mean ≈600 at R-MAT s = 22; 99.8 % in lists of ≥ 64), so the
 // lanes stay busy; the flat form below (one prefix-sum index range over the chunk's wedges) spent
 // ≈70 VALU instructions per wedge on the cursor and the segment search and was issue-bound.
-template <bool LISTS, int U>
+// VM (v-mode): the center c is the middle vertex v; its hash holds out(v) and the walked lists are
+// out(u) for the in-neighbours u of v with od(u) <= od(v).  Otherwise (u-mode) c = u and the walked
+// lists are out(v) for v in out(u), less the edges v-mode takes (vmt > 0: od(v) >= vmt, od(u) <= od(v)).
+template <bool LISTS, int U, bool VM>
 __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __restrict__ tg,
                                                              const uint16_t* __restrict__ tg16, int64_t hot_end,
                                                              const int64_t* __restrict__ ov,
                                                              const int64_t* __restrict__ off,
+                                                             const int64_t* __restrict__ ioff,
+                                                             const uint32_t* __restrict__ itg,
+                                                             const int64_t* __restrict__ iov, int vmt,
                                                              const int64_t* __restrict__ us, int64_t nu,
                                                              const int64_t* __restrict__ ipre,
                                                              const uint32_t* __restrict__ item_q,
@@ -483,12 +509,14 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
         __syncthreads();  // `item` is rewritten next round
         if (it >= total) break;  // block-uniform
         const int64_t lo = item_q[it];
-        const int64_t u = us[lo], b = uniform64(off[u]);
+        const int64_t u = us[lo], b = uniform64(off[u]);  // the center (u-mode: u; v-mode: v)
         const int d = (int)(off[u + 1] - b);
-        const int nvc = (d + kVChunk - 1) / kVChunk;
+        const int64_t nb = VM ? uniform64(ioff[u]) : b;   // its neighbour list: in(v) / out(u)
+        const int nd = VM ? (int)(ioff[u + 1] - nb) : d;
+        const int nvc = (nd + kVChunk - 1) / kVChunk;
         const int local = (int)(it - ipre[lo]);
         const int h0 = (local / nvc) * kBigChunk, v0 = (local % nvc) * kVChunk;
-        const int hn = min(kBigChunk, d - h0), vn = min(kVChunk, d - v0);
+        const int hn = min(kBigChunk, d - h0), vn = min(kVChunk, nd - v0);
         for (int k = threadIdx.x; k < kBigSlots; k += kBigBlock) L.hk[k] = kEmpty;
         for (int k = threadIdx.x; k < (1 << kBigBloomBits) / 32; k += kBigBlock) L.bf[k] = 0;
         __syncthreads();
@@ -498,12 +526,13 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
             bset(L.bf, kBigBloomBits, w);
         }
         for (int k = threadIdx.x; k < vn; k += kBigBlock) {
-            const uint32_t v = tg[b + v0 + k];
+            const uint32_t v = VM ? itg[nb + v0 + k] : tg[b + v0 + k];
             const int64_t vo = off[v];
+            const uint32_t dv = (uint32_t)(off[v + 1] - vo);
             L.vl[k] = v;
-            L.vp[k] = (uint64_t)ov[b + v0 + k];
+            L.vp[k] = (uint64_t)(VM ? iov[nb + v0 + k] : ov[b + v0 + k]);  // the edge u -> v either way
             L.voff[k] = vo;
-            L.dv[k] = (uint32_t)(off[v + 1] - vo);
+            L.dv[k] = VM ? (dv <= (uint32_t)d ? dv : 0u) : (vmt > 0 && dv >= (uint32_t)vmt && (uint32_t)d <= dv ? 0u : dv);
         }
         __syncthreads();
         if (LISTS) {
@@ -519,8 +548,10 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
                     for (int r = 0; r < U; ++r) {
                         if (!((keep >> r) & 1u)) continue;
                         const int sl = hfind(L.hk, 13, w[r]);
-                        if (sl >= 0)
-                            acc += tri_weight(puv, (uint64_t)ov[vo + j0 + r * 64], (uint64_t)ov[b + h0 + L.hi[sl]]);
+                        if (sl >= 0) {
+                            const uint64_t pxw = (uint64_t)ov[vo + j0 + r * 64], pcw = (uint64_t)ov[b + h0 + L.hi[sl]];
+                            acc += VM ? tri_weight(puv, pcw, pxw) : tri_weight(puv, pxw, pcw);
+                        }
                     }
                 }
             }
@@ -711,6 +742,26 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     if (g.hot_end > 0)
         hipLaunchKernelGGL(k_targets16, dim3(grid(s, g.hot_end)), dim3(256), 0, st, P<uint32_t>(g.tg), g.hot_end,
                            P<uint16_t>(g.tg16));
+    // in-lists and v-mode centers (CAPSMI_TRI_VMODE_T: the od(v) threshold; 0 = every edge from u)
+    const char* vt = getenv("CAPSMI_TRI_VMODE_T");
+    g.vmt = vt ? atoi(vt) : 256;
+    if (g.vmt > 0 && ne > 0) {
+        Buf ik = dev_alloc(sizeof(uint64_t) * ne, s);
+        g.iov = dev_alloc(sizeof(int64_t) * ne, s);
+        hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.ov), ne,
+                           P<uint64_t>(ik), P<int64_t>(g.iov));
+        radix_sort_digits(s, P<uint64_t>(ik), P<int64_t>(g.iov), ne, od);  // by (to, from)
+        g.ioff = dev_alloc(sizeof(int64_t) * (n + 1), s);
+        hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), ne, n, P<int64_t>(g.ioff));
+        g.itg = dev_alloc(sizeof(uint32_t) * ne, s);
+        hipLaunchKernelGGL(k_targets, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(ik), ne, P<uint32_t>(g.itg));
+        Buf fvm = dev_alloc(n, s);
+        hipLaunchKernelGGL(k_tri_vm_bins, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), P<int64_t>(g.ioff), n,
+                           g.vmt, P<uint8_t>(fvm));
+        g.nvm = flags_to_indices(s, P<uint8_t>(fvm), n, g.vm_c);
+    } else {
+        g.vmt = 0;
+    }
     Buf fsm = dev_alloc(n, s), fbg = dev_alloc(n, s);
     hipLaunchKernelGGL(k_tri_bins, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), n, P<uint8_t>(fsm),
                        P<uint8_t>(fbg));
@@ -729,47 +780,47 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
         KernelTimer kt(s, "triangles");
         const int64_t sb = g.nsmall * part / nparts, se = g.nsmall * (part + 1) / nparts;
         const int64_t bb = g.nbig * part / nparts, be = g.nbig * (part + 1) / nparts;
-        if (be > bb) {
-            const int64_t nb = be - bb;
-            const int64_t* bu = P<int64_t>(g.big_u) + bb;
-            Buf ib = dev_alloc(sizeof(int64_t) * (2 * nb + 2), s);
+        const int64_t vb = g.nvm * part / nparts, ve = g.nvm * (part + 1) / nparts;
+        const char* walk = getenv("CAPSMI_TRI_WALK");  // "flat": the prefix-sum walk (A/B runs)
+        const bool lists = !(walk && std::string(walk) == "flat");
+        const char* ue = getenv("CAPSMI_TRI_UNROLL");  // target loads in flight per lane: 4, 8 or 16
+        const int un = ue ? atoi(ue) : 8;
+        // items (hash chunk, neighbour chunk) of the centers cs[0, nc), taken from a global counter
+        auto run_items = [&](const int64_t* cs, int64_t nc, bool vm) {
+            Buf ib = dev_alloc(sizeof(int64_t) * (2 * nc + 2), s);
             int64_t* items = P<int64_t>(ib);
-            int64_t* ipre = items + nb;
-            hipLaunchKernelGGL(k_tri_items, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, st, P<int64_t>(g.off), bu,
-                               nb, items);
-            exclusive_scan_i64(items, ipre, nb, s);
-            const int64_t nitems = read_scalar(s, ipre + nb);
+            int64_t* ipre = items + nc;
+            hipLaunchKernelGGL(k_tri_items, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st, P<int64_t>(g.off),
+                               vm ? P<int64_t>(g.ioff) : nullptr, cs, nc, items);
+            exclusive_scan_i64(items, ipre, nc, s);
+            const int64_t nitems = read_scalar(s, ipre + nc);
             Buf iq = dev_alloc(sizeof(uint32_t) * (nitems > 0 ? nitems : 1), s);
-            hipLaunchKernelGGL(k_tri_item_map, dim3(grid(s, nb)), dim3(256), 0, st, ipre, nb, P<uint32_t>(iq));
+            hipLaunchKernelGGL(k_tri_item_map, dim3(grid(s, nc)), dim3(256), 0, st, ipre, nc, P<uint32_t>(iq));
             Buf ctr = dev_alloc(sizeof(unsigned long long), s);
             HIP_CHECK(hipMemsetAsync(P<void>(ctr), 0, sizeof(unsigned long long), st));
             const size_t lds = sizeof(ItemLds);
-            const char* walk = getenv("CAPSMI_TRI_WALK");  // "flat": the prefix-sum walk (A/B runs)
-            const bool lists = !(walk && std::string(walk) == "flat");
-            const char* ue = getenv("CAPSMI_TRI_UNROLL");  // target loads in flight per lane: 4, 8 or 16
-            const int un = ue ? atoi(ue) : 8;
-            auto kf = !lists ? k_tri_big_items<false, 4>
-                      : un == 16 ? k_tri_big_items<true, 16>
-                      : un == 8 ? k_tri_big_items<true, 8> : k_tri_big_items<true, 4>;
+            auto kf = vm ? k_tri_big_items<true, 8, true>
+                      : !lists ? k_tri_big_items<false, 4, false>
+                      : un == 16 ? k_tri_big_items<true, 16, false>
+                      : un == 8 ? k_tri_big_items<true, 8, false> : k_tri_big_items<true, 4, false>;
             HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kf), hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)lds));
             hipLaunchKernelGGL(kf, dim3((unsigned)(s->num_cus * 4)), dim3(kBigBlock), lds, st,
                                P<uint32_t>(g.tg), P<uint16_t>(g.tg16), g.hot_end, P<int64_t>(g.ov), P<int64_t>(g.off),
-                               bu, nb, ipre, P<uint32_t>(iq),
-                               P<unsigned long long>(ctr), P<unsigned long long>(out));
-        }
+                               P<int64_t>(g.ioff), P<uint32_t>(g.itg), P<int64_t>(g.iov), g.vmt, cs, nc, ipre,
+                               P<uint32_t>(iq), P<unsigned long long>(ctr), P<unsigned long long>(out));
+        };
+        if (be > bb) run_items(P<int64_t>(g.big_u) + bb, be - bb, false);
+        if (ve > vb) run_items(P<int64_t>(g.vm_c) + vb, ve - vb, true);
         if (se > sb) {
             const int64_t gs = std::min<int64_t>((se - sb + 3) / 4, (int64_t)s->num_cus * 16);
-            const char* sw = getenv("CAPSMI_TRI_WALK");  // "flat": the prefix-sum walk (A/B runs)
-            const bool slists = !(sw && std::string(sw) == "flat");
-            const char* ue = getenv("CAPSMI_TRI_UNROLL");
-            const int un = ue ? atoi(ue) : 8;
-            auto kfs = !slists ? k_tri_small<false, 4>
+            auto kfs = !lists ? k_tri_small<false, 4>
                        : un == 16 ? k_tri_small<true, 16>
                        : un == 8 ? k_tri_small<true, 8> : k_tri_small<true, 4>;
             hipLaunchKernelGGL(kfs, dim3((unsigned)gs), dim3(kTriBlock), 0, st,
                                P<uint32_t>(g.tg),
-                               P<uint16_t>(g.tg16), g.hot_end, P<int64_t>(g.ov), P<int64_t>(g.off), P<int64_t>(g.small_u) + sb, se - sb,
+                               P<uint16_t>(g.tg16), g.hot_end, P<int64_t>(g.ov), P<int64_t>(g.off), g.vmt,
+                               P<int64_t>(g.small_u) + sb, se - sb,
                                P<unsigned long long>(out));
         }
     }

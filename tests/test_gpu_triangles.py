@@ -20,8 +20,18 @@ def _count(session, n, src, dst, mask=None, nparts=1):
     return sum(g.count(p, nparts) for p in range(nparts))
 
 
+VMODE = ["0", "2", "default"]  # CAPSMI_TRI_VMODE_T: every edge from u / almost every edge from v / 256
+
+
+def _vmode(monkeypatch, t):
+    if t != "default":
+        monkeypatch.setenv("CAPSMI_TRI_VMODE_T", t)
+
+
+@pytest.mark.parametrize("vmode", VMODE)
 @pytest.mark.parametrize("seed", range(8))
-def test_random_multigraphs(session, seed):
+def test_random_multigraphs(session, monkeypatch, seed, vmode):
+    _vmode(monkeypatch, vmode)
     rng = np.random.default_rng(seed)
     n = int(rng.integers(3, 60))
     m = int(rng.integers(0, 600))
@@ -31,7 +41,9 @@ def test_random_multigraphs(session, seed):
     assert _count(session, n, src, dst) == cpu.triangle_enumerate(n, src, dst)
 
 
-def test_node_filter_and_parts(session):
+@pytest.mark.parametrize("vmode", VMODE)
+def test_node_filter_and_parts(session, monkeypatch, vmode):
+    _vmode(monkeypatch, vmode)
     rng = np.random.default_rng(42)
     n, m = 200, 4000
     src = rng.integers(0, n, m).astype(np.int64)
@@ -43,17 +55,21 @@ def test_node_filter_and_parts(session):
     assert _count(session, n, src, dst, mask, nparts=4) == want
 
 
+@pytest.mark.parametrize("vmode", VMODE)
 @pytest.mark.parametrize("walk", ["lists", "flat"])
 @pytest.mark.parametrize("scale", [9, 12])
-def test_rmat(session, monkeypatch, scale, walk):
+def test_rmat(session, monkeypatch, scale, walk, vmode):
+    _vmode(monkeypatch, vmode)
     if walk == "flat":
         monkeypatch.setenv("CAPSMI_TRI_WALK", "flat")
     src, dst = cpu.rmat_edges(scale, 0, 16 << scale)
     assert _count(session, 1 << scale, src, dst) == cpu.triangle_enumerate(1 << scale, src, dst)
 
 
+@pytest.mark.parametrize("vmode", VMODE)
 @pytest.mark.parametrize("walk", ["lists", "flat"])
-def test_dense_big_vertices(session, monkeypatch, walk):
+def test_dense_big_vertices(session, monkeypatch, walk, vmode):
+    _vmode(monkeypatch, vmode)
     """Out-degrees above 64 (one workgroup per vertex) on a dense random multigraph; both wedge
     walks (wave-per-list default, CAPSMI_TRI_WALK=flat prefix-sum walk)."""
     if walk == "flat":
@@ -65,8 +81,10 @@ def test_dense_big_vertices(session, monkeypatch, walk):
     assert _count(session, n, src, dst) == cpu.triangle_enumerate(n, src, dst)
 
 
+@pytest.mark.parametrize("vmode", VMODE)
 @pytest.mark.parametrize("mult", [False, True])
-def test_complete_digraph_chunks(session, mult):
+def test_complete_digraph_chunks(session, monkeypatch, mult, vmode):
+    _vmode(monkeypatch, vmode)
     """Complete digraph on 2200 nodes: out-degrees up to 2199 exceed one LDS chunk (2048).
     Loop-free, so count(*) = trace(M^3) for the multiplicity matrix M (exact in float64 here)."""
     n = 2200
