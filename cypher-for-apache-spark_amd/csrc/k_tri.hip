@@ -173,8 +173,8 @@ __global__ void k_offsets(const uint64_t* __restrict__ ok_, int64_t ne, int64_t 
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr int kSmallDeg = 64;
 constexpr int kWedgeUnroll = 4;  // flat walks: wedges per lane with their target loads in flight together
-// (the list walks take it as a template parameter, 8 by default: 252.9 -> 240.8 ms at s = 24 over 4;
-// 16 gains nothing more, since most lists end within one 512-entry pass)
+// (the list walks take it as a template parameter: 4 by default since the direction choice moved the
+// long hub lists to v-mode -- 126.5 ms against 132.4 with 8; before it, 8 beat 4 by 5 %)
 constexpr int kSmallSlots = 512;  // load <= 1/8: a miss (most wedges) ends after ~1.2 probes
 constexpr int kTriBlock = 256;  // small: 4 waves
 constexpr int kBigBlock = 1024;
@@ -783,8 +783,8 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
         const int64_t vb = g.nvm * part / nparts, ve = g.nvm * (part + 1) / nparts;
         const char* walk = getenv("CAPSMI_TRI_WALK");  // "flat": the prefix-sum walk (A/B runs)
         const bool lists = !(walk && std::string(walk) == "flat");
-        const char* ue = getenv("CAPSMI_TRI_UNROLL");  // target loads in flight per lane: 4, 8 or 16
-        const int un = ue ? atoi(ue) : 8;
+        const char* ue = getenv("CAPSMI_TRI_UNROLL");  // target loads in flight per lane: 4 (default), 8 or 16
+        const int un = ue ? atoi(ue) : 4;
         // items (hash chunk, neighbour chunk) of the centers cs[0, nc), taken from a global counter
         auto run_items = [&](const int64_t* cs, int64_t nc, bool vm) {
             Buf ib = dev_alloc(sizeof(int64_t) * (2 * nc + 2), s);
@@ -799,7 +799,9 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
             Buf ctr = dev_alloc(sizeof(unsigned long long), s);
             HIP_CHECK(hipMemsetAsync(P<void>(ctr), 0, sizeof(unsigned long long), st));
             const size_t lds = sizeof(ItemLds);
-            auto kf = vm ? k_tri_big_items<true, 8, true>
+            const char* uve = getenv("CAPSMI_TRI_UNROLL_VM");  // v-mode loads in flight per lane: 4 or 8
+            const int uv = uve ? atoi(uve) : 4;
+            auto kf = vm ? (uv == 4 ? k_tri_big_items<true, 4, true> : k_tri_big_items<true, 8, true>)
                       : !lists ? k_tri_big_items<false, 4, false>
                       : un == 16 ? k_tri_big_items<true, 16, false>
                       : un == 8 ? k_tri_big_items<true, 8, false> : k_tri_big_items<true, 4, false>;
