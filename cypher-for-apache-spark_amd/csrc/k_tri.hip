@@ -750,7 +750,11 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         g.iov = dev_alloc(sizeof(int64_t) * ne, s);
         hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.ov), ne,
                            P<uint64_t>(ik), P<int64_t>(g.iov));
-        radix_sort_digits(s, P<uint64_t>(ik), P<int64_t>(g.iov), ne, od);  // by (to, from)
+        // by (to, from): the input is in (from, to) order and the LSD sort is stable, so the digits of
+        // `to` alone give that order (3 passes at 2^24 ids instead of 6)
+        std::vector<int> td;
+        for (int sh = 32; sh < 32 + bits; sh += 8) td.push_back(sh);
+        radix_sort_digits(s, P<uint64_t>(ik), P<int64_t>(g.iov), ne, td);
         g.ioff = dev_alloc(sizeof(int64_t) * (n + 1), s);
         hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), ne, n, P<int64_t>(g.ioff));
         g.itg = dev_alloc(sizeof(uint32_t) * ne, s);
