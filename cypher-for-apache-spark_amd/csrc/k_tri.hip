@@ -714,8 +714,9 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         Buf dk = dev_alloc(sizeof(uint64_t) * n, s), dv = dev_alloc(sizeof(int64_t) * n, s);
         hipLaunchKernelGGL(k_deg_keys, dim3(grid(s, n)), dim3(256), 0, st, P<uint32_t>(deg), n, P<uint64_t>(dk),
                            P<int64_t>(dv));
+        // the keys are written in id order and the LSD sort is stable: the degree digits alone give
+        // the (degree, id) order
         std::vector<int> dd;
-        for (int sh = 0; sh < bits; sh += 8) dd.push_back(sh);
         for (int sh = 32; sh < 64; sh += 8) dd.push_back(sh);
         radix_sort_digits(s, P<uint64_t>(dk), P<int64_t>(dv), n, dd);
         hipLaunchKernelGGL(k_rank_ids, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(dv), n, P<uint32_t>(rid),
