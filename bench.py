@@ -131,17 +131,25 @@ def pmc_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this workload
     (profiles/*_<workload>_pmc.json, newest round first), FETCH_SIZE doubled per MI355X_MICROARCH.md
     (gfx950 tallies 128-B reads at 64 B), or None."""
-    if "+" in kernel:  # a timer spanning several kernels: their traffic summed
-        parts = [pmc_traffic(k, workload) for k in kernel.split("+")]
-        return None if any(p is None for p in parts) else sum(parts)
+    if "+" in kernel:  # a timer spanning several kernels: their traffic per timed call, summed
+        parts = [_pmc_entry(k, workload) for k in kernel.split("+")]
+        if any(p is None for p in parts):
+            return None
+        calls = min(p["launches"] for p in parts)  # a kernel launched k times per call (C4: the item
+        return sum(p["hbm_bytes_per_launch"] * p["launches"] / calls for p in parts)  # kernel, u- and v-mode)
+    p = _pmc_entry(kernel, workload)
+    return None if p is None else p["hbm_bytes_per_launch"]
+
+
+def _pmc_entry(kernel, workload):
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}_pmc.json")))
     for f in reversed(files):
         try:
             with open(f) as fh:
                 d = json.load(fh)
             k = d.get("kernels", {}).get(kernel)
-            if k and "hbm_bytes_per_launch" in k:
-                return k["hbm_bytes_per_launch"]
+            if k and "hbm_bytes_per_launch" in k and k.get("launches"):
+                return k
         except (OSError, ValueError):
             continue
     return None
