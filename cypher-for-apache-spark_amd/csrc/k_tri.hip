@@ -54,27 +54,50 @@ __global__ void k_heads(const uint64_t* __restrict__ k, int64_t n, uint64_t mask
         f[i] = (k[i] != kNone && (i == 0 || (k[i] & mask) != (k[i - 1] & mask))) ? 1 : 0;
 }
 
+// end of the valid keys: the first kNone of the sorted keys (one lane, O(log m) reads on the device)
+__global__ void k_first_none(const uint64_t* __restrict__ k, int64_t m, int64_t* __restrict__ out) {
+    int64_t a = 0, b = m;
+    while (a < b) {
+        const int64_t mid = (a + b) / 2;
+        if (k[mid] == kNone) b = mid; else a = mid + 1;
+    }
+    *out = a;
+}
+
 // undirected runs -> (key min<<32|max, payload m(min,max)<<32 | m(max,min)), degrees.  The runs are
 // sorted by their lower end, so a wave's lanes with the same lower end are contiguous: one atomic
 // per such segment (hubs would otherwise serialise hundreds of thousands of adds on one counter).
+// A run longer than kShortRun (multi-edges between two hubs, up to ~10^4 at C4) is not walked by
+// its lane, which would hold its wave for the whole walk: it goes to a list that k_und_long counts
+// with a whole workgroup per run.
+constexpr int64_t kShortRun = 32;
+
+__device__ __forceinline__ uint64_t back_bit(uint64_t key, int msh) { return msh ? (key & 1u) : ((key >> 31) & 1u); }
+
 __global__ void k_und_runs(const uint64_t* __restrict__ k, const int64_t* __restrict__ heads, int64_t nruns,
-                           int64_t nvalid, int msh, uint64_t* __restrict__ ek, int64_t* __restrict__ ev,
-                           uint32_t* __restrict__ deg) {
+                           const int64_t* __restrict__ nvalid_p, int msh, uint64_t* __restrict__ ek,
+                           int64_t* __restrict__ ev, uint32_t* __restrict__ deg, int64_t* __restrict__ longr,
+                           unsigned long long* __restrict__ nlong) {
     const int lane = threadIdx.x & 63;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t nvalid = *nvalid_p;
     for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); r0 < nruns; r0 += stride) {  // wave-uniform
         const int64_t r = r0 + lane;
         const bool act = r < nruns;  // the active lanes are a prefix of the wave
         uint32_t mn = 0;
         if (act) {
             const int64_t h = heads[r], h2 = r + 1 < nruns ? heads[r + 1] : nvalid;
-            uint64_t back = 0;  // relationships max -> min
-            for (int64_t i = h; i < h2; ++i) back += msh ? (k[i] & 1u) : ((k[i] >> 31) & 1u);
             const uint64_t key = k[h];
             mn = (uint32_t)(key >> 32);
             const uint32_t mx = msh ? ((uint32_t)key >> 1) : ((uint32_t)key & 0x7FFFFFFFu);
             ek[r] = ((uint64_t)mn << 32) | mx;
-            ev[r] = (int64_t)((((uint64_t)(h2 - h) - back) << 32) | back);
+            if (h2 - h <= kShortRun) {
+                uint64_t back = 0;  // relationships max -> min
+                for (int64_t i = h; i < h2; ++i) back += back_bit(k[i], msh);
+                ev[r] = (int64_t)((((uint64_t)(h2 - h) - back) << 32) | back);
+            } else {
+                longr[atomicAdd(nlong, 1ull)] = r;
+            }
             atomicAdd(&deg[mx], 1u);
         }
         const uint32_t prev = __shfl_up(mn, 1, 64);
@@ -85,6 +108,29 @@ __global__ void k_und_runs(const uint64_t* __restrict__ k, const int64_t* __rest
             const int next = later ? lane + 1 + __builtin_ctzll(later) : __popcll(am);
             atomicAdd(&deg[mn], (uint32_t)(next - lane));
         }
+    }
+}
+
+// the long runs' payloads: one workgroup per run, a block reduction of the direction bits
+__global__ void __launch_bounds__(256) k_und_long(const uint64_t* __restrict__ k, const int64_t* __restrict__ heads,
+                                                  int64_t nruns, const int64_t* __restrict__ nvalid_p, int msh,
+                                                  const int64_t* __restrict__ longr,
+                                                  const unsigned long long* __restrict__ nlong,
+                                                  int64_t* __restrict__ ev) {
+    __shared__ unsigned long long part[4];
+    const int64_t cnt = (int64_t)*nlong, nvalid = *nvalid_p;
+    for (int64_t q = blockIdx.x; q < cnt; q += gridDim.x) {  // block-uniform
+        const int64_t r = longr[q], h = heads[r], h2 = r + 1 < nruns ? heads[r + 1] : nvalid;
+        unsigned long long back = 0;
+        for (int64_t i = h + threadIdx.x; i < h2; i += 256) back += back_bit(k[i], msh);
+        for (int o = 32; o > 0; o >>= 1) back += __shfl_down(back, o, 64);
+        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = back;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint64_t b = part[0] + part[1] + part[2] + part[3];
+            ev[r] = (int64_t)((((uint64_t)(h2 - h) - b) << 32) | b);
+        }
+        __syncthreads();
     }
 }
 
@@ -683,27 +729,24 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     Buf f = dev_alloc(m > 0 ? m : 1, s), heads;
     hipLaunchKernelGGL(k_heads, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, dmask, P<uint8_t>(f));
     const int64_t ne = flags_to_indices(s, P<uint8_t>(f), m, heads);
-    int64_t nvalid = 0;
-    {
-        // nvalid: binary search for the first kNone in the sorted keys (host-side bisection, O(log m) reads)
-        int64_t a = 0, b = m;
-        while (a < b) {
-            const int64_t mid = (a + b) / 2;
-            uint64_t kv;
-            HIP_CHECK(hipMemcpyAsync(&kv, P<uint64_t>(key) + mid, 8, hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
-            if (kv == kNone) b = mid; else a = mid + 1;
-        }
-        nvalid = a;
-    }
+    Buf nv = dev_alloc(sizeof(int64_t) + sizeof(unsigned long long), s);  // nvalid, long-run count
+    HIP_CHECK(hipMemsetAsync(P<void>(nv), 0, sizeof(int64_t) + sizeof(unsigned long long), st));
+    int64_t* nvalid_p = P<int64_t>(nv);
+    unsigned long long* nlong = reinterpret_cast<unsigned long long*>(nvalid_p + 1);
+    hipLaunchKernelGGL(k_first_none, dim3(1), dim3(1), 0, st, P<uint64_t>(key), m, nvalid_p);
     g.ne = ne;
     g.ek = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), s);
     g.ev = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);
     Buf deg = dev_alloc(sizeof(uint32_t) * n, s);
     HIP_CHECK(hipMemsetAsync(P<void>(deg), 0, sizeof(uint32_t) * n, st));
-    if (ne > 0)
+    if (ne > 0) {
+        Buf longr = dev_alloc(sizeof(int64_t) * (m / kShortRun + 1), s);
         hipLaunchKernelGGL(k_und_runs, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(key), P<int64_t>(heads), ne,
-                           nvalid, msh, P<uint64_t>(g.ek), P<int64_t>(g.ev), P<uint32_t>(deg));
+                           nvalid_p, msh, P<uint64_t>(g.ek), P<int64_t>(g.ev), P<uint32_t>(deg), P<int64_t>(longr), nlong);
+        hipLaunchKernelGGL(k_und_long, dim3(4 * s->num_cus), dim3(256), 0, st, P<uint64_t>(key), P<int64_t>(heads), ne,
+                           nvalid_p, msh, P<int64_t>(longr), nlong, P<int64_t>(g.ev));
+        HIP_CHECK(hipGetLastError());
+    }
     key.reset();
     f.reset();
     heads.reset();
