@@ -750,6 +750,11 @@ capsmi_status capsmi_table_export(const capsmi_table* t, int32_t col, void* host
     use_device(t->sess);
     const Column& c = t->cols[col];
     hipStream_t st = t->sess->stream;
+    if (c.host && !c.valid && c.offset + offset + n <= (int64_t)c.host->size()) {  // host-built words
+        if (n && host_data) std::memcpy(host_data, c.host->data() + c.offset + offset, sizeof(int64_t) * n);
+        if (n && host_valid) std::memset(host_valid, 1, n);
+        return CAPSMI_OK;
+    }
     if (n && host_data)
         HIP_CHECK(hipMemcpyAsync(host_data, c.d() + offset, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
     if (n && host_valid) {

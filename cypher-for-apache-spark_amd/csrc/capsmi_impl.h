@@ -63,6 +63,9 @@ struct Column {
     Buf valid;             // uint8 per row, may be null (no nulls)
     int64_t offset = 0;    // row offset into data/valid (zero-copy skip)
     bool lazy_nullable = false;  // schema of a lazy table's column (no data yet): may hold nulls
+    // host copy of the words of a column built from host values (the fused routes' count rows):
+    // exports read it without a device round trip
+    std::shared_ptr<const std::vector<int64_t>> host;
     const int64_t* d() const { return P<int64_t>(data) + offset; }
     const uint8_t* v() const { return valid ? P<uint8_t>(valid) + offset : nullptr; }
     bool nullable() const { return valid != nullptr || lazy_nullable; }

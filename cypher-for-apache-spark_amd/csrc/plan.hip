@@ -750,9 +750,13 @@ Column i64_column(capsmi_session* s, const std::vector<int64_t>& v) {
     Column c;
     c.type = CAPSMI_I64;
     c.data = dev_alloc(sizeof(int64_t) * (v.empty() ? 1 : v.size()), s);
-    if (!v.empty())
+    c.host = std::make_shared<const std::vector<int64_t>>(v);
+    if (v.size() == 1) {  // one word: a fill kernel, so neither a copy nor a host sync
+        fill_i64(P<int64_t>(c.data), v[0], 1, s->stream);
+    } else if (!v.empty()) {
         HIP_CHECK(hipMemcpyAsync(P<void>(c.data), v.data(), sizeof(int64_t) * v.size(), hipMemcpyHostToDevice, s->stream));
-    HIP_CHECK(hipStreamSynchronize(s->stream));
+        HIP_CHECK(hipStreamSynchronize(s->stream));
+    }
     return c;
 }
 
@@ -968,6 +972,7 @@ bool fused_var_length(capsmi_session* s, const capsmi_table* in, const PlanNode&
         gather_col(P<int64_t>(g_dense->orig), nullptr, c.d(), r->nrows, ::capsmi::P<int64_t>(ids), nullptr, s->stream);
         c.data = ids;
         c.offset = 0;
+        c.host.reset();
     }
     route(s, "var_length");
     return true;
