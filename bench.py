@@ -47,8 +47,8 @@ KERNELS = ("part_scatter1", "part_scatter2_hop1", "part_scatter2", "hop1", "hop2
 # timer name -> kernel name as rocprofv3 reports it (hop1 and hop2 are two instances of k_hop_2d)
 KERNEL_SYMBOL = {"part_scatter1": "k_scatter_l", "part_scatter2_hop1": "k_scatter_s2", "part_scatter2": "k_scatter_s2",
                  "hop1": "k_hop_2d", "hop2": "k_hop_2d", "mid_combine": "k_mid_combine", "bitmap_add": "k_bitmap_add",
-                 "count_part_in": "k_scatter_c", "count_part_out": "k_scatter_c", "count_in": "k_cnt_in",
-                 "count_out": "k_cnt_out", "degrees": "k_degrees"}
+                 "count_part_in": "k_rec_part", "count_part_out": "k_rec_part", "count_in": "k_rec_walk",
+                 "count_out": "k_rec_walk", "degrees": "k_degrees"}
 
 
 def parse():
@@ -425,7 +425,7 @@ def main():
                "hop1": m_local * 8 + n // 8,         # read uint2 pairs, write M
                "hop2": m_local * 8 + n // 8 * 3,     # read uint2 pairs + X1 + X2, write C
                "mid_combine": n // 8 * 5, "bitmap_add": n * 8,
-               "count_part_in": m_local * 24, "count_part_out": m_local * 24,  # chunked partition pass 1
+               "count_part_in": m_local * 18, "count_part_out": m_local * 18,  # read 2 x int64, write a 2-B record
                "degrees": m_local * 16 + n * 8}                  # read int64 pairs, inA + outC
         alg.update(kbytes)
         timed = {k: (c, ms) for k, (c, ms) in kt.items() if c > 0}

@@ -1829,7 +1829,9 @@ capsmi_status capsmi_two_hop_count(capsmi_session* s, int32_t nrels, capsmi_tabl
             dsts.push_back(rel_col(rels[i], dst_col).d());
             ms.push_back(rels[i]->nrows);
         }
-        *out_rows = two_hop_count_part(s, srcs.data(), dsts.data(), ms.data(), nrels, a_ok, b_ok, c_ok);
+        *out_rows = mode && std::string(mode) == "pairs"  // the 8-byte pair partition (A/B)
+                        ? two_hop_count_part(s, srcs.data(), dsts.data(), ms.data(), nrels, a_ok, b_ok, c_ok)
+                        : two_hop_count_rec(s, srcs.data(), dsts.data(), ms.data(), nrels, a_ok, b_ok, c_ok);
         return CAPSMI_OK;
     }
     Buf inA = dev_alloc(sizeof(uint32_t) * (n > 0 ? n : 1), s);

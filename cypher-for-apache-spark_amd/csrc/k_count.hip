@@ -16,6 +16,8 @@
 //           block's LDS copy of the slice's inA (128 KiB, staged once per slice segment).
 // (Pass 2 over the relationships in table order, gathering inA(source) from HBM instead of a second
 // partition, measured 19.6 ms against 8.4 + 5.8 ms at C3.)
+#include <mutex>
+
 #include "part_common.h"
 
 namespace capsmi {
@@ -90,6 +92,435 @@ __global__ void __launch_bounds__(kBlock) k_cnt_out(part::ChunkWalk cw, part::Bi
 }
 
 }  // namespace cnt
+
+// ---- count(*) partitions of 2-byte records -----------------------------------------------------------
+// The pair partition above writes 8 bytes per relationship into 2048 buckets, and at 4 pairs per
+// bucket per tile its chunk tails are partial lines (k_scatter_c ran at 2.7 TB/s).  A count needs
+// less: the in-pass needs only the target of a relationship whose source passes a_ok, the out-pass
+// only the source of one whose target passes c_ok.  So each pass here writes one 2-byte record per
+// kept relationship -- the id's low 16 bits, the bucket being the id's high bits (2^16 ids, <= 1024
+// buckets) -- and a bucket's records leave the workgroup as whole 64-byte pieces: a tile's run is
+// appended behind the < 32 records the bucket holds back in LDS, every complete piece is stored,
+// the rest is held for the next tile.  The walks count a bucket in 16-bit LDS counters (128 KiB)
+// with exact wrap corrections: 16 + 2 + 2 bytes per relationship and pass, against 16 + 8 + 8 for
+// the pair partition.
+namespace rec {
+
+constexpr int kBits = 16;        // ids per bucket
+constexpr int kB = 1024;         // workgroup
+constexpr int kIT = 8;           // relationships per lane per tile
+constexpr int kT = kB * kIT;     // relationships per tile
+constexpr int kPiece = 32;       // records per 64-byte store
+constexpr int kCh = 16384;       // records per chunk (32 KiB; a tile adds <= 257 pieces of its 512)
+constexpr int kMaxBuckets = 1024;
+constexpr int kWalkG = 4;        // chunks in flight per walk block
+constexpr int kInfo = 2048;      // chunk ids staged in LDS per walk block
+constexpr int kBig = 255;        // OUT walk: values >= 0xFF00 per bucket kept exactly in LDS
+constexpr size_t walk_lds() {
+    return sizeof(uint32_t) * (1 << (kBits - 1)) + sizeof(uint2) * kInfo + sizeof(uint32_t) * (kBig + 1);
+}
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+__host__ __device__ constexpr size_t part_lds(int nb) {
+    return sizeof(uint16_t) * ((size_t)kT + (size_t)nb * kPiece) + sizeof(uint32_t) * (8 * (size_t)nb + kB / 64 + 4);
+}
+
+__host__ __device__ constexpr int64_t chunks_per_block(int64_t m, int64_t grid, int nb) {
+    // full chunks, plus per bucket the open one and one retired part-full by the final flush
+    return (((m + kT - 1) / kT + grid - 1) / grid * kT + kCh - 1) / kCh + 2 * (int64_t)nb + 1;
+}
+
+__device__ __forceinline__ bool bit(const part::BitV& v, uint64_t x) { return v.full || part::gbit(v.w, (uint32_t)x); }
+
+// OUT = false: records of targets (bucket = target >> 16) of relationships with a_ok(source); the
+// a_ok, b_ok, c_ok self-loops are counted into `loops`.  OUT = true: records of sources of
+// relationships with c_ok(target).  `f` is a_ok / c_ok.
+template <bool OUT>
+__global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                 int64_t m, int64_t lo, int64_t range, int nb, part::BitV f, part::BitV b,
+                                                 part::BitV c, int64_t chunk0, int64_t cpb, uint16_t* __restrict__ pool,
+                                                 unsigned long long* __restrict__ cmeta,
+                                                 unsigned long long* __restrict__ loops) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+    uint16_t* stage = reinterpret_cast<uint16_t*>(sm);  // kT: this tile's records grouped by bucket
+    uint16_t* hold = stage + kT;                         // nb x kPiece: records held back per bucket
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(hold + (size_t)nb * kPiece);  // run length this tile
+    uint32_t* loc = cnt + nb;  // run start in the stage
+    uint32_t* hc = loc + nb;   // records held (< kPiece)
+    uint32_t* fl = hc + nb;    // records stored in the open chunk (a multiple of kPiece)
+    uint32_t* ph = fl + nb;    // open chunk
+    uint32_t* np = ph + nb;    // chunk opened for this tile's overflow
+    uint32_t* pc = np + nb;    // pieces stored this tile
+    uint32_t* pb = pc + nb;    // first piece of the bucket this tile
+    uint32_t* wtot = pb + nb;
+    uint32_t* misc = wtot + kB / 64;  // [0] next free chunk of this block
+    for (int i = threadIdx.x; i < nb; i += kB) {
+        cnt[i] = 0;
+        hc[i] = 0;
+        fl[i] = 0;
+        ph[i] = kNone;
+        np[i] = kNone;
+    }
+    if (threadIdx.x == 0) misc[0] = (uint32_t)(chunk0 + (int64_t)blockIdx.x * cpb);
+    const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
+    const int64_t stride = (int64_t)gridDim.x * kT;
+    unsigned long long nl = 0;
+    int64_t sr[kIT], tr[kIT];
+    int64_t t0 = (int64_t)blockIdx.x * kT;
+    if (t0 < m) part::load_tile<kB>(src, dst, t0, m, vec, sr, tr);
+    __syncthreads();
+    for (; t0 < m; t0 += stride) {  // block-uniform
+        uint32_t key[kIT], rk[kIT];
+        uint32_t valid = 0;
+#pragma unroll
+        for (int u = 0; u < kIT; ++u) {
+            const int64_t e = t0 + part::item_off<kB>(u);
+            const uint64_t x = (uint64_t)(sr[u] - lo), y = (uint64_t)(tr[u] - lo);
+            bool ok = e < m && x < (uint64_t)range && y < (uint64_t)range;
+            if (OUT) {
+                ok = ok && bit(f, y);
+            } else {
+                ok = ok && bit(f, x);
+                if (ok && x == y && bit(b, x) && bit(c, x)) ++nl;
+            }
+            key[u] = (uint32_t)(OUT ? x : y);
+            valid |= (ok ? 1u : 0u) << u;
+        }
+        if (t0 + stride < m) part::load_tile<kB>(src, dst, t0 + stride, m, vec, sr, tr);  // prefetch
+#pragma unroll
+        for (int u = 0; u < kIT; ++u) rk[u] = ((valid >> u) & 1u) ? atomicAdd(&cnt[key[u] >> kBits], 1u) : 0u;
+        __syncthreads();
+        (void)part::block_exclusive_scan<kB>(cnt, loc, nb, wtot);
+#pragma unroll
+        for (int u = 0; u < kIT; ++u)
+            if ((valid >> u) & 1u) stage[loc[key[u] >> kBits] + rk[u]] = (uint16_t)(key[u] & 0xFFFFu);
+        for (int i = threadIdx.x; i < nb; i += kB) {  // pieces of the held + run sequence; chunks they open
+            const uint32_t npc = (hc[i] + cnt[i]) / kPiece;
+            pc[i] = npc;
+            if (npc) {
+                if (ph[i] == kNone) {
+                    ph[i] = atomicAdd(&misc[0], 1u);
+                    fl[i] = 0;
+                } else if (fl[i] + npc * kPiece > (uint32_t)kCh) {
+                    np[i] = atomicAdd(&misc[0], 1u);
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t P = part::block_exclusive_scan<kB>(pc, pb, nb, wtot);
+        // piece g: 4 lanes x 8 records; element e < held comes from the hold, the rest from the run
+        for (uint32_t x = threadIdx.x; x < P * 4; x += kB) {
+            const uint32_t g = x >> 2, r = x & 3;
+            int lo_b = 0, hi_b = nb;  // last bucket with pb <= g (empty buckets share pb with the next)
+            while (hi_b - lo_b > 1) {
+                const int mid = (lo_b + hi_b) >> 1;
+                if (pb[mid] <= g) lo_b = mid; else hi_b = mid;
+            }
+            int bk = lo_b;
+            while (pc[bk] == 0 || pb[bk] + pc[bk] <= g) ++bk;
+            const uint32_t k = g - pb[bk], h = hc[bk];
+            uint16_t v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t e = k * kPiece + r * 8 + (uint32_t)q;
+                v[q] = e < h ? hold[bk * kPiece + (int)e] : stage[loc[bk] + e - h];
+            }
+            const uint32_t pos = fl[bk] + k * kPiece;
+            const uint32_t ch = pos < (uint32_t)kCh ? ph[bk] : np[bk];
+            const uint32_t off = (pos < (uint32_t)kCh ? pos : pos - (uint32_t)kCh) + r * 8;
+            uint4 w;
+            w.x = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
+            w.y = (uint32_t)v[2] | ((uint32_t)v[3] << 16);
+            w.z = (uint32_t)v[4] | ((uint32_t)v[5] << 16);
+            w.w = (uint32_t)v[6] | ((uint32_t)v[7] << 16);
+            *reinterpret_cast<uint4*>(pool + (size_t)ch * kCh + off) = w;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kIT; ++u) {  // the new held records: the run's items past its last whole piece
+            if ((valid >> u) & 1u) {
+                const uint32_t bk = key[u] >> kBits, e = hc[bk] + rk[u], cut = pc[bk] * kPiece;
+                if (e >= cut) hold[bk * kPiece + (e - cut)] = (uint16_t)(key[u] & 0xFFFFu);
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < nb; i += kB) {
+            const uint32_t tot = hc[i] + cnt[i], npc = pc[i];
+            const uint32_t end = fl[i] + npc * kPiece;
+            if (np[i] != kNone) {  // the open chunk is full: retire it
+                cmeta[ph[i]] = part::chunk_meta(i, (uint32_t)kCh);
+                ph[i] = np[i];
+                np[i] = kNone;
+                fl[i] = end - (uint32_t)kCh;
+            } else {
+                fl[i] = end;
+            }
+            hc[i] = tot - npc * kPiece;
+            cnt[i] = 0;
+        }
+        __syncthreads();
+    }
+    // the held records: into the open chunk, or a new one when there is none or it is full
+    for (int i = threadIdx.x; i < nb; i += kB) {
+        if (hc[i] && (ph[i] == kNone || fl[i] + hc[i] > (uint32_t)kCh)) {
+            if (ph[i] != kNone) cmeta[ph[i]] = part::chunk_meta(i, fl[i]);
+            ph[i] = atomicAdd(&misc[0], 1u);
+            fl[i] = 0;
+        }
+    }
+    __syncthreads();
+    for (int x = threadIdx.x; x < nb * kPiece; x += kB) {
+        const int bk = x / kPiece, e = x % kPiece;
+        if ((uint32_t)e < hc[bk]) pool[(size_t)ph[bk] * kCh + fl[bk] + (uint32_t)e] = hold[x];
+    }
+    for (int i = threadIdx.x; i < nb; i += kB)
+        if (ph[i] != kNone) cmeta[ph[i]] = part::chunk_meta(i, fl[i] + hc[i]);
+    if (!OUT) cnt::block_add(nl, loops);
+}
+
+// Walk of a record partition in bucket order, one pass per bucket: the bucket's 2^16 ids as 16-bit
+// LDS counters, two per word (128 KiB).
+//   OUT = false: inA(t) counted with word atomics; a counter that wraps is corrected exactly in
+//     `corr` (global, rare: ids with >= 2^16 in-relationships): a low half going 0xFFFF -> 0 adds
+//     2^16 to its id and, through the carry, 1 too many to the high id; a high half wrapping (its
+//     own add, or a carry into 0xFFFF) adds 2^16 to the high id.  Counts are stored through b_ok
+//     at each bucket change.
+//   OUT = true: inA + corr of the bucket staged as saturated 16-bit values; 0xFFFF (>= 2^16)
+//     reads the exact value from HBM.  sum += inA(s) per record.
+template <bool OUT>
+__global__ void __launch_bounds__(kB) k_rec_walk(const uint16_t* __restrict__ pool,
+                                                 const unsigned long long* __restrict__ meta,
+                                                 const uint32_t* __restrict__ order, const int64_t* __restrict__ jst,
+                                                 int nb, int64_t n, part::BitV b, uint32_t* __restrict__ inA,
+                                                 int32_t* __restrict__ corr, unsigned long long* __restrict__ sum) {
+    extern __shared__ uint32_t cl[];  // 2^15 words = 2^16 16-bit counters / staged values
+    constexpr int kWords = 1 << (kBits - 1);
+    uint2* cinfo = reinterpret_cast<uint2*>(cl + kWords);  // (chunk, fill) of kInfo chunks of the share
+    uint32_t* bigv = reinterpret_cast<uint32_t*>(cinfo + kInfo);  // OUT: exact values behind 0xFF00 + k
+    uint32_t* nbig = bigv + kBig;
+    const part::SegSplit S(jst, nb, gridDim.x);
+    const int64_t qb = (int64_t)blockIdx.x * S.per, qe = min(qb + S.per, S.nch);
+    unsigned long long acc = 0;
+    if (qb < qe) {  // block-uniform
+        // the chunk ids and fills are staged in LDS kInfo at a time, so a chunk's loads wait for no
+        // index load (order -> meta -> data would be two dependent round trips per chunk)
+        int64_t ibase = qb, iend = qb;
+        auto refill = [&](int64_t from) {
+            __syncthreads();
+            for (int i = threadIdx.x; i < kInfo; i += kB) {
+                const int64_t q = from + i;
+                if (q < qe) {
+                    const uint32_t phys = order[q];
+                    cinfo[i] = make_uint2(phys, (uint32_t)(meta[phys] >> 32));
+                }
+            }
+            ibase = from;
+            iend = min(from + kInfo, qe);
+            __syncthreads();
+        };
+        refill(qb);
+        auto load = [&](int64_t q, uint4 (&v)[2]) -> uint32_t {
+            if (q >= qe) return 0u;
+            const uint2 ci = cinfo[q - ibase];
+            const uint32_t phys = ci.x, fill = ci.y;
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint16_t*>(pool + (size_t)phys * kCh), (short)0,
+                (int)((fill * sizeof(uint16_t) + 15) & ~(size_t)15), 0x00020000);  // whole dwords: masked by `fill` below
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(k * kB + (int)threadIdx.x) * 16u, 0, 2);
+                v[k] = make_uint4(x[0], x[1], x[2], x[3]);
+            }
+            return fill;
+        };
+        auto exact = [&](int64_t x) -> uint32_t {  // OUT: the stored count of id x
+            return x < n && bit(b, (uint64_t)x) ? (uint32_t)((int64_t)inA[x] + corr[x]) : 0u;
+        };
+        auto slot16 = [&](uint32_t v) -> uint32_t {  // OUT: a value as its 16-bit slot
+            if (v < 0xFF00u) return v;
+            const uint32_t k = atomicAdd(nbig, 1u);
+            if (k < (uint32_t)kBig) {
+                bigv[k] = v;
+                return 0xFF00u + k;
+            }
+            return 0xFFFFu;  // read from HBM
+        };
+        auto begin = [&](int j) {
+            const int64_t base = (int64_t)j << kBits;
+            if (OUT && threadIdx.x == 0) *nbig = 0;
+            if (OUT) __syncthreads();
+            for (int i = threadIdx.x; i < kWords; i += kB) {
+                uint32_t w = 0;
+                if (OUT) w = slot16(exact(base + 2 * i)) | (slot16(exact(base + 2 * i + 1)) << 16);
+                cl[i] = w;
+            }
+        };
+        auto flush = [&](int j) {
+            if (OUT) return;
+            const bool own = qb <= jst[j] && qe >= jst[j + 1];  // else the bucket's other blocks add to it too
+            const int64_t base = (int64_t)j << kBits;
+            for (int i = threadIdx.x; i < kWords; i += kB) {
+                const uint32_t w = cl[i];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int64_t x = base + 2 * i + h;
+                    if (x < n) {
+                        const uint32_t keep = bit(b, (uint64_t)x) ? (h ? w >> 16 : w & 0xFFFFu) : 0u;
+                        if (own) inA[x] = keep;
+                        else if (keep) atomicAdd(&inA[x], keep);
+                    }
+                }
+            }
+        };
+        int cur_j = part::slice_of(jst, nb, qb);
+        int64_t j_end = jst[cur_j + 1];
+        begin(cur_j);
+        __syncthreads();
+        uint4 nx[kWalkG][2];
+        uint32_t nfill[kWalkG];
+#pragma unroll
+        for (int g = 0; g < kWalkG; ++g) nfill[g] = load(qb + g, nx[g]);
+        for (int64_t q0 = qb; q0 < qe; q0 += kWalkG) {  // block-uniform; kWalkG chunks in flight
+#pragma unroll
+            for (int g = 0; g < kWalkG; ++g) {  // static slots: each use waits for its own loads only
+                const int64_t q = q0 + g;
+                if (q >= qe) break;
+                const uint4 v0 = nx[g][0], v1 = nx[g][1];
+                const uint32_t fill = nfill[g];
+                if (q + kWalkG >= iend && iend < qe) refill(q + kWalkG);  // block-uniform
+                nfill[g] = load(q + kWalkG, nx[g]);
+                int j = cur_j;
+                while (q >= j_end) j_end = jst[++j + 1];  // empty buckets are skipped
+                if (j != cur_j) {
+                    __syncthreads();
+                    flush(cur_j);
+                    __syncthreads();
+                    begin(j);
+                    __syncthreads();
+                    cur_j = j;
+                }
+                const int64_t base = (int64_t)cur_j << kBits;
+                const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+                // all 16 LDS accesses are issued before any result is used (one wait, not 16)
+                uint32_t got[16];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int k = e >> 1, h = e & 1;
+                    const uint32_t i = ((uint32_t)((k >> 2) * kB) + threadIdx.x) * 8 + (uint32_t)(k & 3) * 2 + (uint32_t)h;
+                    const uint32_t r = (w[k] >> (16 * h)) & 0xFFFFu;
+                    got[e] = 0u;
+                    if (i < fill) got[e] = OUT ? cl[r >> 1] : atomicAdd(&cl[r >> 1], 1u << ((r & 1u) * 16u));
+                }
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int k = e >> 1, h = e & 1;
+                    const uint32_t i = ((uint32_t)((k >> 2) * kB) + threadIdx.x) * 8 + (uint32_t)(k & 3) * 2 + (uint32_t)h;
+                    const uint32_t r = (w[k] >> (16 * h)) & 0xFFFFu, sh = (r & 1u) * 16u;
+                    if (i >= fill) continue;
+                    if (OUT) {
+                        const uint32_t v = (got[e] >> sh) & 0xFFFFu;
+                        acc += v < 0xFF00u ? v : v != 0xFFFFu ? bigv[v - 0xFF00u] : exact(base + r);
+                    } else {
+                        const uint32_t old = got[e];
+                        const int64_t xl = base + (r & ~1u), xh = xl + 1;
+                        if (sh == 0 && (old & 0xFFFFu) == 0xFFFFu) {  // low wrap: + 2^16 low, carry into high
+                            atomicAdd(&corr[xl], 65536);
+                            if (xh < n) atomicAdd(&corr[xh], (old >> 16) == 0xFFFFu ? 65535 : -1);  // carry wrapped high too
+                        } else if (sh == 16 && (old >> 16) == 0xFFFFu) {
+                            atomicAdd(&corr[xh], 65536);
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        flush(cur_j);
+    }
+    if (OUT) cnt::block_add(acc, sum);
+}
+
+}  // namespace rec
+
+// the same count from two record partitions (rec:: above); one id domain of at most 2^26 ids
+int64_t two_hop_count_rec(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
+                          int nt, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok) {
+    using namespace rec;
+    const int64_t lo = b_ok->lo, n = b_ok->hi - b_ok->lo;
+    const part::BitV a{P<uint32_t>(a_ok->words), a_ok->full ? 1 : 0}, b{P<uint32_t>(b_ok->words), b_ok->full ? 1 : 0},
+        c{P<uint32_t>(c_ok->words), c_ok->full ? 1 : 0};
+    hipStream_t st = s->stream;
+    const int nb = (int)((n + (int64_t(1) << kBits) - 1) >> kBits);
+    REQUIRE(nb >= 1 && nb <= kMaxBuckets, CAPSMI_ERR_INTERNAL, "count(*) records: domain too large");
+    Buf inA = dev_alloc(sizeof(uint32_t) * (size_t)n, s);
+    Buf corr = dev_alloc(sizeof(int32_t) * (size_t)n, s);  // wrap corrections of the 16-bit LDS counters
+    Buf acc = dev_alloc(2 * sizeof(unsigned long long), s);  // loops, sum
+    HIP_CHECK(hipMemsetAsync(P<void>(inA), 0, sizeof(uint32_t) * (size_t)n, st));
+    HIP_CHECK(hipMemsetAsync(P<void>(corr), 0, sizeof(int32_t) * (size_t)n, st));
+    HIP_CHECK(hipMemsetAsync(P<void>(acc), 0, 2 * sizeof(unsigned long long), st));
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (const void* f : {reinterpret_cast<const void*>(k_rec_part<false>), reinterpret_cast<const void*>(k_rec_part<true>)})
+            HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)part_lds(kMaxBuckets)));
+        for (const void* f : {reinterpret_cast<const void*>(k_rec_walk<false>), reinterpret_cast<const void*>(k_rec_walk<true>)})
+            HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          (int)walk_lds()));
+    });
+    int64_t mtot = 0;
+    std::vector<int> g1(nt, 0);
+    std::vector<int64_t> c0(nt, 0), cpb(nt, 0);
+    int64_t pool_chunks = 0;
+    for (int i = 0; i < nt; ++i) {
+        if (ms[i] <= 0) continue;
+        mtot += ms[i];
+        g1[i] = (int)std::max<int64_t>(1, std::min<int64_t>(s->num_cus, (ms[i] + 4 * (int64_t)kT - 1) / (4 * (int64_t)kT)));
+        cpb[i] = chunks_per_block(ms[i], g1[i], nb);
+        c0[i] = pool_chunks;
+        pool_chunks += (int64_t)g1[i] * cpb[i];
+    }
+    REQUIRE(pool_chunks < (int64_t)INT32_MAX, CAPSMI_ERR_UNSUPPORTED, "relationship table too large for the count");
+    const int64_t npool = pool_chunks > 0 ? pool_chunks : 1;
+    for (int side = 0; side < 2; ++side) {
+        const bool out = side == 1;
+        ChunkPart cp;
+        cp.L.lo = lo;
+        cp.L.hi = lo + n;
+        cp.L.nt = nb;
+        {
+            KernelTimer kt(s, out ? "count_part_out" : "count_part_in", (double)mtot * 18);
+            cp.pool = dev_alloc(sizeof(uint16_t) * kCh * (size_t)npool, s);
+            cp.meta = dev_alloc(sizeof(unsigned long long) * npool, s);
+            HIP_CHECK(hipMemsetAsync(P<void>(cp.meta), 0, sizeof(unsigned long long) * npool, st));
+            for (int i = 0; i < nt; ++i) {
+                if (ms[i] <= 0) continue;
+                if (out)
+                    hipLaunchKernelGGL(k_rec_part<true>, dim3(g1[i]), dim3(kB), part_lds(nb), st, srcs[i], dsts[i], ms[i],
+                                       lo, n, nb, c, b, c, c0[i], cpb[i], P<uint16_t>(cp.pool),
+                                       P<unsigned long long>(cp.meta), P<unsigned long long>(acc));
+                else
+                    hipLaunchKernelGGL(k_rec_part<false>, dim3(g1[i]), dim3(kB), part_lds(nb), st, srcs[i], dsts[i], ms[i],
+                                       lo, n, nb, a, b, c, c0[i], cpb[i], P<uint16_t>(cp.pool),
+                                       P<unsigned long long>(cp.meta), P<unsigned long long>(acc));
+            }
+            HIP_CHECK(hipGetLastError());
+        }
+        chunk_order(s, nb, pool_chunks, s->num_cus, cp);
+        KernelTimer kt(s, out ? "count_out" : "count_in", (double)mtot * 2 + (double)n * (out ? 8 : 4));
+        const size_t wl = walk_lds();
+        if (out)
+            hipLaunchKernelGGL(k_rec_walk<true>, dim3((unsigned)cp.g2), dim3(kB), wl, st, P<uint16_t>(cp.pool),
+                               P<unsigned long long>(cp.meta), cp.order, cp.jst, nb, n, b, P<uint32_t>(inA),
+                               P<int32_t>(corr), P<unsigned long long>(acc) + 1);
+        else
+            hipLaunchKernelGGL(k_rec_walk<false>, dim3((unsigned)cp.g2), dim3(kB), wl, st, P<uint16_t>(cp.pool),
+                               P<unsigned long long>(cp.meta), cp.order, cp.jst, nb, n, b, P<uint32_t>(inA),
+                               P<int32_t>(corr), P<unsigned long long>(acc) + 1);
+        HIP_CHECK(hipGetLastError());
+    }
+    unsigned long long h[2];
+    HIP_CHECK(hipMemcpyAsync(h, P<void>(acc), sizeof(h), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    return (int64_t)(h[1] - h[0]);
+}
 
 // count(*) of the 2-hop chain over relationship tables (srcs[i], dsts[i], ms[i]); the three node
 // bitmaps share one id domain of at most 2^26 ids (<= 2048 slices).  Returns the count.

@@ -877,9 +877,18 @@ void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_
                                P<unsigned long long>(cp.meta), P<uint32_t>(cp.chist));
     }
     HIP_CHECK(hipGetLastError());
+    cp.mtot = mtot;
+    chunk_order(s, L.nt, pool_chunks, g2_want, cp);
+}
 
-    // used chunks ordered by target slice; pass-2 segments and the exact output offset of every
-    // (segment, source cell); no host round trip until the layout is written
+// used chunks (cp.meta: slice, fill) ordered by target slice and the block-balanced segment split
+// of a consumer grid of g2 blocks; no host round trip
+void chunk_order(capsmi_session* s, int nt, int64_t pool_chunks, int64_t g2_want, ChunkPart& cp) {
+    using namespace part;
+    hipStream_t st = s->stream;
+    Layout L = cp.L;
+    L.nt = nt;
+    const int64_t npool = pool_chunks > 0 ? pool_chunks : 1;
     const int64_t g2 = std::max<int64_t>(1, std::min<int64_t>(g2_want, npool));
     cp.jbuf = dev_alloc(sizeof(int64_t) * (3 * (size_t)L.nt + 2 * (size_t)g2 + 3) + sizeof(uint32_t) * npool +
                              sizeof(int) * g2, s);
@@ -904,7 +913,6 @@ void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_
     HIP_CHECK(hipGetLastError());
     cp.pool_chunks = pool_chunks;
     cp.npool = npool;
-    cp.mtot = mtot;
     cp.g2 = g2;
     cp.jst = jst;
     cp.segbase = segbase;

@@ -306,5 +306,7 @@ struct ChunkPart {
 };
 void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
                      int nt, bool swap, const part::Layout& L, int64_t g2, ChunkPart& cp);
+// the ordering half of chunk_partition for a pool another kernel filled (cp.meta: bucket | fill << 32)
+void chunk_order(capsmi_session* s, int nt, int64_t pool_chunks, int64_t g2, ChunkPart& cp);
 
 }  // namespace capsmi

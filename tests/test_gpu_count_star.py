@@ -1,6 +1,6 @@
-"""2-hop count(*) (capsmi_two_hop_count) in both forms against the closed form of oracle/closed.c:
-the two chunked partitions with LDS slice counts (default) and the per-relationship atomics
-(CAPSMI_COUNT=atomic).  The closed form itself is pinned against binding enumeration in
+"""2-hop count(*) (capsmi_two_hop_count) in every form against the closed form of oracle/closed.c:
+the two partitions of 2-byte records (default), the two chunked pair partitions with LDS slice counts
+(CAPSMI_COUNT=pairs) and the per-relationship atomics (CAPSMI_COUNT=atomic).  The closed form itself is pinned against binding enumeration in
 tests/test_oracle*.py."""
 import numpy as np
 import pytest
@@ -9,11 +9,11 @@ from oracle import cpu
 
 pytestmark = pytest.mark.gpu
 
-MODES = ["part", "atomic"]
+MODES = ["rec", "pairs", "atomic"]
 
 
 def _mode(monkeypatch, mode):
-    if mode != "part":
+    if mode != "rec":
         monkeypatch.setenv("CAPSMI_COUNT", mode)
 
 
@@ -73,7 +73,7 @@ def test_hub_slices_and_split_walks(session, monkeypatch, mode):
     assert graph.two_hop_count(session, [t1, t2], _bm(session, n, a), _bm(session, n, b), _bm(session, n, c)) == rows
 
 
-@pytest.mark.parametrize("mode", ["part"])
+@pytest.mark.parametrize("mode", ["rec", "pairs"])
 @pytest.mark.parametrize("scale,kind", [(12, "person"), (16, "all"), (17, "person")])
 def test_rmat(session, monkeypatch, mode, scale, kind):
     from capsmi import graph
@@ -84,3 +84,25 @@ def test_rmat(session, monkeypatch, mode, scale, kind):
     rows, _ = cpu.two_hop_closed_form(n, src, dst, mask, mask, mask)
     bm = _bm(session, n, mask)
     assert graph.two_hop_count(session, [_rels(session, src, dst)], bm, bm, bm) == rows
+
+
+@pytest.mark.parametrize("mode", ["rec", "pairs"])
+def test_dense_buckets_roll_chunks(session, monkeypatch, mode):
+    """3M relationships into three 2^16-id buckets: every partition block fills several chunks of one
+    bucket (chunk rollover inside a tile, pieces split across chunks), plus a ragged tail and
+    in-degrees far above 2^16 for a few ids."""
+    from capsmi import graph
+    _mode(monkeypatch, mode)
+    rng = np.random.default_rng(23)
+    n = 1 << 20
+    m = 3_000_001
+    src = rng.integers(0, n, m)
+    dst = rng.integers(0, 3 << 16, m)
+    dst[: 300_000] = 12345  # one id with 300k in-edges
+    src[300_000: 400_000] = 777  # and one with 100k out-edges
+    a = (rng.random(n) < 0.95).astype(np.uint8)
+    ones = np.ones(n, np.uint8)
+    rows, _ = cpu.two_hop_closed_form(n, src.astype(np.int64), dst.astype(np.int64), a, ones, ones)
+    got = graph.two_hop_count(session, [_rels(session, src.astype(np.int64), dst.astype(np.int64))], _bm(session, n, a),
+                              _bm(session, n, ones), _bm(session, n, ones))
+    assert got == rows
