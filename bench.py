@@ -43,11 +43,12 @@ C3_QUERY = {"clauses": [{"match": "(a:Person)-[:FRIEND_OF]->(b:Person)-[:FRIEND_
             "return": {"items": [["count(DISTINCT c)", ["count_distinct", ["id", "c"]]]]}}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 KERNELS = ("part_scatter1", "part_scatter2_hop1", "part_scatter2", "hop1", "hop2", "mid_combine", "bitmap_add",
-           "count_part_in", "count_in", "count_part_out", "count_out", "degrees")
+           "count_part", "count_part_in", "count_in", "count_part_out", "count_out", "degrees")
 # timer name -> kernel name as rocprofv3 reports it (hop1 and hop2 are two instances of k_hop_2d)
 KERNEL_SYMBOL = {"part_scatter1": "k_scatter_l", "part_scatter2_hop1": "k_scatter_s2", "part_scatter2": "k_scatter_s2",
                  "hop1": "k_hop_2d", "hop2": "k_hop_2d", "mid_combine": "k_mid_combine", "bitmap_add": "k_bitmap_add",
-                 "count_part_in": "k_rec_part", "count_part_out": "k_rec_part", "count_in": "k_rec_walk",
+                 "count_part": "k_rec_part", "count_part_in": "k_scatter_c", "count_part_out": "k_scatter_c",
+                 "count_in": "k_rec_walk",
                  "count_out": "k_rec_walk", "degrees": "k_degrees"}
 
 
@@ -425,7 +426,8 @@ def main():
                "hop1": m_local * 8 + n // 8,         # read uint2 pairs, write M
                "hop2": m_local * 8 + n // 8 * 3,     # read uint2 pairs + X1 + X2, write C
                "mid_combine": n // 8 * 5, "bitmap_add": n * 8,
-               "count_part_in": m_local * 18, "count_part_out": m_local * 18,  # read 2 x int64, write a 2-B record
+               "count_part": m_local * 20,  # read 2 x int64, write two 2-byte records
+               "count_part_in": m_local * 24, "count_part_out": m_local * 24,  # pair partition (CAPSMI_COUNT=pairs)
                "degrees": m_local * 16 + n * 8}                  # read int64 pairs, inA + outC
         alg.update(kbytes)
         timed = {k: (c, ms) for k, (c, ms) in kt.items() if c > 0}

@@ -110,9 +110,9 @@ constexpr int kBits = 16;        // ids per bucket
 constexpr int kB = 1024;         // workgroup
 constexpr int kIT = 8;           // relationships per lane per tile
 constexpr int kT = kB * kIT;     // relationships per tile
-constexpr int kPiece = 32;       // records per 64-byte store
-constexpr int kCh = 16384;       // records per chunk (32 KiB; a tile adds <= 257 pieces of its 512)
-constexpr int kMaxBuckets = 1024;
+constexpr int kPiece = 16;       // records per 32-byte store
+constexpr int kCh = 8192;        // records per chunk (16 KiB; one 16-byte load per walk lane)
+constexpr int kMaxBuckets = 1024;  // per side
 constexpr int kWalkG = 4;        // chunks in flight per walk block
 constexpr int kInfo = 2048;      // chunk ids staged in LDS per walk block
 constexpr int kBig = 255;        // OUT walk: values >= 0xFF00 per bucket kept exactly in LDS
@@ -121,45 +121,48 @@ constexpr size_t walk_lds() {
 }
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
-__host__ __device__ constexpr size_t part_lds(int nb) {
-    return sizeof(uint16_t) * ((size_t)kT + (size_t)nb * kPiece) + sizeof(uint32_t) * (8 * (size_t)nb + kB / 64 + 4);
+// nb2 = buckets of both sides
+__host__ __device__ constexpr size_t part_lds(int nb2) {
+    return sizeof(uint16_t) * (2 * (size_t)kT + (size_t)nb2 * kPiece) + sizeof(uint16_t) * 2 * (size_t)nb2 +
+           sizeof(uint32_t) * (6 * (size_t)nb2 + kB / 64 + 4);
 }
 
-__host__ __device__ constexpr int64_t chunks_per_block(int64_t m, int64_t grid, int nb) {
-    // full chunks, plus per bucket the open one and one retired part-full by the final flush
-    return (((m + kT - 1) / kT + grid - 1) / grid * kT + kCh - 1) / kCh + 2 * (int64_t)nb + 1;
+__host__ __device__ constexpr int64_t chunks_per_block(int64_t m, int64_t grid, int nb2) {
+    // full chunks of the block's records (two per relationship at most), plus per bucket the open
+    // one and one retired part-full by the final flush
+    return ((((m + kT - 1) / kT + grid - 1) / grid) * 2 * kT + kCh - 1) / kCh + 2 * (int64_t)nb2 + 1;
 }
 
 __device__ __forceinline__ bool bit(const part::BitV& v, uint64_t x) { return v.full || part::gbit(v.w, (uint32_t)x); }
 
-// OUT = false: records of targets (bucket = target >> 16) of relationships with a_ok(source); the
-// a_ok, b_ok, c_ok self-loops are counted into `loops`.  OUT = true: records of sources of
-// relationships with c_ok(target).  `f` is a_ok / c_ok.
-template <bool OUT>
+// One read of the relationships, two record kinds into 2 * nb buckets:
+//   bucket t >> 16        (the in side):  t & 0xFFFF for relationships s -> t with a_ok(s);
+//   bucket nb + (s >> 16) (the out side): s & 0xFFFF for relationships s -> t with c_ok(t);
+// the a_ok, b_ok, c_ok self-loops are counted into `loops`.
 __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
-                                                 int64_t m, int64_t lo, int64_t range, int nb, part::BitV f, part::BitV b,
+                                                 int64_t m, int64_t lo, int64_t range, int nb, part::BitV a, part::BitV b,
                                                  part::BitV c, int64_t chunk0, int64_t cpb, uint16_t* __restrict__ pool,
                                                  unsigned long long* __restrict__ cmeta,
                                                  unsigned long long* __restrict__ loops) {
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
-    uint16_t* stage = reinterpret_cast<uint16_t*>(sm);  // kT: this tile's records grouped by bucket
-    uint16_t* hold = stage + kT;                         // nb x kPiece: records held back per bucket
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(hold + (size_t)nb * kPiece);  // run length this tile
-    uint32_t* loc = cnt + nb;  // run start in the stage
-    uint32_t* hc = loc + nb;   // records held (< kPiece)
-    uint32_t* fl = hc + nb;    // records stored in the open chunk (a multiple of kPiece)
-    uint32_t* ph = fl + nb;    // open chunk
-    uint32_t* np = ph + nb;    // chunk opened for this tile's overflow
-    uint32_t* pc = np + nb;    // pieces stored this tile
-    uint32_t* pb = pc + nb;    // first piece of the bucket this tile
-    uint32_t* wtot = pb + nb;
+    const int nb2 = 2 * nb;
+    uint16_t* stage = reinterpret_cast<uint16_t*>(sm);  // 2 kT: this tile's records grouped by bucket
+    uint16_t* hold = stage + 2 * kT;                     // nb2 x kPiece: records held back per bucket
+    uint16_t* hc = hold + (size_t)nb2 * kPiece;          // records held (< kPiece)
+    uint16_t* fl = hc + nb2;                             // records stored in the open chunk (kCh: none open)
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(fl + nb2);  // run length this tile
+    uint32_t* loc = cnt + nb2;  // run start in the stage
+    uint32_t* ph = loc + nb2;   // open chunk
+    uint32_t* np = ph + nb2;    // first of the chunks opened for this tile's pieces (consecutive)
+    uint32_t* pc = np + nb2;    // pieces stored this tile
+    uint32_t* pb = pc + nb2;    // first piece of the bucket this tile
+    uint32_t* wtot = pb + nb2;
     uint32_t* misc = wtot + kB / 64;  // [0] next free chunk of this block
-    for (int i = threadIdx.x; i < nb; i += kB) {
+    for (int i = threadIdx.x; i < nb2; i += kB) {
         cnt[i] = 0;
         hc[i] = 0;
-        fl[i] = 0;
+        fl[i] = (uint16_t)kCh;
         ph[i] = kNone;
-        np[i] = kNone;
     }
     if (threadIdx.x == 0) misc[0] = (uint32_t)(chunk0 + (int64_t)blockIdx.x * cpb);
     const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
@@ -170,48 +173,47 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
     if (t0 < m) part::load_tile<kB>(src, dst, t0, m, vec, sr, tr);
     __syncthreads();
     for (; t0 < m; t0 += stride) {  // block-uniform
-        uint32_t key[kIT], rk[kIT];
-        uint32_t valid = 0;
+        uint32_t xs[kIT], ys[kIT], rin[kIT], rout[kIT];
+        uint32_t vin = 0, vout = 0;
 #pragma unroll
         for (int u = 0; u < kIT; ++u) {
             const int64_t e = t0 + part::item_off<kB>(u);
             const uint64_t x = (uint64_t)(sr[u] - lo), y = (uint64_t)(tr[u] - lo);
-            bool ok = e < m && x < (uint64_t)range && y < (uint64_t)range;
-            if (OUT) {
-                ok = ok && bit(f, y);
-            } else {
-                ok = ok && bit(f, x);
-                if (ok && x == y && bit(b, x) && bit(c, x)) ++nl;
-            }
-            key[u] = (uint32_t)(OUT ? x : y);
-            valid |= (ok ? 1u : 0u) << u;
+            const bool ok = e < m && x < (uint64_t)range && y < (uint64_t)range;
+            const bool ain = ok && bit(a, x), aout = ok && bit(c, y);
+            if (ain && x == y && bit(b, x) && bit(c, x)) ++nl;
+            xs[u] = (uint32_t)x;
+            ys[u] = (uint32_t)y;
+            vin |= (ain ? 1u : 0u) << u;
+            vout |= (aout ? 1u : 0u) << u;
         }
         if (t0 + stride < m) part::load_tile<kB>(src, dst, t0 + stride, m, vec, sr, tr);  // prefetch
 #pragma unroll
-        for (int u = 0; u < kIT; ++u) rk[u] = ((valid >> u) & 1u) ? atomicAdd(&cnt[key[u] >> kBits], 1u) : 0u;
+        for (int u = 0; u < kIT; ++u) {
+            rin[u] = ((vin >> u) & 1u) ? atomicAdd(&cnt[ys[u] >> kBits], 1u) : 0u;
+            rout[u] = ((vout >> u) & 1u) ? atomicAdd(&cnt[nb + (xs[u] >> kBits)], 1u) : 0u;
+        }
         __syncthreads();
-        (void)part::block_exclusive_scan<kB>(cnt, loc, nb, wtot);
+        (void)part::block_exclusive_scan<kB>(cnt, loc, nb2, wtot);
 #pragma unroll
-        for (int u = 0; u < kIT; ++u)
-            if ((valid >> u) & 1u) stage[loc[key[u] >> kBits] + rk[u]] = (uint16_t)(key[u] & 0xFFFFu);
-        for (int i = threadIdx.x; i < nb; i += kB) {  // pieces of the held + run sequence; chunks they open
-            const uint32_t npc = (hc[i] + cnt[i]) / kPiece;
+        for (int u = 0; u < kIT; ++u) {
+            if ((vin >> u) & 1u) stage[loc[ys[u] >> kBits] + rin[u]] = (uint16_t)(ys[u] & 0xFFFFu);
+            if ((vout >> u) & 1u) stage[loc[nb + (xs[u] >> kBits)] + rout[u]] = (uint16_t)(xs[u] & 0xFFFFu);
+        }
+        for (int i = threadIdx.x; i < nb2; i += kB) {  // pieces of the held + run sequence; chunks they open
+            const uint32_t npc = ((uint32_t)hc[i] + cnt[i]) / kPiece;
             pc[i] = npc;
-            if (npc) {
-                if (ph[i] == kNone) {
-                    ph[i] = atomicAdd(&misc[0], 1u);
-                    fl[i] = 0;
-                } else if (fl[i] + npc * kPiece > (uint32_t)kCh) {
-                    np[i] = atomicAdd(&misc[0], 1u);
-                }
+            if (npc) {  // pieces take positions [fl, fl + npc * kPiece): chunk index pos / kCh past ph
+                const uint32_t nnew = ((uint32_t)fl[i] + npc * kPiece - 1) / kCh;
+                if (nnew) np[i] = atomicAdd(&misc[0], nnew);
             }
         }
         __syncthreads();
-        const uint32_t P = part::block_exclusive_scan<kB>(pc, pb, nb, wtot);
-        // piece g: 4 lanes x 8 records; element e < held comes from the hold, the rest from the run
-        for (uint32_t x = threadIdx.x; x < P * 4; x += kB) {
-            const uint32_t g = x >> 2, r = x & 3;
-            int lo_b = 0, hi_b = nb;  // last bucket with pb <= g (empty buckets share pb with the next)
+        const uint32_t P = part::block_exclusive_scan<kB>(pc, pb, nb2, wtot);
+        // piece g: 2 lanes x 8 records; element e < held comes from the hold, the rest from the run
+        for (uint32_t x = threadIdx.x; x < P * 2; x += kB) {
+            const uint32_t g = x >> 1, r = x & 1;
+            int lo_b = 0, hi_b = nb2;  // last bucket with pb <= g (empty buckets share pb with the next)
             while (hi_b - lo_b > 1) {
                 const int mid = (lo_b + hi_b) >> 1;
                 if (pb[mid] <= g) lo_b = mid; else hi_b = mid;
@@ -225,9 +227,9 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
                 const uint32_t e = k * kPiece + r * 8 + (uint32_t)q;
                 v[q] = e < h ? hold[bk * kPiece + (int)e] : stage[loc[bk] + e - h];
             }
-            const uint32_t pos = fl[bk] + k * kPiece;
-            const uint32_t ch = pos < (uint32_t)kCh ? ph[bk] : np[bk];
-            const uint32_t off = (pos < (uint32_t)kCh ? pos : pos - (uint32_t)kCh) + r * 8;
+            const uint32_t pos = (uint32_t)fl[bk] + k * kPiece, ci = pos / kCh;
+            const uint32_t ch = ci == 0 ? ph[bk] : np[bk] + ci - 1;
+            const uint32_t off = pos - ci * kCh + r * 8;
             uint4 w;
             w.x = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
             w.y = (uint32_t)v[2] | ((uint32_t)v[3] << 16);
@@ -238,44 +240,50 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < kIT; ++u) {  // the new held records: the run's items past its last whole piece
-            if ((valid >> u) & 1u) {
-                const uint32_t bk = key[u] >> kBits, e = hc[bk] + rk[u], cut = pc[bk] * kPiece;
-                if (e >= cut) hold[bk * kPiece + (e - cut)] = (uint16_t)(key[u] & 0xFFFFu);
+            if ((vin >> u) & 1u) {
+                const uint32_t bk = ys[u] >> kBits, e = hc[bk] + rin[u], cut = pc[bk] * kPiece;
+                if (e >= cut) hold[bk * kPiece + (e - cut)] = (uint16_t)(ys[u] & 0xFFFFu);
+            }
+            if ((vout >> u) & 1u) {
+                const uint32_t bk = nb + (xs[u] >> kBits), e = hc[bk] + rout[u], cut = pc[bk] * kPiece;
+                if (e >= cut) hold[bk * kPiece + (e - cut)] = (uint16_t)(xs[u] & 0xFFFFu);
             }
         }
         __syncthreads();
-        for (int i = threadIdx.x; i < nb; i += kB) {
-            const uint32_t tot = hc[i] + cnt[i], npc = pc[i];
-            const uint32_t end = fl[i] + npc * kPiece;
-            if (np[i] != kNone) {  // the open chunk is full: retire it
-                cmeta[ph[i]] = part::chunk_meta(i, (uint32_t)kCh);
-                ph[i] = np[i];
-                np[i] = kNone;
-                fl[i] = end - (uint32_t)kCh;
-            } else {
-                fl[i] = end;
+        for (int i = threadIdx.x; i < nb2; i += kB) {
+            const uint32_t tot = (uint32_t)hc[i] + cnt[i], npc = pc[i];
+            if (npc) {
+                const uint32_t end = (uint32_t)fl[i] + npc * kPiece, nnew = (end - 1) / kCh;
+                if (nnew) {  // the chunks filled by this tile are retired, the last one opened stays open
+                    if (ph[i] != kNone) cmeta[ph[i]] = part::chunk_meta(i, (uint32_t)kCh);
+                    for (uint32_t t = 0; t + 1 < nnew; ++t) cmeta[np[i] + t] = part::chunk_meta(i, (uint32_t)kCh);
+                    ph[i] = np[i] + nnew - 1;
+                    fl[i] = (uint16_t)(end - nnew * kCh);
+                } else {
+                    fl[i] = (uint16_t)end;
+                }
             }
-            hc[i] = tot - npc * kPiece;
+            hc[i] = (uint16_t)(tot - npc * kPiece);
             cnt[i] = 0;
         }
         __syncthreads();
     }
     // the held records: into the open chunk, or a new one when there is none or it is full
-    for (int i = threadIdx.x; i < nb; i += kB) {
-        if (hc[i] && (ph[i] == kNone || fl[i] + hc[i] > (uint32_t)kCh)) {
+    for (int i = threadIdx.x; i < nb2; i += kB) {
+        if (hc[i] && (ph[i] == kNone || (uint32_t)fl[i] + hc[i] > (uint32_t)kCh)) {
             if (ph[i] != kNone) cmeta[ph[i]] = part::chunk_meta(i, fl[i]);
             ph[i] = atomicAdd(&misc[0], 1u);
             fl[i] = 0;
         }
     }
     __syncthreads();
-    for (int x = threadIdx.x; x < nb * kPiece; x += kB) {
+    for (int x = threadIdx.x; x < nb2 * kPiece; x += kB) {
         const int bk = x / kPiece, e = x % kPiece;
         if ((uint32_t)e < hc[bk]) pool[(size_t)ph[bk] * kCh + fl[bk] + (uint32_t)e] = hold[x];
     }
-    for (int i = threadIdx.x; i < nb; i += kB)
-        if (ph[i] != kNone) cmeta[ph[i]] = part::chunk_meta(i, fl[i] + hc[i]);
-    if (!OUT) cnt::block_add(nl, loops);
+    for (int i = threadIdx.x; i < nb2; i += kB)
+        if (ph[i] != kNone) cmeta[ph[i]] = part::chunk_meta(i, (uint32_t)fl[i] + hc[i]);
+    cnt::block_add(nl, loops);
 }
 
 // Walk of a record partition in bucket order, one pass per bucket: the bucket's 2^16 ids as 16-bit
@@ -298,8 +306,12 @@ __global__ void __launch_bounds__(kB) k_rec_walk(const uint16_t* __restrict__ po
     uint2* cinfo = reinterpret_cast<uint2*>(cl + kWords);  // (chunk, fill) of kInfo chunks of the share
     uint32_t* bigv = reinterpret_cast<uint32_t*>(cinfo + kInfo);  // OUT: exact values behind 0xFF00 + k
     uint32_t* nbig = bigv + kBig;
-    const part::SegSplit S(jst, nb, gridDim.x);
-    const int64_t qb = (int64_t)blockIdx.x * S.per, qe = min(qb + S.per, S.nch);
+    // jst: nb + 1 bucket starts in `order` (the side's buckets of the two-sided partition, so
+    // jst[0] need not be 0); block w takes an equal share of the side's chunks
+    const int64_t q00 = jst[0], nch = jst[nb] - q00;
+    int64_t per = (nch + gridDim.x - 1) / gridDim.x;
+    if (per < 1) per = 1;
+    const int64_t qb = q00 + (int64_t)blockIdx.x * per, qe = min(qb + per, q00 + nch);
     unsigned long long acc = 0;
     if (qb < qe) {  // block-uniform
         // the chunk ids and fills are staged in LDS kInfo at a time, so a chunk's loads wait for no
@@ -319,18 +331,15 @@ __global__ void __launch_bounds__(kB) k_rec_walk(const uint16_t* __restrict__ po
             __syncthreads();
         };
         refill(qb);
-        auto load = [&](int64_t q, uint4 (&v)[2]) -> uint32_t {
+        auto load = [&](int64_t q, uint4& v) -> uint32_t {
             if (q >= qe) return 0u;
             const uint2 ci = cinfo[q - ibase];
             const uint32_t phys = ci.x, fill = ci.y;
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                 const_cast<uint16_t*>(pool + (size_t)phys * kCh), (short)0,
                 (int)((fill * sizeof(uint16_t) + 15) & ~(size_t)15), 0x00020000);  // whole dwords: masked by `fill` below
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(k * kB + (int)threadIdx.x) * 16u, 0, 2);
-                v[k] = make_uint4(x[0], x[1], x[2], x[3]);
-            }
+            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)threadIdx.x * 16u, 0, 2);
+            v = make_uint4(x[0], x[1], x[2], x[3]);
             return fill;
         };
         auto exact = [&](int64_t x) -> uint32_t {  // OUT: the stored count of id x
@@ -376,7 +385,7 @@ __global__ void __launch_bounds__(kB) k_rec_walk(const uint16_t* __restrict__ po
         int64_t j_end = jst[cur_j + 1];
         begin(cur_j);
         __syncthreads();
-        uint4 nx[kWalkG][2];
+        uint4 nx[kWalkG];
         uint32_t nfill[kWalkG];
 #pragma unroll
         for (int g = 0; g < kWalkG; ++g) nfill[g] = load(qb + g, nx[g]);
@@ -385,7 +394,7 @@ __global__ void __launch_bounds__(kB) k_rec_walk(const uint16_t* __restrict__ po
             for (int g = 0; g < kWalkG; ++g) {  // static slots: each use waits for its own loads only
                 const int64_t q = q0 + g;
                 if (q >= qe) break;
-                const uint4 v0 = nx[g][0], v1 = nx[g][1];
+                const uint4 v0 = nx[g];
                 const uint32_t fill = nfill[g];
                 if (q + kWalkG >= iend && iend < qe) refill(q + kWalkG);  // block-uniform
                 nfill[g] = load(q + kWalkG, nx[g]);
@@ -400,22 +409,20 @@ __global__ void __launch_bounds__(kB) k_rec_walk(const uint16_t* __restrict__ po
                     cur_j = j;
                 }
                 const int64_t base = (int64_t)cur_j << kBits;
-                const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-                // all 16 LDS accesses are issued before any result is used (one wait, not 16)
-                uint32_t got[16];
+                const uint32_t w[4] = {v0.x, v0.y, v0.z, v0.w};
+                // all 8 LDS accesses are issued before any result is used
+                uint32_t got[8];
 #pragma unroll
-                for (int e = 0; e < 16; ++e) {
-                    const int k = e >> 1, h = e & 1;
-                    const uint32_t i = ((uint32_t)((k >> 2) * kB) + threadIdx.x) * 8 + (uint32_t)(k & 3) * 2 + (uint32_t)h;
-                    const uint32_t r = (w[k] >> (16 * h)) & 0xFFFFu;
+                for (int e = 0; e < 8; ++e) {
+                    const uint32_t i = threadIdx.x * 8 + (uint32_t)e;
+                    const uint32_t r = (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
                     got[e] = 0u;
                     if (i < fill) got[e] = OUT ? cl[r >> 1] : atomicAdd(&cl[r >> 1], 1u << ((r & 1u) * 16u));
                 }
 #pragma unroll
-                for (int e = 0; e < 16; ++e) {
-                    const int k = e >> 1, h = e & 1;
-                    const uint32_t i = ((uint32_t)((k >> 2) * kB) + threadIdx.x) * 8 + (uint32_t)(k & 3) * 2 + (uint32_t)h;
-                    const uint32_t r = (w[k] >> (16 * h)) & 0xFFFFu, sh = (r & 1u) * 16u;
+                for (int e = 0; e < 8; ++e) {
+                    const uint32_t i = threadIdx.x * 8 + (uint32_t)e;
+                    const uint32_t r = (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu, sh = (r & 1u) * 16u;
                     if (i >= fill) continue;
                     if (OUT) {
                         const uint32_t v = (got[e] >> sh) & 0xFFFFu;
@@ -459,8 +466,8 @@ int64_t two_hop_count_rec(capsmi_session* s, const int64_t* const* srcs, const i
     HIP_CHECK(hipMemsetAsync(P<void>(acc), 0, 2 * sizeof(unsigned long long), st));
     static std::once_flag once;
     std::call_once(once, [] {
-        for (const void* f : {reinterpret_cast<const void*>(k_rec_part<false>), reinterpret_cast<const void*>(k_rec_part<true>)})
-            HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)part_lds(kMaxBuckets)));
+        HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_rec_part), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)part_lds(2 * kMaxBuckets)));
         for (const void* f : {reinterpret_cast<const void*>(k_rec_walk<false>), reinterpret_cast<const void*>(k_rec_walk<true>)})
             HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)walk_lds()));
@@ -473,47 +480,44 @@ int64_t two_hop_count_rec(capsmi_session* s, const int64_t* const* srcs, const i
         if (ms[i] <= 0) continue;
         mtot += ms[i];
         g1[i] = (int)std::max<int64_t>(1, std::min<int64_t>(s->num_cus, (ms[i] + 4 * (int64_t)kT - 1) / (4 * (int64_t)kT)));
-        cpb[i] = chunks_per_block(ms[i], g1[i], nb);
+        cpb[i] = chunks_per_block(ms[i], g1[i], 2 * nb);
         c0[i] = pool_chunks;
         pool_chunks += (int64_t)g1[i] * cpb[i];
     }
     REQUIRE(pool_chunks < (int64_t)INT32_MAX, CAPSMI_ERR_UNSUPPORTED, "relationship table too large for the count");
     const int64_t npool = pool_chunks > 0 ? pool_chunks : 1;
-    for (int side = 0; side < 2; ++side) {
-        const bool out = side == 1;
-        ChunkPart cp;
-        cp.L.lo = lo;
-        cp.L.hi = lo + n;
-        cp.L.nt = nb;
-        {
-            KernelTimer kt(s, out ? "count_part_out" : "count_part_in", (double)mtot * 18);
-            cp.pool = dev_alloc(sizeof(uint16_t) * kCh * (size_t)npool, s);
-            cp.meta = dev_alloc(sizeof(unsigned long long) * npool, s);
-            HIP_CHECK(hipMemsetAsync(P<void>(cp.meta), 0, sizeof(unsigned long long) * npool, st));
-            for (int i = 0; i < nt; ++i) {
-                if (ms[i] <= 0) continue;
-                if (out)
-                    hipLaunchKernelGGL(k_rec_part<true>, dim3(g1[i]), dim3(kB), part_lds(nb), st, srcs[i], dsts[i], ms[i],
-                                       lo, n, nb, c, b, c, c0[i], cpb[i], P<uint16_t>(cp.pool),
-                                       P<unsigned long long>(cp.meta), P<unsigned long long>(acc));
-                else
-                    hipLaunchKernelGGL(k_rec_part<false>, dim3(g1[i]), dim3(kB), part_lds(nb), st, srcs[i], dsts[i], ms[i],
-                                       lo, n, nb, a, b, c, c0[i], cpb[i], P<uint16_t>(cp.pool),
-                                       P<unsigned long long>(cp.meta), P<unsigned long long>(acc));
-            }
-            HIP_CHECK(hipGetLastError());
+    ChunkPart cp;
+    cp.L.lo = lo;
+    cp.L.hi = lo + n;
+    cp.L.nt = 2 * nb;
+    {
+        KernelTimer kt(s, "count_part", (double)mtot * 20);  // read 2 x int64, write two 2-byte records
+        cp.pool = dev_alloc(sizeof(uint16_t) * kCh * (size_t)npool, s);
+        cp.meta = dev_alloc(sizeof(unsigned long long) * npool, s);
+        HIP_CHECK(hipMemsetAsync(P<void>(cp.meta), 0, sizeof(unsigned long long) * npool, st));
+        for (int i = 0; i < nt; ++i) {
+            if (ms[i] <= 0) continue;
+            hipLaunchKernelGGL(k_rec_part, dim3(g1[i]), dim3(kB), part_lds(2 * nb), st, srcs[i], dsts[i], ms[i], lo, n, nb, a,
+                               b, c, c0[i], cpb[i], P<uint16_t>(cp.pool), P<unsigned long long>(cp.meta),
+                               P<unsigned long long>(acc));
         }
-        chunk_order(s, nb, pool_chunks, s->num_cus, cp);
-        KernelTimer kt(s, out ? "count_out" : "count_in", (double)mtot * 2 + (double)n * (out ? 8 : 4));
-        const size_t wl = walk_lds();
-        if (out)
-            hipLaunchKernelGGL(k_rec_walk<true>, dim3((unsigned)cp.g2), dim3(kB), wl, st, P<uint16_t>(cp.pool),
-                               P<unsigned long long>(cp.meta), cp.order, cp.jst, nb, n, b, P<uint32_t>(inA),
-                               P<int32_t>(corr), P<unsigned long long>(acc) + 1);
-        else
-            hipLaunchKernelGGL(k_rec_walk<false>, dim3((unsigned)cp.g2), dim3(kB), wl, st, P<uint16_t>(cp.pool),
-                               P<unsigned long long>(cp.meta), cp.order, cp.jst, nb, n, b, P<uint32_t>(inA),
-                               P<int32_t>(corr), P<unsigned long long>(acc) + 1);
+        HIP_CHECK(hipGetLastError());
+    }
+    chunk_order(s, 2 * nb, pool_chunks, s->num_cus, cp);
+    const size_t wl = walk_lds();
+    const unsigned g2 = (unsigned)s->num_cus;
+    {
+        KernelTimer kt(s, "count_in", (double)mtot * 2 + (double)n * 4);
+        hipLaunchKernelGGL(k_rec_walk<false>, dim3(g2), dim3(kB), wl, st, P<uint16_t>(cp.pool),
+                           P<unsigned long long>(cp.meta), cp.order, cp.jst, nb, n, b, P<uint32_t>(inA), P<int32_t>(corr),
+                           P<unsigned long long>(acc) + 1);
+        HIP_CHECK(hipGetLastError());
+    }
+    {
+        KernelTimer kt(s, "count_out", (double)mtot * 2 + (double)n * 8);
+        hipLaunchKernelGGL(k_rec_walk<true>, dim3(g2), dim3(kB), wl, st, P<uint16_t>(cp.pool),
+                           P<unsigned long long>(cp.meta), cp.order, cp.jst + nb, nb, n, b, P<uint32_t>(inA),
+                           P<int32_t>(corr), P<unsigned long long>(acc) + 1);
         HIP_CHECK(hipGetLastError());
     }
     unsigned long long h[2];
