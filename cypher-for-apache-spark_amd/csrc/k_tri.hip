@@ -234,11 +234,22 @@ __device__ __forceinline__ uint32_t fold24(uint32_t w) { return (w ^ (w >> 24)) 
 __device__ __forceinline__ uint32_t mul24(uint32_t a, uint32_t b) { return a * b; }
 __device__ __forceinline__ uint32_t hslot(uint32_t w, int log2cap) { return mul24(fold24(w), 0x9E3779u) >> (32 - log2cap); }
 
+#ifndef CAPSMI_TRI_IDBLOOM
+#define CAPSMI_TRI_IDBLOOM 1
+#endif
+
 // One-bit pre-filter in front of each hash: a wave's probe loop runs as long as its longest
 // chain, so most wedges (misses) are rejected with one LDS read instead.
 constexpr int kSmallBloomBits = 10, kBigBloomBits = 16;
 
-__device__ __forceinline__ uint32_t bbit(uint32_t w, int bits) { return mul24(fold24(w), 0xC2B2AFu) >> (32 - bits); }
+// CAPSMI_TRI_IDBLOOM: the filter bit is the id's low bits.  Ids are in degree order (hubs first): a
+// hub list's entries are small ids, exact under 2^bits, and other ids' low bits spread like a
+// hash's, so the filter passes no more than before while every probe saves the fold and the
+// multiply.  (The hash slot keeps the multiplicative hash: with linear probing, runs of
+// consecutive ids would form long clusters.)
+__device__ __forceinline__ uint32_t bbit(uint32_t w, int bits) {
+    return CAPSMI_TRI_IDBLOOM ? (w & ((1u << bits) - 1)) : mul24(fold24(w), 0xC2B2AFu) >> (32 - bits);
+}
 
 __device__ __forceinline__ void bset(uint32_t* bf, int bits, uint32_t w) {
     const uint32_t x = bbit(w, bits);
