@@ -122,9 +122,12 @@ constexpr size_t walk_lds() {
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 // nb2 = buckets of both sides
+// pieces of one tile: (held + run records) / kPiece summed over the buckets
+__host__ __device__ constexpr int max_pieces(int nb2) { return (2 * kT + nb2 * (kPiece - 1)) / kPiece; }
+
 __host__ __device__ constexpr size_t part_lds(int nb2) {
     return sizeof(uint16_t) * (2 * (size_t)kT + (size_t)nb2 * kPiece) + sizeof(uint16_t) * 2 * (size_t)nb2 +
-           sizeof(uint32_t) * (6 * (size_t)nb2 + kB / 64 + 4);
+           sizeof(uint32_t) * (6 * (size_t)nb2 + kB / 64 + 4) + sizeof(uint16_t) * (size_t)max_pieces(nb2);
 }
 
 __host__ __device__ constexpr int64_t chunks_per_block(int64_t m, int64_t grid, int nb2) {
@@ -158,6 +161,7 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
     uint32_t* pb = pc + nb2;    // first piece of the bucket this tile
     uint32_t* wtot = pb + nb2;
     uint32_t* misc = wtot + kB / 64;  // [0] next free chunk of this block
+    uint16_t* owner = reinterpret_cast<uint16_t*>(misc + 4);  // bucket of each piece of the tile
     for (int i = threadIdx.x; i < nb2; i += kB) {
         cnt[i] = 0;
         hc[i] = 0;
@@ -210,16 +214,13 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
         }
         __syncthreads();
         const uint32_t P = part::block_exclusive_scan<kB>(pc, pb, nb2, wtot);
+        for (int i = threadIdx.x; i < nb2; i += kB)  // piece -> bucket
+            for (uint32_t k = 0; k < pc[i]; ++k) owner[pb[i] + k] = (uint16_t)i;
+        __syncthreads();
         // piece g: 2 lanes x 8 records; element e < held comes from the hold, the rest from the run
         for (uint32_t x = threadIdx.x; x < P * 2; x += kB) {
             const uint32_t g = x >> 1, r = x & 1;
-            int lo_b = 0, hi_b = nb2;  // last bucket with pb <= g (empty buckets share pb with the next)
-            while (hi_b - lo_b > 1) {
-                const int mid = (lo_b + hi_b) >> 1;
-                if (pb[mid] <= g) lo_b = mid; else hi_b = mid;
-            }
-            int bk = lo_b;
-            while (pc[bk] == 0 || pb[bk] + pc[bk] <= g) ++bk;
+            const int bk = owner[g];
             const uint32_t k = g - pb[bk], h = hc[bk];
             uint16_t v[8];
 #pragma unroll

@@ -15,7 +15,7 @@ def _order(session, values, ty, desc=False):
     return np.asarray(t.orderBy(("k", "desc" if desc else "asc")).column("i").values, dtype=np.int64)
 
 
-@pytest.mark.parametrize("n", [1, 7, 4095, 4096, 4097, 100_003, 1 << 20])
+@pytest.mark.parametrize("n", [1, 7, 4095, 4096, 4097, 100_003, 1 << 20, 1024 * 12288 + 12289])  # last: 12288-key tiles
 def test_order_by_is_stable_argsort(session, n):
     from capsmi.expr import I64
     rng = np.random.default_rng(n)
