@@ -265,7 +265,8 @@ def main():
     recv = torch.empty(world * 2, k_own, dtype=torch.int32, device="cuda")  # rank-major (rank, X1|X2) rows
     nsend = torch.empty(k_own, dtype=torch.int32, device="cuda")
     nrecv = torch.empty(world * k_own, dtype=torch.int32, device="cuda")
-    flag = torch.ones(1, dtype=torch.int32, device="cuda")
+    scan_stats = torch.zeros(2, dtype=torch.int64, device="cuda")  # (owned set bits, duplicate flag), summed
+    cnt_dev = torch.zeros(1, dtype=torch.int64, device="cuda")
 
     def node_scan():
         """The :Person scan (a, b, c).  N > 1: every rank scans its owned rows into its slice of the
@@ -273,12 +274,15 @@ def main():
         p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")
         if not distributed:
             return p
+        bits, uniq = p.stats()  # this rank's owned rows (known on the host after the scan)
         p.copy_words(wb, we, nsend.data_ptr(), to_bitmap=False)
         dist.all_gather_into_tensor(nrecv, nsend)
         p.copy_words(0, nw, nrecv.data_ptr(), to_bitmap=True)
-        flag.fill_(1 if p.stats()[1] else 0)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        return p.refresh(bool(flag.item()))
+        scan_stats[0].fill_(bits)
+        scan_stats[1].fill_(0 if uniq else 1)
+        dist.all_reduce(scan_stats)  # the gathered bitmap's set bits and any duplicate, in one collective
+        total_bits, dups = scan_stats.tolist()  # the step's one host round trip before the partition
+        return p.assume(total_bits, dups == 0)
 
     def exchange_and_finish(p, mark_dst):
         if distributed:  # hop-1 frontier: every rank needs X1/X2 of every middle node; one all-gather
@@ -286,12 +290,11 @@ def main():
             dist.all_gather_into_tensor(recv, send)
             mid.view(2, world, k_own).copy_(recv.view(world, 2, k_own).transpose(0, 1))
         mark_dst(p)
-        local_cnt = graph.words_popcount(sess, dstw.data_ptr(), wb, we)
-        if distributed:
-            t = torch.tensor([local_cnt], dtype=torch.int64, device="cuda")
-            dist.all_reduce(t)
-            return int(t.item())
-        return local_cnt
+        if distributed:  # owned popcount on the device, summed by the all-reduce: one host read
+            graph.words_popcount_device(sess, dstw.data_ptr(), wb, we, cnt_dev.data_ptr())
+            dist.all_reduce(cnt_dev)
+            return int(cnt_dev.item())
+        return graph.words_popcount(sess, dstw.data_ptr(), wb, we)
 
     def step_cold():
         p = node_scan()  # node scan of :Person (a, b, c)

@@ -131,6 +131,7 @@ _SIGS = {
     "capsmi_bitmap_release": (c_int32, [P]),
     "capsmi_bitmap_words": (c_int32, [P, PP, POINTER(c_int64)]),
     "capsmi_bitmap_refresh": (c_int32, [P, c_int32]),
+    "capsmi_bitmap_assume": (c_int32, [P, c_int64, c_int32]),
     "capsmi_bitmap_copy_words": (c_int32, [P, c_int64, c_int64, c_void_p, c_int32]),
     "capsmi_expand_filter": (c_int32, [P, P, c_char_p, c_char_p, P, P, c_int32, STRS, STRS, PP]),
     "capsmi_two_hop_count_distinct": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, P, P, POINTER(c_int64)]),
@@ -138,6 +139,7 @@ _SIGS = {
     "capsmi_two_hop_mark_mid": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, P, c_void_p, c_void_p]),
     "capsmi_two_hop_mark_dst": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, P, c_void_p, c_void_p]),
     "capsmi_words_popcount": (c_int32, [P, c_void_p, c_int64, c_int64, POINTER(c_int64)]),
+    "capsmi_words_popcount_device": (c_int32, [P, c_void_p, c_int64, c_int64, c_void_p]),
     "capsmi_relpart_build": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, c_int64, c_int64, PP]),
     "capsmi_relpart_build_mark_mid": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, P, P, P, PP]),
     "capsmi_relpart_size": (c_int32, [P, POINTER(c_int64)]),

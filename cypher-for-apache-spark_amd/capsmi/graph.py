@@ -66,6 +66,11 @@ class NodeBitmap:
         _lib.call("capsmi_bitmap_refresh", self._h, 1 if unique_rows else 0)
         return self
 
+    def assume(self, set_bits: int, unique_rows: bool = True) -> "NodeBitmap":
+        """State the set-bit count after the words were written (no device popcount, no sync)."""
+        _lib.call("capsmi_bitmap_assume", self._h, set_bits, 1 if unique_rows else 0)
+        return self
+
     def release(self) -> None:
         if self._h:
             _lib.call("capsmi_bitmap_release", self._h)
@@ -303,6 +308,12 @@ def words_popcount(session: Session, words_ptr: int, w_begin: int, w_end: int) -
     v = ctypes.c_int64()
     _lib.call("capsmi_words_popcount", session.handle, ctypes.c_void_p(words_ptr), w_begin, w_end, ctypes.byref(v))
     return v.value
+
+
+def words_popcount_device(session: Session, words_ptr: int, w_begin: int, w_end: int, out_ptr: int) -> None:
+    """The popcount into a device int64 at `out_ptr` (e.g. a torch tensor's data_ptr), no host sync."""
+    _lib.call("capsmi_words_popcount_device", session.handle, ctypes.c_void_p(words_ptr), w_begin, w_end,
+              ctypes.c_void_p(out_ptr))
 
 
 def cluster_by(rels: GpuTable, key_col: str, lo: int, hi: int) -> GpuTable:

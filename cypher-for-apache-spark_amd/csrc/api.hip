@@ -1237,6 +1237,16 @@ capsmi_status capsmi_bitmap_refresh(capsmi_bitmap* b, int32_t unique_rows) {
     API_END
 }
 
+capsmi_status capsmi_bitmap_assume(capsmi_bitmap* b, int64_t set_bits, int32_t unique_rows) {
+    API_BEGIN
+    need(b, "bitmap");
+    REQUIRE(set_bits >= 0 && set_bits <= b->hi - b->lo, CAPSMI_ERR_ILLEGAL_ARGUMENT, "set-bit count outside the domain");
+    b->set_bits = set_bits;
+    b->full = b->set_bits == b->hi - b->lo;
+    b->any_dup = unique_rows == 0;
+    API_END
+}
+
 capsmi_status capsmi_bitmap_copy_words(capsmi_bitmap* b, int64_t w_begin, int64_t w_end, uint32_t* ext,
                                        int32_t to_bitmap) {
     API_BEGIN
@@ -1801,6 +1811,17 @@ capsmi_status capsmi_words_popcount(capsmi_session* s, const uint32_t* words, in
     need(out, "out");
     use_device(s);
     *out = words_popcount(s, words, w_begin, w_end);
+    API_END
+}
+
+capsmi_status capsmi_words_popcount_device(capsmi_session* s, const uint32_t* words, int64_t w_begin, int64_t w_end,
+                                           int64_t* dev_out) {
+    API_BEGIN
+    need(s, "session");
+    need(words, "words");
+    need(dev_out, "dev_out");
+    use_device(s);
+    words_popcount_async(s, words, w_begin, w_end, dev_out);
     API_END
 }
 

@@ -402,5 +402,6 @@ bool compile_range_pred(const capsmi_table* t, int32_t nn, const capsmi_expr* pr
 void bitmap_add_rows(capsmi_bitmap* b, const int64_t* ids, const uint8_t* ids_valid, const uint8_t* flags, int64_t n,
                      int64_t* dev_counters, const RangePred* rp = nullptr);
 int64_t words_popcount(capsmi_session* s, const uint32_t* w, int64_t w_begin, int64_t w_end);
+void words_popcount_async(capsmi_session* s, const uint32_t* w, int64_t w_begin, int64_t w_end, int64_t* dev_out);
 
 }  // namespace capsmi

@@ -729,14 +729,17 @@ bool compile_range_pred(const capsmi_table* t, int32_t nn, const capsmi_expr* pr
     return true;
 }
 
-int64_t words_popcount(capsmi_session* s, const uint32_t* w, int64_t w_begin, int64_t w_end) {
-    Buf out = dev_alloc(8, s);
-    HIP_CHECK(hipMemsetAsync(P<void>(out), 0, 8, s->stream));
+void words_popcount_async(capsmi_session* s, const uint32_t* w, int64_t w_begin, int64_t w_end, int64_t* dev_out) {
+    HIP_CHECK(hipMemsetAsync(dev_out, 0, 8, s->stream));
     if (w_end > w_begin)
         hipLaunchKernelGGL(k_popcount, dim3(grid_cap((w_end - w_begin + 3) / 4, (int64_t)s->num_cus * 4)), dim3(256), 0,
-                           s->stream, w, w_begin, w_end,
-                           P<unsigned long long>(out));
+                           s->stream, w, w_begin, w_end, reinterpret_cast<unsigned long long*>(dev_out));
     HIP_CHECK(hipGetLastError());
+}
+
+int64_t words_popcount(capsmi_session* s, const uint32_t* w, int64_t w_begin, int64_t w_end) {
+    Buf out = dev_alloc(8, s);
+    words_popcount_async(s, w, w_begin, w_end, P<int64_t>(out));
     return read_scalar(s, P<int64_t>(out));
 }
 

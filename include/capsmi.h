@@ -323,6 +323,10 @@ capsmi_status capsmi_bitmap_release(capsmi_bitmap* b);
  * every rank's scan was duplicate-free (the all-reduced AND of capsmi_bitmap_stats) */
 capsmi_status capsmi_bitmap_words(capsmi_bitmap* b, uint32_t** words, int64_t* nwords);
 capsmi_status capsmi_bitmap_refresh(capsmi_bitmap* b, int32_t unique_rows);
+/* the same without the device popcount (no synchronisation): the caller states the set-bit count,
+ * e.g. the all-reduced sum of every rank's capsmi_bitmap_stats over its owned rows, taken before
+ * the all-gather */
+capsmi_status capsmi_bitmap_assume(capsmi_bitmap* b, int64_t set_bits, int32_t unique_rows);
 /* stream-ordered device copy of words [w_begin, w_end): to_bitmap = 0 copies bitmap -> ext,
  * 1 copies ext -> bitmap (ext: a caller device buffer of w_end - w_begin words) */
 capsmi_status capsmi_bitmap_copy_words(capsmi_bitmap* b, int64_t w_begin, int64_t w_end, uint32_t* ext,
@@ -438,6 +442,10 @@ capsmi_status capsmi_triangle_count(capsmi_session* s, int32_t nrels, capsmi_tab
 /* popcount of words [w_begin, w_end) of a device bitmap, result in *out (host) */
 capsmi_status capsmi_words_popcount(capsmi_session* s, const uint32_t* words, int64_t w_begin, int64_t w_end,
                                     int64_t* out);
+/* the same into a device int64 (*dev_out, overwritten), stream-ordered, no host synchronisation (the
+ * count feeds a collective directly) */
+capsmi_status capsmi_words_popcount_device(capsmi_session* s, const uint32_t* words, int64_t w_begin, int64_t w_end,
+                                           int64_t* dev_out);
 
 /* Cache analogue (Table.cache -> DataFrameTable.cache, SparkTable.scala:240-246): a copy of a
  * relationship table with rows clustered by `key_col` (dense ids in [id_lo, id_hi)).  Row multiset
