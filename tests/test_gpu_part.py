@@ -287,3 +287,58 @@ def test_owner_partitioned_two_hop_with_torch_in_between(nparts):
         total += graph.words_popcount(s, dst.data_ptr(), wb, we)
         rps[r].release()
     assert total == ref
+
+
+@pytest.mark.parametrize("nparts", [2, 4])
+def test_sharded_node_scan_assume_and_device_popcount(nparts):
+    """The multi-GPU node scan and answer without host popcounts: every rank scans its owned
+    :Person rows, the owned word slices are stitched (the all-gather), the summed owned set-bit
+    counts are stated with capsmi_bitmap_assume, and each rank's owned hop-2 popcount goes into a
+    device int64 (capsmi_words_popcount_device) that is summed on the device."""
+    import torch
+    from capsmi import Session, graph
+    from capsmi.expr import Ands, BinOp, Col, Lit
+    scale = 15
+    n, m = 1 << scale, 16 << scale
+    nw = (n + 31) // 32
+    s = Session(0)
+    s.set_stream(torch.cuda.current_stream().cuda_stream)
+    persons = graph.rmat_nodes(s, scale, graph.NODES_PERSON, 3)
+    full = graph.rmat_rels(s, scale, 0, m, graph.RMAT_GRAPH500, 5)
+    p_ref = graph.NodeBitmap(s, 0, n).add_scan(persons, "id")
+    ref = graph.two_hop_count_distinct(s, [full], p_ref, p_ref, p_ref)
+    bits_ref, uniq_ref = p_ref.stats()
+    words = torch.zeros(nw, dtype=torch.int32, device="cuda")
+    total_bits = 0
+    for r in range(nparts):
+        wb, we = graph.owner_words(n, r, nparts)
+        own = persons.filter(Ands((BinOp(">=", Col("id"), Lit(32 * wb)), BinOp("<", Col("id"), Lit(min(32 * we, n))))))
+        q = graph.NodeBitmap(s, 0, n).add_scan(own, "id")
+        total_bits += q.stats()[0]
+        q.copy_words(wb, we, words[wb:we].data_ptr(), to_bitmap=False)
+        q.release()
+    p = graph.NodeBitmap(s, 0, n)
+    p.copy_words(0, nw, words.data_ptr(), to_bitmap=True)
+    p.assume(total_bits, True)
+    assert p.stats() == (bits_ref, uniq_ref)
+    rels = [graph.rmat_rels(s, scale, 0, m, graph.RMAT_GRAPH500, 5, part_col=graph.PART_TARGET, part=r, nparts=nparts)
+            for r in range(nparts)]
+    mids = [torch.zeros(2 * nw, dtype=torch.int32, device="cuda") for _ in range(nparts)]
+    scratch = torch.zeros(nw, dtype=torch.int32, device="cuda")
+    rps = [graph.RelPartition.build_mark_mid(s, [rels[r]], p, p, mids[r].data_ptr(), scratch.data_ptr())
+           for r in range(nparts)]
+    mid = torch.zeros(2 * nw, dtype=torch.int32, device="cuda")
+    for r in range(nparts):
+        wb, we = graph.owner_words(n, r, nparts)
+        mid[wb:we] = mids[r][wb:we]
+        mid[nw + wb:nw + we] = mids[r][nw + wb:nw + we]
+    counts = torch.zeros(nparts, dtype=torch.int64, device="cuda")
+    for r in range(nparts):
+        wb, we = graph.owner_words(n, r, nparts)
+        dst = torch.zeros(nw, dtype=torch.int32, device="cuda")
+        rps[r].mark_dst(p, p, mid.data_ptr(), dst.data_ptr())
+        graph.words_popcount_device(s, dst.data_ptr(), wb, we, counts[r:r + 1].data_ptr())
+        rps[r].release()
+    assert int(counts.sum().item()) == ref
+    with pytest.raises(Exception):
+        p.assume(n + 1, True)  # a count outside the domain is refused
