@@ -236,6 +236,7 @@ class GpuTable:
         self.session = session
         self._h = handle
         self._schema = None  # (names, types): tables are immutable, so the schema is read once
+        self._index = None  # name -> position (expression compilation)
 
     # ---- lifetime ------------------------------------------------------------------------
     @property
@@ -388,9 +389,13 @@ class GpuTable:
         _lib.call("capsmi_select", self._h, len(cols), _lib.strs(cols), ctypes.byref(out))
         return self._wrap(out)
 
+    def _column_index(self) -> dict:
+        if self._index is None:  # name -> position, built once per table (expressions are compiled per column)
+            self._index = {n: i for i, n in enumerate(self._read_schema()[0])}
+        return self._index
+
     def _program(self, e: Expr):
-        names = self.physicalColumns
-        index = {n: i for i, n in enumerate(names)}
+        index = self._column_index()
 
         def col(name: str) -> int:
             if name not in index:
