@@ -411,30 +411,31 @@ __global__ void __launch_bounds__(kB) k_rec_walk(const uint16_t* __restrict__ po
                 }
                 const int64_t base = (int64_t)cur_j << kBits;
                 const uint32_t w[4] = {v0.x, v0.y, v0.z, v0.w};
-                // all 8 LDS accesses are issued before any result is used
-                uint32_t got[8];
+                // all 8 LDS accesses are issued before any result is used; the wrap test is one
+                // compare per record, its (rare) corrections out of line
+                const int lim = (int)fill - (int)threadIdx.x * 8;  // records of this lane below the fill
+                uint32_t got[8], rr[8];
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
-                    const uint32_t i = threadIdx.x * 8 + (uint32_t)e;
-                    const uint32_t r = (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+                    rr[e] = __builtin_amdgcn_ubfe(w[e >> 1], 16 * (e & 1), 16);
                     got[e] = 0u;
-                    if (i < fill) got[e] = OUT ? cl[r >> 1] : atomicAdd(&cl[r >> 1], 1u << ((r & 1u) * 16u));
+                    if (e < lim) {
+                        uint32_t* word = &cl[rr[e] >> 1];
+                        got[e] = OUT ? *word : atomicAdd(word, 1u << ((rr[e] & 1u) << 4));
+                    }
                 }
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
-                    const uint32_t i = threadIdx.x * 8 + (uint32_t)e;
-                    const uint32_t r = (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu, sh = (r & 1u) * 16u;
-                    if (i >= fill) continue;
+                    if (e >= lim) continue;
+                    const uint32_t v = __builtin_amdgcn_ubfe(got[e], (rr[e] & 1u) << 4, 16);
                     if (OUT) {
-                        const uint32_t v = (got[e] >> sh) & 0xFFFFu;
-                        acc += v < 0xFF00u ? v : v != 0xFFFFu ? bigv[v - 0xFF00u] : exact(base + r);
-                    } else {
-                        const uint32_t old = got[e];
-                        const int64_t xl = base + (r & ~1u), xh = xl + 1;
-                        if (sh == 0 && (old & 0xFFFFu) == 0xFFFFu) {  // low wrap: + 2^16 low, carry into high
+                        acc += v < 0xFF00u ? v : v != 0xFFFFu ? bigv[v - 0xFF00u] : exact(base + rr[e]);
+                    } else if (v == 0xFFFFu) {  // this add wrapped its half (rare: ids with >= 2^16 in-relationships)
+                        const int64_t xl = base + (rr[e] & ~1u), xh = xl + 1;
+                        if (!(rr[e] & 1u)) {  // low half: + 2^16 to it, and the carry went into the high half
                             atomicAdd(&corr[xl], 65536);
-                            if (xh < n) atomicAdd(&corr[xh], (old >> 16) == 0xFFFFu ? 65535 : -1);  // carry wrapped high too
-                        } else if (sh == 16 && (old >> 16) == 0xFFFFu) {
+                            if (xh < n) atomicAdd(&corr[xh], (got[e] >> 16) == 0xFFFFu ? 65535 : -1);  // carry wrapped high too
+                        } else {
                             atomicAdd(&corr[xh], 65536);
                         }
                     }
