@@ -106,3 +106,31 @@ def test_dense_buckets_roll_chunks(session, monkeypatch, mode):
     got = graph.two_hop_count(session, [_rels(session, src.astype(np.int64), dst.astype(np.int64))], _bm(session, n, a),
                               _bm(session, n, ones), _bm(session, n, ones))
     assert got == rows
+
+
+@pytest.mark.parametrize("mode", ["rec", "pairs"])
+def test_offset_domain(session, monkeypatch, mode):
+    """Bitmaps over [lo, lo + n) with lo far from 0 and n not a multiple of the 2^16-id bucket:
+    records are ids relative to lo, the last bucket is partial, and relationships leaving the domain
+    on either side are dropped."""
+    from capsmi import ColumnData, I64, graph
+    _mode(monkeypatch, mode)
+    rng = np.random.default_rng(31)
+    lo, n, m = 1 << 33, 200_003, 1_500_000
+    src = rng.integers(0, n, m)
+    dst = rng.integers(0, n, m)
+    src[:1000] = dst[:1000]  # self-loops
+    src[1000:1100] = n + 7  # outside the domain
+    dst[1100:1200] = -5
+    keep = (src >= 0) & (src < n) & (dst >= 0) & (dst < n)
+    a = (rng.random(n) < 0.8).astype(np.uint8)
+    b = (rng.random(n) < 0.9).astype(np.uint8)
+    c = (rng.random(n) < 0.85).astype(np.uint8)
+    rows, _ = cpu.two_hop_closed_form(n, src[keep].astype(np.int64), dst[keep].astype(np.int64), a, b, c)
+
+    def bm(mask):
+        nodes = session.table([ColumnData("id", I64, (np.nonzero(mask)[0] + lo).astype(np.int64))])
+        return graph.NodeBitmap(session, lo, lo + n).add_scan(nodes)
+
+    rels = _rels(session, (src + lo).astype(np.int64), (dst + lo).astype(np.int64))
+    assert graph.two_hop_count(session, [rels], bm(a), bm(b), bm(c)) == rows
