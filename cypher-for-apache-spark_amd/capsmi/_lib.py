@@ -140,6 +140,10 @@ _SIGS = {
     "capsmi_two_hop_mark_dst": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, P, c_void_p, c_void_p]),
     "capsmi_words_popcount": (c_int32, [P, c_void_p, c_int64, c_int64, POINTER(c_int64)]),
     "capsmi_words_popcount_device": (c_int32, [P, c_void_p, c_int64, c_int64, c_void_p]),
+    "capsmi_count_shard_begin": (c_int32, [P, c_int32, c_void_p, c_char_p, c_char_p, P, P, P, c_int64, c_int64, c_void_p,
+                                           POINTER(c_void_p)]),
+    "capsmi_count_shard_finish": (c_int32, [P, c_void_p, c_void_p]),
+    "capsmi_count_shard_release": (c_int32, [P]),
     "capsmi_relpart_build": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, c_int64, c_int64, PP]),
     "capsmi_relpart_build_mark_mid": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, P, P, P, PP]),
     "capsmi_relpart_size": (c_int32, [P, POINTER(c_int64)]),

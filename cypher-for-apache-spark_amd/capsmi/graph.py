@@ -121,6 +121,46 @@ def two_hop_count(session: Session, rels: Sequence[GpuTable], a_ok: NodeBitmap, 
     return v.value
 
 
+class CountShard:
+    """count(*) of the 2-hop chain on one rank of an owner(target) partition (capsmi_count_shard_*).
+
+    ``begin`` writes the in-degrees of the owned ids [own_lo, own_hi) (domain-relative) to the device
+    buffer at ``owned_ptr`` (uint32); the caller all-gathers those slices into one array of every
+    id's in-degree and ``finish`` writes this rank's part of the count to the device int64 at
+    ``out_ptr``.  The ranks' parts sum to the count.  Both calls are stream-ordered.
+    """
+
+    def __init__(self, session: Session, rels: Sequence[GpuTable], a_ok: NodeBitmap, b_ok: NodeBitmap,
+                 c_ok: NodeBitmap, own_lo: int, own_hi: int, owned_ptr: int, src_col: str = "source",
+                 dst_col: str = "target"):
+        h = ctypes.c_void_p()
+        _lib.call("capsmi_count_shard_begin", session.handle, len(rels), _handles(rels), src_col.encode(),
+                  dst_col.encode(), a_ok.handle, b_ok.handle, c_ok.handle, own_lo, own_hi,
+                  ctypes.c_void_p(owned_ptr), ctypes.byref(h))
+        self.handle = h
+        self._keep = (session, list(rels), a_ok, b_ok, c_ok)
+
+    def finish(self, in_all_ptr: int, out_ptr: int) -> None:
+        _lib.call("capsmi_count_shard_finish", self.handle, ctypes.c_void_p(in_all_ptr), ctypes.c_void_p(out_ptr))
+
+    def close(self) -> None:
+        if self.handle:
+            _lib.call("capsmi_count_shard_release", self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def two_hop_mark_mid(session: Session, rels: Sequence[GpuTable], a_ok: NodeBitmap, b_ok: NodeBitmap,
                      mid_ptr: int, scratch_ptr: int, src_col: str = "source", dst_col: str = "target") -> None:
     _lib.call("capsmi_two_hop_mark_mid", session.handle, len(rels), _handles(rels), src_col.encode(),

@@ -13,6 +13,7 @@
 #include <unordered_set>
 
 #include "capsmi_impl.h"
+#include "part_common.h"
 
 namespace capsmi {
 
@@ -1822,6 +1823,61 @@ capsmi_status capsmi_words_popcount_device(capsmi_session* s, const uint32_t* wo
     need(dev_out, "dev_out");
     use_device(s);
     words_popcount_async(s, words, w_begin, w_end, dev_out);
+    API_END
+}
+
+struct capsmi_count_shard {
+    capsmi::CountRec cr;
+};
+
+capsmi_status capsmi_count_shard_begin(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                                       const char* dst_col, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok,
+                                       const capsmi_bitmap* c_ok, int64_t own_lo, int64_t own_hi, uint32_t* owned_in,
+                                       capsmi_count_shard** out) {
+    API_BEGIN
+    need(s, "session");
+    need(out, "out");
+    check_bitmap(a_ok, "a_ok");
+    check_bitmap(b_ok, "b_ok");
+    check_bitmap(c_ok, "c_ok");
+    REQUIRE(!a_ok->any_dup && !b_ok->any_dup && !c_ok->any_dup, CAPSMI_ERR_UNSUPPORTED,
+            "closed-form count(*) needs each node id in one scanned row");
+    const int64_t n = b_ok->hi - b_ok->lo;
+    REQUIRE(a_ok->lo == b_ok->lo && a_ok->hi == b_ok->hi && c_ok->lo == b_ok->lo && c_ok->hi == b_ok->hi,
+            CAPSMI_ERR_ILLEGAL_ARGUMENT, "count shard: the three bitmaps must share one id domain");
+    REQUIRE(n > 0 && n <= (int64_t(1) << 26), CAPSMI_ERR_UNSUPPORTED, "count shard: id domain of 1 .. 2^26 ids");
+    REQUIRE(0 <= own_lo && own_lo <= own_hi && own_hi <= n, CAPSMI_ERR_ILLEGAL_ARGUMENT, "count shard: owned range");
+    REQUIRE(own_hi == own_lo || owned_in, CAPSMI_ERR_ILLEGAL_ARGUMENT, "null argument: owned_in");
+    use_device(s);
+    std::vector<const int64_t*> srcs, dsts;
+    std::vector<int64_t> ms;
+    for (int i = 0; i < nrels; ++i) {
+        need(rels[i], "rels[i]");
+        M(rels[i]);
+        srcs.push_back(rel_col(rels[i], src_col).d());
+        dsts.push_back(rel_col(rels[i], dst_col).d());
+        ms.push_back(rels[i]->nrows);
+    }
+    auto h = std::make_unique<capsmi_count_shard>();
+    count_rec_begin(s, srcs.data(), dsts.data(), ms.data(), nrels, a_ok, b_ok, c_ok, h->cr);
+    count_rec_fold(h->cr, own_lo, own_hi, owned_in);
+    *out = h.release();
+    API_END
+}
+
+capsmi_status capsmi_count_shard_finish(capsmi_count_shard* h, const uint32_t* in_all, int64_t* dev_out) {
+    API_BEGIN
+    need(h, "count shard");
+    need(in_all, "in_all");
+    need(dev_out, "dev_out");
+    use_device(h->cr.s);
+    count_rec_finish(h->cr, in_all, dev_out);
+    API_END
+}
+
+capsmi_status capsmi_count_shard_release(capsmi_count_shard* h) {
+    API_BEGIN
+    delete h;
     API_END
 }
 

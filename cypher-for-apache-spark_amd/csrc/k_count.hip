@@ -343,8 +343,10 @@ __global__ void __launch_bounds__(kB) k_rec_walk(const uint16_t* __restrict__ po
             v = make_uint4(x[0], x[1], x[2], x[3]);
             return fill;
         };
-        auto exact = [&](int64_t x) -> uint32_t {  // OUT: the stored count of id x
-            return x < n && bit(b, (uint64_t)x) ? (uint32_t)((int64_t)inA[x] + corr[x]) : 0u;
+        auto exact = [&](int64_t x) -> uint32_t {  // OUT: the stored count of id x (corr null: folded already)
+            if (x >= n) return 0u;
+            if (!corr) return inA[x];
+            return bit(b, (uint64_t)x) ? (uint32_t)((int64_t)inA[x] + corr[x]) : 0u;
         };
         auto slot16 = [&](uint32_t v) -> uint32_t {  // OUT: a value as its 16-bit slot
             if (v < 0xFF00u) return v;
@@ -450,9 +452,25 @@ __global__ void __launch_bounds__(kB) k_rec_walk(const uint16_t* __restrict__ po
 
 }  // namespace rec
 
-// the same count from two record partitions (rec:: above); one id domain of at most 2^26 ids
-int64_t two_hop_count_rec(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
-                          int nt, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok) {
+namespace rec {
+
+// owned in-degrees, folded: out[x - own_lo] = b_ok(x) ? inA(x) + corr(x) : 0
+__global__ void k_rec_fold(const uint32_t* __restrict__ inA, const int32_t* __restrict__ corr, part::BitV b,
+                           int64_t own_lo, int64_t own_hi, uint32_t* __restrict__ out) {
+    for (int64_t x = own_lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < own_hi;
+         x += (int64_t)gridDim.x * blockDim.x)
+        out[x - own_lo] = bit(b, (uint64_t)x) ? (uint32_t)((int64_t)inA[x] + corr[x]) : 0u;
+}
+
+__global__ void k_rec_result(const unsigned long long* __restrict__ acc, int64_t* __restrict__ out) {
+    *out = (int64_t)(acc[1] - acc[0]);  // sum - self-loops
+}
+
+}  // namespace rec
+
+// phase 1: the two-sided record partition and the IN walk (inA of every target this table holds)
+void count_rec_begin(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
+                     const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok, CountRec& cr) {
     using namespace rec;
     const int64_t lo = b_ok->lo, n = b_ok->hi - b_ok->lo;
     const part::BitV a{P<uint32_t>(a_ok->words), a_ok->full ? 1 : 0}, b{P<uint32_t>(b_ok->words), b_ok->full ? 1 : 0},
@@ -460,12 +478,17 @@ int64_t two_hop_count_rec(capsmi_session* s, const int64_t* const* srcs, const i
     hipStream_t st = s->stream;
     const int nb = (int)((n + (int64_t(1) << kBits) - 1) >> kBits);
     REQUIRE(nb >= 1 && nb <= kMaxBuckets, CAPSMI_ERR_INTERNAL, "count(*) records: domain too large");
-    Buf inA = dev_alloc(sizeof(uint32_t) * (size_t)n, s);
-    Buf corr = dev_alloc(sizeof(int32_t) * (size_t)n, s);  // wrap corrections of the 16-bit LDS counters
-    Buf acc = dev_alloc(2 * sizeof(unsigned long long), s);  // loops, sum
-    HIP_CHECK(hipMemsetAsync(P<void>(inA), 0, sizeof(uint32_t) * (size_t)n, st));
-    HIP_CHECK(hipMemsetAsync(P<void>(corr), 0, sizeof(int32_t) * (size_t)n, st));
-    HIP_CHECK(hipMemsetAsync(P<void>(acc), 0, 2 * sizeof(unsigned long long), st));
+    cr.s = s;
+    cr.n = n;
+    cr.nb = nb;
+    cr.bw = b.w;
+    cr.b_full = b.full;
+    cr.inA = dev_alloc(sizeof(uint32_t) * (size_t)n, s);
+    cr.corr = dev_alloc(sizeof(int32_t) * (size_t)n, s);  // wrap corrections of the 16-bit LDS counters
+    cr.acc = dev_alloc(2 * sizeof(unsigned long long), s);  // loops, sum
+    HIP_CHECK(hipMemsetAsync(P<void>(cr.inA), 0, sizeof(uint32_t) * (size_t)n, st));
+    HIP_CHECK(hipMemsetAsync(P<void>(cr.corr), 0, sizeof(int32_t) * (size_t)n, st));
+    HIP_CHECK(hipMemsetAsync(P<void>(cr.acc), 0, 2 * sizeof(unsigned long long), st));
     static std::once_flag once;
     std::call_once(once, [] {
         HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_rec_part), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -487,8 +510,9 @@ int64_t two_hop_count_rec(capsmi_session* s, const int64_t* const* srcs, const i
         pool_chunks += (int64_t)g1[i] * cpb[i];
     }
     REQUIRE(pool_chunks < (int64_t)INT32_MAX, CAPSMI_ERR_UNSUPPORTED, "relationship table too large for the count");
+    cr.mtot = mtot;
     const int64_t npool = pool_chunks > 0 ? pool_chunks : 1;
-    ChunkPart cp;
+    ChunkPart& cp = cr.cp;
     cp.L.lo = lo;
     cp.L.hi = lo + n;
     cp.L.nt = 2 * nb;
@@ -501,31 +525,63 @@ int64_t two_hop_count_rec(capsmi_session* s, const int64_t* const* srcs, const i
             if (ms[i] <= 0) continue;
             hipLaunchKernelGGL(k_rec_part, dim3(g1[i]), dim3(kB), part_lds(2 * nb), st, srcs[i], dsts[i], ms[i], lo, n, nb, a,
                                b, c, c0[i], cpb[i], P<uint16_t>(cp.pool), P<unsigned long long>(cp.meta),
-                               P<unsigned long long>(acc));
+                               P<unsigned long long>(cr.acc));
         }
         HIP_CHECK(hipGetLastError());
     }
     chunk_order(s, 2 * nb, pool_chunks, s->num_cus, cp);
-    const size_t wl = walk_lds();
-    const unsigned g2 = (unsigned)s->num_cus;
     {
         KernelTimer kt(s, "count_in", (double)mtot * 2 + (double)n * 4);
-        hipLaunchKernelGGL(k_rec_walk<false>, dim3(g2), dim3(kB), wl, st, P<uint16_t>(cp.pool),
-                           P<unsigned long long>(cp.meta), cp.order, cp.jst, nb, n, b, P<uint32_t>(inA), P<int32_t>(corr),
-                           P<unsigned long long>(acc) + 1);
+        hipLaunchKernelGGL(k_rec_walk<false>, dim3((unsigned)s->num_cus), dim3(kB), walk_lds(), st, P<uint16_t>(cp.pool),
+                           P<unsigned long long>(cp.meta), cp.order, cp.jst, nb, n, b, P<uint32_t>(cr.inA),
+                           P<int32_t>(cr.corr), P<unsigned long long>(cr.acc) + 1);
         HIP_CHECK(hipGetLastError());
     }
+}
+
+// the folded in-degrees of ids [own_lo, own_hi) (domain-relative) into `out` (device)
+void count_rec_fold(CountRec& cr, int64_t own_lo, int64_t own_hi, uint32_t* out) {
+    using namespace rec;
+    const part::BitV b{cr.bw, cr.b_full};
+    if (own_hi > own_lo)
+        hipLaunchKernelGGL(k_rec_fold, dim3((unsigned)std::min<int64_t>((own_hi - own_lo + 255) / 256, 4096)), dim3(256), 0,
+                           cr.s->stream, P<uint32_t>(cr.inA), P<int32_t>(cr.corr), b, own_lo, own_hi, out);
+    HIP_CHECK(hipGetLastError());
+}
+
+// phase 2: the OUT walk, sum of inA(source) over the out-records; in_all = every id's folded
+// in-degree (null: this table's own, corrections applied on the fly).  The result (sum - the
+// counted self-loops) goes to dev_out (device int64) when given, else it is returned.
+int64_t count_rec_finish(CountRec& cr, const uint32_t* in_all, int64_t* dev_out) {
+    using namespace rec;
+    capsmi_session* s = cr.s;
+    hipStream_t st = s->stream;
+    const part::BitV b{cr.bw, cr.b_full};
     {
-        KernelTimer kt(s, "count_out", (double)mtot * 2 + (double)n * 8);
-        hipLaunchKernelGGL(k_rec_walk<true>, dim3(g2), dim3(kB), wl, st, P<uint16_t>(cp.pool),
-                           P<unsigned long long>(cp.meta), cp.order, cp.jst + nb, nb, n, b, P<uint32_t>(inA),
-                           P<int32_t>(corr), P<unsigned long long>(acc) + 1);
+        KernelTimer kt(s, "count_out", (double)cr.mtot * 2 + (double)cr.n * 8);
+        hipLaunchKernelGGL(k_rec_walk<true>, dim3((unsigned)s->num_cus), dim3(kB), walk_lds(), st, P<uint16_t>(cr.cp.pool),
+                           P<unsigned long long>(cr.cp.meta), cr.cp.order, cr.cp.jst + cr.nb, cr.nb, cr.n, b,
+                           in_all ? const_cast<uint32_t*>(in_all) : P<uint32_t>(cr.inA),
+                           in_all ? nullptr : P<int32_t>(cr.corr), P<unsigned long long>(cr.acc) + 1);
         HIP_CHECK(hipGetLastError());
+    }
+    if (dev_out) {
+        hipLaunchKernelGGL(k_rec_result, dim3(1), dim3(1), 0, st, P<unsigned long long>(cr.acc), dev_out);
+        HIP_CHECK(hipGetLastError());
+        return 0;
     }
     unsigned long long h[2];
-    HIP_CHECK(hipMemcpyAsync(h, P<void>(acc), sizeof(h), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(h, P<void>(cr.acc), sizeof(h), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
     return (int64_t)(h[1] - h[0]);
+}
+
+// the same count from two record partitions (rec:: above); one id domain of at most 2^26 ids
+int64_t two_hop_count_rec(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
+                          int nt, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok) {
+    CountRec cr;
+    count_rec_begin(s, srcs, dsts, ms, nt, a_ok, b_ok, c_ok, cr);
+    return count_rec_finish(cr, nullptr, nullptr);
 }
 
 // count(*) of the 2-hop chain over relationship tables (srcs[i], dsts[i], ms[i]); the three node

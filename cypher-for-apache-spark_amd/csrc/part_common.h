@@ -309,4 +309,21 @@ void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_
 // the ordering half of chunk_partition for a pool another kernel filled (cp.meta: bucket | fill << 32)
 void chunk_order(capsmi_session* s, int nt, int64_t pool_chunks, int64_t g2, ChunkPart& cp);
 
+// the record form in phases (k_count.hip): begin = partition + in-degree walk, fold = the owned
+// ids' in-degrees for an all-gather, finish = the out walk over all ids' in-degrees
+struct CountRec {
+    capsmi_session* s = nullptr;
+    int64_t n = 0, mtot = 0;
+    int nb = 0;
+    const uint32_t* bw = nullptr;
+    int b_full = 0;
+    Buf inA, corr, acc;
+    ChunkPart cp;
+};
+void count_rec_begin(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
+                     const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok, CountRec& cr);
+void count_rec_fold(CountRec& cr, int64_t own_lo, int64_t own_hi, uint32_t* out);
+int64_t count_rec_finish(CountRec& cr, const uint32_t* in_all, int64_t* dev_out);
+
+
 }  // namespace capsmi

@@ -439,6 +439,21 @@ capsmi_status capsmi_trigraph_stats(const capsmi_trigraph* g, int64_t* nodes, in
 capsmi_status capsmi_trigraph_release(capsmi_trigraph* g);
 capsmi_status capsmi_triangle_count(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
                                     const char* dst_col, const capsmi_bitmap* n_ok, int64_t* out_rows);
+/* count(*) of the 2-hop chain (capsmi_two_hop_count) on one rank of an owner(target) partition:
+ * this rank's tables hold every relationship into its owned ids [own_lo, own_hi) (relative to the
+ * bitmaps' lo).  begin partitions them and writes the owned ids' in-degrees inA (relationships from
+ * a_ok sources, b_ok applied) to owned_in (device, own_hi - own_lo uint32), stream-ordered; the
+ * caller all-gathers the owned slices into one array of every id's inA, and finish sums inA(b) over
+ * this rank's relationships b -> y with c_ok(y), less its a/b/c-ok self-loops, into *dev_out (device
+ * int64, stream-ordered): the all-reduced sum of the ranks' parts is the count.  Σ_b inA(b)·outC(b)
+ * (RelationalPlanner.scala:113-177 join rows, closed form in DESIGN.md §4) */
+typedef struct capsmi_count_shard capsmi_count_shard;
+capsmi_status capsmi_count_shard_begin(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                                       const char* dst_col, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok,
+                                       const capsmi_bitmap* c_ok, int64_t own_lo, int64_t own_hi, uint32_t* owned_in,
+                                       capsmi_count_shard** out);
+capsmi_status capsmi_count_shard_finish(capsmi_count_shard* h, const uint32_t* in_all, int64_t* dev_out);
+capsmi_status capsmi_count_shard_release(capsmi_count_shard* h);
 /* popcount of words [w_begin, w_end) of a device bitmap, result in *out (host) */
 capsmi_status capsmi_words_popcount(capsmi_session* s, const uint32_t* words, int64_t w_begin, int64_t w_end,
                                     int64_t* out);

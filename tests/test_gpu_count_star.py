@@ -134,3 +134,49 @@ def test_offset_domain(session, monkeypatch, mode):
 
     rels = _rels(session, (src + lo).astype(np.int64), (dst + lo).astype(np.int64))
     assert graph.two_hop_count(session, [rels], bm(a), bm(b), bm(c)) == rows
+
+
+@pytest.mark.parametrize("nparts", [1, 3, 8])
+def test_sharded_count(nparts):
+    """The multi-GPU count(*) (capsmi_count_shard_*) with N owner(target) shards on one device: each
+    shard holds the relationships into its owned id range (graph.owner_words: a ragged last range;
+    plus, on rank 0, relationships whose target leaves the domain), writes its owned in-degrees, the
+    slices are stitched into one array (the all-gather) and the shards' device parts sum to the
+    closed form.  Self-loops, sources outside the domain and an in-degree above 2^16 included."""
+    import torch
+    from capsmi import Session, graph
+    s = Session(0)
+    s.set_stream(torch.cuda.current_stream().cuda_stream)
+    rng = np.random.default_rng(41 + nparts)
+    n, m = 300_001, 2_000_000
+    src = rng.integers(0, n, m)
+    dst = rng.integers(0, n, m)
+    dst[:200_000] = 4242
+    src[200_000:201_000] = dst[200_000:201_000]
+    src[201_000:201_100] = n + 3
+    dst[201_100:201_200] = -1
+    keep = (src >= 0) & (src < n) & (dst >= 0) & (dst < n)
+    a = (rng.random(n) < 0.9).astype(np.uint8)
+    b = (rng.random(n) < 0.8).astype(np.uint8)
+    c = (rng.random(n) < 0.85).astype(np.uint8)
+    rows, _ = cpu.two_hop_closed_form(n, src[keep].astype(np.int64), dst[keep].astype(np.int64), a, b, c)
+    A, B, C = _bm(s, n, a), _bm(s, n, b), _bm(s, n, c)
+    in_all = torch.zeros(n, dtype=torch.int32, device="cuda")
+    parts = torch.zeros(nparts, dtype=torch.int64, device="cuda")
+    shards = []
+    for r in range(nparts):
+        wb, we = graph.owner_words(n, r, nparts)
+        own_lo, own_hi = 32 * wb, min(32 * we, n)
+        sel = (dst >= own_lo) & (dst < own_hi)
+        if r == 0:
+            sel |= (dst < 0) | (dst >= n)
+        rel = _rels(s, src[sel].astype(np.int64), dst[sel].astype(np.int64))
+        owned = torch.full((max(own_hi - own_lo, 1),), 0x5eed, dtype=torch.int32, device="cuda")
+        sh = graph.CountShard(s, [rel], A, B, C, own_lo, own_hi, owned.data_ptr())
+        in_all[own_lo:own_hi] = owned[: own_hi - own_lo]
+        shards.append((sh, rel, owned))
+    for r, (sh, _, _) in enumerate(shards):
+        sh.finish(in_all.data_ptr(), parts[r:r + 1].data_ptr())
+        sh.close()
+    assert int(parts.sum().item()) == rows
+    assert graph.two_hop_count(s, [_rels(s, src.astype(np.int64), dst.astype(np.int64))], A, B, C) == rows
