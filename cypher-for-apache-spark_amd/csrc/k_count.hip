@@ -214,8 +214,11 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
         }
         __syncthreads();
         const uint32_t P = part::block_exclusive_scan<kB>(pc, pb, nb2, wtot);
-        for (int i = threadIdx.x; i < nb2; i += kB)  // piece -> bucket
-            for (uint32_t k = 0; k < pc[i]; ++k) owner[pb[i] + k] = (uint16_t)i;
+        for (int i = threadIdx.x; i < nb2; i += kB) {  // piece -> bucket; pc becomes the first held rank
+            const uint32_t npc = pc[i];
+            for (uint32_t k = 0; k < npc; ++k) owner[pb[i] + k] = (uint16_t)i;
+            pc[i] = npc * kPiece - (uint32_t)hc[i];  // a run item of rank >= this (signed) is held
+        }
         __syncthreads();
         // piece g: 2 lanes x 8 records; element e < held comes from the hold, the rest from the run
         for (uint32_t x = threadIdx.x; x < P * 2; x += kB) {
@@ -242,17 +245,19 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
 #pragma unroll
         for (int u = 0; u < kIT; ++u) {  // the new held records: the run's items past its last whole piece
             if ((vin >> u) & 1u) {
-                const uint32_t bk = ys[u] >> kBits, e = hc[bk] + rin[u], cut = pc[bk] * kPiece;
-                if (e >= cut) hold[bk * kPiece + (e - cut)] = (uint16_t)(ys[u] & 0xFFFFu);
+                const uint32_t bk = ys[u] >> kBits;
+                const int d = (int)rin[u] - (int)pc[bk];
+                if (d >= 0) hold[bk * kPiece + d] = (uint16_t)(ys[u] & 0xFFFFu);
             }
             if ((vout >> u) & 1u) {
-                const uint32_t bk = nb + (xs[u] >> kBits), e = hc[bk] + rout[u], cut = pc[bk] * kPiece;
-                if (e >= cut) hold[bk * kPiece + (e - cut)] = (uint16_t)(xs[u] & 0xFFFFu);
+                const uint32_t bk = nb + (xs[u] >> kBits);
+                const int d = (int)rout[u] - (int)pc[bk];
+                if (d >= 0) hold[bk * kPiece + d] = (uint16_t)(xs[u] & 0xFFFFu);
             }
         }
         __syncthreads();
         for (int i = threadIdx.x; i < nb2; i += kB) {
-            const uint32_t tot = (uint32_t)hc[i] + cnt[i], npc = pc[i];
+            const uint32_t tot = (uint32_t)hc[i] + cnt[i], npc = tot / kPiece;
             if (npc) {
                 const uint32_t end = (uint32_t)fl[i] + npc * kPiece, nnew = (end - 1) / kCh;
                 if (nnew) {  // the chunks filled by this tile are retired, the last one opened stays open
