@@ -180,3 +180,28 @@ def test_sharded_count(nparts):
         sh.close()
     assert int(parts.sum().item()) == rows
     assert graph.two_hop_count(s, [_rels(s, src.astype(np.int64), dst.astype(np.int64))], A, B, C) == rows
+
+
+def test_sharded_count_refusals():
+    """capsmi_count_shard_begin refuses what the phased count cannot answer: bitmaps over different
+    id domains, an owned range outside the domain, a null owned buffer for a non-empty range."""
+    import torch
+    from capsmi import ColumnData, I64, Session, graph
+    session = Session(0)
+    session.set_stream(torch.cuda.current_stream().cuda_stream)
+    n = 1000
+    ones = np.ones(n, np.uint8)
+    A = _bm(session, n, ones)
+    rel = _rels(session, np.arange(10, dtype=np.int64), np.arange(1, 11, dtype=np.int64))
+    other = graph.NodeBitmap(session, 0, n + 64).add_scan(session.table([ColumnData("id", I64, np.arange(5))]))
+    buf = torch.zeros(n, dtype=torch.int32, device="cuda")
+    with pytest.raises(Exception):
+        graph.CountShard(session, [rel], A, other, A, 0, n, buf.data_ptr())
+    with pytest.raises(Exception):
+        graph.CountShard(session, [rel], A, A, A, 0, n + 32, buf.data_ptr())
+    with pytest.raises(Exception):
+        graph.CountShard(session, [rel], A, A, A, 0, 64, 0)
+    with graph.CountShard(session, [rel], A, A, A, 0, n, buf.data_ptr()) as sh:  # and a valid one still works
+        out = torch.zeros(1, dtype=torch.int64, device="cuda")
+        sh.finish(buf.data_ptr(), out.data_ptr())
+        assert int(out.item()) == 9  # chain 0->1->...->10: 9 two-hop pairs inside [0, 1000)
