@@ -174,7 +174,10 @@ def shard_diagnostic(args):
     mid = torch.zeros(2 * nw, dtype=torch.int32, device="cuda")
     scratch = torch.zeros(nw, dtype=torch.int32, device="cuda")
     dstw = torch.zeros(nw, dtype=torch.int32, device="cuda")
-    per_rank, rows = [], []
+    own_in = torch.zeros(n, dtype=torch.int32, device="cuda")
+    in_all = torch.zeros(n, dtype=torch.int32, device="cuda")  # stands in for the gathered in-degrees (timing)
+    cnt_dev = torch.zeros(1, dtype=torch.int64, device="cuda")
+    per_rank, per_rank_count, rows = [], [], []
     for r in range(N):
         rels = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42, part_col=graph.PART_TARGET, part=r,
                                nparts=N)
@@ -195,12 +198,29 @@ def shard_diagnostic(args):
             step()
         torch.cuda.synchronize()
         per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
+
+        def step_count():  # count(*) shard: partition + IN walk + owned fold, OUT walk (no gather / all-reduce)
+            p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")
+            sh = graph.CountShard(sess, [rels], p, p, p, 32 * wb, min(32 * we, n), own_in.data_ptr())
+            sh.finish(in_all.data_ptr(), cnt_dev.data_ptr())
+            sh.close()
+
+        for _ in range(args.warmup):
+            step_count()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step_count()
+        torch.cuda.synchronize()
+        per_rank_count.append((time.perf_counter() - t0) / args.steps * 1e3)
         rows.append(rels.size)
         del rels
     mean = sum(per_rank) / N
     print(json.dumps({"diagnostic": f"C3 cold step, every rank's owner(target) shard of {N} on one GPU, no exchange",
                       "scale": scale, "per_rank_ms": per_rank, "max_ms": max(per_rank), "mean_ms": mean,
-                      "imbalance_max_over_mean": max(per_rank) / mean, "rels_per_rank": rows}), flush=True)
+                      "imbalance_max_over_mean": max(per_rank) / mean, "rels_per_rank": rows,
+                      "count_star_per_rank_ms": per_rank_count, "count_star_max_ms": max(per_rank_count)}),
+          flush=True)
     sess.close()
 
 

@@ -113,12 +113,8 @@ constexpr int kT = kB * kIT;     // relationships per tile
 constexpr int kPiece = 16;       // records per 32-byte store
 constexpr int kCh = 8192;        // records per chunk (16 KiB; one 16-byte load per walk lane)
 constexpr int kMaxBuckets = 1024;  // per side
-constexpr int kWalkG = 4;        // chunks in flight per walk block
-constexpr int kInfo = 2048;      // chunk ids staged in LDS per walk block
 constexpr int kBig = 255;        // OUT walk: values >= 0xFF00 per bucket kept exactly in LDS
-constexpr size_t walk_lds() {
-    return sizeof(uint32_t) * (1 << (kBits - 1)) + sizeof(uint2) * kInfo + sizeof(uint32_t) * (kBig + 1);
-}
+constexpr size_t walk_lds() { return sizeof(uint32_t) * ((1 << (kBits - 1)) + kBig + 2); }
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 // nb2 = buckets of both sides
@@ -309,9 +305,10 @@ __global__ void __launch_bounds__(kB) k_rec_walk(const uint16_t* __restrict__ po
                                                  int32_t* __restrict__ corr, unsigned long long* __restrict__ sum) {
     extern __shared__ uint32_t cl[];  // 2^15 words = 2^16 16-bit counters / staged values
     constexpr int kWords = 1 << (kBits - 1);
-    uint2* cinfo = reinterpret_cast<uint2*>(cl + kWords);  // (chunk, fill) of kInfo chunks of the share
-    uint32_t* bigv = reinterpret_cast<uint32_t*>(cinfo + kInfo);  // OUT: exact values behind 0xFF00 + k
+    uint32_t* bigv = cl + kWords;  // OUT: exact values behind 0xFF00 + k
     uint32_t* nbig = bigv + kBig;
+    uint32_t* qn = nbig + 1;  // next chunk of the bucket visit (waves take chunks from it)
+    const int lane = threadIdx.x & 63;
     // jst: nb + 1 bucket starts in `order` (the side's buckets of the two-sided partition, so
     // jst[0] need not be 0); block w takes an equal share of the side's chunks
     const int64_t q00 = jst[0], nch = jst[nb] - q00;
@@ -320,34 +317,6 @@ __global__ void __launch_bounds__(kB) k_rec_walk(const uint16_t* __restrict__ po
     const int64_t qb = q00 + (int64_t)blockIdx.x * per, qe = min(qb + per, q00 + nch);
     unsigned long long acc = 0;
     if (qb < qe) {  // block-uniform
-        // the chunk ids and fills are staged in LDS kInfo at a time, so a chunk's loads wait for no
-        // index load (order -> meta -> data would be two dependent round trips per chunk)
-        int64_t ibase = qb, iend = qb;
-        auto refill = [&](int64_t from) {
-            __syncthreads();
-            for (int i = threadIdx.x; i < kInfo; i += kB) {
-                const int64_t q = from + i;
-                if (q < qe) {
-                    const uint32_t phys = order[q];
-                    cinfo[i] = make_uint2(phys, (uint32_t)(meta[phys] >> 32));
-                }
-            }
-            ibase = from;
-            iend = min(from + kInfo, qe);
-            __syncthreads();
-        };
-        refill(qb);
-        auto load = [&](int64_t q, uint4& v) -> uint32_t {
-            if (q >= qe) return 0u;
-            const uint2 ci = cinfo[q - ibase];
-            const uint32_t phys = ci.x, fill = ci.y;
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<uint16_t*>(pool + (size_t)phys * kCh), (short)0,
-                (int)((fill * sizeof(uint16_t) + 15) & ~(size_t)15), 0x00020000);  // whole dwords: masked by `fill` below
-            const auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)threadIdx.x * 16u, 0, 2);
-            v = make_uint4(x[0], x[1], x[2], x[3]);
-            return fill;
-        };
         auto exact = [&](int64_t x) -> uint32_t {  // OUT: the stored count of id x (corr null: folded already)
             if (x >= n) return 0u;
             if (!corr) return inA[x];
@@ -364,8 +333,11 @@ __global__ void __launch_bounds__(kB) k_rec_walk(const uint16_t* __restrict__ po
         };
         auto begin = [&](int j) {
             const int64_t base = (int64_t)j << kBits;
-            if (OUT && threadIdx.x == 0) *nbig = 0;
-            if (OUT) __syncthreads();
+            if (threadIdx.x == 0) {
+                *qn = 0;
+                *nbig = 0;
+            }
+            __syncthreads();
             for (int i = threadIdx.x; i < kWords; i += kB) {
                 uint32_t w = 0;
                 if (OUT) w = slot16(exact(base + 2 * i)) | (slot16(exact(base + 2 * i + 1)) << 16);
@@ -389,68 +361,86 @@ __global__ void __launch_bounds__(kB) k_rec_walk(const uint16_t* __restrict__ po
                 }
             }
         };
-        int cur_j = part::slice_of(jst, nb, qb);
-        int64_t j_end = jst[cur_j + 1];
-        begin(cur_j);
-        __syncthreads();
-        uint4 nx[kWalkG];
-        uint32_t nfill[kWalkG];
+        auto grab = [&]() -> uint32_t {  // the wave's next chunk of the visit (wave-uniform)
+            uint32_t t = 0;
+            if (lane == 0) t = atomicAdd(qn, 1u);
+            return __shfl(t, 0, 64);
+        };
+        // records r of a 16-byte group at [8 * lane-group, + 8): lim = records of it below the fill
+        auto walk8 = [&](const uint4 v0, int lim, int64_t base) {
+            const uint32_t w[4] = {v0.x, v0.y, v0.z, v0.w};
+            // all 8 LDS accesses are issued before any result is used; the wrap test is one
+            // compare per record, its (rare) corrections out of line
+            uint32_t got[8], rr[8];
 #pragma unroll
-        for (int g = 0; g < kWalkG; ++g) nfill[g] = load(qb + g, nx[g]);
-        for (int64_t q0 = qb; q0 < qe; q0 += kWalkG) {  // block-uniform; kWalkG chunks in flight
-#pragma unroll
-            for (int g = 0; g < kWalkG; ++g) {  // static slots: each use waits for its own loads only
-                const int64_t q = q0 + g;
-                if (q >= qe) break;
-                const uint4 v0 = nx[g];
-                const uint32_t fill = nfill[g];
-                if (q + kWalkG >= iend && iend < qe) refill(q + kWalkG);  // block-uniform
-                nfill[g] = load(q + kWalkG, nx[g]);
-                int j = cur_j;
-                while (q >= j_end) j_end = jst[++j + 1];  // empty buckets are skipped
-                if (j != cur_j) {
-                    __syncthreads();
-                    flush(cur_j);
-                    __syncthreads();
-                    begin(j);
-                    __syncthreads();
-                    cur_j = j;
+            for (int e = 0; e < 8; ++e) {
+                rr[e] = __builtin_amdgcn_ubfe(w[e >> 1], 16 * (e & 1), 16);
+                got[e] = 0u;
+                if (e < lim) {
+                    uint32_t* word = &cl[rr[e] >> 1];
+                    got[e] = OUT ? *word : atomicAdd(word, 1u << ((rr[e] & 1u) << 4));
                 }
-                const int64_t base = (int64_t)cur_j << kBits;
-                const uint32_t w[4] = {v0.x, v0.y, v0.z, v0.w};
-                // all 8 LDS accesses are issued before any result is used; the wrap test is one
-                // compare per record, its (rare) corrections out of line
-                const int lim = (int)fill - (int)threadIdx.x * 8;  // records of this lane below the fill
-                uint32_t got[8], rr[8];
+            }
 #pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    rr[e] = __builtin_amdgcn_ubfe(w[e >> 1], 16 * (e & 1), 16);
-                    got[e] = 0u;
-                    if (e < lim) {
-                        uint32_t* word = &cl[rr[e] >> 1];
-                        got[e] = OUT ? *word : atomicAdd(word, 1u << ((rr[e] & 1u) << 4));
-                    }
-                }
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    if (e >= lim) continue;
-                    const uint32_t v = __builtin_amdgcn_ubfe(got[e], (rr[e] & 1u) << 4, 16);
-                    if (OUT) {
-                        acc += v < 0xFF00u ? v : v != 0xFFFFu ? bigv[v - 0xFF00u] : exact(base + rr[e]);
-                    } else if (v == 0xFFFFu) {  // this add wrapped its half (rare: ids with >= 2^16 in-relationships)
-                        const int64_t xl = base + (rr[e] & ~1u), xh = xl + 1;
-                        if (!(rr[e] & 1u)) {  // low half: + 2^16 to it, and the carry went into the high half
-                            atomicAdd(&corr[xl], 65536);
-                            if (xh < n) atomicAdd(&corr[xh], (got[e] >> 16) == 0xFFFFu ? 65535 : -1);  // carry wrapped high too
-                        } else {
-                            atomicAdd(&corr[xh], 65536);
-                        }
+            for (int e = 0; e < 8; ++e) {
+                if (e >= lim) continue;
+                const uint32_t v = __builtin_amdgcn_ubfe(got[e], (rr[e] & 1u) << 4, 16);
+                if (OUT) {
+                    acc += v < 0xFF00u ? v : v != 0xFFFFu ? bigv[v - 0xFF00u] : exact(base + rr[e]);
+                } else if (v == 0xFFFFu) {  // this add wrapped its half (rare: ids with >= 2^16 in-relationships)
+                    const int64_t xl = base + (rr[e] & ~1u), xh = xl + 1;
+                    if (!(rr[e] & 1u)) {  // low half: + 2^16 to it, and the carry went into the high half
+                        atomicAdd(&corr[xl], 65536);
+                        if (xh < n) atomicAdd(&corr[xh], (got[e] >> 16) == 0xFFFFu ? 65535 : -1);  // carry wrapped high too
+                    } else {
+                        atomicAdd(&corr[xh], 65536);
                     }
                 }
             }
+        };
+        // One visit per bucket the share touches.  Inside a visit each wave takes whole chunks from
+        // an LDS cursor and walks them 512 records (one 16-byte load per lane) at a time, so a
+        // part-full chunk costs its own records, not a whole block's pass.
+        int cur_j = part::slice_of(jst, nb, qb);
+        for (;;) {  // block-uniform
+            const int64_t c0 = max(qb, jst[cur_j]), c1 = min(qe, jst[cur_j + 1]);
+            begin(cur_j);
+            __syncthreads();
+            const int64_t base = (int64_t)cur_j << kBits;
+            uint32_t t = grab();
+            uint32_t phys = 0, fill = 0;
+            if (c0 + t < c1) {
+                phys = order[c0 + t];
+                fill = (uint32_t)(meta[phys] >> 32);
+            }
+            while (c0 + t < c1) {  // wave-uniform
+                const uint32_t tn = grab();  // the next chunk's ids are fetched while this one is walked
+                uint32_t pn = 0, fn = 0;
+                if (c0 + tn < c1) {
+                    pn = order[c0 + tn];
+                    fn = (uint32_t)(meta[pn] >> 32);
+                }
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint16_t*>(pool + (size_t)phys * kCh), (short)0,
+                    (int)((fill * sizeof(uint16_t) + 15) & ~(size_t)15), 0x00020000);  // whole dwords: masked by lim
+                auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)lane * 16u, 0, 2);
+                for (uint32_t o = 0; o < fill; o += 512) {  // wave-uniform
+                    const uint4 v = make_uint4(x[0], x[1], x[2], x[3]);
+                    if (o + 512 < fill) x = __builtin_amdgcn_raw_buffer_load_b128(rs, (o + 512) * 2u + (uint32_t)lane * 16u, 0, 2);
+                    walk8(v, (int)(fill - o) - lane * 8, base);
+                }
+                t = tn;
+                phys = pn;
+                fill = fn;
+            }
+            __syncthreads();
+            flush(cur_j);
+            if (c1 >= qe) break;
+            do {
+                ++cur_j;
+            } while (jst[cur_j + 1] <= jst[cur_j]);  // empty buckets are skipped
+            __syncthreads();
         }
-        __syncthreads();
-        flush(cur_j);
     }
     if (OUT) cnt::block_add(acc, sum);
 }
