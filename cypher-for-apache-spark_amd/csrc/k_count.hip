@@ -423,11 +423,18 @@ __global__ void __launch_bounds__(kB) k_rec_walk(const uint16_t* __restrict__ po
                 const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
                     const_cast<uint16_t*>(pool + (size_t)phys * kCh), (short)0,
                     (int)((fill * sizeof(uint16_t) + 15) & ~(size_t)15), 0x00020000);  // whole dwords: masked by lim
-                auto x = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)lane * 16u, 0, 2);
-                for (uint32_t o = 0; o < fill; o += 512) {  // wave-uniform
-                    const uint4 v = make_uint4(x[0], x[1], x[2], x[3]);
-                    if (o + 512 < fill) x = __builtin_amdgcn_raw_buffer_load_b128(rs, (o + 512) * 2u + (uint32_t)lane * 16u, 0, 2);
-                    walk8(v, (int)(fill - o) - lane * 8, base);
+                // two 512-record groups in flight per wave (one 16-byte load per lane each)
+                auto x0 = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)lane * 16u, 0, 2);
+                auto x1 = __builtin_amdgcn_raw_buffer_load_b128(rs, 1024u + (uint32_t)lane * 16u, 0, 2);
+                for (uint32_t o = 0; o < fill; o += 1024) {  // wave-uniform
+                    const uint4 v0 = make_uint4(x0[0], x0[1], x0[2], x0[3]);
+                    const uint4 v1 = make_uint4(x1[0], x1[1], x1[2], x1[3]);
+                    if (o + 1024 < fill) {
+                        x0 = __builtin_amdgcn_raw_buffer_load_b128(rs, (o + 1024) * 2u + (uint32_t)lane * 16u, 0, 2);
+                        x1 = __builtin_amdgcn_raw_buffer_load_b128(rs, (o + 1536) * 2u + (uint32_t)lane * 16u, 0, 2);
+                    }
+                    walk8(v0, (int)(fill - o) - lane * 8, base);
+                    if (o + 512 < fill) walk8(v1, (int)(fill - o) - 512 - lane * 8, base);
                 }
                 t = tn;
                 phys = pn;
