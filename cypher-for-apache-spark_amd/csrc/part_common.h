@@ -217,69 +217,72 @@ struct NoBegin {
 };
 
 // begin(j) runs (between barriers) before the first pair of each slice the block visits.
-// G chunks are loaded per step (the next group while the current one is visited): with many
-// buckets the chunks are only partly filled, and one chunk in flight per block left the walk
-// latency-bound.
+// Inside a slice visit each wave takes whole chunks from an LDS cursor and walks them 512 pairs at
+// a time (four 16-byte loads per lane, all issued before the pairs are visited), with the next
+// chunk's ids fetched ahead: a part-full chunk (most of them when the slices are many) costs its own
+// pairs, not a pass of the whole block.  Visits must not depend on the order of the pairs.
+// (G, the chunks in flight of the former block-per-chunk walk, is kept for the callers.)
 template <int BLK, int G = 1, class Visit, class Flush, class Begin = NoBegin>
 __device__ void walk_chunks(const ChunkWalk& cw, Visit visit, Flush flush, Begin begin = Begin()) {
-    static_assert(BLK * kItems == kCh, "a block loads one chunk per step");
+    constexpr int kLd = 4;                 // 16-byte loads per lane per step
+    constexpr uint32_t kStep = 64 * kLd * 2;  // pairs per wave step
+    __shared__ uint32_t qn;                // next chunk of the slice visit
     const int64_t w = blockIdx.x, blocks = gridDim.x;
     const SegSplit S(cw.jst, cw.nt, blocks);
     const int64_t qb = w * S.per, qe = min(qb + S.per, S.nch);
-    auto load_chunk = [&](int64_t q, uint2 (&pr)[kItems]) -> uint32_t {
-        if (q >= qe) return 0;
-        const uint32_t phys = cw.order[q];
-        const uint32_t fill = (uint32_t)(cw.meta[phys] >> 32);
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint2*>(cw.pool + (size_t)phys * kCh), (short)0, (int)(fill * sizeof(uint2)), 0x00020000);
-#pragma unroll
-        for (int k = 0; k < kItems / 2; ++k) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(k * BLK + (int)threadIdx.x) * 16u, 0, 2);  // nt
-            pr[2 * k] = make_uint2(v[0], v[1]);
-            pr[2 * k + 1] = make_uint2(v[2], v[3]);
-        }
-        return fill;
-    };
     if (qb >= qe) return;  // block-uniform
-    uint2 nx[G][kItems];
-    uint32_t nfill[G];
-#pragma unroll
-    for (int g = 0; g < G; ++g) nfill[g] = load_chunk(qb + g, nx[g]);
+    const int lane = threadIdx.x & 63;
+    auto grab = [&]() -> uint32_t {  // wave-uniform
+        uint32_t t = 0;
+        if (lane == 0) t = atomicAdd(&qn, 1u);
+        return __shfl(t, 0, 64);
+    };
     int cur_j = slice_of(cw.jst, cw.nt, qb);
-    int64_t j_end = cw.jst[cur_j + 1];  // chunk q belongs to a later slice once q >= j_end
-    begin(cur_j);
-    __syncthreads();
-    for (int64_t q0 = qb; q0 < qe; q0 += G) {  // block-uniform
-        uint2 pr[G][kItems];
-        uint32_t fill[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            fill[g] = nfill[g];
-#pragma unroll
-            for (int k = 0; k < kItems; ++k) pr[g][k] = nx[g][k];
+    for (;;) {  // block-uniform: one visit per slice of the share
+        const int64_t c0 = max(qb, cw.jst[cur_j]), c1 = min(qe, cw.jst[cur_j + 1]);
+        if (threadIdx.x == 0) qn = 0;
+        begin(cur_j);
+        __syncthreads();
+        const int j = cur_j;
+        uint32_t t = grab(), phys = 0, fill = 0;
+        if (c0 + t < c1) {
+            phys = cw.order[c0 + t];
+            fill = (uint32_t)(cw.meta[phys] >> 32);
         }
-#pragma unroll
-        for (int g = 0; g < G; ++g) nfill[g] = load_chunk(q0 + G + g, nx[g]);
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const int64_t q = q0 + g;
-            if (q >= qe) break;
-            int j = cur_j;
-            while (q >= j_end) j_end = cw.jst[++j + 1];  // empty slices are skipped
-            if (j != cur_j) {
-                __syncthreads();
-                flush(cur_j);
-                begin(j);
-                __syncthreads();
-                cur_j = j;
+        while (c0 + t < c1) {  // wave-uniform
+            const uint32_t tn = grab();
+            uint32_t pn = 0, fn = 0;
+            if (c0 + tn < c1) {
+                pn = cw.order[c0 + tn];
+                fn = (uint32_t)(cw.meta[pn] >> 32);
             }
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint2*>(cw.pool + (size_t)phys * kCh), (short)0, (int)(fill * sizeof(uint2)), 0x00020000);
+            for (uint32_t o = 0; o < fill; o += kStep) {  // wave-uniform
+                uint2 pr[2 * kLd];
 #pragma unroll
-            for (int k = 0; k < kItems; ++k)
-                if ((uint32_t)(2 * ((k >> 1) * BLK + (int)threadIdx.x) + (k & 1)) < fill[g]) visit(pr[g][k], j);
+                for (int k = 0; k < kLd; ++k) {
+                    const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+                        rs, (o + 2u * (uint32_t)(k * 64 + lane)) * 8u, 0, 2);  // nt
+                    pr[2 * k] = make_uint2(v[0], v[1]);
+                    pr[2 * k + 1] = make_uint2(v[2], v[3]);
+                }
+#pragma unroll
+                for (int k = 0; k < 2 * kLd; ++k)
+                    if (o + 2u * (uint32_t)((k >> 1) * 64 + lane) + (uint32_t)(k & 1) < fill) visit(pr[k], j);
+            }
+            t = tn;
+            phys = pn;
+            fill = fn;
         }
+        __syncthreads();
+        flush(cur_j);
+        if (c1 >= qe) break;
+        do {
+            ++cur_j;
+        } while (cw.jst[cur_j + 1] <= cw.jst[cur_j]);  // empty slices are skipped
+        __syncthreads();
     }
-    __syncthreads();
-    flush(cur_j);
 }
 
 // whether block w's chunk share holds all of slice j's chunks (then its flush owns the slice)
