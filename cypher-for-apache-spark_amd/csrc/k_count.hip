@@ -110,7 +110,12 @@ constexpr int kBits = 16;        // ids per bucket
 constexpr int kB = 1024;         // workgroup
 constexpr int kIT = 8;           // relationships per lane per tile
 constexpr int kT = kB * kIT;     // relationships per tile
-constexpr int kPiece = 16;       // records per 32-byte store
+#ifndef CAPSMI_REC_PIECE
+#define CAPSMI_REC_PIECE 16
+#endif
+constexpr int kPiece = CAPSMI_REC_PIECE;  // records per piece store (8 or 16: one or two 16-byte lanes)
+static_assert(kPiece == 8 || kPiece == 16, "a piece is one or two 16-byte lane stores");
+constexpr int kPieceLanes = kPiece / 8;
 constexpr int kCh = 8192;        // records per chunk (16 KiB; one 16-byte load per walk lane)
 constexpr int kMaxBuckets = 1024;  // per side
 constexpr int kBig = 255;        // OUT walk: values >= 0xFF00 per bucket kept exactly in LDS
@@ -216,9 +221,9 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
             pc[i] = npc * kPiece - (uint32_t)hc[i];  // a run item of rank >= this (signed) is held
         }
         __syncthreads();
-        // piece g: 2 lanes x 8 records; element e < held comes from the hold, the rest from the run
-        for (uint32_t x = threadIdx.x; x < P * 2; x += kB) {
-            const uint32_t g = x >> 1, r = x & 1;
+        // piece g: kPieceLanes lanes x 8 records; element e < held comes from the hold, the rest from the run
+        for (uint32_t x = threadIdx.x; x < P * kPieceLanes; x += kB) {
+            const uint32_t g = x / kPieceLanes, r = x % kPieceLanes;
             const int bk = owner[g];
             const uint32_t k = g - pb[bk], h = hc[bk];
             uint16_t v[8];
