@@ -110,6 +110,8 @@ _SIGS = {
     "capsmi_table_schema": (c_int32, [P, POINTER(c_int32), c_char_p, c_size_t, POINTER(c_int32), POINTER(c_int32),
                                       c_int32]),
     "capsmi_table_export": (c_int32, [P, c_int32, c_void_p, c_void_p, c_int64, c_int64]),
+    "capsmi_table_export_list": (c_int32, [P, c_int32, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64,
+                                           POINTER(c_int64)]),
     "capsmi_table_column_device_ptr": (c_int32, [P, c_int32, PP, PP]),
     "capsmi_cache": (c_int32, [P, PP]),
     "capsmi_select": (c_int32, [P, c_int32, STRS, PP]),

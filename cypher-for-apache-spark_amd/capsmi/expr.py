@@ -20,6 +20,7 @@ from typing import Callable, Sequence, Tuple, Union
 
 # physical types (include/capsmi.h)
 I64, BOOL, F64, STR = 0, 1, 2, 3
+LIST = 8  # list column of element type t: LIST + t (include/capsmi.h CAPSMI_LIST_*; Collect results)
 TYPE_NAMES = {I64: "I64", BOOL: "BOOL", F64: "F64", STR: "STR"}
 
 # expression opcodes (include/capsmi.h CAPSMI_X_*)

@@ -28,7 +28,7 @@ from typing import Dict, FrozenSet, List, Optional, Sequence, Tuple
 import numpy as np
 
 from .expr import (BOOL, F64, I64, STR, Ands, BinOp, Col, Expr, In, IsNotNull, IsNull, Lit, Not, Ors, ands, eq)
-from .table import ColumnData
+from .table import ColumnData, decode_value
 
 
 class PlanningError(RuntimeError):
@@ -420,7 +420,8 @@ def to_expr(spec, header: Sequence[str]) -> Expr:
 
 
 AGGS = {"count*": "count_star", "count": "count", "count_distinct": "count", "min": "min", "max": "max",
-        "sum": "sum", "avg": "avg"}
+        "sum": "sum", "avg": "avg", "collect": "collect", "collect_distinct": "collect"}
+DISTINCT_AGGS = ("count_distinct", "collect_distinct")
 
 
 # ---------------------------------------------------------------------------------------------
@@ -779,7 +780,22 @@ class Planner:
         computed = []
         for i, (alias, spec) in enumerate(items):
             kind = spec[0]
-            if kind == "rels":  # var-length list: keep the hop columns, assembled on the host
+            if kind == "entity":
+                # a node / relationship variable: every column it owns (RecordHeader.ownedBy,
+                # RecordHeader.scala:96-104) -- when aggregating these are all grouping keys, as
+                # DataFrameTable.group groups by header.ownedBy(var) (SparkTable.scala:128-133)
+                v = spec[1]
+                owned = [h for h in cur.header if h == v or h.startswith(v + ".") or h.startswith(v + ":")]
+                if v not in cur.header or not (v in cur.node_vars or v in cur.rel_vars):
+                    raise PlanningError(f"{v} is not a node or relationship variable")
+                parts = []
+                for h in owned:
+                    new = f"__ret{i}{h[len(v):]}"
+                    computed.append((Col(h), new))
+                    plain.append(new)
+                    parts.append((h[len(v):], new))
+                outs.append(("entity", alias, (v in cur.rel_vars, parts)))
+            elif kind == "rels":  # var-length list: keep the hop columns, assembled on the host
                 upper = varlen[spec[1]]
                 cols = []
                 for h in range(1, upper + 1):
@@ -796,7 +812,7 @@ class Planner:
                 if kind != "count*":
                     inp = f"__aggin{i}"
                     computed.append((to_expr(spec[1], cur.header), inp))
-                aggs.append((AGGS[kind], inp, kind == "count_distinct", name))
+                aggs.append((AGGS[kind], inp, kind in DISTINCT_AGGS, name))
                 outs.append(("col", alias, name))
             else:
                 name = f"__ret{i}"
@@ -823,21 +839,16 @@ class Planner:
 
 def result_rows(table, outs, dictionary) -> List[dict]:
     """Decode a RETURN table to Cypher-like values (strings decoded, var-length lists assembled as
-    [id, source, target, type] per relationship)."""
+    [id, source, target, type] per relationship, entities as CAPSNode / CAPSRelationship-like dicts:
+    {"id", "labels", "props"} / {"id", "src", "dst", "type", "props"}, null properties left out as
+    CAPSNode's property map leaves them out)."""
     cols = {c.name: c for c in table.to_columns()}
     n = table.size
 
     def val(c: ColumnData, r: int):
         if c.valid is not None and not c.valid[r]:
             return None
-        v = c.values[r]
-        if c.type == BOOL:
-            return bool(v)
-        if c.type == STR:
-            return dictionary.decode(int(v))
-        if c.type == F64:
-            return float(v)
-        return int(v)
+        return decode_value(c.type, c.values[r], dictionary)
 
     rows = []
     for r in range(n):
@@ -845,6 +856,8 @@ def result_rows(table, outs, dictionary) -> List[dict]:
         for kind, alias, spec in outs:
             if kind == "col":
                 row[alias] = val(cols[spec], r)
+            elif kind == "entity":
+                row[alias] = _entity_value(spec, {suf: val(cols[c], r) for suf, c in spec[1]})
             else:
                 lst = []
                 for h in range(0, len(spec), 4):
@@ -855,3 +868,15 @@ def result_rows(table, outs, dictionary) -> List[dict]:
                 row[alias] = lst
         rows.append(row)
     return rows
+
+
+def _entity_value(spec, vals: dict):
+    is_rel, _ = spec
+    if vals[""] is None:  # an OPTIONAL MATCH miss
+        return None
+    if is_rel:
+        props = {k[1:]: v for k, v in vals.items() if k.startswith(".") and not k.startswith(".__") and v is not None}
+        return {"id": vals[""], "src": vals[".__src"], "dst": vals[".__dst"], "type": vals[".__type"], "props": props}
+    labels = sorted(k[1:] for k, v in vals.items() if k.startswith(":") and v)
+    props = {k[1:]: v for k, v in vals.items() if k.startswith(".") and v is not None}
+    return {"id": vals[""], "labels": labels, "props": props}

@@ -17,15 +17,17 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib
-from .expr import BOOL, F64, I64, STR, Expr, compile_program, to_ctypes
+from .expr import BOOL, F64, I64, LIST, STR, Expr, compile_program, to_ctypes
 
 JOIN_TYPES = {"inner": 0, "left_outer": 1, "right_outer": 2, "full_outer": 3, "cross": 4}
-AGG_KINDS = {"count_star": 0, "count": 1, "min": 2, "max": 3, "sum": 4, "avg": 5}
+AGG_KINDS = {"count_star": 0, "count": 1, "min": 2, "max": 3, "sum": 4, "avg": 5, "collect": 6}
 
 
 @dataclass
 class ColumnData:
-    """Host column: ``values`` int64 (I64/BOOL/STR codes) or float64 (F64); ``valid`` bool mask or None."""
+    """Host column: ``values`` int64 (I64/BOOL/STR codes) or float64 (F64); ``valid`` bool mask or None.
+    A list column (type LIST + element type) holds one numpy array of element words per row (object
+    array; float64 elements for F64 lists)."""
     name: str
     type: int
     values: np.ndarray
@@ -36,6 +38,19 @@ class ColumnData:
         if self.type == F64:
             return np.ascontiguousarray(v.astype(np.float64)).view(np.int64)
         return np.ascontiguousarray(v.astype(np.int64))
+
+
+def decode_value(ty: int, v, dictionary):
+    """One exported value as a Python value (CypherValue analogue); lists element by element."""
+    if ty >= LIST:
+        return [decode_value(ty - LIST, x, dictionary) for x in v]
+    if ty == BOOL:
+        return bool(v)
+    if ty == STR:
+        return dictionary.decode(int(v))
+    if ty == F64:
+        return float(v)
+    return int(v)
 
 
 class StringDictionary:
@@ -335,6 +350,8 @@ class GpuTable:
         if n is None:
             n = size - offset
         ty = self.columnType[name]
+        if ty >= LIST:
+            return self._list_column(name, idx, ty, offset, n)
         vals = np.empty(n, dtype=np.int64)
         valid = np.empty(n, dtype=np.uint8)
         _lib.call("capsmi_table_export", self._h, idx, vals.ctypes.data if n else None,
@@ -344,6 +361,24 @@ class GpuTable:
         if ty == F64:
             vals = vals.view(np.float64)
         return ColumnData(name, ty, vals, valid.astype(bool) if nullable.value else None)
+
+    def _list_column(self, name: str, idx: int, ty: int, offset: int, n: int) -> ColumnData:
+        """A list column's rows (include/capsmi.h capsmi_table_export_list)."""
+        total = ctypes.c_int64()
+        _lib.call("capsmi_table_export_list", self._h, idx, offset, n, None, None, None, 0, ctypes.byref(total))
+        offs = np.empty(n + 1, dtype=np.int64)
+        valid = np.empty(max(1, n), dtype=np.uint8)
+        vals = np.empty(max(1, total.value), dtype=np.int64)
+        _lib.call("capsmi_table_export_list", self._h, idx, offset, n, offs.ctypes.data, valid.ctypes.data,
+                  vals.ctypes.data, len(vals), ctypes.byref(total))
+        if ty - LIST == F64:
+            vals = vals.view(np.float64)
+        rows = np.empty(n, dtype=object)
+        for i in range(n):
+            rows[i] = vals[offs[i]:offs[i + 1]]
+        nullable = ctypes.c_int32()
+        _lib.call("capsmi_table_column_nullable", self._h, idx, ctypes.byref(nullable))
+        return ColumnData(name, ty, rows, valid[:n].astype(bool) if nullable.value else None)
 
     def to_columns(self) -> List[ColumnData]:
         return [self.column(c) for c in self.physicalColumns]
@@ -359,16 +394,7 @@ class GpuTable:
                 if c.valid is not None and not c.valid[r]:
                     row[c.name] = None
                     continue
-                v = c.values[r]
-                if c.type == BOOL:
-                    v = bool(v)
-                elif c.type == STR:
-                    v = self.session.dictionary.decode(int(v))
-                elif c.type == F64:
-                    v = float(v)
-                else:
-                    v = int(v)
-                row[c.name] = v
+                row[c.name] = decode_value(c.type, c.values[r], self.session.dictionary)
             out.append(row)
         return out
 

@@ -249,6 +249,7 @@ void gather_into(capsmi_table* out, const capsmi_table* t, const Buf& idx, int64
         Column o;
         o.name = c.name;
         o.type = c.type;
+        o.list = c.list;  // list rows are indices into the same store
         o.data = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
         if (c.valid || may_miss) o.valid = dev_alloc(n > 0 ? n : 1, s);
         gather_col(c.d(), c.v(), P<int64_t>(idx), n, P<int64_t>(o.data), P<uint8_t>(o.valid), s->stream);
@@ -258,6 +259,7 @@ void gather_into(capsmi_table* out, const capsmi_table* t, const Buf& idx, int64
 
 KeyCols key_cols(const capsmi_table* t, const std::vector<int>& idx) {
     REQUIRE((int)idx.size() <= kMaxKeys, CAPSMI_ERR_NOT_IMPLEMENTED, "more than 8 key columns");
+    for (int i : idx) no_list_key(t->cols[i].type, t->cols[i].name, "a key");
     KeyCols k;
     k.n = (int)idx.size();
     for (int i = 0; i < kMaxKeys; ++i) {
@@ -273,6 +275,7 @@ KeyCols key_cols(const capsmi_table* t, const std::vector<int>& idx) {
 // folded columns alive while the returned KeyCols is in use.
 KeyCols group_key_cols(capsmi_session* s, const capsmi_table* t, const std::vector<int>& idx, std::vector<Buf>& hold) {
     if ((int)idx.size() <= kMaxKeys) return key_cols(t, idx);
+    for (int i : idx) no_list_key(t->cols[i].type, t->cols[i].name, "a key");
     KeyCols k;
     size_t next = 0;
     const int64_t* folded = nullptr;
@@ -426,6 +429,7 @@ Buf order_perm(capsmi_table* t, const std::vector<int>& keys, const std::vector<
     Buf kbuf = dev_alloc(sizeof(uint64_t) * n, s);
     for (int k = (int)keys.size() - 1; k >= 0; --k) {
         const Column& c = t->cols[keys[k]];
+        no_list_key(c.type, c.name, "a sort key");
         order_keys(s, c.d(), c.v(), c.type, desc[k] != 0, false, P<int64_t>(perm), n, P<uint64_t>(kbuf));
         radix_sort_pairs(s, P<uint64_t>(kbuf), P<int64_t>(perm), n, 0, 64);
         if (c.valid) {
@@ -766,6 +770,51 @@ capsmi_status capsmi_table_export(const capsmi_table* t, int32_t col, void* host
     API_END
 }
 
+capsmi_status capsmi_table_export_list(const capsmi_table* t, int32_t col, int64_t offset, int64_t n,
+                                       int64_t* host_offsets, uint8_t* host_valid, void* host_values,
+                                       int64_t values_cap, int64_t* nvalues) {
+    API_BEGIN
+    need(t, "table");
+    need(nvalues, "nvalues");
+    M(t);
+    REQUIRE(col >= 0 && col < (int)t->cols.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT, "column index out of range");
+    REQUIRE(offset >= 0 && n >= 0 && offset + n <= t->nrows, CAPSMI_ERR_ILLEGAL_ARGUMENT, "export range out of bounds");
+    const Column& c = t->cols[col];
+    REQUIRE(is_list_type(c.type) && c.list, CAPSMI_ERR_ILLEGAL_ARGUMENT, "column '" + c.name + "' is not a list column");
+    use_device(t->sess);
+    hipStream_t st = t->sess->stream;
+    const ListStore& L = *c.list;
+    // the rows' list indices and validity, then the store's offsets and values (one round trip)
+    std::vector<int64_t> idx(n), off(L.nlists + 1), vals(L.nvalues);
+    std::vector<uint8_t> ok(n, 1);
+    if (n) HIP_CHECK(hipMemcpyAsync(idx.data(), c.d() + offset, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
+    if (n && c.valid) HIP_CHECK(hipMemcpyAsync(ok.data(), c.v() + offset, n, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipMemcpyAsync(off.data(), P<int64_t>(L.offsets), sizeof(int64_t) * (L.nlists + 1), hipMemcpyDeviceToHost, st));
+    if (L.nvalues)
+        HIP_CHECK(hipMemcpyAsync(vals.data(), P<int64_t>(L.values), sizeof(int64_t) * L.nvalues, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    int64_t total = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (!ok[i]) continue;
+        REQUIRE(idx[i] >= 0 && idx[i] < L.nlists, CAPSMI_ERR_INTERNAL, "list row index out of range");
+        total += off[idx[i] + 1] - off[idx[i]];
+    }
+    *nvalues = total;
+    if (!host_values) return CAPSMI_OK;
+    need(host_offsets, "host_offsets");
+    REQUIRE(values_cap >= total, CAPSMI_ERR_ILLEGAL_ARGUMENT, "list value buffer too small");
+    int64_t* out = static_cast<int64_t*>(host_values);
+    int64_t pos = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        host_offsets[i] = pos;
+        if (host_valid) host_valid[i] = ok[i];
+        if (!ok[i]) continue;
+        for (int64_t k = off[idx[i]]; k < off[idx[i] + 1]; ++k) out[pos++] = vals[k];
+    }
+    host_offsets[n] = pos;
+    API_END
+}
+
 capsmi_status capsmi_table_column_device_ptr(const capsmi_table* t, int32_t col, const void** data,
                                              const uint8_t** valid) {
     API_BEGIN
@@ -937,6 +986,15 @@ capsmi_status eager_union_all(capsmi_table* a, capsmi_table* b, capsmi_table** o
         if (b->nrows)
             HIP_CHECK(hipMemcpyAsync(P<int64_t>(c.data) + a->nrows, y.d(), sizeof(int64_t) * b->nrows,
                                      hipMemcpyDeviceToDevice, s->stream));
+        if (is_list_type(x.type)) {
+            REQUIRE(x.list && y.list, CAPSMI_ERR_INTERNAL, "list column without a store");
+            // lists of both sides in one store: b's lists follow a's, b's row indices shift by a's list count
+            c.list = x.list;
+            if (x.list != y.list) {
+                c.list = concat_lists(s, *x.list, *y.list);
+                add_i64(P<int64_t>(c.data) + a->nrows, x.list->nlists, b->nrows, s->stream);
+            }
+        }
         if (x.valid || y.valid) {
             c.valid = dev_alloc(n > 0 ? n : 1, s);
             if (x.valid) { if (a->nrows) HIP_CHECK(hipMemcpyAsync(P<uint8_t>(c.valid), x.v(), a->nrows, hipMemcpyDeviceToDevice, s->stream)); }
@@ -1064,6 +1122,7 @@ capsmi_status eager_group(capsmi_table* t, int32_t nby, const char* const* by, i
         c.data = dev_alloc(sizeof(int64_t) * ng, s);
         const Column* in = nullptr;
         if (ag.kind != CAPSMI_AGG_COUNT_STAR) in = &t->cols[col_index(t, ag.input)];
+        if (in && !(ag.kind == CAPSMI_AGG_COUNT && !ag.distinct)) no_list_key(in->type, in->name, "an aggregate input");
         switch (ag.kind) {
             case CAPSMI_AGG_COUNT_STAR:
                 c.type = CAPSMI_I64;
@@ -1132,6 +1191,13 @@ capsmi_status eager_group(capsmi_table* t, int32_t nby, const char* const* by, i
                 agg_count(P<int64_t>(gid), in->v(), n, P<int64_t>(cnt), st);
                 avg_finish(P<double>(sum), P<int64_t>(cnt), ng, in->type == CAPSMI_I64, P<int64_t>(c.data),
                            P<uint8_t>(c.valid), st);
+                break;
+            }
+            case CAPSMI_AGG_COLLECT: {
+                // sort_array(collect_list / collect_set): row g of the result is list g of the store
+                c.type = CAPSMI_LIST + in->type;
+                c.list = collect_lists(s, P<int64_t>(gid), ng, in->d(), in->v(), in->type, n, ag.distinct != 0);
+                iota_i64(P<int64_t>(c.data), 0, ng, st);
                 break;
             }
             default:
@@ -2095,6 +2161,7 @@ capsmi_status capsmi_table_fingerprint(capsmi_table* t, int32_t ncols, const cha
     std::vector<const int64_t*> d;
     std::vector<const uint8_t*> v;
     for (int i : idx) {
+        no_list_key(t->cols[i].type, t->cols[i].name, "a fingerprint column");
         d.push_back(t->cols[i].d());
         v.push_back(t->cols[i].v());
     }

@@ -56,11 +56,23 @@ Buf dev_alloc(size_t bytes, capsmi_session* s);
 template <class T>
 inline T* P(const Buf& b) { return b ? static_cast<T*>(b->ptr) : nullptr; }
 
+// Values of a list column (CAPSMI_LIST_*): list k holds values[offsets[k] .. offsets[k+1]).  A list
+// column's row word is the index k of its list, so gathers (filter, join, order, union) move list
+// rows like any other column and the store rides along by reference.
+struct ListStore {
+    int32_t elem = CAPSMI_I64;  // element type
+    int64_t nlists = 0, nvalues = 0;
+    Buf offsets;                // int64, nlists + 1
+    Buf values;                 // int64 words, nvalues
+};
+inline bool is_list_type(int32_t t) { return t >= CAPSMI_LIST_I64 && t <= CAPSMI_LIST_STR; }
+
 struct Column {
     std::string name;
     int32_t type = CAPSMI_I64;
     Buf data;              // int64 words
     Buf valid;             // uint8 per row, may be null (no nulls)
+    std::shared_ptr<const ListStore> list;  // list columns only
     int64_t offset = 0;    // row offset into data/valid (zero-copy skip)
     bool lazy_nullable = false;  // schema of a lazy table's column (no data yet): may hold nulls
     // host copy of the words of a column built from host values (the fused routes' count rows):
@@ -233,6 +245,14 @@ void agg_minmax(const int64_t* gid, const int64_t* v, const uint8_t* valid, int6
 void avg_finish(const double* sum, const int64_t* cnt, int64_t ng, bool to_i64, int64_t* out, uint8_t* valid,
                 hipStream_t st);
 void minmax_finish(int64_t* v, int type, bool is_max, int64_t ng, hipStream_t st);
+// Collect (k_list.hip): sort_array(collect_list / collect_set) of column (v, valid) per group id
+// (ng groups) into a list store
+std::shared_ptr<ListStore> collect_lists(capsmi_session* s, const int64_t* gid, int64_t ng, const int64_t* v,
+                                         const uint8_t* valid, int type, int64_t n, bool distinct);
+// one store holding a's lists, then b's (b's list k becomes a.nlists + k)
+std::shared_ptr<ListStore> concat_lists(capsmi_session* s, const ListStore& a, const ListStore& b);
+// REQUIRE(!is_list_type) for a column used as a key / expression operand
+void no_list_key(int32_t type, const std::string& name, const char* what);
 // radix-partitioned equi-join (k_rjoin.hip): (probe row, build row) pairs grouped by key-hash
 // partition; build row -1 for an unmatched or null-key probe row when `outer`.  Returns #pairs.
 int64_t radix_join(capsmi_session* s, const KeyCols& bk, int64_t nb, const KeyCols& pk, int64_t np, bool outer,

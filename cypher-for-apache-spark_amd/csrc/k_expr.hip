@@ -311,6 +311,7 @@ void validate_program(const capsmi_table* t, int32_t nn, const capsmi_expr* prog
                 REQUIRE(x.arg >= 0 && x.arg < (int)t->cols.size(), CAPSMI_ERR_ILLEGAL_ARGUMENT,
                         "expression column index out of range");
                 REQUIRE(x.arg < kMaxCols, CAPSMI_ERR_NOT_IMPLEMENTED, "expression references column >= 64");
+                if (nn > 1) no_list_key(t->cols[x.arg].type, t->cols[x.arg].name, "an expression operand");
                 pops = 0; break;
             case CAPSMI_X_LIT: case CAPSMI_X_NULL: pops = 0; break;
             case CAPSMI_X_NOT: case CAPSMI_X_ISNULL: case CAPSMI_X_ISNOTNULL: case CAPSMI_X_NEG: pops = 1; break;

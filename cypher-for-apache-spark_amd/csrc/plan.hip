@@ -1575,6 +1575,8 @@ capsmi_status capsmi_join(capsmi_table* l, capsmi_table* r, int32_t join_type, i
             for (int i = 0; i < npairs; ++i) {
                 const int a = col_of(l, lcols[i]), b = col_of(r, rcols[i]);
                 const int ta = l->cols[a].type, tb = r->cols[b].type;
+                no_list_key(ta, l->cols[a].name, "a join key");
+                no_list_key(tb, r->cols[b].name, "a join key");
                 const bool na = ta == CAPSMI_I64 || ta == CAPSMI_F64, nb = tb == CAPSMI_I64 || tb == CAPSMI_F64;
                 REQUIRE(ta == tb || (na && nb), CAPSMI_ERR_ILLEGAL_ARGUMENT,
                         "join key types differ: " + l->cols[a].name + " vs " + r->cols[b].name);
@@ -1617,7 +1619,8 @@ capsmi_status capsmi_order_by(capsmi_table* t, int32_t nkeys, const char* const*
         p->kind = PlanNode::ORDER;
         hold(*p, t);
         for (int i = 0; i < nkeys; ++i) {
-            (void)col_of(t, cols[i]);
+            const int c = col_of(t, cols[i]);
+            no_list_key(t->cols[c].type, t->cols[c].name, "a sort key");
             p->a.push_back(cols[i]);
             p->flags.push_back(descending ? descending[i] : 0);
         }
@@ -1656,6 +1659,7 @@ capsmi_status capsmi_limit(capsmi_table* t, int64_t n, capsmi_table** out) {
 
 capsmi_status capsmi_distinct(capsmi_table* t, capsmi_table** out) {
     return build(t, out, [&] {
+        for (auto& c : t->cols) no_list_key(c.type, c.name, "a distinct key");
         auto p = std::make_shared<PlanNode>();
         p->kind = PlanNode::DISTINCT;
         hold(*p, t);
@@ -1671,7 +1675,8 @@ capsmi_status capsmi_distinct_on(capsmi_table* t, int32_t ncols, const char* con
         p->kind = PlanNode::DISTINCT_ON;
         hold(*p, t);
         for (int i = 0; i < ncols; ++i) {
-            (void)col_of(t, cols[i]);
+            const int c = col_of(t, cols[i]);
+            no_list_key(t->cols[c].type, t->cols[c].name, "a distinct key");
             p->a.push_back(cols[i]);
         }
         std::vector<Column> sch;
@@ -1690,6 +1695,7 @@ capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, 
         std::vector<Column> sch;
         for (int i = 0; i < nby; ++i) {
             const int c = col_of(t, by[i]);
+            no_list_key(t->cols[c].type, t->cols[c].name, "a grouping key");
             p->a.push_back(by[i]);
             sch.push_back(schema_of(t->cols[c]));
         }
@@ -1716,9 +1722,17 @@ capsmi_status capsmi_group(capsmi_table* t, int32_t nby, const char* const* by, 
                 }
                 case CAPSMI_AGG_MIN: case CAPSMI_AGG_MAX: {
                     const Column& c = t->cols[col_of(t, ag.input)];
+                    no_list_key(c.type, c.name, "an aggregate input");
                     sp.input = c.name;
                     ty = c.type;
                     nullable = true;
+                    break;
+                }
+                case CAPSMI_AGG_COLLECT: {  // sort_array(collect_list / collect_set), SparkTable.scala:169-177
+                    const Column& c = t->cols[col_of(t, ag.input)];
+                    no_list_key(c.type, c.name, "an aggregate input");
+                    sp.input = c.name;
+                    ty = CAPSMI_LIST + c.type;
                     break;
                 }
                 default: throw Error(CAPSMI_ERR_NOT_IMPLEMENTED, "Aggregation function " + std::to_string(ag.kind));

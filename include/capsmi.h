@@ -61,6 +61,20 @@ enum {
     CAPSMI_STR = 3   /* CTString, dictionary code */
 };
 
+/* List columns (CTList(elem)): the result of a Collect aggregator (SparkTable.scala:169-177,
+ * functions.sort_array(collect_list / collect_set)).  The column type is CAPSMI_LIST + element type
+ * (CAPSMI_LIST_I64 ... CAPSMI_LIST_STR); rows are read with capsmi_table_export_list.  List columns
+ * travel through select / drop / rename / filter / join payloads / union all / order-by payloads /
+ * skip / limit; using one as a join, grouping, distinct or sort key, or inside an expression, is
+ * CAPSMI_ERR_NOT_IMPLEMENTED. */
+enum {
+    CAPSMI_LIST = 8,
+    CAPSMI_LIST_I64 = 8,
+    CAPSMI_LIST_BOOL = 9,
+    CAPSMI_LIST_F64 = 10,
+    CAPSMI_LIST_STR = 11
+};
+
 /* Input-only value widths of capsmi_col_desc.type: widened at ingest the way
  * DataFrameOps.withCypherCompatibleTypes lifts Spark columns (spark-cypher/.../impl/DataFrameOps.scala:185-198,
  * SparkConversions.scala:162-168): Byte/Short/Integer -> Long, Float -> Double; a Boolean byte -> BOOL. */
@@ -147,7 +161,10 @@ enum {
     CAPSMI_AGG_MIN = 2,        /*                               SparkTable.scala:163-164 */
     CAPSMI_AGG_MAX = 3,        /*                               SparkTable.scala:160-161 */
     CAPSMI_AGG_SUM = 4,        /*                               SparkTable.scala:166-167 */
-    CAPSMI_AGG_AVG = 5         /* avg -> F64                    SparkTable.scala:141-146 */
+    CAPSMI_AGG_AVG = 5,        /* avg -> F64                    SparkTable.scala:141-146 */
+    CAPSMI_AGG_COLLECT = 6     /* sort_array(collect_list) / sort_array(collect_set) when `distinct`:
+                                  the group's non-null values in ascending order, a list column
+                                  (an empty list for a group without values)  SparkTable.scala:169-177 */
 };
 
 typedef struct {
@@ -231,6 +248,15 @@ capsmi_status capsmi_table_schema(const capsmi_table* t, int32_t* ncols, char* n
  * copies rows [offset, offset+n) of one column to the host; host_valid may be NULL */
 capsmi_status capsmi_table_export(const capsmi_table* t, int32_t col, void* host_data, uint8_t* host_valid,
                                   int64_t offset, int64_t n);
+/* rows [offset, offset+n) of a list column (CAPSMI_LIST_*) to the host: row i's elements are
+ * host_values[host_offsets[i] .. host_offsets[i+1]) (host_offsets has n + 1 entries; a null row is
+ * empty with host_valid[i] = 0; host_valid may be NULL).  *nvalues = the number of elements of the
+ * range; host_values == NULL only reports it (host_offsets may then be NULL too); otherwise
+ * values_cap must be >= *nvalues, else ILLEGAL_ARGUMENT.  Elements are 8-byte words of the element
+ * type.  (CAPSRecords.collect of a CTList column, rowToCypherMap.scala) */
+capsmi_status capsmi_table_export_list(const capsmi_table* t, int32_t col, int64_t offset, int64_t n,
+                                       int64_t* host_offsets, uint8_t* host_valid, void* host_values,
+                                       int64_t values_cap, int64_t* nvalues);
 /* zero-copy device view of a column (valid pointer NULL when the column has no nulls) */
 capsmi_status capsmi_table_column_device_ptr(const capsmi_table* t, int32_t col, const void** data,
                                              const uint8_t** valid);

@@ -66,6 +66,17 @@ def eval_expr(spec, b: dict, g: Graph):
         return ent["props"].get(spec[2]) if ent else None
     if op in ("var", "id"):
         return b.get(spec[1])
+    if op == "entity":  # CAPSNode / CAPSRelationship value (null properties left out)
+        v = b.get(spec[1])
+        if v is None:
+            return None
+        if b.get("__kind_" + spec[1]) == "rel":
+            r = g.rels[v]
+            return {"id": v, "src": r["src"], "dst": r["dst"], "type": r["type"],
+                    "props": {k: x for k, x in sorted(r["props"].items()) if x is not None}}
+        n = g.nodes[v]
+        return {"id": v, "labels": sorted(n["labels"]),
+                "props": {k: x for k, x in sorted(n["props"].items()) if x is not None}}
     if op == "type":
         v = b.get(spec[1])
         return None if v is None else g.rels[v]["type"]
@@ -282,7 +293,8 @@ def _var_paths(g: Graph, start: int, rel: RelPat, lower: int, upper: int, prior:
 
 def project(g: Graph, rows: List[dict], ret: dict) -> List[dict]:
     items = ret["items"]
-    aggs = [(a, s) for a, s in items if s[0] in ("count*", "count", "count_distinct", "min", "max", "sum", "avg")]
+    aggs = [(a, s) for a, s in items
+            if s[0] in ("count*", "count", "count_distinct", "min", "max", "sum", "avg", "collect", "collect_distinct")]
     plain = [(a, s) for a, s in items if (a, s) not in aggs]
 
     def plain_val(s, b):
@@ -325,6 +337,10 @@ def project(g: Graph, rows: List[dict], ret: dict) -> List[dict]:
                 row[a] = len(vals)
             elif s[0] == "count_distinct":
                 row[a] = len(set(vals))
+            elif s[0] == "collect":  # sort_array(collect_list), SparkTable.scala:169-177
+                row[a] = sorted(vals)
+            elif s[0] == "collect_distinct":  # sort_array(collect_set)
+                row[a] = sorted(set(vals))
             elif s[0] == "min":
                 row[a] = min(vals) if vals else None
             elif s[0] == "max":

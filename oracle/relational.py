@@ -13,8 +13,8 @@ documented behaviour as CAPS relies on it):
   join: inner/outer/cross, `===` never matches null      SparkTable.scala:205-229
   unionAll: positional, types must match                 SparkTable.scala:190-203
   distinct / dropDuplicates: nulls group together        SparkTable.scala:231-235
-  group: count(lit 0), count, countDistinct (nulls ignored), min, max, sum, avg
-                                                         SparkTable.scala:121-188
+  group: count(lit 0), count, countDistinct (nulls ignored), min, max, sum, avg,
+         collect / collect(DISTINCT) as sorted lists     SparkTable.scala:121-188
   orderBy: ASC nulls first, DESC nulls last              SparkTable.scala:94-103
 Tables here are plain numpy columns; the implementation deliberately shares nothing with the
 device code (sort/searchsorted joins instead of hash tables, np.unique instead of hashing).
@@ -27,6 +27,7 @@ from typing import List, Sequence, Tuple
 import numpy as np
 
 I64, BOOL, F64, STR = 0, 1, 2, 3
+LIST = 8  # list of element type t: LIST + t (Collect results; one numpy array per row)
 
 
 class OracleError(RuntimeError):
@@ -167,7 +168,8 @@ class NumpyTable:
             if ty < 0:
                 ty = getattr(e, "type", -1)
                 ty = ty if ty is not None and ty >= 0 else I64
-            vals = vals.astype(np.float64 if ty == F64 else np.int64)
+            if ty < LIST:  # a list column is only ever aliased
+                vals = vals.astype(np.float64 if ty == F64 else np.int64)
             out[name] = Col_(ty, vals, valid)
         return self._new(out, self.n)
 
@@ -237,6 +239,17 @@ class NumpyTable:
                 continue
             c = self.cols[inp]
             m = c.valid
+            if kind == "collect":  # sort_array(collect_list / collect_set), SparkTable.scala:169-177
+                lists = np.empty(ng, dtype=object)
+                for k in range(ng):
+                    v = c.values[m & (gid == k)]
+                    if distinct:  # collect_set: equal 64-bit words are one value
+                        v = np.unique(v.view(np.int64)).view(v.dtype) if len(v) else v
+                    lists[k] = np.sort(v, kind="stable")
+                out[name] = Col_(LIST + c.type, lists, np.ones(ng, dtype=bool))
+                continue
+            if c.type >= LIST:
+                raise OracleError(f"aggregate {kind} over a list column")
             if kind == "count":
                 if distinct:
                     sel = np.nonzero(m)[0]
@@ -302,6 +315,8 @@ def _verify_entity(t: NumpyTable, keys, flags):
 def _key_matrix(cols: Sequence[Col_], n: int, with_nulls: bool) -> np.ndarray:
     parts = []
     for c in cols:
+        if c.type >= LIST:
+            raise OracleError("list column as a key")
         v = c.values.view(np.int64) if c.values.dtype == np.float64 else c.values
         if with_nulls:
             parts.append(np.where(c.valid, v, 0))

@@ -34,6 +34,8 @@ def _norm(v):
         return ("b", v)
     if isinstance(v, list):
         return ("l", tuple(_norm(x) for x in v))
+    if isinstance(v, dict):  # node / relationship values
+        return ("d", tuple(sorted((k, _norm(x)) for k, x in v.items())))
     return ("v", v)
 
 

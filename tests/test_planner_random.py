@@ -33,6 +33,16 @@ QUERIES = [
      "return": {"items": [["a", ID("a")], ["b", ID("b")]]}},
     {"clauses": [{"match": "(a)-[r]->(c), (b)-->(d)", "where": ["and", ["=", V("b"), V("c")], ["<", V("a"), V("d")]]}],
      "return": {"items": [["a", ID("a")], ["r", ID("r")], ["b", ID("b")], ["d", ID("d")]]}},
+    # entity values; grouping by an entity variable groups by every column it owns
+    # (SparkTable.scala:128-133 header.ownedBy) -- and collect / collect(DISTINCT) (:169-177)
+    {"clauses": [{"match": "(a)-[r]->(b)"}],
+     "return": {"items": [["a", ["entity", "a"]], ["n", ["count*"]], ["bs", ["collect", ID("b")]]]}},
+    {"clauses": [{"match": "(a:A)-[r:R]-(b)"}],
+     "return": {"items": [["r", ["entity", "r"]], ["vs", ["collect_distinct", V("b")]], ["m", ["max", V("a")]]]}},
+    {"clauses": [{"match": "(a:A)"}, {"optional_match": "(a)-[s:S]->(b)"}],
+     "return": {"items": [["a", ["entity", "a"]], ["s", ["entity", "s"]], ["b", ["entity", "b"]]]}},
+    {"clauses": [{"match": "(a)-->(b)-->(c)"}],
+     "return": {"items": [["b", ["entity", "b"]], ["cs", ["collect_distinct", ID("c")]], ["vs", ["collect", V("a")]]]}},
 ]
 
 
@@ -80,3 +90,29 @@ def test_planner_matches_enumeration(backend, seed):
         got = result_rows(table, outs, backend.dictionary)
         want = en.project(graph, en.match(graph, q), q["return"])
         assert same_rows(got, want), (q, got, want)
+
+
+@pytest.mark.parametrize("backend", BACKENDS, indirect=True)
+def test_entity_grouping_keeps_owned_columns(backend):
+    """Node id 0 sits in two node tables (labels {A} and {B}, different `v`): a label-free node scan
+    yields it twice (ScanGraph.scala:72-76), and grouping by the variable groups by every column it
+    owns -- id, label flags, properties (SparkTable.scala:128-133) -- so the two rows stay two groups
+    (grouping by the id column alone would merge them into one group of 2)."""
+    from capsmi.expr import BOOL, I64
+    from capsmi.planner import ID as IDC, EntityTable, Planner, ScanGraph, result_rows
+    from capsmi.table import ColumnData
+    A = backend.table([ColumnData(IDC, I64, np.array([0, 1])), ColumnData("v", I64, np.array([10, 11]))])
+    B = backend.table([ColumnData(IDC, I64, np.array([0])), ColumnData("v", I64, np.array([20]))])
+    nodes = [EntityTable("node", frozenset({"A"}), {"v": I64}, A.as_node_table(IDC)),
+             EntityTable("node", frozenset({"B"}), {"v": I64}, B.as_node_table(IDC))]
+    sg = ScanGraph(backend, nodes, [])
+    q = {"clauses": [{"match": "(a)"}], "return": {"items": [["a", ["entity", "a"]], ["n", ["count*"]]]}}
+    table, outs = Planner(sg).run(q)
+    got = result_rows(table, outs, backend.dictionary)
+    want = [{"a": {"id": 0, "labels": ["A"], "props": {"v": 10}}, "n": 1},
+            {"a": {"id": 0, "labels": ["B"], "props": {"v": 20}}, "n": 1},
+            {"a": {"id": 1, "labels": ["A"], "props": {"v": 11}}, "n": 1}]
+    assert same_rows(got, want), got
+    q2 = {"clauses": [{"match": "(a)"}], "return": {"items": [["a", ID("a")], ["n", ["count*"]]]}}
+    table, outs = Planner(sg).run(q2)  # grouping by id(a), an expression: one group per id
+    assert same_rows(result_rows(table, outs, backend.dictionary), [{"a": 0, "n": 2}, {"a": 1, "n": 1}])
