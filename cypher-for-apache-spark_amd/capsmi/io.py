@@ -12,7 +12,7 @@ device.
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Optional, Tuple
 
 import numpy as np
 
@@ -23,10 +23,11 @@ NODE_LABEL = "V"
 REL_TYPE = "E"
 
 
-def read_edge_list(path: str, delimiter: str = " ", comment: str = "#") -> Tuple[np.ndarray, np.ndarray]:
-    """Host arrays of an edge-list file (vectorised C parser; the device path is edge_list_graph)."""
+def read_edge_list(path: str, delimiter: Optional[str] = " ", comment: str = "#") -> Tuple[np.ndarray, np.ndarray]:
+    """Host arrays of an edge-list file (vectorised C parser; the device path is edge_list_graph).
+    ``delimiter`` None: whitespace-separated."""
     import pandas as pd
-    sep = r"\s+" if delimiter == " " else delimiter
+    sep = r"\s+" if delimiter is None else delimiter
     df = pd.read_csv(path, sep=sep, comment=comment or None, header=None, usecols=[0, 1], dtype=np.int64,
                      engine="c")
     return df[0].to_numpy(np.int64), df[1].to_numpy(np.int64)
@@ -49,7 +50,8 @@ def _graph_of(session: Session, rels: GpuTable) -> Tuple[GpuTable, GpuTable]:
     return nodes, rels
 
 
-def edge_list_graph(session: Session, path: str, delimiter: str = " ", comment: str = "#") -> Tuple[GpuTable, GpuTable]:
+def edge_list_graph(session: Session, path: str, delimiter: Optional[str] = " ",
+                    comment: str = "#") -> Tuple[GpuTable, GpuTable]:
     """EdgeListDataSource.graph: the file parsed by libcapsmi's native CSV reader (host threads), rel ids
     = row numbers, nodes = distinct endpoints on the device."""
     rels = session.read_csv([path], ["source", "target"], [I64, I64], delimiter, comment, row_id_col="id")

@@ -169,18 +169,20 @@ class Session:
     def encode_str(self, s: str) -> int:
         return self.dictionary.encode(s)
 
-    def read_csv(self, paths: Sequence[str], names: Sequence[str], types: Sequence[int], delimiter: str = ",",
+    def read_csv(self, paths: Sequence[str], names: Sequence[str], types: Sequence[int], delimiter: Optional[str] = ",",
                  comment: Optional[str] = None, row_id_col: Optional[str] = None) -> "GpuTable":
         """DataFrameReader.csv with an explicit schema, parsed natively by host threads into a device
-        table (include/capsmi.h capsmi_read_csv).  String fields are encoded with this session's
-        dictionary."""
+        table (include/capsmi.h capsmi_read_csv).  ``delimiter`` is Spark's one-character ``sep``;
+        None opts in to whitespace splitting (runs of blanks).  String fields are encoded with this
+        session's dictionary."""
         def intern(_ctx, ptr, n):
             return self.dictionary.encode(ctypes.string_at(ptr, n).decode("utf-8"))
 
         cb = _lib.INTERN_FN(intern)
         tys = (ctypes.c_int32 * max(1, len(types)))(*types)
         out = ctypes.c_void_p()
-        _lib.call("capsmi_read_csv", self._h, len(paths), _lib.strs(list(paths)), delimiter.encode()[:1],
+        _lib.call("capsmi_read_csv", self._h, len(paths), _lib.strs(list(paths)),
+                  b"\0" if delimiter is None else delimiter.encode()[:1],
                   (comment or "\0").encode()[:1], len(names), _lib.strs(list(names)), tys, cb, None,
                   row_id_col.encode() if row_id_col else None, ctypes.byref(out))
         return GpuTable(self, out)

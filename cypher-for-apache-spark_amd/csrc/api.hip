@@ -1894,6 +1894,8 @@ capsmi_status capsmi_words_popcount_device(capsmi_session* s, const uint32_t* wo
 
 struct capsmi_count_shard {
     capsmi::CountRec cr;
+    capsmi::Buf b_words;    // b_ok's words, read by finish: kept alive with the handle
+    bool finished = false;  // finish adds into the handle's accumulator once
 };
 
 capsmi_status capsmi_count_shard_begin(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
@@ -1925,6 +1927,7 @@ capsmi_status capsmi_count_shard_begin(capsmi_session* s, int32_t nrels, capsmi_
         ms.push_back(rels[i]->nrows);
     }
     auto h = std::make_unique<capsmi_count_shard>();
+    h->b_words = b_ok->words;
     count_rec_begin(s, srcs.data(), dsts.data(), ms.data(), nrels, a_ok, b_ok, c_ok, h->cr);
     count_rec_fold(h->cr, own_lo, own_hi, owned_in);
     *out = h.release();
@@ -1936,13 +1939,17 @@ capsmi_status capsmi_count_shard_finish(capsmi_count_shard* h, const uint32_t* i
     need(h, "count shard");
     need(in_all, "in_all");
     need(dev_out, "dev_out");
+    REQUIRE(!h->finished, CAPSMI_ERR_ILLEGAL_ARGUMENT, "count shard: finish called twice on one handle");
     use_device(h->cr.s);
     count_rec_finish(h->cr, in_all, dev_out);
+    h->finished = true;
     API_END
 }
 
 capsmi_status capsmi_count_shard_release(capsmi_count_shard* h) {
     API_BEGIN
+    if (!h) return CAPSMI_OK;
+    use_device(h->cr.s);
     delete h;
     API_END
 }

@@ -42,7 +42,7 @@ int n_threads() {
 inline bool blank(char c) { return c == ' ' || c == '\t'; }
 
 // One field at p (line end le).  Quoted fields drop their quotes; "" and \" inside them are one
-// quote (copied to `tmp`).  With collapse (delimiter ' '), runs of blanks separate fields.
+// quote (copied to `tmp`).  With collapse (delimiter 0, an opt-in), runs of blanks separate fields.
 // On return p is past the field and its delimiter, `more` tells whether another field follows;
 // false on a malformed (unterminated / trailing-garbage) quoted field.
 bool next_field(const char*& p, const char* le, char delim, bool collapse, const char*& fb, const char*& fe,
@@ -109,7 +109,7 @@ bool next_field(const char*& p, const char* le, char delim, bool collapse, const
 void parse_chunk(Chunk& c, const char* file_base, const std::string& fname, char delim, char comment,
                  const std::vector<int32_t>& types) {
     const int nc = (int)types.size();
-    const bool collapse = delim == ' ';
+    const bool collapse = delim == 0;  // whitespace-separated (opt-in; Spark's sep is one character)
     c.data.assign(nc, {});
     c.valid.assign(nc, {});
     c.arena.assign(nc, {});
@@ -127,7 +127,9 @@ void parse_chunk(Chunk& c, const char* file_base, const std::string& fname, char
         if (lend > p && lend[-1] == '\r') --lend;
         const char* q = p;
         while (q < lend && blank(*q)) ++q;
-        if (q == lend || (comment && *q == comment)) {  // blank or comment line
+        // a comment line starts with the comment character itself (univocity's comment test, which
+        // Spark's CSV reader uses); a line of blanks holds no record
+        if (q == lend || (comment && *p == comment)) {
             p = next;
             continue;
         }
@@ -165,9 +167,14 @@ void parse_chunk(Chunk& c, const char* file_base, const std::string& fname, char
                         std::memcpy(&w, &d, 8);
                         break;
                     }
-                    case CAPSMI_BOOL: {
+                    case CAPSMI_BOOL: {  // Spark's CSV BooleanType: "true" / "false", any case, nothing else
                         const size_t len = (size_t)(fe - fb);
-                        w = len == 4 && strncasecmp(fb, "true", 4) == 0 ? 1 : 0;
+                        if (len == 4 && strncasecmp(fb, "true", 4) == 0) w = 1;
+                        else if (len == 5 && strncasecmp(fb, "false", 5) == 0) w = 0;
+                        else {
+                            fail(p, "not a Boolean: '" + std::string(fb, fe) + "'");
+                            return;
+                        }
                         break;
                     }
                     default:

@@ -478,6 +478,8 @@ capsmi_status capsmi_count_shard_begin(capsmi_session* s, int32_t nrels, capsmi_
                                        const char* dst_col, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok,
                                        const capsmi_bitmap* c_ok, int64_t own_lo, int64_t own_hi, uint32_t* owned_in,
                                        capsmi_count_shard** out);
+/* finish runs once per handle (a second call is ILLEGAL_ARGUMENT); the handle keeps what it reads of
+ * the bitmaps, so they may be released after begin */
 capsmi_status capsmi_count_shard_finish(capsmi_count_shard* h, const uint32_t* in_all, int64_t* dev_out);
 capsmi_status capsmi_count_shard_release(capsmi_count_shard* h);
 /* popcount of words [w_begin, w_end) of a device bitmap, result in *out (host) */
@@ -506,8 +508,10 @@ capsmi_status capsmi_owner_words(int64_t nbits, int32_t part, int32_t nparts, in
                                  int64_t* w_end);
 /* ---- ingest ----------------------------------------------------
  * DataFrameReader.csv with an explicit schema, as EdgeListDataSource (EdgeListDataSource.scala:76-97)
- * and the FS graph source read their tables: files in order, no header, `delimiter` (' ' = runs of
- * blanks), '"' quotes, an empty unquoted field is null, lines starting with `comment` (0 = none)
+ * and the FS graph source read their tables: files in order, no header, `delimiter` one character
+ * (as Spark's `sep`: "1  2" with ' ' is 1, null, 2; 0 = opt-in whitespace splitting, runs of blanks
+ * separate fields), '"' quotes, an empty unquoted field is null, lines whose first character is
+ * `comment` (0 = none) and lines of blanks skipped
  * skipped; Spark's PERMISSIVE token counts (missing trailing fields null, extra tokens dropped);
  * a token that does not parse as its column type is ILLEGAL_ARGUMENT.  Parsed by host threads
  * (CAPSMI_INGEST_THREADS, default OMP_NUM_THREADS), copied to the device.  types: CAPSMI_I64 /

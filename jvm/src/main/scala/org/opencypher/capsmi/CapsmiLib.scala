@@ -30,6 +30,7 @@ object Capsmi {
   final val BOOL = 1 // CTBoolean, label / relationship-type flags
   final val F64 = 2  // CTFloat
   final val STR = 3  // CTString as an order-preserving dictionary code
+  final val LIST = 8 // CTList(elem): LIST + elem type (Collect results; read with capsmi_table_export_list)
   // host widths widened at ingest (DataFrameOps.withCypherCompatibleTypes)
   final val IN_I32 = 16
   final val IN_I16 = 17
@@ -79,6 +80,7 @@ object Capsmi {
   final val AGG_MAX = 3
   final val AGG_SUM = 4
   final val AGG_AVG = 5
+  final val AGG_COLLECT = 6 // sort_array(collect_list / collect_set)
 }
 
 @Structure.FieldOrder(Array("name", "type", "data", "valid"))
@@ -164,6 +166,8 @@ trait CapsmiLib extends Library {
   def capsmi_table_schema(t: Pointer, ncols: IntByReference, names: Array[Byte], namesLen: Long, types: Array[Int],
                           nullable: Array[Int], maxCols: Int): Int
   def capsmi_table_export(t: Pointer, col: Int, hostData: Pointer, hostValid: Pointer, offset: Long, n: Long): Int
+  def capsmi_table_export_list(t: Pointer, col: Int, offset: Long, n: Long, hostOffsets: Pointer, hostValid: Pointer,
+                               hostValues: Pointer, valuesCap: Long, nvalues: LongByReference): Int
   def capsmi_table_column_device_ptr(t: Pointer, col: Int, data: PointerByReference, valid: PointerByReference): Int
   def capsmi_table_fingerprint(t: Pointer, ncols: Int, cols: Array[String], count: LongByReference,
                                sum: LongByReference, xr: LongByReference): Int

@@ -8,7 +8,7 @@
 package org.opencypher.capsmi
 
 import com.sun.jna.Pointer
-import com.sun.jna.ptr.{LongByReference, PointerByReference}
+import com.sun.jna.ptr.{IntByReference, LongByReference, PointerByReference}
 import org.opencypher.okapi.api.graph.{GraphName, Namespace, QualifiedGraphName}
 import org.opencypher.okapi.api.io.conversion.{EntityMapping, NodeMapping, RelationshipMapping}
 import org.opencypher.okapi.api.schema.Schema
@@ -70,6 +70,9 @@ final class GpuSession(device: Int = 0) extends RelationalCypherSession[GpuTable
   }
 
   val dictionary = new StringDictionary
+
+  /** Graph tags -> number of dense ids, for the graphs GpuGraphFactory compacted (capsmi_graph_compact). */
+  val denseIdsByGraph: scala.collection.mutable.Map[Set[Int], Long] = scala.collection.mutable.Map.empty
 
   override val catalog: CypherCatalog = new CypherCatalog
 
@@ -297,11 +300,21 @@ case class GpuGraphFactory(implicit val session: GpuSession) extends RelationalC
 
   def create(tags: Set[Int], maybeSchema: Option[Schema],
              entityTables: org.opencypher.okapi.relational.api.io.EntityTable[GpuTable]*): Graph = {
-    // dense ids for the fused kernels when the graph's ids do not fit one 2^30 window (capsmi_graph_compact)
+    // dense ids for the fused kernels when the graph's ids do not fit one 2^30 window
+    // (capsmi_graph_compact), as capsmi.table.Session.compact_if_sparse decides it
     val nodes = entityTables.collect { case n: GpuNodeTable => n.table.handle }.toArray
     val rels = entityTables.collect { case r: GpuRelationshipTable => r.table.handle }.toArray
-    val dense = new LongByReference
-    CapsmiLib.check(CapsmiLib.I.capsmi_graph_compact(session.handle, nodes.length, nodes, rels.length, rels, dense))
+    val spans = (nodes ++ rels).flatMap { h =>
+      val (k, lo, hi) = (new IntByReference, new LongByReference, new LongByReference)
+      CapsmiLib.check(CapsmiLib.I.capsmi_table_entity(h, k, lo, hi))
+      if (k.getValue != 0 && hi.getValue > lo.getValue) Some((lo.getValue, hi.getValue)) else None
+    }
+    val compacted = spans.nonEmpty && spans.map(_._2).max - spans.map(_._1).min > (1L << 30)
+    if (compacted) {
+      val dense = new LongByReference
+      CapsmiLib.check(CapsmiLib.I.capsmi_graph_compact(session.handle, nodes.length, nodes, rels.length, rels, dense))
+      session.denseIdsByGraph += tags -> dense.getValue  // inspectable: which graphs run on a dense remap
+    }
     val schema = maybeSchema.getOrElse(entityTables.map(_.schema).reduce(_ ++ _))
     new org.opencypher.okapi.relational.impl.graph.ScanGraph(entityTables, schema, tags)
   }

@@ -46,9 +46,20 @@ object GpuTable {
       case Capsmi.BOOL => CTBoolean
       case Capsmi.F64 => CTFloat
       case Capsmi.STR => CTString
+      case l if l >= Capsmi.LIST && l <= Capsmi.LIST + Capsmi.STR => CTList(cypherType(l - Capsmi.LIST, nullable = false))
       case other => throw IllegalArgumentException("a capsmi column type", other)
     }
     if (nullable) t.nullable else t
+  }
+
+  /** Rows exported per host round trip (rows() streams a table of any size in chunks of this). */
+  private val ExportChunk = 1 << 20
+
+  private def decode(ty: Int, w: Long)(implicit session: GpuSession): CypherValue = ty match {
+    case Capsmi.I64 => CypherValue(w)
+    case Capsmi.F64 => CypherValue(java.lang.Double.longBitsToDouble(w))
+    case Capsmi.BOOL => CypherValue(w != 0)
+    case Capsmi.STR => CypherValue(session.dictionary.decode(w))
   }
 }
 
@@ -64,16 +75,29 @@ final class GpuTable private (val handle: Pointer)(implicit val session: GpuSess
 
   private def wrap(f: com.sun.jna.ptr.PointerByReference => Int): GpuTable = GpuTable(table(f))
 
-  /** (name, physical type, nullable) per column: one call, the plan's schema without running it. */
+  /** (name, physical type, nullable) per column: one call, the plan's schema without running it.  Names
+    * are read by walking the NUL terminators (an empty name is a valid column name); a table wider
+    * than the first guess is asked again with arrays of its width. */
   private lazy val schema: Seq[(String, Int, Boolean)] = {
-    val maxCols = 4096
-    val names = new Array[Byte](maxCols * 256)
-    val types = new Array[Int](maxCols)
-    val nullable = new Array[Int](maxCols)
-    val n = new IntByReference
-    check(I.capsmi_table_schema(handle, n, names, names.length, types, nullable, maxCols))
-    val split = new String(names, "UTF-8").split('\u0000')
-    (0 until n.getValue).map(i => (split(i), types(i), nullable(i) != 0))
+    def read(maxCols: Int, nameBytes: Int): Seq[(String, Int, Boolean)] = {
+      val names = new Array[Byte](nameBytes)
+      val types = new Array[Int](maxCols)
+      val nullable = new Array[Int](maxCols)
+      val n = new IntByReference
+      val rc = I.capsmi_table_schema(handle, n, names, names.length, types, nullable, maxCols)
+      if (rc == Capsmi.ERR_ILLEGAL_ARGUMENT && nameBytes < (1 << 28)) return read(maxCols, nameBytes * 4)  // names did not fit
+      check(rc)
+      if (n.getValue > maxCols) return read(n.getValue, math.max(nameBytes, n.getValue * 256))
+      var pos = 0
+      (0 until n.getValue).map { i =>
+        var end = pos
+        while (names(end) != 0) end += 1
+        val name = new String(names, pos, end - pos, "UTF-8")
+        pos = end + 1
+        (name, types(i), nullable(i) != 0)
+      }
+    }
+    read(256, 65536)
   }
 
   override def physicalColumns: Seq[String] = schema.map(_._1)
@@ -87,25 +111,35 @@ final class GpuTable private (val handle: Pointer)(implicit val session: GpuSess
     v.getValue
   }
 
-  /** DataFrameTable.rows (SparkTable.scala:55-57): one host export per column, decoded per row. */
+  /** DataFrameTable.rows (SparkTable.scala:55-57): exported ExportChunk rows at a time (one host export
+    * per column and chunk), so tables above 2^31 rows stream; list columns (Collect results) come
+    * back as CypherList. */
   override def rows: Iterator[String => CypherValue] = {
     val n = size
-    val cols = schema.zipWithIndex.map { case ((name, ty, _), c) =>
-      val data = new com.sun.jna.Memory(math.max(8L, 8L * n))
-      val valid = new com.sun.jna.Memory(math.max(1L, n))
-      check(I.capsmi_table_export(handle, c, data, valid, 0, n))
-      (name, ty, data.getLongArray(0, n.toInt), valid.getByteArray(0, n.toInt))
-    }
-    (0 until n.toInt).iterator.map { r =>
-      val row = cols.map { case (name, ty, d, v) =>
-        name -> (if (v(r) == 0) CypherValue(null) else ty match {
-          case Capsmi.I64 => CypherValue(d(r))
-          case Capsmi.F64 => CypherValue(java.lang.Double.longBitsToDouble(d(r)))
-          case Capsmi.BOOL => CypherValue(d(r) != 0)
-          case Capsmi.STR => CypherValue(session.dictionary.decode(d(r)))
-        })
-      }.toMap
-      row
+    Iterator.iterate(0L)(_ + ExportChunk).takeWhile(_ < n).flatMap { off =>
+      val k = math.min(ExportChunk.toLong, n - off).toInt
+      val cols: Seq[(String, Int => CypherValue)] = schema.zipWithIndex.map { case ((name, ty, _), c) =>
+        val valid = new com.sun.jna.Memory(math.max(1L, k.toLong))
+        if (ty >= Capsmi.LIST) {
+          val total = new LongByReference
+          check(I.capsmi_table_export_list(handle, c, off, k, null, null, null, 0, total))
+          val offs = new com.sun.jna.Memory(8L * (k + 1))
+          val vals = new com.sun.jna.Memory(math.max(8L, 8L * total.getValue))
+          check(I.capsmi_table_export_list(handle, c, off, k, offs, valid, vals, total.getValue, total))
+          val o = offs.getLongArray(0, k + 1)
+          val w = vals.getLongArray(0, total.getValue.toInt)
+          val v = valid.getByteArray(0, k)
+          name -> ((r: Int) => if (v(r) == 0) CypherValue(null)
+            else CypherList((o(r) until o(r + 1)).map(i => decode(ty - Capsmi.LIST, w(i.toInt))): _*))
+        } else {
+          val data = new com.sun.jna.Memory(math.max(8L, 8L * k))
+          check(I.capsmi_table_export(handle, c, data, valid, off, k))
+          val d = data.getLongArray(0, k)
+          val v = valid.getByteArray(0, k)
+          name -> ((r: Int) => if (v(r) == 0) CypherValue(null) else decode(ty, d(r)))
+        }
+      }
+      (0 until k).iterator.map(r => cols.map { case (name, get) => name -> get(r) }.toMap)
     }
   }
 
@@ -141,16 +175,19 @@ final class GpuTable private (val handle: Pointer)(implicit val session: GpuSess
 
   override def distinct(cols: String*): GpuTable = wrap(I.capsmi_distinct_on(handle, cols.size, cols.toArray, _))
 
-  /** SparkTable.scala:121-188 for the aggregators the device path has (collect is not among them). */
+  /** SparkTable.scala:121-188.  Grouping keys are every column the grouped variables own
+    * (header.ownedBy, SparkTable.scala:128-133): a node variable groups by its id, label and property
+    * columns, which the Aggregate's header keeps (RelationalOperator.scala:345). */
   override def group(by: Set[Var], aggregations: Set[(Aggregator, (String, CypherType))])
     (implicit header: RecordHeader, parameters: CypherMap): GpuTable = {
-    val byCols = by.toSeq.map(header.column)
+    val byCols = by.toSeq.flatMap(v => header.ownedBy(v).toSeq.map(header.column)).distinct
     val inputs = aggregations.toSeq.collect {
       case (Avg(e), _) => e
       case (Count(e, _), _) => e
       case (Max(e), _) => e
       case (Min(e), _) => e
       case (Sum(e), _) => e
+      case (Collect(e, _), _) => e
     }
     val (withInputs, inCols) = columnsFor(inputs)
     val inputOf = inputs.zip(inCols).toMap
@@ -161,6 +198,7 @@ final class GpuTable private (val handle: Pointer)(implicit val session: GpuSess
       case (Max(e), (out, _)) => (Capsmi.AGG_MAX, false, Some(inputOf(e)), out)
       case (Sum(e), (out, _)) => (Capsmi.AGG_SUM, false, Some(inputOf(e)), out)
       case (Avg(e), (out, _)) => (Capsmi.AGG_AVG, false, Some(inputOf(e)), out)
+      case (Collect(e, distinct), (out, _)) => (Capsmi.AGG_COLLECT, distinct, Some(inputOf(e)), out)
       case (other, _) => throw NotImplementedException(s"aggregator $other on the device path")
     }
     withInputs.wrap(I.capsmi_group(withInputs.handle, byCols.size, byCols.toArray, specs.size, CapsmiLib.aggs(specs), _))

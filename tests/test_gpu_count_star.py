@@ -108,6 +108,33 @@ def test_dense_buckets_roll_chunks(session, monkeypatch, mode):
     assert got == rows
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_rec_counter_wraps_on_even_and_odd_ids(session, monkeypatch, seed):
+    """The IN walk counts two ids per 32-bit LDS word in 16-bit halves (even id low, odd id high).
+    Pairs (x even, x + 1) with more than 2^16 in-relationships each exercise the low-half wrap (its
+    carry reaches the high half), the high-half wrap, and a low-half carry into a high half sitting
+    at 0xFFFF (x + 1 with 65535 mod 65536 in-relationships) -- each against the closed form."""
+    from capsmi import graph
+    _mode(monkeypatch, "rec")
+    rng = np.random.default_rng(100 + seed)
+    n = 1 << 18
+    counts = {2000: 200_001, 2001: 131_071, 4000: 65_536, 4001: 65_535, 6000: 70_000, 8000: 65_535, 8001: 196_607,
+              65534: 131_072, 65535: 65_537}
+    dst = np.concatenate([np.full(c, x, np.int64) for x, c in counts.items()] + [rng.integers(0, n, 400_000)])
+    rng.shuffle(dst)
+    src = rng.integers(0, n, len(dst)).astype(np.int64)
+    src[:50] = dst[:50]  # a few self-loops
+    a = (rng.random(n) < 0.9).astype(np.uint8)
+    b = (rng.random(n) < 0.97).astype(np.uint8)
+    for x in counts:
+        b[x] = 1
+    ones = np.ones(n, np.uint8)
+    rows, _ = cpu.two_hop_closed_form(n, src, dst, a, b, ones)
+    got = graph.two_hop_count(session, [_rels(session, src, dst)], _bm(session, n, a), _bm(session, n, b),
+                              _bm(session, n, ones))
+    assert got == rows
+
+
 @pytest.mark.parametrize("mode", ["rec", "pairs"])
 def test_offset_domain(session, monkeypatch, mode):
     """Bitmaps over [lo, lo + n) with lo far from 0 and n not a multiple of the 2^16-id bucket:
@@ -205,3 +232,15 @@ def test_sharded_count_refusals():
         out = torch.zeros(1, dtype=torch.int64, device="cuda")
         sh.finish(buf.data_ptr(), out.data_ptr())
         assert int(out.item()) == 9  # chain 0->1->...->10: 9 two-hop pairs inside [0, 1000)
+        from capsmi._lib import IllegalArgumentException
+        with pytest.raises(IllegalArgumentException, match="twice"):  # one finish per handle
+            sh.finish(buf.data_ptr(), out.data_ptr())
+        assert int(out.item()) == 9
+    # the handle keeps what it reads of b_ok: releasing the bitmaps between begin and finish is safe
+    B = _bm(session, n, ones)
+    sh = graph.CountShard(session, [rel], A, B, A, 0, n, buf.data_ptr())
+    B.release()
+    out = torch.zeros(1, dtype=torch.int64, device="cuda")
+    sh.finish(buf.data_ptr(), out.data_ptr())
+    sh.close()
+    assert int(out.item()) == 9

@@ -13,12 +13,12 @@ def test_edge_list_formats(session, tmp_path):
     from capsmi import io
     p = tmp_path / "e.txt"
     p.write_text("# header comment\n1 2\n  3   4\r\n\n# mid comment\n1099511627776 -5\n7\t8\n")
-    nodes, rels = io.edge_list_graph(session, str(p))
+    nodes, rels = io.edge_list_graph(session, str(p), delimiter=None)  # whitespace-separated (opt-in)
     assert rels.column("id").values.tolist() == [0, 1, 2, 3]
     assert rels.column("source").values.tolist() == [1, 3, 1099511627776, 7]
     assert rels.column("target").values.tolist() == [2, 4, -5, 8]
     assert sorted(nodes.column("id").values.tolist()) == sorted({1, 2, 3, 4, 1099511627776, -5, 7, 8})
-    s, d = io.read_edge_list(str(p))
+    s, d = io.read_edge_list(str(p), delimiter=None)
     np.testing.assert_array_equal(s, rels.column("source").values)
 
 
@@ -48,13 +48,36 @@ def test_csv_fields(session, tmp_path):
 
 def test_csv_errors(session, tmp_path):
     from capsmi import _lib
-    from capsmi.expr import I64
+    from capsmi.expr import BOOL, I64
     p = tmp_path / "bad.csv"
     p.write_text("1,2\n3,x4\n")
     with pytest.raises(_lib.IllegalArgumentException, match="not a Long"):
         session.read_csv([str(p)], ["a", "b"], [I64, I64])
+    for token in ("flase", "1", "yes", "t"):  # Spark's CSV Boolean takes true / false only
+        p.write_text(f"1,true\n2,FALSE\n3,{token}\n")
+        with pytest.raises(_lib.IllegalArgumentException, match="not a Boolean"):
+            session.read_csv([str(p)], ["a", "b"], [I64, BOOL])
     with pytest.raises(_lib.IllegalArgumentException, match="cannot open"):
         session.read_csv([str(tmp_path / "missing.csv")], ["a"], [I64])
+
+
+def test_csv_delimiter_and_comment_lines(session, tmp_path):
+    """Spark's `sep` is one character: with ' ', two spaces hold an empty (null) field, and a leading
+    space starts with an empty field; a comment is a line whose FIRST character is the comment
+    character; lines of blanks hold no record.  Whitespace splitting is the opt-in delimiter None."""
+    from capsmi.expr import I64
+    p = tmp_path / "e.txt"
+    p.write_text("# header\n1 2\n3  4\n 5 6\n  # not a comment\n   \n7 8\n")
+    t = session.read_csv([str(p)], ["a", "b"], [I64, I64], delimiter=" ", comment="#")
+    a, b = t.column("a"), t.column("b")
+    got = [(None if not a.valid[i] else int(a.values[i]), None if not b.valid[i] else int(b.values[i]))
+           for i in range(t.size)]
+    assert got[:3] == [(1, 2), (3, None), (None, 5)]
+    assert got[-1] == (7, 8) and len(got) == 5  # '  # not...' is a record: (null, null) -> fields '', ''
+    assert got[3] == (None, None)
+    p.write_text("# header\n1 2\n3   4\n\t5\t 6\n")
+    t = session.read_csv([str(p)], ["a", "b"], [I64, I64], delimiter=None, comment="#")
+    assert list(zip(t.column("a").values.tolist(), t.column("b").values.tolist())) == [(1, 2), (3, 4), (5, 6)]
 
 
 def test_many_files_and_chunks(session, tmp_path):
