@@ -9,11 +9,16 @@ relationship table [id, source, target] (int64, generation order) is generated o
 ranks each rank holds the relationships whose target falls in its owner range (one rank per GPU,
 strong scaling: the graph is fixed).
 
-A step = the whole query from the resident entity tables:
-  cold (the reported value): node-scan bitmap, radix partition of the relationship table,
-       hop 1, RCCL all-gather of the hop-1 frontier (N > 1), hop 2, popcount (+ all-reduce);
+A step = the whole query from the resident entity tables, issued as the Table[T] calls the relational
+planner emits (Planner(sg).run) and routed by libcapsmi to the fused kernels:
+  cold (the reported value): node-scan bitmap, radix partition of the relationship table, hop 1, hop 2,
+       popcount.  N > 1: every rank runs the same query over its shard of the distributed graph
+       (relationships by a hash of their target, node rows by a hash of their id:
+       capsmi_graph_distribute); the route all-gathers the owned node-scan and hop-1 frontier bitmap
+       slices and all-reduces the count over RCCL (capsmi_session_set_ranks);
   warm: the same with the partition kept from an earlier query (Cache analogue);
-  stream: no partition, both hops stream the table in generation order (comparison).
+  count: count(*) of the same match through the route;
+  direct / direct_warm / stream (N = 1): the same kernels called explicitly (comparison).
 
 metric value = matched rows / s, where matched rows = count(*) of the same MATCH, i.e. the bindings
 CAPS's joins would emit.  It is computed once in closed form (sum_b in(b)*out(b) - self-loops) on the
@@ -254,28 +259,38 @@ def main():
     n = 1 << scale
     m_total = ef << scale
     nw = (n + 31) // 32
-    shards = args.shard_of if (args.shard_of and not distributed) else world
+    shards = args.shard_of if (args.shard_of and not distributed) else 1
     assert nw % shards == 0, "owner slices must be equal for the all-gather"
-    wb, we = graph.owner_words(n, rank, shards)
+    part = rank if shards > 1 else 0  # --shard-of diagnostic only; N > 1 ranks shard by hash below
+    wb, we = graph.owner_words(n, part, shards)
     modes = [m.strip() for m in args.modes.split(",") if m.strip()]
     if args.shard_of:  # count(*) of one shard alone is not a share of the count: skip it
         modes = [m for m in modes if not m.startswith("count")] or ["cold"]
-    elif distributed:  # count(*) over ranks: the phased count below (no atomic A/B form)
-        modes = [m for m in modes if m != "count_atomic"] or ["cold"]
+    elif distributed:  # the drop-in route on every rank (no explicit-kernel or atomic A/B forms)
+        modes = [m for m in modes if m in ("cold", "warm", "count")] or ["cold"]
 
-    # ---- ingest (untimed): partitioned relationship table + Person node table --------------------
+    # ---- ingest (untimed): relationship table + Person node table ---------------------------------
+    # N > 1: every rank generates the graph and keeps its shard -- the relationships whose target it
+    # owns and the :Person rows of the ids it owns, ownership by a hash of the id (capsmi_owned_rows) --
+    # then registers the shard (capsmi_graph_distribute); ingest is untimed
     t0 = time.perf_counter()
     rels = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42,
-                           part_col=graph.PART_TARGET if shards > 1 else graph.PART_NONE, part=rank, nparts=shards)
+                           part_col=graph.PART_TARGET if shards > 1 else graph.PART_NONE, part=part, nparts=shards)
     persons = graph.rmat_nodes(sess, scale, graph.NODES_ALL)
-    if distributed:  # each rank holds (and scans) the :Person rows of the ids it owns
-        from capsmi.expr import Ands, BinOp, Col, Lit
-        own_lo, own_hi = 32 * wb, min(32 * we, n)
-        persons = persons.filter(Ands((BinOp(">=", Col("id"), Lit(own_lo)), BinOp("<", Col("id"), Lit(own_hi))))) \
-            .as_node_table("id")
+    if distributed:
+        from capsmi.dist import distribute, join_ranks
+        join_ranks(sess)
+        rels = rels.owned_rows("target", 0, n).as_rel_table("id", "source", "target")
+        persons = persons.owned_rows("id", 0, n).as_node_table("id")
+        distribute(sess, 0, n, [persons], [rels], nodes_owned=True, rels_by="target")
     m_local = rels.size
     sess.sync()
     ingest_s = time.perf_counter() - t0
+    if distributed:  # the shards' sizes (balance of the hash ownership), on every rank
+        sizes = torch.zeros(world, dtype=torch.int64, device="cuda")
+        sizes[rank] = m_local
+        dist.all_reduce(sizes)
+        rels_per_rank = sizes.tolist()
 
     mid = torch.zeros(2 * nw, dtype=torch.int32, device="cuda")
     scratch = torch.zeros(nw, dtype=torch.int32, device="cuda")
@@ -371,6 +386,8 @@ def main():
     sg_cold = scan_graph(rels)
     # Cache analogue: a second handle on the same columns, marked cache() so the route keeps its layout
     rels_cached = rels.select("id", "source", "target").as_rel_table("id", "source", "target").cache()
+    if distributed:
+        distribute(sess, 0, n, [], [rels_cached], nodes_owned=True, rels_by="target")
     sg_warm = scan_graph(rels_cached)
 
     def run_planner(sg):
@@ -393,7 +410,7 @@ def main():
     steps = {"cold": lambda: run_planner(sg_cold), "warm": lambda: run_planner(sg_warm),
              "direct": step_cold, "direct_warm": step_warm, "stream": step_stream,
              "count": run_count, "count_atomic": lambda: run_count(True)}
-    if distributed or shards != world:  # the recogniser plans one device: ranks run the phased kernels
+    if shards != 1:  # --shard-of diagnostic: one shard's kernels, no exchange
         steps["cold"], steps["warm"], steps["count"] = step_cold, step_warm, step_count_shards
 
     kbytes = {}  # per-launch algorithmic bytes the library declares for a timer (count(*) walks)
@@ -446,7 +463,7 @@ def main():
         p = graph.NodeBitmap(sess, 0, n).add_scan(all_persons, "id")
         matched = graph.two_hop_count(sess, [full], p, p, p)
         answers = {m: r[1] for m, r in results.items()}
-        if shards != world:
+        if shards != 1:
             check = f"not applicable (--shard-of {shards}: rank 0's shard alone)"
         elif fx is None:
             check = "no fixture for this scale"
@@ -476,7 +493,8 @@ def main():
         dom = max(timed, key=lambda k: timed[k][1])
         avg_ms = timed[dom][1] / timed[dom][0]
         achieved = alg[dom] / (avg_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(KERNEL_SYMBOL[dom], "c3")
+        # committed PMC summaries are 1-GPU profiles of the whole table: they say nothing about a shard
+        traffic = pmc_traffic(KERNEL_SYMBOL[dom], "c3") if world == 1 and shards == 1 else None
         query_alg = 2 * 24 * m_total + 3 * 8 * n  # SURVEY.md §8d C3 B_alg (whole query, all ranks)
         line = {
             "metric": METRIC,
@@ -495,11 +513,13 @@ def main():
                                    "RETURN count(DISTINCT c)",
                        "mode": head, "scale": scale, "nodes": n, "relationships": m_total,
                        "rmat": [0.57, 0.19, 0.19, 0.05], "seed": 42,
-                       "parallelism": f"rels partitioned by owner(target) over {world} GPU(s); "
-                                      "hop-1 frontier all-gather + count all-reduce over RCCL",
+                       "parallelism": (f"dp{world}: relationships hash-partitioned by target over {world} GPUs "
+                                       "(capsmi_graph_distribute); node-scan and hop-1 frontier bitmap all-gathers "
+                                       "+ count all-reduce over RCCL inside the route") if world > 1 else
+                       "single GPU (no exchange)",
                        "route": ("Planner(sg).run(query): lazy Table[T] plan -> fused two-hop kernels "
-                                 f"({routed} plans routed)") if world == 1 and shards == 1 and
-                       head in ("cold", "warm") else "explicit phased kernel calls"},
+                                 f"({routed} plans routed on this rank)") if shards == 1 and
+                       head in ("cold", "warm", "count") else "explicit phased kernel calls"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": KERNEL_SYMBOL[dom],
                          "kernel_ms": avg_ms, "alg_bytes_per_launch": alg[dom]},
@@ -511,7 +531,10 @@ def main():
                       "kernel_ms": {k: v[1] / v[0] for k, v in timed.items()},
                       "rels_local_rank0": m_local, "ingest_s": ingest_s},
         }
-        if shards != world:
+        if distributed:
+            line["query"]["rels_per_rank"] = rels_per_rank
+            line["query"]["rels_max_over_mean"] = max(rels_per_rank) / (sum(rels_per_rank) / world)
+        if shards != 1:
             line["config"]["diagnostic"] = f"rank 0's shard of {shards} on one GPU, no exchange (not the metric)"
         # warm (layout cached): the query reads the cached 8-B packed layout once per hop instead of the
         # int64 (source, target) scans, plus the three node scans -- its own algorithmic bytes

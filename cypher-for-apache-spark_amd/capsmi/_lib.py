@@ -83,6 +83,11 @@ PP = POINTER(c_void_p)
 STRS = POINTER(c_char_p)
 
 INTERN_FN = ctypes.CFUNCTYPE(c_int64, c_void_p, ctypes.POINTER(ctypes.c_char), c_size_t)
+# capsmi_collective_fn(ctx, op, send, recv, count, dtype) -> 0 on success
+COLLECTIVE_FN = ctypes.CFUNCTYPE(c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_int64, c_int32)
+COLL_ALL_GATHER, COLL_ALL_REDUCE_SUM, COLL_ALL_REDUCE_MAX, COLL_U32 = 0, 1, 2, 100
+NODES_REPLICATED, NODES_OWNED = 0, 1
+RELS_BY_SOURCE, RELS_BY_TARGET = 0, 1
 
 # name -> (restype-is-status, argtypes)
 _SIGS = {
@@ -182,6 +187,12 @@ _SIGS = {
     "capsmi_read_csv": (c_int32, [P, c_int32, STRS, ctypes.c_char, ctypes.c_char, c_int32, STRS, POINTER(c_int32),
                                   INTERN_FN, c_void_p, c_char_p, PP]),
     "capsmi_session_route_count": (c_int32, [P, c_char_p, POINTER(c_int64)]),
+    "capsmi_session_set_unrouted_limit": (c_int32, [P, c_int64]),
+    "capsmi_session_set_ranks": (c_int32, [P, c_int32, c_int32, COLLECTIVE_FN, c_void_p]),
+    "capsmi_graph_distribute": (c_int32, [P, c_int64, c_int64, c_int32, PP, c_int32, c_int32, PP, c_int32]),
+    "capsmi_owned_rows": (c_int32, [P, P, c_char_p, c_int64, c_int64, PP]),
+    "capsmi_table_partitioned": (c_int32, [P, POINTER(c_int32)]),
+    "capsmi_id_owner": (c_int32, [c_int64, c_int64, c_int32, c_int64, POINTER(c_int32), POINTER(c_int64)]),
 }
 
 EXPORTED = tuple(_SIGS)

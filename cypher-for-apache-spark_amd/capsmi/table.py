@@ -238,9 +238,34 @@ class Session:
         by operator (include/capsmi.h capsmi_session_set_fused)."""
         _lib.call("capsmi_session_set_fused", self._h, 1 if enabled else 0)
 
+    def set_unrouted_limit(self, max_bytes: int) -> None:
+        """Refuse unrouted joins whose estimated output exceeds `max_bytes` (0: no limit;
+        include/capsmi.h capsmi_session_set_unrouted_limit)."""
+        _lib.call("capsmi_session_set_unrouted_limit", self._h, int(max_bytes))
+
+    def set_ranks(self, rank: int, world: int, collective=None) -> None:
+        """This process is rank `rank` of `world`; `collective(op, send_ptr, recv_ptr, count, dtype)`
+        runs the exchange on this session's stream (capsmi.dist.TorchCollective; include/capsmi.h
+        capsmi_session_set_ranks)."""
+        if collective is None:
+            self._coll = None
+            _lib.call("capsmi_session_set_ranks", self._h, rank, world, _lib.COLLECTIVE_FN(), None)
+            return
+
+        def fn(_ctx, op, send, recv, count, dtype):
+            try:
+                collective(op, send, recv, count, dtype)
+                return 0
+            except Exception as e:  # reported as CAPSMI_ERR_DEVICE by the library
+                self.collective_error = e
+                return 1
+
+        self._coll = _lib.COLLECTIVE_FN(fn)  # kept alive with the session
+        _lib.call("capsmi_session_set_ranks", self._h, rank, world, self._coll, None)
+
     def route_count(self, name: str) -> int:
         """Plans routed to fused entry point `name` ("expand", "expand_count", "two_hop", "triangle",
-        "var_length") so far."""
+        "var_length") so far; "miss" counts materialisations where a pattern ran unrouted."""
         v = ctypes.c_int64()
         _lib.call("capsmi_session_route_count", self._h, name.encode(), ctypes.byref(v))
         return v.value
@@ -323,6 +348,19 @@ class GpuTable:
         out = ctypes.c_void_p()
         _lib.call("capsmi_rel_table", self._h, id_col.encode(), src_col.encode(), dst_col.encode(), len(type_cols),
                   _lib.strs(type_cols), ctypes.byref(out))
+        return self._wrap(out)
+
+    @property
+    def partitioned(self) -> bool:
+        """Whether the rows are this rank's partition of a distributed result."""
+        v = ctypes.c_int32()
+        _lib.call("capsmi_table_partitioned", self._h, ctypes.byref(v))
+        return bool(v.value)
+
+    def owned_rows(self, col: str, id_lo: int, id_hi: int) -> "GpuTable":
+        """The rows whose Long column `col` holds an id this rank owns (include/capsmi.h capsmi_owned_rows)."""
+        out = ctypes.c_void_p()
+        _lib.call("capsmi_owned_rows", self.session.handle, self._h, col.encode(), id_lo, id_hi, ctypes.byref(out))
         return self._wrap(out)
 
     def entity(self) -> Tuple[int, int, int]:

@@ -99,6 +99,21 @@ struct PlanNode;  // lazy Table[T] operator (plan.hip)
 struct DenseIds {
     int64_t n = 0;
     Buf orig;
+    // a distributed graph's domain (capsmi_graph_distribute): dense = h(x) = ((x - lo) * mul) mod 2^kbits,
+    // x = (dense * mul_inv mod 2^kbits) + lo; no orig table
+    bool scrambled = false;
+    int kbits = 0;
+    uint64_t mul = 0, mul_inv = 0;
+    int64_t lo = 0;
+};
+
+// A rank's shard of a distributed graph (capsmi_graph_distribute): owned dense ids are
+// [rank * 32 * slice_words, (rank + 1) * 32 * slice_words) of the scrambled domain
+struct Shard {
+    int kind = 0;   // 1 node table, 2 relationship table
+    int mode = 0;   // node: CAPSMI_NODES_*; relationship: CAPSMI_RELS_*
+    int rank = 0, world = 1;
+    int64_t slice_words = 0;
 };
 
 }  // namespace capsmi
@@ -129,6 +144,13 @@ struct capsmi_session {
     // fused-path routing of lazy plans (plan.hip): enabled flag and per-route counters
     bool fused = true;
     std::map<std::string, int64_t> routes;
+    // multi-GPU rank view (capsmi_session_set_ranks): the host's collective on this session's stream
+    int rank = 0, world = 1;
+    capsmi_collective_fn coll = nullptr;
+    void* coll_ctx = nullptr;
+    // refuse unrouted joins whose estimated output exceeds this many bytes (0 = no limit;
+    // capsmi_session_set_unrouted_limit)
+    int64_t unrouted_limit = 0;
 };
 
 namespace capsmi {
@@ -166,6 +188,8 @@ struct capsmi_table {
     // dense ids of a compacted graph: node tables `did`, relationship tables `dsrc` / `ddst` (int64 per row)
     std::shared_ptr<capsmi::DenseIds> dense;
     capsmi::Column did, dsrc, ddst;
+    std::shared_ptr<const capsmi::Shard> shard;  // this rank's shard of a distributed graph
+    bool partitioned = false;  // rows are this rank's partition of a distributed result
     std::map<std::string, std::shared_ptr<capsmi_relpart>> layouts;
     bool lazy() const { return (bool)plan; }
     int find(const std::string& n) const {
@@ -251,6 +275,24 @@ std::shared_ptr<ListStore> collect_lists(capsmi_session* s, const int64_t* gid, 
                                          const uint8_t* valid, int type, int64_t n, bool distinct);
 // one store holding a's lists, then b's (b's list k becomes a.nlists + k)
 std::shared_ptr<ListStore> concat_lists(capsmi_session* s, const ListStore& a, const ListStore& b);
+// multi-GPU (k_dist.hip): the session's collective, stream-ordered (capsmi_collective_fn)
+void collective(capsmi_session* s, int op, const void* send, void* recv, int64_t count, int dtype);
+// the scrambled domain of [lo, hi) over `world` ranks: kbits, mul, mul_inv, slice words, domain size
+struct Scramble {
+    int kbits;
+    uint64_t mul, mul_inv;
+    int64_t lo, hi, slice_words, n;
+};
+Scramble make_scramble(int64_t lo, int64_t hi, int world);
+// out[i] = h(in[i]); counts rows outside [lo, hi) into bad[0] and rows whose h is outside
+// [own_lo, own_hi) into bad[1] (when own_lo < own_hi)
+void scramble_ids(capsmi_session* s, const Scramble& sc, const int64_t* in, int64_t n, int64_t* out, int64_t own_lo,
+                  int64_t own_hi, unsigned long long* bad);
+// x = h^-1(d) for n dense ids, in place
+void unscramble_ids(capsmi_session* s, const DenseIds& d, int64_t* v, int64_t n);
+// flags[i] = h(in[i]) in [own_lo, own_hi) (ids outside [lo, hi): 0)
+void owned_flags(capsmi_session* s, const Scramble& sc, const int64_t* in, int64_t n, int64_t own_lo, int64_t own_hi,
+                 uint8_t* flags);
 // REQUIRE(!is_list_type) for a column used as a key / expression operand
 void no_list_key(int32_t type, const std::string& name, const char* what);
 // radix-partitioned equi-join (k_rjoin.hip): (probe row, build row) pairs grouped by key-hash

@@ -1,0 +1,304 @@
+// k_dist.hip -- multi-GPU shards of a graph: the rank view of a session, hash
+// ownership of ids, and the registration of a rank's entity tables as its shard.
+//
+// Spark partitions every DataFrame and shuffles rows by a hash of the join / grouping key before
+// joins and aggregates (Exchange hashpartitioning, SparkTable.scala:133, 226).  Here ownership is
+// fixed once per graph: ids are scrambled by a bijection of the graph's id window, and each rank
+// owns one contiguous range of scrambled ids, so balance does not depend on how the ids were assigned
+// (R-MAT hubs, edge lists whose hubs sit at ids 0..1000).  The fused kernels run on the scrambled ids
+// (the dense key columns of capsmi_graph_compact's machinery); the routes in plan.hip exchange
+// bitmap slices and counts through the host's collective (capsmi_session_set_ranks).
+#include <memory>
+
+#include "capsmi_impl.h"
+
+namespace capsmi {
+
+void set_last_error(const std::string& m);
+
+namespace {
+
+constexpr uint64_t kScrambleMul = 0x9E3779B97F4A7C15ULL;  // odd: a bijection modulo any 2^k
+
+inline unsigned grid_for(int64_t n) {
+    const int64_t g = (n + 255) / 256;
+    return (unsigned)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
+__device__ __forceinline__ int64_t h_of(int64_t x, int64_t lo, uint64_t mul, uint64_t mask) {
+    return (int64_t)(((uint64_t)(x - lo) * mul) & mask);
+}
+
+__global__ void k_scramble(const int64_t* __restrict__ in, int64_t n, int64_t lo, int64_t hi, uint64_t mul,
+                           uint64_t mask, int64_t own_lo, int64_t own_hi, int64_t* __restrict__ out,
+                           unsigned long long* __restrict__ bad) {
+    unsigned long long outside = 0, foreign = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = in[i];
+        const bool ok = x >= lo && x < hi;
+        const int64_t d = ok ? h_of(x, lo, mul, mask) : 0;
+        out[i] = d;
+        outside += ok ? 0 : 1;
+        foreign += (own_lo < own_hi && ok && (d < own_lo || d >= own_hi)) ? 1 : 0;
+    }
+    if (outside) atomicAdd(&bad[0], outside);
+    if (foreign) atomicAdd(&bad[1], foreign);
+}
+
+__global__ void k_unscramble(int64_t* __restrict__ v, int64_t n, int64_t lo, uint64_t mul_inv, uint64_t mask) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        v[i] = (int64_t)(((uint64_t)v[i] * mul_inv) & mask) + lo;
+}
+
+__global__ void k_owned_flags(const int64_t* __restrict__ in, int64_t n, int64_t lo, int64_t hi, uint64_t mul,
+                              uint64_t mask, int64_t own_lo, int64_t own_hi, uint8_t* __restrict__ flags) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = in[i];
+        const int64_t d = h_of(x, lo, mul, mask);
+        flags[i] = (x >= lo && x < hi && d >= own_lo && d < own_hi) ? 1 : 0;
+    }
+}
+
+}  // namespace
+
+void collective(capsmi_session* s, int op, const void* send, void* recv, int64_t count, int dtype) {
+    REQUIRE(s->coll != nullptr, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            "a distributed route needs the session's collective (capsmi_session_set_ranks)");
+    const int32_t rc = s->coll(s->coll_ctx, op, send, recv, count, dtype);
+    REQUIRE(rc == 0, CAPSMI_ERR_DEVICE, "the host collective failed (op " + std::to_string(op) + ")");
+}
+
+Scramble make_scramble(int64_t lo, int64_t hi, int world) {
+    REQUIRE(hi > lo && (uint64_t)(hi - lo) <= (uint64_t(1) << 30), CAPSMI_ERR_UNSUPPORTED,
+            "distributed graph: the id domain must hold 1 .. 2^30 ids");
+    REQUIRE(world >= 1, CAPSMI_ERR_ILLEGAL_ARGUMENT, "world size");
+    Scramble sc;
+    sc.kbits = 5;
+    while ((int64_t(1) << sc.kbits) < hi - lo) ++sc.kbits;
+    sc.mul = kScrambleMul;
+    uint64_t inv = kScrambleMul;  // Newton: each step doubles the correct low bits (3 -> 6 -> ... -> 96)
+    for (int i = 0; i < 5; ++i) inv *= 2 - kScrambleMul * inv;
+    sc.mul_inv = inv;
+    sc.lo = lo;
+    sc.hi = hi;
+    const int64_t words = (int64_t(1) << sc.kbits) / 32;
+    sc.slice_words = (words + world - 1) / world;
+    sc.n = (int64_t)world * 32 * sc.slice_words;
+    return sc;
+}
+
+void scramble_ids(capsmi_session* s, const Scramble& sc, const int64_t* in, int64_t n, int64_t* out, int64_t own_lo,
+                  int64_t own_hi, unsigned long long* bad) {
+    if (n <= 0) return;
+    const uint64_t mask = (uint64_t(1) << sc.kbits) - 1;
+    hipLaunchKernelGGL(k_scramble, dim3(grid_for(n)), dim3(256), 0, s->stream, in, n, sc.lo, sc.hi, sc.mul, mask,
+                       own_lo, own_hi, out, bad);
+    HIP_CHECK(hipGetLastError());
+}
+
+void unscramble_ids(capsmi_session* s, const DenseIds& d, int64_t* v, int64_t n) {
+    REQUIRE(d.scrambled, CAPSMI_ERR_INTERNAL, "unscramble of a non-scrambled domain");
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_unscramble, dim3(grid_for(n)), dim3(256), 0, s->stream, v, n, d.lo, d.mul_inv,
+                       (uint64_t(1) << d.kbits) - 1);
+    HIP_CHECK(hipGetLastError());
+}
+
+void owned_flags(capsmi_session* s, const Scramble& sc, const int64_t* in, int64_t n, int64_t own_lo, int64_t own_hi,
+                 uint8_t* flags) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_owned_flags, dim3(grid_for(n)), dim3(256), 0, s->stream, in, n, sc.lo, sc.hi, sc.mul,
+                       (uint64_t(1) << sc.kbits) - 1, own_lo, own_hi, flags);
+    HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace capsmi
+
+using namespace capsmi;
+
+namespace {
+
+#define D_BEGIN try {
+#define D_END                                                   \
+    }                                                           \
+    catch (const capsmi::Error& e) {                            \
+        set_last_error(e.what());                               \
+        return e.code;                                          \
+    }                                                           \
+    catch (const std::bad_alloc&) {                             \
+        set_last_error("host allocation failed");               \
+        return CAPSMI_ERR_OUT_OF_MEMORY;                        \
+    }                                                           \
+    catch (const std::exception& e) {                           \
+        set_last_error(e.what());                               \
+        return CAPSMI_ERR_INTERNAL;                             \
+    }                                                           \
+    return CAPSMI_OK;
+
+void need(const void* p, const char* what) {
+    REQUIRE(p != nullptr, CAPSMI_ERR_ILLEGAL_ARGUMENT, std::string("null argument: ") + what);
+}
+
+Column key_column(capsmi_session* s, int64_t rows) {
+    Column c;
+    c.type = CAPSMI_I64;
+    c.data = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), s);
+    return c;
+}
+
+}  // namespace
+
+extern "C" {
+
+capsmi_status capsmi_session_set_ranks(capsmi_session* s, int32_t rank, int32_t world, capsmi_collective_fn fn,
+                                       void* ctx) {
+    D_BEGIN
+    need(s, "session");
+    REQUIRE(world >= 1 && rank >= 0 && rank < world, CAPSMI_ERR_ILLEGAL_ARGUMENT, "rank / world");
+    REQUIRE(world == 1 || fn != nullptr, CAPSMI_ERR_ILLEGAL_ARGUMENT, "a multi-rank session needs a collective");
+    s->rank = rank;
+    s->world = world;
+    s->coll = fn;
+    s->coll_ctx = ctx;
+    D_END
+}
+
+capsmi_status capsmi_graph_distribute(capsmi_session* s, int64_t id_lo, int64_t id_hi, int32_t nnodes,
+                                      capsmi_table* const* nodes, int32_t node_mode, int32_t nrels,
+                                      capsmi_table* const* rels, int32_t rel_mode) {
+    D_BEGIN
+    need(s, "session");
+    REQUIRE(nnodes >= 0 && nrels >= 0 && (nnodes == 0 || nodes) && (nrels == 0 || rels), CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            "entity table arrays");
+    REQUIRE(node_mode == CAPSMI_NODES_REPLICATED || node_mode == CAPSMI_NODES_OWNED, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            "node mode");
+    REQUIRE(rel_mode == CAPSMI_RELS_BY_SOURCE || rel_mode == CAPSMI_RELS_BY_TARGET, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            "relationship mode");
+    HIP_CHECK(hipSetDevice(s->device));
+    const Scramble sc = make_scramble(id_lo, id_hi, s->world);
+    const int64_t own_lo = (int64_t)s->rank * 32 * sc.slice_words, own_hi = own_lo + 32 * sc.slice_words;
+    Buf bad = dev_alloc(2 * sizeof(unsigned long long), s);
+    HIP_CHECK(hipMemsetAsync(P<void>(bad), 0, 2 * sizeof(unsigned long long), s->stream));
+    struct Pending {
+        capsmi_table* t;
+        Column a, b;  // node: did; relationship: dsrc, ddst
+    };
+    std::vector<Pending> work;
+    auto keys = [&](capsmi_table* t, int kind) {
+        need(t, "entity table");
+        REQUIRE(t->sess == s, CAPSMI_ERR_ILLEGAL_ARGUMENT, "table of another session");
+        materialize(t);
+        REQUIRE(t->entity && t->entity->kind == kind, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+                kind == 1 ? "capsmi_graph_distribute: nodes must be registered node tables (capsmi_node_table)"
+                          : "capsmi_graph_distribute: rels must be registered relationship tables (capsmi_rel_table)");
+        REQUIRE(!t->dense || t->shard, CAPSMI_ERR_UNSUPPORTED, "a compacted table cannot also be distributed");
+        Pending p{t, key_column(s, t->nrows), key_column(s, t->nrows)};
+        const EntityInfo& e = *t->entity;
+        if (kind == 1) {
+            const bool owned = node_mode == CAPSMI_NODES_OWNED;
+            scramble_ids(s, sc, t->cols[e.id].d(), t->nrows, P<int64_t>(p.a.data), owned ? own_lo : 0, owned ? own_hi : 0,
+                         P<unsigned long long>(bad));
+        } else {
+            const bool by_src = rel_mode == CAPSMI_RELS_BY_SOURCE;
+            scramble_ids(s, sc, t->cols[e.src].d(), t->nrows, P<int64_t>(p.a.data), by_src ? own_lo : 0,
+                         by_src ? own_hi : 0, P<unsigned long long>(bad));
+            scramble_ids(s, sc, t->cols[e.dst].d(), t->nrows, P<int64_t>(p.b.data), by_src ? 0 : own_lo,
+                         by_src ? 0 : own_hi, P<unsigned long long>(bad));
+        }
+        work.push_back(std::move(p));
+    };
+    for (int i = 0; i < nnodes; ++i) keys(nodes[i], 1);
+    for (int i = 0; i < nrels; ++i) keys(rels[i], 2);
+    unsigned long long h[2] = {0, 0};
+    HIP_CHECK(hipMemcpyAsync(h, P<void>(bad), sizeof(h), hipMemcpyDeviceToHost, s->stream));
+    HIP_CHECK(hipStreamSynchronize(s->stream));
+    REQUIRE(h[0] == 0, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            std::to_string(h[0]) + " ids outside the distributed graph's domain [" + std::to_string(id_lo) + ", " +
+                std::to_string(id_hi) + ")");
+    REQUIRE(h[1] == 0, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            std::to_string(h[1]) + " rows of this rank's shard are owned by another rank (capsmi_owned_rows)");
+    auto dom = std::make_shared<DenseIds>();
+    dom->n = sc.n;
+    dom->scrambled = true;
+    dom->kbits = sc.kbits;
+    dom->mul = sc.mul;
+    dom->mul_inv = sc.mul_inv;
+    dom->lo = id_lo;
+    for (Pending& p : work) {
+        auto sh = std::make_shared<Shard>();
+        sh->kind = p.t->entity->kind;
+        sh->mode = sh->kind == 1 ? node_mode : rel_mode;
+        sh->rank = s->rank;
+        sh->world = s->world;
+        sh->slice_words = sc.slice_words;
+        p.t->dense = dom;
+        if (sh->kind == 1) {
+            p.t->did = p.a;
+        } else {
+            p.t->dsrc = p.a;
+            p.t->ddst = p.b;
+        }
+        p.t->shard = sh;
+        p.t->partitioned = s->world > 1 && !(sh->kind == 1 && node_mode == CAPSMI_NODES_REPLICATED);
+        p.t->layouts.clear();
+    }
+    D_END
+}
+
+capsmi_status capsmi_owned_rows(capsmi_session* s, capsmi_table* t, const char* col, int64_t id_lo, int64_t id_hi,
+                                capsmi_table** out) {
+    D_BEGIN
+    need(s, "session");
+    need(t, "table");
+    need(col, "column");
+    need(out, "out");
+    HIP_CHECK(hipSetDevice(s->device));
+    materialize(t);
+    const int c = t->find(col);
+    REQUIRE(c >= 0, CAPSMI_ERR_ILLEGAL_ARGUMENT, std::string("no column named '") + col + "'");
+    REQUIRE(t->cols[c].type == CAPSMI_I64 && !t->cols[c].valid, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            std::string("owner column '") + col + "' must be a non-null Long column");
+    const Scramble sc = make_scramble(id_lo, id_hi, s->world);
+    const int64_t own_lo = (int64_t)s->rank * 32 * sc.slice_words, own_hi = own_lo + 32 * sc.slice_words;
+    Buf flags = dev_alloc(t->nrows > 0 ? t->nrows : 1, s);
+    owned_flags(s, sc, t->cols[c].d(), t->nrows, own_lo, own_hi, P<uint8_t>(flags));
+    Buf idx;
+    const int64_t n = flags_to_indices(s, P<uint8_t>(flags), t->nrows, idx);
+    auto* o = new capsmi_table();
+    o->sess = s;
+    o->nrows = n;
+    for (const Column& x : t->cols) {
+        Column y;
+        y.name = x.name;
+        y.type = x.type;
+        y.list = x.list;
+        y.data = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
+        if (x.valid) y.valid = dev_alloc(n > 0 ? n : 1, s);
+        gather_col(x.d(), x.v(), P<int64_t>(idx), n, P<int64_t>(y.data), P<uint8_t>(y.valid), s->stream);
+        o->cols.push_back(std::move(y));
+    }
+    *out = o;
+    D_END
+}
+
+capsmi_status capsmi_id_owner(int64_t id_lo, int64_t id_hi, int32_t world, int64_t id, int32_t* owner,
+                              int64_t* dense_id) {
+    D_BEGIN
+    const Scramble sc = make_scramble(id_lo, id_hi, world);
+    REQUIRE(id >= id_lo && id < id_hi, CAPSMI_ERR_ILLEGAL_ARGUMENT, "id outside the domain");
+    const int64_t d = (int64_t)(((uint64_t)(id - id_lo) * sc.mul) & ((uint64_t(1) << sc.kbits) - 1));
+    if (owner) *owner = (int32_t)(d / (32 * sc.slice_words));
+    if (dense_id) *dense_id = d;
+    D_END
+}
+
+capsmi_status capsmi_table_partitioned(const capsmi_table* t, int32_t* out) {
+    D_BEGIN
+    need(t, "table");
+    need(out, "out");
+    materialize(const_cast<capsmi_table*>(t));
+    *out = t->partitioned ? 1 : 0;
+    D_END
+}
+
+}  // extern "C"

@@ -599,7 +599,64 @@ bool classify(const Path& P, Classified& c) {
 // else the dense ids of a compacted graph (capsmi_graph_compact) shared by every scanned table.
 thread_local const DenseIds* g_dense = nullptr;  // domain of the route being planned (one at a time)
 
+// The rank view of a route over a distributed graph (capsmi_graph_distribute, k_dist.hip): the scanned
+// tables are this rank's shards; the route exchanges through the session's collective.
+struct DistView {
+    bool on = false;  // world > 1
+    int rank = 0, world = 1;
+    int64_t slice_words = 0;
+    int rel_mode = -1;  // CAPSMI_RELS_* of the relationship shards
+};
+thread_local DistView g_dist;
+
+// every scanned table a shard of one distributed graph (then g_dense / g_dist are set), none, or a mix (false)
+bool dist_window(const std::vector<Path>& B, bool* any, int64_t* lo, int64_t* hi) {
+    const DenseIds* d = nullptr;
+    const Shard* sh = nullptr;
+    bool all = true;
+    int rel_mode = -1;
+    *any = false;
+    for (const Path& P : B)
+        for (const Scan& sc : P.inst) {
+            int node_mode = -1;
+            for (const Member& m : sc.m) {
+                const capsmi_table* t = m.base;
+                if (!t->shard) { all = false; continue; }
+                *any = true;
+                const DenseIds* e = t->dense.get();  // one domain: equal scramble (tables distributed apart)
+                if (d && (e->n != d->n || e->kbits != d->kbits || e->lo != d->lo || e->mul != d->mul)) return false;
+                d = e;
+                sh = t->shard.get();
+                if (sh->kind == 2) {
+                    if (rel_mode >= 0 && rel_mode != sh->mode) return false;
+                    rel_mode = sh->mode;
+                } else {  // one node scan: all members replicated or all owned
+                    if (node_mode >= 0 && node_mode != sh->mode) return false;
+                    node_mode = sh->mode;
+                }
+            }
+        }
+    if (!*any) return true;
+    if (!all || !d || d->n > (int64_t(1) << 30)) return false;
+    g_dense = d;
+    *lo = 0;
+    *hi = d->n;
+    if (sh->world > 1) {
+        g_dist.on = true;
+        g_dist.rank = sh->rank;
+        g_dist.world = sh->world;
+        g_dist.slice_words = sh->slice_words;
+        g_dist.rel_mode = rel_mode;
+    }
+    return true;
+}
+
 bool id_window(const std::vector<Path>& B, int64_t* lo, int64_t* hi) {
+    g_dist = DistView();
+    g_dense = nullptr;
+    bool any_shard = false;
+    if (!dist_window(B, &any_shard, lo, hi)) return false;
+    if (any_shard) return true;
     int64_t l = INT64_MAX, h = INT64_MIN;
     const DenseIds* d = nullptr;
     bool all_dense = true;
@@ -612,13 +669,12 @@ bool id_window(const std::vector<Path>& B, int64_t* lo, int64_t* hi) {
                 l = std::min(l, m.base->entity->lo);
                 h = std::max(h, m.base->entity->hi);
             }
-    g_dense = nullptr;
     if (l < h && (uint64_t)(h - l) <= (uint64_t(1) << 30)) {
         *lo = l;
         *hi = h;
         return true;
     }
-    if (all_dense && d && d->n > 0 && (uint64_t)d->n <= (uint64_t(1) << 30)) {
+    if (all_dense && d && !d->scrambled && d->n > 0 && (uint64_t)d->n <= (uint64_t(1) << 30)) {
         g_dense = d;
         *lo = 0;
         *hi = d->n;
@@ -654,6 +710,29 @@ std::string member_prog_key(const capsmi_table* base, const std::vector<capsmi_e
     std::string k(reinterpret_cast<const char*>(&base), sizeof(base));
     k.append(reinterpret_cast<const char*>(prog.data()), prog.size() * sizeof(capsmi_expr));
     return k + "|";
+}
+
+// A node scan over OWNED shards (multi-GPU): every rank set the bits of the ids it owns, which lie in
+// its slice of the words; one all-gather of the slices completes the bitmap on every rank, and one SUM
+// all-reduce gives its set-bit count and whether any rank saw a duplicate row (an id's rows are all on
+// its owner, so duplicates are rank-local).
+void gather_owned_bitmap(capsmi_session* s, capsmi_bitmap* b) {
+    const int64_t S = g_dist.slice_words;
+    REQUIRE(b->nwords == S * g_dist.world, CAPSMI_ERR_INTERNAL, "distributed bitmap geometry");
+    Buf full = dev_alloc(sizeof(uint32_t) * (size_t)b->nwords, s);
+    collective(s, CAPSMI_COLL_ALL_GATHER, P<uint32_t>(b->words) + (int64_t)g_dist.rank * S, P<uint32_t>(full), S,
+               CAPSMI_COLL_U32);
+    b->words = full;
+    Buf st = dev_alloc(2 * sizeof(int64_t), s);
+    fill_i64(P<int64_t>(st), b->set_bits, 1, s->stream);
+    fill_i64(P<int64_t>(st) + 1, b->any_dup ? 1 : 0, 1, s->stream);
+    collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(st), P<int64_t>(st), 2, CAPSMI_I64);
+    int64_t h[2];
+    HIP_CHECK(hipMemcpyAsync(h, P<void>(st), sizeof(h), hipMemcpyDeviceToHost, s->stream));
+    HIP_CHECK(hipStreamSynchronize(s->stream));
+    b->set_bits = h[0];
+    b->any_dup = h[1] > 0;
+    b->full = b->set_bits == b->hi - b->lo;
 }
 
 // bitmap of node instance `inst` with its predicate conjuncts over [lo, hi); identical scans share one.
@@ -694,6 +773,9 @@ capsmi_bitmap* node_bitmap(capsmi_session* s, const Path& P, const Classified& c
                                          (int32_t)progs[i].size(), pr));
         }
     }
+    bool owned = false;
+    for (const Member& m : sc.m) owned = owned || (m.base->shard && m.base->shard->mode == CAPSMI_NODES_OWNED);
+    if (g_dist.on && owned) gather_owned_bitmap(s, b);
     return b->any_dup ? nullptr : b;
 }
 
@@ -805,6 +887,55 @@ bool all_pairs_unique(const Classified& c, int nh) {
 }
 
 void route(capsmi_session* s, const char* name) { s->routes[name] += 1; }
+thread_local bool g_missed = false;  // a pattern shape went unrouted during the current materialisation
+
+int64_t sum_over_ranks(capsmi_session* s, int64_t v) {
+    Buf t = dev_alloc(sizeof(int64_t), s);
+    fill_i64(P<int64_t>(t), v, 1, s->stream);
+    collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(t), P<int64_t>(t), 1, CAPSMI_I64);
+    return read_scalar(s, P<int64_t>(t));
+}
+
+// 2-hop count(DISTINCT end) over relationship shards BY_TARGET: hop 1 is complete for the
+// middle ids this rank owns (their in-relationships are all here), one all-gather of the owned slices of
+// the frontier (X1, X2) gives every rank the whole frontier, hop 2 marks the end ids this rank owns, and
+// the owned popcounts add up in one all-reduce.  `cached`: the relationship layout kept by cache().
+int64_t dist_two_hop_distinct(capsmi_session* s, const capsmi_relpart* cached, int32_t nt, capsmi_table* const* views,
+                              const capsmi_bitmap* a, const capsmi_bitmap* b, const capsmi_bitmap* c) {
+    const int64_t S = g_dist.slice_words, nw = b->nwords, r = g_dist.rank;
+    REQUIRE(nw == S * g_dist.world, CAPSMI_ERR_INTERNAL, "distributed bitmap geometry");
+    Buf mid = dev_alloc(sizeof(uint32_t) * 2 * nw, s), scratch = dev_alloc(sizeof(uint32_t) * nw, s);
+    Buf full = dev_alloc(sizeof(uint32_t) * 2 * nw, s), dst = dev_alloc(sizeof(uint32_t) * nw, s);
+    capsmi_relpart* rp = nullptr;
+    if (cached) check(capsmi_two_hop_mark_mid_part(s, cached, a, b, P<uint32_t>(mid), P<uint32_t>(scratch)));
+    else check(capsmi_relpart_build_mark_mid(s, nt, views, "s", "t", a, b, P<uint32_t>(mid), P<uint32_t>(scratch), &rp));
+    std::unique_ptr<capsmi_relpart, capsmi_status (*)(capsmi_relpart*)> hold(rp, capsmi_relpart_release);
+    collective(s, CAPSMI_COLL_ALL_GATHER, P<uint32_t>(mid) + r * S, P<uint32_t>(full), S, CAPSMI_COLL_U32);
+    collective(s, CAPSMI_COLL_ALL_GATHER, P<uint32_t>(mid) + nw + r * S, P<uint32_t>(full) + nw, S, CAPSMI_COLL_U32);
+    check(capsmi_two_hop_mark_dst_part(s, cached ? cached : rp, b, c, P<uint32_t>(full), P<uint32_t>(dst)));
+    Buf cnt = dev_alloc(sizeof(int64_t), s);
+    check(capsmi_words_popcount_device(s, P<uint32_t>(dst), r * S, (r + 1) * S, P<int64_t>(cnt)));
+    collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(cnt), P<int64_t>(cnt), 1, CAPSMI_I64);
+    return read_scalar(s, P<int64_t>(cnt));
+}
+
+// 2-hop count(*) over relationship shards BY_TARGET: each rank's relationships into its owned ids give
+// their complete in-degrees inA; one all-gather of the owned slices gives every rank inA of every id; each
+// rank sums inA(source) over its relationships (less its self-loops) and one all-reduce adds the parts
+int64_t dist_two_hop_count(capsmi_session* s, int32_t nt, capsmi_table* const* views, const capsmi_bitmap* a,
+                           const capsmi_bitmap* b, const capsmi_bitmap* c) {
+    const int64_t S = g_dist.slice_words, n = b->hi - b->lo, r = g_dist.rank;
+    const int64_t own_lo = r * 32 * S, own_hi = std::min(own_lo + 32 * S, n);
+    Buf owned = dev_alloc(sizeof(uint32_t) * 32 * S, s), in_all = dev_alloc(sizeof(uint32_t) * 32 * S * g_dist.world, s);
+    Buf cnt = dev_alloc(sizeof(int64_t), s);
+    capsmi_count_shard* h = nullptr;
+    check(capsmi_count_shard_begin(s, nt, views, "s", "t", a, b, c, own_lo, own_hi, P<uint32_t>(owned), &h));
+    std::unique_ptr<capsmi_count_shard, capsmi_status (*)(capsmi_count_shard*)> hold(h, capsmi_count_shard_release);
+    collective(s, CAPSMI_COLL_ALL_GATHER, P<uint32_t>(owned), P<uint32_t>(in_all), 32 * S, CAPSMI_COLL_U32);
+    check(capsmi_count_shard_finish(h, P<uint32_t>(in_all), P<int64_t>(cnt)));
+    collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(cnt), P<int64_t>(cnt), 1, CAPSMI_I64);
+    return read_scalar(s, P<int64_t>(cnt));
+}
 
 // count(*) / count(DISTINCT end | start) of one branch: 1 hop, a 2-hop chain, or the closed triangle.
 // Returns false when the shape or a precondition does not hold.
@@ -834,6 +965,7 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
             total += o->nrows;
             capsmi_table_release(o);
         }
+        if (g_dist.on) total = sum_over_ranks(s, total);  // each rank counted its own relationships
         vals.assign(kinds.size(), total);
         route(s, "expand_count");
         return true;
@@ -842,6 +974,11 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
         RelViews v1;
         rel_views(P, P.hops[1], v1);
         if (v1.sig != v0.sig || !all_pairs_unique(c, 2)) return false;
+        if (g_dist.on) {  // over relationship shards BY_TARGET: count(*) and count(DISTINCT end)
+            if (g_dist.rel_mode != CAPSMI_RELS_BY_TARGET) return false;
+            for (int k : kinds)
+                if (k == A_DISTINCT_START || (k == A_COUNT && hi - lo > (int64_t(1) << 26))) return false;
+        }
         capsmi_bitmap* a = node_bitmap(s, P, c, P.pos_node[0], lo, hi, bs);
         capsmi_bitmap* b = node_bitmap(s, P, c, P.pos_node[1], lo, hi, bs);
         capsmi_bitmap* cc = node_bitmap(s, P, c, P.pos_node[2], lo, hi, bs);
@@ -852,7 +989,11 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
         for (const Member& m : R.m) keep = keep && m.base->keep_layouts;
         for (int k : kinds) {
             int64_t x = 0;
-            if (k == A_COUNT) {
+            if (g_dist.on && k == A_COUNT) {
+                x = dist_two_hop_count(s, (int32_t)nt, v0.t.data(), a, b, cc);
+            } else if (g_dist.on && !keep) {
+                x = dist_two_hop_distinct(s, nullptr, (int32_t)nt, v0.t.data(), a, b, cc);
+            } else if (k == A_COUNT) {
                 check(capsmi_two_hop_count(s, (int32_t)nt, v0.t.data(), "s", "t", a, b, cc, &x));
             } else if (keep) {
                 const bool rev = k == A_DISTINCT_START;  // distinct start = distinct end of the reversed walk
@@ -866,7 +1007,8 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
                                            capsmi_relpart_release(q);
                                        })).first;
                 }
-                check(capsmi_two_hop_count_distinct_part(s, it->second.get(), rev ? cc : a, b, rev ? a : cc, &x));
+                if (g_dist.on) x = dist_two_hop_distinct(s, it->second.get(), 0, nullptr, a, b, cc);
+                else check(capsmi_two_hop_count_distinct_part(s, it->second.get(), rev ? cc : a, b, rev ? a : cc, &x));
             } else if (k == A_DISTINCT_END) {
                 check(capsmi_two_hop_count_distinct(s, (int32_t)nt, v0.t.data(), "s", "t", a, b, cc, &x));
             } else {  // distinct start: the same walk over the reversed relationships
@@ -877,7 +1019,7 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
         route(s, "two_hop");
         return true;
     }
-    if (nh == 3 && P.pos_node.size() == 3 && same_orientation(P)) {
+    if (nh == 3 && P.pos_node.size() == 3 && same_orientation(P) && !g_dist.on) {
         // P0 -h0-> P1 -h1-> P2 -h2-> P0 (the closing hop is the ExpandInto)
         const Hop &h0 = P.hops[0], &h1 = P.hops[1], &h2 = P.hops[2];
         if (!(h0.from == 0 && h0.to == 1 && h1.from == 1 && h1.to == 2 && h2.from == 2 && h2.to == 0)) return false;
@@ -963,13 +1105,21 @@ bool fused_var_length(capsmi_session* s, const capsmi_table* in, const PlanNode&
     if (first || (lens.count(0) && zero_key != akey)) return false;  // a path of >= 1 hop; one start scan
     const int l = *lens.begin(), u = *lens.rbegin();
     if (l < 0 || u > 3 || u - l + 1 != (int)lens.size()) return false;
+    if (g_dist.on) return false;  // the sharded C5 needs in- and out-relationship shards (capsmi_varlen_shard_*)
     check(capsmi_var_length_count(s, (int32_t)views.t.size(), views.t.data(), "s", "t", abm, bbm, l, u, g.a[0].c_str(),
                                   ag.output.c_str(), out));
     if (g_dense) {  // start ids back to the graph's Long ids
         capsmi_table* r = *out;
         Column& c = r->cols[0];
         Buf ids = dev_alloc(sizeof(int64_t) * (r->nrows > 0 ? r->nrows : 1), s);
-        gather_col(P<int64_t>(g_dense->orig), nullptr, c.d(), r->nrows, ::capsmi::P<int64_t>(ids), nullptr, s->stream);
+        if (g_dense->scrambled) {
+            if (r->nrows)
+                HIP_CHECK(hipMemcpyAsync(::capsmi::P<int64_t>(ids), c.d(), sizeof(int64_t) * r->nrows,
+                                         hipMemcpyDeviceToDevice, s->stream));
+            unscramble_ids(s, *g_dense, ::capsmi::P<int64_t>(ids), r->nrows);
+        } else {
+            gather_col(P<int64_t>(g_dense->orig), nullptr, c.d(), r->nrows, ::capsmi::P<int64_t>(ids), nullptr, s->stream);
+        }
         c.data = ids;
         c.offset = 0;
         c.host.reset();
@@ -1073,13 +1223,31 @@ bool fused_projection(capsmi_session* s, const capsmi_table* t, const std::vecto
             acc = u;
         }
     }
+    acc->partitioned = g_dist.on;  // this rank's relationships' rows
     *out = acc;
     route(s, "expand");
     return true;
 }
 
 // try the fused shapes for lazy table `t`; on success *out is its materialised content
+bool try_fused_shapes(capsmi_table* t, capsmi_table** out);
+
+bool has_hop(const std::vector<Path>& B) {
+    for (const Path& P : B) if (!P.hops.empty()) return true;
+    return false;
+}
+
+// a plan over entity tables in a pattern shape that no fused route took: counted once per
+// materialisation as route "miss" (capsmi_session_route_count)
 bool try_fused(capsmi_table* t, capsmi_table** out) {
+    if (try_fused_shapes(t, out)) return true;
+    const PlanNode& p = *t->plan;
+    std::vector<Path> B;
+    if (as_paths(p.kind == PlanNode::GROUP ? p.in[0] : t, B) && has_hop(B)) g_missed = true;
+    return false;
+}
+
+bool try_fused_shapes(capsmi_table* t, capsmi_table** out) {
     capsmi_session* s = t->sess;
     if (!s->fused) return false;
     const PlanNode& p = *t->plan;
@@ -1243,12 +1411,73 @@ Res finish(Res r, const Names& need, const std::vector<Pred>& preds) {
             prog.push_back(a);
         }
         check(eager_filter_keep(r.t, (int32_t)prog.size(), prog.data(), keep, &o));
+        o->partitioned = r.t->partitioned;
         return owned(o);
     }
     if (keep.size() == r.t->cols.size()) return r;
     auto c = cstrs(keep);
     check(eager_select(r.t, (int32_t)c.size(), c.data(), &o));
+    o->partitioned = r.t->partitioned;
     return owned(o);
+}
+
+// A row-local operator keeps its input's partitioning; an operator that needs every row of its input
+// (join, aggregate, distinct, order, skip, limit) cannot run on one rank's partition of a distributed
+// result -- Spark would insert an Exchange there (SparkTable.scala:133, 226), this backend only has the
+// exchanges of the fused routes.
+void refuse_partitioned(const capsmi_table* in, const char* op) {
+    REQUIRE(!in->partitioned, CAPSMI_ERR_UNSUPPORTED,
+            std::string(op) + " over one rank's partition of a distributed graph needs an exchange the fused routes "
+                              "do not provide (route this pattern, or run it on one device)");
+}
+
+// ---- unrouted-plan size guard (capsmi_session_set_unrouted_limit) ------------------------------------
+// System-R estimates of a lazy plan's rows: a join emits |L| |R| / max(ndv(l), ndv(r)) rows, where the
+// ndv of an entity key column is its scan's rows (node ids) or min(rows, id window) (endpoints).
+double key_ndv(const capsmi_table* t, const std::string& col, double rows) {
+    Scan sc;
+    const int c = find_col(t, col);
+    if (c < 0 || !as_scan(t, sc)) return rows;
+    double n = 0, span = 0;
+    for (const Member& m : sc.m) {
+        n += (double)m.base->nrows;
+        span = std::max(span, (double)(m.base->entity->hi - m.base->entity->lo));
+    }
+    if (sc.role[c] == ROLE_ID) return std::max(1.0, n);
+    if (sc.role[c] == ROLE_SRC || sc.role[c] == ROLE_DST) return std::max(1.0, std::min(n, span));
+    return rows;
+}
+
+double est_rows(const capsmi_table* t) {
+    if (!t->lazy()) return (double)t->nrows;
+    const PlanNode& p = *t->plan;
+    switch (p.kind) {
+        case PlanNode::UNION: return est_rows(p.in[0]) + est_rows(p.in[1]);
+        case PlanNode::SKIP: return std::max(0.0, est_rows(p.in[0]) - (double)p.n);
+        case PlanNode::LIMIT: return std::min((double)p.n, est_rows(p.in[0]));
+        case PlanNode::JOIN: {
+            const double l = est_rows(p.in[0]), r = est_rows(p.in[1]);
+            if (p.jt == CAPSMI_JOIN_CROSS) return l * r;
+            double ndv = 1;
+            for (size_t i = 0; i < p.a.size(); ++i)
+                ndv = std::max(ndv, std::max(key_ndv(p.in[0], p.a[i], l), key_ndv(p.in[1], p.b[i], r)));
+            double e = l * r / ndv;
+            if (p.jt == CAPSMI_JOIN_LEFT_OUTER || p.jt == CAPSMI_JOIN_FULL_OUTER) e = std::max(e, l);
+            if (p.jt == CAPSMI_JOIN_RIGHT_OUTER || p.jt == CAPSMI_JOIN_FULL_OUTER) e = std::max(e, r);
+            return e;
+        }
+        default: return est_rows(p.in[0]);
+    }
+}
+
+void guard_join(const capsmi_table* t) {
+    const int64_t limit = t->sess->unrouted_limit;
+    if (limit <= 0) return;
+    const double bytes = est_rows(t) * (double)t->cols.size() * 9.0;  // 8-B words + validity bytes
+    REQUIRE(bytes <= (double)limit, CAPSMI_ERR_UNSUPPORTED,
+            "unrouted join estimated at " + std::to_string((long long)(bytes / 1e9)) + " GB (" +
+                std::to_string((long long)est_rows(t)) + " rows) exceeds the session limit of " +
+                std::to_string((long long)(limit / 1000000000LL)) + " GB; no fused route matched this pattern");
 }
 
 using Parents = std::map<const capsmi_table*, int>;
@@ -1302,6 +1531,7 @@ Res exec(capsmi_table* t, const Names& need, std::vector<Pred> preds, const Pare
             if (r.t->find(a) < 0) return r;
             capsmi_table* o = nullptr;
             check(eager_with_column_renamed(r.t, a.c_str(), b.c_str(), &o));
+            o->partitioned = r.t->partitioned;
             return owned(o);
         }
         case PlanNode::WITH_COLUMNS: {
@@ -1336,6 +1566,7 @@ Res exec(capsmi_table* t, const Names& need, std::vector<Pred> preds, const Pare
                 }
                 capsmi_table* o = nullptr;
                 check(eager_with_columns(r.t, (int32_t)cols.size(), cols.data(), &o));
+                o->partitioned = r.t->partitioned;
                 r = owned(o);
             }
             return finish(std::move(r), need, stay);
@@ -1364,8 +1595,11 @@ Res exec(capsmi_table* t, const Names& need, std::vector<Pred> preds, const Pare
             for (const std::string& n : out) add(has(L, n) ? nl : nr, n);
             for (const std::string& n : p.a) add(nl, n);
             for (const std::string& n : p.b) add(nr, n);
+            guard_join(t);
             Res a = exec(x, nl, std::move(pl), par);
             Res b = exec(y, nr, std::move(pr), par);
+            refuse_partitioned(a.t, "a join");
+            refuse_partitioned(b.t, "a join");
             auto lk = cstrs(p.a), rk = cstrs(p.b);
             capsmi_table* o = nullptr;
             check(eager_join(a.t, b.t, p.jt, (int32_t)lk.size(), lk.data(), rk.data(), &o));
@@ -1397,8 +1631,11 @@ Res exec(capsmi_table* t, const Names& need, std::vector<Pred> preds, const Pare
             run.aggs = p.aggs;
             run.jt = p.jt;
             run.n = p.n;
+            bool part = false;
             for (size_t i = 0; i < p.in.size(); ++i) {
                 Res r = exec(p.in[i], nin[i], {}, par);
+                if (p.kind != PlanNode::UNION) refuse_partitioned(r.t, "an aggregate, distinct, order, skip or limit");
+                part = part || r.t->partitioned;
                 if (p.kind == PlanNode::UNION) {  // positional: the input's schema order
                     capsmi_table* o = nullptr;
                     auto c = cstrs(nin[i]);
@@ -1407,7 +1644,9 @@ Res exec(capsmi_table* t, const Names& need, std::vector<Pred> preds, const Pare
                 }
                 hold(run, r.t);
             }
-            return finish(owned(exec_node(run)), need, preds);
+            capsmi_table* o = exec_node(run);
+            o->partitioned = part;
+            return finish(owned(o), need, preds);
         }
     }
     return Res();
@@ -1425,12 +1664,23 @@ void materialize(capsmi_table* t) {
     Names uniq;
     for (const std::string& n : all) add(uniq, n);
     capsmi_table* r = nullptr;
+    const bool outer_missed = g_missed;  // a shared sub-plan materialises inside another materialisation
+    g_missed = false;
+    int64_t routed_before = 0;
+    for (auto& kv : t->sess->routes) routed_before += kv.first == "miss" ? 0 : kv.second;
     {
         Res e = exec(t, uniq, {}, par);
         auto c = cstrs(all);
         check(eager_select(e.t, (int32_t)c.size(), c.data(), &r));  // schema order, an owned table
+        r->partitioned = e.t->partitioned;
     }
+    int64_t routed_after = 0;
+    for (auto& kv : t->sess->routes) routed_after += kv.first == "miss" ? 0 : kv.second;
+    if (g_missed && routed_after == routed_before) t->sess->routes["miss"] += 1;  // a pattern ran unrouted
+    g_missed = outer_missed;
+    const bool part = r->partitioned;
     adopt(t, r);
+    t->partitioned = part;
     t->plan.reset();  // the inputs are released unless shared elsewhere
 }
 
@@ -1748,6 +1998,14 @@ capsmi_status capsmi_session_set_fused(capsmi_session* s, int32_t enabled) {
     P_BEGIN
     need(s, "session");
     s->fused = enabled != 0;
+    P_END
+}
+
+capsmi_status capsmi_session_set_unrouted_limit(capsmi_session* s, int64_t max_bytes) {
+    P_BEGIN
+    need(s, "session");
+    REQUIRE(max_bytes >= 0, CAPSMI_ERR_ILLEGAL_ARGUMENT, "negative limit");
+    s->unrouted_limit = max_bytes;
     P_END
 }
 

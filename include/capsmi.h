@@ -220,7 +220,14 @@ typedef struct {
     const capsmi_value* values;
 } capsmi_param;
 capsmi_status capsmi_session_set_params(capsmi_session* s, int32_t nparams, const capsmi_param* params);
+/* route "miss" counts materialisations in which a pattern over entity tables (joins of node and
+ * relationship scans) matched no fused shape and ran operator by operator */
 capsmi_status capsmi_session_route_count(capsmi_session* s, const char* name, int64_t* count);
+/* refuse (CAPSMI_ERR_UNSUPPORTED, before any work) an unrouted join whose estimated output -- System-R
+ * row estimates, entity key columns' distinct counts from their scans -- exceeds max_bytes of 8-byte
+ * words; 0 (the default) = no limit.  A guard against a pattern that misses every fused shape and
+ * would materialise its bindings (~10^13 rows at the C3 scale). */
+capsmi_status capsmi_session_set_unrouted_limit(capsmi_session* s, int64_t max_bytes);
 
 /* ---- tables (CypherTable: okapi-api/.../api/table/CypherTable.scala:41-68) -------- */
 /* CAPSNodeTable/CAPSRelationshipTable ingest (spark-cypher/.../api/io/CAPSTable.scala:47-214): copies */
@@ -496,6 +503,58 @@ capsmi_status capsmi_words_popcount_device(capsmi_session* s, const uint32_t* wo
 capsmi_status capsmi_cluster_by(capsmi_table* rels, const char* key_col, int64_t id_lo, int64_t id_hi,
                                 capsmi_table** out);
 
+/* ---- multi-GPU: one process per GPU over a distributed graph -------------------
+ * Spark runs each Table operator over partitions and inserts a hash Exchange before joins and
+ * aggregations (SparkTable.scala:133, 226; partitions set in CAPSSession.scala:115-131).  Here every
+ * rank runs the same query (the same Table[T] calls) over its shard of a distributed graph; the fused
+ * routes call the host's collective at their exchange points, so one rank's materialisation is one
+ * rank's share of the job and the collective completes the answer on every rank.
+ *
+ * Ownership (hash partitioning): ids of the graph's domain [id_lo, id_hi) are scrambled by the
+ * bijection h(x) = ((x - id_lo) * 0x9E3779B97F4A7C15) mod 2^k (2^k >= id_hi - id_lo, k >= 5) and rank
+ * r owns the h-range [r * 32 * S, (r + 1) * 32 * S), S = ceil(2^k / (32 * world)) words -- balanced
+ * whatever the id order (hubs at small ids included); the fused kernels run on h(x).
+ *
+ * The collective: enqueue one collective on the session's stream, ordered after the work queued on it
+ * and before the work queued after the call returns (e.g. torch.distributed / RCCL on that stream).
+ * ALL_GATHER: `count` elements from every rank into recv, rank-major (world x count);
+ * ALL_REDUCE_SUM / _MAX: `count` elements, send and recv may be equal.  dtype CAPSMI_I64 (int64) or
+ * CAPSMI_COLL_U32 (uint32 words).  Return 0 on success. */
+enum { CAPSMI_COLL_ALL_GATHER = 0, CAPSMI_COLL_ALL_REDUCE_SUM = 1, CAPSMI_COLL_ALL_REDUCE_MAX = 2 };
+enum { CAPSMI_COLL_U32 = 100 };
+typedef int32_t (*capsmi_collective_fn)(void* ctx, int32_t op, const void* send, void* recv, int64_t count,
+                                        int32_t dtype);
+/* this process is rank `rank` of `world`; fn may be NULL only for world == 1 */
+capsmi_status capsmi_session_set_ranks(capsmi_session* s, int32_t rank, int32_t world, capsmi_collective_fn fn,
+                                       void* ctx);
+enum { CAPSMI_NODES_REPLICATED = 0, CAPSMI_NODES_OWNED = 1 };
+enum { CAPSMI_RELS_BY_SOURCE = 0, CAPSMI_RELS_BY_TARGET = 1 };
+/* Registers this rank's entity tables (capsmi_node_table / capsmi_rel_table) as its shard of a graph
+ * over the id domain [id_lo, id_hi) (the same on every rank, covering every id; hi - lo <= 2^30):
+ * node tables hold every node row (REPLICATED) or the rows of the ids this rank owns (OWNED);
+ * relationship tables hold the relationships whose target (BY_TARGET) or source (BY_SOURCE) this rank
+ * owns.  Checked: ids inside the domain and the shard's rows owned (else ILLEGAL_ARGUMENT).  The
+ * tables keep their scrambled key columns.  Routed on a distributed graph: Expand projections (rows of
+ * this rank's relationships) and count(*) (one SUM all-reduce); with BY_TARGET the 2-hop
+ * count(DISTINCT end) (all-gathers of the owned node-scan bitmap words and hop-1 frontier, one
+ * all-reduce) and the 2-hop count(*) (an all-gather of the owned in-degrees, one all-reduce).  A
+ * plan over a distributed graph that would need another exchange (a generic join, aggregate, distinct
+ * or ordering over partitioned rows) is CAPSMI_ERR_UNSUPPORTED; capsmi_table_partitioned tells which
+ * results hold this rank's rows only. */
+capsmi_status capsmi_graph_distribute(capsmi_session* s, int64_t id_lo, int64_t id_hi, int32_t nnodes,
+                                      capsmi_table* const* nodes, int32_t node_mode, int32_t nrels,
+                                      capsmi_table* const* rels, int32_t rel_mode);
+/* the rows of `t` whose Long column `col` holds an id this rank owns in [id_lo, id_hi) (ingest: a
+ * rank keeps its shard of a table every rank read); a new materialised table */
+capsmi_status capsmi_owned_rows(capsmi_session* s, capsmi_table* t, const char* col, int64_t id_lo, int64_t id_hi,
+                                capsmi_table** out);
+/* the rank owning Long id `id` of the domain [id_lo, id_hi) among `world` ranks, and its scrambled
+ * dense id (host computation, no device) */
+capsmi_status capsmi_id_owner(int64_t id_lo, int64_t id_hi, int32_t world, int64_t id, int32_t* owner,
+                              int64_t* dense_id);
+/* 1 when t's rows are this rank's partition of a distributed result, else 0 (materialises t) */
+capsmi_status capsmi_table_partitioned(const capsmi_table* t, int32_t* out);
+
 /* ---- synthetic input -----------------------------------------------------
  * R-MAT relationship table [id, source, target] generated on the device, identical edge for edge
  * to oracle/rmat.c.  Keeps edges e in [e_begin, e_end) whose `part_col` (0 = source, 1 = target,
@@ -511,8 +570,7 @@ capsmi_status capsmi_owner_words(int64_t nbits, int32_t part, int32_t nparts, in
  * and the FS graph source read their tables: files in order, no header, `delimiter` one character
  * (as Spark's `sep`: "1  2" with ' ' is 1, null, 2; 0 = opt-in whitespace splitting, runs of blanks
  * separate fields), '"' quotes, an empty unquoted field is null, lines whose first character is
- * `comment` (0 = none) and lines of blanks skipped
- * skipped; Spark's PERMISSIVE token counts (missing trailing fields null, extra tokens dropped);
+ * `comment` (0 = none) and lines of blanks skipped; Spark's PERMISSIVE token counts (missing trailing fields null, extra tokens dropped);
  * a token that does not parse as its column type is ILLEGAL_ARGUMENT.  Parsed by host threads
  * (CAPSMI_INGEST_THREADS, default OMP_NUM_THREADS), copied to the device.  types: CAPSMI_I64 /
  * F64 / BOOL / STR; STR fields go through `intern` (the caller's dictionary), in row order.

@@ -35,10 +35,15 @@ def _run(wl, scale, n=2):
 
 
 def test_c3_two_ranks():
+    """bench.py's N-rank C3: every mode (cold, warm, count(*)) is Planner(sg).run through the route on
+    every rank of the distributed graph; shards balanced by the hash ownership."""
     d = _run("c3", 16)
     assert d["n_gpus"] == 2
     assert d["query"]["check_vs_fixture"] == "ok"
     assert d["query"]["rels_local_rank0"] < 16 << 16  # rank 0 holds only its owner(target) share
+    assert d["query"]["rels_max_over_mean"] < 1.05
+    assert d["config"]["route"].startswith("Planner(sg).run") and "plans routed" in d["config"]["route"]
+    assert d["roofline"]["traffic"] is None  # the committed PMC profiles are 1-GPU runs
 
 
 def test_c5_two_ranks():
