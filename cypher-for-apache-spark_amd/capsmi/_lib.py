@@ -161,6 +161,8 @@ _SIGS = {
     "capsmi_trigraph_release": (c_int32, [P]),
     "capsmi_trigraph_stats": (c_int32, [P, POINTER(c_int64), POINTER(c_int64)]),
     "capsmi_triangle_count": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, POINTER(c_int64)]),
+    "capsmi_undirected_count": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, c_int32, P, P, P, c_int32,
+                                          POINTER(c_int64)]),
     "capsmi_var_length_count": (c_int32, [P, c_int32, PP, c_char_p, c_char_p, P, P, c_int32, c_int32, c_char_p,
                                           c_char_p, PP]),
     "capsmi_varlen_shard_begin": (c_int32, [P, c_int32, PP, c_int32, PP, c_char_p, c_char_p, P, P, c_int32, c_int32,

@@ -1533,6 +1533,31 @@ capsmi_status capsmi_relpart_build_mark_mid(capsmi_session* s, int32_t nrels, ca
     API_END
 }
 
+capsmi_status capsmi_undirected_count(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                                      const char* dst_col, int32_t hops, const capsmi_bitmap* a_ok,
+                                      const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok, int32_t kind, int64_t* out) {
+    API_BEGIN
+    need(s, "session");
+    need(out, "out");
+    check_bitmap(a_ok, "a_ok");
+    check_bitmap(b_ok, "b_ok");
+    REQUIRE(hops == 1 || hops == 2, CAPSMI_ERR_ILLEGAL_ARGUMENT, "undirected patterns: 1 or 2 hops");
+    REQUIRE(kind >= 0 && kind <= 2, CAPSMI_ERR_ILLEGAL_ARGUMENT, "undirected patterns: kind");
+    if (hops == 2) check_bitmap(c_ok, "c_ok");
+    use_device(s);
+    std::vector<const int64_t*> srcs, dsts;
+    std::vector<int64_t> ms;
+    for (int i = 0; i < nrels; ++i) {
+        need(rels[i], "rels[i]");
+        M(rels[i]);
+        srcs.push_back(rel_col(rels[i], src_col).d());
+        dsts.push_back(rel_col(rels[i], dst_col).d());
+        ms.push_back(rels[i]->nrows);
+    }
+    *out = undirected_count(s, srcs.data(), dsts.data(), ms.data(), nrels, hops, a_ok, b_ok, hops == 2 ? c_ok : b_ok, kind);
+    API_END
+}
+
 capsmi_status capsmi_var_length_count(capsmi_session* s, int32_t nrels, capsmi_table* const* rels,
                                       const char* src_col, const char* dst_col, const capsmi_bitmap* a_ok,
                                       const capsmi_bitmap* b_ok, int32_t lower, int32_t upper, const char* id_name,

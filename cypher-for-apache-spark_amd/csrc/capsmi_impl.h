@@ -387,6 +387,18 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
                const capsmi_bitmap* n_ok, TriGraph& g);
 uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts);
 
+// undirected Expand patterns (k_undirected.hip): hops 1 or 2; kind 0 count(*), 1 count(DISTINCT end),
+// 2 count(DISTINCT start); c unused for one hop
+int64_t undirected_count(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
+                         int nt, int hops, const capsmi_bitmap* a, const capsmi_bitmap* b, const capsmi_bitmap* c,
+                         int kind);
+
+// the 2-hop chain grouped by its start (k_grouped.hip): rows (relative start id, count(*) or count(DISTINCT
+// end)); false when the distinct keys would exceed key_budget bytes
+bool grouped_two_hop(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
+                     int nt, const capsmi_bitmap* a, const capsmi_bitmap* b, const capsmi_bitmap* c, bool distinct,
+                     int64_t key_budget, Buf& out_ids, Buf& out_vals, int64_t* rows);
+
 // fused var-length grouped count (k_varlen.hip)
 int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
                          int nt, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, int lower, int upper,

@@ -202,6 +202,9 @@ struct Scan {
     int kind = 0;  // 1 node, 2 relationship
     std::vector<Member> m;
     std::vector<int> role;  // per scan column: ROLE_* in every member, else ROLE_NONE
+    // relationship scan filtered to start <> end: the incoming branch of an undirected Expand
+    // (RelationalPlanner.scala:130-131)
+    bool no_loops = false;
 };
 
 void scan_roles(Scan& sc, size_t ncols) {
@@ -287,9 +290,20 @@ bool as_scan(const capsmi_table* t, Scan& sc) {
         }
         case PlanNode::UNION: {
             Scan r;
-            if (!as_scan(in, sc) || !as_scan(p.in[1], r) || sc.kind != r.kind) return false;
+            if (!as_scan(in, sc) || !as_scan(p.in[1], r) || sc.kind != r.kind || sc.no_loops || r.no_loops) return false;
             for (Member& m : r.m) sc.m.push_back(std::move(m));
             break;
+        }
+        case PlanNode::FILTER: {  // only NOT(start = end) / start <> end over a relationship scan
+            if (!as_scan(in, sc) || sc.kind != 2 || sc.no_loops) return false;
+            const auto& pr = p.progs[0];
+            const bool neq = pr.size() == 3 && pr[2].op == CAPSMI_X_NEQ;
+            const bool negated_eq = pr.size() == 4 && pr[2].op == CAPSMI_X_EQ && pr[3].op == CAPSMI_X_NOT;
+            if (!(neq || negated_eq) || pr[0].op != CAPSMI_X_COL || pr[1].op != CAPSMI_X_COL) return false;
+            const int r0 = sc.role[pr[0].arg], r1 = sc.role[pr[1].arg];
+            if (!((r0 == ROLE_SRC && r1 == ROLE_DST) || (r0 == ROLE_DST && r1 == ROLE_SRC))) return false;
+            sc.no_loops = true;
+            return true;  // same columns, same roles
         }
         default: return false;
     }
@@ -374,6 +388,61 @@ int position_of(const Path& P, const Role& r) {
 
 bool as_paths(const capsmi_table* t, std::vector<Path>& out);
 
+// one left path joined with scan R (JOIN node p over left input `in`): a node scan completes a position,
+// a relationship scan adds a hop (Expand) or closes one (ExpandInto)
+bool join_path(Path P, const capsmi_table* in, const PlanNode& p, const Scan& R, std::vector<Path>& out) {
+    const int ri = (int)P.inst.size();
+    std::vector<int> lk, rk;
+    for (size_t i = 0; i < p.a.size(); ++i) {
+        lk.push_back(find_col(in, p.a[i]));
+        rk.push_back(find_col(p.in[1], p.b[i]));
+        if (lk.back() < 0 || rk.back() < 0) return false;
+    }
+    P.inst.push_back(R);
+    if (R.kind == 1) {
+        if (lk.size() != 1 || R.role[rk[0]] != ROLE_ID) return false;
+        const int pos = position_of(P, P.cols[lk[0]]);
+        if (pos < 0 || P.pos_node[pos] >= 0) return false;
+        P.pos_node[pos] = ri;
+    } else {
+        if (lk.size() == 1) {  // Expand: a new position
+            const int pos = position_of(P, P.cols[lk[0]]);
+            const int rr = R.role[rk[0]];
+            if (pos < 0 || (rr != ROLE_SRC && rr != ROLE_DST)) return false;
+            Hop h;
+            h.rel = ri;
+            h.from = pos;
+            h.to = (int)P.pos_node.size();
+            h.from_role = rr;
+            h.to_role = rr == ROLE_SRC ? ROLE_DST : ROLE_SRC;
+            P.pos_node.push_back(-1);
+            P.hops.push_back(h);
+        } else if (lk.size() == 2) {  // ExpandInto: both ends bound
+            const int p1 = position_of(P, P.cols[lk[0]]), p2 = position_of(P, P.cols[lk[1]]);
+            const int r1 = R.role[rk[0]], r2 = R.role[rk[1]];
+            if (p1 < 0 || p2 < 0 || !((r1 == ROLE_SRC && r2 == ROLE_DST) || (r1 == ROLE_DST && r2 == ROLE_SRC)))
+                return false;
+            Hop h;
+            h.rel = ri;
+            h.from = r1 == ROLE_SRC ? p1 : p2;
+            h.to = r1 == ROLE_SRC ? p2 : p1;
+            P.hops.push_back(h);
+        } else {
+            return false;
+        }
+    }
+    const capsmi_table* rt = p.in[1];
+    for (size_t k = 0; k < rt->cols.size(); ++k) {
+        Role r;
+        r.k = R.kind == 1 ? RK_NODE : RK_REL;
+        r.inst = ri;
+        r.scol = (int)k;
+        P.cols.push_back(r);
+    }
+    out.push_back(std::move(P));
+    return true;
+}
+
 bool as_paths_node(const capsmi_table* t, std::vector<Path>& out) {
     const PlanNode& p = *t->plan;
     const capsmi_table* in = p.in[0];
@@ -382,57 +451,11 @@ bool as_paths_node(const capsmi_table* t, std::vector<Path>& out) {
             if (p.jt != CAPSMI_JOIN_INNER) return false;
             std::vector<Path> L;
             Scan R;
-            if (!as_paths(in, L) || L.size() != 1 || !as_scan(p.in[1], R)) return false;
-            Path P = std::move(L[0]);
-            const int ri = (int)P.inst.size();
-            std::vector<int> lk, rk;
-            for (size_t i = 0; i < p.a.size(); ++i) {
-                lk.push_back(find_col(in, p.a[i]));
-                rk.push_back(find_col(p.in[1], p.b[i]));
-                if (lk.back() < 0 || rk.back() < 0) return false;
-            }
-            P.inst.push_back(R);
-            if (R.kind == 1) {
-                if (lk.size() != 1 || R.role[rk[0]] != ROLE_ID) return false;
-                const int pos = position_of(P, P.cols[lk[0]]);
-                if (pos < 0 || P.pos_node[pos] >= 0) return false;
-                P.pos_node[pos] = ri;
-            } else {
-                if (lk.size() == 1) {  // Expand: a new position
-                    const int pos = position_of(P, P.cols[lk[0]]);
-                    const int rr = R.role[rk[0]];
-                    if (pos < 0 || (rr != ROLE_SRC && rr != ROLE_DST)) return false;
-                    Hop h;
-                    h.rel = ri;
-                    h.from = pos;
-                    h.to = (int)P.pos_node.size();
-                    h.from_role = rr;
-                    h.to_role = rr == ROLE_SRC ? ROLE_DST : ROLE_SRC;
-                    P.pos_node.push_back(-1);
-                    P.hops.push_back(h);
-                } else if (lk.size() == 2) {  // ExpandInto: both ends bound
-                    const int p1 = position_of(P, P.cols[lk[0]]), p2 = position_of(P, P.cols[lk[1]]);
-                    const int r1 = R.role[rk[0]], r2 = R.role[rk[1]];
-                    if (p1 < 0 || p2 < 0 || !((r1 == ROLE_SRC && r2 == ROLE_DST) || (r1 == ROLE_DST && r2 == ROLE_SRC)))
-                        return false;
-                    Hop h;
-                    h.rel = ri;
-                    h.from = r1 == ROLE_SRC ? p1 : p2;
-                    h.to = r1 == ROLE_SRC ? p2 : p1;
-                    P.hops.push_back(h);
-                } else {
-                    return false;
-                }
-            }
-            const capsmi_table* rt = p.in[1];
-            for (size_t k = 0; k < rt->cols.size(); ++k) {
-                Role r;
-                r.k = R.kind == 1 ? RK_NODE : RK_REL;
-                r.inst = ri;
-                r.scol = (int)k;
-                P.cols.push_back(r);
-            }
-            out.push_back(std::move(P));
+            if (!as_paths(in, L) || L.empty() || !as_scan(p.in[1], R)) return false;
+            // a join over a union of branches is the union of the joins (the second hop of an
+            // undirected Expand joins both branches of the first)
+            for (Path& lp : L)
+                if (!join_path(std::move(lp), in, p, R, out)) return false;
             return true;
         }
         case PlanNode::FILTER: {
@@ -887,6 +910,11 @@ bool all_pairs_unique(const Classified& c, int nh) {
 }
 
 void route(capsmi_session* s, const char* name) { s->routes[name] += 1; }
+
+bool any_no_loops(const Path& P) {  // an undirected branch: only fused_undirected takes it
+    for (const Scan& sc : P.inst) if (sc.no_loops) return true;
+    return false;
+}
 thread_local bool g_missed = false;  // a pattern shape went unrouted during the current materialisation
 
 int64_t sum_over_ranks(capsmi_session* s, int64_t v) {
@@ -941,7 +969,7 @@ int64_t dist_two_hop_count(capsmi_session* s, int32_t nt, capsmi_table* const* v
 // Returns false when the shape or a precondition does not hold.
 bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kinds, std::vector<int64_t>& vals) {
     Classified c;
-    if (!classify(P, c)) return false;
+    if (any_no_loops(P) || !classify(P, c)) return false;
     for (int x : P.pos_node) if (x < 0) return false;
     const size_t nh = P.hops.size();
     if (nh < 1 || nh > 3) return false;
@@ -1042,6 +1070,158 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
     return false;
 }
 
+// Undirected Expand chains of 1 or 2 hops (RelationalPlanner.scala:126-136): 2^hops branches, one per
+// orientation of the hops, the incoming hops over relationships with start <> end, the same node scans at
+// every position, pairwise uniqueness of the relationships; count(*) / count(DISTINCT end | start).
+bool fused_undirected(capsmi_session* s, const capsmi_table* in, const PlanNode& g, const std::vector<Path>& B,
+                      std::vector<int64_t>& vals) {
+    const size_t h = B[0].hops.size();
+    if (h < 1 || h > 2 || B.size() != (size_t(1) << h)) return false;
+    std::set<int> orients;
+    std::vector<Classified> cls(B.size());
+    std::vector<int> kinds;
+    for (size_t bi = 0; bi < B.size(); ++bi) {
+        const Path& P = B[bi];
+        if (P.hops.size() != h || !is_chain(P)) return false;
+        for (int x : P.pos_node) if (x < 0) return false;
+        int o = 0;
+        for (size_t i = 0; i < h; ++i) {
+            const bool incoming = P.hops[i].from_role == ROLE_DST;
+            if (P.inst[P.hops[i].rel].no_loops != incoming) return false;
+            o |= (incoming ? 1 : 0) << i;
+        }
+        orients.insert(o);
+        if (!classify(P, cls[bi])) return false;
+        if (h == 2 ? !all_pairs_unique(cls[bi], 2) : !cls[bi].uniq.empty()) return false;
+        std::vector<int> k;
+        if (!agg_kinds(in, g, P, 0, (int)h, k)) return false;
+        if (bi == 0) kinds = k;
+        else if (k != kinds) return false;
+    }
+    if (orients.size() != B.size()) return false;
+    int64_t lo, hi;
+    if (!id_window(B, &lo, &hi) || g_dist.on) return false;  // no distributed form (yet)
+    // one relationship set for every hop of every branch, read as (start, end)
+    auto plain_views = [&](const Path& P, const Hop& hp, RelViews& v) {
+        Hop fwd = hp;
+        fwd.from_role = ROLE_SRC;
+        fwd.to_role = ROLE_DST;
+        rel_views(P, fwd, v);
+    };
+    RelViews v0;
+    plain_views(B[0], B[0].hops[0], v0);
+    for (const Path& P : B)
+        for (const Hop& hp : P.hops) {
+            RelViews v;
+            plain_views(P, hp, v);
+            if (v.sig != v0.sig) return false;
+        }
+    // one node scan per position, identical in every branch
+    BitmapSet bs;
+    std::vector<capsmi_bitmap*> pos(h + 1, nullptr);
+    for (size_t q = 0; q <= h; ++q) {
+        std::string k0;
+        pos[q] = node_bitmap(s, B[0], cls[0], B[0].pos_node[q], lo, hi, bs, &k0);
+        if (!pos[q]) return false;
+        for (size_t bi = 1; bi < B.size(); ++bi) {
+            std::string kq;
+            if (!node_bitmap(s, B[bi], cls[bi], B[bi].pos_node[q], lo, hi, bs, &kq) || kq != k0) return false;
+        }
+    }
+    std::vector<const int64_t*> srcs, dsts;
+    std::vector<int64_t> ms;
+    for (capsmi_table* t : v0.t) {
+        srcs.push_back(t->cols[0].d());
+        dsts.push_back(t->cols[1].d());
+        ms.push_back(t->nrows);
+    }
+    for (int k : kinds) {
+        const int kind = k == A_COUNT ? 0 : (k == A_DISTINCT_END ? 1 : 2);
+        vals.push_back(undirected_count(s, srcs.data(), dsts.data(), ms.data(), (int)srcs.size(), (int)h, pos[0], pos[1],
+                                        h == 2 ? pos[2] : pos[1], kind));
+    }
+    route(s, "undirected");
+    return true;
+}
+
+// the start ids of a route's rows back to the graph's Long ids (relative ids in [0, n) of the route's window)
+void ids_to_long(capsmi_session* s, int64_t lo, int64_t* v, int64_t n) {
+    if (n <= 0) return;
+    if (!g_dense) {
+        add_i64(v, lo, n, s->stream);
+    } else if (g_dense->scrambled) {
+        unscramble_ids(s, *g_dense, v, n);
+    } else {
+        Buf ids = dev_alloc(sizeof(int64_t) * n, s);
+        gather_col(P<int64_t>(g_dense->orig), nullptr, v, n, P<int64_t>(ids), nullptr, s->stream);
+        HIP_CHECK(hipMemcpyAsync(v, P<void>(ids), sizeof(int64_t) * n, hipMemcpyDeviceToDevice, s->stream));
+    }
+}
+
+// C3's grouped form: the 2-hop chain grouped by its start node, count(*) / count(DISTINCT end)
+bool fused_grouped_two_hop(capsmi_session* s, const capsmi_table* in, const PlanNode& g, const std::vector<Path>& B,
+                           capsmi_table** out) {
+    if (B.size() != 1 || g.a.size() != 1 || g.aggs.empty()) return false;
+    const Path& P = B[0];
+    if (any_no_loops(P) || P.hops.size() != 2 || !is_chain(P) || !same_orientation(P)) return false;
+    for (int x : P.pos_node) if (x < 0) return false;
+    const int gc = find_col(in, g.a[0]);
+    if (gc < 0 || position_of(P, P.cols[gc]) != 0 || !id_like(P, P.cols[gc])) return false;
+    std::vector<int> kinds;
+    if (!agg_kinds(in, g, P, 0, 2, kinds)) return false;
+    for (int k : kinds) if (k == A_DISTINCT_START) return false;
+    Classified c;
+    if (!classify(P, c) || !all_pairs_unique(c, 2)) return false;
+    RelViews v0, v1;
+    rel_views(P, P.hops[0], v0);
+    rel_views(P, P.hops[1], v1);
+    if (v0.sig != v1.sig) return false;
+    std::vector<Path> one{P};
+    int64_t lo, hi;
+    if (!id_window(one, &lo, &hi) || g_dist.on) return false;
+    BitmapSet bs;
+    capsmi_bitmap* a = node_bitmap(s, P, c, P.pos_node[0], lo, hi, bs);
+    capsmi_bitmap* b = node_bitmap(s, P, c, P.pos_node[1], lo, hi, bs);
+    capsmi_bitmap* cc = node_bitmap(s, P, c, P.pos_node[2], lo, hi, bs);
+    if (!a || !b || !cc) return false;
+    std::vector<const int64_t*> srcs, dsts;
+    std::vector<int64_t> ms;
+    for (capsmi_table* t : v0.t) {
+        srcs.push_back(t->cols[0].d());
+        dsts.push_back(t->cols[1].d());
+        ms.push_back(t->nrows);
+    }
+    size_t free_b = 0, total_b = 0;
+    HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+    auto* r = result_table(s, 0);
+    std::unique_ptr<capsmi_table> guard(r);
+    int64_t rows = -1;
+    for (size_t i = 0; i < kinds.size(); ++i) {
+        Buf ids, vals;
+        int64_t nrow = 0;
+        if (!grouped_two_hop(s, srcs.data(), dsts.data(), ms.data(), (int)srcs.size(), a, b, cc, kinds[i] != A_COUNT,
+                             (int64_t)(free_b / 2), ids, vals, &nrow))
+            return false;  // the keys would not fit: the generic plan (and its size guard) decides
+        REQUIRE(rows < 0 || rows == nrow, CAPSMI_ERR_INTERNAL, "grouped 2-hop: aggregates disagree on the groups");
+        if (i == 0) {
+            rows = nrow;
+            ids_to_long(s, lo, ::capsmi::P<int64_t>(ids), nrow);
+            Column k;
+            k.type = CAPSMI_I64;
+            k.data = ids;
+            r->cols.push_back(std::move(k));
+        }
+        Column v;
+        v.type = CAPSMI_I64;
+        v.data = vals;
+        r->cols.push_back(std::move(v));
+    }
+    r->nrows = rows;
+    *out = guard.release();
+    route(s, "two_hop_grouped");
+    return true;
+}
+
 // group by the start node, count(*), over the branches of a bounded var-length expand
 bool fused_var_length(capsmi_session* s, const capsmi_table* in, const PlanNode& g, const std::vector<Path>& B,
                       capsmi_table** out) {
@@ -1060,6 +1240,7 @@ bool fused_var_length(capsmi_session* s, const capsmi_table* in, const PlanNode&
     bool first = true;
     for (size_t bi = 0; bi < B.size(); ++bi) {
         const Path& P = B[bi];
+        if (any_no_loops(P)) return false;
         const int k = (int)P.hops.size();
         if (k == 0) {
             // lower = 0: copyEntity(source -> target) of the start scan (VarLengthExpandPlanner.scala:146-153,
@@ -1132,7 +1313,7 @@ bool fused_var_length(capsmi_session* s, const capsmi_table* in, const PlanNode&
 bool fused_projection(capsmi_session* s, const capsmi_table* t, const std::vector<Path>& B, capsmi_table** out) {
     if (B.size() != 1) return false;
     const Path& P = B[0];
-    if (P.hops.size() != 1 || !is_chain(P) || P.pos_node[0] < 0 || P.pos_node[1] < 0) return false;
+    if (P.hops.size() != 1 || !is_chain(P) || P.pos_node[0] < 0 || P.pos_node[1] < 0 || any_no_loops(P)) return false;
     Classified c;
     if (!classify(P, c) || !c.uniq.empty()) return false;
     const Hop& h = P.hops[0];
@@ -1256,7 +1437,18 @@ bool try_fused_shapes(capsmi_table* t, capsmi_table** out) {
         std::vector<Path> B;
         if (!as_paths(in, B) || B.empty()) return false;
         if (p.a.empty()) {
-            if (B.size() != 1) return false;
+            if (B.size() != 1) {
+                std::vector<int64_t> vals;
+                if (!fused_undirected(s, in, p, B, vals)) return false;
+                auto* r = result_table(s, 1);
+                for (size_t i = 0; i < vals.size(); ++i) {
+                    Column c = i64_column(s, {vals[i]});
+                    c.name = p.aggs[i].output;
+                    r->cols.push_back(std::move(c));
+                }
+                *out = r;
+                return true;
+            }
             std::vector<int> kinds;
             const int end = (int)B[0].pos_node.size() - 1;
             if (!agg_kinds(in, p, B[0], 0, B[0].hops.size() == 3 ? 0 : end, kinds)) return false;
@@ -1271,6 +1463,7 @@ bool try_fused_shapes(capsmi_table* t, capsmi_table** out) {
             *out = r;
             return true;
         }
+        if (fused_grouped_two_hop(s, in, p, B, out)) return true;
         return fused_var_length(s, in, p, B, out);
     }
     std::vector<Path> B;
@@ -1434,10 +1627,10 @@ void refuse_partitioned(const capsmi_table* in, const char* op) {
 // ---- unrouted-plan size guard (capsmi_session_set_unrouted_limit) ------------------------------------
 // System-R estimates of a lazy plan's rows: a join emits |L| |R| / max(ndv(l), ndv(r)) rows, where the
 // ndv of an entity key column is its scan's rows (node ids) or min(rows, id window) (endpoints).
-double key_ndv(const capsmi_table* t, const std::string& col, double rows) {
+double key_ndv(const capsmi_table* t, const std::string& col) {  // -1: not known (not an entity key)
     Scan sc;
     const int c = find_col(t, col);
-    if (c < 0 || !as_scan(t, sc)) return rows;
+    if (c < 0 || !as_scan(t, sc)) return -1;
     double n = 0, span = 0;
     for (const Member& m : sc.m) {
         n += (double)m.base->nrows;
@@ -1445,7 +1638,7 @@ double key_ndv(const capsmi_table* t, const std::string& col, double rows) {
     }
     if (sc.role[c] == ROLE_ID) return std::max(1.0, n);
     if (sc.role[c] == ROLE_SRC || sc.role[c] == ROLE_DST) return std::max(1.0, std::min(n, span));
-    return rows;
+    return -1;
 }
 
 double est_rows(const capsmi_table* t) {
@@ -1458,9 +1651,10 @@ double est_rows(const capsmi_table* t) {
         case PlanNode::JOIN: {
             const double l = est_rows(p.in[0]), r = est_rows(p.in[1]);
             if (p.jt == CAPSMI_JOIN_CROSS) return l * r;
-            double ndv = 1;
+            double ndv = -1;  // the larger known key cardinality (an intermediate result's keys: unknown)
             for (size_t i = 0; i < p.a.size(); ++i)
-                ndv = std::max(ndv, std::max(key_ndv(p.in[0], p.a[i], l), key_ndv(p.in[1], p.b[i], r)));
+                ndv = std::max(ndv, std::max(key_ndv(p.in[0], p.a[i]), key_ndv(p.in[1], p.b[i])));
+            if (ndv < 1) ndv = std::max(1.0, std::max(l, r));
             double e = l * r / ndv;
             if (p.jt == CAPSMI_JOIN_LEFT_OUTER || p.jt == CAPSMI_JOIN_FULL_OUTER) e = std::max(e, l);
             if (p.jt == CAPSMI_JOIN_RIGHT_OUTER || p.jt == CAPSMI_JOIN_FULL_OUTER) e = std::max(e, r);

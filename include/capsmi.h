@@ -430,6 +430,15 @@ capsmi_status capsmi_two_hop_mark_dst_part(capsmi_session* s, const capsmi_relpa
 capsmi_status capsmi_two_hop_count_distinct_part(capsmi_session* s, const capsmi_relpart* p, const capsmi_bitmap* a_ok,
                                                  const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok,
                                                  int64_t* out_distinct);
+/* Undirected Expand patterns, fused.  An undirected Expand is the union of the outgoing branch and the
+ * incoming branch over relationships whose start differs from their end (RelationalPlanner.scala:126-136):
+ *   hops = 1: MATCH (a)-[r]-(b) WHERE a_ok(a) AND b_ok(b)
+ *   hops = 2: MATCH (a)-[r1]-(b)-[r2]-(c) WHERE a_ok(a) AND b_ok(b) AND c_ok(c)   [r1 <> r2 implied]
+ * RETURN count(*) (kind 0), count(DISTINCT the last node) (kind 1) or count(DISTINCT a) (kind 2); c_ok
+ * is ignored for one hop.  The bitmaps share one id domain. */
+capsmi_status capsmi_undirected_count(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
+                                      const char* dst_col, int32_t hops, const capsmi_bitmap* a_ok,
+                                      const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok, int32_t kind, int64_t* out);
 /* BoundedVarLengthExpand + grouped count, fused (C5):
  *   MATCH (a)-[r*lower..upper]->(b) WHERE a_ok(a) AND b_ok(b) RETURN id(a) AS <id_name>, count(*) AS <count_name>
  * with edge-distinct paths (VarLengthExpandPlanner.scala:83-136, 179-180), 0 <= lower <= upper <= 3,

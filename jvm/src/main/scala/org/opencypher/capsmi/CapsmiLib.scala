@@ -81,6 +81,16 @@ object Capsmi {
   final val AGG_SUM = 4
   final val AGG_AVG = 5
   final val AGG_COLLECT = 6 // sort_array(collect_list / collect_set)
+
+  // multi-GPU: collectives the library asks the host for, shard layouts (capsmi_graph_distribute)
+  final val COLL_ALL_GATHER = 0
+  final val COLL_ALL_REDUCE_SUM = 1
+  final val COLL_ALL_REDUCE_MAX = 2
+  final val COLL_U32 = 100
+  final val NODES_REPLICATED = 0
+  final val NODES_OWNED = 1
+  final val RELS_BY_SOURCE = 0
+  final val RELS_BY_TARGET = 1
 }
 
 @Structure.FieldOrder(Array("name", "type", "data", "valid"))
@@ -131,6 +141,12 @@ class CapsmiParam extends Structure {
   var values: Pointer = _
 }
 
+/** capsmi_collective_fn: one collective on the session's stream (e.g. an RCCL communicator the executor
+  * holds, over xGMI); 0 on success. */
+trait CollectiveFn extends Callback {
+  def invoke(ctx: Pointer, op: Int, send: Pointer, recv: Pointer, count: Long, dtype: Int): Int
+}
+
 /** capsmi_intern_fn: strings of a CSV column handed, in row order, to the session's dictionary. */
 trait InternFn extends Callback {
   def invoke(ctx: Pointer, s: Pointer, n: Long): Long
@@ -151,6 +167,15 @@ trait CapsmiLib extends Library {
   def capsmi_session_set_fused(s: Pointer, enabled: Int): Int
   def capsmi_session_set_params(s: Pointer, nparams: Int, params: CapsmiParam): Int
   def capsmi_session_route_count(s: Pointer, name: String, count: LongByReference): Int
+  def capsmi_session_set_unrouted_limit(s: Pointer, maxBytes: Long): Int
+
+  // multi-GPU (one process per GPU): rank view, shards of a distributed graph
+  def capsmi_session_set_ranks(s: Pointer, rank: Int, world: Int, fn: CollectiveFn, ctx: Pointer): Int
+  def capsmi_graph_distribute(s: Pointer, idLo: Long, idHi: Long, nnodes: Int, nodes: Array[Pointer], nodeMode: Int,
+                              nrels: Int, rels: Array[Pointer], relMode: Int): Int
+  def capsmi_owned_rows(s: Pointer, t: Pointer, col: String, idLo: Long, idHi: Long, out: PointerByReference): Int
+  def capsmi_table_partitioned(t: Pointer, out: IntByReference): Int
+  def capsmi_id_owner(idLo: Long, idHi: Long, world: Int, id: Long, owner: IntByReference, denseId: LongByReference): Int
 
   // tables
   def capsmi_table_from_host(s: Pointer, ncols: Int, cols: ColDesc, nrows: Long, out: PointerByReference): Int
@@ -212,6 +237,8 @@ trait CapsmiLib extends Library {
                                     a: Pointer, b: Pointer, c: Pointer, outDistinct: LongByReference): Int
   def capsmi_triangle_count(s: Pointer, nrels: Int, rels: Array[Pointer], srcCol: String, dstCol: String, nOk: Pointer,
                             outRows: LongByReference): Int
+  def capsmi_undirected_count(s: Pointer, nrels: Int, rels: Array[Pointer], srcCol: String, dstCol: String, hops: Int,
+                              a: Pointer, b: Pointer, c: Pointer, kind: Int, out: LongByReference): Int
   def capsmi_var_length_count(s: Pointer, nrels: Int, rels: Array[Pointer], srcCol: String, dstCol: String, a: Pointer,
                               b: Pointer, lower: Int, upper: Int, idName: String, countName: String,
                               out: PointerByReference): Int

@@ -50,6 +50,9 @@ def load():
         lib.orc_var_length_count.restype = ctypes.c_int
         lib.orc_var_length_count.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, U8P, U8P, ctypes.c_int,
                                              ctypes.c_int, I64P, I64P, ctypes.c_int]
+        lib.orc_two_hop_undirected_enumerate.restype = ctypes.c_int
+        lib.orc_two_hop_undirected_enumerate.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, U8P, U8P, U8P,
+                                                         I64P, I64P, I64P, ctypes.c_int]
         # closed.c
         lib.orc_c2_masks.restype = None
         lib.orc_c2_masks.argtypes = [ctypes.c_int64, ctypes.c_uint64, U8P, U8P]
@@ -128,6 +131,15 @@ def two_hop_enumerate(n, src, dst, a_ok=None, b_ok=None, c_ok=None, grouped=Fals
     if grouped:
         return rows.value, dist.value, grows, gdist
     return rows.value, dist.value
+
+
+def two_hop_undirected_enumerate(n, src, dst, a_ok=None, b_ok=None, c_ok=None, threads=0):
+    """(count(*), count(DISTINCT c), count(DISTINCT a)) of MATCH (a)-[r1]-(b)-[r2]-(c) by enumeration."""
+    rows, dc, da = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    if load().orc_two_hop_undirected_enumerate(n, len(src), _p64(src), _p64(dst), _p8(a_ok), _p8(b_ok), _p8(c_ok),
+                                               ctypes.byref(rows), ctypes.byref(dc), ctypes.byref(da), threads):
+        raise MemoryError("orc_two_hop_undirected_enumerate")
+    return rows.value, dc.value, da.value
 
 
 def two_hop_closed_form(n, src, dst, a_ok=None, b_ok=None, c_ok=None):

@@ -116,6 +116,64 @@ static int64_t* csr_edges(int64_t n, int64_t m, const int64_t* key, const int64_
  * out_rows = count(*), out_distinct = count(DISTINCT c).
  * Optional per-a output: if group_distinct != NULL, group_distinct[a] = count(DISTINCT c) for that a
  * and group_rows[a] = count(*) for that a.  Returns 0, or -1 on allocation failure. */
+/* Undirected 2-hop by enumeration: MATCH (a)-[r1]-(b)-[r2]-(c) with r1 <> r2.  An undirected Expand is
+ * the outgoing branch plus the incoming branch over relationships whose start differs from their end
+ * (RelationalPlanner.scala:126-136): from a node, every relationship e = (s, t) is the arc s -> t and,
+ * for s != t, the arc t -> s.  Every (arc1 into b, arc2 out of b) with different relationships is one
+ * binding; count(*), count(DISTINCT c) and count(DISTINCT a).  Test oracle for the fused undirected
+ * route (csrc/k_undirected.hip), pinned to oracle/enumerate.py in tests/test_oracle_pins.py. */
+int orc_two_hop_undirected_enumerate(int64_t n, int64_t m, const int64_t* src, const int64_t* dst,
+                                     const uint8_t* a_ok, const uint8_t* b_ok, const uint8_t* c_ok,
+                                     int64_t* out_rows, int64_t* out_distinct_c, int64_t* out_distinct_a,
+                                     int nthreads) {
+    int64_t k = 0;
+    for (int64_t e = 0; e < m; ++e) k += src[e] == dst[e] ? 1 : 2;
+    int64_t* as = (int64_t*)malloc((size_t)(k ? k : 1) * sizeof(int64_t));
+    int64_t* at = (int64_t*)malloc((size_t)(k ? k : 1) * sizeof(int64_t));
+    int64_t* ae = (int64_t*)malloc((size_t)(k ? k : 1) * sizeof(int64_t));
+    uint8_t* mc = (uint8_t*)calloc((size_t)(n ? n : 1), 1);
+    uint8_t* ma = (uint8_t*)calloc((size_t)(n ? n : 1), 1);
+    if (!as || !at || !ae || !mc || !ma) { free(as); free(at); free(ae); free(mc); free(ma); return -1; }
+    int64_t j = 0;
+    for (int64_t e = 0; e < m; ++e) {
+        as[j] = src[e]; at[j] = dst[e]; ae[j++] = e;
+        if (src[e] != dst[e]) { as[j] = dst[e]; at[j] = src[e]; ae[j++] = e; }
+    }
+    int64_t* off = csr_offsets(n, k, as);
+    int64_t* adj = off ? csr_edges(n, k, as, off) : NULL;
+    if (!off || !adj) { free(as); free(at); free(ae); free(mc); free(ma); free(off); free(adj); return -1; }
+    int64_t rows = 0;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#endif
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : rows)
+    for (int64_t a = 0; a < n; ++a) {
+        if (!OK(a_ok, a)) continue;
+        int64_t arows = 0;
+        for (int64_t i = off[a]; i < off[a + 1]; ++i) {
+            const int64_t x1 = adj[i], b = at[x1];
+            if (!OK(b_ok, b)) continue;
+            for (int64_t q = off[b]; q < off[b + 1]; ++q) {
+                const int64_t x2 = adj[q];
+                if (ae[x2] == ae[x1]) continue; /* r1 = r2 */
+                const int64_t c = at[x2];
+                if (!OK(c_ok, c)) continue;
+                ++arows;
+                if (!mc[c]) mc[c] = 1; /* benign race: every writer stores 1 */
+            }
+        }
+        if (arows) ma[a] = 1;
+        rows += arows;
+    }
+    int64_t dc = 0, da = 0;
+    for (int64_t i = 0; i < n; ++i) { dc += mc[i]; da += ma[i]; }
+    *out_rows = rows;
+    *out_distinct_c = dc;
+    *out_distinct_a = da;
+    free(as); free(at); free(ae); free(mc); free(ma); free(off); free(adj);
+    return 0;
+}
+
 int orc_two_hop_enumerate(int64_t n, int64_t m, const int64_t* src, const int64_t* dst,
                           const uint8_t* a_ok, const uint8_t* b_ok, const uint8_t* c_ok,
                           int64_t* out_rows, int64_t* out_distinct,

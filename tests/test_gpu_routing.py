@@ -247,3 +247,23 @@ def test_lazy_schema_errors_at_call(session):
     with pytest.raises(_lib.IllegalArgumentException):
         u.join(u, "inner", ("b", "b"))
     assert u.size == 5
+
+
+@pytest.mark.parametrize("scale,kind", [(12, "all"), (14, "all"), (12, "person")])
+def test_c3_grouped_routed(session, scale, kind):
+    """C3's grouped form (RETURN id(a), count(DISTINCT c), the parity variant at s <= 14) and
+    the grouped count(*), routed to the grouped 2-hop kernels (csrc/k_grouped.hip), against per-a
+    enumeration (oracle/rmat.c orc_two_hop_enumerate), and the same plan operator by operator."""
+    from oracle import cpu
+    sg = _graph(session, scale, kind=kind)
+    q = {"clauses": [{"match": "(a:Person)-[:FRIEND_OF]->(b:Person)-[:FRIEND_OF]->(c:Person)"}],
+         "return": {"items": [["a", ["id", "a"]], ["dc", ["count_distinct", ["id", "c"]]], ["n", ["count*"]]]}}
+    got = _routed(session, "two_hop_grouped", lambda: _run(session, sg, q))
+    n = 1 << scale
+    src, dst = cpu.rmat_edges(scale, 0, 16 << scale)
+    mask = np.ones(n, np.uint8) if kind == "all" else cpu.person_mask(n).astype(np.uint8)
+    _, _, grows, gdist = cpu.two_hop_enumerate(n, src, dst, mask, mask, mask, grouped=True)
+    want = [{"a": int(a), "dc": int(gdist[a]), "n": int(grows[a])} for a in np.nonzero(grows)[0]]
+    assert same_rows(got, want)
+    if scale == 12:
+        assert same_rows(_run(session, sg, q, fused=False), want)

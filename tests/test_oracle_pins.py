@@ -6,6 +6,7 @@ For every graph -- the CREATE graph of every golden case (the reference's own te
 random multigraphs with self-loops, multi-edges and labels -- and for every relationship-type
 restriction and node label, the C checker must equal enumerate.py on:
   C3 shape  MATCH (a:L)-[:T]->(b:L)-[:T]->(c:L) RETURN count(*), count(DISTINCT c)
+            MATCH (a:L)-[:T]-(b:L)-[:T]-(c:L) RETURN count(*), count(DISTINCT c), count(DISTINCT a)
   C4 shape  MATCH (a:L)-[:T]->(b:L)-[:T]->(c:L)-[:T]->(a) RETURN count(*)
   C5 shape  MATCH (a:L)-[:T*lo..hi]->(b:L) RETURN id(a), count(*)
 """
@@ -81,6 +82,12 @@ def _check_graph(g):
         assert cpu.two_hop_enumerate(n, src, dst, mask, mask, mask) == expect, (label, rtype)
         assert cpu.two_hop_closed_form(n, src, dst, mask, mask, mask) == expect, (label, rtype)
         assert cpu.two_hop_closed_form_mt(n, src, dst, mask, mask, mask, threads=2) == expect, (label, rtype)
+        # C3 undirected: outgoing + incoming-without-self-loops per hop, r1 <> r2
+        want = _enum(g, f"(a{lab})-{ty}-(b{lab})-{ty}-(c{lab})",
+                     [["rows", ["count*"]], ["dc", ["count_distinct", ["id", "c"]]],
+                      ["da", ["count_distinct", ["id", "a"]]]])[0]
+        assert cpu.two_hop_undirected_enumerate(n, src, dst, mask, mask, mask) == (want["rows"], want["dc"], want["da"]), \
+            (label, rtype)
         # C4 (rmat.c enumeration has no node mask: keep the relationships with both ends in the scan)
         want = _enum(g, f"(a{lab})-{ty}->(b{lab})-{ty}->(c{lab})-{ty}->(a)", [["rows", ["count*"]]])[0]["rows"]
         keep = (mask[src] != 0) & (mask[dst] != 0) if len(src) else np.zeros(0, bool)
