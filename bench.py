@@ -48,10 +48,12 @@ C3_QUERY = {"clauses": [{"match": "(a:Person)-[:FRIEND_OF]->(b:Person)-[:FRIEND_
             "return": {"items": [["count(DISTINCT c)", ["count_distinct", ["id", "c"]]]]}}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 KERNELS = ("part_scatter1", "part_scatter2_hop1", "part_scatter2", "hop1", "hop2", "mid_combine", "bitmap_add",
+           "bitmap_range",
            "count_part", "count_part_in", "count_in", "count_part_out", "count_out", "degrees")
 # timer name -> kernel name as rocprofv3 reports it (hop1 and hop2 are two instances of k_hop_2d)
 KERNEL_SYMBOL = {"part_scatter1": "k_scatter_l", "part_scatter2_hop1": "k_scatter_s2", "part_scatter2": "k_scatter_s2",
                  "hop1": "k_hop_2d", "hop2": "k_hop_2d", "mid_combine": "k_mid_combine", "bitmap_add": "k_bitmap_add",
+                 "bitmap_range": "k_bits_range",
                  "count_part": "k_rec_part", "count_part_in": "k_scatter_c", "count_part_out": "k_scatter_c",
                  "count_in": "k_rec_walk",
                  "count_out": "k_rec_walk", "degrees": "k_degrees"}

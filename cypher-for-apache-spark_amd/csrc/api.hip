@@ -1242,8 +1242,20 @@ capsmi_status capsmi_bitmap_add_scan(capsmi_bitmap* b, capsmi_table* nodes, cons
     M(nodes);
     capsmi_session* s = b->sess;
     use_device(s);
-    const Column& idc = nodes->cols[col_index(nodes, id_col)];
+    const int idx = col_index(nodes, id_col);
+    const Column& idc = nodes->cols[idx];
     REQUIRE(idc.type == CAPSMI_I64, CAPSMI_ERR_ILLEGAL_ARGUMENT, "node id column must be Long");
+    const EntityInfo* e = nodes->entity.get();
+    if (nnodes == 0 && e && e->kind == 1 && e->ids_exact && e->id == idx && b->set_bits == 0 && b->rows_added == 0 &&
+        e->lo >= b->lo && e->hi <= b->hi) {
+        // a registered node table whose ids are exactly [lo, hi), each once (register_entity): the scan
+        // sets that range, with no pass over the rows and no host round trip
+        bitmap_set_range(b, e->lo - b->lo, e->hi - b->lo);
+        b->rows_added = nodes->nrows;
+        b->set_bits = nodes->nrows;
+        b->full = b->set_bits == b->hi - b->lo;
+        return CAPSMI_OK;
+    }
     Buf flags;
     RangePred rp;
     std::vector<capsmi_expr> bound;
@@ -2150,7 +2162,7 @@ capsmi_status capsmi_rmat_nodes(capsmi_session* s, int32_t scale, int32_t kind, 
         graph::ages(s, P<int64_t>(ids), rows, seed, P<int64_t>(a.data));
         o->cols.push_back(std::move(a));
     }
-    attach_entity(o, 1, 0, n);  // [id] / [id, age]: a registered node table
+    attach_entity(o, 1, 0, n, kind == 0);  // [id] / [id, age]: a registered node table (all ids: exactly [0, n))
     *out = o;
     API_END
 }

@@ -90,6 +90,7 @@ struct EntityInfo {
     int id = -1, src = -1, dst = -1;  // column indices of the key columns
     int64_t lo = 0, hi = 0;       // [min, max + 1) of the ids (node) or of both endpoints (relationship)
     int64_t rows = 0;
+    bool ids_exact = false;       // node: the ids are exactly [lo, hi), each once (checked at registration)
 };
 struct PlanNode;  // lazy Table[T] operator (plan.hip)
 
@@ -337,10 +338,15 @@ struct PartLayout {
     int sbits;       // 19 while nt * ns <= 16384, coarser for larger domains
     int ncells;      // nt * ns, j-major (target slice major)
     int tbits;       // target slice = 2^tbits ids (19 for the 2-hop layout)
+    int packed = 0;  // 2-hop layout: 5-byte cell-relative pairs (sbits + tbits <= 40), else uint2
 };
 struct RelPart {
     PartLayout L;
-    Buf pairs;  // uint2 (source - lo, target - lo) per kept relationship, grouped by cell
+    // per kept relationship, grouped by cell: uint2 (source - lo, target - lo), or when L.packed the
+    // cell-relative key k = (source low sbits) << tbits | (target low tbits) as two arrays, the low
+    // word u32[cap] and the high byte u8[cap] behind it
+    Buf pairs;
+    int64_t cap = 0;  // entries per array (kept + slack)
     Buf boff;   // int64 cell offsets (ncells + 1); boff[ncells] = kept
     int64_t kept = 0;  // -1: on the device only (relpart_kept reads it)
     int64_t rows = 0;  // relationships offered to the build (>= kept)
@@ -431,7 +437,7 @@ void validate_program(const capsmi_table* t, int32_t nn, const capsmi_expr* prog
 void materialize(capsmi_table* t);
 // mark a materialised table in canonical entity layout (ids first) as a node (1) / relationship (2)
 // table whose ids (endpoints) lie in [lo, hi)
-void attach_entity(capsmi_table* t, int kind, int64_t lo, int64_t hi);
+void attach_entity(capsmi_table* t, int kind, int64_t lo, int64_t hi, bool ids_exact = false);
 inline capsmi_table* M(const capsmi_table* t) {
     materialize(const_cast<capsmi_table*>(t));
     return const_cast<capsmi_table*>(t);
@@ -475,6 +481,7 @@ struct RangePred {
 bool compile_range_pred(const capsmi_table* t, int32_t nn, const capsmi_expr* prog, RangePred& rp);
 void bitmap_add_rows(capsmi_bitmap* b, const int64_t* ids, const uint8_t* ids_valid, const uint8_t* flags, int64_t n,
                      int64_t* dev_counters, const RangePred* rp = nullptr);
+void bitmap_set_range(capsmi_bitmap* b, int64_t b0, int64_t b1);  // bits [b0, b1) of the window
 int64_t words_popcount(capsmi_session* s, const uint32_t* w, int64_t w_begin, int64_t w_end);
 void words_popcount_async(capsmi_session* s, const uint32_t* w, int64_t w_begin, int64_t w_end, int64_t* dev_out);
 

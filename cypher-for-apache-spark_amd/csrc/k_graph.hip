@@ -627,6 +627,17 @@ __global__ void k_fingerprint(FpCols fc, int64_t n, unsigned long long* __restri
     }
 }
 
+// bits [b0, b1) of w set, the other bits of the words they touch kept (a registered node table whose
+// ids are exactly one window, capsmi_bitmap_add_scan)
+__global__ void k_bits_range(uint32_t* __restrict__ w, int64_t b0, int64_t b1) {
+    const int64_t w0 = b0 >> 5, w1 = (b1 + 31) >> 5;
+    for (int64_t i = w0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < w1; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t lo = i * 32 > b0 ? i * 32 : b0, hi = i * 32 + 32 < b1 ? i * 32 + 32 : b1;
+        const uint32_t m = (uint32_t)(((hi - lo) == 32 ? 0xFFFFFFFFull : ((1ull << (hi - lo)) - 1)) << (lo - i * 32));
+        w[i] = m == 0xFFFFFFFFu ? m : (w[i] | m);
+    }
+}
+
 inline int grid_cap(int64_t n, int64_t cap) {
     int64_t g = (n + 255) / 256;
     if (g < 1) g = 1;
@@ -647,6 +658,15 @@ void bitmap_add_rows(capsmi_bitmap* b, const int64_t* ids, const uint8_t* ids_va
     hipLaunchKernelGGL(k_bitmap_add, dim3((unsigned)std::max<int64_t>(g, 1)), dim3(256), 0, b->sess->stream,
                        P<uint32_t>(b->words), b->lo, b->hi, ids, ids_valid, flags, n, aligned,
                        (unsigned long long*)dev_counters, rp ? *rp : RangePred());
+    HIP_CHECK(hipGetLastError());
+}
+
+void bitmap_set_range(capsmi_bitmap* b, int64_t b0, int64_t b1) {
+    if (b1 <= b0) return;
+    KernelTimer kt(b->sess, "bitmap_range");
+    const int64_t words = ((b1 + 31) >> 5) - (b0 >> 5);
+    hipLaunchKernelGGL(k_bits_range, dim3((unsigned)grid_cap(words, (int64_t)b->sess->num_cus * 4)), dim3(256), 0,
+                       b->sess->stream, P<uint32_t>(b->words), b0, b1);
     HIP_CHECK(hipGetLastError());
 }
 

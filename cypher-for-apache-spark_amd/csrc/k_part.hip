@@ -555,13 +555,40 @@ struct Hop1Out {
     int64_t gwords;
 };
 
+// The 2-hop layout's pair store.  Packed (L.packed): the cell-relative key
+// k = (s mod 2^sbits) << tbits | (t mod 2^tbits), at most 40 bits, split into its low word w[pos]
+// and high byte b[pos] -- 5 bytes per relationship instead of 8; the cell gives the slices back.
+struct PairOut {
+    uint2* p;     // unpacked
+    uint32_t* w;  // packed: low words
+    uint8_t* b;   // packed: high bytes
+};
+
+__device__ __forceinline__ uint64_t cell_key(const Layout& L, uint2 v) {
+    return (uint64_t)(v.x & ((1u << L.sbits) - 1u)) << L.tbits | (v.y & ((1u << L.tbits) - 1u));
+}
+
+// pair of a cell-relative key in cell (j, i)
+__device__ __forceinline__ uint2 key_pair(const Layout& L, uint32_t sbase, uint32_t tbase, uint32_t w, uint32_t b) {
+    const uint64_t k = (uint64_t)b << 32 | w;
+    return make_uint2(sbase + (uint32_t)(k >> L.tbits), tbase + (w & ((1u << L.tbits) - 1u)));
+}
+
 // ---- pass 2: block w's segments (chunks of one target slice each) -> the slices' source cells -----
 // Output offsets are exact and precomputed, so the reservation per tile is an LDS cursor bump and the
 // layout is deterministic.  The next chunk is loaded (buffer loads clipped at its fill) while this
 // one is regrouped.  With HOP1 the block also runs hop 1 on the pairs it moves: M(t) for s != t
 // marked in an LDS copy of the current slice (flushed through b_ok when it changes), self-loops
 // -> S1 / S2.
-template <bool HOP1>
+// output line in items: 128 bytes of pairs, or of the packed low words
+__host__ __device__ constexpr int s2_line(bool pk) { return pk ? 32 : kLine; }
+
+// LDS bytes of the per-cell held items (packed: low word + high byte each)
+__host__ __device__ constexpr size_t s2_hold_bytes(int nb, bool pk) {
+    return pk ? (((size_t)nb * s2_line(true) * 5 + 15) & ~(size_t)15) : sizeof(uint2) * (size_t)nb * kLine;
+}
+
+template <bool HOP1, bool PK>  // PK: without HOP1 (LDS)
 __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict__ pool,
                                                         const unsigned long long* __restrict__ cmeta,
                                                         const uint32_t* __restrict__ order,
@@ -569,13 +596,18 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
                                                         const int64_t* __restrict__ segbase,
                                                         const int* __restrict__ ja, const uint32_t* __restrict__ prel,
                                                         const int64_t* __restrict__ coff, Layout L,
-                                                        uint2* __restrict__ out, int64_t trash, Hop1Out h1) {
+                                                        PairOut out, int64_t trash, Hop1Out h1) {
+    constexpr int LN = s2_line(PK);
     extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
     const int nb = L.ns;
     const int64_t w = blockIdx.x, blocks = gridDim.x;
     uint2* stage = reinterpret_cast<uint2*>(smem);
-    uint2* hold = stage + kTile;  // per source cell: the items of its unfinished output line, slot = index & 15
-    uint32_t* cur = reinterpret_cast<uint32_t*>(hold + (size_t)nb * kLine);  // next output index per cell (< 2^32)
+    // per source cell: the items of its unfinished output line, slot = index mod LN
+    unsigned char* hbase = reinterpret_cast<unsigned char*>(stage + kTile);
+    uint2* hold = reinterpret_cast<uint2*>(hbase);
+    uint32_t* holdw = reinterpret_cast<uint32_t*>(hbase);
+    uint8_t* holdb = hbase + sizeof(uint32_t) * (size_t)nb * LN;
+    uint32_t* cur = reinterpret_cast<uint32_t*>(hbase + s2_hold_bytes(nb, PK));  // next output index per cell (< 2^32)
     uint32_t* cnt = cur + nb;
     uint32_t* loc = cnt + nb;
     uint32_t* hc = loc + nb;  // items held per cell (all in the line of cur)
@@ -583,12 +615,38 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
     uint32_t* tl = wtot + kSBlock / 64;  // HOP1: target slice marks
     const SegSplit S(jst, L.nt, blocks);
     for (int i = threadIdx.x; i < nb; i += kSBlock) hc[i] = 0;
+    auto put = [&](uint32_t pos, uint2 v) {
+        if (PK) {
+            const uint64_t k = cell_key(L, v);
+            out.w[pos] = (uint32_t)k;
+            out.b[pos] = (uint8_t)(k >> 32);
+        } else {
+            out.p[pos] = v;
+        }
+    };
+    auto hold_put = [&](int slot, uint2 v) {
+        if (PK) {
+            const uint64_t k = cell_key(L, v);
+            holdw[slot] = (uint32_t)k;
+            holdb[slot] = (uint8_t)(k >> 32);
+        } else {
+            hold[slot] = v;
+        }
+    };
+    auto hold_out = [&](uint32_t pos, int slot) {
+        if (PK) {
+            out.w[pos] = holdw[slot];
+            out.b[pos] = holdb[slot];
+        } else {
+            out.p[pos] = hold[slot];
+        }
+    };
     auto flush_held = [&]() {  // the segment's unfinished lines (shared with a neighbouring segment)
-        for (int x = threadIdx.x; x < nb * kLine; x += kSBlock) {
-            const int b = x / kLine, k = x % kLine;
+        for (int x = threadIdx.x; x < nb * LN; x += kSBlock) {
+            const int b = x / LN, k = x % LN;
             if ((uint32_t)k < hc[b]) {
                 const uint32_t pos = cur[b] - hc[b] + (uint32_t)k;
-                out[pos] = hold[b * kLine + (int)(pos & (kLine - 1))];
+                hold_out(pos, b * LN + (int)(pos & (LN - 1)));
             }
         }
     };
@@ -674,12 +732,12 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
         // Whole output lines: a cell's run is stored up to the last line boundary it reaches, the
         // rest held in LDS; held items go out when their line completes, together with the run
         // items that complete it (so a line is written within one tile, not in pieces by two).
-        for (int x = threadIdx.x; x < nb * kLine; x += kSBlock) {
-            const int b = x / kLine, k = x % kLine;
+        for (int x = threadIdx.x; x < nb * LN; x += kSBlock) {
+            const int b = x / LN, k = x % LN;
             if ((uint32_t)k < hc[b]) {
                 const uint32_t c = cur[b], pos = c - hc[b] + (uint32_t)k;
-                if (((c + cnt[b]) & ~(uint32_t)(kLine - 1)) > (c & ~(uint32_t)(kLine - 1)))
-                    out[pos] = hold[b * kLine + (int)(pos & (kLine - 1))];
+                if (((c + cnt[b]) & ~(uint32_t)(LN - 1)) > (c & ~(uint32_t)(LN - 1)))
+                    hold_out(pos, b * LN + (int)(pos & (LN - 1)));
             }
         }
 #pragma unroll
@@ -692,19 +750,19 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
             const uint2 v = stage[idx];
             const int b = min((int)(v.x >> L.sbits), nb - 1);  // stale stage entries past `total`
             const uint32_t pos = cur[b] + idx - loc[b];
-            const uint32_t cut = (cur[b] + cnt[b]) & ~(uint32_t)(kLine - 1);
+            const uint32_t cut = (cur[b] + cnt[b]) & ~(uint32_t)(LN - 1);
             if (idx >= total)
-                out[trash + threadIdx.x] = v;
+                put((uint32_t)trash + threadIdx.x, v);
             else if (pos < cut)
-                out[pos] = v;
+                put(pos, v);
             else
-                hold[b * kLine + (int)(pos & (kLine - 1))] = v;
+                hold_put(b * LN + (int)(pos & (LN - 1)), v);
         }
         __syncthreads();
         for (int i = threadIdx.x; i < nb; i += kSBlock) {
             const uint32_t c = cur[i], n = cnt[i];
-            const uint32_t cut = (c + n) & ~(uint32_t)(kLine - 1);
-            hc[i] = cut > (c & ~(uint32_t)(kLine - 1)) ? c + n - cut : hc[i] + n;
+            const uint32_t cut = (c + n) & ~(uint32_t)(LN - 1);
+            hc[i] = cut > (c & ~(uint32_t)(LN - 1)) ? c + n - cut : hc[i] + n;
             cur[i] = c + n;
         }
     }
@@ -720,8 +778,33 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const uint2* __restrict_
 //         Target filter b_ok at flush.
 //   HOP2: C(t) |= X1(s) for s != t, X2(s) for s == t.  Target filter c_ok at flush.
 // `sb` is the per-relationship source bitmap (a_ok or X1); `tmask` the target filter.
-template <bool HOP1, bool SRC_FULL>
-__global__ void __launch_bounds__(kBlock) k_hop_2d(const uint2* __restrict__ pairs, const int64_t* __restrict__ coff,
+// this lane's kN packed items of the cell walk starting at the 4-aligned index b: item u is
+// b + 4 * ((u >> 2) * B + lane) + (u & 3), one 16-byte low-word load and one 4-byte high-byte load
+// per four items (streamed once: non-temporal)
+template <int B>
+__device__ __forceinline__ int item_off4(int u) {
+    return 4 * ((u >> 2) * B + (int)threadIdx.x) + (u & 3);
+}
+
+template <int B, int N>
+__device__ __forceinline__ void load_packed(const uint32_t* __restrict__ w, const uint8_t* __restrict__ hb, int64_t b,
+                                            uint32_t (&lw)[N], uint32_t (&hw)[N / 4]) {
+    typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+    const v4u32* __restrict__ v = reinterpret_cast<const v4u32*>(w + b);
+    const uint32_t* __restrict__ h = reinterpret_cast<const uint32_t*>(hb + b);
+#pragma unroll
+    for (int k = 0; k < N / 4; ++k) {
+        const v4u32 x = __builtin_nontemporal_load(v + k * B + (int)threadIdx.x);
+        lw[4 * k] = x.x;
+        lw[4 * k + 1] = x.y;
+        lw[4 * k + 2] = x.z;
+        lw[4 * k + 3] = x.w;
+        hw[k] = __builtin_nontemporal_load(h + k * B + (int)threadIdx.x);
+    }
+}
+
+template <bool HOP1, bool SRC_FULL, bool PK>
+__global__ void __launch_bounds__(kBlock) k_hop_2d(PairOut pairs, const int64_t* __restrict__ coff,
                                                    int64_t min_per, Layout L, BitV sb,
                                                    const uint32_t* __restrict__ X2, BitV tmask,
                                                    uint32_t* __restrict__ out, uint32_t* __restrict__ S1,
@@ -765,7 +848,7 @@ __global__ void __launch_bounds__(kBlock) k_hop_2d(const uint2* __restrict__ pai
             for (int k = threadIdx.x; k < kSliceWords; k += kBlock) sl[k] = w0 + k < gwords ? sb.w[w0 + k] : 0u;
         }
         __syncthreads();
-        const uint32_t tbase = (uint32_t)j << kSliceBits, sbase = (uint32_t)i << kSliceBits;
+        const uint32_t tbase = (uint32_t)j << L.tbits, sbase = (uint32_t)i << L.sbits;  // pull: sbits = kSliceBits
         auto visit = [&](const uint2 pr) {
             const uint32_t s = pr.x, t = pr.y;
             if (s != t) {
@@ -781,14 +864,28 @@ __global__ void __launch_bounds__(kBlock) k_hop_2d(const uint2* __restrict__ pai
                 if (gbit(X2, s)) lds_set(tl, t - tbase);
             }
         };
-        for (int64_t cb = e0 & ~int64_t(1); cb < ce; cb += (int64_t)kBlock * kUnroll) {  // block-uniform, even
-            uint2 p[kUnroll];
-            load_pairs<kBlock, kUnroll>(pairs, cb, p);
-            const int lo = (int)max(e0 - cb, (int64_t)0), hi = (int)min(ce - cb, (int64_t)kBlock * kUnroll);
+        if (PK) {  // 5 bytes per item: twice the items per step for the same loads in flight
+            constexpr int U = 2 * kUnroll;
+            for (int64_t cb = e0 & ~int64_t(3); cb < ce; cb += (int64_t)kBlock * U) {  // block-uniform
+                uint32_t lw[U], hw[U / 4];
+                load_packed<kBlock, U>(pairs.w, pairs.b, cb, lw, hw);
+                const int lo = (int)max(e0 - cb, (int64_t)0), hi = (int)min(ce - cb, (int64_t)kBlock * U);
 #pragma unroll
-            for (int u = 0; u < kUnroll; ++u) {
-                const int e = item_off<kBlock>(u);
-                if (e >= lo && e < hi) visit(p[u]);
+                for (int u = 0; u < U; ++u) {
+                    const int e = item_off4<kBlock>(u);
+                    if (e >= lo && e < hi) visit(key_pair(L, sbase, tbase, lw[u], (hw[u >> 2] >> (8 * (u & 3))) & 0xFFu));
+                }
+            }
+        } else {
+            for (int64_t cb = e0 & ~int64_t(1); cb < ce; cb += (int64_t)kBlock * kUnroll) {  // block-uniform, even
+                uint2 p[kUnroll];
+                load_pairs<kBlock, kUnroll>(pairs.p, cb, p);
+                const int lo = (int)max(e0 - cb, (int64_t)0), hi = (int)min(ce - cb, (int64_t)kBlock * kUnroll);
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) {
+                    const int e = item_off<kBlock>(u);
+                    if (e >= lo && e < hi) visit(p[u]);
+                }
             }
         }
         e0 = ce;
@@ -819,7 +916,20 @@ static part::Layout make_layout(int64_t lo, int64_t hi) {
     if (L.ns < 1) L.ns = 1;
     L.ncells = L.nt * L.ns;
     L.tbits = part::kSliceBits;
+    const char* fmt = getenv("CAPSMI_PAIRS");  // "uint2": the 8-byte pairs (A/B runs)
+    L.packed = L.sbits + L.tbits <= 40 && !(fmt && std::string(fmt) == "uint2");  // 5-byte cell keys
     return L;
+}
+
+static part::PairOut pair_out(const RelPart& rp) {
+    part::PairOut o{};
+    if (rp.L.packed) {
+        o.w = P<uint32_t>(rp.pairs);
+        o.b = reinterpret_cast<uint8_t*>(o.w + rp.cap);
+    } else {
+        o.p = P<uint2>(rp.pairs);
+    }
+    return o;
 }
 
 template <typename K>
@@ -927,6 +1037,11 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
     using namespace part;
     hipStream_t st = s->stream;
     rp.L = make_layout(lo, hi);
+    // Only a layout kept for later queries (capsmi_relpart_build, the cache() route) is packed: pass 2
+    // writing the packed form is slower (C3: 3.45 -> 3.9-4.45 ms unfused, 3.73 -> 4.14 ms with hop 1
+    // fused) while each hop over it gains 0.2-0.4 ms (hop 1 1.30 -> 0.90, hop 2 1.57 -> 1.35 ms), so a
+    // layout read by one query's two hops is left in 8-byte pairs
+    if (h1) rp.L.packed = 0;
     const Layout& L = rp.L;
     REQUIRE(L.nt <= kMaxTSlices && L.ncells <= kMaxCells, CAPSMI_ERR_INTERNAL, "layout too large");
     if (h1)
@@ -955,18 +1070,20 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
     rp.boff = dev_alloc(sizeof(int64_t) * (L.ncells + 1), s);  // cell offsets
     exclusive_scan_i64(P<int64_t>(tot), P<int64_t>(rp.boff), L.ncells, s);
     HIP_CHECK(hipGetLastError());
-    rp.pairs = dev_alloc(sizeof(uint2) * (mtot + kPad), s);  // kept <= mtot
+    rp.cap = mtot + kPad;  // kept <= mtot; slack for the hops' whole-step loads and pass 2's trash stores
+    rp.pairs = dev_alloc(L.packed ? 5 * (size_t)rp.cap : sizeof(uint2) * (size_t)rp.cap, s);
 
     Hop1Out ho{};
     if (fuse) ho = Hop1Out{BitV{P<uint32_t>(h1->b->words), h1->b->full ? 1 : 0}, h1->M, h1->S1, h1->S2, h1->b->nwords};
-    const size_t lds2 = sizeof(uint2) * ((size_t)kTile + (size_t)L.ns * kLine) +
+    const size_t lds2 = sizeof(uint2) * (size_t)kTile + s2_hold_bytes(L.ns, L.packed) +
                         sizeof(uint32_t) * (4 * L.ns + kSBlock / 64) + (fuse ? sizeof(uint32_t) * kSliceWords : 0);
-    auto k2 = fuse ? k_scatter_s2<true> : k_scatter_s2<false>;
+    REQUIRE(lds2 <= (size_t)160 * 1024, CAPSMI_ERR_INTERNAL, "pass-2 LDS");
+    auto k2 = L.packed ? k_scatter_s2<false, true> : fuse ? k_scatter_s2<true, false> : k_scatter_s2<false, false>;
     allow_lds(k2, lds2);
     {
         KernelTimer kt(s, fuse ? "part_scatter2_hop1" : "part_scatter2");
         hipLaunchKernelGGL(k2, dim3((unsigned)g2), dim3(kSBlock), lds2, st, P<uint2>(pool), P<unsigned long long>(meta),
-                           order, jst, segbase, ja, psum, P<int64_t>(rp.boff), L, P<uint2>(rp.pairs), mtot, ho);
+                           order, jst, segbase, ja, psum, P<int64_t>(rp.boff), L, pair_out(rp), mtot, ho);
     }
     HIP_CHECK(hipGetLastError());
     rp.kept = -1;  // known on the device (boff[ncells]); read only when asked (relpart_kept)
@@ -978,7 +1095,7 @@ template <bool HOP1, bool SRC_FULL>
 static void launch_hop(capsmi_session* s, const RelPart& rp, part::BitV sb, const uint32_t* X2, part::BitV tmask,
                        uint32_t* out, uint32_t* S1, uint32_t* S2, int64_t gwords) {
     const size_t lds = sizeof(uint32_t) * 2 * part::kSliceWords;
-    auto k = part::k_hop_2d<HOP1, SRC_FULL>;
+    auto k = rp.L.packed ? part::k_hop_2d<HOP1, SRC_FULL, true> : part::k_hop_2d<HOP1, SRC_FULL, false>;
     allow_lds(k, lds);
     // one 128 KiB-LDS block per CU at a time; a few rounds of blocks, equal relationship shares
     // (at least kBlock * kUnroll each; blocks past the end exit at once).  Grid sized from the upper
@@ -987,7 +1104,7 @@ static void launch_hop(capsmi_session* s, const RelPart& rp, part::BitV sb, cons
     int64_t blocks = (int64_t)s->num_cus * 4;
     const int64_t bound = rp.kept >= 0 ? rp.kept : rp.rows;
     blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, (bound + min_per - 1) / min_per));
-    hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(part::kBlock), lds, s->stream, P<uint2>(rp.pairs),
+    hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(part::kBlock), lds, s->stream, pair_out(rp),
                        P<int64_t>(rp.boff), min_per, rp.L, sb, X2, tmask, out, S1, S2, gwords);
     HIP_CHECK(hipGetLastError());
 }
@@ -1023,13 +1140,15 @@ __device__ __forceinline__ uint64_t pair_mix(uint2 p) {
     return z ^ (z >> 31);
 }
 
-__global__ void __launch_bounds__(256) k_cell_digest(const uint2* __restrict__ pairs, const int64_t* __restrict__ boff,
+__global__ void __launch_bounds__(256) k_cell_digest(part::PairOut pairs, const int64_t* __restrict__ boff,
                                                     part::Layout L, unsigned long long* __restrict__ sums,
                                                     unsigned long long* __restrict__ bad) {
     const int c = blockIdx.x;
+    const uint32_t sbase = (uint32_t)(c % L.ns) << L.sbits, tbase = (uint32_t)(c / L.ns) << L.tbits;
     unsigned long long acc = 0, nb = 0;
     for (int64_t i = boff[c] + threadIdx.x; i < boff[c + 1]; i += 256) {
-        const uint2 p = pairs[i];
+        // packed: the pair comes back through its cell, so a misplaced one shows as a wrong sum
+        const uint2 p = L.packed ? part::key_pair(L, sbase, tbase, pairs.w[i], pairs.b[i]) : pairs.p[i];
         acc += pair_mix(p);
         if (part::cell_of(L, p.x, p.y) != c) ++nb;
     }
@@ -1044,7 +1163,7 @@ void relpart_digest(capsmi_session* s, const RelPart& rp, int64_t* counts, uint6
     Buf d = dev_alloc(sizeof(unsigned long long) * (nc + 1), s);
     HIP_CHECK(hipMemsetAsync(P<void>(d), 0, sizeof(unsigned long long) * (nc + 1), st));
     if (rp.rows > 0) {
-        hipLaunchKernelGGL(k_cell_digest, dim3(nc), dim3(256), 0, st, P<uint2>(rp.pairs), P<int64_t>(rp.boff), rp.L,
+        hipLaunchKernelGGL(k_cell_digest, dim3(nc), dim3(256), 0, st, pair_out(rp), P<int64_t>(rp.boff), rp.L,
                            P<unsigned long long>(d), P<unsigned long long>(d) + nc);
         HIP_CHECK(hipGetLastError());
         HIP_CHECK(hipMemcpyAsync(off.data(), P<void>(rp.boff), sizeof(int64_t) * (nc + 1), hipMemcpyDeviceToHost, st));

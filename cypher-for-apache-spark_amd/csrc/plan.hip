@@ -1473,7 +1473,7 @@ bool try_fused_shapes(capsmi_table* t, capsmi_table** out) {
 
 }  // namespace
 
-void attach_entity(capsmi_table* t, int kind, int64_t lo, int64_t hi) {
+void attach_entity(capsmi_table* t, int kind, int64_t lo, int64_t hi, bool ids_exact) {
     auto e = std::make_shared<EntityInfo>();
     e->kind = kind;
     e->id = 0;
@@ -1484,6 +1484,7 @@ void attach_entity(capsmi_table* t, int kind, int64_t lo, int64_t hi) {
     e->rows = t->nrows;
     e->lo = lo;
     e->hi = hi;
+    e->ids_exact = ids_exact;
     t->entity = e;
 }
 
@@ -2270,6 +2271,15 @@ static capsmi_table* register_entity(capsmi_table* t, int kind, const std::vecto
         }
         e->lo = mm[0];
         e->hi = mm[1] == INT64_MAX ? INT64_MAX : mm[1] + 1;
+        if (kind == 1 && mm[1] != INT64_MAX && e->hi - e->lo == t->nrows && t->nrows <= (int64_t(1) << 31)) {
+            // as many rows as ids in [min, max]: the ids are exactly that window iff none repeats
+            capsmi_bitmap* b = nullptr;
+            check(capsmi_bitmap_create(s, e->lo, e->hi, &b));
+            const capsmi_status st = capsmi_bitmap_add_scan(b, t, t->cols[0].name.c_str(), 0, nullptr);
+            e->ids_exact = st == CAPSMI_OK && !b->any_dup && b->set_bits == t->nrows;
+            capsmi_bitmap_release(b);
+            check(st);
+        }
     }
     auto* o = new capsmi_table();
     o->sess = t->sess;

@@ -283,3 +283,34 @@ def test_bitmap_add_scan_bits(session, case):
     everyone = graph.NodeBitmap(session, lo, hi).add_scan(session.table([ColumnData("id", I64, dom)]))
     out = graph.expand_filter(session, rels, bm, everyone, ["source"], ["s"])
     np.testing.assert_array_equal(np.sort(out.column("s").values), allids)
+
+
+@pytest.mark.parametrize("case", ["exact", "exact_wider_window", "dup_and_gap", "sparse"])
+def test_bitmap_scan_of_exact_node_table(session, case):
+    """A registered node table whose ids are exactly one window (checked at capsmi_node_table) scans
+    into the bitmap as a range fill; the words and stats must equal a row-by-row scan of the same
+    ids, and tables that only look exact (a duplicate plus a gap) take the row path."""
+    import torch
+    from capsmi import ColumnData, I64, graph
+    rng = np.random.default_rng(5)
+    lo = 1000
+    ids = rng.permutation(np.arange(lo, lo + 70001)).astype(np.int64)
+    if case == "dup_and_gap":
+        ids[17] = ids[18]
+    elif case == "sparse":
+        ids = ids[::3].copy()
+    wlo, whi = (lo - 45, lo + 70001 + 77) if case == "exact_wider_window" else (lo, lo + 70001)
+    if case == "sparse":
+        wlo, whi = int(ids.min()), int(ids.max()) + 1
+    plain = session.table([ColumnData("id", I64, ids)])
+    node = plain.as_node_table("id")
+    nw = (whi - wlo + 31) // 32
+    words = []
+    for t in (node, plain):
+        bm = graph.NodeBitmap(session, wlo, whi).add_scan(t, "id")
+        w = torch.zeros(nw, dtype=torch.int32, device="cuda")
+        bm.copy_words(0, nw, w.data_ptr(), to_bitmap=False)  # on the session's stream
+        session.sync()
+        words.append((w.cpu().numpy(), bm.stats()))
+    np.testing.assert_array_equal(words[0][0], words[1][0])
+    assert words[0][1] == words[1][1] == (len(np.unique(ids)), len(np.unique(ids)) == len(ids))
