@@ -48,4 +48,10 @@ for _ in range(20):
     t.column(outs[0][2])
 pr.disable()
 pstats.Stats(pr).sort_stats("tottime").print_stats(12)
+pr = cProfile.Profile()  # plan construction alone: where the Python time goes
+pr.enable()
+for _ in range(200):
+    t, outs = Planner(sg).run(bench.C3_QUERY)
+pr.disable()
+pstats.Stats(pr).sort_stats("tottime").print_stats(30)
 s.close()

@@ -7,7 +7,7 @@ import sys
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
 first = sys.argv[2]
 min_gap = float(sys.argv[3]) if len(sys.argv) > 3 else 0.0
-idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(first)]
+idx = [i for i, r in enumerate(rows) if first in r["Kernel_Name"]]
 s, e = (idx[-2], idx[-1]) if len(idx) > 1 else (idx[-1], len(rows))
 t0 = prev = int(rows[s]["Start_Timestamp"])
 busy = idle = 0
