@@ -17,7 +17,9 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib
-from .expr import BOOL, F64, I64, LIST, STR, Expr, compile_program, to_ctypes
+from .expr import BOOL, F64, I64, LIST, STR, CapsmiExpr, Col, Expr, compile_program, to_ctypes
+
+_EXPR_PTR = ctypes.POINTER(CapsmiExpr)
 
 JOIN_TYPES = {"inner": 0, "left_outer": 1, "right_outer": 2, "full_outer": 3, "cross": 4}
 AGG_KINDS = {"count_star": 0, "count": 1, "min": 2, "max": 3, "sum": 4, "avg": 5, "collect": 6}
@@ -279,6 +281,7 @@ class GpuTable:
         self._h = handle
         self._schema = None  # (names, types): tables are immutable, so the schema is read once
         self._index = None  # name -> position (expression compilation)
+        self._leaf = None  # column name -> its one-node program (the planner's scans project columns)
 
     # ---- lifetime ------------------------------------------------------------------------
     @property
@@ -461,6 +464,12 @@ class GpuTable:
         return self._index
 
     def _program(self, e: Expr):
+        if type(e) is Col:  # the common leaf: one program per (table, column), reused (C copies it)
+            if self._leaf is None:
+                self._leaf = {}
+            hit = self._leaf.get(e.name)
+            if hit is not None:
+                return 1, hit
         index = self._column_index()
 
         def col(name: str) -> int:
@@ -469,7 +478,10 @@ class GpuTable:
             return index[name]
 
         prog = compile_program(e, col, self.session.encode_str)
-        return len(prog), to_ctypes(prog)
+        arr = to_ctypes(prog)
+        if type(e) is Col:
+            self._leaf[e.name] = arr
+        return len(prog), arr
 
     def filter(self, expr: Expr) -> "GpuTable":
         n, prog = self._program(expr)
@@ -542,7 +554,7 @@ class GpuTable:
             keep.append(prog)
             arr[i].name = name.encode()
             arr[i].nnodes = n
-            arr[i].prog = ctypes.cast(prog, ctypes.POINTER(type(prog._type_())))
+            arr[i].prog = ctypes.cast(prog, _EXPR_PTR)
         out = ctypes.c_void_p()
         _lib.call("capsmi_with_columns", self._h, len(columns), arr, ctypes.byref(out))
         return self._wrap(out)

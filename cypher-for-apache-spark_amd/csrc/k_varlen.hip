@@ -190,13 +190,21 @@ struct RegionBloom {
     int sublog;                // log2(regions per slice)
 };
 
-__device__ __forceinline__ unsigned long long rb_bit(const RegionBloom& b, uint32_t y, unsigned long long k) {
-    return ((unsigned long long)(y >> (kVlBits - b.sublog)) << b.rshift) | (splitmix(k ^ 0x5DEECE66DULL) & b.rmask);
+// A key sets three bits of ONE 32-bit word of its region (a blocked filter: one load per test).  At 8
+// bits per pair that is ~4 % false candidates against 22 % for one bit at 4 bits per pair -- and at
+// C5 only 0.3 % of the relationships have a reverse, so the false candidates were nearly all of the
+// 7.5·10^6 exact-table inserts.
+__device__ __forceinline__ void rb_pos(const RegionBloom& b, unsigned long long k, uint32_t& word, uint32_t& mask) {
+    const unsigned long long h = splitmix(k ^ 0x5DEECE66DULL);
+    word = (uint32_t)(h & (b.rmask >> 5));
+    mask = (1u << ((h >> 40) & 31)) | (1u << ((h >> 46) & 31)) | (1u << ((h >> 52) & 31));
 }
 
 __device__ __forceinline__ bool rb_test(const RegionBloom& b, uint32_t y, unsigned long long k) {
-    const unsigned long long x = rb_bit(b, y, k);
-    return (b.w[x >> 5] >> (x & 31)) & 1u;
+    uint32_t word, mask;
+    rb_pos(b, k, word, mask);
+    const unsigned long long base = (unsigned long long)(y >> (kVlBits - b.sublog)) << (b.rshift - 5);
+    return (b.w[base + word] & mask) == mask;
 }
 
 // Second-level filter of the candidate pairs (those the RegionBloom passes): one region of
@@ -257,19 +265,35 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_deg(ChunkWalk cw, const uint32_
     if (f2part)
         for (int i = threadIdx.x; i < kF2Words; i += kVlBlock) f2[i] = 0;
     __syncthreads();
-    walk_chunks(
+    part::walk_chunks_n<kVlBlock>(
         cw,
-        [&](uint2 p, int) {  // p = (t, s)
-            const uint32_t t = p.x, s = p.y;
-            if (od) {
-                if (bit_of(bw, b_full, t)) atomicAdd(&a_od[s & (kVlIds - 1)], 1ULL);
-                if (s == t) atomicAdd(&sl[s], 1ULL);
+        [&](const uint2 (&pr)[part::kWalkItems], uint32_t valid, int) {  // pr[k] = (t, s)
+            constexpr int K = part::kWalkItems;
+            uint32_t bwd[K], rw[K], rm[K];  // every global word of the step loaded before any is used
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t t = pr[k].x, s = pr[k].y;
+                bwd[k] = (od && !b_full) ? bw[t >> 5] : 0xFFFFFFFFu;
+                if (f2part) {
+                    uint32_t word;
+                    rb_pos(bl, pkey(t, s), word, rm[k]);
+                    rw[k] = bl.w[((unsigned long long)(s >> (kVlBits - bl.sublog)) << (bl.rshift - 5)) + word];
+                }
             }
-            if (f2part && rb_test(bl, s, pkey(t, s))) {
-                uint32_t word, bits;
-                f2_pos(pkey(s, t), word, bits);
-                atomicOr(&f2[word], bits);
-                ++mine;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (!((valid >> k) & 1u)) continue;
+                const uint32_t t = pr[k].x, s = pr[k].y;
+                if (od) {
+                    if ((bwd[k] >> (t & 31)) & 1u) atomicAdd(&a_od[s & (kVlIds - 1)], 1ULL);
+                    if (s == t) atomicAdd(&sl[s], 1ULL);
+                }
+                if (f2part && (rw[k] & rm[k]) == rm[k]) {
+                    uint32_t word, bits;
+                    f2_pos(pkey(s, t), word, bits);
+                    atomicOr(&f2[word], bits);
+                    ++mine;
+                }
             }
         },
         [&](int j) {
@@ -297,11 +321,15 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_w(ChunkWalk cw, int64_t n, cons
     unsigned long long* a_w = vl_lds;
     for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_w[i] = 0;
     __syncthreads();
-    walk_chunks(
+    part::walk_chunks_n<kVlBlock>(
         cw,
-        [&](uint2 p, int) {  // p = (t, s)
-            const unsigned long long x = od[p.x];
-            if (x) atomicAdd(&a_w[p.y & (kVlIds - 1)], x);
+        [&](const uint2 (&pr)[part::kWalkItems], uint32_t valid, int) {  // pr[k] = (t, s)
+            unsigned long long x[part::kWalkItems];
+#pragma unroll
+            for (int k = 0; k < part::kWalkItems; ++k) x[k] = od[pr[k].x];  // all gathers first
+#pragma unroll
+            for (int k = 0; k < part::kWalkItems; ++k)
+                if (((valid >> k) & 1u) && x[k]) atomicAdd(&a_w[pr[k].y & (kVlIds - 1)], x[k]);
         },
         [&](int j) { flush_acc(a_w, W, j, n); });
 }
@@ -312,7 +340,7 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_ins(ChunkWalk cw, RegionBloom b
     walk_chunks(
         cw,
         [&](uint2 p, int) {  // p = (b, a)
-            if (rb_test(bl, p.y, pkey(p.x, p.y)) && f2_test(f2, p.x, pkey(p.x, p.y))) pair_insert(h, hkey(p.y, p.x));
+            if (f2_test(f2, p.x, pkey(p.x, p.y)) && rb_test(bl, p.y, pkey(p.x, p.y))) pair_insert(h, hkey(p.y, p.x));
         },
         [&](int) {});
 }
@@ -332,8 +360,9 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_bset(ChunkWalk cw, RegionBloom 
             cw,
             [&](uint2 p, int) {
                 if ((int)((p.y >> rb) & (nsub - 1)) != sub) return;
-                const unsigned long long x = splitmix(pkey(p.x, p.y) ^ 0x5DEECE66DULL) & bl.rmask;
-                atomicOr(&rb_lds[x >> 5], 1u << (x & 31));
+                uint32_t word, mask;
+                rb_pos(bl, pkey(p.x, p.y), word, mask);
+                atomicOr(&rb_lds[word], mask);
             },
             [&](int j) {
                 uint4* g = part + ((((size_t)blockIdx.x + j) * nsub + sub) << (bl.rshift - 7));
@@ -422,18 +451,39 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_t(ChunkWalk cw, const uint32_t*
     unsigned long long *a_t2 = vl_lds, *a_t3 = vl_lds + kVlIds;
     for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_t2[i] = a_t3[i] = 0;
     __syncthreads();
-    walk_chunks(
+    part::walk_chunks_n<kVlBlock>(
         cw,
-        [&](uint2 p, int) {
-            const uint32_t b = p.x, a = p.y, i = a & (kVlIds - 1);
-            if (h.slot && rb_test(bl, a, pkey(b, a)) && f2_test(f2, b, pkey(b, a))) pair_insert(h, hkey(a, b));
-            if (!bit_of(aw, a_full, a)) return;
-            if (ody) {  // T3 also wanted
-                const longlong2 v = ody[b];
-                atomicAdd(&a_t2[i], (unsigned long long)v.x);
-                atomicAdd(&a_t3[i], (unsigned long long)v.y);  // two's complement sum
-            } else {
-                atomicAdd(&a_t2[i], od[b]);
+        [&](const uint2 (&pr)[part::kWalkItems], uint32_t valid, int) {
+            constexpr int K = part::kWalkItems;
+            // every gather of the step issued before any is used: (od, Y) of each target and, with the
+            // filters, the second-level word of each reverse key (its table, 64 KiB per slice, passes
+            // ~0.3 % of the pairs at C5, so the first-level region is read for those only -- it bounds
+            // the inserts by the counted candidates, so it stays)
+            longlong2 v[K];
+            unsigned long long o1[K];
+            uint32_t fw[K], fb[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t b = pr[k].x;  // zero pairs past a chunk's fill: in range
+                if (ody) v[k] = ody[b]; else o1[k] = od[b];
+                if (h.slot) {
+                    uint32_t word;
+                    f2_pos(pkey(b, pr[k].y), word, fb[k]);
+                    fw[k] = f2[((size_t)(b >> kVlBits) * kF2Words) + word];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                if (!((valid >> k) & 1u)) continue;
+                const uint32_t b = pr[k].x, a = pr[k].y, i = a & (kVlIds - 1);
+                if (h.slot && (fw[k] & fb[k]) == fb[k] && rb_test(bl, a, pkey(b, a))) pair_insert(h, hkey(a, b));
+                if (!bit_of(aw, a_full, a)) continue;
+                if (ody) {  // T3 also wanted
+                    atomicAdd(&a_t2[i], (unsigned long long)v[k].x);
+                    atomicAdd(&a_t3[i], (unsigned long long)v[k].y);  // two's complement sum
+                } else {
+                    atomicAdd(&a_t2[i], o1[k]);
+                }
             }
         },
         [&](int j) {
@@ -493,17 +543,19 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
         RegionBloom bl{nullptr, 0, 0, 0};
         PairHash h{nullptr, nullptr, nullptr, 0};
         if (need3) {
-            // filter of the directed pairs: 8 bits per pair of an average region where a region of
-            // at most 128 KiB (LDS) allows; a slice gets 2^sublog regions only past 4 bits per pair
-            // (each region is one more pass of k_vl_bset: on C5, 4 bits/pair and 22% false
-            // candidates beat 2 regions by ~0.1 ms and 4 by ~0.3)
+            // filter of the directed pairs (RegionBloom): a region holds at most 2^20 bits (128 KiB of
+            // LDS while k_vl_bset builds it), so a slice with more pairs gets 2^sublog regions, one
+            // more k_vl_bset pass each
             KernelTimer kt(s, "varlen_rev");
             chunk_partition(s, srcs, dsts, ms, nt, false, L, s->num_cus, ct);
             const int64_t per_slice = (mtot + L.nt - 1) / L.nt;
+            // 8 bits per pair (CAPSMI_VL_BITS), in 2^sublog regions of <= 2^20 bits per slice
+            int64_t bits_per = 8;
+            if (const char* e = getenv("CAPSMI_VL_BITS")) bits_per = atoi(e) < 2 ? 2 : (atoi(e) > 64 ? 64 : atoi(e));
             int sublog = 0, rshift = 10;
-            while (sublog < 3 && (int64_t(4) * per_slice >> sublog) > (int64_t(1) << 20)) ++sublog;
+            while (sublog < 3 && (bits_per * per_slice >> sublog) > (int64_t(1) << 20)) ++sublog;
             if (const char* e = getenv("CAPSMI_VL_SUBLOG")) sublog = atoi(e) < 0 ? 0 : (atoi(e) > 5 ? 5 : atoi(e));
-            while ((int64_t(1) << rshift) < (int64_t(8) * per_slice >> sublog) && rshift < 20) ++rshift;
+            while ((int64_t(1) << rshift) < (bits_per * per_slice >> sublog) && rshift < 20) ++rshift;
             const int64_t nreg = (int64_t)L.nt << sublog;
             const size_t rbytes = (size_t(1) << rshift) / 8;
             bw = dev_alloc(rbytes * nreg, s);

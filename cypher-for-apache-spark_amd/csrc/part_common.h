@@ -222,9 +222,14 @@ struct NoBegin {
 // chunk's ids fetched ahead: a part-full chunk (most of them when the slices are many) costs its own
 // pairs, not a pass of the whole block.  Visits must not depend on the order of the pairs.
 // (G, the chunks in flight of the former block-per-chunk walk, is kept for the callers.)
-template <int BLK, int G = 1, class Visit, class Flush, class Begin = NoBegin>
-__device__ void walk_chunks(const ChunkWalk& cw, Visit visit, Flush flush, Begin begin = Begin()) {
-    constexpr int kLd = 4;                 // 16-byte loads per lane per step
+constexpr int kWalkItems = 8;  // pairs per lane per walk step (four 16-byte loads)
+
+// The walk below with the visit taking a lane's whole step: visit(pr, valid, j), pr[k] valid where
+// bit k of `valid` is set (entries past a chunk's fill read as zero pairs).  Lets a visit issue the
+// gathers of all its items before it uses any (a per-item visit waits for each in turn).
+template <int BLK, int G = 1, class VisitN, class Flush, class Begin = NoBegin>
+__device__ void walk_chunks_n(const ChunkWalk& cw, VisitN visit, Flush flush, Begin begin = Begin()) {
+    constexpr int kLd = kWalkItems / 2;    // 16-byte loads per lane per step
     constexpr uint32_t kStep = 64 * kLd * 2;  // pairs per wave step
     __shared__ uint32_t qn;                // next chunk of the slice visit
     const int64_t w = blockIdx.x, blocks = gridDim.x;
@@ -267,9 +272,11 @@ __device__ void walk_chunks(const ChunkWalk& cw, Visit visit, Flush flush, Begin
                     pr[2 * k] = make_uint2(v[0], v[1]);
                     pr[2 * k + 1] = make_uint2(v[2], v[3]);
                 }
+                uint32_t valid = 0;
 #pragma unroll
                 for (int k = 0; k < 2 * kLd; ++k)
-                    if (o + 2u * (uint32_t)((k >> 1) * 64 + lane) + (uint32_t)(k & 1) < fill) visit(pr[k], j);
+                    valid |= (o + 2u * (uint32_t)((k >> 1) * 64 + lane) + (uint32_t)(k & 1) < fill ? 1u : 0u) << k;
+                visit(pr, valid, j);
             }
             t = tn;
             phys = pn;
@@ -283,6 +290,18 @@ __device__ void walk_chunks(const ChunkWalk& cw, Visit visit, Flush flush, Begin
         } while (cw.jst[cur_j + 1] <= cw.jst[cur_j]);  // empty slices are skipped
         __syncthreads();
     }
+}
+
+template <int BLK, int G = 1, class Visit, class Flush, class Begin = NoBegin>
+__device__ void walk_chunks(const ChunkWalk& cw, Visit visit, Flush flush, Begin begin = Begin()) {
+    walk_chunks_n<BLK, G>(
+        cw,
+        [&](const uint2 (&pr)[kWalkItems], uint32_t valid, int j) {
+#pragma unroll
+            for (int k = 0; k < kWalkItems; ++k)
+                if ((valid >> k) & 1u) visit(pr[k], j);
+        },
+        flush, begin);
 }
 
 // whether block w's chunk share holds all of slice j's chunks (then its flush owns the slice)
