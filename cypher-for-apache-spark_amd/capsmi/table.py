@@ -17,9 +17,10 @@ from typing import Iterable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib
-from .expr import BOOL, F64, I64, LIST, STR, CapsmiExpr, Col, Expr, compile_program, to_ctypes
+from .expr import BOOL, F64, I64, LIST, STR, CapsmiExpr, Col, Expr, Lit, compile_program, to_ctypes
 
 _EXPR_PTR = ctypes.POINTER(CapsmiExpr)
+_LIT_PROGS = {}  # (python type, value, declared type) -> one-node program of a Boolean / Long / null literal
 
 JOIN_TYPES = {"inner": 0, "left_outer": 1, "right_outer": 2, "full_outer": 3, "cross": 4}
 AGG_KINDS = {"count_star": 0, "count": 1, "min": 2, "max": 3, "sum": 4, "avg": 5, "collect": 6}
@@ -470,6 +471,12 @@ class GpuTable:
             hit = self._leaf.get(e.name)
             if hit is not None:
                 return 1, hit
+        elif type(e) is Lit and (e.value is None or type(e.value) in (bool, int)):  # label flags, nulls
+            key = (type(e.value), e.value, e.type)
+            hit = _LIT_PROGS.get(key)
+            if hit is None:
+                hit = _LIT_PROGS[key] = to_ctypes(compile_program(e, None, None))
+            return 1, hit
         index = self._column_index()
 
         def col(name: str) -> int:
