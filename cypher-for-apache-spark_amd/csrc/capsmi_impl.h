@@ -381,10 +381,11 @@ struct TriGraph {
     Buf ek, ev, sl;   // undirected keys / payload (pair terms), self-loop counts
     Buf small_u, big_u;  // vertices with out-degree in [2, 64] / above 64
     int64_t nsmall = 0, nbig = 0;
-    // Direction choice per oriented edge u -> v (the wedges through it cost od(v) probes walking
-    // out(v) from u, or od(u) walking out(u) from v): with vmt > 0 the edges with od(v) >= vmt and
-    // od(u) <= od(v) are taken from v ("v-mode"), over the in-lists (ioff, itg, iov: sources and
-    // payloads of the oriented edges grouped by target); vm_c = the v-mode centers.
+    // Direction choice per oriented edge u -> v at position p of out(u) (out-lists are sorted, and
+    // every wedge u -> v -> w that can close has w < v, so from v only the prefix out(u)[0, p) needs
+    // walking; from u the whole out(v)): with vmt > 0 the edges with od(v) >= vmt and p < od(v) are
+    // taken from v ("v-mode"), over the in-lists (ioff, itg, iov: sources and oriented-edge indexes
+    // grouped by target, so p = iov - off[u] and the payload is ov[iov]); vm_c = the v-mode centers.
     int vmt = 0;
     Buf ioff, itg, iov, vm_c;
     int64_t nvm = 0;

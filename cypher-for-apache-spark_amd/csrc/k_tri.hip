@@ -172,13 +172,14 @@ __global__ void k_orient(const uint64_t* __restrict__ ek, const int64_t* __restr
     }
 }
 
-// in-lists: oriented keys (from << 32 | to) swapped to (to << 32 | from), payloads alongside
-__global__ void k_swap_keys(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ ov, int64_t ne,
-                            uint64_t* __restrict__ ik, int64_t* __restrict__ iv) {
+// in-lists: oriented keys (from << 32 | to) swapped to (to << 32 | from), the oriented edge's index
+// alongside (its position in out(from) bounds the v-mode walk; its payload is read through it)
+__global__ void k_swap_keys(const uint64_t* __restrict__ ok_, int64_t ne, uint64_t* __restrict__ ik,
+                            int64_t* __restrict__ iv) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t k = ok_[i];
         ik[i] = (k << 32) | (k >> 32);
-        iv[i] = ov[i];
+        iv[i] = i;
     }
 }
 
@@ -387,7 +388,7 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
             const uint64_t pv = (uint64_t)ov[b + lane];
             const int64_t vo = off[v];
             dv = (uint32_t)(off[v + 1] - vo);
-            if (vmt > 0 && dv >= (uint32_t)vmt && (uint32_t)d <= dv) dv = 0;  // v-mode takes u -> v
+            if (vmt > 0 && dv >= (uint32_t)vmt && (uint32_t)lane < dv) dv = 0;  // v-mode takes u -> v
             W.vl[lane] = v;
             W.vp[lane] = pv;
             W.voff[lane] = vo;
@@ -418,7 +419,11 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
                     for (int r = 0; r < U; ++r) {
                         if (!((keep >> r) & 1u)) continue;
                         const int sl = hfind(W.hk, 9, w[r]);
+#if CAPSMI_TRI_DIAG
+                        if (sl >= 0) acc += 1;
+#else
                         if (sl >= 0) acc += tri_weight(puv, (uint64_t)ov[vo + j0 + r * 64], W.vp[W.hi[sl]]);
+#endif
                     }
                 }
             }
@@ -586,10 +591,14 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
             const uint32_t v = VM ? itg[nb + v0 + k] : tg[b + v0 + k];
             const int64_t vo = off[v];
             const uint32_t dv = (uint32_t)(off[v + 1] - vo);
+            const int64_t e = VM ? iov[nb + v0 + k] : b + v0 + k;  // the edge u -> v either way
             L.vl[k] = v;
-            L.vp[k] = (uint64_t)(VM ? iov[nb + v0 + k] : ov[b + v0 + k]);  // the edge u -> v either way
+            L.vp[k] = (uint64_t)ov[e];
             L.voff[k] = vo;
-            L.dv[k] = VM ? (dv <= (uint32_t)d ? dv : 0u) : (vmt > 0 && dv >= (uint32_t)vmt && (uint32_t)d <= dv ? 0u : dv);
+            // v-mode walks out(u) below the center: the prefix [0, p) of out(u), p = position of the
+            // edge; u-mode skips the edges v-mode takes (od(v) >= vmt and p < od(v))
+            const uint32_t p = (uint32_t)(e - (VM ? vo : b));
+            L.dv[k] = VM ? (p < (uint32_t)d ? p : 0u) : (vmt > 0 && dv >= (uint32_t)vmt && p < dv ? 0u : dv);
         }
         __syncthreads();
         if (LISTS) {
@@ -606,8 +615,12 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
                         if (!((keep >> r) & 1u)) continue;
                         const int sl = hfind(L.hk, 13, w[r]);
                         if (sl >= 0) {
+#if CAPSMI_TRI_DIAG  // timing diagnostic only (wrong counts): hits without their payload loads
+                            acc += 1;
+#else
                             const uint64_t pxw = (uint64_t)ov[vo + j0 + r * 64], pcw = (uint64_t)ov[b + h0 + L.hi[sl]];
                             acc += VM ? tri_weight(puv, pcw, pxw) : tri_weight(puv, pxw, pcw);
+#endif
                         }
                     }
                 }
@@ -803,8 +816,8 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     if (g.vmt > 0 && ne > 0) {
         Buf ik = dev_alloc(sizeof(uint64_t) * ne, s);
         g.iov = dev_alloc(sizeof(int64_t) * ne, s);
-        hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.ov), ne,
-                           P<uint64_t>(ik), P<int64_t>(g.iov));
+        hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, P<uint64_t>(ik),
+                           P<int64_t>(g.iov));
         // by (to, from): the input is in (from, to) order and the LSD sort is stable, so the digits of
         // `to` alone give that order (3 passes at 2^24 ids instead of 6)
         std::vector<int> td;
