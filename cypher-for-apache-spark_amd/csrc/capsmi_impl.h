@@ -371,12 +371,10 @@ void relpart_hop2(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* c, 
 struct TriGraph {
     int64_t lo = 0, n = 0, ne = 0;
     Buf ok, ov, off;  // oriented keys (from<<32|to), payload (m(from,to)<<32|m(to,from)), CSR offsets (n + 1)
-    Buf tg;           // uint32 targets of the oriented edges (the `to` of ok)
-    // Ids are the degree order (0 = highest (degree, id)), so the hub vertices' out-lists -- the ones
-    // the wedge walk re-reads -- are the prefix [0, hot_end) of tg, and their targets are hubs too:
-    // that prefix is also kept as uint16 (vertices 0 .. 2^16 - 1)
-    Buf tg16;
-    int64_t hot_end = 0;
+    // uint32 targets of the oriented edges (the `to` of ok, ib bits) with the edge's two multiplicities
+    // in cb bits each above it (all-ones: read ov); ids are the degree order (0 = highest (degree, id))
+    Buf tg;
+    int ib = 0, cb = 0;
     Buf orig;         // int64 per vertex: relative id of the degree-order id (unused by the count)
     Buf ek, ev, sl;   // undirected keys / payload (pair terms), self-loop counts
     Buf small_u, big_u;  // vertices with out-degree in [2, 64] / above 64

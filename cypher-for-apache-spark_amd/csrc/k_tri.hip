@@ -190,10 +190,6 @@ __global__ void k_tri_vm_bins(const int64_t* __restrict__ off, const int64_t* __
         f[v] = off[v + 1] - off[v] >= vmt && ioff[v + 1] > ioff[v];
 }
 
-__global__ void k_targets16(const uint32_t* __restrict__ tg, int64_t n, uint16_t* __restrict__ tg16) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        tg16[i] = (uint16_t)tg[i];
-}
 
 // CSR offsets of the oriented (sorted) edges: off[v] = first edge with source >= v
 __global__ void k_offsets(const uint64_t* __restrict__ ok_, int64_t ne, int64_t n, int64_t* __restrict__ off) {
@@ -262,13 +258,35 @@ __device__ __forceinline__ bool btest(const uint32_t* bf, int bits, uint32_t w) 
     return (bf[x >> 5] >> (x & 31)) & 1u;
 }
 
-// key w, and the index of its entry in the hashed list (the payload is read through it, on hits)
+// Oriented targets carry their edge's multiplicities (`TgCode`): word = to | f << ib | b << (ib + cb),
+// f = m(from, to), b = m(to, from), cb bits each; a field at its all-ones value (cmask) marks an
+// exception whose exact payload is read from ov.  The wedge walks then resolve a hit from the two words
+// alone (a hit used to cost two dependent 8-byte payload loads: 47 of the 116 ms at C4, measured by a
+// run with the loads removed).  With 2^24 ids, cb = 4: < 1 % of the hits need an exact payload (R-MAT
+// s = 20 / 22, hits whose edges carry a multiplicity >= 15).
+struct TgCode {
+    uint32_t ib, cb;  // id bits, code bits per direction (0: every payload is an exception)
+    __host__ __device__ uint32_t idmask() const { return ib >= 32 ? ~0u : (1u << ib) - 1u; }
+    __host__ __device__ uint32_t cmask() const { return (1u << cb) - 1u; }
+};
+
+__device__ __forceinline__ uint32_t tid(uint32_t word, TgCode c) { return word & c.idmask(); }
+
+// payload (f << 32 | b) of a coded word, or the exact one at ov[pos] for an exception
+__device__ __forceinline__ uint64_t tpay(uint32_t word, TgCode c, const int64_t* __restrict__ ov, int64_t pos) {
+    const uint32_t f = (word >> c.ib) & c.cmask(), b = (word >> (c.ib + c.cb)) & c.cmask();
+    if (f == c.cmask() || b == c.cmask()) return (uint64_t)ov[pos];
+    return (uint64_t)f << 32 | b;
+}
+
+// word (id + code bits; the id is the hash key), and the index of its entry in the hashed list (the
+// exact payload of an exception is read through it)
 template <class Idx>
-__device__ __forceinline__ void hinsert(uint32_t* hk, Idx* hi, int log2cap, uint32_t w, uint32_t idx) {
+__device__ __forceinline__ void hinsert(uint32_t* hk, Idx* hi, int log2cap, uint32_t id, uint32_t word, uint32_t idx) {
     const uint32_t mask = (1u << log2cap) - 1;
-    uint32_t sl = hslot(w, log2cap);
+    uint32_t sl = hslot(id, log2cap);
     while (true) {
-        const uint32_t prev = atomicCAS(&hk[sl], kEmpty, w);
+        const uint32_t prev = atomicCAS(&hk[sl], kEmpty, word);
         if (prev == kEmpty) {
             hi[sl] = (Idx)idx;
             return;
@@ -277,13 +295,14 @@ __device__ __forceinline__ void hinsert(uint32_t* hk, Idx* hi, int log2cap, uint
     }
 }
 
-__device__ __forceinline__ int hfind(const uint32_t* hk, int log2cap, uint32_t w) {
+// slot of id w (keys compared under idm), or -1
+__device__ __forceinline__ int hfind(const uint32_t* hk, int log2cap, uint32_t w, uint32_t idm) {
     const uint32_t mask = (1u << log2cap) - 1;
     uint32_t sl = hslot(w, log2cap);
     while (true) {
         const uint32_t k = hk[sl];
-        if (k == w) return (int)sl;
         if (k == kEmpty) return -1;
+        if ((k & idm) == w) return (int)sl;
         sl = (sl + 1) & mask;
     }
 }
@@ -316,11 +335,6 @@ struct SmallWave {
     uint32_t dv[kSmallDeg];
 };
 
-// target of oriented edge `pos`: 2 bytes inside the hub prefix, 4 beyond it
-__device__ __forceinline__ uint32_t target(const uint32_t* __restrict__ tg, const uint16_t* __restrict__ tg16,
-                                          int64_t hot_end, int64_t pos) {
-    return pos < hot_end ? (uint32_t)tg16[pos] : tg[pos];
-}
 
 // a wave-uniform 64-bit value into scalar registers, so addresses built on it take the scalar base +
 // 32-bit lane offset form instead of 64-bit vector arithmetic per load
@@ -330,29 +344,21 @@ __device__ __forceinline__ int64_t uniform64(int64_t v) {
 }
 
 // One pass of a wave over U x 64 consecutive entries of a list (this lane: entries j0 + r * 64):
-// the list lies wholly inside or wholly outside the 16-bit hub prefix, so the choice is made once,
-// and the loads are unconditional at clamped indexes (entries past the end become kEmpty), which
-// keeps them free of per-load branches.  Then the U pre-filter words are read together before any
-// is tested; `keep` marks the entries that pass.
+// the loads are unconditional at clamped indexes, which keeps them free of per-load branches.  Then
+// the U pre-filter words are read together before any is tested; `keep` marks the entries that pass.
+// w[] are the coded words (id + multiplicities).
 template <int U>
-__device__ __forceinline__ void list_pass(const uint32_t* __restrict__ tg, const uint16_t* __restrict__ tg16,
-                                          int64_t hot_end, int64_t vo, int dv, int j0, const uint32_t* bf, int bits,
-                                          uint32_t (&w)[U], uint32_t& keep) {
+__device__ __forceinline__ void list_pass(const uint32_t* __restrict__ tg, TgCode tc, int64_t vo, int dv, int j0,
+                                          const uint32_t* bf, int bits, uint32_t (&w)[U], uint32_t& keep) {
     // unsigned 32-bit indexes off a scalar base: the loads take the scalar-base + lane-offset form
     const uint32_t last = (uint32_t)dv - 1u, j = (uint32_t)j0;
-    if (vo + dv <= hot_end) {  // wave-uniform
-        const char* __restrict__ p = reinterpret_cast<const char*>(tg16 + vo);
+    const char* __restrict__ p = reinterpret_cast<const char*>(tg + vo);
 #pragma unroll
-        for (int r = 0; r < U; ++r) w[r] = *reinterpret_cast<const uint16_t*>(p + (min(j + (uint32_t)r * 64u, last) << 1));
-    } else {
-        const char* __restrict__ p = reinterpret_cast<const char*>(tg + vo);
-#pragma unroll
-        for (int r = 0; r < U; ++r) w[r] = *reinterpret_cast<const uint32_t*>(p + (min(j + (uint32_t)r * 64u, last) << 2));
-    }
+    for (int r = 0; r < U; ++r) w[r] = *reinterpret_cast<const uint32_t*>(p + (min(j + (uint32_t)r * 64u, last) << 2));
     uint32_t word[U], bit[U];
 #pragma unroll
     for (int r = 0; r < U; ++r) {
-        bit[r] = bbit(w[r], bits);
+        bit[r] = bbit(tid(w[r], tc), bits);
         word[r] = bf[bit[r] >> 5];
     }
     keep = 0;  // branch-free: in range and pre-filter bit set
@@ -362,8 +368,7 @@ __device__ __forceinline__ void list_pass(const uint32_t* __restrict__ tg, const
 }
 
 template <bool LISTS, int U>  // LISTS: the wave walks each out(v) with all lanes (as k_tri_big_items<true>)
-__global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restrict__ tg,
-                                                         const uint16_t* __restrict__ tg16, int64_t hot_end,
+__global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restrict__ tg, TgCode tc,
                                                          const int64_t* __restrict__ ov,
                                                          const int64_t* __restrict__ off, int vmt,
                                                          const int64_t* __restrict__ us, int64_t nu,
@@ -384,7 +389,7 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
         __builtin_amdgcn_wave_barrier();
         uint32_t dv = 0;
         if (lane < d) {
-            const uint32_t v = tg[b + lane];
+            const uint32_t v = tid(tg[b + lane], tc);
             const uint64_t pv = (uint64_t)ov[b + lane];
             const int64_t vo = off[v];
             dv = (uint32_t)(off[v + 1] - vo);
@@ -393,7 +398,7 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
             W.vp[lane] = pv;
             W.voff[lane] = vo;
             W.dv[lane] = dv;
-            hinsert(W.hk, W.hi, 9, v, (uint32_t)lane);
+            hinsert(W.hk, W.hi, 9, v, v, (uint32_t)lane);
             bset(W.bf, kSmallBloomBits, v);
         }
         uint32_t x = dv;  // wave inclusive scan of the out-degrees of the v's
@@ -414,16 +419,12 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
                 const uint64_t puv = W.vp[k];
                 for (int j0 = lane; j0 < (int)dvk; j0 += U * 64) {
                     uint32_t w[U], keep;  // U target loads in flight per lane
-                    list_pass<U>(tg, tg16, hot_end, vo, (int)dvk, j0, W.bf, kSmallBloomBits, w, keep);
+                    list_pass<U>(tg, tc, vo, (int)dvk, j0, W.bf, kSmallBloomBits, w, keep);
 #pragma unroll
                     for (int r = 0; r < U; ++r) {
                         if (!((keep >> r) & 1u)) continue;
-                        const int sl = hfind(W.hk, 9, w[r]);
-#if CAPSMI_TRI_DIAG
-                        if (sl >= 0) acc += 1;
-#else
-                        if (sl >= 0) acc += tri_weight(puv, (uint64_t)ov[vo + j0 + r * 64], W.vp[W.hi[sl]]);
-#endif
+                        const int sl = hfind(W.hk, 9, tid(w[r], tc), ~0u);
+                        if (sl >= 0) acc += tri_weight(puv, tpay(w[r], tc, ov, vo + j0 + r * 64), W.vp[W.hi[sl]]);
                     }
                 }
             }
@@ -450,12 +451,12 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
                 }
                 ii[k] = i;
                 pos[k] = base + f;
-                w[k] = f < total ? target(tg, tg16, hot_end, pos[k]) : kEmpty;
+                w[k] = f < total ? tid(tg[pos[k]], tc) : kEmpty;
             }
 #pragma unroll
             for (int k = 0; k < kWedgeUnroll; ++k) {
                 if (w[k] == kEmpty || !btest(W.bf, kSmallBloomBits, w[k])) continue;
-                const int sl = hfind(W.hk, 9, w[k]);
+                const int sl = hfind(W.hk, 9, w[k], ~0u);
                 if (sl >= 0) acc += tri_weight(W.vp[ii[k]], (uint64_t)ov[pos[k]], W.vp[W.hi[sl]]);
             }
         }
@@ -547,8 +548,7 @@ __global__ void k_tri_item_map(const int64_t* __restrict__ ipre, int64_t nu, uin
 // out(u) for the in-neighbours u of v with od(u) <= od(v).  Otherwise (u-mode) c = u and the walked
 // lists are out(v) for v in out(u), less the edges v-mode takes (vmt > 0: od(v) >= vmt, od(u) <= od(v)).
 template <bool LISTS, int U, bool VM>
-__global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __restrict__ tg,
-                                                             const uint16_t* __restrict__ tg16, int64_t hot_end,
+__global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __restrict__ tg, TgCode tc,
                                                              const int64_t* __restrict__ ov,
                                                              const int64_t* __restrict__ off,
                                                              const int64_t* __restrict__ ioff,
@@ -583,12 +583,12 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
         for (int k = threadIdx.x; k < (1 << kBigBloomBits) / 32; k += kBigBlock) L.bf[k] = 0;
         __syncthreads();
         for (int k = threadIdx.x; k < hn; k += kBigBlock) {
-            const uint32_t w = tg[b + h0 + k];
-            hinsert(L.hk, L.hi, 13, w, (uint32_t)k);
+            const uint32_t word = tg[b + h0 + k], w = tid(word, tc);
+            hinsert(L.hk, L.hi, 13, w, word, (uint32_t)k);
             bset(L.bf, kBigBloomBits, w);
         }
         for (int k = threadIdx.x; k < vn; k += kBigBlock) {
-            const uint32_t v = VM ? itg[nb + v0 + k] : tg[b + v0 + k];
+            const uint32_t v = VM ? itg[nb + v0 + k] : tid(tg[b + v0 + k], tc);
             const int64_t vo = off[v];
             const uint32_t dv = (uint32_t)(off[v + 1] - vo);
             const int64_t e = VM ? iov[nb + v0 + k] : b + v0 + k;  // the edge u -> v either way
@@ -609,18 +609,15 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
                 const uint64_t puv = L.vp[k];
                 for (int j0 = lane; j0 < (int)dv; j0 += U * 64) {
                     uint32_t w[U], keep;  // U target loads in flight per lane
-                    list_pass<U>(tg, tg16, hot_end, vo, (int)dv, j0, L.bf, kBigBloomBits, w, keep);
+                    list_pass<U>(tg, tc, vo, (int)dv, j0, L.bf, kBigBloomBits, w, keep);
 #pragma unroll
                     for (int r = 0; r < U; ++r) {
                         if (!((keep >> r) & 1u)) continue;
-                        const int sl = hfind(L.hk, 13, w[r]);
+                        const int sl = hfind(L.hk, 13, tid(w[r], tc), tc.idmask());
                         if (sl >= 0) {
-#if CAPSMI_TRI_DIAG  // timing diagnostic only (wrong counts): hits without their payload loads
-                            acc += 1;
-#else
-                            const uint64_t pxw = (uint64_t)ov[vo + j0 + r * 64], pcw = (uint64_t)ov[b + h0 + L.hi[sl]];
+                            const uint64_t pxw = tpay(w[r], tc, ov, vo + j0 + r * 64);
+                            const uint64_t pcw = tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]);
                             acc += VM ? tri_weight(puv, pcw, pxw) : tri_weight(puv, pxw, pcw);
-#endif
                         }
                     }
                 }
@@ -647,12 +644,12 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
                 }
                 ii[k] = i;
                 pos[k] = base + f;
-                w[k] = f < tw ? target(tg, tg16, hot_end, pos[k]) : kEmpty;
+                w[k] = f < tw ? tid(tg[pos[k]], tc) : kEmpty;
             }
 #pragma unroll
             for (int k = 0; k < kWedgeUnroll; ++k) {
                 if (w[k] == kEmpty || !btest(L.bf, kBigBloomBits, w[k])) continue;
-                const int sl = hfind(L.hk, 13, w[k]);
+                const int sl = hfind(L.hk, 13, w[k], tc.idmask());
                 if (sl >= 0) acc += tri_weight(L.vp[ii[k]], (uint64_t)ov[pos[k]], (uint64_t)ov[b + h0 + L.hi[sl]]);
             }
         }
@@ -675,6 +672,17 @@ __global__ void k_tri_bins(const int64_t* __restrict__ off, int64_t n, uint8_t* 
 __global__ void k_targets(const uint64_t* __restrict__ ok_, int64_t ne, uint32_t* __restrict__ tg) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x)
         tg[i] = (uint32_t)ok_[i];
+}
+
+// coded targets: to | min(m(from,to), cmask) << ib | min(m(to,from), cmask) << (ib + cb)
+__global__ void k_targets_coded(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ ov, int64_t ne, TgCode tc,
+                                uint32_t* __restrict__ tg) {
+    const uint64_t cm = tc.cmask();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t p = (uint64_t)ov[i];
+        const uint32_t f = (uint32_t)min(p >> 32, cm), b = (uint32_t)min(p & 0xffffffffULL, cm);
+        tg[i] = (uint32_t)ok_[i] | (tc.cb ? f << tc.ib | b << (tc.ib + tc.cb) : 0u);
+    }
 }
 
 // pair and self terms
@@ -801,15 +809,11 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     g.off = dev_alloc(sizeof(int64_t) * (n + 1), s);
     hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, n, P<int64_t>(g.off));
     g.tg = dev_alloc(sizeof(uint32_t) * (ne > 0 ? ne : 1), s);
+    g.ib = bits;
+    g.cb = std::min(4, (32 - bits) / 2);
     if (ne > 0)
-        hipLaunchKernelGGL(k_targets, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, P<uint32_t>(g.tg));
-    // the hub prefix: out-lists of vertices 0 .. 2^16 - 1, whose targets are smaller ids, as uint16
-    const int64_t nhub = std::min<int64_t>(n, int64_t(1) << 16);
-    g.hot_end = read_scalar(s, P<int64_t>(g.off) + nhub);
-    g.tg16 = dev_alloc(sizeof(uint16_t) * (g.hot_end > 0 ? g.hot_end : 1), s);
-    if (g.hot_end > 0)
-        hipLaunchKernelGGL(k_targets16, dim3(grid(s, g.hot_end)), dim3(256), 0, st, P<uint32_t>(g.tg), g.hot_end,
-                           P<uint16_t>(g.tg16));
+        hipLaunchKernelGGL(k_targets_coded, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.ov), ne,
+                           TgCode{(uint32_t)g.ib, (uint32_t)g.cb}, P<uint32_t>(g.tg));
     // in-lists and v-mode centers (CAPSMI_TRI_VMODE_T: the od(v) threshold; 0 = every edge from u)
     const char* vt = getenv("CAPSMI_TRI_VMODE_T");
     g.vmt = vt ? atoi(vt) : 256;
@@ -853,6 +857,7 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
         const int64_t sb = g.nsmall * part / nparts, se = g.nsmall * (part + 1) / nparts;
         const int64_t bb = g.nbig * part / nparts, be = g.nbig * (part + 1) / nparts;
         const int64_t vb = g.nvm * part / nparts, ve = g.nvm * (part + 1) / nparts;
+        const TgCode tc{(uint32_t)g.ib, (uint32_t)g.cb};
         const char* walk = getenv("CAPSMI_TRI_WALK");  // "flat": the prefix-sum walk (A/B runs)
         const bool lists = !(walk && std::string(walk) == "flat");
         const char* ue = getenv("CAPSMI_TRI_UNROLL");  // target loads in flight per lane: 4 (default), 8 or 16
@@ -880,7 +885,7 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
             HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kf), hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)lds));
             hipLaunchKernelGGL(kf, dim3((unsigned)(s->num_cus * 4)), dim3(kBigBlock), lds, st,
-                               P<uint32_t>(g.tg), P<uint16_t>(g.tg16), g.hot_end, P<int64_t>(g.ov), P<int64_t>(g.off),
+                               P<uint32_t>(g.tg), tc, P<int64_t>(g.ov), P<int64_t>(g.off),
                                P<int64_t>(g.ioff), P<uint32_t>(g.itg), P<int64_t>(g.iov), g.vmt, cs, nc, ipre,
                                P<uint32_t>(iq), P<unsigned long long>(ctr), P<unsigned long long>(out));
         };
@@ -892,8 +897,7 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
                        : un == 16 ? k_tri_small<true, 16>
                        : un == 8 ? k_tri_small<true, 8> : k_tri_small<true, 4>;
             hipLaunchKernelGGL(kfs, dim3((unsigned)gs), dim3(kTriBlock), 0, st,
-                               P<uint32_t>(g.tg),
-                               P<uint16_t>(g.tg16), g.hot_end, P<int64_t>(g.ov), P<int64_t>(g.off), g.vmt,
+                               P<uint32_t>(g.tg), tc, P<int64_t>(g.ov), P<int64_t>(g.off), g.vmt,
                                P<int64_t>(g.small_u) + sb, se - sb,
                                P<unsigned long long>(out));
         }
