@@ -14,6 +14,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "../../include/capsmi.h"
@@ -327,6 +328,10 @@ void radix_sort_pairs(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t 
 // the same over an explicit list of 8-bit digit positions (LSD order; digits no key uses skipped);
 // vals may be null (keys only)
 void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, const std::vector<int>& shifts);
+// the same, calling cb(keys as they stand) on the stream after the first `at` passes (an intermediate
+// order, e.g. by the low digits alone; cb(keys) at once when nothing is sorted)
+void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, const std::vector<int>& shifts,
+                       int at, const std::function<void(const uint64_t*)>& cb);
 void order_keys(capsmi_session* s, const int64_t* col, const uint8_t* valid, int type, bool desc, bool null_pass,
                 const int64_t* perm, int64_t n, uint64_t* key);
 
@@ -382,10 +387,10 @@ struct TriGraph {
     // Direction choice per oriented edge u -> v at position p of out(u) (out-lists are sorted, and
     // every wedge u -> v -> w that can close has w < v, so from v only the prefix out(u)[0, p) needs
     // walking; from u the whole out(v)): with vmt > 0 the edges with od(v) >= vmt and p < od(v) are
-    // taken from v ("v-mode"), over the in-lists (ioff, itg, iov: sources and oriented-edge indexes
-    // grouped by target, so p = iov - off[u] and the payload is ov[iov]); vm_c = the v-mode centers.
+    // taken from v ("v-mode"), over the in-lists (ioff, itg, ipos: sources and positions p of the
+    // oriented edges grouped by target; the edge is off[u] + p); vm_c = the v-mode centers.
     int vmt = 0;
-    Buf ioff, itg, iov, vm_c;
+    Buf ioff, itg, ipos, vm_c;
     int64_t nvm = 0;
 };
 void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,

@@ -18,6 +18,8 @@
 
 #include "capsmi_impl.h"
 
+#include <functional>
+
 namespace capsmi {
 
 namespace {
@@ -179,7 +181,8 @@ __global__ void __launch_bounds__(B) k_scatter(const uint64_t* __restrict__ keys
 }
 
 template <int B, int IT>
-void sort_passes(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, const std::vector<int>& shifts) {
+void sort_passes(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, const std::vector<int>& shifts,
+                 int at, const std::function<void(const uint64_t*)>& cb) {
     constexpr int T = B * IT;
     static std::once_flag once;  // the staged tile takes more than 64 KiB of LDS
     std::call_once(once, [] {
@@ -210,6 +213,7 @@ void sort_passes(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, co
         std::swap(ki, ko);
         std::swap(vi, vo);
         ++passes;
+        if (passes == at && cb) cb(ki);
     }
     if (passes & 1) {
         HIP_CHECK(hipMemcpyAsync(keys, ki, sizeof(uint64_t) * n, hipMemcpyDeviceToDevice, st));
@@ -230,13 +234,21 @@ void radix_sort_pairs(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t 
 // output arrays (C4 at s=24, 2^28 pairs: 2.4-3.3 -> 1.6-2.5 ms per pass).  Key-only sorts and
 // smaller ones use 4096-key tiles (two 512-lane blocks per CU): a 2^28-key pass takes 1.19 ms
 // there against 1.4 ms with the larger tile.  CAPSMI_SORT_TILE=4096|12288|16384 forces one.
-void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, const std::vector<int>& shifts) {
-    if (n <= 1 || shifts.empty()) return;
+void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, const std::vector<int>& shifts,
+                       int at, const std::function<void(const uint64_t*)>& cb) {
+    if (n <= 1 || shifts.empty()) {
+        if (cb) cb(keys);
+        return;
+    }
     static const int forced = getenv("CAPSMI_SORT_TILE") ? atoi(getenv("CAPSMI_SORT_TILE")) : 0;  // A/B runs
     const int tile = forced ? forced : (vals && n >= (int64_t(1024) * 12288)) ? 12288 : 4096;
-    if (tile == 12288) sort_passes<1024, 12>(s, keys, vals, n, shifts);
-    else if (tile == 16384) sort_passes<1024, 16>(s, keys, vals, n, shifts);
-    else sort_passes<512, 8>(s, keys, vals, n, shifts);
+    if (tile == 12288) sort_passes<1024, 12>(s, keys, vals, n, shifts, at, cb);
+    else if (tile == 16384) sort_passes<1024, 16>(s, keys, vals, n, shifts, at, cb);
+    else sort_passes<512, 8>(s, keys, vals, n, shifts, at, cb);
+}
+
+void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, const std::vector<int>& shifts) {
+    radix_sort_digits(s, keys, vals, n, shifts, 0, nullptr);
 }
 
 }  // namespace capsmi

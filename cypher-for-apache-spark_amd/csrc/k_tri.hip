@@ -64,8 +64,12 @@ __global__ void k_first_none(const uint64_t* __restrict__ k, int64_t m, int64_t*
     *out = a;
 }
 
-// undirected runs -> (key min<<32|max, payload m(min,max)<<32 | m(max,min)), degrees.  The runs are
-// sorted by their lower end, so a wave's lanes with the same lower end are contiguous: one atomic
+// undirected runs -> (key min<<32|max, payload m(min,max)<<32 | m(max,min)), and the lower ends'
+// degrees.  The degree that orders the vertices is the relationship count (multi-edges counted, loops
+// not): any total order gives the same count, and this one is a sum over sorted keys on both sides
+// (k_deg_max counts the upper ends over the keys sorted by max), where the simple-graph degree needed
+// one random atomic per undirected edge at its upper end (~8 of k_und_runs' 11 ms at C4).  The runs
+// are sorted by their lower end, so a wave's lanes with the same lower end are contiguous: one atomic
 // per such segment (hubs would otherwise serialise hundreds of thousands of adds on one counter).
 // A run longer than kShortRun (multi-edges between two hubs, up to ~10^4 at C4) is not walked by
 // its lane, which would hold its wave for the whole walk: it goes to a list that k_und_long counts
@@ -85,8 +89,10 @@ __global__ void k_und_runs(const uint64_t* __restrict__ k, const int64_t* __rest
         const int64_t r = r0 + lane;
         const bool act = r < nruns;  // the active lanes are a prefix of the wave
         uint32_t mn = 0;
+        int64_t h = 0, h2 = 0;
         if (act) {
-            const int64_t h = heads[r], h2 = r + 1 < nruns ? heads[r + 1] : nvalid;
+            h = heads[r];
+            h2 = r + 1 < nruns ? heads[r + 1] : nvalid;
             const uint64_t key = k[h];
             mn = (uint32_t)(key >> 32);
             const uint32_t mx = msh ? ((uint32_t)key >> 1) : ((uint32_t)key & 0x7FFFFFFFu);
@@ -98,16 +104,35 @@ __global__ void k_und_runs(const uint64_t* __restrict__ k, const int64_t* __rest
             } else {
                 longr[atomicAdd(nlong, 1ull)] = r;
             }
-            atomicAdd(&deg[mx], 1u);
         }
         const uint32_t prev = __shfl_up(mn, 1, 64);
         const bool head = act && (lane == 0 || prev != mn);
         const unsigned long long hb = __ballot(head), am = __ballot(act);
-        if (head) {
-            const unsigned long long later = lane == 63 ? 0ULL : hb >> (lane + 1);
-            const int next = later ? lane + 1 + __builtin_ctzll(later) : __popcll(am);
-            atomicAdd(&deg[mn], (uint32_t)(next - lane));
+        const unsigned long long later = lane == 63 ? 0ULL : hb >> (lane + 1);
+        const int next = later ? lane + 1 + __builtin_ctzll(later) : __popcll(am);
+        const int64_t seg_end = __shfl(h2, head ? next - 1 : lane, 64);  // end of the segment's last run
+        if (head) atomicAdd(&deg[mn], (uint32_t)(seg_end - h));
+    }
+}
+
+// upper-end degrees over the undirected keys sorted by their upper end (the max digits' passes of
+// the key sort): consecutive lanes with the same end add once (dropped keys are segments of their own)
+__global__ void k_deg_max(const uint64_t* __restrict__ k, int64_t m, int msh, uint32_t* __restrict__ deg) {
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < m; i0 += stride) {  // wave-uniform
+        const int64_t i = i0 + lane;
+        uint32_t mx = 0xFFFFFFFFu;  // no valid key has it (ids < 2^31)
+        if (i < m) {
+            const uint64_t key = k[i];
+            if (key != kNone) mx = msh ? ((uint32_t)key >> 1) : ((uint32_t)key & 0x7FFFFFFFu);
         }
+        const uint32_t prev = __shfl_up(mx, 1, 64);
+        const bool head = lane == 0 || prev != mx;
+        const unsigned long long hb = __ballot(head);
+        const unsigned long long later = lane == 63 ? 0ULL : hb >> (lane + 1);
+        const int next = later ? lane + 1 + __builtin_ctzll(later) : 64;
+        if (head && mx != 0xFFFFFFFFu) atomicAdd(&deg[mx], (uint32_t)(next - lane));
     }
 }
 
@@ -153,33 +178,109 @@ __global__ void k_rank_ids(const int64_t* __restrict__ by_order, int64_t n, uint
     }
 }
 
+struct TgCode {
+    uint32_t ib, cb;  // id bits, code bits per direction (0: every payload is an exception)
+    __host__ __device__ uint32_t idmask() const { return ib >= 32 ? ~0u : (1u << ib) - 1u; }
+    __host__ __device__ uint32_t cmask() const { return (1u << cb) - 1u; }
+};
+
 // orient each undirected edge from the lower (degree, id) end -- towards the smaller degree-order id;
-// key = rid(from)<<32 | rid(to), payload = m(from,to)<<32 | m(to,from)
+// key = rid(from)<<32 | rid(to), payload = m(from,to)<<32 | m(to,from).
+// Coded (tc.cb > 0): the key's low word is the coded target word (multiplicities above the id, outside
+// every sorted digit, so a key-only sort carries them), and only the exceptions' exact payloads are
+// kept, appended as (key, payload) to exc (one atomic per wave) and placed after the sort (k_exc_place).
+// Uncoded: the payload goes to ov[i], sorted along as the value.
 __global__ void k_orient(const uint64_t* __restrict__ ek, const int64_t* __restrict__ ev, int64_t ne,
-                         const uint32_t* __restrict__ rid, uint64_t* __restrict__ ok_, int64_t* __restrict__ ov) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t x = (uint32_t)(ek[i] >> 32), y = (uint32_t)ek[i];
-        const uint64_t v = (uint64_t)ev[i];
-        const uint32_t mxy = (uint32_t)(v >> 32), myx = (uint32_t)v;
-        const uint32_t rx = rid[x], ry = rid[y];
-        if (rx > ry) {  // x is lower in (degree, id)
-            ok_[i] = ((uint64_t)rx << 32) | ry;
-            ov[i] = (int64_t)(((uint64_t)mxy << 32) | myx);
-        } else {
-            ok_[i] = ((uint64_t)ry << 32) | rx;
-            ov[i] = (int64_t)(((uint64_t)myx << 32) | mxy);
+                         const uint32_t* __restrict__ rid, TgCode tc, uint64_t* __restrict__ ok_,
+                         int64_t* __restrict__ ov, uint64_t* __restrict__ exc, unsigned long long* __restrict__ nexc) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t cm = tc.cmask();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < ne; i0 += stride) {  // wave-uniform
+        const int64_t i = i0 + lane;
+        bool ex = false;
+        uint64_t key = 0, pay = 0;
+        if (i < ne) {
+            const uint32_t x = (uint32_t)(ek[i] >> 32), y = (uint32_t)ek[i];
+            const uint64_t v = (uint64_t)ev[i];
+            const uint32_t mxy = (uint32_t)(v >> 32), myx = (uint32_t)v;
+            const uint32_t rx = rid[x], ry = rid[y];
+            const bool xf = rx > ry;  // x is lower in (degree, id)
+            const uint32_t f = xf ? mxy : myx, b = xf ? myx : mxy;
+            key = xf ? ((uint64_t)rx << 32) | ry : ((uint64_t)ry << 32) | rx;
+            pay = ((uint64_t)f << 32) | b;
+            if (tc.cb) {
+                key |= (uint64_t)(min(f, cm) << tc.ib | min(b, cm) << (tc.ib + tc.cb));
+                ex = f >= cm || b >= cm;
+            } else {
+                ov[i] = (int64_t)pay;
+            }
+            ok_[i] = key;
+        }
+        const unsigned long long eb = __ballot(ex);
+        if (eb) {  // wave-uniform
+            unsigned long long base = 0;
+            if (lane == __builtin_ctzll(eb)) base = atomicAdd(nexc, (unsigned long long)__popcll(eb));
+            base = __shfl(base, __builtin_ctzll(eb), 64);
+            if (ex) {
+                const unsigned long long at = base + __popcll(eb & ((1ULL << lane) - 1));
+                exc[2 * at] = key;
+                exc[2 * at + 1] = pay;
+            }
         }
     }
 }
 
-// in-lists: oriented keys (from << 32 | to) swapped to (to << 32 | from), the oriented edge's index
-// alongside (its position in out(from) bounds the v-mode walk; its payload is read through it)
-__global__ void k_swap_keys(const uint64_t* __restrict__ ok_, int64_t ne, uint64_t* __restrict__ ik,
-                            int64_t* __restrict__ iv) {
+// exceptions' exact payloads into ov at their keys' positions in the sorted oriented keys: (from, to)
+// is unique and the keys are in (from, to) order -- not in 64-bit order, the unsorted multiplicity bits
+// lying above `to`, so they are masked off for the search
+__global__ void k_exc_place(const uint64_t* __restrict__ exc, const unsigned long long* __restrict__ nexc,
+                            const uint64_t* __restrict__ ok_, int64_t ne, TgCode tc, int64_t* __restrict__ ov) {
+    const int64_t cnt = (int64_t)*nexc;
+    const uint64_t km = ~((((uint64_t)1 << (2 * tc.cb)) - 1) << tc.ib);
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < cnt; j += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t key = exc[2 * j] & km;
+        int64_t lo = 0, hi = ne;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((ok_[mid] & km) < key) lo = mid + 1; else hi = mid;
+        }
+        ov[lo] = (int64_t)exc[2 * j + 1];
+    }
+}
+
+// in-lists: the oriented edge's position in out(from) bounds the v-mode walk (and locates its payload).
+// Packed (iv == nullptr; ids of <= 24 bits, positions < 2^16): key = to << (ib + 16) | from << 16 | pos,
+// sorted on the digits of `to` alone.  Otherwise key = to << 32 | from with the edge index as the value.
+__global__ void k_swap_keys(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ off, int64_t ne, TgCode tc,
+                            uint64_t* __restrict__ ik, int64_t* __restrict__ iv) {
+    const uint32_t idm = tc.idmask();
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t k = ok_[i];
-        ik[i] = (k << 32) | (k >> 32);
-        iv[i] = i;
+        const uint64_t from = k >> 32, to = (uint32_t)k & idm;
+        if (iv) {
+            ik[i] = (to << 32) | from;
+            iv[i] = i;
+        } else {
+            ik[i] = (to << (tc.ib + 16)) | (from << 16) | (uint64_t)(i - off[from]);
+        }
+    }
+}
+
+// in-list sources and positions from the sorted in-keys (packed: both from the key; else pos = e - off[from])
+__global__ void k_in_split(const uint64_t* __restrict__ ik, const int64_t* __restrict__ iv, const int64_t* __restrict__ off,
+                           int64_t ne, TgCode tc, uint32_t* __restrict__ itg, uint32_t* __restrict__ ipos) {
+    const uint32_t idm = tc.idmask();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = ik[i];
+        if (iv) {
+            const uint32_t from = (uint32_t)k;
+            itg[i] = from;
+            ipos[i] = (uint32_t)(iv[i] - off[from]);
+        } else {
+            itg[i] = (uint32_t)(k >> 16) & idm;
+            ipos[i] = (uint32_t)(k & 0xFFFFu);
+        }
     }
 }
 
@@ -191,11 +292,11 @@ __global__ void k_tri_vm_bins(const int64_t* __restrict__ off, const int64_t* __
 }
 
 
-// CSR offsets of the oriented (sorted) edges: off[v] = first edge with source >= v
-__global__ void k_offsets(const uint64_t* __restrict__ ok_, int64_t ne, int64_t n, int64_t* __restrict__ off) {
+// CSR offsets of sorted keys whose group field starts at bit `sh`: off[v] = first key with field >= v
+__global__ void k_offsets(const uint64_t* __restrict__ ok_, int64_t ne, int64_t n, int sh, int64_t* __restrict__ off) {
     for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= n; v += (int64_t)gridDim.x * blockDim.x) {
         int64_t lo = 0, hi = ne;
-        const uint64_t target = (uint64_t)v << 32;
+        const uint64_t target = (uint64_t)v << sh;
         while (lo < hi) {
             const int64_t mid = (lo + hi) >> 1;
             if (ok_[mid] < target) lo = mid + 1; else hi = mid;
@@ -264,16 +365,12 @@ __device__ __forceinline__ bool btest(const uint32_t* bf, int bits, uint32_t w) 
 // alone (a hit used to cost two dependent 8-byte payload loads: 47 of the 116 ms at C4, measured by a
 // run with the loads removed).  With 2^24 ids, cb = 4: < 1 % of the hits need an exact payload (R-MAT
 // s = 20 / 22, hits whose edges carry a multiplicity >= 15).
-struct TgCode {
-    uint32_t ib, cb;  // id bits, code bits per direction (0: every payload is an exception)
-    __host__ __device__ uint32_t idmask() const { return ib >= 32 ? ~0u : (1u << ib) - 1u; }
-    __host__ __device__ uint32_t cmask() const { return (1u << cb) - 1u; }
-};
 
 __device__ __forceinline__ uint32_t tid(uint32_t word, TgCode c) { return word & c.idmask(); }
 
 // payload (f << 32 | b) of a coded word, or the exact one at ov[pos] for an exception
 __device__ __forceinline__ uint64_t tpay(uint32_t word, TgCode c, const int64_t* __restrict__ ov, int64_t pos) {
+    if (c.cb == 0) return (uint64_t)ov[pos];
     const uint32_t f = (word >> c.ib) & c.cmask(), b = (word >> (c.ib + c.cb)) & c.cmask();
     if (f == c.cmask() || b == c.cmask()) return (uint64_t)ov[pos];
     return (uint64_t)f << 32 | b;
@@ -390,7 +487,7 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
         uint32_t dv = 0;
         if (lane < d) {
             const uint32_t v = tid(tg[b + lane], tc);
-            const uint64_t pv = (uint64_t)ov[b + lane];
+            const uint64_t pv = tpay(tg[b + lane], tc, ov, b + lane);
             const int64_t vo = off[v];
             dv = (uint32_t)(off[v + 1] - vo);
             if (vmt > 0 && dv >= (uint32_t)vmt && (uint32_t)lane < dv) dv = 0;  // v-mode takes u -> v
@@ -457,7 +554,7 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
             for (int k = 0; k < kWedgeUnroll; ++k) {
                 if (w[k] == kEmpty || !btest(W.bf, kSmallBloomBits, w[k])) continue;
                 const int sl = hfind(W.hk, 9, w[k], ~0u);
-                if (sl >= 0) acc += tri_weight(W.vp[ii[k]], (uint64_t)ov[pos[k]], W.vp[W.hi[sl]]);
+                if (sl >= 0) acc += tri_weight(W.vp[ii[k]], tpay(tg[pos[k]], tc, ov, pos[k]), W.vp[W.hi[sl]]);
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -553,7 +650,7 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
                                                              const int64_t* __restrict__ off,
                                                              const int64_t* __restrict__ ioff,
                                                              const uint32_t* __restrict__ itg,
-                                                             const int64_t* __restrict__ iov, int vmt,
+                                                             const uint32_t* __restrict__ ipos, int vmt,
                                                              const int64_t* __restrict__ us, int64_t nu,
                                                              const int64_t* __restrict__ ipre,
                                                              const uint32_t* __restrict__ item_q,
@@ -591,9 +688,9 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
             const uint32_t v = VM ? itg[nb + v0 + k] : tid(tg[b + v0 + k], tc);
             const int64_t vo = off[v];
             const uint32_t dv = (uint32_t)(off[v + 1] - vo);
-            const int64_t e = VM ? iov[nb + v0 + k] : b + v0 + k;  // the edge u -> v either way
+            const int64_t e = VM ? vo + ipos[nb + v0 + k] : b + v0 + k;  // the edge u -> v either way
             L.vl[k] = v;
-            L.vp[k] = (uint64_t)ov[e];
+            L.vp[k] = tpay(tg[e], tc, ov, e);
             L.voff[k] = vo;
             // v-mode walks out(u) below the center: the prefix [0, p) of out(u), p = position of the
             // edge; u-mode skips the edges v-mode takes (od(v) >= vmt and p < od(v))
@@ -650,7 +747,8 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
             for (int k = 0; k < kWedgeUnroll; ++k) {
                 if (w[k] == kEmpty || !btest(L.bf, kBigBloomBits, w[k])) continue;
                 const int sl = hfind(L.hk, 13, w[k], tc.idmask());
-                if (sl >= 0) acc += tri_weight(L.vp[ii[k]], (uint64_t)ov[pos[k]], (uint64_t)ov[b + h0 + L.hi[sl]]);
+                if (sl >= 0)
+                    acc += tri_weight(L.vp[ii[k]], tpay(tg[pos[k]], tc, ov, pos[k]), tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]));
             }
         }
         __syncthreads();
@@ -674,16 +772,6 @@ __global__ void k_targets(const uint64_t* __restrict__ ok_, int64_t ne, uint32_t
         tg[i] = (uint32_t)ok_[i];
 }
 
-// coded targets: to | min(m(from,to), cmask) << ib | min(m(to,from), cmask) << (ib + cb)
-__global__ void k_targets_coded(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ ov, int64_t ne, TgCode tc,
-                                uint32_t* __restrict__ tg) {
-    const uint64_t cm = tc.cmask();
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t p = (uint64_t)ov[i];
-        const uint32_t f = (uint32_t)min(p >> 32, cm), b = (uint32_t)min(p & 0xffffffffULL, cm);
-        tg[i] = (uint32_t)ok_[i] | (tc.cb ? f << tc.ib | b << (tc.ib + tc.cb) : 0u);
-    }
-}
 
 // pair and self terms
 __global__ void k_pair_terms(const uint64_t* __restrict__ ek, const int64_t* __restrict__ ev, int64_t ne,
@@ -752,11 +840,18 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
             off += ms[i];
         }
     }
-    // one sort of the undirected keys: digits of max (and the direction bit when msh) then of min
+    // one sort of the undirected keys: digits of max (and the direction bit when msh) then of min; the
+    // upper ends' degrees are counted between the two halves, while the keys are in max order
+    Buf deg = dev_alloc(sizeof(uint32_t) * n, s);
+    HIP_CHECK(hipMemsetAsync(P<void>(deg), 0, sizeof(uint32_t) * n, st));
     std::vector<int> kd;
     for (int sh = 0; sh < bits + msh; sh += 8) kd.push_back(sh);
+    const int nmax = (int)kd.size();
     for (int sh = 32; sh < 32 + bits; sh += 8) kd.push_back(sh);
-    radix_sort_digits(s, P<uint64_t>(key), nullptr, m, kd);
+    radix_sort_digits(s, P<uint64_t>(key), nullptr, m, kd, nmax, [&](const uint64_t* kmax) {
+        if (m > 0)
+            hipLaunchKernelGGL(k_deg_max, dim3(grid(s, m)), dim3(256), 0, st, kmax, m, msh, P<uint32_t>(deg));
+    });
     const uint64_t dmask = msh ? ~1ULL : ~(1ULL << 31);
     Buf f = dev_alloc(m > 0 ? m : 1, s), heads;
     hipLaunchKernelGGL(k_heads, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, dmask, P<uint8_t>(f));
@@ -769,8 +864,6 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     g.ne = ne;
     g.ek = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), s);
     g.ev = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);
-    Buf deg = dev_alloc(sizeof(uint32_t) * n, s);
-    HIP_CHECK(hipMemsetAsync(P<void>(deg), 0, sizeof(uint32_t) * n, st));
     if (ne > 0) {
         Buf longr = dev_alloc(sizeof(int64_t) * (m / kShortRun + 1), s);
         hipLaunchKernelGGL(k_und_runs, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(key), P<int64_t>(heads), ne,
@@ -797,40 +890,56 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         hipLaunchKernelGGL(k_rank_ids, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(dv), n, P<uint32_t>(rid),
                            P<int64_t>(g.orig));
     }
+    // coded targets: the ids' sorted digits end at ib = 8 * ceil(bits / 8); with ib <= 24 the two
+    // 4-bit multiplicity fields fit above them
+    g.ib = (bits + 7) / 8 * 8;
+    g.cb = g.ib <= 24 ? 4 : 0;
+    const TgCode tc{(uint32_t)g.ib, (uint32_t)g.cb};
     g.ok = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), s);
-    g.ov = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);
+    g.ov = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);  // coded: written at the exceptions only
+    Buf exc = dev_alloc(tc.cb ? sizeof(uint64_t) * 2 * (ne > 0 ? ne : 1) : 8, s);
+    HIP_CHECK(hipMemsetAsync(P<void>(nv), 0, sizeof(int64_t) + sizeof(unsigned long long), st));  // nlong reused: nexc
     if (ne > 0)
         hipLaunchKernelGGL(k_orient, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ek), P<int64_t>(g.ev), ne,
-                           P<uint32_t>(rid), P<uint64_t>(g.ok), P<int64_t>(g.ov));
+                           P<uint32_t>(rid), tc, P<uint64_t>(g.ok), P<int64_t>(g.ov), P<uint64_t>(exc), nlong);
     std::vector<int> od;  // (source, target): grouped and target-sorted lists
     for (int sh = 0; sh < bits; sh += 8) od.push_back(sh);
     for (int sh = 32; sh < 32 + bits; sh += 8) od.push_back(sh);
-    radix_sort_digits(s, P<uint64_t>(g.ok), P<int64_t>(g.ov), ne, od);  // no kNone among the oriented keys
+    // no kNone among the oriented keys; coded: key-only (the payloads ride in the key)
+    radix_sort_digits(s, P<uint64_t>(g.ok), tc.cb ? nullptr : P<int64_t>(g.ov), ne, od);
+    if (tc.cb && ne > 0)
+        hipLaunchKernelGGL(k_exc_place, dim3(grid(s, ne / 64 + 1)), dim3(256), 0, st, P<uint64_t>(exc), nlong,
+                           P<uint64_t>(g.ok), ne, tc, P<int64_t>(g.ov));
+    exc.reset();
     g.off = dev_alloc(sizeof(int64_t) * (n + 1), s);
-    hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, n, P<int64_t>(g.off));
+    hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, n, 32, P<int64_t>(g.off));
     g.tg = dev_alloc(sizeof(uint32_t) * (ne > 0 ? ne : 1), s);
-    g.ib = bits;
-    g.cb = std::min(4, (32 - bits) / 2);
     if (ne > 0)
-        hipLaunchKernelGGL(k_targets_coded, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.ov), ne,
-                           TgCode{(uint32_t)g.ib, (uint32_t)g.cb}, P<uint32_t>(g.tg));
+        hipLaunchKernelGGL(k_targets, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, P<uint32_t>(g.tg));
     // in-lists and v-mode centers (CAPSMI_TRI_VMODE_T: the od(v) threshold; 0 = every edge from u)
     const char* vt = getenv("CAPSMI_TRI_VMODE_T");
     g.vmt = vt ? atoi(vt) : 256;
     if (g.vmt > 0 && ne > 0) {
-        Buf ik = dev_alloc(sizeof(uint64_t) * ne, s);
-        g.iov = dev_alloc(sizeof(int64_t) * ne, s);
-        hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, P<uint64_t>(ik),
-                           P<int64_t>(g.iov));
+        // packed in-keys (key-only sort) when ids and positions fit: od(u) <= sqrt(2m) under a degree
+        // order (every out-neighbour has at least u's degree), so m < 2^31 relationships bound it by 2^16
+        const bool packed = g.ib <= 24 && m < (int64_t(1) << 31);
+        const int tsh = packed ? g.ib + 16 : 32;
+        Buf ik = dev_alloc(sizeof(uint64_t) * ne, s), iv = packed ? Buf() : dev_alloc(sizeof(int64_t) * ne, s);
+        hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off), ne, tc,
+                           P<uint64_t>(ik), packed ? nullptr : P<int64_t>(iv));
         // by (to, from): the input is in (from, to) order and the LSD sort is stable, so the digits of
         // `to` alone give that order (3 passes at 2^24 ids instead of 6)
         std::vector<int> td;
-        for (int sh = 32; sh < 32 + bits; sh += 8) td.push_back(sh);
-        radix_sort_digits(s, P<uint64_t>(ik), P<int64_t>(g.iov), ne, td);
+        for (int sh = tsh; sh < tsh + bits; sh += 8) td.push_back(sh);
+        radix_sort_digits(s, P<uint64_t>(ik), packed ? nullptr : P<int64_t>(iv), ne, td);
         g.ioff = dev_alloc(sizeof(int64_t) * (n + 1), s);
-        hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), ne, n, P<int64_t>(g.ioff));
+        hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), ne, n, tsh,
+                           P<int64_t>(g.ioff));
         g.itg = dev_alloc(sizeof(uint32_t) * ne, s);
-        hipLaunchKernelGGL(k_targets, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(ik), ne, P<uint32_t>(g.itg));
+        g.ipos = dev_alloc(sizeof(uint32_t) * ne, s);
+        hipLaunchKernelGGL(k_in_split, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(ik),
+                           packed ? nullptr : P<int64_t>(iv), P<int64_t>(g.off), ne, tc, P<uint32_t>(g.itg),
+                           P<uint32_t>(g.ipos));
         Buf fvm = dev_alloc(n, s);
         hipLaunchKernelGGL(k_tri_vm_bins, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), P<int64_t>(g.ioff), n,
                            g.vmt, P<uint8_t>(fvm));
@@ -886,7 +995,7 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
                                           (int)lds));
             hipLaunchKernelGGL(kf, dim3((unsigned)(s->num_cus * 4)), dim3(kBigBlock), lds, st,
                                P<uint32_t>(g.tg), tc, P<int64_t>(g.ov), P<int64_t>(g.off),
-                               P<int64_t>(g.ioff), P<uint32_t>(g.itg), P<int64_t>(g.iov), g.vmt, cs, nc, ipre,
+                               P<int64_t>(g.ioff), P<uint32_t>(g.itg), P<uint32_t>(g.ipos), g.vmt, cs, nc, ipre,
                                P<uint32_t>(iq), P<unsigned long long>(ctr), P<unsigned long long>(out));
         };
         if (be > bb) run_items(P<int64_t>(g.big_u) + bb, be - bb, false);
