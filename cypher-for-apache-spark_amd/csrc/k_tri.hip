@@ -605,6 +605,10 @@ __device__ uint32_t big_scan(const uint32_t* in, uint32_t* outp, int n, uint32_t
 // Big u are split into work items (hash chunk of out(u), chunk of kVChunk v's of out(u)) so a hub's
 // wedges spread over many workgroups; items are taken from a global counter (dynamic balance).
 constexpr int kVChunk = 256;
+// neighbour chunks per item: the item builds its hash chunk once and walks up to kVGroup chunks of
+// lists against it (one chunk per item rebuilt the same hash for every 256 lists: at C4 the items'
+// setup without their walks took 12-13 ms of each launch)
+constexpr int kVGroup = 8;
 
 struct ItemLds {
     uint32_t bf[(1 << kBigBloomBits) / 32];
@@ -626,7 +630,7 @@ __global__ void k_tri_items(const int64_t* __restrict__ off, const int64_t* __re
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nu) return;
     const int64_t c = us[q], d = off[c + 1] - off[c], nd = ioff ? ioff[c + 1] - ioff[c] : d;
-    items[q] = ((d + kBigChunk - 1) / kBigChunk) * ((nd + kVChunk - 1) / kVChunk);
+    items[q] = ((d + kBigChunk - 1) / kBigChunk) * ((nd + kVChunk * kVGroup - 1) / (kVChunk * kVGroup));
 }
 
 // item -> its u's index q (items of q are [ipre[q], ipre[q+1])): one load per item instead of a
@@ -672,83 +676,88 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
         const int d = (int)(off[u + 1] - b);
         const int64_t nb = VM ? uniform64(ioff[u]) : b;   // its neighbour list: in(v) / out(u)
         const int nd = VM ? (int)(ioff[u + 1] - nb) : d;
-        const int nvc = (nd + kVChunk - 1) / kVChunk;
+        const int nvc = (nd + kVChunk - 1) / kVChunk, ngr = (nvc + kVGroup - 1) / kVGroup;
         const int local = (int)(it - ipre[lo]);
-        const int h0 = (local / nvc) * kBigChunk, v0 = (local % nvc) * kVChunk;
-        const int hn = min(kBigChunk, d - h0), vn = min(kVChunk, nd - v0);
-        for (int k = threadIdx.x; k < kBigSlots; k += kBigBlock) L.hk[k] = kEmpty;
+        const int h0 = (local / ngr) * kBigChunk, c0 = (local % ngr) * kVGroup, c1 = min(nvc, c0 + kVGroup);
+        const int hn = min(kBigChunk, d - h0);
+        int lc = 6;  // hash capacity 2^lc >= 4 hn (load <= 1/4), cleared as far as it is used
+        while ((1 << lc) < 4 * hn) ++lc;
+        for (int k = threadIdx.x; k < (1 << lc); k += kBigBlock) L.hk[k] = kEmpty;
         for (int k = threadIdx.x; k < (1 << kBigBloomBits) / 32; k += kBigBlock) L.bf[k] = 0;
         __syncthreads();
         for (int k = threadIdx.x; k < hn; k += kBigBlock) {
             const uint32_t word = tg[b + h0 + k], w = tid(word, tc);
-            hinsert(L.hk, L.hi, 13, w, word, (uint32_t)k);
+            hinsert(L.hk, L.hi, lc, w, word, (uint32_t)k);
             bset(L.bf, kBigBloomBits, w);
         }
-        for (int k = threadIdx.x; k < vn; k += kBigBlock) {
-            const uint32_t v = VM ? itg[nb + v0 + k] : tid(tg[b + v0 + k], tc);
-            const int64_t vo = off[v];
-            const uint32_t dv = (uint32_t)(off[v + 1] - vo);
-            const int64_t e = VM ? vo + ipos[nb + v0 + k] : b + v0 + k;  // the edge u -> v either way
-            L.vl[k] = v;
-            L.vp[k] = tpay(tg[e], tc, ov, e);
-            L.voff[k] = vo;
-            // v-mode walks out(u) below the center: the prefix [0, p) of out(u), p = position of the
-            // edge; u-mode skips the edges v-mode takes (od(v) >= vmt and p < od(v))
-            const uint32_t p = (uint32_t)(e - (VM ? vo : b));
-            L.dv[k] = VM ? (p < (uint32_t)d ? p : 0u) : (vmt > 0 && dv >= (uint32_t)vmt && p < dv ? 0u : dv);
-        }
-        __syncthreads();
-        if (LISTS) {
-            const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-            for (int k = wave; k < vn; k += kBigBlock / 64) {
-                const int64_t vo = uniform64(L.voff[k]);
-                const int64_t dv = (int64_t)__builtin_amdgcn_readfirstlane(L.dv[k]);
-                const uint64_t puv = L.vp[k];
-                for (int j0 = lane; j0 < (int)dv; j0 += U * 64) {
-                    uint32_t w[U], keep;  // U target loads in flight per lane
-                    list_pass<U>(tg, tc, vo, (int)dv, j0, L.bf, kBigBloomBits, w, keep);
+        for (int c = c0; c < c1; ++c) {  // block-uniform
+            const int v0 = c * kVChunk, vn = min(kVChunk, nd - v0);
+            if (c > c0) __syncthreads();  // the previous chunk's walks are done with the list table
+            for (int k = threadIdx.x; k < vn; k += kBigBlock) {
+                const uint32_t v = VM ? itg[nb + v0 + k] : tid(tg[b + v0 + k], tc);
+                const int64_t vo = off[v];
+                const uint32_t dv = (uint32_t)(off[v + 1] - vo);
+                const int64_t e = VM ? vo + ipos[nb + v0 + k] : b + v0 + k;  // the edge u -> v either way
+                L.vl[k] = v;
+                L.vp[k] = tpay(tg[e], tc, ov, e);
+                L.voff[k] = vo;
+                // v-mode walks out(u) below the center: the prefix [0, p) of out(u), p = position of the
+                // edge; u-mode skips the edges v-mode takes (od(v) >= vmt and p < od(v))
+                const uint32_t p = (uint32_t)(e - (VM ? vo : b));
+                L.dv[k] = VM ? (p < (uint32_t)d ? p : 0u) : (vmt > 0 && dv >= (uint32_t)vmt && p < dv ? 0u : dv);
+            }
+            __syncthreads();
+            if (LISTS) {
+                const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+                for (int k = wave; k < vn; k += kBigBlock / 64) {
+                    const int64_t vo = uniform64(L.voff[k]);
+                    const int64_t dv = (int64_t)__builtin_amdgcn_readfirstlane(L.dv[k]);
+                    const uint64_t puv = L.vp[k];
+                    for (int j0 = lane; j0 < (int)dv; j0 += U * 64) {
+                        uint32_t w[U], keep;  // U target loads in flight per lane
+                        list_pass<U>(tg, tc, vo, (int)dv, j0, L.bf, kBigBloomBits, w, keep);
 #pragma unroll
-                    for (int r = 0; r < U; ++r) {
-                        if (!((keep >> r) & 1u)) continue;
-                        const int sl = hfind(L.hk, 13, tid(w[r], tc), tc.idmask());
-                        if (sl >= 0) {
-                            const uint64_t pxw = tpay(w[r], tc, ov, vo + j0 + r * 64);
-                            const uint64_t pcw = tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]);
-                            acc += VM ? tri_weight(puv, pcw, pxw) : tri_weight(puv, pxw, pcw);
+                        for (int r = 0; r < U; ++r) {
+                            if (!((keep >> r) & 1u)) continue;
+                            const int sl = hfind(L.hk, lc, tid(w[r], tc), tc.idmask());
+                            if (sl >= 0) {
+                                const uint64_t pxw = tpay(w[r], tc, ov, vo + j0 + r * 64);
+                                const uint64_t pcw = tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]);
+                                acc += VM ? tri_weight(puv, pcw, pxw) : tri_weight(puv, pxw, pcw);
+                            }
                         }
                     }
                 }
+                continue;
             }
-            __syncthreads();
-            continue;
-        }
-        const uint32_t tw = big_scan(L.dv, L.pre, vn, L.wtot);
-        int i = 0;  // the lane's current v, as in k_tri_small
-        int64_t base = L.voff[0];
-        uint32_t nxt = vn > 1 ? L.pre[1] : 0xFFFFFFFFu;
-        for (uint32_t f0 = threadIdx.x; f0 < tw; f0 += kWedgeUnroll * kBigBlock) {
-            // kWedgeUnroll wedges per lane: all their target loads in flight before the probes
-            int ii[kWedgeUnroll];
-            int64_t pos[kWedgeUnroll];
-            uint32_t w[kWedgeUnroll];
+            const uint32_t tw = big_scan(L.dv, L.pre, vn, L.wtot);
+            int i = 0;  // the lane's current v, as in k_tri_small
+            int64_t base = L.voff[0];
+            uint32_t nxt = vn > 1 ? L.pre[1] : 0xFFFFFFFFu;
+            for (uint32_t f0 = threadIdx.x; f0 < tw; f0 += kWedgeUnroll * kBigBlock) {
+                // kWedgeUnroll wedges per lane: all their target loads in flight before the probes
+                int ii[kWedgeUnroll];
+                int64_t pos[kWedgeUnroll];
+                uint32_t w[kWedgeUnroll];
 #pragma unroll
-            for (int k = 0; k < kWedgeUnroll; ++k) {
-                const uint32_t f = f0 + k * kBigBlock;
-                if (f < tw && f >= nxt) {
-                    i = seg_from(L.pre, i + 1, vn, f);
-                    base = L.voff[i] - (int64_t)L.pre[i];
-                    nxt = i + 1 < vn ? L.pre[i + 1] : 0xFFFFFFFFu;
+                for (int k = 0; k < kWedgeUnroll; ++k) {
+                    const uint32_t f = f0 + k * kBigBlock;
+                    if (f < tw && f >= nxt) {
+                        i = seg_from(L.pre, i + 1, vn, f);
+                        base = L.voff[i] - (int64_t)L.pre[i];
+                        nxt = i + 1 < vn ? L.pre[i + 1] : 0xFFFFFFFFu;
+                    }
+                    ii[k] = i;
+                    pos[k] = base + f;
+                    w[k] = f < tw ? tid(tg[pos[k]], tc) : kEmpty;
                 }
-                ii[k] = i;
-                pos[k] = base + f;
-                w[k] = f < tw ? tid(tg[pos[k]], tc) : kEmpty;
-            }
 #pragma unroll
-            for (int k = 0; k < kWedgeUnroll; ++k) {
-                if (w[k] == kEmpty || !btest(L.bf, kBigBloomBits, w[k])) continue;
-                const int sl = hfind(L.hk, 13, w[k], tc.idmask());
-                if (sl >= 0)
-                    acc += tri_weight(L.vp[ii[k]], tpay(tg[pos[k]], tc, ov, pos[k]), tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]));
+                for (int k = 0; k < kWedgeUnroll; ++k) {
+                    if (w[k] == kEmpty || !btest(L.bf, kBigBloomBits, w[k])) continue;
+                    const int sl = hfind(L.hk, lc, w[k], tc.idmask());
+                    if (sl >= 0)
+                        acc += tri_weight(L.vp[ii[k]], tpay(tg[pos[k]], tc, ov, pos[k]), tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]));
+                }
             }
         }
         __syncthreads();
