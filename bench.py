@@ -572,7 +572,7 @@ SINGLE = {
 # timer name -> kernel symbol (rocprofv3 / PMC summary name) where they differ
 SINGLE_SYMBOL = {"direct_join_probe": "k_direct_probe", "radix_join_count": "k_join", "radix_join_write": "k_join",
                  "expand_filter": "k_expand_pairs", "part_scatter1": "k_scatter_l", "varlen_deg": "k_vl_deg",
-                 "varlen_w": "k_vl_w", "varlen_t": "k_vl_t", "varlen_rev": "k_vl_bset", "varlen_recip": "k_vl_recip", "varlen_cand": "k_vl_cand", "triangles": "k_tri_big_items+k_tri_small"}
+                 "varlen_w": "k_vl_w", "varlen_t": "k_vl_t", "varlen_rev": "k_vl_bset", "varlen_recip": "k_vl_recip", "varlen_cand": "k_vl_cins", "triangles": "k_tri_big_items+k_tri_small"}
 
 
 def run_single(args):

@@ -251,16 +251,47 @@ __device__ __forceinline__ void flush_acc(unsigned long long* acc, unsigned long
 // candidate pairs s -> t (those the first-level filter passes) marked in the block's F2 region for
 // slice(s), stored whole per slice segment into partial slot w + j (k_vl_bset's scheme), and
 // counted.  One 1024-lane block per CU either way (64 KiB accumulators + 64 KiB F2 region).
+// Candidate list (cl set, the single-GPU form): the candidates' exact-table keys hkey(s, t) are
+// written to cl (count in *ncand) through a per-wave LDS buffer flushed with one global add per
+// kClFlush keys, instead of the F2 region -- the T walk then needs no filter test per relationship.
+constexpr int kClWave = 512;   // keys buffered per wave (16 waves: 64 KiB, the F2 region's LDS)
+constexpr int kClFlush = 256;  // a wave flushes its buffer at the start of a step once it holds this many
+
+__device__ __forceinline__ void cl_flush(unsigned long long* buf, uint32_t& cnt_lds, unsigned long long* cl,
+                                         unsigned long long* ncand) {  // wave-level
+    const int lane = threadIdx.x & 63;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t n = min(__builtin_amdgcn_readfirstlane(cnt_lds), (uint32_t)kClWave);
+    if (n == 0) return;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(ncand, (unsigned long long)n);
+    base = __shfl(base, 0, 64);
+    for (uint32_t i = lane; i < n; i += 64) cl[base + i] = buf[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) cnt_lds = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 __global__ void __launch_bounds__(kVlBlock) k_vl_deg(ChunkWalk cw, const uint32_t* __restrict__ bw, int b_full,
                                                      int64_t n, unsigned long long* __restrict__ od,
                                                      unsigned long long* __restrict__ sl, RegionBloom bl,
-                                                     uint4* __restrict__ f2part, unsigned long long* __restrict__ ncand) {
+                                                     uint4* __restrict__ f2part, unsigned long long* __restrict__ ncand,
+                                                     unsigned long long* __restrict__ cl) {
     extern __shared__ unsigned long long vl_lds[];
     unsigned long long* a_od = vl_lds;
     uint32_t* f2 = reinterpret_cast<uint32_t*>(vl_lds + kVlIds);
+    const int wave = threadIdx.x >> 6;
+    unsigned long long* cbuf = vl_lds + kVlIds + (size_t)wave * kClWave;  // cl: the F2 region's space
     __shared__ unsigned int cand;
+    __shared__ uint32_t ccnt[kVlBlock / 64];
     if (threadIdx.x == 0) cand = 0;
+    if (threadIdx.x < kVlBlock / 64) ccnt[threadIdx.x] = 0;
     unsigned int mine = 0;  // this lane's candidates (one LDS add per wave at the end)
+    const bool cands = f2part || cl;
     for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_od[i] = 0;
     if (f2part)
         for (int i = threadIdx.x; i < kF2Words; i += kVlBlock) f2[i] = 0;
@@ -269,12 +300,13 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_deg(ChunkWalk cw, const uint32_
         cw,
         [&](const uint2 (&pr)[part::kWalkItems], uint32_t valid, int) {  // pr[k] = (t, s)
             constexpr int K = part::kWalkItems;
+            if (cl && __builtin_amdgcn_readfirstlane(ccnt[wave]) >= (uint32_t)kClFlush) cl_flush(cbuf, ccnt[wave], cl, ncand);
             uint32_t bwd[K], rw[K], rm[K];  // every global word of the step loaded before any is used
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const uint32_t t = pr[k].x, s = pr[k].y;
                 bwd[k] = (od && !b_full) ? bw[t >> 5] : 0xFFFFFFFFu;
-                if (f2part) {
+                if (cands) {
                     uint32_t word;
                     rb_pos(bl, pkey(t, s), word, rm[k]);
                     rw[k] = bl.w[((unsigned long long)(s >> (kVlBits - bl.sublog)) << (bl.rshift - 5)) + word];
@@ -288,7 +320,16 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_deg(ChunkWalk cw, const uint32_
                     if ((bwd[k] >> (t & 31)) & 1u) atomicAdd(&a_od[s & (kVlIds - 1)], 1ULL);
                     if (s == t) atomicAdd(&sl[s], 1ULL);
                 }
-                if (f2part && (rw[k] & rm[k]) == rm[k]) {
+                if (cands && (rw[k] & rm[k]) == rm[k]) {
+                    if (cl) {
+                        const uint32_t q = atomicAdd(&ccnt[wave], 1u);
+                        if (q < (uint32_t)kClWave) {
+                            cbuf[q] = hkey(s, t);
+                        } else {  // the step overfilled the buffer: straight to the list (rare)
+                            cl[atomicAdd(ncand, 1ULL)] = hkey(s, t);
+                        }
+                        continue;
+                    }
                     uint32_t word, bits;
                     f2_pos(pkey(s, t), word, bits);
                     atomicOr(&f2[word], bits);
@@ -306,6 +347,7 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_deg(ChunkWalk cw, const uint32_
                 for (int i = threadIdx.x; i < kF2Words; i += kVlBlock) f2[i] = 0;
             }
         });
+    if (cl) cl_flush(cbuf, ccnt[wave], cl, ncand);
     if (f2part) {
         for (int o = 32; o > 0; o >>= 1) mine += __shfl_down(mine, o, 64);
         if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&cand, mine);
@@ -343,6 +385,14 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_ins(ChunkWalk cw, RegionBloom b
             if (f2_test(f2, p.x, pkey(p.x, p.y)) && rb_test(bl, p.y, pkey(p.x, p.y))) pair_insert(h, hkey(p.y, p.x));
         },
         [&](int) {});
+}
+
+// the candidate list into the exact table (single-GPU form)
+__global__ void k_vl_cins(const unsigned long long* __restrict__ cl, const unsigned long long* __restrict__ ncand,
+                          PairHash h) {
+    const int64_t cnt = (int64_t)*ncand;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * blockDim.x)
+        pair_insert(h, cl[i]);
 }
 
 // target partition (pair = (source, target), j = slice(t)): mark pair (s, t) in t's region.  Each
@@ -573,16 +623,23 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
             cand = dev_alloc(sizeof(int64_t), s);
             HIP_CHECK(hipMemsetAsync(P<void>(cand), 0, sizeof(int64_t), st));
         }
+        // candidates of the reverse-multiplicity count: a list written by the degree walk (default), or
+        // the F2 filter tested again in the T walk (CAPSMI_VL_F2=1, the earlier form; A/B)
+        const char* f2e = getenv("CAPSMI_VL_F2");
+        const bool use_f2 = f2e && atoi(f2e) != 0;
+        Buf clist;
         {
             KernelTimer kt(s, "varlen_deg");
             Buf f2part;
-            if (need3) {
+            if (need3 && use_f2) {
                 f2 = dev_alloc(sizeof(uint32_t) * kF2Words * (size_t)L.nt, s);
                 f2part = dev_alloc(sizeof(uint32_t) * kF2Words * ((size_t)cp.g2 + L.nt), s);
             }
+            if (need3 && !use_f2) clist = dev_alloc(sizeof(unsigned long long) * (size_t)mtot, s);
             hipLaunchKernelGGL(k_vl_deg, dim3(g), dim3(kVlBlock), lds2, st, cw, d.b, d.b_full, n, P<unsigned long long>(od),
-                               P<unsigned long long>(sl), bl, P<uint4>(f2part), P<unsigned long long>(cand));
-            if (need3) {
+                               P<unsigned long long>(sl), bl, P<uint4>(f2part), P<unsigned long long>(cand),
+                               P<unsigned long long>(clist));
+            if (need3 && use_f2) {
                 const RegionBloom f2b{P<uint32_t>(f2), 0, 19, 0};  // kF2Words * 32 = 2^19 bits per slice
                 hipLaunchKernelGGL(k_vl_bmerge, dim3(grid(s, (int64_t)(kF2Words / 4) * L.nt)), dim3(256), 0, st, cp.jst,
                                    L.nt, cp.g2, P<uint4>(f2part), f2b);
@@ -606,15 +663,21 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
             HIP_CHECK(hipMemsetAsync(P<void>(hc), 0, sizeof(unsigned int) * (cap + 1), st));
             h = PairHash{P<unsigned long long>(hk), P<unsigned int>(hc), P<unsigned int>(hc) + cap,
                          (unsigned long long)(cap - 1)};
+            if (!use_f2) {
+                KernelTimer kt(s, "varlen_cand");
+                hipLaunchKernelGGL(k_vl_cins, dim3(grid(s, nc)), dim3(256), 0, st, P<unsigned long long>(clist),
+                                   P<unsigned long long>(cand), h);
+            }
             ody = dev_alloc(2 * nb, s);
             hipLaunchKernelGGL(k_vl_y, dim3(grid(s, n)), dim3(256), 0, st, n, d.b, d.b_full, P<unsigned long long>(od),
                                P<unsigned long long>(W), P<unsigned long long>(sl), P<longlong2>(ody));
         }
         {
             KernelTimer kt(s, "varlen_t");
+            const PairHash ht = use_f2 ? h : PairHash{nullptr, nullptr, nullptr, 0};  // list form: no inserts here
             hipLaunchKernelGGL(k_vl_t, dim3(g), dim3(kVlBlock), lds2, st, cw, d.a, d.a_full, n, P<unsigned long long>(od),
                                need3 ? P<longlong2>(ody) : nullptr, P<unsigned long long>(T2),
-                               P<unsigned long long>(T3), bl, P<uint32_t>(f2), h);
+                               P<unsigned long long>(T3), bl, P<uint32_t>(f2), ht);
         }
         if (need3) {
             KernelTimer kt(s, "varlen_recip");
@@ -772,7 +835,7 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
         KernelTimer kt(s, "varlen_deg");
         hipLaunchKernelGGL(k_vl_deg, dim3((unsigned)v->cp.g2), dim3(kVlBlock), lds2, st, cw, v->d.b, v->d.b_full, n,
                            reinterpret_cast<unsigned long long*>(od), P<unsigned long long>(v->sl),
-                           RegionBloom{nullptr, 0, 0, 0}, nullptr, nullptr);
+                           RegionBloom{nullptr, 0, 0, 0}, nullptr, nullptr, nullptr);
     }
     const int64_t mall = mout + min_;
     if (v->need3 && mall > 0) {
@@ -811,7 +874,7 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
         {
             Buf f2part = dev_alloc(sizeof(uint32_t) * kF2Words * ((size_t)ca.g2 + L.nt), s);
             hipLaunchKernelGGL(k_vl_deg, dim3((unsigned)ca.g2), dim3(kVlBlock), lds2, st, aw, v->d.b, v->d.b_full, n,
-                               nullptr, nullptr, bl, P<uint4>(f2part), P<unsigned long long>(cand));
+                               nullptr, nullptr, bl, P<uint4>(f2part), P<unsigned long long>(cand), nullptr);
             const RegionBloom f2b{P<uint32_t>(v->f2), 0, 19, 0};
             hipLaunchKernelGGL(k_vl_bmerge, dim3(grid(s, (int64_t)(kF2Words / 4) * L.nt)), dim3(256), 0, st, ca.jst,
                                L.nt, ca.g2, P<uint4>(f2part), f2b);
