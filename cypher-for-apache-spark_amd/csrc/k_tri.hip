@@ -321,9 +321,6 @@ constexpr int kWedgeUnroll = 4;  // flat walks: wedges per lane with their targe
 // long hub lists to v-mode -- 126.5 ms against 132.4 with 8; before it, 8 beat 4 by 5 %)
 constexpr int kSmallSlots = 512;  // load <= 1/8: a miss (most wedges) ends after ~1.2 probes
 constexpr int kTriBlock = 256;  // small: 4 waves
-constexpr int kBigBlock = 1024;
-constexpr int kBigChunk = 2048;  // out-list entries per LDS chunk
-constexpr int kBigSlots = 8192;  // load <= 1/4
 
 // Multiplicative hashes on the full-rate 24-bit multiplier (a 32-bit v_mul_lo is quarter rate, and
 // the walks are VALU-bound): the id's bits above 24 are folded in first, so every bit counts
@@ -564,9 +561,10 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
     if (lane == 0 && acc) atomicAdd(out, acc);
 }
 
-// block-wide exclusive scan of n <= kBigChunk values (kBigBlock lanes); returns the total
+// block-wide exclusive scan of n <= 2 B values (B lanes); returns the total
+template <int B>
 __device__ uint32_t big_scan(const uint32_t* in, uint32_t* outp, int n, uint32_t* wtot) {
-    const int per = (n + kBigBlock - 1) / kBigBlock;
+    const int per = (n + B - 1) / B;
     const int b = threadIdx.x * per;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t sum = 0;
@@ -581,13 +579,13 @@ __device__ uint32_t big_scan(const uint32_t* in, uint32_t* outp, int n, uint32_t
     if (lane == 63) wtot[wave] = x;
     __syncthreads();
     if (threadIdx.x < 64) {
-        uint32_t v = lane < kBigBlock / 64 ? wtot[lane] : 0u;
+        uint32_t v = lane < B / 64 ? wtot[lane] : 0u;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = __shfl_up(v, o, 64);
             if (lane >= o) v += y;
         }
-        if (lane < kBigBlock / 64) wtot[lane] = v;
+        if (lane < B / 64) wtot[lane] = v;
     }
     __syncthreads();
     uint32_t pre = x - sum + (wave > 0 ? wtot[wave - 1] : 0u);
@@ -597,7 +595,7 @@ __device__ uint32_t big_scan(const uint32_t* in, uint32_t* outp, int n, uint32_t
             outp[b + k] = pre;
             pre += c;
         }
-    const uint32_t total = wtot[kBigBlock / 64 - 1];
+    const uint32_t total = wtot[B / 64 - 1];
     __syncthreads();
     return total;
 }
@@ -610,27 +608,32 @@ constexpr int kVChunk = 256;
 // setup without their walks took 12-13 ms of each launch)
 constexpr int kVGroup = 8;
 
+// Items run in B-lane workgroups with hash chunks of 2 B out-list entries (4 slots each): 1024 lanes
+// for v-mode (hub centers with long out-lists), 512 for u-mode, whose many small items are bound by
+// their setup's load latency -- four 512-lane items in flight per CU instead of two 1024-lane ones.
+template <int B>
 struct ItemLds {
+    static constexpr int kChunk = 2 * B, kSlots = 4 * kChunk;
     uint32_t bf[(1 << kBigBloomBits) / 32];
-    uint32_t hk[kBigSlots];
-    uint16_t hi[kBigSlots];  // position of the key in out(u)'s hash chunk: payload = ov[b + h0 + hi]
+    uint32_t hk[kSlots];
+    uint16_t hi[kSlots];  // position of the key in out(u)'s hash chunk: payload = ov[b + h0 + hi]
     uint64_t vp[kVChunk];
     int64_t voff[kVChunk];
     uint32_t vl[kVChunk];
     uint32_t dv[kVChunk];
     uint32_t pre[kVChunk];
-    uint32_t wtot[kBigBlock / 64];
+    uint32_t wtot[B / 64];
     unsigned long long item;
 };
 
 // items of center q: hash chunks of out(c) x chunks of its neighbour list (out(c), or in(c) when
 // ioff is set: v-mode)
 __global__ void k_tri_items(const int64_t* __restrict__ off, const int64_t* __restrict__ ioff,
-                            const int64_t* __restrict__ us, int64_t nu, int64_t* __restrict__ items) {
+                            const int64_t* __restrict__ us, int64_t nu, int chunk, int64_t* __restrict__ items) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nu) return;
     const int64_t c = us[q], d = off[c + 1] - off[c], nd = ioff ? ioff[c + 1] - ioff[c] : d;
-    items[q] = ((d + kBigChunk - 1) / kBigChunk) * ((nd + kVChunk * kVGroup - 1) / (kVChunk * kVGroup));
+    items[q] = ((d + chunk - 1) / chunk) * ((nd + kVChunk * kVGroup - 1) / (kVChunk * kVGroup));
 }
 
 // item -> its u's index q (items of q are [ipre[q], ipre[q+1])): one load per item instead of a
@@ -648,8 +651,8 @@ __global__ void k_tri_item_map(const int64_t* __restrict__ ipre, int64_t nu, uin
 // VM (v-mode): the center c is the middle vertex v; its hash holds out(v) and the walked lists are
 // out(u) for the in-neighbours u of v with od(u) <= od(v).  Otherwise (u-mode) c = u and the walked
 // lists are out(v) for v in out(u), less the edges v-mode takes (vmt > 0: od(v) >= vmt, od(u) <= od(v)).
-template <bool LISTS, int U, bool VM>
-__global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __restrict__ tg, TgCode tc,
+template <bool LISTS, int U, bool VM, int B>
+__global__ void __launch_bounds__(B) k_tri_big_items(const uint32_t* __restrict__ tg, TgCode tc,
                                                              const int64_t* __restrict__ ov,
                                                              const int64_t* __restrict__ off,
                                                              const int64_t* __restrict__ ioff,
@@ -661,7 +664,8 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
                                                              unsigned long long* __restrict__ ctr,
                                                              unsigned long long* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    ItemLds& L = *reinterpret_cast<ItemLds*>(lds_raw);
+    ItemLds<B>& L = *reinterpret_cast<ItemLds<B>*>(lds_raw);
+    constexpr int CH = ItemLds<B>::kChunk;
     unsigned long long& item = L.item;
     const int64_t total = ipre[nu];
     unsigned long long acc = 0;
@@ -678,14 +682,14 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
         const int nd = VM ? (int)(ioff[u + 1] - nb) : d;
         const int nvc = (nd + kVChunk - 1) / kVChunk, ngr = (nvc + kVGroup - 1) / kVGroup;
         const int local = (int)(it - ipre[lo]);
-        const int h0 = (local / ngr) * kBigChunk, c0 = (local % ngr) * kVGroup, c1 = min(nvc, c0 + kVGroup);
-        const int hn = min(kBigChunk, d - h0);
+        const int h0 = (local / ngr) * CH, c0 = (local % ngr) * kVGroup, c1 = min(nvc, c0 + kVGroup);
+        const int hn = min(CH, d - h0);
         int lc = 6;  // hash capacity 2^lc >= 4 hn (load <= 1/4), cleared as far as it is used
         while ((1 << lc) < 4 * hn) ++lc;
-        for (int k = threadIdx.x; k < (1 << lc); k += kBigBlock) L.hk[k] = kEmpty;
-        for (int k = threadIdx.x; k < (1 << kBigBloomBits) / 32; k += kBigBlock) L.bf[k] = 0;
+        for (int k = threadIdx.x; k < (1 << lc); k += B) L.hk[k] = kEmpty;
+        for (int k = threadIdx.x; k < (1 << kBigBloomBits) / 32; k += B) L.bf[k] = 0;
         __syncthreads();
-        for (int k = threadIdx.x; k < hn; k += kBigBlock) {
+        for (int k = threadIdx.x; k < hn; k += B) {
             const uint32_t word = tg[b + h0 + k], w = tid(word, tc);
             hinsert(L.hk, L.hi, lc, w, word, (uint32_t)k);
             bset(L.bf, kBigBloomBits, w);
@@ -693,7 +697,7 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
         for (int c = c0; c < c1; ++c) {  // block-uniform
             const int v0 = c * kVChunk, vn = min(kVChunk, nd - v0);
             if (c > c0) __syncthreads();  // the previous chunk's walks are done with the list table
-            for (int k = threadIdx.x; k < vn; k += kBigBlock) {
+            for (int k = threadIdx.x; k < vn; k += B) {
                 const uint32_t v = VM ? itg[nb + v0 + k] : tid(tg[b + v0 + k], tc);
                 const int64_t vo = off[v];
                 const uint32_t dv = (uint32_t)(off[v + 1] - vo);
@@ -709,7 +713,7 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
             __syncthreads();
             if (LISTS) {
                 const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-                for (int k = wave; k < vn; k += kBigBlock / 64) {
+                for (int k = wave; k < vn; k += B / 64) {
                     const int64_t vo = uniform64(L.voff[k]);
                     const int64_t dv = (int64_t)__builtin_amdgcn_readfirstlane(L.dv[k]);
                     const uint64_t puv = L.vp[k];
@@ -730,18 +734,18 @@ __global__ void __launch_bounds__(kBigBlock) k_tri_big_items(const uint32_t* __r
                 }
                 continue;
             }
-            const uint32_t tw = big_scan(L.dv, L.pre, vn, L.wtot);
+            const uint32_t tw = big_scan<B>(L.dv, L.pre, vn, L.wtot);
             int i = 0;  // the lane's current v, as in k_tri_small
             int64_t base = L.voff[0];
             uint32_t nxt = vn > 1 ? L.pre[1] : 0xFFFFFFFFu;
-            for (uint32_t f0 = threadIdx.x; f0 < tw; f0 += kWedgeUnroll * kBigBlock) {
+            for (uint32_t f0 = threadIdx.x; f0 < tw; f0 += kWedgeUnroll * B) {
                 // kWedgeUnroll wedges per lane: all their target loads in flight before the probes
                 int ii[kWedgeUnroll];
                 int64_t pos[kWedgeUnroll];
                 uint32_t w[kWedgeUnroll];
 #pragma unroll
                 for (int k = 0; k < kWedgeUnroll; ++k) {
-                    const uint32_t f = f0 + k * kBigBlock;
+                    const uint32_t f = f0 + k * B;
                     if (f < tw && f >= nxt) {
                         i = seg_from(L.pre, i + 1, vn, f);
                         base = L.voff[i] - (int64_t)L.pre[i];
@@ -985,24 +989,30 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
             Buf ib = dev_alloc(sizeof(int64_t) * (2 * nc + 2), s);
             int64_t* items = P<int64_t>(ib);
             int64_t* ipre = items + nc;
+            const char* ube = getenv("CAPSMI_TRI_UBLOCK");  // u-mode workgroup: 512 (default) or 1024
+            const char* vbe = getenv("CAPSMI_TRI_VBLOCK");  // v-mode workgroup: 1024 (default) or 512
+            const int B = !lists ? 1024 : vm ? (vbe && atoi(vbe) == 512 ? 512 : 1024) : (ube && atoi(ube) == 1024 ? 1024 : 512);
             hipLaunchKernelGGL(k_tri_items, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st, P<int64_t>(g.off),
-                               vm ? P<int64_t>(g.ioff) : nullptr, cs, nc, items);
+                               vm ? P<int64_t>(g.ioff) : nullptr, cs, nc, 2 * B, items);
             exclusive_scan_i64(items, ipre, nc, s);
             const int64_t nitems = read_scalar(s, ipre + nc);
             Buf iq = dev_alloc(sizeof(uint32_t) * (nitems > 0 ? nitems : 1), s);
             hipLaunchKernelGGL(k_tri_item_map, dim3(grid(s, nc)), dim3(256), 0, st, ipre, nc, P<uint32_t>(iq));
             Buf ctr = dev_alloc(sizeof(unsigned long long), s);
             HIP_CHECK(hipMemsetAsync(P<void>(ctr), 0, sizeof(unsigned long long), st));
-            const size_t lds = sizeof(ItemLds);
+            const size_t lds = B == 1024 ? sizeof(ItemLds<1024>) : sizeof(ItemLds<512>);
             const char* uve = getenv("CAPSMI_TRI_UNROLL_VM");  // v-mode loads in flight per lane: 4 or 8
             const int uv = uve ? atoi(uve) : 4;
-            auto kf = vm ? (uv == 4 ? k_tri_big_items<true, 4, true> : k_tri_big_items<true, 8, true>)
-                      : !lists ? k_tri_big_items<false, 4, false>
-                      : un == 16 ? k_tri_big_items<true, 16, false>
-                      : un == 8 ? k_tri_big_items<true, 8, false> : k_tri_big_items<true, 4, false>;
+            auto kf = vm ? (B == 512 ? k_tri_big_items<true, 4, true, 512>
+                            : uv == 4 ? k_tri_big_items<true, 4, true, 1024> : k_tri_big_items<true, 8, true, 1024>)
+                      : !lists ? k_tri_big_items<false, 4, false, 1024>
+                      : B == 512 ? (un == 8 ? k_tri_big_items<true, 8, false, 512> : k_tri_big_items<true, 4, false, 512>)
+                      : un == 16 ? k_tri_big_items<true, 16, false, 1024>
+                      : un == 8 ? k_tri_big_items<true, 8, false, 1024> : k_tri_big_items<true, 4, false, 1024>;
             HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kf), hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)lds));
-            hipLaunchKernelGGL(kf, dim3((unsigned)(s->num_cus * 4)), dim3(kBigBlock), lds, st,
+            // resident: two 1024-lane or four 512-lane workgroups per CU (LDS), twice that queued
+            hipLaunchKernelGGL(kf, dim3((unsigned)(s->num_cus * (B == 1024 ? 4 : 8))), dim3(B), lds, st,
                                P<uint32_t>(g.tg), tc, P<int64_t>(g.ov), P<int64_t>(g.off),
                                P<int64_t>(g.ioff), P<uint32_t>(g.itg), P<uint32_t>(g.ipos), g.vmt, cs, nc, ipre,
                                P<uint32_t>(iq), P<unsigned long long>(ctr), P<unsigned long long>(out));
