@@ -122,3 +122,20 @@ def test_wide_id_range(session):
     nodes = session.table([ColumnData("id", I64, ids)])
     ok = graph.NodeBitmap(session, 0, n).add_scan(nodes)
     assert graph.triangle_count(session, [rels], ok) == cpu.triangle_enumerate(k, a.astype(np.int64), b.astype(np.int64))
+
+
+@pytest.mark.parametrize("vmode", VMODE)
+def test_exception_multiplicities(session, monkeypatch, vmode):
+    """Multiplicities from 1 to 40 in both directions: the 4-bit codes of the oriented targets saturate
+    (>= 15) for many edges, whose exact payloads are placed after the key-only sort (k_exc_place) and
+    read on hits from either side of a wedge."""
+    _vmode(monkeypatch, vmode)
+    rng = np.random.default_rng(17)
+    n = 90
+    a, b = np.nonzero(rng.random((n, n)) < 0.25)
+    keep = a != b
+    a, b = a[keep], b[keep]
+    reps = rng.integers(1, 41, len(a)) * (rng.random(len(a)) < 0.3) + 1
+    src = np.repeat(a, reps).astype(np.int64)
+    dst = np.repeat(b, reps).astype(np.int64)
+    assert _count(session, n, src, dst) == cpu.triangle_closed_form(n, src, dst)

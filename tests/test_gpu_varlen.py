@@ -251,3 +251,33 @@ def test_sharded_matches_enumeration(session, nparts):
         got = _sharded(session, n, src, dst, a_mask, b_mask, lo, hi, nparts)
         _, g = cpu.var_length_count(n, src, dst, lo, hi, a_mask.astype(np.uint8), b_mask.astype(np.uint8))
         assert got == {int(i): int(g[i]) for i in np.nonzero(g)[0]}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("f2", ["0", "1"])
+def test_dense_reciprocal_candidates(session, monkeypatch, f2):
+    """Every relationship of a complete digraph (plus doubled pairs) has its reverse: every one is a
+    reverse-count candidate, so a wave's step fills its LDS candidate buffer past capacity and the
+    overflow goes straight to the list (k_vl_deg, list form); CAPSMI_VL_F2=1 runs the F2-filter form.
+    Checked against the closed form (oracle/closed.c, pinned to enumeration by test_oracle_pins.py)."""
+    from capsmi import ColumnData, I64, graph
+    monkeypatch.setenv("CAPSMI_VL_F2", f2)
+    n = 180
+    a, b = np.nonzero(~np.eye(n, dtype=bool))
+    extra = np.arange(0, len(a), 7)  # doubled pairs: multiplicities 2
+    src = np.concatenate([a, a[extra]]).astype(np.int64)
+    dst = np.concatenate([b, b[extra]]).astype(np.int64)
+    rng = np.random.default_rng(3)
+    a_mask = rng.random(n) < 0.8
+    b_mask = rng.random(n) < 0.7
+    rels = [_table(session, src, dst)]
+    a_nodes = session.table([ColumnData("id", I64, np.nonzero(a_mask)[0])])
+    b_nodes = session.table([ColumnData("id", I64, np.nonzero(b_mask)[0])])
+    a_ok = graph.NodeBitmap(session, 0, n).add_scan(a_nodes)
+    b_ok = graph.NodeBitmap(session, 0, n).add_scan(b_nodes)
+    for lo, hi in [(1, 3), (2, 3), (3, 3)]:
+        out = graph.var_length_count(session, rels, a_ok, b_ok, lo, hi, "a", "cnt")
+        _, g = cpu.var_length_closed_form(n, src, dst, lo, hi, a_mask.astype(np.uint8), b_mask.astype(np.uint8))
+        want = {int(i): int(g[i]) for i in np.nonzero(g)[0]}
+        got = dict(zip(out.column("a").values.tolist(), out.column("cnt").values.tolist()))
+        assert got == want
