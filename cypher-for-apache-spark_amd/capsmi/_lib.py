@@ -238,14 +238,29 @@ def check(status: int, what: str = "") -> None:
         raise cls(f"{what}: {last_error()}" if what else last_error())
 
 
+_FN = {}  # name -> bound foreign function (skips the CDLL attribute lookup per call)
+
+
 def call(name: str, *args) -> None:
-    check(getattr(load(), name)(*args), name)
+    fn = _FN.get(name)
+    if fn is None:
+        fn = _FN[name] = getattr(load(), name)
+    status = fn(*args)
+    if status != OK:
+        check(status, name)
+
+
+_STRS = {}  # tuple of names -> its char* array (column-name lists repeat across a query's calls)
 
 
 def strs(names):
-    arr = (c_char_p * max(1, len(names)))()
-    for i, n in enumerate(names):
-        arr[i] = n.encode()
+    key = tuple(names)
+    arr = _STRS.get(key)
+    if arr is None:
+        arr = (c_char_p * max(1, len(key)))(*[n.encode() for n in key])
+        if len(_STRS) > 4096:
+            _STRS.clear()
+        _STRS[key] = arr
     return arr
 
 

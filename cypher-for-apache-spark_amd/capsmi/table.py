@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import bisect
 import ctypes
+import threading
 from dataclasses import dataclass
 from typing import Iterable, List, Optional, Sequence, Tuple
 
@@ -18,6 +19,8 @@ import numpy as np
 
 from . import _lib
 from .expr import BOOL, F64, I64, LIST, STR, CapsmiExpr, Col, Expr, Lit, compile_program, to_ctypes
+
+_TLS = threading.local()
 
 _EXPR_PTR = ctypes.POINTER(CapsmiExpr)
 _LIT_PROGS = {}  # (python type, value, declared type) -> one-node program of a Boolean / Long / null literal
@@ -317,7 +320,9 @@ class GpuTable:
     def _read_schema(self):
         if self._schema is None:  # one call for names and types (include/capsmi.h capsmi_table_schema)
             n = ctypes.c_int32()
-            buf = ctypes.create_string_buffer(16384)
+            buf = getattr(_TLS, "names", None)  # a reusable name buffer per thread (ctypes drops the GIL)
+            if buf is None:
+                buf = _TLS.names = ctypes.create_string_buffer(16384)
             types = (ctypes.c_int32 * self._MAXC)()
             _lib.call("capsmi_table_schema", self._h, ctypes.byref(n), buf, len(buf), types, None, self._MAXC)
             if n.value > self._MAXC:
