@@ -286,6 +286,7 @@ class GpuTable:
         self._schema = None  # (names, types): tables are immutable, so the schema is read once
         self._index = None  # name -> position (expression compilation)
         self._leaf = None  # column name -> its one-node program (the planner's scans project columns)
+        self._wcols = None  # withColumns argument arrays of column / literal projections, by structure
 
     # ---- lifetime ------------------------------------------------------------------------
     @property
@@ -559,6 +560,24 @@ class GpuTable:
         return self._wrap(out)
 
     def withColumns(self, *columns: Tuple[Expr, str]) -> "GpuTable":
+        # the scans' projections (columns and label / null literals) repeat on the same entity tables
+        # query after query: their argument arrays are kept per table, keyed by their structure
+        key = []
+        for e, name in columns:
+            if type(e) is Col:
+                key.append((name, e.name))
+            elif type(e) is Lit and (e.value is None or type(e.value) in (bool, int)):
+                key.append((name, type(e.value), e.value, e.type))
+            else:
+                key = None
+                break
+        if key is not None:
+            key = tuple(key)
+            hit = self._wcols.get(key) if self._wcols is not None else None
+            if hit is not None:
+                out = ctypes.c_void_p()
+                _lib.call("capsmi_with_columns", self._h, len(columns), hit[0], ctypes.byref(out))
+                return self._wrap(out)
         arr = (_lib.ExprColumn * max(1, len(columns)))()
         keep = []
         for i, (e, name) in enumerate(columns):
@@ -567,6 +586,10 @@ class GpuTable:
             arr[i].name = name.encode()
             arr[i].nnodes = n
             arr[i].prog = ctypes.cast(prog, _EXPR_PTR)
+        if key is not None:
+            if self._wcols is None or len(self._wcols) > 256:
+                self._wcols = {}
+            self._wcols[key] = (arr, keep)  # keep: the programs the array points into
         out = ctypes.c_void_p()
         _lib.call("capsmi_with_columns", self._h, len(columns), arr, ctypes.byref(out))
         return self._wrap(out)
