@@ -1274,6 +1274,16 @@ capsmi_status capsmi_bitmap_add_scan(capsmi_bitmap* b, capsmi_table* nodes, cons
     Buf cnt = dev_alloc(3 * sizeof(int64_t), s);
     HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, 3 * sizeof(int64_t), s->stream));
     bitmap_add_rows(b, idc.d(), idc.v(), P<uint8_t>(flags), nodes->nrows, P<int64_t>(cnt), &rp);
+    if (e && e->kind == 1 && e->ids_unique && e->id == idx && !idc.v() && b->set_bits == 0 && b->rows_added == 0 &&
+        e->lo >= b->lo && e->hi <= b->hi) {
+        // A registered node table without repeated or null ids, inside the window, into an empty bitmap:
+        // no row can be out of range or a duplicate, so nothing needs reading back -- the scan costs no
+        // host round trip.  With a predicate the set-bit count is left unknown (computed when asked).
+        b->rows_added = nodes->nrows;
+        b->set_bits = nnodes == 0 ? nodes->nrows : -1;
+        b->full = b->set_bits == b->hi - b->lo;
+        return CAPSMI_OK;
+    }
     int64_t h[3];
     HIP_CHECK(hipMemcpyAsync(h, P<void>(cnt), sizeof(h), hipMemcpyDeviceToHost, s->stream));
     HIP_CHECK(hipStreamSynchronize(s->stream));
@@ -1292,6 +1302,10 @@ capsmi_status capsmi_bitmap_add_scan(capsmi_bitmap* b, capsmi_table* nodes, cons
 capsmi_status capsmi_bitmap_stats(capsmi_bitmap* b, int64_t* set_bits, int32_t* unique_rows) {
     API_BEGIN
     need(b, "bitmap");
+    if (b->set_bits < 0) {  // left unknown by a scan with a predicate
+        b->set_bits = words_popcount(b->sess, P<uint32_t>(b->words), 0, b->nwords);
+        b->full = b->set_bits == b->hi - b->lo;
+    }
     if (set_bits) *set_bits = b->set_bits;
     if (unique_rows) *unique_rows = b->any_dup ? 0 : 1;
     API_END
@@ -2162,7 +2176,8 @@ capsmi_status capsmi_rmat_nodes(capsmi_session* s, int32_t scale, int32_t kind, 
         graph::ages(s, P<int64_t>(ids), rows, seed, P<int64_t>(a.data));
         o->cols.push_back(std::move(a));
     }
-    attach_entity(o, 1, 0, n, kind == 0);  // [id] / [id, age]: a registered node table (all ids: exactly [0, n))
+    // [id] / [id, age]: a registered node table (all ids: exactly [0, n); each id generated once either way)
+    attach_entity(o, 1, 0, n, kind == 0, true);
     *out = o;
     API_END
 }

@@ -92,6 +92,7 @@ struct EntityInfo {
     int64_t lo = 0, hi = 0;       // [min, max + 1) of the ids (node) or of both endpoints (relationship)
     int64_t rows = 0;
     bool ids_exact = false;       // node: the ids are exactly [lo, hi), each once (checked at registration)
+    bool ids_unique = false;      // node: no id occurs twice and none is null (checked at registration)
 };
 struct PlanNode;  // lazy Table[T] operator (plan.hip)
 
@@ -441,7 +442,7 @@ void validate_program(const capsmi_table* t, int32_t nn, const capsmi_expr* prog
 void materialize(capsmi_table* t);
 // mark a materialised table in canonical entity layout (ids first) as a node (1) / relationship (2)
 // table whose ids (endpoints) lie in [lo, hi)
-void attach_entity(capsmi_table* t, int kind, int64_t lo, int64_t hi, bool ids_exact = false);
+void attach_entity(capsmi_table* t, int kind, int64_t lo, int64_t hi, bool ids_exact = false, bool ids_unique = false);
 inline capsmi_table* M(const capsmi_table* t) {
     materialize(const_cast<capsmi_table*>(t));
     return const_cast<capsmi_table*>(t);

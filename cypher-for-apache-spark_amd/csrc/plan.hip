@@ -742,6 +742,8 @@ std::string member_prog_key(const capsmi_table* base, const std::vector<capsmi_e
 void gather_owned_bitmap(capsmi_session* s, capsmi_bitmap* b) {
     const int64_t S = g_dist.slice_words;
     REQUIRE(b->nwords == S * g_dist.world, CAPSMI_ERR_INTERNAL, "distributed bitmap geometry");
+    // a scan that left its count unknown (capsmi_bitmap_add_scan): this rank's bits, before the gather
+    if (b->set_bits < 0) b->set_bits = words_popcount(s, P<uint32_t>(b->words), 0, b->nwords);
     Buf full = dev_alloc(sizeof(uint32_t) * (size_t)b->nwords, s);
     collective(s, CAPSMI_COLL_ALL_GATHER, P<uint32_t>(b->words) + (int64_t)g_dist.rank * S, P<uint32_t>(full), S,
                CAPSMI_COLL_U32);
@@ -1473,7 +1475,7 @@ bool try_fused_shapes(capsmi_table* t, capsmi_table** out) {
 
 }  // namespace
 
-void attach_entity(capsmi_table* t, int kind, int64_t lo, int64_t hi, bool ids_exact) {
+void attach_entity(capsmi_table* t, int kind, int64_t lo, int64_t hi, bool ids_exact, bool ids_unique) {
     auto e = std::make_shared<EntityInfo>();
     e->kind = kind;
     e->id = 0;
@@ -1485,6 +1487,7 @@ void attach_entity(capsmi_table* t, int kind, int64_t lo, int64_t hi, bool ids_e
     e->lo = lo;
     e->hi = hi;
     e->ids_exact = ids_exact;
+    e->ids_unique = ids_exact || ids_unique;
     t->entity = e;
 }
 
@@ -2271,12 +2274,15 @@ static capsmi_table* register_entity(capsmi_table* t, int kind, const std::vecto
         }
         e->lo = mm[0];
         e->hi = mm[1] == INT64_MAX ? INT64_MAX : mm[1] + 1;
-        if (kind == 1 && mm[1] != INT64_MAX && e->hi - e->lo == t->nrows && t->nrows <= (int64_t(1) << 31)) {
-            // as many rows as ids in [min, max]: the ids are exactly that window iff none repeats
+        if (kind == 1 && mm[1] != INT64_MAX && e->hi - e->lo <= (int64_t(1) << 31) && !t->cols[0].valid) {
+            // one bitmap pass over [min, max]: whether an id repeats (a node scan of a table without
+            // repeats then needs no count read back, capsmi_bitmap_add_scan), and whether the ids are
+            // exactly that window (as many rows as ids in it, none repeated)
             capsmi_bitmap* b = nullptr;
             check(capsmi_bitmap_create(s, e->lo, e->hi, &b));
             const capsmi_status st = capsmi_bitmap_add_scan(b, t, t->cols[0].name.c_str(), 0, nullptr);
-            e->ids_exact = st == CAPSMI_OK && !b->any_dup && b->set_bits == t->nrows;
+            e->ids_unique = st == CAPSMI_OK && !b->any_dup;
+            e->ids_exact = e->ids_unique && b->set_bits == t->nrows && e->hi - e->lo == t->nrows;
             capsmi_bitmap_release(b);
             check(st);
         }
