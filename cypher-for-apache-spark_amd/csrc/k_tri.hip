@@ -636,11 +636,11 @@ __global__ void k_tri_items(const int64_t* __restrict__ off, const int64_t* __re
     items[q] = ((d + chunk - 1) / chunk) * ((nd + kVChunk * kVGroup - 1) / (kVChunk * kVGroup));
 }
 
-// item -> its u's index q (items of q are [ipre[q], ipre[q+1])): one load per item instead of a
+// item -> (its center's index q) | (its index among q's items) << 32: one load per item instead of a
 // ~20-step dependent binary search over ipre at the start of every item
-__global__ void k_tri_item_map(const int64_t* __restrict__ ipre, int64_t nu, uint32_t* __restrict__ item_q) {
+__global__ void k_tri_item_map(const int64_t* __restrict__ ipre, int64_t nu, uint64_t* __restrict__ item_ql) {
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nu; q += (int64_t)gridDim.x * blockDim.x)
-        for (int64_t it = ipre[q]; it < ipre[q + 1]; ++it) item_q[it] = (uint32_t)q;
+        for (int64_t it = ipre[q]; it < ipre[q + 1]; ++it) item_ql[it] = (uint64_t)q | ((uint64_t)(it - ipre[q]) << 32);
 }
 
 // LISTS (default): each wave walks whole out(v) lists of the item's v chunk (wave q takes v = q, q + 16,
@@ -651,6 +651,9 @@ __global__ void k_tri_item_map(const int64_t* __restrict__ ipre, int64_t nu, uin
 // VM (v-mode): the center c is the middle vertex v; its hash holds out(v) and the walked lists are
 // out(u) for the in-neighbours u of v with od(u) <= od(v).  Otherwise (u-mode) c = u and the walked
 // lists are out(v) for v in out(u), less the edges v-mode takes (vmt > 0: od(v) >= vmt, od(u) <= od(v)).
+// Register budget: two 1024-lane items per CU need 8 waves per SIMD, i.e. an SGPR granule of at most
+// 96 (800 per SIMD): .amdhsa_next_free_sgpr <= 74 here.  At 77 the v-mode launch admitted one item
+// per CU and took 113 instead of 69 ms (the u-mode 512-lane one 25 instead of 21.6 ms).
 template <bool LISTS, int U, bool VM, int B>
 __global__ void __launch_bounds__(B) k_tri_big_items(const uint32_t* __restrict__ tg, TgCode tc,
                                                              const int64_t* __restrict__ ov,
@@ -660,7 +663,7 @@ __global__ void __launch_bounds__(B) k_tri_big_items(const uint32_t* __restrict_
                                                              const uint32_t* __restrict__ ipos, int vmt,
                                                              const int64_t* __restrict__ us, int64_t nu,
                                                              const int64_t* __restrict__ ipre,
-                                                             const uint32_t* __restrict__ item_q,
+                                                             const uint64_t* __restrict__ item_ql,
                                                              unsigned long long* __restrict__ ctr,
                                                              unsigned long long* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -675,13 +678,14 @@ __global__ void __launch_bounds__(B) k_tri_big_items(const uint32_t* __restrict_
         const int64_t it = (int64_t)item;
         __syncthreads();  // `item` is rewritten next round
         if (it >= total) break;  // block-uniform
-        const int64_t lo = item_q[it];
+        const uint64_t iw = item_ql[it];
+        const int64_t lo = (uint32_t)iw;
         const int64_t u = us[lo], b = uniform64(off[u]);  // the center (u-mode: u; v-mode: v)
         const int d = (int)(off[u + 1] - b);
         const int64_t nb = VM ? uniform64(ioff[u]) : b;   // its neighbour list: in(v) / out(u)
         const int nd = VM ? (int)(ioff[u + 1] - nb) : d;
         const int nvc = (nd + kVChunk - 1) / kVChunk, ngr = (nvc + kVGroup - 1) / kVGroup;
-        const int local = (int)(it - ipre[lo]);
+        const int local = (int)(iw >> 32);
         const int h0 = (local / ngr) * CH, c0 = (local % ngr) * kVGroup, c1 = min(nvc, c0 + kVGroup);
         const int hn = min(CH, d - h0);
         int lc = 6;  // hash capacity 2^lc >= 4 hn (load <= 1/4), cleared as far as it is used
@@ -996,8 +1000,8 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
                                vm ? P<int64_t>(g.ioff) : nullptr, cs, nc, 2 * B, items);
             exclusive_scan_i64(items, ipre, nc, s);
             const int64_t nitems = read_scalar(s, ipre + nc);
-            Buf iq = dev_alloc(sizeof(uint32_t) * (nitems > 0 ? nitems : 1), s);
-            hipLaunchKernelGGL(k_tri_item_map, dim3(grid(s, nc)), dim3(256), 0, st, ipre, nc, P<uint32_t>(iq));
+            Buf iq = dev_alloc(sizeof(uint64_t) * (nitems > 0 ? nitems : 1), s);
+            hipLaunchKernelGGL(k_tri_item_map, dim3(grid(s, nc)), dim3(256), 0, st, ipre, nc, P<uint64_t>(iq));
             Buf ctr = dev_alloc(sizeof(unsigned long long), s);
             HIP_CHECK(hipMemsetAsync(P<void>(ctr), 0, sizeof(unsigned long long), st));
             const size_t lds = B == 1024 ? sizeof(ItemLds<1024>) : sizeof(ItemLds<512>);
@@ -1015,7 +1019,8 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
             hipLaunchKernelGGL(kf, dim3((unsigned)(s->num_cus * (B == 1024 ? 4 : 8))), dim3(B), lds, st,
                                P<uint32_t>(g.tg), tc, P<int64_t>(g.ov), P<int64_t>(g.off),
                                P<int64_t>(g.ioff), P<uint32_t>(g.itg), P<uint32_t>(g.ipos), g.vmt, cs, nc, ipre,
-                               P<uint32_t>(iq), P<unsigned long long>(ctr), P<unsigned long long>(out));
+                               P<uint64_t>(iq), P<unsigned long long>(ctr),
+                               P<unsigned long long>(out));
         };
         if (be > bb) run_items(P<int64_t>(g.big_u) + bb, be - bb, false);
         if (ve > vb) run_items(P<int64_t>(g.vm_c) + vb, ve - vb, true);
