@@ -1444,11 +1444,13 @@ static void part_mid(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* 
 // build + hop 1 in one go (hop 1 rides on the build's second pass when a is full)
 static void build_part_mid(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
                            const char* dst_col, const capsmi_bitmap* a, const capsmi_bitmap* b, uint32_t* X1,
-                           uint32_t* X2, uint32_t* S1, RelPart& rp) {
+                           uint32_t* X2, uint32_t* S1, RelPart& rp, bool zeroed = false) {
     const int64_t nw = b->nwords;
-    HIP_CHECK(hipMemsetAsync(X1, 0, sizeof(uint32_t) * nw, s->stream));
-    HIP_CHECK(hipMemsetAsync(X2, 0, sizeof(uint32_t) * nw, s->stream));
-    HIP_CHECK(hipMemsetAsync(S1, 0, sizeof(uint32_t) * nw, s->stream));
+    if (!zeroed) {  // zeroed: the caller cleared X1, X2, S1 with its own buffers in one fill
+        HIP_CHECK(hipMemsetAsync(X1, 0, sizeof(uint32_t) * nw, s->stream));
+        HIP_CHECK(hipMemsetAsync(X2, 0, sizeof(uint32_t) * nw, s->stream));
+        HIP_CHECK(hipMemsetAsync(S1, 0, sizeof(uint32_t) * nw, s->stream));
+    }
     const RelPartHop1 h1{a, b, X1, S1, X2};
     build_part(s, nrels, rels, src_col, dst_col, b->lo, b->hi, rp, &h1);
     graph::mid_combine(s, X1, X2, S1, nw);
@@ -1495,16 +1497,22 @@ capsmi_status capsmi_two_hop_count_distinct(capsmi_session* s, int32_t nrels, ca
     check_bitmap(c_ok, "c_ok");
     use_device(s);
     const int64_t nw = b_ok->nwords > 0 ? b_ok->nwords : 1;
+    if (same_domain(a_ok, b_ok, c_ok)) {
+        // cold radix-partitioned path: partition + two LDS-resident hops; X1, X2, S1 and the
+        // distinct targets' bitmap in one buffer, cleared by one fill
+        Buf x = dev_alloc(sizeof(uint32_t) * nw * 4, s);
+        uint32_t* X1 = P<uint32_t>(x);
+        HIP_CHECK(hipMemsetAsync(X1, 0, sizeof(uint32_t) * nw * 4, s->stream));
+        RelPart rp;
+        build_part_mid(s, nrels, rels, src_col, dst_col, a_ok, b_ok, X1, X1 + nw, X1 + 2 * nw, rp, true);
+        relpart_hop2(s, rp, c_ok, X1, X1 + nw, X1 + 3 * nw);
+        *out_distinct = words_popcount(s, X1 + 3 * nw, 0, c_ok->nwords);
+        return CAPSMI_OK;
+    }
     Buf x = dev_alloc(sizeof(uint32_t) * nw * 3, s);
     Buf cw = dev_alloc(sizeof(uint32_t) * (c_ok->nwords > 0 ? c_ok->nwords : 1), s);
     uint32_t* X1 = P<uint32_t>(x);
-    if (same_domain(a_ok, b_ok, c_ok)) {
-        // cold radix-partitioned path: partition + two LDS-resident hops
-        RelPart rp;
-        build_part_mid(s, nrels, rels, src_col, dst_col, a_ok, b_ok, X1, X1 + nw, X1 + 2 * nw, rp);
-        HIP_CHECK(hipMemsetAsync(P<void>(cw), 0, sizeof(uint32_t) * c_ok->nwords, s->stream));
-        relpart_hop2(s, rp, c_ok, X1, X1 + nw, P<uint32_t>(cw));
-    } else {
+    {
         two_hop_mid(s, nrels, rels, src_col, dst_col, a_ok, b_ok, X1, X1 + nw, X1 + 2 * nw);
         two_hop_dst(s, nrels, rels, src_col, dst_col, b_ok, c_ok, X1, X1 + nw, P<uint32_t>(cw));
     }

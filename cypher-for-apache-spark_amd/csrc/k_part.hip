@@ -17,6 +17,8 @@
 // target slices as packed uint32 pairs, pass 2 scatters each target slice into its source cells.
 // Both scatters stage an 8192-relationship tile in LDS grouped by bucket, so the HBM writes are
 // runs of whole cache lines rather than 8-byte scatters.
+#include <map>
+#include <mutex>
 #include "part_common.h"
 
 namespace capsmi {
@@ -934,8 +936,19 @@ static part::PairOut pair_out(const RelPart& rp) {
 
 template <typename K>
 static void allow_lds(K kernel, size_t bytes) {
+    // set once per (device, kernel) and raised only when a launch needs more: the attribute call
+    // costs host time on every query otherwise
+    static std::mutex mu;
+    static std::map<std::pair<int, const void*>, size_t> done;
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    const auto key = std::make_pair(dev, reinterpret_cast<const void*>(kernel));
+    std::lock_guard<std::mutex> g(mu);
+    auto it = done.find(key);
+    if (it != done.end() && it->second >= bytes) return;
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)bytes));
+    done[key] = bytes;
 }
 
 void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
