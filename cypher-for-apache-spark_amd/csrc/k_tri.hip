@@ -621,8 +621,9 @@ struct ItemLds {
     int64_t voff[kVChunk];
     uint32_t vl[kVChunk];
     uint32_t dv[kVChunk];
-    uint32_t pre[kVChunk];
+    uint32_t pre[kVChunk];  // flat walk: prefix sums; list walks: the long and short lists' indexes (2 x uint16)
     uint32_t wtot[B / 64];
+    uint32_t ncnt[4];  // list walks: [2 (c & 1) + 0/1] long / short lists of chunk c
     unsigned long long item;
 };
 
@@ -655,7 +656,7 @@ __global__ void k_tri_item_map(const int64_t* __restrict__ ipre, int64_t nu, uin
 // 96 (800 per SIMD): .amdhsa_next_free_sgpr <= 74 here.  At 77 the v-mode launch admitted one item
 // per CU and took 113 instead of 69 ms (the u-mode 512-lane one 25 instead of 21.6 ms).
 template <bool LISTS, int U, bool VM, int B>
-__global__ void __launch_bounds__(B) k_tri_big_items(const uint32_t* __restrict__ tg, TgCode tc,
+__global__ void __launch_bounds__(B, 8) k_tri_big_items(const uint32_t* __restrict__ tg, TgCode tc,
                                                              const int64_t* __restrict__ ov,
                                                              const int64_t* __restrict__ off,
                                                              const int64_t* __restrict__ ioff,
@@ -692,6 +693,7 @@ __global__ void __launch_bounds__(B) k_tri_big_items(const uint32_t* __restrict_
         while ((1 << lc) < 4 * hn) ++lc;
         for (int k = threadIdx.x; k < (1 << lc); k += B) L.hk[k] = kEmpty;
         for (int k = threadIdx.x; k < (1 << kBigBloomBits) / 32; k += B) L.bf[k] = 0;
+        if (threadIdx.x < 4) L.ncnt[threadIdx.x] = 0;
         __syncthreads();
         for (int k = threadIdx.x; k < hn; k += B) {
             const uint32_t word = tg[b + h0 + k], w = tid(word, tc);
@@ -701,6 +703,10 @@ __global__ void __launch_bounds__(B) k_tri_big_items(const uint32_t* __restrict_
         for (int c = c0; c < c1; ++c) {  // block-uniform
             const int v0 = c * kVChunk, vn = min(kVChunk, nd - v0);
             if (c > c0) __syncthreads();  // the previous chunk's walks are done with the list table
+            uint16_t* lk = reinterpret_cast<uint16_t*>(L.pre);  // LISTS: lists of > 64 entries
+            uint16_t* sk = lk + kVChunk;                        // LISTS: lists of 1..64 entries
+            uint32_t* nc = L.ncnt + 2 * (c & 1);
+            if (LISTS && threadIdx.x < 2) L.ncnt[2 * ((c + 1) & 1) + threadIdx.x] = 0;  // read last by chunk c - 1
             for (int k = threadIdx.x; k < vn; k += B) {
                 const uint32_t v = VM ? itg[nb + v0 + k] : tid(tg[b + v0 + k], tc);
                 const int64_t vo = off[v];
@@ -712,12 +718,51 @@ __global__ void __launch_bounds__(B) k_tri_big_items(const uint32_t* __restrict_
                 // v-mode walks out(u) below the center: the prefix [0, p) of out(u), p = position of the
                 // edge; u-mode skips the edges v-mode takes (od(v) >= vmt and p < od(v))
                 const uint32_t p = (uint32_t)(e - (VM ? vo : b));
-                L.dv[k] = VM ? (p < (uint32_t)d ? p : 0u) : (vmt > 0 && dv >= (uint32_t)vmt && p < dv ? 0u : dv);
+                const uint32_t dw = VM ? (p < (uint32_t)d ? p : 0u) : (vmt > 0 && dv >= (uint32_t)vmt && p < dv ? 0u : dv);
+                L.dv[k] = dw;
+                if (LISTS && dw > 64u) lk[atomicAdd(&nc[0], 1u)] = (uint16_t)k;
+                else if (LISTS && dw > 0u) sk[atomicAdd(&nc[1], 1u)] = (uint16_t)k;
             }
             __syncthreads();
             if (LISTS) {
                 const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-                for (int k = wave; k < vn; k += B / 64) {
+                const int nlong = (int)__builtin_amdgcn_readfirstlane(nc[0]);
+                const int nshort = (int)__builtin_amdgcn_readfirstlane(nc[1]);
+                // short lists (most of them: the median v-mode prefix is ≈56 entries at s = 20): four per
+                // pass of the wave, 16 lanes each, four loads per lane -- four lists' lines in flight at
+                // once instead of one list's one or two.  The list index is per lane (vector registers:
+                // U uniform list bases would cost the SGPR budget above)
+                for (int q0 = wave * 4; q0 < nshort; q0 += (B / 64) * 4) {
+                    const int g = lane >> 4, e = lane & 15;
+                    const bool live = q0 + g < nshort;
+                    const int k = sk[live ? q0 + g : q0];
+                    const int64_t vo = L.voff[k];
+                    const uint32_t dvk = live ? L.dv[k] : 0u, last = (dvk ? dvk : 1u) - 1u;
+                    uint32_t w[4], word[4], bit[4], keep = 0;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) w[t] = tg[vo + (int64_t)min((uint32_t)(e + 16 * t), last)];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        bit[t] = bbit(tid(w[t], tc), kBigBloomBits);
+                        word[t] = L.bf[bit[t] >> 5];
+                    }
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        keep |= ((uint32_t)((uint32_t)(e + 16 * t) < dvk) & (word[t] >> (bit[t] & 31))) << t;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        if (!((keep >> t) & 1u)) continue;
+                        const int sl = hfind(L.hk, lc, tid(w[t], tc), tc.idmask());
+                        if (sl >= 0) {
+                            const uint64_t pxw = tpay(w[t], tc, ov, vo + e + 16 * t);
+                            const uint64_t pcw = tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]);
+                            const uint64_t puv = L.vp[k];
+                            acc += VM ? tri_weight(puv, pcw, pxw) : tri_weight(puv, pxw, pcw);
+                        }
+                    }
+                }
+                for (int q = wave; q < nlong; q += B / 64) {  // long lists: one per wave, U x 64 entries a pass
+                    const int k = lk[q];
                     const int64_t vo = uniform64(L.voff[k]);
                     const int64_t dv = (int64_t)__builtin_amdgcn_readfirstlane(L.dv[k]);
                     const uint64_t puv = L.vp[k];
