@@ -607,6 +607,12 @@ constexpr int kVChunk = 256;
 // lists against it (one chunk per item rebuilt the same hash for every 256 lists: at C4 the items'
 // setup without their walks took 12-13 ms of each launch)
 constexpr int kVGroup = 8;
+// lanes per short list in the item walks (lists of <= 4 kSG entries: 64 / kSG of them per wave pass)
+#ifndef CAPSMI_TRI_SG
+#define CAPSMI_TRI_SG 16
+#endif
+constexpr int kSG = CAPSMI_TRI_SG;
+static_assert(kSG == 8 || kSG == 16 || kSG == 32, "short-list lanes");
 
 // Items run in B-lane workgroups with hash chunks of 2 B out-list entries (4 slots each): 1024 lanes
 // for v-mode (hub centers with long out-lists), 512 for u-mode, whose many small items are bound by
@@ -720,7 +726,7 @@ __global__ void __launch_bounds__(B, 8) k_tri_big_items(const uint32_t* __restri
                 const uint32_t p = (uint32_t)(e - (VM ? vo : b));
                 const uint32_t dw = VM ? (p < (uint32_t)d ? p : 0u) : (vmt > 0 && dv >= (uint32_t)vmt && p < dv ? 0u : dv);
                 L.dv[k] = dw;
-                if (LISTS && dw > 64u) lk[atomicAdd(&nc[0], 1u)] = (uint16_t)k;
+                if (LISTS && dw > 4u * kSG) lk[atomicAdd(&nc[0], 1u)] = (uint16_t)k;
                 else if (LISTS && dw > 0u) sk[atomicAdd(&nc[1], 1u)] = (uint16_t)k;
             }
             __syncthreads();
@@ -732,15 +738,15 @@ __global__ void __launch_bounds__(B, 8) k_tri_big_items(const uint32_t* __restri
                 // pass of the wave, 16 lanes each, four loads per lane -- four lists' lines in flight at
                 // once instead of one list's one or two.  The list index is per lane (vector registers:
                 // U uniform list bases would cost the SGPR budget above)
-                for (int q0 = wave * 4; q0 < nshort; q0 += (B / 64) * 4) {
-                    const int g = lane >> 4, e = lane & 15;
+                for (int q0 = wave * (64 / kSG); q0 < nshort; q0 += (B / 64) * (64 / kSG)) {
+                    const int g = lane / kSG, e = lane % kSG;
                     const bool live = q0 + g < nshort;
                     const int k = sk[live ? q0 + g : q0];
                     const int64_t vo = L.voff[k];
                     const uint32_t dvk = live ? L.dv[k] : 0u, last = (dvk ? dvk : 1u) - 1u;
                     uint32_t w[4], word[4], bit[4], keep = 0;
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) w[t] = tg[vo + (int64_t)min((uint32_t)(e + 16 * t), last)];
+                    for (int t = 0; t < 4; ++t) w[t] = tg[vo + (int64_t)min((uint32_t)(e + kSG * t), last)];
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
                         bit[t] = bbit(tid(w[t], tc), kBigBloomBits);
@@ -748,13 +754,13 @@ __global__ void __launch_bounds__(B, 8) k_tri_big_items(const uint32_t* __restri
                     }
 #pragma unroll
                     for (int t = 0; t < 4; ++t)
-                        keep |= ((uint32_t)((uint32_t)(e + 16 * t) < dvk) & (word[t] >> (bit[t] & 31))) << t;
+                        keep |= ((uint32_t)((uint32_t)(e + kSG * t) < dvk) & (word[t] >> (bit[t] & 31))) << t;
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
                         if (!((keep >> t) & 1u)) continue;
                         const int sl = hfind(L.hk, lc, tid(w[t], tc), tc.idmask());
                         if (sl >= 0) {
-                            const uint64_t pxw = tpay(w[t], tc, ov, vo + e + 16 * t);
+                            const uint64_t pxw = tpay(w[t], tc, ov, vo + e + kSG * t);
                             const uint64_t pcw = tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]);
                             const uint64_t puv = L.vp[k];
                             acc += VM ? tri_weight(puv, pcw, pxw) : tri_weight(puv, pxw, pcw);
