@@ -629,7 +629,8 @@ struct ItemLds {
     uint32_t dv[kVChunk];
     uint32_t pre[kVChunk];  // flat walk: prefix sums; list walks: the long and short lists' indexes (2 x uint16)
     uint32_t wtot[B / 64];
-    uint32_t ncnt[4];  // list walks: [2 (c & 1) + 0/1] long / short lists of chunk c
+    uint16_t mk[kVChunk];  // list walks: the medium lists' indexes
+    uint32_t ncnt[6];  // list walks: [3 (c & 1) + 0/1/2] long / short / medium lists of chunk c
     unsigned long long item;
 };
 
@@ -699,7 +700,7 @@ __global__ void __launch_bounds__(B, 8) k_tri_big_items(const uint32_t* __restri
         while ((1 << lc) < 4 * hn) ++lc;
         for (int k = threadIdx.x; k < (1 << lc); k += B) L.hk[k] = kEmpty;
         for (int k = threadIdx.x; k < (1 << kBigBloomBits) / 32; k += B) L.bf[k] = 0;
-        if (threadIdx.x < 4) L.ncnt[threadIdx.x] = 0;
+        if (threadIdx.x < 6) L.ncnt[threadIdx.x] = 0;
         __syncthreads();
         for (int k = threadIdx.x; k < hn; k += B) {
             const uint32_t word = tg[b + h0 + k], w = tid(word, tc);
@@ -711,8 +712,8 @@ __global__ void __launch_bounds__(B, 8) k_tri_big_items(const uint32_t* __restri
             if (c > c0) __syncthreads();  // the previous chunk's walks are done with the list table
             uint16_t* lk = reinterpret_cast<uint16_t*>(L.pre);  // LISTS: lists of > 64 entries
             uint16_t* sk = lk + kVChunk;                        // LISTS: lists of 1..64 entries
-            uint32_t* nc = L.ncnt + 2 * (c & 1);
-            if (LISTS && threadIdx.x < 2) L.ncnt[2 * ((c + 1) & 1) + threadIdx.x] = 0;  // read last by chunk c - 1
+            uint32_t* nc = L.ncnt + 3 * (c & 1);
+            if (LISTS && threadIdx.x < 3) L.ncnt[3 * ((c + 1) & 1) + threadIdx.x] = 0;  // read last by chunk c - 1
             for (int k = threadIdx.x; k < vn; k += B) {
                 const uint32_t v = VM ? itg[nb + v0 + k] : tid(tg[b + v0 + k], tc);
                 const int64_t vo = off[v];
@@ -726,7 +727,8 @@ __global__ void __launch_bounds__(B, 8) k_tri_big_items(const uint32_t* __restri
                 const uint32_t p = (uint32_t)(e - (VM ? vo : b));
                 const uint32_t dw = VM ? (p < (uint32_t)d ? p : 0u) : (vmt > 0 && dv >= (uint32_t)vmt && p < dv ? 0u : dv);
                 L.dv[k] = dw;
-                if (LISTS && dw > 4u * kSG) lk[atomicAdd(&nc[0], 1u)] = (uint16_t)k;
+                if (LISTS && dw > 8u * kSG) lk[atomicAdd(&nc[0], 1u)] = (uint16_t)k;
+                else if (LISTS && dw > 4u * kSG) L.mk[atomicAdd(&nc[2], 1u)] = (uint16_t)k;
                 else if (LISTS && dw > 0u) sk[atomicAdd(&nc[1], 1u)] = (uint16_t)k;
             }
             __syncthreads();
@@ -738,35 +740,42 @@ __global__ void __launch_bounds__(B, 8) k_tri_big_items(const uint32_t* __restri
                 // pass of the wave, 16 lanes each, four loads per lane -- four lists' lines in flight at
                 // once instead of one list's one or two.  The list index is per lane (vector registers:
                 // U uniform list bases would cost the SGPR budget above)
-                for (int q0 = wave * (64 / kSG); q0 < nshort; q0 += (B / 64) * (64 / kSG)) {
-                    const int g = lane / kSG, e = lane % kSG;
-                    const bool live = q0 + g < nshort;
-                    const int k = sk[live ? q0 + g : q0];
-                    const int64_t vo = L.voff[k];
-                    const uint32_t dvk = live ? L.dv[k] : 0u, last = (dvk ? dvk : 1u) - 1u;
-                    uint32_t w[4], word[4], bit[4], keep = 0;
+                const int nmed = (int)__builtin_amdgcn_readfirstlane(nc[2]);
+                // ks[0, nk): lists of <= 4 << sgl entries, (64 >> sgl) per wave pass, 1 << sgl lanes each
+                auto grouped = [&](const uint16_t* ks, int nk, int sgl) {
+                    const int per = 64 >> sgl, sg = 1 << sgl;
+                    for (int q0 = wave * per; q0 < nk; q0 += (B / 64) * per) {
+                        const int g = lane >> sgl, e = lane & (sg - 1);
+                        const bool live = q0 + g < nk;
+                        const int k = ks[live ? q0 + g : q0];
+                        const int64_t vo = L.voff[k];
+                        const uint32_t dvk = live ? L.dv[k] : 0u, last = (dvk ? dvk : 1u) - 1u;
+                        uint32_t w[4], word[4], bit[4], keep = 0;
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) w[t] = tg[vo + (int64_t)min((uint32_t)(e + kSG * t), last)];
+                        for (int t = 0; t < 4; ++t) w[t] = tg[vo + (int64_t)min((uint32_t)(e + sg * t), last)];
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        bit[t] = bbit(tid(w[t], tc), kBigBloomBits);
-                        word[t] = L.bf[bit[t] >> 5];
-                    }
+                        for (int t = 0; t < 4; ++t) {
+                            bit[t] = bbit(tid(w[t], tc), kBigBloomBits);
+                            word[t] = L.bf[bit[t] >> 5];
+                        }
 #pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        keep |= ((uint32_t)((uint32_t)(e + kSG * t) < dvk) & (word[t] >> (bit[t] & 31))) << t;
+                        for (int t = 0; t < 4; ++t)
+                            keep |= ((uint32_t)((uint32_t)(e + sg * t) < dvk) & (word[t] >> (bit[t] & 31))) << t;
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        if (!((keep >> t) & 1u)) continue;
-                        const int sl = hfind(L.hk, lc, tid(w[t], tc), tc.idmask());
-                        if (sl >= 0) {
-                            const uint64_t pxw = tpay(w[t], tc, ov, vo + e + kSG * t);
-                            const uint64_t pcw = tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]);
-                            const uint64_t puv = L.vp[k];
-                            acc += VM ? tri_weight(puv, pcw, pxw) : tri_weight(puv, pxw, pcw);
+                        for (int t = 0; t < 4; ++t) {
+                            if (!((keep >> t) & 1u)) continue;
+                            const int sl = hfind(L.hk, lc, tid(w[t], tc), tc.idmask());
+                            if (sl >= 0) {
+                                const uint64_t pxw = tpay(w[t], tc, ov, vo + e + sg * t);
+                                const uint64_t pcw = tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]);
+                                const uint64_t puv = L.vp[k];
+                                acc += VM ? tri_weight(puv, pcw, pxw) : tri_weight(puv, pxw, pcw);
+                            }
                         }
                     }
-                }
+                };
+                grouped(sk, nshort, kSG == 8 ? 3 : kSG == 16 ? 4 : 5);
+                grouped(L.mk, nmed, kSG == 8 ? 4 : kSG == 16 ? 5 : 6);
                 for (int q = wave; q < nlong; q += B / 64) {  // long lists: one per wave, U x 64 entries a pass
                     const int k = lk[q];
                     const int64_t vo = uniform64(L.voff[k]);
