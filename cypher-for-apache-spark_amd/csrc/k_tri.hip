@@ -507,7 +507,44 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         if (LISTS) {
-            for (int k = 0; k < d; ++k) {
+            // lists of <= 64 / <= 128 entries walked four / two per pass (as in k_tri_big_items), the
+            // rest one per pass with U loads per lane
+            const uint64_t sm = __ballot(dv > 0u && dv <= 64u), mm = __ballot(dv > 64u && dv <= 128u);
+            uint64_t lm = __ballot(dv > 128u);
+            auto grouped = [&](uint64_t mask, int sgl) {
+                const int per = 64 >> sgl, sg = 1 << sgl, g = lane >> sgl, e = lane & (sg - 1);
+                while (mask) {  // wave-uniform
+                    uint64_t m = mask;
+                    for (int i = 0; i < g; ++i) m &= m - 1;  // this lane group's list: the g-th of the mask
+                    const bool live = m != 0;
+                    const int k = __builtin_ctzll(live ? m : mask);
+                    for (int i = 0; i < per; ++i) mask &= mask - 1;
+                    const int64_t vo = W.voff[k];
+                    const uint32_t dvk = live ? W.dv[k] : 0u, last = (dvk ? dvk : 1u) - 1u;
+                    uint32_t w[4], word[4], bit[4], keep = 0;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) w[t] = tg[vo + (int64_t)min((uint32_t)(e + sg * t), last)];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        bit[t] = bbit(tid(w[t], tc), kSmallBloomBits);
+                        word[t] = W.bf[bit[t] >> 5];
+                    }
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        keep |= ((uint32_t)((uint32_t)(e + sg * t) < dvk) & (word[t] >> (bit[t] & 31))) << t;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        if (!((keep >> t) & 1u)) continue;
+                        const int sl = hfind(W.hk, 9, tid(w[t], tc), ~0u);
+                        if (sl >= 0) acc += tri_weight(W.vp[k], tpay(w[t], tc, ov, vo + e + sg * t), W.vp[W.hi[sl]]);
+                    }
+                }
+            };
+            grouped(sm, 4);
+            grouped(mm, 5);
+            while (lm) {  // wave-uniform
+                const int k = __builtin_ctzll(lm);
+                lm &= lm - 1;
                 const int64_t vo = uniform64(W.voff[k]);
                 const uint32_t dvk = __builtin_amdgcn_readfirstlane(W.dv[k]);
                 const uint64_t puv = W.vp[k];
