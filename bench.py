@@ -46,6 +46,10 @@ C3_COUNT_QUERY = {"clauses": [{"match": "(a:Person)-[:FRIEND_OF]->(b:Person)-[:F
                   "return": {"items": [["n", ["count*"]]]}}
 C3_QUERY = {"clauses": [{"match": "(a:Person)-[:FRIEND_OF]->(b:Person)-[:FRIEND_OF]->(c:Person)"}],
             "return": {"items": [["count(DISTINCT c)", ["count_distinct", ["id", "c"]]]]}}
+C4_QUERY = {"clauses": [{"match": "(a:Person)-[r1:FRIEND_OF]->(b:Person)-[r2:FRIEND_OF]->(c:Person)-[r3:FRIEND_OF]->(a)"}],
+            "return": {"items": [["n", ["count*"]]]}}
+C5_QUERY = {"clauses": [{"match": "(a:Person)-[:KNOWS*1..3]->(b:Person)"}],
+            "return": {"items": [["id", ["id", "a"]], ["count", ["count*"]]]}}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 KERNELS = ("part_scatter1", "part_scatter2_hop1", "part_scatter2", "hop1", "hop2", "mid_combine", "bitmap_add",
            "bitmap_range",
@@ -78,6 +82,9 @@ def parse():
     p.add_argument("--c2-route", default="direct", choices=("direct", "planner", "joins"),
                    help="C2: explicit expand kernels (direct), Planner(sg).run routed to the fused expand "
                         "(planner), or the same plan operator by operator through the generic radix joins (joins)")
+    p.add_argument("--direct-multi", action="store_true",
+                   help="C4/C5 at N > 1: the explicit-kernel calls of rounds 1-3 (replicated trigraph build; "
+                        "hand-wired varlen shards) instead of the routed query")
     p.add_argument("--workload", default="c3", choices=("c2", "c3", "c4", "c5"),
                    help="c3 (default, the BASELINE metric) or the single-GPU C2/C4/C5 lines (SURVEY.md 8d)")
     return p.parse_args()
@@ -575,6 +582,11 @@ SINGLE_SYMBOL = {"direct_join_probe": "k_direct_probe", "radix_join_count": "k_j
                  "varlen_w": "k_vl_w", "varlen_t": "k_vl_t", "varlen_rev": "k_vl_bset", "varlen_recip": "k_vl_recip", "varlen_cand": "k_vl_cins", "triangles": "k_tri_big_items+k_tri_small"}
 
 
+def route_counts(sess):
+    names = ("expand", "expand_count", "two_hop", "triangle", "var_length", "miss")
+    return ", ".join(f"{k} {sess.route_count(k)}" for k in names if sess.route_count(k))
+
+
 def run_single(args):
     """C2 / C4 / C5 on one GPU: cold = the whole query from resident entity tables.
     value = matched rows / s; matched rows = the query's bindings (C2: result rows; C4: count(*);
@@ -602,8 +614,20 @@ def run_single(args):
         init_dist(dist, local)
     sess = Session(local)
     sess.set_stream(torch.cuda.current_stream().cuda_stream)
-    shard_c5 = wl == "c5" and world > 1
-    if shard_c5:  # ingest (untimed): out-relationships of owned sources + in-relationships from other ranks
+    # N > 1, C4 / C5: the drop-in route over a distributed graph -- every rank runs
+    # Planner(sg).run over its shard; libcapsmi's distributed routes exchange through RCCL (C4: the pairs
+    # to their lower end's owner and the oriented ranges, all-gathered; C5: owner(source) shards whose
+    # in-relationships were exchanged at registration, od / Y all-reduced).  Ingest is untimed.
+    dist_route = world > 1 and wl in ("c4", "c5") and not args.direct_multi
+    shard_c5 = wl == "c5" and world > 1 and not dist_route
+    if dist_route:
+        from capsmi.dist import distribute, join_ranks
+        join_ranks(sess)
+        by = "source" if wl == "c5" else "target"
+        rels_all = graph.rmat_rels(sess, scale, 0, m, probs, 42)
+        rels = rels_all.owned_rows(by, 0, n).as_rel_table("id", "source", "target")
+        del rels_all
+    elif shard_c5:  # ingest (untimed): out-relationships of owned sources + in-relationships from other ranks
         wb, we = graph.owner_words(n, rank, world)
         own_lo, own_hi = min(32 * wb, n), min(32 * we, n)
         rels = graph.rmat_rels(sess, scale, 0, m, probs, 42, part_col=graph.PART_SOURCE, part=rank, nparts=world)
@@ -618,18 +642,29 @@ def run_single(args):
         rels = graph.rmat_rels(sess, scale, 0, m, probs, 42)
     kind = graph.NODES_PERSON if wl == "c2" else graph.NODES_ALL
     nodes = graph.rmat_nodes(sess, scale, kind, 42)
+    if dist_route:
+        nodes = nodes.owned_rows("id", 0, n).as_node_table("id")
+        distribute(sess, 0, n, [nodes], [rels], nodes_owned=True, rels_by=by)
     sess.sync()
     pred = Ands((BinOp(">=", Col("age"), Lit(18)), BinOp("<", Col("age"), Lit(65))))
     cache = {}
-    route = args.c2_route if wl == "c2" and world == 1 else "direct"
+    route = args.c2_route if wl == "c2" and world == 1 else ("planner" if dist_route else "direct")
     if route != "direct":
         from capsmi.planner import EntityTable, Planner, ScanGraph
-        sg = ScanGraph(sess, [EntityTable("node", frozenset({"Person"}), {"age": 0}, nodes, id_col="id")],
-                       [EntityTable("rel", frozenset({"FRIEND_OF"}), {}, rels, id_col="id", src_col="source",
-                                    dst_col="target")])
+        props = {"age": 0} if wl == "c2" else {}
+        sg = ScanGraph(sess, [EntityTable("node", frozenset({"Person"}), props, nodes, id_col="id")],
+                       [EntityTable("rel", frozenset({"KNOWS" if wl == "c5" else "FRIEND_OF"}), {}, rels, id_col="id",
+                                    src_col="source", dst_col="target")])
         sess.set_fused(route == "planner")
 
     def step():
+        if route != "direct" and wl == "c4":  # the routed query on every rank; the count is whole on each
+            t, outs = Planner(sg).run(C4_QUERY)
+            return int(t.column(outs[0][2]).values[0]), None
+        if route != "direct" and wl == "c5":  # rows of this rank's owned start nodes (partitioned)
+            t, outs = Planner(sg).run(C5_QUERY)
+            t.size  # materialise inside the timed region
+            return None, t
         if route != "direct":  # the Cypher query through the planner mirror
             t, outs = Planner(sg).run(C2_QUERY)
             cache["outs"] = [outs[0][2], outs[1][2]]
@@ -702,13 +737,13 @@ def run_single(args):
     check = None
     if wl == "c5":
         res = int(out.column("count").values.sum())  # untimed export
-        if shard_c5:  # the ranks' rows are disjoint: total = sum; rank 0 checks the unsharded answer
+        if shard_c5 or dist_route:  # the ranks' rows are disjoint: total = sum; rank 0 checks the unsharded answer
             t = torch.tensor([res], dtype=torch.int64, device="cuda")
             dist.all_reduce(t)
             res = int(t.item())
             if rank == 0:
                 full = graph.rmat_rels(sess, scale, 0, m, probs, 42)
-                ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id")
+                ok = graph.NodeBitmap(sess, 0, n).add_scan(graph.rmat_nodes(sess, scale, graph.NODES_ALL, 42), "id")
                 ref = int(graph.var_length_count(sess, [full], ok, ok, 1, 3).column("count").values.sum())
                 check = "ok" if ref == res else f"MISMATCH {res} vs unsharded {ref}"
                 del full
@@ -767,7 +802,15 @@ def run_single(args):
                   "query_frac_of_peak": b_alg / sec / 1e9 / HBM_PEAK_GBS,
                   "kernel_ms": {k: v[1] / v[0] for k, v in kt.items()}},
     }
-    if shard_c5:
+    if dist_route:
+        line["config"]["route"] = f"Planner(sg).run over a distributed graph ({route_counts(sess)})"
+        line["config"]["parallelism"] = (
+            f"C4 over {world} GPU(s): relationships by owner(target); undirected pairs exchanged (all-to-all) to "
+            f"their lower end's owner, oriented ranges exchanged by degree order and all-gathered into a replicated "
+            f"oriented graph, work-balanced center shares, one all-reduce" if wl == "c4" else
+            f"C5 over {world} GPU(s): owner(source) shards, in-relationships exchanged (all-to-all) at registration; "
+            f"od and Y all-reduced between phases; each rank the rows of its owned start nodes")
+    elif shard_c5:
         line["config"]["parallelism"] = (f"owner(source) shards over {world} GPU(s); od and Y all-reduced between "
                                          f"phases; in-relationships exchanged at ingest")
     elif wl == "c2" and world > 1:

@@ -85,7 +85,13 @@ STRS = POINTER(c_char_p)
 INTERN_FN = ctypes.CFUNCTYPE(c_int64, c_void_p, ctypes.POINTER(ctypes.c_char), c_size_t)
 # capsmi_collective_fn(ctx, op, send, recv, count, dtype) -> 0 on success
 COLLECTIVE_FN = ctypes.CFUNCTYPE(c_int32, c_void_p, c_int32, c_void_p, c_void_p, c_int64, c_int32)
-COLL_ALL_GATHER, COLL_ALL_REDUCE_SUM, COLL_ALL_REDUCE_MAX, COLL_U32 = 0, 1, 2, 100
+COLL_ALL_GATHER, COLL_ALL_REDUCE_SUM, COLL_ALL_REDUCE_MAX, COLL_ALL_TO_ALL_V, COLL_U32 = 0, 1, 2, 3, 100
+
+
+class CollVec(ctypes.Structure):
+    """capsmi_coll_vec: one side of an ALL_TO_ALL_V (device data, host counts per rank)."""
+    _fields_ = [("data", c_void_p), ("counts", POINTER(c_int64))]
+
 NODES_REPLICATED, NODES_OWNED = 0, 1
 RELS_BY_SOURCE, RELS_BY_TARGET = 0, 1
 

@@ -6,10 +6,15 @@ One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  The l
 pointers on the session's stream; they are wrapped as torch tensors (``__cuda_array_interface__``,
 zero-copy) and the collective runs on torch's current stream -- the session runs on that same stream
 (``Session.set_stream``), so kernels and collectives stay in one order.  With the gloo backend (a
-rehearsal of several ranks on one GPU) the stream is drained around each collective.
+rehearsal of several ranks on one GPU) the stream is drained around each collective, and the
+all-to-all goes through host copies (gloo's all-to-all takes host tensors).
+
+The ALL_TO_ALL_V is Spark's Exchange hashpartitioning (SparkTable.scala:133, 226): the library has
+exchanged the per-rank counts already (an ALL_GATHER), so both count lists arrive with the call.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Sequence
 
 from . import _lib
@@ -28,18 +33,40 @@ class _DevPtr:
 
 def device_view(ptr: int, count: int, dtype: int):
     import torch
+    if count == 0 or not ptr:
+        return torch.empty(0, dtype=torch.int64 if dtype == 0 else torch.int32, device="cuda")
     return torch.as_tensor(_DevPtr(ptr, count, _DT[dtype]), device="cuda")
 
 
-class TorchCollective:
-    """capsmi_collective_fn over torch.distributed (RCCL or, for rehearsals, gloo)."""
+def host_view(ptr: int, count: int, dtype: int):
+    """A host buffer as a tensor (no copy): the collective over host memory (CPU rehearsals / tests)."""
+    import torch
+    tdt = torch.int64 if dtype == 0 else torch.int32
+    if count == 0 or not ptr:
+        return torch.empty(0, dtype=tdt)
+    ct = ctypes.c_int64 if dtype == 0 else ctypes.c_int32
+    return torch.frombuffer((ct * int(count)).from_address(int(ptr)), dtype=tdt)
 
-    def __init__(self, group=None):
+
+def a2av_lists(send: int, recv: int, world: int):
+    """(send data, send counts, recv data, recv counts) of an ALL_TO_ALL_V call's descriptors."""
+    sv = _lib.CollVec.from_address(int(send))
+    rv = _lib.CollVec.from_address(int(recv))
+    return sv.data or 0, [int(sv.counts[q]) for q in range(world)], rv.data or 0, [int(rv.counts[q]) for q in range(world)]
+
+
+class TorchCollective:
+    """capsmi_collective_fn over torch.distributed (RCCL or, for rehearsals, gloo).  `device="cpu"`
+    takes host pointers (the gloo CPU tests of the exchange logic)."""
+
+    def __init__(self, group=None, device: str = "cuda"):
         import torch.distributed as dist
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group)
-        self.drain = dist.get_backend(group) != "nccl"
+        self.device = device
+        self.drain = device == "cuda" and dist.get_backend(group) != "nccl"
+        self.view = device_view if device == "cuda" else host_view
 
     def __call__(self, op: int, send: int, recv: int, count: int, dtype: int) -> None:
         import torch
@@ -47,14 +74,24 @@ class TorchCollective:
         if self.drain:
             torch.cuda.current_stream().synchronize()
         if op == _lib.COLL_ALL_GATHER:
-            dist.all_gather_into_tensor(device_view(recv, count * self.world, dtype), device_view(send, count, dtype),
+            dist.all_gather_into_tensor(self.view(recv, count * self.world, dtype), self.view(send, count, dtype),
                                         group=self.group)
         elif op in (_lib.COLL_ALL_REDUCE_SUM, _lib.COLL_ALL_REDUCE_MAX):
-            r = device_view(recv, count, dtype)
+            r = self.view(recv, count, dtype)
             if send != recv:
-                r.copy_(device_view(send, count, dtype))
+                r.copy_(self.view(send, count, dtype))
             dist.all_reduce(r, op=dist.ReduceOp.SUM if op == _lib.COLL_ALL_REDUCE_SUM else dist.ReduceOp.MAX,
                             group=self.group)
+        elif op == _lib.COLL_ALL_TO_ALL_V:
+            assert count == self.world, (count, self.world)
+            sd, sc, rd, rc = a2av_lists(send, recv, self.world)
+            inp, out = self.view(sd, sum(sc), dtype), self.view(rd, sum(rc), dtype)
+            if self.drain:  # gloo: host tensors
+                host = torch.empty(sum(rc), dtype=out.dtype)
+                dist.all_to_all_single(host, inp.cpu(), output_split_sizes=rc, input_split_sizes=sc, group=self.group)
+                out.copy_(host)
+            else:
+                dist.all_to_all_single(out, inp, output_split_sizes=rc, input_split_sizes=sc, group=self.group)
         else:
             raise ValueError(f"collective op {op}")
         if self.drain:
@@ -70,7 +107,8 @@ def join_ranks(session: Session, group=None) -> None:
 def distribute(session: Session, id_lo: int, id_hi: int, nodes: Sequence[GpuTable], rels: Sequence[GpuTable],
                nodes_owned: bool = True, rels_by: str = "target") -> None:
     """Register this rank's entity tables as its shard of a graph over ids [id_lo, id_hi)
-    (include/capsmi.h capsmi_graph_distribute)."""
+    (include/capsmi.h capsmi_graph_distribute).  rels_by="source" also exchanges the relationships into
+    this rank's owned ids from other ranks' sources (the shard's in-relationships)."""
     na = (_lib.c_void_p * max(1, len(nodes)))(*[t.handle for t in nodes])
     ra = (_lib.c_void_p * max(1, len(rels)))(*[t.handle for t in rels])
     _lib.call("capsmi_graph_distribute", session.handle, id_lo, id_hi, len(nodes), na,

@@ -784,32 +784,50 @@ capsmi_status capsmi_table_export_list(const capsmi_table* t, int32_t col, int64
     use_device(t->sess);
     hipStream_t st = t->sess->stream;
     const ListStore& L = *c.list;
-    // the rows' list indices and validity, then the store's offsets and values (one round trip)
-    std::vector<int64_t> idx(n), off(L.nlists + 1), vals(L.nvalues);
+    // the rows' list indices and validity first; then only the span of the store those rows reference
+    // (the lists of a slice of a group result are one contiguous run of the store), so exporting a
+    // slice moves the slice's lists, and the size probe (host_values == NULL) moves no values at all
+    std::vector<int64_t> idx(n);
     std::vector<uint8_t> ok(n, 1);
     if (n) HIP_CHECK(hipMemcpyAsync(idx.data(), c.d() + offset, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st));
     if (n && c.valid) HIP_CHECK(hipMemcpyAsync(ok.data(), c.v() + offset, n, hipMemcpyDeviceToHost, st));
-    HIP_CHECK(hipMemcpyAsync(off.data(), P<int64_t>(L.offsets), sizeof(int64_t) * (L.nlists + 1), hipMemcpyDeviceToHost, st));
-    if (L.nvalues)
-        HIP_CHECK(hipMemcpyAsync(vals.data(), P<int64_t>(L.values), sizeof(int64_t) * L.nvalues, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    int64_t total = 0;
+    int64_t lmin = INT64_MAX, lmax = -1;
     for (int64_t i = 0; i < n; ++i) {
         if (!ok[i]) continue;
         REQUIRE(idx[i] >= 0 && idx[i] < L.nlists, CAPSMI_ERR_INTERNAL, "list row index out of range");
-        total += off[idx[i] + 1] - off[idx[i]];
+        lmin = std::min(lmin, idx[i]);
+        lmax = std::max(lmax, idx[i]);
     }
+    std::vector<int64_t> off;  // offsets of lists [lmin, lmax + 1]
+    if (lmax >= 0) {
+        off.resize(lmax - lmin + 2);
+        HIP_CHECK(hipMemcpyAsync(off.data(), P<int64_t>(L.offsets) + lmin, sizeof(int64_t) * off.size(),
+                                 hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+    }
+    int64_t total = 0;
+    for (int64_t i = 0; i < n; ++i)
+        if (ok[i]) total += off[idx[i] - lmin + 1] - off[idx[i] - lmin];
     *nvalues = total;
     if (!host_values) return CAPSMI_OK;
     need(host_offsets, "host_offsets");
     REQUIRE(values_cap >= total, CAPSMI_ERR_ILLEGAL_ARGUMENT, "list value buffer too small");
+    std::vector<int64_t> vals;  // values of the span
+    if (lmax >= 0 && off.back() > off.front()) {
+        vals.resize(off.back() - off.front());
+        HIP_CHECK(hipMemcpyAsync(vals.data(), P<int64_t>(L.values) + off.front(), sizeof(int64_t) * vals.size(),
+                                 hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+    }
     int64_t* out = static_cast<int64_t*>(host_values);
     int64_t pos = 0;
     for (int64_t i = 0; i < n; ++i) {
         host_offsets[i] = pos;
         if (host_valid) host_valid[i] = ok[i];
         if (!ok[i]) continue;
-        for (int64_t k = off[idx[i]]; k < off[idx[i] + 1]; ++k) out[pos++] = vals[k];
+        const int64_t b = off[idx[i] - lmin] - off.front(), e = off[idx[i] - lmin + 1] - off.front();
+        for (int64_t k = b; k < e; ++k) out[pos++] = vals[k];
     }
     host_offsets[n] = pos;
     API_END

@@ -192,6 +192,10 @@ struct capsmi_table {
     std::shared_ptr<capsmi::DenseIds> dense;
     capsmi::Column did, dsrc, ddst;
     std::shared_ptr<const capsmi::Shard> shard;  // this rank's shard of a distributed graph
+    // BY_SOURCE relationship shards: the relationships of other ranks' sources into this rank's owned ids
+    // (dense source / target, exchanged at capsmi_graph_distribute)
+    capsmi::Column in_src, in_dst;
+    int64_t in_rows = 0;
     bool partitioned = false;  // rows are this rank's partition of a distributed result
     std::map<std::string, std::shared_ptr<capsmi_relpart>> layouts;
     bool lazy() const { return (bool)plan; }
@@ -280,6 +284,14 @@ std::shared_ptr<ListStore> collect_lists(capsmi_session* s, const int64_t* gid, 
 std::shared_ptr<ListStore> concat_lists(capsmi_session* s, const ListStore& a, const ListStore& b);
 // multi-GPU (k_dist.hip): the session's collective, stream-ordered (capsmi_collective_fn)
 void collective(capsmi_session* s, int op, const void* send, void* recv, int64_t count, int dtype);
+// ALL_TO_ALL_V with host count lists (world entries each)
+void collective_a2av(capsmi_session* s, const void* send, const int64_t* send_counts, void* recv,
+                     const int64_t* recv_counts, int dtype);
+// hash Exchange of u64 words to rank dest[i] (low byte; 0xFF: not sent); dest / words are reordered
+// scratch; returns the received words (rank-major), *nrecv of them; synchronises
+Buf exchange_words(capsmi_session* s, uint64_t* dest, uint64_t* words, int64_t n, int64_t* nrecv);
+// every rank's words concatenated in rank order; synchronises
+Buf gather_words(capsmi_session* s, const uint64_t* words, int64_t n, int64_t* ntotal);
 // the scrambled domain of [lo, hi) over `world` ranks: kbits, mul, mul_inv, slice words, domain size
 struct Scramble {
     int kbits;
@@ -393,9 +405,23 @@ struct TriGraph {
     int vmt = 0;
     Buf ioff, itg, ipos, vm_c;
     int64_t nvm = 0;
+    // ek / ev entries (= ne on one device; on a rank of a distributed build the undirected edges whose
+    // lower end it owns, while ok / tg hold every oriented edge)
+    int64_t nek = 0;
+    bool dist = false;
+    // per-center work estimates (list entries walked) for the work-balanced shares of tri_count: prefix
+    // sums over big_u / vm_c / small_u, nbig + 1 / nvm + 1 / nsmall + 1 entries, host copies (empty:
+    // equal center counts)
+    std::vector<int64_t> wbig, wvm, wsmall;
+};
+// a distributed build (multi-GPU C4): this rank's relationships are any 1/world of them; the owner of a
+// dense id x is x / span
+struct TriDist {
+    int rank = 0, world = 1;
+    int64_t span = 0;
 };
 void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
-               const capsmi_bitmap* n_ok, TriGraph& g);
+               const capsmi_bitmap* n_ok, TriGraph& g, const TriDist* dd = nullptr);
 uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts);
 
 // undirected Expand patterns (k_undirected.hip): hops 1 or 2; kind 0 count(*), 1 count(DISTINCT end),

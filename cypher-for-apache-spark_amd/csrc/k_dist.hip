@@ -50,6 +50,41 @@ __global__ void k_unscramble(int64_t* __restrict__ v, int64_t n, int64_t lo, uin
         v[i] = (int64_t)(((uint64_t)v[i] * mul_inv) & mask) + lo;
 }
 
+// counts[q] = #{i : low byte of the sorted dest[i] == q}, q < world: one binary search per rank boundary
+__global__ void k_dest_counts(const uint64_t* __restrict__ dest, int64_t n, int world, int64_t* __restrict__ counts) {
+    const int q = threadIdx.x;
+    if (q > world) return;
+    __shared__ int64_t at[257];
+    int64_t a = 0, b = n;  // first i with dest[i] >= q
+    while (a < b) {
+        const int64_t mid = (a + b) >> 1;
+        if ((int64_t)(dest[mid] & 0xFF) < q) a = mid + 1; else b = mid;
+    }
+    at[q] = a;
+    __syncthreads();
+    if (q < world) counts[q] = at[q + 1] - at[q];
+}
+
+// (source, target) rows whose target another rank owns -> one word source << 32 | target to that rank
+__global__ void k_in_words(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, int64_t span,
+                           int rank, int world, uint64_t* __restrict__ dest, uint64_t* __restrict__ w) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = dst[i];
+        int q = (int)(t / span);
+        q = q < world ? q : world - 1;
+        dest[i] = q == rank ? 0xFF : (uint64_t)q;
+        w[i] = ((uint64_t)src[i] << 32) | (uint64_t)t;
+    }
+}
+
+__global__ void k_unpack_words(const uint64_t* __restrict__ w, int64_t n, int64_t* __restrict__ a,
+                               int64_t* __restrict__ b) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        a[i] = (int64_t)(w[i] >> 32);
+        b[i] = (int64_t)(uint32_t)w[i];
+    }
+}
+
 __global__ void k_owned_flags(const int64_t* __restrict__ in, int64_t n, int64_t lo, int64_t hi, uint64_t mul,
                               uint64_t mask, int64_t own_lo, int64_t own_hi, uint8_t* __restrict__ flags) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -66,6 +101,77 @@ void collective(capsmi_session* s, int op, const void* send, void* recv, int64_t
             "a distributed route needs the session's collective (capsmi_session_set_ranks)");
     const int32_t rc = s->coll(s->coll_ctx, op, send, recv, count, dtype);
     REQUIRE(rc == 0, CAPSMI_ERR_DEVICE, "the host collective failed (op " + std::to_string(op) + ")");
+}
+
+void collective_a2av(capsmi_session* s, const void* send, const int64_t* send_counts, void* recv,
+                     const int64_t* recv_counts, int dtype) {
+    capsmi_coll_vec sv{const_cast<void*>(send), send_counts}, rv{recv, recv_counts};
+    collective(s, CAPSMI_COLL_ALL_TO_ALL_V, &sv, &rv, s->world, dtype);
+}
+
+// The hash Exchange of u64 words (SparkTable.scala:133, 226 insert one before every join and grouping):
+// word i goes to rank dest[i] (its low byte; 0xFF = keep it out of the exchange).  One stable 8-bit radix
+// pass groups the words by destination, an ALL_GATHER of the per-rank counts gives every rank the whole
+// count matrix, and one ALL_TO_ALL_V moves the words.  dest and words are scratch (reordered).  Returns
+// the received words, rank-major by source rank; synchronises (the counts come to the host).
+Buf exchange_words(capsmi_session* s, uint64_t* dest, uint64_t* words, int64_t n, int64_t* nrecv) {
+    const int W = s->world;
+    REQUIRE(W >= 1 && W < 255, CAPSMI_ERR_UNSUPPORTED, "exchange: at most 254 ranks");
+    hipStream_t st = s->stream;
+    radix_sort_digits(s, dest, reinterpret_cast<int64_t*>(words), n, {0});
+    Buf cnt = dev_alloc(sizeof(int64_t) * (W + (size_t)W * W), s);
+    int64_t* mine = P<int64_t>(cnt);
+    int64_t* all = mine + W;
+    if (n > 0) {
+        hipLaunchKernelGGL(k_dest_counts, dim3(1), dim3(256), 0, st, dest, n, W, mine);
+        HIP_CHECK(hipGetLastError());
+    } else {
+        HIP_CHECK(hipMemsetAsync(mine, 0, sizeof(int64_t) * W, st));
+    }
+    collective(s, CAPSMI_COLL_ALL_GATHER, mine, all, W, CAPSMI_I64);
+    std::vector<int64_t> m((size_t)W * W);
+    HIP_CHECK(hipMemcpyAsync(m.data(), all, sizeof(int64_t) * m.size(), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    std::vector<int64_t> sc(W), rc(W);
+    int64_t tot = 0;
+    for (int q = 0; q < W; ++q) {
+        sc[q] = m[(size_t)s->rank * W + q];  // row r of the matrix: what this rank sends to q
+        rc[q] = m[(size_t)q * W + s->rank];
+        tot += rc[q];
+    }
+    Buf out = dev_alloc(sizeof(uint64_t) * (tot > 0 ? tot : 1), s);
+    collective_a2av(s, words, sc.data(), P<void>(out), rc.data(), CAPSMI_I64);
+    *nrecv = tot;
+    return out;
+}
+
+// every rank's n words, concatenated in rank order (counts first, then one ALL_GATHER padded to the
+// largest share, compacted on the device); synchronises
+Buf gather_words(capsmi_session* s, const uint64_t* words, int64_t n, int64_t* ntotal) {
+    const int W = s->world;
+    hipStream_t st = s->stream;
+    Buf cnt = dev_alloc(sizeof(int64_t) * (1 + W), s);
+    fill_i64(P<int64_t>(cnt), n, 1, st);
+    collective(s, CAPSMI_COLL_ALL_GATHER, P<int64_t>(cnt), P<int64_t>(cnt) + 1, 1, CAPSMI_I64);
+    std::vector<int64_t> c(W);
+    HIP_CHECK(hipMemcpyAsync(c.data(), P<int64_t>(cnt) + 1, sizeof(int64_t) * W, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    int64_t mx = 0, tot = 0;
+    for (int64_t x : c) { mx = std::max(mx, x); tot += x; }
+    Buf pad = dev_alloc(sizeof(uint64_t) * (mx > 0 ? mx : 1), s);
+    if (n > 0) HIP_CHECK(hipMemcpyAsync(P<void>(pad), words, sizeof(uint64_t) * n, hipMemcpyDeviceToDevice, st));
+    Buf all = dev_alloc(sizeof(uint64_t) * (size_t)(mx > 0 ? mx : 1) * W, s);
+    if (mx > 0) collective(s, CAPSMI_COLL_ALL_GATHER, P<void>(pad), P<void>(all), mx, CAPSMI_I64);
+    Buf out = dev_alloc(sizeof(uint64_t) * (tot > 0 ? tot : 1), s);
+    int64_t at = 0;
+    for (int q = 0; q < W; ++q) {
+        if (c[q] > 0)
+            HIP_CHECK(hipMemcpyAsync(P<uint64_t>(out) + at, P<uint64_t>(all) + (size_t)q * mx, sizeof(uint64_t) * c[q],
+                                     hipMemcpyDeviceToDevice, st));
+        at += c[q];
+    }
+    *ntotal = tot;
+    return out;
 }
 
 Scramble make_scramble(int64_t lo, int64_t hi, int world) {
@@ -176,6 +282,11 @@ capsmi_status capsmi_graph_distribute(capsmi_session* s, int64_t id_lo, int64_t 
             "relationship mode");
     HIP_CHECK(hipSetDevice(s->device));
     const Scramble sc = make_scramble(id_lo, id_hi, s->world);
+    // the routes run on the padded scrambled domain (whole word slices per rank): refuse here, not at
+    // every later query, a window whose padding takes it past the 2^30 ids the fused kernels address
+    REQUIRE(sc.n <= (int64_t(1) << 30), CAPSMI_ERR_UNSUPPORTED,
+            "distributed graph: the id domain padded to " + std::to_string(s->world) + " whole word slices holds " +
+                std::to_string(sc.n) + " ids, above 2^30");
     const int64_t own_lo = (int64_t)s->rank * 32 * sc.slice_words, own_hi = own_lo + 32 * sc.slice_words;
     Buf bad = dev_alloc(2 * sizeof(unsigned long long), s);
     HIP_CHECK(hipMemsetAsync(P<void>(bad), 0, 2 * sizeof(unsigned long long), s->stream));
@@ -241,6 +352,28 @@ capsmi_status capsmi_graph_distribute(capsmi_session* s, int64_t id_lo, int64_t 
         p.t->shard = sh;
         p.t->partitioned = s->world > 1 && !(sh->kind == 1 && node_mode == CAPSMI_NODES_REPLICATED);
         p.t->layouts.clear();
+        p.t->in_src = p.t->in_dst = Column();
+        p.t->in_rows = 0;
+        // BY_SOURCE: the relationships into this rank's owned ids from other ranks' sources, by one
+        // exchange (every rank takes part, in table order), kept with the shard
+        if (sh->kind == 2 && rel_mode == CAPSMI_RELS_BY_SOURCE && (s->world > 1 || s->coll)) {
+            const int64_t m = p.t->nrows;
+            Buf dest = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s), w = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s);
+            if (m > 0)
+                hipLaunchKernelGGL(k_in_words, dim3(grid_for(m)), dim3(256), 0, s->stream, P<int64_t>(p.a.data),
+                                   P<int64_t>(p.b.data), m, 32 * sc.slice_words, s->rank,
+                                   s->world, P<uint64_t>(dest), P<uint64_t>(w));
+            HIP_CHECK(hipGetLastError());
+            int64_t nin = 0;
+            Buf got = exchange_words(s, P<uint64_t>(dest), P<uint64_t>(w), m, &nin);
+            p.t->in_src = key_column(s, nin);
+            p.t->in_dst = key_column(s, nin);
+            if (nin > 0)
+                hipLaunchKernelGGL(k_unpack_words, dim3(grid_for(nin)), dim3(256), 0, s->stream, P<uint64_t>(got), nin,
+                                   P<int64_t>(p.t->in_src.data), P<int64_t>(p.t->in_dst.data));
+            HIP_CHECK(hipGetLastError());
+            p.t->in_rows = nin;
+        }
     }
     D_END
 }

@@ -13,6 +13,8 @@
 // undirected edge from the lower (degree, id) end and intersecting sorted out-lists.  The two
 // directed multiplicities of each undirected edge ride along with the oriented adjacency, so the
 // intersection loop reads no other table.
+#include <algorithm>
+
 #include "capsmi_impl.h"
 
 namespace capsmi {
@@ -911,6 +913,84 @@ __global__ void k_self_terms(const uint32_t* __restrict__ sl, int64_t n, unsigne
     if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
 }
 
+// ---- the distributed build (multi-GPU C4) --------------------------------------------------------
+// destination of an undirected key: the owner of its lower end, which then holds every relationship of
+// the pair (kNone: dropped, not sent)
+__global__ void k_tri_dest_min(const uint64_t* __restrict__ key, int64_t m, int64_t span, int world,
+                               uint64_t* __restrict__ dest) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = key[i];
+        const int64_t q = k == kNone ? 0xFF : (int64_t)(k >> 32) / span;
+        dest[i] = (uint64_t)(k == kNone ? 0xFF : (q < world ? q : world - 1));
+    }
+}
+
+constexpr int kHistBins = 4096;
+
+// coarse histogram of the oriented keys' sources (degree-order id >> hb)
+__global__ void k_tri_from_hist(const uint64_t* __restrict__ ok_, int64_t ne, int hb,
+                                unsigned long long* __restrict__ hist) {
+    __shared__ unsigned int h[kHistBins];
+    for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) h[b] = 0;
+    __syncthreads();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&h[(uint32_t)(ok_[i] >> 32) >> hb], 1u);
+    __syncthreads();
+    for (int b = threadIdx.x; b < kHistBins; b += blockDim.x)
+        if (h[b]) atomicAdd(&hist[b], (unsigned long long)h[b]);
+}
+
+// destination of an oriented key: the rank whose range of source bins [bbeg[q], bbeg[q + 1]) holds it
+__global__ void k_tri_dest_from(const uint64_t* __restrict__ ok_, int64_t ne, int hb, const int64_t* __restrict__ bbeg,
+                                int world, uint64_t* __restrict__ dest) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t bin = (int64_t)((uint32_t)(ok_[i] >> 32) >> hb);
+        int a = 0, b = world - 1;  // the last q with bbeg[q] <= bin
+        while (a < b) {
+            const int mid = (a + b + 1) >> 1;
+            if (bbeg[mid] <= bin) a = mid; else b = mid - 1;
+        }
+        dest[i] = (uint64_t)a;
+    }
+}
+
+// Work of a u-mode center (the list entries its walks read): out(u) for the hash, and out(v) for every
+// edge u -> v at position p that u-mode takes (not od(v) >= vmt with p < od(v)); one wave per center
+__global__ void k_tri_work_u(const int64_t* __restrict__ cs, int64_t nc, const int64_t* __restrict__ off,
+                             const uint32_t* __restrict__ tg, uint32_t idmask, int vmt, int64_t* __restrict__ w) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < nc;
+         c += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        const int64_t u = cs[c], b = off[u], d = off[u + 1] - b;
+        int64_t acc = 0;
+        for (int64_t p = lane; p < d; p += 64) {
+            const uint32_t v = tg[b + p] & idmask;
+            const int64_t odv = off[v + 1] - off[v];
+            if (!(vmt > 0 && odv >= vmt && p < odv)) acc += odv;
+        }
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+        if (lane == 0) w[c] = acc + d;
+    }
+}
+
+// work of a v-mode center: out(v) for the hash and the prefix out(u)[0, p) of every in-edge it takes
+__global__ void k_tri_work_v(const int64_t* __restrict__ cs, int64_t nc, const int64_t* __restrict__ off,
+                             const int64_t* __restrict__ ioff, const uint32_t* __restrict__ ipos,
+                             int64_t* __restrict__ w) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < nc;
+         c += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        const int64_t v = cs[c], odv = off[v + 1] - off[v];
+        int64_t acc = 0;
+        for (int64_t j = ioff[v] + lane; j < ioff[v + 1]; j += 64) {
+            const int64_t p = ipos[j];
+            if (p < odv) acc += p;
+        }
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+        if (lane == 0) w[c] = acc + odv;
+    }
+}
+
 inline int grid(const capsmi_session* s, int64_t n) {
     int64_t g = (n + 255) / 256;
     const int64_t cap = (int64_t)s->num_cus * 16;
@@ -927,17 +1007,28 @@ inline int bits_for(uint64_t range) {
 
 }  // namespace tri
 
+// Distributed (dd != null, multi-GPU C4): every rank builds from its 1/world of the
+// relationships and ends with the same replicated oriented graph.  The undirected keys go to the owner of
+// their lower end (one exchange), so each rank sorts 1/world of them and holds every relationship of its
+// pairs (exact multiplicities); degrees and self-loop counts are summed over the ranks; each rank orients
+// its pairs, sends the oriented keys to the rank of their source's degree-order range (ranges balanced by
+// a coarse all-reduced histogram), sorts its range, and one all-gather in rank order concatenates the
+// sorted ranges into the whole sorted key array.  The in-lists and bins are then built from it on every
+// rank (replicated), with per-center work estimates for tri_count's balanced shares.
 void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
-               const capsmi_bitmap* n_ok, TriGraph& g) {
+               const capsmi_bitmap* n_ok, TriGraph& g, const TriDist* dd) {
     using namespace tri;
     hipStream_t st = s->stream;
     const int64_t lo = n_ok->lo, hi = n_ok->hi, n = hi - lo;
     REQUIRE(n > 0 && (uint64_t)n <= (uint64_t(1) << 31), CAPSMI_ERR_UNSUPPORTED, "triangle count needs <= 2^31 ids");
     g.lo = lo;
     g.n = n;
+    g.dist = dd != nullptr;
     int64_t m = 0;
     for (int i = 0; i < nt; ++i) m += ms[i];
     const int bits = bits_for((uint64_t)n);
+    REQUIRE(!dd || (bits + 7) / 8 * 8 <= 24, CAPSMI_ERR_UNSUPPORTED,
+            "distributed triangle count: at most 2^24 ids (coded oriented keys)");
     // the direction bit rides unsorted at bit 31 when max's digits end at or below bit 24
     const int msh = bits > 24 ? 1 : 0;
     g.sl = dev_alloc(sizeof(uint32_t) * n, s);
@@ -954,6 +1045,17 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
             off += ms[i];
         }
     }
+    if (dd) {  // every relationship of a pair to the owner of the pair's lower end
+        KernelTimer kt(s, "tri_exchange");
+        Buf dest = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s);
+        if (m > 0)
+            hipLaunchKernelGGL(k_tri_dest_min, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, dd->span,
+                               dd->world, P<uint64_t>(dest));
+        HIP_CHECK(hipGetLastError());
+        int64_t mr = 0;
+        key = exchange_words(s, P<uint64_t>(dest), P<uint64_t>(key), m, &mr);
+        m = mr;
+    }
     // one sort of the undirected keys: digits of max (and the direction bit when msh) then of min; the
     // upper ends' degrees are counted between the two halves, while the keys are in max order
     Buf deg = dev_alloc(sizeof(uint32_t) * n, s);
@@ -969,7 +1071,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     const uint64_t dmask = msh ? ~1ULL : ~(1ULL << 31);
     Buf f = dev_alloc(m > 0 ? m : 1, s), heads;
     hipLaunchKernelGGL(k_heads, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, dmask, P<uint8_t>(f));
-    const int64_t ne = flags_to_indices(s, P<uint8_t>(f), m, heads);
+    int64_t ne = flags_to_indices(s, P<uint8_t>(f), m, heads);
     Buf nv = dev_alloc(sizeof(int64_t) + sizeof(unsigned long long), s);  // nvalid, long-run count
     HIP_CHECK(hipMemsetAsync(P<void>(nv), 0, sizeof(int64_t) + sizeof(unsigned long long), st));
     int64_t* nvalid_p = P<int64_t>(nv);
@@ -989,6 +1091,11 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     key.reset();
     f.reset();
     heads.reset();
+    g.nek = ne;
+    if (dd) {  // a pair's relationships are all on one rank: the sums over the ranks are exact
+        collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<uint32_t>(deg), P<uint32_t>(deg), n, CAPSMI_COLL_U32);
+        collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<uint32_t>(g.sl), P<uint32_t>(g.sl), n, CAPSMI_COLL_U32);
+    }
     // degree-order ids (hubs first): sort the vertices by (degree, id)
     Buf rid = dev_alloc(sizeof(uint32_t) * n, s);
     g.orig = dev_alloc(sizeof(int64_t) * n, s);
@@ -1019,8 +1126,54 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     std::vector<int> od;  // (source, target): grouped and target-sorted lists
     for (int sh = 0; sh < bits; sh += 8) od.push_back(sh);
     for (int sh = 32; sh < 32 + bits; sh += 8) od.push_back(sh);
-    // no kNone among the oriented keys; coded: key-only (the payloads ride in the key)
-    radix_sort_digits(s, P<uint64_t>(g.ok), tc.cb ? nullptr : P<int64_t>(g.ov), ne, od);
+    if (dd) {
+        KernelTimer kt(s, "tri_exchange");
+        // the exceptions' exact payloads (rare): every rank's list, for the placement in the whole key array
+        const int64_t nexc = (int64_t)read_scalar(s, reinterpret_cast<const int64_t*>(nlong));
+        int64_t nexc_all = 0;
+        exc = gather_words(s, P<uint64_t>(exc), 2 * nexc, &nexc_all);
+        fill_i64(reinterpret_cast<int64_t*>(nlong), nexc_all / 2, 1, st);
+        // source ranges of coarse degree-order bins, balanced by the all-reduced bin counts
+        const int hb = bits > 12 ? bits - 12 : 0;
+        const int64_t nbins = ((n - 1) >> hb) + 1;
+        const int W = dd->world;
+        Buf hist = dev_alloc(sizeof(int64_t) * (kHistBins + W + 1), s);
+        HIP_CHECK(hipMemsetAsync(P<void>(hist), 0, sizeof(int64_t) * kHistBins, st));
+        if (ne > 0)
+            hipLaunchKernelGGL(k_tri_from_hist, dim3(std::min(grid(s, ne), 4 * s->num_cus)), dim3(1024), 0, st,
+                               P<uint64_t>(g.ok), ne, hb, P<unsigned long long>(hist));
+        HIP_CHECK(hipGetLastError());
+        collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(hist), P<int64_t>(hist), kHistBins, CAPSMI_I64);
+        std::vector<int64_t> h(kHistBins), bb(W + 1);
+        HIP_CHECK(hipMemcpyAsync(h.data(), P<int64_t>(hist), sizeof(int64_t) * kHistBins, hipMemcpyDeviceToHost, st));
+        HIP_CHECK(hipStreamSynchronize(st));
+        int64_t tot = 0;
+        for (int64_t b = 0; b < nbins; ++b) tot += h[b];
+        int64_t cum = 0, b = 0;
+        bb[0] = 0;
+        for (int q = 1; q < W; ++q) {
+            const int64_t want = tot * q / W;
+            while (b < nbins && cum + h[b] <= want) cum += h[b++];
+            bb[q] = b;
+        }
+        bb[W] = nbins;
+        int64_t* bbeg = P<int64_t>(hist) + kHistBins;
+        HIP_CHECK(hipMemcpyAsync(bbeg, bb.data(), sizeof(int64_t) * (W + 1), hipMemcpyHostToDevice, st));
+        Buf dest = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), s);
+        if (ne > 0)
+            hipLaunchKernelGGL(k_tri_dest_from, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, hb, bbeg, W,
+                               P<uint64_t>(dest));
+        HIP_CHECK(hipGetLastError());
+        int64_t nr = 0;
+        Buf mine = exchange_words(s, P<uint64_t>(dest), P<uint64_t>(g.ok), ne, &nr);
+        radix_sort_digits(s, P<uint64_t>(mine), nullptr, nr, od);  // this rank's source range, sorted
+        g.ok = gather_words(s, P<uint64_t>(mine), nr, &ne);          // the ranges in rank order: all sorted
+        g.ov = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);
+    } else {
+        // no kNone among the oriented keys; coded: key-only (the payloads ride in the key)
+        radix_sort_digits(s, P<uint64_t>(g.ok), tc.cb ? nullptr : P<int64_t>(g.ov), ne, od);
+    }
+    g.ne = ne;
     if (tc.cb && ne > 0)
         hipLaunchKernelGGL(k_exc_place, dim3(grid(s, ne / 64 + 1)), dim3(256), 0, st, P<uint64_t>(exc), nlong,
                            P<uint64_t>(g.ok), ne, tc, P<int64_t>(g.ov));
@@ -1067,6 +1220,29 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     g.nsmall = flags_to_indices(s, P<uint8_t>(fsm), n, g.small_u);
     g.nbig = flags_to_indices(s, P<uint8_t>(fbg), n, g.big_u);
     HIP_CHECK(hipGetLastError());
+    if (dd) {  // work-balanced shares: prefix sums of the centers' walked entries, host copies
+        auto work = [&](const Buf& cs, int64_t nc, bool vm, std::vector<int64_t>& out) {
+            Buf w = dev_alloc(sizeof(int64_t) * (2 * nc + 2), s);
+            if (nc > 0) {
+                const unsigned gw = (unsigned)std::min<int64_t>((nc + 3) / 4, (int64_t)s->num_cus * 16);
+                if (vm)
+                    hipLaunchKernelGGL(k_tri_work_v, dim3(gw), dim3(256), 0, st, P<int64_t>(cs), nc, P<int64_t>(g.off),
+                                       P<int64_t>(g.ioff), P<uint32_t>(g.ipos), P<int64_t>(w));
+                else
+                    hipLaunchKernelGGL(k_tri_work_u, dim3(gw), dim3(256), 0, st, P<int64_t>(cs), nc, P<int64_t>(g.off),
+                                       P<uint32_t>(g.tg), tc.idmask(), g.vmt, P<int64_t>(w));
+                HIP_CHECK(hipGetLastError());
+            }
+            exclusive_scan_i64(P<int64_t>(w), P<int64_t>(w) + nc + 1, nc, s);
+            out.resize(nc + 1);
+            HIP_CHECK(hipMemcpyAsync(out.data(), P<int64_t>(w) + nc + 1, sizeof(int64_t) * (nc + 1),
+                                     hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+        };
+        work(g.big_u, g.nbig, false, g.wbig);
+        work(g.vm_c, g.nvm, true, g.wvm);
+        work(g.small_u, g.nsmall, false, g.wsmall);
+    }
 }
 
 // count for vertex share `part` of `nparts` (each bin sliced evenly); pair/self terms with part 0
@@ -1077,9 +1253,25 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
     HIP_CHECK(hipMemsetAsync(P<void>(out), 0, 24, st));
     {
         KernelTimer kt(s, "triangles");
-        const int64_t sb = g.nsmall * part / nparts, se = g.nsmall * (part + 1) / nparts;
-        const int64_t bb = g.nbig * part / nparts, be = g.nbig * (part + 1) / nparts;
-        const int64_t vb = g.nvm * part / nparts, ve = g.nvm * (part + 1) / nparts;
+        // this part's slice of each center list: equal work (the walked-entry prefix sums of a distributed
+        // build), else equal center counts
+        auto share = [&](int64_t nc, const std::vector<int64_t>& w, int64_t& b, int64_t& e) {
+            if (nc > 0 && w.size() == (size_t)nc + 1 && w[nc] > 0) {
+                auto at = [&](int q) -> int64_t {
+                    if (q >= nparts) return nc;
+                    return std::lower_bound(w.begin(), w.end(), w[nc] * q / nparts) - w.begin();
+                };
+                b = std::min(at(part), nc);
+                e = std::min(at(part + 1), nc);
+            } else {
+                b = nc * part / nparts;
+                e = nc * (part + 1) / nparts;
+            }
+        };
+        int64_t sb, se, bb, be, vb, ve;
+        share(g.nsmall, g.wsmall, sb, se);
+        share(g.nbig, g.wbig, bb, be);
+        share(g.nvm, g.wvm, vb, ve);
         const TgCode tc{(uint32_t)g.ib, (uint32_t)g.cb};
         const char* walk = getenv("CAPSMI_TRI_WALK");  // "flat": the prefix-sum walk (A/B runs)
         const bool lists = !(walk && std::string(walk) == "flat");
@@ -1132,13 +1324,14 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
                                P<unsigned long long>(out));
         }
     }
-    if (part == 0) {
-        if (g.ne > 0)
-            hipLaunchKernelGGL(k_pair_terms, dim3(grid(s, g.ne)), dim3(256), 0, st, P<uint64_t>(g.ek), P<int64_t>(g.ev),
-                               g.ne, P<uint32_t>(g.sl), P<unsigned long long>(out) + 1);
+    // pair terms over this graph's undirected edges (a distributed build's ek holds this rank's pairs, so
+    // every part adds its own), self terms once
+    if ((part == 0 || g.dist) && g.nek > 0)
+        hipLaunchKernelGGL(k_pair_terms, dim3(grid(s, g.nek)), dim3(256), 0, st, P<uint64_t>(g.ek), P<int64_t>(g.ev),
+                           g.nek, P<uint32_t>(g.sl), P<unsigned long long>(out) + 1);
+    if (part == 0)
         hipLaunchKernelGGL(k_self_terms, dim3(grid(s, g.n)), dim3(256), 0, st, P<uint32_t>(g.sl), g.n,
                            P<unsigned long long>(out) + 2);
-    }
     HIP_CHECK(hipGetLastError());
     uint64_t h[3];
     HIP_CHECK(hipMemcpyAsync(h, P<void>(out), 24, hipMemcpyDeviceToHost, st));

@@ -50,6 +50,7 @@ __device__ __forceinline__ void block_add(unsigned long long* acc, unsigned long
         for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += part[i];
         if (t) atomicAdd(acc, t);
     }
+    __syncthreads();  // part[] is reused by the next call: thread 0 must have read it first
 }
 
 // arcs leaving / entering each id and the r1 = r2 bindings (count(*) of the 2-hop, and the 1-hop arcs)

@@ -636,6 +636,7 @@ thread_local DistView g_dist;
 bool dist_window(const std::vector<Path>& B, bool* any, int64_t* lo, int64_t* hi) {
     const DenseIds* d = nullptr;
     const Shard* sh = nullptr;
+    const capsmi_session* sess = nullptr;
     bool all = true;
     int rel_mode = -1;
     *any = false;
@@ -646,6 +647,7 @@ bool dist_window(const std::vector<Path>& B, bool* any, int64_t* lo, int64_t* hi
                 const capsmi_table* t = m.base;
                 if (!t->shard) { all = false; continue; }
                 *any = true;
+                sess = t->sess;
                 const DenseIds* e = t->dense.get();  // one domain: equal scramble (tables distributed apart)
                 if (d && (e->n != d->n || e->kbits != d->kbits || e->lo != d->lo || e->mul != d->mul)) return false;
                 d = e;
@@ -664,7 +666,9 @@ bool dist_window(const std::vector<Path>& B, bool* any, int64_t* lo, int64_t* hi
     g_dense = d;
     *lo = 0;
     *hi = d->n;
-    if (sh->world > 1) {
+    // world 1 with a collective: the distributed routes over the one shard (their exchanges run through
+    // the collective, e.g. RCCL at world size 1)
+    if (sh->world > 1 || (sess && sess->coll != nullptr)) {
         g_dist.on = true;
         g_dist.rank = sh->rank;
         g_dist.world = sh->world;
@@ -967,6 +971,27 @@ int64_t dist_two_hop_count(capsmi_session* s, int32_t nt, capsmi_table* const* v
     return read_scalar(s, P<int64_t>(cnt));
 }
 
+// the cyclic triangle count over a distributed graph (any relationship mode): the distributed trigraph
+// build (k_tri.hip tri_build: pairs exchanged to their lower end's owner, oriented ranges exchanged and
+// all-gathered), this rank's work share of the centers, one all-reduce of the parts
+int64_t dist_triangle_count(capsmi_session* s, const std::vector<capsmi_table*>& views, const capsmi_bitmap* n_ok) {
+    std::vector<const int64_t*> srcs, dsts;
+    std::vector<int64_t> ms;
+    for (capsmi_table* t : views) {
+        srcs.push_back(t->cols[0].d());
+        dsts.push_back(t->cols[1].d());
+        ms.push_back(t->nrows);
+    }
+    TriDist dd;
+    dd.rank = g_dist.rank;
+    dd.world = g_dist.world;
+    dd.span = 32 * g_dist.slice_words;
+    TriGraph g;
+    tri_build(s, srcs.data(), dsts.data(), ms.data(), (int)srcs.size(), n_ok, g, &dd);
+    const uint64_t part = tri_count(s, g, g_dist.rank, g_dist.world);
+    return sum_over_ranks(s, (int64_t)part);
+}
+
 // count(*) / count(DISTINCT end | start) of one branch: 1 hop, a 2-hop chain, or the closed triangle.
 // Returns false when the shape or a precondition does not hold.
 bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kinds, std::vector<int64_t>& vals) {
@@ -1049,7 +1074,7 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
         route(s, "two_hop");
         return true;
     }
-    if (nh == 3 && P.pos_node.size() == 3 && same_orientation(P) && !g_dist.on) {
+    if (nh == 3 && P.pos_node.size() == 3 && same_orientation(P)) {
         // P0 -h0-> P1 -h1-> P2 -h2-> P0 (the closing hop is the ExpandInto)
         const Hop &h0 = P.hops[0], &h1 = P.hops[1], &h2 = P.hops[2];
         if (!(h0.from == 0 && h0.to == 1 && h1.from == 1 && h1.to == 2 && h2.from == 2 && h2.to == 0)) return false;
@@ -1064,7 +1089,8 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
         capsmi_bitmap* cc = node_bitmap(s, P, c, P.pos_node[2], lo, hi, bs, &k2);
         if (!a || !b || !cc || k0 != k1 || k1 != k2) return false;  // one node filter for all three
         int64_t x = 0;
-        check(capsmi_triangle_count(s, (int32_t)nt, v0.t.data(), "s", "t", a, &x));
+        if (g_dist.on) x = dist_triangle_count(s, v0.t, a);
+        else check(capsmi_triangle_count(s, (int32_t)nt, v0.t.data(), "s", "t", a, &x));
         vals.assign(kinds.size(), x);
         route(s, "triangle");
         return true;
@@ -1224,6 +1250,53 @@ bool fused_grouped_two_hop(capsmi_session* s, const capsmi_table* in, const Plan
     return true;
 }
 
+// The var-length grouped count over BY_SOURCE shards: this rank owns the
+// start ids [rank * span, (rank + 1) * span) and holds their out-relationships (`views`) plus the
+// relationships into its owned ids from other ranks (the bases' in-shards, exchanged at registration).
+// begin (owned od, reverse multiplicities) -> all-reduce od -> mid (owned Y) -> all-reduce Y -> finish:
+// the (relative dense id, count) rows of the owned start nodes.
+void dist_var_length(capsmi_session* s, const std::vector<capsmi_table*>& views,
+                     const std::vector<const capsmi_table*>& bases, const capsmi_bitmap* a, const capsmi_bitmap* b,
+                     int lower, int upper, const std::string& id_name, const std::string& count_name,
+                     capsmi_table** out) {
+    std::vector<const int64_t*> srcs, dsts, isrcs, idsts;
+    std::vector<int64_t> ms, ims;
+    for (capsmi_table* t : views) {
+        srcs.push_back(t->cols[0].d());
+        dsts.push_back(t->cols[1].d());
+        ms.push_back(t->nrows);
+    }
+    for (const capsmi_table* t : bases) {
+        if (t->in_rows <= 0) continue;
+        isrcs.push_back(t->in_src.d());
+        idsts.push_back(t->in_dst.d());
+        ims.push_back(t->in_rows);
+    }
+    const int64_t n = b->hi - b->lo, span = 32 * g_dist.slice_words;
+    const int64_t own_lo = std::min<int64_t>(g_dist.rank * span, n), own_hi = std::min<int64_t>(own_lo + span, n);
+    Buf od = dev_alloc(sizeof(int64_t) * n, s), y = dev_alloc(sizeof(int64_t) * n, s);
+    VarlenShard* v = varlen_shard_begin(s, srcs.data(), dsts.data(), ms.data(), (int)srcs.size(), isrcs.data(),
+                                        idsts.data(), ims.data(), (int)isrcs.size(), a, b, lower, upper, own_lo + b->lo,
+                                        own_hi + b->lo, P<int64_t>(od));
+    std::unique_ptr<VarlenShard, void (*)(VarlenShard*)> hold(v, varlen_shard_free);
+    collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(od), P<int64_t>(od), n, CAPSMI_I64);
+    varlen_shard_mid(v, P<int64_t>(y));
+    collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(y), P<int64_t>(y), n, CAPSMI_I64);
+    Buf ids, cnt;
+    const int64_t rows = varlen_shard_finish(v, ids, cnt);
+    auto* r = result_table(s, rows);
+    Column ic, cc;
+    ic.name = id_name;
+    ic.type = CAPSMI_I64;
+    ic.data = ids;
+    cc.name = count_name;
+    cc.type = CAPSMI_I64;
+    cc.data = cnt;
+    r->cols.push_back(std::move(ic));
+    r->cols.push_back(std::move(cc));
+    *out = r;
+}
+
 // group by the start node, count(*), over the branches of a bounded var-length expand
 bool fused_var_length(capsmi_session* s, const capsmi_table* in, const PlanNode& g, const std::vector<Path>& B,
                       capsmi_table** out) {
@@ -1235,9 +1308,13 @@ bool fused_var_length(capsmi_session* s, const capsmi_table* in, const PlanNode&
     std::string akey, bkey, rsig;
     int64_t lo, hi;
     if (!id_window(B, &lo, &hi)) return false;
+    // the sharded count needs every owned source's out-relationships (BY_SOURCE shards); decided before any
+    // node scan, whose gathers would otherwise run for nothing
+    if (g_dist.on && g_dist.rel_mode != CAPSMI_RELS_BY_SOURCE) return false;
     BitmapSet bs;
     capsmi_bitmap *abm = nullptr, *bbm = nullptr;
     RelViews views;
+    std::vector<const capsmi_table*> bases;  // the relationship tables behind `views` (their in-shards)
     std::string zero_key;  // the zero-length branch's start scan (lower = 0)
     bool first = true;
     for (size_t bi = 0; bi < B.size(); ++bi) {
@@ -1277,10 +1354,16 @@ bool fused_var_length(capsmi_session* s, const capsmi_table* in, const PlanNode&
         capsmi_bitmap* b = node_bitmap(s, P, c, P.pos_node[k], lo, hi, bs, &kb);
         if (!a || !b) return false;
         for (int h = 0; h < k; ++h) {
+            if (g_dist.on && P.hops[h].from_role != ROLE_SRC) return false;  // outgoing over BY_SOURCE shards
             RelViews v;
             rel_views(P, P.hops[h], v);
-            if (first && h == 0) { rsig = v.sig; views.t.swap(v.t); }
-            else if (v.sig != rsig) return false;
+            if (first && h == 0) {
+                rsig = v.sig;
+                views.t.swap(v.t);
+                for (const Member& m : P.inst[P.hops[h].rel].m) bases.push_back(m.base);
+            } else if (v.sig != rsig) {
+                return false;
+            }
         }
         if (first) { akey = ka; bkey = kb; abm = a; bbm = b; first = false; }
         else if (ka != akey || kb != bkey) return false;
@@ -1288,9 +1371,10 @@ bool fused_var_length(capsmi_session* s, const capsmi_table* in, const PlanNode&
     if (first || (lens.count(0) && zero_key != akey)) return false;  // a path of >= 1 hop; one start scan
     const int l = *lens.begin(), u = *lens.rbegin();
     if (l < 0 || u > 3 || u - l + 1 != (int)lens.size()) return false;
-    if (g_dist.on) return false;  // the sharded C5 needs in- and out-relationship shards (capsmi_varlen_shard_*)
-    check(capsmi_var_length_count(s, (int32_t)views.t.size(), views.t.data(), "s", "t", abm, bbm, l, u, g.a[0].c_str(),
-                                  ag.output.c_str(), out));
+    if (g_dist.on) dist_var_length(s, views.t, bases, abm, bbm, l, u, g.a[0], ag.output, out);
+    else
+        check(capsmi_var_length_count(s, (int32_t)views.t.size(), views.t.data(), "s", "t", abm, bbm, l, u,
+                                      g.a[0].c_str(), ag.output.c_str(), out));
     if (g_dense) {  // start ids back to the graph's Long ids
         capsmi_table* r = *out;
         Column& c = r->cols[0];
@@ -1307,6 +1391,7 @@ bool fused_var_length(capsmi_session* s, const capsmi_table* in, const PlanNode&
         c.offset = 0;
         c.host.reset();
     }
+    (*out)->partitioned = g_dist.on && g_dist.world > 1;  // the rows of this rank's owned start nodes
     route(s, "var_length");
     return true;
 }

@@ -527,10 +527,20 @@ capsmi_status capsmi_cluster_by(capsmi_table* rels, const char* key_col, int64_t
  * The collective: enqueue one collective on the session's stream, ordered after the work queued on it
  * and before the work queued after the call returns (e.g. torch.distributed / RCCL on that stream).
  * ALL_GATHER: `count` elements from every rank into recv, rank-major (world x count);
- * ALL_REDUCE_SUM / _MAX: `count` elements, send and recv may be equal.  dtype CAPSMI_I64 (int64) or
- * CAPSMI_COLL_U32 (uint32 words).  Return 0 on success. */
-enum { CAPSMI_COLL_ALL_GATHER = 0, CAPSMI_COLL_ALL_REDUCE_SUM = 1, CAPSMI_COLL_ALL_REDUCE_MAX = 2 };
+ * ALL_REDUCE_SUM / _MAX: `count` elements, send and recv may be equal;
+ * ALL_TO_ALL_V (Spark's Exchange hashpartitioning, SparkTable.scala:133, 226): `send` and `recv` point to
+ * host capsmi_coll_vec descriptors and `count` is the world size; this rank sends send->counts[q]
+ * elements, the q-th rank-major segment of send->data, to rank q and receives recv->counts[q] elements
+ * from rank q into the q-th segment of recv->data (the library has exchanged the counts beforehand with
+ * an ALL_GATHER, so both lists agree across ranks).  dtype CAPSMI_I64 (int64) or CAPSMI_COLL_U32
+ * (uint32 words).  Return 0 on success. */
+enum { CAPSMI_COLL_ALL_GATHER = 0, CAPSMI_COLL_ALL_REDUCE_SUM = 1, CAPSMI_COLL_ALL_REDUCE_MAX = 2,
+       CAPSMI_COLL_ALL_TO_ALL_V = 3 };
 enum { CAPSMI_COLL_U32 = 100 };
+typedef struct {
+    void* data;             /* device buffer, rank-major segments */
+    const int64_t* counts;  /* host, world entries (elements per rank) */
+} capsmi_coll_vec;
 typedef int32_t (*capsmi_collective_fn)(void* ctx, int32_t op, const void* send, void* recv, int64_t count,
                                         int32_t dtype);
 /* this process is rank `rank` of `world`; fn may be NULL only for world == 1 */
@@ -543,13 +553,20 @@ enum { CAPSMI_RELS_BY_SOURCE = 0, CAPSMI_RELS_BY_TARGET = 1 };
  * node tables hold every node row (REPLICATED) or the rows of the ids this rank owns (OWNED);
  * relationship tables hold the relationships whose target (BY_TARGET) or source (BY_SOURCE) this rank
  * owns.  Checked: ids inside the domain and the shard's rows owned (else ILLEGAL_ARGUMENT).  The
- * tables keep their scrambled key columns.  Routed on a distributed graph: Expand projections (rows of
- * this rank's relationships) and count(*) (one SUM all-reduce); with BY_TARGET the 2-hop
- * count(DISTINCT end) (all-gathers of the owned node-scan bitmap words and hop-1 frontier, one
- * all-reduce) and the 2-hop count(*) (an all-gather of the owned in-degrees, one all-reduce).  A
- * plan over a distributed graph that would need another exchange (a generic join, aggregate, distinct
+ * tables keep their scrambled key columns.  With BY_SOURCE, registration also exchanges (ALL_TO_ALL_V)
+ * every relationship whose target another rank owns to that rank, which keeps it as its shard's
+ * in-relationships (the var-length route's reverse multiplicities need them).  Routed on a distributed
+ * graph: Expand projections (rows of this rank's relationships) and count(*) (one SUM all-reduce); with
+ * BY_TARGET the 2-hop count(DISTINCT end) (all-gathers of the owned node-scan bitmap words and hop-1
+ * frontier, one all-reduce) and the 2-hop count(*) (an all-gather of the owned in-degrees, one
+ * all-reduce); either mode: the cyclic triangle count (undirected keys exchanged to the owner of their
+ * lower end, the oriented lists exchanged by degree-order range and all-gathered into a replicated
+ * oriented graph, each rank counting a work share, one all-reduce); with BY_SOURCE the var-length
+ * grouped count (od and Y all-reduced between its phases; the rows of each rank's owned start nodes).
+ * A plan over a distributed graph that would need another exchange (a generic join, aggregate, distinct
  * or ordering over partitioned rows) is CAPSMI_ERR_UNSUPPORTED; capsmi_table_partitioned tells which
- * results hold this rank's rows only. */
+ * results hold this rank's rows only.  A session given a collective at world size 1 runs the same
+ * distributed routes over its single shard (every exchange then goes through the collective). */
 capsmi_status capsmi_graph_distribute(capsmi_session* s, int64_t id_lo, int64_t id_hi, int32_t nnodes,
                                       capsmi_table* const* nodes, int32_t node_mode, int32_t nrels,
                                       capsmi_table* const* rels, int32_t rel_mode);

@@ -86,6 +86,7 @@ object Capsmi {
   final val COLL_ALL_GATHER = 0
   final val COLL_ALL_REDUCE_SUM = 1
   final val COLL_ALL_REDUCE_MAX = 2
+  final val COLL_ALL_TO_ALL_V = 3 // send / recv point to CapsmiCollVec descriptors, count = world size
   final val COLL_U32 = 100
   final val NODES_REPLICATED = 0
   final val NODES_OWNED = 1
@@ -139,6 +140,14 @@ class CapsmiParam extends Structure {
   var count: Int = 0
   var reserved: Int = 0
   var values: Pointer = _
+}
+
+/** capsmi_coll_vec: an ALL_TO_ALL_V side -- device data in rank-major segments, host counts per rank
+  * (inside the CollectiveFn: `Structure.newInstance(classOf[CapsmiCollVec], ptr)` then `read()`). */
+@Structure.FieldOrder(Array("data", "counts"))
+class CapsmiCollVec extends Structure {
+  var data: Pointer = _
+  var counts: Pointer = _
 }
 
 /** capsmi_collective_fn: one collective on the session's stream (e.g. an RCCL communicator the executor

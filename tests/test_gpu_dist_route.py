@@ -1,8 +1,16 @@
-"""The drop-in path on several ranks: 2 ranks sharing the GPU (gloo collectives -- RCCL
-refuses two ranks per device) run Planner(sg).run over their shards of an edge-list graph whose hubs
-sit at ids 0..999.  Ownership is a hash of the id (include/capsmi.h capsmi_graph_distribute), so the
-shards balance even though contiguous id ranges would not; every rank routes the C3 queries to the
-distributed two-hop kernels and gets the whole answer, which must equal the oracle closed form."""
+"""The drop-in path on several ranks: ranks run Planner(sg).run over their shards of a
+distributed graph and libcapsmi routes the plans to the distributed kernels.
+
+- 2 ranks sharing the GPU over gloo (RCCL refuses two ranks per device) on an edge list whose hubs sit
+  at ids 0..999.  Ownership is a hash of the id (include/capsmi.h capsmi_graph_distribute), so the
+  shards balance even though contiguous id ranges would not.  BY_TARGET shards: the C3 queries, the
+  expand, the cached layout, and the cyclic triangle (C4: the distributed trigraph build with its two
+  exchanges); BY_SOURCE shards: the triangle and the var-length grouped count (C5: in-relationships
+  exchanged at registration, od / Y all-reduced, each rank the rows of its owned starts).  Every answer
+  equals the oracle (oracle/closed.c closed forms, pinned by tests/test_oracle_pins.py).
+- 1 rank over RCCL (backend nccl, world size 1): the same routes with every exchange through
+  torch.distributed's NCCL(=RCCL) branch of capsmi.dist.TorchCollective -- all-gathers, all-reduces and
+  the ALL_TO_ALL_V -- against the R-MAT fixtures (tests/golden/rmat_full.json: C3 s = 20, C4 s = 14)."""
 import json
 import os
 import socket
@@ -30,45 +38,100 @@ def _hub_edges(path, seed=7, n=1 << 16, m=400_000, hubs=1000):
     src = np.where(rng.random(m) < 0.5, rng.integers(0, hubs, m), rng.integers(0, n, m))
     dst = np.where(rng.random(m) < 0.5, rng.integers(0, hubs, m), rng.integers(0, n, m))
     src[:500] = dst[:500]  # self-loops
+    src[500:3000], dst[500:3000] = dst[3000:5500], src[3000:5500]  # reciprocal pairs (C5's reverse terms)
     np.savetxt(path, np.stack([src, dst], axis=1), fmt="%d", delimiter=" ")
     return n, src.astype(np.int64), dst.astype(np.int64)
 
 
-def _ranks(edges, lo, hi, world=2, nodes="owned"):
-    env = dict(os.environ, CAPSMI_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+def _ranks(graph, lo, hi, world=2, nodes="owned", rels_by="target", queries="c3,tri", backend="gloo", out=None):
+    env = dict(os.environ, CAPSMI_DIST_BACKEND=backend, MASTER_ADDR="127.0.0.1")
+    out = out or str(graph)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", "dist_route_worker.py"),
-           str(edges), str(lo), str(hi), nodes]
+           str(graph), str(lo), str(hi), nodes, "--rels-by", rels_by, "--queries", queries, "--out", out]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-4000:]
-    out = []
+    res = []
     for r in range(world):
-        with open(f"{edges}.rank{r}.json") as f:
-            out.append(json.load(f))
-    assert sorted(o["rank"] for o in out) == list(range(world))
-    return out
+        with open(f"{out}.rank{r}.json") as f:
+            res.append(json.load(f))
+    assert sorted(o["rank"] for o in res) == list(range(world))
+    return res
 
 
 @pytest.mark.parametrize("nodes", ["owned", "replicated"])
-def test_routed_c3_on_two_ranks_with_hubs(tmp_path, nodes):
+def test_routed_c3_c4_on_two_ranks_with_hubs(tmp_path, nodes):
     from oracle import cpu
     edges = tmp_path / "hubs.txt"
     n, src, dst = _hub_edges(edges)
     lo, hi = int(min(src.min(), dst.min())), int(max(src.max(), dst.max())) + 1
     rows, distinct = cpu.two_hop_closed_form(n, src, dst)
-    out = _ranks(edges, lo, hi, nodes=nodes)
+    tri = cpu.triangle_closed_form(n, src, dst)
+    out = _ranks(edges, lo, hi, nodes=nodes, queries="c3,expand,warm,tri,varlen")
     m = len(src)
     for o in out:  # every rank holds the whole answer
         assert o["count_star"] == rows, o
         assert o["count_distinct_c"] == distinct, o
         assert o["warm_distinct"] == distinct, o
         assert o["expand_count"] == m, o
+        assert o["triangle"] == tri, o
         assert o["expand_partitioned"] is True
         assert o["routes"]["two_hop"] >= 3 and o["routes"]["expand_count"] >= 1 and o["routes"]["expand"] >= 1, o
-        assert o["triangle"].startswith("refused"), o
+        assert o["routes"]["triangle"] >= 1, o
+        assert o["varlen"].startswith("refused"), o  # var-length needs BY_SOURCE shards
     assert sum(o["expand_rows_local"] for o in out) == m
     assert sum(o["rels_local"] for o in out) == m
     mean = m / len(out)
     assert all(abs(o["rels_local"] - mean) / mean < 0.05 for o in out), [o["rels_local"] for o in out]
     # contiguous owner ranges of the raw ids would put the hubs on rank 0
     assert (dst < n // 2).mean() > 0.7
+
+
+def test_routed_c4_c5_by_source_on_two_ranks(tmp_path):
+    from oracle import cpu
+    edges = tmp_path / "hubs_src.txt"
+    n, src, dst = _hub_edges(edges, seed=11, m=200_000)
+    lo, hi = 0, n
+    tri = cpu.triangle_closed_form(n, src, dst)
+    _, per_a = cpu.var_length_closed_form(n, src, dst, 1, 3)
+    out = _ranks(edges, lo, hi, rels_by="source", queries="c3,tri,varlen")
+    got = {}
+    for o in out:
+        assert o["triangle"] == tri, o
+        assert o["c3"].startswith("refused"), o  # the 2-hop routes need BY_TARGET shards
+        assert o["varlen_partitioned"] is True
+        assert o["routes"]["triangle"] >= 1 and o["routes"]["var_length"] >= 1, o
+        for a, c in o["varlen_rows"]:
+            assert a not in got, a  # each start id on exactly one rank
+            got[a] = c
+    want = {int(i): int(per_a[i]) for i in np.nonzero(per_a)[0]}
+    assert got == want
+    assert sum(o["rels_local"] for o in out) == len(src)
+
+
+def _fixture(key):
+    with open(os.path.join(ROOT, "tests", "golden", "rmat_full.json")) as f:
+        return json.load(f)["cases"][key]
+
+
+def test_routes_over_rccl_world1(tmp_path):
+    """The NCCL(=RCCL) branch of TorchCollective (zero-copy device views, no stream drain) under the
+    drop-in route before the driver's multi-GPU run: C3 at s = 20 (BY_TARGET: all-gathers of the node
+    scan, the frontier and the in-degrees, all-reduces) and C4 at s = 14 (BY_SOURCE: the in-relationship
+    ALL_TO_ALL_V at registration, the trigraph build's two exchanges and its all-gathers)."""
+    c3 = _fixture("c3_s20")
+    o = _ranks("rmat:20", 0, 1 << 20, world=1, rels_by="target", queries="c3", backend="nccl",
+               out=str(tmp_path / "r20"))[0]
+    assert o["backend"] == "nccl" and o["world"] == 1
+    assert o["count_distinct_c"] == c3["count_distinct_c"], o
+    assert o["count_star"] == c3["count_star"], o
+    assert o["routes"]["two_hop"] >= 2, o
+    c4 = _fixture("c4_s14")
+    o = _ranks("rmat:14", 0, 1 << 14, world=1, rels_by="source", queries="tri,varlen", backend="nccl",
+               out=str(tmp_path / "r14"))[0]
+    assert o["triangle"] == c4["count_star"], o
+    assert o["routes"]["triangle"] >= 1 and o["routes"]["var_length"] >= 1, o
+    from oracle import cpu
+    src, dst = cpu.rmat_edges(14, 0, 16 << 14)
+    _, per_a = cpu.var_length_closed_form(1 << 14, src, dst, 1, 3)
+    assert {a: c for a, c in o["varlen_rows"]} == {int(i): int(per_a[i]) for i in np.nonzero(per_a)[0]}

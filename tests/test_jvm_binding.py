@@ -59,7 +59,8 @@ def _c_functions():
 
 
 SCALA_STRUCTS = {"ColDesc": "capsmi_col_desc", "CapsmiExpr": "capsmi_expr", "CapsmiExprColumn": "capsmi_expr_column",
-                 "CapsmiAgg": "capsmi_agg", "CapsmiValue": "capsmi_value", "CapsmiParam": "capsmi_param"}
+                 "CapsmiAgg": "capsmi_agg", "CapsmiValue": "capsmi_value", "CapsmiParam": "capsmi_param",
+                 "CapsmiCollVec": "capsmi_coll_vec"}
 
 
 def test_constants_match_header():
