@@ -436,10 +436,24 @@ def main():
         return out
 
     results = {}
+    gate = None
+    if distributed:
+        from capsmi.dist import serial_gate
+        gate = serial_gate()  # CAPSMI_SERIAL_LOCK: the serialised rehearsal of N ranks on one GPU
+    busy = {}
     for mode in modes:
         step = steps[mode]
+        if gate is not None:
+            def step(inner=steps[mode]):
+                gate.acquire()
+                try:
+                    return inner()
+                finally:
+                    gate.release()
         for _ in range(args.warmup):
             res = step()
+        if gate is not None:
+            gate.busy = 0.0
         _lib.call("capsmi_session_set_profiling", sess.handle, 1)
         kernel_times()  # reset
         if distributed:
@@ -458,6 +472,11 @@ def main():
             tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             elapsed = float(tt.item())
+        if gate is not None:
+            bt = torch.zeros(world, dtype=torch.float64, device="cuda")
+            bt[rank] = gate.busy / args.steps * 1e3
+            dist.all_reduce(bt)
+            busy[mode] = [round(x, 3) for x in bt.tolist()]
         results[mode] = (elapsed / args.steps, res, kt)
     if "rp" in cached:
         cached["rp"].release()
@@ -545,16 +564,28 @@ def main():
             line["query"]["rels_max_over_mean"] = max(rels_per_rank) / (sum(rels_per_rank) / world)
         if shards != 1:
             line["config"]["diagnostic"] = f"rank 0's shard of {shards} on one GPU, no exchange (not the metric)"
-        # warm (layout cached): the query reads the cached 8-B packed layout once per hop instead of the
-        # int64 (source, target) scans, plus the three node scans -- its own algorithmic bytes
-        warm_alg = 2 * 8 * m_total + 3 * 8 * n
+        # warm (layout cached): the query reads the cached layout -- 5-B packed pairs --
+        # once per hop, plus the hop bitmaps' slices (the node scans of exact-id tables set a range and
+        # read nothing): its PHYSICAL bytes, not SURVEY's B_alg (which is the cold plan's scans)
+        warm_phys = 2 * 5 * m_total + 3 * n // 8
         for mode in modes[1:]:
             s2, r2, kt2 = results[mode]
-            b2 = warm_alg if mode in ("warm", "direct_warm") else query_alg
-            line["query"][mode] = {"ms_per_step": s2 * 1e3, "value": matched / s2,
-                                   ("count_star" if mode.startswith("count") else "count_distinct_c"): r2,
-                                   "alg_bytes_query": b2, "query_frac_of_peak": b2 / s2 / 1e9 / (HBM_PEAK_GBS * world),
-                                   "kernel_ms": {k: v[1] / v[0] for k, v in kt2.items() if v[0] > 0}}
+            entry = {"ms_per_step": s2 * 1e3, "value": matched / s2,
+                     ("count_star" if mode.startswith("count") else "count_distinct_c"): r2,
+                     "kernel_ms": {k: v[1] / v[0] for k, v in kt2.items() if v[0] > 0}}
+            if mode in ("warm", "direct_warm"):
+                entry.update({"phys_bytes_query": warm_phys,
+                              "phys_basis": "cached 5-B packed layout read once per hop + hop bitmaps",
+                              "phys_frac_of_peak": warm_phys / s2 / 1e9 / (HBM_PEAK_GBS * world)})
+            else:
+                entry.update({"alg_bytes_query": query_alg,
+                              "query_frac_of_peak": query_alg / s2 / 1e9 / (HBM_PEAK_GBS * world)})
+            line["query"][mode] = entry
+        if busy:
+            line["rehearsal"] = {"kind": f"{world} gloo ranks sharing one GPU, GPU work serialised by a lock "
+                                         f"(CAPSMI_SERIAL_LOCK): a rank's busy ms per step is its share on a device of "
+                                         f"its own, collectives excluded; ms_per_step is NOT a multi-GPU time",
+                                 "busy_ms_per_rank": busy}
         line["cpu_baseline"] = cpu_baseline(scale, ef) if (not args.no_cpu_baseline and world == 1) else None
         print(json.dumps(line), flush=True)
         if check is not None and check.startswith("MISMATCH"):
@@ -703,8 +734,25 @@ def run_single(args):
 
     kernels = ("direct_join_probe", "radix_join_count", "radix_join_write", "bitmap_add", "expand_filter", "tri_pack", "triangles", "part_scatter1", "varlen_deg", "varlen_w", "varlen_rev",
                "varlen_cand", "varlen_recip", "varlen_t")
+    gate = None
+    if world > 1:
+        from capsmi.dist import serial_gate
+        gate = serial_gate()  # CAPSMI_SERIAL_LOCK: the serialised rehearsal of N ranks on one GPU
+    inner_step = step
+
+    def step():
+        if gate is None:
+            return inner_step()
+        gate.acquire()
+        try:
+            return inner_step()
+        finally:
+            gate.release()
+
     for _ in range(args.warmup):
         step()
+    if gate is not None:
+        gate.busy = 0.0
     _lib.call("capsmi_session_set_profiling", sess.handle, 1)
     for k in kernels:  # reset
         _lib.call("capsmi_session_kernel_time", sess.handle, k.encode(), ctypes.byref(ctypes.c_int64()),
@@ -802,6 +850,15 @@ def run_single(args):
                   "query_frac_of_peak": b_alg / sec / 1e9 / HBM_PEAK_GBS,
                   "kernel_ms": {k: v[1] / v[0] for k, v in kt.items()}},
     }
+    if gate is not None:  # per-rank busy time of the serialised rehearsal (collectives excluded)
+        bt = torch.zeros(world, dtype=torch.float64, device="cuda")
+        bt[rank] = gate.busy / args.steps * 1e3
+        dist.all_reduce(bt)
+        line["rehearsal"] = {"kind": f"{world} gloo ranks sharing one GPU, GPU work serialised by a lock "
+                                     f"(CAPSMI_SERIAL_LOCK): each rank's busy ms per step is its share on a device of "
+                                     f"its own, collectives excluded; ms_per_step above is NOT a multi-GPU time",
+                             "busy_ms_per_rank": [round(x, 3) for x in bt.tolist()],
+                             "busy_ms_max": round(max(bt.tolist()), 3)}
     if dist_route:
         line["config"]["route"] = f"Planner(sg).run over a distributed graph ({route_counts(sess)})"
         line["config"]["parallelism"] = (

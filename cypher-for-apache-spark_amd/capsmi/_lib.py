@@ -196,6 +196,7 @@ _SIGS = {
                                   INTERN_FN, c_void_p, c_char_p, PP]),
     "capsmi_session_route_count": (c_int32, [P, c_char_p, POINTER(c_int64)]),
     "capsmi_session_set_unrouted_limit": (c_int32, [P, c_int64]),
+    "capsmi_session_set_csv_partitioning": (c_int32, [P, c_int64, c_int64, c_int64]),
     "capsmi_session_set_ranks": (c_int32, [P, c_int32, c_int32, COLLECTIVE_FN, c_void_p]),
     "capsmi_graph_distribute": (c_int32, [P, c_int64, c_int64, c_int32, PP, c_int32, c_int32, PP, c_int32]),
     "capsmi_owned_rows": (c_int32, [P, P, c_char_p, c_int64, c_int64, PP]),

@@ -55,6 +55,48 @@ def a2av_lists(send: int, recv: int, world: int):
     return sv.data or 0, [int(sv.counts[q]) for q in range(world)], rv.data or 0, [int(rv.counts[q]) for q in range(world)]
 
 
+class SerialGate:
+    """A rehearsal of N ranks on one GPU with their GPU work serialised (gloo ranks, CAPSMI_SERIAL_LOCK=
+    <file>): a rank holds an inter-process lock while it runs between collectives and gives it up inside
+    every collective, so no two ranks' kernels overlap and a rank's busy time (lock held) is what its
+    share of the step takes on a device of its own -- the collectives' own time excluded (SURVEY.md 8e
+    per-rank diagnostic; the multi-GPU scaling itself is measured by the driver on an 8-GPU node)."""
+
+    def __init__(self, path: str):
+        import os
+        self.fd = os.open(path, os.O_CREAT | os.O_RDWR, 0o600)
+        self.busy = 0.0
+        self.t0 = None
+
+    def acquire(self) -> None:
+        import fcntl
+        import time
+        fcntl.flock(self.fd, fcntl.LOCK_EX)
+        self.t0 = time.perf_counter()
+
+    def release(self) -> None:
+        import fcntl
+        import time
+        import torch
+        torch.cuda.synchronize()
+        self.busy += time.perf_counter() - self.t0
+        self.t0 = None
+        fcntl.flock(self.fd, fcntl.LOCK_UN)
+
+
+def serial_gate():
+    """The SerialGate of this process when CAPSMI_SERIAL_LOCK is set, else None."""
+    import os
+    global _GATE
+    path = os.environ.get("CAPSMI_SERIAL_LOCK")
+    if path and _GATE is None:
+        _GATE = SerialGate(path)
+    return _GATE
+
+
+_GATE = None
+
+
 class TorchCollective:
     """capsmi_collective_fn over torch.distributed (RCCL or, for rehearsals, gloo).  `device="cpu"`
     takes host pointers (the gloo CPU tests of the exchange logic)."""
@@ -67,12 +109,25 @@ class TorchCollective:
         self.device = device
         self.drain = device == "cuda" and dist.get_backend(group) != "nccl"
         self.view = device_view if device == "cuda" else host_view
+        self.gate = serial_gate() if self.drain else None
 
     def __call__(self, op: int, send: int, recv: int, count: int, dtype: int) -> None:
         import torch
         dist = self.dist
         if self.drain:
             torch.cuda.current_stream().synchronize()
+        gated = self.gate is not None and self.gate.t0 is not None
+        if gated:  # the serialised rehearsal: another rank runs while this one waits in the collective
+            self.gate.release()
+        try:
+            self._run(op, send, recv, count, dtype)
+        finally:
+            if gated:
+                self.gate.acquire()
+
+    def _run(self, op: int, send: int, recv: int, count: int, dtype: int) -> None:
+        import torch
+        dist = self.dist
         if op == _lib.COLL_ALL_GATHER:
             dist.all_gather_into_tensor(self.view(recv, count * self.world, dtype), self.view(send, count, dtype),
                                         group=self.group)

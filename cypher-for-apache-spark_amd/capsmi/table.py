@@ -249,6 +249,13 @@ class Session:
         include/capsmi.h capsmi_session_set_unrouted_limit)."""
         _lib.call("capsmi_session_set_unrouted_limit", self._h, int(max_bytes))
 
+    def set_csv_partitioning(self, default_parallelism: int, max_partition_bytes: int = 128 << 20,
+                             open_cost_bytes: int = 4 << 20) -> None:
+        """read_csv row ids as Spark's monotonically_increasing_id over its file-scan partitions
+        (include/capsmi.h capsmi_session_set_csv_partitioning); 0 = one partition (row numbers)."""
+        _lib.call("capsmi_session_set_csv_partitioning", self._h, int(default_parallelism), int(max_partition_bytes),
+                  int(open_cost_bytes))
+
     def set_ranks(self, rank: int, world: int, collective=None) -> None:
         """This process is rank `rank` of `world`; `collective(op, send_ptr, recv_ptr, count, dtype)`
         runs the exchange on this session's stream (capsmi.dist.TorchCollective; include/capsmi.h

@@ -154,6 +154,9 @@ struct capsmi_session {
     // refuse unrouted joins whose estimated output exceeds this many bytes (0 = no limit;
     // capsmi_session_set_unrouted_limit)
     int64_t unrouted_limit = 0;
+    // capsmi_read_csv row ids over Spark's file-scan partitions (capsmi_session_set_csv_partitioning;
+    // parallelism 0: one partition)
+    int64_t csv_parallelism = 0, csv_max_partition_bytes = int64_t(128) << 20, csv_open_cost = int64_t(4) << 20;
 };
 
 namespace capsmi {

@@ -30,6 +30,7 @@ struct Chunk {
     std::vector<std::vector<uint8_t>> valid;
     std::vector<std::string> arena;                        // STR columns: the field texts back to back
     std::vector<std::vector<std::pair<uint64_t, uint32_t>>> sref;  // per non-null STR field: (arena offset, length)
+    std::vector<int64_t> lstart;  // byte offset in its file of each row's line (Spark partition ids only)
     std::string err;
 };
 
@@ -107,7 +108,7 @@ bool next_field(const char*& p, const char* le, char delim, bool collapse, const
 // tokens are dropped.  A token that does not parse as its column's type is an error (reported with
 // its byte offset) rather than a silent null.
 void parse_chunk(Chunk& c, const char* file_base, const std::string& fname, char delim, char comment,
-                 const std::vector<int32_t>& types) {
+                 const std::vector<int32_t>& types, bool want_pos) {
     const int nc = (int)types.size();
     const bool collapse = delim == 0;  // whitespace-separated (opt-in; Spark's sep is one character)
     c.data.assign(nc, {});
@@ -186,9 +187,67 @@ void parse_chunk(Chunk& c, const char* file_base, const std::string& fname, char
             c.data[k].push_back(w);
             c.valid[k].push_back(null ? 0 : 1);
         }
+        if (want_pos) c.lstart.push_back((int64_t)(p - file_base));
         ++c.rows;
         p = next;
     }
+}
+
+// monotonically_increasing_id over the partitions of Spark 2.2.1's file scan (EdgeListDataSource.scala:86;
+// FileSourceScanExec.createNonBucketedReadRDD, third-party, restated): maxSplitBytes = min(maxPartitionBytes,
+// max(openCostInBytes, totalBytes / defaultParallelism)), totalBytes = sum of (length + openCostInBytes); each
+// file is split every maxSplitBytes; the splits are sorted by length, descending and stable, and packed
+// "next fit" into partitions (a split that would take the partition past maxSplitBytes closes it first; each
+// split adds its length + openCostInBytes).  A split [o, o + len) reads the lines whose first byte lies in
+// (o, o + len], and the file's first line (Hadoop's LineRecordReader skips a split's first, partial line and
+// reads one line past its end).  Partition p's rows are numbered through its splits in order:
+// id = p << 33 | row.  Rows (parsed records) come in file / line order; each gets its id.
+void spark_row_ids(const std::vector<int64_t>& lens, const std::vector<Chunk>& chunks,
+                   const std::vector<size_t>& chunk_file, int64_t par, int64_t max_part, int64_t open_cost,
+                   std::vector<int64_t>& ids) {
+    int64_t total = 0;
+    for (int64_t L : lens) total += L + open_cost;
+    const int64_t per_core = total / par;
+    const int64_t split = std::max<int64_t>(1, std::min(max_part, std::max(open_cost, per_core)));
+    struct Split {
+        size_t f;
+        int64_t k, len, part = 0, base = 0, rows = 0;
+    };
+    std::vector<Split> sp;
+    std::vector<size_t> first(lens.size());  // index of file f's first split
+    for (size_t f = 0; f < lens.size(); ++f) {
+        first[f] = sp.size();
+        for (int64_t o = 0, k = 0; o < lens[f]; o += split, ++k) sp.push_back({f, k, std::min(split, lens[f] - o)});
+    }
+    auto split_of = [&](size_t f, int64_t b) -> size_t {  // the split reading the line that starts at byte b
+        const int64_t k = b == 0 ? 0 : (b - 1) / split;
+        return first[f] + (size_t)k;
+    };
+    for (size_t ci = 0; ci < chunks.size(); ++ci)
+        for (int64_t b : chunks[ci].lstart) sp[split_of(chunk_file[ci], b)].rows += 1;
+    std::vector<size_t> order(sp.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return sp[a].len > sp[b].len; });
+    int64_t part = 0, cur = 0, base = 0;
+    bool open = false;
+    for (size_t i : order) {
+        if (open && cur + sp[i].len > split) {  // closePartition()
+            ++part;
+            cur = 0;
+            base = 0;
+        }
+        sp[i].part = part;
+        sp[i].base = base;
+        base += sp[i].rows;
+        cur += sp[i].len + open_cost;
+        open = true;
+    }
+    std::vector<int64_t> seen(sp.size(), 0);
+    for (size_t ci = 0; ci < chunks.size(); ++ci)
+        for (int64_t b : chunks[ci].lstart) {
+            Split& x = sp[split_of(chunk_file[ci], b)];
+            ids.push_back((x.part << 33) | (x.base + seen[&x - sp.data()]++));
+        }
 }
 
 std::string read_file(const char* path) {
@@ -242,7 +301,8 @@ capsmi_table* read_csv(capsmi_session* s, const std::vector<std::string>& paths,
         for (int i = 0; i < std::min<int>(nt, (int)chunks.size()); ++i)
             th.emplace_back([&] {
                 for (size_t k; (k = next.fetch_add(1)) < chunks.size();)
-                    parse_chunk(chunks[k], texts[chunk_file[k]].data(), paths[chunk_file[k]], delim, comment, types);
+                    parse_chunk(chunks[k], texts[chunk_file[k]].data(), paths[chunk_file[k]], delim, comment, types,
+                                row_id_col != nullptr && s->csv_parallelism > 0);
             });
         for (auto& x : th) x.join();
     }
@@ -269,12 +329,25 @@ capsmi_table* read_csv(capsmi_session* s, const std::vector<std::string>& paths,
     t->sess = s;
     t->nrows = rows;
     hipStream_t st = s->stream;
-    if (row_id_col) {  // monotonically_increasing_id of a single partition: the row number
+    if (row_id_col) {  // monotonically_increasing_id: one partition (the row number) or Spark's file splits
         Column c;
         c.name = row_id_col;
         c.type = CAPSMI_I64;
         c.data = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), s);
-        iota_i64(P<int64_t>(c.data), 0, rows, st);
+        if (s->csv_parallelism > 0) {
+            std::vector<int64_t> lens;
+            for (auto& x : texts) lens.push_back((int64_t)x.size());
+            std::vector<int64_t> ids;
+            ids.reserve(rows);
+            spark_row_ids(lens, chunks, chunk_file, s->csv_parallelism, s->csv_max_partition_bytes, s->csv_open_cost,
+                          ids);
+            if (rows)
+                HIP_CHECK(hipMemcpyAsync(P<int64_t>(c.data), ids.data(), sizeof(int64_t) * rows, hipMemcpyHostToDevice,
+                                         st));
+            HIP_CHECK(hipStreamSynchronize(st));
+        } else {
+            iota_i64(P<int64_t>(c.data), 0, rows, st);
+        }
         t->cols.push_back(std::move(c));
     }
     for (int k = 0; k < nc; ++k) {

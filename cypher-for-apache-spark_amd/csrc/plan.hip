@@ -2284,6 +2284,18 @@ capsmi_status capsmi_session_set_fused(capsmi_session* s, int32_t enabled) {
     P_END
 }
 
+capsmi_status capsmi_session_set_csv_partitioning(capsmi_session* s, int64_t default_parallelism,
+                                                  int64_t max_partition_bytes, int64_t open_cost_bytes) {
+    P_BEGIN
+    need(s, "session");
+    REQUIRE(default_parallelism >= 0 && max_partition_bytes > 0 && open_cost_bytes >= 0, CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            "csv partitioning: parallelism >= 0, max partition bytes > 0, open cost >= 0");
+    s->csv_parallelism = default_parallelism;
+    s->csv_max_partition_bytes = max_partition_bytes;
+    s->csv_open_cost = open_cost_bytes;
+    P_END
+}
+
 capsmi_status capsmi_session_set_unrouted_limit(capsmi_session* s, int64_t max_bytes) {
     P_BEGIN
     need(s, "session");

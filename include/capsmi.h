@@ -600,9 +600,21 @@ capsmi_status capsmi_owner_words(int64_t nbits, int32_t part, int32_t nparts, in
  * a token that does not parse as its column type is ILLEGAL_ARGUMENT.  Parsed by host threads
  * (CAPSMI_INGEST_THREADS, default OMP_NUM_THREADS), copied to the device.  types: CAPSMI_I64 /
  * F64 / BOOL / STR; STR fields go through `intern` (the caller's dictionary), in row order.
- * row_id_col != NULL prepends a Long column of row numbers (monotonically_increasing_id of one
- * partition). */
+ * row_id_col != NULL prepends a Long column of monotonically_increasing_id values
+ * (EdgeListDataSource.scala:86): by default those of one partition (the row numbers); see
+ * capsmi_session_set_csv_partitioning for Spark's multi-partition ids. */
 typedef int64_t (*capsmi_intern_fn)(void* ctx, const char* s, size_t len);
+/* Row ids of capsmi_read_csv as monotonically_increasing_id over the partitions of Spark 2.2.1's file scan
+ * (FileSourceScanExec.createNonBucketedReadRDD; third-party, restated in csrc/ingest.hip spark_row_ids):
+ * maxSplitBytes = min(max_partition_bytes, max(open_cost_bytes, total / default_parallelism)), total =
+ * sum of (file length + open_cost_bytes); files split every maxSplitBytes; splits sorted by length
+ * (descending, stable) and packed next-fit into partitions; a line belongs to the split holding the byte
+ * before its first byte (Hadoop's LineRecordReader); id = partition << 33 | row within the partition.
+ * default_parallelism = the session's core count (CAPSSession.local(): local[*]); 0 restores one partition.
+ * Spark's defaults: max_partition_bytes 128 MiB (spark.sql.files.maxPartitionBytes), open_cost_bytes 4 MiB
+ * (spark.sql.files.openCostInBytes). */
+capsmi_status capsmi_session_set_csv_partitioning(capsmi_session* s, int64_t default_parallelism,
+                                                  int64_t max_partition_bytes, int64_t open_cost_bytes);
 capsmi_status capsmi_read_csv(capsmi_session* s, int32_t nfiles, const char* const* paths, char delimiter, char comment,
                               int32_t ncols, const char* const* names, const int32_t* types, capsmi_intern_fn intern,
                               void* intern_ctx, const char* row_id_col, capsmi_table** out);

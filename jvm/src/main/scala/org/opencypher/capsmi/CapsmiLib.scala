@@ -177,6 +177,8 @@ trait CapsmiLib extends Library {
   def capsmi_session_set_params(s: Pointer, nparams: Int, params: CapsmiParam): Int
   def capsmi_session_route_count(s: Pointer, name: String, count: LongByReference): Int
   def capsmi_session_set_unrouted_limit(s: Pointer, maxBytes: Long): Int
+  def capsmi_session_set_csv_partitioning(s: Pointer, defaultParallelism: Long, maxPartitionBytes: Long,
+                                          openCostBytes: Long): Int
 
   // multi-GPU (one process per GPU): rank view, shards of a distributed graph
   def capsmi_session_set_ranks(s: Pointer, rank: Int, world: Int, fn: CollectiveFn, ctx: Pointer): Int

@@ -113,3 +113,32 @@ def test_ingest_rate(session, tmp_path):
     print(f"edge-list ingest: {n} edges in {dt:.2f} s = {n / dt / 1e6:.1f} M edges/s (incl. node distinct)")
     assert n == len(a)
     np.testing.assert_array_equal(rels.column("target").values[-5:], a[-5:, 1])
+
+
+@pytest.mark.parametrize("par,maxp,cost", [(4, 4096, 512), (3, 1 << 20, 1 << 12), (16, 700, 0), (8, 128 << 20, 4 << 20)])
+def test_spark_partition_row_ids(session, tmp_path, par, maxp, cost):
+    """capsmi_session_set_csv_partitioning: read_csv's row ids are Spark's monotonically_increasing_id over
+    its file-scan partitions (EdgeListDataSource.scala:86), checked against the independent restatement
+    tests/spark_ids.py (parity unpinned: no reference fixture holds a multi-partition read)."""
+    from capsmi.expr import I64
+    from spark_ids import spark_row_ids
+    rng = np.random.default_rng(par)
+    paths, blobs = [], []
+    for f, n in enumerate([2000, 37, 900, 1]):
+        lines = [f"{a} {b}" for a, b in rng.integers(0, 1 << 40, (n, 2))]
+        if f == 2:
+            lines.insert(5, "# a comment")
+            lines.insert(9, "")
+        text = ("\n".join(lines) + ("\n" if f != 1 else "")).encode()
+        p = tmp_path / f"part-{f}.txt"
+        p.write_bytes(text)
+        paths.append(str(p))
+        blobs.append(text)
+    session.set_csv_partitioning(par, maxp, cost)
+    try:
+        t = session.read_csv(paths, ["source", "target"], [I64, I64], delimiter=" ", comment="#", row_id_col="id")
+    finally:
+        session.set_csv_partitioning(0)
+    want = spark_row_ids(blobs, par, maxp, cost, comment=b"#")
+    assert t.column("id").values.tolist() == want
+    assert len(set(want)) == len(want)
