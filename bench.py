@@ -46,6 +46,12 @@ C3_COUNT_QUERY = {"clauses": [{"match": "(a:Person)-[:FRIEND_OF]->(b:Person)-[:F
                   "return": {"items": [["n", ["count*"]]]}}
 C3_QUERY = {"clauses": [{"match": "(a:Person)-[:FRIEND_OF]->(b:Person)-[:FRIEND_OF]->(c:Person)"}],
             "return": {"items": [["count(DISTINCT c)", ["count_distinct", ["id", "c"]]]]}}
+# the undirected 2-hop (RelationalPlanner.scala:126-136: out ∪ in-without-loops per hop), bench modes und_count /
+# und_distinct, checked against tests/golden/rmat_full.json c3u_s<scale>
+C3U_COUNT_QUERY = {"clauses": [{"match": "(a:Person)-[:FRIEND_OF]-(b:Person)-[:FRIEND_OF]-(c:Person)"}],
+                   "return": {"items": [["n", ["count*"]]]}}
+C3U_QUERY = {"clauses": [{"match": "(a:Person)-[:FRIEND_OF]-(b:Person)-[:FRIEND_OF]-(c:Person)"}],
+             "return": {"items": [["count(DISTINCT c)", ["count_distinct", ["id", "c"]]]]}}
 C4_QUERY = {"clauses": [{"match": "(a:Person)-[r1:FRIEND_OF]->(b:Person)-[r2:FRIEND_OF]->(c:Person)-[r3:FRIEND_OF]->(a)"}],
             "return": {"items": [["n", ["count*"]]]}}
 C5_QUERY = {"clauses": [{"match": "(a:Person)-[:KNOWS*1..3]->(b:Person)"}],
@@ -53,14 +59,16 @@ C5_QUERY = {"clauses": [{"match": "(a:Person)-[:KNOWS*1..3]->(b:Person)"}],
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 KERNELS = ("part_scatter1", "part_scatter2_hop1", "part_scatter2", "hop1", "hop2", "mid_combine", "bitmap_add",
            "bitmap_range",
-           "count_part", "count_part_in", "count_in", "count_part_out", "count_out", "degrees")
+           "count_part", "count_part_in", "count_in", "count_part_out", "count_out", "degrees", "und_count_part",
+           "und_count", "und_distinct")
 # timer name -> kernel name as rocprofv3 reports it (hop1 and hop2 are two instances of k_hop_2d)
 KERNEL_SYMBOL = {"part_scatter1": "k_scatter_l", "part_scatter2_hop1": "k_scatter_s2", "part_scatter2": "k_scatter_s2",
                  "hop1": "k_hop_2d", "hop2": "k_hop_2d", "mid_combine": "k_mid_combine", "bitmap_add": "k_bitmap_add",
                  "bitmap_range": "k_bits_range",
                  "count_part": "k_rec_part", "count_part_in": "k_scatter_c", "count_part_out": "k_scatter_c",
                  "count_in": "k_rec_walk",
-                 "count_out": "k_rec_walk", "degrees": "k_degrees"}
+                 "count_out": "k_rec_walk", "degrees": "k_degrees", "und_count_part": "k_rec_part",
+                 "und_count": "k_und_deg", "und_distinct": "k_und_hop1+k_und_hop2"}
 
 
 def parse():
@@ -73,7 +81,8 @@ def parse():
     p.add_argument("--modes", default="cold,warm,direct,count",
                    help="comma list of cold, warm (the planner route, N=1), direct, direct_warm (explicit kernel "
                         "calls), stream, count / count_atomic (count(*) of the same match through the route, "
-                        "partitioned / per-relationship atomic degrees) (first = value)")
+                        "partitioned / per-relationship atomic degrees), und_count / und_distinct (the undirected "
+                        "2-hop count(*) / count(DISTINCT c) through the route) (first = value)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-scale", type=int, default=None, help="oracle sample scale (default per workload)")
     p.add_argument("--shard-of", type=int, default=0,
@@ -283,13 +292,15 @@ def main():
     # owns and the :Person rows of the ids it owns, ownership by a hash of the id (capsmi_owned_rows) --
     # then registers the shard (capsmi_graph_distribute); ingest is untimed
     t0 = time.perf_counter()
-    rels = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42,
-                           part_col=graph.PART_TARGET if shards > 1 else graph.PART_NONE, part=part, nparts=shards)
+    if distributed:
+        rels = owned_rmat_rels(sess, graph, scale, m_total, graph.RMAT_GRAPH500, "target", n)
+    else:
+        rels = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42,
+                               part_col=graph.PART_TARGET if shards > 1 else graph.PART_NONE, part=part, nparts=shards)
     persons = graph.rmat_nodes(sess, scale, graph.NODES_ALL)
     if distributed:
         from capsmi.dist import distribute, join_ranks
         join_ranks(sess)
-        rels = rels.owned_rows("target", 0, n).as_rel_table("id", "source", "target")
         persons = persons.owned_rows("id", 0, n).as_node_table("id")
         distribute(sess, 0, n, [persons], [rels], nodes_owned=True, rels_by="target")
     m_local = rels.size
@@ -416,7 +427,12 @@ def main():
             else:
                 os.environ["CAPSMI_COUNT"] = prev
 
-    steps = {"cold": lambda: run_planner(sg_cold), "warm": lambda: run_planner(sg_warm),
+    def run_und(q):  # the undirected queries through the route (fused_undirected)
+        t, outs = Planner(sg_cold).run(q)
+        return int(t.column(outs[0][2]).values[0])
+
+    steps = {"und_count": lambda: run_und(C3U_COUNT_QUERY), "und_distinct": lambda: run_und(C3U_QUERY),
+             "cold": lambda: run_planner(sg_cold), "warm": lambda: run_planner(sg_warm),
              "direct": step_cold, "direct_warm": step_warm, "stream": step_stream,
              "count": run_count, "count_atomic": lambda: run_count(True)}
     if shards != 1:  # --shard-of diagnostic: one shard's kernels, no exchange
@@ -496,8 +512,10 @@ def main():
         elif fx is None:
             check = "no fixture for this scale"
         else:
-            bad = {m: v for m, v in answers.items()
-                   if v != (fx["count_star"] if m.startswith("count") else fx["count_distinct_c"])}
+            fxu = fixture(f"c3u_s{scale}") or {}
+            want = {m: (fxu.get("count_star") if m == "und_count" else fxu.get("count_distinct_c") if m == "und_distinct"
+                        else fx["count_star"] if m.startswith("count") else fx["count_distinct_c"]) for m in answers}
+            bad = {m: v for m, v in answers.items() if v != want[m]}
             if matched != fx["count_star"]:
                 bad["count_star"] = matched
             check = "ok" if not bad else f"MISMATCH {bad} vs fixture {fx['count_distinct_c']} / {fx['count_star']}"
@@ -514,6 +532,7 @@ def main():
                "hop2": m_local * 8 + n // 8 * 3,     # read uint2 pairs + X1 + X2, write C
                "mid_combine": n // 8 * 5, "bitmap_add": n * 8,
                "count_part": m_local * 20,  # read 2 x int64, write two 2-byte records
+               "und_count_part": m_local * 24,  # read 2 x int64, write up to four 2-byte records
                "count_part_in": m_local * 24, "count_part_out": m_local * 24,  # pair partition (CAPSMI_COUNT=pairs)
                "degrees": m_local * 16 + n * 8}                  # read int64 pairs, inA + outC
         alg.update(kbytes)
@@ -571,7 +590,7 @@ def main():
         for mode in modes[1:]:
             s2, r2, kt2 = results[mode]
             entry = {"ms_per_step": s2 * 1e3, "value": matched / s2,
-                     ("count_star" if mode.startswith("count") else "count_distinct_c"): r2,
+                     ("count_star" if mode in ("count", "count_atomic", "und_count") else "count_distinct_c"): r2,
                      "kernel_ms": {k: v[1] / v[0] for k, v in kt2.items() if v[0] > 0}}
             if mode in ("warm", "direct_warm"):
                 entry.update({"phys_bytes_query": warm_phys,
@@ -611,6 +630,18 @@ SINGLE = {
 SINGLE_SYMBOL = {"direct_join_probe": "k_direct_probe", "radix_join_count": "k_join", "radix_join_write": "k_join",
                  "expand_filter": "k_expand_pairs", "part_scatter1": "k_scatter_l", "varlen_deg": "k_vl_deg",
                  "varlen_w": "k_vl_w", "varlen_t": "k_vl_t", "varlen_rev": "k_vl_bset", "varlen_recip": "k_vl_recip", "varlen_cand": "k_vl_cins", "triangles": "k_tri_big_items+k_tri_small"}
+
+
+def owned_rmat_rels(sess, graph, scale, m, probs, col, n, chunks=8):
+    """This rank's shard of the R-MAT relationships (the rows whose `col` id it owns), generated in `chunks`
+    edge ranges so that no rank ever holds the whole table (ingest, untimed)."""
+    out = None
+    step = -(-m // chunks)
+    for b in range(0, m, step):
+        part = graph.rmat_rels(sess, scale, b, min(m, b + step), probs, 42).owned_rows(col, 0, n)
+        out = part if out is None else out.unionAll(part)
+        out.size  # materialise: the chunk's full table is released
+    return out.as_rel_table("id", "source", "target")
 
 
 def route_counts(sess):
@@ -655,9 +686,7 @@ def run_single(args):
         from capsmi.dist import distribute, join_ranks
         join_ranks(sess)
         by = "source" if wl == "c5" else "target"
-        rels_all = graph.rmat_rels(sess, scale, 0, m, probs, 42)
-        rels = rels_all.owned_rows(by, 0, n).as_rel_table("id", "source", "target")
-        del rels_all
+        rels = owned_rmat_rels(sess, graph, scale, m, probs, by, n)
     elif shard_c5:  # ingest (untimed): out-relationships of owned sources + in-relationships from other ranks
         wb, we = graph.owner_words(n, rank, world)
         own_lo, own_hi = min(32 * wb, n), min(32 * we, n)

@@ -326,8 +326,10 @@ bool direct_join(capsmi_session* s, const KeyCols& bk, int64_t nb, const KeyCols
 int64_t two_hop_count_part(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
                            int nt, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok);
 // the same from two partitions of 2-byte records (k_count.hip rec::), the default
+// undirected: the 2-hop of undirected Expands (both arcs of every relationship, r1 = r2 bindings subtracted)
 int64_t two_hop_count_rec(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
-                          int nt, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok);
+                          int nt, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok,
+                          bool undirected = false);
 void cross_pairs(int64_t nl, int64_t nr, int64_t* out_l, int64_t* out_r, hipStream_t st);
 
 // expressions (k_expr.hip)

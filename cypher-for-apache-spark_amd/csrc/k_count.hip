@@ -131,10 +131,15 @@ __host__ __device__ constexpr size_t part_lds(int nb2) {
            sizeof(uint32_t) * (6 * (size_t)nb2 + kB / 64 + 4) + sizeof(uint16_t) * (size_t)max_pieces(nb2);
 }
 
-__host__ __device__ constexpr int64_t chunks_per_block(int64_t m, int64_t grid, int nb2) {
-    // full chunks of the block's records (two per relationship at most), plus per bucket the open
-    // one and one retired part-full by the final flush
-    return ((((m + kT - 1) / kT + grid - 1) / grid) * 2 * kT + kCh - 1) / kCh + 2 * (int64_t)nb2 + 1;
+// relationships per lane and per tile: the undirected form emits up to four records per relationship
+// (both arcs), so its tiles hold half the relationships and the same 2 kT records
+__host__ __device__ constexpr int part_it(bool und) { return und ? kIT / 2 : kIT; }
+
+__host__ __device__ constexpr int64_t chunks_per_block(int64_t m, int64_t grid, int nb2, bool und = false) {
+    // full chunks of the block's records (2 kT per tile at most), plus per bucket the open one and one
+    // retired part-full by the final flush
+    const int64_t T = (int64_t)kB * part_it(und);
+    return ((((m + T - 1) / T + grid - 1) / grid) * 2 * kT + kCh - 1) / kCh + 2 * (int64_t)nb2 + 1;
 }
 
 __device__ __forceinline__ bool bit(const part::BitV& v, uint64_t x) { return v.full || part::gbit(v.w, (uint32_t)x); }
@@ -143,11 +148,18 @@ __device__ __forceinline__ bool bit(const part::BitV& v, uint64_t x) { return v.
 //   bucket t >> 16        (the in side):  t & 0xFFFF for relationships s -> t with a_ok(s);
 //   bucket nb + (s >> 16) (the out side): s & 0xFFFF for relationships s -> t with c_ok(t);
 // the a_ok, b_ok, c_ok self-loops are counted into `loops`.
+// UND (undirected 2-hop, RelationalPlanner.scala:126-136: out ∪ in-without-loops per hop): each relationship
+// s -> t is the arc s -> t and, when s != t, the arc t -> s; every arc x -> y gives an in record of y when
+// a_ok(x) and an out record of x when c_ok(y), so the walks give sum_b b_ok(b) inU(b) outU(b); `loops`
+// gets the bindings with r1 = r2 (a non-loop walked in and back out, [a(s) b(t) c(s)] + [a(t) b(s) c(t)], a
+// loop [a b c](s)).
+template <bool UND>
 __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                  int64_t m, int64_t lo, int64_t range, int nb, part::BitV a, part::BitV b,
                                                  part::BitV c, int64_t chunk0, int64_t cpb, uint16_t* __restrict__ pool,
                                                  unsigned long long* __restrict__ cmeta,
                                                  unsigned long long* __restrict__ loops) {
+    constexpr int IT = part_it(UND), T = kB * IT;
     extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
     const int nb2 = 2 * nb;
     uint16_t* stage = reinterpret_cast<uint16_t*>(sm);  // 2 kT: this tile's records grouped by bucket
@@ -171,22 +183,30 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
     }
     if (threadIdx.x == 0) misc[0] = (uint32_t)(chunk0 + (int64_t)blockIdx.x * cpb);
     const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
-    const int64_t stride = (int64_t)gridDim.x * kT;
+    const int64_t stride = (int64_t)gridDim.x * T;
     unsigned long long nl = 0;
-    int64_t sr[kIT], tr[kIT];
-    int64_t t0 = (int64_t)blockIdx.x * kT;
+    int64_t sr[IT], tr[IT];
+    int64_t t0 = (int64_t)blockIdx.x * T;
     if (t0 < m) part::load_tile<kB>(src, dst, t0, m, vec, sr, tr);
     __syncthreads();
     for (; t0 < m; t0 += stride) {  // block-uniform
-        uint32_t xs[kIT], ys[kIT], rin[kIT], rout[kIT];
-        uint32_t vin = 0, vout = 0;
+        uint32_t xs[IT], ys[IT], rin[IT], rout[IT], rin2[UND ? IT : 1], rout2[UND ? IT : 1];
+        uint32_t vin = 0, vout = 0, vin2 = 0, vout2 = 0;
 #pragma unroll
-        for (int u = 0; u < kIT; ++u) {
+        for (int u = 0; u < IT; ++u) {
             const int64_t e = t0 + part::item_off<kB>(u);
             const uint64_t x = (uint64_t)(sr[u] - lo), y = (uint64_t)(tr[u] - lo);
             const bool ok = e < m && x < (uint64_t)range && y < (uint64_t)range;
             const bool ain = ok && bit(a, x), aout = ok && bit(c, y);
-            if (ain && x == y && bit(b, x) && bit(c, x)) ++nl;
+            if (!UND) {
+                if (ain && x == y && bit(b, x) && bit(c, x)) ++nl;
+            } else if (ok) {  // the reverse arc y -> x of a non-loop, and the r1 = r2 bindings
+                const bool ay = bit(a, y), cx = bit(c, x), bx = bit(b, x), by = bit(b, y);
+                const bool two = x != y;
+                vin2 |= (two && ay ? 1u : 0u) << u;
+                vout2 |= (two && cx ? 1u : 0u) << u;
+                nl += two ? (ain && by && cx ? 1 : 0) + (ay && bx && aout ? 1 : 0) : (ain && bx && cx ? 1 : 0);
+            }
             xs[u] = (uint32_t)x;
             ys[u] = (uint32_t)y;
             vin |= (ain ? 1u : 0u) << u;
@@ -194,16 +214,24 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
         }
         if (t0 + stride < m) part::load_tile<kB>(src, dst, t0 + stride, m, vec, sr, tr);  // prefetch
 #pragma unroll
-        for (int u = 0; u < kIT; ++u) {
+        for (int u = 0; u < IT; ++u) {
             rin[u] = ((vin >> u) & 1u) ? atomicAdd(&cnt[ys[u] >> kBits], 1u) : 0u;
             rout[u] = ((vout >> u) & 1u) ? atomicAdd(&cnt[nb + (xs[u] >> kBits)], 1u) : 0u;
+            if (UND) {
+                rin2[u] = ((vin2 >> u) & 1u) ? atomicAdd(&cnt[xs[u] >> kBits], 1u) : 0u;
+                rout2[u] = ((vout2 >> u) & 1u) ? atomicAdd(&cnt[nb + (ys[u] >> kBits)], 1u) : 0u;
+            }
         }
         __syncthreads();
         (void)part::block_exclusive_scan<kB>(cnt, loc, nb2, wtot);
 #pragma unroll
-        for (int u = 0; u < kIT; ++u) {
+        for (int u = 0; u < IT; ++u) {
             if ((vin >> u) & 1u) stage[loc[ys[u] >> kBits] + rin[u]] = (uint16_t)(ys[u] & 0xFFFFu);
             if ((vout >> u) & 1u) stage[loc[nb + (xs[u] >> kBits)] + rout[u]] = (uint16_t)(xs[u] & 0xFFFFu);
+            if (UND) {
+                if ((vin2 >> u) & 1u) stage[loc[xs[u] >> kBits] + rin2[u]] = (uint16_t)(xs[u] & 0xFFFFu);
+                if ((vout2 >> u) & 1u) stage[loc[nb + (ys[u] >> kBits)] + rout2[u]] = (uint16_t)(ys[u] & 0xFFFFu);
+            }
         }
         for (int i = threadIdx.x; i < nb2; i += kB) {  // pieces of the held + run sequence; chunks they open
             const uint32_t npc = ((uint32_t)hc[i] + cnt[i]) / kPiece;
@@ -244,7 +272,7 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
         }
         __syncthreads();
 #pragma unroll
-        for (int u = 0; u < kIT; ++u) {  // the new held records: the run's items past its last whole piece
+        for (int u = 0; u < IT; ++u) {  // the new held records: the run's items past its last whole piece
             if ((vin >> u) & 1u) {
                 const uint32_t bk = ys[u] >> kBits;
                 const int d = (int)rin[u] - (int)pc[bk];
@@ -254,6 +282,16 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
                 const uint32_t bk = nb + (xs[u] >> kBits);
                 const int d = (int)rout[u] - (int)pc[bk];
                 if (d >= 0) hold[bk * kPiece + d] = (uint16_t)(xs[u] & 0xFFFFu);
+            }
+            if (UND && ((vin2 >> u) & 1u)) {
+                const uint32_t bk = xs[u] >> kBits;
+                const int d = (int)rin2[u] - (int)pc[bk];
+                if (d >= 0) hold[bk * kPiece + d] = (uint16_t)(xs[u] & 0xFFFFu);
+            }
+            if (UND && ((vout2 >> u) & 1u)) {
+                const uint32_t bk = nb + (ys[u] >> kBits);
+                const int d = (int)rout2[u] - (int)pc[bk];
+                if (d >= 0) hold[bk * kPiece + d] = (uint16_t)(ys[u] & 0xFFFFu);
             }
         }
         __syncthreads();
@@ -477,7 +515,8 @@ __global__ void k_rec_result(const unsigned long long* __restrict__ acc, int64_t
 
 // phase 1: the two-sided record partition and the IN walk (inA of every target this table holds)
 void count_rec_begin(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
-                     const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok, CountRec& cr) {
+                     const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok, CountRec& cr,
+                     bool undirected) {
     using namespace rec;
     const int64_t lo = b_ok->lo, n = b_ok->hi - b_ok->lo;
     const part::BitV a{P<uint32_t>(a_ok->words), a_ok->full ? 1 : 0}, b{P<uint32_t>(b_ok->words), b_ok->full ? 1 : 0},
@@ -498,8 +537,8 @@ void count_rec_begin(capsmi_session* s, const int64_t* const* srcs, const int64_
     HIP_CHECK(hipMemsetAsync(P<void>(cr.acc), 0, 2 * sizeof(unsigned long long), st));
     static std::once_flag once;
     std::call_once(once, [] {
-        HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_rec_part), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)part_lds(2 * kMaxBuckets)));
+        for (const void* f : {reinterpret_cast<const void*>(k_rec_part<false>), reinterpret_cast<const void*>(k_rec_part<true>)})
+            HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)part_lds(2 * kMaxBuckets)));
         for (const void* f : {reinterpret_cast<const void*>(k_rec_walk<false>), reinterpret_cast<const void*>(k_rec_walk<true>)})
             HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
                                           (int)walk_lds()));
@@ -511,8 +550,9 @@ void count_rec_begin(capsmi_session* s, const int64_t* const* srcs, const int64_
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
         mtot += ms[i];
-        g1[i] = (int)std::max<int64_t>(1, std::min<int64_t>(s->num_cus, (ms[i] + 4 * (int64_t)kT - 1) / (4 * (int64_t)kT)));
-        cpb[i] = chunks_per_block(ms[i], g1[i], 2 * nb);
+        const int64_t T = (int64_t)kB * part_it(undirected);
+        g1[i] = (int)std::max<int64_t>(1, std::min<int64_t>(s->num_cus, (ms[i] + 4 * T - 1) / (4 * T)));
+        cpb[i] = chunks_per_block(ms[i], g1[i], 2 * nb, undirected);
         c0[i] = pool_chunks;
         pool_chunks += (int64_t)g1[i] * cpb[i];
     }
@@ -524,15 +564,16 @@ void count_rec_begin(capsmi_session* s, const int64_t* const* srcs, const int64_
     cp.L.hi = lo + n;
     cp.L.nt = 2 * nb;
     {
-        KernelTimer kt(s, "count_part", (double)mtot * 20);  // read 2 x int64, write two 2-byte records
+        // read 2 x int64, write two 2-byte records (undirected: four)
+        KernelTimer kt(s, undirected ? "und_count_part" : "count_part", (double)mtot * (undirected ? 24 : 20));
         cp.pool = dev_alloc(sizeof(uint16_t) * kCh * (size_t)npool, s);
         cp.meta = dev_alloc(sizeof(unsigned long long) * npool, s);
         HIP_CHECK(hipMemsetAsync(P<void>(cp.meta), 0, sizeof(unsigned long long) * npool, st));
         for (int i = 0; i < nt; ++i) {
             if (ms[i] <= 0) continue;
-            hipLaunchKernelGGL(k_rec_part, dim3(g1[i]), dim3(kB), part_lds(2 * nb), st, srcs[i], dsts[i], ms[i], lo, n, nb, a,
-                               b, c, c0[i], cpb[i], P<uint16_t>(cp.pool), P<unsigned long long>(cp.meta),
-                               P<unsigned long long>(cr.acc));
+            hipLaunchKernelGGL(undirected ? k_rec_part<true> : k_rec_part<false>, dim3(g1[i]), dim3(kB), part_lds(2 * nb), st,
+                               srcs[i], dsts[i], ms[i], lo, n, nb, a, b, c, c0[i], cpb[i], P<uint16_t>(cp.pool),
+                               P<unsigned long long>(cp.meta), P<unsigned long long>(cr.acc));
         }
         HIP_CHECK(hipGetLastError());
     }
@@ -585,9 +626,10 @@ int64_t count_rec_finish(CountRec& cr, const uint32_t* in_all, int64_t* dev_out)
 
 // the same count from two record partitions (rec:: above); one id domain of at most 2^26 ids
 int64_t two_hop_count_rec(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
-                          int nt, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok) {
+                          int nt, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok,
+                          bool undirected) {
     CountRec cr;
-    count_rec_begin(s, srcs, dsts, ms, nt, a_ok, b_ok, c_ok, cr);
+    count_rec_begin(s, srcs, dsts, ms, nt, a_ok, b_ok, c_ok, cr, undirected);
     return count_rec_finish(cr, nullptr, nullptr);
 }
 

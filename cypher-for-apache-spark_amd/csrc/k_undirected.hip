@@ -177,7 +177,13 @@ int64_t undirected_count(capsmi_session* s, const int64_t* const* srcs, const in
         HIP_CHECK(hipGetLastError());
         return words_popcount(s, P<uint32_t>(M), 0, nw);
     }
-    if (kind == 0) {  // 2-hop count(*)
+    const char* ce = getenv("CAPSMI_COUNT");  // "atomic": the per-relationship atomic degrees below (A/B)
+    if (kind == 0 && n <= (int64_t(1) << 26) && !(ce && std::string(ce) == "atomic")) {
+        // 2-hop count(*): the two-sided record partition of the directed count(*) with both arcs of every
+        // relationship (k_count.hip k_rec_part<true>), walks in LDS, no per-relationship global atomics
+        return two_hop_count_rec(s, srcs, dsts, ms, nt, a, b, c, true);
+    }
+    if (kind == 0) {  // 2-hop count(*), atomic degrees (domains above 2^26 ids)
         KernelTimer kt(s, "und_count");
         Buf inU = dev_alloc(sizeof(uint32_t) * n, s), outU = dev_alloc(sizeof(uint32_t) * n, s);
         HIP_CHECK(hipMemsetAsync(P<void>(inU), 0, sizeof(uint32_t) * n, st));

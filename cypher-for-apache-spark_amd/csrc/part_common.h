@@ -343,7 +343,8 @@ struct CountRec {
     ChunkPart cp;
 };
 void count_rec_begin(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
-                     const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok, CountRec& cr);
+                     const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok, CountRec& cr,
+                     bool undirected = false);
 void count_rec_fold(CountRec& cr, int64_t own_lo, int64_t own_hi, uint32_t* out);
 int64_t count_rec_finish(CountRec& cr, const uint32_t* in_all, int64_t* dev_out);
 

@@ -94,6 +94,79 @@ int orc_two_hop_closed_form_mt(int64_t n, int64_t m, const int64_t* src, const i
     return 0;
 }
 
+/* Undirected 2-hop (a)-[r1]-(b)-[r2]-(c), r1 <> r2 (RelationalPlanner.scala:126-136: out ∪ in-without-loops per
+ * hop; MatchBehaviour.scala:258-279).  Every relationship e = (s, t) is the arc s -> t and, when s != t, the
+ * arc t -> s.  With inU(b) = a_ok arcs into b and outU(b) = c_ok arcs out of b:
+ *   count(*) = sum_b [b_ok] inU(b) outU(b) - corr, corr = the bindings with r1 = r2 (a non-loop walked in
+ *   and back out: [a(s) b(t) c(s)] + [a(t) b(s) c(t)]; a loop: [a b c](s));
+ *   count(DISTINCT c): K(b) = a_ok arcs into b capped at 2, x(b) the other end of the only one when K = 1;
+ *   an arc b -> c (c_ok, b_ok) extends a binding iff K(b) = 2, or K(b) = 1 and c != x(b).
+ * The same derivation as the device path (csrc/k_undirected.hip, csrc/k_count.hip k_rec_part<true>);
+ * pinned against rmat.c orc_two_hop_undirected_enumerate (tests/test_oracle_pins.py). */
+int orc_two_hop_undirected_closed_form(int64_t n, int64_t m, const int64_t* src, const int64_t* dst,
+                                       const uint8_t* a_ok, const uint8_t* b_ok, const uint8_t* c_ok,
+                                       int64_t* out_rows, int64_t* out_distinct, int nthreads) {
+    int64_t* in_u = (int64_t*)calloc((size_t)(n ? n : 1), sizeof(int64_t));
+    int64_t* out_u = (int64_t*)calloc((size_t)(n ? n : 1), sizeof(int64_t));
+    int64_t* kx = (int64_t*)calloc((size_t)(n ? n : 1), sizeof(int64_t)); /* 0, x + 1, or -1 (two or more) */
+    uint8_t* mark = (uint8_t*)calloc((size_t)(n ? n : 1), 1);
+    if (!in_u || !out_u || !kx || !mark) { free(in_u); free(out_u); free(kx); free(mark); return -1; }
+    set_threads(nthreads);
+    int64_t corr = 0, rows = 0, d = 0;
+#pragma omp parallel for schedule(static) reduction(+ : corr)
+    for (int64_t e = 0; e < m; ++e) {
+        const int64_t s = src[e], t = dst[e];
+        if (OK(a_ok, s)) {
+#pragma omp atomic
+            in_u[t]++;
+        }
+        if (OK(c_ok, t)) {
+#pragma omp atomic
+            out_u[s]++;
+        }
+        if (s != t) {
+            if (OK(a_ok, t)) {
+#pragma omp atomic
+                in_u[s]++;
+            }
+            if (OK(c_ok, s)) {
+#pragma omp atomic
+                out_u[t]++;
+            }
+            corr += (OK(a_ok, s) && OK(b_ok, t) && OK(c_ok, s)) + (OK(a_ok, t) && OK(b_ok, s) && OK(c_ok, t));
+        } else {
+            corr += OK(a_ok, s) && OK(b_ok, s) && OK(c_ok, s);
+        }
+    }
+#pragma omp parallel for schedule(static) reduction(+ : rows)
+    for (int64_t b = 0; b < n; ++b)
+        if (OK(b_ok, b)) rows += in_u[b] * out_u[b];
+    for (int64_t e = 0; e < m; ++e) { /* K(b), x(b): the a_ok arcs into b_ok ids (sequential) */
+        const int64_t s = src[e], t = dst[e];
+        for (int dir = 0; dir < (s != t ? 2 : 1); ++dir) {
+            const int64_t x = dir ? t : s, b = dir ? s : t;
+            if (!OK(a_ok, x) || !OK(b_ok, b)) continue;
+            kx[b] = kx[b] == 0 ? x + 1 : -1;
+        }
+    }
+#pragma omp parallel for schedule(static)
+    for (int64_t e = 0; e < m; ++e) {
+        const int64_t s = src[e], t = dst[e];
+        for (int dir = 0; dir < (s != t ? 2 : 1); ++dir) {
+            const int64_t b = dir ? t : s, c = dir ? s : t;
+            if (!OK(c_ok, c)) continue;
+            const int64_t k = kx[b];
+            if (k == -1 || (k != 0 && k - 1 != c)) mark[c] = 1;
+        }
+    }
+#pragma omp parallel for schedule(static) reduction(+ : d)
+    for (int64_t i = 0; i < n; ++i) d += mark[i];
+    *out_rows = rows - corr;
+    *out_distinct = d;
+    free(in_u); free(out_u); free(kx); free(mark);
+    return 0;
+}
+
 /* ---- sorted adjacency helpers ------------------------------------------------------------- */
 static int cmp_i64(const void* a, const void* b) {
     const int64_t x = *(const int64_t*)a, y = *(const int64_t*)b;

@@ -203,6 +203,15 @@ def var_length_closed_form(n, src, dst, lo, hi, a_ok=None, b_ok=None, threads=0)
     return rows.value, g
 
 
+def two_hop_undirected_closed_form(n, src, dst, a_ok=None, b_ok=None, c_ok=None, threads=0):
+    """(count(*), count(DISTINCT c)) of (a)-[r1]-(b)-[r2]-(c), r1 <> r2 (closed.c)."""
+    rows, d = ctypes.c_int64(), ctypes.c_int64()
+    if load().orc_two_hop_undirected_closed_form(n, len(src), _p64(src), _p64(dst), _p8(a_ok), _p8(b_ok), _p8(c_ok),
+                                                 ctypes.byref(rows), ctypes.byref(d), threads):
+        raise MemoryError("orc_two_hop_undirected_closed_form")
+    return rows.value, d.value
+
+
 def triangle_closed_form(n, src, dst, n_ok=None, threads=0):
     rows = ctypes.c_int64()
     rc = load().orc_triangle_closed_form(n, len(src), _p64(src), _p64(dst), _p8(n_ok), ctypes.byref(rows), threads)

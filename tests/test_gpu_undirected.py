@@ -107,3 +107,33 @@ def test_route_miss_counter_and_unrouted_guard(session):
         assert Planner(sg).run(q)[0].size == t.size  # a small unrouted join still runs
     finally:
         session.set_unrouted_limit(0)
+
+
+@pytest.mark.parametrize("scale", [16, 20])
+def test_undirected_two_hop_vs_fixture(session, scale):
+    """count(*) through the two-sided record partition with both arcs (k_count.hip k_rec_part<true>), and the
+    atomic form (CAPSMI_COUNT=atomic, A/B), and count(DISTINCT c), against the committed closed-form fixtures
+    (tests/golden/rmat_full.json c3u_s16 / c3u_s20; oracle/closed.c orc_two_hop_undirected_closed_form)."""
+    import json
+    import os
+    from capsmi.planner import EntityTable, Planner, ScanGraph, result_rows
+    from capsmi import graph
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "tests", "golden", "rmat_full.json")) as f:
+        fx = json.load(f)["cases"][f"c3u_s{scale}"]
+    rels = graph.rmat_rels(session, scale, 0, 16 << scale, graph.RMAT_GRAPH500, 42)
+    nodes = graph.rmat_nodes(session, scale, graph.NODES_ALL, 42)
+    sg = ScanGraph(session, [EntityTable("node", frozenset({"Person"}), {}, nodes, id_col="id")],
+                   [EntityTable("rel", frozenset({"FRIEND_OF"}), {}, rels, id_col="id", src_col="source",
+                                dst_col="target")])
+    q = {"clauses": [{"match": "(a:Person)-[:FRIEND_OF]-(b:Person)-[:FRIEND_OF]-(c:Person)"}],
+         "return": {"items": [["n", ["count*"]], ["dc", ["count_distinct", ["id", "c"]]]]}}
+    t, outs = Planner(sg).run(q)
+    got = result_rows(t, outs, session.dictionary)[0]
+    assert (got["n"], got["dc"]) == (fx["count_star"], fx["count_distinct_c"])
+    os.environ["CAPSMI_COUNT"] = "atomic"
+    try:
+        t, outs = Planner(sg).run({"clauses": q["clauses"], "return": {"items": [["n", ["count*"]]]}})
+        assert result_rows(t, outs, session.dictionary)[0]["n"] == fx["count_star"]
+    finally:
+        del os.environ["CAPSMI_COUNT"]

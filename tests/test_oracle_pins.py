@@ -88,6 +88,8 @@ def _check_graph(g):
                       ["da", ["count_distinct", ["id", "a"]]]])[0]
         assert cpu.two_hop_undirected_enumerate(n, src, dst, mask, mask, mask) == (want["rows"], want["dc"], want["da"]), \
             (label, rtype)
+        assert cpu.two_hop_undirected_closed_form(n, src, dst, mask, mask, mask, threads=2) == \
+            (want["rows"], want["dc"]), (label, rtype)
         # C4 (rmat.c enumeration has no node mask: keep the relationships with both ends in the scan)
         want = _enum(g, f"(a{lab})-{ty}->(b{lab})-{ty}->(c{lab})-{ty}->(a)", [["rows", ["count*"]]])[0]["rows"]
         keep = (mask[src] != 0) & (mask[dst] != 0) if len(src) else np.zeros(0, bool)
@@ -135,6 +137,10 @@ def test_closed_forms_equal_enumeration_on_rmat(scale, probs, ef):
     for a_ok, b_ok in [(None, None), (person, person), (adult, person)]:
         assert cpu.two_hop_closed_form_mt(n, src, dst, a_ok, b_ok, b_ok) == \
             cpu.two_hop_enumerate(n, src, dst, a_ok, b_ok, b_ok)
+        assert cpu.two_hop_undirected_closed_form(n, src, dst, a_ok, b_ok, b_ok) == \
+            cpu.two_hop_undirected_enumerate(n, src, dst, a_ok, b_ok, b_ok)[:2]
+        assert cpu.two_hop_undirected_closed_form(n, src, dst, b_ok, a_ok, person) == \
+            cpu.two_hop_undirected_enumerate(n, src, dst, b_ok, a_ok, person)[:2]
         tot, g = cpu.var_length_count(n, src, dst, 1, 3, a_ok, b_ok)
         tot2, g2 = cpu.var_length_closed_form(n, src, dst, 1, 3, a_ok, b_ok)
         assert tot == tot2
