@@ -6,6 +6,8 @@ shapes at materialisation.  Each test runs a BASELINE query shape through ``Plan
 R-MAT inputs, checks the answer against the CPU oracle (or enumeration), checks that the fused route
 was taken (route counters, kernel timers), and that the same plan run operator by operator
 (``set_fused(False)``) gives the same rows."""
+import os
+
 import numpy as np
 import pytest
 
@@ -249,7 +251,7 @@ def test_lazy_schema_errors_at_call(session):
     assert u.size == 5
 
 
-@pytest.mark.parametrize("scale,kind", [(12, "all"), (14, "all"), (12, "person")])
+@pytest.mark.parametrize("scale,kind", [(12, "all"), (14, "all"), (12, "person"), (16, "person"), (20, "all")])
 def test_c3_grouped_routed(session, scale, kind):
     """C3's grouped form (RETURN id(a), count(DISTINCT c), the parity variant at s <= 14) and
     the grouped count(*), routed to the grouped 2-hop kernels (csrc/k_grouped.hip), against per-a
@@ -267,3 +269,8 @@ def test_c3_grouped_routed(session, scale, kind):
     assert same_rows(got, want)
     if scale == 12:
         assert same_rows(_run(session, sg, q, fused=False), want)
+        os.environ["CAPSMI_GROUPED"] = "keys"  # the per-binding key sort (A/B): the same rows
+        try:
+            assert same_rows(_run(session, sg, q), want)
+        finally:
+            del os.environ["CAPSMI_GROUPED"]
