@@ -295,6 +295,13 @@ void collective_a2av(capsmi_session* s, const void* send, const int64_t* send_co
 Buf exchange_words(capsmi_session* s, uint64_t* dest, uint64_t* words, int64_t n, int64_t* nrecv);
 // every rank's words concatenated in rank order; synchronises
 Buf gather_words(capsmi_session* s, const uint64_t* words, int64_t n, int64_t* ntotal);
+// the generic operators' row exchanges over partitioned tables (k_dist.hip): rows to rank dest[r]; rows
+// hash-partitioned by key columns; this rank's slice of a replicated table; every rank's rows
+capsmi_table* exchange_rows(capsmi_session* s, const capsmi_table* t, uint64_t* dest);
+capsmi_table* exchange_by_keys(capsmi_session* s, const capsmi_table* t, const std::vector<int>& keys,
+                               const std::vector<int>& as_f64, bool null_local);
+capsmi_table* slice_rows(capsmi_session* s, const capsmi_table* t);
+capsmi_table* gather_rows(capsmi_session* s, const capsmi_table* t);
 // the scrambled domain of [lo, hi) over `world` ranks: kbits, mul, mul_inv, slice words, domain size
 struct Scramble {
     int kbits;

@@ -85,6 +85,55 @@ __global__ void k_unpack_words(const uint64_t* __restrict__ w, int64_t n, int64_
     }
 }
 
+// destination of each row: a hash of its key columns mod world (Spark's HashPartitioning); rows with a
+// null key go to `null_rank` when it is >= 0 (they match nothing: joins keep them where they are), else
+// nulls hash as a tag (grouping: nulls form one group).  as_f64[k]: hash key k as a double (a Long key
+// joined with a Double key, widened by the join)
+struct KeyHashCols {
+    const int64_t* d[8];
+    const uint8_t* v[8];
+    int as_f64[8];
+    int n;
+};
+__device__ __forceinline__ uint64_t dmix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+__global__ void k_key_dest(KeyHashCols k, int64_t n, int world, int null_rank, uint64_t* __restrict__ dest) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t h = 0x243F6A8885A308D3ULL;
+        bool any_null = false;
+        for (int c = 0; c < k.n; ++c) {
+            const bool nul = k.v[c] && !k.v[c][r];
+            any_null = any_null || nul;
+            uint64_t v = nul ? 0 : (uint64_t)k.d[c][r];
+            if (!nul && k.as_f64[c] == 1) {  // a Long widened to its double
+                const double x = (double)(int64_t)v;
+                v = __double_as_longlong(x);
+            }
+            if (!nul && k.as_f64[c] && (v << 1) == 0) v = 0;  // -0.0 == 0.0
+            h = dmix64(h ^ (v + (nul ? 0x3C6EF372FE94F82BULL : 0) + (uint64_t)c * 0x9E3779B97F4A7C15ULL));
+        }
+        dest[r] = (any_null && null_rank >= 0) ? (uint64_t)null_rank : (h % (uint64_t)world);
+    }
+}
+
+__global__ void k_row_dest_slice(int64_t n, int rank, int world, uint64_t* __restrict__ dest) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+        dest[r] = (uint64_t)(r % world == rank ? rank : 0xFF);
+}
+
+__global__ void k_valid_to_words(const uint8_t* __restrict__ v, int64_t n, int64_t* __restrict__ w) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+        w[r] = v ? v[r] : 1;
+}
+
+__global__ void k_words_to_valid(const int64_t* __restrict__ w, int64_t n, uint8_t* __restrict__ v) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+        v[r] = (uint8_t)(w[r] != 0);
+}
+
 __global__ void k_owned_flags(const int64_t* __restrict__ in, int64_t n, int64_t lo, int64_t hi, uint64_t mul,
                               uint64_t mask, int64_t own_lo, int64_t own_hi, uint8_t* __restrict__ flags) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -172,6 +221,153 @@ Buf gather_words(capsmi_session* s, const uint64_t* words, int64_t n, int64_t* n
     }
     *ntotal = tot;
     return out;
+}
+
+// ---- row exchanges of the generic operators over partitioned tables (Spark's Exchange) ------------
+namespace {
+capsmi_table* new_table(capsmi_session* s, int64_t nrows) {
+    auto* t = new capsmi_table();
+    t->sess = s;
+    t->nrows = nrows;
+    return t;
+}
+
+void no_lists(const capsmi_table* t) {
+    for (const Column& c : t->cols)
+        REQUIRE(!is_list_type(c.type), CAPSMI_ERR_UNSUPPORTED,
+                "list column '" + c.name + "' in an exchange of a distributed result");
+}
+}  // namespace
+
+// Rows of t to the rank dest[r] (low byte; 0xFF: dropped): one stable 8-bit radix pass orders the row
+// indices by destination, every column is gathered in that order and exchanged (one ALL_TO_ALL_V per
+// column, validity as a word column).  Returns this rank's received rows, rank-major, same schema.
+capsmi_table* exchange_rows(capsmi_session* s, const capsmi_table* t, uint64_t* dest) {
+    no_lists(t);
+    hipStream_t st = s->stream;
+    const int W = s->world;
+    const int64_t n = t->nrows;
+    Buf idx = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
+    iota_i64(P<int64_t>(idx), 0, n, st);
+    radix_sort_digits(s, dest, P<int64_t>(idx), n, {0});
+    Buf cnt = dev_alloc(sizeof(int64_t) * (W + (size_t)W * W), s);
+    int64_t* mine = P<int64_t>(cnt);
+    if (n > 0) hipLaunchKernelGGL(k_dest_counts, dim3(1), dim3(256), 0, st, dest, n, W, mine);
+    else HIP_CHECK(hipMemsetAsync(mine, 0, sizeof(int64_t) * W, st));
+    HIP_CHECK(hipGetLastError());
+    collective(s, CAPSMI_COLL_ALL_GATHER, mine, mine + W, W, CAPSMI_I64);
+    std::vector<int64_t> mat((size_t)W * W);
+    HIP_CHECK(hipMemcpyAsync(mat.data(), mine + W, sizeof(int64_t) * mat.size(), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    std::vector<int64_t> sc(W), rc(W);
+    int64_t nsend = 0, nrecv = 0;
+    for (int q = 0; q < W; ++q) {
+        sc[q] = mat[(size_t)s->rank * W + q];
+        rc[q] = mat[(size_t)q * W + s->rank];
+        nsend += sc[q];
+        nrecv += rc[q];
+    }
+    auto* o = new_table(s, nrecv);
+    Buf tmp = dev_alloc(sizeof(int64_t) * (nsend > 0 ? nsend : 1), s);
+    for (const Column& c : t->cols) {
+        Column x;
+        x.name = c.name;
+        x.type = c.type;
+        x.data = dev_alloc(sizeof(int64_t) * (nrecv > 0 ? nrecv : 1), s);
+        gather_col(c.d(), nullptr, P<int64_t>(idx), nsend, P<int64_t>(tmp), nullptr, st);
+        collective_a2av(s, P<int64_t>(tmp), sc.data(), P<int64_t>(x.data), rc.data(), CAPSMI_I64);
+        if (c.valid) {
+            Buf vw = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s), rw = dev_alloc(sizeof(int64_t) * (nrecv > 0 ? nrecv : 1), s);
+            if (n > 0)
+                hipLaunchKernelGGL(k_valid_to_words, dim3(grid_for(n)), dim3(256), 0, st, c.v(), n, P<int64_t>(vw));
+            gather_col(P<int64_t>(vw), nullptr, P<int64_t>(idx), nsend, P<int64_t>(tmp), nullptr, st);
+            collective_a2av(s, P<int64_t>(tmp), sc.data(), P<int64_t>(rw), rc.data(), CAPSMI_I64);
+            x.valid = dev_alloc(nrecv > 0 ? nrecv : 1, s);
+            if (nrecv > 0)
+                hipLaunchKernelGGL(k_words_to_valid, dim3(grid_for(nrecv)), dim3(256), 0, st, P<int64_t>(rw), nrecv,
+                                   P<uint8_t>(x.valid));
+            HIP_CHECK(hipGetLastError());
+        }
+        o->cols.push_back(std::move(x));
+    }
+    o->partitioned = true;
+    return o;
+}
+
+// Rows of t hash-partitioned by its key columns `keys` (HashPartitioning): equal keys meet on one rank.
+// as_f64 (may be empty): per key 1 = a Long key hashed as the double it widens to, 2 = a Double key.
+// null_local: rows with a null key stay on this rank (they match nothing), else nulls hash as one value.
+capsmi_table* exchange_by_keys(capsmi_session* s, const capsmi_table* t, const std::vector<int>& keys,
+                               const std::vector<int>& as_f64, bool null_local) {
+    REQUIRE(keys.size() <= 8, CAPSMI_ERR_UNSUPPORTED, "exchange on more than 8 key columns");
+    KeyHashCols k{};
+    k.n = (int)keys.size();
+    for (size_t i = 0; i < keys.size(); ++i) {
+        const Column& c = t->cols.at(keys[i]);
+        k.d[i] = c.d();
+        k.v[i] = c.v();
+        k.as_f64[i] = i < as_f64.size() ? as_f64[i] : (c.type == CAPSMI_F64 ? 2 : 0);
+    }
+    const int64_t n = t->nrows;
+    Buf dest = dev_alloc(sizeof(uint64_t) * (n > 0 ? n : 1), s);
+    if (n > 0)
+        hipLaunchKernelGGL(k_key_dest, dim3(grid_for(n)), dim3(256), 0, s->stream, k, n, s->world,
+                           null_local ? s->rank : -1, P<uint64_t>(dest));
+    HIP_CHECK(hipGetLastError());
+    return exchange_rows(s, t, P<uint64_t>(dest));
+}
+
+// this rank's share of a table every rank holds whole (rows r with r mod world = rank)
+capsmi_table* slice_rows(capsmi_session* s, const capsmi_table* t) {
+    const int64_t n = t->nrows;
+    Buf dest = dev_alloc(sizeof(uint64_t) * (n > 0 ? n : 1), s);
+    if (n > 0)
+        hipLaunchKernelGGL(k_row_dest_slice, dim3(grid_for(n)), dim3(256), 0, s->stream, n, s->rank, s->world,
+                           P<uint64_t>(dest));
+    HIP_CHECK(hipGetLastError());
+    return exchange_rows(s, t, P<uint64_t>(dest));  // keeps its own share (sends to itself only)
+}
+
+// every rank's rows of t, concatenated in rank order (the ranks' partitions of a distributed result ->
+// the whole result on every rank)
+capsmi_table* gather_rows(capsmi_session* s, const capsmi_table* t) {
+    no_lists(t);
+    hipStream_t st = s->stream;
+    const int64_t n = t->nrows;
+    int64_t tot = 0;
+    std::vector<std::pair<Buf, Buf>> cols;
+    for (const Column& c : t->cols) {
+        Buf d = gather_words(s, reinterpret_cast<const uint64_t*>(c.d()), n, &tot), v;
+        if (c.valid) {
+            Buf vw = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
+            if (n > 0) hipLaunchKernelGGL(k_valid_to_words, dim3(grid_for(n)), dim3(256), 0, st, c.v(), n, P<int64_t>(vw));
+            HIP_CHECK(hipGetLastError());
+            int64_t t2 = 0;
+            Buf rw = gather_words(s, P<uint64_t>(vw), n, &t2);
+            v = dev_alloc(tot > 0 ? tot : 1, s);
+            if (tot > 0)
+                hipLaunchKernelGGL(k_words_to_valid, dim3(grid_for(tot)), dim3(256), 0, st, P<int64_t>(rw), tot, P<uint8_t>(v));
+            HIP_CHECK(hipGetLastError());
+        }
+        cols.push_back({d, v});
+    }
+    if (t->cols.empty()) {  // no columns: the row count alone
+        Buf c = dev_alloc(sizeof(int64_t), s);
+        fill_i64(P<int64_t>(c), n, 1, st);
+        collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(c), P<int64_t>(c), 1, CAPSMI_I64);
+        tot = read_scalar(s, P<int64_t>(c));
+    }
+    auto* o = new_table(s, tot);
+    for (size_t i = 0; i < t->cols.size(); ++i) {
+        Column x;
+        x.name = t->cols[i].name;
+        x.type = t->cols[i].type;
+        x.data = cols[i].first;
+        x.valid = cols[i].second;
+        o->cols.push_back(std::move(x));
+    }
+    o->partitioned = false;
+    return o;
 }
 
 Scramble make_scramble(int64_t lo, int64_t hi, int world) {

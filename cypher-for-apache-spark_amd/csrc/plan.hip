@@ -1703,14 +1703,54 @@ Res finish(Res r, const Names& need, const std::vector<Pred>& preds) {
     return owned(o);
 }
 
-// A row-local operator keeps its input's partitioning; an operator that needs every row of its input
-// (join, aggregate, distinct, order, skip, limit) cannot run on one rank's partition of a distributed
-// result -- Spark would insert an Exchange there (SparkTable.scala:133, 226), this backend only has the
-// exchanges of the fused routes.
-void refuse_partitioned(const capsmi_table* in, const char* op) {
-    REQUIRE(!in->partitioned, CAPSMI_ERR_UNSUPPORTED,
-            std::string(op) + " over one rank's partition of a distributed graph needs an exchange the fused routes "
-                              "do not provide (route this pattern, or run it on one device)");
+// ---- Exchanges of the generic operators over a distributed result ------------------------------------
+// A row-local operator keeps its input's partitioning.  An operator that needs rows of other ranks gets
+// the Exchange Spark's planner would insert (SparkTable.scala:133 groupBy, :226 join; CAPSSession.scala:
+// 118-119 partitions), built on the session's collective (k_dist.hip exchange_rows):
+//   join: a broadcast join when one side is whole on every rank and the partitioned side is the one whose
+//     rows the join type preserves (inner, cross, left outer with the left partitioned, right outer with the
+//     right partitioned); else both sides hash-partitioned on the join keys (a whole side first takes its
+//     slice; rows with a null key stay where they are: they match nothing).  The result is partitioned.
+//   grouping with keys, distinct: hash-partitioned on the grouping / distinct columns (nulls form one
+//     group), then the local operator: the result is partitioned (each group on one rank).
+//   a global aggregate, order by, skip, limit: every rank's rows gathered (all-gather), then the local
+//     operator: the result is whole on every rank.
+//   union all of a partitioned and a whole input: the whole one takes its slice.
+// String keys hash their dictionary codes: the ranks of a distributed graph share one dictionary (the same
+// ingest on every rank, as the JVM shim's session-wide dictionary).
+Res owned(capsmi_table* t);
+
+std::vector<int> key_indices(const capsmi_table* t, const Names& cols) {
+    std::vector<int> k;
+    for (const std::string& c : cols) k.push_back(col_of(t, c.c_str()));
+    return k;
+}
+
+// join inputs made co-partitioned (see above); false when neither side is partitioned
+bool dist_join_inputs(capsmi_session* s, int jt, const Names& lk, const Names& rk, Res& a, Res& b) {
+    const bool pa = a.t->partitioned, pb = b.t->partitioned;
+    if (!pa && !pb) return false;
+    if (jt == CAPSMI_JOIN_CROSS) {
+        if (pa && pb) b = owned(gather_rows(s, b.t));  // broadcast the right side
+        return true;
+    }
+    if ((jt == CAPSMI_JOIN_INNER && (!pa || !pb)) || (jt == CAPSMI_JOIN_LEFT_OUTER && pa && !pb) ||
+        (jt == CAPSMI_JOIN_RIGHT_OUTER && !pa && pb))
+        return true;  // broadcast join: the whole side is on every rank
+    if (!pa) a = owned(slice_rows(s, a.t));
+    if (!pb) b = owned(slice_rows(s, b.t));
+    const std::vector<int> li = key_indices(a.t, lk), ri = key_indices(b.t, rk);
+    std::vector<int> lf(li.size(), 0), rf(ri.size(), 0);
+    for (size_t i = 0; i < li.size(); ++i) {  // a Long key joined with a Double key hashes as the double
+        const int32_t x = a.t->cols[li[i]].type, y = b.t->cols[ri[i]].type;
+        if (x == CAPSMI_F64 || y == CAPSMI_F64) {
+            lf[i] = x == CAPSMI_F64 ? 2 : 1;
+            rf[i] = y == CAPSMI_F64 ? 2 : 1;
+        }
+    }
+    a = owned(exchange_by_keys(s, a.t, li, lf, true));
+    b = owned(exchange_by_keys(s, b.t, ri, rf, true));
+    return true;
 }
 
 // ---- unrouted-plan size guard (capsmi_session_set_unrouted_limit) ------------------------------------
@@ -1881,11 +1921,11 @@ Res exec(capsmi_table* t, const Names& need, std::vector<Pred> preds, const Pare
             guard_join(t);
             Res a = exec(x, nl, std::move(pl), par);
             Res b = exec(y, nr, std::move(pr), par);
-            refuse_partitioned(a.t, "a join");
-            refuse_partitioned(b.t, "a join");
+            const bool part = dist_join_inputs(t->sess, p.jt, p.a, p.b, a, b);
             auto lk = cstrs(p.a), rk = cstrs(p.b);
             capsmi_table* o = nullptr;
             check(eager_join(a.t, b.t, p.jt, (int32_t)lk.size(), lk.data(), rk.data(), &o));
+            o->partitioned = part;
             a.reset();
             b.reset();
             return finish(owned(o), need, stay);
@@ -1915,18 +1955,36 @@ Res exec(capsmi_table* t, const Names& need, std::vector<Pred> preds, const Pare
             run.jt = p.jt;
             run.n = p.n;
             bool part = false;
+            std::vector<Res> ins;
             for (size_t i = 0; i < p.in.size(); ++i) {
                 Res r = exec(p.in[i], nin[i], {}, par);
-                if (p.kind != PlanNode::UNION) refuse_partitioned(r.t, "an aggregate, distinct, order, skip or limit");
+                if (r.t->partitioned && p.kind != PlanNode::UNION) {  // the Exchange this operator needs
+                    capsmi_session* ss = t->sess;
+                    if ((p.kind == PlanNode::GROUP && !p.a.empty()) || p.kind == PlanNode::DISTINCT_ON) {
+                        r = owned(exchange_by_keys(ss, r.t, key_indices(r.t, p.a), {}, false));
+                    } else if (p.kind == PlanNode::DISTINCT) {
+                        std::vector<int> all(r.t->cols.size());
+                        for (size_t k = 0; k < all.size(); ++k) all[k] = (int)k;
+                        r = owned(exchange_by_keys(ss, r.t, all, {}, false));
+                    } else {  // global aggregate, order by, skip, limit: every rank's rows
+                        r = owned(gather_rows(ss, r.t));
+                    }
+                }
                 part = part || r.t->partitioned;
                 if (p.kind == PlanNode::UNION) {  // positional: the input's schema order
                     capsmi_table* o = nullptr;
                     auto c = cstrs(nin[i]);
                     check(eager_select(r.t, (int32_t)c.size(), c.data(), &o));
+                    o->partitioned = r.t->partitioned;
                     r = owned(o);
                 }
-                hold(run, r.t);
+                ins.push_back(std::move(r));
             }
+            if (p.kind == PlanNode::UNION && part)  // a whole input joins a partitioned one by its slice
+                for (Res& r : ins)
+                    if (!r.t->partitioned) r = owned(slice_rows(t->sess, r.t));
+            for (Res& r : ins) hold(run, r.t);
+            ins.clear();
             capsmi_table* o = exec_node(run);
             o->partitioned = part;
             return finish(owned(o), need, preds);

@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 T=${1:-dist}
-timeout -k 10 600 python -u -m pytest tests/test_gpu_dist_route.py tests/test_gpu_triangles.py tests/test_gpu_varlen.py tests/test_gpu_routing.py tests/test_gpu_ingest.py tests/test_gpu_undirected.py tests/test_gpu_count_star.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest tests/test_gpu_dist_route.py tests/test_gpu_dist_golden.py tests/test_gpu_triangles.py tests/test_gpu_varlen.py tests/test_gpu_routing.py tests/test_gpu_ingest.py tests/test_gpu_undirected.py tests/test_gpu_count_star.py -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1 || exit $?
 # the undirected 2-hop at s = 26 through the route (count(*): the record partition with both arcs), beside
 # the directed cold / count(*) lines
 timeout -k 10 600 python -u bench.py --modes cold,count,und_count,und_distinct --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/${T}_und_bench.log 2>&1 || exit $?
