@@ -134,6 +134,36 @@ __global__ void k_words_to_valid(const int64_t* __restrict__ w, int64_t n, uint8
         v[r] = (uint8_t)(w[r] != 0);
 }
 
+// list columns: each row's list length (0 for a null row) in the order `idx` (or row order when null)
+__global__ void k_list_lens(const int64_t* __restrict__ li, const uint8_t* __restrict__ valid,
+                            const int64_t* __restrict__ off, const int64_t* __restrict__ idx, int64_t n,
+                            int64_t* __restrict__ len) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = idx ? idx[k] : k;
+        len[k] = (valid && !valid[r]) ? 0 : off[li[r] + 1] - off[li[r]];
+    }
+}
+
+// the rows' list values back to back in the order `idx` (voff: exclusive prefix of their lengths)
+__global__ void k_list_pack(const int64_t* __restrict__ li, const uint8_t* __restrict__ valid,
+                            const int64_t* __restrict__ off, const int64_t* __restrict__ vals,
+                            const int64_t* __restrict__ idx, int64_t n, const int64_t* __restrict__ voff,
+                            int64_t* __restrict__ out) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = idx ? idx[k] : k;
+        if (valid && !valid[r]) continue;
+        const int64_t b = off[li[r]], e = off[li[r] + 1];
+        for (int64_t j = b; j < e; ++j) out[voff[k] + (j - b)] = vals[j];
+    }
+}
+
+// value counts per destination: voff at the row-segment boundaries (rs: W + 1 row starts)
+__global__ void k_seg_values(const int64_t* __restrict__ voff, const int64_t* __restrict__ rs, int W,
+                             int64_t* __restrict__ out) {
+    const int q = threadIdx.x;
+    if (q < W) out[q] = voff[rs[q + 1]] - voff[rs[q]];
+}
+
 __global__ void k_owned_flags(const int64_t* __restrict__ in, int64_t n, int64_t lo, int64_t hi, uint64_t mul,
                               uint64_t mask, int64_t own_lo, int64_t own_hi, uint8_t* __restrict__ flags) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -232,10 +262,27 @@ capsmi_table* new_table(capsmi_session* s, int64_t nrows) {
     return t;
 }
 
-void no_lists(const capsmi_table* t) {
-    for (const Column& c : t->cols)
-        REQUIRE(!is_list_type(c.type), CAPSMI_ERR_UNSUPPORTED,
-                "list column '" + c.name + "' in an exchange of a distributed result");
+}  // namespace
+
+namespace {
+// a list column of n rows over (lengths, values): row r holds list r (null rows: empty lists, valid 0)
+Column list_column(capsmi_session* s, const Column& like, const Buf& lens, int64_t n, const Buf& values,
+                   int64_t nvalues, const Buf& valid) {
+    auto L = std::make_shared<ListStore>();
+    L->elem = like.list->elem;
+    L->nlists = n;
+    L->nvalues = nvalues;
+    L->offsets = dev_alloc(sizeof(int64_t) * (n + 1), s);
+    exclusive_scan_i64(P<int64_t>(lens), P<int64_t>(L->offsets), n, s);
+    L->values = values;
+    Column x;
+    x.name = like.name;
+    x.type = like.type;
+    x.data = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
+    iota_i64(P<int64_t>(x.data), 0, n, s->stream);
+    x.valid = valid;
+    x.list = L;
+    return x;
 }
 }  // namespace
 
@@ -243,7 +290,6 @@ void no_lists(const capsmi_table* t) {
 // indices by destination, every column is gathered in that order and exchanged (one ALL_TO_ALL_V per
 // column, validity as a word column).  Returns this rank's received rows, rank-major, same schema.
 capsmi_table* exchange_rows(capsmi_session* s, const capsmi_table* t, uint64_t* dest) {
-    no_lists(t);
     hipStream_t st = s->stream;
     const int W = s->world;
     const int64_t n = t->nrows;
@@ -269,7 +315,59 @@ capsmi_table* exchange_rows(capsmi_session* s, const capsmi_table* t, uint64_t* 
     }
     auto* o = new_table(s, nrecv);
     Buf tmp = dev_alloc(sizeof(int64_t) * (nsend > 0 ? nsend : 1), s);
+    Buf rs;  // list columns: the W + 1 starts of the destination segments of the ordered rows
     for (const Column& c : t->cols) {
+        if (is_list_type(c.type)) {  // lengths with the rows, then the values with per-rank value counts
+            REQUIRE(c.list, CAPSMI_ERR_INTERNAL, "list column without a store");
+            if (!rs) {
+                rs = dev_alloc(sizeof(int64_t) * (W + 1), s);
+                std::vector<int64_t> h(W + 1, 0);
+                for (int q = 0; q < W; ++q) h[q + 1] = h[q] + sc[q];
+                HIP_CHECK(hipMemcpyAsync(P<int64_t>(rs), h.data(), sizeof(int64_t) * (W + 1), hipMemcpyHostToDevice, st));
+            }
+            const ListStore& L = *c.list;
+            Buf lens = dev_alloc(sizeof(int64_t) * (nsend + 1), s), voff = dev_alloc(sizeof(int64_t) * (nsend + 1), s);
+            if (nsend > 0)
+                hipLaunchKernelGGL(k_list_lens, dim3(grid_for(nsend)), dim3(256), 0, st, c.d(), c.v(),
+                                   P<int64_t>(L.offsets), P<int64_t>(idx), nsend, P<int64_t>(lens));
+            exclusive_scan_i64(P<int64_t>(lens), P<int64_t>(voff), nsend, s);
+            Buf vc = dev_alloc(sizeof(int64_t) * (W + (size_t)W * W), s);
+            hipLaunchKernelGGL(k_seg_values, dim3(1), dim3(256), 0, st, P<int64_t>(voff), P<int64_t>(rs), W, P<int64_t>(vc));
+            HIP_CHECK(hipGetLastError());
+            collective(s, CAPSMI_COLL_ALL_GATHER, P<int64_t>(vc), P<int64_t>(vc) + W, W, CAPSMI_I64);
+            std::vector<int64_t> vm((size_t)W * W), vs(W), vr(W);
+            HIP_CHECK(hipMemcpyAsync(vm.data(), P<int64_t>(vc) + W, sizeof(int64_t) * vm.size(), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            int64_t vsend = 0, vrecv = 0;
+            for (int q = 0; q < W; ++q) {
+                vs[q] = vm[(size_t)s->rank * W + q];
+                vr[q] = vm[(size_t)q * W + s->rank];
+                vsend += vs[q];
+                vrecv += vr[q];
+            }
+            Buf packed = dev_alloc(sizeof(int64_t) * (vsend > 0 ? vsend : 1), s);
+            if (nsend > 0)
+                hipLaunchKernelGGL(k_list_pack, dim3(grid_for(nsend)), dim3(256), 0, st, c.d(), c.v(), P<int64_t>(L.offsets),
+                                   P<int64_t>(L.values), P<int64_t>(idx), nsend, P<int64_t>(voff), P<int64_t>(packed));
+            HIP_CHECK(hipGetLastError());
+            Buf rlens = dev_alloc(sizeof(int64_t) * (nrecv + 1), s), rvals = dev_alloc(sizeof(int64_t) * (vrecv > 0 ? vrecv : 1), s);
+            collective_a2av(s, P<int64_t>(lens), sc.data(), P<int64_t>(rlens), rc.data(), CAPSMI_I64);
+            collective_a2av(s, P<int64_t>(packed), vs.data(), P<int64_t>(rvals), vr.data(), CAPSMI_I64);
+            Buf valid;
+            if (c.valid) {
+                Buf vw = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s), rw = dev_alloc(sizeof(int64_t) * (nrecv > 0 ? nrecv : 1), s);
+                if (n > 0) hipLaunchKernelGGL(k_valid_to_words, dim3(grid_for(n)), dim3(256), 0, st, c.v(), n, P<int64_t>(vw));
+                gather_col(P<int64_t>(vw), nullptr, P<int64_t>(idx), nsend, P<int64_t>(tmp), nullptr, st);
+                collective_a2av(s, P<int64_t>(tmp), sc.data(), P<int64_t>(rw), rc.data(), CAPSMI_I64);
+                valid = dev_alloc(nrecv > 0 ? nrecv : 1, s);
+                if (nrecv > 0)
+                    hipLaunchKernelGGL(k_words_to_valid, dim3(grid_for(nrecv)), dim3(256), 0, st, P<int64_t>(rw), nrecv,
+                                       P<uint8_t>(valid));
+                HIP_CHECK(hipGetLastError());
+            }
+            o->cols.push_back(list_column(s, c, rlens, nrecv, rvals, vrecv, valid));
+            continue;
+        }
         Column x;
         x.name = c.name;
         x.type = c.type;
@@ -331,13 +429,35 @@ capsmi_table* slice_rows(capsmi_session* s, const capsmi_table* t) {
 // every rank's rows of t, concatenated in rank order (the ranks' partitions of a distributed result ->
 // the whole result on every rank)
 capsmi_table* gather_rows(capsmi_session* s, const capsmi_table* t) {
-    no_lists(t);
     hipStream_t st = s->stream;
     const int64_t n = t->nrows;
     int64_t tot = 0;
     std::vector<std::pair<Buf, Buf>> cols;
-    for (const Column& c : t->cols) {
-        Buf d = gather_words(s, reinterpret_cast<const uint64_t*>(c.d()), n, &tot), v;
+    std::vector<std::pair<Buf, int64_t>> lvals(t->cols.size());  // list columns: gathered values
+    for (size_t ci = 0; ci < t->cols.size(); ++ci) {
+        const Column& c = t->cols[ci];
+        Buf d, v;
+        if (is_list_type(c.type)) {  // gathered lengths (as the column data for now) and values
+            REQUIRE(c.list, CAPSMI_ERR_INTERNAL, "list column without a store");
+            const ListStore& L = *c.list;
+            Buf lens = dev_alloc(sizeof(int64_t) * (n + 1), s), voff = dev_alloc(sizeof(int64_t) * (n + 1), s);
+            if (n > 0)
+                hipLaunchKernelGGL(k_list_lens, dim3(grid_for(n)), dim3(256), 0, st, c.d(), c.v(), P<int64_t>(L.offsets),
+                                   (const int64_t*)nullptr, n, P<int64_t>(lens));
+            exclusive_scan_i64(P<int64_t>(lens), P<int64_t>(voff), n, s);
+            const int64_t nv = read_scalar(s, P<int64_t>(voff) + n);
+            Buf packed = dev_alloc(sizeof(int64_t) * (nv > 0 ? nv : 1), s);
+            if (n > 0)
+                hipLaunchKernelGGL(k_list_pack, dim3(grid_for(n)), dim3(256), 0, st, c.d(), c.v(), P<int64_t>(L.offsets),
+                                   P<int64_t>(L.values), (const int64_t*)nullptr, n, P<int64_t>(voff), P<int64_t>(packed));
+            HIP_CHECK(hipGetLastError());
+            int64_t tv = 0;
+            lvals[ci] = {gather_words(s, P<uint64_t>(packed), nv, &tv), 0};
+            lvals[ci].second = tv;
+            d = gather_words(s, P<uint64_t>(lens), n, &tot);
+        } else {
+            d = gather_words(s, reinterpret_cast<const uint64_t*>(c.d()), n, &tot);
+        }
         if (c.valid) {
             Buf vw = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
             if (n > 0) hipLaunchKernelGGL(k_valid_to_words, dim3(grid_for(n)), dim3(256), 0, st, c.v(), n, P<int64_t>(vw));
@@ -359,6 +479,11 @@ capsmi_table* gather_rows(capsmi_session* s, const capsmi_table* t) {
     }
     auto* o = new_table(s, tot);
     for (size_t i = 0; i < t->cols.size(); ++i) {
+        if (is_list_type(t->cols[i].type)) {
+            o->cols.push_back(list_column(s, t->cols[i], cols[i].first, tot, lvals[i].first, lvals[i].second,
+                                          cols[i].second));
+            continue;
+        }
         Column x;
         x.name = t->cols[i].name;
         x.type = t->cols[i].type;
