@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
             const uint64_t x = (uint64_t)(sr[u] - lo), y = (uint64_t)(tr[u] - lo);
             const bool ok = e < m && x < (uint64_t)range && y < (uint64_t)range;
             const bool ain = ok && bit(a, x), aout = ok && bit(c, y);
-            if (!UND) {
+            if constexpr (!UND) {
                 if (ain && x == y && bit(b, x) && bit(c, x)) ++nl;
             } else if (ok) {  // the reverse arc y -> x of a non-loop, and the r1 = r2 bindings
                 const bool ay = bit(a, y), cx = bit(c, x), bx = bit(b, x), by = bit(b, y);
@@ -217,7 +217,7 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
         for (int u = 0; u < IT; ++u) {
             rin[u] = ((vin >> u) & 1u) ? atomicAdd(&cnt[ys[u] >> kBits], 1u) : 0u;
             rout[u] = ((vout >> u) & 1u) ? atomicAdd(&cnt[nb + (xs[u] >> kBits)], 1u) : 0u;
-            if (UND) {
+            if constexpr (UND) {
                 rin2[u] = ((vin2 >> u) & 1u) ? atomicAdd(&cnt[xs[u] >> kBits], 1u) : 0u;
                 rout2[u] = ((vout2 >> u) & 1u) ? atomicAdd(&cnt[nb + (ys[u] >> kBits)], 1u) : 0u;
             }
@@ -228,7 +228,7 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
         for (int u = 0; u < IT; ++u) {
             if ((vin >> u) & 1u) stage[loc[ys[u] >> kBits] + rin[u]] = (uint16_t)(ys[u] & 0xFFFFu);
             if ((vout >> u) & 1u) stage[loc[nb + (xs[u] >> kBits)] + rout[u]] = (uint16_t)(xs[u] & 0xFFFFu);
-            if (UND) {
+            if constexpr (UND) {
                 if ((vin2 >> u) & 1u) stage[loc[xs[u] >> kBits] + rin2[u]] = (uint16_t)(xs[u] & 0xFFFFu);
                 if ((vout2 >> u) & 1u) stage[loc[nb + (ys[u] >> kBits)] + rout2[u]] = (uint16_t)(ys[u] & 0xFFFFu);
             }
@@ -283,15 +283,17 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
                 const int d = (int)rout[u] - (int)pc[bk];
                 if (d >= 0) hold[bk * kPiece + d] = (uint16_t)(xs[u] & 0xFFFFu);
             }
-            if (UND && ((vin2 >> u) & 1u)) {
-                const uint32_t bk = xs[u] >> kBits;
-                const int d = (int)rin2[u] - (int)pc[bk];
-                if (d >= 0) hold[bk * kPiece + d] = (uint16_t)(xs[u] & 0xFFFFu);
-            }
-            if (UND && ((vout2 >> u) & 1u)) {
-                const uint32_t bk = nb + (ys[u] >> kBits);
-                const int d = (int)rout2[u] - (int)pc[bk];
-                if (d >= 0) hold[bk * kPiece + d] = (uint16_t)(ys[u] & 0xFFFFu);
+            if constexpr (UND) {
+                if ((vin2 >> u) & 1u) {
+                    const uint32_t bk = xs[u] >> kBits;
+                    const int d = (int)rin2[u] - (int)pc[bk];
+                    if (d >= 0) hold[bk * kPiece + d] = (uint16_t)(xs[u] & 0xFFFFu);
+                }
+                if ((vout2 >> u) & 1u) {
+                    const uint32_t bk = nb + (ys[u] >> kBits);
+                    const int d = (int)rout2[u] - (int)pc[bk];
+                    if (d >= 0) hold[bk * kPiece + d] = (uint16_t)(ys[u] & 0xFFFFu);
+                }
             }
         }
         __syncthreads();

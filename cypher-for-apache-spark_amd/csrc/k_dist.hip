@@ -52,15 +52,16 @@ __global__ void k_unscramble(int64_t* __restrict__ v, int64_t n, int64_t lo, uin
 
 // counts[q] = #{i : low byte of the sorted dest[i] == q}, q < world: one binary search per rank boundary
 __global__ void k_dest_counts(const uint64_t* __restrict__ dest, int64_t n, int world, int64_t* __restrict__ counts) {
-    const int q = threadIdx.x;
-    if (q > world) return;
+    const int q = threadIdx.x;  // one block of 256 lanes, world < 255
     __shared__ int64_t at[257];
-    int64_t a = 0, b = n;  // first i with dest[i] >= q
-    while (a < b) {
-        const int64_t mid = (a + b) >> 1;
-        if ((int64_t)(dest[mid] & 0xFF) < q) a = mid + 1; else b = mid;
+    if (q <= world) {
+        int64_t a = 0, b = n;  // first i with dest[i] >= q
+        while (a < b) {
+            const int64_t mid = (a + b) >> 1;
+            if ((int64_t)(dest[mid] & 0xFF) < q) a = mid + 1; else b = mid;
+        }
+        at[q] = a;
     }
-    at[q] = a;
     __syncthreads();
     if (q < world) counts[q] = at[q + 1] - at[q];
 }

@@ -1029,6 +1029,13 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     const int bits = bits_for((uint64_t)n);
     REQUIRE(!dd || (bits + 7) / 8 * 8 <= 24, CAPSMI_ERR_UNSUPPORTED,
             "distributed triangle count: at most 2^24 ids (coded oriented keys)");
+    int64_t m_all = m;  // every rank's relationships (bounds the out-degrees below)
+    if (dd) {
+        Buf t = dev_alloc(sizeof(int64_t), s);
+        fill_i64(P<int64_t>(t), m, 1, st);
+        collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(t), P<int64_t>(t), 1, CAPSMI_I64);
+        m_all = read_scalar(s, P<int64_t>(t));
+    }
     // the direction bit rides unsorted at bit 31 when max's digits end at or below bit 24
     const int msh = bits > 24 ? 1 : 0;
     g.sl = dev_alloc(sizeof(uint32_t) * n, s);
@@ -1189,7 +1196,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     if (g.vmt > 0 && ne > 0) {
         // packed in-keys (key-only sort) when ids and positions fit: od(u) <= sqrt(2m) under a degree
         // order (every out-neighbour has at least u's degree), so m < 2^31 relationships bound it by 2^16
-        const bool packed = g.ib <= 24 && m < (int64_t(1) << 31);
+        const bool packed = g.ib <= 24 && m_all < (int64_t(1) << 31);
         const int tsh = packed ? g.ib + 16 : 32;
         Buf ik = dev_alloc(sizeof(uint64_t) * ne, s), iv = packed ? Buf() : dev_alloc(sizeof(int64_t) * ne, s);
         hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off), ne, tc,
