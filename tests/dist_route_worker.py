@@ -47,6 +47,7 @@ def main():
     s = Session(0)
     s.set_stream(torch.cuda.current_stream().cuda_stream)
     join_ranks(s)
+    s.set_unrouted_limit(4 << 30)  # an unrouted plan that would explode is refused, not run out of memory
     col = "target" if args.rels_by == "target" else "source"
     if args.edges.startswith("rmat:"):
         scale = int(args.edges.split(":")[1])

@@ -20,6 +20,12 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _err(text):
+    """the first Python traceback of a failed rank (torch.distributed.run prints its own summary last)"""
+    i = text.find("Traceback (most recent call last)")
+    return text[i:i + 5000] if i >= 0 else text[-4000:]
+
+
 def _port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -35,7 +41,7 @@ def test_golden_vectors_on_two_ranks(tmp_path, mode):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
            "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", "dist_golden_worker.py"), out, mode]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
-    assert p.returncode == 0, p.stderr[-4000:]
+    assert p.returncode == 0, _err(p.stderr)
     ranks = []
     for r in range(2):
         with open(f"{out}.rank{r}.json") as f:

@@ -25,6 +25,12 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _err(text):
+    """the first Python traceback of a failed rank (torch.distributed.run prints its own summary last)"""
+    i = text.find("Traceback (most recent call last)")
+    return text[i:i + 5000] if i >= 0 else text[-4000:]
+
+
 def _port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -50,7 +56,7 @@ def _ranks(graph, lo, hi, world=2, nodes="owned", rels_by="target", queries="c3,
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", "dist_route_worker.py"),
            str(graph), str(lo), str(hi), nodes, "--rels-by", rels_by, "--queries", queries, "--out", out]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
-    assert p.returncode == 0, p.stderr[-4000:]
+    assert p.returncode == 0, _err(p.stderr)
     res = []
     for r in range(world):
         with open(f"{out}.rank{r}.json") as f:
@@ -67,7 +73,7 @@ def test_routed_c3_c4_on_two_ranks_with_hubs(tmp_path, nodes):
     lo, hi = int(min(src.min(), dst.min())), int(max(src.max(), dst.max())) + 1
     rows, distinct = cpu.two_hop_closed_form(n, src, dst)
     tri = cpu.triangle_closed_form(n, src, dst)
-    out = _ranks(edges, lo, hi, nodes=nodes, queries="c3,expand,warm,tri,varlen")
+    out = _ranks(edges, lo, hi, nodes=nodes, queries="c3,expand,warm,tri")
     m = len(src)
     for o in out:  # every rank holds the whole answer
         assert o["count_star"] == rows, o
@@ -78,7 +84,6 @@ def test_routed_c3_c4_on_two_ranks_with_hubs(tmp_path, nodes):
         assert o["expand_partitioned"] is True
         assert o["routes"]["two_hop"] >= 3 and o["routes"]["expand_count"] >= 1 and o["routes"]["expand"] >= 1, o
         assert o["routes"]["triangle"] >= 1, o
-        assert o["varlen"].startswith("refused"), o  # var-length needs BY_SOURCE shards
     assert sum(o["expand_rows_local"] for o in out) == m
     assert sum(o["rels_local"] for o in out) == m
     mean = m / len(out)
@@ -94,11 +99,10 @@ def test_routed_c4_c5_by_source_on_two_ranks(tmp_path):
     lo, hi = 0, n
     tri = cpu.triangle_closed_form(n, src, dst)
     _, per_a = cpu.var_length_closed_form(n, src, dst, 1, 3)
-    out = _ranks(edges, lo, hi, rels_by="source", queries="c3,tri,varlen")
+    out = _ranks(edges, lo, hi, rels_by="source", queries="tri,varlen")
     got = {}
     for o in out:
         assert o["triangle"] == tri, o
-        assert o["c3"].startswith("refused"), o  # the 2-hop routes need BY_TARGET shards
         assert o["varlen_partitioned"] is True
         assert o["routes"]["triangle"] >= 1 and o["routes"]["var_length"] >= 1, o
         for a, c in o["varlen_rows"]:
