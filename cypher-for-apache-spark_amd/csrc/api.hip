@@ -159,6 +159,8 @@ Buf dev_alloc(size_t bytes, capsmi_session* s) {
                 if (auto p = w.lock()) trim_ctx_locked(c, *p);
         }
         (void)hipDeviceSynchronize();
+        hipMemPool_t pool;  // and the freed memory the stream-ordered pool still reserves
+        if (hipDeviceGetDefaultMemPool(&pool, s->device) == hipSuccess) (void)hipMemPoolTrimTo(pool, 0);
         e = hipMallocAsync(&b->ptr, want, s->stream);
     }
     if (e != hipSuccess) {
@@ -492,7 +494,10 @@ capsmi_status capsmi_session_create(int32_t device, capsmi_session** out) {
     HIP_CHECK(hipHostMalloc((void**)&s->pinned, 64, hipHostMallocDefault));
     hipMemPool_t pool;
     if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+        // keep freed pool memory mapped (no unmap / remap per query); CAPSMI_POOL_KEEP_BYTES caps what the
+        // pool keeps when several processes share one device (a rehearsal of N ranks on one GPU)
         uint64_t thr = UINT64_MAX;
+        if (const char* e = getenv("CAPSMI_POOL_KEEP_BYTES")) thr = strtoull(e, nullptr, 10);
         (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
     }
     *out = s;

@@ -421,9 +421,10 @@ struct TriGraph {
     // lower end it owns, while ok / tg hold every oriented edge)
     int64_t nek = 0;
     bool dist = false;
-    // per-center work estimates (list entries walked) for the work-balanced shares of tri_count: prefix
-    // sums over big_u / vm_c / small_u, nbig + 1 / nvm + 1 / nsmall + 1 entries, host copies (empty:
-    // equal center counts)
+    // work-balanced shares of tri_count over `wparts` parts (a distributed build: the world size): the
+    // first center of each part in big_u / vm_c / small_u (wparts + 1 entries each), cut where the prefix
+    // sums of the centers' walked entries reach equal shares (empty: equal center counts)
+    int wparts = 0;
     std::vector<int64_t> wbig, wvm, wsmall;
 };
 // a distributed build (multi-GPU C4): this rank's relationships are any 1/world of them; the owner of a

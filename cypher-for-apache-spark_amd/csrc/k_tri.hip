@@ -991,6 +991,21 @@ __global__ void k_tri_work_v(const int64_t* __restrict__ cs, int64_t nc, const i
     }
 }
 
+// part boundaries: cut[q] = first center whose exclusive work prefix reaches total * q / parts (q < parts),
+// cut[parts] = nc; pre holds nc + 1 prefix sums
+__global__ void k_tri_cuts(const int64_t* __restrict__ pre, int64_t nc, int parts, int64_t* __restrict__ cut) {
+    const int q = threadIdx.x;
+    if (q > parts) return;  // one thread per boundary, no barrier
+    if (q == parts) { cut[q] = nc; return; }
+    const int64_t want = (int64_t)((__int128)pre[nc] * q / parts);
+    int64_t a = 0, b = nc;  // first i in [0, nc] with pre[i] >= want
+    while (a < b) {
+        const int64_t mid = (a + b) >> 1;
+        if (pre[mid] < want) a = mid + 1; else b = mid;
+    }
+    cut[q] = a;
+}
+
 inline int grid(const capsmi_session* s, int64_t n) {
     int64_t g = (n + 255) / 256;
     const int64_t cap = (int64_t)s->num_cus * 16;
@@ -1053,7 +1068,6 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         }
     }
     if (dd) {  // every relationship of a pair to the owner of the pair's lower end
-        KernelTimer kt(s, "tri_exchange");
         Buf dest = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s);
         if (m > 0)
             hipLaunchKernelGGL(k_tri_dest_min, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, dd->span,
@@ -1063,6 +1077,8 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         key = exchange_words(s, P<uint64_t>(dest), P<uint64_t>(key), m, &mr);
         m = mr;
     }
+    // build phases timed on the device (pure device work between the exchanges; bench kernel_ms)
+    std::unique_ptr<KernelTimer> ph(new KernelTimer(s, "tri_sort_und"));
     // one sort of the undirected keys: digits of max (and the direction bit when msh) then of min; the
     // upper ends' degrees are counted between the two halves, while the keys are in max order
     Buf deg = dev_alloc(sizeof(uint32_t) * n, s);
@@ -1099,11 +1115,13 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     f.reset();
     heads.reset();
     g.nek = ne;
+    ph.reset();
     if (dd) {  // a pair's relationships are all on one rank: the sums over the ranks are exact
         collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<uint32_t>(deg), P<uint32_t>(deg), n, CAPSMI_COLL_U32);
         collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<uint32_t>(g.sl), P<uint32_t>(g.sl), n, CAPSMI_COLL_U32);
     }
     // degree-order ids (hubs first): sort the vertices by (degree, id)
+    ph.reset(new KernelTimer(s, "tri_order"));
     Buf rid = dev_alloc(sizeof(uint32_t) * n, s);
     g.orig = dev_alloc(sizeof(int64_t) * n, s);
     {
@@ -1133,8 +1151,8 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     std::vector<int> od;  // (source, target): grouped and target-sorted lists
     for (int sh = 0; sh < bits; sh += 8) od.push_back(sh);
     for (int sh = 32; sh < 32 + bits; sh += 8) od.push_back(sh);
+    ph.reset();
     if (dd) {
-        KernelTimer kt(s, "tri_exchange");
         // the exceptions' exact payloads (rare): every rank's list, for the placement in the whole key array
         const int64_t nexc = (int64_t)read_scalar(s, reinterpret_cast<const int64_t*>(nlong));
         int64_t nexc_all = 0;
@@ -1173,14 +1191,19 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         HIP_CHECK(hipGetLastError());
         int64_t nr = 0;
         Buf mine = exchange_words(s, P<uint64_t>(dest), P<uint64_t>(g.ok), ne, &nr);
-        radix_sort_digits(s, P<uint64_t>(mine), nullptr, nr, od);  // this rank's source range, sorted
+        {
+            KernelTimer kt(s, "tri_sort_or");
+            radix_sort_digits(s, P<uint64_t>(mine), nullptr, nr, od);  // this rank's source range, sorted
+        }
         g.ok = gather_words(s, P<uint64_t>(mine), nr, &ne);          // the ranges in rank order: all sorted
         g.ov = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);
     } else {
         // no kNone among the oriented keys; coded: key-only (the payloads ride in the key)
+        KernelTimer kt(s, "tri_sort_or");
         radix_sort_digits(s, P<uint64_t>(g.ok), tc.cb ? nullptr : P<int64_t>(g.ov), ne, od);
     }
     g.ne = ne;
+    ph.reset(new KernelTimer(s, "tri_post"));
     if (tc.cb && ne > 0)
         hipLaunchKernelGGL(k_exc_place, dim3(grid(s, ne / 64 + 1)), dim3(256), 0, st, P<uint64_t>(exc), nlong,
                            P<uint64_t>(g.ok), ne, tc, P<int64_t>(g.ov));
@@ -1227,7 +1250,9 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     g.nsmall = flags_to_indices(s, P<uint8_t>(fsm), n, g.small_u);
     g.nbig = flags_to_indices(s, P<uint8_t>(fbg), n, g.big_u);
     HIP_CHECK(hipGetLastError());
+    ph.reset();
     if (dd) {  // work-balanced shares: prefix sums of the centers' walked entries, host copies
+        KernelTimer kt(s, "tri_work");
         auto work = [&](const Buf& cs, int64_t nc, bool vm, std::vector<int64_t>& out) {
             Buf w = dev_alloc(sizeof(int64_t) * (2 * nc + 2), s);
             if (nc > 0) {
@@ -1241,11 +1266,16 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
                 HIP_CHECK(hipGetLastError());
             }
             exclusive_scan_i64(P<int64_t>(w), P<int64_t>(w) + nc + 1, nc, s);
-            out.resize(nc + 1);
-            HIP_CHECK(hipMemcpyAsync(out.data(), P<int64_t>(w) + nc + 1, sizeof(int64_t) * (nc + 1),
-                                     hipMemcpyDeviceToHost, st));
+            const int W = dd->world;
+            Buf cut = dev_alloc(sizeof(int64_t) * (W + 1), s);
+            hipLaunchKernelGGL(k_tri_cuts, dim3(1), dim3(256), 0, st, P<int64_t>(w) + nc + 1, nc, W, P<int64_t>(cut));
+            HIP_CHECK(hipGetLastError());
+            out.resize(W + 1);
+            HIP_CHECK(hipMemcpyAsync(out.data(), P<int64_t>(cut), sizeof(int64_t) * (W + 1), hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
         };
+        REQUIRE(dd->world <= 255, CAPSMI_ERR_UNSUPPORTED, "distributed triangle count: at most 255 ranks");
+        g.wparts = dd->world;
         work(g.big_u, g.nbig, false, g.wbig);
         work(g.vm_c, g.nvm, true, g.wvm);
         work(g.small_u, g.nsmall, false, g.wsmall);
@@ -1262,14 +1292,10 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
         KernelTimer kt(s, "triangles");
         // this part's slice of each center list: equal work (the walked-entry prefix sums of a distributed
         // build), else equal center counts
-        auto share = [&](int64_t nc, const std::vector<int64_t>& w, int64_t& b, int64_t& e) {
-            if (nc > 0 && w.size() == (size_t)nc + 1 && w[nc] > 0) {
-                auto at = [&](int q) -> int64_t {
-                    if (q >= nparts) return nc;
-                    return std::lower_bound(w.begin(), w.end(), w[nc] * q / nparts) - w.begin();
-                };
-                b = std::min(at(part), nc);
-                e = std::min(at(part + 1), nc);
+        auto share = [&](int64_t nc, const std::vector<int64_t>& cut, int64_t& b, int64_t& e) {
+            if (g.wparts == nparts && cut.size() == (size_t)nparts + 1) {
+                b = std::min(cut[part], nc);
+                e = std::min(cut[part + 1], nc);
             } else {
                 b = nc * part / nparts;
                 e = nc * (part + 1) / nparts;
