@@ -294,7 +294,8 @@ def main():
     t0 = time.perf_counter()
     ingest_gate = None
     if distributed:
-        from capsmi.dist import serial_gate
+        from capsmi.dist import distribute, join_ranks, serial_gate
+        join_ranks(sess)  # the rank view first: capsmi_owned_rows owns by (rank, world)
         ingest_gate = serial_gate()  # a serialised rehearsal also serialises the ranks' ingest peaks
         if ingest_gate:
             ingest_gate.acquire()
@@ -304,8 +305,6 @@ def main():
                                part_col=graph.PART_TARGET if shards > 1 else graph.PART_NONE, part=part, nparts=shards)
     persons = graph.rmat_nodes(sess, scale, graph.NODES_ALL)
     if distributed:
-        from capsmi.dist import distribute, join_ranks
-        join_ranks(sess)
         persons = persons.owned_rows("id", 0, n).as_node_table("id")
         distribute(sess, 0, n, [persons], [rels], nodes_owned=True, rels_by="target")
     m_local = rels.size

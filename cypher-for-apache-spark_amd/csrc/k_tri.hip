@@ -973,6 +973,21 @@ __global__ void k_tri_work_u(const int64_t* __restrict__ cs, int64_t nc, const i
     }
 }
 
+// the same for the small centers (a few entries each): one lane per center keeps 64 of them in flight
+__global__ void k_tri_work_u1(const int64_t* __restrict__ cs, int64_t nc, const int64_t* __restrict__ off,
+                              const uint32_t* __restrict__ tg, uint32_t idmask, int vmt, int64_t* __restrict__ w) {
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t u = cs[c], b = off[u], d = off[u + 1] - b;
+        int64_t acc = d;
+        for (int64_t p = 0; p < d; ++p) {
+            const uint32_t v = tg[b + p] & idmask;
+            const int64_t odv = off[v + 1] - off[v];
+            if (!(vmt > 0 && odv >= vmt && p < odv)) acc += odv;
+        }
+        w[c] = acc;
+    }
+}
+
 // work of a v-mode center: out(v) for the hash and the prefix out(u)[0, p) of every in-edge it takes
 __global__ void k_tri_work_v(const int64_t* __restrict__ cs, int64_t nc, const int64_t* __restrict__ off,
                              const int64_t* __restrict__ ioff, const uint32_t* __restrict__ ipos,
@@ -1253,11 +1268,14 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     ph.reset();
     if (dd) {  // work-balanced shares: prefix sums of the centers' walked entries, host copies
         KernelTimer kt(s, "tri_work");
-        auto work = [&](const Buf& cs, int64_t nc, bool vm, std::vector<int64_t>& out) {
+        auto work = [&](const Buf& cs, int64_t nc, bool vm, bool small, std::vector<int64_t>& out) {
             Buf w = dev_alloc(sizeof(int64_t) * (2 * nc + 2), s);
             if (nc > 0) {
                 const unsigned gw = (unsigned)std::min<int64_t>((nc + 3) / 4, (int64_t)s->num_cus * 16);
-                if (vm)
+                if (small)
+                    hipLaunchKernelGGL(k_tri_work_u1, dim3(grid(s, nc)), dim3(256), 0, st, P<int64_t>(cs), nc,
+                                       P<int64_t>(g.off), P<uint32_t>(g.tg), tc.idmask(), g.vmt, P<int64_t>(w));
+                else if (vm)
                     hipLaunchKernelGGL(k_tri_work_v, dim3(gw), dim3(256), 0, st, P<int64_t>(cs), nc, P<int64_t>(g.off),
                                        P<int64_t>(g.ioff), P<uint32_t>(g.ipos), P<int64_t>(w));
                 else
@@ -1276,9 +1294,9 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         };
         REQUIRE(dd->world <= 255, CAPSMI_ERR_UNSUPPORTED, "distributed triangle count: at most 255 ranks");
         g.wparts = dd->world;
-        work(g.big_u, g.nbig, false, g.wbig);
-        work(g.vm_c, g.nvm, true, g.wvm);
-        work(g.small_u, g.nsmall, false, g.wsmall);
+        work(g.big_u, g.nbig, false, false, g.wbig);
+        work(g.vm_c, g.nvm, true, false, g.wvm);
+        work(g.small_u, g.nsmall, false, true, g.wsmall);
     }
 }
 
