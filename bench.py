@@ -94,6 +94,9 @@ def parse():
     p.add_argument("--direct-multi", action="store_true",
                    help="C4/C5 at N > 1: the explicit-kernel calls of rounds 1-3 (replicated trigraph build; "
                         "hand-wired varlen shards) instead of the routed query")
+    p.add_argument("--dist1", action="store_true",
+                   help="diagnostic (C3): the distributed route at world size 1 over RCCL (launch with "
+                        "torch.distributed.run --nproc-per-node 1): the route's fixed per-rank cost, exchanges included")
     p.add_argument("--workload", default="c3", choices=("c2", "c3", "c4", "c5"),
                    help="c3 (default, the BASELINE metric) or the single-GPU C2/C4/C5 lines (SURVEY.md 8d)")
     return p.parse_args()
@@ -261,7 +264,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world == 1 and args.gpus > 1:
         sys.exit("run with torch.distributed.run for --gpus > 1")
-    distributed = world > 1
+    distributed = world > 1 or args.dist1
     local = local % max(1, torch.cuda.device_count())  # rehearsal: several ranks may share one GPU (gloo)
     torch.cuda.set_device(local)
     if distributed:

@@ -117,6 +117,9 @@ struct Shard {
     int mode = 0;   // node: CAPSMI_NODES_*; relationship: CAPSMI_RELS_*
     int rank = 0, world = 1;
     int64_t slice_words = 0;
+    // node table: its rows (over every rank's shard when OWNED) are each id of the whole scrambled
+    // domain exactly once, so a predicate-free scan sets every bit without reading a row or exchanging
+    bool covers = false;
 };
 
 }  // namespace capsmi

@@ -671,6 +671,27 @@ capsmi_status capsmi_graph_distribute(capsmi_session* s, int64_t id_lo, int64_t 
             p.t->dsrc = p.a;
             p.t->ddst = p.b;
         }
+        if (sh->kind == 1 && id_hi - id_lo == sc.n) {
+            // coverage (Shard::covers): this shard's rows and repeated ids over the domain, summed over the
+            // ranks for OWNED shards (an id's rows all live on its owner, so repeats are rank-local)
+            capsmi_bitmap bm;
+            bm.sess = s;
+            bm.lo = 0;
+            bm.hi = sc.n;
+            bm.nwords = sc.n / 32;
+            bm.words = dev_alloc(sizeof(uint32_t) * (size_t)bm.nwords, s);
+            HIP_CHECK(hipMemsetAsync(P<void>(bm.words), 0, sizeof(uint32_t) * (size_t)bm.nwords, s->stream));
+            Buf cnt = dev_alloc(3 * sizeof(int64_t), s);
+            HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, 3 * sizeof(int64_t), s->stream));
+            bitmap_add_rows(&bm, P<int64_t>(p.a.data), nullptr, nullptr, p.t->nrows, P<int64_t>(cnt));
+            fill_i64(P<int64_t>(cnt), p.t->nrows, 1, s->stream);  // (rows, repeats)
+            if (node_mode == CAPSMI_NODES_OWNED && (s->world > 1 || s->coll))
+                collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(cnt), P<int64_t>(cnt), 2, CAPSMI_I64);
+            int64_t rc[2];
+            HIP_CHECK(hipMemcpyAsync(rc, P<void>(cnt), sizeof(rc), hipMemcpyDeviceToHost, s->stream));
+            HIP_CHECK(hipStreamSynchronize(s->stream));
+            sh->covers = rc[0] == sc.n && rc[1] == 0;
+        }
         p.t->shard = sh;
         p.t->partitioned = s->world > 1 && !(sh->kind == 1 && node_mode == CAPSMI_NODES_REPLICATED);
         p.t->layouts.clear();

@@ -789,6 +789,15 @@ capsmi_bitmap* node_bitmap(capsmi_session* s, const Path& P, const Classified& c
     capsmi_bitmap* b = nullptr;
     check(capsmi_bitmap_create(s, lo, hi, &b));
     bs.made.push_back({key, b});
+    if (g_dist.on && g_dense && sc.m.size() == 1 && progs[0].empty() && sc.m[0].base->shard &&
+        sc.m[0].base->shard->covers && lo == 0 && hi == g_dense->n) {
+        // a node table covering the whole domain (over the ranks' shards, checked at registration): every
+        // bit set, no row read, no exchange
+        bitmap_set_range(b, 0, hi);
+        b->rows_added = b->set_bits = hi;
+        b->full = true;
+        return b;
+    }
     for (size_t i = 0; i < sc.m.size(); ++i) {
         const Member& m = sc.m[i];
         const capsmi_expr* pr = progs[i].empty() ? nullptr : progs[i].data();
