@@ -900,6 +900,14 @@ def run_single(args):
                   "query_frac_of_peak": b_alg / sec / 1e9 / HBM_PEAK_GBS,
                   "kernel_ms": {k: v[1] / v[0] for k, v in kt.items()}},
     }
+    if world > 1:  # every rank's timed phases (ms per step): the balance of the shares
+        kr = torch.zeros(world, len(kernels), dtype=torch.float64, device="cuda")
+        for i, k in enumerate(kernels):
+            if k in kt:
+                kr[rank, i] = kt[k][1] / args.steps
+        dist.all_reduce(kr)
+        line["query"]["kernel_ms_per_rank"] = {k: [round(x, 3) for x in kr[:, i].tolist()]
+                                               for i, k in enumerate(kernels) if kr[:, i].sum() > 0}
     if gate is not None:  # per-rank busy time of the serialised rehearsal (collectives excluded)
         bt = torch.zeros(world, dtype=torch.float64, device="cuda")
         bt[rank] = gate.busy / args.steps * 1e3

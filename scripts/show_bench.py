@@ -4,7 +4,11 @@ import json
 import sys
 
 for f in sys.argv[1:]:
-    line = [l for l in open(f) if l.startswith("{")][-1]
+    lines = [l for l in open(f) if l.startswith("{")]
+    if not lines:
+        print(f"{f}: no JSON line")
+        continue
+    line = lines[-1]
     d = json.loads(line)
     q = d.get("query", {})
     print(f"{f}: {d['ms_per_step']:.3f} ms/step  value={d['value']:.4g}  kernel={d['roofline'] and d['roofline']['kernel']} "
@@ -17,3 +21,5 @@ for f in sys.argv[1:]:
             print(f"    mode {k}: {v['ms_per_step']:.3f} ms  " + " ".join(f"{a}={b:.3f}" for a, b in v.get("kernel_ms", {}).items()))
     if d.get("rehearsal"):
         print("    rehearsal busy ms per rank:", d["rehearsal"].get("busy_ms_per_rank"))
+    for k, v in q.get("kernel_ms_per_rank", {}).items():
+        print(f"    per rank {k:16s}", v)
