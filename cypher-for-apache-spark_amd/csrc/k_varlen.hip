@@ -376,23 +376,37 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_w(ChunkWalk cw, int64_t n, cons
         [&](int j) { flush_acc(a_w, W, j, n); });
 }
 
-// pairs a -> b passing both filters into the exact table (the sharded form's separate walk)
-__global__ void __launch_bounds__(kVlBlock) k_vl_ins(ChunkWalk cw, RegionBloom bl, const uint32_t* __restrict__ f2,
-                                                     PairHash h) {
-    walk_chunks(
-        cw,
-        [&](uint2 p, int) {  // p = (b, a)
-            if (f2_test(f2, p.x, pkey(p.x, p.y)) && rb_test(bl, p.y, pkey(p.x, p.y))) pair_insert(h, hkey(p.y, p.x));
-        },
-        [&](int) {});
-}
-
-// the candidate list into the exact table (single-GPU form)
+// the candidate list into the exact table
 __global__ void k_vl_cins(const unsigned long long* __restrict__ cl, const unsigned long long* __restrict__ ncand,
                           PairHash h) {
     const int64_t cnt = (int64_t)*ncand;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * blockDim.x)
         pair_insert(h, cl[i]);
+}
+
+// the sharded form's candidates straight from the relationship columns (a shard holds few relationships:
+// a flat pass with one filter word per relationship beats partitioning them by source first): the
+// relationships s -> t whose reverse may exist, as exact-table keys, one global add per wave
+__global__ void k_vl_flatcand(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, int64_t lo,
+                              RegionBloom bl, unsigned long long* __restrict__ cl, unsigned long long* __restrict__ ncand) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~(int64_t)63; e0 < m;
+         e0 += (int64_t)gridDim.x * blockDim.x) {  // wave-uniform
+        const int64_t e = e0 + lane;
+        bool c = false;
+        uint32_t s = 0, t = 0;
+        if (e < m) {
+            s = (uint32_t)(src[e] - lo);
+            t = (uint32_t)(dst[e] - lo);
+            c = rb_test(bl, s, pkey(t, s));
+        }
+        const unsigned long long bal = __ballot(c);
+        if (!bal) continue;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(ncand, (unsigned long long)__popcll(bal));
+        base = __shfl(base, 0, 64);
+        if (c) cl[base + __popcll(bal & ((1ULL << lane) - 1))] = hkey(s, t);
+    }
 }
 
 // target partition (pair = (source, target), j = slice(t)): mark pair (s, t) in t's region.  Each
@@ -766,7 +780,8 @@ namespace capsmi {
 // relationships into its owned ids from other ranks' sources ("in", exchanged once at ingest).
 //   begin : out by source slice -> od, s of owned ids (0 elsewhere: the caller sums od over ranks);
 //           R(a) for owned a from out + in (every reciprocal pair of an owned a is there both ways):
-//           first-level filter by target, second level by source, exact table, k_vl_recip
+//           filter of out ∪ in by target, candidates by one flat pass (k_vl_flatcand), exact table,
+//           k_vl_recip
 //   mid   : W(v) of owned v from the summed od -> Y of owned v (0 elsewhere: the caller sums Y)
 //   finish: T2, T3 of owned a from the summed od and Y -> rows of owned a
 struct VarlenShard {
@@ -777,7 +792,7 @@ struct VarlenShard {
     bool need3 = false;
     part::Layout L{};
     ChunkPart cp;  // out, by source slice
-    Buf sl, W, T2, T3, ody, bw, f2, hk, hc;
+    Buf sl, W, T2, T3, ody, bw, hk, hc;
     int64_t* od = nullptr;  // caller buffers (n int64 each), summed over ranks by the caller
     int64_t* y = nullptr;
 };
@@ -847,7 +862,7 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
             am.push_back(ims[i]);
         }
         const int na = (int)as.size();
-        ChunkPart ct, ca;
+        ChunkPart ct;
         KernelTimer kt(s, "varlen_rev");
         chunk_partition(s, as.data(), ad.data(), am.data(), na, false, L, s->num_cus, ct);
         const int64_t per_slice = (mall + L.nt - 1) / L.nt;
@@ -866,19 +881,13 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
             hipLaunchKernelGGL(k_vl_bmerge, dim3(grid(s, (int64_t)(rbytes / 16) * L.nt)), dim3(256), 0, st, ct.jst, L.nt,
                                ct.g2, P<uint4>(part), bl);
         }
-        chunk_partition(s, as.data(), ad.data(), am.data(), na, true, L, s->num_cus, ca);
-        const ChunkWalk aw{P<uint2>(ca.pool), P<unsigned long long>(ca.meta), ca.order, ca.jst, ca.segbase, ca.ja, L.nt};
-        v->f2 = dev_alloc(sizeof(uint32_t) * kF2Words * (size_t)L.nt, s);
-        Buf cand = dev_alloc(sizeof(int64_t), s);
+        // candidates (reverse maybe present) of out ∪ in: one flat pass over the columns into a list
+        Buf cand = dev_alloc(sizeof(int64_t), s), clist = dev_alloc(sizeof(unsigned long long) * (size_t)mall, s);
         HIP_CHECK(hipMemsetAsync(P<void>(cand), 0, sizeof(int64_t), st));
-        {
-            Buf f2part = dev_alloc(sizeof(uint32_t) * kF2Words * ((size_t)ca.g2 + L.nt), s);
-            hipLaunchKernelGGL(k_vl_deg, dim3((unsigned)ca.g2), dim3(kVlBlock), lds2, st, aw, v->d.b, v->d.b_full, n,
-                               nullptr, nullptr, bl, P<uint4>(f2part), P<unsigned long long>(cand), nullptr);
-            const RegionBloom f2b{P<uint32_t>(v->f2), 0, 19, 0};
-            hipLaunchKernelGGL(k_vl_bmerge, dim3(grid(s, (int64_t)(kF2Words / 4) * L.nt)), dim3(256), 0, st, ca.jst,
-                               L.nt, ca.g2, P<uint4>(f2part), f2b);
-        }
+        for (int i = 0; i < na; ++i)
+            if (am[i] > 0)
+                hipLaunchKernelGGL(k_vl_flatcand, dim3(grid(s, am[i])), dim3(256), 0, st, as[i], ad[i], am[i], v->d.lo, bl,
+                                   P<unsigned long long>(clist), P<unsigned long long>(cand));
         const int64_t nc = read_scalar(s, P<int64_t>(cand));
         int64_t cap = 1024;
         while (cap < 2 * nc) cap <<= 1;
@@ -888,7 +897,8 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
         HIP_CHECK(hipMemsetAsync(P<void>(v->hc), 0, sizeof(unsigned int) * (cap + 1), st));
         const PairHash h{P<unsigned long long>(v->hk), P<unsigned int>(v->hc), P<unsigned int>(v->hc) + cap,
                          (unsigned long long)(cap - 1)};
-        hipLaunchKernelGGL(k_vl_ins, dim3((unsigned)ca.g2), dim3(kVlBlock), 0, st, aw, bl, P<uint32_t>(v->f2), h);
+        hipLaunchKernelGGL(k_vl_cins, dim3(grid(s, nc)), dim3(256), 0, st, P<unsigned long long>(clist),
+                           P<unsigned long long>(cand), h);
         hipLaunchKernelGGL(k_vl_recip, dim3(grid(s, cap)), dim3(256), 0, st, h, v->d.a, v->d.a_full, v->d.b,
                            v->d.b_full, P<unsigned long long>(v->T3), (uint32_t)v->own_lo, (uint32_t)v->own_hi);
     }
