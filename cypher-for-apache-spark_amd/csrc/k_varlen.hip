@@ -888,16 +888,17 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
             if (am[i] > 0)
                 hipLaunchKernelGGL(k_vl_flatcand, dim3(grid(s, am[i])), dim3(256), 0, st, as[i], ad[i], am[i], v->d.lo, bl,
                                    P<unsigned long long>(clist), P<unsigned long long>(cand));
-        const int64_t nc = read_scalar(s, P<int64_t>(cand));
+        // the table sized by the shard's relationships (a bound on the candidates) rather than by their
+        // count read back: no host round trip inside the phase (a shard's table stays small)
         int64_t cap = 1024;
-        while (cap < 2 * nc) cap <<= 1;
+        while (cap < 2 * mall) cap <<= 1;
         v->hk = dev_alloc(sizeof(unsigned long long) * cap, s);
         v->hc = dev_alloc(sizeof(unsigned int) * (cap + 1), s);
         HIP_CHECK(hipMemsetAsync(P<void>(v->hk), 0, sizeof(unsigned long long) * cap, st));
         HIP_CHECK(hipMemsetAsync(P<void>(v->hc), 0, sizeof(unsigned int) * (cap + 1), st));
         const PairHash h{P<unsigned long long>(v->hk), P<unsigned int>(v->hc), P<unsigned int>(v->hc) + cap,
                          (unsigned long long)(cap - 1)};
-        hipLaunchKernelGGL(k_vl_cins, dim3(grid(s, nc)), dim3(256), 0, st, P<unsigned long long>(clist),
+        hipLaunchKernelGGL(k_vl_cins, dim3(grid(s, mall)), dim3(256), 0, st, P<unsigned long long>(clist),
                            P<unsigned long long>(cand), h);
         hipLaunchKernelGGL(k_vl_recip, dim3(grid(s, cap)), dim3(256), 0, st, h, v->d.a, v->d.a_full, v->d.b,
                            v->d.b_full, P<unsigned long long>(v->T3), (uint32_t)v->own_lo, (uint32_t)v->own_hi);
