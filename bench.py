@@ -95,7 +95,7 @@ def parse():
                    help="C4/C5 at N > 1: the explicit-kernel calls of rounds 1-3 (replicated trigraph build; "
                         "hand-wired varlen shards) instead of the routed query")
     p.add_argument("--dist1", action="store_true",
-                   help="diagnostic (C3): the distributed route at world size 1 over RCCL (launch with "
+                   help="diagnostic (C3, C4, C5): the distributed route at world size 1 over RCCL (launch with "
                         "torch.distributed.run --nproc-per-node 1): the route's fixed per-rank cost, exchanges included")
     p.add_argument("--workload", default="c3", choices=("c2", "c3", "c4", "c5"),
                    help="c3 (default, the BASELINE metric) or the single-GPU C2/C4/C5 lines (SURVEY.md 8d)")
@@ -677,9 +677,10 @@ def run_single(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dw = world > 1 or (args.dist1 and wl in ("c4", "c5"))  # --dist1: the distributed route at world size 1
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
-    if world > 1:  # C2: rels by owner(source), local expand; C4: replicated oriented graph, vertex shares;
+    if dw:  # C2: rels by owner(source), local expand; C4: replicated oriented graph, vertex shares;
         # C5: owner(source) shards
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -690,7 +691,7 @@ def run_single(args):
     # Planner(sg).run over its shard; libcapsmi's distributed routes exchange through RCCL (C4: the pairs
     # to their lower end's owner and the oriented ranges, all-gathered; C5: owner(source) shards whose
     # in-relationships were exchanged at registration, od / Y all-reduced).  Ingest is untimed.
-    dist_route = world > 1 and wl in ("c4", "c5") and not args.direct_multi
+    dist_route = dw and wl in ("c4", "c5") and not args.direct_multi
     shard_c5 = wl == "c5" and world > 1 and not dist_route
     ingest_gate = None
     if dist_route:
@@ -782,7 +783,7 @@ def run_single(args):
     kernels = ("direct_join_probe", "radix_join_count", "radix_join_write", "bitmap_add", "expand_filter", "tri_pack",
                "tri_sort_und", "tri_order", "tri_sort_or", "tri_post", "tri_work", "triangles", "part_scatter1",
                "varlen_part", "varlen_deg", "varlen_w", "varlen_rev",
-               "varlen_cand", "varlen_recip", "varlen_t")
+               "varlen_cand", "varlen_recip", "varlen_t", "vls_rev_part", "vls_rev_bloom", "vls_rev_cand", "vls_rev_recip")
     gate = None
     if world > 1:
         from capsmi.dist import serial_gate
@@ -807,17 +808,17 @@ def run_single(args):
         _lib.call("capsmi_session_kernel_time", sess.handle, k.encode(), ctypes.byref(ctypes.c_int64()),
                   ctypes.byref(ctypes.c_double()))
         _lib.call("capsmi_session_kernel_bytes", sess.handle, k.encode(), ctypes.byref(ctypes.c_double()))
-    if world > 1:
+    if dw:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res, out = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dw:
         dist.barrier()
     sec = (time.perf_counter() - t0) / args.steps
-    if world > 1:
+    if dw:
         tt = torch.tensor([sec], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         sec = float(tt.item())
@@ -867,7 +868,7 @@ def run_single(args):
     else:
         fcheck = "ok" if res == fx["sum_count"] else f"MISMATCH sum {res} vs fixture {fx['sum_count']}"
         if world == 1 and fcheck == "ok":
-            fp = list(out.fingerprint(["id", "count"]))
+            fp = list(out.fingerprint(cache.get("c5_cols", ["id", "count"])))
             want = [fx["fingerprint"][0], int(fx["fingerprint"][1]), int(fx["fingerprint"][2])]
             fcheck = "ok" if fp == want else f"MISMATCH fingerprint {fp} vs fixture {want}"
     matched = res
@@ -943,7 +944,7 @@ def run_single(args):
     if rank == 0:
         print(json.dumps(line), flush=True)
     sess.close()
-    if world > 1:
+    if dw:
         dist.destroy_process_group()
     if fcheck.startswith("MISMATCH"):
         sys.exit(f"bench: result differs from the oracle fixture: {fcheck}")

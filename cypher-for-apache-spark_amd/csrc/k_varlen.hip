@@ -386,26 +386,57 @@ __global__ void k_vl_cins(const unsigned long long* __restrict__ cl, const unsig
 
 // the sharded form's candidates straight from the relationship columns (a shard holds few relationships:
 // a flat pass with one filter word per relationship beats partitioning them by source first): the
-// relationships s -> t whose reverse may exist, as exact-table keys, one global add per wave
-__global__ void k_vl_flatcand(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, int64_t lo,
-                              RegionBloom bl, unsigned long long* __restrict__ cl, unsigned long long* __restrict__ ncand) {
-    const int lane = threadIdx.x & 63;
-    for (int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~(int64_t)63; e0 < m;
-         e0 += (int64_t)gridDim.x * blockDim.x) {  // wave-uniform
-        const int64_t e = e0 + lane;
-        bool c = false;
-        uint32_t s = 0, t = 0;
-        if (e < m) {
-            s = (uint32_t)(src[e] - lo);
-            t = (uint32_t)(dst[e] - lo);
-            c = rb_test(bl, s, pkey(t, s));
+// relationships s -> t whose reverse may exist, as exact-table keys.  A block takes kFcIt x 256
+// relationships per step and claims its candidates' slots with one global add (one add per wave put
+// ~5·10^5 adds on the one counter at C5 and took 6.3 ms for 3.4·10^7 relationships).
+constexpr int kFcBlock = 256, kFcIt = 16;
+
+__global__ void __launch_bounds__(kFcBlock) k_vl_flatcand(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                          int64_t m, int64_t lo, RegionBloom bl,
+                                                          unsigned long long* __restrict__ cl,
+                                                          unsigned long long* __restrict__ ncand) {
+    constexpr int T = kFcBlock * kFcIt, W = kFcBlock / 64;
+    __shared__ uint32_t wsum[W];
+    __shared__ unsigned long long base;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t t0 = (int64_t)blockIdx.x * T; t0 < m; t0 += (int64_t)gridDim.x * T) {  // block-uniform
+        uint32_t ss[kFcIt], tt[kFcIt], mask = 0;
+#pragma unroll
+        for (int u = 0; u < kFcIt; ++u) {
+            const int64_t e = t0 + (int64_t)u * kFcBlock + threadIdx.x;
+            ss[u] = tt[u] = 0;
+            if (e < m) {
+                ss[u] = (uint32_t)(src[e] - lo);
+                tt[u] = (uint32_t)(dst[e] - lo);
+            }
         }
-        const unsigned long long bal = __ballot(c);
-        if (!bal) continue;
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(ncand, (unsigned long long)__popcll(bal));
-        base = __shfl(base, 0, 64);
-        if (c) cl[base + __popcll(bal & ((1ULL << lane) - 1))] = hkey(s, t);
+#pragma unroll
+        for (int u = 0; u < kFcIt; ++u) {
+            const int64_t e = t0 + (int64_t)u * kFcBlock + threadIdx.x;
+            if (e < m && rb_test(bl, ss[u], pkey(tt[u], ss[u]))) mask |= 1u << u;
+        }
+        const uint32_t c = (uint32_t)__popc(mask);
+        uint32_t incl = c;  // block exclusive prefix of the lanes' candidate counts
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        uint32_t pre = 0, tot = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            pre += w < wave ? wsum[w] : 0u;
+            tot += wsum[w];
+        }
+        if (threadIdx.x == 0) base = tot ? atomicAdd(ncand, (unsigned long long)tot) : 0ULL;
+        __syncthreads();
+        unsigned long long pos = base + pre + incl - c;
+#pragma unroll
+        for (int u = 0; u < kFcIt; ++u)
+            if ((mask >> u) & 1u) cl[pos++] = hkey(ss[u], tt[u]);
+        __syncthreads();  // wsum and base are rewritten by the next step
     }
 }
 
@@ -864,7 +895,9 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
         const int na = (int)as.size();
         ChunkPart ct;
         KernelTimer kt(s, "varlen_rev");
+        std::unique_ptr<KernelTimer> sub(new KernelTimer(s, "vls_rev_part"));
         chunk_partition(s, as.data(), ad.data(), am.data(), na, false, L, s->num_cus, ct);
+        sub.reset(new KernelTimer(s, "vls_rev_bloom"));
         const int64_t per_slice = (mall + L.nt - 1) / L.nt;
         int rshift = 10;
         while ((int64_t(1) << rshift) < int64_t(8) * per_slice && rshift < 20) ++rshift;
@@ -881,25 +914,32 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
             hipLaunchKernelGGL(k_vl_bmerge, dim3(grid(s, (int64_t)(rbytes / 16) * L.nt)), dim3(256), 0, st, ct.jst, L.nt,
                                ct.g2, P<uint4>(part), bl);
         }
+        sub.reset(new KernelTimer(s, "vls_rev_cand"));
         // candidates (reverse maybe present) of out ∪ in: one flat pass over the columns into a list
         Buf cand = dev_alloc(sizeof(int64_t), s), clist = dev_alloc(sizeof(unsigned long long) * (size_t)mall, s);
         HIP_CHECK(hipMemsetAsync(P<void>(cand), 0, sizeof(int64_t), st));
         for (int i = 0; i < na; ++i)
             if (am[i] > 0)
-                hipLaunchKernelGGL(k_vl_flatcand, dim3(grid(s, am[i])), dim3(256), 0, st, as[i], ad[i], am[i], v->d.lo, bl,
+                hipLaunchKernelGGL(k_vl_flatcand,
+                                   dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((am[i] + kFcBlock * kFcIt - 1) /
+                                                                                             (kFcBlock * kFcIt),
+                                                                                         (int64_t)s->num_cus * 8))),
+                                   dim3(kFcBlock), 0, st, as[i], ad[i], am[i], v->d.lo, bl,
                                    P<unsigned long long>(clist), P<unsigned long long>(cand));
-        // the table sized by the shard's relationships (a bound on the candidates) rather than by their
-        // count read back: no host round trip inside the phase (a shard's table stays small)
+        // the table sized by the candidates' count (one read back: a table sized by the relationships
+        // instead costs more in clearing and scanning than the round trip)
+        const int64_t nc = read_scalar(s, P<int64_t>(cand));
         int64_t cap = 1024;
-        while (cap < 2 * mall) cap <<= 1;
+        while (cap < 2 * nc) cap <<= 1;
         v->hk = dev_alloc(sizeof(unsigned long long) * cap, s);
         v->hc = dev_alloc(sizeof(unsigned int) * (cap + 1), s);
         HIP_CHECK(hipMemsetAsync(P<void>(v->hk), 0, sizeof(unsigned long long) * cap, st));
         HIP_CHECK(hipMemsetAsync(P<void>(v->hc), 0, sizeof(unsigned int) * (cap + 1), st));
         const PairHash h{P<unsigned long long>(v->hk), P<unsigned int>(v->hc), P<unsigned int>(v->hc) + cap,
                          (unsigned long long)(cap - 1)};
-        hipLaunchKernelGGL(k_vl_cins, dim3(grid(s, mall)), dim3(256), 0, st, P<unsigned long long>(clist),
+        hipLaunchKernelGGL(k_vl_cins, dim3(grid(s, nc)), dim3(256), 0, st, P<unsigned long long>(clist),
                            P<unsigned long long>(cand), h);
+        sub.reset(new KernelTimer(s, "vls_rev_recip"));
         hipLaunchKernelGGL(k_vl_recip, dim3(grid(s, cap)), dim3(256), 0, st, h, v->d.a, v->d.a_full, v->d.b,
                            v->d.b_full, P<unsigned long long>(v->T3), (uint32_t)v->own_lo, (uint32_t)v->own_hi);
     }

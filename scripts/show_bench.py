@@ -3,7 +3,12 @@
 import json
 import sys
 
+import os
+
 for f in sys.argv[1:]:
+    if not os.path.exists(f):
+        print(f"{f}: missing")
+        continue
     lines = [l for l in open(f) if l.startswith("{")]
     if not lines:
         print(f"{f}: no JSON line")
