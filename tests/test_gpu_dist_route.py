@@ -10,7 +10,8 @@ distributed graph and libcapsmi routes the plans to the distributed kernels.
   equals the oracle (oracle/closed.c closed forms, pinned by tests/test_oracle_pins.py).
 - 1 rank over RCCL (backend nccl, world size 1): the same routes with every exchange through
   torch.distributed's NCCL(=RCCL) branch of capsmi.dist.TorchCollective -- all-gathers, all-reduces and
-  the ALL_TO_ALL_V -- against the R-MAT fixtures (tests/golden/rmat_full.json: C3 s = 20, C4 s = 14)."""
+  the ALL_TO_ALL_V, the C4 part in chunked calls -- against the R-MAT fixtures (tests/golden/rmat_full.json:
+  C3 s = 20, C4 s = 14)."""
 import json
 import os
 import socket
@@ -49,8 +50,9 @@ def _hub_edges(path, seed=7, n=1 << 16, m=400_000, hubs=1000):
     return n, src.astype(np.int64), dst.astype(np.int64)
 
 
-def _ranks(graph, lo, hi, world=2, nodes="owned", rels_by="target", queries="c3,tri", backend="gloo", out=None):
-    env = dict(os.environ, CAPSMI_DIST_BACKEND=backend, MASTER_ADDR="127.0.0.1")
+def _ranks(graph, lo, hi, world=2, nodes="owned", rels_by="target", queries="c3,tri", backend="gloo", out=None,
+           env_extra=None):
+    env = dict(os.environ, CAPSMI_DIST_BACKEND=backend, MASTER_ADDR="127.0.0.1", **(env_extra or {}))
     out = out or str(graph)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", "dist_route_worker.py"),
@@ -131,8 +133,10 @@ def test_routes_over_rccl_world1(tmp_path):
     assert o["count_star"] == c3["count_star"], o
     assert o["routes"]["two_hop"] >= 2, o
     c4 = _fixture("c4_s14")
+    # CAPSMI_COLL_CHUNK: the build's exchanges and all-gathers (2^18 words here) in RCCL calls of at most
+    # 2^16 words -- the chunked rounds that keep a full-size build (2^28 words) below RCCL's 2 GiB limit
     o = _ranks("rmat:14", 0, 1 << 14, world=1, rels_by="source", queries="tri,varlen", backend="nccl",
-               out=str(tmp_path / "r14"))[0]
+               out=str(tmp_path / "r14"), env_extra={"CAPSMI_COLL_CHUNK": str(1 << 16)})[0]
     assert o["triangle"] == c4["count_star"], o
     assert o["routes"]["triangle"] >= 1 and o["routes"]["var_length"] >= 1, o
     from oracle import cpu
