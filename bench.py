@@ -543,6 +543,7 @@ def main():
                "mid_combine": n // 8 * 5, "bitmap_add": n * 8,
                "count_part": m_local * 20,  # read 2 x int64, write two 2-byte records
                "und_count_part": m_local * 24,  # read 2 x int64, write up to four 2-byte records
+               "und_distinct": m_local * 32 + n * 4,  # two streams of 2 x int64; the per-id state word
                "count_part_in": m_local * 24, "count_part_out": m_local * 24,  # pair partition (CAPSMI_COUNT=pairs)
                "degrees": m_local * 16 + n * 8}                  # read int64 pairs, inA + outC
         alg.update(kbytes)

@@ -24,7 +24,6 @@ namespace capsmi {
 
 namespace {
 
-constexpr uint32_t kMany = 0xFFFFFFFFu;
 
 inline unsigned grid_for(int64_t n, int block = 256) {
     const int64_t g = (n + block - 1) / block;
@@ -90,35 +89,47 @@ __global__ void k_und_product(const uint32_t* __restrict__ inU, const uint32_t* 
     block_add(&acc[2], sum);
 }
 
-__device__ __forceinline__ void und_note(uint32_t* st, int64_t b, int64_t x) {
-    const uint32_t old = atomicCAS(&st[b], 0u, (uint32_t)x + 1u);
-    if (old != 0u && old != kMany) atomicExch(&st[b], kMany);
+// K(b) as two bitmaps (8 MiB each at 2^26 ids, cache-resident where the 4-byte state words were not):
+// B1 = at least one a_ok arc into b, B2 = at least two; x(b) (the first arc's other end) is read only
+// where K(b) = 1.  An arc reads B2 first -- hubs, which take most arcs, are settled by that one cached
+// read -- then sets its B1 bit: the arc that found it clear is the first and stores x(b); one that found
+// it set sets B2.
+__device__ __forceinline__ bool bit_at(const uint32_t* w, int64_t i) { return (w[i >> 5] >> (i & 31)) & 1u; }
+
+__device__ __forceinline__ void und_note(uint32_t* B1, uint32_t* B2, uint32_t* xb, int64_t b, int64_t x) {
+    if (bit_at(B2, b)) return;
+    const uint32_t m = 1u << (b & 31);
+    if (atomicOr(&B1[b >> 5], m) & m) atomicOr(&B2[b >> 5], m);
+    else xb[b] = (uint32_t)x;
 }
 
 // hop 1 of the distinct 2-hop: K(b) / x(b) from the a_ok arcs into b_ok ids
 __global__ void k_und_hop1(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, int64_t lo,
-                           int64_t n, Bits a, Bits b, uint32_t* __restrict__ st) {
+                           int64_t n, Bits a, Bits b, uint32_t* __restrict__ B1, uint32_t* __restrict__ B2,
+                           uint32_t* __restrict__ xb) {
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t s = src[e] - lo, t = dst[e] - lo;
         if (s < 0 || s >= n || t < 0 || t >= n) continue;
-        if (ok(a, s) && ok(b, t)) und_note(st, t, s);
-        if (s != t && ok(a, t) && ok(b, s)) und_note(st, s, t);
+        if (ok(a, s) && ok(b, t)) und_note(B1, B2, xb, t, s);
+        if (s != t && ok(a, t) && ok(b, s)) und_note(B1, B2, xb, s, t);
     }
 }
 
-__device__ __forceinline__ bool extends(const uint32_t* st, int64_t b, int64_t c) {
-    const uint32_t k = st[b];
-    return k == kMany || (k != 0u && (int64_t)(k - 1u) != c);
+__device__ __forceinline__ bool extends(const uint32_t* B1, const uint32_t* B2, const uint32_t* xb, int64_t b,
+                                        int64_t c) {
+    return bit_at(B2, b) || (bit_at(B1, b) && (int64_t)xb[b] != c);
 }
 
 // hop 2: mark every c_ok end of an arc b -> c that extends a binding
 __global__ void k_und_hop2(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, int64_t lo,
-                           int64_t n, Bits c, const uint32_t* __restrict__ st, uint32_t* __restrict__ C) {
+                           int64_t n, Bits c, const uint32_t* __restrict__ B1, const uint32_t* __restrict__ B2,
+                           const uint32_t* __restrict__ xb, uint32_t* __restrict__ C) {
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t s = src[e] - lo, t = dst[e] - lo;
         if (s < 0 || s >= n || t < 0 || t >= n) continue;
-        if (ok(c, t) && extends(st, s, t)) atomicOr(&C[t >> 5], 1u << (t & 31));
-        if (s != t && ok(c, s) && extends(st, t, s)) atomicOr(&C[s >> 5], 1u << (s & 31));
+        // check, then set: most ends are reached many times, and a set bit needs no atomic
+        if (ok(c, t) && !bit_at(C, t) && extends(B1, B2, xb, s, t)) atomicOr(&C[t >> 5], 1u << (t & 31));
+        if (s != t && ok(c, s) && !bit_at(C, s) && extends(B1, B2, xb, t, s)) atomicOr(&C[s >> 5], 1u << (s & 31));
     }
 }
 
@@ -205,19 +216,21 @@ int64_t undirected_count(capsmi_session* s, const int64_t* const* srcs, const in
     KernelTimer kt(s, "und_distinct");
     const capsmi_bitmap* A = kind == 2 ? c : a;
     const capsmi_bitmap* Cc = kind == 2 ? a : c;
-    Buf stt = dev_alloc(sizeof(uint32_t) * n, s), C = dev_alloc(sizeof(uint32_t) * nw, s);
-    HIP_CHECK(hipMemsetAsync(P<void>(stt), 0, sizeof(uint32_t) * n, st));
-    HIP_CHECK(hipMemsetAsync(P<void>(C), 0, sizeof(uint32_t) * nw, st));
+    // B1, B2, C: three bitmaps in one buffer (one fill); x(b) needs no clearing (read only where B1 says
+    // an arc stored it)
+    Buf bm = dev_alloc(sizeof(uint32_t) * 3 * nw, s), xb = dev_alloc(sizeof(uint32_t) * n, s);
+    HIP_CHECK(hipMemsetAsync(P<void>(bm), 0, sizeof(uint32_t) * 3 * nw, st));
+    uint32_t *B1 = P<uint32_t>(bm), *B2 = B1 + nw, *C = B2 + nw;
     for (int i = 0; i < nt; ++i)
         if (ms[i] > 0)
             hipLaunchKernelGGL(k_und_hop1, dim3(grid_for(ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], lo, n,
-                               bits_of(A), bits_of(b), P<uint32_t>(stt));
+                               bits_of(A), bits_of(b), B1, B2, P<uint32_t>(xb));
     for (int i = 0; i < nt; ++i)
         if (ms[i] > 0)
             hipLaunchKernelGGL(k_und_hop2, dim3(grid_for(ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], lo, n,
-                               bits_of(Cc), P<uint32_t>(stt), P<uint32_t>(C));
+                               bits_of(Cc), B1, B2, P<uint32_t>(xb), C);
     HIP_CHECK(hipGetLastError());
-    return words_popcount(s, P<uint32_t>(C), 0, nw);
+    return words_popcount(s, C, 0, nw);
 }
 
 }  // namespace capsmi
