@@ -139,13 +139,13 @@ __global__ void k_und_mark1(const int64_t* __restrict__ src, const int64_t* __re
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t s = src[e] - lo, t = dst[e] - lo;
         if (s < 0 || s >= n || t < 0 || t >= n) continue;
-        if (ok(a, s) && ok(b, t)) {
+        if (ok(a, s) && ok(b, t)) {  // check, then set (hub ends are marked by many arcs)
             const int64_t x = mark_start ? s : t;
-            atomicOr(&M[x >> 5], 1u << (x & 31));
+            if (!bit_at(M, x)) atomicOr(&M[x >> 5], 1u << (x & 31));
         }
         if (s != t && ok(a, t) && ok(b, s)) {
             const int64_t x = mark_start ? t : s;
-            atomicOr(&M[x >> 5], 1u << (x & 31));
+            if (!bit_at(M, x)) atomicOr(&M[x >> 5], 1u << (x & 31));
         }
     }
 }
