@@ -429,6 +429,9 @@ struct TriGraph {
     // sums of the centers' walked entries reach equal shares (empty: equal center counts)
     int wparts = 0;
     std::vector<int64_t> wbig, wvm, wsmall;
+    // a distributed build's in-lists hold only this rank's v-mode share (centers in one id range cut by
+    // binned v-mode work), so vm_c is exactly the centers of its part
+    bool vm_own = false;
 };
 // a distributed build (multi-GPU C4): this rank's relationships are any 1/world of them; the owner of a
 // dense id x is x / span

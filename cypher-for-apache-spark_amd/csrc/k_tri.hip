@@ -973,6 +973,67 @@ __global__ void k_tri_work_u(const int64_t* __restrict__ cs, int64_t nc, const i
     }
 }
 
+// ---- v-mode shares without replicated in-lists (distributed build) -----------------------------------
+// v-mode centers are the vertices with od(v) >= vmt; under the degree order they sit at the low ids.
+// vmax + 1 bounds them (one atomic max per wave).
+__global__ void k_tri_vmax(const int64_t* __restrict__ off, int64_t n, int vmt, unsigned long long* __restrict__ vmax) {
+    unsigned long long best = 0;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+        if (off[v + 1] - off[v] >= vmt) best = max(best, (unsigned long long)v + 1);
+    for (int o = 32; o > 0; o >>= 1) best = max(best, (unsigned long long)__shfl_down(best, o, 64));
+    if ((threadIdx.x & 63) == 0 && best) atomicMax(vmax, best);
+}
+
+constexpr int kVwBins = 8192;  // bins of the v-mode work over [0, vmax): 64 KiB of LDS counters
+
+// the v-mode work of every edge u -> v at position p that v-mode takes (od(v) >= vmt, p < od(v)): the
+// p entries of out(u) its walk reads, plus one, summed per bin of v (bin width bw) in LDS, flushed once
+__global__ void __launch_bounds__(1024) k_tri_vwork(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ off,
+                                                    int64_t ne, uint32_t idm, int vmt, int64_t bw,
+                                                    unsigned long long* __restrict__ bins) {
+    __shared__ unsigned long long h[kVwBins];
+    for (int i = threadIdx.x; i < kVwBins; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = ok_[e];
+        const uint32_t u = (uint32_t)(k >> 32), v = (uint32_t)k & idm;
+        const int64_t odv = off[v + 1] - off[v];
+        if (odv < vmt) continue;
+        const int64_t p = e - off[u];
+        if (p < odv) atomicAdd(&h[min((int64_t)v / bw, (int64_t)kVwBins - 1)], (unsigned long long)p + 1ULL);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kVwBins; i += blockDim.x)
+        if (h[i]) atomicAdd(&bins[i], h[i]);
+}
+
+// the edges whose in-list entry this rank's v-mode share walks: v in [v_lo, v_hi), od(v) >= vmt, p < od(v)
+__global__ void k_tri_in_flags(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ off, int64_t ne,
+                               uint32_t idm, int vmt, int64_t v_lo, int64_t v_hi, uint8_t* __restrict__ f) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = ok_[e];
+        const uint32_t u = (uint32_t)(k >> 32), v = (uint32_t)k & idm;
+        bool take = false;
+        if (v >= v_lo && v < v_hi) {
+            const int64_t odv = off[v + 1] - off[v];
+            take = odv >= vmt && e - off[u] < odv;
+        }
+        f[e] = take ? 1 : 0;
+    }
+}
+
+// packed in-keys (to << (ib + 16) | from << 16 | pos) of the selected edges, in edge order
+__global__ void k_swap_keys_sel(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ off,
+                                const int64_t* __restrict__ sel, int64_t nsel, TgCode tc, uint64_t* __restrict__ ik) {
+    const uint32_t idm = tc.idmask();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nsel; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = sel[i];
+        const uint64_t k = ok_[e];
+        const uint64_t from = k >> 32, to = (uint32_t)k & idm;
+        ik[i] = (to << (tc.ib + 16)) | (from << 16) | (uint64_t)(e - off[from]);
+    }
+}
+
 // the same for the small centers (a few entries each): one lane per center keeps 64 of them in flight
 __global__ void k_tri_work_u1(const int64_t* __restrict__ cs, int64_t nc, const int64_t* __restrict__ off,
                               const uint32_t* __restrict__ tg, uint32_t idmask, int vmt, int64_t* __restrict__ w) {
@@ -1236,22 +1297,80 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         // order (every out-neighbour has at least u's degree), so m < 2^31 relationships bound it by 2^16
         const bool packed = g.ib <= 24 && m_all < (int64_t(1) << 31);
         const int tsh = packed ? g.ib + 16 : 32;
-        Buf ik = dev_alloc(sizeof(uint64_t) * ne, s), iv = packed ? Buf() : dev_alloc(sizeof(int64_t) * ne, s);
-        hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off), ne, tc,
-                           P<uint64_t>(ik), packed ? nullptr : P<int64_t>(iv));
-        // by (to, from): the input is in (from, to) order and the LSD sort is stable, so the digits of
-        // `to` alone give that order (3 passes at 2^24 ids instead of 6)
-        std::vector<int> td;
-        for (int sh = tsh; sh < tsh + bits; sh += 8) td.push_back(sh);
-        radix_sort_digits(s, P<uint64_t>(ik), packed ? nullptr : P<int64_t>(iv), ne, td);
-        g.ioff = dev_alloc(sizeof(int64_t) * (n + 1), s);
-        hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), ne, n, tsh,
-                           P<int64_t>(g.ioff));
-        g.itg = dev_alloc(sizeof(uint32_t) * ne, s);
-        g.ipos = dev_alloc(sizeof(uint32_t) * ne, s);
-        hipLaunchKernelGGL(k_in_split, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(ik),
-                           packed ? nullptr : P<int64_t>(iv), P<int64_t>(g.off), ne, tc, P<uint32_t>(g.itg),
-                           P<uint32_t>(g.ipos));
+        std::vector<int> td;  // by (to, from): the input is in (from, to) order and the LSD sort is stable, so
+        for (int sh = tsh; sh < tsh + bits; sh += 8) td.push_back(sh);  // the digits of `to` alone give that order
+        if (dd && packed && dd->world > 1) {
+            // A rank walks only its v-mode share, so it builds only that share's in-lists (the whole
+            // in-list sort was ≈6 ms of every rank's replicated post-processing at s = 24): the v-mode
+            // work of every edge, binned by v over [0, vmax) (the centers sit at the low degree-order ids),
+            // is cut into world ranges of equal work -- the same cuts on every rank -- and only the edges
+            // into this rank's range get in-list entries
+            Buf vb = dev_alloc(sizeof(unsigned long long) * (kVwBins + 1), s);
+            HIP_CHECK(hipMemsetAsync(P<void>(vb), 0, sizeof(unsigned long long) * (kVwBins + 1), st));
+            unsigned long long* vmaxp = P<unsigned long long>(vb) + kVwBins;
+            hipLaunchKernelGGL(k_tri_vmax, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), n, g.vmt, vmaxp);
+            const int64_t vmax = read_scalar(s, reinterpret_cast<const int64_t*>(vmaxp));
+            const int64_t bw = std::max<int64_t>(1, (vmax + kVwBins - 1) / kVwBins);
+            const int W = dd->world;
+            int64_t v_lo = 0, v_hi = 0;
+            if (vmax > 0) {
+                hipLaunchKernelGGL(k_tri_vwork, dim3(std::min(grid(s, ne), 4 * s->num_cus)), dim3(1024), 0, st,
+                                   P<uint64_t>(g.ok), P<int64_t>(g.off), ne, tc.idmask(), g.vmt, bw,
+                                   P<unsigned long long>(vb));
+                HIP_CHECK(hipGetLastError());
+                std::vector<unsigned long long> hb(kVwBins);
+                HIP_CHECK(hipMemcpyAsync(hb.data(), P<void>(vb), sizeof(unsigned long long) * kVwBins,
+                                         hipMemcpyDeviceToHost, st));
+                HIP_CHECK(hipStreamSynchronize(st));
+                unsigned long long tot = 0;
+                for (unsigned long long x : hb) tot += x;
+                std::vector<int64_t> cut(W + 1, 0);  // first bin of each rank's range
+                unsigned long long cum = 0;
+                int64_t b = 0;
+                for (int q = 1; q < W; ++q) {
+                    const unsigned long long want = (unsigned long long)((__int128)tot * q / W);
+                    while (b < kVwBins && cum + hb[b] <= want) cum += hb[b++];
+                    cut[q] = b;
+                }
+                cut[W] = kVwBins;
+                v_lo = cut[dd->rank] * bw;
+                v_hi = dd->rank + 1 == W ? n : std::min<int64_t>(n, cut[dd->rank + 1] * bw);
+            }
+            Buf f = dev_alloc(ne, s), sel;
+            hipLaunchKernelGGL(k_tri_in_flags, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off),
+                               ne, tc.idmask(), g.vmt, v_lo, v_hi, P<uint8_t>(f));
+            HIP_CHECK(hipGetLastError());
+            const int64_t nsel = flags_to_indices(s, P<uint8_t>(f), ne, sel);
+            f.reset();
+            Buf ik = dev_alloc(sizeof(uint64_t) * (nsel > 0 ? nsel : 1), s);
+            if (nsel > 0)
+                hipLaunchKernelGGL(k_swap_keys_sel, dim3(grid(s, nsel)), dim3(256), 0, st, P<uint64_t>(g.ok),
+                                   P<int64_t>(g.off), P<int64_t>(sel), nsel, tc, P<uint64_t>(ik));
+            sel.reset();
+            radix_sort_digits(s, P<uint64_t>(ik), nullptr, nsel, td);
+            g.ioff = dev_alloc(sizeof(int64_t) * (n + 1), s);
+            hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), nsel, n, tsh,
+                               P<int64_t>(g.ioff));
+            g.itg = dev_alloc(sizeof(uint32_t) * (nsel > 0 ? nsel : 1), s);
+            g.ipos = dev_alloc(sizeof(uint32_t) * (nsel > 0 ? nsel : 1), s);
+            if (nsel > 0)
+                hipLaunchKernelGGL(k_in_split, dim3(grid(s, nsel)), dim3(256), 0, st, P<uint64_t>(ik), nullptr,
+                                   P<int64_t>(g.off), nsel, tc, P<uint32_t>(g.itg), P<uint32_t>(g.ipos));
+            g.vm_own = true;
+        } else {
+            Buf ik = dev_alloc(sizeof(uint64_t) * ne, s), iv = packed ? Buf() : dev_alloc(sizeof(int64_t) * ne, s);
+            hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off), ne,
+                               tc, P<uint64_t>(ik), packed ? nullptr : P<int64_t>(iv));
+            radix_sort_digits(s, P<uint64_t>(ik), packed ? nullptr : P<int64_t>(iv), ne, td);
+            g.ioff = dev_alloc(sizeof(int64_t) * (n + 1), s);
+            hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), ne, n, tsh,
+                               P<int64_t>(g.ioff));
+            g.itg = dev_alloc(sizeof(uint32_t) * ne, s);
+            g.ipos = dev_alloc(sizeof(uint32_t) * ne, s);
+            hipLaunchKernelGGL(k_in_split, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(ik),
+                               packed ? nullptr : P<int64_t>(iv), P<int64_t>(g.off), ne, tc, P<uint32_t>(g.itg),
+                               P<uint32_t>(g.ipos));
+        }
         Buf fvm = dev_alloc(n, s);
         hipLaunchKernelGGL(k_tri_vm_bins, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), P<int64_t>(g.ioff), n,
                            g.vmt, P<uint8_t>(fvm));
@@ -1295,7 +1414,12 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         REQUIRE(dd->world <= 255, CAPSMI_ERR_UNSUPPORTED, "distributed triangle count: at most 255 ranks");
         g.wparts = dd->world;
         work(g.big_u, g.nbig, false, false, g.wbig);
-        work(g.vm_c, g.nvm, true, false, g.wvm);
+        if (g.vm_own) {  // every v-mode center of this build is this rank's
+            g.wvm.assign(dd->world + 1, 0);
+            for (int q = dd->rank + 1; q <= dd->world; ++q) g.wvm[q] = g.nvm;
+        } else {
+            work(g.vm_c, g.nvm, true, false, g.wvm);
+        }
         work(g.small_u, g.nsmall, false, true, g.wsmall);
     }
 }
