@@ -114,8 +114,20 @@ class TorchCollective:
         self.world = dist.get_world_size(group)
         self.device = device
         self.drain = device == "cuda" and dist.get_backend(group) != "nccl"
-        self.view = device_view if device == "cuda" else host_view
+        self._make_view = device_view if device == "cuda" else host_view
+        self._views = {}  # (ptr, count, dtype) -> tensor: the library's block cache hands back the same
+        # buffers query after query, so their views are built once (a view costs tens of microseconds)
         self.gate = serial_gate() if self.drain else None
+
+    def view(self, ptr: int, count: int, dtype: int):
+        key = (int(ptr or 0), int(count), int(dtype))
+        t = self._views.get(key)
+        if t is None:
+            t = self._make_view(ptr, count, dtype)
+            if len(self._views) >= 256:
+                self._views.clear()
+            self._views[key] = t
+        return t
 
     def __call__(self, op: int, send: int, recv: int, count: int, dtype: int) -> None:
         import torch

@@ -939,6 +939,18 @@ int64_t sum_over_ranks(capsmi_session* s, int64_t v) {
     return read_scalar(s, P<int64_t>(t));
 }
 
+// the owned X1 / X2 slices side by side (one all-gather for both), and back into [X1 | X2] after it
+__global__ void k_pack_x12(const uint32_t* __restrict__ mid, int64_t nw, int64_t S, int64_t r, uint32_t* __restrict__ send) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * S; i += (int64_t)gridDim.x * blockDim.x)
+        send[i] = mid[(i < S ? 0 : nw) + r * S + (i < S ? i : i - S)];
+}
+__global__ void k_unpack_x12(const uint32_t* __restrict__ got, int64_t nw, int64_t S, uint32_t* __restrict__ full) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * nw; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t q = (i / S) >> 1, h = (i / S) & 1, k = i % S;  // got = [rank][X1 | X2][S]
+        full[h * nw + q * S + k] = got[i];
+    }
+}
+
 // 2-hop count(DISTINCT end) over relationship shards BY_TARGET: hop 1 is complete for the
 // middle ids this rank owns (their in-relationships are all here), one all-gather of the owned slices of
 // the frontier (X1, X2) gives every rank the whole frontier, hop 2 marks the end ids this rank owns, and
@@ -953,8 +965,17 @@ int64_t dist_two_hop_distinct(capsmi_session* s, const capsmi_relpart* cached, i
     if (cached) check(capsmi_two_hop_mark_mid_part(s, cached, a, b, P<uint32_t>(mid), P<uint32_t>(scratch)));
     else check(capsmi_relpart_build_mark_mid(s, nt, views, "s", "t", a, b, P<uint32_t>(mid), P<uint32_t>(scratch), &rp));
     std::unique_ptr<capsmi_relpart, capsmi_status (*)(capsmi_relpart*)> hold(rp, capsmi_relpart_release);
-    collective(s, CAPSMI_COLL_ALL_GATHER, P<uint32_t>(mid) + r * S, P<uint32_t>(full), S, CAPSMI_COLL_U32);
-    collective(s, CAPSMI_COLL_ALL_GATHER, P<uint32_t>(mid) + nw + r * S, P<uint32_t>(full) + nw, S, CAPSMI_COLL_U32);
+    {  // one all-gather of the owned (X1, X2) slice pairs instead of one per frontier
+        Buf x12 = dev_alloc(sizeof(uint32_t) * (2 * S + 2 * nw), s);
+        uint32_t *send = P<uint32_t>(x12), *got = send + 2 * S;
+        const unsigned gs = (unsigned)std::max<int64_t>(1, std::min<int64_t>((2 * S + 255) / 256, (int64_t)s->num_cus * 8));
+        const unsigned gn = (unsigned)std::max<int64_t>(1, std::min<int64_t>((2 * nw + 255) / 256, (int64_t)s->num_cus * 8));
+        hipLaunchKernelGGL(k_pack_x12, dim3(gs), dim3(256), 0, s->stream, P<uint32_t>(mid), nw, S, r, send);
+        HIP_CHECK(hipGetLastError());
+        collective(s, CAPSMI_COLL_ALL_GATHER, send, got, 2 * S, CAPSMI_COLL_U32);
+        hipLaunchKernelGGL(k_unpack_x12, dim3(gn), dim3(256), 0, s->stream, got, nw, S, P<uint32_t>(full));
+        HIP_CHECK(hipGetLastError());
+    }
     check(capsmi_two_hop_mark_dst_part(s, cached ? cached : rp, b, c, P<uint32_t>(full), P<uint32_t>(dst)));
     Buf cnt = dev_alloc(sizeof(int64_t), s);
     check(capsmi_words_popcount_device(s, P<uint32_t>(dst), r * S, (r + 1) * S, P<int64_t>(cnt)));
