@@ -356,8 +356,15 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_deg(ChunkWalk cw, const uint32_
     }
 }
 
+// od narrowed to 32 bits for the W walk's gathers: half the bytes, so more of it stays in each XCD's L2
+// (an out-degree is below 2^32: relationship counts are)
+__global__ void k_vl_narrow(const unsigned long long* __restrict__ od, int64_t n, uint32_t* __restrict__ od32) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        od32[i] = (uint32_t)od[i];
+}
+
 // pass 2: W(v) = sum_{v -> w} od(w); 64 KiB of LDS, two blocks per CU for the random od gathers
-__global__ void __launch_bounds__(kVlBlock) k_vl_w(ChunkWalk cw, int64_t n, const unsigned long long* __restrict__ od,
+__global__ void __launch_bounds__(kVlBlock) k_vl_w(ChunkWalk cw, int64_t n, const uint32_t* __restrict__ od,
                                                    unsigned long long* __restrict__ W) {
     extern __shared__ unsigned long long vl_lds[];
     unsigned long long* a_w = vl_lds;
@@ -368,7 +375,7 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_w(ChunkWalk cw, int64_t n, cons
         [&](const uint2 (&pr)[part::kWalkItems], uint32_t valid, int) {  // pr[k] = (t, s)
             unsigned long long x[part::kWalkItems];
 #pragma unroll
-            for (int k = 0; k < part::kWalkItems; ++k) x[k] = od[pr[k].x];  // all gathers first
+            for (int k = 0; k < part::kWalkItems; ++k) x[k] = od[pr[k].x];  // all gathers first (4 B each)
 #pragma unroll
             for (int k = 0; k < part::kWalkItems; ++k)
                 if (((valid >> k) & 1u) && x[k]) atomicAdd(&a_w[pr[k].y & (kVlIds - 1)], x[k]);
@@ -494,12 +501,24 @@ __global__ void k_vl_bmerge(const int64_t* __restrict__ jst, int nt, int64_t blo
 }
 
 // (od(b), Y(b) = W(b) - s(b) b_ok(b)) side by side: pass 3 gathers both with one access
+// (od, Y) also as one 8-byte word, od << 40 | Y, while od < 2^24 and 0 <= Y < 2^40 everywhere (*fits cleared
+// otherwise): the T walk then gathers half the bytes
+constexpr int kPkShift = 40;
+__device__ __forceinline__ void pack8(int64_t i, long long od, long long y, unsigned long long* pk, unsigned int* fits) {
+    const bool ok = od >= 0 && od < (1LL << (64 - kPkShift)) && y >= 0 && y < (1LL << kPkShift);
+    pk[i] = ((unsigned long long)od << kPkShift) | (unsigned long long)y;
+    if (!ok) atomicAnd(fits, 0u);
+}
+
 __global__ void k_vl_y(int64_t n, const uint32_t* __restrict__ bw, int b_full, const unsigned long long* __restrict__ od,
                        const unsigned long long* __restrict__ W, const unsigned long long* __restrict__ sl,
-                       longlong2* __restrict__ ody) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        ody[i] = make_longlong2((long long)od[i],
-                                (long long)W[i] - (bit_of(bw, b_full, (uint32_t)i) ? (long long)sl[i] : 0LL));
+                       longlong2* __restrict__ ody, unsigned long long* __restrict__ pk, unsigned int* __restrict__ fits) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const long long o = (long long)od[i];
+        const long long y = (long long)W[i] - (bit_of(bw, b_full, (uint32_t)i) ? (long long)sl[i] : 0LL);
+        ody[i] = make_longlong2(o, y);
+        if (pk) pack8(i, o, y, pk, fits);
+    }
 }
 
 // sharded form: Y(b) alone (partial: the owner's W), then (od, Y) packed once both are reduced
@@ -511,9 +530,11 @@ __global__ void k_vl_yonly(int64_t n, const uint32_t* __restrict__ bw, int b_ful
 }
 
 __global__ void k_vl_pack(int64_t n, const long long* __restrict__ od, const long long* __restrict__ Y,
-                          longlong2* __restrict__ ody) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+                          longlong2* __restrict__ ody, unsigned long long* __restrict__ pk, unsigned int* __restrict__ fits) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         ody[i] = make_longlong2(od[i], Y[i]);
+        if (pk) pack8(i, od[i], Y[i], pk, fits);
+    }
 }
 
 // R(a) = sum_b m(a, b) m(b, a) b_ok(b) over the candidate table (every pair with its reverse present
@@ -541,8 +562,11 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_t(ChunkWalk cw, const uint32_t*
                                                    int64_t n, const unsigned long long* __restrict__ od,
                                                    const longlong2* __restrict__ ody, unsigned long long* __restrict__ T2,
                                                    unsigned long long* __restrict__ T3, RegionBloom bl,
-                                                   const uint32_t* __restrict__ f2, PairHash h) {
+                                                   const uint32_t* __restrict__ f2, PairHash h,
+                                                   const unsigned long long* __restrict__ pk,
+                                                   const unsigned int* __restrict__ fits) {
     extern __shared__ unsigned long long vl_lds[];
+    const bool p8 = ody && pk && *fits;  // uniform: the 8-byte (od, Y) words
     unsigned long long *a_t2 = vl_lds, *a_t3 = vl_lds + kVlIds;
     for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_t2[i] = a_t3[i] = 0;
     __syncthreads();
@@ -560,7 +584,14 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_t(ChunkWalk cw, const uint32_t*
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const uint32_t b = pr[k].x;  // zero pairs past a chunk's fill: in range
-                if (ody) v[k] = ody[b]; else o1[k] = od[b];
+                if (p8) {
+                    const unsigned long long w = pk[b];
+                    v[k] = make_longlong2((long long)(w >> kPkShift), (long long)(w & ((1ULL << kPkShift) - 1)));
+                } else if (ody) {
+                    v[k] = ody[b];
+                } else {
+                    o1[k] = od[b];
+                }
                 if (h.slot) {
                     uint32_t word;
                     f2_pos(pkey(b, pr[k].y), word, fb[k]);
@@ -634,7 +665,8 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
         for (const void* f : {reinterpret_cast<const void*>(k_vl_deg), reinterpret_cast<const void*>(k_vl_w),
                               reinterpret_cast<const void*>(k_vl_t)})
             HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
-        Buf ody, bw, hk, hc, cand, f2;
+        Buf ody, pk, bw, hk, hc, cand, f2;
+        unsigned int* fits = nullptr;
         RegionBloom bl{nullptr, 0, 0, 0};
         PairHash h{nullptr, nullptr, nullptr, 0};
         if (need3) {
@@ -693,7 +725,10 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
         if (need3) {
             {
                 KernelTimer kt(s, "varlen_w");
-                hipLaunchKernelGGL(k_vl_w, dim3(g), dim3(kVlBlock), lds2 / 2, st, cw, n, P<unsigned long long>(od),
+                Buf od32 = dev_alloc(sizeof(uint32_t) * (size_t)n, s);
+                hipLaunchKernelGGL(k_vl_narrow, dim3(grid(s, n)), dim3(256), 0, st, P<unsigned long long>(od), n,
+                                   P<uint32_t>(od32));
+                hipLaunchKernelGGL(k_vl_w, dim3(g), dim3(kVlBlock), lds2 / 2, st, cw, n, P<uint32_t>(od32),
                                    P<unsigned long long>(W));
             }
             const int64_t nc = read_scalar(s, P<int64_t>(cand));
@@ -714,15 +749,20 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
                                    P<unsigned long long>(cand), h);
             }
             ody = dev_alloc(2 * nb, s);
+            pk = dev_alloc(nb + sizeof(unsigned int), s);  // the 8-byte words, then the fits flag
+            fits = reinterpret_cast<unsigned int*>(P<unsigned long long>(pk) + n);
+            HIP_CHECK(hipMemsetAsync(fits, 1, sizeof(unsigned int), st));  // nonzero: fits
             hipLaunchKernelGGL(k_vl_y, dim3(grid(s, n)), dim3(256), 0, st, n, d.b, d.b_full, P<unsigned long long>(od),
-                               P<unsigned long long>(W), P<unsigned long long>(sl), P<longlong2>(ody));
+                               P<unsigned long long>(W), P<unsigned long long>(sl), P<longlong2>(ody),
+                               P<unsigned long long>(pk), fits);
         }
         {
             KernelTimer kt(s, "varlen_t");
             const PairHash ht = use_f2 ? h : PairHash{nullptr, nullptr, nullptr, 0};  // list form: no inserts here
             hipLaunchKernelGGL(k_vl_t, dim3(g), dim3(kVlBlock), lds2, st, cw, d.a, d.a_full, n, P<unsigned long long>(od),
                                need3 ? P<longlong2>(ody) : nullptr, P<unsigned long long>(T2),
-                               P<unsigned long long>(T3), bl, P<uint32_t>(f2), ht);
+                               P<unsigned long long>(T3), bl, P<uint32_t>(f2), ht,
+                               need3 ? P<unsigned long long>(pk) : nullptr, fits);
         }
         if (need3) {
             KernelTimer kt(s, "varlen_recip");
@@ -823,7 +863,7 @@ struct VarlenShard {
     bool need3 = false;
     part::Layout L{};
     ChunkPart cp;  // out, by source slice
-    Buf sl, W, T2, T3, ody, bw, hk, hc;
+    Buf sl, W, T2, T3, ody, pk, bw, hk, hc;
     int64_t* od = nullptr;  // caller buffers (n int64 each), summed over ranks by the caller
     int64_t* y = nullptr;
 };
@@ -958,8 +998,11 @@ void varlen_shard_mid(VarlenShard* v, int64_t* y) {
         const ChunkWalk cw{P<uint2>(v->cp.pool), P<unsigned long long>(v->cp.meta), v->cp.order, v->cp.jst,
                            v->cp.segbase, v->cp.ja, v->L.nt};
         KernelTimer kt(s, "varlen_w");
+        Buf od32 = dev_alloc(sizeof(uint32_t) * (size_t)v->n, s);
+        hipLaunchKernelGGL(k_vl_narrow, dim3(grid(s, v->n)), dim3(256), 0, st,
+                           reinterpret_cast<const unsigned long long*>(v->od), v->n, P<uint32_t>(od32));
         hipLaunchKernelGGL(k_vl_w, dim3((unsigned)v->cp.g2), dim3(kVlBlock), sizeof(unsigned long long) * kVlIds, st,
-                           cw, v->n, reinterpret_cast<const unsigned long long*>(v->od), P<unsigned long long>(v->W));
+                           cw, v->n, P<uint32_t>(od32), P<unsigned long long>(v->W));
     }
     hipLaunchKernelGGL(k_vl_yonly, dim3(grid(s, v->n)), dim3(256), 0, st, v->n, v->d.b, v->d.b_full,
                        P<unsigned long long>(v->W), P<unsigned long long>(v->sl), reinterpret_cast<long long*>(y));
@@ -971,11 +1014,16 @@ int64_t varlen_shard_finish(VarlenShard* v, Buf& out_ids, Buf& out_cnt) {
     capsmi_session* s = v->s;
     hipStream_t st = s->stream;
     const int64_t n = v->n;
+    unsigned int* fits = nullptr;
     if (v->need3) {
         REQUIRE(v->y != nullptr, CAPSMI_ERR_ILLEGAL_ARGUMENT, "varlen shard: mid() before finish()");
         v->ody = dev_alloc(2 * sizeof(int64_t) * n, s);
+        v->pk = dev_alloc(sizeof(unsigned long long) * n + sizeof(unsigned int), s);
+        fits = reinterpret_cast<unsigned int*>(P<unsigned long long>(v->pk) + n);
+        HIP_CHECK(hipMemsetAsync(fits, 1, sizeof(unsigned int), st));  // nonzero: fits
         hipLaunchKernelGGL(k_vl_pack, dim3(grid(s, n)), dim3(256), 0, st, n, reinterpret_cast<const long long*>(v->od),
-                           reinterpret_cast<const long long*>(v->y), P<longlong2>(v->ody));
+                           reinterpret_cast<const long long*>(v->y), P<longlong2>(v->ody), P<unsigned long long>(v->pk),
+                           fits);
     }
     if (v->cp.pool) {
         const ChunkWalk cw{P<uint2>(v->cp.pool), P<unsigned long long>(v->cp.meta), v->cp.order, v->cp.jst,
@@ -985,7 +1033,8 @@ int64_t varlen_shard_finish(VarlenShard* v, Buf& out_ids, Buf& out_cnt) {
                            cw, v->d.a, v->d.a_full, n, reinterpret_cast<const unsigned long long*>(v->od),
                            v->need3 ? P<longlong2>(v->ody) : nullptr, P<unsigned long long>(v->T2),
                            P<unsigned long long>(v->T3), RegionBloom{nullptr, 0, 0, 0}, nullptr,
-                           PairHash{nullptr, nullptr, nullptr, 0});
+                           PairHash{nullptr, nullptr, nullptr, 0}, v->need3 ? P<unsigned long long>(v->pk) : nullptr,
+                           fits);
     }
     Buf cnt = dev_alloc(sizeof(int64_t) * n, s), flags = dev_alloc(n, s);
     hipLaunchKernelGGL(k_final, dim3(grid(s, n)), dim3(256), 0, st, n, v->d, v->lower, v->upper,
