@@ -1,5 +1,6 @@
 """Every golden vector of the reference's acceptance tests (tests/golden/acceptance.json, predicates.json)
-over a graph distributed on 2 ranks (gloo ranks sharing the GPU; tests/dist_golden_worker.py): routed plans
+over a graph distributed on 2 ranks (gloo ranks sharing the GPU; tests/dist_golden_worker.py), and on one rank
+over RCCL: routed plans
 and operator-by-operator plans whose joins, groupings, distincts, global aggregates and orderings take the
 generic executor's Exchanges (csrc/plan.hip; Spark's Exchange before joins and aggregates, SparkTable.scala:
 133, 226).  A partitioned result's rows, summed over the ranks, and a whole result on every rank must equal
@@ -34,33 +35,39 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("mode", ["fused", "unfused"])
-def test_golden_vectors_on_two_ranks(tmp_path, mode):
+# (ranks, backend, mode): 2 gloo ranks sharing the GPU, routed and unrouted; and 1 rank over RCCL (backend
+# nccl), unrouted, so every Exchange of the generic executor -- the ALL_TO_ALL_V of hash-partitioned joins
+# and groupings, the all-gathers of global aggregates and ordering -- runs through RCCL, in chunked calls
+# (CAPSMI_COLL_CHUNK=64: the golden graphs are small)
+@pytest.mark.parametrize("world,backend,mode", [(2, "gloo", "fused"), (2, "gloo", "unfused"), (1, "nccl", "unfused")])
+def test_golden_vectors_on_two_ranks(tmp_path, world, backend, mode):
     out = str(tmp_path / "golden")
-    env = dict(os.environ, CAPSMI_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+    env = dict(os.environ, CAPSMI_DIST_BACKEND=backend, MASTER_ADDR="127.0.0.1")
+    if backend == "nccl":
+        env["CAPSMI_COLL_CHUNK"] = "64"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}", "--master-addr",
            "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", "dist_golden_worker.py"), out, mode]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)
     assert p.returncode == 0, _err(p.stderr)
     ranks = []
-    for r in range(2):
+    for r in range(world):
         with open(f"{out}.rank{r}.json") as f:
             ranks.append(json.load(f))
     refused, checked = [], 0
     for _, case in all_cases():
         name = case["name"]
-        a, b = ranks[0][name], ranks[1][name]
-        if "error" in a or "error" in b:
-            refused.append((name, a.get("error"), b.get("error")))
+        res = [x[name] for x in ranks]
+        if any("error" in x for x in res):
+            refused.append((name, [x.get("error") for x in res]))
             continue
-        assert a["partitioned"] == b["partitioned"], name
-        if a["partitioned"]:
-            got = a["rows"] + b["rows"]
+        assert len({x["partitioned"] for x in res}) == 1, name
+        if res[0]["partitioned"]:
+            got = [row for x in res for row in x["rows"]]
             assert same_rows(got, case["expected"]), (name, got, case["expected"])
         else:
-            for x in (a, b):
+            for x in res:
                 assert same_rows(x["rows"], case["expected"], case.get("ordered", False)), (name, x["rows"],
                                                                                                case["expected"])
         checked += 1
     assert not refused, refused
-    print(f"{mode}: {checked} golden vectors equal on 2 ranks")
+    print(f"{mode}: {checked} golden vectors equal on {world} rank(s) over {backend}")
