@@ -462,6 +462,7 @@ def main():
         return out
 
     results = {}
+    medians = {}  # this rank's median step (ms): SURVEY.md 8d asks for the median beside the mean
     gate = None
     if distributed:
         from capsmi.dist import serial_gate
@@ -486,12 +487,16 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        marks = []  # each step ends with its answer on the host (a device sync): per-step times for the median
         for _ in range(args.steps):
             res = step()
+            marks.append(time.perf_counter())
         torch.cuda.synchronize()
         if distributed:
             dist.barrier()
         elapsed = time.perf_counter() - t0
+        per_step = [b - a for a, b in zip([t0] + marks[:-1], marks)]
+        medians[mode] = sorted(per_step)[len(per_step) // 2] * 1e3 if per_step else None
         kt = kernel_times()
         _lib.call("capsmi_session_set_profiling", sess.handle, 0)
         if distributed:
@@ -562,6 +567,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": sec * 1e3,
+            "ms_per_step_median_rank0": medians.get(head),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -600,7 +606,7 @@ def main():
         warm_phys = 2 * 5 * m_total + 3 * n // 8
         for mode in modes[1:]:
             s2, r2, kt2 = results[mode]
-            entry = {"ms_per_step": s2 * 1e3, "value": matched / s2,
+            entry = {"ms_per_step": s2 * 1e3, "ms_per_step_median_rank0": medians.get(mode), "value": matched / s2,
                      ("count_star" if mode in ("count", "count_atomic", "und_count") else "count_distinct_c"): r2,
                      "kernel_ms": {k: v[1] / v[0] for k, v in kt2.items() if v[0] > 0}}
             if mode in ("warm", "direct_warm"):
