@@ -57,6 +57,22 @@ C4_QUERY = {"clauses": [{"match": "(a:Person)-[r1:FRIEND_OF]->(b:Person)-[r2:FRI
 C5_QUERY = {"clauses": [{"match": "(a:Person)-[:KNOWS*1..3]->(b:Person)"}],
             "return": {"items": [["id", ["id", "a"]], ["count", ["count*"]]]}}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PAR_SOURCE = ("dp{w}: relationships hash-partitioned by source over {w} GPUs (capsmi_graph_distribute, north_star's "
+              "owner(source)); hop-1 frontier slices exchanged by ALL_TO_ALL_V and ORed on their owner, end-bitmap "
+              "slices the same, count all-reduce, over RCCL inside the route")
+PAR_TARGET = ("dp{w}: relationships hash-partitioned by target over {w} GPUs (capsmi_graph_distribute); hop-1 "
+              "frontier bitmap all-gather + count all-reduce over RCCL inside the route")
+# what each C3-line mode runs (config.workload of a line headed by that mode), and the key of its answer
+MODE_QUERY = {
+    "und_count": ("C3 undirected: MATCH (a:Person)-[:FRIEND_OF]-(b:Person)-[:FRIEND_OF]-(c:Person) RETURN count(*)",
+                  "und_count_star"),
+    "und_distinct": ("C3 undirected: MATCH (a:Person)-[:FRIEND_OF]-(b:Person)-[:FRIEND_OF]-(c:Person) "
+                     "RETURN count(DISTINCT c)", "und_count_distinct_c"),
+    "count": ("C3: MATCH (a:Person)-[:FRIEND_OF]->(b:Person)-[:FRIEND_OF]->(c:Person) RETURN count(*)", "count_star"),
+    "count_atomic": ("C3: MATCH (a:Person)-[:FRIEND_OF]->(b:Person)-[:FRIEND_OF]->(c:Person) RETURN count(*)",
+                     "count_star"),
+}
+C3_WORKLOAD = "C3: MATCH (a:Person)-[:FRIEND_OF]->(b:Person)-[:FRIEND_OF]->(c:Person) RETURN count(DISTINCT c)"
 KERNELS = ("part_scatter1", "part_scatter2_hop1", "part_scatter2", "hop1", "hop2", "mid_combine", "bitmap_add",
            "bitmap_range",
            "count_part", "count_part_in", "count_in", "count_part_out", "count_out", "degrees", "und_count_part",
@@ -86,8 +102,11 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-scale", type=int, default=None, help="oracle sample scale (default per workload)")
     p.add_argument("--shard-of", type=int, default=0,
-                   help="diagnostic (C3): time rank 0's shard of an N-way owner(target) partition on one GPU, "
+                   help="diagnostic (C3): time every rank's shard of an N-way partition (--rels-by) on one GPU, "
                         "no exchange; the line is not the metric")
+    p.add_argument("--rels-by", default="source", choices=("source", "target"),
+                   help="C3 at N > 1 / --dist1 / --shard-of: relationships partitioned by the owner of their source "
+                        "(north_star; the one distribution every route takes) or of their target")
     p.add_argument("--c2-route", default="direct", choices=("direct", "planner", "joins"),
                    help="C2: explicit expand kernels (direct), Planner(sg).run routed to the fused expand "
                         "(planner), or the same plan operator by operator through the generic radix joins (joins)")
@@ -183,10 +202,10 @@ def _pmc_entry(kernel, workload):
 
 
 def shard_diagnostic(args):
-    """--shard-of N on one GPU: every rank's owner(target) shard of the C3 cold step, timed one after
-    the other (kernels only: the frontier exchange and the count all-reduce are not run, the node scan
-    is the whole table).  Reports per-rank times and the max -- the projected N-GPU step before the
-    collectives.  Not the metric."""
+    """--shard-of N on one GPU: every rank's owner(source) (or --rels-by target) shard of the C3 cold step,
+    timed one after the other (kernels only: the frontier exchange and the count all-reduce are not run,
+    the node scan is the whole table).  Reports per-rank times and the max -- the projected N-GPU step
+    before the collectives.  Not the metric."""
     import torch
     from capsmi import Session, graph
     N = args.shard_of
@@ -205,9 +224,11 @@ def shard_diagnostic(args):
     cnt_dev = torch.zeros(1, dtype=torch.int64, device="cuda")
     per_rank, per_rank_count, rows = [], [], []
     for r in range(N):
-        rels = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42, part_col=graph.PART_TARGET, part=r,
-                               nparts=N)
+        by_src = args.rels_by == "source"
+        rels = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42,
+                               part_col=graph.PART_SOURCE if by_src else graph.PART_TARGET, part=r, nparts=N)
         wb, we = graph.owner_words(n, r, N)
+        cs, cd = ("target", "source") if by_src else ("source", "target")  # count(*): reversed over BY_SOURCE
 
         def step():
             p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")
@@ -227,7 +248,7 @@ def shard_diagnostic(args):
 
         def step_count():  # count(*) shard: partition + IN walk + owned fold, OUT walk (no gather / all-reduce)
             p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")
-            sh = graph.CountShard(sess, [rels], p, p, p, 32 * wb, min(32 * we, n), own_in.data_ptr())
+            sh = graph.CountShard(sess, [rels], p, p, p, 32 * wb, min(32 * we, n), own_in.data_ptr(), cs, cd)
             sh.finish(in_all.data_ptr(), cnt_dev.data_ptr())
             sh.close()
 
@@ -242,7 +263,8 @@ def shard_diagnostic(args):
         rows.append(rels.size)
         del rels
     mean = sum(per_rank) / N
-    print(json.dumps({"diagnostic": f"C3 cold step, every rank's owner(target) shard of {N} on one GPU, no exchange",
+    print(json.dumps({"diagnostic": f"C3 cold step, every rank's owner({args.rels_by}) shard of {N} on one GPU, "
+                                    "no exchange",
                       "scale": scale, "per_rank_ms": per_rank, "max_ms": max(per_rank), "mean_ms": mean,
                       "imbalance_max_over_mean": max(per_rank) / mean, "rels_per_rank": rows,
                       "count_star_per_rank_ms": per_rank_count, "count_star_max_ms": max(per_rank_count)}),
@@ -302,14 +324,14 @@ def main():
         ingest_gate = serial_gate()  # a serialised rehearsal also serialises the ranks' ingest peaks
         if ingest_gate:
             ingest_gate.acquire()
-        rels = owned_rmat_rels(sess, graph, scale, m_total, graph.RMAT_GRAPH500, "target", n)
+        rels = owned_rmat_rels(sess, graph, scale, m_total, graph.RMAT_GRAPH500, args.rels_by, n)
     else:
         rels = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42,
                                part_col=graph.PART_TARGET if shards > 1 else graph.PART_NONE, part=part, nparts=shards)
     persons = graph.rmat_nodes(sess, scale, graph.NODES_ALL)
     if distributed:
         persons = persons.owned_rows("id", 0, n).as_node_table("id")
-        distribute(sess, 0, n, [persons], [rels], nodes_owned=True, rels_by="target")
+        distribute(sess, 0, n, [persons], [rels], nodes_owned=True, rels_by=args.rels_by)
     m_local = rels.size
     sess.sync()
     if ingest_gate:
@@ -417,7 +439,7 @@ def main():
     # Cache analogue: a second handle on the same columns, marked cache() so the route keeps its layout
     rels_cached = rels.select("id", "source", "target").as_rel_table("id", "source", "target").cache()
     if distributed:
-        distribute(sess, 0, n, [], [rels_cached], nodes_owned=True, rels_by="target")
+        distribute(sess, 0, n, [], [rels_cached], nodes_owned=True, rels_by=args.rels_by)
     sg_warm = scan_graph(rels_cached)
 
     def run_planner(sg):
@@ -521,6 +543,10 @@ def main():
         all_persons = graph.rmat_nodes(sess, scale, graph.NODES_ALL) if distributed else persons
         p = graph.NodeBitmap(sess, 0, n).add_scan(all_persons, "id")
         matched = graph.two_hop_count(sess, [full], p, p, p)
+        # the undirected modes' bindings: the undirected count(*) (its own run's answer when und_count ran, else
+        # the oracle fixture), so their value is undirected bindings / s, not the directed match's
+        fxu0 = fixture(f"c3u_s{scale}") or {}
+        und_matched = results["und_count"][1] if "und_count" in results else fxu0.get("count_star")
         answers = {m: r[1] for m, r in results.items()}
         if shards != 1:
             check = f"not applicable (--shard-of {shards}: rank 0's shard alone)"
@@ -539,6 +565,9 @@ def main():
     if rank == 0:
         head = modes[0]
         sec, res, kt = results[head]
+
+        def rows_of(mode):  # matched rows of a mode's query
+            return und_matched if mode.startswith("und_") else matched
         # per-kernel algorithmic bytes (this rank's rels): what each kernel must touch by its function
         alg = {"part_scatter1": m_local * 24,        # read 2 x int64, write packed uint2
                "part_scatter2_hop1": m_local * 16 + n // 8,  # read + write uint2, write M
@@ -561,7 +590,7 @@ def main():
         query_alg = 2 * 24 * m_total + 3 * 8 * n  # SURVEY.md §8d C3 B_alg (whole query, all ranks)
         line = {
             "metric": METRIC,
-            "value": matched / sec,
+            "value": rows_of(head) / sec if rows_of(head) is not None else None,
             "unit": "matched rows/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -573,21 +602,18 @@ def main():
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic R-MAT (on-device counter-based generator, oracle/rmat.c definition)",
-            "config": {"workload": "C3: MATCH (a:Person)-[:FRIEND_OF]->(b:Person)-[:FRIEND_OF]->(c:Person) "
-                                   "RETURN count(DISTINCT c)",
+            "config": {"workload": MODE_QUERY.get(head, (C3_WORKLOAD,))[0],
                        "mode": head, "scale": scale, "nodes": n, "relationships": m_total,
                        "rmat": [0.57, 0.19, 0.19, 0.05], "seed": 42,
-                       "parallelism": (f"dp{world}: relationships hash-partitioned by target over {world} GPUs "
-                                       "(capsmi_graph_distribute); node-scan and hop-1 frontier bitmap all-gathers "
-                                       "+ count all-reduce over RCCL inside the route") if world > 1 else
-                       "single GPU (no exchange)",
+                       "parallelism": (PAR_SOURCE if args.rels_by == "source" else PAR_TARGET).format(w=world)
+                       if world > 1 else "single GPU (no exchange)",
                        "route": ("Planner(sg).run(query): lazy Table[T] plan -> fused two-hop kernels "
                                  f"({routed} plans routed on this rank)") if shards == 1 and
                        head in ("cold", "warm", "count") else "explicit phased kernel calls"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": KERNEL_SYMBOL[dom],
                          "kernel_ms": avg_ms, "alg_bytes_per_launch": alg[dom]},
-            "query": {"count_distinct_c": res, "matched_rows": matched,
+            "query": {MODE_QUERY.get(head, (None, "count_distinct_c"))[1]: res, "matched_rows": rows_of(head),
                       "check_vs_fixture": check,  # tests/golden/rmat_full.json (oracle closed form)
                       "alg_bytes_query": query_alg,
                       "query_alg_GBs": query_alg / sec / 1e9,
@@ -606,13 +632,23 @@ def main():
         warm_phys = 2 * 5 * m_total + 3 * n // 8
         for mode in modes[1:]:
             s2, r2, kt2 = results[mode]
-            entry = {"ms_per_step": s2 * 1e3, "ms_per_step_median_rank0": medians.get(mode), "value": matched / s2,
-                     ("count_star" if mode in ("count", "count_atomic", "und_count") else "count_distinct_c"): r2,
+            entry = {"ms_per_step": s2 * 1e3, "ms_per_step_median_rank0": medians.get(mode),
+                     "value": rows_of(mode) / s2 if rows_of(mode) is not None else None,
+                     MODE_QUERY.get(mode, (None, "count_distinct_c"))[1]: r2,
                      "kernel_ms": {k: v[1] / v[0] for k, v in kt2.items() if v[0] > 0}}
+            if mode.startswith("und_"):
+                entry["workload"] = MODE_QUERY[mode][0]
+                entry["matched_rows"] = und_matched
             if mode in ("warm", "direct_warm"):
                 entry.update({"phys_bytes_query": warm_phys,
                               "phys_basis": "cached 5-B packed layout read once per hop + hop bitmaps",
                               "phys_frac_of_peak": warm_phys / s2 / 1e9 / (HBM_PEAK_GBS * world)})
+            elif mode.startswith("und_"):
+                # SURVEY.md 8d's B_alg over the undirected plan: 2^2 branches (outgoing / incoming per hop), each
+                # 2 relationship scans (24 B/rel: the ids feed r1 <> r2) and 3 node scans
+                und_alg = 8 * 24 * m_total + 12 * 8 * n
+                entry.update({"alg_bytes_query": und_alg, "alg_basis": "SURVEY 8d B_alg of the 4-branch undirected plan",
+                              "query_frac_of_peak": und_alg / s2 / 1e9 / (HBM_PEAK_GBS * world)})
             else:
                 entry.update({"alg_bytes_query": query_alg,
                               "query_frac_of_peak": query_alg / s2 / 1e9 / (HBM_PEAK_GBS * world)})
@@ -986,6 +1022,16 @@ def cpu_baseline_single(wl, scale, ef, probs, full_scale):
             "sample": f"CPU restatement, not CAPS: the device algorithm -- {what} -- on R-MAT scale {same_scale} "
                       f"({'the full workload' if same_scale == full_scale else 'a bounded sample'}), edge factor "
                       f"{ef}: {rows} rows, {dt:.2f} s"}
+    if wl == "c4" and same_scale != full_scale:
+        # the same algorithm on the FULL workload is ~20 min of CPU: carried from the fixture run that made the
+        # committed answer (tests/golden/make_rmat_full.py, build container, times recorded in rmat_full.json)
+        fx = fixture(f"c4_s{full_scale}")
+        if fx and fx.get("cpu_seconds"):
+            line["full_size"] = {"value": fx["count_star"] / fx["cpu_seconds"], "unit": "matched rows/s",
+                                 "seconds": fx["cpu_seconds"], "rows": fx["count_star"],
+                                 "sample": f"the same triangle listing on the full R-MAT scale {full_scale} input, "
+                                           f"timed when tests/golden/make_rmat_full.py made the fixture (build "
+                                           f"container, OpenMP), not re-run on this host"}
     if wl == "c2":
         return line
     n = 1 << scale

@@ -21,7 +21,6 @@ from . import _lib
 from .table import GpuTable, Session
 
 _DT = {0: "<i8", _lib.COLL_U32: "<i4"}
-COLL_CHUNK_ELEMS = 1 << 26  # words one collective call moves in all (512 MiB of int64)
 
 
 class _DevPtr:
@@ -100,16 +99,13 @@ _GATE = None
 
 class TorchCollective:
     """capsmi_collective_fn over torch.distributed (RCCL or, for rehearsals, gloo).  `device="cpu"`
-    takes host pointers (the gloo CPU tests of the exchange logic)."""
+    takes host pointers (the gloo CPU tests of the exchange logic).  One call of the library is one
+    torch.distributed call: libcapsmi itself cuts every collective to at most CAPSMI_COLL_CHUNK elements
+    (csrc/k_dist.hip collective / collective_a2av), so no adapter splits anything."""
 
-    def __init__(self, group=None, device: str = "cuda", chunk_elems: int | None = None):
-        import os
-
+    def __init__(self, group=None, device: str = "cuda"):
         import torch.distributed as dist
         self.dist = dist
-        # elements one collective call moves in all (CAPSMI_COLL_CHUNK): the C4 build's exchanges and
-        # all-gathers carry up to 2^28 words (2 GiB), which go out in calls of at most this many
-        self.chunk = max(1, int(chunk_elems or os.environ.get("CAPSMI_COLL_CHUNK", COLL_CHUNK_ELEMS)))
         self.group = group
         self.world = dist.get_world_size(group)
         self.device = device
@@ -131,7 +127,6 @@ class TorchCollective:
 
     def __call__(self, op: int, send: int, recv: int, count: int, dtype: int) -> None:
         import torch
-        dist = self.dist
         if self.drain:
             torch.cuda.current_stream().synchronize()
         gated = self.gate is not None and self.gate.t0 is not None
@@ -148,71 +143,28 @@ class TorchCollective:
         dist = self.dist
         W = self.world
         if op == _lib.COLL_ALL_GATHER:
-            out, inp = self.view(recv, count * W, dtype), self.view(send, count, dtype)
-            per = max(1, self.chunk // W)
-            if count <= per:
-                dist.all_gather_into_tensor(out, inp, group=self.group)
-            else:  # rank-major slices of at most `per` words per rank, placed into the rank-major output
-                o2 = out.view(W, count)
-                for off in range(0, count, per):
-                    c = min(per, count - off)
-                    tmp = torch.empty(W * c, dtype=out.dtype, device=out.device)
-                    dist.all_gather_into_tensor(tmp, inp[off:off + c], group=self.group)
-                    o2[:, off:off + c].copy_(tmp.view(W, c))
+            dist.all_gather_into_tensor(self.view(recv, count * W, dtype), self.view(send, count, dtype),
+                                        group=self.group)
         elif op in (_lib.COLL_ALL_REDUCE_SUM, _lib.COLL_ALL_REDUCE_MAX):
             r = self.view(recv, count, dtype)
             if send != recv:
                 r.copy_(self.view(send, count, dtype))
             rop = dist.ReduceOp.SUM if op == _lib.COLL_ALL_REDUCE_SUM else dist.ReduceOp.MAX
-            for off in range(0, max(count, 1), self.chunk):
-                dist.all_reduce(r[off:off + self.chunk], op=rop, group=self.group)
+            dist.all_reduce(r, op=rop, group=self.group)
         elif op == _lib.COLL_ALL_TO_ALL_V:
             assert count == W, (count, W)
             sd, sc, rd, rc = a2av_lists(send, recv, W)
             inp, out = self.view(sd, sum(sc), dtype), self.view(rd, sum(rc), dtype)
             if self.drain:  # gloo: host tensors
                 host = torch.empty(sum(rc), dtype=out.dtype)
-                self._a2av(host, inp.cpu(), sc, rc)
+                dist.all_to_all_single(host, inp.cpu(), output_split_sizes=rc, input_split_sizes=sc, group=self.group)
                 out.copy_(host)
             else:
-                self._a2av(out, inp, sc, rc)
+                dist.all_to_all_single(out, inp, output_split_sizes=rc, input_split_sizes=sc, group=self.group)
         else:
             raise ValueError(f"collective op {op}")
         if self.drain:
             torch.cuda.current_stream().synchronize()
-
-    def _a2av(self, dst, src, sc, rc) -> None:
-        """all_to_all_single in rounds of at most `chunk / world` words per (source, destination) pair; the
-        ranks agree on the number of rounds by one MAX all-reduce when any rank needs more than one."""
-        import torch
-        dist = self.dist
-        W = self.world
-        per = max(1, self.chunk // W)
-        local = max(1, -(-max(max(sc), max(rc)) // per))
-        rounds = local
-        if W > 1:
-            t = torch.tensor([local], dtype=torch.int64, device=src.device)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-            rounds = int(t.item())
-        if rounds == 1:
-            dist.all_to_all_single(dst, src, output_split_sizes=rc, input_split_sizes=sc, group=self.group)
-            return
-        so, ro = [0] * W, [0] * W
-        for q in range(1, W):
-            so[q] = so[q - 1] + sc[q - 1]
-            ro[q] = ro[q - 1] + rc[q - 1]
-        for k in range(rounds):
-            ss = [min(per, max(0, sc[q] - k * per)) for q in range(W)]
-            rr = [min(per, max(0, rc[q] - k * per)) for q in range(W)]
-            parts = [src[so[q] + k * per:so[q] + k * per + ss[q]] for q in range(W) if ss[q]]
-            tin = torch.cat(parts) if parts else src.new_empty(0)
-            tout = dst.new_empty(sum(rr))
-            dist.all_to_all_single(tout, tin, output_split_sizes=rr, input_split_sizes=ss, group=self.group)
-            pos = 0
-            for q in range(W):
-                if rr[q]:
-                    dst[ro[q] + k * per:ro[q] + k * per + rr[q]].copy_(tout[pos:pos + rr[q]])
-                    pos += rr[q]
 
 
 def join_ranks(session: Session, group=None) -> None:

@@ -290,9 +290,14 @@ std::shared_ptr<ListStore> collect_lists(capsmi_session* s, const int64_t* gid, 
 std::shared_ptr<ListStore> concat_lists(capsmi_session* s, const ListStore& a, const ListStore& b);
 // multi-GPU (k_dist.hip): the session's collective, stream-ordered (capsmi_collective_fn)
 void collective(capsmi_session* s, int op, const void* send, void* recv, int64_t count, int dtype);
-// ALL_TO_ALL_V with host count lists (world entries each)
+// calls of the host collective move at most coll_chunk() elements (CAPSMI_COLL_CHUNK); collective() and
+// collective_a2av() split larger ones
+int64_t coll_chunk();
+// ALL_TO_ALL_V with host count lists (world entries each); max_pair: the largest entry of the whole count
+// matrix (equal on every rank), which fixes the number of rounds
 void collective_a2av(capsmi_session* s, const void* send, const int64_t* send_counts, void* recv,
-                     const int64_t* recv_counts, int dtype);
+                     const int64_t* recv_counts, int dtype, int64_t max_pair);
+int64_t matrix_max(const std::vector<int64_t>& m);
 // hash Exchange of u64 words to rank dest[i] (low byte; 0xFF: not sent); dest / words are reordered
 // scratch; returns the received words (rank-major), *nrecv of them; synchronises
 Buf exchange_words(capsmi_session* s, uint64_t* dest, uint64_t* words, int64_t n, int64_t* nrecv);
@@ -444,16 +449,23 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
 uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts);
 
 // undirected Expand patterns (k_undirected.hip): hops 1 or 2; kind 0 count(*), 1 count(DISTINCT end),
-// 2 count(DISTINCT start); c unused for one hop
+// 2 count(DISTINCT start); c unused for one hop.  marks (kinds 1, 2; b's nwords words): the distinct ids'
+// bitmap is written there instead of counted (returns 0) -- a rank's partial marks of a distributed route
 int64_t undirected_count(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
                          int nt, int hops, const capsmi_bitmap* a, const capsmi_bitmap* b, const capsmi_bitmap* c,
-                         int kind);
+                         int kind, uint32_t* marks = nullptr);
 
 // the 2-hop chain grouped by its start (k_grouped.hip): rows (relative start id, count(*) or count(DISTINCT
 // end)); false when the distinct keys would exceed key_budget bytes
+// dd (a rank of a distributed graph, BY_SOURCE shards: sources owned, dense ids [rank * span, (rank + 1) *
+// span) owned): the rows of the owned starts, outC / the hop-2 lists exchanged between the ranks
+struct GroupedDist {
+    int rank = 0, world = 1;
+    int64_t span = 0;
+};
 bool grouped_two_hop(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
                      int nt, const capsmi_bitmap* a, const capsmi_bitmap* b, const capsmi_bitmap* c, bool distinct,
-                     int64_t key_budget, Buf& out_ids, Buf& out_vals, int64_t* rows);
+                     int64_t key_budget, Buf& out_ids, Buf& out_vals, int64_t* rows, const GroupedDist* dd = nullptr);
 
 // fused var-length grouped count (k_varlen.hip)
 int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,

@@ -176,17 +176,111 @@ __global__ void k_owned_flags(const int64_t* __restrict__ in, int64_t n, int64_t
 
 }  // namespace
 
-void collective(capsmi_session* s, int op, const void* send, void* recv, int64_t count, int dtype) {
+// Elements one call of the host's collective moves in all (CAPSMI_COLL_CHUNK, default 2^26: 512 MiB of
+// int64).  Every call the library makes is cut to this size here, so no host adapter (TorchCollective, the
+// JVM CollectiveFn) ever receives a larger one.  Round 4's C4 route at world size 1 faulted
+// (hipErrorIllegalAddress) in the first run that handed RCCL 2^28-word (2^31-byte) calls; the same build
+// equals its fixture with every call below 2^31 bytes.
+int64_t coll_chunk() {
+    static const int64_t c = [] {
+        const char* e = getenv("CAPSMI_COLL_CHUNK");
+        const long long v = e ? atoll(e) : 0;
+        return v > 0 ? (int64_t)v : (int64_t(1) << 26);
+    }();
+    return c;
+}
+
+namespace {
+size_t coll_elem_bytes(int dtype) { return dtype == CAPSMI_COLL_U32 ? 4 : 8; }
+
+void coll_call(capsmi_session* s, int op, const void* send, void* recv, int64_t count, int dtype) {
     REQUIRE(s->coll != nullptr, CAPSMI_ERR_ILLEGAL_ARGUMENT,
             "a distributed route needs the session's collective (capsmi_session_set_ranks)");
     const int32_t rc = s->coll(s->coll_ctx, op, send, recv, count, dtype);
     REQUIRE(rc == 0, CAPSMI_ERR_DEVICE, "the host collective failed (op " + std::to_string(op) + ")");
 }
+}  // namespace
 
+void collective(capsmi_session* s, int op, const void* send, void* recv, int64_t count, int dtype) {
+    REQUIRE(op != CAPSMI_COLL_ALL_TO_ALL_V, CAPSMI_ERR_INTERNAL, "ALL_TO_ALL_V goes through collective_a2av");
+    const int W = s->world > 0 ? s->world : 1;
+    const int64_t chunk = coll_chunk();
+    const size_t es = coll_elem_bytes(dtype);
+    if (op == CAPSMI_COLL_ALL_GATHER) {
+        const int64_t per = std::max<int64_t>(1, chunk / W);  // words per rank in one call
+        if (count <= per) {
+            coll_call(s, op, send, recv, count, dtype);
+            return;
+        }
+        // slices of `per` words per rank gathered into a staging buffer (rank-major W x c), then placed
+        // into the rank-major output (W x count) by one strided copy
+        Buf tmp = dev_alloc(es * (size_t)W * (size_t)per, s);
+        for (int64_t off = 0; off < count; off += per) {
+            const int64_t c = std::min(per, count - off);
+            coll_call(s, op, static_cast<const char*>(send) + es * off, P<void>(tmp), c, dtype);
+            HIP_CHECK(hipMemcpy2DAsync(static_cast<char*>(recv) + es * off, es * count, P<void>(tmp), es * c, es * c, W,
+                                       hipMemcpyDeviceToDevice, s->stream));
+        }
+        return;
+    }
+    if (count <= chunk) {
+        coll_call(s, op, send, recv, count, dtype);
+        return;
+    }
+    for (int64_t off = 0; off < count; off += chunk)  // all-reduces are element-wise: consecutive sub-ranges
+        coll_call(s, op, static_cast<const char*>(send) + es * off, static_cast<char*>(recv) + es * off,
+                  std::min(chunk, count - off), dtype);
+}
+
+// max_pair: the largest entry of the whole W x W count matrix (the same on every rank, which all-gathered
+// it): the ranks then agree on the number of rounds without a collective of their own
 void collective_a2av(capsmi_session* s, const void* send, const int64_t* send_counts, void* recv,
-                     const int64_t* recv_counts, int dtype) {
-    capsmi_coll_vec sv{const_cast<void*>(send), send_counts}, rv{recv, recv_counts};
-    collective(s, CAPSMI_COLL_ALL_TO_ALL_V, &sv, &rv, s->world, dtype);
+                     const int64_t* recv_counts, int dtype, int64_t max_pair) {
+    const int W = s->world;
+    const int64_t per = std::max<int64_t>(1, coll_chunk() / std::max(W, 1));  // words per (source, destination)
+    const int64_t rounds = std::max<int64_t>(1, (max_pair + per - 1) / per);
+    if (rounds == 1) {
+        capsmi_coll_vec sv{const_cast<void*>(send), send_counts}, rv{recv, recv_counts};
+        coll_call(s, CAPSMI_COLL_ALL_TO_ALL_V, &sv, &rv, W, dtype);
+        return;
+    }
+    // rounds of at most `per` words per pair: round k moves words [k * per, (k + 1) * per) of every segment,
+    // packed into / unpacked from staging buffers
+    const size_t es = coll_elem_bytes(dtype);
+    std::vector<int64_t> so(W + 1, 0), ro(W + 1, 0), ss(W), rr(W);
+    for (int q = 0; q < W; ++q) {
+        so[q + 1] = so[q] + send_counts[q];
+        ro[q + 1] = ro[q] + recv_counts[q];
+    }
+    Buf ts = dev_alloc(es * (size_t)W * (size_t)per, s), tr = dev_alloc(es * (size_t)W * (size_t)per, s);
+    const char* sb = static_cast<const char*>(send);
+    char* rb = static_cast<char*>(recv);
+    for (int64_t k = 0; k < rounds; ++k) {
+        int64_t at = 0;
+        for (int q = 0; q < W; ++q) {
+            ss[q] = std::min(per, std::max<int64_t>(0, send_counts[q] - k * per));
+            rr[q] = std::min(per, std::max<int64_t>(0, recv_counts[q] - k * per));
+            if (ss[q] > 0)
+                HIP_CHECK(hipMemcpyAsync(P<char>(ts) + es * at, sb + es * (so[q] + k * per), es * ss[q],
+                                         hipMemcpyDeviceToDevice, s->stream));
+            at += ss[q];
+        }
+        capsmi_coll_vec sv{P<void>(ts), ss.data()}, rv{P<void>(tr), rr.data()};
+        coll_call(s, CAPSMI_COLL_ALL_TO_ALL_V, &sv, &rv, W, dtype);
+        at = 0;
+        for (int q = 0; q < W; ++q) {
+            if (rr[q] > 0)
+                HIP_CHECK(hipMemcpyAsync(rb + es * (ro[q] + k * per), P<char>(tr) + es * at, es * rr[q],
+                                         hipMemcpyDeviceToDevice, s->stream));
+            at += rr[q];
+        }
+    }
+}
+
+int64_t matrix_max(const std::vector<int64_t>& m) {
+    int64_t x = 0;
+    for (int64_t v : m) x = std::max(x, v);
+    return x;
 }
 
 // The hash Exchange of u64 words (SparkTable.scala:133, 226 insert one before every join and grouping):
@@ -220,7 +314,7 @@ Buf exchange_words(capsmi_session* s, uint64_t* dest, uint64_t* words, int64_t n
         tot += rc[q];
     }
     Buf out = dev_alloc(sizeof(uint64_t) * (tot > 0 ? tot : 1), s);
-    collective_a2av(s, words, sc.data(), P<void>(out), rc.data(), CAPSMI_I64);
+    collective_a2av(s, words, sc.data(), P<void>(out), rc.data(), CAPSMI_I64, matrix_max(m));
     *nrecv = tot;
     return out;
 }
@@ -266,6 +360,22 @@ capsmi_table* new_table(capsmi_session* s, int64_t nrows) {
 }  // namespace
 
 namespace {
+// per column of t: whether any rank's rows carry a validity buffer (one MAX all-reduce of the flags)
+std::vector<bool> agreed_validity(capsmi_session* s, const capsmi_table* t) {
+    const size_t nc = t->cols.size();
+    std::vector<bool> out(nc, false);
+    if (nc == 0) return out;
+    std::vector<int64_t> h(nc);
+    for (size_t i = 0; i < nc; ++i) h[i] = t->cols[i].valid ? 1 : 0;
+    Buf f = dev_alloc(sizeof(int64_t) * nc, s);
+    HIP_CHECK(hipMemcpyAsync(P<int64_t>(f), h.data(), sizeof(int64_t) * nc, hipMemcpyHostToDevice, s->stream));
+    collective(s, CAPSMI_COLL_ALL_REDUCE_MAX, P<int64_t>(f), P<int64_t>(f), (int64_t)nc, CAPSMI_I64);
+    HIP_CHECK(hipMemcpyAsync(h.data(), P<int64_t>(f), sizeof(int64_t) * nc, hipMemcpyDeviceToHost, s->stream));
+    HIP_CHECK(hipStreamSynchronize(s->stream));
+    for (size_t i = 0; i < nc; ++i) out[i] = h[i] != 0;
+    return out;
+}
+
 // a list column of n rows over (lengths, values): row r holds list r (null rows: empty lists, valid 0)
 Column list_column(capsmi_session* s, const Column& like, const Buf& lens, int64_t n, const Buf& values,
                    int64_t nvalues, const Buf& valid) {
@@ -293,7 +403,11 @@ Column list_column(capsmi_session* s, const Column& like, const Buf& lens, int64
 capsmi_table* exchange_rows(capsmi_session* s, const capsmi_table* t, uint64_t* dest) {
     hipStream_t st = s->stream;
     const int W = s->world;
+    REQUIRE(W >= 1 && W < 255, CAPSMI_ERR_UNSUPPORTED, "exchange: at most 254 ranks");
     const int64_t n = t->nrows;
+    // validity buffers depend on the data (read_csv allocates one only where a rank's rows hold a null):
+    // the ranks agree on which columns carry one, so every rank issues the same collectives
+    const std::vector<bool> nullable = agreed_validity(s, t);
     Buf idx = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
     iota_i64(P<int64_t>(idx), 0, n, st);
     radix_sort_digits(s, dest, P<int64_t>(idx), n, {0});
@@ -304,6 +418,7 @@ capsmi_table* exchange_rows(capsmi_session* s, const capsmi_table* t, uint64_t* 
     HIP_CHECK(hipGetLastError());
     collective(s, CAPSMI_COLL_ALL_GATHER, mine, mine + W, W, CAPSMI_I64);
     std::vector<int64_t> mat((size_t)W * W);
+    int64_t mat_max = 0;
     HIP_CHECK(hipMemcpyAsync(mat.data(), mine + W, sizeof(int64_t) * mat.size(), hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
     std::vector<int64_t> sc(W), rc(W);
@@ -314,10 +429,12 @@ capsmi_table* exchange_rows(capsmi_session* s, const capsmi_table* t, uint64_t* 
         nsend += sc[q];
         nrecv += rc[q];
     }
+    mat_max = matrix_max(mat);
     auto* o = new_table(s, nrecv);
     Buf tmp = dev_alloc(sizeof(int64_t) * (nsend > 0 ? nsend : 1), s);
     Buf rs;  // list columns: the W + 1 starts of the destination segments of the ordered rows
-    for (const Column& c : t->cols) {
+    for (size_t ci = 0; ci < t->cols.size(); ++ci) {
+        const Column& c = t->cols[ci];
         if (is_list_type(c.type)) {  // lengths with the rows, then the values with per-rank value counts
             REQUIRE(c.list, CAPSMI_ERR_INTERNAL, "list column without a store");
             if (!rs) {
@@ -352,14 +469,14 @@ capsmi_table* exchange_rows(capsmi_session* s, const capsmi_table* t, uint64_t* 
                                    P<int64_t>(L.values), P<int64_t>(idx), nsend, P<int64_t>(voff), P<int64_t>(packed));
             HIP_CHECK(hipGetLastError());
             Buf rlens = dev_alloc(sizeof(int64_t) * (nrecv + 1), s), rvals = dev_alloc(sizeof(int64_t) * (vrecv > 0 ? vrecv : 1), s);
-            collective_a2av(s, P<int64_t>(lens), sc.data(), P<int64_t>(rlens), rc.data(), CAPSMI_I64);
-            collective_a2av(s, P<int64_t>(packed), vs.data(), P<int64_t>(rvals), vr.data(), CAPSMI_I64);
+            collective_a2av(s, P<int64_t>(lens), sc.data(), P<int64_t>(rlens), rc.data(), CAPSMI_I64, mat_max);
+            collective_a2av(s, P<int64_t>(packed), vs.data(), P<int64_t>(rvals), vr.data(), CAPSMI_I64, matrix_max(vm));
             Buf valid;
-            if (c.valid) {
+            if (nullable[ci]) {
                 Buf vw = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s), rw = dev_alloc(sizeof(int64_t) * (nrecv > 0 ? nrecv : 1), s);
                 if (n > 0) hipLaunchKernelGGL(k_valid_to_words, dim3(grid_for(n)), dim3(256), 0, st, c.v(), n, P<int64_t>(vw));
                 gather_col(P<int64_t>(vw), nullptr, P<int64_t>(idx), nsend, P<int64_t>(tmp), nullptr, st);
-                collective_a2av(s, P<int64_t>(tmp), sc.data(), P<int64_t>(rw), rc.data(), CAPSMI_I64);
+                collective_a2av(s, P<int64_t>(tmp), sc.data(), P<int64_t>(rw), rc.data(), CAPSMI_I64, mat_max);
                 valid = dev_alloc(nrecv > 0 ? nrecv : 1, s);
                 if (nrecv > 0)
                     hipLaunchKernelGGL(k_words_to_valid, dim3(grid_for(nrecv)), dim3(256), 0, st, P<int64_t>(rw), nrecv,
@@ -374,13 +491,13 @@ capsmi_table* exchange_rows(capsmi_session* s, const capsmi_table* t, uint64_t* 
         x.type = c.type;
         x.data = dev_alloc(sizeof(int64_t) * (nrecv > 0 ? nrecv : 1), s);
         gather_col(c.d(), nullptr, P<int64_t>(idx), nsend, P<int64_t>(tmp), nullptr, st);
-        collective_a2av(s, P<int64_t>(tmp), sc.data(), P<int64_t>(x.data), rc.data(), CAPSMI_I64);
-        if (c.valid) {
+        collective_a2av(s, P<int64_t>(tmp), sc.data(), P<int64_t>(x.data), rc.data(), CAPSMI_I64, mat_max);
+        if (nullable[ci]) {
             Buf vw = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s), rw = dev_alloc(sizeof(int64_t) * (nrecv > 0 ? nrecv : 1), s);
             if (n > 0)
                 hipLaunchKernelGGL(k_valid_to_words, dim3(grid_for(n)), dim3(256), 0, st, c.v(), n, P<int64_t>(vw));
             gather_col(P<int64_t>(vw), nullptr, P<int64_t>(idx), nsend, P<int64_t>(tmp), nullptr, st);
-            collective_a2av(s, P<int64_t>(tmp), sc.data(), P<int64_t>(rw), rc.data(), CAPSMI_I64);
+            collective_a2av(s, P<int64_t>(tmp), sc.data(), P<int64_t>(rw), rc.data(), CAPSMI_I64, mat_max);
             x.valid = dev_alloc(nrecv > 0 ? nrecv : 1, s);
             if (nrecv > 0)
                 hipLaunchKernelGGL(k_words_to_valid, dim3(grid_for(nrecv)), dim3(256), 0, st, P<int64_t>(rw), nrecv,
@@ -432,6 +549,7 @@ capsmi_table* slice_rows(capsmi_session* s, const capsmi_table* t) {
 capsmi_table* gather_rows(capsmi_session* s, const capsmi_table* t) {
     hipStream_t st = s->stream;
     const int64_t n = t->nrows;
+    const std::vector<bool> nullable = agreed_validity(s, t);  // the same collectives on every rank
     int64_t tot = 0;
     std::vector<std::pair<Buf, Buf>> cols;
     std::vector<std::pair<Buf, int64_t>> lvals(t->cols.size());  // list columns: gathered values
@@ -459,7 +577,7 @@ capsmi_table* gather_rows(capsmi_session* s, const capsmi_table* t) {
         } else {
             d = gather_words(s, reinterpret_cast<const uint64_t*>(c.d()), n, &tot);
         }
-        if (c.valid) {
+        if (nullable[ci]) {
             Buf vw = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
             if (n > 0) hipLaunchKernelGGL(k_valid_to_words, dim3(grid_for(n)), dim3(256), 0, st, c.v(), n, P<int64_t>(vw));
             HIP_CHECK(hipGetLastError());

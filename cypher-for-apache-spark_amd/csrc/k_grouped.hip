@@ -347,14 +347,23 @@ static int64_t gd_pairs(capsmi_session* s, const int64_t* S, const int64_t* T, i
 // count(DISTINCT c) per a by LDS sets over the deduplicated lists (above)
 static void grouped_distinct_sets(capsmi_session* s, const int64_t* S, const int64_t* T, int64_t m, int64_t lo,
                                   int64_t n, const capsmi_bitmap* a, const capsmi_bitmap* b, const capsmi_bitmap* c,
-                                  Buf& out_ids, Buf& out_vals, int64_t* rows) {
+                                  bool dist, Buf& out_ids, Buf& out_vals, int64_t* rows) {
     hipStream_t st = s->stream;
     KernelTimer kt(s, "grouped_distinct");
     Buf loops = dev_alloc(sizeof(unsigned int) * n, s);
     HIP_CHECK(hipMemsetAsync(P<void>(loops), 0, sizeof(unsigned int) * n, st));
     Buf k1, off1, k2, off2;
     gd_pairs(s, S, T, m, lo, n, a, b, P<unsigned int>(loops), k1, off1);
-    gd_pairs(s, S, T, m, lo, n, b, c, nullptr, k2, off2);
+    const int64_t ne2 = gd_pairs(s, S, T, m, lo, n, b, c, nullptr, k2, off2);
+    if (dist) {
+        // BY_SOURCE shards: this rank's deduplicated (b, y) keys are those of its owned b's, an id range that
+        // grows with the rank, so every rank's keys concatenated in rank order are the whole sorted key set:
+        // one all-gather, then the offsets over it (each rank walks the out2(b) of any b its a's reach)
+        int64_t tot = 0;
+        k2 = gather_words(s, P<uint64_t>(k2), ne2, &tot);
+        hipLaunchKernelGGL(k_gd_off, dim3(grid_for(n + 1)), dim3(256), 0, st, P<uint64_t>(k2), tot, n, P<int64_t>(off2));
+        HIP_CHECK(hipGetLastError());
+    }
     Buf w = dev_alloc(sizeof(int64_t) * n, s), cnt = dev_alloc(sizeof(int64_t) * n, s);
     HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, sizeof(int64_t) * n, st));
     hipLaunchKernelGGL(k_gd_work, dim3(grid_for(n * 64, 256)), dim3(256), 0, st, P<uint64_t>(k1), P<int64_t>(off1),
@@ -392,7 +401,7 @@ static void grouped_distinct_sets(capsmi_session* s, const int64_t* S, const int
 // Returns false (nothing produced) when the count(DISTINCT c) keys would not fit `key_budget` bytes.
 bool grouped_two_hop(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
                      int nt, const capsmi_bitmap* a, const capsmi_bitmap* b, const capsmi_bitmap* c, bool distinct,
-                     int64_t key_budget, Buf& out_ids, Buf& out_vals, int64_t* rows) {
+                     int64_t key_budget, Buf& out_ids, Buf& out_vals, int64_t* rows, const GroupedDist* dd) {
     REQUIRE(a->lo == b->lo && a->hi == b->hi && c->lo == b->lo && c->hi == b->hi, CAPSMI_ERR_ILLEGAL_ARGUMENT,
             "grouped 2-hop: the node bitmaps must share one id domain");
     const int64_t lo = b->lo, n = b->hi - b->lo;
@@ -417,6 +426,15 @@ bool grouped_two_hop(capsmi_session* s, const int64_t* const* srcs, const int64_
     if (m) hipLaunchKernelGGL(k_g_lists, dim3(grid_for(m)), dim3(256), 0, st, P<int64_t>(S), P<int64_t>(T), m, lo, n,
                               bits_of(b), bits_of(c), P<uint64_t>(lkey), P<int64_t>(lval), P<unsigned long long>(outc));
     HIP_CHECK(hipGetLastError());
+    if (dd && !distinct) {
+        // BY_SOURCE shards: outC(b) is complete for the owned b's (their out-relationships are all here); one
+        // all-gather of the owned slices gives every rank outC of every id
+        REQUIRE(dd->span * dd->world == n, CAPSMI_ERR_INTERNAL, "grouped 2-hop: distributed domain geometry");
+        Buf full = dev_alloc(sizeof(unsigned long long) * n, s);
+        collective(s, CAPSMI_COLL_ALL_GATHER, P<unsigned long long>(outc) + dd->rank * dd->span, P<void>(full), dd->span,
+                   CAPSMI_I64);
+        outc = full;
+    }
     if (!distinct) {
         Buf per_a = dev_alloc(sizeof(unsigned long long) * n, s);
         HIP_CHECK(hipMemsetAsync(P<void>(per_a), 0, sizeof(unsigned long long) * n, st));
@@ -436,8 +454,8 @@ bool grouped_two_hop(capsmi_session* s, const int64_t* const* srcs, const int64_
         return true;
     }
     const char* ge = getenv("CAPSMI_GROUPED");  // "keys": the per-binding key sort below (A/B; bounded by memory)
-    if (!(ge && std::string(ge) == "keys")) {
-        grouped_distinct_sets(s, P<int64_t>(S), P<int64_t>(T), m, lo, n, a, b, c, out_ids, out_vals, rows);
+    if (dd || !(ge && std::string(ge) == "keys")) {
+        grouped_distinct_sets(s, P<int64_t>(S), P<int64_t>(T), m, lo, n, a, b, c, dd != nullptr, out_ids, out_vals, rows);
         return true;
     }
     // bindings per r1 and their key offsets

@@ -1120,6 +1120,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     const int bits = bits_for((uint64_t)n);
     REQUIRE(!dd || (bits + 7) / 8 * 8 <= 24, CAPSMI_ERR_UNSUPPORTED,
             "distributed triangle count: at most 2^24 ids (coded oriented keys)");
+    REQUIRE(!dd || dd->world < 255, CAPSMI_ERR_UNSUPPORTED, "distributed triangle count: at most 254 ranks (exchanges)");
     int64_t m_all = m;  // every rank's relationships (bounds the out-degrees below)
     if (dd) {
         Buf t = dev_alloc(sizeof(int64_t), s);
@@ -1411,7 +1412,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
             HIP_CHECK(hipMemcpyAsync(out.data(), P<int64_t>(cut), sizeof(int64_t) * (W + 1), hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
         };
-        REQUIRE(dd->world <= 255, CAPSMI_ERR_UNSUPPORTED, "distributed triangle count: at most 255 ranks");
+        REQUIRE(dd->world < 255, CAPSMI_ERR_UNSUPPORTED, "distributed triangle count: at most 254 ranks");
         g.wparts = dd->world;
         work(g.big_u, g.nbig, false, false, g.wbig);
         if (g.vm_own) {  // every v-mode center of this build is this rank's

@@ -156,7 +156,7 @@ Bits bits_of(const capsmi_bitmap* b) { return Bits{P<uint32_t>(b->words), b->ful
 
 int64_t undirected_count(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
                          int nt, int hops, const capsmi_bitmap* a, const capsmi_bitmap* b, const capsmi_bitmap* c,
-                         int kind) {
+                         int kind, uint32_t* marks) {
     REQUIRE(hops == 1 || hops == 2, CAPSMI_ERR_INTERNAL, "undirected hops");
     REQUIRE(a->lo == b->lo && a->hi == b->hi && (!c || (c->lo == b->lo && c->hi == b->hi)), CAPSMI_ERR_ILLEGAL_ARGUMENT,
             "undirected patterns: the node bitmaps must share one id domain");
@@ -179,14 +179,19 @@ int64_t undirected_count(capsmi_session* s, const int64_t* const* srcs, const in
         return (int64_t)h[1];
     }
     if (hops == 1) {  // count(DISTINCT end | start)
-        Buf M = dev_alloc(sizeof(uint32_t) * nw, s);
-        HIP_CHECK(hipMemsetAsync(P<void>(M), 0, sizeof(uint32_t) * nw, st));
+        Buf own;
+        uint32_t* M = marks;
+        if (!M) {
+            own = dev_alloc(sizeof(uint32_t) * nw, s);
+            M = P<uint32_t>(own);
+        }
+        HIP_CHECK(hipMemsetAsync(M, 0, sizeof(uint32_t) * nw, st));
         for (int i = 0; i < nt; ++i)
             if (ms[i] > 0)
                 hipLaunchKernelGGL(k_und_mark1, dim3(grid_for(ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], lo, n,
-                                   bits_of(a), bits_of(b), kind == 2 ? 1 : 0, P<uint32_t>(M));
+                                   bits_of(a), bits_of(b), kind == 2 ? 1 : 0, M);
         HIP_CHECK(hipGetLastError());
-        return words_popcount(s, P<uint32_t>(M), 0, nw);
+        return marks ? 0 : words_popcount(s, M, 0, nw);
     }
     const char* ce = getenv("CAPSMI_COUNT");  // "atomic": the per-relationship atomic degrees below (A/B)
     if (kind == 0 && n <= (int64_t(1) << 26) && !(ce && std::string(ce) == "atomic")) {
@@ -221,6 +226,10 @@ int64_t undirected_count(capsmi_session* s, const int64_t* const* srcs, const in
     Buf bm = dev_alloc(sizeof(uint32_t) * 3 * nw, s), xb = dev_alloc(sizeof(uint32_t) * n, s);
     HIP_CHECK(hipMemsetAsync(P<void>(bm), 0, sizeof(uint32_t) * 3 * nw, st));
     uint32_t *B1 = P<uint32_t>(bm), *B2 = B1 + nw, *C = B2 + nw;
+    if (marks) {  // the caller's end bitmap (a rank's partial marks, ORed over the ranks by the caller)
+        C = marks;
+        HIP_CHECK(hipMemsetAsync(C, 0, sizeof(uint32_t) * nw, st));
+    }
     for (int i = 0; i < nt; ++i)
         if (ms[i] > 0)
             hipLaunchKernelGGL(k_und_hop1, dim3(grid_for(ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], lo, n,
@@ -230,7 +239,7 @@ int64_t undirected_count(capsmi_session* s, const int64_t* const* srcs, const in
             hipLaunchKernelGGL(k_und_hop2, dim3(grid_for(ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], lo, n,
                                bits_of(Cc), B1, B2, P<uint32_t>(xb), C);
     HIP_CHECK(hipGetLastError());
-    return words_popcount(s, C, 0, nw);
+    return marks ? 0 : words_popcount(s, C, 0, nw);
 }
 
 }  // namespace capsmi

@@ -853,6 +853,21 @@ void rel_views(const Path& P, const Hop& h, RelViews& v) {
     for (auto& k : sig) v.sig += k;
 }
 
+// the same relationship views read backwards: (s, t) <- (t, s), zero-copy
+void reversed_views(const RelViews& v, RelViews& r) {
+    for (capsmi_table* x : v.t) {
+        auto* y = new capsmi_table();
+        y->sess = x->sess;
+        y->nrows = x->nrows;
+        Column a = x->cols[1], b = x->cols[0];
+        a.name = "s";
+        b.name = "t";
+        y->cols = {a, b};
+        r.t.push_back(y);
+    }
+    r.sig = v.sig + "~";
+}
+
 bool id_like(const Path& P, const Role& r) {  // a non-null id / endpoint column
     if (r.k == RK_NODE) return P.inst[r.inst].role[r.scol] == ROLE_ID;
     if (r.k == RK_REL) return P.inst[r.inst].role[r.scol] != ROLE_NONE;
@@ -932,6 +947,12 @@ bool any_no_loops(const Path& P) {  // an undirected branch: only fused_undirect
 }
 thread_local bool g_missed = false;  // a pattern shape went unrouted during the current materialisation
 
+int bits_for_ids(int64_t n) {  // bits of the largest relative id (k_tri.hip bits_for)
+    int b = 1;
+    while (b < 63 && (int64_t(1) << b) < n) ++b;
+    return b;
+}
+
 int64_t sum_over_ranks(capsmi_session* s, int64_t v) {
     Buf t = dev_alloc(sizeof(int64_t), s);
     fill_i64(P<int64_t>(t), v, 1, s->stream);
@@ -981,6 +1002,92 @@ int64_t dist_two_hop_distinct(capsmi_session* s, const capsmi_relpart* cached, i
     check(capsmi_words_popcount_device(s, P<uint32_t>(dst), r * S, (r + 1) * S, P<int64_t>(cnt)));
     collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(cnt), P<int64_t>(cnt), 1, CAPSMI_I64);
     return read_scalar(s, P<int64_t>(cnt));
+}
+
+// [X1 | X2] (2 x W x S words) -> rank-major send segments [q][X1 slice q | X2 slice q] (2 x S each)
+__global__ void k_x12_by_owner(const uint32_t* __restrict__ mid, int64_t nw, int64_t S, int W, uint32_t* __restrict__ send) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * nw; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t q = i / (2 * S), h = (i / S) & 1, k = i % S;
+        send[i] = mid[h * nw + q * S + k];
+    }
+}
+// OR of the W received [X1 | X2] slice pairs (got = [source rank][2][S]) into this rank's slices of full
+// [X1 | X2] (words outside them zero: hop 2 reads X only at the owned sources of this rank's relationships)
+__global__ void k_x12_or(const uint32_t* __restrict__ got, int W, int64_t nw, int64_t S, int64_t r,
+                         uint32_t* __restrict__ full) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 2 * S; i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t v = 0;
+        for (int q = 0; q < W; ++q) v |= got[(int64_t)q * 2 * S + i];
+        const int64_t h = i / S, k = i % S;
+        full[h * nw + r * S + k] = v;
+    }
+}
+// popcount of the OR of W received slices of S words (got = [source rank][S]) added into *cnt
+__global__ void k_or_popcount(const uint32_t* __restrict__ got, int W, int64_t S, unsigned long long* __restrict__ cnt) {
+    unsigned long long c = 0;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < S; k += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t v = 0;
+        for (int q = 0; q < W; ++q) v |= got[(int64_t)q * S + k];
+        c += __popc(v);
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
+}
+
+unsigned small_grid(capsmi_session* s, int64_t n) {
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, (int64_t)s->num_cus * 8));
+}
+
+// The union of every rank's partial bitmap `words` (W x S words, rank-major slices) counted: one equal-count
+// ALL_TO_ALL_V gives each rank every rank's copy of its owned slice, ORed and popcounted on the device, and
+// one all-reduce adds the owned counts -- the reduce-scatter(OR) + popcount of SURVEY.md 8e (bitwise OR is
+// not an RCCL reduction).  Returns the count (the step's one host read).
+int64_t or_reduce_count(capsmi_session* s, const uint32_t* words) {
+    const int64_t S = g_dist.slice_words;
+    const int W = g_dist.world;
+    Buf got = dev_alloc(sizeof(uint32_t) * (size_t)W * S, s), cnt = dev_alloc(sizeof(int64_t), s);
+    std::vector<int64_t> c(W, S);
+    collective_a2av(s, words, c.data(), P<void>(got), c.data(), CAPSMI_COLL_U32, S);
+    HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, sizeof(int64_t), s->stream));
+    hipLaunchKernelGGL(k_or_popcount, dim3(small_grid(s, S)), dim3(256), 0, s->stream, P<uint32_t>(got), W, S,
+                       P<unsigned long long>(cnt));
+    HIP_CHECK(hipGetLastError());
+    collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(cnt), P<int64_t>(cnt), 1, CAPSMI_I64);
+    return read_scalar(s, P<int64_t>(cnt));
+}
+
+// 2-hop count(DISTINCT end) over relationship shards BY_SOURCE (north_star's owner(source)):
+// hop 1 over this rank's relationships (sources owned, middles anywhere) marks a partial frontier
+// X1 = M | S1, X2 = M | S2 for every id -- S1 / S2 (self-loops) are complete on the owner, and M is an OR
+// over the ranks; one ALL_TO_ALL_V of the slices + OR gives each rank the whole frontier of its owned
+// middles, which are exactly the sources of its hop-2 relationships; hop 2 marks ends anywhere, and the
+// OR-reduce + popcount of the end bitmap gives the answer (or_reduce_count).
+int64_t dist_two_hop_distinct_src(capsmi_session* s, const capsmi_relpart* cached, int32_t nt, capsmi_table* const* views,
+                                  const capsmi_bitmap* a, const capsmi_bitmap* b, const capsmi_bitmap* c) {
+    const int64_t S = g_dist.slice_words, nw = b->nwords, r = g_dist.rank;
+    const int W = g_dist.world;
+    REQUIRE(nw == S * W, CAPSMI_ERR_INTERNAL, "distributed bitmap geometry");
+    Buf mid = dev_alloc(sizeof(uint32_t) * 2 * nw, s), scratch = dev_alloc(sizeof(uint32_t) * nw, s);
+    Buf full = dev_alloc(sizeof(uint32_t) * 2 * nw, s), dst = dev_alloc(sizeof(uint32_t) * nw, s);
+    capsmi_relpart* rp = nullptr;
+    if (cached) check(capsmi_two_hop_mark_mid_part(s, cached, a, b, P<uint32_t>(mid), P<uint32_t>(scratch)));
+    else check(capsmi_relpart_build_mark_mid(s, nt, views, "s", "t", a, b, P<uint32_t>(mid), P<uint32_t>(scratch), &rp));
+    std::unique_ptr<capsmi_relpart, capsmi_status (*)(capsmi_relpart*)> hold(rp, capsmi_relpart_release);
+    {
+        Buf x12 = dev_alloc(sizeof(uint32_t) * 4 * nw, s);
+        uint32_t *send = P<uint32_t>(x12), *got = send + 2 * nw;
+        hipLaunchKernelGGL(k_x12_by_owner, dim3(small_grid(s, 2 * nw)), dim3(256), 0, s->stream, P<uint32_t>(mid), nw, S,
+                           W, send);
+        HIP_CHECK(hipGetLastError());
+        std::vector<int64_t> cnt(W, 2 * S);
+        collective_a2av(s, send, cnt.data(), got, cnt.data(), CAPSMI_COLL_U32, 2 * S);
+        HIP_CHECK(hipMemsetAsync(P<void>(full), 0, sizeof(uint32_t) * 2 * nw, s->stream));
+        hipLaunchKernelGGL(k_x12_or, dim3(small_grid(s, 2 * S)), dim3(256), 0, s->stream, got, W, nw, S, r,
+                           P<uint32_t>(full));
+        HIP_CHECK(hipGetLastError());
+    }
+    check(capsmi_two_hop_mark_dst_part(s, cached ? cached : rp, b, c, P<uint32_t>(full), P<uint32_t>(dst)));
+    return or_reduce_count(s, P<uint32_t>(dst));
 }
 
 // 2-hop count(*) over relationship shards BY_TARGET: each rank's relationships into its owned ids give
@@ -1059,11 +1166,9 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
         RelViews v1;
         rel_views(P, P.hops[1], v1);
         if (v1.sig != v0.sig || !all_pairs_unique(c, 2)) return false;
-        if (g_dist.on) {  // over relationship shards BY_TARGET: count(*) and count(DISTINCT end)
-            if (g_dist.rel_mode != CAPSMI_RELS_BY_TARGET) return false;
+        if (g_dist.on)  // the distributed count(*) folds in-degrees of at most 2^26 ids (k_count.hip)
             for (int k : kinds)
-                if (k == A_DISTINCT_START || (k == A_COUNT && hi - lo > (int64_t(1) << 26))) return false;
-        }
+                if (k == A_COUNT && hi - lo > (int64_t(1) << 26)) return false;
         capsmi_bitmap* a = node_bitmap(s, P, c, P.pos_node[0], lo, hi, bs);
         capsmi_bitmap* b = node_bitmap(s, P, c, P.pos_node[1], lo, hi, bs);
         capsmi_bitmap* cc = node_bitmap(s, P, c, P.pos_node[2], lo, hi, bs);
@@ -1072,32 +1177,47 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
         const Scan& R = P.inst[P.hops[0].rel];
         bool keep = !R.m.empty();
         for (const Member& m : R.m) keep = keep && m.base->keep_layouts;
+        // the reversed relationships (distinct start = distinct end of the reversed walk; and over BY_SOURCE
+        // shards the count(*) runs as the BY_TARGET count of the reversed graph)
+        RelViews rv;
+        reversed_views(v0, rv);
+        const bool by_tgt = g_dist.rel_mode == CAPSMI_RELS_BY_TARGET;
         for (int k : kinds) {
             int64_t x = 0;
-            if (g_dist.on && k == A_COUNT) {
-                x = dist_two_hop_count(s, (int32_t)nt, v0.t.data(), a, b, cc);
-            } else if (g_dist.on && !keep) {
-                x = dist_two_hop_distinct(s, nullptr, (int32_t)nt, v0.t.data(), a, b, cc);
-            } else if (k == A_COUNT) {
-                check(capsmi_two_hop_count(s, (int32_t)nt, v0.t.data(), "s", "t", a, b, cc, &x));
-            } else if (keep) {
-                const bool rev = k == A_DISTINCT_START;  // distinct start = distinct end of the reversed walk
+            const bool rev = k == A_DISTINCT_START;
+            capsmi_table* const* vw = rev ? rv.t.data() : v0.t.data();
+            const capsmi_bitmap* A = rev ? cc : a;
+            const capsmi_bitmap* C = rev ? a : cc;
+            const capsmi_relpart* lay = nullptr;
+            if (keep && k != A_COUNT) {
                 const std::string key = v0.sig + (rev ? "<" : ">") + std::to_string(lo) + ":" + std::to_string(hi);
                 auto& cache = R.m[0].base->layouts;
                 auto it = cache.find(key);
                 if (it == cache.end()) {
                     capsmi_relpart* rp = nullptr;
-                    check(capsmi_relpart_build(s, (int32_t)nt, v0.t.data(), rev ? "t" : "s", rev ? "s" : "t", lo, hi, &rp));
+                    check(capsmi_relpart_build(s, (int32_t)nt, vw, "s", "t", lo, hi, &rp));
                     it = cache.emplace(key, std::shared_ptr<capsmi_relpart>(rp, [](capsmi_relpart* q) {
                                            capsmi_relpart_release(q);
                                        })).first;
                 }
-                if (g_dist.on) x = dist_two_hop_distinct(s, it->second.get(), 0, nullptr, a, b, cc);
-                else check(capsmi_two_hop_count_distinct_part(s, it->second.get(), rev ? cc : a, b, rev ? a : cc, &x));
-            } else if (k == A_DISTINCT_END) {
-                check(capsmi_two_hop_count_distinct(s, (int32_t)nt, v0.t.data(), "s", "t", a, b, cc, &x));
-            } else {  // distinct start: the same walk over the reversed relationships
-                check(capsmi_two_hop_count_distinct(s, (int32_t)nt, v0.t.data(), "t", "s", cc, b, a, &x));
+                lay = it->second.get();
+            }
+            if (g_dist.on && k == A_COUNT) {
+                // every relationship into an owned id (BY_TARGET), or out of one (BY_SOURCE: the reversed graph)
+                x = by_tgt ? dist_two_hop_count(s, (int32_t)nt, v0.t.data(), a, b, cc)
+                           : dist_two_hop_count(s, (int32_t)nt, rv.t.data(), cc, b, a);
+            } else if (g_dist.on) {
+                // the walk's relationships arrive by their end's owner (BY_TARGET forwards, BY_SOURCE reversed):
+                // the all-gather form; by their start's owner: the OR-reduce form
+                const bool end_owned = by_tgt != rev;
+                x = end_owned ? dist_two_hop_distinct(s, lay, lay ? 0 : (int32_t)nt, lay ? nullptr : vw, A, b, C)
+                              : dist_two_hop_distinct_src(s, lay, lay ? 0 : (int32_t)nt, lay ? nullptr : vw, A, b, C);
+            } else if (k == A_COUNT) {
+                check(capsmi_two_hop_count(s, (int32_t)nt, v0.t.data(), "s", "t", a, b, cc, &x));
+            } else if (lay) {
+                check(capsmi_two_hop_count_distinct_part(s, lay, A, b, C, &x));
+            } else {
+                check(capsmi_two_hop_count_distinct(s, (int32_t)nt, vw, "s", "t", A, b, C, &x));
             }
             vals.push_back(x);
         }
@@ -1118,6 +1238,8 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
         capsmi_bitmap* b = node_bitmap(s, P, c, P.pos_node[1], lo, hi, bs, &k1);
         capsmi_bitmap* cc = node_bitmap(s, P, c, P.pos_node[2], lo, hi, bs, &k2);
         if (!a || !b || !cc || k0 != k1 || k1 != k2) return false;  // one node filter for all three
+        // the distributed build codes oriented targets in 24 bits: larger domains take the generic plan
+        if (g_dist.on && (bits_for_ids(hi - lo) + 7) / 8 * 8 > 24) return false;
         int64_t x = 0;
         if (g_dist.on) x = dist_triangle_count(s, v0.t, a);
         else check(capsmi_triangle_count(s, (int32_t)nt, v0.t.data(), "s", "t", a, &x));
@@ -1126,6 +1248,57 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
         return true;
     }
     return false;
+}
+
+// a copy of bitmap b restricted to this rank's owned ids (whole word slices [rank * S, (rank + 1) * S))
+std::unique_ptr<capsmi_bitmap> owned_mask(capsmi_session* s, const capsmi_bitmap* b) {
+    const int64_t S = g_dist.slice_words, r = g_dist.rank;
+    REQUIRE(b->nwords == S * g_dist.world, CAPSMI_ERR_INTERNAL, "distributed bitmap geometry");
+    auto m = std::make_unique<capsmi_bitmap>();
+    m->sess = s;
+    m->lo = b->lo;
+    m->hi = b->hi;
+    m->nwords = b->nwords;
+    m->words = dev_alloc(sizeof(uint32_t) * (size_t)b->nwords, s);
+    m->any_dup = b->any_dup;
+    HIP_CHECK(hipMemsetAsync(P<void>(m->words), 0, sizeof(uint32_t) * (size_t)b->nwords, s->stream));
+    HIP_CHECK(hipMemcpyAsync(P<uint32_t>(m->words) + r * S, P<uint32_t>(b->words) + r * S, sizeof(uint32_t) * S,
+                             hipMemcpyDeviceToDevice, s->stream));
+    return m;
+}
+
+// The undirected 1- / 2-hop routes over BY_SOURCE shards.  A rank's relationships (sources owned) hold each
+// relationship once over the ranks; with its in-relationships (targets owned, exchanged at registration)
+// they are every relationship incident to an owned id.
+//   1 hop: the arcs of the rank's own relationships: count(*) summed, distinct ends ORed over the ranks;
+//   2 hops: the middle b restricted to owned ids, over every relationship incident to them, so inU(b),
+//   outU(b), K(b) and x(b) are complete: count(*) summed, the distinct ends ORed (or_reduce_count).
+void dist_undirected(capsmi_session* s, const Scan& R, const std::vector<const int64_t*>& srcs,
+                     const std::vector<const int64_t*>& dsts, const std::vector<int64_t>& ms, int h,
+                     const std::vector<capsmi_bitmap*>& pos, const std::vector<int>& kinds, std::vector<int64_t>& vals) {
+    std::vector<const int64_t*> as = srcs, ad = dsts;  // + the in-relationships
+    std::vector<int64_t> am = ms;
+    for (const Member& m : R.m) {
+        if (m.base->in_rows <= 0) continue;
+        as.push_back(m.base->in_src.d());
+        ad.push_back(m.base->in_dst.d());
+        am.push_back(m.base->in_rows);
+    }
+    std::unique_ptr<capsmi_bitmap> bown;
+    if (h == 2) bown = owned_mask(s, pos[1]);
+    Buf marks = dev_alloc(sizeof(uint32_t) * (size_t)pos[0]->nwords, s);
+    for (int k : kinds) {
+        const int kind = k == A_COUNT ? 0 : (k == A_DISTINCT_END ? 1 : 2);
+        int64_t x;
+        if (h == 1) {
+            x = undirected_count(s, srcs.data(), dsts.data(), ms.data(), (int)srcs.size(), 1, pos[0], pos[1], pos[1], kind,
+                                 kind ? P<uint32_t>(marks) : nullptr);
+        } else {
+            x = undirected_count(s, as.data(), ad.data(), am.data(), (int)as.size(), 2, pos[0], bown.get(), pos[2], kind,
+                                 kind ? P<uint32_t>(marks) : nullptr);
+        }
+        vals.push_back(kind ? or_reduce_count(s, P<uint32_t>(marks)) : sum_over_ranks(s, x));
+    }
 }
 
 // Undirected Expand chains of 1 or 2 hops (RelationalPlanner.scala:126-136): 2^hops branches, one per
@@ -1158,7 +1331,9 @@ bool fused_undirected(capsmi_session* s, const capsmi_table* in, const PlanNode&
     }
     if (orients.size() != B.size()) return false;
     int64_t lo, hi;
-    if (!id_window(B, &lo, &hi) || g_dist.on) return false;  // no distributed form (yet)
+    if (!id_window(B, &lo, &hi)) return false;
+    // distributed: BY_SOURCE shards, whose in-relationships complete every owned id's incident set
+    if (g_dist.on && g_dist.rel_mode != CAPSMI_RELS_BY_SOURCE) return false;
     // one relationship set for every hop of every branch, read as (start, end)
     auto plain_views = [&](const Path& P, const Hop& hp, RelViews& v) {
         Hop fwd = hp;
@@ -1192,6 +1367,11 @@ bool fused_undirected(capsmi_session* s, const capsmi_table* in, const PlanNode&
         srcs.push_back(t->cols[0].d());
         dsts.push_back(t->cols[1].d());
         ms.push_back(t->nrows);
+    }
+    if (g_dist.on) {
+        dist_undirected(s, B[0].inst[B[0].hops[0].rel], srcs, dsts, ms, (int)h, pos, kinds, vals);
+        route(s, "undirected");
+        return true;
     }
     for (int k : kinds) {
         const int kind = k == A_COUNT ? 0 : (k == A_DISTINCT_END ? 1 : 2);
@@ -1236,7 +1416,8 @@ bool fused_grouped_two_hop(capsmi_session* s, const capsmi_table* in, const Plan
     if (v0.sig != v1.sig) return false;
     std::vector<Path> one{P};
     int64_t lo, hi;
-    if (!id_window(one, &lo, &hi) || g_dist.on) return false;
+    if (!id_window(one, &lo, &hi)) return false;
+    if (g_dist.on && g_dist.rel_mode != CAPSMI_RELS_BY_SOURCE) return false;  // the rows of owned starts
     BitmapSet bs;
     capsmi_bitmap* a = node_bitmap(s, P, c, P.pos_node[0], lo, hi, bs);
     capsmi_bitmap* b = node_bitmap(s, P, c, P.pos_node[1], lo, hi, bs);
@@ -1257,8 +1438,12 @@ bool fused_grouped_two_hop(capsmi_session* s, const capsmi_table* in, const Plan
     for (size_t i = 0; i < kinds.size(); ++i) {
         Buf ids, vals;
         int64_t nrow = 0;
+        GroupedDist gd;
+        gd.rank = g_dist.rank;
+        gd.world = g_dist.world;
+        gd.span = 32 * g_dist.slice_words;
         if (!grouped_two_hop(s, srcs.data(), dsts.data(), ms.data(), (int)srcs.size(), a, b, cc, kinds[i] != A_COUNT,
-                             (int64_t)(free_b / 2), ids, vals, &nrow))
+                             (int64_t)(free_b / 2), ids, vals, &nrow, g_dist.on ? &gd : nullptr))
             return false;  // the keys would not fit: the generic plan (and its size guard) decides
         REQUIRE(rows < 0 || rows == nrow, CAPSMI_ERR_INTERNAL, "grouped 2-hop: aggregates disagree on the groups");
         if (i == 0) {
@@ -1275,6 +1460,7 @@ bool fused_grouped_two_hop(capsmi_session* s, const capsmi_table* in, const Plan
         r->cols.push_back(std::move(v));
     }
     r->nrows = rows;
+    r->partitioned = g_dist.on && g_dist.world > 1;  // the rows of this rank's owned start nodes
     *out = guard.release();
     route(s, "two_hop_grouped");
     return true;

@@ -77,12 +77,29 @@ def main():
         except _lib.UnsupportedOperationException as e:
             return "refused: " + str(e)[:120]
 
-    if "c3" in queries:
-        if args.rels_by == "target":
-            out["count_star"] = run([["n", ["count*"]]])[0]["n"]
-            out["count_distinct_c"] = run([["n", ["count_distinct", ["id", "c"]]]])[0]["n"]
-        else:  # the 2-hop routes need BY_TARGET shards: refused, not run on one rank's rows
-            out["c3"] = refused(lambda: run([["n", ["count_distinct", ["id", "c"]]]]))
+    if "c3" in queries:  # either mode: all-gather (end's owner holds the walk) or OR-reduce (start's owner) forms
+        out["count_star"] = run([["n", ["count*"]]])[0]["n"]
+        out["count_distinct_c"] = run([["n", ["count_distinct", ["id", "c"]]]])[0]["n"]
+        out["count_distinct_a"] = run([["n", ["count_distinct", ["id", "a"]]]])[0]["n"]
+    if "und" in queries:  # undirected 1 / 2 hops: BY_SOURCE shards + their in-relationships
+        if args.rels_by == "source":
+            u1 = run([["n", ["count*"]], ["d", ["count_distinct", ["id", "b"]]]], "(a:V)-[:E]-(b:V)")[0]
+            u2 = run([["n", ["count*"]], ["dc", ["count_distinct", ["id", "c"]]], ["da", ["count_distinct", ["id", "a"]]]],
+                     "(a:V)-[:E]-(b:V)-[:E]-(c:V)")[0]
+            out["und1"] = [u1["n"], u1["d"]]
+            out["und2"] = [u2["n"], u2["dc"], u2["da"]]
+        else:
+            out["und"] = refused(lambda: run([["n", ["count*"]]], "(a:V)-[:E]-(b:V)-[:E]-(c:V)"))
+    if "grouped" in queries:  # RETURN id(a), count(*) / count(DISTINCT c): the rows of this rank's owned starts
+        if args.rels_by == "source":
+            t, outs = Planner(sg).run({"clauses": [{"match": C3}],
+                                       "return": {"items": [["a", ["id", "a"]], ["dc", ["count_distinct", ["id", "c"]]],
+                                                            ["n", ["count*"]]]}})
+            rows = result_rows(t, outs, s.dictionary)
+            out["grouped_rows"] = [[r["a"], r["dc"], r["n"]] for r in rows]
+            out["grouped_partitioned"] = t.partitioned
+        else:
+            out["grouped"] = refused(lambda: run([["a", ["id", "a"]], ["n", ["count*"]]]))
     if "expand" in queries:
         out["expand_count"] = run([["n", ["count*"]]], "(a:V)-[:E]->(b:V)")[0]["n"]
         # rows of this rank's relationships (partitioned result)
@@ -109,7 +126,7 @@ def main():
         else:
             out["varlen"] = refused(lambda: run([["a", ["id", "a"]], ["n", ["count*"]]], "(a:V)-[:E*1..3]->(b:V)"))
     out["routes"] = {k: s.route_count(k) for k in ("two_hop", "expand_count", "expand", "triangle", "var_length",
-                                                   "miss")}
+                                                   "undirected", "two_hop_grouped", "miss")}
     with open(f"{out_path}.rank{rank}.json", "w") as f:  # one file per rank: stdout lines interleave
         json.dump(out, f)
     s.close()

@@ -93,21 +93,9 @@ def _rank_main(rank, world, port, q):
                                         for r in [rank]], np.int64) for q in range(world)])
     want = np.concatenate([[r * 1000 + rank * 100 + i for i in range(r + rank + 1)] for r in range(world)])
     out["raw"] = bool(np.array_equal(got, want))
-    # 1b. the same exchange, an all-gather and an all-reduce in chunked calls (rounds of at most
-    # chunk / world words per pair: the C4 build's 2^28-word exchanges at full size)
-    from capsmi import _lib
-    small = TorchCollective(device="cpu", chunk_elems=4)
-    got = _a2av(small, world, [np.array([rank * 1000 + q * 100 + i for i in range(rank + q + 1)], np.int64)
-                               for q in range(world)])
-    out["raw_chunked"] = bool(np.array_equal(got, want))
-    mine = np.arange(11, dtype=np.int64) + 100 * rank
-    allg = np.zeros(11 * world, np.int64)
-    small(_lib.COLL_ALL_GATHER, mine.ctypes.data, allg.ctypes.data, 11, 0)
-    out["gather_chunked"] = bool(np.array_equal(allg, np.concatenate([np.arange(11) + 100 * r for r in range(world)])))
-    red = np.arange(9, dtype=np.int64) * (rank + 1)
-    small(_lib.COLL_ALL_REDUCE_SUM, red.ctypes.data, red.ctypes.data, 9, 0)
-    out["reduce_chunked"] = bool(np.array_equal(red, np.arange(9) * sum(r + 1 for r in range(world))))
-
+    # (calls above CAPSMI_COLL_CHUNK elements are cut by libcapsmi itself, csrc/k_dist.hip collective /
+    # collective_a2av, before they reach the adapter: covered on the GPU by tests/test_gpu_dist_golden.py and
+    # tests/test_gpu_dist_route.py with small CAPSMI_COLL_CHUNK values)
     n, src, dst = _graph()
     k, S = _scramble(n, world)
     span = 32 * S
@@ -215,7 +203,6 @@ def test_exchange_and_distributed_triangle_build_gloo(world):
         assert p.exitcode == 0
     for r, o in got.items():
         assert o["raw"] and o["pairs_owned"] and o["sorted"] and o["in_exchange"], (r, o)
-        assert o["raw_chunked"] and o["gather_chunked"] and o["reduce_chunked"], (r, o)
     sizes = got[0]["range_sizes"]
     assert max(sizes) <= 1.5 * (sum(sizes) / world) + 64, sizes  # balanced source ranges
     n, src, dst = _graph()

@@ -71,3 +71,38 @@ def test_golden_vectors_on_two_ranks(tmp_path, world, backend, mode):
         checked += 1
     assert not refused, refused
     print(f"{mode}: {checked} golden vectors equal on {world} rank(s) over {backend}")
+
+
+def test_nulls_on_one_rank_only(tmp_path):
+    """A nullable column whose validity buffer exists on one rank only (tests/dist_nulls_worker.py): the ranks
+    agree on which columns carry validity before an Exchange (csrc/k_dist.hip agreed_validity), so they issue
+    the same collectives; grouping on it, projecting it through the expand's joins and counting it give the
+    expected rows (nulls grouped together and not counted, SparkTable.scala:121-188)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from dist_nulls_worker import N, age, edges
+    out = str(tmp_path / "nulls")
+    env = dict(os.environ, CAPSMI_DIST_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", "dist_nulls_worker.py"), out]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=200)
+    assert p.returncode == 0, _err(p.stderr)
+    ranks = []
+    for r in range(2):
+        with open(f"{out}.rank{r}.json") as f:
+            ranks.append(json.load(f))
+    assert [x["has_valid"] for x in ranks] == [True, False]  # the case the agreement is for
+    ages = {x: age(x, 2) for x in range(N)}
+    groups = {}
+    for a in ages.values():
+        groups[a] = groups.get(a, 0) + 1
+    want = {"group": [{"k": k, "n": n} for k, n in groups.items()],
+            "expand": [{"x": ages[s], "y": ages[t]} for _, s, t in edges()],
+            "count": [{"c": sum(a is not None for a in ages.values())}]}
+    for name, rows in want.items():
+        res = [x[name] for x in ranks]
+        if res[0]["partitioned"]:
+            got = [row for x in res for row in x["rows"]]
+            assert same_rows(got, rows), (name, got, rows)
+        else:
+            for x in res:
+                assert same_rows(x["rows"], rows), (name, x["rows"], rows)

@@ -5,13 +5,16 @@ distributed graph and libcapsmi routes the plans to the distributed kernels.
   at ids 0..999.  Ownership is a hash of the id (include/capsmi.h capsmi_graph_distribute), so the
   shards balance even though contiguous id ranges would not.  BY_TARGET shards: the C3 queries, the
   expand, the cached layout, and the cyclic triangle (C4: the distributed trigraph build with its two
-  exchanges); BY_SOURCE shards: the triangle and the var-length grouped count (C5: in-relationships
-  exchanged at registration, od / Y all-reduced, each rank the rows of its owned starts).  Every answer
-  equals the oracle (oracle/closed.c closed forms, pinned by tests/test_oracle_pins.py).
+  exchanges); BY_SOURCE shards (north_star's owner(source)), registered once: every hot-path shape -- C3
+  count(*) / count(DISTINCT c) / count(DISTINCT a), undirected 1- and 2-hop, the grouped 2-hop, the
+  triangle and the var-length grouped count (C5: in-relationships exchanged at registration, od / Y
+  all-reduced, each rank the rows of its owned starts).  Every answer equals the oracle (oracle/closed.c
+  closed forms and enumeration, pinned by tests/test_oracle_pins.py).
 - 1 rank over RCCL (backend nccl, world size 1): the same routes with every exchange through
   torch.distributed's NCCL(=RCCL) branch of capsmi.dist.TorchCollective -- all-gathers, all-reduces and
-  the ALL_TO_ALL_V, the C4 part in chunked calls -- against the R-MAT fixtures (tests/golden/rmat_full.json:
-  C3 s = 20, C4 s = 14)."""
+  the ALL_TO_ALL_V, cut into rounds by libcapsmi under a small CAPSMI_COLL_CHUNK -- against the R-MAT
+  fixtures (tests/golden/rmat_full.json: C3 s = 20 in both modes, C4 s = 14) and the oracle (the six
+  shapes at s = 14 over BY_SOURCE shards)."""
 import json
 import os
 import socket
@@ -74,17 +77,19 @@ def test_routed_c3_c4_on_two_ranks_with_hubs(tmp_path, nodes):
     n, src, dst = _hub_edges(edges)
     lo, hi = int(min(src.min(), dst.min())), int(max(src.max(), dst.max())) + 1
     rows, distinct = cpu.two_hop_closed_form(n, src, dst)
+    _, distinct_a = cpu.two_hop_closed_form(n, dst, src)
     tri = cpu.triangle_closed_form(n, src, dst)
     out = _ranks(edges, lo, hi, nodes=nodes, queries="c3,expand,warm,tri")
     m = len(src)
     for o in out:  # every rank holds the whole answer
         assert o["count_star"] == rows, o
         assert o["count_distinct_c"] == distinct, o
+        assert o["count_distinct_a"] == distinct_a, o
         assert o["warm_distinct"] == distinct, o
         assert o["expand_count"] == m, o
         assert o["triangle"] == tri, o
         assert o["expand_partitioned"] is True
-        assert o["routes"]["two_hop"] >= 3 and o["routes"]["expand_count"] >= 1 and o["routes"]["expand"] >= 1, o
+        assert o["routes"]["two_hop"] >= 4 and o["routes"]["expand_count"] >= 1 and o["routes"]["expand"] >= 1, o
         assert o["routes"]["triangle"] >= 1, o
     assert sum(o["expand_rows_local"] for o in out) == m
     assert sum(o["rels_local"] for o in out) == m
@@ -94,24 +99,54 @@ def test_routed_c3_c4_on_two_ranks_with_hubs(tmp_path, nodes):
     assert (dst < n // 2).mean() > 0.7
 
 
-def test_routed_c4_c5_by_source_on_two_ranks(tmp_path):
+def _six_shapes(n, src, dst):
+    """the oracle's answers for the six hot-path shapes over one graph (every node V)"""
     from oracle import cpu
+    rows, dc = cpu.two_hop_closed_form(n, src, dst)
+    _, da = cpu.two_hop_closed_form(n, dst, src)  # distinct starts = distinct ends of the reversed graph
+    u_rows, u_dc = cpu.two_hop_undirected_closed_form(n, src, dst)
+    loops = int((src == dst).sum())
+    ends = int(np.unique(np.concatenate([src, dst])).size)  # every endpoint is an arc's end
+    _, _, grows, gdist = cpu.two_hop_enumerate(n, src, dst, grouped=True)
+    grouped = {int(a): (int(gdist[a]), int(grows[a])) for a in np.nonzero(grows)[0]}
+    _, per_a = cpu.var_length_closed_form(n, src, dst, 1, 3)
+    return {"count_star": rows, "count_distinct_c": dc, "count_distinct_a": da,
+            "und1": [2 * len(src) - loops, ends], "und2": [u_rows, u_dc, u_dc],  # (a)-(b)-(c) is symmetric
+            "grouped": grouped, "triangle": cpu.triangle_closed_form(n, src, dst),
+            "varlen": {int(i): int(per_a[i]) for i in np.nonzero(per_a)[0]}}
+
+
+def _check_six(out, want, m):
+    got_g, got_v = {}, {}
+    for o in out:  # the count shapes whole on every rank, the grouped rows partitioned by owned start
+        for k in ("count_star", "count_distinct_c", "count_distinct_a", "und1", "und2", "triangle"):
+            assert o[k] == want[k], (k, o[k], want[k])
+        assert o["expand_count"] == m, o
+        r = o["routes"]
+        assert r["two_hop"] >= 3 and r["undirected"] >= 2 and r["two_hop_grouped"] >= 1, r
+        assert r["triangle"] >= 1 and r["var_length"] >= 1 and r["expand_count"] >= 1, r
+        assert r["miss"] == 0, r
+        for a, dc, c in o["grouped_rows"]:
+            assert a not in got_g, a  # each start id on exactly one rank
+            got_g[a] = (dc, c)
+        for a, c in o["varlen_rows"]:
+            assert a not in got_v, a
+            got_v[a] = c
+    assert got_g == want["grouped"]
+    assert got_v == want["varlen"]
+
+
+def test_one_by_source_distribution_routes_every_shape(tmp_path):
+    """north_star's partitioning (relationships by owner(source)) registered once: C3 count(*) / count(DISTINCT
+    c) / count(DISTINCT a), the undirected 1- and 2-hop counts, the grouped 2-hop, the triangle (C4) and the
+    var-length grouped count (C5) all routed on 2 ranks, none refused or run operator by operator (miss 0)."""
     edges = tmp_path / "hubs_src.txt"
     n, src, dst = _hub_edges(edges, seed=11, m=200_000)
-    lo, hi = 0, n
-    tri = cpu.triangle_closed_form(n, src, dst)
-    _, per_a = cpu.var_length_closed_form(n, src, dst, 1, 3)
-    out = _ranks(edges, lo, hi, rels_by="source", queries="tri,varlen")
-    got = {}
+    want = _six_shapes(n, src, dst)
+    out = _ranks(edges, 0, n, rels_by="source", queries="c3,und,grouped,tri,varlen,expand")
+    _check_six(out, want, len(src))
     for o in out:
-        assert o["triangle"] == tri, o
-        assert o["varlen_partitioned"] is True
-        assert o["routes"]["triangle"] >= 1 and o["routes"]["var_length"] >= 1, o
-        for a, c in o["varlen_rows"]:
-            assert a not in got, a  # each start id on exactly one rank
-            got[a] = c
-    want = {int(i): int(per_a[i]) for i in np.nonzero(per_a)[0]}
-    assert got == want
+        assert o["varlen_partitioned"] is True and o["grouped_partitioned"] is True
     assert sum(o["rels_local"] for o in out) == len(src)
 
 
@@ -132,14 +167,16 @@ def test_routes_over_rccl_world1(tmp_path):
     assert o["count_distinct_c"] == c3["count_distinct_c"], o
     assert o["count_star"] == c3["count_star"], o
     assert o["routes"]["two_hop"] >= 2, o
+    o = _ranks("rmat:20", 0, 1 << 20, world=1, rels_by="source", queries="c3", backend="nccl",
+               out=str(tmp_path / "r20s"))[0]
+    assert o["count_distinct_c"] == c3["count_distinct_c"], o
+    assert o["count_star"] == c3["count_star"], o
     c4 = _fixture("c4_s14")
-    # CAPSMI_COLL_CHUNK: the build's exchanges and all-gathers (2^18 words here) in RCCL calls of at most
-    # 2^16 words -- the chunked rounds that keep a full-size build (2^28 words) below RCCL's 2 GiB limit
-    o = _ranks("rmat:14", 0, 1 << 14, world=1, rels_by="source", queries="tri,varlen", backend="nccl",
-               out=str(tmp_path / "r14"), env_extra={"CAPSMI_COLL_CHUNK": str(1 << 16)})[0]
+    # CAPSMI_COLL_CHUNK: every collective above 2^12 words cut by libcapsmi into rounds (k_dist.hip collective,
+    # collective_a2av) -- the path that keeps a full-size C4 build's 2^28-word exchanges in bounded RCCL calls
+    o = _ranks("rmat:14", 0, 1 << 14, world=1, rels_by="source", queries="c3,und,grouped,tri,varlen,expand",
+               backend="nccl", out=str(tmp_path / "r14"), env_extra={"CAPSMI_COLL_CHUNK": str(1 << 12)})[0]
     assert o["triangle"] == c4["count_star"], o
-    assert o["routes"]["triangle"] >= 1 and o["routes"]["var_length"] >= 1, o
     from oracle import cpu
     src, dst = cpu.rmat_edges(14, 0, 16 << 14)
-    _, per_a = cpu.var_length_closed_form(1 << 14, src, dst, 1, 3)
-    assert {a: c for a, c in o["varlen_rows"]} == {int(i): int(per_a[i]) for i in np.nonzero(per_a)[0]}
+    _check_six([o], _six_shapes(1 << 14, src, dst), len(src))
