@@ -76,7 +76,7 @@ C3_WORKLOAD = "C3: MATCH (a:Person)-[:FRIEND_OF]->(b:Person)-[:FRIEND_OF]->(c:Pe
 KERNELS = ("part_scatter1", "part_scatter2_hop1", "part_scatter2", "hop1", "hop2", "mid_combine", "bitmap_add",
            "bitmap_range",
            "count_part", "count_part_in", "count_in", "count_part_out", "count_out", "degrees", "und_count_part",
-           "und_count", "und_distinct")
+           "und_count", "und_distinct", "und_hop1", "und_hop2")
 # timer name -> kernel name as rocprofv3 reports it (hop1 and hop2 are two instances of k_hop_2d)
 KERNEL_SYMBOL = {"part_scatter1": "k_scatter_l", "part_scatter2_hop1": "k_scatter_s2", "part_scatter2": "k_scatter_s2",
                  "hop1": "k_hop_2d", "hop2": "k_hop_2d", "mid_combine": "k_mid_combine", "bitmap_add": "k_bitmap_add",
@@ -84,7 +84,8 @@ KERNEL_SYMBOL = {"part_scatter1": "k_scatter_l", "part_scatter2_hop1": "k_scatte
                  "count_part": "k_rec_part", "count_part_in": "k_scatter_c", "count_part_out": "k_scatter_c",
                  "count_in": "k_rec_walk",
                  "count_out": "k_rec_walk", "degrees": "k_degrees", "und_count_part": "k_rec_part",
-                 "und_count": "k_und_deg", "und_distinct": "k_und_hop1+k_und_hop2"}
+                 "und_count": "k_und_deg", "und_distinct": "k_und_hop1+k_und_hop2", "und_hop1": "k_und_2d",
+                 "und_hop2": "k_und_2d"}
 
 
 def parse():

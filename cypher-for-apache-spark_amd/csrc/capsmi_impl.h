@@ -398,8 +398,9 @@ struct RelPartHop1 {
     const capsmi_bitmap* b;
     uint32_t *M, *S1, *S2;
 };
+// unpacked: keep 8-byte pairs whatever the domain (a layout walked by kernels that read uint2 pairs only)
 void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
-                   int64_t lo, int64_t hi, RelPart& rp, const RelPartHop1* h1 = nullptr);
+                   int64_t lo, int64_t hi, RelPart& rp, const RelPartHop1* h1 = nullptr, bool unpacked = false);
 void relpart_hop1(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* a, const capsmi_bitmap* b, uint32_t* M,
                   uint32_t* S1, uint32_t* S2);
 void relpart_hop2(capsmi_session* s, const RelPart& rp, const capsmi_bitmap* c, const uint32_t* X1, const uint32_t* X2,
@@ -454,6 +455,12 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts);
 int64_t undirected_count(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
                          int nt, int hops, const capsmi_bitmap* a, const capsmi_bitmap* b, const capsmi_bitmap* c,
                          int kind, uint32_t* marks = nullptr);
+// the undirected 2-hop count(DISTINCT end) over the 2-D cell layout (k_und_part.hip), domains of at most
+// 2^26 ids (undirected_distinct_part_ok); marks as above
+bool undirected_distinct_part_ok(int64_t n);
+int64_t undirected_distinct_part(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts,
+                                 const int64_t* ms, int nt, const capsmi_bitmap* a, const capsmi_bitmap* b,
+                                 const capsmi_bitmap* c, uint32_t* marks);
 
 // the 2-hop chain grouped by its start (k_grouped.hip): rows (relative start id, count(*) or count(DISTINCT
 // end)); false when the distinct keys would exceed key_budget bytes

@@ -1047,7 +1047,7 @@ void chunk_order(capsmi_session* s, int nt, int64_t pool_chunks, int64_t g2_want
 }
 
 void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
-                   int64_t lo, int64_t hi, RelPart& rp, const RelPartHop1* h1) {
+                   int64_t lo, int64_t hi, RelPart& rp, const RelPartHop1* h1, bool unpacked) {
     REQUIRE(hi > lo && (uint64_t)(hi - lo) <= (uint64_t(1) << 30), CAPSMI_ERR_UNSUPPORTED,
             "partitioned layout needs an id domain of at most 2^30 ids");
     using namespace part;
@@ -1057,7 +1057,7 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
     // writing the packed form is slower (C3: 3.45 -> 3.9-4.45 ms unfused, 3.73 -> 4.14 ms with hop 1
     // fused) while each hop over it gains 0.2-0.4 ms (hop 1 1.30 -> 0.90, hop 2 1.57 -> 1.35 ms), so a
     // layout read by one query's two hops is left in 8-byte pairs
-    if (h1) rp.L.packed = 0;
+    if (h1 || unpacked) rp.L.packed = 0;
     const Layout& L = rp.L;
     REQUIRE(L.nt <= kMaxTSlices && L.ncells <= kMaxCells, CAPSMI_ERR_INTERNAL, "layout too large");
     if (h1)

@@ -218,9 +218,12 @@ int64_t undirected_count(capsmi_session* s, const int64_t* const* srcs, const in
         return (int64_t)(h[2] - h[0]);
     }
     // 2-hop count(DISTINCT end); distinct start is the same walk from the other end (the arcs are symmetric)
-    KernelTimer kt(s, "und_distinct");
     const capsmi_bitmap* A = kind == 2 ? c : a;
     const capsmi_bitmap* Cc = kind == 2 ? a : c;
+    const char* ue = getenv("CAPSMI_UND");  // "stream": the per-arc streaming form below (A/B)
+    if (undirected_distinct_part_ok(n) && !(ue && std::string(ue) == "stream"))
+        return undirected_distinct_part(s, srcs, dsts, ms, nt, A, b, Cc, marks);  // the 2-D cell layout
+    KernelTimer kt(s, "und_distinct");
     // B1, B2, C: three bitmaps in one buffer (one fill); x(b) needs no clearing (read only where B1 says
     // an arc stored it)
     Buf bm = dev_alloc(sizeof(uint32_t) * 3 * nw, s), xb = dev_alloc(sizeof(uint32_t) * n, s);

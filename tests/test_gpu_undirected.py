@@ -137,3 +137,48 @@ def test_undirected_two_hop_vs_fixture(session, scale):
         assert result_rows(t, outs, session.dictionary)[0]["n"] == fx["count_star"]
     finally:
         del os.environ["CAPSMI_COUNT"]
+
+
+@pytest.mark.parametrize("mode", ["layout", "stream"])
+def test_undirected_distinct_layout_and_stream_forms(session, mode):
+    """count(DISTINCT c) / count(DISTINCT a) of the undirected 2-hop over the 2-D cell layout (csrc/k_und_part.hip,
+    the default up to 2^26 ids: both hops grouped by the slice the arcs go into, K(b) in LDS) and the streaming form
+    (CAPSMI_UND=stream), with node filters at the ends or at the middle, against the closed form
+    (oracle/closed.c orc_two_hop_undirected_closed_form, pinned to enumeration in tests/test_oracle_pins.py).
+    R-MAT scale 21: 4 x 4 slices, so the walks cross slices and workgroups."""
+    import os
+    from capsmi.planner import EntityTable, Planner, ScanGraph, result_rows
+    from capsmi import graph
+    from oracle import cpu
+    scale = 21
+    n = 1 << scale
+    rels = graph.rmat_rels(session, scale, 0, 16 << scale, graph.RMAT_GRAPH500, 42)
+    sg = ScanGraph(session, [EntityTable("node", frozenset({"Person"}), {"age": 0},
+                                         graph.rmat_nodes(session, scale, graph.NODES_PERSON, 42), id_col="id"),
+                             EntityTable("node", frozenset({"Company"}), {},
+                                         graph.rmat_nodes(session, scale, graph.NODES_COMPANY, 42), id_col="id")],
+                   [EntityTable("rel", frozenset({"R"}), {}, rels, id_col="id", src_col="source", dst_col="target")])
+    src, dst = cpu.rmat_edges(scale, 0, 16 << scale)
+    person = cpu.person_mask(n).astype(np.uint8)
+    every = np.ones(n, np.uint8)
+    prev = os.environ.get("CAPSMI_UND")
+    if mode == "stream":
+        os.environ["CAPSMI_UND"] = "stream"
+    try:
+        for pattern, (am, bm, cm) in (("(a:Person)-[:R]-(b)-[:R]-(c:Person)", (person, every, person)),
+                                      ("(a)-[:R]-(b:Person)-[:R]-(c)", (every, person, every)),
+                                      ("(a:Person)-[:R]-(b)-[:R]-(c)", (person, every, every))):
+            q = {"clauses": [{"match": pattern}],
+                 "return": {"items": [["dc", ["count_distinct", ["id", "c"]]], ["da", ["count_distinct", ["id", "a"]]]]}}
+            before = session.route_count("undirected")
+            t, outs = Planner(sg).run(q)
+            got = result_rows(t, outs, session.dictionary)[0]
+            assert session.route_count("undirected") == before + 1, pattern
+            _, dc = cpu.two_hop_undirected_closed_form(n, src, dst, am, bm, cm)
+            _, da = cpu.two_hop_undirected_closed_form(n, src, dst, cm, bm, am)
+            assert (got["dc"], got["da"]) == (dc, da), (pattern, mode)
+    finally:
+        if prev is None:
+            os.environ.pop("CAPSMI_UND", None)
+        else:
+            os.environ["CAPSMI_UND"] = prev
