@@ -105,9 +105,10 @@ def parse():
     p.add_argument("--shard-of", type=int, default=0,
                    help="diagnostic (C3): time every rank's shard of an N-way partition (--rels-by) on one GPU, "
                         "no exchange; the line is not the metric")
-    p.add_argument("--rels-by", default="source", choices=("source", "target"),
-                   help="C3 at N > 1 / --dist1 / --shard-of: relationships partitioned by the owner of their source "
-                        "(north_star; the one distribution every route takes) or of their target")
+    p.add_argument("--rels-by", default="target", choices=("source", "target"),
+                   help="C3 at N > 1 / --dist1 / --shard-of: relationships partitioned by the owner of their target "
+                        "(default: 15 %% faster per rank at 8 shards, DESIGN.md §7.8) or of their source (north_star; "
+                        "the one distribution every route takes)")
     p.add_argument("--c2-route", default="direct", choices=("direct", "planner", "joins"),
                    help="C2: explicit expand kernels (direct), Planner(sg).run routed to the fused expand "
                         "(planner), or the same plan operator by operator through the generic radix joins (joins)")

@@ -342,3 +342,31 @@ def test_sharded_node_scan_assume_and_device_popcount(nparts):
     assert int(counts.sum().item()) == ref
     with pytest.raises(Exception):
         p.assume(n + 1, True)  # a count outside the domain is refused
+
+
+@pytest.mark.parametrize("cached", [False, True])
+def test_six_byte_pass1_pool(session, cached, monkeypatch):
+    """The 6-byte pass-1 pool (CAPSMI_P1=6: csrc/k_part.hip k_scatter_l6, pass 2 reading key = source << 19 |
+    target offset) gives the same layout as the 8-byte default: cell counts and digests, and the 2-hop answer,
+    unpacked (one query's layout) and packed (cached)."""
+    from capsmi import graph
+    scale = 21
+    n = 1 << scale
+    rels = graph.rmat_rels(session, scale, 0, 8 << scale)
+    src, dst = rels.column("source").values, rels.column("target").values
+    rng = np.random.default_rng(9)
+    ok, okc = rng.random(n) < 0.8, rng.random(n) < 0.6
+    a, c = _bitmap(session, n, np.nonzero(ok)[0]), _bitmap(session, n, np.nonzero(okc)[0])
+    want = _np_count_distinct(n, src, dst, ok, ok, okc)
+    monkeypatch.setenv("CAPSMI_PAIRS", "packed" if cached else "uint2")
+    digests = []
+    for fmt in ("8", "6"):
+        monkeypatch.setenv("CAPSMI_P1", fmt)
+        rp = graph.RelPartition(session, [rels], 0, n)
+        counts, sums, bad, geom = rp.digest()
+        assert bad == 0, fmt
+        digests.append((np.asarray(counts).tolist(), np.asarray(sums).tolist(), geom))
+        assert rp.count_distinct(a, a, c) == want, fmt
+        rp.release()
+        assert graph.two_hop_count_distinct(session, [rels], a, a, c) == want, fmt
+    assert digests[0] == digests[1]
