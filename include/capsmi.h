@@ -533,7 +533,9 @@ capsmi_status capsmi_cluster_by(capsmi_table* rels, const char* key_col, int64_t
  * elements, the q-th rank-major segment of send->data, to rank q and receives recv->counts[q] elements
  * from rank q into the q-th segment of recv->data (the library has exchanged the counts beforehand with
  * an ALL_GATHER, so both lists agree across ranks).  dtype CAPSMI_I64 (int64) or CAPSMI_COLL_U32
- * (uint32 words).  Return 0 on success. */
+ * (uint32 words).  No call moves more than CAPSMI_COLL_CHUNK elements in all (environment, default
+ * 2^26): the library cuts larger all-gathers, all-reduces and exchanges into several calls itself, so a
+ * transport maps each call to one collective.  Return 0 on success. */
 enum { CAPSMI_COLL_ALL_GATHER = 0, CAPSMI_COLL_ALL_REDUCE_SUM = 1, CAPSMI_COLL_ALL_REDUCE_MAX = 2,
        CAPSMI_COLL_ALL_TO_ALL_V = 3 };
 enum { CAPSMI_COLL_U32 = 100 };
@@ -555,17 +557,20 @@ enum { CAPSMI_RELS_BY_SOURCE = 0, CAPSMI_RELS_BY_TARGET = 1 };
  * owns.  Checked: ids inside the domain and the shard's rows owned (else ILLEGAL_ARGUMENT).  The
  * tables keep their scrambled key columns.  With BY_SOURCE, registration also exchanges (ALL_TO_ALL_V)
  * every relationship whose target another rank owns to that rank, which keeps it as its shard's
- * in-relationships (the var-length route's reverse multiplicities need them).  Routed on a distributed
- * graph: Expand projections (rows of this rank's relationships) and count(*) (one SUM all-reduce); with
- * BY_TARGET the 2-hop count(DISTINCT end) (all-gathers of the owned node-scan bitmap words and hop-1
- * frontier, one all-reduce) and the 2-hop count(*) (an all-gather of the owned in-degrees, one
- * all-reduce); either mode: the cyclic triangle count (undirected keys exchanged to the owner of their
- * lower end, the oriented lists exchanged by degree-order range and all-gathered into a replicated
- * oriented graph, each rank counting a work share, one all-reduce); with BY_SOURCE the var-length
- * grouped count (od and Y all-reduced between its phases; the rows of each rank's owned start nodes).
- * A plan over a distributed graph that would need another exchange (a generic join, aggregate, distinct
- * or ordering over partitioned rows) is CAPSMI_ERR_UNSUPPORTED; capsmi_table_partitioned tells which
- * results hold this rank's rows only.  A session given a collective at world size 1 runs the same
+ * in-relationships (the var-length and undirected routes need them).  Routed on a distributed graph:
+ * Expand projections (rows of this rank's relationships) and count(*) (one SUM all-reduce); either mode:
+ * the 2-hop count(*), count(DISTINCT end) and count(DISTINCT start) (all-gathers of owned frontier slices
+ * when the walk's relationships arrive by their end's owner, an ALL_TO_ALL_V + OR of frontier and end
+ * bitmap slices when by their start's owner; the count(*) through an all-gather of owned degrees) and the
+ * cyclic triangle count (undirected keys exchanged to the owner of their lower end, the oriented lists
+ * exchanged by degree-order range and all-gathered into a replicated oriented graph, each rank counting a
+ * work share, one all-reduce); with BY_SOURCE also the var-length grouped count (od and Y all-reduced
+ * between its phases; the rows of each rank's owned start nodes), the undirected 1- / 2-hop counts (the
+ * middles restricted to owned ids over the relationships incident to them, marks OR-reduced) and the 2-hop
+ * grouped by its start (outC and the deduplicated hop-2 lists all-gathered; rows of the owned starts).
+ * Any other plan runs operator by operator with the Exchanges Spark would insert (hash-partitioned joins
+ * and groupings, gathers for global aggregates and ordering); capsmi_table_partitioned tells which results
+ * hold this rank's rows only.  A session given a collective at world size 1 runs the same
  * distributed routes over its single shard (every exchange then goes through the collective). */
 capsmi_status capsmi_graph_distribute(capsmi_session* s, int64_t id_lo, int64_t id_hi, int32_t nnodes,
                                       capsmi_table* const* nodes, int32_t node_mode, int32_t nrels,
