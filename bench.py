@@ -118,6 +118,9 @@ def parse():
     p.add_argument("--dist1", action="store_true",
                    help="diagnostic (C3, C4, C5): the distributed route at world size 1 over RCCL (launch with "
                         "torch.distributed.run --nproc-per-node 1): the route's fixed per-rank cost, exchanges included")
+    p.add_argument("--tri-parts", type=int, default=0,
+                   help="diagnostic (C4, one GPU): the work-balanced shares of N ranks (CAPSMI_TRI_WPARTS) of one "
+                        "trigraph, each share's count timed alone -- the per-rank triangle phase without contention")
     p.add_argument("--workload", default="c3", choices=("c2", "c3", "c4", "c5"),
                    help="c3 (default, the BASELINE metric) or the single-GPU C2/C4/C5 lines (SURVEY.md 8d)")
     return p.parse_args()
@@ -981,6 +984,26 @@ def run_single(args):
                                    "planner": "Planner(sg).run, recognised and routed to the fused expand",
                                    "joins": "Planner(sg).run operator by operator: node scans, two generic "
                                             "radix joins, filter, select (fused routing off)"}[route]
+    if wl == "c4" and args.tri_parts > 1 and world == 1:
+        os.environ["CAPSMI_TRI_WPARTS"] = str(args.tri_parts)
+        ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id")
+        g = graph.TriGraph(sess, [rels], ok)
+        per, tot = [], 0
+        for r in range(args.tri_parts):
+            g.count(r, args.tri_parts)  # warm
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            c = g.count(r, args.tri_parts)
+            torch.cuda.synchronize()
+            per.append(round((time.perf_counter() - t1) * 1e3, 3))
+            tot += c  # the pair / self terms come with part 0 only: the parts add up to the count
+        g.release()
+        del os.environ["CAPSMI_TRI_WPARTS"]
+        line["query"]["tri_parts"] = {"parts": args.tri_parts, "ms_per_part": per, "max_ms": max(per),
+                                      "mean_ms": sum(per) / len(per), "max_over_mean": max(per) / (sum(per) / len(per)),
+                                      "sum_of_parts_ok": tot == res,
+                                      "note": "work-balanced shares of one single-GPU trigraph, each part counted "
+                                              "alone (wall time incl. the pair/self terms of part 0)"}
     line["query"]["check_vs_fixture"] = fcheck
     if check is not None or (world > 1 and wl in ("c2", "c5")):
         line["query"]["check_vs_unsharded"] = check

@@ -1386,7 +1386,11 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     g.nbig = flags_to_indices(s, P<uint8_t>(fbg), n, g.big_u);
     HIP_CHECK(hipGetLastError());
     ph.reset();
-    if (dd) {  // work-balanced shares: prefix sums of the centers' walked entries, host copies
+    // work-balanced shares of a distributed build's world; CAPSMI_TRI_WPARTS=N computes them for N parts of a
+    // single-device build too (diagnostic: each part's count timed alone, bench.py --tri-parts)
+    const char* wpe = getenv("CAPSMI_TRI_WPARTS");
+    const int wparts = dd ? dd->world : (wpe ? std::max(0, atoi(wpe)) : 0);
+    if (wparts > 1 || dd) {  // work-balanced shares: prefix sums of the centers' walked entries, host copies
         KernelTimer kt(s, "tri_work");
         auto work = [&](const Buf& cs, int64_t nc, bool vm, bool small, std::vector<int64_t>& out) {
             Buf w = dev_alloc(sizeof(int64_t) * (2 * nc + 2), s);
@@ -1404,7 +1408,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
                 HIP_CHECK(hipGetLastError());
             }
             exclusive_scan_i64(P<int64_t>(w), P<int64_t>(w) + nc + 1, nc, s);
-            const int W = dd->world;
+            const int W = wparts;
             Buf cut = dev_alloc(sizeof(int64_t) * (W + 1), s);
             hipLaunchKernelGGL(k_tri_cuts, dim3(1), dim3(256), 0, st, P<int64_t>(w) + nc + 1, nc, W, P<int64_t>(cut));
             HIP_CHECK(hipGetLastError());
@@ -1412,12 +1416,12 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
             HIP_CHECK(hipMemcpyAsync(out.data(), P<int64_t>(cut), sizeof(int64_t) * (W + 1), hipMemcpyDeviceToHost, st));
             HIP_CHECK(hipStreamSynchronize(st));
         };
-        REQUIRE(dd->world < 255, CAPSMI_ERR_UNSUPPORTED, "distributed triangle count: at most 254 ranks");
-        g.wparts = dd->world;
+        REQUIRE(wparts < 255, CAPSMI_ERR_UNSUPPORTED, "distributed triangle count: at most 254 ranks");
+        g.wparts = wparts;
         work(g.big_u, g.nbig, false, false, g.wbig);
         if (g.vm_own) {  // every v-mode center of this build is this rank's
-            g.wvm.assign(dd->world + 1, 0);
-            for (int q = dd->rank + 1; q <= dd->world; ++q) g.wvm[q] = g.nvm;
+            g.wvm.assign(wparts + 1, 0);
+            for (int q = dd->rank + 1; q <= wparts; ++q) g.wvm[q] = g.nvm;
         } else {
             work(g.vm_c, g.nvm, true, false, g.wvm);
         }
