@@ -1223,12 +1223,16 @@ void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
         const int64_t full = (ms[i] + kCh - 1) / kCh;
+        // tiles per block: 8 for large inputs; small ones (a rank's 1/8 shard of C5: 2^22 relationships) take
+        // 2, so the pass spreads over the CUs instead of 64 blocks walking 8 tiles each (124 us for 2^22
+        // relationships at 64 blocks, round-5 kernel trace, profiles/r05_c5_small_trace_stats.csv)
+        const int64_t tmin = ms[i] <= (int64_t(1) << 24) ? 2 : 8;
         int64_t g = std::min<int64_t>((int64_t)s->num_cus * (kSBlock / kP1Block),
-                                      (ms[i] + 8 * (int64_t)kP1Tile - 1) / (8 * (int64_t)kP1Tile));
-        // (at most ~32 open chunks per filled one: a 1/8 shard of C5's 2^25 relationships got 32 blocks
-        // at the earlier bound of 8, and its three partitions took 1.33 ms against 0.29 ms for the
-        // whole table's two)
-        g = std::min<int64_t>(g, std::max<int64_t>(1, 32 * full / L.nt));
+                                      (ms[i] + tmin * (int64_t)kP1Tile - 1) / (tmin * (int64_t)kP1Tile));
+        // (at most ~32 open chunks per filled one -- 64 for small inputs, whose pools are small anyway: a 1/8
+        // shard of C5's 2^25 relationships got 32 blocks at the earlier bound of 8, and its three
+        // partitions took 1.33 ms against 0.29 ms for the whole table's two)
+        g = std::min<int64_t>(g, std::max<int64_t>(1, (tmin == 2 ? 64 : 32) * full / L.nt));
         g1[i] = (int)std::max<int64_t>(1, g);
         c0[i] = pool_chunks;
         pool_chunks += (int64_t)g1[i] * chunks_per_block(ms[i], g1[i], L.nt);

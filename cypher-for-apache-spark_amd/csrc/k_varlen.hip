@@ -142,7 +142,37 @@ struct PairHash {
     unsigned int* ovf;
     unsigned int* any_ovf;
     unsigned long long mask;
+    // sized on the device (the sharded form): the mask lives at *dmask, written by k_vl_hsize from the
+    // candidate count, so no host round trip sits between the candidates and the table
+    const unsigned long long* dmask = nullptr;
 };
+
+__device__ __forceinline__ PairHash sized(PairHash h) {
+    if (h.dmask) {
+        h.mask = *h.dmask;
+        h.any_ovf = h.ovf + h.mask + 1;
+    }
+    return h;
+}
+
+// the table's size from the candidate count: the power of two >= 2 * count (at least 1024) -- as the host
+// sizes it in the single-device form -- capped by the allocation (cap_max slots)
+__global__ void k_vl_hsize(const unsigned long long* __restrict__ ncand, unsigned long long cap_max,
+                           unsigned long long* __restrict__ dmask) {
+    unsigned long long cap = 1024;
+    while (cap < 2 * *ncand && cap < cap_max) cap <<= 1;
+    *dmask = cap - 1;
+}
+
+// clears the device-sized table's slots [0, cap) and overflow words [0, cap]
+__global__ void k_vl_hclear(PairHash h) {
+    h = sized(h);
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i <= h.mask + 1;
+         i += (unsigned long long)gridDim.x * blockDim.x) {
+        if (i <= h.mask) h.slot[i] = 0;
+        h.ovf[i] = 0;  // ovf[cap] is any_ovf
+    }
+}
 
 __device__ __forceinline__ unsigned long long hkey(uint32_t s, uint32_t t) {
     return (((unsigned long long)s << 24) | t) + 1;
@@ -386,6 +416,7 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_w(ChunkWalk cw, int64_t n, cons
 // the candidate list into the exact table
 __global__ void k_vl_cins(const unsigned long long* __restrict__ cl, const unsigned long long* __restrict__ ncand,
                           PairHash h) {
+    h = sized(h);
     const int64_t cnt = (int64_t)*ncand;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * blockDim.x)
         pair_insert(h, cl[i]);
@@ -541,6 +572,7 @@ __global__ void k_vl_pack(int64_t n, const long long* __restrict__ od, const lon
 // is in it, both ways): T3(a) -= R(a) for a_ok(a)
 __global__ void k_vl_recip(PairHash h, const uint32_t* __restrict__ aw, int a_full, const uint32_t* __restrict__ bw,
                            int b_full, unsigned long long* __restrict__ T3, uint32_t own_lo, uint32_t own_hi) {
+    h = sized(h);
     const bool ovf = *h.any_ovf != 0;
     for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i <= h.mask;
          i += (unsigned long long)gridDim.x * blockDim.x) {
@@ -966,22 +998,27 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
                                                                                          (int64_t)s->num_cus * 8))),
                                    dim3(kFcBlock), 0, st, as[i], ad[i], am[i], v->d.lo, bl,
                                    P<unsigned long long>(clist), P<unsigned long long>(cand));
-        // the table sized by the candidates' count (one read back: a table sized by the relationships
-        // instead costs more in clearing and scanning than the round trip)
-        const int64_t nc = read_scalar(s, P<int64_t>(cand));
-        int64_t cap = 1024;
-        while (cap < 2 * nc) cap <<= 1;
-        v->hk = dev_alloc(sizeof(unsigned long long) * cap, s);
-        v->hc = dev_alloc(sizeof(unsigned int) * (cap + 1), s);
-        HIP_CHECK(hipMemsetAsync(P<void>(v->hk), 0, sizeof(unsigned long long) * cap, st));
-        HIP_CHECK(hipMemsetAsync(P<void>(v->hc), 0, sizeof(unsigned int) * (cap + 1), st));
-        const PairHash h{P<unsigned long long>(v->hk), P<unsigned int>(v->hc), P<unsigned int>(v->hc) + cap,
-                         (unsigned long long)(cap - 1)};
-        hipLaunchKernelGGL(k_vl_cins, dim3(grid(s, nc)), dim3(256), 0, st, P<unsigned long long>(clist),
+        // the table sized on the device from the candidates' count (k_vl_hsize): allocated for the upper bound
+        // (every relationship a candidate), cleared and scanned only as far as the count needs -- no host
+        // round trip (round 4 read the count back: ~40 us of an idle device per rank and query)
+        int64_t cap_max = 1024;
+        while (cap_max < 2 * mall) cap_max <<= 1;
+        v->hk = dev_alloc(sizeof(unsigned long long) * (cap_max + 1), s);  // + the device mask word
+        v->hc = dev_alloc(sizeof(unsigned int) * (cap_max + 1), s);
+        unsigned long long* dmask = P<unsigned long long>(v->hk) + cap_max;
+        hipLaunchKernelGGL(k_vl_hsize, dim3(1), dim3(1), 0, st, P<unsigned long long>(cand), (unsigned long long)cap_max,
+                           dmask);
+        // any_ovf sits behind the slots' overflow words at ovf[cap]: the device-sized cap, so k_vl_hclear
+        // clears it and the kernels find it through the mask (ovf + mask + 1)
+        PairHash h{P<unsigned long long>(v->hk), P<unsigned int>(v->hc), nullptr, (unsigned long long)(cap_max - 1),
+                   dmask};
+        const unsigned gmax = (unsigned)std::min<int64_t>(grid(s, cap_max), (int64_t)s->num_cus * 8);
+        hipLaunchKernelGGL(k_vl_hclear, dim3(gmax), dim3(256), 0, st, h);
+        hipLaunchKernelGGL(k_vl_cins, dim3(gmax), dim3(256), 0, st, P<unsigned long long>(clist),
                            P<unsigned long long>(cand), h);
         sub.reset(new KernelTimer(s, "vls_rev_recip"));
-        hipLaunchKernelGGL(k_vl_recip, dim3(grid(s, cap)), dim3(256), 0, st, h, v->d.a, v->d.a_full, v->d.b,
-                           v->d.b_full, P<unsigned long long>(v->T3), (uint32_t)v->own_lo, (uint32_t)v->own_hi);
+        hipLaunchKernelGGL(k_vl_recip, dim3(gmax), dim3(256), 0, st, h, v->d.a, v->d.a_full, v->d.b, v->d.b_full,
+                           P<unsigned long long>(v->T3), (uint32_t)v->own_lo, (uint32_t)v->own_hi);
     }
     HIP_CHECK(hipGetLastError());
     return v.release();
