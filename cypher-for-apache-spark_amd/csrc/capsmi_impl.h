@@ -425,6 +425,11 @@ struct TriGraph {
     // oriented edges grouped by target; the edge is off[u] + p); vm_c = the v-mode centers.
     int vmt = 0;
     Buf ioff, itg, ipos, vm_c;
+    // direction-split lists (k_tri.hip "direction-split lists"): tgs = every out_f(x) then every out_b(x),
+    // fbo = their starts (2n + 2 uint32); with split set the in-lists are ikey (to << 40 | record index, sorted)
+    // and irec (records: coded source word | pf | pb << 16) instead of itg / ipos
+    bool split = false;
+    Buf tgs, fbo, ikey, irec;
     int64_t nvm = 0;
     // ek / ev entries (= ne on one device; on a rank of a distributed build the undirected edges whose
     // lower end it owns, while ok / tg hold every oriented edge)

@@ -286,6 +286,152 @@ __global__ void k_in_split(const uint64_t* __restrict__ ik, const int64_t* __res
     }
 }
 
+// ---- direction-split lists ------------------------------------------------------------------------
+// A wedge closes a cycle in one direction only: u -> v -> w -> u needs m(v,w) >= 1 and u -> w -> v -> u
+// needs m(w,v) >= 1 (the two terms of tri_weight).  Each out-list is therefore also kept as two lists:
+// out_f(x) = {w : m(x,w) >= 1} and out_b(x) = {w : m(w,x) >= 1}, both sorted, in one array `tgs` (all
+// the f lists, then all the b lists; word = id | m << ib with the one multiplicity that list needs,
+// capped at 2^(32 - ib) - 1: read the exact value from out(x) then).  A walk of out(v) for the edge
+// u -> v becomes a walk of out_f(v) when m(u,v) >= 1 plus one of out_b(v) when m(v,u) >= 1; R-MAT's
+// undirected pairs are single-direction for 97 % (class (1,0) or (0,1)), so a walk reads about half the
+// entries.  fbo[2x] / fbo[2x + 1] = start of out_f(x) / out_b(x) (2n + 2 entries, uint32: the lists
+// hold < 2^32 entries whenever the packed in-keys are used).  Exclusive ranks: rk[2e] = the f-entries
+// before oriented edge e, rk[2e + 1] = nF + the b-entries before it (the in-lists' prefix lengths).
+constexpr int kSplitTile = 2048;  // 256 lanes x 8 consecutive edges
+
+__device__ __forceinline__ void split_flags(uint32_t w, TgCode tc, uint32_t& f, uint32_t& b) {
+    f = (w >> tc.ib) & tc.cmask();
+    b = (w >> (tc.ib + tc.cb)) & tc.cmask();
+}
+
+__global__ void __launch_bounds__(256) k_split_count(const uint32_t* __restrict__ tg, int64_t ne, TgCode tc,
+                                                     int64_t* __restrict__ cnt, int64_t ntiles) {
+    const int64_t base = (int64_t)blockIdx.x * kSplitTile + (int64_t)threadIdx.x * 8;
+    int64_t cf = 0, cb = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (base + j < ne) {
+            uint32_t f, b;
+            split_flags(tg[base + j], tc, f, b);
+            cf += f != 0;
+            cb += b != 0;
+        }
+    for (int o = 32; o > 0; o >>= 1) {
+        cf += __shfl_down(cf, o, 64);
+        cb += __shfl_down(cb, o, 64);
+    }
+    __shared__ int64_t s[2][4];
+    if ((threadIdx.x & 63) == 0) {
+        s[0][threadIdx.x >> 6] = cf;
+        s[1][threadIdx.x >> 6] = cb;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        cnt[blockIdx.x] = s[0][0] + s[0][1] + s[0][2] + s[0][3];
+        cnt[ntiles + 1 + blockIdx.x] = s[1][0] + s[1][1] + s[1][2] + s[1][3];
+    }
+}
+
+// tile-exclusive ranks, the split words and rk; pre = the tiles' exclusive f / b prefix sums
+// (pre[0, ntiles], pre[ntiles + 1, 2 ntiles + 1])
+__global__ void __launch_bounds__(256) k_split_write(const uint32_t* __restrict__ tg, const int64_t* __restrict__ ov,
+                                                     int64_t ne, TgCode tc, const int64_t* __restrict__ pre,
+                                                     int64_t ntiles, uint32_t* __restrict__ tgs,
+                                                     uint32_t* __restrict__ rk) {
+    const int64_t base = (int64_t)blockIdx.x * kSplitTile + (int64_t)threadIdx.x * 8;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t w[8];
+    uint32_t cf = 0, cb = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        w[j] = base + j < ne ? tg[base + j] : 0u;
+        uint32_t f, b;
+        split_flags(w[j], tc, f, b);
+        cf += f != 0;
+        cb += b != 0;
+    }
+    // block-exclusive scan of the packed (f, b) counts (each < 2^16 per tile)
+    const uint32_t mine = cf | cb << 16;
+    uint32_t x = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    __shared__ uint32_t wt[4];
+    if (lane == 63) wt[wave] = x;
+    __syncthreads();
+    uint32_t wb = 0;
+    for (int q = 0; q < wave; ++q) wb += wt[q];
+    const uint32_t ex = x - mine + wb;
+    const int64_t nF = pre[ntiles];
+    int64_t rf = pre[blockIdx.x] + (ex & 0xFFFFu), rb = nF + pre[ntiles + 1 + blockIdx.x] + (ex >> 16);
+    const uint32_t cap = ~0u >> tc.ib, idm = tc.idmask();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int64_t e = base + j;
+        if (e >= ne) break;
+        uint32_t f, b;
+        split_flags(w[j], tc, f, b);
+        rk[2 * e] = (uint32_t)rf;
+        rk[2 * e + 1] = (uint32_t)rb;
+        if (f == tc.cmask() || b == tc.cmask()) {  // an exception: the exact multiplicities
+            const uint64_t p = (uint64_t)ov[e];
+            f = (uint32_t)min<uint64_t>(p >> 32, cap);
+            b = (uint32_t)min<uint64_t>(p & 0xffffffffULL, cap);
+        }
+        if (f) tgs[rf++] = (w[j] & idm) | f << tc.ib;
+        if (b) tgs[rb++] = (w[j] & idm) | b << tc.ib;
+    }
+}
+
+// list starts: fbo[2x] = rk_f at off[x] (nF past the last edge), fbo[2x + 1] likewise for the b lists
+__global__ void k_split_off(const int64_t* __restrict__ off, int64_t n, int64_t ne, const uint32_t* __restrict__ rk,
+                            uint32_t nF, uint32_t nFB, uint32_t* __restrict__ fbo) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x <= n; x += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = off[x];
+        fbo[2 * x] = e < ne ? rk[2 * e] : nF;
+        fbo[2 * x + 1] = e < ne ? rk[2 * e + 1] : nFB;
+    }
+}
+
+// in-list records of the split walks, in oriented-edge order (sequential reads; `to` is a hub, its
+// offsets cached): rec[e] = from | the edge's multiplicity codes (a coded word whose id is the source)
+// in the low word, pf | pb << 16 (the f / b entries of out(from) below `to`) in the high word -- 0 when
+// v-mode does not take the edge (p >= od(to): u-mode walks it); the in-key to << 40 | e, sorted on the
+// digits of `to` (stable: edge order within a target); the v-mode items read the records through it
+__global__ void k_swap_keys_sp(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ off, int64_t ne,
+                               TgCode tc, const uint32_t* __restrict__ tg, const uint32_t* __restrict__ rk,
+                               const uint32_t* __restrict__ fbo, uint64_t* __restrict__ ik, uint64_t* __restrict__ rec) {
+    const uint32_t idm = tc.idmask();
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = ok_[e];
+        const uint32_t from = (uint32_t)(k >> 32), to = (uint32_t)k & idm;
+        const bool take = e - off[from] < off[to + 1] - off[to];
+        const uint32_t pfb = take ? (rk[2 * e] - fbo[2 * from]) | (rk[2 * e + 1] - fbo[2 * from + 1]) << 16 : 0u;
+        rec[e] = (uint64_t)(from | (tg[e] & ~idm)) | (uint64_t)pfb << 32;
+        ik[e] = (uint64_t)to << 40 | (uint64_t)e;
+    }
+}
+
+// the selected edges' in-keys and records (a distributed build's share; sel in edge order)
+__global__ void k_swap_keys_sp_sel(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ off,
+                                   const int64_t* __restrict__ sel, int64_t nsel, TgCode tc,
+                                   const uint32_t* __restrict__ tg, const uint32_t* __restrict__ rk,
+                                   const uint32_t* __restrict__ fbo, uint64_t* __restrict__ ik, uint64_t* __restrict__ rec) {
+    const uint32_t idm = tc.idmask();
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nsel; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = sel[i];
+        const uint64_t k = ok_[e];
+        const uint32_t from = (uint32_t)(k >> 32), to = (uint32_t)k & idm;
+        const uint32_t pfb = (rk[2 * e] - fbo[2 * from]) | (rk[2 * e + 1] - fbo[2 * from + 1]) << 16;  // taken
+        rec[i] = (uint64_t)(from | (tg[e] & ~idm)) | (uint64_t)pfb << 32;
+        ik[i] = (uint64_t)to << 40 | (uint64_t)i;
+    }
+}
+
+constexpr uint64_t kInRecMask = (uint64_t(1) << 40) - 1;  // the record index of a split in-key
+
 // v-mode centers: od(v) >= vmt with at least one in-edge
 __global__ void k_tri_vm_bins(const int64_t* __restrict__ off, const int64_t* __restrict__ ioff, int64_t n, int vmt,
                               uint8_t* __restrict__ f) {
@@ -873,6 +1019,334 @@ __global__ void __launch_bounds__(B, 8) k_tri_big_items(const uint32_t* __restri
     if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
 }
 
+// ---- walks over the direction-split lists (k_split_write) ---------------------------------------------
+// The exact multiplicity payload of x -> w (w in out(x)): a search of the sorted out(x) -- only for a
+// split word at its cap or an in-list word whose codes are an exception (rare: m >= 2^(32 - ib) - 1 / 15)
+__device__ __forceinline__ uint64_t exact_pay(const uint32_t* __restrict__ tg, TgCode tc, const int64_t* __restrict__ ov,
+                                           const int64_t* __restrict__ off, uint32_t x, uint32_t w) {
+    int64_t lo = off[x], hi = off[x + 1];
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (tid(tg[mid], tc) < w) lo = mid + 1; else hi = mid;
+    }
+    return tpay(tg[lo], tc, ov, lo);
+}
+
+// m of a split word: the list's multiplicity (f list of x: m(x,w); b list: m(w,x))
+__device__ __forceinline__ uint64_t split_m(uint32_t word, TgCode tc, bool bl, const uint32_t* __restrict__ tg,
+                                            const int64_t* __restrict__ ov, const int64_t* __restrict__ off, uint32_t x) {
+    const uint32_t m = word >> tc.ib, cap = ~0u >> tc.ib;
+    if (m != cap) return m;
+    const uint64_t p = exact_pay(tg, tc, ov, off, x, tid(word, tc));
+    return bl ? (p & 0xffffffffULL) : (p >> 32);
+}
+
+// the hit's third factor from the hashed entry's payload ph = (m(c,w), m(w,c)): an f list closes through
+// m(w,c), a b list through m(c,w)
+__device__ __forceinline__ uint64_t split_field(uint64_t ph, bool bl) { return bl ? (ph >> 32) : (ph & 0xffffffffULL); }
+
+struct SmallWaveSp {
+    uint32_t bf[(1 << kSmallBloomBits) / 32];
+    uint32_t hk[kSmallSlots];
+    uint8_t hi[kSmallSlots];     // lane of the key's entry: payload = vp[hi]
+    uint64_t vp[kSmallDeg];      // payload of u -> v
+    uint32_t vl[kSmallDeg];      // v (exact multiplicities)
+    uint32_t lo[2 * kSmallDeg];  // list l (f: l < 64, b: l >= 64) of v = l & 63: tgs[lo, lo + ln)
+    uint32_t ln[2 * kSmallDeg];
+    uint32_t kq[2 * kSmallDeg];  // its constant factor: m(u,v) (f) / m(v,u) (b)
+};
+
+// k_tri_small over the split lists: each v of out(u) gives an f and a b list (either may be empty)
+template <int U>
+__global__ void __launch_bounds__(kTriBlock) k_tri_small_sp(const uint32_t* __restrict__ tg, TgCode tc,
+                                                            const int64_t* __restrict__ ov,
+                                                            const int64_t* __restrict__ off,
+                                                            const uint32_t* __restrict__ tgs,
+                                                            const uint32_t* __restrict__ fbo, int vmt,
+                                                            const int64_t* __restrict__ us, int64_t nu,
+                                                            unsigned long long* __restrict__ out) {
+    __shared__ SmallWaveSp sw[kTriBlock / 64];
+    SmallWaveSp& W = sw[threadIdx.x >> 6];
+    const int lane = threadIdx.x & 63;
+    unsigned long long acc = 0;
+    const int64_t nwaves = (int64_t)gridDim.x * (kTriBlock / 64);
+    for (int64_t q = (int64_t)blockIdx.x * (kTriBlock / 64) + (threadIdx.x >> 6); q < nu; q += nwaves) {
+        const int64_t u = us[q];
+        const int64_t b = off[u];
+        const int d = (int)(off[u + 1] - b);
+#pragma unroll
+        for (int k = 0; k < kSmallSlots / 64; ++k) W.hk[lane + 64 * k] = kEmpty;
+        if (lane < (1 << kSmallBloomBits) / 32) W.bf[lane] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        uint32_t lf = 0, lb = 0;
+        if (lane < d) {
+            const uint32_t word = tg[b + lane], v = tid(word, tc);
+            const uint64_t pv = tpay(word, tc, ov, b + lane);
+            const uint32_t dv = (uint32_t)(off[v + 1] - off[v]);
+            const bool skip = vmt > 0 && dv >= (uint32_t)vmt && (uint32_t)lane < dv;  // v-mode takes u -> v
+            const uint32_t f0 = fbo[2 * v], b0 = fbo[2 * v + 1], f1 = fbo[2 * v + 2], b1 = fbo[2 * v + 3];
+            const uint32_t kf = (uint32_t)(pv >> 32), kb = (uint32_t)pv;
+            lf = skip || !kf ? 0u : f1 - f0;
+            lb = skip || !kb ? 0u : b1 - b0;
+            W.vl[lane] = v;
+            W.vp[lane] = pv;
+            W.lo[lane] = f0;
+            W.ln[lane] = lf;
+            W.kq[lane] = kf;
+            W.lo[64 + lane] = b0;
+            W.ln[64 + lane] = lb;
+            W.kq[64 + lane] = kb;
+            hinsert(W.hk, W.hi, 9, v, v, (uint32_t)lane);
+            bset(W.bf, kSmallBloomBits, v);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        auto hit = [&](int l, uint32_t word, int sl) {
+            const bool bl = l >= 64;
+            const uint64_t m = split_m(word, tc, bl, tg, ov, off, W.vl[l & 63]);
+            acc += (unsigned long long)W.kq[l] * m * split_field(W.vp[W.hi[sl]], bl);
+        };
+        // lists of <= 64 / <= 128 entries four / two per pass (16 / 32 lanes, 4 loads each)
+        auto grouped = [&](uint64_t mask, int sgl, int ko) {
+            const int per = 64 >> sgl, sg = 1 << sgl, g = lane >> sgl, e = lane & (sg - 1);
+            while (mask) {  // wave-uniform
+                uint64_t m = mask;
+                for (int i = 0; i < g; ++i) m &= m - 1;
+                const bool live = m != 0;
+                const int l = __builtin_ctzll(live ? m : mask) + ko;
+                for (int i = 0; i < per; ++i) mask &= mask - 1;
+                const uint32_t lo = W.lo[l];
+                const uint32_t dvk = live ? W.ln[l] : 0u, last = (dvk ? dvk : 1u) - 1u;
+                uint32_t w[4], word[4], bit[4], keep = 0;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) w[t] = tgs[(int64_t)lo + min((uint32_t)(e + sg * t), last)];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    bit[t] = bbit(tid(w[t], tc), kSmallBloomBits);
+                    word[t] = W.bf[bit[t] >> 5];
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t)
+                    keep |= ((uint32_t)((uint32_t)(e + sg * t) < dvk) & (word[t] >> (bit[t] & 31))) << t;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    if (!((keep >> t) & 1u)) continue;
+                    const int sl = hfind(W.hk, 9, tid(w[t], tc), ~0u);
+                    if (sl >= 0) hit(l, w[t], sl);
+                }
+            }
+        };
+        auto longs = [&](uint64_t lm, int ko) {
+            while (lm) {  // wave-uniform
+                const int l = __builtin_ctzll(lm) + ko;
+                lm &= lm - 1;
+                const int64_t lo = (int64_t)__builtin_amdgcn_readfirstlane(W.lo[l]);
+                const uint32_t dvk = __builtin_amdgcn_readfirstlane(W.ln[l]);
+                for (int j0 = lane; j0 < (int)dvk; j0 += U * 64) {
+                    uint32_t w[U], keep;
+                    list_pass<U>(tgs, tc, lo, (int)dvk, j0, W.bf, kSmallBloomBits, w, keep);
+#pragma unroll
+                    for (int r = 0; r < U; ++r) {
+                        if (!((keep >> r) & 1u)) continue;
+                        const int sl = hfind(W.hk, 9, tid(w[r], tc), ~0u);
+                        if (sl >= 0) hit(l, w[r], sl);
+                    }
+                }
+            }
+        };
+        grouped(__ballot(lf > 0u && lf <= 64u), 4, 0);
+        grouped(__ballot(lb > 0u && lb <= 64u), 4, 64);
+        grouped(__ballot(lf > 64u && lf <= 128u), 5, 0);
+        grouped(__ballot(lb > 64u && lb <= 128u), 5, 64);
+        longs(__ballot(lf > 128u), 0);
+        longs(__ballot(lb > 128u), 64);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the wave's LDS is reused for the next u
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if (lane == 0 && acc) atomicAdd(out, acc);
+}
+
+// Items over the split lists: a chunk holds kVChunk / 2 edges, i.e. kVChunk lists (2e: f, 2e + 1: b),
+// and an item walks kVGroupSp chunks -- the same kVChunk * kVGroup edges per item as k_tri_big_items
+constexpr int kEChunkSp = kVChunk / 2, kVGroupSp = 2 * kVGroup;
+
+template <int B>
+struct ItemLdsSp {
+    static constexpr int kChunk = 2 * B, kSlots = 4 * kChunk;
+    uint32_t bf[(1 << kBigBloomBits) / 32];
+    uint32_t hk[kSlots];
+    uint16_t hi[kSlots];
+    uint32_t lo[kVChunk];  // list l: tgs[lo, lo + ln), constant factor kq
+    uint32_t ln[kVChunk];
+    uint32_t kq[kVChunk];
+    uint32_t vl[kEChunkSp];  // the lists' owner: v (u-mode) / u (v-mode)
+    uint16_t lk[kVChunk], sk[kVChunk], mk[kVChunk];  // long / short / medium lists
+    uint32_t ncnt[6];
+    unsigned long long item;
+};
+
+// k_tri_big_items (LISTS) over the split lists.  u-mode: the lists of edge u -> v are out_f(v) (when
+// m(u,v) >= 1; factor m(u,v)) and out_b(v) (m(v,u)); v-mode (center c, in-edge u -> c): the prefixes of
+// out_f(u) (factor m(c,u)) and out_b(u) (factor m(u,c)) below c, of lengths pf / pb from ipos.
+template <int U, bool VM, int B>
+__global__ void __launch_bounds__(B, 8) k_tri_items_sp(const uint32_t* __restrict__ tg, TgCode tc,
+                                                        const int64_t* __restrict__ ov,
+                                                        const int64_t* __restrict__ off,
+                                                        const uint32_t* __restrict__ tgs,
+                                                        const uint32_t* __restrict__ fbo,
+                                                        const int64_t* __restrict__ ioff,
+                                                        const uint64_t* __restrict__ ikey,
+                                                        const uint64_t* __restrict__ irec, int vmt,
+                                                        const int64_t* __restrict__ us, int64_t total,
+                                                        const uint64_t* __restrict__ item_ql,
+                                                        unsigned long long* __restrict__ ctr,
+                                                        unsigned long long* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+    ItemLdsSp<B>& L = *reinterpret_cast<ItemLdsSp<B>*>(lds_raw);
+    constexpr int CH = ItemLdsSp<B>::kChunk;
+    unsigned long long& item = L.item;
+    unsigned long long acc = 0;
+    while (true) {
+        if (threadIdx.x == 0) item = atomicAdd(ctr, 1ULL);
+        __syncthreads();
+        const int64_t it = (int64_t)item;
+        __syncthreads();  // `item` is rewritten next round
+        if (it >= total) break;  // block-uniform
+        const uint64_t iw = item_ql[it];
+        const int64_t c = us[(uint32_t)iw], b = uniform64(off[c]);  // the center (u-mode: u; v-mode: v)
+        const int d = (int)(off[c + 1] - b);
+        const int64_t nb = VM ? uniform64(ioff[c]) : b;  // its neighbour list: in(v) / out(u)
+        const int nd = VM ? (int)(ioff[c + 1] - nb) : d;
+        const int nvc = (nd + kEChunkSp - 1) / kEChunkSp, ngr = (nvc + kVGroupSp - 1) / kVGroupSp;
+        const int local = (int)(iw >> 32);
+        const int h0 = (local / ngr) * CH, c0 = (local % ngr) * kVGroupSp, c1 = min(nvc, c0 + kVGroupSp);
+        const int hn = min(CH, d - h0);
+        int lc = 6;  // hash capacity 2^lc >= 4 hn (load <= 1/4), cleared as far as it is used
+        while ((1 << lc) < 4 * hn) ++lc;
+        for (int k = threadIdx.x; k < (1 << lc); k += B) L.hk[k] = kEmpty;
+        for (int k = threadIdx.x; k < (1 << kBigBloomBits) / 32; k += B) L.bf[k] = 0;
+        if (threadIdx.x < 6) L.ncnt[threadIdx.x] = 0;
+        __syncthreads();
+        for (int k = threadIdx.x; k < hn; k += B) {
+            const uint32_t word = tg[b + h0 + k], w = tid(word, tc);
+            hinsert(L.hk, L.hi, lc, w, word, (uint32_t)k);
+            bset(L.bf, kBigBloomBits, w);
+        }
+        for (int ch = c0; ch < c1; ++ch) {  // block-uniform
+            const int v0 = ch * kEChunkSp, vn = min(kEChunkSp, nd - v0);
+            if (ch > c0) __syncthreads();  // the previous chunk's walks are done with the list table
+            uint32_t* nc = L.ncnt + 3 * (ch & 1);
+            if (threadIdx.x < 3) L.ncnt[3 * ((ch + 1) & 1) + threadIdx.x] = 0;  // read last by chunk ch - 1
+            for (int k = threadIdx.x; k < vn; k += B) {
+                uint32_t x, f0, b0, lf, lb, kf, kb;
+                if (VM) {  // in-edge x -> c: prefixes of out_f(x) / out_b(x) below c
+                    const uint64_t r = irec[ikey[nb + v0 + k] & kInRecMask];
+                    const uint32_t word = (uint32_t)r;
+                    x = tid(word, tc);
+                    const uint32_t fc = (word >> tc.ib) & tc.cmask(), bc = (word >> (tc.ib + tc.cb)) & tc.cmask();
+                    uint64_t p = (uint64_t)fc << 32 | bc;
+                    if (fc == tc.cmask() || bc == tc.cmask()) p = exact_pay(tg, tc, ov, off, x, (uint32_t)c);
+                    kf = (uint32_t)p;           // m(c, x)
+                    kb = (uint32_t)(p >> 32);   // m(x, c)
+                    const uint32_t ip = (uint32_t)(r >> 32);
+                    f0 = fbo[2 * x];
+                    b0 = fbo[2 * x + 1];
+                    lf = kf ? ip & 0xFFFFu : 0u;
+                    lb = kb ? ip >> 16 : 0u;
+                } else {  // out-edge c -> x: out_f(x) / out_b(x) unless v-mode takes the edge
+                    const uint32_t word = tg[b + v0 + k];
+                    x = tid(word, tc);
+                    const uint64_t p = tpay(word, tc, ov, b + v0 + k);
+                    kf = (uint32_t)(p >> 32);   // m(c, x)
+                    kb = (uint32_t)p;           // m(x, c)
+                    const uint32_t dv = (uint32_t)(off[x + 1] - off[x]);
+                    const bool skip = vmt > 0 && dv >= (uint32_t)vmt && (uint32_t)(v0 + k) < dv;
+                    f0 = fbo[2 * x];
+                    b0 = fbo[2 * x + 1];
+                    lf = skip || !kf ? 0u : fbo[2 * x + 2] - f0;
+                    lb = skip || !kb ? 0u : fbo[2 * x + 3] - b0;
+                }
+                L.vl[k] = x;
+                L.lo[2 * k] = f0;
+                L.ln[2 * k] = lf;
+                L.kq[2 * k] = kf;
+                L.lo[2 * k + 1] = b0;
+                L.ln[2 * k + 1] = lb;
+                L.kq[2 * k + 1] = kb;
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const uint32_t dw = t ? lb : lf;
+                    const uint16_t l = (uint16_t)(2 * k + t);
+                    if (dw > 8u * kSG) L.lk[atomicAdd(&nc[0], 1u)] = l;
+                    else if (dw > 4u * kSG) L.mk[atomicAdd(&nc[2], 1u)] = l;
+                    else if (dw > 0u) L.sk[atomicAdd(&nc[1], 1u)] = l;
+                }
+            }
+            __syncthreads();
+            const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+            const int nlong = (int)__builtin_amdgcn_readfirstlane(nc[0]);
+            const int nshort = (int)__builtin_amdgcn_readfirstlane(nc[1]);
+            const int nmed = (int)__builtin_amdgcn_readfirstlane(nc[2]);
+            auto hit = [&](int l, uint32_t word, int sl) {
+                const bool bl = l & 1;
+                const uint64_t m = split_m(word, tc, bl, tg, ov, off, L.vl[l >> 1]);
+                const uint64_t pcw = tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]);
+                acc += (unsigned long long)L.kq[l] * m * split_field(pcw, bl);
+            };
+            auto grouped = [&](const uint16_t* ks, int nk, int sgl) {
+                const int per = 64 >> sgl, sg = 1 << sgl;
+                for (int q0 = wave * per; q0 < nk; q0 += (B / 64) * per) {
+                    const int g = lane >> sgl, e = lane & (sg - 1);
+                    const bool live = q0 + g < nk;
+                    const int l = ks[live ? q0 + g : q0];
+                    const uint32_t lo = L.lo[l];
+                    const uint32_t dvk = live ? L.ln[l] : 0u, last = (dvk ? dvk : 1u) - 1u;
+                    uint32_t w[4], word[4], bit[4], keep = 0;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) w[t] = tgs[(int64_t)lo + min((uint32_t)(e + sg * t), last)];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        bit[t] = bbit(tid(w[t], tc), kBigBloomBits);
+                        word[t] = L.bf[bit[t] >> 5];
+                    }
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        keep |= ((uint32_t)((uint32_t)(e + sg * t) < dvk) & (word[t] >> (bit[t] & 31))) << t;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        if (!((keep >> t) & 1u)) continue;
+                        const int sl = hfind(L.hk, lc, tid(w[t], tc), tc.idmask());
+                        if (sl >= 0) hit(l, w[t], sl);
+                    }
+                }
+            };
+            grouped(L.sk, nshort, kSG == 8 ? 3 : kSG == 16 ? 4 : 5);
+            grouped(L.mk, nmed, kSG == 8 ? 4 : kSG == 16 ? 5 : 6);
+            for (int q = wave; q < nlong; q += B / 64) {  // long lists: one per wave, U x 64 entries a pass
+                const int l = L.lk[q];
+                const int64_t lo = (int64_t)__builtin_amdgcn_readfirstlane(L.lo[l]);
+                const int dv = (int)__builtin_amdgcn_readfirstlane(L.ln[l]);
+                for (int j0 = lane; j0 < dv; j0 += U * 64) {
+                    uint32_t w[U], keep;
+                    list_pass<U>(tgs, tc, lo, dv, j0, L.bf, kBigBloomBits, w, keep);
+#pragma unroll
+                    for (int r = 0; r < U; ++r) {
+                        if (!((keep >> r) & 1u)) continue;
+                        const int sl = hfind(L.hk, lc, tid(w[r], tc), tc.idmask());
+                        if (sl >= 0) hit(l, w[r], sl);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+
 // u with 2 <= out-degree: small (<= 64) and big lists; also the 4-byte target array
 __global__ void k_tri_bins(const int64_t* __restrict__ off, int64_t n, uint8_t* __restrict__ fs,
                            uint8_t* __restrict__ fb) {
@@ -1050,8 +1524,10 @@ __global__ void k_tri_work_u1(const int64_t* __restrict__ cs, int64_t nc, const 
 }
 
 // work of a v-mode center: out(v) for the hash and the prefix out(u)[0, p) of every in-edge it takes
+// (split: ipos = pf | pb << 16, both walked, 0 for the edges it does not take)
 __global__ void k_tri_work_v(const int64_t* __restrict__ cs, int64_t nc, const int64_t* __restrict__ off,
                              const int64_t* __restrict__ ioff, const uint32_t* __restrict__ ipos,
+                             const uint64_t* __restrict__ ikey, const uint64_t* __restrict__ irec,
                              int64_t* __restrict__ w) {
     const int lane = threadIdx.x & 63;
     for (int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < nc;
@@ -1059,6 +1535,11 @@ __global__ void k_tri_work_v(const int64_t* __restrict__ cs, int64_t nc, const i
         const int64_t v = cs[c], odv = off[v + 1] - off[v];
         int64_t acc = 0;
         for (int64_t j = ioff[v] + lane; j < ioff[v + 1]; j += 64) {
+            if (irec) {  // split: (pf, pb), 0 for the edges v-mode does not take
+                const uint32_t p = (uint32_t)(irec[ikey[j] & kInRecMask] >> 32);
+                acc += (p & 0xFFFFu) + (p >> 16);
+                continue;
+            }
             const int64_t p = ipos[j];
             if (p < odv) acc += p;
         }
@@ -1290,16 +1771,44 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     g.tg = dev_alloc(sizeof(uint32_t) * (ne > 0 ? ne : 1), s);
     if (ne > 0)
         hipLaunchKernelGGL(k_targets, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, P<uint32_t>(g.tg));
+    // packed in-keys (key-only sort) when ids and positions fit: od(u) <= sqrt(2m) under a degree
+    // order (every out-neighbour has at least u's degree), so m < 2^31 relationships bound it by 2^16
+    const bool packed = g.ib <= 24 && m_all < (int64_t(1) << 31);
+    // direction-split lists (coded targets; CAPSMI_TRI_SPLIT=0: the combined walks, A/B)
+    // (the flat walk of the A/B runs reads the combined in-lists: no split under CAPSMI_TRI_WALK=flat)
+    const char* spe = getenv("CAPSMI_TRI_SPLIT");
+    const char* wke = getenv("CAPSMI_TRI_WALK");
+    g.split = tc.cb > 0 && packed && ne > 0 && !(spe && atoi(spe) == 0) && !(wke && std::string(wke) == "flat");
+    Buf rk;  // per oriented edge: f / b ranks (the in-lists' prefix lengths)
+    if (g.split) {
+        const int64_t ntiles = (ne + kSplitTile - 1) / kSplitTile;
+        Buf cnt = dev_alloc(sizeof(int64_t) * 2 * (ntiles + 1), s), pre = dev_alloc(sizeof(int64_t) * 2 * (ntiles + 1), s);
+        hipLaunchKernelGGL(k_split_count, dim3((unsigned)ntiles), dim3(256), 0, st, P<uint32_t>(g.tg), ne, tc,
+                           P<int64_t>(cnt), ntiles);
+        HIP_CHECK(hipGetLastError());
+        exclusive_scan_i64(P<int64_t>(cnt), P<int64_t>(pre), ntiles, s);
+        exclusive_scan_i64(P<int64_t>(cnt) + ntiles + 1, P<int64_t>(pre) + ntiles + 1, ntiles, s);
+        const int64_t nF = read_scalar(s, P<int64_t>(pre) + ntiles);
+        const int64_t nB = read_scalar(s, P<int64_t>(pre) + 2 * ntiles + 1);
+        REQUIRE(nF + nB < (int64_t(1) << 32), CAPSMI_ERR_INTERNAL, "split lists exceed 2^32 entries");
+        g.tgs = dev_alloc(sizeof(uint32_t) * (nF + nB > 0 ? nF + nB : 1), s);
+        rk = dev_alloc(sizeof(uint32_t) * 2 * ne, s);
+        hipLaunchKernelGGL(k_split_write, dim3((unsigned)ntiles), dim3(256), 0, st, P<uint32_t>(g.tg), P<int64_t>(g.ov),
+                           ne, tc, P<int64_t>(pre), ntiles, P<uint32_t>(g.tgs), P<uint32_t>(rk));
+        g.fbo = dev_alloc(sizeof(uint32_t) * (2 * n + 2), s);
+        hipLaunchKernelGGL(k_split_off, dim3(grid(s, n + 1)), dim3(256), 0, st, P<int64_t>(g.off), n, ne,
+                           P<uint32_t>(rk), (uint32_t)nF, (uint32_t)(nF + nB), P<uint32_t>(g.fbo));
+        HIP_CHECK(hipGetLastError());
+    }
     // in-lists and v-mode centers (CAPSMI_TRI_VMODE_T: the od(v) threshold; 0 = every edge from u)
     const char* vt = getenv("CAPSMI_TRI_VMODE_T");
     g.vmt = vt ? atoi(vt) : 256;
     if (g.vmt > 0 && ne > 0) {
-        // packed in-keys (key-only sort) when ids and positions fit: od(u) <= sqrt(2m) under a degree
-        // order (every out-neighbour has at least u's degree), so m < 2^31 relationships bound it by 2^16
-        const bool packed = g.ib <= 24 && m_all < (int64_t(1) << 31);
         const int tsh = packed ? g.ib + 16 : 32;
         std::vector<int> td;  // by (to, from): the input is in (from, to) order and the LSD sort is stable, so
         for (int sh = tsh; sh < tsh + bits; sh += 8) td.push_back(sh);  // the digits of `to` alone give that order
+        std::vector<int> tds;  // split: in-key to << 40 | edge index
+        for (int sh = 40; sh < 40 + bits; sh += 8) tds.push_back(sh);
         if (dd && packed && dd->world > 1) {
             // A rank walks only its v-mode share, so it builds only that share's in-lists (the whole
             // in-list sort was ≈6 ms of every rank's replicated post-processing at s = 24): the v-mode
@@ -1343,34 +1852,56 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
             HIP_CHECK(hipGetLastError());
             const int64_t nsel = flags_to_indices(s, P<uint8_t>(f), ne, sel);
             f.reset();
-            Buf ik = dev_alloc(sizeof(uint64_t) * (nsel > 0 ? nsel : 1), s);
-            if (nsel > 0)
+            Buf ik = dev_alloc(sizeof(uint64_t) * (nsel > 0 ? nsel : 1), s), rec;
+            if (g.split) rec = dev_alloc(sizeof(uint64_t) * (nsel > 0 ? nsel : 1), s);
+            if (nsel > 0 && g.split)
+                hipLaunchKernelGGL(k_swap_keys_sp_sel, dim3(grid(s, nsel)), dim3(256), 0, st, P<uint64_t>(g.ok),
+                                   P<int64_t>(g.off), P<int64_t>(sel), nsel, tc, P<uint32_t>(g.tg), P<uint32_t>(rk),
+                                   P<uint32_t>(g.fbo), P<uint64_t>(ik), P<uint64_t>(rec));
+            else if (nsel > 0)
                 hipLaunchKernelGGL(k_swap_keys_sel, dim3(grid(s, nsel)), dim3(256), 0, st, P<uint64_t>(g.ok),
                                    P<int64_t>(g.off), P<int64_t>(sel), nsel, tc, P<uint64_t>(ik));
             sel.reset();
-            radix_sort_digits(s, P<uint64_t>(ik), nullptr, nsel, td);
+            radix_sort_digits(s, P<uint64_t>(ik), nullptr, nsel, g.split ? tds : td);
             g.ioff = dev_alloc(sizeof(int64_t) * (n + 1), s);
-            hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), nsel, n, tsh,
-                               P<int64_t>(g.ioff));
-            g.itg = dev_alloc(sizeof(uint32_t) * (nsel > 0 ? nsel : 1), s);
-            g.ipos = dev_alloc(sizeof(uint32_t) * (nsel > 0 ? nsel : 1), s);
-            if (nsel > 0)
+            hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), nsel, n,
+                               g.split ? 40 : tsh, P<int64_t>(g.ioff));
+            if (g.split) {
+                g.ikey = std::move(ik);
+                g.irec = std::move(rec);
+            } else {
+                g.itg = dev_alloc(sizeof(uint32_t) * (nsel > 0 ? nsel : 1), s);
+                g.ipos = dev_alloc(sizeof(uint32_t) * (nsel > 0 ? nsel : 1), s);
+            }
+            if (nsel > 0 && !g.split)
                 hipLaunchKernelGGL(k_in_split, dim3(grid(s, nsel)), dim3(256), 0, st, P<uint64_t>(ik), nullptr,
                                    P<int64_t>(g.off), nsel, tc, P<uint32_t>(g.itg), P<uint32_t>(g.ipos));
             g.vm_own = true;
         } else {
-            Buf ik = dev_alloc(sizeof(uint64_t) * ne, s), iv = packed ? Buf() : dev_alloc(sizeof(int64_t) * ne, s);
-            hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off), ne,
-                               tc, P<uint64_t>(ik), packed ? nullptr : P<int64_t>(iv));
-            radix_sort_digits(s, P<uint64_t>(ik), packed ? nullptr : P<int64_t>(iv), ne, td);
+            Buf ik = dev_alloc(sizeof(uint64_t) * ne, s), iv = packed && !g.split ? Buf() : dev_alloc(sizeof(int64_t) * ne, s);
+            if (g.split)  // iv: the records (k_swap_keys_sp)
+                hipLaunchKernelGGL(k_swap_keys_sp, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off),
+                                   ne, tc, P<uint32_t>(g.tg), P<uint32_t>(rk), P<uint32_t>(g.fbo), P<uint64_t>(ik),
+                                   P<uint64_t>(iv));
+            else
+                hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off), ne,
+                                   tc, P<uint64_t>(ik), packed ? nullptr : P<int64_t>(iv));
+            rk.reset();
+            radix_sort_digits(s, P<uint64_t>(ik), packed || g.split ? nullptr : P<int64_t>(iv), ne, g.split ? tds : td);
             g.ioff = dev_alloc(sizeof(int64_t) * (n + 1), s);
-            hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), ne, n, tsh,
-                               P<int64_t>(g.ioff));
-            g.itg = dev_alloc(sizeof(uint32_t) * ne, s);
-            g.ipos = dev_alloc(sizeof(uint32_t) * ne, s);
-            hipLaunchKernelGGL(k_in_split, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(ik),
-                               packed ? nullptr : P<int64_t>(iv), P<int64_t>(g.off), ne, tc, P<uint32_t>(g.itg),
-                               P<uint32_t>(g.ipos));
+            hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), ne, n,
+                               g.split ? 40 : tsh, P<int64_t>(g.ioff));
+            if (g.split) {
+                g.ikey = std::move(ik);
+                g.irec = std::move(iv);
+            } else {
+                g.itg = dev_alloc(sizeof(uint32_t) * ne, s);
+                g.ipos = dev_alloc(sizeof(uint32_t) * ne, s);
+            }
+            if (!g.split)
+                hipLaunchKernelGGL(k_in_split, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(ik),
+                                   packed ? nullptr : P<int64_t>(iv), P<int64_t>(g.off), ne, tc, P<uint32_t>(g.itg),
+                                   P<uint32_t>(g.ipos));
         }
         Buf fvm = dev_alloc(n, s);
         hipLaunchKernelGGL(k_tri_vm_bins, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), P<int64_t>(g.ioff), n,
@@ -1401,7 +1932,8 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
                                        P<int64_t>(g.off), P<uint32_t>(g.tg), tc.idmask(), g.vmt, P<int64_t>(w));
                 else if (vm)
                     hipLaunchKernelGGL(k_tri_work_v, dim3(gw), dim3(256), 0, st, P<int64_t>(cs), nc, P<int64_t>(g.off),
-                                       P<int64_t>(g.ioff), P<uint32_t>(g.ipos), P<int64_t>(w));
+                                       P<int64_t>(g.ioff), P<uint32_t>(g.ipos), P<uint64_t>(g.ikey), P<uint64_t>(g.irec),
+                                       P<int64_t>(w));
                 else
                     hipLaunchKernelGGL(k_tri_work_u, dim3(gw), dim3(256), 0, st, P<int64_t>(cs), nc, P<int64_t>(g.off),
                                        P<uint32_t>(g.tg), tc.idmask(), g.vmt, P<int64_t>(w));
@@ -1429,6 +1961,12 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     }
 }
 
+namespace {
+void set_lds_attr(const void* k, size_t bytes) {
+    HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+}
+}  // namespace
+
 // count for vertex share `part` of `nparts` (each bin sliced evenly); pair/self terms with part 0
 uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
     using namespace tri;
@@ -1455,6 +1993,8 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
         const TgCode tc{(uint32_t)g.ib, (uint32_t)g.cb};
         const char* walk = getenv("CAPSMI_TRI_WALK");  // "flat": the prefix-sum walk (A/B runs)
         const bool lists = !(walk && std::string(walk) == "flat");
+        // split in-lists hold (pf, pb) and coded sources: only the split walks read them
+        REQUIRE(!g.split || lists, CAPSMI_ERR_UNSUPPORTED, "triangle count: the flat walk needs a build without split lists");
         const char* ue = getenv("CAPSMI_TRI_UNROLL");  // target loads in flight per lane: 4 (default), 8 or 16
         const int un = ue ? atoi(ue) : 4;
         // items (hash chunk, neighbour chunk) of the centers cs[0, nc), taken from a global counter
@@ -1482,10 +2022,21 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
                       : B == 512 ? (un == 8 ? k_tri_big_items<true, 8, false, 512> : k_tri_big_items<true, 4, false, 512>)
                       : un == 16 ? k_tri_big_items<true, 16, false, 1024>
                       : un == 8 ? k_tri_big_items<true, 8, false, 1024> : k_tri_big_items<true, 4, false, 1024>;
-            HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kf), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          (int)lds));
             // resident: two 1024-lane or four 512-lane workgroups per CU (LDS), twice that queued
-            hipLaunchKernelGGL(kf, dim3((unsigned)(s->num_cus * (B == 1024 ? 4 : 8))), dim3(B), lds, st,
+            const dim3 ig((unsigned)(s->num_cus * (B == 1024 ? 4 : 8)));
+            if (g.split && lists) {  // the walks over the direction-split lists
+                const size_t ldsp = B == 1024 ? sizeof(ItemLdsSp<1024>) : sizeof(ItemLdsSp<512>);
+                auto kp = vm ? (B == 512 ? k_tri_items_sp<4, true, 512> : k_tri_items_sp<4, true, 1024>)
+                             : (B == 512 ? k_tri_items_sp<4, false, 512> : k_tri_items_sp<4, false, 1024>);
+                set_lds_attr(reinterpret_cast<const void*>(kp), ldsp);
+                hipLaunchKernelGGL(kp, ig, dim3(B), ldsp, st, P<uint32_t>(g.tg), tc, P<int64_t>(g.ov), P<int64_t>(g.off),
+                                   P<uint32_t>(g.tgs), P<uint32_t>(g.fbo), P<int64_t>(g.ioff), P<uint64_t>(g.ikey),
+                                   P<uint64_t>(g.irec), g.vmt, cs, nitems, P<uint64_t>(iq), P<unsigned long long>(ctr),
+                                   P<unsigned long long>(out));
+                return;
+            }
+            set_lds_attr(reinterpret_cast<const void*>(kf), lds);
+            hipLaunchKernelGGL(kf, ig, dim3(B), lds, st,
                                P<uint32_t>(g.tg), tc, P<int64_t>(g.ov), P<int64_t>(g.off),
                                P<int64_t>(g.ioff), P<uint32_t>(g.itg), P<uint32_t>(g.ipos), g.vmt, cs, nc, ipre,
                                P<uint64_t>(iq), P<unsigned long long>(ctr),
@@ -1493,7 +2044,12 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
         };
         if (be > bb) run_items(P<int64_t>(g.big_u) + bb, be - bb, false);
         if (ve > vb) run_items(P<int64_t>(g.vm_c) + vb, ve - vb, true);
-        if (se > sb) {
+        if (se > sb && g.split && lists) {
+            const int64_t gs = std::min<int64_t>((se - sb + 3) / 4, (int64_t)s->num_cus * 16);
+            hipLaunchKernelGGL(k_tri_small_sp<4>, dim3((unsigned)gs), dim3(kTriBlock), 0, st, P<uint32_t>(g.tg), tc,
+                               P<int64_t>(g.ov), P<int64_t>(g.off), P<uint32_t>(g.tgs), P<uint32_t>(g.fbo), g.vmt,
+                               P<int64_t>(g.small_u) + sb, se - sb, P<unsigned long long>(out));
+        } else if (se > sb) {
             const int64_t gs = std::min<int64_t>((se - sb + 3) / 4, (int64_t)s->num_cus * 16);
             auto kfs = !lists ? k_tri_small<false, 4>
                        : un == 16 ? k_tri_small<true, 16>

@@ -40,11 +40,16 @@ def _kernels(obj, tmp):
                     reason="k_tri.o not built or no ROCm llvm tools")
 def test_item_kernels_keep_two_items_per_cu(tmp_path):
     ks = _kernels(OBJ, str(tmp_path))
-    items = {k: v for k, v in ks.items() if "k_tri_big_items" in k}
+    items = {k: v for k, v in ks.items() if "k_tri_big_items" in k or "k_tri_items_sp" in k}
     assert items, "no k_tri_big_items kernels in the object"
+    assert any("k_tri_items_sp" in k for k in items), "no split-list item kernels in the object"
     for name, (sg, vg) in items.items():
         m = re.search(r"k_tri_big_itemsILb(\d)ELi(\d+)ELb(\d)ELi(\d+)E", name)
-        lists, unroll, vm, block = (int(x) for x in m.groups())
+        if m:
+            lists, unroll, vm, block = (int(x) for x in m.groups())
+        else:  # k_tri_items_sp<U, VM, B>: list walks
+            m = re.search(r"k_tri_items_spILi(\d+)ELb(\d)ELi(\d+)E", name)
+            lists, (unroll, vm, block) = 1, (int(x) for x in m.groups())
         if not lists or unroll > 8:  # A/B variants (flat walk, 16 loads in flight)
             continue
         granule = -(-sg // 16) * 16 + 16
