@@ -178,6 +178,12 @@ def init_dist(dist, local):
         dist.init_process_group(backend)
 
 
+# the C4 walk kernels: over the direction-split lists (the library's default whenever the targets are coded,
+# i.e. <= 2^24 ids -- C4's config), or the combined lists (CAPSMI_TRI_SPLIT=0 / the flat walk, A/B runs)
+TRI_SYMBOL = ("k_tri_big_items+k_tri_small" if os.environ.get("CAPSMI_TRI_SPLIT") == "0"
+              or os.environ.get("CAPSMI_TRI_WALK") == "flat" else "k_tri_items_sp+k_tri_small_sp")
+
+
 def pmc_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this workload
     (profiles/*_<workload>_pmc.json, newest round first), FETCH_SIZE doubled per MI355X_MICROARCH.md
@@ -687,7 +693,7 @@ SINGLE = {
 # timer name -> kernel symbol (rocprofv3 / PMC summary name) where they differ
 SINGLE_SYMBOL = {"direct_join_probe": "k_direct_probe", "radix_join_count": "k_join", "radix_join_write": "k_join",
                  "expand_filter": "k_expand_pairs", "part_scatter1": "k_scatter_l", "varlen_deg": "k_vl_deg",
-                 "varlen_w": "k_vl_w", "varlen_t": "k_vl_t", "varlen_rev": "k_vl_bset", "varlen_recip": "k_vl_recip", "varlen_cand": "k_vl_cins", "triangles": "k_tri_big_items+k_tri_small"}
+                 "varlen_w": "k_vl_w", "varlen_t": "k_vl_t", "varlen_rev": "k_vl_bset", "varlen_recip": "k_vl_recip", "varlen_cand": "k_vl_cins", "triangles": TRI_SYMBOL}
 
 
 def owned_rmat_rels(sess, graph, scale, m, probs, col, n, chunks=8):

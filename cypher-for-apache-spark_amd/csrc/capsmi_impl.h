@@ -427,7 +427,8 @@ struct TriGraph {
     Buf ioff, itg, ipos, vm_c;
     // direction-split lists (k_tri.hip "direction-split lists"): tgs = every out_f(x) then every out_b(x),
     // fbo = their starts (2n + 2 uint32); with split set the in-lists are ikey (to << 40 | record index, sorted)
-    // and irec (records: coded source word | pf | pb << 16) instead of itg / ipos
+    // and irec (16-byte records: coded source word, pf | pb << 16, the source's f / b list starts) instead of
+    // itg / ipos
     bool split = false;
     Buf tgs, fbo, ikey, irec;
     int64_t nvm = 0;

@@ -162,19 +162,24 @@ __global__ void __launch_bounds__(256) k_und_long(const uint64_t* __restrict__ k
 }
 
 // (degree, id) sort keys of the vertices
+// (degree, id) keys -- the id rides in the low word, so the sort is key-only -- and the maximum degree
+// (one atomic per wave: the sort then takes only the degree digits it has)
 __global__ void k_deg_keys(const uint32_t* __restrict__ deg, int64_t n, uint64_t* __restrict__ key,
-                           int64_t* __restrict__ val) {
+                           unsigned int* __restrict__ dmax) {
+    uint32_t best = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         key[i] = ((uint64_t)deg[i] << 32) | (uint64_t)i;
-        val[i] = i;
+        best = max(best, deg[i]);
     }
+    for (int o = 32; o > 0; o >>= 1) best = max(best, (uint32_t)__shfl_down(best, o, 64));
+    if ((threadIdx.x & 63) == 0 && best) atomicMax(dmax, best);
 }
 
 // degree-order ids: the vertex at position p of the ascending (degree, id) order gets n - 1 - p
-__global__ void k_rank_ids(const int64_t* __restrict__ by_order, int64_t n, uint32_t* __restrict__ rid,
+__global__ void k_rank_ids(const uint64_t* __restrict__ by_order, int64_t n, uint32_t* __restrict__ rid,
                            int64_t* __restrict__ orig) {
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t v = by_order[p], r = n - 1 - p;
+        const int64_t v = (int64_t)(uint32_t)by_order[p], r = n - 1 - p;
         rid[v] = (uint32_t)r;
         orig[r] = v;
     }
@@ -195,39 +200,54 @@ struct TgCode {
 __global__ void k_orient(const uint64_t* __restrict__ ek, const int64_t* __restrict__ ev, int64_t ne,
                          const uint32_t* __restrict__ rid, TgCode tc, uint64_t* __restrict__ ok_,
                          int64_t* __restrict__ ov, uint64_t* __restrict__ exc, unsigned long long* __restrict__ nexc) {
+    // four edges per lane and pass, their loads (and the random rid gathers) issued together
+    constexpr int U = 4;
     const int lane = threadIdx.x & 63;
     const uint32_t cm = tc.cmask();
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63); i0 < ne; i0 += stride) {  // wave-uniform
-        const int64_t i = i0 + lane;
-        bool ex = false;
-        uint64_t key = 0, pay = 0;
-        if (i < ne) {
-            const uint32_t x = (uint32_t)(ek[i] >> 32), y = (uint32_t)ek[i];
-            const uint64_t v = (uint64_t)ev[i];
-            const uint32_t mxy = (uint32_t)(v >> 32), myx = (uint32_t)v;
-            const uint32_t rx = rid[x], ry = rid[y];
-            const bool xf = rx > ry;  // x is lower in (degree, id)
-            const uint32_t f = xf ? mxy : myx, b = xf ? myx : mxy;
-            key = xf ? ((uint64_t)rx << 32) | ry : ((uint64_t)ry << 32) | rx;
-            pay = ((uint64_t)f << 32) | b;
-            if (tc.cb) {
-                key |= (uint64_t)(min(f, cm) << tc.ib | min(b, cm) << (tc.ib + tc.cb));
-                ex = f >= cm || b >= cm;
-            } else {
-                ov[i] = (int64_t)pay;
-            }
-            ok_[i] = key;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * U;
+    for (int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63)) * U; i0 < ne; i0 += stride) {  // wave-uniform
+        uint64_t kk[U], vv[U];
+        uint32_t rx[U], ry[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int64_t i = i0 + j * 64 + lane;
+            kk[j] = i < ne ? ek[i] : 0;
+            vv[j] = i < ne ? (uint64_t)ev[i] : 0;
         }
-        const unsigned long long eb = __ballot(ex);
-        if (eb) {  // wave-uniform
-            unsigned long long base = 0;
-            if (lane == __builtin_ctzll(eb)) base = atomicAdd(nexc, (unsigned long long)__popcll(eb));
-            base = __shfl(base, __builtin_ctzll(eb), 64);
-            if (ex) {
-                const unsigned long long at = base + __popcll(eb & ((1ULL << lane) - 1));
-                exc[2 * at] = key;
-                exc[2 * at + 1] = pay;
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            rx[j] = rid[(uint32_t)(kk[j] >> 32)];
+            ry[j] = rid[(uint32_t)kk[j]];
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int64_t i = i0 + j * 64 + lane;
+            bool ex = false;
+            uint64_t key = 0, pay = 0;
+            if (i < ne) {
+                const uint32_t mxy = (uint32_t)(vv[j] >> 32), myx = (uint32_t)vv[j];
+                const bool xf = rx[j] > ry[j];  // x is lower in (degree, id)
+                const uint32_t f = xf ? mxy : myx, b = xf ? myx : mxy;
+                key = xf ? ((uint64_t)rx[j] << 32) | ry[j] : ((uint64_t)ry[j] << 32) | rx[j];
+                pay = ((uint64_t)f << 32) | b;
+                if (tc.cb) {
+                    key |= (uint64_t)(min(f, cm) << tc.ib | min(b, cm) << (tc.ib + tc.cb));
+                    ex = f >= cm || b >= cm;
+                } else {
+                    ov[i] = (int64_t)pay;
+                }
+                ok_[i] = key;
+            }
+            const unsigned long long eb = __ballot(ex);
+            if (eb) {  // wave-uniform
+                unsigned long long base = 0;
+                if (lane == __builtin_ctzll(eb)) base = atomicAdd(nexc, (unsigned long long)__popcll(eb));
+                base = __shfl(base, __builtin_ctzll(eb), 64);
+                if (ex) {
+                    const unsigned long long at = base + __popcll(eb & ((1ULL << lane) - 1));
+                    exc[2 * at] = key;
+                    exc[2 * at + 1] = pay;
+                }
             }
         }
     }
@@ -380,8 +400,9 @@ __global__ void __launch_bounds__(256) k_split_write(const uint32_t* __restrict_
             f = (uint32_t)min<uint64_t>(p >> 32, cap);
             b = (uint32_t)min<uint64_t>(p & 0xffffffffULL, cap);
         }
-        if (f) tgs[rf++] = (w[j] & idm) | f << tc.ib;
-        if (b) tgs[rb++] = (w[j] & idm) | b << tc.ib;
+        const uint32_t id = w[j] & idm;
+        if (f) tgs[rf++] = id | f << tc.ib;
+        if (b) tgs[rb++] = id | b << tc.ib;
     }
 }
 
@@ -396,21 +417,49 @@ __global__ void k_split_off(const int64_t* __restrict__ off, int64_t n, int64_t 
 }
 
 // in-list records of the split walks, in oriented-edge order (sequential reads; `to` is a hub, its
-// offsets cached): rec[e] = from | the edge's multiplicity codes (a coded word whose id is the source)
-// in the low word, pf | pb << 16 (the f / b entries of out(from) below `to`) in the high word -- 0 when
-// v-mode does not take the edge (p >= od(to): u-mode walks it); the in-key to << 40 | e, sorted on the
-// digits of `to` (stable: edge order within a target); the v-mode items read the records through it
+// offsets cached), 16 bytes: x = from | the edge's multiplicity codes (a coded word whose id is the
+// source), y = pf | pb << 16 (the f / b entries of out(from) below `to`; 0 when v-mode does not take the
+// edge: p >= od(to), u-mode walks it), z / w = the starts of out_f(from) / out_b(from) -- so a v-mode
+// list's setup is one dependent load after its key; the in-key to << 40 | e, sorted on the digits of `to`
+// (stable: edge order within a target); the v-mode items read the records through it
 __global__ void k_swap_keys_sp(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ off, int64_t ne,
                                TgCode tc, const uint32_t* __restrict__ tg, const uint32_t* __restrict__ rk,
-                               const uint32_t* __restrict__ fbo, uint64_t* __restrict__ ik, uint64_t* __restrict__ rec) {
+                               const uint32_t* __restrict__ fbo, uint64_t* __restrict__ ik, uint4* __restrict__ rec) {
+    constexpr int U = 4;  // edges per lane and pass, loads issued together
     const uint32_t idm = tc.idmask();
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = ok_[e];
-        const uint32_t from = (uint32_t)(k >> 32), to = (uint32_t)k & idm;
-        const bool take = e - off[from] < off[to + 1] - off[to];
-        const uint32_t pfb = take ? (rk[2 * e] - fbo[2 * from]) | (rk[2 * e + 1] - fbo[2 * from + 1]) << 16 : 0u;
-        rec[e] = (uint64_t)(from | (tg[e] & ~idm)) | (uint64_t)pfb << 32;
-        ik[e] = (uint64_t)to << 40 | (uint64_t)e;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * U;
+    for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x * U + threadIdx.x; e0 < ne; e0 += stride) {
+        uint64_t k[U];
+        uint32_t w[U], r0[U], r1[U];
+        int64_t of[U], t0[U], t1[U];
+        uint32_t fb0[U], fb1[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int64_t e = min(e0 + (int64_t)j * blockDim.x, ne - 1);
+            k[j] = ok_[e];
+            w[j] = tg[e];
+            r0[j] = rk[2 * e];
+            r1[j] = rk[2 * e + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint32_t from = (uint32_t)(k[j] >> 32), to = (uint32_t)k[j] & idm;
+            of[j] = off[from];
+            t0[j] = off[to];
+            t1[j] = off[to + 1];
+            fb0[j] = fbo[2 * from];
+            fb1[j] = fbo[2 * from + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int64_t e = e0 + (int64_t)j * blockDim.x;
+            if (e >= ne) break;
+            const uint32_t from = (uint32_t)(k[j] >> 32), to = (uint32_t)k[j] & idm;
+            const bool take = e - of[j] < t1[j] - t0[j];
+            const uint32_t pfb = take ? (r0[j] - fb0[j]) | (r1[j] - fb1[j]) << 16 : 0u;
+            rec[e] = make_uint4(from | (w[j] & ~idm), pfb, fb0[j], fb1[j]);
+            ik[e] = (uint64_t)to << 40 | (uint64_t)e;
+        }
     }
 }
 
@@ -418,19 +467,21 @@ __global__ void k_swap_keys_sp(const uint64_t* __restrict__ ok_, const int64_t* 
 __global__ void k_swap_keys_sp_sel(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ off,
                                    const int64_t* __restrict__ sel, int64_t nsel, TgCode tc,
                                    const uint32_t* __restrict__ tg, const uint32_t* __restrict__ rk,
-                                   const uint32_t* __restrict__ fbo, uint64_t* __restrict__ ik, uint64_t* __restrict__ rec) {
+                                   const uint32_t* __restrict__ fbo, uint64_t* __restrict__ ik, uint4* __restrict__ rec) {
     const uint32_t idm = tc.idmask();
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nsel; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t e = sel[i];
         const uint64_t k = ok_[e];
         const uint32_t from = (uint32_t)(k >> 32), to = (uint32_t)k & idm;
-        const uint32_t pfb = (rk[2 * e] - fbo[2 * from]) | (rk[2 * e + 1] - fbo[2 * from + 1]) << 16;  // taken
-        rec[i] = (uint64_t)(from | (tg[e] & ~idm)) | (uint64_t)pfb << 32;
+        const uint32_t f0 = fbo[2 * from], b0 = fbo[2 * from + 1];
+        const uint32_t pfb = (rk[2 * e] - f0) | (rk[2 * e + 1] - b0) << 16;  // taken
+        rec[i] = make_uint4(from | (tg[e] & ~idm), pfb, f0, b0);
         ik[i] = (uint64_t)to << 40 | (uint64_t)i;
     }
 }
 
 constexpr uint64_t kInRecMask = (uint64_t(1) << 40) - 1;  // the record index of a split in-key
+
 
 // v-mode centers: od(v) >= vmt with at least one in-edge
 __global__ void k_tri_vm_bins(const int64_t* __restrict__ off, const int64_t* __restrict__ ioff, int64_t n, int vmt,
@@ -1169,21 +1220,23 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small_sp(const uint32_t* __re
     if (lane == 0 && acc) atomicAdd(out, acc);
 }
 
-// Items over the split lists: a chunk holds kVChunk / 2 edges, i.e. kVChunk lists (2e: f, 2e + 1: b),
-// and an item walks kVGroupSp chunks -- the same kVChunk * kVGroup edges per item as k_tri_big_items
-constexpr int kEChunkSp = kVChunk / 2, kVGroupSp = 2 * kVGroup;
+// Items over the split lists: a chunk holds EC edges, i.e. 2 EC lists (2e: f, 2e + 1: b), and an item
+// walks 2048 / EC chunks -- the same kVChunk * kVGroup edges per item as k_tri_big_items.  EC = 256 for
+// the 1024-lane v-mode items (half the chunk setups: each is a dependent key -> record load), 128 for the
+// 512-lane ones (four per CU: their LDS holds 128-edge tables only)
+__host__ __device__ constexpr int sp_edges(bool vm, int b) { return vm && b == 1024 ? kVChunk : kVChunk / 2; }
 
-template <int B>
+template <int B, int EC>
 struct ItemLdsSp {
-    static constexpr int kChunk = 2 * B, kSlots = 4 * kChunk;
+    static constexpr int kChunk = 2 * B, kSlots = 4 * kChunk, NL = 2 * EC;
     uint32_t bf[(1 << kBigBloomBits) / 32];
     uint32_t hk[kSlots];
     uint16_t hi[kSlots];
-    uint32_t lo[kVChunk];  // list l: tgs[lo, lo + ln), constant factor kq
-    uint32_t ln[kVChunk];
-    uint32_t kq[kVChunk];
-    uint32_t vl[kEChunkSp];  // the lists' owner: v (u-mode) / u (v-mode)
-    uint16_t lk[kVChunk], sk[kVChunk], mk[kVChunk];  // long / short / medium lists
+    uint32_t lo[NL];  // list l: tgs[lo, lo + ln), constant factor kq
+    uint32_t ln[NL];
+    uint32_t kq[NL];
+    uint32_t vl[EC];  // the lists' owner: v (u-mode) / u (v-mode)
+    uint16_t lk[NL], sk[NL], mk[NL];  // long / short / medium lists
     uint32_t ncnt[6];
     unsigned long long item;
 };
@@ -1199,14 +1252,15 @@ __global__ void __launch_bounds__(B, 8) k_tri_items_sp(const uint32_t* __restric
                                                         const uint32_t* __restrict__ fbo,
                                                         const int64_t* __restrict__ ioff,
                                                         const uint64_t* __restrict__ ikey,
-                                                        const uint64_t* __restrict__ irec, int vmt,
+                                                        const uint4* __restrict__ irec, int vmt,
                                                         const int64_t* __restrict__ us, int64_t total,
                                                         const uint64_t* __restrict__ item_ql,
                                                         unsigned long long* __restrict__ ctr,
                                                         unsigned long long* __restrict__ out) {
+    constexpr int EC = sp_edges(VM, B), VG = kVChunk * kVGroup / EC;
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
-    ItemLdsSp<B>& L = *reinterpret_cast<ItemLdsSp<B>*>(lds_raw);
-    constexpr int CH = ItemLdsSp<B>::kChunk;
+    ItemLdsSp<B, EC>& L = *reinterpret_cast<ItemLdsSp<B, EC>*>(lds_raw);
+    constexpr int CH = ItemLdsSp<B, EC>::kChunk;
     unsigned long long& item = L.item;
     unsigned long long acc = 0;
     while (true) {
@@ -1220,9 +1274,9 @@ __global__ void __launch_bounds__(B, 8) k_tri_items_sp(const uint32_t* __restric
         const int d = (int)(off[c + 1] - b);
         const int64_t nb = VM ? uniform64(ioff[c]) : b;  // its neighbour list: in(v) / out(u)
         const int nd = VM ? (int)(ioff[c + 1] - nb) : d;
-        const int nvc = (nd + kEChunkSp - 1) / kEChunkSp, ngr = (nvc + kVGroupSp - 1) / kVGroupSp;
+        const int nvc = (nd + EC - 1) / EC, ngr = (nvc + VG - 1) / VG;
         const int local = (int)(iw >> 32);
-        const int h0 = (local / ngr) * CH, c0 = (local % ngr) * kVGroupSp, c1 = min(nvc, c0 + kVGroupSp);
+        const int h0 = (local / ngr) * CH, c0 = (local % ngr) * VG, c1 = min(nvc, c0 + VG);
         const int hn = min(CH, d - h0);
         int lc = 6;  // hash capacity 2^lc >= 4 hn (load <= 1/4), cleared as far as it is used
         while ((1 << lc) < 4 * hn) ++lc;
@@ -1236,24 +1290,24 @@ __global__ void __launch_bounds__(B, 8) k_tri_items_sp(const uint32_t* __restric
             bset(L.bf, kBigBloomBits, w);
         }
         for (int ch = c0; ch < c1; ++ch) {  // block-uniform
-            const int v0 = ch * kEChunkSp, vn = min(kEChunkSp, nd - v0);
+            const int v0 = ch * EC, vn = min(EC, nd - v0);
             if (ch > c0) __syncthreads();  // the previous chunk's walks are done with the list table
             uint32_t* nc = L.ncnt + 3 * (ch & 1);
             if (threadIdx.x < 3) L.ncnt[3 * ((ch + 1) & 1) + threadIdx.x] = 0;  // read last by chunk ch - 1
             for (int k = threadIdx.x; k < vn; k += B) {
                 uint32_t x, f0, b0, lf, lb, kf, kb;
                 if (VM) {  // in-edge x -> c: prefixes of out_f(x) / out_b(x) below c
-                    const uint64_t r = irec[ikey[nb + v0 + k] & kInRecMask];
-                    const uint32_t word = (uint32_t)r;
+                    const uint4 r = irec[ikey[nb + v0 + k] & kInRecMask];
+                    const uint32_t word = r.x;
                     x = tid(word, tc);
                     const uint32_t fc = (word >> tc.ib) & tc.cmask(), bc = (word >> (tc.ib + tc.cb)) & tc.cmask();
                     uint64_t p = (uint64_t)fc << 32 | bc;
                     if (fc == tc.cmask() || bc == tc.cmask()) p = exact_pay(tg, tc, ov, off, x, (uint32_t)c);
                     kf = (uint32_t)p;           // m(c, x)
                     kb = (uint32_t)(p >> 32);   // m(x, c)
-                    const uint32_t ip = (uint32_t)(r >> 32);
-                    f0 = fbo[2 * x];
-                    b0 = fbo[2 * x + 1];
+                    const uint32_t ip = r.y;
+                    f0 = r.z;
+                    b0 = r.w;
                     lf = kf ? ip & 0xFFFFu : 0u;
                     lb = kb ? ip >> 16 : 0u;
                 } else {  // out-edge c -> x: out_f(x) / out_b(x) unless v-mode takes the edge
@@ -1527,7 +1581,7 @@ __global__ void k_tri_work_u1(const int64_t* __restrict__ cs, int64_t nc, const 
 // (split: ipos = pf | pb << 16, both walked, 0 for the edges it does not take)
 __global__ void k_tri_work_v(const int64_t* __restrict__ cs, int64_t nc, const int64_t* __restrict__ off,
                              const int64_t* __restrict__ ioff, const uint32_t* __restrict__ ipos,
-                             const uint64_t* __restrict__ ikey, const uint64_t* __restrict__ irec,
+                             const uint64_t* __restrict__ ikey, const uint4* __restrict__ irec,
                              int64_t* __restrict__ w) {
     const int lane = threadIdx.x & 63;
     for (int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < nc;
@@ -1536,7 +1590,7 @@ __global__ void k_tri_work_v(const int64_t* __restrict__ cs, int64_t nc, const i
         int64_t acc = 0;
         for (int64_t j = ioff[v] + lane; j < ioff[v + 1]; j += 64) {
             if (irec) {  // split: (pf, pb), 0 for the edges v-mode does not take
-                const uint32_t p = (uint32_t)(irec[ikey[j] & kInRecMask] >> 32);
+                const uint32_t p = irec[ikey[j] & kInRecMask].y;
                 acc += (p & 0xFFFFu) + (p >> 16);
                 continue;
             }
@@ -1683,15 +1737,17 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     Buf rid = dev_alloc(sizeof(uint32_t) * n, s);
     g.orig = dev_alloc(sizeof(int64_t) * n, s);
     {
-        Buf dk = dev_alloc(sizeof(uint64_t) * n, s), dv = dev_alloc(sizeof(int64_t) * n, s);
+        Buf dk = dev_alloc(sizeof(uint64_t) * n, s), dm = dev_alloc(sizeof(int64_t), s);
+        HIP_CHECK(hipMemsetAsync(P<void>(dm), 0, sizeof(int64_t), st));
         hipLaunchKernelGGL(k_deg_keys, dim3(grid(s, n)), dim3(256), 0, st, P<uint32_t>(deg), n, P<uint64_t>(dk),
-                           P<int64_t>(dv));
+                           reinterpret_cast<unsigned int*>(P<int64_t>(dm)));
+        const uint64_t dmax = (uint64_t)read_scalar(s, P<int64_t>(dm));
         // the keys are written in id order and the LSD sort is stable: the degree digits alone give
         // the (degree, id) order
         std::vector<int> dd;
-        for (int sh = 32; sh < 64; sh += 8) dd.push_back(sh);
-        radix_sort_digits(s, P<uint64_t>(dk), P<int64_t>(dv), n, dd);
-        hipLaunchKernelGGL(k_rank_ids, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(dv), n, P<uint32_t>(rid),
+        for (int sh = 32; sh < 64 && (dmax >> (sh - 32)) != 0; sh += 8) dd.push_back(sh);
+        radix_sort_digits(s, P<uint64_t>(dk), nullptr, n, dd);
+        hipLaunchKernelGGL(k_rank_ids, dim3(grid(s, n)), dim3(256), 0, st, P<uint64_t>(dk), n, P<uint32_t>(rid),
                            P<int64_t>(g.orig));
     }
     // coded targets: the ids' sorted digits end at ib = 8 * ceil(bits / 8); with ib <= 24 the two
@@ -1853,11 +1909,11 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
             const int64_t nsel = flags_to_indices(s, P<uint8_t>(f), ne, sel);
             f.reset();
             Buf ik = dev_alloc(sizeof(uint64_t) * (nsel > 0 ? nsel : 1), s), rec;
-            if (g.split) rec = dev_alloc(sizeof(uint64_t) * (nsel > 0 ? nsel : 1), s);
+            if (g.split) rec = dev_alloc(sizeof(uint4) * (nsel > 0 ? nsel : 1), s);
             if (nsel > 0 && g.split)
                 hipLaunchKernelGGL(k_swap_keys_sp_sel, dim3(grid(s, nsel)), dim3(256), 0, st, P<uint64_t>(g.ok),
                                    P<int64_t>(g.off), P<int64_t>(sel), nsel, tc, P<uint32_t>(g.tg), P<uint32_t>(rk),
-                                   P<uint32_t>(g.fbo), P<uint64_t>(ik), P<uint64_t>(rec));
+                                   P<uint32_t>(g.fbo), P<uint64_t>(ik), P<uint4>(rec));
             else if (nsel > 0)
                 hipLaunchKernelGGL(k_swap_keys_sel, dim3(grid(s, nsel)), dim3(256), 0, st, P<uint64_t>(g.ok),
                                    P<int64_t>(g.off), P<int64_t>(sel), nsel, tc, P<uint64_t>(ik));
@@ -1878,11 +1934,12 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
                                    P<int64_t>(g.off), nsel, tc, P<uint32_t>(g.itg), P<uint32_t>(g.ipos));
             g.vm_own = true;
         } else {
-            Buf ik = dev_alloc(sizeof(uint64_t) * ne, s), iv = packed && !g.split ? Buf() : dev_alloc(sizeof(int64_t) * ne, s);
+            Buf ik = dev_alloc(sizeof(uint64_t) * ne, s);
+            Buf iv = g.split ? dev_alloc(sizeof(uint4) * ne, s) : packed ? Buf() : dev_alloc(sizeof(int64_t) * ne, s);
             if (g.split)  // iv: the records (k_swap_keys_sp)
                 hipLaunchKernelGGL(k_swap_keys_sp, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off),
                                    ne, tc, P<uint32_t>(g.tg), P<uint32_t>(rk), P<uint32_t>(g.fbo), P<uint64_t>(ik),
-                                   P<uint64_t>(iv));
+                                   P<uint4>(iv));
             else
                 hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off), ne,
                                    tc, P<uint64_t>(ik), packed ? nullptr : P<int64_t>(iv));
@@ -1932,7 +1989,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
                                        P<int64_t>(g.off), P<uint32_t>(g.tg), tc.idmask(), g.vmt, P<int64_t>(w));
                 else if (vm)
                     hipLaunchKernelGGL(k_tri_work_v, dim3(gw), dim3(256), 0, st, P<int64_t>(cs), nc, P<int64_t>(g.off),
-                                       P<int64_t>(g.ioff), P<uint32_t>(g.ipos), P<uint64_t>(g.ikey), P<uint64_t>(g.irec),
+                                       P<int64_t>(g.ioff), P<uint32_t>(g.ipos), P<uint64_t>(g.ikey), P<uint4>(g.irec),
                                        P<int64_t>(w));
                 else
                     hipLaunchKernelGGL(k_tri_work_u, dim3(gw), dim3(256), 0, st, P<int64_t>(cs), nc, P<int64_t>(g.off),
@@ -2025,13 +2082,15 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
             // resident: two 1024-lane or four 512-lane workgroups per CU (LDS), twice that queued
             const dim3 ig((unsigned)(s->num_cus * (B == 1024 ? 4 : 8)));
             if (g.split && lists) {  // the walks over the direction-split lists
-                const size_t ldsp = B == 1024 ? sizeof(ItemLdsSp<1024>) : sizeof(ItemLdsSp<512>);
+                const size_t ldsp = B == 1024 ? (vm ? sizeof(ItemLdsSp<1024, sp_edges(true, 1024)>)
+                                                      : sizeof(ItemLdsSp<1024, sp_edges(false, 1024)>))
+                                              : sizeof(ItemLdsSp<512, sp_edges(false, 512)>);
                 auto kp = vm ? (B == 512 ? k_tri_items_sp<4, true, 512> : k_tri_items_sp<4, true, 1024>)
                              : (B == 512 ? k_tri_items_sp<4, false, 512> : k_tri_items_sp<4, false, 1024>);
                 set_lds_attr(reinterpret_cast<const void*>(kp), ldsp);
                 hipLaunchKernelGGL(kp, ig, dim3(B), ldsp, st, P<uint32_t>(g.tg), tc, P<int64_t>(g.ov), P<int64_t>(g.off),
                                    P<uint32_t>(g.tgs), P<uint32_t>(g.fbo), P<int64_t>(g.ioff), P<uint64_t>(g.ikey),
-                                   P<uint64_t>(g.irec), g.vmt, cs, nitems, P<uint64_t>(iq), P<unsigned long long>(ctr),
+                                   P<uint4>(g.irec), g.vmt, cs, nitems, P<uint64_t>(iq), P<unsigned long long>(ctr),
                                    P<unsigned long long>(out));
                 return;
             }

@@ -21,11 +21,21 @@ def _count(session, n, src, dst, mask=None, nparts=1):
 
 
 VMODE = ["0", "2", "default"]  # CAPSMI_TRI_VMODE_T: every edge from u / almost every edge from v / 256
+# walks: lists over the direction-split lists (default), lists over the combined out-lists, the flat
+# prefix-sum walk
+WALKS = ["lists", "lists-nosplit", "flat"]
 
 
 def _vmode(monkeypatch, t):
     if t != "default":
         monkeypatch.setenv("CAPSMI_TRI_VMODE_T", t)
+
+
+def _walk(monkeypatch, walk):
+    if walk == "flat":
+        monkeypatch.setenv("CAPSMI_TRI_WALK", "flat")
+    elif walk == "lists-nosplit":
+        monkeypatch.setenv("CAPSMI_TRI_SPLIT", "0")
 
 
 @pytest.mark.parametrize("vmode", VMODE)
@@ -56,24 +66,22 @@ def test_node_filter_and_parts(session, monkeypatch, vmode):
 
 
 @pytest.mark.parametrize("vmode", VMODE)
-@pytest.mark.parametrize("walk", ["lists", "flat"])
+@pytest.mark.parametrize("walk", WALKS)
 @pytest.mark.parametrize("scale", [9, 12])
 def test_rmat(session, monkeypatch, scale, walk, vmode):
     _vmode(monkeypatch, vmode)
-    if walk == "flat":
-        monkeypatch.setenv("CAPSMI_TRI_WALK", "flat")
+    _walk(monkeypatch, walk)
     src, dst = cpu.rmat_edges(scale, 0, 16 << scale)
     assert _count(session, 1 << scale, src, dst) == cpu.triangle_enumerate(1 << scale, src, dst)
 
 
 @pytest.mark.parametrize("vmode", VMODE)
-@pytest.mark.parametrize("walk", ["lists", "flat"])
+@pytest.mark.parametrize("walk", WALKS)
 def test_dense_big_vertices(session, monkeypatch, walk, vmode):
+    """Out-degrees above 64 (one workgroup per vertex) on a dense random multigraph; every wedge walk
+    (wave-per-list over split or combined lists, CAPSMI_TRI_WALK=flat prefix-sum walk)."""
     _vmode(monkeypatch, vmode)
-    """Out-degrees above 64 (one workgroup per vertex) on a dense random multigraph; both wedge
-    walks (wave-per-list default, CAPSMI_TRI_WALK=flat prefix-sum walk)."""
-    if walk == "flat":
-        monkeypatch.setenv("CAPSMI_TRI_WALK", "flat")
+    _walk(monkeypatch, walk)
     rng = np.random.default_rng(11)
     n, m = 300, 40000
     src = rng.integers(0, n, m).astype(np.int64)
@@ -82,9 +90,11 @@ def test_dense_big_vertices(session, monkeypatch, walk, vmode):
 
 
 @pytest.mark.parametrize("vmode", VMODE)
+@pytest.mark.parametrize("walk", ["lists", "lists-nosplit"])
 @pytest.mark.parametrize("mult", [False, True])
-def test_complete_digraph_chunks(session, monkeypatch, mult, vmode):
+def test_complete_digraph_chunks(session, monkeypatch, mult, walk, vmode):
     _vmode(monkeypatch, vmode)
+    _walk(monkeypatch, walk)
     """Complete digraph on 2200 nodes: out-degrees up to 2199 exceed one LDS chunk (2048).
     Loop-free, so count(*) = trace(M^3) for the multiplicity matrix M (exact in float64 here)."""
     n = 2200
@@ -138,4 +148,26 @@ def test_exception_multiplicities(session, monkeypatch, vmode):
     reps = rng.integers(1, 41, len(a)) * (rng.random(len(a)) < 0.3) + 1
     src = np.repeat(a, reps).astype(np.int64)
     dst = np.repeat(b, reps).astype(np.int64)
+    assert _count(session, n, src, dst) == cpu.triangle_closed_form(n, src, dst)
+
+
+@pytest.mark.parametrize("vmode", VMODE)
+@pytest.mark.parametrize("walk", ["lists", "lists-nosplit"])
+def test_split_word_cap(session, monkeypatch, walk, vmode):
+    """Ids above 2^16 (24 id bits): a split-list word holds 8 multiplicity bits, so multiplicities of
+    255 and more are read exactly from the combined list."""
+    _vmode(monkeypatch, vmode)
+    _walk(monkeypatch, walk)
+    rng = np.random.default_rng(23)
+    n = 70000
+    k = 120
+    a, b = np.nonzero(rng.random((k, k)) < 0.3)
+    keep = a != b
+    a, b = a[keep], b[keep]
+    reps = np.where(rng.random(len(a)) < 0.1, rng.integers(250, 320, len(a)), rng.integers(1, 3, len(a)))
+    src = np.repeat(a, reps).astype(np.int64)
+    dst = np.repeat(b, reps).astype(np.int64)
+    far = rng.integers(k, n, 2000).astype(np.int64)  # ids up to 70000, a few edges into the dense part
+    src = np.concatenate([src, far, [n - 1]])
+    dst = np.concatenate([dst, rng.integers(0, k, 2000).astype(np.int64), [0]])
     assert _count(session, n, src, dst) == cpu.triangle_closed_form(n, src, dst)
