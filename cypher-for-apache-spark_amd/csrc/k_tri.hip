@@ -872,12 +872,13 @@ struct ItemLds {
 
 // items of center q: hash chunks of out(c) x chunks of its neighbour list (out(c), or in(c) when
 // ioff is set: v-mode)
+// (epi: neighbour-list entries per item -- kVChunk * kVGroup, or the split items' EPI)
 __global__ void k_tri_items(const int64_t* __restrict__ off, const int64_t* __restrict__ ioff,
-                            const int64_t* __restrict__ us, int64_t nu, int chunk, int64_t* __restrict__ items) {
+                            const int64_t* __restrict__ us, int64_t nu, int chunk, int epi, int64_t* __restrict__ items) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nu) return;
     const int64_t c = us[q], d = off[c + 1] - off[c], nd = ioff ? ioff[c + 1] - ioff[c] : d;
-    items[q] = ((d + chunk - 1) / chunk) * ((nd + kVChunk * kVGroup - 1) / (kVChunk * kVGroup));
+    items[q] = ((d + chunk - 1) / chunk) * ((nd + epi - 1) / epi);
 }
 
 // item -> (its center's index q) | (its index among q's items) << 32: one load per item instead of a
@@ -1222,9 +1223,9 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small_sp(const uint32_t* __re
 
 // Items over the split lists: a chunk holds EC edges, i.e. 2 EC lists (2e: f, 2e + 1: b), and an item
 // walks 2048 / EC chunks -- the same kVChunk * kVGroup edges per item as k_tri_big_items.  EC = 256 for
-// the 1024-lane v-mode items (half the chunk setups: each is a dependent key -> record load), 128 for the
-// 512-lane ones (four per CU: their LDS holds 128-edge tables only)
-__host__ __device__ constexpr int sp_edges(bool vm, int b) { return vm && b == 1024 ? kVChunk : kVChunk / 2; }
+// 1024-lane items (half the chunk setups: each is a dependent key -> record load), 128 for 512-lane ones
+// (four per CU: their LDS holds 128-edge tables only)
+__host__ __device__ constexpr int sp_edges(int b) { return b == 1024 ? kVChunk : kVChunk / 2; }
 
 template <int B, int EC>
 struct ItemLdsSp {
@@ -1244,7 +1245,7 @@ struct ItemLdsSp {
 // k_tri_big_items (LISTS) over the split lists.  u-mode: the lists of edge u -> v are out_f(v) (when
 // m(u,v) >= 1; factor m(u,v)) and out_b(v) (m(v,u)); v-mode (center c, in-edge u -> c): the prefixes of
 // out_f(u) (factor m(c,u)) and out_b(u) (factor m(u,c)) below c, of lengths pf / pb from ipos.
-template <int U, bool VM, int B>
+template <int U, bool VM, int B, int EC = sp_edges(B), int EPI = kVChunk * kVGroup>
 __global__ void __launch_bounds__(B, 8) k_tri_items_sp(const uint32_t* __restrict__ tg, TgCode tc,
                                                         const int64_t* __restrict__ ov,
                                                         const int64_t* __restrict__ off,
@@ -1257,7 +1258,7 @@ __global__ void __launch_bounds__(B, 8) k_tri_items_sp(const uint32_t* __restric
                                                         const uint64_t* __restrict__ item_ql,
                                                         unsigned long long* __restrict__ ctr,
                                                         unsigned long long* __restrict__ out) {
-    constexpr int EC = sp_edges(VM, B), VG = kVChunk * kVGroup / EC;
+    constexpr int VG = EPI / EC;  // chunks per item
     extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
     ItemLdsSp<B, EC>& L = *reinterpret_cast<ItemLdsSp<B, EC>*>(lds_raw);
     constexpr int CH = ItemLdsSp<B, EC>::kChunk;
@@ -2062,8 +2063,14 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
             const char* ube = getenv("CAPSMI_TRI_UBLOCK");  // u-mode workgroup: 512 (default) or 1024
             const char* vbe = getenv("CAPSMI_TRI_VBLOCK");  // v-mode workgroup: 1024 (default) or 512
             const int B = !lists ? 1024 : vm ? (vbe && atoi(vbe) == 512 ? 512 : 1024) : (ube && atoi(ube) == 1024 ? 1024 : 512);
+            // split items of 1024 lanes: 512 (v-mode) / 256 (u-mode) edges per chunk (CAPSMI_TRI_EC=256|512 forces
+            // one; v-mode 256 -> 512: triangles 55.4 -> 54.0 ms), kVChunk * kVGroup edges per item (4096: the same)
+            const char* ece = getenv("CAPSMI_TRI_EC");
+            const bool spl = g.split && lists;
+            const int ec = spl && B == 1024 ? (ece ? atoi(ece) : (vm ? 512 : 256)) : 128;
+            const int epi = kVChunk * kVGroup;
             hipLaunchKernelGGL(k_tri_items, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st, P<int64_t>(g.off),
-                               vm ? P<int64_t>(g.ioff) : nullptr, cs, nc, 2 * B, items);
+                               vm ? P<int64_t>(g.ioff) : nullptr, cs, nc, 2 * B, epi, items);
             exclusive_scan_i64(items, ipre, nc, s);
             const int64_t nitems = read_scalar(s, ipre + nc);
             Buf iq = dev_alloc(sizeof(uint64_t) * (nitems > 0 ? nitems : 1), s);
@@ -2082,11 +2089,13 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
             // resident: two 1024-lane or four 512-lane workgroups per CU (LDS), twice that queued
             const dim3 ig((unsigned)(s->num_cus * (B == 1024 ? 4 : 8)));
             if (g.split && lists) {  // the walks over the direction-split lists
-                const size_t ldsp = B == 1024 ? (vm ? sizeof(ItemLdsSp<1024, sp_edges(true, 1024)>)
-                                                      : sizeof(ItemLdsSp<1024, sp_edges(false, 1024)>))
-                                              : sizeof(ItemLdsSp<512, sp_edges(false, 512)>);
-                auto kp = vm ? (B == 512 ? k_tri_items_sp<4, true, 512> : k_tri_items_sp<4, true, 1024>)
-                             : (B == 512 ? k_tri_items_sp<4, false, 512> : k_tri_items_sp<4, false, 1024>);
+                const bool e512 = B == 1024 && ec == 512;
+                const size_t ldsp = B == 1024 ? (e512 ? sizeof(ItemLdsSp<1024, 512>) : sizeof(ItemLdsSp<1024, sp_edges(1024)>))
+                                              : sizeof(ItemLdsSp<512, sp_edges(512)>);
+                auto kp = vm ? (B == 512 ? k_tri_items_sp<4, true, 512>
+                                : e512 ? k_tri_items_sp<4, true, 1024, 512> : k_tri_items_sp<4, true, 1024>)
+                             : (B == 512 ? k_tri_items_sp<4, false, 512>
+                                         : e512 ? k_tri_items_sp<4, false, 1024, 512> : k_tri_items_sp<4, false, 1024>);
                 set_lds_attr(reinterpret_cast<const void*>(kp), ldsp);
                 hipLaunchKernelGGL(kp, ig, dim3(B), ldsp, st, P<uint32_t>(g.tg), tc, P<int64_t>(g.ov), P<int64_t>(g.off),
                                    P<uint32_t>(g.tgs), P<uint32_t>(g.fbo), P<int64_t>(g.ioff), P<uint64_t>(g.ikey),
