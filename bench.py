@@ -835,7 +835,7 @@ def run_single(args):
         return None, out
 
     kernels = ("direct_join_probe", "radix_join_count", "radix_join_write", "bitmap_add", "expand_filter", "tri_pack",
-               "tri_sort_und", "tri_order", "tri_sort_or", "tri_post", "tri_work", "triangles", "part_scatter1",
+               "tri_deg", "tri_sort_und", "tri_order", "tri_sort_or", "tri_post", "tri_work", "triangles", "part_scatter1",
                "varlen_part", "varlen_deg", "varlen_w", "varlen_rev",
                "varlen_cand", "varlen_recip", "varlen_t", "vls_rev_part", "vls_rev_bloom", "vls_rev_cand", "vls_rev_recip")
     gate = None

@@ -113,7 +113,7 @@ __global__ void k_und_runs(const uint64_t* __restrict__ k, const int64_t* __rest
         const unsigned long long later = lane == 63 ? 0ULL : hb >> (lane + 1);
         const int next = later ? lane + 1 + __builtin_ctzll(later) : __popcll(am);
         const int64_t seg_end = __shfl(h2, head ? next - 1 : lane, 64);  // end of the segment's last run
-        if (head) atomicAdd(&deg[mn], (uint32_t)(seg_end - h));
+        if (head && deg) atomicAdd(&deg[mn], (uint32_t)(seg_end - h));
     }
 }
 
@@ -215,9 +215,9 @@ __global__ void k_orient(const uint64_t* __restrict__ ek, const int64_t* __restr
             vv[j] = i < ne ? (uint64_t)ev[i] : 0;
         }
 #pragma unroll
-        for (int j = 0; j < U; ++j) {
-            rx[j] = rid[(uint32_t)(kk[j] >> 32)];
-            ry[j] = rid[(uint32_t)kk[j]];
+        for (int j = 0; j < U; ++j) {  // (rid null: the keys are degree-order ids already)
+            rx[j] = rid ? rid[(uint32_t)(kk[j] >> 32)] : (uint32_t)(kk[j] >> 32);
+            ry[j] = rid ? rid[(uint32_t)kk[j]] : (uint32_t)kk[j];
         }
 #pragma unroll
         for (int j = 0; j < U; ++j) {
@@ -251,6 +251,103 @@ __global__ void k_orient(const uint64_t* __restrict__ ek, const int64_t* __restr
             }
         }
     }
+}
+
+// ---- the direct oriented build (ids <= 2^24) --------------------------------------------------------------
+// The orientation needs only SOME total order in which hubs come first (any order gives the same count;
+// the degree order bounds the out-lists).  So the degrees are estimated from a hashed sample of the
+// relationships (every one below 2^22 relationships), the vertices ranked, and every relationship packed
+// straight into its oriented key: one sort of the raw oriented keys then groups each pair's relationships
+// (multiplicities per direction from the direction bit) in the order the lists need -- instead of a sort
+// of undirected keys, the orientation, and a second sort of the oriented ones.
+constexpr int kDegLds = 1 << 14;  // per-block LDS counters for the lowest ids (R-MAT's hubs: few hot counters)
+
+__device__ __forceinline__ uint32_t mix32(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdULL;
+    x ^= x >> 33;
+    return (uint32_t)x;
+}
+
+__global__ void __launch_bounds__(256) k_deg_sample(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                    int64_t m, int64_t e0, int64_t lo, int64_t hi,
+                                                    const uint32_t* __restrict__ okw, int full, uint32_t smask,
+                                                    uint32_t* __restrict__ deg) {
+    __shared__ uint32_t h[kDegLds];
+    for (int i = threadIdx.x; i < kDegLds; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+        if (mix32((uint64_t)(e0 + e)) & smask) continue;
+        const int64_t sv = src[e], tv = dst[e];
+        bool ok = sv >= lo && sv < hi && tv >= lo && tv < hi && sv != tv;
+        if (!ok) continue;
+        const uint64_t xs = (uint64_t)(sv - lo), xt = (uint64_t)(tv - lo);
+        if (!full && !(((okw[xs >> 5] >> (xs & 31)) & 1u) && ((okw[xt >> 5] >> (xt & 31)) & 1u))) continue;
+        if (xs < kDegLds) atomicAdd(&h[xs], 1u); else atomicAdd(&deg[xs], 1u);
+        if (xt < kDegLds) atomicAdd(&h[xt], 1u); else atomicAdd(&deg[xt], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kDegLds; i += blockDim.x)
+        if (h[i]) atomicAdd(&deg[i], h[i]);
+}
+
+// raw oriented keys: from << 32 | dir << 31 | to in degree-order ids (from = the lower (degree, id) end,
+// the larger rid; dir = 1 for a relationship to -> from), kNone for dropped ones; self-loops counted in sl
+__global__ void k_pack_or(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, int64_t lo,
+                          int64_t hi, const uint32_t* __restrict__ okw, int full, const uint32_t* __restrict__ rid,
+                          uint64_t* __restrict__ key, uint32_t* __restrict__ sl) {
+    constexpr int U = 4;  // relationships per lane and pass: the random rid gathers of four in flight together
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x * U;
+    for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x * U + threadIdx.x; e0 < m; e0 += stride) {
+        uint64_t xs[U], xt[U];
+        bool ok[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int64_t e = e0 + (int64_t)j * blockDim.x;
+            const int64_t sv = e < m ? src[e] : lo - 1, tv = e < m ? dst[e] : lo - 1;
+            ok[j] = sv >= lo && sv < hi && tv >= lo && tv < hi;
+            xs[j] = ok[j] ? (uint64_t)(sv - lo) : 0;
+            xt[j] = ok[j] ? (uint64_t)(tv - lo) : 0;
+        }
+        if (!full) {
+#pragma unroll
+            for (int j = 0; j < U; ++j)
+                ok[j] = ok[j] && ((okw[xs[j] >> 5] >> (xs[j] & 31)) & 1u) && ((okw[xt[j] >> 5] >> (xt[j] & 31)) & 1u);
+        }
+        uint32_t rs[U], rt[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            rs[j] = rid[xs[j]];
+            rt[j] = rid[xt[j]];
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int64_t e = e0 + (int64_t)j * blockDim.x;
+            if (e >= m) break;
+            uint64_t k = kNone;
+            if (ok[j]) {
+                if (xs[j] == xt[j]) atomicAdd(&sl[xs[j]], 1u);
+                else k = rs[j] > rt[j] ? ((uint64_t)rs[j] << 32) | rt[j] : ((uint64_t)rt[j] << 32) | (1u << 31) | rs[j];
+            }
+            key[e] = k;
+        }
+    }
+}
+
+// sl in degree-order ids
+__global__ void k_perm_u32(const uint32_t* __restrict__ a, const int64_t* __restrict__ orig, int64_t n,
+                           uint32_t* __restrict__ b) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+        b[r] = a[orig[r]];
+}
+
+// the largest out-degree (packed in-keys need positions below 2^16)
+__global__ void k_max_od(const int64_t* __restrict__ off, int64_t n, unsigned long long* __restrict__ mx) {
+    unsigned long long best = 0;
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
+        best = max(best, (unsigned long long)(off[v + 1] - off[v]));
+    for (int o = 32; o > 0; o >>= 1) best = max(best, (unsigned long long)__shfl_down(best, o, 64));
+    if ((threadIdx.x & 63) == 0 && best) atomicMax(mx, best);
 }
 
 // exceptions' exact payloads into ov at their keys' positions in the sorted oriented keys: (from, to)
@@ -1463,7 +1560,7 @@ __global__ void k_tri_from_hist(const uint64_t* __restrict__ ok_, int64_t ne, in
     for (int b = threadIdx.x; b < kHistBins; b += blockDim.x) h[b] = 0;
     __syncthreads();
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x)
-        atomicAdd(&h[(uint32_t)(ok_[i] >> 32) >> hb], 1u);
+        if (ok_[i] != kNone) atomicAdd(&h[(uint32_t)(ok_[i] >> 32) >> hb], 1u);  // (kNone: a dropped relationship)
     __syncthreads();
     for (int b = threadIdx.x; b < kHistBins; b += blockDim.x)
         if (h[b]) atomicAdd(&hist[b], (unsigned long long)h[b]);
@@ -1473,6 +1570,10 @@ __global__ void k_tri_from_hist(const uint64_t* __restrict__ ok_, int64_t ne, in
 __global__ void k_tri_dest_from(const uint64_t* __restrict__ ok_, int64_t ne, int hb, const int64_t* __restrict__ bbeg,
                                 int world, uint64_t* __restrict__ dest) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ne; i += (int64_t)gridDim.x * blockDim.x) {
+        if (ok_[i] == kNone) {  // dropped, not sent
+            dest[i] = 0xFF;
+            continue;
+        }
         const int64_t bin = (int64_t)((uint32_t)(ok_[i] >> 32) >> hb);
         int a = 0, b = world - 1;  // the last q with bbeg[q] <= bin
         while (a < b) {
@@ -1664,158 +1765,306 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(t), P<int64_t>(t), 1, CAPSMI_I64);
         m_all = read_scalar(s, P<int64_t>(t));
     }
-    // the direction bit rides unsorted at bit 31 when max's digits end at or below bit 24
-    const int msh = bits > 24 ? 1 : 0;
-    g.sl = dev_alloc(sizeof(uint32_t) * n, s);
-    HIP_CHECK(hipMemsetAsync(P<void>(g.sl), 0, sizeof(uint32_t) * n, st));
-    Buf key = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s);
-    {
-        KernelTimer kt(s, "tri_pack");
-        int64_t off = 0;
-        for (int i = 0; i < nt; ++i) {
-            if (ms[i] > 0)
-                hipLaunchKernelGGL(k_pack, dim3(grid(s, ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], lo, hi,
-                                   P<uint32_t>(n_ok->words), n_ok->full ? 1 : 0, msh, P<uint64_t>(key) + off,
-                                   P<uint32_t>(g.sl));
-            off += ms[i];
-        }
-    }
-    if (dd) {  // every relationship of a pair to the owner of the pair's lower end
-        Buf dest = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s);
-        if (m > 0)
-            hipLaunchKernelGGL(k_tri_dest_min, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, dd->span,
-                               dd->world, P<uint64_t>(dest));
-        HIP_CHECK(hipGetLastError());
-        int64_t mr = 0;
-        key = exchange_words(s, P<uint64_t>(dest), P<uint64_t>(key), m, &mr);
-        m = mr;
-    }
-    // build phases timed on the device (pure device work between the exchanges; bench kernel_ms)
-    std::unique_ptr<KernelTimer> ph(new KernelTimer(s, "tri_sort_und"));
-    // one sort of the undirected keys: digits of max (and the direction bit when msh) then of min; the
-    // upper ends' degrees are counted between the two halves, while the keys are in max order
-    Buf deg = dev_alloc(sizeof(uint32_t) * n, s);
-    HIP_CHECK(hipMemsetAsync(P<void>(deg), 0, sizeof(uint32_t) * n, st));
-    std::vector<int> kd;
-    for (int sh = 0; sh < bits + msh; sh += 8) kd.push_back(sh);
-    const int nmax = (int)kd.size();
-    for (int sh = 32; sh < 32 + bits; sh += 8) kd.push_back(sh);
-    radix_sort_digits(s, P<uint64_t>(key), nullptr, m, kd, nmax, [&](const uint64_t* kmax) {
-        if (m > 0)
-            hipLaunchKernelGGL(k_deg_max, dim3(grid(s, m)), dim3(256), 0, st, kmax, m, msh, P<uint32_t>(deg));
-    });
-    const uint64_t dmask = msh ? ~1ULL : ~(1ULL << 31);
-    Buf f = dev_alloc(m > 0 ? m : 1, s), heads;
-    hipLaunchKernelGGL(k_heads, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, dmask, P<uint8_t>(f));
-    int64_t ne = flags_to_indices(s, P<uint8_t>(f), m, heads);
-    Buf nv = dev_alloc(sizeof(int64_t) + sizeof(unsigned long long), s);  // nvalid, long-run count
-    HIP_CHECK(hipMemsetAsync(P<void>(nv), 0, sizeof(int64_t) + sizeof(unsigned long long), st));
-    int64_t* nvalid_p = P<int64_t>(nv);
-    unsigned long long* nlong = reinterpret_cast<unsigned long long*>(nvalid_p + 1);
-    hipLaunchKernelGGL(k_first_none, dim3(1), dim3(1), 0, st, P<uint64_t>(key), m, nvalid_p);
-    g.ne = ne;
-    g.ek = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), s);
-    g.ev = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);
-    if (ne > 0) {
-        Buf longr = dev_alloc(sizeof(int64_t) * (m / kShortRun + 1), s);
-        hipLaunchKernelGGL(k_und_runs, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(key), P<int64_t>(heads), ne,
-                           nvalid_p, msh, P<uint64_t>(g.ek), P<int64_t>(g.ev), P<uint32_t>(deg), P<int64_t>(longr), nlong);
-        hipLaunchKernelGGL(k_und_long, dim3(4 * s->num_cus), dim3(256), 0, st, P<uint64_t>(key), P<int64_t>(heads), ne,
-                           nvalid_p, msh, P<int64_t>(longr), nlong, P<int64_t>(g.ev));
-        HIP_CHECK(hipGetLastError());
-    }
-    key.reset();
-    f.reset();
-    heads.reset();
-    g.nek = ne;
-    ph.reset();
-    if (dd) {  // a pair's relationships are all on one rank: the sums over the ranks are exact
-        collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<uint32_t>(deg), P<uint32_t>(deg), n, CAPSMI_COLL_U32);
-        collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<uint32_t>(g.sl), P<uint32_t>(g.sl), n, CAPSMI_COLL_U32);
-    }
-    // degree-order ids (hubs first): sort the vertices by (degree, id)
-    ph.reset(new KernelTimer(s, "tri_order"));
-    Buf rid = dev_alloc(sizeof(uint32_t) * n, s);
-    g.orig = dev_alloc(sizeof(int64_t) * n, s);
-    {
-        Buf dk = dev_alloc(sizeof(uint64_t) * n, s), dm = dev_alloc(sizeof(int64_t), s);
-        HIP_CHECK(hipMemsetAsync(P<void>(dm), 0, sizeof(int64_t), st));
-        hipLaunchKernelGGL(k_deg_keys, dim3(grid(s, n)), dim3(256), 0, st, P<uint32_t>(deg), n, P<uint64_t>(dk),
-                           reinterpret_cast<unsigned int*>(P<int64_t>(dm)));
-        const uint64_t dmax = (uint64_t)read_scalar(s, P<int64_t>(dm));
-        // the keys are written in id order and the LSD sort is stable: the degree digits alone give
-        // the (degree, id) order
-        std::vector<int> dd;
-        for (int sh = 32; sh < 64 && (dmax >> (sh - 32)) != 0; sh += 8) dd.push_back(sh);
-        radix_sort_digits(s, P<uint64_t>(dk), nullptr, n, dd);
-        hipLaunchKernelGGL(k_rank_ids, dim3(grid(s, n)), dim3(256), 0, st, P<uint64_t>(dk), n, P<uint32_t>(rid),
-                           P<int64_t>(g.orig));
-    }
     // coded targets: the ids' sorted digits end at ib = 8 * ceil(bits / 8); with ib <= 24 the two
     // 4-bit multiplicity fields fit above them
     g.ib = (bits + 7) / 8 * 8;
     g.cb = g.ib <= 24 ? 4 : 0;
     const TgCode tc{(uint32_t)g.ib, (uint32_t)g.cb};
-    g.ok = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), s);
-    g.ov = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);  // coded: written at the exceptions only
-    Buf exc = dev_alloc(tc.cb ? sizeof(uint64_t) * 2 * (ne > 0 ? ne : 1) : 8, s);
-    HIP_CHECK(hipMemsetAsync(P<void>(nv), 0, sizeof(int64_t) + sizeof(unsigned long long), st));  // nlong reused: nexc
-    if (ne > 0)
-        hipLaunchKernelGGL(k_orient, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ek), P<int64_t>(g.ev), ne,
-                           P<uint32_t>(rid), tc, P<uint64_t>(g.ok), P<int64_t>(g.ov), P<uint64_t>(exc), nlong);
     std::vector<int> od;  // (source, target): grouped and target-sorted lists
     for (int sh = 0; sh < bits; sh += 8) od.push_back(sh);
     for (int sh = 32; sh < 32 + bits; sh += 8) od.push_back(sh);
-    ph.reset();
-    if (dd) {
-        // the exceptions' exact payloads (rare): every rank's list, for the placement in the whole key array
-        const int64_t nexc = (int64_t)read_scalar(s, reinterpret_cast<const int64_t*>(nlong));
-        int64_t nexc_all = 0;
-        exc = gather_words(s, P<uint64_t>(exc), 2 * nexc, &nexc_all);
-        fill_i64(reinterpret_cast<int64_t*>(nlong), nexc_all / 2, 1, st);
-        // source ranges of coarse degree-order bins, balanced by the all-reduced bin counts
-        const int hb = bits > 12 ? bits - 12 : 0;
-        const int64_t nbins = ((n - 1) >> hb) + 1;
-        const int W = dd->world;
-        Buf hist = dev_alloc(sizeof(int64_t) * (kHistBins + W + 1), s);
-        HIP_CHECK(hipMemsetAsync(P<void>(hist), 0, sizeof(int64_t) * kHistBins, st));
-        if (ne > 0)
-            hipLaunchKernelGGL(k_tri_from_hist, dim3(std::min(grid(s, ne), 4 * s->num_cus)), dim3(1024), 0, st,
-                               P<uint64_t>(g.ok), ne, hb, P<unsigned long long>(hist));
-        HIP_CHECK(hipGetLastError());
-        collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(hist), P<int64_t>(hist), kHistBins, CAPSMI_I64);
-        std::vector<int64_t> h(kHistBins), bb(W + 1);
-        HIP_CHECK(hipMemcpyAsync(h.data(), P<int64_t>(hist), sizeof(int64_t) * kHistBins, hipMemcpyDeviceToHost, st));
-        HIP_CHECK(hipStreamSynchronize(st));
-        int64_t tot = 0;
-        for (int64_t b = 0; b < nbins; ++b) tot += h[b];
-        int64_t cum = 0, b = 0;
-        bb[0] = 0;
-        for (int q = 1; q < W; ++q) {
-            const int64_t want = tot * q / W;
-            while (b < nbins && cum + h[b] <= want) cum += h[b++];
-            bb[q] = b;
-        }
-        bb[W] = nbins;
-        int64_t* bbeg = P<int64_t>(hist) + kHistBins;
-        HIP_CHECK(hipMemcpyAsync(bbeg, bb.data(), sizeof(int64_t) * (W + 1), hipMemcpyHostToDevice, st));
-        Buf dest = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), s);
-        if (ne > 0)
-            hipLaunchKernelGGL(k_tri_dest_from, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, hb, bbeg, W,
-                               P<uint64_t>(dest));
-        HIP_CHECK(hipGetLastError());
-        int64_t nr = 0;
-        Buf mine = exchange_words(s, P<uint64_t>(dest), P<uint64_t>(g.ok), ne, &nr);
+    Buf nv = dev_alloc(sizeof(int64_t) + sizeof(unsigned long long), s);  // nvalid, long-run count (then nexc)
+    HIP_CHECK(hipMemsetAsync(P<void>(nv), 0, sizeof(int64_t) + sizeof(unsigned long long), st));
+    int64_t* nvalid_p = P<int64_t>(nv);
+    unsigned long long* nlong = reinterpret_cast<unsigned long long*>(nvalid_p + 1);
+    Buf exc;
+    int64_t ne = 0;
+    std::unique_ptr<KernelTimer> ph;
+    // the direct oriented build ("the direct oriented build" above) for ids <= 2^24; CAPSMI_TRI_BUILD=sorted:
+    // the undirected sort, orientation and oriented sort (also the build above 2^24 ids)
+    const char* tbe = getenv("CAPSMI_TRI_BUILD");
+    const bool direct = bits <= 24 && !(tbe && std::string(tbe) == "sorted");
+    if (direct) {
+        ph.reset(new KernelTimer(s, "tri_deg"));
+        Buf deg = dev_alloc(sizeof(uint32_t) * n, s);
+        HIP_CHECK(hipMemsetAsync(P<void>(deg), 0, sizeof(uint32_t) * n, st));
+        // sampled degrees: 1 in 32 relationships above 2^22 (CAPSMI_TRI_DEG_SAMPLE = a power of two, 1 = all).
+        // At C4 (2^28): all of them took 20 ms of atomics (hubs' counters) and the walks 53.6 ms; 1 in 16 / 64
+        // ≈ 1 ms, walks 54.2 ms
+        const char* dse = getenv("CAPSMI_TRI_DEG_SAMPLE");
+        int rate = dse ? std::max(1, atoi(dse)) : (m_all > (int64_t(1) << 22) ? 32 : 1);
+        while (rate & (rate - 1)) rate &= rate - 1;
         {
-            KernelTimer kt(s, "tri_sort_or");
-            radix_sort_digits(s, P<uint64_t>(mine), nullptr, nr, od);  // this rank's source range, sorted
+            int64_t e0 = 0;
+            for (int i = 0; i < nt; ++i) {
+                if (ms[i] > 0)
+                    hipLaunchKernelGGL(k_deg_sample, dim3(std::min(grid(s, ms[i]), 4 * s->num_cus)), dim3(256), 0, st,
+                                       srcs[i], dsts[i], ms[i], e0, lo, hi, P<uint32_t>(n_ok->words), n_ok->full ? 1 : 0,
+                                       (uint32_t)(rate - 1), P<uint32_t>(deg));
+                e0 += ms[i];
+            }
+            HIP_CHECK(hipGetLastError());
         }
-        g.ok = gather_words(s, P<uint64_t>(mine), nr, &ne);          // the ranges in rank order: all sorted
-        g.ov = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);
+        ph.reset();
+        if (dd) collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<uint32_t>(deg), P<uint32_t>(deg), n, CAPSMI_COLL_U32);
+        ph.reset(new KernelTimer(s, "tri_order"));
+        Buf rid = dev_alloc(sizeof(uint32_t) * n, s);
+        g.orig = dev_alloc(sizeof(int64_t) * n, s);
+        {
+            Buf dk = dev_alloc(sizeof(uint64_t) * n, s), dm = dev_alloc(sizeof(int64_t), s);
+            HIP_CHECK(hipMemsetAsync(P<void>(dm), 0, sizeof(int64_t), st));
+            hipLaunchKernelGGL(k_deg_keys, dim3(grid(s, n)), dim3(256), 0, st, P<uint32_t>(deg), n, P<uint64_t>(dk),
+                               reinterpret_cast<unsigned int*>(P<int64_t>(dm)));
+            const uint64_t dmax = (uint64_t)read_scalar(s, P<int64_t>(dm));
+            std::vector<int> dg;
+            for (int sh = 32; sh < 64 && (dmax >> (sh - 32)) != 0; sh += 8) dg.push_back(sh);
+            radix_sort_digits(s, P<uint64_t>(dk), nullptr, n, dg);
+            hipLaunchKernelGGL(k_rank_ids, dim3(grid(s, n)), dim3(256), 0, st, P<uint64_t>(dk), n, P<uint32_t>(rid),
+                               P<int64_t>(g.orig));
+        }
+        deg.reset();
+        ph.reset(new KernelTimer(s, "tri_pack"));
+        Buf sl0 = dev_alloc(sizeof(uint32_t) * n, s);
+        HIP_CHECK(hipMemsetAsync(P<void>(sl0), 0, sizeof(uint32_t) * n, st));
+        Buf key = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s);
+        {
+            int64_t off = 0;
+            for (int i = 0; i < nt; ++i) {
+                if (ms[i] > 0)
+                    hipLaunchKernelGGL(k_pack_or, dim3(grid(s, ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], lo, hi,
+                                       P<uint32_t>(n_ok->words), n_ok->full ? 1 : 0, P<uint32_t>(rid),
+                                       P<uint64_t>(key) + off, P<uint32_t>(sl0));
+                off += ms[i];
+            }
+            HIP_CHECK(hipGetLastError());
+        }
+        ph.reset();
+        rid.reset();
+        if (dd) collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<uint32_t>(sl0), P<uint32_t>(sl0), n, CAPSMI_COLL_U32);
+        g.sl = dev_alloc(sizeof(uint32_t) * n, s);  // in degree-order ids, as the pair terms' keys
+        hipLaunchKernelGGL(k_perm_u32, dim3(grid(s, n)), dim3(256), 0, st, P<uint32_t>(sl0), P<int64_t>(g.orig), n,
+                           P<uint32_t>(g.sl));
+        sl0.reset();
+        if (dd) {
+            // every relationship to the rank of its source's degree-order range (ranges balanced by the
+            // all-reduced counts of a coarse source histogram): a pair's relationships meet on one rank
+            const int hb = bits > 12 ? bits - 12 : 0;
+            const int64_t nbins = ((n - 1) >> hb) + 1;
+            const int W = dd->world;
+            Buf hist = dev_alloc(sizeof(int64_t) * (kHistBins + W + 1), s);
+            HIP_CHECK(hipMemsetAsync(P<void>(hist), 0, sizeof(int64_t) * kHistBins, st));
+            if (m > 0)
+                hipLaunchKernelGGL(k_tri_from_hist, dim3(std::min(grid(s, m), 4 * s->num_cus)), dim3(1024), 0, st,
+                                   P<uint64_t>(key), m, hb, P<unsigned long long>(hist));
+            HIP_CHECK(hipGetLastError());
+            collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(hist), P<int64_t>(hist), kHistBins, CAPSMI_I64);
+            std::vector<int64_t> h(kHistBins), bb(W + 1);
+            HIP_CHECK(hipMemcpyAsync(h.data(), P<int64_t>(hist), sizeof(int64_t) * kHistBins, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            int64_t tot = 0;
+            for (int64_t b = 0; b < nbins; ++b) tot += h[b];
+            int64_t cum = 0, b = 0;
+            bb[0] = 0;
+            for (int q = 1; q < W; ++q) {
+                const int64_t want = tot * q / W;
+                while (b < nbins && cum + h[b] <= want) cum += h[b++];
+                bb[q] = b;
+            }
+            bb[W] = nbins;
+            int64_t* bbeg = P<int64_t>(hist) + kHistBins;
+            HIP_CHECK(hipMemcpyAsync(bbeg, bb.data(), sizeof(int64_t) * (W + 1), hipMemcpyHostToDevice, st));
+            Buf dest = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s);
+            if (m > 0)
+                hipLaunchKernelGGL(k_tri_dest_from, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, hb, bbeg, W,
+                                   P<uint64_t>(dest));
+            HIP_CHECK(hipGetLastError());
+            int64_t mr = 0;
+            key = exchange_words(s, P<uint64_t>(dest), P<uint64_t>(key), m, &mr);
+            m = mr;
+        }
+        // one sort of the raw oriented keys (the direction bit unsorted at bit 31), runs = the pairs
+        ph.reset(new KernelTimer(s, "tri_sort_or"));
+        radix_sort_digits(s, P<uint64_t>(key), nullptr, m, od);
+        Buf f = dev_alloc(m > 0 ? m : 1, s), heads;
+        hipLaunchKernelGGL(k_heads, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, ~(1ULL << 31), P<uint8_t>(f));
+        const int64_t nruns = flags_to_indices(s, P<uint8_t>(f), m, heads);
+        f.reset();
+        hipLaunchKernelGGL(k_first_none, dim3(1), dim3(1), 0, st, P<uint64_t>(key), m, nvalid_p);
+        g.ek = dev_alloc(sizeof(uint64_t) * (nruns > 0 ? nruns : 1), s);
+        g.ev = dev_alloc(sizeof(int64_t) * (nruns > 0 ? nruns : 1), s);
+        if (nruns > 0) {  // (from << 32 | to, m(from, to) << 32 | m(to, from)) per pair
+            Buf longr = dev_alloc(sizeof(int64_t) * (m / kShortRun + 1), s);
+            hipLaunchKernelGGL(k_und_runs, dim3(grid(s, nruns)), dim3(256), 0, st, P<uint64_t>(key), P<int64_t>(heads),
+                               nruns, nvalid_p, 0, P<uint64_t>(g.ek), P<int64_t>(g.ev), (uint32_t*)nullptr,
+                               P<int64_t>(longr), nlong);
+            hipLaunchKernelGGL(k_und_long, dim3(4 * s->num_cus), dim3(256), 0, st, P<uint64_t>(key), P<int64_t>(heads),
+                               nruns, nvalid_p, 0, P<int64_t>(longr), nlong, P<int64_t>(g.ev));
+            HIP_CHECK(hipGetLastError());
+        }
+        key.reset();
+        heads.reset();
+        g.nek = nruns;
+        // coded keys (already oriented and sorted: k_orient with the identity order) and the exceptions
+        g.ok = dev_alloc(sizeof(uint64_t) * (nruns > 0 ? nruns : 1), s);
+        g.ov = dev_alloc(sizeof(int64_t) * (nruns > 0 ? nruns : 1), s);
+        exc = dev_alloc(sizeof(uint64_t) * 2 * (nruns > 0 ? nruns : 1), s);
+        HIP_CHECK(hipMemsetAsync(P<void>(nv), 0, sizeof(int64_t) + sizeof(unsigned long long), st));  // nlong: nexc
+        if (nruns > 0)
+            hipLaunchKernelGGL(k_orient, dim3(grid(s, nruns)), dim3(256), 0, st, P<uint64_t>(g.ek), P<int64_t>(g.ev), nruns,
+                               (const uint32_t*)nullptr, tc, P<uint64_t>(g.ok), P<int64_t>(g.ov), P<uint64_t>(exc), nlong);
+        HIP_CHECK(hipGetLastError());
+        ne = nruns;
+        ph.reset();
+        if (dd) {  // the ranges in rank order (sorted), every rank's exceptions
+            const int64_t nexc = (int64_t)read_scalar(s, reinterpret_cast<const int64_t*>(nlong));
+            int64_t nexc_all = 0;
+            exc = gather_words(s, P<uint64_t>(exc), 2 * nexc, &nexc_all);
+            fill_i64(reinterpret_cast<int64_t*>(nlong), nexc_all / 2, 1, st);
+            g.ok = gather_words(s, P<uint64_t>(g.ok), nruns, &ne);
+            g.ov = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);
+        }
     } else {
-        // no kNone among the oriented keys; coded: key-only (the payloads ride in the key)
-        KernelTimer kt(s, "tri_sort_or");
-        radix_sort_digits(s, P<uint64_t>(g.ok), tc.cb ? nullptr : P<int64_t>(g.ov), ne, od);
+        // the direction bit rides unsorted at bit 31 when max's digits end at or below bit 24
+        const int msh = bits > 24 ? 1 : 0;
+        g.sl = dev_alloc(sizeof(uint32_t) * n, s);
+        HIP_CHECK(hipMemsetAsync(P<void>(g.sl), 0, sizeof(uint32_t) * n, st));
+        Buf key = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s);
+        {
+            KernelTimer kt(s, "tri_pack");
+            int64_t off = 0;
+            for (int i = 0; i < nt; ++i) {
+                if (ms[i] > 0)
+                    hipLaunchKernelGGL(k_pack, dim3(grid(s, ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], lo, hi,
+                                       P<uint32_t>(n_ok->words), n_ok->full ? 1 : 0, msh, P<uint64_t>(key) + off,
+                                       P<uint32_t>(g.sl));
+                off += ms[i];
+            }
+        }
+        if (dd) {  // every relationship of a pair to the owner of the pair's lower end
+            Buf dest = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s);
+            if (m > 0)
+                hipLaunchKernelGGL(k_tri_dest_min, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, dd->span,
+                                   dd->world, P<uint64_t>(dest));
+            HIP_CHECK(hipGetLastError());
+            int64_t mr = 0;
+            key = exchange_words(s, P<uint64_t>(dest), P<uint64_t>(key), m, &mr);
+            m = mr;
+        }
+        // build phases timed on the device (pure device work between the exchanges; bench kernel_ms)
+        ph.reset(new KernelTimer(s, "tri_sort_und"));
+        // one sort of the undirected keys: digits of max (and the direction bit when msh) then of min; the
+        // upper ends' degrees are counted between the two halves, while the keys are in max order
+        Buf deg = dev_alloc(sizeof(uint32_t) * n, s);
+        HIP_CHECK(hipMemsetAsync(P<void>(deg), 0, sizeof(uint32_t) * n, st));
+        std::vector<int> kd;
+        for (int sh = 0; sh < bits + msh; sh += 8) kd.push_back(sh);
+        const int nmax = (int)kd.size();
+        for (int sh = 32; sh < 32 + bits; sh += 8) kd.push_back(sh);
+        radix_sort_digits(s, P<uint64_t>(key), nullptr, m, kd, nmax, [&](const uint64_t* kmax) {
+            if (m > 0)
+                hipLaunchKernelGGL(k_deg_max, dim3(grid(s, m)), dim3(256), 0, st, kmax, m, msh, P<uint32_t>(deg));
+        });
+        const uint64_t dmask = msh ? ~1ULL : ~(1ULL << 31);
+        Buf f = dev_alloc(m > 0 ? m : 1, s), heads;
+        hipLaunchKernelGGL(k_heads, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, dmask, P<uint8_t>(f));
+        ne = flags_to_indices(s, P<uint8_t>(f), m, heads);
+        hipLaunchKernelGGL(k_first_none, dim3(1), dim3(1), 0, st, P<uint64_t>(key), m, nvalid_p);
+        g.ne = ne;
+        g.ek = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), s);
+        g.ev = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);
+        if (ne > 0) {
+            Buf longr = dev_alloc(sizeof(int64_t) * (m / kShortRun + 1), s);
+            hipLaunchKernelGGL(k_und_runs, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(key), P<int64_t>(heads), ne,
+                               nvalid_p, msh, P<uint64_t>(g.ek), P<int64_t>(g.ev), P<uint32_t>(deg), P<int64_t>(longr), nlong);
+            hipLaunchKernelGGL(k_und_long, dim3(4 * s->num_cus), dim3(256), 0, st, P<uint64_t>(key), P<int64_t>(heads), ne,
+                               nvalid_p, msh, P<int64_t>(longr), nlong, P<int64_t>(g.ev));
+            HIP_CHECK(hipGetLastError());
+        }
+        key.reset();
+        f.reset();
+        heads.reset();
+        g.nek = ne;
+        ph.reset();
+        if (dd) {  // a pair's relationships are all on one rank: the sums over the ranks are exact
+            collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<uint32_t>(deg), P<uint32_t>(deg), n, CAPSMI_COLL_U32);
+            collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<uint32_t>(g.sl), P<uint32_t>(g.sl), n, CAPSMI_COLL_U32);
+        }
+        // degree-order ids (hubs first): sort the vertices by (degree, id)
+        ph.reset(new KernelTimer(s, "tri_order"));
+        Buf rid = dev_alloc(sizeof(uint32_t) * n, s);
+        g.orig = dev_alloc(sizeof(int64_t) * n, s);
+        {
+            Buf dk = dev_alloc(sizeof(uint64_t) * n, s), dm = dev_alloc(sizeof(int64_t), s);
+            HIP_CHECK(hipMemsetAsync(P<void>(dm), 0, sizeof(int64_t), st));
+            hipLaunchKernelGGL(k_deg_keys, dim3(grid(s, n)), dim3(256), 0, st, P<uint32_t>(deg), n, P<uint64_t>(dk),
+                               reinterpret_cast<unsigned int*>(P<int64_t>(dm)));
+            const uint64_t dmax = (uint64_t)read_scalar(s, P<int64_t>(dm));
+            // the keys are written in id order and the LSD sort is stable: the degree digits alone give
+            // the (degree, id) order
+            std::vector<int> dd;
+            for (int sh = 32; sh < 64 && (dmax >> (sh - 32)) != 0; sh += 8) dd.push_back(sh);
+            radix_sort_digits(s, P<uint64_t>(dk), nullptr, n, dd);
+            hipLaunchKernelGGL(k_rank_ids, dim3(grid(s, n)), dim3(256), 0, st, P<uint64_t>(dk), n, P<uint32_t>(rid),
+                               P<int64_t>(g.orig));
+        }
+        g.ok = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), s);
+        g.ov = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);  // coded: written at the exceptions only
+        exc = dev_alloc(tc.cb ? sizeof(uint64_t) * 2 * (ne > 0 ? ne : 1) : 8, s);
+        HIP_CHECK(hipMemsetAsync(P<void>(nv), 0, sizeof(int64_t) + sizeof(unsigned long long), st));  // nlong reused: nexc
+        if (ne > 0)
+            hipLaunchKernelGGL(k_orient, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ek), P<int64_t>(g.ev), ne,
+                               P<uint32_t>(rid), tc, P<uint64_t>(g.ok), P<int64_t>(g.ov), P<uint64_t>(exc), nlong);
+        ph.reset();
+        if (dd) {
+            // the exceptions' exact payloads (rare): every rank's list, for the placement in the whole key array
+            const int64_t nexc = (int64_t)read_scalar(s, reinterpret_cast<const int64_t*>(nlong));
+            int64_t nexc_all = 0;
+            exc = gather_words(s, P<uint64_t>(exc), 2 * nexc, &nexc_all);
+            fill_i64(reinterpret_cast<int64_t*>(nlong), nexc_all / 2, 1, st);
+            // source ranges of coarse degree-order bins, balanced by the all-reduced bin counts
+            const int hb = bits > 12 ? bits - 12 : 0;
+            const int64_t nbins = ((n - 1) >> hb) + 1;
+            const int W = dd->world;
+            Buf hist = dev_alloc(sizeof(int64_t) * (kHistBins + W + 1), s);
+            HIP_CHECK(hipMemsetAsync(P<void>(hist), 0, sizeof(int64_t) * kHistBins, st));
+            if (ne > 0)
+                hipLaunchKernelGGL(k_tri_from_hist, dim3(std::min(grid(s, ne), 4 * s->num_cus)), dim3(1024), 0, st,
+                                   P<uint64_t>(g.ok), ne, hb, P<unsigned long long>(hist));
+            HIP_CHECK(hipGetLastError());
+            collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(hist), P<int64_t>(hist), kHistBins, CAPSMI_I64);
+            std::vector<int64_t> h(kHistBins), bb(W + 1);
+            HIP_CHECK(hipMemcpyAsync(h.data(), P<int64_t>(hist), sizeof(int64_t) * kHistBins, hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            int64_t tot = 0;
+            for (int64_t b = 0; b < nbins; ++b) tot += h[b];
+            int64_t cum = 0, b = 0;
+            bb[0] = 0;
+            for (int q = 1; q < W; ++q) {
+                const int64_t want = tot * q / W;
+                while (b < nbins && cum + h[b] <= want) cum += h[b++];
+                bb[q] = b;
+            }
+            bb[W] = nbins;
+            int64_t* bbeg = P<int64_t>(hist) + kHistBins;
+            HIP_CHECK(hipMemcpyAsync(bbeg, bb.data(), sizeof(int64_t) * (W + 1), hipMemcpyHostToDevice, st));
+            Buf dest = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), s);
+            if (ne > 0)
+                hipLaunchKernelGGL(k_tri_dest_from, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, hb, bbeg, W,
+                                   P<uint64_t>(dest));
+            HIP_CHECK(hipGetLastError());
+            int64_t nr = 0;
+            Buf mine = exchange_words(s, P<uint64_t>(dest), P<uint64_t>(g.ok), ne, &nr);
+            {
+                KernelTimer kt(s, "tri_sort_or");
+                radix_sort_digits(s, P<uint64_t>(mine), nullptr, nr, od);  // this rank's source range, sorted
+            }
+            g.ok = gather_words(s, P<uint64_t>(mine), nr, &ne);          // the ranges in rank order: all sorted
+            g.ov = dev_alloc(sizeof(int64_t) * (ne > 0 ? ne : 1), s);
+        } else {
+            // no kNone among the oriented keys; coded: key-only (the payloads ride in the key)
+            KernelTimer kt(s, "tri_sort_or");
+            radix_sort_digits(s, P<uint64_t>(g.ok), tc.cb ? nullptr : P<int64_t>(g.ov), ne, od);
+        }
     }
     g.ne = ne;
     ph.reset(new KernelTimer(s, "tri_post"));
@@ -1830,7 +2079,13 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         hipLaunchKernelGGL(k_targets, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, P<uint32_t>(g.tg));
     // packed in-keys (key-only sort) when ids and positions fit: od(u) <= sqrt(2m) under a degree
     // order (every out-neighbour has at least u's degree), so m < 2^31 relationships bound it by 2^16
-    const bool packed = g.ib <= 24 && m_all < (int64_t(1) << 31);
+    bool packed = g.ib <= 24 && m_all < (int64_t(1) << 31);
+    if (packed && ne > 0) {  // (an estimated degree order does not carry the sqrt(2m) bound: check it)
+        Buf t = dev_alloc(sizeof(unsigned long long), s);
+        HIP_CHECK(hipMemsetAsync(P<void>(t), 0, sizeof(unsigned long long), st));
+        hipLaunchKernelGGL(k_max_od, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), n, P<unsigned long long>(t));
+        packed = read_scalar(s, reinterpret_cast<const int64_t*>(P<unsigned long long>(t))) < 65536;
+    }
     // direction-split lists (coded targets; CAPSMI_TRI_SPLIT=0: the combined walks, A/B)
     // (the flat walk of the A/B runs reads the combined in-lists: no split under CAPSMI_TRI_WALK=flat)
     const char* spe = getenv("CAPSMI_TRI_SPLIT");
