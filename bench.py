@@ -119,7 +119,7 @@ def parse():
                    help="diagnostic (C3, C4, C5): the distributed route at world size 1 over RCCL (launch with "
                         "torch.distributed.run --nproc-per-node 1): the route's fixed per-rank cost, exchanges included")
     p.add_argument("--tri-parts", type=int, default=0,
-                   help="diagnostic (C4, one GPU): the work-balanced shares of N ranks (CAPSMI_TRI_WPARTS) of one "
+                   help="diagnostic (C4, one GPU): the interleaved center shares of N ranks of one "
                         "trigraph, each share's count timed alone -- the per-rank triangle phase without contention")
     p.add_argument("--workload", default="c3", choices=("c2", "c3", "c4", "c5"),
                    help="c3 (default, the BASELINE metric) or the single-GPU C2/C4/C5 lines (SURVEY.md 8d)")
@@ -975,9 +975,10 @@ def run_single(args):
     if dist_route:
         line["config"]["route"] = f"Planner(sg).run over a distributed graph ({route_counts(sess)})"
         line["config"]["parallelism"] = (
-            f"C4 over {world} GPU(s): relationships by owner(target); undirected pairs exchanged (all-to-all) to "
-            f"their lower end's owner, oriented ranges exchanged by degree order and all-gathered into a replicated "
-            f"oriented graph, work-balanced center shares, one all-reduce" if wl == "c4" else
+            f"C4 over {world} GPU(s): relationships by owner(target); sampled degrees all-reduced, every relationship "
+            f"packed into its oriented key and exchanged (all-to-all) to the rank of its source's degree-order range, "
+            f"sorted and deduplicated there, the ranges all-gathered into a replicated oriented graph, interleaved "
+            f"center shares, one all-reduce" if wl == "c4" else
             f"C5 over {world} GPU(s): owner(source) shards, in-relationships exchanged (all-to-all) at registration; "
             f"od and Y all-reduced between phases; each rank the rows of its owned start nodes")
     elif shard_c5:
@@ -991,7 +992,6 @@ def run_single(args):
                                    "joins": "Planner(sg).run operator by operator: node scans, two generic "
                                             "radix joins, filter, select (fused routing off)"}[route]
     if wl == "c4" and args.tri_parts > 1 and world == 1:
-        os.environ["CAPSMI_TRI_WPARTS"] = str(args.tri_parts)
         ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id")
         g = graph.TriGraph(sess, [rels], ok)
         per, tot = [], 0
@@ -1004,11 +1004,10 @@ def run_single(args):
             per.append(round((time.perf_counter() - t1) * 1e3, 3))
             tot += c  # the pair / self terms come with part 0 only: the parts add up to the count
         g.release()
-        del os.environ["CAPSMI_TRI_WPARTS"]
         line["query"]["tri_parts"] = {"parts": args.tri_parts, "ms_per_part": per, "max_ms": max(per),
                                       "mean_ms": sum(per) / len(per), "max_over_mean": max(per) / (sum(per) / len(per)),
                                       "sum_of_parts_ok": tot == res,
-                                      "note": "work-balanced shares of one single-GPU trigraph, each part counted "
+                                      "note": "interleaved center shares of one single-GPU trigraph, each part counted "
                                               "alone (wall time incl. the pair/self terms of part 0)"}
     line["query"]["check_vs_fixture"] = fcheck
     if check is not None or (world > 1 and wl in ("c2", "c5")):

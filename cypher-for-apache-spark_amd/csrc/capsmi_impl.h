@@ -436,13 +436,9 @@ struct TriGraph {
     // lower end it owns, while ok / tg hold every oriented edge)
     int64_t nek = 0;
     bool dist = false;
-    // work-balanced shares of tri_count over `wparts` parts (a distributed build: the world size): the
-    // first center of each part in big_u / vm_c / small_u (wparts + 1 entries each), cut where the prefix
-    // sums of the centers' walked entries reach equal shares (empty: equal center counts)
-    int wparts = 0;
-    std::vector<int64_t> wbig, wvm, wsmall;
-    // a distributed build's in-lists hold only this rank's v-mode share (centers in one id range cut by
-    // binned v-mode work), so vm_c is exactly the centers of its part
+    // tri_count's part p of P takes every P-th center of big_u / vm_c / small_u from p (interleaved shares);
+    // a distributed build's in-lists hold only the v-mode centers v with v mod world = rank, so vm_c is
+    // exactly its share
     bool vm_own = false;
 };
 // a distributed build (multi-GPU C4): this rank's relationships are any 1/world of them; the owner of a

@@ -255,11 +255,13 @@ __global__ void k_orient(const uint64_t* __restrict__ ek, const int64_t* __restr
 
 // ---- the direct oriented build (ids <= 2^24) --------------------------------------------------------------
 // The orientation needs only SOME total order in which hubs come first (any order gives the same count;
-// the degree order bounds the out-lists).  So the degrees are estimated from a hashed sample of the
-// relationships (every one below 2^22 relationships), the vertices ranked, and every relationship packed
+// the degree order bounds the out-lists).  So the degrees are estimated from a sample of the relationships
+// (one at a hashed offset in every block of `rate`; every one below 2^22), the vertices ranked, and every
+// relationship packed
 // straight into its oriented key: one sort of the raw oriented keys then groups each pair's relationships
 // (multiplicities per direction from the direction bit) in the order the lists need -- instead of a sort
 // of undirected keys, the orientation, and a second sort of the oriented ones.
+constexpr int kSplitTile = 2048;  // tiled passes: 256 lanes x 8 consecutive keys / edges
 constexpr int kDegLds = 1 << 14;  // per-block LDS counters for the lowest ids (R-MAT's hubs: few hot counters)
 
 __device__ __forceinline__ uint32_t mix32(uint64_t x) {
@@ -271,13 +273,16 @@ __device__ __forceinline__ uint32_t mix32(uint64_t x) {
 
 __global__ void __launch_bounds__(256) k_deg_sample(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                     int64_t m, int64_t e0, int64_t lo, int64_t hi,
-                                                    const uint32_t* __restrict__ okw, int full, uint32_t smask,
+                                                    const uint32_t* __restrict__ okw, int full, uint32_t rate,
                                                     uint32_t* __restrict__ deg) {
+    // one relationship per block of `rate`, at a hashed offset inside it: only the sampled ones are read
     __shared__ uint32_t h[kDegLds];
     for (int i = threadIdx.x; i < kDegLds; i += blockDim.x) h[i] = 0;
     __syncthreads();
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
-        if (mix32((uint64_t)(e0 + e)) & smask) continue;
+    const int64_t ns = (m + rate - 1) / rate;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < ns; j += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = j * rate + (int64_t)(mix32((uint64_t)(e0 / rate + j)) & (rate - 1));
+        if (e >= m) continue;
         const int64_t sv = src[e], tv = dst[e];
         bool ok = sv >= lo && sv < hi && tv >= lo && tv < hi && sv != tv;
         if (!ok) continue;
@@ -414,7 +419,6 @@ __global__ void k_in_split(const uint64_t* __restrict__ ik, const int64_t* __res
 // entries.  fbo[2x] / fbo[2x + 1] = start of out_f(x) / out_b(x) (2n + 2 entries, uint32: the lists
 // hold < 2^32 entries whenever the packed in-keys are used).  Exclusive ranks: rk[2e] = the f-entries
 // before oriented edge e, rk[2e + 1] = nF + the b-entries before it (the in-lists' prefix lengths).
-constexpr int kSplitTile = 2048;  // 256 lanes x 8 consecutive edges
 
 __device__ __forceinline__ void split_flags(uint32_t w, TgCode tc, uint32_t& f, uint32_t& b) {
     f = (w >> tc.ib) & tc.cmask();
@@ -1584,67 +1588,15 @@ __global__ void k_tri_dest_from(const uint64_t* __restrict__ ok_, int64_t ne, in
     }
 }
 
-// Work of a u-mode center (the list entries its walks read): out(u) for the hash, and out(v) for every
-// edge u -> v at position p that u-mode takes (not od(v) >= vmt with p < od(v)); one wave per center
-__global__ void k_tri_work_u(const int64_t* __restrict__ cs, int64_t nc, const int64_t* __restrict__ off,
-                             const uint32_t* __restrict__ tg, uint32_t idmask, int vmt, int64_t* __restrict__ w) {
-    const int lane = threadIdx.x & 63;
-    for (int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < nc;
-         c += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-        const int64_t u = cs[c], b = off[u], d = off[u + 1] - b;
-        int64_t acc = 0;
-        for (int64_t p = lane; p < d; p += 64) {
-            const uint32_t v = tg[b + p] & idmask;
-            const int64_t odv = off[v + 1] - off[v];
-            if (!(vmt > 0 && odv >= vmt && p < odv)) acc += odv;
-        }
-        for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
-        if (lane == 0) w[c] = acc + d;
-    }
-}
-
 // ---- v-mode shares without replicated in-lists (distributed build) -----------------------------------
-// v-mode centers are the vertices with od(v) >= vmt; under the degree order they sit at the low ids.
-// vmax + 1 bounds them (one atomic max per wave).
-__global__ void k_tri_vmax(const int64_t* __restrict__ off, int64_t n, int vmt, unsigned long long* __restrict__ vmax) {
-    unsigned long long best = 0;
-    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < n; v += (int64_t)gridDim.x * blockDim.x)
-        if (off[v + 1] - off[v] >= vmt) best = max(best, (unsigned long long)v + 1);
-    for (int o = 32; o > 0; o >>= 1) best = max(best, (unsigned long long)__shfl_down(best, o, 64));
-    if ((threadIdx.x & 63) == 0 && best) atomicMax(vmax, best);
-}
-
-constexpr int kVwBins = 8192;  // bins of the v-mode work over [0, vmax): 64 KiB of LDS counters
-
-// the v-mode work of every edge u -> v at position p that v-mode takes (od(v) >= vmt, p < od(v)): the
-// p entries of out(u) its walk reads, plus one, summed per bin of v (bin width bw) in LDS, flushed once
-__global__ void __launch_bounds__(1024) k_tri_vwork(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ off,
-                                                    int64_t ne, uint32_t idm, int vmt, int64_t bw,
-                                                    unsigned long long* __restrict__ bins) {
-    __shared__ unsigned long long h[kVwBins];
-    for (int i = threadIdx.x; i < kVwBins; i += blockDim.x) h[i] = 0;
-    __syncthreads();
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = ok_[e];
-        const uint32_t u = (uint32_t)(k >> 32), v = (uint32_t)k & idm;
-        const int64_t odv = off[v + 1] - off[v];
-        if (odv < vmt) continue;
-        const int64_t p = e - off[u];
-        if (p < odv) atomicAdd(&h[min((int64_t)v / bw, (int64_t)kVwBins - 1)], (unsigned long long)p + 1ULL);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kVwBins; i += blockDim.x)
-        if (h[i]) atomicAdd(&bins[i], h[i]);
-}
-
-// the edges whose in-list entry this rank's v-mode share walks: v in [v_lo, v_hi), od(v) >= vmt, p < od(v)
+// the edges whose in-list entry this rank's v-mode share walks: v mod world = rank, od(v) >= vmt, p < od(v)
 __global__ void k_tri_in_flags(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ off, int64_t ne,
-                               uint32_t idm, int vmt, int64_t v_lo, int64_t v_hi, uint8_t* __restrict__ f) {
+                               uint32_t idm, int vmt, int world, int rank, uint8_t* __restrict__ f) {
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
         const uint64_t k = ok_[e];
         const uint32_t u = (uint32_t)(k >> 32), v = (uint32_t)k & idm;
         bool take = false;
-        if (v >= v_lo && v < v_hi) {
+        if ((int)(v % (uint32_t)world) == rank) {
             const int64_t odv = off[v + 1] - off[v];
             take = odv >= vmt && e - off[u] < odv;
         }
@@ -1664,59 +1616,10 @@ __global__ void k_swap_keys_sel(const uint64_t* __restrict__ ok_, const int64_t*
     }
 }
 
-// the same for the small centers (a few entries each): one lane per center keeps 64 of them in flight
-__global__ void k_tri_work_u1(const int64_t* __restrict__ cs, int64_t nc, const int64_t* __restrict__ off,
-                              const uint32_t* __restrict__ tg, uint32_t idmask, int vmt, int64_t* __restrict__ w) {
-    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nc; c += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t u = cs[c], b = off[u], d = off[u + 1] - b;
-        int64_t acc = d;
-        for (int64_t p = 0; p < d; ++p) {
-            const uint32_t v = tg[b + p] & idmask;
-            const int64_t odv = off[v + 1] - off[v];
-            if (!(vmt > 0 && odv >= vmt && p < odv)) acc += odv;
-        }
-        w[c] = acc;
-    }
-}
-
-// work of a v-mode center: out(v) for the hash and the prefix out(u)[0, p) of every in-edge it takes
-// (split: ipos = pf | pb << 16, both walked, 0 for the edges it does not take)
-__global__ void k_tri_work_v(const int64_t* __restrict__ cs, int64_t nc, const int64_t* __restrict__ off,
-                             const int64_t* __restrict__ ioff, const uint32_t* __restrict__ ipos,
-                             const uint64_t* __restrict__ ikey, const uint4* __restrict__ irec,
-                             int64_t* __restrict__ w) {
-    const int lane = threadIdx.x & 63;
-    for (int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < nc;
-         c += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-        const int64_t v = cs[c], odv = off[v + 1] - off[v];
-        int64_t acc = 0;
-        for (int64_t j = ioff[v] + lane; j < ioff[v + 1]; j += 64) {
-            if (irec) {  // split: (pf, pb), 0 for the edges v-mode does not take
-                const uint32_t p = irec[ikey[j] & kInRecMask].y;
-                acc += (p & 0xFFFFu) + (p >> 16);
-                continue;
-            }
-            const int64_t p = ipos[j];
-            if (p < odv) acc += p;
-        }
-        for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
-        if (lane == 0) w[c] = acc + odv;
-    }
-}
-
-// part boundaries: cut[q] = first center whose exclusive work prefix reaches total * q / parts (q < parts),
-// cut[parts] = nc; pre holds nc + 1 prefix sums
-__global__ void k_tri_cuts(const int64_t* __restrict__ pre, int64_t nc, int parts, int64_t* __restrict__ cut) {
-    const int q = threadIdx.x;
-    if (q > parts) return;  // one thread per boundary, no barrier
-    if (q == parts) { cut[q] = nc; return; }
-    const int64_t want = (int64_t)((__int128)pre[nc] * q / parts);
-    int64_t a = 0, b = nc;  // first i in [0, nc] with pre[i] >= want
-    while (a < b) {
-        const int64_t mid = (a + b) >> 1;
-        if (pre[mid] < want) a = mid + 1; else b = mid;
-    }
-    cut[q] = a;
+// every parts-th center from `part`
+__global__ void k_tri_stride(const int64_t* __restrict__ cs, int part, int parts, int64_t cnt, int64_t* __restrict__ out) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += (int64_t)gridDim.x * blockDim.x)
+        out[k] = cs[part + k * (int64_t)parts];
 }
 
 inline int grid(const capsmi_session* s, int64_t n) {
@@ -1798,9 +1701,9 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
             int64_t e0 = 0;
             for (int i = 0; i < nt; ++i) {
                 if (ms[i] > 0)
-                    hipLaunchKernelGGL(k_deg_sample, dim3(std::min(grid(s, ms[i]), 4 * s->num_cus)), dim3(256), 0, st,
-                                       srcs[i], dsts[i], ms[i], e0, lo, hi, P<uint32_t>(n_ok->words), n_ok->full ? 1 : 0,
-                                       (uint32_t)(rate - 1), P<uint32_t>(deg));
+                    hipLaunchKernelGGL(k_deg_sample, dim3(std::min(grid(s, ms[i] / rate + 1), 4 * s->num_cus)), dim3(256),
+                                       0, st, srcs[i], dsts[i], ms[i], e0, lo, hi, P<uint32_t>(n_ok->words),
+                                       n_ok->full ? 1 : 0, (uint32_t)rate, P<uint32_t>(deg));
                 e0 += ms[i];
             }
             HIP_CHECK(hipGetLastError());
@@ -1905,6 +1808,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         heads.reset();
         g.nek = nruns;
         // coded keys (already oriented and sorted: k_orient with the identity order) and the exceptions
+        // (a fused three-pass run detection -- tile counts, heads' starts, differences -- measured 1.4 ms slower)
         g.ok = dev_alloc(sizeof(uint64_t) * (nruns > 0 ? nruns : 1), s);
         g.ov = dev_alloc(sizeof(int64_t) * (nruns > 0 ? nruns : 1), s);
         exc = dev_alloc(sizeof(uint64_t) * 2 * (nruns > 0 ? nruns : 1), s);
@@ -2122,45 +2026,12 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         std::vector<int> tds;  // split: in-key to << 40 | edge index
         for (int sh = 40; sh < 40 + bits; sh += 8) tds.push_back(sh);
         if (dd && packed && dd->world > 1) {
-            // A rank walks only its v-mode share, so it builds only that share's in-lists (the whole
-            // in-list sort was ≈6 ms of every rank's replicated post-processing at s = 24): the v-mode
-            // work of every edge, binned by v over [0, vmax) (the centers sit at the low degree-order ids),
-            // is cut into world ranges of equal work -- the same cuts on every rank -- and only the edges
-            // into this rank's range get in-list entries
-            Buf vb = dev_alloc(sizeof(unsigned long long) * (kVwBins + 1), s);
-            HIP_CHECK(hipMemsetAsync(P<void>(vb), 0, sizeof(unsigned long long) * (kVwBins + 1), st));
-            unsigned long long* vmaxp = P<unsigned long long>(vb) + kVwBins;
-            hipLaunchKernelGGL(k_tri_vmax, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), n, g.vmt, vmaxp);
-            const int64_t vmax = read_scalar(s, reinterpret_cast<const int64_t*>(vmaxp));
-            const int64_t bw = std::max<int64_t>(1, (vmax + kVwBins - 1) / kVwBins);
-            const int W = dd->world;
-            int64_t v_lo = 0, v_hi = 0;
-            if (vmax > 0) {
-                hipLaunchKernelGGL(k_tri_vwork, dim3(std::min(grid(s, ne), 4 * s->num_cus)), dim3(1024), 0, st,
-                                   P<uint64_t>(g.ok), P<int64_t>(g.off), ne, tc.idmask(), g.vmt, bw,
-                                   P<unsigned long long>(vb));
-                HIP_CHECK(hipGetLastError());
-                std::vector<unsigned long long> hb(kVwBins);
-                HIP_CHECK(hipMemcpyAsync(hb.data(), P<void>(vb), sizeof(unsigned long long) * kVwBins,
-                                         hipMemcpyDeviceToHost, st));
-                HIP_CHECK(hipStreamSynchronize(st));
-                unsigned long long tot = 0;
-                for (unsigned long long x : hb) tot += x;
-                std::vector<int64_t> cut(W + 1, 0);  // first bin of each rank's range
-                unsigned long long cum = 0;
-                int64_t b = 0;
-                for (int q = 1; q < W; ++q) {
-                    const unsigned long long want = (unsigned long long)((__int128)tot * q / W);
-                    while (b < kVwBins && cum + hb[b] <= want) cum += hb[b++];
-                    cut[q] = b;
-                }
-                cut[W] = kVwBins;
-                v_lo = cut[dd->rank] * bw;
-                v_hi = dd->rank + 1 == W ? n : std::min<int64_t>(n, cut[dd->rank + 1] * bw);
-            }
+            // A rank walks only its v-mode share, so it builds only that share's in-lists (the whole in-list sort
+            // was ≈6 ms of every rank's replicated post-processing at s = 24): the centers v with v mod W = rank,
+            // interleaved so every rank gets hubs and small centers alike
             Buf f = dev_alloc(ne, s), sel;
             hipLaunchKernelGGL(k_tri_in_flags, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off),
-                               ne, tc.idmask(), g.vmt, v_lo, v_hi, P<uint8_t>(f));
+                               ne, tc.idmask(), g.vmt, dd->world, dd->rank, P<uint8_t>(f));
             HIP_CHECK(hipGetLastError());
             const int64_t nsel = flags_to_indices(s, P<uint8_t>(f), ne, sel);
             f.reset();
@@ -2230,48 +2101,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     g.nbig = flags_to_indices(s, P<uint8_t>(fbg), n, g.big_u);
     HIP_CHECK(hipGetLastError());
     ph.reset();
-    // work-balanced shares of a distributed build's world; CAPSMI_TRI_WPARTS=N computes them for N parts of a
-    // single-device build too (diagnostic: each part's count timed alone, bench.py --tri-parts)
-    const char* wpe = getenv("CAPSMI_TRI_WPARTS");
-    const int wparts = dd ? dd->world : (wpe ? std::max(0, atoi(wpe)) : 0);
-    if (wparts > 1 || dd) {  // work-balanced shares: prefix sums of the centers' walked entries, host copies
-        KernelTimer kt(s, "tri_work");
-        auto work = [&](const Buf& cs, int64_t nc, bool vm, bool small, std::vector<int64_t>& out) {
-            Buf w = dev_alloc(sizeof(int64_t) * (2 * nc + 2), s);
-            if (nc > 0) {
-                const unsigned gw = (unsigned)std::min<int64_t>((nc + 3) / 4, (int64_t)s->num_cus * 16);
-                if (small)
-                    hipLaunchKernelGGL(k_tri_work_u1, dim3(grid(s, nc)), dim3(256), 0, st, P<int64_t>(cs), nc,
-                                       P<int64_t>(g.off), P<uint32_t>(g.tg), tc.idmask(), g.vmt, P<int64_t>(w));
-                else if (vm)
-                    hipLaunchKernelGGL(k_tri_work_v, dim3(gw), dim3(256), 0, st, P<int64_t>(cs), nc, P<int64_t>(g.off),
-                                       P<int64_t>(g.ioff), P<uint32_t>(g.ipos), P<uint64_t>(g.ikey), P<uint4>(g.irec),
-                                       P<int64_t>(w));
-                else
-                    hipLaunchKernelGGL(k_tri_work_u, dim3(gw), dim3(256), 0, st, P<int64_t>(cs), nc, P<int64_t>(g.off),
-                                       P<uint32_t>(g.tg), tc.idmask(), g.vmt, P<int64_t>(w));
-                HIP_CHECK(hipGetLastError());
-            }
-            exclusive_scan_i64(P<int64_t>(w), P<int64_t>(w) + nc + 1, nc, s);
-            const int W = wparts;
-            Buf cut = dev_alloc(sizeof(int64_t) * (W + 1), s);
-            hipLaunchKernelGGL(k_tri_cuts, dim3(1), dim3(256), 0, st, P<int64_t>(w) + nc + 1, nc, W, P<int64_t>(cut));
-            HIP_CHECK(hipGetLastError());
-            out.resize(W + 1);
-            HIP_CHECK(hipMemcpyAsync(out.data(), P<int64_t>(cut), sizeof(int64_t) * (W + 1), hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
-        };
-        REQUIRE(wparts < 255, CAPSMI_ERR_UNSUPPORTED, "distributed triangle count: at most 254 ranks");
-        g.wparts = wparts;
-        work(g.big_u, g.nbig, false, false, g.wbig);
-        if (g.vm_own) {  // every v-mode center of this build is this rank's
-            g.wvm.assign(wparts + 1, 0);
-            for (int q = dd->rank + 1; q <= wparts; ++q) g.wvm[q] = g.nvm;
-        } else {
-            work(g.vm_c, g.nvm, true, false, g.wvm);
-        }
-        work(g.small_u, g.nsmall, false, true, g.wsmall);
-    }
+    REQUIRE(!dd || dd->world < 255, CAPSMI_ERR_UNSUPPORTED, "distributed triangle count: at most 254 ranks");
 }
 
 namespace {
@@ -2280,7 +2110,7 @@ void set_lds_attr(const void* k, size_t bytes) {
 }
 }  // namespace
 
-// count for vertex share `part` of `nparts` (each bin sliced evenly); pair/self terms with part 0
+// count for vertex share `part` of `nparts` (interleaved center lists); pair/self terms with part 0
 uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
     using namespace tri;
     hipStream_t st = s->stream;
@@ -2288,21 +2118,27 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
     HIP_CHECK(hipMemsetAsync(P<void>(out), 0, 24, st));
     {
         KernelTimer kt(s, "triangles");
-        // this part's slice of each center list: equal work (the walked-entry prefix sums of a distributed
-        // build), else equal center counts
-        auto share = [&](int64_t nc, const std::vector<int64_t>& cut, int64_t& b, int64_t& e) {
-            if (g.wparts == nparts && cut.size() == (size_t)nparts + 1) {
-                b = std::min(cut[part], nc);
-                e = std::min(cut[part + 1], nc);
-            } else {
-                b = nc * part / nparts;
-                e = nc * (part + 1) / nparts;
-            }
+        // this part's share of each center list: every nparts-th center from `part` (interleaved, so each part
+        // gets hubs and small centers alike -- the contiguous work-estimated cuts of round 4 left the shares of
+        // a single trigraph at max / mean 1.41); a distributed build's in-lists hold its own v-mode centers only
+        std::vector<Buf> keep;
+        auto share = [&](const Buf& cs, int64_t nc, bool own, const int64_t*& p, int64_t& cnt) {
+            p = P<int64_t>(cs);
+            cnt = nc;
+            if (nparts <= 1 || own || nc == 0) return;
+            cnt = nc > part ? (nc - part + nparts - 1) / nparts : 0;
+            if (cnt == 0) return;
+            keep.emplace_back(dev_alloc(sizeof(int64_t) * cnt, s));
+            hipLaunchKernelGGL(k_tri_stride, dim3(grid(s, cnt)), dim3(256), 0, st, P<int64_t>(cs), part, nparts, cnt,
+                               P<int64_t>(keep.back()));
+            HIP_CHECK(hipGetLastError());
+            p = P<int64_t>(keep.back());
         };
-        int64_t sb, se, bb, be, vb, ve;
-        share(g.nsmall, g.wsmall, sb, se);
-        share(g.nbig, g.wbig, bb, be);
-        share(g.nvm, g.wvm, vb, ve);
+        const int64_t *sp, *bp, *vp;
+        int64_t sn, bn, vn;
+        share(g.small_u, g.nsmall, false, sp, sn);
+        share(g.big_u, g.nbig, false, bp, bn);
+        share(g.vm_c, g.nvm, g.vm_own, vp, vn);
         const TgCode tc{(uint32_t)g.ib, (uint32_t)g.cb};
         const char* walk = getenv("CAPSMI_TRI_WALK");  // "flat": the prefix-sum walk (A/B runs)
         const bool lists = !(walk && std::string(walk) == "flat");
@@ -2365,22 +2201,21 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
                                P<uint64_t>(iq), P<unsigned long long>(ctr),
                                P<unsigned long long>(out));
         };
-        if (be > bb) run_items(P<int64_t>(g.big_u) + bb, be - bb, false);
-        if (ve > vb) run_items(P<int64_t>(g.vm_c) + vb, ve - vb, true);
-        if (se > sb && g.split && lists) {
-            const int64_t gs = std::min<int64_t>((se - sb + 3) / 4, (int64_t)s->num_cus * 16);
+        if (bn > 0) run_items(bp, bn, false);
+        if (vn > 0) run_items(vp, vn, true);
+        if (sn > 0 && g.split && lists) {
+            const int64_t gs = std::min<int64_t>((sn + 3) / 4, (int64_t)s->num_cus * 16);
             hipLaunchKernelGGL(k_tri_small_sp<4>, dim3((unsigned)gs), dim3(kTriBlock), 0, st, P<uint32_t>(g.tg), tc,
                                P<int64_t>(g.ov), P<int64_t>(g.off), P<uint32_t>(g.tgs), P<uint32_t>(g.fbo), g.vmt,
-                               P<int64_t>(g.small_u) + sb, se - sb, P<unsigned long long>(out));
-        } else if (se > sb) {
-            const int64_t gs = std::min<int64_t>((se - sb + 3) / 4, (int64_t)s->num_cus * 16);
+                               sp, sn, P<unsigned long long>(out));
+        } else if (sn > 0) {
+            const int64_t gs = std::min<int64_t>((sn + 3) / 4, (int64_t)s->num_cus * 16);
             auto kfs = !lists ? k_tri_small<false, 4>
                        : un == 16 ? k_tri_small<true, 16>
                        : un == 8 ? k_tri_small<true, 8> : k_tri_small<true, 4>;
             hipLaunchKernelGGL(kfs, dim3((unsigned)gs), dim3(kTriBlock), 0, st,
                                P<uint32_t>(g.tg), tc, P<int64_t>(g.ov), P<int64_t>(g.off), g.vmt,
-                               P<int64_t>(g.small_u) + sb, se - sb,
-                               P<unsigned long long>(out));
+                               sp, sn, P<unsigned long long>(out));
         }
     }
     // pair terms over this graph's undirected edges (a distributed build's ek holds this rank's pairs, so
