@@ -1346,7 +1346,7 @@ struct ItemLdsSp {
 // k_tri_big_items (LISTS) over the split lists.  u-mode: the lists of edge u -> v are out_f(v) (when
 // m(u,v) >= 1; factor m(u,v)) and out_b(v) (m(v,u)); v-mode (center c, in-edge u -> c): the prefixes of
 // out_f(u) (factor m(c,u)) and out_b(u) (factor m(u,c)) below c, of lengths pf / pb from ipos.
-template <int U, bool VM, int B, int EC = sp_edges(B), int EPI = kVChunk * kVGroup>
+template <int U, bool VM, int B, int EC = sp_edges(B), int EPI = kVChunk * kVGroup, int SG = kSG>
 __global__ void __launch_bounds__(B, 8) k_tri_items_sp(const uint32_t* __restrict__ tg, TgCode tc,
                                                         const int64_t* __restrict__ ov,
                                                         const int64_t* __restrict__ off,
@@ -1436,8 +1436,8 @@ __global__ void __launch_bounds__(B, 8) k_tri_items_sp(const uint32_t* __restric
                 for (int t = 0; t < 2; ++t) {
                     const uint32_t dw = t ? lb : lf;
                     const uint16_t l = (uint16_t)(2 * k + t);
-                    if (dw > 8u * kSG) L.lk[atomicAdd(&nc[0], 1u)] = l;
-                    else if (dw > 4u * kSG) L.mk[atomicAdd(&nc[2], 1u)] = l;
+                    if (dw > 8u * SG) L.lk[atomicAdd(&nc[0], 1u)] = l;
+                    else if (dw > 4u * SG) L.mk[atomicAdd(&nc[2], 1u)] = l;
                     else if (dw > 0u) L.sk[atomicAdd(&nc[1], 1u)] = l;
                 }
             }
@@ -1479,8 +1479,8 @@ __global__ void __launch_bounds__(B, 8) k_tri_items_sp(const uint32_t* __restric
                     }
                 }
             };
-            grouped(L.sk, nshort, kSG == 8 ? 3 : kSG == 16 ? 4 : 5);
-            grouped(L.mk, nmed, kSG == 8 ? 4 : kSG == 16 ? 5 : 6);
+            grouped(L.sk, nshort, SG == 8 ? 3 : SG == 16 ? 4 : 5);
+            grouped(L.mk, nmed, SG == 8 ? 4 : SG == 16 ? 5 : 6);
             for (int q = wave; q < nlong; q += B / 64) {  // long lists: one per wave, U x 64 entries a pass
                 const int l = L.lk[q];
                 const int64_t lo = (int64_t)__builtin_amdgcn_readfirstlane(L.lo[l]);
@@ -2183,9 +2183,14 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
                 const bool e512 = B == 1024 && ec == 512;
                 const size_t ldsp = B == 1024 ? (e512 ? sizeof(ItemLdsSp<1024, 512>) : sizeof(ItemLdsSp<1024, sp_edges(1024)>))
                                               : sizeof(ItemLdsSp<512, sp_edges(512)>);
+                // CAPSMI_TRI_SG_SP=8: 8 lanes per short list (8 lists a wave pass) in the default configurations (A/B)
+                const char* sge = getenv("CAPSMI_TRI_SG_SP");
+                const bool sg8 = sge && atoi(sge) == 8;
+                constexpr int D = kVChunk * kVGroup;
                 auto kp = vm ? (B == 512 ? k_tri_items_sp<4, true, 512>
-                                : e512 ? k_tri_items_sp<4, true, 1024, 512> : k_tri_items_sp<4, true, 1024>)
-                             : (B == 512 ? k_tri_items_sp<4, false, 512>
+                                : e512 ? (sg8 ? k_tri_items_sp<4, true, 1024, 512, D, 8> : k_tri_items_sp<4, true, 1024, 512>)
+                                       : k_tri_items_sp<4, true, 1024>)
+                             : (B == 512 ? (sg8 ? k_tri_items_sp<4, false, 512, sp_edges(512), D, 8> : k_tri_items_sp<4, false, 512>)
                                          : e512 ? k_tri_items_sp<4, false, 1024, 512> : k_tri_items_sp<4, false, 1024>);
                 set_lds_attr(reinterpret_cast<const void*>(kp), ldsp);
                 hipLaunchKernelGGL(kp, ig, dim3(B), ldsp, st, P<uint32_t>(g.tg), tc, P<int64_t>(g.ov), P<int64_t>(g.off),

@@ -470,7 +470,7 @@ capsmi_status capsmi_varlen_shard_release(capsmi_varlen_shard* v);
  *   MATCH (a)-[r1]->(b)-[r2]->(c)-[r3]->(a) WHERE n_ok(a) AND n_ok(b) AND n_ok(c) RETURN count(*)
  * (two Expands + ExpandInto on (c, a), RelationalPlanner.scala:113-154, plus pairwise uniqueness).
  * The oriented simple graph with multiplicities (a trigraph) is built once; counting can be split into
- * `nparts` slices of its oriented edges (multi-GPU replicas: each rank counts its part, results sum). */
+ * `nparts` interleaved shares of its centers (multi-GPU replicas: each rank counts its part, results sum). */
 typedef struct capsmi_trigraph capsmi_trigraph;
 capsmi_status capsmi_trigraph_build(capsmi_session* s, int32_t nrels, capsmi_table* const* rels, const char* src_col,
                                     const char* dst_col, const capsmi_bitmap* n_ok, capsmi_trigraph** out);
@@ -562,9 +562,10 @@ enum { CAPSMI_RELS_BY_SOURCE = 0, CAPSMI_RELS_BY_TARGET = 1 };
  * the 2-hop count(*), count(DISTINCT end) and count(DISTINCT start) (all-gathers of owned frontier slices
  * when the walk's relationships arrive by their end's owner, an ALL_TO_ALL_V + OR of frontier and end
  * bitmap slices when by their start's owner; the count(*) through an all-gather of owned degrees) and the
- * cyclic triangle count (undirected keys exchanged to the owner of their lower end, the oriented lists
- * exchanged by degree-order range and all-gathered into a replicated oriented graph, each rank counting a
- * work share, one all-reduce); with BY_SOURCE also the var-length grouped count (od and Y all-reduced
+ * cyclic triangle count (sampled degrees all-reduced, every relationship packed into its oriented key and
+ * exchanged to the rank of its source's degree-order range, sorted and deduplicated there, the ranges
+ * all-gathered into a replicated oriented graph, each rank counting an interleaved share of the centers, one
+ * all-reduce); with BY_SOURCE also the var-length grouped count (od and Y all-reduced
  * between its phases; the rows of each rank's owned start nodes), the undirected 1- / 2-hop counts (the
  * middles restricted to owned ids over the relationships incident to them, marks OR-reduced) and the 2-hop
  * grouped by its start (outC and the deduplicated hop-2 lists all-gathered; rows of the owned starts).
