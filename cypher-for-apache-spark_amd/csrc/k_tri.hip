@@ -2183,14 +2183,11 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
                 const bool e512 = B == 1024 && ec == 512;
                 const size_t ldsp = B == 1024 ? (e512 ? sizeof(ItemLdsSp<1024, 512>) : sizeof(ItemLdsSp<1024, sp_edges(1024)>))
                                               : sizeof(ItemLdsSp<512, sp_edges(512)>);
-                // CAPSMI_TRI_SG_SP=8: 8 lanes per short list (8 lists a wave pass) in the default configurations (A/B)
-                const char* sge = getenv("CAPSMI_TRI_SG_SP");
-                const bool sg8 = sge && atoi(sge) == 8;
-                constexpr int D = kVChunk * kVGroup;
+                // (8 lanes per short list instead of 16 -- 8 lists a wave pass for the halved split lists --
+                // measured 54.4 -> 55.4 ms)
                 auto kp = vm ? (B == 512 ? k_tri_items_sp<4, true, 512>
-                                : e512 ? (sg8 ? k_tri_items_sp<4, true, 1024, 512, D, 8> : k_tri_items_sp<4, true, 1024, 512>)
-                                       : k_tri_items_sp<4, true, 1024>)
-                             : (B == 512 ? (sg8 ? k_tri_items_sp<4, false, 512, sp_edges(512), D, 8> : k_tri_items_sp<4, false, 512>)
+                                : e512 ? k_tri_items_sp<4, true, 1024, 512> : k_tri_items_sp<4, true, 1024>)
+                             : (B == 512 ? k_tri_items_sp<4, false, 512>
                                          : e512 ? k_tri_items_sp<4, false, 1024, 512> : k_tri_items_sp<4, false, 1024>);
                 set_lds_attr(reinterpret_cast<const void*>(kp), ldsp);
                 hipLaunchKernelGGL(kp, ig, dim3(B), ldsp, st, P<uint32_t>(g.tg), tc, P<int64_t>(g.ov), P<int64_t>(g.off),
