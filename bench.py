@@ -118,6 +118,9 @@ def parse():
     p.add_argument("--dist1", action="store_true",
                    help="diagnostic (C3, C4, C5): the distributed route at world size 1 over RCCL (launch with "
                         "torch.distributed.run --nproc-per-node 1): the route's fixed per-rank cost, exchanges included")
+    p.add_argument("--plan-in-step", action="store_true",
+                   help="C3 planned modes: build each step's plan inside the timed region (before round 5's "
+                        "SURVEY.md 8d timing, the planning was part of every step)")
     p.add_argument("--tri-parts", type=int, default=0,
                    help="diagnostic (C4, one GPU): the interleaved center shares of N ranks of one "
                         "trigraph, each share's count timed alone -- the per-rank triangle phase without contention")
@@ -437,8 +440,11 @@ def main():
     # ---- the drop-in route: the relational plan of the query, as the planner emits it ----------------
     # Planner(sg).run issues the Table[T] calls RelationalPlanner would (node / relationship scans, two
     # Expand joins per hop, the r1 <> r2 filter, the count(DISTINCT c) aggregate); libcapsmi's
-    # recogniser maps the lazy plan onto the same fused kernels at materialisation.  Planning and
-    # routing run inside the timed region.
+    # recogniser maps the lazy plan onto the same fused kernels at materialisation.  The timed region is
+    # SURVEY.md §8d's: from handing the plan to the backend (the lazy table's first action: recognition,
+    # routing, every kernel) to the answer on the host.  Each timed step executes its own plan, built
+    # before the timed region (a lazy plan holds no rows and runs nothing until that action); the
+    # planning itself is timed apart (query.plan_ms).  --plan-in-step times planning inside each step.
     from capsmi.planner import EntityTable, Planner, ScanGraph
     person_et = EntityTable("node", frozenset({"Person"}), {}, persons, id_col="id")
 
@@ -478,6 +484,16 @@ def main():
              "cold": lambda: run_planner(sg_cold), "warm": lambda: run_planner(sg_warm),
              "direct": step_cold, "direct_warm": step_warm, "stream": step_stream,
              "count": run_count, "count_atomic": lambda: run_count(True)}
+    # the planned modes: (build the lazy plan, execute it)
+    plans_of = {"cold": lambda: Planner(sg_cold).run(C3_QUERY), "warm": lambda: Planner(sg_warm).run(C3_QUERY),
+                "count": lambda: Planner(sg_cold).run(C3_COUNT_QUERY),
+                "und_count": lambda: Planner(sg_cold).run(C3U_COUNT_QUERY),
+                "und_distinct": lambda: Planner(sg_cold).run(C3U_QUERY)}
+
+    def execute(plan):
+        t, outs = plan
+        return int(t.column(outs[0][2]).values[0])
+    plan_ms = {}
     if shards != 1:  # --shard-of diagnostic: one shard's kernels, no exchange
         steps["cold"], steps["warm"], steps["count"] = step_cold, step_warm, step_count_shards
 
@@ -512,6 +528,19 @@ def main():
                     gate.release()
         for _ in range(args.warmup):
             res = step()
+        pre = mode in plans_of and shards == 1 and not args.plan_in_step
+        if pre:  # this mode's plans, one per timed step, built before the timed region (timed apart)
+            tp = time.perf_counter()
+            queue = [plans_of[mode]() for _ in range(args.steps)]
+            plan_ms[mode] = (time.perf_counter() - tp) / args.steps * 1e3
+            step = lambda: execute(queue.pop(0))  # noqa: E731 (each plan executed once, then dropped)
+            if gate is not None:
+                def step(inner=step):
+                    gate.acquire()
+                    try:
+                        return inner()
+                    finally:
+                        gate.release()
         if gate is not None:
             gate.busy = 0.0
         _lib.call("capsmi_session_set_profiling", sess.handle, 1)
@@ -632,6 +661,11 @@ def main():
                       "kernel_ms": {k: v[1] / v[0] for k, v in timed.items()},
                       "rels_local_rank0": m_local, "ingest_s": ingest_s},
         }
+        if head in plan_ms:  # planning outside the timed region, reported beside it
+            line["query"]["plan_ms"] = plan_ms[head]
+            line["query"]["ms_per_step_with_planning"] = sec * 1e3 + plan_ms[head]
+            line["query"]["timed_region"] = ("SURVEY.md 8d: from handing each step's lazy plan to the backend to "
+                                             "the answer on the host; planning timed apart (plan_ms)")
         if distributed:
             line["query"]["rels_per_rank"] = rels_per_rank
             line["query"]["rels_max_over_mean"] = max(rels_per_rank) / (sum(rels_per_rank) / world)
