@@ -431,6 +431,7 @@ struct TriGraph {
     // itg / ipos
     bool split = false;
     Buf tgs, fbo, ikey, irec;
+    Buf vrec;  // per vertex {f start, b start, f len | b len << 16, od} (k_vrec): one load per list setup
     int64_t nvm = 0;
     // ek / ev entries (= ne on one device; on a rank of a distributed build the undirected edges whose
     // lower end it owns, while ok / tg hold every oriented edge)

@@ -517,6 +517,17 @@ __global__ void k_split_off(const int64_t* __restrict__ off, int64_t n, int64_t 
     }
 }
 
+// per-vertex list record of the split walks: {start of out_f(x), start of out_b(x), |out_f(x)| | |out_b(x)| << 16,
+// od(x)} -- one 16-byte load sets up both lists of an edge u -> x (and the v-mode skip test) instead of the
+// offsets' and the list starts' separate lines (lengths < 2^16: the split walks run with packed in-keys)
+__global__ void k_vrec(const int64_t* __restrict__ off, const uint32_t* __restrict__ fbo, int64_t n,
+                       uint4* __restrict__ vrec) {
+    for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t f0 = fbo[2 * x], b0 = fbo[2 * x + 1];
+        vrec[x] = make_uint4(f0, b0, (fbo[2 * x + 2] - f0) | (fbo[2 * x + 3] - b0) << 16, (uint32_t)(off[x + 1] - off[x]));
+    }
+}
+
 // in-list records of the split walks, in oriented-edge order (sequential reads; `to` is a hub, its
 // offsets cached), 16 bytes: x = from | the edge's multiplicity codes (a coded word whose id is the
 // source), y = pf | pb << 16 (the f / b entries of out(from) below `to`; 0 when v-mode does not take the
@@ -1215,7 +1226,7 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small_sp(const uint32_t* __re
                                                             const int64_t* __restrict__ ov,
                                                             const int64_t* __restrict__ off,
                                                             const uint32_t* __restrict__ tgs,
-                                                            const uint32_t* __restrict__ fbo, int vmt,
+                                                            const uint4* __restrict__ vrec, int vmt,
                                                             const int64_t* __restrict__ us, int64_t nu,
                                                             unsigned long long* __restrict__ out) {
     __shared__ SmallWaveSp sw[kTriBlock / 64];
@@ -1236,12 +1247,12 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small_sp(const uint32_t* __re
         if (lane < d) {
             const uint32_t word = tg[b + lane], v = tid(word, tc);
             const uint64_t pv = tpay(word, tc, ov, b + lane);
-            const uint32_t dv = (uint32_t)(off[v + 1] - off[v]);
+            const uint4 vr = vrec[v];
+            const uint32_t dv = vr.w, f0 = vr.x, b0 = vr.y;
             const bool skip = vmt > 0 && dv >= (uint32_t)vmt && (uint32_t)lane < dv;  // v-mode takes u -> v
-            const uint32_t f0 = fbo[2 * v], b0 = fbo[2 * v + 1], f1 = fbo[2 * v + 2], b1 = fbo[2 * v + 3];
             const uint32_t kf = (uint32_t)(pv >> 32), kb = (uint32_t)pv;
-            lf = skip || !kf ? 0u : f1 - f0;
-            lb = skip || !kb ? 0u : b1 - b0;
+            lf = skip || !kf ? 0u : vr.z & 0xFFFFu;
+            lb = skip || !kb ? 0u : vr.z >> 16;
             W.vl[lane] = v;
             W.vp[lane] = pv;
             W.lo[lane] = f0;
@@ -1351,7 +1362,7 @@ __global__ void __launch_bounds__(B, 8) k_tri_items_sp(const uint32_t* __restric
                                                         const int64_t* __restrict__ ov,
                                                         const int64_t* __restrict__ off,
                                                         const uint32_t* __restrict__ tgs,
-                                                        const uint32_t* __restrict__ fbo,
+                                                        const uint4* __restrict__ vrec,
                                                         const int64_t* __restrict__ ioff,
                                                         const uint64_t* __restrict__ ikey,
                                                         const uint4* __restrict__ irec, int vmt,
@@ -1418,12 +1429,13 @@ __global__ void __launch_bounds__(B, 8) k_tri_items_sp(const uint32_t* __restric
                     const uint64_t p = tpay(word, tc, ov, b + v0 + k);
                     kf = (uint32_t)(p >> 32);   // m(c, x)
                     kb = (uint32_t)p;           // m(x, c)
-                    const uint32_t dv = (uint32_t)(off[x + 1] - off[x]);
+                    const uint4 vr = vrec[x];
+                    const uint32_t dv = vr.w;
                     const bool skip = vmt > 0 && dv >= (uint32_t)vmt && (uint32_t)(v0 + k) < dv;
-                    f0 = fbo[2 * x];
-                    b0 = fbo[2 * x + 1];
-                    lf = skip || !kf ? 0u : fbo[2 * x + 2] - f0;
-                    lb = skip || !kb ? 0u : fbo[2 * x + 3] - b0;
+                    f0 = vr.x;
+                    b0 = vr.y;
+                    lf = skip || !kf ? 0u : vr.z & 0xFFFFu;
+                    lb = skip || !kb ? 0u : vr.z >> 16;
                 }
                 L.vl[k] = x;
                 L.lo[2 * k] = f0;
@@ -2014,6 +2026,9 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         g.fbo = dev_alloc(sizeof(uint32_t) * (2 * n + 2), s);
         hipLaunchKernelGGL(k_split_off, dim3(grid(s, n + 1)), dim3(256), 0, st, P<int64_t>(g.off), n, ne,
                            P<uint32_t>(rk), (uint32_t)nF, (uint32_t)(nF + nB), P<uint32_t>(g.fbo));
+        g.vrec = dev_alloc(sizeof(uint4) * n, s);
+        hipLaunchKernelGGL(k_vrec, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), P<uint32_t>(g.fbo), n,
+                           P<uint4>(g.vrec));
         HIP_CHECK(hipGetLastError());
     }
     // in-lists and v-mode centers (CAPSMI_TRI_VMODE_T: the od(v) threshold; 0 = every edge from u)
@@ -2191,7 +2206,7 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
                                          : e512 ? k_tri_items_sp<4, false, 1024, 512> : k_tri_items_sp<4, false, 1024>);
                 set_lds_attr(reinterpret_cast<const void*>(kp), ldsp);
                 hipLaunchKernelGGL(kp, ig, dim3(B), ldsp, st, P<uint32_t>(g.tg), tc, P<int64_t>(g.ov), P<int64_t>(g.off),
-                                   P<uint32_t>(g.tgs), P<uint32_t>(g.fbo), P<int64_t>(g.ioff), P<uint64_t>(g.ikey),
+                                   P<uint32_t>(g.tgs), P<uint4>(g.vrec), P<int64_t>(g.ioff), P<uint64_t>(g.ikey),
                                    P<uint4>(g.irec), g.vmt, cs, nitems, P<uint64_t>(iq), P<unsigned long long>(ctr),
                                    P<unsigned long long>(out));
                 return;
@@ -2208,7 +2223,7 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
         if (sn > 0 && g.split && lists) {
             const int64_t gs = std::min<int64_t>((sn + 3) / 4, (int64_t)s->num_cus * 16);
             hipLaunchKernelGGL(k_tri_small_sp<4>, dim3((unsigned)gs), dim3(kTriBlock), 0, st, P<uint32_t>(g.tg), tc,
-                               P<int64_t>(g.ov), P<int64_t>(g.off), P<uint32_t>(g.tgs), P<uint32_t>(g.fbo), g.vmt,
+                               P<int64_t>(g.ov), P<int64_t>(g.off), P<uint32_t>(g.tgs), P<uint4>(g.vrec), g.vmt,
                                sp, sn, P<unsigned long long>(out));
         } else if (sn > 0) {
             const int64_t gs = std::min<int64_t>((sn + 3) / 4, (int64_t)s->num_cus * 16);
