@@ -119,7 +119,7 @@ def parse():
                    help="diagnostic (C3, C4, C5): the distributed route at world size 1 over RCCL (launch with "
                         "torch.distributed.run --nproc-per-node 1): the route's fixed per-rank cost, exchanges included")
     p.add_argument("--plan-in-step", action="store_true",
-                   help="C3 planned modes: build each step's plan inside the timed region (before round 5's "
+                   help="planned modes (C3; the routed C2 / C4 / C5): build each step's plan inside the timed region (before round 5's "
                         "SURVEY.md 8d timing, the planning was part of every step)")
     p.add_argument("--tri-parts", type=int, default=0,
                    help="diagnostic (C4, one GPU): the interleaved center shares of N ranks of one "
@@ -823,19 +823,23 @@ def run_single(args):
                                     src_col="source", dst_col="target")])
         sess.set_fused(route == "planner")
 
-    def step():
-        if route != "direct" and wl == "c4":  # the routed query on every rank; the count is whole on each
-            t, outs = Planner(sg).run(C4_QUERY)
+    def plan_of():  # the routed query's lazy plan (holds no rows, runs nothing until its first action)
+        return Planner(sg).run({"c4": C4_QUERY, "c5": C5_QUERY}.get(wl, C2_QUERY))
+
+    def run_plan(plan):  # from handing the plan to the backend to the answer on the host
+        t, outs = plan
+        if wl == "c4":  # the routed query on every rank; the count is whole on each
             return int(t.column(outs[0][2]).values[0]), None
-        if route != "direct" and wl == "c5":  # rows of this rank's owned start nodes (partitioned)
-            t, outs = Planner(sg).run(C5_QUERY)
+        if wl == "c5":  # rows of this rank's owned start nodes (partitioned)
             t.size  # materialise inside the timed region
             cache["c5_cols"] = [outs[0][2], outs[1][2]]
             return None, t
-        if route != "direct":  # the Cypher query through the planner mirror
-            t, outs = Planner(sg).run(C2_QUERY)
-            cache["outs"] = [outs[0][2], outs[1][2]]
-            return t.size, t
+        cache["outs"] = [outs[0][2], outs[1][2]]  # C2 through the planner mirror
+        return t.size, t
+
+    def step():
+        if route != "direct":
+            return run_plan(plan_of())
         if wl == "c2":
             a_ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id", pred)
             b_ok = graph.NodeBitmap(sess, 0, n).add_scan(nodes, "id")
@@ -889,6 +893,12 @@ def run_single(args):
 
     for _ in range(args.warmup):
         step()
+    plan_ms = None
+    if route != "direct" and not args.plan_in_step:  # as the C3 modes: each timed step executes its own
+        tp = time.perf_counter()                     # plan, built before the timed region (timed apart)
+        queue = [plan_of() for _ in range(args.steps)]
+        plan_ms = (time.perf_counter() - tp) / args.steps * 1e3
+        inner_step = lambda: run_plan(queue.pop(0))  # noqa: E731 (each plan executed once, then dropped)
     if gate is not None:
         gate.busy = 0.0
     _lib.call("capsmi_session_set_profiling", sess.handle, 1)
@@ -1006,6 +1016,13 @@ def run_single(args):
                                      f"its own, collectives excluded; ms_per_step above is NOT a multi-GPU time",
                              "busy_ms_per_rank": [round(x, 3) for x in bt.tolist()],
                              "busy_ms_max": round(max(bt.tolist()), 3)}
+    if route != "direct":
+        if plan_ms is not None:  # planning outside the timed region, reported beside it
+            line["query"]["plan_ms"] = plan_ms
+            line["query"]["ms_per_step_with_planning"] = sec * 1e3 + plan_ms
+        line["query"]["timed_region"] = ("SURVEY.md 8d: from handing each step's lazy plan to the backend to the "
+                                         "answer on the host; planning timed apart (plan_ms)" if plan_ms is not None
+                                         else "planning inside each step (--plan-in-step)")
     if dist_route:
         line["config"]["route"] = f"Planner(sg).run over a distributed graph ({route_counts(sess)})"
         line["config"]["parallelism"] = (

@@ -513,6 +513,11 @@ capsmi_status capsmi_session_destroy(capsmi_session* s) {
     alloc_ctx_close(s);
     (void)hipStreamSynchronize(s->stream);
     (void)hipStreamSynchronize(s->own_stream);
+    for (auto& p : s->pending) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    for (hipEvent_t e : s->ev_pool) (void)hipEventDestroy(e);
     (void)hipHostFree(s->pinned);
     (void)hipStreamDestroy(s->own_stream);
     delete s;
@@ -539,6 +544,14 @@ capsmi_status capsmi_session_set_profiling(capsmi_session* s, int32_t enabled) {
     API_BEGIN
     need(s, "session");
     s->prof = enabled != 0;
+    if (s->prof) {  // the timers' events made here, not inside the timed queries
+        use_device(s);
+        while (s->ev_pool.size() < 1024) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreate(&e) != hipSuccess) break;
+            s->ev_pool.push_back(e);
+        }
+    }
     API_END
 }
 
@@ -584,8 +597,8 @@ capsmi_status capsmi_session_kernel_time(capsmi_session* s, const char* name, in
         auto& t = s->totals[p.name];
         t.first += 1;
         t.second += ms;
-        (void)hipEventDestroy(p.a);
-        (void)hipEventDestroy(p.b);
+        s->ev_pool.push_back(p.a);
+        s->ev_pool.push_back(p.b);
     }
     s->pending.clear();
     auto it = s->totals.find(name);

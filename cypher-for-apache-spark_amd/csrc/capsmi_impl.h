@@ -145,6 +145,17 @@ struct capsmi_session {
         hipEvent_t a, b;
     };
     std::vector<Pending> pending;
+    std::vector<hipEvent_t> ev_pool;  // resolved timer events, reused (no event creation inside a timed query)
+    hipEvent_t take_event() {
+        hipEvent_t e = nullptr;
+        if (!ev_pool.empty()) {
+            e = ev_pool.back();
+            ev_pool.pop_back();
+        } else if (hipEventCreate(&e) != hipSuccess) {
+            e = nullptr;
+        }
+        return e;
+    }
     std::map<std::string, std::pair<int64_t, double>> totals;
     std::map<std::string, double> alg_bytes;  // algorithmic bytes of the timed launches, per name
     // fused-path routing of lazy plans (plan.hip): enabled flag and per-route counters
@@ -170,9 +181,16 @@ struct KernelTimer {
     hipEvent_t a = nullptr, b = nullptr;
     // bytes: the launch's algorithmic bytes (inputs read once, outputs written once), if known
     KernelTimer(capsmi_session* s_, const char* n, double bytes = 0) : s(s_), name(n) {
-        if (s->prof && hipEventCreate(&a) == hipSuccess && hipEventCreate(&b) == hipSuccess) {
+        if (!s->prof) return;
+        a = s->take_event();
+        b = s->take_event();
+        if (a && b) {
             (void)hipEventRecord(a, s->stream);
             if (bytes > 0) s->alg_bytes[name] += bytes;
+        } else {
+            for (hipEvent_t* e : {&a, &b})
+                if (*e) s->ev_pool.push_back(*e);
+            a = b = nullptr;
         }
     }
     ~KernelTimer() {

@@ -89,7 +89,8 @@ __global__ void k_t(const int64_t* __restrict__ src, const int64_t* __restrict__
 // pass 4: per node, the count over lengths lower..upper; flags rows with count > 0
 __global__ void k_final(int64_t n, Dom d, int lower, int upper, const unsigned long long* __restrict__ od,
                         const unsigned long long* __restrict__ s, const unsigned long long* __restrict__ T2,
-                        const unsigned long long* __restrict__ T3, int64_t* __restrict__ cnt, uint8_t* __restrict__ f) {
+                        const unsigned long long* __restrict__ T3, int64_t* __restrict__ cnt, uint8_t* __restrict__ f,
+                        int64_t own_lo, int64_t own_hi) {  // rows only for the owned a (relative [own_lo, own_hi))
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t a = d.lo + i;
         int64_t total = 0;
@@ -104,7 +105,7 @@ __global__ void k_final(int64_t n, Dom d, int lower, int upper, const unsigned l
             if (lower <= 3 && upper >= 3) total += c3;
         }
         cnt[i] = total;
-        f[i] = total > 0 ? 1 : 0;
+        f[i] = total > 0 && i >= own_lo && i < own_hi ? 1 : 0;
     }
 }
 
@@ -532,23 +533,23 @@ __global__ void k_vl_bmerge(const int64_t* __restrict__ jst, int nt, int64_t blo
 }
 
 // (od(b), Y(b) = W(b) - s(b) b_ok(b)) side by side: pass 3 gathers both with one access
-// (od, Y) also as one 8-byte word, od << 40 | Y, while od < 2^24 and 0 <= Y < 2^40 everywhere (*fits cleared
-// otherwise): the T walk then gathers half the bytes
+// (od, Y) also as one 8-byte word, od << 40 | Y, while od < 2^24 and 0 <= Y < 2^40 everywhere (*misfit set
+// otherwise; zeroed with the other accumulators): the T walk then gathers half the bytes
 constexpr int kPkShift = 40;
-__device__ __forceinline__ void pack8(int64_t i, long long od, long long y, unsigned long long* pk, unsigned int* fits) {
+__device__ __forceinline__ void pack8(int64_t i, long long od, long long y, unsigned long long* pk, unsigned int* misfit) {
     const bool ok = od >= 0 && od < (1LL << (64 - kPkShift)) && y >= 0 && y < (1LL << kPkShift);
     pk[i] = ((unsigned long long)od << kPkShift) | (unsigned long long)y;
-    if (!ok) atomicAnd(fits, 0u);
+    if (!ok) atomicOr(misfit, 1u);
 }
 
 __global__ void k_vl_y(int64_t n, const uint32_t* __restrict__ bw, int b_full, const unsigned long long* __restrict__ od,
                        const unsigned long long* __restrict__ W, const unsigned long long* __restrict__ sl,
-                       longlong2* __restrict__ ody, unsigned long long* __restrict__ pk, unsigned int* __restrict__ fits) {
+                       longlong2* __restrict__ ody, unsigned long long* __restrict__ pk, unsigned int* __restrict__ misfit) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const long long o = (long long)od[i];
         const long long y = (long long)W[i] - (bit_of(bw, b_full, (uint32_t)i) ? (long long)sl[i] : 0LL);
         ody[i] = make_longlong2(o, y);
-        if (pk) pack8(i, o, y, pk, fits);
+        if (pk) pack8(i, o, y, pk, misfit);
     }
 }
 
@@ -561,10 +562,10 @@ __global__ void k_vl_yonly(int64_t n, const uint32_t* __restrict__ bw, int b_ful
 }
 
 __global__ void k_vl_pack(int64_t n, const long long* __restrict__ od, const long long* __restrict__ Y,
-                          longlong2* __restrict__ ody, unsigned long long* __restrict__ pk, unsigned int* __restrict__ fits) {
+                          longlong2* __restrict__ ody, unsigned long long* __restrict__ pk, unsigned int* __restrict__ misfit) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         ody[i] = make_longlong2(od[i], Y[i]);
-        if (pk) pack8(i, od[i], Y[i], pk, fits);
+        if (pk) pack8(i, od[i], Y[i], pk, misfit);
     }
 }
 
@@ -596,9 +597,9 @@ __global__ void __launch_bounds__(kVlBlock) k_vl_t(ChunkWalk cw, const uint32_t*
                                                    unsigned long long* __restrict__ T3, RegionBloom bl,
                                                    const uint32_t* __restrict__ f2, PairHash h,
                                                    const unsigned long long* __restrict__ pk,
-                                                   const unsigned int* __restrict__ fits) {
+                                                   const unsigned int* __restrict__ misfit) {
     extern __shared__ unsigned long long vl_lds[];
-    const bool p8 = ody && pk && *fits;  // uniform: the 8-byte (od, Y) words
+    const bool p8 = ody && pk && *misfit == 0;  // uniform: the 8-byte (od, Y) words
     unsigned long long *a_t2 = vl_lds, *a_t3 = vl_lds + kVlIds;
     for (int i = threadIdx.x; i < kVlIds; i += kVlBlock) a_t2[i] = a_t3[i] = 0;
     __syncthreads();
@@ -658,6 +659,36 @@ inline int grid(const capsmi_session* s, int64_t n) {
     return (int)g;
 }
 
+// the accumulators and flags of one query zeroed by one launch (blockIdx.y = buffer) instead of a fill each:
+// at 1/8 of C5 a fill is ~2 us of device time behind ~5 us of host launch time
+constexpr int kZeroMax = 8;
+struct ZeroList {
+    unsigned long long* p[kZeroMax];
+    int64_t n[kZeroMax];  // 8-byte words
+};
+
+__global__ void k_vl_zero(ZeroList z) {
+    unsigned long long* p = z.p[blockIdx.y];
+    const int64_t n = z.n[blockIdx.y];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0;
+}
+
+void zero_words(capsmi_session* s, std::initializer_list<std::pair<void*, int64_t>> bufs) {
+    ZeroList z{};
+    int k = 0;
+    int64_t nmax = 0;
+    for (const auto& b : bufs) {
+        if (!b.first || b.second <= 0) continue;
+        REQUIRE(k < kZeroMax, CAPSMI_ERR_INTERNAL, "zero_words: too many buffers");
+        z.p[k] = static_cast<unsigned long long*>(b.first);
+        z.n[k] = b.second;
+        nmax = std::max(nmax, b.second);
+        ++k;
+    }
+    if (!k) return;
+    hipLaunchKernelGGL(k_vl_zero, dim3(grid(s, nmax), k), dim3(256), 0, s->stream, z);
+}
+
 }  // namespace varlen
 
 // rows (a, count) of the fused var-length grouped count; returns the table's row count
@@ -672,8 +703,12 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
     const size_t nb = sizeof(uint64_t) * (n > 0 ? n : 1);
     Buf od = dev_alloc(nb, s), sl = dev_alloc(nb, s), W = dev_alloc(nb, s), T2 = dev_alloc(nb, s),
         T3 = dev_alloc(nb, s);
-    for (Buf* b : {&od, &sl, &W, &T2, &T3}) HIP_CHECK(hipMemsetAsync(P<void>(*b), 0, nb, st));
     const bool need3 = upper >= 3;
+    // the (od, Y) words and their misfit flag (behind them), the candidate count: zeroed with the rest
+    Buf pk = need3 ? dev_alloc(nb + sizeof(uint64_t), s) : Buf(), cand = need3 ? dev_alloc(sizeof(int64_t), s) : Buf();
+    const int64_t nw = (int64_t)(nb / sizeof(uint64_t));
+    zero_words(s, {{P<void>(od), nw}, {P<void>(sl), nw}, {P<void>(W), nw}, {P<void>(T2), nw}, {P<void>(T3), nw},
+                   {need3 ? static_cast<void*>(P<unsigned long long>(pk) + nw) : nullptr, 1}, {P<void>(cand), 1}});
     int64_t mtot = 0;
     for (int i = 0; i < nt; ++i) mtot += ms[i] > 0 ? ms[i] : 0;
     if (n > 0 && n < (int64_t(1) << 24) && mtot > 0) {  // hkey: ids < 2^24 - 1
@@ -697,8 +732,8 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
         for (const void* f : {reinterpret_cast<const void*>(k_vl_deg), reinterpret_cast<const void*>(k_vl_w),
                               reinterpret_cast<const void*>(k_vl_t)})
             HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
-        Buf ody, pk, bw, hk, hc, cand, f2;
-        unsigned int* fits = nullptr;
+        Buf ody, bw, hk, hc, f2;
+        unsigned int* misfit = nullptr;
         RegionBloom bl{nullptr, 0, 0, 0};
         PairHash h{nullptr, nullptr, nullptr, 0};
         if (need3) {
@@ -729,8 +764,6 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
                 hipLaunchKernelGGL(k_vl_bmerge, dim3(grid(s, (int64_t)(rbytes / 16) * nreg)), dim3(256), 0, st, ct.jst,
                                    L.nt, ct.g2, P<uint4>(part), bl);
             }
-            cand = dev_alloc(sizeof(int64_t), s);
-            HIP_CHECK(hipMemsetAsync(P<void>(cand), 0, sizeof(int64_t), st));
         }
         // candidates of the reverse-multiplicity count: a list written by the degree walk (default), or
         // the F2 filter tested again in the T walk (CAPSMI_VL_F2=1, the earlier form; A/B)
@@ -781,12 +814,10 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
                                    P<unsigned long long>(cand), h);
             }
             ody = dev_alloc(2 * nb, s);
-            pk = dev_alloc(nb + sizeof(unsigned int), s);  // the 8-byte words, then the fits flag
-            fits = reinterpret_cast<unsigned int*>(P<unsigned long long>(pk) + n);
-            HIP_CHECK(hipMemsetAsync(fits, 1, sizeof(unsigned int), st));  // nonzero: fits
+            misfit = reinterpret_cast<unsigned int*>(P<unsigned long long>(pk) + nw);
             hipLaunchKernelGGL(k_vl_y, dim3(grid(s, n)), dim3(256), 0, st, n, d.b, d.b_full, P<unsigned long long>(od),
                                P<unsigned long long>(W), P<unsigned long long>(sl), P<longlong2>(ody),
-                               P<unsigned long long>(pk), fits);
+                               P<unsigned long long>(pk), misfit);
         }
         {
             KernelTimer kt(s, "varlen_t");
@@ -794,7 +825,7 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
             hipLaunchKernelGGL(k_vl_t, dim3(g), dim3(kVlBlock), lds2, st, cw, d.a, d.a_full, n, P<unsigned long long>(od),
                                need3 ? P<longlong2>(ody) : nullptr, P<unsigned long long>(T2),
                                P<unsigned long long>(T3), bl, P<uint32_t>(f2), ht,
-                               need3 ? P<unsigned long long>(pk) : nullptr, fits);
+                               need3 ? P<unsigned long long>(pk) : nullptr, misfit);
         }
         if (need3) {
             KernelTimer kt(s, "varlen_recip");
@@ -859,7 +890,7 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
     Buf cnt = dev_alloc(nb, s), flags = dev_alloc(n > 0 ? n : 1, s);
     hipLaunchKernelGGL(k_final, dim3(grid(s, n)), dim3(256), 0, st, n, d, lower, upper, P<unsigned long long>(od),
                        P<unsigned long long>(sl), P<unsigned long long>(T2), P<unsigned long long>(T3),
-                       P<int64_t>(cnt), P<uint8_t>(flags));
+                       P<int64_t>(cnt), P<uint8_t>(flags), (int64_t)0, n);
     HIP_CHECK(hipGetLastError());
     Buf idx;
     const int64_t rows = flags_to_indices(s, P<uint8_t>(flags), n, idx);
@@ -895,7 +926,7 @@ struct VarlenShard {
     bool need3 = false;
     part::Layout L{};
     ChunkPart cp;  // out, by source slice
-    Buf sl, W, T2, T3, ody, pk, bw, hk, hc;
+    Buf sl, W, T2, T3, ody, pk, bw, hk, hc, cand;
     int64_t* od = nullptr;  // caller buffers (n int64 each), summed over ranks by the caller
     int64_t* y = nullptr;
 };
@@ -922,12 +953,16 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
     v->need3 = upper >= 3;
     v->od = od;
     const size_t nb = sizeof(uint64_t) * n;
-    HIP_CHECK(hipMemsetAsync(od, 0, nb, st));
     v->sl = dev_alloc(nb, s);
     v->W = dev_alloc(nb, s);
     v->T2 = dev_alloc(nb, s);
     v->T3 = dev_alloc(nb, s);
-    for (Buf* b : {&v->sl, &v->W, &v->T2, &v->T3}) HIP_CHECK(hipMemsetAsync(P<void>(*b), 0, nb, st));
+    if (v->need3) {  // finish()'s (od, Y) words + misfit flag, the candidate count: zeroed here with the rest
+        v->pk = dev_alloc(nb + sizeof(uint64_t), s);
+        v->cand = dev_alloc(sizeof(int64_t), s);
+    }
+    zero_words(s, {{od, n}, {P<void>(v->sl), n}, {P<void>(v->W), n}, {P<void>(v->T2), n}, {P<void>(v->T3), n},
+                   {v->need3 ? static_cast<void*>(P<unsigned long long>(v->pk) + n) : nullptr, 1}, {P<void>(v->cand), 1}});
     Layout& L = v->L;
     L.lo = v->d.lo;
     L.hi = v->d.hi;
@@ -988,8 +1023,8 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
         }
         sub.reset(new KernelTimer(s, "vls_rev_cand"));
         // candidates (reverse maybe present) of out ∪ in: one flat pass over the columns into a list
-        Buf cand = dev_alloc(sizeof(int64_t), s), clist = dev_alloc(sizeof(unsigned long long) * (size_t)mall, s);
-        HIP_CHECK(hipMemsetAsync(P<void>(cand), 0, sizeof(int64_t), st));
+        Buf& cand = v->cand;
+        Buf clist = dev_alloc(sizeof(unsigned long long) * (size_t)mall, s);
         for (int i = 0; i < na; ++i)
             if (am[i] > 0)
                 hipLaunchKernelGGL(k_vl_flatcand,
@@ -1029,8 +1064,10 @@ void varlen_shard_mid(VarlenShard* v, int64_t* y) {
     capsmi_session* s = v->s;
     hipStream_t st = s->stream;
     v->y = y;
-    HIP_CHECK(hipMemsetAsync(y, 0, sizeof(int64_t) * v->n, st));
-    if (!v->need3) return;
+    if (!v->need3) {  // no Y: the caller still sums the (zero) vector over the ranks
+        HIP_CHECK(hipMemsetAsync(y, 0, sizeof(int64_t) * v->n, st));
+        return;
+    }  // else k_vl_yonly writes every entry
     if (v->cp.pool) {
         const ChunkWalk cw{P<uint2>(v->cp.pool), P<unsigned long long>(v->cp.meta), v->cp.order, v->cp.jst,
                            v->cp.segbase, v->cp.ja, v->L.nt};
@@ -1051,16 +1088,14 @@ int64_t varlen_shard_finish(VarlenShard* v, Buf& out_ids, Buf& out_cnt) {
     capsmi_session* s = v->s;
     hipStream_t st = s->stream;
     const int64_t n = v->n;
-    unsigned int* fits = nullptr;
+    unsigned int* misfit = nullptr;
     if (v->need3) {
         REQUIRE(v->y != nullptr, CAPSMI_ERR_ILLEGAL_ARGUMENT, "varlen shard: mid() before finish()");
         v->ody = dev_alloc(2 * sizeof(int64_t) * n, s);
-        v->pk = dev_alloc(sizeof(unsigned long long) * n + sizeof(unsigned int), s);
-        fits = reinterpret_cast<unsigned int*>(P<unsigned long long>(v->pk) + n);
-        HIP_CHECK(hipMemsetAsync(fits, 1, sizeof(unsigned int), st));  // nonzero: fits
+        misfit = reinterpret_cast<unsigned int*>(P<unsigned long long>(v->pk) + n);  // zeroed in begin()
         hipLaunchKernelGGL(k_vl_pack, dim3(grid(s, n)), dim3(256), 0, st, n, reinterpret_cast<const long long*>(v->od),
                            reinterpret_cast<const long long*>(v->y), P<longlong2>(v->ody), P<unsigned long long>(v->pk),
-                           fits);
+                           misfit);
     }
     if (v->cp.pool) {
         const ChunkWalk cw{P<uint2>(v->cp.pool), P<unsigned long long>(v->cp.meta), v->cp.order, v->cp.jst,
@@ -1071,14 +1106,13 @@ int64_t varlen_shard_finish(VarlenShard* v, Buf& out_ids, Buf& out_cnt) {
                            v->need3 ? P<longlong2>(v->ody) : nullptr, P<unsigned long long>(v->T2),
                            P<unsigned long long>(v->T3), RegionBloom{nullptr, 0, 0, 0}, nullptr,
                            PairHash{nullptr, nullptr, nullptr, 0}, v->need3 ? P<unsigned long long>(v->pk) : nullptr,
-                           fits);
+                           misfit);
     }
     Buf cnt = dev_alloc(sizeof(int64_t) * n, s), flags = dev_alloc(n, s);
     hipLaunchKernelGGL(k_final, dim3(grid(s, n)), dim3(256), 0, st, n, v->d, v->lower, v->upper,
                        reinterpret_cast<const unsigned long long*>(v->od), P<unsigned long long>(v->sl),
-                       P<unsigned long long>(v->T2), P<unsigned long long>(v->T3), P<int64_t>(cnt), P<uint8_t>(flags));
-    if (v->own_lo > 0) HIP_CHECK(hipMemsetAsync(P<uint8_t>(flags), 0, v->own_lo, st));  // rows of owned a only
-    if (v->own_hi < n) HIP_CHECK(hipMemsetAsync(P<uint8_t>(flags) + v->own_hi, 0, n - v->own_hi, st));
+                       P<unsigned long long>(v->T2), P<unsigned long long>(v->T3), P<int64_t>(cnt), P<uint8_t>(flags),
+                       v->own_lo, v->own_hi);
     HIP_CHECK(hipGetLastError());
     Buf idx;
     const int64_t rows = flags_to_indices(s, P<uint8_t>(flags), n, idx);
