@@ -210,8 +210,9 @@ def _sharded(session, n, src, dst, a_mask, b_mask, lo, hi, nparts):
     b_ok = graph.NodeBitmap(session, 0, n).add_scan(session.table([ColumnData("id", I64, np.nonzero(b_mask)[0])]))
     nw = (n + 31) // 32
     bounds = [(min(32 * (r * nw // nparts), n), min(32 * ((r + 1) * nw // nparts), n)) for r in range(nparts)]
-    ods = [torch.zeros(n, dtype=torch.int64, device="cuda") for _ in range(nparts)]
-    ys = [torch.zeros(n, dtype=torch.int64, device="cuda") for _ in range(nparts)]
+    # garbage in the caller's buffers: begin() must zero od, mid() must write (or clear) every Y entry
+    ods = [torch.full((n,), 7777, dtype=torch.int64, device="cuda") for _ in range(nparts)]
+    ys = [torch.full((n,), -999, dtype=torch.int64, device="cuda") for _ in range(nparts)]
     shards = []
     for r, (ol, oh) in enumerate(bounds):
         own_s = (src >= ol) & (src < oh)
@@ -251,6 +252,25 @@ def test_sharded_matches_enumeration(session, nparts):
         got = _sharded(session, n, src, dst, a_mask, b_mask, lo, hi, nparts)
         _, g = cpu.var_length_count(n, src, dst, lo, hi, a_mask.astype(np.uint8), b_mask.astype(np.uint8))
         assert got == {int(i): int(g[i]) for i in np.nonzero(g)[0]}
+
+
+@pytest.mark.gpu
+def test_pack_misfit_hub(session):
+    """A source with od >= 2^24 does not fit the 8-byte (od, Y) words: the misfit flag (zeroed with the
+    accumulators, raised by k_vl_y / k_vl_pack) sends the T walk to the 16-byte (od, Y) pairs.  Single
+    GPU and sharded over 2 owners, against the closed form."""
+    rng = np.random.default_rng(11)
+    n, hub, rest = 1000, (1 << 24) + 1000, 20_000
+    src = np.concatenate([np.zeros(hub, np.int64), rng.integers(0, n, rest)]).astype(np.int64)
+    dst = np.concatenate([rng.integers(0, n, hub), rng.integers(0, n, rest)]).astype(np.int64)
+    ones = np.ones(n, dtype=np.uint8)
+    _, g = cpu.var_length_closed_form(n, src, dst, 1, 3, ones, ones)
+    want = {int(i): int(g[i]) for i in np.nonzero(g)[0]}
+    from capsmi import ColumnData, I64, graph
+    full = graph.NodeBitmap(session, 0, n).add_scan(session.table([ColumnData("id", I64, np.arange(n))]))
+    out = graph.var_length_count(session, [_table(session, src, dst)], full, full, 1, 3, "a", "cnt")
+    assert dict(zip(out.column("a").values.tolist(), out.column("cnt").values.tolist())) == want
+    assert _sharded(session, n, src, dst, ones.astype(bool), ones.astype(bool), 1, 3, 2) == want
 
 
 @pytest.mark.gpu
