@@ -1,7 +1,8 @@
 """Host timeline of the C3 cold route (diagnostic): every libcapsmi call one step makes, with its
 start offset and duration, so the device-idle window between two steps (result read -> next
 query's first launch) can be attributed to Python planning, library calls or syncs.
-Usage: python3 scripts/host_calls.py [scale] [mode: cold|direct]"""
+Usage: python3 scripts/host_calls.py [scale] [plan: pre|in]  (pre: the plan built before the step, as bench.py
+times it per SURVEY 8d; in: planning inside the step)"""
 import os
 import sys
 import time
@@ -34,8 +35,11 @@ def traced(name, *args):
         LOG.append((name, t0, time.perf_counter()))
 
 
-def step():
-    t, outs = Planner(sg).run(bench.C3_QUERY)
+pre = (sys.argv[2] if len(sys.argv) > 2 else "pre") == "pre"
+
+
+def step(plan=None):
+    t, outs = plan if plan is not None else Planner(sg).run(bench.C3_QUERY)
     return int(t.column(outs[0][2]).values[0])
 
 
@@ -45,9 +49,11 @@ torch.cuda.synchronize()
 _lib.call = traced  # the modules call _lib.call through the module attribute
 steps = []
 for _ in range(5):
+    plan = Planner(sg).run(bench.C3_QUERY) if pre else None
+    torch.cuda.synchronize()
     LOG.clear()
     t0 = time.perf_counter()
-    r = step()
+    r = step(plan)
     t1 = time.perf_counter()
     steps.append((t0, t1, list(LOG)))
 for t0, t1, log in steps[-2:]:
