@@ -144,6 +144,14 @@ __host__ __device__ constexpr int64_t chunks_per_block(int64_t m, int64_t grid, 
 
 __device__ __forceinline__ bool bit(const part::BitV& v, uint64_t x) { return v.full || part::gbit(v.w, (uint32_t)x); }
 
+// FULL: every node filter full (a query without node predicates) -- the tests fold away and the filter views
+// leave the kernel's scalar registers (the general form spills them to VGPR lanes).  Taken for the undirected
+// form only: C3u's und_count_part 11.50 -> 10.63 ms; the directed form, already at 128 VGPRs, spills 108 bytes
+// to scratch when specialised -- the 64-bit addresses of its misaligned / last-tile load path -- and
+// count_part goes 6.94 -> 10.85 ms
+template <bool FULL>
+__device__ __forceinline__ bool fbit(const part::BitV& v, uint64_t x) { return FULL || bit(v, x); }
+
 // One read of the relationships, two record kinds into 2 * nb buckets:
 //   bucket t >> 16        (the in side):  t & 0xFFFF for relationships s -> t with a_ok(s);
 //   bucket nb + (s >> 16) (the out side): s & 0xFFFF for relationships s -> t with c_ok(t);
@@ -153,7 +161,7 @@ __device__ __forceinline__ bool bit(const part::BitV& v, uint64_t x) { return v.
 // a_ok(x) and an out record of x when c_ok(y), so the walks give sum_b b_ok(b) inU(b) outU(b); `loops`
 // gets the bindings with r1 = r2 (a non-loop walked in and back out, [a(s) b(t) c(s)] + [a(t) b(s) c(t)], a
 // loop [a b c](s)).
-template <bool UND>
+template <bool UND, bool FULL = false>
 __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                  int64_t m, int64_t lo, int64_t range, int nb, part::BitV a, part::BitV b,
                                                  part::BitV c, int64_t chunk0, int64_t cpb, uint16_t* __restrict__ pool,
@@ -197,11 +205,11 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
             const int64_t e = t0 + part::item_off<kB>(u);
             const uint64_t x = (uint64_t)(sr[u] - lo), y = (uint64_t)(tr[u] - lo);
             const bool ok = e < m && x < (uint64_t)range && y < (uint64_t)range;
-            const bool ain = ok && bit(a, x), aout = ok && bit(c, y);
+            const bool ain = ok && fbit<FULL>(a, x), aout = ok && fbit<FULL>(c, y);
             if constexpr (!UND) {
-                if (ain && x == y && bit(b, x) && bit(c, x)) ++nl;
+                if (ain && x == y && fbit<FULL>(b, x) && fbit<FULL>(c, x)) ++nl;
             } else if (ok) {  // the reverse arc y -> x of a non-loop, and the r1 = r2 bindings
-                const bool ay = bit(a, y), cx = bit(c, x), bx = bit(b, x), by = bit(b, y);
+                const bool ay = fbit<FULL>(a, y), cx = fbit<FULL>(c, x), bx = fbit<FULL>(b, x), by = fbit<FULL>(b, y);
                 const bool two = x != y;
                 vin2 |= (two && ay ? 1u : 0u) << u;
                 vout2 |= (two && cx ? 1u : 0u) << u;
@@ -539,7 +547,8 @@ void count_rec_begin(capsmi_session* s, const int64_t* const* srcs, const int64_
     HIP_CHECK(hipMemsetAsync(P<void>(cr.acc), 0, 2 * sizeof(unsigned long long), st));
     static std::once_flag once;
     std::call_once(once, [] {
-        for (const void* f : {reinterpret_cast<const void*>(k_rec_part<false>), reinterpret_cast<const void*>(k_rec_part<true>)})
+        for (const void* f : {reinterpret_cast<const void*>(k_rec_part<false>), reinterpret_cast<const void*>(k_rec_part<true>),
+                              reinterpret_cast<const void*>(k_rec_part<true, true>)})
             HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)part_lds(2 * kMaxBuckets)));
         for (const void* f : {reinterpret_cast<const void*>(k_rec_walk<false>), reinterpret_cast<const void*>(k_rec_walk<true>)})
             HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -573,7 +582,10 @@ void count_rec_begin(capsmi_session* s, const int64_t* const* srcs, const int64_
         HIP_CHECK(hipMemsetAsync(P<void>(cp.meta), 0, sizeof(unsigned long long) * npool, st));
         for (int i = 0; i < nt; ++i) {
             if (ms[i] <= 0) continue;
-            hipLaunchKernelGGL(undirected ? k_rec_part<true> : k_rec_part<false>, dim3(g1[i]), dim3(kB), part_lds(2 * nb), st,
+            const char* fe = getenv("CAPSMI_REC_FULL");  // A/B: 0 keeps the general form
+            const bool full = a.full && b.full && c.full && !(fe && atoi(fe) == 0);
+            auto kf = undirected ? (full ? k_rec_part<true, true> : k_rec_part<true>) : k_rec_part<false>;
+            hipLaunchKernelGGL(kf, dim3(g1[i]), dim3(kB), part_lds(2 * nb), st,
                                srcs[i], dsts[i], ms[i], lo, n, nb, a, b, c, c0[i], cpb[i], P<uint16_t>(cp.pool),
                                P<unsigned long long>(cp.meta), P<unsigned long long>(cr.acc));
         }
