@@ -110,12 +110,15 @@ def test_route_miss_counter_and_unrouted_guard(session):
 
 
 @pytest.mark.parametrize("scale", [16, 20])
-def test_undirected_two_hop_vs_fixture(session, scale):
-    """count(*) through the two-sided record partition with both arcs (k_count.hip k_rec_part<true>), and the
-    atomic form (CAPSMI_COUNT=atomic, A/B), and count(DISTINCT c), against the committed closed-form fixtures
-    (tests/golden/rmat_full.json c3u_s16 / c3u_s20; oracle/closed.c orc_two_hop_undirected_closed_form)."""
+@pytest.mark.parametrize("full_form", ["1", "0"])
+def test_undirected_two_hop_vs_fixture(session, scale, full_form, monkeypatch):
+    """count(*) through the two-sided record partition with both arcs (k_count.hip k_rec_part<true>; with every
+    node filter full, its full-filter form unless CAPSMI_REC_FULL=0), and the atomic form (CAPSMI_COUNT=atomic,
+    A/B), and count(DISTINCT c), against the committed closed-form fixtures (tests/golden/rmat_full.json
+    c3u_s16 / c3u_s20; oracle/closed.c orc_two_hop_undirected_closed_form)."""
     import json
     import os
+    monkeypatch.setenv("CAPSMI_REC_FULL", full_form)
     from capsmi.planner import EntityTable, Planner, ScanGraph, result_rows
     from capsmi import graph
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
