@@ -251,6 +251,10 @@ void fill_u8(uint8_t* p, uint8_t v, int64_t n, hipStream_t st);
 void iota_i64(int64_t* p, int64_t start, int64_t n, hipStream_t st);
 // indices i (ascending) with flags[i] != 0; returns count (synchronises)
 int64_t flags_to_indices(capsmi_session* s, const uint8_t* flags, int64_t n, Buf& out_idx);
+// the rows i < n with flags[i] set, as (id_base + i, val[i]) columns in row order, sized n; returns the row
+// count (read once, after the writes are queued)
+int64_t flags_to_rows(capsmi_session* s, const uint8_t* flags, int64_t n, const int64_t* val, int64_t id_base,
+                      Buf& out_ids, Buf& out_vals);
 // dst[i] = idx[i] < 0 ? null : src[idx[i]]; dst_valid written iff non-null
 void gather_col(const int64_t* src, const uint8_t* src_valid, const int64_t* idx, int64_t n,
                 int64_t* dst, uint8_t* dst_valid, hipStream_t st);

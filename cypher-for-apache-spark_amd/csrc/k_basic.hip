@@ -120,6 +120,31 @@ __global__ void __launch_bounds__(kBlock) k_flag_count(const uint8_t* __restrict
     if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
 }
 
+// the rows of the set flags as two columns at once: ids[pos] = base + i, vals[pos] = val[i] (flags_to_rows)
+__global__ void __launch_bounds__(kBlock) k_flag_rows(const uint8_t* __restrict__ f, int64_t n,
+                                                      const int64_t* __restrict__ off, const int64_t* __restrict__ val,
+                                                      int64_t id_base, int64_t* __restrict__ ids,
+                                                      int64_t* __restrict__ vals) {
+    const int64_t base = (int64_t)blockIdx.x * kTile + (int64_t)threadIdx.x * kItems;
+    uint8_t fl[kItems];
+    int64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+        fl[j] = (base + j < n && f[base + j]) ? 1 : 0;
+        c += fl[j];
+    }
+    __shared__ int64_t lds[kBlock / 64];
+    int64_t tot;
+    int64_t pos = block_excl_scan(c, lds, &tot) + off[blockIdx.x];
+#pragma unroll
+    for (int j = 0; j < kItems; ++j)
+        if (fl[j]) {
+            ids[pos] = id_base + base + j;
+            vals[pos] = val[base + j];
+            ++pos;
+        }
+}
+
 __global__ void __launch_bounds__(kBlock) k_flag_write(const uint8_t* __restrict__ f, int64_t n,
                                                        const int64_t* __restrict__ off,
                                                        int64_t* __restrict__ idx) {
@@ -215,6 +240,23 @@ int64_t flags_to_indices(capsmi_session* s, const uint8_t* flags, int64_t n, Buf
                        P<int64_t>(out_idx));
     HIP_CHECK(hipGetLastError());
     return total;
+}
+
+int64_t flags_to_rows(capsmi_session* s, const uint8_t* flags, int64_t n, const int64_t* val, int64_t id_base,
+                      Buf& out_ids, Buf& out_vals) {
+    hipStream_t st = s->stream;
+    out_ids = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
+    out_vals = dev_alloc(sizeof(int64_t) * (n > 0 ? n : 1), s);
+    if (n == 0) return 0;
+    const int64_t ntiles = (n + kTile - 1) / kTile;
+    Buf cnt = dev_alloc(sizeof(int64_t) * ntiles, s);
+    Buf off = dev_alloc(sizeof(int64_t) * (ntiles + 1), s);
+    hipLaunchKernelGGL(k_flag_count, dim3((unsigned)ntiles), dim3(kBlock), 0, st, flags, n, P<int64_t>(cnt));
+    exclusive_scan_i64(P<int64_t>(cnt), P<int64_t>(off), ntiles, s);
+    hipLaunchKernelGGL(k_flag_rows, dim3((unsigned)ntiles), dim3(kBlock), 0, st, flags, n, P<int64_t>(off), val, id_base,
+                       P<int64_t>(out_ids), P<int64_t>(out_vals));
+    HIP_CHECK(hipGetLastError());
+    return read_scalar(s, P<int64_t>(off) + ntiles);  // the one host round trip, behind the writes
 }
 
 void gather_col(const int64_t* src, const uint8_t* src_valid, const int64_t* idx, int64_t n, int64_t* dst,

@@ -892,17 +892,8 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
                        P<unsigned long long>(sl), P<unsigned long long>(T2), P<unsigned long long>(T3),
                        P<int64_t>(cnt), P<uint8_t>(flags), (int64_t)0, n);
     HIP_CHECK(hipGetLastError());
-    Buf idx;
-    const int64_t rows = flags_to_indices(s, P<uint8_t>(flags), n, idx);
-    out_ids = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), s);
-    out_cnt = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), s);
-    // ids = lo + idx; counts = cnt[idx]
-    gather_col(P<int64_t>(cnt), nullptr, P<int64_t>(idx), rows, P<int64_t>(out_cnt), nullptr, st);
-    if (rows > 0) {
-        HIP_CHECK(hipMemcpyAsync(P<void>(out_ids), P<void>(idx), sizeof(int64_t) * rows, hipMemcpyDeviceToDevice, st));
-        add_i64(P<int64_t>(out_ids), d.lo, rows, st);
-    }
-    return rows;
+    // rows (lo + i, cnt[i]) of the flagged a, written before the count is read
+    return flags_to_rows(s, P<uint8_t>(flags), n, P<int64_t>(cnt), d.lo, out_ids, out_cnt);
 }
 
 }  // namespace capsmi
@@ -1114,16 +1105,7 @@ int64_t varlen_shard_finish(VarlenShard* v, Buf& out_ids, Buf& out_cnt) {
                        P<unsigned long long>(v->T2), P<unsigned long long>(v->T3), P<int64_t>(cnt), P<uint8_t>(flags),
                        v->own_lo, v->own_hi);
     HIP_CHECK(hipGetLastError());
-    Buf idx;
-    const int64_t rows = flags_to_indices(s, P<uint8_t>(flags), n, idx);
-    out_ids = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), s);
-    out_cnt = dev_alloc(sizeof(int64_t) * (rows > 0 ? rows : 1), s);
-    gather_col(P<int64_t>(cnt), nullptr, P<int64_t>(idx), rows, P<int64_t>(out_cnt), nullptr, st);
-    if (rows > 0) {
-        HIP_CHECK(hipMemcpyAsync(P<void>(out_ids), P<void>(idx), sizeof(int64_t) * rows, hipMemcpyDeviceToDevice, st));
-        add_i64(P<int64_t>(out_ids), v->d.lo, rows, st);
-    }
-    return rows;
+    return flags_to_rows(s, P<uint8_t>(flags), n, P<int64_t>(cnt), v->d.lo, out_ids, out_cnt);
 }
 
 void varlen_shard_free(VarlenShard* v) { delete v; }
