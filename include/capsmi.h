@@ -191,7 +191,8 @@ capsmi_status capsmi_session_set_stream(capsmi_session* s, void* hip_stream);
 capsmi_status capsmi_session_use_stream(capsmi_session* s, void* hip_stream);
 capsmi_status capsmi_session_sync(capsmi_session* s);
 /* per-kernel HIP-event timing of the fused graph kernels (off by default; SURVEY.md §5 tracing).
- * While enabled, each hot launch is bracketed by events on the session stream. */
+ * While enabled, each hot launch is bracketed by events on the session stream.  Enabling creates a pool of
+ * events up front (resolved ones return to it), so timed queries make no event-creation calls. */
 capsmi_status capsmi_session_set_profiling(capsmi_session* s, int32_t enabled);
 /* resolve pending events (synchronises) and report totals for kernel `name` ("hop1", "hop2",
  * "expand_filter", "bitmap_add", ...): launches and summed milliseconds; then the counters reset. */
