@@ -536,40 +536,41 @@ __global__ void k_vrec(const int64_t* __restrict__ off, const uint32_t* __restri
 // (stable: edge order within a target); the v-mode items read the records through it
 __global__ void k_swap_keys_sp(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ off, int64_t ne,
                                TgCode tc, const uint32_t* __restrict__ tg, const uint32_t* __restrict__ rk,
-                               const uint32_t* __restrict__ fbo, uint64_t* __restrict__ ik, uint4* __restrict__ rec) {
+                               const uint32_t* __restrict__ fbo, const uint4* __restrict__ vrec,
+                               uint64_t* __restrict__ ik, uint4* __restrict__ rec) {
     constexpr int U = 4;  // edges per lane and pass, loads issued together
     const uint32_t idm = tc.idmask();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x * U;
     for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x * U + threadIdx.x; e0 < ne; e0 += stride) {
         uint64_t k[U];
-        uint32_t w[U], r0[U], r1[U];
-        int64_t of[U], t0[U], t1[U];
-        uint32_t fb0[U], fb1[U];
+        uint32_t w[U];
+        uint2 r[U], fb[U];
+        int64_t of[U];
+        uint32_t odt[U];
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             const int64_t e = min(e0 + (int64_t)j * blockDim.x, ne - 1);
             k[j] = ok_[e];
             w[j] = tg[e];
-            r0[j] = rk[2 * e];
-            r1[j] = rk[2 * e + 1];
+            r[j] = reinterpret_cast<const uint2*>(rk)[e];
         }
+        // three lane loads per edge: off(from), the from's list starts (one 8-byte word) and od(to) from the
+        // to's 16-byte vertex record (was: off(to) and off(to + 1), and the two starts apart)
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             const uint32_t from = (uint32_t)(k[j] >> 32), to = (uint32_t)k[j] & idm;
             of[j] = off[from];
-            t0[j] = off[to];
-            t1[j] = off[to + 1];
-            fb0[j] = fbo[2 * from];
-            fb1[j] = fbo[2 * from + 1];
+            fb[j] = reinterpret_cast<const uint2*>(fbo)[from];
+            odt[j] = vrec[to].w;
         }
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             const int64_t e = e0 + (int64_t)j * blockDim.x;
             if (e >= ne) break;
             const uint32_t from = (uint32_t)(k[j] >> 32), to = (uint32_t)k[j] & idm;
-            const bool take = e - of[j] < t1[j] - t0[j];
-            const uint32_t pfb = take ? (r0[j] - fb0[j]) | (r1[j] - fb1[j]) << 16 : 0u;
-            rec[e] = make_uint4(from | (w[j] & ~idm), pfb, fb0[j], fb1[j]);
+            const bool take = e - of[j] < (int64_t)odt[j];
+            const uint32_t pfb = take ? (r[j].x - fb[j].x) | (r[j].y - fb[j].y) << 16 : 0u;
+            rec[e] = make_uint4(from | (w[j] & ~idm), pfb, fb[j].x, fb[j].y);
             ik[e] = (uint64_t)to << 40 | (uint64_t)e;
         }
     }
@@ -2080,8 +2081,8 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
             Buf iv = g.split ? dev_alloc(sizeof(uint4) * ne, s) : packed ? Buf() : dev_alloc(sizeof(int64_t) * ne, s);
             if (g.split)  // iv: the records (k_swap_keys_sp)
                 hipLaunchKernelGGL(k_swap_keys_sp, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off),
-                                   ne, tc, P<uint32_t>(g.tg), P<uint32_t>(rk), P<uint32_t>(g.fbo), P<uint64_t>(ik),
-                                   P<uint4>(iv));
+                                   ne, tc, P<uint32_t>(g.tg), P<uint32_t>(rk), P<uint32_t>(g.fbo), P<uint4>(g.vrec),
+                                   P<uint64_t>(ik), P<uint4>(iv));
             else
                 hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off), ne,
                                    tc, P<uint64_t>(ik), packed ? nullptr : P<int64_t>(iv));
