@@ -425,15 +425,29 @@ __device__ __forceinline__ void split_flags(uint32_t w, TgCode tc, uint32_t& f, 
     b = (w >> (tc.ib + tc.cb)) & tc.cmask();
 }
 
+// a lane's 8 consecutive target words (base a multiple of 8): two 16-byte loads, 0 past ne
+__device__ __forceinline__ void load8_words(const uint32_t* __restrict__ tg, int64_t base, int64_t ne, uint32_t (&w)[8]) {
+    if (base + 8 <= ne) {
+        const uint4 a = reinterpret_cast<const uint4*>(tg + base)[0], b = reinterpret_cast<const uint4*>(tg + base)[1];
+        w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+        w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = base + j < ne ? tg[base + j] : 0u;
+    }
+}
+
 __global__ void __launch_bounds__(256) k_split_count(const uint32_t* __restrict__ tg, int64_t ne, TgCode tc,
                                                      int64_t* __restrict__ cnt, int64_t ntiles) {
     const int64_t base = (int64_t)blockIdx.x * kSplitTile + (int64_t)threadIdx.x * 8;
     int64_t cf = 0, cb = 0;
+    uint32_t w[8];
+    load8_words(tg, base, ne, w);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
         if (base + j < ne) {
             uint32_t f, b;
-            split_flags(tg[base + j], tc, f, b);
+            split_flags(w[j], tc, f, b);
             cf += f != 0;
             cb += b != 0;
         }
@@ -463,9 +477,9 @@ __global__ void __launch_bounds__(256) k_split_write(const uint32_t* __restrict_
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t w[8];
     uint32_t cf = 0, cb = 0;
+    load8_words(tg, base, ne, w);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        w[j] = base + j < ne ? tg[base + j] : 0u;
         uint32_t f, b;
         split_flags(w[j], tc, f, b);
         cf += f != 0;
@@ -494,8 +508,7 @@ __global__ void __launch_bounds__(256) k_split_write(const uint32_t* __restrict_
         if (e >= ne) break;
         uint32_t f, b;
         split_flags(w[j], tc, f, b);
-        rk[2 * e] = (uint32_t)rf;
-        rk[2 * e + 1] = (uint32_t)rb;
+        reinterpret_cast<uint2*>(rk)[e] = make_uint2((uint32_t)rf, (uint32_t)rb);
         if (f == tc.cmask() || b == tc.cmask()) {  // an exception: the exact multiplicities
             const uint64_t p = (uint64_t)ov[e];
             f = (uint32_t)min<uint64_t>(p >> 32, cap);

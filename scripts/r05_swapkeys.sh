@@ -1,4 +1,4 @@
-# Round 5: k_swap_keys_sp with three lane loads per edge (od(to) from vrec, the list starts as one word):
+# Round 5: C4 build load merging (k_swap_keys_sp: three lane loads per edge; k_split_count / k_split_write: 16-byte loads):
 # triangle parity, then the C4 line twice.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
