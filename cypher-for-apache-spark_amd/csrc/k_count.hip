@@ -161,6 +161,60 @@ __device__ __forceinline__ bool fbit(const part::BitV& v, uint64_t x) { return F
 // a_ok(x) and an out record of x when c_ok(y), so the walks give sum_b b_ok(b) inU(b) outU(b); `loops`
 // gets the bindings with r1 = r2 (a non-loop walked in and back out, [a(s) b(t) c(s)] + [a(t) b(s) c(t)], a
 // loop [a b c](s)).
+// One block scan for both per-bucket prefixes of a tile (k_rec_part): the record runs (loc, of cnt) and the
+// pieces the held + run records complete (pb, of pc = (hc + cnt) / kPiece), as the 16-bit halves of one word
+// (a tile holds at most 2 kT = 2^14 records and fewer than 2^12 pieces, so the low half never carries); the
+// pre-pass also opens the chunks the pieces need.  Three barriers where two scans and the pass between them
+// took seven.  Returns the tile's piece count.
+__device__ uint32_t scan_runs_pieces(const uint32_t* cnt, const uint16_t* hc, const uint16_t* fl, uint32_t* loc,
+                                     uint32_t* pc, uint32_t* pb, uint32_t* np, uint32_t* misc, int n,
+                                     uint32_t* wtot) {
+    const int per = (n + kB - 1) / kB;
+    const int b = threadIdx.x * per;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t sum = 0;
+    for (int k = 0; k < per; ++k)
+        if (b + k < n) {
+            const int i = b + k;
+            const uint32_t c = cnt[i], npc = ((uint32_t)hc[i] + c) / kPiece;
+            pc[i] = npc;
+            if (npc) {  // pieces take positions [fl, fl + npc * kPiece): chunk index pos / kCh past ph
+                const uint32_t nnew = ((uint32_t)fl[i] + npc * kPiece - 1) / kCh;
+                if (nnew) np[i] = atomicAdd(&misc[0], nnew);
+            }
+            sum += c | npc << 16;
+        }
+    uint32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wtot[wave] = x;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        uint32_t v = lane < kB / 64 ? wtot[lane] : 0u;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(v, o, 64);
+            if (lane >= o) v += y;
+        }
+        if (lane < kB / 64) wtot[lane] = v;
+    }
+    __syncthreads();
+    uint32_t pre = x - sum + (wave > 0 ? wtot[wave - 1] : 0u);
+    for (int k = 0; k < per; ++k)
+        if (b + k < n) {
+            const int i = b + k;
+            loc[i] = pre & 0xFFFFu;
+            pb[i] = pre >> 16;
+            pre += cnt[i] | pc[i] << 16;
+        }
+    const uint32_t total = wtot[kB / 64 - 1];
+    __syncthreads();
+    return total >> 16;
+}
+
 template <bool UND, bool FULL = false>
 __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
                                                  int64_t m, int64_t lo, int64_t range, int nb, part::BitV a, part::BitV b,
@@ -231,7 +285,7 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
             }
         }
         __syncthreads();
-        (void)part::block_exclusive_scan<kB>(cnt, loc, nb2, wtot);
+        const uint32_t P = scan_runs_pieces(cnt, hc, fl, loc, pc, pb, np, misc, nb2, wtot);
 #pragma unroll
         for (int u = 0; u < IT; ++u) {
             if ((vin >> u) & 1u) stage[loc[ys[u] >> kBits] + rin[u]] = (uint16_t)(ys[u] & 0xFFFFu);
@@ -241,16 +295,6 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
                 if ((vout2 >> u) & 1u) stage[loc[nb + (ys[u] >> kBits)] + rout2[u]] = (uint16_t)(ys[u] & 0xFFFFu);
             }
         }
-        for (int i = threadIdx.x; i < nb2; i += kB) {  // pieces of the held + run sequence; chunks they open
-            const uint32_t npc = ((uint32_t)hc[i] + cnt[i]) / kPiece;
-            pc[i] = npc;
-            if (npc) {  // pieces take positions [fl, fl + npc * kPiece): chunk index pos / kCh past ph
-                const uint32_t nnew = ((uint32_t)fl[i] + npc * kPiece - 1) / kCh;
-                if (nnew) np[i] = atomicAdd(&misc[0], nnew);
-            }
-        }
-        __syncthreads();
-        const uint32_t P = part::block_exclusive_scan<kB>(pc, pb, nb2, wtot);
         for (int i = threadIdx.x; i < nb2; i += kB) {  // piece -> bucket; pc becomes the first held rank
             const uint32_t npc = pc[i];
             for (uint32_t k = 0; k < npc; ++k) owner[pb[i] + k] = (uint16_t)i;
