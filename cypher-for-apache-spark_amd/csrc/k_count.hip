@@ -348,7 +348,8 @@ __global__ void __launch_bounds__(kB) k_rec_part(const int64_t* __restrict__ src
                 }
             }
         }
-        __syncthreads();
+        // (no barrier: the bookkeeping below reads and writes neither `hold` nor `pc`, the held records above
+        // touch nothing else; both only had to follow the piece stores)
         for (int i = threadIdx.x; i < nb2; i += kB) {
             const uint32_t tot = (uint32_t)hc[i] + cnt[i], npc = tot / kPiece;
             if (npc) {
