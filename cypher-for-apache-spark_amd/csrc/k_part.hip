@@ -989,7 +989,7 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const void* __restrict__
                 }
             }
         __syncthreads();
-        const uint32_t total = block_exclusive_scan<kSBlock>(cnt, loc, nb, wtot);
+        const uint32_t total = small_exclusive_scan<kSBlock>(cnt, loc, nb, wtot);
         // Whole output lines: a cell's run is stored up to the last line boundary it reaches, the
         // rest held in LDS; held items go out when their line completes, together with the run
         // items that complete it (so a line is written within one tile, not in pieces by two).

@@ -66,6 +66,30 @@ __device__ uint32_t block_exclusive_scan(const uint32_t* in, uint32_t* out, int 
     return total;
 }
 
+// The same scan for n <= 128 (the partition passes' per-tile histograms at C3: 128 source slices): wave 0
+// alone, two counters per lane, then one barrier -- instead of three; larger n take block_exclusive_scan.
+// `wtot` word 0 carries the total to the block.
+template <int B>
+__device__ uint32_t small_exclusive_scan(const uint32_t* in, uint32_t* out, int n, uint32_t* wtot) {
+    if (n > 128) return block_exclusive_scan<B>(in, out, n, wtot);  // block-uniform
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x, i0 = 2 * lane;
+        const uint32_t a = i0 < n ? in[i0] : 0u, b = i0 + 1 < n ? in[i0 + 1] : 0u;
+        uint32_t x = a + b;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        const uint32_t ex = x - a - b;
+        if (i0 < n) out[i0] = ex;
+        if (i0 + 1 < n) out[i0 + 1] = ex + a;
+        if (lane == 63) wtot[0] = x;
+    }
+    __syncthreads();
+    return wtot[0];
+}
+
 __device__ __forceinline__ int cell_of(const Layout& L, uint32_t s, uint32_t t) {
     return (int)(t >> L.tbits) * L.ns + (int)(s >> L.sbits);
 }
