@@ -24,7 +24,10 @@
  *    Nullability is a byte per row (1 = valid), or absent when a column has no nulls.
  *  - A session is externally synchronised (one caller thread, like a CAPS
  *    driver) and owns one HIP stream on one gfx950 device.  Device work is
- *    stream-ordered; calls that return a size to the host synchronise.
+ *    stream-ordered; calls that return a size to the host synchronise.  Caller
+ *    device buffers (ext words, owned_in, dev_out, ...) are read and written in
+ *    the session stream's order only: the host orders its own writes to them
+ *    before the call (one stream, or an event the session stream waits on).
  */
 #ifndef CAPSMI_H
 #define CAPSMI_H
@@ -362,7 +365,11 @@ capsmi_status capsmi_bitmap_refresh(capsmi_bitmap* b, int32_t unique_rows);
  * the all-gather */
 capsmi_status capsmi_bitmap_assume(capsmi_bitmap* b, int64_t set_bits, int32_t unique_rows);
 /* stream-ordered device copy of words [w_begin, w_end): to_bitmap = 0 copies bitmap -> ext,
- * 1 copies ext -> bitmap (ext: a caller device buffer of w_end - w_begin words) */
+ * 1 copies ext -> bitmap (ext: a caller device buffer of w_end - w_begin words).  Like every call
+ * taking a caller device pointer, the copy is queued on the SESSION's stream: `ext` must already be
+ * written (allocated, zero-filled, ...) in that stream's order -- run the host's own device work on
+ * the same stream (capsmi_session_use_stream) or make the session stream wait on it -- and the host
+ * may read it only after capsmi_session_sync or stream-ordered work behind it */
 capsmi_status capsmi_bitmap_copy_words(capsmi_bitmap* b, int64_t w_begin, int64_t w_end, uint32_t* ext,
                                        int32_t to_bitmap);
 

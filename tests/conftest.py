@@ -30,7 +30,14 @@ def gpu_available() -> bool:
 
 @pytest.fixture(scope="session")
 def session():
+    """One session for the GPU tests, bound to torch's current stream: the tests hand torch buffers
+    (``torch.zeros(...).data_ptr()``) to library calls, and a zero-fill queued on torch's stream is
+    only ordered before the library's copies when both run on one stream (include/capsmi.h, the
+    external-buffer contract).  On the session's own non-blocking stream a late fill could overwrite
+    words the library had already copied (GPUTEST_r05: test_bitmap_scan_of_exact_node_table)."""
+    import torch
     from capsmi import Session
     s = Session(0)
+    s.set_stream(torch.cuda.current_stream().cuda_stream)
     yield s
     s.close()
