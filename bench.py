@@ -75,14 +75,13 @@ MODE_QUERY = {
 C3_WORKLOAD = "C3: MATCH (a:Person)-[:FRIEND_OF]->(b:Person)-[:FRIEND_OF]->(c:Person) RETURN count(DISTINCT c)"
 KERNELS = ("part_scatter1", "part_scatter2_hop1", "part_scatter2", "hop1", "hop2", "mid_combine", "bitmap_add",
            "bitmap_range",
-           "count_part", "count_part_in", "count_in", "count_part_out", "count_out", "degrees", "und_count_part",
+           "count_part", "count_in", "count_out", "degrees", "und_count_part",
            "und_count", "und_distinct", "und_hop1", "und_hop2")
 # timer name -> kernel name as rocprofv3 reports it (hop1 and hop2 are two instances of k_hop_2d)
 KERNEL_SYMBOL = {"part_scatter1": "k_scatter_l", "part_scatter2_hop1": "k_scatter_s2", "part_scatter2": "k_scatter_s2",
                  "hop1": "k_hop_2d", "hop2": "k_hop_2d", "mid_combine": "k_mid_combine", "bitmap_add": "k_bitmap_add",
                  "bitmap_range": "k_bits_range",
-                 "count_part": "k_rec_part", "count_part_in": "k_scatter_c", "count_part_out": "k_scatter_c",
-                 "count_in": "k_rec_walk",
+                 "count_part": "k_rec_part", "count_in": "k_rec_walk",
                  "count_out": "k_rec_walk", "degrees": "k_degrees", "und_count_part": "k_rec_part",
                  "und_count": "k_und_deg", "und_distinct": "k_und_hop1+k_und_hop2", "und_hop1": "k_und_2d",
                  "und_hop2": "k_und_2d"}
@@ -182,9 +181,9 @@ def init_dist(dist, local):
 
 
 # the C4 walk kernels: over the direction-split lists (the library's default whenever the targets are coded,
-# i.e. <= 2^24 ids -- C4's config), or the combined lists (CAPSMI_TRI_SPLIT=0 / the flat walk, A/B runs)
+# i.e. <= 2^24 ids -- C4's config), or the combined lists (config CAPSMI_TRI_SPLIT=0)
 TRI_SYMBOL = ("k_tri_big_items+k_tri_small" if os.environ.get("CAPSMI_TRI_SPLIT") == "0"
-              or os.environ.get("CAPSMI_TRI_WALK") == "flat" else "k_tri_items_sp+k_tri_small_sp")
+              else "k_tri_items_sp+k_tri_small_sp")
 
 
 def pmc_traffic(kernel, workload):
@@ -464,17 +463,10 @@ def main():
         return int(t.column(outs[0][2]).values[0])
 
     def run_count(atomic=False):  # count(*) of the same match through the route
-        prev = os.environ.get("CAPSMI_COUNT")  # a caller's A/B choice (scripts/ab.sh) stays in force
-        if atomic:
-            os.environ["CAPSMI_COUNT"] = "atomic"
-        try:
+        # (the session's configuration: a caller's CAPSMI_COUNT in the environment stays in force otherwise)
+        with sess.configured(**({"CAPSMI_COUNT": "atomic"} if atomic else {})):
             t, outs = Planner(sg_cold).run(C3_COUNT_QUERY)
             return int(t.column(outs[0][2]).values[0])
-        finally:
-            if prev is None:
-                os.environ.pop("CAPSMI_COUNT", None)
-            else:
-                os.environ["CAPSMI_COUNT"] = prev
 
     def run_und(q):  # the undirected queries through the route (fused_undirected)
         t, outs = Planner(sg_cold).run(q)
@@ -618,7 +610,6 @@ def main():
                "count_part": m_local * 20,  # read 2 x int64, write two 2-byte records
                "und_count_part": m_local * 24,  # read 2 x int64, write up to four 2-byte records
                "und_distinct": m_local * 32 + n * 4,  # two streams of 2 x int64; the per-id state word
-               "count_part_in": m_local * 24, "count_part_out": m_local * 24,  # pair partition (CAPSMI_COUNT=pairs)
                "degrees": m_local * 16 + n * 8}                  # read int64 pairs, inA + outC
         alg.update(kbytes)
         timed = {k: (c, ms) for k, (c, ms) in kt.items() if c > 0}

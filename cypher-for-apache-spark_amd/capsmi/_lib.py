@@ -104,6 +104,8 @@ _SIGS = {
     "capsmi_session_set_stream": (c_int32, [P, c_void_p]),
     "capsmi_session_use_stream": (c_int32, [P, c_void_p]),
     "capsmi_session_sync": (c_int32, [P]),
+    "capsmi_session_set_config": (c_int32, [P, c_char_p, c_char_p]),
+    "capsmi_config_check": (c_int32, [c_char_p, c_char_p]),
     "capsmi_session_set_profiling": (c_int32, [P, c_int32]),
     "capsmi_session_kernel_time": (c_int32, [P, c_char_p, POINTER(c_int64), POINTER(ctypes.c_double)]),
     "capsmi_session_kernel_bytes": (c_int32, [P, c_char_p, POINTER(ctypes.c_double)]),

@@ -10,6 +10,7 @@ Every operator executes in libcapsmi.so (HIP, gfx950); Python only marshals hand
 from __future__ import annotations
 
 import bisect
+import contextlib
 import ctypes
 import threading
 from dataclasses import dataclass
@@ -143,6 +144,24 @@ class Session:
 
     def sync(self) -> None:
         _lib.call("capsmi_session_sync", self._h)
+
+    def set_config(self, name: str, value: Optional[str]) -> None:
+        """One CAPSMI_* knob for this session (include/capsmi.h capsmi_session_set_config); the environment is
+        read only when the session is created.  None = back to the environment's value or the default."""
+        _lib.call("capsmi_session_set_config", self._h, name.encode(),
+                  None if value is None else str(value).encode())
+
+    @contextlib.contextmanager
+    def configured(self, **knobs):
+        """``with session.configured(CAPSMI_COUNT="atomic"): ...`` -- the knobs for the block, then back to the
+        environment's values (or the defaults)."""
+        for k, v in knobs.items():
+            self.set_config(k, v)
+        try:
+            yield self
+        finally:
+            for k in knobs:
+                self.set_config(k, None)
 
     def close(self) -> None:
         if self._h:

@@ -312,13 +312,7 @@ bool types_joinable(int a, int b) {
 // -- one global hash table, for builds whose table stays cache-resident; "radix" -- both sides
 // radix-partitioned to LDS tables, for larger builds.  CAPSMI_JOIN=direct|hash|radix forces one for
 // A/B runs (direct still falls back when the keys are not eligible).
-enum JoinStrategy { JS_AUTO, JS_DIRECT, JS_HASH, JS_RADIX };
-JoinStrategy forced_join_strategy() {
-    const char* e = getenv("CAPSMI_JOIN");
-    if (!e) return JS_AUTO;
-    const std::string v(e);
-    return v == "direct" ? JS_DIRECT : v == "hash" ? JS_HASH : v == "radix" ? JS_RADIX : JS_AUTO;
-}
+enum JoinStrategy { JS_AUTO, JS_DIRECT, JS_HASH, JS_RADIX };  // Config::join
 // from 2^22 build rows (a global table of ~128 MB, half the MALL) the radix join measured faster:
 // 3.4 vs 3.9 ms at 2^22, 14.3 vs 16.2 at 2^24, 62.6 vs 70.1 at 2^26 (scripts/join_bench.py)
 constexpr int64_t kRadixBuildRows = int64_t(1) << 22;
@@ -368,7 +362,7 @@ capsmi_table* join_impl(capsmi_table* l, capsmi_table* r, int jt, const std::vec
         }
         const bool outer = jt != CAPSMI_JOIN_INNER;
         Buf pi, bi, matched;
-        const JoinStrategy js = forced_join_strategy();
+        const JoinStrategy js = (JoinStrategy)s->cfg.join;
         bool done = false;
         if (jt != CAPSMI_JOIN_FULL_OUTER && (js == JS_AUTO || js == JS_DIRECT) && bk.n == 1 &&
             B->cols[(build_left ? lk : rk)[0]].type == CAPSMI_I64 && Pr->cols[(build_left ? rk : lk)[0]].type == CAPSMI_I64)
@@ -463,6 +457,114 @@ void check_bitmap(const capsmi_bitmap* b, const char* what) {
 }  // namespace
 
 // =============================== C ABI ========================================================
+namespace capsmi {
+namespace {
+bool parse_int(const char* v, int64_t lo, int64_t hi, int64_t& out) {
+    if (!v || !*v) return false;
+    char* end = nullptr;
+    const long long x = strtoll(v, &end, 10);
+    if (*end != '\0' || x < lo || x > hi) return false;
+    out = x;
+    return true;
+}
+bool parse_choice(const char* v, std::initializer_list<const char*> names, int& out) {
+    int k = 0;
+    for (const char* n : names) {
+        if (v && std::string(v) == n) {
+            out = k;
+            return true;
+        }
+        ++k;
+    }
+    return false;
+}
+// one knob from `v` (never NULL here); false = unknown name or bad value (c unchanged)
+bool apply(Config& c, const std::string& name, const char* v) {
+    int64_t x = 0;
+    int k = 0;
+    if (name == "CAPSMI_JOIN") {
+        if (!parse_choice(v, {"auto", "direct", "hash", "radix"}, k)) return false;
+        c.join = k;
+    } else if (name == "CAPSMI_COUNT") {
+        if (!parse_choice(v, {"rec", "atomic"}, k)) return false;
+        c.count_atomic = k == 1;
+    } else if (name == "CAPSMI_REC_FULL") {
+        if (!parse_int(v, 0, 1, x)) return false;
+        c.rec_full = x != 0;
+    } else if (name == "CAPSMI_GROUPED") {
+        if (!parse_choice(v, {"sets", "keys"}, k)) return false;
+        c.grouped_keys = k == 1;
+    } else if (name == "CAPSMI_PAIRS") {
+        if (!parse_choice(v, {"auto", "packed", "uint2"}, k)) return false;
+        c.pairs = k;
+    } else if (name == "CAPSMI_TRI_BUILD") {
+        if (!parse_choice(v, {"direct", "sorted"}, k)) return false;
+        c.tri_sorted_build = k == 1;
+    } else if (name == "CAPSMI_TRI_DEG_SAMPLE") {
+        if (!parse_int(v, 0, 1 << 20, x)) return false;
+        c.tri_deg_sample = (int)x;
+    } else if (name == "CAPSMI_TRI_SPLIT") {
+        if (!parse_int(v, 0, 1, x)) return false;
+        c.tri_split = x != 0;
+    } else if (name == "CAPSMI_TRI_VMODE_T") {
+        if (!parse_int(v, 0, 1 << 30, x)) return false;
+        c.tri_vmode_t = (int)x;
+    } else if (name == "CAPSMI_UND") {
+        if (!parse_choice(v, {"part", "stream"}, k)) return false;
+        c.und_stream = k == 1;
+    } else if (name == "CAPSMI_VL_BITS") {
+        if (!parse_int(v, 2, 64, x)) return false;
+        c.vl_bits = (int)x;
+    } else if (name == "CAPSMI_VL_SUBLOG") {
+        if (!parse_int(v, -1, 5, x)) return false;
+        c.vl_sublog = (int)x;
+    } else if (name == "CAPSMI_VL_F2") {
+        if (!parse_int(v, 0, 1, x)) return false;
+        c.vl_f2 = x != 0;
+    } else if (name == "CAPSMI_COLL_CHUNK") {
+        if (!parse_int(v, 1, int64_t(1) << 40, x)) return false;
+        c.coll_chunk = x;
+    } else if (name == "CAPSMI_INGEST_THREADS") {
+        if (!parse_int(v, 0, 1024, x)) return false;
+        c.ingest_threads = (int)x;
+    } else {
+        return false;
+    }
+    return true;
+}
+// every knob with its default's text (Config's initialisers)
+const std::pair<const char*, const char*> kKnobs[] = {
+    {"CAPSMI_JOIN", "auto"},         {"CAPSMI_COUNT", "rec"},        {"CAPSMI_REC_FULL", "1"},
+    {"CAPSMI_GROUPED", "sets"},      {"CAPSMI_PAIRS", "auto"},       {"CAPSMI_TRI_BUILD", "direct"},
+    {"CAPSMI_TRI_DEG_SAMPLE", "0"},  {"CAPSMI_TRI_SPLIT", "1"},      {"CAPSMI_TRI_VMODE_T", "256"},
+    {"CAPSMI_UND", "part"},          {"CAPSMI_VL_BITS", "8"},        {"CAPSMI_VL_SUBLOG", "-1"},
+    {"CAPSMI_VL_F2", "0"},           {"CAPSMI_COLL_CHUNK", "67108864"}, {"CAPSMI_INGEST_THREADS", "0"}};
+}  // namespace
+
+Config config_from_env() {
+    Config c;
+    for (const auto& k : kKnobs)
+        if (const char* e = getenv(k.first))
+            if (!apply(c, k.first, e)) fprintf(stderr, "capsmi: ignoring %s=%s (not a valid value)\n", k.first, e);
+    return c;
+}
+
+bool config_set(Config& c, const char* name, const char* value) {
+    if (!name) return false;
+    const std::string n(name);
+    if (value) return apply(c, n, value);
+    for (const auto& k : kKnobs)  // back to the environment's value, or the default
+        if (n == k.first) {
+            const char* e = getenv(k.first);
+            Config t = c;
+            if (!(e && apply(t, n, e))) apply(t, n, k.second);
+            c = t;
+            return true;
+        }
+    return false;
+}
+}  // namespace capsmi
+
 extern "C" {
 
 size_t capsmi_last_error(char* buf, size_t n) {
@@ -485,6 +587,7 @@ capsmi_status capsmi_session_create(int32_t device, capsmi_session** out) {
     HIP_CHECK(hipSetDevice(device));
     auto* s = new capsmi_session();
     s->device = device;
+    s->cfg = capsmi::config_from_env();  // the knobs, once
     HIP_CHECK(hipStreamCreateWithFlags(&s->own_stream, hipStreamNonBlocking));
     s->stream = s->own_stream;
     alloc_ctx_open(s);
@@ -605,6 +708,24 @@ capsmi_status capsmi_session_kernel_time(capsmi_session* s, const char* name, in
     if (launches) *launches = it == s->totals.end() ? 0 : it->second.first;
     if (total_ms) *total_ms = it == s->totals.end() ? 0.0 : it->second.second;
     if (it != s->totals.end()) s->totals.erase(it);
+    API_END
+}
+
+capsmi_status capsmi_session_set_config(capsmi_session* s, const char* name, const char* value) {
+    API_BEGIN
+    need(s, "session");
+    REQUIRE(capsmi::config_set(s->cfg, name, value), CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            std::string("unknown configuration knob or value: ") + (name ? name : "(null)") + " = " +
+                (value ? value : "(default)"));
+    API_END
+}
+
+capsmi_status capsmi_config_check(const char* name, const char* value) {
+    API_BEGIN
+    capsmi::Config c;
+    REQUIRE(capsmi::config_set(c, name, value), CAPSMI_ERR_ILLEGAL_ARGUMENT,
+            std::string("unknown configuration knob or value: ") + (name ? name : "(null)") + " = " +
+                (value ? value : "(default)"));
     API_END
 }
 
@@ -2063,8 +2184,8 @@ capsmi_status capsmi_two_hop_count(capsmi_session* s, int32_t nrels, capsmi_tabl
     use_device(s);
     const int64_t n = b_ok->hi - b_ok->lo;
     const bool same_domain = a_ok->lo == b_ok->lo && a_ok->hi == b_ok->hi && c_ok->lo == b_ok->lo && c_ok->hi == b_ok->hi;
-    const char* mode = getenv("CAPSMI_COUNT");  // "atomic": the per-relationship atomic form (A/B runs)
-    if (same_domain && n > 0 && n <= (int64_t(1) << 26) && !(mode && std::string(mode) == "atomic")) {
+    // (config CAPSMI_COUNT=atomic forces the per-relationship atomic form below, the one above 2^26 ids)
+    if (same_domain && n > 0 && n <= (int64_t(1) << 26) && !s->cfg.count_atomic) {
         std::vector<const int64_t*> srcs, dsts;
         std::vector<int64_t> ms;
         for (int i = 0; i < nrels; ++i) {
@@ -2074,9 +2195,7 @@ capsmi_status capsmi_two_hop_count(capsmi_session* s, int32_t nrels, capsmi_tabl
             dsts.push_back(rel_col(rels[i], dst_col).d());
             ms.push_back(rels[i]->nrows);
         }
-        *out_rows = mode && std::string(mode) == "pairs"  // the 8-byte pair partition (A/B)
-                        ? two_hop_count_part(s, srcs.data(), dsts.data(), ms.data(), nrels, a_ok, b_ok, c_ok)
-                        : two_hop_count_rec(s, srcs.data(), dsts.data(), ms.data(), nrels, a_ok, b_ok, c_ok);
+        *out_rows = two_hop_count_rec(s, srcs.data(), dsts.data(), ms.data(), nrels, a_ok, b_ok, c_ok);
         return CAPSMI_OK;
     }
     Buf inA = dev_alloc(sizeof(uint32_t) * (n > 0 ? n : 1), s);

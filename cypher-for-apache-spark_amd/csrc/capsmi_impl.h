@@ -124,7 +124,43 @@ struct Shard {
 
 }  // namespace capsmi
 
+namespace capsmi {
+// Session configuration: every CAPSMI_* knob of the library, read from the environment
+// ONCE, when the session is created (capsmi_session_create), and changed afterwards only through
+// capsmi_session_set_config -- no call site reads the environment.  The defaults are the measured
+// choices; the non-defaults force the fallback forms (used above a size limit or when a layout does not
+// fit) at sizes where tests can check them against the oracle.  Process-wide, outside this struct:
+// CAPSMI_CACHE_BYTES (the block cache shared by all sessions, read at the first allocation) and
+// CAPSMI_POOL_KEEP_BYTES (the device pool's release threshold, set at each session create).
+struct Config {
+    int join = 0;                 // CAPSMI_JOIN = auto | direct | hash | radix (0..3): force a join strategy
+    bool count_atomic = false;    // CAPSMI_COUNT = atomic: 2-hop count(*) by per-relationship atomic degrees
+                                  //   (the form above 2^26 ids) instead of the record partition
+    bool rec_full = true;         // CAPSMI_REC_FULL = 0: the undirected record partition's general form also
+                                  //   for full node filters
+    bool grouped_keys = false;    // CAPSMI_GROUPED = keys: grouped count(DISTINCT c) by the per-binding key sort
+    int pairs = 0;                // CAPSMI_PAIRS = packed | uint2 (1 | 2): force the cached layout's pair form
+    bool tri_sorted_build = false;  // CAPSMI_TRI_BUILD = sorted: the sort-oriented trigraph build (above 2^24 ids)
+    int tri_deg_sample = 0;       // CAPSMI_TRI_DEG_SAMPLE: 1 in k relationships for the degree order (0: auto)
+    bool tri_split = true;        // CAPSMI_TRI_SPLIT = 0: the combined (not direction-split) triangle walks
+    int tri_vmode_t = 256;        // CAPSMI_TRI_VMODE_T: od(v) threshold of the v-mode walks (0: all u-mode)
+    bool und_stream = false;      // CAPSMI_UND = stream: undirected count(DISTINCT) by the streaming form
+                                  //   (the form above 2^26 ids) instead of the cell layout
+    int vl_bits = 8;              // CAPSMI_VL_BITS: bits per pair of the var-length reverse-pair filter
+    int vl_sublog = -1;           // CAPSMI_VL_SUBLOG: filter regions per slice, log2 (-1: auto)
+    bool vl_f2 = false;           // CAPSMI_VL_F2 = 1: the second-level filter in the T walk (the sharded form's)
+    int64_t coll_chunk = int64_t(1) << 26;  // CAPSMI_COLL_CHUNK: elements per host collective call
+    int ingest_threads = 0;       // CAPSMI_INGEST_THREADS (0: OMP_NUM_THREADS, else up to 16 hardware threads)
+};
+// the environment's values over the defaults
+Config config_from_env();
+// one knob by its environment name; value NULL = back to the environment's value (or the default).
+// Returns false for an unknown name or an unparsable value.
+bool config_set(Config& c, const char* name, const char* value);
+}  // namespace capsmi
+
 struct capsmi_session {
+    capsmi::Config cfg;  // read once at create (capsmi::Config)
     std::shared_ptr<capsmi::AllocCtx> alloc;  // block cache of this session (api.hip)
     struct Param {
         int32_t type = 0;
@@ -314,7 +350,7 @@ std::shared_ptr<ListStore> concat_lists(capsmi_session* s, const ListStore& a, c
 void collective(capsmi_session* s, int op, const void* send, void* recv, int64_t count, int dtype);
 // calls of the host collective move at most coll_chunk() elements (CAPSMI_COLL_CHUNK); collective() and
 // collective_a2av() split larger ones
-int64_t coll_chunk();
+int64_t coll_chunk(const capsmi_session* s);
 // ALL_TO_ALL_V with host count lists (world entries each); max_pair: the largest entry of the whole count
 // matrix (equal on every rank), which fixes the number of rounds
 void collective_a2av(capsmi_session* s, const void* send, const int64_t* send_counts, void* recv,
@@ -323,8 +359,10 @@ int64_t matrix_max(const std::vector<int64_t>& m);
 // hash Exchange of u64 words to rank dest[i] (low byte; 0xFF: not sent); dest / words are reordered
 // scratch; returns the received words (rank-major), *nrecv of them; synchronises
 Buf exchange_words(capsmi_session* s, uint64_t* dest, uint64_t* words, int64_t n, int64_t* nrecv);
-// every rank's words concatenated in rank order; synchronises
-Buf gather_words(capsmi_session* s, const uint64_t* words, int64_t n, int64_t* ntotal);
+// every rank's words concatenated in rank order; synchronises.  budget_bytes > 0: when the gathered words
+// (padded staging + result) would exceed the smallest rank's budget, every rank returns an empty Buf with
+// *ntotal = -1, together, right after the all-gather of the (count, budget) pairs
+Buf gather_words(capsmi_session* s, const uint64_t* words, int64_t n, int64_t* ntotal, int64_t budget_bytes = 0);
 // the generic operators' row exchanges over partitioned tables (k_dist.hip): rows to rank dest[r]; rows
 // hash-partitioned by key columns; this rank's slice of a replicated table; every rank's rows
 capsmi_table* exchange_rows(capsmi_session* s, const capsmi_table* t, uint64_t* dest);
@@ -358,10 +396,6 @@ int64_t radix_join(capsmi_session* s, const KeyCols& bk, int64_t nb, const KeyCo
 // not eligible (then nothing was produced)
 bool direct_join(capsmi_session* s, const KeyCols& bk, int64_t nb, const KeyCols& pk, int64_t np, bool outer,
                  Buf& out_p, Buf& out_b, int64_t* total);
-// 2-hop count(*) from two chunked partitions with LDS counts (k_count.hip); bitmaps over one domain of
-// at most 2^26 ids
-int64_t two_hop_count_part(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
-                           int nt, const capsmi_bitmap* a_ok, const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok);
 // the same from two partitions of 2-byte records (k_count.hip rec::), the default
 // undirected: the 2-hop of undirected Expands (both arcs of every relationship, r1 = r2 bindings subtracted)
 int64_t two_hop_count_rec(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,

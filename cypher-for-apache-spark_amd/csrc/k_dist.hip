@@ -181,14 +181,7 @@ __global__ void k_owned_flags(const int64_t* __restrict__ in, int64_t n, int64_t
 // JVM CollectiveFn) ever receives a larger one.  Round 4's C4 route at world size 1 faulted
 // (hipErrorIllegalAddress) in the first run that handed RCCL 2^28-word (2^31-byte) calls; the same build
 // equals its fixture with every call below 2^31 bytes.
-int64_t coll_chunk() {
-    static const int64_t c = [] {
-        const char* e = getenv("CAPSMI_COLL_CHUNK");
-        const long long v = e ? atoll(e) : 0;
-        return v > 0 ? (int64_t)v : (int64_t(1) << 26);
-    }();
-    return c;
-}
+int64_t coll_chunk(const capsmi_session* s) { return s->cfg.coll_chunk > 0 ? s->cfg.coll_chunk : (int64_t(1) << 26); }
 
 namespace {
 size_t coll_elem_bytes(int dtype) { return dtype == CAPSMI_COLL_U32 ? 4 : 8; }
@@ -204,7 +197,7 @@ void coll_call(capsmi_session* s, int op, const void* send, void* recv, int64_t 
 void collective(capsmi_session* s, int op, const void* send, void* recv, int64_t count, int dtype) {
     REQUIRE(op != CAPSMI_COLL_ALL_TO_ALL_V, CAPSMI_ERR_INTERNAL, "ALL_TO_ALL_V goes through collective_a2av");
     const int W = s->world > 0 ? s->world : 1;
-    const int64_t chunk = coll_chunk();
+    const int64_t chunk = coll_chunk(s);
     const size_t es = coll_elem_bytes(dtype);
     if (op == CAPSMI_COLL_ALL_GATHER) {
         const int64_t per = std::max<int64_t>(1, chunk / W);  // words per rank in one call
@@ -237,7 +230,7 @@ void collective(capsmi_session* s, int op, const void* send, void* recv, int64_t
 void collective_a2av(capsmi_session* s, const void* send, const int64_t* send_counts, void* recv,
                      const int64_t* recv_counts, int dtype, int64_t max_pair) {
     const int W = s->world;
-    const int64_t per = std::max<int64_t>(1, coll_chunk() / std::max(W, 1));  // words per (source, destination)
+    const int64_t per = std::max<int64_t>(1, coll_chunk(s) / std::max(W, 1));  // words per (source, destination)
     const int64_t rounds = std::max<int64_t>(1, (max_pair + per - 1) / per);
     if (rounds == 1) {
         capsmi_coll_vec sv{const_cast<void*>(send), send_counts}, rv{recv, recv_counts};
@@ -321,17 +314,29 @@ Buf exchange_words(capsmi_session* s, uint64_t* dest, uint64_t* words, int64_t n
 
 // every rank's n words, concatenated in rank order (counts first, then one ALL_GATHER padded to the
 // largest share, compacted on the device); synchronises
-Buf gather_words(capsmi_session* s, const uint64_t* words, int64_t n, int64_t* ntotal) {
+Buf gather_words(capsmi_session* s, const uint64_t* words, int64_t n, int64_t* ntotal, int64_t budget_bytes) {
     const int W = s->world;
     hipStream_t st = s->stream;
-    Buf cnt = dev_alloc(sizeof(int64_t) * (1 + W), s);
-    fill_i64(P<int64_t>(cnt), n, 1, st);
-    collective(s, CAPSMI_COLL_ALL_GATHER, P<int64_t>(cnt), P<int64_t>(cnt) + 1, 1, CAPSMI_I64);
-    std::vector<int64_t> c(W);
-    HIP_CHECK(hipMemcpyAsync(c.data(), P<int64_t>(cnt) + 1, sizeof(int64_t) * W, hipMemcpyDeviceToHost, st));
+    // (count, budget) of every rank: the ranks' budgets may differ (free device memory), so each decides on
+    // the smallest -- the same decision everywhere, no rank left waiting inside a collective
+    Buf cnt = dev_alloc(sizeof(int64_t) * 2 * (1 + W), s);
+    const int64_t mine[2] = {n, budget_bytes > 0 ? budget_bytes : INT64_MAX};
+    HIP_CHECK(hipMemcpyAsync(P<int64_t>(cnt), mine, sizeof(mine), hipMemcpyHostToDevice, st));
+    collective(s, CAPSMI_COLL_ALL_GATHER, P<int64_t>(cnt), P<int64_t>(cnt) + 2, 2, CAPSMI_I64);
+    std::vector<int64_t> cb(2 * W), c(W);
+    HIP_CHECK(hipMemcpyAsync(cb.data(), P<int64_t>(cnt) + 2, sizeof(int64_t) * 2 * W, hipMemcpyDeviceToHost, st));
     HIP_CHECK(hipStreamSynchronize(st));
-    int64_t mx = 0, tot = 0;
-    for (int64_t x : c) { mx = std::max(mx, x); tot += x; }
+    int64_t mx = 0, tot = 0, budget = INT64_MAX;
+    for (int q = 0; q < W; ++q) {
+        c[q] = cb[2 * q];
+        mx = std::max(mx, c[q]);
+        tot += c[q];
+        budget = std::min(budget, cb[2 * q + 1]);
+    }
+    if ((double)sizeof(uint64_t) * ((double)mx * W + (double)mx + (double)tot) > (double)budget) {
+        *ntotal = -1;
+        return Buf();
+    }
     Buf pad = dev_alloc(sizeof(uint64_t) * (mx > 0 ? mx : 1), s);
     if (n > 0) HIP_CHECK(hipMemcpyAsync(P<void>(pad), words, sizeof(uint64_t) * n, hipMemcpyDeviceToDevice, st));
     Buf all = dev_alloc(sizeof(uint64_t) * (size_t)(mx > 0 ? mx : 1) * W, s);

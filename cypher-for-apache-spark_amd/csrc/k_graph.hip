@@ -810,10 +810,9 @@ void expand_filter(capsmi_session* s, const int64_t* src, const int64_t* dst, in
     if (pairs) {
         auto k = nout == 1 ? k_expand_pairs<1> : nout == 2 ? k_expand_pairs<2> : nout == 3 ? k_expand_pairs<3>
                                                                                      : k_expand_pairs<4>;
-        // workgroups per CU (CAPSMI_EP_GRID, A/B): C2 s = 24 expand 2.27 / 2.25 / 2.23 ms at 4 / 8 / 16 -- more
-        // workgroups than resident ones balance the tail of the tile loop
-        const char* ge = getenv("CAPSMI_EP_GRID");
-        const int64_t gp = std::min<int64_t>((m + kEpTile - 1) / kEpTile, (int64_t)s->num_cus * (ge ? atoi(ge) : 16));
+        // 16 workgroups per CU: C2 s = 24 expand 2.27 / 2.25 / 2.23 ms at 4 / 8 / 16 -- more workgroups than
+        // resident ones balance the tail of the tile loop
+        const int64_t gp = std::min<int64_t>((m + kEpTile - 1) / kEpTile, (int64_t)s->num_cus * 16);
         hipLaunchKernelGGL(k, dim3((unsigned)gp), dim3(kEpBlock), 0, s->stream, src, dst, m, al, view(a), view(b),
                            from_dst, out_d[0], nout > 1 ? out_d[1] : nullptr, nout > 2 ? out_d[2] : nullptr,
                            nout > 3 ? out_d[3] : nullptr, (unsigned long long*)dev_count);

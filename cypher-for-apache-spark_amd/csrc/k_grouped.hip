@@ -345,9 +345,11 @@ static int64_t gd_pairs(capsmi_session* s, const int64_t* S, const int64_t* T, i
 }
 
 // count(DISTINCT c) per a by LDS sets over the deduplicated lists (above)
-static void grouped_distinct_sets(capsmi_session* s, const int64_t* S, const int64_t* T, int64_t m, int64_t lo,
+// Returns false (nothing produced, on every rank alike) when a distributed run's gathered hop-2 keys would
+// not fit `key_budget` bytes.
+static bool grouped_distinct_sets(capsmi_session* s, const int64_t* S, const int64_t* T, int64_t m, int64_t lo,
                                   int64_t n, const capsmi_bitmap* a, const capsmi_bitmap* b, const capsmi_bitmap* c,
-                                  bool dist, Buf& out_ids, Buf& out_vals, int64_t* rows) {
+                                  bool dist, int64_t key_budget, Buf& out_ids, Buf& out_vals, int64_t* rows) {
     hipStream_t st = s->stream;
     KernelTimer kt(s, "grouped_distinct");
     Buf loops = dev_alloc(sizeof(unsigned int) * n, s);
@@ -359,8 +361,10 @@ static void grouped_distinct_sets(capsmi_session* s, const int64_t* S, const int
         // BY_SOURCE shards: this rank's deduplicated (b, y) keys are those of its owned b's, an id range that
         // grows with the rank, so every rank's keys concatenated in rank order are the whole sorted key set:
         // one all-gather, then the offsets over it (each rank walks the out2(b) of any b its a's reach)
+        // (the whole key set on every rank: refused together above the key budget)
         int64_t tot = 0;
-        k2 = gather_words(s, P<uint64_t>(k2), ne2, &tot);
+        k2 = gather_words(s, P<uint64_t>(k2), ne2, &tot, key_budget > 0 ? key_budget : 0);
+        if (tot < 0) return false;
         hipLaunchKernelGGL(k_gd_off, dim3(grid_for(n + 1)), dim3(256), 0, st, P<uint64_t>(k2), tot, n, P<int64_t>(off2));
         HIP_CHECK(hipGetLastError());
     }
@@ -395,6 +399,7 @@ static void grouped_distinct_sets(capsmi_session* s, const int64_t* S, const int
     out_vals = dev_alloc(sizeof(int64_t) * (g > 0 ? g : 1), s);
     gather_col(P<int64_t>(cnt), nullptr, P<int64_t>(idx), g, P<int64_t>(out_vals), nullptr, st);
     *rows = g;
+    return true;
 }
 
 // rows (relative id of a, value) of the grouped 2-hop; distinct = count(DISTINCT c), else count(*).
@@ -453,11 +458,10 @@ bool grouped_two_hop(capsmi_session* s, const int64_t* const* srcs, const int64_
         *rows = g;
         return true;
     }
-    const char* ge = getenv("CAPSMI_GROUPED");  // "keys": the per-binding key sort below (A/B; bounded by memory)
-    if (dd || !(ge && std::string(ge) == "keys")) {
-        grouped_distinct_sets(s, P<int64_t>(S), P<int64_t>(T), m, lo, n, a, b, c, dd != nullptr, out_ids, out_vals, rows);
-        return true;
-    }
+    // (config CAPSMI_GROUPED=keys: the per-binding key sort below, bounded by memory)
+    if (dd || !s->cfg.grouped_keys)
+        return grouped_distinct_sets(s, P<int64_t>(S), P<int64_t>(T), m, lo, n, a, b, c, dd != nullptr, key_budget,
+                                     out_ids, out_vals, rows);
     // bindings per r1 and their key offsets
     Buf per_r1 = dev_alloc(sizeof(int64_t) * (m > 0 ? m : 1), s), start = dev_alloc(sizeof(int64_t) * (m + 1), s);
     if (m) hipLaunchKernelGGL(k_g_count, dim3(grid_for(m)), dim3(256), 0, st, P<int64_t>(S), P<int64_t>(T), m, lo, n,

@@ -414,234 +414,11 @@ __global__ void __launch_bounds__(B, MINW) k_scatter_l(const int64_t* __restrict
     }
 }
 
-// ---- pass 1, 6-byte items (the C3 2-hop layout; domains of at most 2^29 ids) ---------------------------
-// The chunk's slice j gives a target's high bits, so an item is key = source << tbits | (target mod 2^tbits),
-// at most 48 bits: a u32 array of the low words and a u16 array of the high halves per chunk, 6 bytes per
-// relationship instead of 8 (pass 1 writes and pass 2 reads 2 bytes less per relationship).  Whole lines
-// as in k_scatter_l, now of the u16 array: 64 items (two lines of the u32 array).  A slice's tail of fewer
-// than 64 items is held in LDS; when a tile completes its line, the held items go out from the hold and
-// the run's items behind them from the stage (no re-staging: the stage holds this tile's runs only).
-constexpr int kLine6 = 64;
-
 // this lane's item u of a 4-items-per-load walk starting at the 4-aligned index b: item u is
 // b + 4 * ((u >> 2) * B + lane) + (u & 3)
 template <int B>
 __device__ __forceinline__ int item_off4(int u) {
     return 4 * ((u >> 2) * B + (int)threadIdx.x) + (u & 3);
-}
-
-__device__ __forceinline__ uint32_t held6(uint32_t o, uint32_t f) { return o == kNone ? 0u : (f & (kLine6 - 1)); }
-
-__device__ __forceinline__ uint64_t key6(uint2 p, int tbits) {
-    return (uint64_t)p.x << tbits | (p.y & ((1u << tbits) - 1u));
-}
-
-struct Pool6 {
-    uint8_t* base;
-    __device__ __forceinline__ uint32_t* w(uint32_t c) const {
-        return reinterpret_cast<uint32_t*>(base + (size_t)c * kCh * 6);
-    }
-    __device__ __forceinline__ uint16_t* h(uint32_t c) const {
-        return reinterpret_cast<uint16_t*>(base + (size_t)c * kCh * 6 + (size_t)kCh * 4);
-    }
-    __device__ __forceinline__ void put(uint32_t c, uint32_t pos, uint32_t lw, uint16_t hw) const {
-        w(c)[pos] = lw;
-        h(c)[pos] = hw;
-    }
-};
-
-__host__ __device__ constexpr size_t scatter1l6_lds(int nb, int ns, int block, int tile) {
-    return sizeof(uint2) * (size_t)tile + 6 * (size_t)nb * kLine6 +
-           sizeof(uint32_t) * ((size_t)nb * hist_words(ns) + 7 * (size_t)nb + block / 64 + 4);
-}
-
-// wave 0: as p1l_settle, for a stage that holds the runs alone
-__device__ __forceinline__ void p6_settle(const Layout& L, int hw, const uint2* stage, uint32_t* H, uint32_t* cp,
-                                          const uint32_t* loc, uint32_t* ph, uint32_t* fl, const uint32_t* p1,
-                                          const uint32_t* opened, uint32_t* misc, unsigned long long* cmeta,
-                                          uint32_t* chist) {
-    const int nb = L.nt, lane = threadIdx.x & 63;
-    const uint32_t nop = misc[0];
-    for (uint32_t x = lane; x < nop * (uint32_t)hw; x += 64) {
-        const int b = (int)opened[x / hw], w = (int)(x % hw);
-        if (ph[b] != kNone) {
-            chist[(size_t)ph[b] * hw + w] = H[b * hw + w];
-            H[b * hw + w] = 0;
-        }
-    }
-    wave_lds_order();
-    for (uint32_t k = 0; k < nop; ++k) {  // run items past the old chunk's room belong to the opened one
-        const int b = (int)opened[k];
-        const uint32_t room = ph[b] == kNone ? 0u : (uint32_t)kCh - fl[b];
-        for (uint32_t r = room + lane; r < cp[b]; r += 64) hist_add(H, hw, b, stage[loc[b] + r].x >> L.sbits);
-    }
-    wave_lds_order();
-    for (int i = lane; i < nb; i += 64) {
-        const uint32_t c = cp[i];
-        if (!c) continue;
-        if (p1[i] == kNone) {
-            fl[i] += c;
-        } else {
-            if (ph[i] != kNone) cmeta[ph[i]] = chunk_meta(i, (uint32_t)kCh);
-            fl[i] = ph[i] == kNone ? c : fl[i] + c - (uint32_t)kCh;
-            ph[i] = p1[i];
-        }
-        cp[i] = 0;
-    }
-    if (lane == 0) {
-        misc[1] += nop;
-        misc[0] = 0;
-    }
-    wave_lds_order();
-}
-
-// wave 0: run starts of this tile (the runs alone), the chunks they open, the staged total (misc[2])
-__device__ __forceinline__ void p6_plan(int nb, const uint32_t* cn, uint32_t* loc, const uint32_t* ph,
-                                        const uint32_t* fl, uint32_t* p1, uint32_t* opened, uint32_t* misc) {
-    const int lane = threadIdx.x & 63;
-    const int per = (nb + 63) / 64, b0 = lane * per, b1 = min(b0 + per, nb);
-    uint32_t sum = 0, need = 0;
-    for (int i = b0; i < b1; ++i) {
-        const uint32_t c = cn[i];
-        sum += c;
-        need += (c && (ph[i] == kNone || fl[i] + c > (uint32_t)kCh)) ? 1u : 0u;
-    }
-    const uint32_t is = wave_incl_scan(sum), in = wave_incl_scan(need);
-    uint32_t pre = is - sum, k = in - need;
-    const uint32_t nf = misc[1];
-    for (int i = b0; i < b1; ++i) {
-        const uint32_t c = cn[i];
-        loc[i] = pre;
-        pre += c;
-        uint32_t np = kNone;
-        if (c && (ph[i] == kNone || fl[i] + c > (uint32_t)kCh)) {
-            np = nf + k;
-            opened[k++] = (uint32_t)i;
-        }
-        p1[i] = np;
-    }
-    if (lane == 63) {
-        misc[0] = in;
-        misc[2] = is;
-    }
-    wave_lds_order();
-}
-
-template <int B, int IT, int MINW>
-__global__ void __launch_bounds__(B, MINW) k_scatter_l6(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
-                                                       int64_t m, Layout L, int64_t chunk0, Pool6 pool,
-                                                       unsigned long long* __restrict__ cmeta,
-                                                       uint32_t* __restrict__ chist) {
-    constexpr int T = B * IT;
-    static_assert(T <= kCh && kCh % kLine6 == 0, "a pass-1 run must span at most two chunks");
-    extern __shared__ __attribute__((aligned(16))) unsigned long long smem[];
-    const int nb = L.nt, hw = hist_words(L.ns), tb = L.tbits;
-    uint2* stage = reinterpret_cast<uint2*>(smem);                      // this tile's runs
-    uint32_t* holdw = reinterpret_cast<uint32_t*>(stage + T);           // nb x kLine6 held low words
-    uint16_t* holdh = reinterpret_cast<uint16_t*>(holdw + (size_t)nb * kLine6);  // ... and high halves
-    uint32_t* H = reinterpret_cast<uint32_t*>(holdh + (size_t)nb * kLine6);
-    uint32_t* cnt = H + (size_t)nb * hw;
-    uint32_t* loc = cnt + 2 * nb;
-    uint32_t* ph = loc + nb;
-    uint32_t* fl = ph + nb;  // logical fill of the open chunk (held items included)
-    uint32_t* p1 = fl + nb;
-    uint32_t* opened = p1 + nb;
-    uint32_t* misc = opened + nb;
-    for (int i = threadIdx.x; i < nb * hw; i += B) H[i] = 0;
-    for (int i = threadIdx.x; i < nb; i += B) {
-        cnt[i] = 0;
-        cnt[nb + i] = 0;
-        ph[i] = kNone;
-        fl[i] = 0;
-    }
-    if (threadIdx.x == 0) {
-        misc[0] = 0;
-        misc[1] = (uint32_t)(chunk0 + (int64_t)blockIdx.x * chunks_per_block(m, gridDim.x, nb, T));
-    }
-    __syncthreads();
-    const uint64_t range = (uint64_t)(L.hi - L.lo);
-    const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
-    const int64_t stride = (int64_t)gridDim.x * T;
-    int64_t sr[IT], tr[IT];
-    int64_t t0 = (int64_t)blockIdx.x * T;
-    if (t0 < m) load_tile<B>(src, dst, t0, m, vec, sr, tr);
-    int par = 0;
-    bool pending = false;
-    for (; t0 < m; t0 += stride, par ^= 1) {
-        uint32_t* cn = cnt + par * nb;
-        uint2 pr[IT];
-        uint32_t rk[IT];
-        uint32_t valid = 0;
-#pragma unroll
-        for (int u = 0; u < IT; ++u) {
-            const int64_t e = t0 + item_off<B>(u);
-            const uint64_t s = (uint64_t)(sr[u] - L.lo), t = (uint64_t)(tr[u] - L.lo);
-            const bool ok = e < m && s < range && t < range;
-            pr[u] = make_uint2((uint32_t)s, (uint32_t)t);
-            valid |= (ok ? 1u : 0u) << u;
-            rk[u] = 0;
-        }
-        if (t0 + stride < m) load_tile<B>(src, dst, t0 + stride, m, vec, sr, tr);  // prefetch
-#pragma unroll
-        for (int u = 0; u < IT; ++u)
-            if ((valid >> u) & 1u) rk[u] = atomicAdd(&cn[pr[u].y >> tb], 1u);
-        __syncthreads();
-        if (threadIdx.x < 64) {
-            if (pending) p6_settle(L, hw, stage, H, cnt + (par ^ 1) * nb, loc, ph, fl, p1, opened, misc, cmeta, chist);
-            p6_plan(nb, cn, loc, ph, fl, p1, opened, misc);
-        }
-        __syncthreads();
-        pending = true;
-        const uint32_t total = misc[2];
-        // held items whose line this tile completes go out first (their slots are refilled below)
-        for (int x = threadIdx.x; x < nb * kLine6; x += B) {
-            const int b = x / kLine6, k = x % kLine6;
-            const uint32_t o = ph[b], f = fl[b];
-            if ((uint32_t)k < held6(o, f)) {
-                const uint32_t line = f & ~(uint32_t)(kLine6 - 1);
-                if (min(f + cn[b], (uint32_t)kCh) >= line + kLine6) pool.put(o, line + k, holdw[x], holdh[x]);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < IT; ++u)
-            if ((valid >> u) & 1u) stage[loc[pr[u].y >> tb] + rk[u]] = pr[u];
-        __syncthreads();
-        // run item r of slice b: position f + r of the open chunk while it fits, else r - room of the opened
-        // chunk p1[b]; positions below the last complete line of the chunk it lands in are stored, the rest held
-        for (uint32_t idx = threadIdx.x; idx < total; idx += B) {
-            const uint2 p = stage[idx];
-            const int b = min((int)(p.y >> tb), nb - 1);
-            const uint32_t r = idx - loc[b], o = ph[b], f = fl[b], c = cn[b];
-            const uint32_t room = o == kNone ? 0u : (uint32_t)kCh - f;
-            const bool first = r < room;
-            if (first) hist_add(H, hw, b, p.x >> L.sbits);
-            const uint32_t end = first ? min(f + c, (uint32_t)kCh) : c - room;
-            const uint32_t pos = first ? f + r : r - room;
-            const uint64_t k = key6(p, tb);
-            if (pos < (end & ~(uint32_t)(kLine6 - 1))) {
-                pool.put(first ? o : p1[b], pos, (uint32_t)k, (uint16_t)(k >> 32));
-            } else {
-                const int slot = b * kLine6 + (int)(pos & (kLine6 - 1));
-                holdw[slot] = (uint32_t)k;
-                holdh[slot] = (uint16_t)(k >> 32);
-            }
-        }
-    }
-    __syncthreads();
-    if (pending && threadIdx.x < 64)
-        p6_settle(L, hw, stage, H, cnt + (par ^ 1) * nb, loc, ph, fl, p1, opened, misc, cmeta, chist);
-    __syncthreads();
-    for (int x = threadIdx.x; x < nb * kLine6; x += B) {  // held tails
-        const int b = x / kLine6, k = x % kLine6;
-        const uint32_t h = held6(ph[b], fl[b]);
-        if ((uint32_t)k < h) pool.put(ph[b], fl[b] - h + k, holdw[x], holdh[x]);
-    }
-    for (int i = threadIdx.x; i < nb; i += B)
-        if (ph[i] != kNone) cmeta[ph[i]] = chunk_meta(i, fl[i]);
-    for (int x = threadIdx.x; x < nb * hw; x += B) {
-        const uint32_t p = ph[x / hw];
-        if (p != kNone) chist[(size_t)p * hw + x % hw] = H[x];
-    }
 }
 
 // used chunks (fill > 0) grouped by target slice (order within a slice is arbitrary).  Each block
@@ -820,7 +597,7 @@ __host__ __device__ constexpr size_t s2_hold_bytes(int nb, bool pk) {
     return pk ? (((size_t)nb * s2_line(true) * 5 + 15) & ~(size_t)15) : sizeof(uint2) * (size_t)nb * kLine;
 }
 
-template <bool HOP1, bool PK, bool F6 = false>  // PK: without HOP1 (LDS); F6: the 6-byte pass-1 pool
+template <bool HOP1, bool PK>  // PK: without HOP1 (LDS)
 __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const void* __restrict__ pool_,
                                                         const unsigned long long* __restrict__ cmeta,
                                                         const uint32_t* __restrict__ order,
@@ -883,30 +660,9 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const void* __restrict__
         }
     };
     const uint2* pool = static_cast<const uint2*>(pool_);
-    // F6: raw (low word, high half) items, decoded against the chunk's slice when used (the prefetch may be
-    // the next segment's chunk); item k of this lane is item_off4(k)
     auto load_chunk = [&](int64_t q, uint2 (&pr)[kItems]) -> uint32_t {
         const uint32_t phys = order[q];
         const uint32_t fill = (uint32_t)(cmeta[phys] >> 32);
-        if (F6) {
-            uint8_t* base = const_cast<uint8_t*>(static_cast<const uint8_t*>(pool_)) + (size_t)phys * kCh * 6;
-            const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, (int)(fill * 4u), 0x00020000);
-            // range checks are per dword: the high halves' bound rounded up to whole dwords, or an odd fill
-            // would lose its last item's half (the item past the fill is masked by the valid test below)
-            const __amdgpu_buffer_rsrc_t rh =
-                __builtin_amdgcn_make_buffer_rsrc(base + (size_t)kCh * 4, (short)0, (int)((fill * 2u + 3u) & ~3u), 0x00020000);
-#pragma unroll
-            for (int k = 0; k < kItems / 4; ++k) {
-                const uint32_t at = (uint32_t)(k * kSBlock + (int)threadIdx.x);
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rw, at * 16u, 0, 0);
-                const auto h = __builtin_amdgcn_raw_buffer_load_b64(rh, at * 8u, 0, 0);
-                pr[4 * k] = make_uint2(v[0], h[0] & 0xFFFFu);
-                pr[4 * k + 1] = make_uint2(v[1], h[0] >> 16);
-                pr[4 * k + 2] = make_uint2(v[2], h[1] & 0xFFFFu);
-                pr[4 * k + 3] = make_uint2(v[3], h[1] >> 16);
-            }
-            return fill;
-        }
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint2*>(pool + (size_t)phys * kCh), (short)0, (int)(fill * sizeof(uint2)), 0x00020000);
 #pragma unroll
@@ -954,14 +710,7 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const void* __restrict__
         }
         uint2 pr[kItems];
 #pragma unroll
-        for (int k = 0; k < kItems; ++k) {
-            if (F6) {  // key = source << tbits | target offset -> (source, target)
-                const uint32_t tb = (uint32_t)L.tbits;
-                pr[k] = make_uint2((nx[k].x >> tb) | (nx[k].y << (32 - tb)), tbase | (nx[k].x & ((1u << tb) - 1u)));
-            } else {
-                pr[k] = nx[k];
-            }
-        }
+        for (int k = 0; k < kItems; ++k) pr[k] = nx[k];
         const uint32_t fill = nfill;
         if (q + 1 < qe) nfill = load_chunk(q + 1, nx);  // prefetch (may be the next segment's)
         for (int i = threadIdx.x; i < nb; i += kSBlock) cnt[i] = 0;
@@ -970,7 +719,7 @@ __global__ void __launch_bounds__(kSBlock) k_scatter_s2(const void* __restrict__
         uint32_t valid = 0;
 #pragma unroll
         for (int k = 0; k < kItems; ++k) {
-            valid |= ((uint32_t)(F6 ? item_off4<kSBlock>(k) : item_off<kSBlock>(k)) < fill ? 1u : 0u) << k;
+            valid |= ((uint32_t)item_off<kSBlock>(k) < fill ? 1u : 0u) << k;
             rk[k] = 0;
         }
 #pragma unroll
@@ -1157,7 +906,7 @@ __global__ void __launch_bounds__(kBlock) k_hop_2d(PairOut pairs, const int64_t*
 }  // namespace part
 
 // ================================ host side =====================================================
-static part::Layout make_layout(int64_t lo, int64_t hi) {
+static part::Layout make_layout(int64_t lo, int64_t hi, bool allow_packed) {
     part::Layout L;
     L.lo = lo;
     L.hi = hi;
@@ -1173,8 +922,7 @@ static part::Layout make_layout(int64_t lo, int64_t hi) {
     if (L.ns < 1) L.ns = 1;
     L.ncells = L.nt * L.ns;
     L.tbits = part::kSliceBits;
-    const char* fmt = getenv("CAPSMI_PAIRS");  // "uint2": the 8-byte pairs (A/B runs)
-    L.packed = L.sbits + L.tbits <= 40 && !(fmt && std::string(fmt) == "uint2");  // 5-byte cell keys
+    L.packed = allow_packed && L.sbits + L.tbits <= 40;  // 5-byte cell keys
     return L;
 }
 
@@ -1207,14 +955,10 @@ static void allow_lds(K kernel, size_t bytes) {
 }
 
 void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
-                     int nt, bool swap, const part::Layout& L, int64_t g2_want, ChunkPart& cp, bool f6) {
+                     int nt, bool swap, const part::Layout& L, int64_t g2_want, ChunkPart& cp) {
     using namespace part;
     hipStream_t st = s->stream;
     cp.L = L;
-    // 6-byte items: (source, target offset) keys of at most 48 bits, and the whole-line LDS of k_scatter_l6
-    f6 = f6 && !swap && (uint64_t)(L.hi - L.lo) <= (uint64_t(1) << (48 - L.tbits)) &&
-         scatter1l6_lds(L.nt, L.ns, kP1Block, kP1Tile) <= (size_t)160 * 1024;
-    cp.f6 = f6;
     // pass 1 grid: one 1024-lane block per CU, fewer for small inputs so the open chunks
     // (blocks x slices) stay within a few times the filled ones
     std::vector<int> g1(nt, 0);
@@ -1242,27 +986,21 @@ void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_
             "relationship table too large for the layout");
     const int64_t npool = pool_chunks > 0 ? pool_chunks : 1;
     const int hw = hist_words(L.ns);
-    cp.pool = dev_alloc((f6 ? 6 : sizeof(uint2)) * kCh * (size_t)(npool + 1), s);  // + a trash chunk
+    cp.pool = dev_alloc(sizeof(uint2) * kCh * (size_t)(npool + 1), s);  // + a trash chunk
     cp.meta = dev_alloc(sizeof(unsigned long long) * npool, s);
     cp.chist = dev_alloc(sizeof(uint32_t) * hw * (size_t)npool, s);
     HIP_CHECK(hipMemsetAsync(P<void>(cp.meta), 0, sizeof(unsigned long long) * npool, st));
     const size_t lds1l = scatter1l_lds(L.nt, L.ns, kP1Block, kP1Tile);
     const bool lines = lds1l <= (size_t)160 * 1024;
-    const size_t lds1 = f6 ? scatter1l6_lds(L.nt, L.ns, kP1Block, kP1Tile) : lines ? lds1l : scatter1_lds(L.nt, L.ns);
-    if (f6)
-        allow_lds(k_scatter_l6<kP1Block, kItems, 4>, lds1);
-    else if (lines)
+    const size_t lds1 = lines ? lds1l : scatter1_lds(L.nt, L.ns);
+    if (lines)
         allow_lds(k_scatter_l<kP1Block, kItems, 4>, lds1);
     else
         allow_lds(k_scatter_c<kP1Block, kItems, 4, kP1NT>, lds1);
     for (int i = 0; i < nt; ++i) {
         if (ms[i] <= 0) continue;
         KernelTimer kt(s, "part_scatter1");
-        if (f6)
-            hipLaunchKernelGGL((k_scatter_l6<kP1Block, kItems, 4>), dim3(g1[i]), dim3(kP1Block), lds1, st, srcs[i], dsts[i],
-                               ms[i], L, c0[i], Pool6{P<uint8_t>(cp.pool)}, P<unsigned long long>(cp.meta),
-                               P<uint32_t>(cp.chist));
-        else if (lines)
+        if (lines)
             hipLaunchKernelGGL((k_scatter_l<kP1Block, kItems, 4>), dim3(g1[i]), dim3(kP1Block), lds1, st, srcs[i], dsts[i],
                                ms[i], L, swap ? 1 : 0, c0[i], (size_t)npool * kCh, P<uint2>(cp.pool),
                                P<unsigned long long>(cp.meta), P<uint32_t>(cp.chist));
@@ -1321,7 +1059,7 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
             "partitioned layout needs an id domain of at most 2^30 ids");
     using namespace part;
     hipStream_t st = s->stream;
-    rp.L = make_layout(lo, hi);
+    rp.L = make_layout(lo, hi, s->cfg.pairs != 2);  // config CAPSMI_PAIRS=uint2: 8-byte pairs
     // Only a layout kept for later queries (capsmi_relpart_build, the cache() route) is packed: pass 2
     // writing the packed form is slower (C3: 3.45 -> 3.9-4.45 ms unfused, 3.73 -> 4.14 ms with hop 1
     // fused) while each hop over it gains 0.2-0.4 ms (hop 1 1.30 -> 0.90, hop 2 1.57 -> 1.35 ms), so a
@@ -1335,13 +1073,9 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
 
     const bool fuse = h1 && h1->a->full;
     ChunkPart cp;
-    // CAPSMI_P1=6: the 6-byte pass-1 pool (A/B).  Measured at C3 (round 5, same box): pass 1 5.26 -> 5.58 ms
-    // and pass 2 + hop 1 3.76 -> 4.45 ms for 2 bytes less per relationship each way -- both passes are bound
-    // by their LDS / VALU phases, not HBM: four times the held slots per tile in pass 1, sub-dword stores,
-    // a second load stream and the decode in pass 2.  The 8-byte pool stays the default.
-    const char* p1e = getenv("CAPSMI_P1");
-    chunk_partition(s, srcs, dsts, ms, nt, false, L, (int64_t)s->num_cus * (fuse ? 1 : 2), cp,
-                    p1e && std::string(p1e) == "6");
+    // (measured and removed in round 6: a 6-byte pass-1 pool, u32 + u16 arrays per chunk -- pass 1 5.26 ->
+    // 5.58 ms, pass 2 + hop 1 3.76 -> 4.45 ms at C3; both passes are bound by their LDS / VALU phases)
+    chunk_partition(s, srcs, dsts, ms, nt, false, L, (int64_t)s->num_cus * (fuse ? 1 : 2), cp);
     const int64_t g2 = cp.g2, mtot = cp.mtot;
     const int64_t maxg = g2 + L.nt;  // segments <= blocks + slices
     int64_t* jst = cp.jst;
@@ -1369,9 +1103,7 @@ void relpart_build(capsmi_session* s, const int64_t* const* srcs, const int64_t*
     const size_t lds2 = sizeof(uint2) * (size_t)kTile + s2_hold_bytes(L.ns, L.packed) +
                         sizeof(uint32_t) * (4 * L.ns + kSBlock / 64) + (fuse ? sizeof(uint32_t) * kSliceWords : 0);
     REQUIRE(lds2 <= (size_t)160 * 1024, CAPSMI_ERR_INTERNAL, "pass-2 LDS");
-    auto k2 = L.packed ? (cp.f6 ? k_scatter_s2<false, true, true> : k_scatter_s2<false, true, false>)
-              : fuse   ? (cp.f6 ? k_scatter_s2<true, false, true> : k_scatter_s2<true, false, false>)
-                       : (cp.f6 ? k_scatter_s2<false, false, true> : k_scatter_s2<false, false, false>);
+    auto k2 = L.packed ? k_scatter_s2<false, true> : fuse ? k_scatter_s2<true, false> : k_scatter_s2<false, false>;
     allow_lds(k2, lds2);
     {
         KernelTimer kt(s, fuse ? "part_scatter2_hop1" : "part_scatter2");

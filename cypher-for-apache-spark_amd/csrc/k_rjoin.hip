@@ -70,15 +70,16 @@ __device__ __forceinline__ bool keys_equal(const KeyCols& pk, const KeyCols& bk,
 }
 
 // WRITE = false: cnt[q] = matches of probe row q (outer: max(1, .)); true: its pairs at off[q].
-// q = the original row (porder: output in probe-row order, so the gathers of the probe side's
-// columns that follow read sequentially, for a random scatter of counts and pairs here) or the
-// row's partition-sorted position (every access here sequential; the output in partition order).
+// q = the row's partition-sorted position: every access here is sequential and the output is in
+// partition order.  (Output in probe-row order -- sequential gathers of the probe side's columns
+// afterwards, for a random scatter of counts and pairs here -- measured slower at every size of
+// scripts/join_bench.py and was removed in round 6.)
 template <bool WRITE>
 __global__ void __launch_bounds__(kBlock) k_join(const uint64_t* __restrict__ ph, const int64_t* __restrict__ prow,
                                                  const int64_t* __restrict__ poff, const uint64_t* __restrict__ bh,
                                                  const int64_t* __restrict__ brow, const int64_t* __restrict__ boff,
                                                  const int64_t* __restrict__ ipre, int64_t nparts, int64_t nitems,
-                                                 KeyCols pk, KeyCols bk, int verify, int outer, int porder,
+                                                 KeyCols pk, KeyCols bk, int verify, int outer,
                                                  int64_t* __restrict__ cnt, const int64_t* __restrict__ off,
                                                  int64_t* __restrict__ out_p, int64_t* __restrict__ out_b) {
     __shared__ uint64_t hk[kSlots];
@@ -102,7 +103,7 @@ __global__ void __launch_bounds__(kBlock) k_join(const uint64_t* __restrict__ ph
             mine[r] = i < t1 ? i : -1;
             hv[r] = i < t1 ? ph[i] : 0;
             got[r] = 0;
-            base[r] = WRITE && i < t1 ? off[porder ? prow[i] : i] : 0;
+            base[r] = WRITE && i < t1 ? off[i] : 0;
         }
         for (int64_t c0 = b0; c0 < b1; c0 += kChunk) {  // block-uniform
             const int64_t c1 = min(c0 + kChunk, b1);
@@ -143,7 +144,7 @@ __global__ void __launch_bounds__(kBlock) k_join(const uint64_t* __restrict__ ph
         for (int r = 0; r < kRows; ++r) {
             if (mine[r] < 0) continue;
             if (!WRITE) {
-                cnt[porder ? prow[mine[r]] : mine[r]] = (outer && got[r] == 0) ? 1 : got[r];
+                cnt[mine[r]] = (outer && got[r] == 0) ? 1 : got[r];
             } else if (outer && got[r] == 0) {
                 const int64_t o = base[r];
                 out_p[o] = prow[mine[r]];
@@ -153,16 +154,11 @@ __global__ void __launch_bounds__(kBlock) k_join(const uint64_t* __restrict__ ph
     }
 }
 
-// probe rows with a null key in an outer join: one (row, -1) pair each
-__global__ void k_null_count(const int64_t* __restrict__ rows, int64_t n, int64_t* __restrict__ cnt) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        cnt[rows[i]] = 1;
-}
-
-__global__ void k_null_rows(const int64_t* __restrict__ rows, int64_t n, const int64_t* __restrict__ off,
-                            int64_t base, int64_t* __restrict__ out_p, int64_t* __restrict__ out_b) {
+// probe rows with a null key in an outer join: one (row, -1) pair each, after the matched pairs
+__global__ void k_null_rows(const int64_t* __restrict__ rows, int64_t n, int64_t base, int64_t* __restrict__ out_p,
+                            int64_t* __restrict__ out_b) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t o = off ? off[rows[i]] : base + i;
+        const int64_t o = base + i;
         out_p[o] = rows[i];
         out_b[o] = -1;
     }
@@ -258,28 +254,22 @@ int64_t radix_join(capsmi_session* s, const KeyCols& bk, int64_t nb, const KeyCo
     HIP_CHECK(hipGetLastError());
     const int64_t nitems = read_scalar(s, ipre + nparts);
     const int verify = pk.n > 1 ? 1 : 0;
-    // partition order (default) measured faster than probe order at every size of scripts/join_bench.py
-    const char* ord = getenv("CAPSMI_RADIX_ORDER");
-    const bool porder = ord && std::string(ord) == "probe";
-    const int64_t nc = porder ? np : Pr.n;  // counts per original row / per sorted position
+    const int64_t nc = Pr.n;  // counts per partition-sorted position
     Buf cnt = dev_alloc(sizeof(int64_t) * (nc > 0 ? nc : 1), s);
     // rows of partitions without build rows get no work item (inner joins): their count stays 0
     HIP_CHECK(hipMemsetAsync(P<void>(cnt), 0, sizeof(int64_t) * (nc > 0 ? nc : 1), st));
-    if (porder && outer && Pr.nnull > 0)
-        hipLaunchKernelGGL(k_null_count, dim3(grid(Pr.nnull)), dim3(256), 0, st, P<int64_t>(Pr.nulls), Pr.nnull,
-                           P<int64_t>(cnt));
     const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nitems, (int64_t)s->num_cus * 8));
     {
         KernelTimer kt(s, "radix_join_count", (double)Pr.n * (16 + 8) + (double)B.n * 16);
         if (nitems > 0)
             hipLaunchKernelGGL(k_join<false>, dim3(g), dim3(kBlock), 0, st, P<uint64_t>(Pr.h), P<int64_t>(Pr.row), poff,
                                P<uint64_t>(B.h), P<int64_t>(B.row), boff, ipre, nparts, nitems, pk, bk, verify,
-                               outer ? 1 : 0, porder ? 1 : 0, P<int64_t>(cnt), nullptr, nullptr, nullptr);
+                               outer ? 1 : 0, P<int64_t>(cnt), nullptr, nullptr, nullptr);
     }
     Buf off = dev_alloc(sizeof(int64_t) * (nc + 1), s);
     exclusive_scan_i64(P<int64_t>(cnt), P<int64_t>(off), nc, s);
-    const int64_t matched = read_scalar(s, P<int64_t>(off) + nc);  // porder: includes the null-key rows
-    const int64_t total = matched + (!porder && outer ? Pr.nnull : 0);
+    const int64_t matched = read_scalar(s, P<int64_t>(off) + nc);
+    const int64_t total = matched + (outer ? Pr.nnull : 0);
     out_p = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), s);
     out_b = dev_alloc(sizeof(int64_t) * (total > 0 ? total : 1), s);
     {
@@ -287,11 +277,11 @@ int64_t radix_join(capsmi_session* s, const KeyCols& bk, int64_t nb, const KeyCo
         if (nitems > 0 && matched > 0)
             hipLaunchKernelGGL(k_join<true>, dim3(g), dim3(kBlock), 0, st, P<uint64_t>(Pr.h), P<int64_t>(Pr.row), poff,
                                P<uint64_t>(B.h), P<int64_t>(B.row), boff, ipre, nparts, nitems, pk, bk, verify,
-                               outer ? 1 : 0, porder ? 1 : 0, nullptr, P<int64_t>(off), P<int64_t>(out_p), P<int64_t>(out_b));
+                               outer ? 1 : 0, nullptr, P<int64_t>(off), P<int64_t>(out_p), P<int64_t>(out_b));
     }
     if (outer && Pr.nnull > 0)
         hipLaunchKernelGGL(k_null_rows, dim3(grid(Pr.nnull)), dim3(256), 0, st, P<int64_t>(Pr.nulls), Pr.nnull,
-                           porder ? P<int64_t>(off) : nullptr, matched, P<int64_t>(out_p), P<int64_t>(out_b));
+                           matched, P<int64_t>(out_p), P<int64_t>(out_b));
     HIP_CHECK(hipGetLastError());
     return total;
 }

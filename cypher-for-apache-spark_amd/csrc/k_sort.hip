@@ -68,83 +68,16 @@ __global__ void __launch_bounds__(B) k_hist(const uint64_t* __restrict__ keys, i
     for (int i = threadIdx.x; i < 256; i += B) hist[(int64_t)i * ntiles + blockIdx.x] = h[i];
 }
 
-struct DigitShifts {
-    int sh[8];
-    int np;
-};
-
-// every pass's global digit histogram in one read of the keys (grid-stride over tiles of B x IT keys;
-// per-wave ballot aggregation as k_hist, per-block LDS counts, one atomic per (block, pass, digit))
-template <int B, int IT>
-__global__ void __launch_bounds__(B) k_hist_all(const uint64_t* __restrict__ keys, int64_t n, DigitShifts ds,
-                                                unsigned long long* __restrict__ gh) {
-    constexpr int T = B * IT;
-    __shared__ unsigned int h[8][256];
-    for (int i = threadIdx.x; i < 8 * 256; i += B) h[i >> 8][i & 255] = 0;
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wbase = (int)(threadIdx.x >> 6) * 64 * IT;
-    for (int64_t tbase = (int64_t)blockIdx.x * T; tbase < n; tbase += (int64_t)gridDim.x * T) {
-        const int cnt_tile = (int)min((int64_t)T, n - tbase);
-        uint64_t k[IT];
-#pragma unroll
-        for (int j = 0; j < IT; ++j) {
-            const int idx = wbase + j * 64 + lane;
-            k[j] = idx < cnt_tile ? keys[tbase + idx] : 0;
-        }
-        for (int p = 0; p < ds.np; ++p) {
-#pragma unroll
-            for (int j = 0; j < IT; ++j) {
-                const bool act = wbase + j * 64 + lane < cnt_tile;
-                const int d = (int)((k[j] >> ds.sh[p]) & 255);
-                int rank, cnt;
-                wave_digit_rank(act, d, rank, cnt);
-                if (act && rank == 0) atomicAdd(&h[p][d], (unsigned)cnt);
-            }
-        }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < ds.np * 256; i += B)
-        if (h[i >> 8][i & 255]) atomicAdd(&gh[i], (unsigned long long)h[i >> 8][i & 255]);
-}
-
-// per pass: exclusive prefix of the 256 digit counts (one 256-lane block per pass)
-__global__ void k_digit_starts(const unsigned long long* __restrict__ gh, int64_t* __restrict__ starts) {
-    __shared__ unsigned long long w[4];
-    const int d = threadIdx.x, lane = d & 63, wv = d >> 6;
-    const unsigned long long c = gh[blockIdx.x * 256 + d];
-    unsigned long long x = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) w[wv] = x;
-    __syncthreads();
-    unsigned long long base = 0;
-    for (int q = 0; q < wv; ++q) base += w[q];
-    starts[blockIdx.x * 256 + d] = (int64_t)(base + x - c);
-}
-
 template <int B>
 constexpr size_t scatter_lds(int tile) {
     return sizeof(uint64_t) * tile + sizeof(int64_t) * 256 + sizeof(unsigned short) * (B / 64) * 256 +
            sizeof(unsigned int) * (256 + B / 64 + 1);
 }
 
-// Onesweep form (OS): no per-pass histogram kernel.  The digits' global starts come from one histogram
-// pass over the keys for every digit position (k_hist_all); a tile takes its index from a ticket counter
-// (so every lower tile has started), publishes its digit counts, and sums the counts of the tiles before
-// it by a decoupled look-back over status words (flag << 56 | count): flag 2p + 1 = aggregate, 2p + 2 =
-// inclusive prefix, for pass p (older passes' words read as not ready, so one clear serves every pass).
-constexpr int kStatusShift = 56;
-constexpr uint64_t kStatusMask = (uint64_t(1) << kStatusShift) - 1;
-
-template <int B, int IT, bool VALS, bool OS>
+template <int B, int IT, bool VALS>
 __global__ void __launch_bounds__(B) k_scatter(const uint64_t* __restrict__ keys, const int64_t* __restrict__ vals,
                                                int64_t n, int shift, int64_t ntiles, const int64_t* __restrict__ offs,
-                                               uint64_t* __restrict__ okeys, int64_t* __restrict__ ovals,
-                                               uint64_t* __restrict__ status, unsigned int* __restrict__ ticket,
-                                               int pass) {
+                                               uint64_t* __restrict__ okeys, int64_t* __restrict__ ovals) {
     constexpr int T = B * IT, W = B / 64;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];  // scatter_lds<B>(T) bytes
     uint64_t* stage = smem;                                              // the tile in digit order (keys, then values)
@@ -153,12 +86,7 @@ __global__ void __launch_bounds__(B) k_scatter(const uint64_t* __restrict__ keys
     unsigned int* tstart = reinterpret_cast<unsigned int*>(&wc[W][0]);  // the digit's first position in the tile
     unsigned int* wsum = tstart + 256;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    int64_t tile = blockIdx.x;
-    if (OS) {
-        if (threadIdx.x == 0) wsum[W] = atomicAdd(ticket, 1u);
-        __syncthreads();
-        tile = wsum[W];
-    }
+    const int64_t tile = blockIdx.x;
     const int64_t tbase = tile * T;
     const int cnt_tile = (int)min((int64_t)T, n - tbase);
     // wave w owns keys [w * 64 * IT, (w + 1) * 64 * IT) of the tile: index order inside a wave is
@@ -172,8 +100,7 @@ __global__ void __launch_bounds__(B) k_scatter(const uint64_t* __restrict__ keys
         const int idx = wbase + j * 64 + lane;
         k[j] = idx < cnt_tile ? keys[tbase + idx] : 0;
     }
-    if (!OS)
-        for (int i = threadIdx.x; i < 256; i += B) gbase[i] = offs[(int64_t)i * ntiles + blockIdx.x];
+    for (int i = threadIdx.x; i < 256; i += B) gbase[i] = offs[(int64_t)i * ntiles + blockIdx.x];
 #pragma unroll
     for (int i = 0; i < 4; ++i) wc[wid][i * 64 + lane] = 0;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -205,28 +132,6 @@ __global__ void __launch_bounds__(B) k_scatter(const uint64_t* __restrict__ keys
             const unsigned int c = wc[w][threadIdx.x];
             wc[w][threadIdx.x] = (unsigned short)tot;
             tot += c;
-        }
-    }
-    if (OS && threadIdx.x < 256) {  // decoupled look-back for this digit's start in the output
-        const int d = threadIdx.x;
-        const uint64_t agg = (uint64_t)(2 * pass + 1) << kStatusShift, inc = (uint64_t)(2 * pass + 2) << kStatusShift;
-        uint64_t* me = status + tile * 256 + d;
-        if (tile == 0) {
-            __hip_atomic_store(me, inc | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            gbase[d] = offs[d];
-        } else {
-            __hip_atomic_store(me, agg | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint64_t excl = 0;
-            for (int64_t j = tile - 1; j >= 0;) {
-                const uint64_t v = __hip_atomic_load(status + j * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t f = v & ~kStatusMask;
-                if (f != agg && f != inc) continue;  // not published yet for this pass: poll again
-                excl += v & kStatusMask;
-                if (f == inc) break;
-                --j;
-            }
-            __hip_atomic_store(me, inc | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            gbase[d] = offs[d] + (int64_t)excl;  // offs: the digit's global start (k_hist_all)
         }
     }
     // tile-local digit starts: exclusive scan of the totals (one per lane of waves 0-3)
@@ -283,63 +188,32 @@ void sort_passes(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, co
     constexpr int T = B * IT;
     static std::once_flag once;  // the staged tile takes more than 64 KiB of LDS
     std::call_once(once, [] {
-        for (const void* k : {reinterpret_cast<const void*>(k_scatter<B, IT, true, false>),
-                              reinterpret_cast<const void*>(k_scatter<B, IT, false, false>),
-                              reinterpret_cast<const void*>(k_scatter<B, IT, true, true>),
-                              reinterpret_cast<const void*>(k_scatter<B, IT, false, true>)})
+        for (const void* k : {reinterpret_cast<const void*>(k_scatter<B, IT, true>),
+                              reinterpret_cast<const void*>(k_scatter<B, IT, false>)})
             HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)scatter_lds<B>(T)));
     });
     hipStream_t st = s->stream;
     const int64_t ntiles = (n + T - 1) / T;
-    // a histogram kernel and a scan per pass (default), or onesweep (CAPSMI_SORT=onesweep, up to 8 digits):
-    // measured at C4 (s = 24, 2^28 keys, 6 digits) the onesweep passes were slower -- tri_sort_und 16.5 ->
-    // 20.2 ms, tri_sort_or 11.8 -> 15.2 ms: the look-back's agent-scope polls cross the XCDs' L2s
-    const char* sf = getenv("CAPSMI_SORT");
-    const bool onesweep = sf && std::string(sf) == "onesweep";
-    const bool os = onesweep && shifts.size() <= 8 && ntiles > 1;
-    const int np = (int)shifts.size();
-    Buf hist, offs, status;
-    if (os) {  // digit starts of every pass, status words, tickets (one clear)
-        offs = dev_alloc(sizeof(int64_t) * 256 * np + sizeof(unsigned long long) * 256 * np + sizeof(unsigned) * 8, s);
-        unsigned long long* gh = reinterpret_cast<unsigned long long*>(P<int64_t>(offs) + 256 * np);
-        HIP_CHECK(hipMemsetAsync(gh, 0, sizeof(unsigned long long) * 256 * np + sizeof(unsigned) * 8, st));
-        status = dev_alloc(sizeof(uint64_t) * 256 * ntiles, s);
-        HIP_CHECK(hipMemsetAsync(P<void>(status), 0, sizeof(uint64_t) * 256 * ntiles, st));
-        DigitShifts ds{};
-        for (int p = 0; p < np; ++p) ds.sh[p] = shifts[p];
-        ds.np = np;
-        const int64_t hb = std::min<int64_t>(ntiles, (int64_t)s->num_cus * 4);
-        hipLaunchKernelGGL((k_hist_all<B, IT>), dim3((unsigned)hb), dim3(B), 0, st, keys, n, ds, gh);
-        hipLaunchKernelGGL(k_digit_starts, dim3((unsigned)np), dim3(256), 0, st, gh, P<int64_t>(offs));
-        HIP_CHECK(hipGetLastError());
-    } else {
-        hist = dev_alloc(sizeof(int64_t) * 256 * ntiles, s);
-        offs = dev_alloc(sizeof(int64_t) * (256 * ntiles + 1), s);
-    }
-    unsigned int* tickets = os ? reinterpret_cast<unsigned int*>(P<int64_t>(offs) + 512 * np) : nullptr;
+    // a histogram kernel and a scan per pass.  (A onesweep form -- every pass's histogram from one read, tiles
+    // finding their starts by decoupled look-back -- measured slower at C4 and removed in round 6: tri_sort_und
+    // 16.5 -> 20.2 ms, tri_sort_or 11.8 -> 15.2 ms; the look-back's agent-scope polls cross the XCDs' L2s)
+    Buf hist = dev_alloc(sizeof(int64_t) * 256 * ntiles, s);
+    Buf offs = dev_alloc(sizeof(int64_t) * (256 * ntiles + 1), s);
     Buf k2 = dev_alloc(sizeof(uint64_t) * n, s);
     Buf v2 = vals ? dev_alloc(sizeof(int64_t) * n, s) : Buf();
     uint64_t *ki = keys, *ko = P<uint64_t>(k2);
     int64_t *vi = vals, *vo = P<int64_t>(v2);
     int passes = 0;
     for (const int shift : shifts) {
-        if (os) {
-            const int64_t* po = P<int64_t>(offs) + 256 * passes;
-            if (vals)
-                hipLaunchKernelGGL((k_scatter<B, IT, true, true>), dim3((unsigned)ntiles), dim3(B), scatter_lds<B>(T), st, ki,
-                                   vi, n, shift, ntiles, po, ko, vo, P<uint64_t>(status), tickets + passes, passes);
-            else
-                hipLaunchKernelGGL((k_scatter<B, IT, false, true>), dim3((unsigned)ntiles), dim3(B), scatter_lds<B>(T), st,
-                                   ki, vi, n, shift, ntiles, po, ko, vo, P<uint64_t>(status), tickets + passes, passes);
-        } else {
+        {
             hipLaunchKernelGGL((k_hist<B, IT>), dim3((unsigned)ntiles), dim3(B), 0, st, ki, n, shift, ntiles, P<int64_t>(hist));
             exclusive_scan_i64(P<int64_t>(hist), P<int64_t>(offs), 256 * ntiles, s);
             if (vals)
-                hipLaunchKernelGGL((k_scatter<B, IT, true, false>), dim3((unsigned)ntiles), dim3(B), scatter_lds<B>(T), st, ki,
-                                   vi, n, shift, ntiles, P<int64_t>(offs), ko, vo, nullptr, nullptr, 0);
+                hipLaunchKernelGGL((k_scatter<B, IT, true>), dim3((unsigned)ntiles), dim3(B), scatter_lds<B>(T), st, ki,
+                                   vi, n, shift, ntiles, P<int64_t>(offs), ko, vo);
             else
-                hipLaunchKernelGGL((k_scatter<B, IT, false, false>), dim3((unsigned)ntiles), dim3(B), scatter_lds<B>(T), st,
-                                   ki, vi, n, shift, ntiles, P<int64_t>(offs), ko, vo, nullptr, nullptr, 0);
+                hipLaunchKernelGGL((k_scatter<B, IT, false>), dim3((unsigned)ntiles), dim3(B), scatter_lds<B>(T), st,
+                                   ki, vi, n, shift, ntiles, P<int64_t>(offs), ko, vo);
         }
         HIP_CHECK(hipGetLastError());
         std::swap(ki, ko);
@@ -365,17 +239,14 @@ void radix_sort_pairs(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t 
 // of a tile then averages 48 keys, so random digits cost fewer partial-line writes in the two
 // output arrays (C4 at s=24, 2^28 pairs: 2.4-3.3 -> 1.6-2.5 ms per pass).  Key-only sorts and
 // smaller ones use 4096-key tiles (two 512-lane blocks per CU): a 2^28-key pass takes 1.19 ms
-// there against 1.4 ms with the larger tile.  CAPSMI_SORT_TILE=4096|12288|16384 forces one.
+// there against 1.4 ms with the larger tile.
 void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, const std::vector<int>& shifts,
                        int at, const std::function<void(const uint64_t*)>& cb) {
     if (n <= 1 || shifts.empty()) {
         if (cb) cb(keys);
         return;
     }
-    static const int forced = getenv("CAPSMI_SORT_TILE") ? atoi(getenv("CAPSMI_SORT_TILE")) : 0;  // A/B runs
-    const int tile = forced ? forced : (vals && n >= (int64_t(1024) * 12288)) ? 12288 : 4096;
-    if (tile == 12288) sort_passes<1024, 12>(s, keys, vals, n, shifts, at, cb);
-    else if (tile == 16384) sort_passes<1024, 16>(s, keys, vals, n, shifts, at, cb);
+    if (vals && n >= (int64_t(1024) * 12288)) sort_passes<1024, 12>(s, keys, vals, n, shifts, at, cb);
     else sort_passes<512, 8>(s, keys, vals, n, shifts, at, cb);
 }
 

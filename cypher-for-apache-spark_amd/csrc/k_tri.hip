@@ -641,9 +641,8 @@ __global__ void k_offsets(const uint64_t* __restrict__ ok_, int64_t ne, int64_t 
 // 1024-lane workgroup (their lists are taken in chunks when they exceed the LDS hash).
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 constexpr int kSmallDeg = 64;
-constexpr int kWedgeUnroll = 4;  // flat walks: wedges per lane with their target loads in flight together
-// (the list walks take it as a template parameter: 4 by default since the direction choice moved the
-// long hub lists to v-mode -- 126.5 ms against 132.4 with 8; before it, 8 beat 4 by 5 %)
+// (the list walks' target loads in flight per lane, U: 4 since the direction choice moved the long hub
+// lists to v-mode -- 126.5 ms against 132.4 with 8; before it, 8 beat 4 by 5 %)
 constexpr int kSmallSlots = 512;  // load <= 1/8: a miss (most wedges) ends after ~1.2 probes
 constexpr int kTriBlock = 256;  // small: 4 waves
 
@@ -733,16 +732,6 @@ __device__ __forceinline__ unsigned long long tri_weight(uint64_t puv, uint64_t 
     return m_uv * m_vw * m_wu + m_uw * m_wv * m_vu;
 }
 
-// last i in [lo, d) with pre[i] <= f, given pre[lo] <= f (pre[0] = 0)
-__device__ __forceinline__ int seg_from(const uint32_t* pre, int lo, int d, uint32_t f) {
-    int hi = d;
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (pre[mid] <= f) lo = mid; else hi = mid;
-    }
-    return lo;
-}
-
 struct SmallWave {
     uint32_t bf[(1 << kSmallBloomBits) / 32];
     uint32_t hk[kSmallSlots];
@@ -750,7 +739,6 @@ struct SmallWave {
     uint64_t vp[kSmallDeg];
     int64_t voff[kSmallDeg];
     uint32_t vl[kSmallDeg];
-    uint32_t pre[kSmallDeg];
     uint32_t dv[kSmallDeg];
 };
 
@@ -786,7 +774,8 @@ __device__ __forceinline__ void list_pass(const uint32_t* __restrict__ tg, TgCod
         keep |= ((uint32_t)(j + (uint32_t)r * 64u <= last) & (word[r] >> (bit[r] & 31))) << r;
 }
 
-template <bool LISTS, int U>  // LISTS: the wave walks each out(v) with all lanes (as k_tri_big_items<true>)
+// the wave walks each out(v) with all lanes (as k_tri_big_items)
+template <int U>
 __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restrict__ tg, TgCode tc,
                                                          const int64_t* __restrict__ ov,
                                                          const int64_t* __restrict__ off, int vmt,
@@ -820,100 +809,59 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
             hinsert(W.hk, W.hi, 9, v, v, (uint32_t)lane);
             bset(W.bf, kSmallBloomBits, v);
         }
-        uint32_t x = dv;  // wave inclusive scan of the out-degrees of the v's
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane < d) W.pre[lane] = x - dv;
-        const uint32_t total = __shfl(x, 63, 64);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (LISTS) {
-            // lists of <= 64 / <= 128 entries walked four / two per pass (as in k_tri_big_items), the
-            // rest one per pass with U loads per lane
-            const uint64_t sm = __ballot(dv > 0u && dv <= 64u), mm = __ballot(dv > 64u && dv <= 128u);
-            uint64_t lm = __ballot(dv > 128u);
-            auto grouped = [&](uint64_t mask, int sgl) {
-                const int per = 64 >> sgl, sg = 1 << sgl, g = lane >> sgl, e = lane & (sg - 1);
-                while (mask) {  // wave-uniform
-                    uint64_t m = mask;
-                    for (int i = 0; i < g; ++i) m &= m - 1;  // this lane group's list: the g-th of the mask
-                    const bool live = m != 0;
-                    const int k = __builtin_ctzll(live ? m : mask);
-                    for (int i = 0; i < per; ++i) mask &= mask - 1;
-                    const int64_t vo = W.voff[k];
-                    const uint32_t dvk = live ? W.dv[k] : 0u, last = (dvk ? dvk : 1u) - 1u;
-                    uint32_t w[4], word[4], bit[4], keep = 0;
+        // lists of <= 64 / <= 128 entries walked four / two per pass (as in k_tri_big_items), the
+        // rest one per pass with U loads per lane
+        const uint64_t sm = __ballot(dv > 0u && dv <= 64u), mm = __ballot(dv > 64u && dv <= 128u);
+        uint64_t lm = __ballot(dv > 128u);
+        auto grouped = [&](uint64_t mask, int sgl) {
+            const int per = 64 >> sgl, sg = 1 << sgl, g = lane >> sgl, e = lane & (sg - 1);
+            while (mask) {  // wave-uniform
+                uint64_t m = mask;
+                for (int i = 0; i < g; ++i) m &= m - 1;  // this lane group's list: the g-th of the mask
+                const bool live = m != 0;
+                const int k = __builtin_ctzll(live ? m : mask);
+                for (int i = 0; i < per; ++i) mask &= mask - 1;
+                const int64_t vo = W.voff[k];
+                const uint32_t dvk = live ? W.dv[k] : 0u, last = (dvk ? dvk : 1u) - 1u;
+                uint32_t w[4], word[4], bit[4], keep = 0;
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) w[t] = tg[vo + (int64_t)min((uint32_t)(e + sg * t), last)];
+                for (int t = 0; t < 4; ++t) w[t] = tg[vo + (int64_t)min((uint32_t)(e + sg * t), last)];
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        bit[t] = bbit(tid(w[t], tc), kSmallBloomBits);
-                        word[t] = W.bf[bit[t] >> 5];
-                    }
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        keep |= ((uint32_t)((uint32_t)(e + sg * t) < dvk) & (word[t] >> (bit[t] & 31))) << t;
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        if (!((keep >> t) & 1u)) continue;
-                        const int sl = hfind(W.hk, 9, tid(w[t], tc), ~0u);
-                        if (sl >= 0) acc += tri_weight(W.vp[k], tpay(w[t], tc, ov, vo + e + sg * t), W.vp[W.hi[sl]]);
-                    }
+                for (int t = 0; t < 4; ++t) {
+                    bit[t] = bbit(tid(w[t], tc), kSmallBloomBits);
+                    word[t] = W.bf[bit[t] >> 5];
                 }
-            };
-            grouped(sm, 4);
-            grouped(mm, 5);
-            while (lm) {  // wave-uniform
-                const int k = __builtin_ctzll(lm);
-                lm &= lm - 1;
-                const int64_t vo = uniform64(W.voff[k]);
-                const uint32_t dvk = __builtin_amdgcn_readfirstlane(W.dv[k]);
-                const uint64_t puv = W.vp[k];
-                for (int j0 = lane; j0 < (int)dvk; j0 += U * 64) {
-                    uint32_t w[U], keep;  // U target loads in flight per lane
-                    list_pass<U>(tg, tc, vo, (int)dvk, j0, W.bf, kSmallBloomBits, w, keep);
 #pragma unroll
-                    for (int r = 0; r < U; ++r) {
-                        if (!((keep >> r) & 1u)) continue;
-                        const int sl = hfind(W.hk, 9, tid(w[r], tc), ~0u);
-                        if (sl >= 0) acc += tri_weight(puv, tpay(w[r], tc, ov, vo + j0 + r * 64), W.vp[W.hi[sl]]);
-                    }
+                for (int t = 0; t < 4; ++t)
+                    keep |= ((uint32_t)((uint32_t)(e + sg * t) < dvk) & (word[t] >> (bit[t] & 31))) << t;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    if (!((keep >> t) & 1u)) continue;
+                    const int sl = hfind(W.hk, 9, tid(w[t], tc), ~0u);
+                    if (sl >= 0) acc += tri_weight(W.vp[k], tpay(w[t], tc, ov, vo + e + sg * t), W.vp[W.hi[sl]]);
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();  // the wave's LDS is reused for the next u
-            continue;
-        }
-        // the lane's current v: index, list base (voff - pre) and the next v's first wedge, in
-        // registers; LDS is read only when the lane moves to another v
-        int i = 0;
-        int64_t base = W.voff[0];
-        uint32_t nxt = d > 1 ? W.pre[1] : 0xFFFFFFFFu;
-        for (uint32_t f0 = lane; f0 < total; f0 += kWedgeUnroll * 64) {
-            int ii[kWedgeUnroll];
-            int64_t pos[kWedgeUnroll];
-            uint32_t w[kWedgeUnroll];
+        };
+        grouped(sm, 4);
+        grouped(mm, 5);
+        while (lm) {  // wave-uniform
+            const int k = __builtin_ctzll(lm);
+            lm &= lm - 1;
+            const int64_t vo = uniform64(W.voff[k]);
+            const uint32_t dvk = __builtin_amdgcn_readfirstlane(W.dv[k]);
+            const uint64_t puv = W.vp[k];
+            for (int j0 = lane; j0 < (int)dvk; j0 += U * 64) {
+                uint32_t w[U], keep;  // U target loads in flight per lane
+                list_pass<U>(tg, tc, vo, (int)dvk, j0, W.bf, kSmallBloomBits, w, keep);
 #pragma unroll
-            for (int k = 0; k < kWedgeUnroll; ++k) {
-                const uint32_t f = f0 + k * 64;
-                if (f < total && f >= nxt) {
-                    i = seg_from(W.pre, i + 1, d, f);
-                    base = W.voff[i] - (int64_t)W.pre[i];
-                    nxt = i + 1 < d ? W.pre[i + 1] : 0xFFFFFFFFu;
+                for (int r = 0; r < U; ++r) {
+                    if (!((keep >> r) & 1u)) continue;
+                    const int sl = hfind(W.hk, 9, tid(w[r], tc), ~0u);
+                    if (sl >= 0) acc += tri_weight(puv, tpay(w[r], tc, ov, vo + j0 + r * 64), W.vp[W.hi[sl]]);
                 }
-                ii[k] = i;
-                pos[k] = base + f;
-                w[k] = f < total ? tid(tg[pos[k]], tc) : kEmpty;
-            }
-#pragma unroll
-            for (int k = 0; k < kWedgeUnroll; ++k) {
-                if (w[k] == kEmpty || !btest(W.bf, kSmallBloomBits, w[k])) continue;
-                const int sl = hfind(W.hk, 9, w[k], ~0u);
-                if (sl >= 0) acc += tri_weight(W.vp[ii[k]], tpay(tg[pos[k]], tc, ov, pos[k]), W.vp[W.hi[sl]]);
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -921,45 +869,6 @@ __global__ void __launch_bounds__(kTriBlock) k_tri_small(const uint32_t* __restr
     }
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
     if (lane == 0 && acc) atomicAdd(out, acc);
-}
-
-// block-wide exclusive scan of n <= 2 B values (B lanes); returns the total
-template <int B>
-__device__ uint32_t big_scan(const uint32_t* in, uint32_t* outp, int n, uint32_t* wtot) {
-    const int per = (n + B - 1) / B;
-    const int b = threadIdx.x * per;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t sum = 0;
-    for (int k = 0; k < per; ++k)
-        if (b + k < n) sum += in[b + k];
-    uint32_t x = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wtot[wave] = x;
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        uint32_t v = lane < B / 64 ? wtot[lane] : 0u;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(v, o, 64);
-            if (lane >= o) v += y;
-        }
-        if (lane < B / 64) wtot[lane] = v;
-    }
-    __syncthreads();
-    uint32_t pre = x - sum + (wave > 0 ? wtot[wave - 1] : 0u);
-    for (int k = 0; k < per; ++k)
-        if (b + k < n) {
-            const uint32_t c = in[b + k];
-            outp[b + k] = pre;
-            pre += c;
-        }
-    const uint32_t total = wtot[B / 64 - 1];
-    __syncthreads();
-    return total;
 }
 
 // Big u are split into work items (hash chunk of out(u), chunk of kVChunk v's of out(u)) so a hub's
@@ -989,10 +898,9 @@ struct ItemLds {
     int64_t voff[kVChunk];
     uint32_t vl[kVChunk];
     uint32_t dv[kVChunk];
-    uint32_t pre[kVChunk];  // flat walk: prefix sums; list walks: the long and short lists' indexes (2 x uint16)
-    uint32_t wtot[B / 64];
-    uint16_t mk[kVChunk];  // list walks: the medium lists' indexes
-    uint32_t ncnt[6];  // list walks: [3 (c & 1) + 0/1/2] long / short / medium lists of chunk c
+    uint32_t pre[kVChunk];  // the long and short lists' indexes (2 x uint16)
+    uint16_t mk[kVChunk];   // the medium lists' indexes
+    uint32_t ncnt[6];       // [3 (c & 1) + 0/1/2] long / short / medium lists of chunk c
     unsigned long long item;
 };
 
@@ -1014,18 +922,18 @@ __global__ void k_tri_item_map(const int64_t* __restrict__ ipre, int64_t nu, uin
         for (int64_t it = ipre[q]; it < ipre[q + 1]; ++it) item_ql[it] = (uint64_t)q | ((uint64_t)(it - ipre[q]) << 32);
 }
 
-// LISTS (default): each wave walks whole out(v) lists of the item's v chunk (wave q takes v = q, q + 16,
-// ...), its lanes striding the list -- coalesced loads, no per-wedge segment search.  The wedges of
-// big u lie in long lists (wedge-weighted mean ≈600 at R-MAT s = 22; 99.8 % in lists of ≥ 64), so the
-// lanes stay busy; the flat form below (one prefix-sum index range over the chunk's wedges) spent
-// ≈70 VALU instructions per wedge on the cursor and the segment search and was issue-bound.
+// Each wave walks whole out(v) lists of the item's v chunk (wave q takes v = q, q + 16, ...), its lanes
+// striding the list -- coalesced loads, no per-wedge segment search.  The wedges of big u lie in long
+// lists (wedge-weighted mean ≈600 at R-MAT s = 22; 99.8 % in lists of ≥ 64), so the lanes stay busy; a
+// flat form (one prefix-sum index range over the chunk's wedges, removed in round 6) spent ≈70 VALU
+// instructions per wedge on the cursor and the segment search and was issue-bound.
 // VM (v-mode): the center c is the middle vertex v; its hash holds out(v) and the walked lists are
 // out(u) for the in-neighbours u of v with od(u) <= od(v).  Otherwise (u-mode) c = u and the walked
 // lists are out(v) for v in out(u), less the edges v-mode takes (vmt > 0: od(v) >= vmt, od(u) <= od(v)).
 // Register budget: two 1024-lane items per CU need 8 waves per SIMD, i.e. an SGPR granule of at most
 // 96 (800 per SIMD): .amdhsa_next_free_sgpr <= 74 here.  At 77 the v-mode launch admitted one item
 // per CU and took 113 instead of 69 ms (the u-mode 512-lane one 25 instead of 21.6 ms).
-template <bool LISTS, int U, bool VM, int B>
+template <int U, bool VM, int B>
 __global__ void __launch_bounds__(B, 8) k_tri_big_items(const uint32_t* __restrict__ tg, TgCode tc,
                                                              const int64_t* __restrict__ ov,
                                                              const int64_t* __restrict__ off,
@@ -1073,10 +981,10 @@ __global__ void __launch_bounds__(B, 8) k_tri_big_items(const uint32_t* __restri
         for (int c = c0; c < c1; ++c) {  // block-uniform
             const int v0 = c * kVChunk, vn = min(kVChunk, nd - v0);
             if (c > c0) __syncthreads();  // the previous chunk's walks are done with the list table
-            uint16_t* lk = reinterpret_cast<uint16_t*>(L.pre);  // LISTS: lists of > 64 entries
-            uint16_t* sk = lk + kVChunk;                        // LISTS: lists of 1..64 entries
+            uint16_t* lk = reinterpret_cast<uint16_t*>(L.pre);  // lists of > 64 entries
+            uint16_t* sk = lk + kVChunk;                        // lists of 1..64 entries
             uint32_t* nc = L.ncnt + 3 * (c & 1);
-            if (LISTS && threadIdx.x < 3) L.ncnt[3 * ((c + 1) & 1) + threadIdx.x] = 0;  // read last by chunk c - 1
+            if (threadIdx.x < 3) L.ncnt[3 * ((c + 1) & 1) + threadIdx.x] = 0;  // read last by chunk c - 1
             for (int k = threadIdx.x; k < vn; k += B) {
                 const uint32_t v = VM ? itg[nb + v0 + k] : tid(tg[b + v0 + k], tc);
                 const int64_t vo = off[v];
@@ -1090,104 +998,72 @@ __global__ void __launch_bounds__(B, 8) k_tri_big_items(const uint32_t* __restri
                 const uint32_t p = (uint32_t)(e - (VM ? vo : b));
                 const uint32_t dw = VM ? (p < (uint32_t)d ? p : 0u) : (vmt > 0 && dv >= (uint32_t)vmt && p < dv ? 0u : dv);
                 L.dv[k] = dw;
-                if (LISTS && dw > 8u * kSG) lk[atomicAdd(&nc[0], 1u)] = (uint16_t)k;
-                else if (LISTS && dw > 4u * kSG) L.mk[atomicAdd(&nc[2], 1u)] = (uint16_t)k;
-                else if (LISTS && dw > 0u) sk[atomicAdd(&nc[1], 1u)] = (uint16_t)k;
+                if (dw > 8u * kSG) lk[atomicAdd(&nc[0], 1u)] = (uint16_t)k;
+                else if (dw > 4u * kSG) L.mk[atomicAdd(&nc[2], 1u)] = (uint16_t)k;
+                else if (dw > 0u) sk[atomicAdd(&nc[1], 1u)] = (uint16_t)k;
             }
             __syncthreads();
-            if (LISTS) {
-                const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-                const int nlong = (int)__builtin_amdgcn_readfirstlane(nc[0]);
-                const int nshort = (int)__builtin_amdgcn_readfirstlane(nc[1]);
-                // short lists (most of them: the median v-mode prefix is ≈56 entries at s = 20): four per
-                // pass of the wave, 16 lanes each, four loads per lane -- four lists' lines in flight at
-                // once instead of one list's one or two.  The list index is per lane (vector registers:
-                // U uniform list bases would cost the SGPR budget above)
-                const int nmed = (int)__builtin_amdgcn_readfirstlane(nc[2]);
-                // ks[0, nk): lists of <= 4 << sgl entries, (64 >> sgl) per wave pass, 1 << sgl lanes each
-                auto grouped = [&](const uint16_t* ks, int nk, int sgl) {
-                    const int per = 64 >> sgl, sg = 1 << sgl;
-                    for (int q0 = wave * per; q0 < nk; q0 += (B / 64) * per) {
-                        const int g = lane >> sgl, e = lane & (sg - 1);
-                        const bool live = q0 + g < nk;
-                        const int k = ks[live ? q0 + g : q0];
-                        const int64_t vo = L.voff[k];
-                        const uint32_t dvk = live ? L.dv[k] : 0u, last = (dvk ? dvk : 1u) - 1u;
-                        uint32_t w[4], word[4], bit[4], keep = 0;
+            const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+            const int nlong = (int)__builtin_amdgcn_readfirstlane(nc[0]);
+            const int nshort = (int)__builtin_amdgcn_readfirstlane(nc[1]);
+            // short lists (most of them: the median v-mode prefix is ≈56 entries at s = 20): four per
+            // pass of the wave, 16 lanes each, four loads per lane -- four lists' lines in flight at
+            // once instead of one list's one or two.  The list index is per lane (vector registers:
+            // U uniform list bases would cost the SGPR budget above)
+            const int nmed = (int)__builtin_amdgcn_readfirstlane(nc[2]);
+            // ks[0, nk): lists of <= 4 << sgl entries, (64 >> sgl) per wave pass, 1 << sgl lanes each
+            auto grouped = [&](const uint16_t* ks, int nk, int sgl) {
+                const int per = 64 >> sgl, sg = 1 << sgl;
+                for (int q0 = wave * per; q0 < nk; q0 += (B / 64) * per) {
+                    const int g = lane >> sgl, e = lane & (sg - 1);
+                    const bool live = q0 + g < nk;
+                    const int k = ks[live ? q0 + g : q0];
+                    const int64_t vo = L.voff[k];
+                    const uint32_t dvk = live ? L.dv[k] : 0u, last = (dvk ? dvk : 1u) - 1u;
+                    uint32_t w[4], word[4], bit[4], keep = 0;
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) w[t] = tg[vo + (int64_t)min((uint32_t)(e + sg * t), last)];
+                    for (int t = 0; t < 4; ++t) w[t] = tg[vo + (int64_t)min((uint32_t)(e + sg * t), last)];
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            bit[t] = bbit(tid(w[t], tc), kBigBloomBits);
-                            word[t] = L.bf[bit[t] >> 5];
-                        }
-#pragma unroll
-                        for (int t = 0; t < 4; ++t)
-                            keep |= ((uint32_t)((uint32_t)(e + sg * t) < dvk) & (word[t] >> (bit[t] & 31))) << t;
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            if (!((keep >> t) & 1u)) continue;
-                            const int sl = hfind(L.hk, lc, tid(w[t], tc), tc.idmask());
-                            if (sl >= 0) {
-                                const uint64_t pxw = tpay(w[t], tc, ov, vo + e + sg * t);
-                                const uint64_t pcw = tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]);
-                                const uint64_t puv = L.vp[k];
-                                acc += VM ? tri_weight(puv, pcw, pxw) : tri_weight(puv, pxw, pcw);
-                            }
-                        }
+                    for (int t = 0; t < 4; ++t) {
+                        bit[t] = bbit(tid(w[t], tc), kBigBloomBits);
+                        word[t] = L.bf[bit[t] >> 5];
                     }
-                };
-                grouped(sk, nshort, kSG == 8 ? 3 : kSG == 16 ? 4 : 5);
-                grouped(L.mk, nmed, kSG == 8 ? 4 : kSG == 16 ? 5 : 6);
-                for (int q = wave; q < nlong; q += B / 64) {  // long lists: one per wave, U x 64 entries a pass
-                    const int k = lk[q];
-                    const int64_t vo = uniform64(L.voff[k]);
-                    const int64_t dv = (int64_t)__builtin_amdgcn_readfirstlane(L.dv[k]);
-                    const uint64_t puv = L.vp[k];
-                    for (int j0 = lane; j0 < (int)dv; j0 += U * 64) {
-                        uint32_t w[U], keep;  // U target loads in flight per lane
-                        list_pass<U>(tg, tc, vo, (int)dv, j0, L.bf, kBigBloomBits, w, keep);
 #pragma unroll
-                        for (int r = 0; r < U; ++r) {
-                            if (!((keep >> r) & 1u)) continue;
-                            const int sl = hfind(L.hk, lc, tid(w[r], tc), tc.idmask());
-                            if (sl >= 0) {
-                                const uint64_t pxw = tpay(w[r], tc, ov, vo + j0 + r * 64);
-                                const uint64_t pcw = tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]);
-                                acc += VM ? tri_weight(puv, pcw, pxw) : tri_weight(puv, pxw, pcw);
-                            }
+                    for (int t = 0; t < 4; ++t)
+                        keep |= ((uint32_t)((uint32_t)(e + sg * t) < dvk) & (word[t] >> (bit[t] & 31))) << t;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        if (!((keep >> t) & 1u)) continue;
+                        const int sl = hfind(L.hk, lc, tid(w[t], tc), tc.idmask());
+                        if (sl >= 0) {
+                            const uint64_t pxw = tpay(w[t], tc, ov, vo + e + sg * t);
+                            const uint64_t pcw = tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]);
+                            const uint64_t puv = L.vp[k];
+                            acc += VM ? tri_weight(puv, pcw, pxw) : tri_weight(puv, pxw, pcw);
                         }
                     }
                 }
-                continue;
-            }
-            const uint32_t tw = big_scan<B>(L.dv, L.pre, vn, L.wtot);
-            int i = 0;  // the lane's current v, as in k_tri_small
-            int64_t base = L.voff[0];
-            uint32_t nxt = vn > 1 ? L.pre[1] : 0xFFFFFFFFu;
-            for (uint32_t f0 = threadIdx.x; f0 < tw; f0 += kWedgeUnroll * B) {
-                // kWedgeUnroll wedges per lane: all their target loads in flight before the probes
-                int ii[kWedgeUnroll];
-                int64_t pos[kWedgeUnroll];
-                uint32_t w[kWedgeUnroll];
+            };
+            grouped(sk, nshort, kSG == 8 ? 3 : kSG == 16 ? 4 : 5);
+            grouped(L.mk, nmed, kSG == 8 ? 4 : kSG == 16 ? 5 : 6);
+            for (int q = wave; q < nlong; q += B / 64) {  // long lists: one per wave, U x 64 entries a pass
+                const int k = lk[q];
+                const int64_t vo = uniform64(L.voff[k]);
+                const int64_t dv = (int64_t)__builtin_amdgcn_readfirstlane(L.dv[k]);
+                const uint64_t puv = L.vp[k];
+                for (int j0 = lane; j0 < (int)dv; j0 += U * 64) {
+                    uint32_t w[U], keep;  // U target loads in flight per lane
+                    list_pass<U>(tg, tc, vo, (int)dv, j0, L.bf, kBigBloomBits, w, keep);
 #pragma unroll
-                for (int k = 0; k < kWedgeUnroll; ++k) {
-                    const uint32_t f = f0 + k * B;
-                    if (f < tw && f >= nxt) {
-                        i = seg_from(L.pre, i + 1, vn, f);
-                        base = L.voff[i] - (int64_t)L.pre[i];
-                        nxt = i + 1 < vn ? L.pre[i + 1] : 0xFFFFFFFFu;
+                    for (int r = 0; r < U; ++r) {
+                        if (!((keep >> r) & 1u)) continue;
+                        const int sl = hfind(L.hk, lc, tid(w[r], tc), tc.idmask());
+                        if (sl >= 0) {
+                            const uint64_t pxw = tpay(w[r], tc, ov, vo + j0 + r * 64);
+                            const uint64_t pcw = tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]);
+                            acc += VM ? tri_weight(puv, pcw, pxw) : tri_weight(puv, pxw, pcw);
+                        }
                     }
-                    ii[k] = i;
-                    pos[k] = base + f;
-                    w[k] = f < tw ? tid(tg[pos[k]], tc) : kEmpty;
-                }
-#pragma unroll
-                for (int k = 0; k < kWedgeUnroll; ++k) {
-                    if (w[k] == kEmpty || !btest(L.bf, kBigBloomBits, w[k])) continue;
-                    const int sl = hfind(L.hk, lc, w[k], tc.idmask());
-                    if (sl >= 0)
-                        acc += tri_weight(L.vp[ii[k]], tpay(tg[pos[k]], tc, ov, pos[k]), tpay(L.hk[sl], tc, ov, b + h0 + L.hi[sl]));
                 }
             }
         }
@@ -1368,7 +1244,7 @@ struct ItemLdsSp {
     unsigned long long item;
 };
 
-// k_tri_big_items (LISTS) over the split lists.  u-mode: the lists of edge u -> v are out_f(v) (when
+// k_tri_big_items over the split lists.  u-mode: the lists of edge u -> v are out_f(v) (when
 // m(u,v) >= 1; factor m(u,v)) and out_b(v) (m(v,u)); v-mode (center c, in-edge u -> c): the prefixes of
 // out_f(u) (factor m(c,u)) and out_b(u) (factor m(u,c)) below c, of lengths pf / pb from ipos.
 template <int U, bool VM, int B, int EC = sp_edges(B), int EPI = kVChunk * kVGroup, int SG = kSG>
@@ -1709,19 +1585,17 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     Buf exc;
     int64_t ne = 0;
     std::unique_ptr<KernelTimer> ph;
-    // the direct oriented build ("the direct oriented build" above) for ids <= 2^24; CAPSMI_TRI_BUILD=sorted:
-    // the undirected sort, orientation and oriented sort (also the build above 2^24 ids)
-    const char* tbe = getenv("CAPSMI_TRI_BUILD");
-    const bool direct = bits <= 24 && !(tbe && std::string(tbe) == "sorted");
+    // the direct oriented build ("the direct oriented build" above) for ids <= 2^24; config
+    // CAPSMI_TRI_BUILD=sorted: the undirected sort, orientation and oriented sort (the build above 2^24 ids)
+    const bool direct = bits <= 24 && !s->cfg.tri_sorted_build;
     if (direct) {
         ph.reset(new KernelTimer(s, "tri_deg"));
         Buf deg = dev_alloc(sizeof(uint32_t) * n, s);
         HIP_CHECK(hipMemsetAsync(P<void>(deg), 0, sizeof(uint32_t) * n, st));
-        // sampled degrees: 1 in 32 relationships above 2^22 (CAPSMI_TRI_DEG_SAMPLE = a power of two, 1 = all).
+        // sampled degrees: 1 in 32 relationships above 2^22 (config CAPSMI_TRI_DEG_SAMPLE = a power of two, 1 = all).
         // At C4 (2^28): all of them took 20 ms of atomics (hubs' counters) and the walks 53.6 ms; 1 in 16 / 64
         // ≈ 1 ms, walks 54.2 ms
-        const char* dse = getenv("CAPSMI_TRI_DEG_SAMPLE");
-        int rate = dse ? std::max(1, atoi(dse)) : (m_all > (int64_t(1) << 22) ? 32 : 1);
+        int rate = s->cfg.tri_deg_sample > 0 ? s->cfg.tri_deg_sample : (m_all > (int64_t(1) << 22) ? 32 : 1);
         while (rate & (rate - 1)) rate &= rate - 1;
         {
             int64_t e0 = 0;
@@ -2016,11 +1890,9 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         hipLaunchKernelGGL(k_max_od, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), n, P<unsigned long long>(t));
         packed = read_scalar(s, reinterpret_cast<const int64_t*>(P<unsigned long long>(t))) < 65536;
     }
-    // direction-split lists (coded targets; CAPSMI_TRI_SPLIT=0: the combined walks, A/B)
-    // (the flat walk of the A/B runs reads the combined in-lists: no split under CAPSMI_TRI_WALK=flat)
-    const char* spe = getenv("CAPSMI_TRI_SPLIT");
-    const char* wke = getenv("CAPSMI_TRI_WALK");
-    g.split = tc.cb > 0 && packed && ne > 0 && !(spe && atoi(spe) == 0) && !(wke && std::string(wke) == "flat");
+    // direction-split lists (coded targets); the combined walks when the codes or packed keys do not fit
+    // (config tri_split = 0 forces them: tests cover that path at small sizes)
+    g.split = tc.cb > 0 && packed && ne > 0 && s->cfg.tri_split;
     Buf rk;  // per oriented edge: f / b ranks (the in-lists' prefix lengths)
     if (g.split) {
         const int64_t ntiles = (ne + kSplitTile - 1) / kSplitTile;
@@ -2045,9 +1917,8 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
                            P<uint4>(g.vrec));
         HIP_CHECK(hipGetLastError());
     }
-    // in-lists and v-mode centers (CAPSMI_TRI_VMODE_T: the od(v) threshold; 0 = every edge from u)
-    const char* vt = getenv("CAPSMI_TRI_VMODE_T");
-    g.vmt = vt ? atoi(vt) : 256;
+    // in-lists and v-mode centers (config CAPSMI_TRI_VMODE_T: the od(v) threshold; 0 = every edge from u)
+    g.vmt = s->cfg.tri_vmode_t;
     if (g.vmt > 0 && ne > 0) {
         const int tsh = packed ? g.ib + 16 : 32;
         std::vector<int> td;  // by (to, from): the input is in (from, to) order and the LSD sort is stable, so
@@ -2169,25 +2040,16 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
         share(g.big_u, g.nbig, false, bp, bn);
         share(g.vm_c, g.nvm, g.vm_own, vp, vn);
         const TgCode tc{(uint32_t)g.ib, (uint32_t)g.cb};
-        const char* walk = getenv("CAPSMI_TRI_WALK");  // "flat": the prefix-sum walk (A/B runs)
-        const bool lists = !(walk && std::string(walk) == "flat");
-        // split in-lists hold (pf, pb) and coded sources: only the split walks read them
-        REQUIRE(!g.split || lists, CAPSMI_ERR_UNSUPPORTED, "triangle count: the flat walk needs a build without split lists");
-        const char* ue = getenv("CAPSMI_TRI_UNROLL");  // target loads in flight per lane: 4 (default), 8 or 16
-        const int un = ue ? atoi(ue) : 4;
         // items (hash chunk, neighbour chunk) of the centers cs[0, nc), taken from a global counter
         auto run_items = [&](const int64_t* cs, int64_t nc, bool vm) {
             Buf ib = dev_alloc(sizeof(int64_t) * (2 * nc + 2), s);
             int64_t* items = P<int64_t>(ib);
             int64_t* ipre = items + nc;
-            const char* ube = getenv("CAPSMI_TRI_UBLOCK");  // u-mode workgroup: 512 (default) or 1024
-            const char* vbe = getenv("CAPSMI_TRI_VBLOCK");  // v-mode workgroup: 1024 (default) or 512
-            const int B = !lists ? 1024 : vm ? (vbe && atoi(vbe) == 512 ? 512 : 1024) : (ube && atoi(ube) == 1024 ? 1024 : 512);
-            // split items of 1024 lanes: 512 (v-mode) / 256 (u-mode) edges per chunk (CAPSMI_TRI_EC=256|512 forces
-            // one; v-mode 256 -> 512: triangles 55.4 -> 54.0 ms), kVChunk * kVGroup edges per item (4096: the same)
-            const char* ece = getenv("CAPSMI_TRI_EC");
-            const bool spl = g.split && lists;
-            const int ec = spl && B == 1024 ? (ece ? atoi(ece) : (vm ? 512 : 256)) : 128;
+            // workgroups: v-mode 1024 lanes, u-mode 512 (four items in flight per CU for its many small
+            // items; v-mode at 512 lanes re-walks the lists for more hash chunks per hub: 96.0 -> 114 ms).
+            // The v-mode split items take 512 edges per chunk (256 -> 512: triangles 55.4 -> 54.0 ms),
+            // kVChunk * kVGroup edges per item (4096: the same)
+            const int B = vm ? 1024 : 512;
             const int epi = kVChunk * kVGroup;
             hipLaunchKernelGGL(k_tri_items, dim3((unsigned)((nc + 255) / 256)), dim3(256), 0, st, P<int64_t>(g.off),
                                vm ? P<int64_t>(g.ioff) : nullptr, cs, nc, 2 * B, epi, items);
@@ -2198,26 +2060,14 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
             Buf ctr = dev_alloc(sizeof(unsigned long long), s);
             HIP_CHECK(hipMemsetAsync(P<void>(ctr), 0, sizeof(unsigned long long), st));
             const size_t lds = B == 1024 ? sizeof(ItemLds<1024>) : sizeof(ItemLds<512>);
-            const char* uve = getenv("CAPSMI_TRI_UNROLL_VM");  // v-mode loads in flight per lane: 4 or 8
-            const int uv = uve ? atoi(uve) : 4;
-            auto kf = vm ? (B == 512 ? k_tri_big_items<true, 4, true, 512>
-                            : uv == 4 ? k_tri_big_items<true, 4, true, 1024> : k_tri_big_items<true, 8, true, 1024>)
-                      : !lists ? k_tri_big_items<false, 4, false, 1024>
-                      : B == 512 ? (un == 8 ? k_tri_big_items<true, 8, false, 512> : k_tri_big_items<true, 4, false, 512>)
-                      : un == 16 ? k_tri_big_items<true, 16, false, 1024>
-                      : un == 8 ? k_tri_big_items<true, 8, false, 1024> : k_tri_big_items<true, 4, false, 1024>;
+            auto kf = vm ? k_tri_big_items<4, true, 1024> : k_tri_big_items<4, false, 512>;
             // resident: two 1024-lane or four 512-lane workgroups per CU (LDS), twice that queued
             const dim3 ig((unsigned)(s->num_cus * (B == 1024 ? 4 : 8)));
-            if (g.split && lists) {  // the walks over the direction-split lists
-                const bool e512 = B == 1024 && ec == 512;
-                const size_t ldsp = B == 1024 ? (e512 ? sizeof(ItemLdsSp<1024, 512>) : sizeof(ItemLdsSp<1024, sp_edges(1024)>))
-                                              : sizeof(ItemLdsSp<512, sp_edges(512)>);
+            if (g.split) {  // the walks over the direction-split lists
+                const size_t ldsp = vm ? sizeof(ItemLdsSp<1024, 512>) : sizeof(ItemLdsSp<512, sp_edges(512)>);
                 // (8 lanes per short list instead of 16 -- 8 lists a wave pass for the halved split lists --
                 // measured 54.4 -> 55.4 ms)
-                auto kp = vm ? (B == 512 ? k_tri_items_sp<4, true, 512>
-                                : e512 ? k_tri_items_sp<4, true, 1024, 512> : k_tri_items_sp<4, true, 1024>)
-                             : (B == 512 ? k_tri_items_sp<4, false, 512>
-                                         : e512 ? k_tri_items_sp<4, false, 1024, 512> : k_tri_items_sp<4, false, 1024>);
+                auto kp = vm ? k_tri_items_sp<4, true, 1024, 512> : k_tri_items_sp<4, false, 512>;
                 set_lds_attr(reinterpret_cast<const void*>(kp), ldsp);
                 hipLaunchKernelGGL(kp, ig, dim3(B), ldsp, st, P<uint32_t>(g.tg), tc, P<int64_t>(g.ov), P<int64_t>(g.off),
                                    P<uint32_t>(g.tgs), P<uint4>(g.vrec), P<int64_t>(g.ioff), P<uint64_t>(g.ikey),
@@ -2234,17 +2084,14 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
         };
         if (bn > 0) run_items(bp, bn, false);
         if (vn > 0) run_items(vp, vn, true);
-        if (sn > 0 && g.split && lists) {
+        if (sn > 0 && g.split) {
             const int64_t gs = std::min<int64_t>((sn + 3) / 4, (int64_t)s->num_cus * 16);
             hipLaunchKernelGGL(k_tri_small_sp<4>, dim3((unsigned)gs), dim3(kTriBlock), 0, st, P<uint32_t>(g.tg), tc,
                                P<int64_t>(g.ov), P<int64_t>(g.off), P<uint32_t>(g.tgs), P<uint4>(g.vrec), g.vmt,
                                sp, sn, P<unsigned long long>(out));
         } else if (sn > 0) {
             const int64_t gs = std::min<int64_t>((sn + 3) / 4, (int64_t)s->num_cus * 16);
-            auto kfs = !lists ? k_tri_small<false, 4>
-                       : un == 16 ? k_tri_small<true, 16>
-                       : un == 8 ? k_tri_small<true, 8> : k_tri_small<true, 4>;
-            hipLaunchKernelGGL(kfs, dim3((unsigned)gs), dim3(kTriBlock), 0, st,
+            hipLaunchKernelGGL(k_tri_small<4>, dim3((unsigned)gs), dim3(kTriBlock), 0, st,
                                P<uint32_t>(g.tg), tc, P<int64_t>(g.ov), P<int64_t>(g.off), g.vmt,
                                sp, sn, P<unsigned long long>(out));
         }

@@ -193,8 +193,8 @@ int64_t undirected_count(capsmi_session* s, const int64_t* const* srcs, const in
         HIP_CHECK(hipGetLastError());
         return marks ? 0 : words_popcount(s, M, 0, nw);
     }
-    const char* ce = getenv("CAPSMI_COUNT");  // "atomic": the per-relationship atomic degrees below (A/B)
-    if (kind == 0 && n <= (int64_t(1) << 26) && !(ce && std::string(ce) == "atomic")) {
+    // (config CAPSMI_COUNT=atomic: the per-relationship atomic degrees below, the form above 2^26 ids)
+    if (kind == 0 && n <= (int64_t(1) << 26) && !s->cfg.count_atomic) {
         // 2-hop count(*): the two-sided record partition of the directed count(*) with both arcs of every
         // relationship (k_count.hip k_rec_part<true>), walks in LDS, no per-relationship global atomics
         return two_hop_count_rec(s, srcs, dsts, ms, nt, a, b, c, true);
@@ -220,8 +220,8 @@ int64_t undirected_count(capsmi_session* s, const int64_t* const* srcs, const in
     // 2-hop count(DISTINCT end); distinct start is the same walk from the other end (the arcs are symmetric)
     const capsmi_bitmap* A = kind == 2 ? c : a;
     const capsmi_bitmap* Cc = kind == 2 ? a : c;
-    const char* ue = getenv("CAPSMI_UND");  // "stream": the per-arc streaming form below (A/B)
-    if (undirected_distinct_part_ok(n) && !(ue && std::string(ue) == "stream"))
+    // (config CAPSMI_UND=stream: the per-arc streaming form below, the form above 2^26 ids)
+    if (undirected_distinct_part_ok(n) && !s->cfg.und_stream)
         return undirected_distinct_part(s, srcs, dsts, ms, nt, A, b, Cc, marks);  // the 2-D cell layout
     KernelTimer kt(s, "und_distinct");
     // B1, B2, C: three bitmaps in one buffer (one fill); x(b) needs no clearing (read only where B1 says

@@ -743,12 +743,11 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
             KernelTimer kt(s, "varlen_rev");
             chunk_partition(s, srcs, dsts, ms, nt, false, L, s->num_cus, ct);
             const int64_t per_slice = (mtot + L.nt - 1) / L.nt;
-            // 8 bits per pair (CAPSMI_VL_BITS), in 2^sublog regions of <= 2^20 bits per slice
-            int64_t bits_per = 8;
-            if (const char* e = getenv("CAPSMI_VL_BITS")) bits_per = atoi(e) < 2 ? 2 : (atoi(e) > 64 ? 64 : atoi(e));
+            // 8 bits per pair (config CAPSMI_VL_BITS), in 2^sublog regions of <= 2^20 bits per slice
+            const int64_t bits_per = s->cfg.vl_bits;
             int sublog = 0, rshift = 10;
             while (sublog < 3 && (bits_per * per_slice >> sublog) > (int64_t(1) << 20)) ++sublog;
-            if (const char* e = getenv("CAPSMI_VL_SUBLOG")) sublog = atoi(e) < 0 ? 0 : (atoi(e) > 5 ? 5 : atoi(e));
+            if (s->cfg.vl_sublog >= 0) sublog = s->cfg.vl_sublog;  // config CAPSMI_VL_SUBLOG
             while ((int64_t(1) << rshift) < (bits_per * per_slice >> sublog) && rshift < 20) ++rshift;
             const int64_t nreg = (int64_t)L.nt << sublog;
             const size_t rbytes = (size_t(1) << rshift) / 8;
@@ -766,9 +765,8 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
             }
         }
         // candidates of the reverse-multiplicity count: a list written by the degree walk (default), or
-        // the F2 filter tested again in the T walk (CAPSMI_VL_F2=1, the earlier form; A/B)
-        const char* f2e = getenv("CAPSMI_VL_F2");
-        const bool use_f2 = f2e && atoi(f2e) != 0;
+        // the F2 filter tested again in the T walk (config CAPSMI_VL_F2=1, the earlier form; the sharded form's)
+        const bool use_f2 = s->cfg.vl_f2;
         Buf clist;
         {
             KernelTimer kt(s, "varlen_deg");
@@ -797,9 +795,6 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
                                    P<unsigned long long>(W));
             }
             const int64_t nc = read_scalar(s, P<int64_t>(cand));
-            if (getenv("CAPSMI_VL_DEBUG"))
-                fprintf(stderr, "varlen: pairs %lld candidates %lld regions %d x 2^%d bits\n", (long long)mtot,
-                        (long long)nc, L.nt << bl.sublog, bl.rshift);
             int64_t cap = 1024;
             while (cap < 2 * nc) cap <<= 1;
             hk = dev_alloc(sizeof(unsigned long long) * cap, s);

@@ -343,9 +343,6 @@ __device__ __forceinline__ bool owns_slice(const ChunkWalk& cw, int j) {
 // source.  Blocks of a consumer kernel launched with g2 blocks walk segments via part::seg_of.
 struct ChunkPart {
     part::Layout L;
-    // f6: the 2-hop layout's pass-1 pool in 6-byte items (k_part.hip k_scatter_l6): per chunk a u32 array of
-    // kCh low words then a u16 array of the high halves of key = source << tbits | target offset; else uint2
-    bool f6 = false;
     Buf pool, meta, chist, jbuf;
     int64_t pool_chunks = 0, npool = 1, mtot = 0, g2 = 1;
     int64_t* jst = nullptr;      // nt + 1 chunk offsets per bucket in `order`
@@ -354,7 +351,7 @@ struct ChunkPart {
     uint32_t* order = nullptr;   // used chunks grouped by bucket
 };
 void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
-                     int nt, bool swap, const part::Layout& L, int64_t g2, ChunkPart& cp, bool f6 = false);
+                     int nt, bool swap, const part::Layout& L, int64_t g2, ChunkPart& cp);
 // the ordering half of chunk_partition for a pool another kernel filled (cp.meta: bucket | fill << 32)
 void chunk_order(capsmi_session* s, int nt, int64_t pool_chunks, int64_t g2, ChunkPart& cp);
 

@@ -1108,6 +1108,39 @@ int64_t dist_two_hop_count(capsmi_session* s, int32_t nt, capsmi_table* const* v
     return read_scalar(s, P<int64_t>(cnt));
 }
 
+std::unique_ptr<capsmi_bitmap> owned_mask(capsmi_session* s, const capsmi_bitmap* b);
+
+// count(*) over BY_SOURCE shards without moving any per-id array.  A rank's out-shard
+// (sources owned) and its in-shard (the relationships from other ranks' sources into owned ids, exchanged once
+// at capsmi_graph_distribute) hold every relationship incident to an owned id exactly once, so for an owned
+// middle b both inA(b) and outC(b) are complete here: count(*) = sum over the ranks of
+// sum_{owned b} b_ok(b) inA(b) outC(b) - loops(b), one record-partition count over the union with b restricted
+// to owned ids and one 8-byte all-reduce -- per-rank bytes received fall with N (the BY_TARGET form
+// all-gathers 4 B x every id's in-degree).  The walk's orientation picks which in-shard column is the source.
+int64_t dist_two_hop_count_src(capsmi_session* s, const Path& P, const RelViews& v0, const capsmi_bitmap* a,
+                               const capsmi_bitmap* b, const capsmi_bitmap* c) {
+    REQUIRE(!a->any_dup && !b->any_dup && !c->any_dup, CAPSMI_ERR_UNSUPPORTED,
+            "closed-form count(*) needs each node id in one scanned row");
+    const Hop& h = P.hops[0];
+    const bool fwd = h.from_role == ROLE_SRC;
+    std::vector<const int64_t*> srcs, dsts;
+    std::vector<int64_t> ms;
+    for (capsmi_table* t : v0.t) {
+        srcs.push_back(t->cols[0].d());
+        dsts.push_back(t->cols[1].d());
+        ms.push_back(t->nrows);
+    }
+    for (const Member& m : P.inst[h.rel].m) {
+        if (m.base->in_rows <= 0) continue;
+        srcs.push_back(fwd ? m.base->in_src.d() : m.base->in_dst.d());
+        dsts.push_back(fwd ? m.base->in_dst.d() : m.base->in_src.d());
+        ms.push_back(m.base->in_rows);
+    }
+    std::unique_ptr<capsmi_bitmap> bown = owned_mask(s, b);
+    const int64_t x = two_hop_count_rec(s, srcs.data(), dsts.data(), ms.data(), (int)srcs.size(), a, bown.get(), c);
+    return sum_over_ranks(s, x);
+}
+
 // the cyclic triangle count over a distributed graph (any relationship mode): the distributed trigraph
 // build (k_tri.hip tri_build: pairs exchanged to their lower end's owner, oriented ranges exchanged and
 // all-gathered), this rank's work share of the centers, one all-reduce of the parts
@@ -1177,8 +1210,7 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
         const Scan& R = P.inst[P.hops[0].rel];
         bool keep = !R.m.empty();
         for (const Member& m : R.m) keep = keep && m.base->keep_layouts;
-        // the reversed relationships (distinct start = distinct end of the reversed walk; and over BY_SOURCE
-        // shards the count(*) runs as the BY_TARGET count of the reversed graph)
+        // the reversed relationships (distinct start = distinct end of the reversed walk)
         RelViews rv;
         reversed_views(v0, rv);
         const bool by_tgt = g_dist.rel_mode == CAPSMI_RELS_BY_TARGET;
@@ -1203,9 +1235,11 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
                 lay = it->second.get();
             }
             if (g_dist.on && k == A_COUNT) {
-                // every relationship into an owned id (BY_TARGET), or out of one (BY_SOURCE: the reversed graph)
+                // BY_TARGET: every relationship into an owned id, the owned in-degrees all-gathered; BY_SOURCE:
+                // the out- and in-shards of the owned middles, no per-id exchange (dense ids: the in-shard's)
                 x = by_tgt ? dist_two_hop_count(s, (int32_t)nt, v0.t.data(), a, b, cc)
-                           : dist_two_hop_count(s, (int32_t)nt, rv.t.data(), cc, b, a);
+                    : g_dense ? dist_two_hop_count_src(s, P, v0, a, b, cc)
+                              : dist_two_hop_count(s, (int32_t)nt, rv.t.data(), cc, b, a);
             } else if (g_dist.on) {
                 // the walk's relationships arrive by their end's owner (BY_TARGET forwards, BY_SOURCE reversed):
                 // the all-gather form; by their start's owner: the OR-reduce form

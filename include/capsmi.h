@@ -193,6 +193,15 @@ capsmi_status capsmi_session_set_stream(capsmi_session* s, void* hip_stream);
  * torch's default stream is, so kernels and torch work stay ordered */
 capsmi_status capsmi_session_use_stream(capsmi_session* s, void* hip_stream);
 capsmi_status capsmi_session_sync(capsmi_session* s);
+/* session configuration (ConfigOption / CoraConfiguration analogue): every CAPSMI_* knob is
+ * read from the environment once, at capsmi_session_create; this changes one for this session only.
+ * `name` is the knob's environment name (e.g. "CAPSMI_JOIN", "CAPSMI_COUNT"), `value` its text as the
+ * environment would hold it, NULL = back to the environment's value at the time of the call (or the
+ * default).  Unknown names and unparsable values are refused (CAPSMI_ERR_ILLEGAL_ARGUMENT).  The knobs and
+ * their meaning: DESIGN.md §5a. */
+capsmi_status capsmi_session_set_config(capsmi_session* s, const char* name, const char* value);
+/* the same check without a session or device: CAPSMI_OK when capsmi_session_set_config would accept it */
+capsmi_status capsmi_config_check(const char* name, const char* value);
 /* per-kernel HIP-event timing of the fused graph kernels (off by default; SURVEY.md §5 tracing).
  * While enabled, each hot launch is bracketed by events on the session stream.  Enabling creates a pool of
  * events up front (resolved ones return to it), so timed queries make no event-creation calls. */

@@ -41,3 +41,23 @@ def session():
     s.set_stream(torch.cuda.current_stream().cuda_stream)
     yield s
     s.close()
+
+
+@pytest.fixture
+def knobs():
+    """``knobs(session, CAPSMI_COUNT="atomic")``: CAPSMI_* configuration knobs on a session for one test
+    (capsmi_session_set_config -- the library reads the environment only at session create), put back to
+    the environment's values when the test ends."""
+    done = []
+
+    def set_(sess, **kv):
+        for k, v in kv.items():
+            sess.set_config(k, v)
+            done.append((sess, k))
+
+    yield set_
+    for sess, k in reversed(done):
+        try:
+            sess.set_config(k, None)
+        except Exception:  # a session the test closed
+            pass

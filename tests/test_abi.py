@@ -68,3 +68,23 @@ def test_null_arguments_are_rejected():
     b, e = ctypes.c_int64(), ctypes.c_int64()
     assert lib.capsmi_owner_words(1 << 20, 3, 8, ctypes.byref(b), ctypes.byref(e)) == 0
     assert (b.value, e.value) == (3 * 32768 // 8, 4 * 32768 // 8)
+
+
+def test_config_knobs_are_checked():
+    """capsmi_config_check: the session configuration's names and values, refused when
+    unknown -- the removed A/B variants' knobs included -- or unparsable."""
+    from capsmi import _lib
+    lib = _lib.load()
+    ok = [("CAPSMI_JOIN", "radix"), ("CAPSMI_JOIN", "auto"), ("CAPSMI_COUNT", "atomic"), ("CAPSMI_COUNT", "rec"),
+          ("CAPSMI_REC_FULL", "0"), ("CAPSMI_GROUPED", "keys"), ("CAPSMI_PAIRS", "uint2"), ("CAPSMI_TRI_BUILD", "sorted"),
+          ("CAPSMI_TRI_DEG_SAMPLE", "32"), ("CAPSMI_TRI_SPLIT", "0"), ("CAPSMI_TRI_VMODE_T", "0"),
+          ("CAPSMI_UND", "stream"), ("CAPSMI_VL_BITS", "16"), ("CAPSMI_VL_SUBLOG", "3"), ("CAPSMI_VL_F2", "1"),
+          ("CAPSMI_COLL_CHUNK", "64"), ("CAPSMI_INGEST_THREADS", "4"), ("CAPSMI_JOIN", None)]
+    for k, v in ok:
+        assert lib.capsmi_config_check(k.encode(), None if v is None else v.encode()) == _lib.OK, (k, v)
+    bad = [("CAPSMI_JOIN", "sideways"), ("CAPSMI_COUNT", "pairs"), ("CAPSMI_VL_BITS", "1"), ("CAPSMI_TRI_SPLIT", "x"),
+           ("CAPSMI_COLL_CHUNK", "0"), ("CAPSMI_P1", "6"), ("CAPSMI_SORT", "onesweep"), ("CAPSMI_TRI_WALK", "flat"),
+           ("CAPSMI_RADIX_ORDER", "probe"), ("CAPSMI_NOPE", None)]
+    for k, v in bad:
+        assert lib.capsmi_config_check(k.encode(), None if v is None else v.encode()) == _lib.ERR_ILLEGAL_ARGUMENT, (k, v)
+        assert "configuration" in _lib.last_error()

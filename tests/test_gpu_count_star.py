@@ -1,6 +1,6 @@
 """2-hop count(*) (capsmi_two_hop_count) in every form against the closed form of oracle/closed.c:
-the two partitions of 2-byte records (default), the two chunked pair partitions with LDS slice counts
-(CAPSMI_COUNT=pairs) and the per-relationship atomics (CAPSMI_COUNT=atomic).  The closed form itself is pinned against binding enumeration in
+the two partitions of 2-byte records (default) and the per-relationship atomics (config CAPSMI_COUNT=atomic,
+the form above 2^26 ids).  The closed form itself is pinned against binding enumeration in
 tests/test_oracle*.py."""
 import numpy as np
 import pytest
@@ -9,12 +9,11 @@ from oracle import cpu
 
 pytestmark = pytest.mark.gpu
 
-MODES = ["rec", "pairs", "atomic"]
+MODES = ["rec", "atomic"]
 
 
-def _mode(monkeypatch, mode):
-    if mode != "rec":
-        monkeypatch.setenv("CAPSMI_COUNT", mode)
+def _mode(knobs, session, mode):
+    knobs(session, CAPSMI_COUNT=mode)
 
 
 def _bm(session, n, mask):
@@ -30,9 +29,9 @@ def _rels(session, src, dst):
 
 
 @pytest.mark.parametrize("mode", MODES)
-def test_self_loops_and_distinct_masks(session, monkeypatch, mode):
+def test_self_loops_and_distinct_masks(session, knobs, mode):
     from capsmi import graph
-    _mode(monkeypatch, mode)
+    _mode(knobs, session, mode)
     edges = [(0, 0), (1, 1), (1, 1), (3, 2), (2, 2), (4, 5), (5, 5), (5, 6), (2, 5), (6, 2), (3, 3)]
     src = np.array([e[0] for e in edges], dtype=np.int64)
     dst = np.array([e[1] for e in edges], dtype=np.int64)
@@ -46,11 +45,11 @@ def test_self_loops_and_distinct_masks(session, monkeypatch, mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
-def test_hub_slices_and_split_walks(session, monkeypatch, mode):
+def test_hub_slices_and_split_walks(session, knobs, mode):
     """2^21 ids (64 slices of 2^15): hub slices far longer than one chunk, slices split between walk
     blocks, ids outside the domain, self-loops, two tables, distinct a/b/c filters."""
     from capsmi import graph
-    _mode(monkeypatch, mode)
+    _mode(knobs, session, mode)
     rng = np.random.default_rng(17)
     n = 1 << 21
     m = 400000
@@ -73,11 +72,11 @@ def test_hub_slices_and_split_walks(session, monkeypatch, mode):
     assert graph.two_hop_count(session, [t1, t2], _bm(session, n, a), _bm(session, n, b), _bm(session, n, c)) == rows
 
 
-@pytest.mark.parametrize("mode", ["rec", "pairs"])
+@pytest.mark.parametrize("mode", ["rec", "atomic"])
 @pytest.mark.parametrize("scale,kind", [(12, "person"), (16, "all"), (17, "person")])
-def test_rmat(session, monkeypatch, mode, scale, kind):
+def test_rmat(session, knobs, mode, scale, kind):
     from capsmi import graph
-    _mode(monkeypatch, mode)
+    _mode(knobs, session, mode)
     n = 1 << scale
     src, dst = cpu.rmat_edges(scale, 0, 16 << scale)
     mask = np.ones(n, np.uint8) if kind == "all" else cpu.person_mask(n).astype(np.uint8)
@@ -86,13 +85,13 @@ def test_rmat(session, monkeypatch, mode, scale, kind):
     assert graph.two_hop_count(session, [_rels(session, src, dst)], bm, bm, bm) == rows
 
 
-@pytest.mark.parametrize("mode", ["rec", "pairs"])
-def test_dense_buckets_roll_chunks(session, monkeypatch, mode):
+@pytest.mark.parametrize("mode", ["rec", "atomic"])
+def test_dense_buckets_roll_chunks(session, knobs, mode):
     """3M relationships into three 2^16-id buckets: every partition block fills several chunks of one
     bucket (chunk rollover inside a tile, pieces split across chunks), plus a ragged tail and
     in-degrees far above 2^16 for a few ids."""
     from capsmi import graph
-    _mode(monkeypatch, mode)
+    _mode(knobs, session, mode)
     rng = np.random.default_rng(23)
     n = 1 << 20
     m = 3_000_001
@@ -109,13 +108,13 @@ def test_dense_buckets_roll_chunks(session, monkeypatch, mode):
 
 
 @pytest.mark.parametrize("seed", [0, 1])
-def test_rec_counter_wraps_on_even_and_odd_ids(session, monkeypatch, seed):
+def test_rec_counter_wraps_on_even_and_odd_ids(session, knobs, seed):
     """The IN walk counts two ids per 32-bit LDS word in 16-bit halves (even id low, odd id high).
     Pairs (x even, x + 1) with more than 2^16 in-relationships each exercise the low-half wrap (its
     carry reaches the high half), the high-half wrap, and a low-half carry into a high half sitting
     at 0xFFFF (x + 1 with 65535 mod 65536 in-relationships) -- each against the closed form."""
     from capsmi import graph
-    _mode(monkeypatch, "rec")
+    _mode(knobs, session, "rec")
     rng = np.random.default_rng(100 + seed)
     n = 1 << 18
     counts = {2000: 200_001, 2001: 131_071, 4000: 65_536, 4001: 65_535, 6000: 70_000, 8000: 65_535, 8001: 196_607,
@@ -135,13 +134,13 @@ def test_rec_counter_wraps_on_even_and_odd_ids(session, monkeypatch, seed):
     assert got == rows
 
 
-@pytest.mark.parametrize("mode", ["rec", "pairs"])
-def test_offset_domain(session, monkeypatch, mode):
+@pytest.mark.parametrize("mode", ["rec", "atomic"])
+def test_offset_domain(session, knobs, mode):
     """Bitmaps over [lo, lo + n) with lo far from 0 and n not a multiple of the 2^16-id bucket:
     records are ids relative to lo, the last bucket is partial, and relationships leaving the domain
     on either side are dropped."""
     from capsmi import ColumnData, I64, graph
-    _mode(monkeypatch, mode)
+    _mode(knobs, session, mode)
     rng = np.random.default_rng(31)
     lo, n, m = 1 << 33, 200_003, 1_500_000
     src = rng.integers(0, n, m)

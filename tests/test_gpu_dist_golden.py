@@ -38,13 +38,13 @@ def _port():
 # (ranks, backend, mode): 2 gloo ranks sharing the GPU, routed and unrouted; and 1 rank over RCCL (backend
 # nccl), unrouted, so every Exchange of the generic executor -- the ALL_TO_ALL_V of hash-partitioned joins
 # and groupings, the all-gathers of global aggregates and ordering -- runs through RCCL, in chunked calls
-# (CAPSMI_COLL_CHUNK=64: the golden graphs are small)
+# (CAPSMI_COLL_CHUNK=64 on every backend: the golden graphs are small, so at two gloo ranks the all-gathers
+# stage rank-major rounds and the ALL_TO_ALL_V rounds carry unequal, partly empty per-peer counts)
 @pytest.mark.parametrize("world,backend,mode", [(2, "gloo", "fused"), (2, "gloo", "unfused"), (1, "nccl", "unfused")])
 def test_golden_vectors_on_two_ranks(tmp_path, world, backend, mode):
     out = str(tmp_path / "golden")
     env = dict(os.environ, CAPSMI_DIST_BACKEND=backend, MASTER_ADDR="127.0.0.1")
-    if backend == "nccl":
-        env["CAPSMI_COLL_CHUNK"] = "64"
+    env["CAPSMI_COLL_CHUNK"] = "64"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}", "--master-addr",
            "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "tests", "dist_golden_worker.py"), out, mode]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=280)

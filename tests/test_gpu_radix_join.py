@@ -55,27 +55,17 @@ def _pairs(t):
 
 
 def _join(session, L, R, jt, nkeys, mode):
-    """mode: a CAPSMI_JOIN strategy, "radix:probe" = the radix join emitting in probe-row order"""
-    strategy, _, order = mode.partition(":")
-    saved = {k: os.environ.get(k) for k in ("CAPSMI_JOIN", "CAPSMI_RADIX_ORDER")}
-    os.environ["CAPSMI_JOIN"] = strategy
-    os.environ["CAPSMI_RADIX_ORDER"] = order or "partition"
-    try:
+    """mode: a CAPSMI_JOIN strategy (session configuration)"""
+    with session.configured(CAPSMI_JOIN=mode):
         t = L.join(R, jt, *[(f"l_k{i}", f"r_k{i}") for i in range(nkeys)])
         return _pairs(t)
-    finally:
-        for k, v in saved.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
 
 
 def _check(session, lk, rk, jt, lv=None, rv=None, types=None):
     L = _table(session, "l", lk, lv, types)
     R = _table(session, "r", rk, rv, types)
     want = _expected(lk, lv, rk, rv, jt)
-    for mode in ("radix", "radix:probe", "hash", "direct", "auto"):
+    for mode in ("radix", "hash", "direct", "auto"):
         got = _join(session, L, R, jt, len(lk), mode)
         assert got.shape == want.shape, mode
         np.testing.assert_array_equal(got, want, err_msg=mode)

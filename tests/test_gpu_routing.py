@@ -74,19 +74,15 @@ def test_c3_count_distinct_routed(session, scale):
 
 @pytest.mark.parametrize("scale,kind", [(13, "all"), (16, "person")])
 def test_c3_count_star_partitioned(session, scale, kind):
-    """count(*) of C3 from the two chunked partitions with LDS counts (k_count.hip) equals the
-    per-relationship atomic form and the oracle's closed form; at scale 16 a slice of 2^15 ids is
-    shared by several blocks' chunk shares (flushed with atomics)."""
+    """count(*) of C3 from the record partition (k_count.hip) equals the per-relationship atomic form and
+    the oracle's closed form; at scale 16 a bucket's records span several blocks' chunk shares."""
     import os
     from oracle import cpu
     sg = _graph(session, scale, kind=kind)
     q = {"clauses": C3["clauses"], "return": {"items": [["n", ["count*"]]]}}
     got = _routed(session, "two_hop", lambda: _run(session, sg, q))
-    os.environ["CAPSMI_COUNT"] = "atomic"
-    try:
+    with session.configured(CAPSMI_COUNT="atomic"):
         atomic = _run(session, sg, q)
-    finally:
-        del os.environ["CAPSMI_COUNT"]
     n = 1 << scale
     src, dst = cpu.rmat_edges(scale, 0, 16 << scale)
     pm = cpu.person_mask(n) if kind == "person" else np.ones(n, np.uint8)
@@ -269,8 +265,5 @@ def test_c3_grouped_routed(session, scale, kind):
     assert same_rows(got, want)
     if scale == 12:
         assert same_rows(_run(session, sg, q, fused=False), want)
-        os.environ["CAPSMI_GROUPED"] = "keys"  # the per-binding key sort (A/B): the same rows
-        try:
+        with session.configured(CAPSMI_GROUPED="keys"):  # the per-binding key sort: the same rows
             assert same_rows(_run(session, sg, q), want)
-        finally:
-            del os.environ["CAPSMI_GROUPED"]

@@ -1,7 +1,7 @@
 """The device radix sort (k_sort.hip) through ORDER BY: the output order must equal numpy's stable
 argsort exactly -- ties keep their input order (LSD passes rely on that), on ragged sizes around the
-4096-key tile, skewed digits (many equal bytes) and negative / Double keys; both pass forms (per-pass
-histograms, the default, and the onesweep look-back)."""
+4096-key tile, skewed digits (many equal bytes) and negative / Double keys (per-pass histograms; round 6
+removed the measured-slower onesweep form)."""
 import numpy as np
 import pytest
 
@@ -16,20 +16,16 @@ def _order(session, values, ty, desc=False):
     return np.asarray(t.orderBy(("k", "desc" if desc else "asc")).column("i").values, dtype=np.int64)
 
 
-@pytest.mark.parametrize("form", ["passes", "onesweep"])  # CAPSMI_SORT: per-pass histograms / decoupled look-back
 @pytest.mark.parametrize("n", [1, 7, 4095, 4096, 4097, 100_003, 1 << 20, 1024 * 12288 + 12289])  # last: 12288-key tiles
-def test_order_by_is_stable_argsort(session, monkeypatch, n, form):
+def test_order_by_is_stable_argsort(session, n):
     from capsmi.expr import I64
-    monkeypatch.setenv("CAPSMI_SORT", form)
     rng = np.random.default_rng(n)
     k = rng.integers(-50, 50, n).astype(np.int64)  # few distinct keys: long runs of ties
     np.testing.assert_array_equal(_order(session, k, I64), np.argsort(k, kind="stable"))
 
 
-@pytest.mark.parametrize("form", ["passes", "onesweep"])
-def test_order_by_skewed_and_wide_keys(session, monkeypatch, form):
+def test_order_by_skewed_and_wide_keys(session):
     from capsmi.expr import I64
-    monkeypatch.setenv("CAPSMI_SORT", form)
     rng = np.random.default_rng(5)
     n = 3 * 4096 + 17
     k = np.where(rng.random(n) < 0.9, 0, rng.integers(-(1 << 62), 1 << 62, n)).astype(np.int64)  # one hot digit

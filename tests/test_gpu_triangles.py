@@ -21,27 +21,25 @@ def _count(session, n, src, dst, mask=None, nparts=1):
 
 
 VMODE = ["0", "2", "default"]  # CAPSMI_TRI_VMODE_T: every edge from u / almost every edge from v / 256
-# walks: lists over the direction-split lists (default), lists over the combined out-lists, the flat
-# prefix-sum walk
-WALKS = ["lists", "lists-nosplit", "flat"]
+# walks: lists over the direction-split lists (default), lists over the combined out-lists (the form when the
+# split codes do not fit; config CAPSMI_TRI_SPLIT=0)
+WALKS = ["lists", "lists-nosplit"]
 
 
-def _vmode(monkeypatch, t):
+def _vmode(knobs, session, t):
     if t != "default":
-        monkeypatch.setenv("CAPSMI_TRI_VMODE_T", t)
+        knobs(session, CAPSMI_TRI_VMODE_T=t)
 
 
-def _walk(monkeypatch, walk):
-    if walk == "flat":
-        monkeypatch.setenv("CAPSMI_TRI_WALK", "flat")
-    elif walk == "lists-nosplit":
-        monkeypatch.setenv("CAPSMI_TRI_SPLIT", "0")
+def _walk(knobs, session, walk):
+    if walk == "lists-nosplit":
+        knobs(session, CAPSMI_TRI_SPLIT="0")
 
 
 @pytest.mark.parametrize("vmode", VMODE)
 @pytest.mark.parametrize("seed", range(8))
-def test_random_multigraphs(session, monkeypatch, seed, vmode):
-    _vmode(monkeypatch, vmode)
+def test_random_multigraphs(session, knobs, seed, vmode):
+    _vmode(knobs, session, vmode)
     rng = np.random.default_rng(seed)
     n = int(rng.integers(3, 60))
     m = int(rng.integers(0, 600))
@@ -52,8 +50,8 @@ def test_random_multigraphs(session, monkeypatch, seed, vmode):
 
 
 @pytest.mark.parametrize("vmode", VMODE)
-def test_node_filter_and_parts(session, monkeypatch, vmode):
-    _vmode(monkeypatch, vmode)
+def test_node_filter_and_parts(session, knobs, vmode):
+    _vmode(knobs, session, vmode)
     rng = np.random.default_rng(42)
     n, m = 200, 4000
     src = rng.integers(0, n, m).astype(np.int64)
@@ -68,20 +66,20 @@ def test_node_filter_and_parts(session, monkeypatch, vmode):
 @pytest.mark.parametrize("vmode", VMODE)
 @pytest.mark.parametrize("walk", WALKS)
 @pytest.mark.parametrize("scale", [9, 12])
-def test_rmat(session, monkeypatch, scale, walk, vmode):
-    _vmode(monkeypatch, vmode)
-    _walk(monkeypatch, walk)
+def test_rmat(session, knobs, scale, walk, vmode):
+    _vmode(knobs, session, vmode)
+    _walk(knobs, session, walk)
     src, dst = cpu.rmat_edges(scale, 0, 16 << scale)
     assert _count(session, 1 << scale, src, dst) == cpu.triangle_enumerate(1 << scale, src, dst)
 
 
 @pytest.mark.parametrize("vmode", VMODE)
 @pytest.mark.parametrize("walk", WALKS)
-def test_dense_big_vertices(session, monkeypatch, walk, vmode):
+def test_dense_big_vertices(session, knobs, walk, vmode):
     """Out-degrees above 64 (one workgroup per vertex) on a dense random multigraph; every wedge walk
-    (wave-per-list over split or combined lists, CAPSMI_TRI_WALK=flat prefix-sum walk)."""
-    _vmode(monkeypatch, vmode)
-    _walk(monkeypatch, walk)
+    (wave-per-list over split or combined lists)."""
+    _vmode(knobs, session, vmode)
+    _walk(knobs, session, walk)
     rng = np.random.default_rng(11)
     n, m = 300, 40000
     src = rng.integers(0, n, m).astype(np.int64)
@@ -92,9 +90,9 @@ def test_dense_big_vertices(session, monkeypatch, walk, vmode):
 @pytest.mark.parametrize("vmode", VMODE)
 @pytest.mark.parametrize("walk", ["lists", "lists-nosplit"])
 @pytest.mark.parametrize("mult", [False, True])
-def test_complete_digraph_chunks(session, monkeypatch, mult, walk, vmode):
-    _vmode(monkeypatch, vmode)
-    _walk(monkeypatch, walk)
+def test_complete_digraph_chunks(session, knobs, mult, walk, vmode):
+    _vmode(knobs, session, vmode)
+    _walk(knobs, session, walk)
     """Complete digraph on 2200 nodes: out-degrees up to 2199 exceed one LDS chunk (2048).
     Loop-free, so count(*) = trace(M^3) for the multiplicity matrix M (exact in float64 here)."""
     n = 2200
@@ -135,11 +133,11 @@ def test_wide_id_range(session):
 
 
 @pytest.mark.parametrize("vmode", VMODE)
-def test_exception_multiplicities(session, monkeypatch, vmode):
+def test_exception_multiplicities(session, knobs, vmode):
     """Multiplicities from 1 to 40 in both directions: the 4-bit codes of the oriented targets saturate
     (>= 15) for many edges, whose exact payloads are placed after the key-only sort (k_exc_place) and
     read on hits from either side of a wedge."""
-    _vmode(monkeypatch, vmode)
+    _vmode(knobs, session, vmode)
     rng = np.random.default_rng(17)
     n = 90
     a, b = np.nonzero(rng.random((n, n)) < 0.25)
@@ -153,11 +151,11 @@ def test_exception_multiplicities(session, monkeypatch, vmode):
 
 @pytest.mark.parametrize("vmode", VMODE)
 @pytest.mark.parametrize("walk", ["lists", "lists-nosplit"])
-def test_split_word_cap(session, monkeypatch, walk, vmode):
+def test_split_word_cap(session, knobs, walk, vmode):
     """Ids above 2^16 (24 id bits): a split-list word holds 8 multiplicity bits, so multiplicities of
     255 and more are read exactly from the combined list."""
-    _vmode(monkeypatch, vmode)
-    _walk(monkeypatch, walk)
+    _vmode(knobs, session, vmode)
+    _walk(knobs, session, walk)
     rng = np.random.default_rng(23)
     n = 70000
     k = 120
@@ -171,3 +169,68 @@ def test_split_word_cap(session, monkeypatch, walk, vmode):
     src = np.concatenate([src, far, [n - 1]])
     dst = np.concatenate([dst, rng.integers(0, k, 2000).astype(np.int64), [0]])
     assert _count(session, n, src, dst) == cpu.triangle_closed_form(n, src, dst)
+
+
+def _mix32(x):
+    """k_tri.hip mix32 (the degree sample's hashed offset), vectorised over uint64."""
+    x = x.astype(np.uint64)
+    x ^= x >> np.uint64(33)
+    x = x * np.uint64(0xFF51AFD7ED558CCD)
+    x ^= x >> np.uint64(33)
+    return (x & np.uint64(0xFFFFFFFF)).astype(np.uint64)
+
+
+@pytest.mark.parametrize("vmode", VMODE)
+@pytest.mark.parametrize("graph_kind", ["rmat12", "random"])
+def test_sampled_degree_order(session, knobs, graph_kind, vmode):
+    """The direct build's degree order estimated from 1 in 32 relationships (config CAPSMI_TRI_DEG_SAMPLE=32,
+    the C4 default above 2^22 relationships) -- any total order gives the same count."""
+    _vmode(knobs, session, vmode)
+    knobs(session, CAPSMI_TRI_DEG_SAMPLE="32")
+    if graph_kind == "rmat12":
+        n = 1 << 12
+        src, dst = cpu.rmat_edges(12, 0, 16 << 12)
+    else:
+        rng = np.random.default_rng(31)
+        n, m = 3000, 200_000
+        src = rng.integers(0, n, m).astype(np.int64)
+        dst = (src + rng.integers(-40, 41, m)) % n  # local neighbourhoods: many triangles
+        src[:2000] = dst[:2000]  # self-loops
+    assert _count(session, n, src, dst) == cpu.triangle_closed_form(n, src, dst)
+
+
+def test_sampled_order_misranks_a_hub(session, knobs):
+    """A hub whose relationships all sit at positions the 1-in-32 degree sample skips: it ranks below its
+    70,000 neighbours (each of which has a sampled relationship), so every one of its edges is oriented out of
+    it -- an out-degree of 70,000 >= 2^16 breaks the sqrt(2m) bound of an exact degree order, the build
+    checks it (k_max_od) and takes the unpacked in-keys and the combined walks.  The count must not change
+    (ADVICE r05).  Padding relationships whose nodes are filtered out fill the rest of the blocks."""
+    knobs(session, CAPSMI_TRI_DEG_SAMPLE="32")
+    k = 70_000
+    hub, w = 0, np.arange(1, k + 1, dtype=np.int64)
+    pad = k + 1  # a node outside the scanned node table
+    n = k + 2
+    blocks = k
+    m = 32 * blocks
+    sampled = np.arange(blocks, dtype=np.uint64) * np.uint64(32) + (_mix32(np.arange(blocks, dtype=np.uint64)) & np.uint64(31))
+    sampled = sampled.astype(np.int64)
+    free = np.ones(m, bool)
+    free[sampled] = False
+    slots = np.nonzero(free)[0]
+    src = np.full(m, pad, np.int64)
+    dst = np.full(m, pad, np.int64)
+    # sampled slots: w_i -> w_{i+3} (every neighbour gets a sampled relationship)
+    src[sampled], dst[sampled] = w, w[(np.arange(k) + 3) % k]
+    # unsampled slots: hub -> w_i, w_i -> w_{i+1}, and w_j -> hub for every 13th j (directed triangles through the hub)
+    back = w[::13]
+    extra_s = np.concatenate([np.full(k, hub), w, back])
+    extra_d = np.concatenate([w, w[(np.arange(k) + 1) % k], np.full(len(back), hub)])
+    assert len(extra_s) <= len(slots)
+    src[slots[:len(extra_s)]], dst[slots[:len(extra_s)]] = extra_s, extra_d
+    assert not np.isin(np.nonzero((src == hub) | (dst == hub))[0], sampled).any()
+    mask = np.ones(n, bool)
+    mask[pad] = False
+    keep = mask[src] & mask[dst]
+    want = cpu.triangle_closed_form(n, src[keep], dst[keep])
+    assert want > 0
+    assert _count(session, n, src, dst, mask) == want

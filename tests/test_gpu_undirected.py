@@ -111,14 +111,14 @@ def test_route_miss_counter_and_unrouted_guard(session):
 
 @pytest.mark.parametrize("scale", [16, 20])
 @pytest.mark.parametrize("full_form", ["1", "0"])
-def test_undirected_two_hop_vs_fixture(session, scale, full_form, monkeypatch):
+def test_undirected_two_hop_vs_fixture(session, scale, full_form, knobs):
     """count(*) through the two-sided record partition with both arcs (k_count.hip k_rec_part<true>; with every
     node filter full, its full-filter form unless CAPSMI_REC_FULL=0), and the atomic form (CAPSMI_COUNT=atomic,
     A/B), and count(DISTINCT c), against the committed closed-form fixtures (tests/golden/rmat_full.json
     c3u_s16 / c3u_s20; oracle/closed.c orc_two_hop_undirected_closed_form)."""
     import json
     import os
-    monkeypatch.setenv("CAPSMI_REC_FULL", full_form)
+    knobs(session, CAPSMI_REC_FULL=full_form)
     from capsmi.planner import EntityTable, Planner, ScanGraph, result_rows
     from capsmi import graph
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -134,12 +134,9 @@ def test_undirected_two_hop_vs_fixture(session, scale, full_form, monkeypatch):
     t, outs = Planner(sg).run(q)
     got = result_rows(t, outs, session.dictionary)[0]
     assert (got["n"], got["dc"]) == (fx["count_star"], fx["count_distinct_c"])
-    os.environ["CAPSMI_COUNT"] = "atomic"
-    try:
+    with session.configured(CAPSMI_COUNT="atomic"):
         t, outs = Planner(sg).run({"clauses": q["clauses"], "return": {"items": [["n", ["count*"]]]}})
         assert result_rows(t, outs, session.dictionary)[0]["n"] == fx["count_star"]
-    finally:
-        del os.environ["CAPSMI_COUNT"]
 
 
 @pytest.mark.parametrize("mode", ["layout", "stream"])
@@ -164,10 +161,7 @@ def test_undirected_distinct_layout_and_stream_forms(session, mode):
     src, dst = cpu.rmat_edges(scale, 0, 16 << scale)
     person = cpu.person_mask(n).astype(np.uint8)
     every = np.ones(n, np.uint8)
-    prev = os.environ.get("CAPSMI_UND")
-    if mode == "stream":
-        os.environ["CAPSMI_UND"] = "stream"
-    try:
+    with session.configured(CAPSMI_UND="stream" if mode == "stream" else "part"):
         for pattern, (am, bm, cm) in (("(a:Person)-[:R]-(b)-[:R]-(c:Person)", (person, every, person)),
                                       ("(a)-[:R]-(b:Person)-[:R]-(c)", (every, person, every)),
                                       ("(a:Person)-[:R]-(b)-[:R]-(c)", (person, every, every))):
@@ -180,8 +174,3 @@ def test_undirected_distinct_layout_and_stream_forms(session, mode):
             _, dc = cpu.two_hop_undirected_closed_form(n, src, dst, am, bm, cm)
             _, da = cpu.two_hop_undirected_closed_form(n, src, dst, cm, bm, am)
             assert (got["dc"], got["da"]) == (dc, da), (pattern, mode)
-    finally:
-        if prev is None:
-            os.environ.pop("CAPSMI_UND", None)
-        else:
-            os.environ["CAPSMI_UND"] = prev

@@ -191,10 +191,10 @@ def test_sliced_path_top_ids(session):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sublog", [1, 3])
-def test_filter_sub_regions(session, monkeypatch, sublog):
+def test_filter_sub_regions(session, knobs, sublog):
     """Several filter regions per slice (one k_vl_bset pass each, partials ORed by k_vl_bmerge),
     forced through CAPSMI_VL_SUBLOG: same answer."""
-    monkeypatch.setenv("CAPSMI_VL_SUBLOG", str(sublog))
+    knobs(session, CAPSMI_VL_SUBLOG=str(sublog))
     test_many_source_slices(session, 0)
 
 
@@ -275,13 +275,13 @@ def test_pack_misfit_hub(session):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("f2", ["0", "1"])
-def test_dense_reciprocal_candidates(session, monkeypatch, f2):
+def test_dense_reciprocal_candidates(session, knobs, f2):
     """Every relationship of a complete digraph (plus doubled pairs) has its reverse: every one is a
     reverse-count candidate, so a wave's step fills its LDS candidate buffer past capacity and the
     overflow goes straight to the list (k_vl_deg, list form); CAPSMI_VL_F2=1 runs the F2-filter form.
     Checked against the closed form (oracle/closed.c, pinned to enumeration by test_oracle_pins.py)."""
     from capsmi import ColumnData, I64, graph
-    monkeypatch.setenv("CAPSMI_VL_F2", f2)
+    knobs(session, CAPSMI_VL_F2=f2)
     n = 180
     a, b = np.nonzero(~np.eye(n, dtype=bool))
     extra = np.arange(0, len(a), 7)  # doubled pairs: multiplicities 2

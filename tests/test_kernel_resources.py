@@ -44,14 +44,10 @@ def test_item_kernels_keep_two_items_per_cu(tmp_path):
     assert items, "no k_tri_big_items kernels in the object"
     assert any("k_tri_items_sp" in k for k in items), "no split-list item kernels in the object"
     for name, (sg, vg) in items.items():
-        m = re.search(r"k_tri_big_itemsILb(\d)ELi(\d+)ELb(\d)ELi(\d+)E", name)
-        if m:
-            lists, unroll, vm, block = (int(x) for x in m.groups())
-        else:  # k_tri_items_sp<U, VM, B>: list walks
-            m = re.search(r"k_tri_items_spILi(\d+)ELb(\d)ELi(\d+)E", name)
-            lists, (unroll, vm, block) = 1, (int(x) for x in m.groups())
-        if not lists or unroll > 8:  # A/B variants (flat walk, 16 loads in flight)
-            continue
+        # k_tri_big_items<U, VM, B> / k_tri_items_sp<U, VM, B, ...>: the list walks (every instantiation is a
+        # product path since round 6 removed the flat walk and the 8 / 16-load A/B variants)
+        m = re.search(r"k_tri_(?:big_items|items_sp)ILi(\d+)ELb(\d)ELi(\d+)E", name)
+        assert m, name
         granule = -(-sg // 16) * 16 + 16
         waves = 800 // granule
         need = 8  # 2 x 1024 lanes or 4 x 512 lanes per CU = 8 waves per SIMD
