@@ -236,6 +236,7 @@ def shard_diagnostic(args):
     in_all = torch.zeros(n, dtype=torch.int32, device="cuda")  # stands in for the gathered in-degrees (timing)
     cnt_dev = torch.zeros(1, dtype=torch.int64, device="cuda")
     per_rank, per_rank_count, rows = [], [], []
+    kernel_ms = {}  # rank 0's shard, per launch
     for r in range(N):
         by_src = args.rels_by == "source"
         rels = graph.rmat_rels(sess, scale, 0, m_total, graph.RMAT_GRAPH500, 42,
@@ -258,6 +259,18 @@ def shard_diagnostic(args):
             step()
         torch.cuda.synchronize()
         per_rank.append((time.perf_counter() - t0) / args.steps * 1e3)
+        if r == 0:  # per-kernel times of one shard (separate, profiled steps: the timed ones stay unprofiled)
+            import ctypes
+            from capsmi import _lib
+            _lib.call("capsmi_session_set_profiling", sess.handle, 1)
+            for _ in range(args.steps):
+                step()
+            for k in KERNELS:
+                c, ms = ctypes.c_int64(), ctypes.c_double()
+                _lib.call("capsmi_session_kernel_time", sess.handle, k.encode(), ctypes.byref(c), ctypes.byref(ms))
+                if c.value:
+                    kernel_ms[k] = ms.value / c.value
+            _lib.call("capsmi_session_set_profiling", sess.handle, 0)
 
         def step_count():  # count(*) shard: partition + IN walk + owned fold, OUT walk (no gather / all-reduce)
             p = graph.NodeBitmap(sess, 0, n).add_scan(persons, "id")
@@ -280,7 +293,8 @@ def shard_diagnostic(args):
                                     "no exchange",
                       "scale": scale, "per_rank_ms": per_rank, "max_ms": max(per_rank), "mean_ms": mean,
                       "imbalance_max_over_mean": max(per_rank) / mean, "rels_per_rank": rows,
-                      "count_star_per_rank_ms": per_rank_count, "count_star_max_ms": max(per_rank_count)}),
+                      "count_star_per_rank_ms": per_rank_count, "count_star_max_ms": max(per_rank_count),
+                      "rank0_kernel_ms": kernel_ms}),
           flush=True)
     sess.close()
 

@@ -835,6 +835,23 @@ __global__ void __launch_bounds__(kBlock) k_hop_2d(PairOut pairs, const int64_t*
     }
     int cur_j = -1;
     const bool can_pull = !SRC_FULL && L.sbits == kSliceBits;
+    // The source slice a cell pulls is loaded into registers while the cell before it streams (this lane's
+    // kSliceWords / kBlock words, 16-byte loads issued ahead of the cell's pair loads), so the pull no longer
+    // waits for its own load latency behind a barrier; `nxt_i` = the slice held (-1: none).
+    static_assert(kSliceWords % (4 * kBlock) == 0, "pull prefetch: whole 16-byte words per lane");
+    constexpr int kPw = kSliceWords / (4 * kBlock);
+    uint4 nsl[kPw];
+    int nxt_i = -1;
+    auto prefetch_slice = [&](int i2) {
+        const uint4* src4 = reinterpret_cast<const uint4*>(sb.w + (int64_t)i2 * kSliceWords);
+        const int64_t lim4 = (gwords - (int64_t)i2 * kSliceWords) / 4;  // whole uint4 words inside the bitmap
+#pragma unroll
+        for (int k = 0; k < kPw; ++k) {
+            const int64_t x = (int64_t)k * kBlock + threadIdx.x;
+            nsl[k] = x < lim4 ? src4[x] : make_uint4(0u, 0u, 0u, 0u);
+        }
+        nxt_i = i2;
+    };
     while (e0 < e1) {
         while (coff[c + 1] <= e0) ++c;
         const int j = c / L.ns, i = c % L.ns;
@@ -851,7 +868,18 @@ __global__ void __launch_bounds__(kBlock) k_hop_2d(PairOut pairs, const int64_t*
         const bool pull = can_pull && ce - e0 >= kLoadMin;
         if (pull) {
             const int64_t w0 = (int64_t)i * kSliceWords;
-            for (int k = threadIdx.x; k < kSliceWords; k += kBlock) sl[k] = w0 + k < gwords ? sb.w[w0 + k] : 0u;
+            if (nxt_i == i && (gwords - w0) % 4 == 0) {
+                uint4* sl4 = reinterpret_cast<uint4*>(sl);
+#pragma unroll
+                for (int k = 0; k < kPw; ++k) sl4[k * kBlock + threadIdx.x] = nsl[k];
+            } else {
+                for (int k = threadIdx.x; k < kSliceWords; k += kBlock) sl[k] = w0 + k < gwords ? sb.w[w0 + k] : 0u;
+            }
+            nxt_i = -1;
+        }
+        if (can_pull && ce == coff[c + 1] && ce < e1 && ((uintptr_t)sb.w & 15) == 0) {  // the next cell, if it pulls
+            const int c2 = c + 1;
+            if (min(e1, coff[c2 + 1]) - ce >= kLoadMin) prefetch_slice(c2 % L.ns);
         }
         __syncthreads();
         const uint32_t tbase = (uint32_t)j << L.tbits, sbase = (uint32_t)i << L.sbits;  // pull: sbits = kSliceBits

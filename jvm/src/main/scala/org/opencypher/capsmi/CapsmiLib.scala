@@ -170,6 +170,9 @@ trait CapsmiLib extends Library {
   def capsmi_session_set_stream(s: Pointer, hipStream: Pointer): Int
   def capsmi_session_use_stream(s: Pointer, hipStream: Pointer): Int
   def capsmi_session_sync(s: Pointer): Int
+  // session configuration (CAPSMI_* knobs; read from the environment once, at create): name, value (null = default)
+  def capsmi_session_set_config(s: Pointer, name: String, value: String): Int
+  def capsmi_config_check(name: String, value: String): Int
   def capsmi_session_set_profiling(s: Pointer, enabled: Int): Int
   def capsmi_session_kernel_time(s: Pointer, name: String, launches: LongByReference, totalMs: DoubleByReference): Int
   def capsmi_session_kernel_bytes(s: Pointer, name: String, bytes: DoubleByReference): Int
