@@ -252,8 +252,9 @@ struct capsmi_table {
     std::shared_ptr<capsmi::DenseIds> dense;
     capsmi::Column did, dsrc, ddst;
     std::shared_ptr<const capsmi::Shard> shard;  // this rank's shard of a distributed graph
-    // BY_SOURCE relationship shards: the relationships of other ranks' sources into this rank's owned ids
-    // (dense source / target, exchanged at capsmi_graph_distribute)
+    // the complement of a relationship shard (dense source / target, exchanged at capsmi_graph_distribute):
+    // BY_SOURCE, the relationships of other ranks' sources into this rank's owned ids; BY_TARGET, those of
+    // this rank's owned sources into other ranks' ids
     capsmi::Column in_src, in_dst;
     int64_t in_rows = 0;
     bool partitioned = false;  // rows are this rank's partition of a distributed result

@@ -67,11 +67,13 @@ __global__ void k_dest_counts(const uint64_t* __restrict__ dest, int64_t n, int 
 }
 
 // (source, target) rows whose target another rank owns -> one word source << 32 | target to that rank
+// the complement exchange of a relationship shard: each row to the owner of its `key` end (dst for BY_SOURCE
+// shards: their in-relationships; src for BY_TARGET shards: their out-relationships), 0xFF when that is this rank
 __global__ void k_in_words(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, int64_t span,
-                           int rank, int world, uint64_t* __restrict__ dest, uint64_t* __restrict__ w) {
+                           int rank, int world, int key_src, uint64_t* __restrict__ dest, uint64_t* __restrict__ w) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t t = dst[i];
-        int q = (int)(t / span);
+        int q = (int)((key_src ? src[i] : t) / span);
         q = q < world ? q : world - 1;
         dest[i] = q == rank ? 0xFF : (uint64_t)q;
         w[i] = ((uint64_t)src[i] << 32) | (uint64_t)t;
@@ -820,15 +822,19 @@ capsmi_status capsmi_graph_distribute(capsmi_session* s, int64_t id_lo, int64_t 
         p.t->layouts.clear();
         p.t->in_src = p.t->in_dst = Column();
         p.t->in_rows = 0;
-        // BY_SOURCE: the relationships into this rank's owned ids from other ranks' sources, by one
-        // exchange (every rank takes part, in table order), kept with the shard
-        if (sh->kind == 2 && rel_mode == CAPSMI_RELS_BY_SOURCE && (s->world > 1 || s->coll)) {
+        // The complement shard, by one exchange (every rank takes part, in table order), kept with the shard:
+        // BY_SOURCE, the relationships into this rank's owned ids from other ranks' sources; BY_TARGET, the
+        // relationships out of its owned ids into other ranks' targets.  With it a rank holds every
+        // relationship incident to an owned id exactly once (the owned-middle routes: count(*), undirected,
+        // var-length)
+        if (sh->kind == 2 && (s->world > 1 || s->coll)) {
             const int64_t m = p.t->nrows;
             Buf dest = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s), w = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s);
             if (m > 0)
                 hipLaunchKernelGGL(k_in_words, dim3(grid_for(m)), dim3(256), 0, s->stream, P<int64_t>(p.a.data),
                                    P<int64_t>(p.b.data), m, 32 * sc.slice_words, s->rank,
-                                   s->world, P<uint64_t>(dest), P<uint64_t>(w));
+                                   s->world, rel_mode == CAPSMI_RELS_BY_TARGET ? 1 : 0, P<uint64_t>(dest),
+                                   P<uint64_t>(w));
             HIP_CHECK(hipGetLastError());
             int64_t nin = 0;
             Buf got = exchange_words(s, P<uint64_t>(dest), P<uint64_t>(w), m, &nin);

@@ -1110,14 +1110,15 @@ int64_t dist_two_hop_count(capsmi_session* s, int32_t nt, capsmi_table* const* v
 
 std::unique_ptr<capsmi_bitmap> owned_mask(capsmi_session* s, const capsmi_bitmap* b);
 
-// count(*) over BY_SOURCE shards without moving any per-id array.  A rank's out-shard
-// (sources owned) and its in-shard (the relationships from other ranks' sources into owned ids, exchanged once
-// at capsmi_graph_distribute) hold every relationship incident to an owned id exactly once, so for an owned
-// middle b both inA(b) and outC(b) are complete here: count(*) = sum over the ranks of
-// sum_{owned b} b_ok(b) inA(b) outC(b) - loops(b), one record-partition count over the union with b restricted
-// to owned ids and one 8-byte all-reduce -- per-rank bytes received fall with N (the BY_TARGET form
-// all-gathers 4 B x every id's in-degree).  The walk's orientation picks which in-shard column is the source.
-int64_t dist_two_hop_count_src(capsmi_session* s, const Path& P, const RelViews& v0, const capsmi_bitmap* a,
+// count(*) over distributed shards without moving any per-id array.  A rank's shard and
+// its complement (BY_SOURCE: the relationships from other ranks' sources into owned ids; BY_TARGET: those from
+// owned sources into other ranks' ids; exchanged once at capsmi_graph_distribute) hold every relationship
+// incident to an owned id exactly once, so for an owned middle b both inA(b) and outC(b) are complete here:
+// count(*) = sum over the ranks of sum_{owned b} b_ok(b) inA(b) outC(b) - loops(b), one record-partition
+// count over the union with b restricted to owned ids and one 8-byte all-reduce -- per-rank bytes received
+// fall with N (the earlier BY_TARGET form all-gathered 4 B x every id's in-degree, 256 MiB at 2^26 ids).
+// The walk's orientation picks which complement column is the source.
+int64_t dist_two_hop_count_owned(capsmi_session* s, const Path& P, const RelViews& v0, const capsmi_bitmap* a,
                                const capsmi_bitmap* b, const capsmi_bitmap* c) {
     REQUIRE(!a->any_dup && !b->any_dup && !c->any_dup, CAPSMI_ERR_UNSUPPORTED,
             "closed-form count(*) needs each node id in one scanned row");
@@ -1235,11 +1236,11 @@ bool fused_counts(capsmi_session* s, const Path& P, const std::vector<int>& kind
                 lay = it->second.get();
             }
             if (g_dist.on && k == A_COUNT) {
-                // BY_TARGET: every relationship into an owned id, the owned in-degrees all-gathered; BY_SOURCE:
-                // the out- and in-shards of the owned middles, no per-id exchange (dense ids: the in-shard's)
-                x = by_tgt ? dist_two_hop_count(s, (int32_t)nt, v0.t.data(), a, b, cc)
-                    : g_dense ? dist_two_hop_count_src(s, P, v0, a, b, cc)
-                              : dist_two_hop_count(s, (int32_t)nt, rv.t.data(), cc, b, a);
+                // the shard and its complement around the owned middles, no per-id exchange (dense ids: the
+                // complement's); without dense ids the all-gather form (BY_TARGET forwards, BY_SOURCE reversed)
+                x = g_dense ? dist_two_hop_count_owned(s, P, v0, a, b, cc)
+                    : by_tgt ? dist_two_hop_count(s, (int32_t)nt, v0.t.data(), a, b, cc)
+                             : dist_two_hop_count(s, (int32_t)nt, rv.t.data(), cc, b, a);
             } else if (g_dist.on) {
                 // the walk's relationships arrive by their end's owner (BY_TARGET forwards, BY_SOURCE reversed):
                 // the all-gather form; by their start's owner: the OR-reduce form
