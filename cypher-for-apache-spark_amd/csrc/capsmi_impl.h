@@ -352,6 +352,9 @@ void collective(capsmi_session* s, int op, const void* send, void* recv, int64_t
 // calls of the host collective move at most coll_chunk() elements (CAPSMI_COLL_CHUNK); collective() and
 // collective_a2av() split larger ones
 int64_t coll_chunk(const capsmi_session* s);
+// hipFuncAttributeMaxDynamicSharedMemorySize of `kernel`, set once per (device, kernel) and raised only when a
+// launch needs more (the attribute call costs host time on every query otherwise; k_part.hip)
+void lds_attr(const void* kernel, size_t bytes);
 // ALL_TO_ALL_V with host count lists (world entries each); max_pair: the largest entry of the whole count
 // matrix (equal on every rank), which fixes the number of rounds
 void collective_a2av(capsmi_session* s, const void* send, const int64_t* send_counts, void* recv,

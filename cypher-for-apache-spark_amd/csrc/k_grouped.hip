@@ -385,8 +385,7 @@ static bool grouped_distinct_sets(capsmi_session* s, const int64_t* S, const int
                            P<int64_t>(off2), P<unsigned int>(loops), P<int64_t>(cnt));
     if (nl) {
         const size_t lds = sizeof(uint32_t) << (kGdRangeBits - 5);
-        HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_gd_large), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)lds));
+        lds_attr(reinterpret_cast<const void*>(k_gd_large), lds);
         hipLaunchKernelGGL(k_gd_large, dim3((unsigned)std::min<int64_t>(nl, 2 * (int64_t)s->num_cus)), dim3(1024), lds, st,
                            P<int64_t>(large), nl, P<uint64_t>(k1), P<int64_t>(off1), P<uint64_t>(k2), P<int64_t>(off2),
                            P<unsigned int>(loops), n, P<int64_t>(cnt));

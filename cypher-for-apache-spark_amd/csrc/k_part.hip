@@ -79,6 +79,10 @@ __global__ void __launch_bounds__(B, MINW) k_scatter_c(const int64_t* __restrict
         misc[0] = 0;
         misc[1] = (uint32_t)(chunk0 + (int64_t)blockIdx.x * chunks_per_block(m, gridDim.x, nb, T));
     }
+    {  // this block's range of the chunk pool: its metadata cleared here (no host fill of the whole array)
+        const int64_t cpb = chunks_per_block(m, gridDim.x, nb, T), c0b = chunk0 + (int64_t)blockIdx.x * cpb;
+        for (int64_t i = threadIdx.x; i < cpb; i += B) cmeta[c0b + i] = 0;
+    }
     const uint64_t range = (uint64_t)(L.hi - L.lo);
     const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
     const int64_t stride = (int64_t)gridDim.x * T;
@@ -324,6 +328,10 @@ __global__ void __launch_bounds__(B, MINW) k_scatter_l(const int64_t* __restrict
         misc[0] = 0;
         misc[1] = (uint32_t)(chunk0 + (int64_t)blockIdx.x * chunks_per_block(m, gridDim.x, nb, T));
     }
+    {  // this block's range of the chunk pool: its metadata cleared here (no host fill of the whole array)
+        const int64_t cpb = chunks_per_block(m, gridDim.x, nb, T), c0b = chunk0 + (int64_t)blockIdx.x * cpb;
+        for (int64_t i = threadIdx.x; i < cpb; i += B) cmeta[c0b + i] = 0;
+    }
     __syncthreads();
     const uint64_t range = (uint64_t)(L.hi - L.lo);
     const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
@@ -461,6 +469,101 @@ __global__ void __launch_bounds__(kChunkBlock) k_chunk_place(const unsigned long
             const uint32_t j = (uint32_t)cmeta[q];
             order[base[j] + atomicAdd(&h[j], 1u)] = (uint32_t)q;
         }
+}
+
+// block exclusive scan of a[0, n) in place (1024 lanes, each a run of consecutive entries); returns the total
+__device__ uint32_t block_scan_inplace(uint32_t* a, int n, uint32_t* wtot) {
+    constexpr int B = kChunkBlock;
+    const int per = (n + B - 1) / B, b0 = (int)threadIdx.x * per, b1 = min(b0 + per, n);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t sum = 0;
+    for (int i = b0; i < b1; ++i) sum += a[i];
+    uint32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wtot[wave] = x;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        uint32_t v = lane < B / 64 ? wtot[lane] : 0u;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(v, o, 64);
+            if (lane >= o) v += y;
+        }
+        if (lane < B / 64) wtot[lane] = v;
+    }
+    __syncthreads();
+    uint32_t pre = x - sum + (wave > 0 ? wtot[wave - 1] : 0u);
+    for (int i = b0; i < b1; ++i) {
+        const uint32_t c = a[i];
+        a[i] = pre;
+        pre += c;
+    }
+    const uint32_t total = wtot[B / 64 - 1];
+    __syncthreads();
+    return total;
+}
+
+// chunk_order in ONE launch for small pools (a rank's shard, C5's partitions): one workgroup counts the used
+// chunks per slice, scans them (jst), places the chunks (order), and splits them into the g2 consumer blocks'
+// segments (kseg -> segbase, ja) -- instead of a fill, two count / place launches, a copy and two scans
+// (≈28 µs of launches and gaps per partition at a C5 shard of 2^22 relationships)
+constexpr int64_t kOrder1Max = 32768;  // chunks; and nt <= kMaxTSlices, g2 <= 4096
+
+__global__ void __launch_bounds__(kChunkBlock) k_chunk_order1(const unsigned long long* __restrict__ cmeta,
+                                                              int64_t nchunks, int nt, int64_t g2,
+                                                              int64_t* __restrict__ jst_out,
+                                                              uint32_t* __restrict__ order,
+                                                              int64_t* __restrict__ segbase, int* __restrict__ ja) {
+    __shared__ uint32_t h[kMaxTSlices + 1];  // counts -> starts
+    __shared__ uint32_t cur[kMaxTSlices];
+    __shared__ uint32_t ks[4096 + 1];        // segments per consumer block -> their first index
+    __shared__ uint32_t wtot[kChunkBlock / 64];
+    for (int i = threadIdx.x; i <= nt; i += kChunkBlock) h[i] = 0;
+    __syncthreads();
+    for (int64_t q = threadIdx.x; q < nchunks; q += kChunkBlock)
+        if (cmeta[q] >> 32) atomicAdd(&h[(uint32_t)cmeta[q]], 1u);
+    __syncthreads();
+    const uint32_t used = block_scan_inplace(h, nt, wtot);
+    if (threadIdx.x == 0) h[nt] = used;
+    __syncthreads();
+    for (int i = threadIdx.x; i <= nt; i += kChunkBlock) {
+        jst_out[i] = (int64_t)h[i];
+        if (i < nt) cur[i] = h[i];
+    }
+    __syncthreads();
+    for (int64_t q = threadIdx.x; q < nchunks; q += kChunkBlock)
+        if (cmeta[q] >> 32) order[atomicAdd(&cur[(uint32_t)cmeta[q]], 1u)] = (uint32_t)q;
+    // the consumers' split (k_seg_count / SegSplit): block w takes chunks [w per, (w + 1) per) of `order`
+    const int64_t per = max((int64_t)1, ((int64_t)used + g2 - 1) / g2);
+    for (int64_t w = threadIdx.x; w < g2; w += kChunkBlock) {
+        const int64_t q0 = w * per, q1 = min(q0 + per, (int64_t)used);
+        uint32_t k = 0;
+        int a = 0;
+        if (q0 < q1) {
+            int lo = 0, hi = nt;  // last j with start <= q0, and with start <= q1 - 1
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if ((int64_t)h[mid] <= q0) lo = mid; else hi = mid;
+            }
+            a = lo;
+            hi = nt;
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if ((int64_t)h[mid] <= q1 - 1) lo = mid; else hi = mid;
+            }
+            k = (uint32_t)(lo - a + 1);
+        }
+        ks[w] = k;
+        ja[w] = a;
+    }
+    __syncthreads();
+    const uint32_t nseg = block_scan_inplace(ks, (int)g2, wtot);
+    for (int64_t w = threadIdx.x; w < g2; w += kChunkBlock) segbase[w] = (int64_t)ks[w];
+    if (threadIdx.x == 0) segbase[g2] = (int64_t)nseg;
 }
 
 // segments per block, ja(w)
@@ -965,21 +1068,24 @@ static part::PairOut pair_out(const RelPart& rp) {
     return o;
 }
 
-template <typename K>
-static void allow_lds(K kernel, size_t bytes) {
+void lds_attr(const void* kernel, size_t bytes) {
     // set once per (device, kernel) and raised only when a launch needs more: the attribute call
     // costs host time on every query otherwise
     static std::mutex mu;
     static std::map<std::pair<int, const void*>, size_t> done;
     int dev = 0;
     HIP_CHECK(hipGetDevice(&dev));
-    const auto key = std::make_pair(dev, reinterpret_cast<const void*>(kernel));
+    const auto key = std::make_pair(dev, kernel);
     std::lock_guard<std::mutex> g(mu);
     auto it = done.find(key);
     if (it != done.end() && it->second >= bytes) return;
-    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)bytes));
+    HIP_CHECK(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
     done[key] = bytes;
+}
+
+template <typename K>
+static void allow_lds(K kernel, size_t bytes) {
+    lds_attr(reinterpret_cast<const void*>(kernel), bytes);
 }
 
 void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms,
@@ -1017,7 +1123,7 @@ void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_
     cp.pool = dev_alloc(sizeof(uint2) * kCh * (size_t)(npool + 1), s);  // + a trash chunk
     cp.meta = dev_alloc(sizeof(unsigned long long) * npool, s);
     cp.chist = dev_alloc(sizeof(uint32_t) * hw * (size_t)npool, s);
-    HIP_CHECK(hipMemsetAsync(P<void>(cp.meta), 0, sizeof(unsigned long long) * npool, st));
+    // (cp.meta: each pass-1 block clears its own range of chunks)
     const size_t lds1l = scatter1l_lds(L.nt, L.ns, kP1Block, kP1Tile);
     const bool lines = lds1l <= (size_t)160 * 1024;
     const size_t lds1 = lines ? lds1l : scatter1_lds(L.nt, L.ns);
@@ -1060,6 +1166,19 @@ void chunk_order(capsmi_session* s, int nt, int64_t pool_chunks, int64_t g2_want
     int64_t* segbase = kseg + g2;      // g2 + 1
     uint32_t* order = reinterpret_cast<uint32_t*>(segbase + g2 + 2);
     int* ja = reinterpret_cast<int*>(order + npool);
+    if (npool <= kOrder1Max && L.nt <= kMaxTSlices && g2 <= 4096) {  // small pools: one launch
+        hipLaunchKernelGGL(k_chunk_order1, dim3(1), dim3(kChunkBlock), 0, st, P<unsigned long long>(cp.meta),
+                           pool_chunks, L.nt, g2, jst, order, segbase, ja);
+        HIP_CHECK(hipGetLastError());
+        cp.pool_chunks = pool_chunks;
+        cp.npool = npool;
+        cp.g2 = g2;
+        cp.jst = jst;
+        cp.segbase = segbase;
+        cp.ja = ja;
+        cp.order = order;
+        return;
+    }
     HIP_CHECK(hipMemsetAsync(jcnt, 0, sizeof(int64_t) * L.nt, st));
     const unsigned cg = (unsigned)((npool + kChunkPer - 1) / kChunkPer);
     hipLaunchKernelGGL(k_chunk_count, dim3(cg), dim3(kChunkBlock), sizeof(uint32_t) * L.nt, st,

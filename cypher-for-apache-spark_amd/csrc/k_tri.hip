@@ -2005,9 +2005,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
 }
 
 namespace {
-void set_lds_attr(const void* k, size_t bytes) {
-    HIP_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-}
+void set_lds_attr(const void* k, size_t bytes) { lds_attr(k, bytes); }
 }  // namespace
 
 // count for vertex share `part` of `nparts` (interleaved center lists); pair/self terms with part 0

@@ -731,7 +731,7 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
         const size_t lds2 = 2 * sizeof(unsigned long long) * kVlIds;
         for (const void* f : {reinterpret_cast<const void*>(k_vl_deg), reinterpret_cast<const void*>(k_vl_w),
                               reinterpret_cast<const void*>(k_vl_t)})
-            HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+            lds_attr(f, lds2);
         Buf ody, bw, hk, hc, f2;
         unsigned int* misfit = nullptr;
         RegionBloom bl{nullptr, 0, 0, 0};
@@ -757,8 +757,7 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
                 Buf part = dev_alloc(rbytes * (((size_t)ct.g2 + L.nt) << sublog), s);
                 const ChunkWalk tw{P<uint2>(ct.pool), P<unsigned long long>(ct.meta), ct.order, ct.jst, ct.segbase,
                                    ct.ja, L.nt};
-                HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_vl_bset),
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)rbytes));
+                lds_attr(reinterpret_cast<const void*>(k_vl_bset), rbytes);
                 hipLaunchKernelGGL(k_vl_bset, dim3((unsigned)ct.g2), dim3(kVlBlock), rbytes, st, tw, bl, P<uint4>(part));
                 hipLaunchKernelGGL(k_vl_bmerge, dim3(grid(s, (int64_t)(rbytes / 16) * nreg)), dim3(256), 0, st, ct.jst,
                                    L.nt, ct.g2, P<uint4>(part), bl);
@@ -963,7 +962,7 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
     const size_t lds2 = 2 * sizeof(unsigned long long) * kVlIds;
     for (const void* f : {reinterpret_cast<const void*>(k_vl_deg), reinterpret_cast<const void*>(k_vl_w),
                           reinterpret_cast<const void*>(k_vl_t)})
-        HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+        lds_attr(f, lds2);
     if (mout > 0) {
         {
             KernelTimer kt(s, "varlen_part");
@@ -1001,8 +1000,7 @@ VarlenShard* varlen_shard_begin(capsmi_session* s, const int64_t* const* srcs, c
             Buf part = dev_alloc(rbytes * ((size_t)ct.g2 + L.nt), s);
             const ChunkWalk tw{P<uint2>(ct.pool), P<unsigned long long>(ct.meta), ct.order, ct.jst, ct.segbase, ct.ja,
                                L.nt};
-            HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_vl_bset),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)rbytes));
+            lds_attr(reinterpret_cast<const void*>(k_vl_bset), rbytes);
             hipLaunchKernelGGL(k_vl_bset, dim3((unsigned)ct.g2), dim3(kVlBlock), rbytes, st, tw, bl, P<uint4>(part));
             hipLaunchKernelGGL(k_vl_bmerge, dim3(grid(s, (int64_t)(rbytes / 16) * L.nt)), dim3(256), 0, st, ct.jst, L.nt,
                                ct.g2, P<uint4>(part), bl);
