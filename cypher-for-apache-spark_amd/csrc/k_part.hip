@@ -24,6 +24,10 @@
 namespace capsmi {
 
 namespace part {
+// Cache policies measured at C3 (round 6, alternating libraries on one box; default policy everywhere else):
+// non-temporal pass-1 loads 5.23 -> 5.50 ms, non-temporal pass-1 stores 5.23 -> 5.28, non-temporal pass-2 chunk
+// loads 3.56 -> 3.60 (hop 2 1.49 -> 1.61), non-temporal pass-2 layout stores 3.56 -> 3.69 with hop 2 1.49 -> 1.36
+// (the step unchanged).  The hops' pair loads stay non-temporal.
 
 // ---- pass 1: int64 (source, target) -> packed pairs in per-workgroup chunks of one target slice ------
 //
@@ -78,10 +82,6 @@ __global__ void __launch_bounds__(B, MINW) k_scatter_c(const int64_t* __restrict
     if (threadIdx.x == 0) {
         misc[0] = 0;
         misc[1] = (uint32_t)(chunk0 + (int64_t)blockIdx.x * chunks_per_block(m, gridDim.x, nb, T));
-    }
-    {  // this block's range of the chunk pool: its metadata cleared here (no host fill of the whole array)
-        const int64_t cpb = chunks_per_block(m, gridDim.x, nb, T), c0b = chunk0 + (int64_t)blockIdx.x * cpb;
-        for (int64_t i = threadIdx.x; i < cpb; i += B) cmeta[c0b + i] = 0;
     }
     const uint64_t range = (uint64_t)(L.hi - L.lo);
     const bool vec = (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
@@ -327,10 +327,6 @@ __global__ void __launch_bounds__(B, MINW) k_scatter_l(const int64_t* __restrict
     if (threadIdx.x == 0) {
         misc[0] = 0;
         misc[1] = (uint32_t)(chunk0 + (int64_t)blockIdx.x * chunks_per_block(m, gridDim.x, nb, T));
-    }
-    {  // this block's range of the chunk pool: its metadata cleared here (no host fill of the whole array)
-        const int64_t cpb = chunks_per_block(m, gridDim.x, nb, T), c0b = chunk0 + (int64_t)blockIdx.x * cpb;
-        for (int64_t i = threadIdx.x; i < cpb; i += B) cmeta[c0b + i] = 0;
     }
     __syncthreads();
     const uint64_t range = (uint64_t)(L.hi - L.lo);
@@ -1123,7 +1119,8 @@ void chunk_partition(capsmi_session* s, const int64_t* const* srcs, const int64_
     cp.pool = dev_alloc(sizeof(uint2) * kCh * (size_t)(npool + 1), s);  // + a trash chunk
     cp.meta = dev_alloc(sizeof(unsigned long long) * npool, s);
     cp.chist = dev_alloc(sizeof(uint32_t) * hw * (size_t)npool, s);
-    // (cp.meta: each pass-1 block clears its own range of chunks)
+    // (clearing each block's metadata range inside pass 1 instead measured 5.25 -> 5.39 ms at C3: the fill stays)
+    HIP_CHECK(hipMemsetAsync(P<void>(cp.meta), 0, sizeof(unsigned long long) * npool, st));
     const size_t lds1l = scatter1l_lds(L.nt, L.ns, kP1Block, kP1Tile);
     const bool lines = lds1l <= (size_t)160 * 1024;
     const size_t lds1 = lines ? lds1l : scatter1_lds(L.nt, L.ns);
