@@ -1,4 +1,4 @@
-"""Generic-join strategy sweep (CAPSMI_JOIN=hash|radix, radix output in partition or probe order): inner joins of random 64-bit keys
+"""Generic-join strategy sweep (session configuration CAPSMI_JOIN=hash|radix): inner joins of random 64-bit keys
 (no dense range, so the direct-address table is out) with 2 payload columns a side, build sizes
 2^22..2^26, probe = 4 x build, ~1 match per probe row.  Prints one JSON line per (size, strategy)."""
 import json
@@ -25,10 +25,8 @@ def main():
         Pt = s.table([ColumnData("pk", I64, pkeys), ColumnData("p1", I64, np.arange(4 * nb)),
                       ColumnData("p2", I64, np.arange(4 * nb) * 5)])
         B.size, Pt.size
-        for mode in ("hash", "radix", "radix:probe"):
-            strategy, _, order = mode.partition(":")
-            os.environ["CAPSMI_JOIN"] = strategy
-            os.environ["CAPSMI_RADIX_ORDER"] = order or "partition"
+        for mode in ("hash", "radix"):
+            s.set_config("CAPSMI_JOIN", mode)
             times = []
             for it in range(4):
                 s.sync()
