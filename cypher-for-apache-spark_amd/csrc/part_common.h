@@ -15,7 +15,8 @@ constexpr int kItems = 8;                        // relationships per lane per t
 constexpr int kSBlock = 1024;                    // scatter workgroups
 constexpr int kTile = kSBlock * kItems;          // relationships per scatter tile (8192)
 constexpr int kCh = kTile;                       // pairs per pass-1 chunk: a tile's run spans <= 2 chunks
-constexpr int kP1Block = 1024;                   // pass-1 workgroup (512 x 2 per CU measured slower)
+constexpr int kP1Block = 1024;                   // pass-1 workgroup (512 x 2 per CU measured slower; 768 lanes
+                                                 // with 134 VGPRs, round 6: pass 1 5.25 -> 5.97 ms at C3)
 constexpr int kP1Tile = kP1Block * kItems;       // pass-1 tile (<= kCh)
 static_assert(kP1Tile <= kCh, "a pass-1 run must span at most two chunks");
 constexpr bool kP1NT = false;                    // pass-1 pool stores non-temporal
