@@ -425,6 +425,9 @@ void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t
 // order, e.g. by the low digits alone; cb(keys) at once when nothing is sorted)
 void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, const std::vector<int>& shifts,
                        int at, const std::function<void(const uint64_t*)>& cb);
+// keys only; an odd number of passes leaves the result in the sort's other buffer, which `keys` then holds
+// (no copy back)
+void radix_sort_keys(capsmi_session* s, Buf& keys, int64_t n, const std::vector<int>& shifts);
 void order_keys(capsmi_session* s, const int64_t* col, const uint8_t* valid, int type, bool desc, bool null_pass,
                 const int64_t* perm, int64_t n, uint64_t* key);
 
@@ -476,6 +479,7 @@ struct TriGraph {
     int ib = 0, cb = 0;
     Buf orig;         // int64 per vertex: relative id of the degree-order id (unused by the count)
     Buf ek, ev, sl;   // undirected keys / payload (pair terms), self-loop counts
+    Buf pair;         // the direct build: the pair terms' sum (u64), added up while the runs are written
     Buf small_u, big_u;  // vertices with out-degree in [2, 64] / above 64
     int64_t nsmall = 0, nbig = 0;
     // Direction choice per oriented edge u -> v at position p of out(u) (out-lists are sorted, and

@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(B) k_scatter(const uint64_t* __restrict__ keys
 
 template <int B, int IT>
 void sort_passes(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, const std::vector<int>& shifts,
-                 int at, const std::function<void(const uint64_t*)>& cb) {
+                 int at, const std::function<void(const uint64_t*)>& cb, Buf* kbuf = nullptr) {
     constexpr int T = B * IT;
     static std::once_flag once;  // the staged tile takes more than 64 KiB of LDS
     std::call_once(once, [] {
@@ -221,7 +221,9 @@ void sort_passes(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, co
         ++passes;
         if (passes == at && cb) cb(ki);
     }
-    if (passes & 1) {
+    if ((passes & 1) && kbuf && !vals) {  // the caller takes the other buffer: no copy back
+        *kbuf = k2;
+    } else if (passes & 1) {
         HIP_CHECK(hipMemcpyAsync(keys, ki, sizeof(uint64_t) * n, hipMemcpyDeviceToDevice, st));
         if (vals) HIP_CHECK(hipMemcpyAsync(vals, vi, sizeof(int64_t) * n, hipMemcpyDeviceToDevice, st));
     }
@@ -252,6 +254,11 @@ void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t
 
 void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, const std::vector<int>& shifts) {
     radix_sort_digits(s, keys, vals, n, shifts, 0, nullptr);
+}
+
+void radix_sort_keys(capsmi_session* s, Buf& keys, int64_t n, const std::vector<int>& shifts) {
+    if (n <= 1 || shifts.empty()) return;
+    sort_passes<512, 8>(s, P<uint64_t>(keys), nullptr, n, shifts, 0, nullptr, &keys);
 }
 
 }  // namespace capsmi

@@ -339,6 +339,219 @@ __global__ void k_pack_or(const int64_t* __restrict__ src, const int64_t* __rest
     }
 }
 
+// ---- the runs of the sorted raw oriented keys (the direct build) ----
+// One pass counts the run heads of every 4096-key tile, a scan places the tiles, one pass writes: the head
+// lane of a run (one pair's relationships; the direction bit at 31 is not sorted) counts the run's keys and
+// direction bits -- inside the tile from LDS, past its end from memory -- and writes the pair's coded
+// oriented key and target word, its exception when a multiplicity reaches the code's all-ones, and its pair
+// term when both directions occur.  Runs longer than kShortRun go to k_or_long (a workgroup per run).  This
+// replaces the head flags and their compaction, k_und_runs, k_orient with the identity order, k_targets and
+// k_pair_terms of the direct build.
+constexpr int kOrB = 256, kOrIt = 16, kOrTile = kOrB * kOrIt;
+constexpr uint64_t kOrMask = ~(1ULL << 31);
+
+struct OrOut {
+    uint64_t* ok;               // coded oriented keys
+    uint32_t* tg;               // their low words (null: written later, after a distributed build's gather)
+    int64_t* ov;                // exact payloads: every one uncoded, the exceptions' when exc is null
+    uint64_t* exc;              // (key, payload) of the exceptions (coded; a distributed build, whose keys move)
+    unsigned long long* nexc;
+    int64_t* longr;             // (run, head index) of the long runs
+    unsigned long long* nlong;
+    const uint32_t* sl;         // self-loop counts in degree-order ids
+    int64_t* pair;              // the pair terms: one partial sum per tile, the long runs' at index ntiles
+};
+
+// the pair (from, to) = km's ids with f relationships from -> to and b to -> from: run r's outputs; returns
+// whether it is an exception (coded) and its key / payload, adds its pair term to acc
+__device__ __forceinline__ bool or_emit(int64_t r, uint64_t km, uint32_t f, uint32_t b, TgCode tc, const OrOut& o,
+                                        unsigned long long& acc, uint64_t& key, uint64_t& pay) {
+    const uint32_t from = (uint32_t)(km >> 32), to = (uint32_t)km;
+    key = ((uint64_t)from << 32) | to;
+    pay = ((uint64_t)f << 32) | b;
+    bool ex = false;
+    if (tc.cb) {
+        const uint32_t cm = tc.cmask();
+        key |= (uint64_t)(min(f, cm) << tc.ib | min(b, cm) << (tc.ib + tc.cb));
+        ex = f >= cm || b >= cm;
+    }
+    if (!tc.cb || (ex && !o.exc)) o.ov[r] = (int64_t)pay;
+    o.ok[r] = key;
+    if (o.tg) o.tg[r] = (uint32_t)key;
+    if (f && b) acc += 3ULL * ((uint64_t)o.sl[from] + o.sl[to]) * f * b;
+    return ex;
+}
+
+__global__ void __launch_bounds__(kOrB) k_or_count(const uint64_t* __restrict__ key, int64_t m, int64_t* __restrict__ cnt) {
+    __shared__ int ws[kOrB / 64];
+    const int64_t base = (int64_t)blockIdx.x * kOrTile;
+    uint64_t k[kOrIt], p[kOrIt];
+#pragma unroll
+    for (int j = 0; j < kOrIt; ++j) {
+        const int64_t i = base + j * kOrB + threadIdx.x;
+        k[j] = i < m ? key[i] : kNone;
+        p[j] = i > 0 && i < m ? key[i - 1] : kNone;
+    }
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < kOrIt; ++j) c += k[j] != kNone && (k[j] & kOrMask) != (p[j] & kOrMask);
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ void __launch_bounds__(kOrB) k_or_write(const uint64_t* __restrict__ key, int64_t m,
+                                                   const int64_t* __restrict__ pre, TgCode tc, OrOut o) {
+    __shared__ uint64_t tk[kOrTile];
+    __shared__ int wc[kOrIt * (kOrB / 64)];  // heads per (item, wave), then their exclusive prefix in key order
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const unsigned long long lt = lane == 0 ? 0ULL : (~0ULL >> (64 - lane));
+    const int64_t base = (int64_t)blockIdx.x * kOrTile;
+    const int nt = (int)min((int64_t)kOrTile, m - base);
+    uint64_t k[kOrIt];
+#pragma unroll
+    for (int j = 0; j < kOrIt; ++j) {
+        const int i = j * kOrB + (int)threadIdx.x;
+        k[j] = i < nt ? key[base + i] : kNone;
+        if (i < nt) tk[i] = k[j];
+    }
+    const uint64_t before = base > 0 ? key[base - 1] : kNone;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kOrIt; ++j) {
+        const int i = j * kOrB + (int)threadIdx.x;
+        const uint64_t p = i > 0 ? tk[i - 1] : before;
+        const unsigned long long hb = __ballot(i < nt && k[j] != kNone && (k[j] & kOrMask) != (p & kOrMask));
+        if (lane == 0) wc[j * (kOrB / 64) + wid] = __popcll(hb);
+    }
+    __syncthreads();
+    if (wid == 0) {  // 64 (item, wave) counts in key order: one wave's scan
+        const int v = wc[lane];
+        int incl = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        wc[lane] = incl - v;
+    }
+    __syncthreads();
+    const int64_t r0 = pre[blockIdx.x];
+    unsigned long long acc = 0;
+    // per item: the key and its head bit again from LDS (no register arrays indexed in a rolled loop); the
+    // head lane counts its run from the next key on (most runs are one relationship: one LDS read)
+#pragma unroll 1
+    for (int j = 0; j < kOrIt; ++j) {
+        const int i = j * kOrB + (int)threadIdx.x;
+        const uint64_t kj = i < nt ? tk[i] : kNone;
+        const uint64_t p = i > 0 ? tk[i - 1] : before;
+        const bool head = i < nt && kj != kNone && (kj & kOrMask) != (p & kOrMask);
+        const unsigned long long hb = __ballot(head);
+        bool ex = false;
+        uint64_t okey = 0, pay = 0;
+        if (head) {
+            const int64_t r = r0 + wc[j * (kOrB / 64) + wid] + __popcll(hb & lt);
+            const uint64_t km = kj & kOrMask;
+            uint32_t len = 1, bk = (uint32_t)(kj >> 31) & 1u;
+            int q = i + 1;
+            bool ended = false;
+            for (; q < nt && len < (uint32_t)kShortRun; ++q) {  // inside the tile
+                const uint64_t x = tk[q];
+                if ((x & kOrMask) != km) {
+                    ended = true;
+                    break;
+                }
+                bk += (uint32_t)(x >> 31) & 1u;
+                ++len;
+            }
+            if (!ended && len < (uint32_t)kShortRun) {  // past the tile end (rare)
+                for (int64_t gi = base + q;; ++gi) {
+                    if (gi >= m) {
+                        ended = true;
+                        break;
+                    }
+                    const uint64_t x = key[gi];
+                    if ((x & kOrMask) != km) {
+                        ended = true;
+                        break;
+                    }
+                    bk += (uint32_t)(x >> 31) & 1u;
+                    if (++len >= (uint32_t)kShortRun) break;
+                }
+            }
+            if (ended) {
+                ex = or_emit(r, km, len - bk, bk, tc, o, acc, okey, pay);
+            } else {
+                const unsigned long long at = atomicAdd(o.nlong, 1ull);
+                o.longr[2 * at] = r;
+                o.longr[2 * at + 1] = base + i;
+            }
+        }
+        if (o.exc) {
+            const unsigned long long eb = __ballot(ex);
+            if (eb) {  // wave-uniform
+                unsigned long long at0 = 0;
+                if (lane == __builtin_ctzll(eb)) at0 = atomicAdd(o.nexc, (unsigned long long)__popcll(eb));
+                at0 = __shfl(at0, __builtin_ctzll(eb), 64);
+                if (ex) {
+                    const unsigned long long at = at0 + __popcll(eb & lt);
+                    o.exc[2 * at] = okey;
+                    o.exc[2 * at + 1] = pay;
+                }
+            }
+        }
+    }
+    // the tile's pair terms: one partial (no same-address atomics; summed by a scan)
+    __shared__ unsigned long long pw[kOrB / 64];
+    for (int s = 32; s > 0; s >>= 1) acc += __shfl_down(acc, s, 64);
+    if (lane == 0) pw[wid] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) o.pair[blockIdx.x] = (int64_t)(pw[0] + pw[1] + pw[2] + pw[3]);
+}
+
+// the long runs (multi-edges between hubs): a workgroup walks each run 256 keys at a time
+__global__ void __launch_bounds__(256) k_or_long(const uint64_t* __restrict__ key, int64_t m, int64_t ntiles, TgCode tc,
+                                                 OrOut o) {
+    __shared__ int stop;
+    __shared__ unsigned int part[4];
+    const int64_t cnt = (int64_t)*o.nlong;
+    for (int64_t q = blockIdx.x; q < cnt; q += gridDim.x) {  // block-uniform
+        const int64_t r = o.longr[2 * q], h = o.longr[2 * q + 1];
+        const uint64_t km = key[h] & kOrMask;
+        uint32_t bk = 0;
+        int64_t len = 0;
+        for (int64_t c0 = h;; c0 += 256) {
+            if (threadIdx.x == 0) stop = 256;
+            __syncthreads();
+            const int64_t i = c0 + threadIdx.x;
+            const uint64_t x = i < m ? key[i] : kNone;
+            if ((x & kOrMask) != km) atomicMin(&stop, (int)threadIdx.x);
+            __syncthreads();
+            const int st = stop;
+            if ((int)threadIdx.x < st) bk += (uint32_t)(x >> 31) & 1u;
+            len += st;
+            __syncthreads();  // stop is reset by the next chunk
+            if (st < 256) break;
+        }
+        for (int s = 32; s > 0; s >>= 1) bk += __shfl_down(bk, s, 64);
+        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = bk;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t b = part[0] + part[1] + part[2] + part[3];
+            unsigned long long acc = 0;
+            uint64_t okey, pay;
+            if (or_emit(r, km, (uint32_t)len - b, b, tc, o, acc, okey, pay) && o.exc) {
+                const unsigned long long at = atomicAdd(o.nexc, 1ull);
+                o.exc[2 * at] = okey;
+                o.exc[2 * at + 1] = pay;
+            }
+            if (acc) atomicAdd(reinterpret_cast<unsigned long long*>(o.pair + ntiles), acc);
+        }
+        __syncthreads();
+    }
+}
+
 // sl in degree-order ids
 __global__ void k_perm_u32(const uint32_t* __restrict__ a, const int64_t* __restrict__ orig, int64_t n,
                            uint32_t* __restrict__ b) {
@@ -1688,35 +1901,41 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         // one sort of the raw oriented keys (the direction bit unsorted at bit 31), runs = the pairs
         ph.reset(new KernelTimer(s, "tri_sort_or"));
         radix_sort_digits(s, P<uint64_t>(key), nullptr, m, od);
-        Buf f = dev_alloc(m > 0 ? m : 1, s), heads;
-        hipLaunchKernelGGL(k_heads, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, ~(1ULL << 31), P<uint8_t>(f));
-        const int64_t nruns = flags_to_indices(s, P<uint8_t>(f), m, heads);
-        f.reset();
-        hipLaunchKernelGGL(k_first_none, dim3(1), dim3(1), 0, st, P<uint64_t>(key), m, nvalid_p);
-        g.ek = dev_alloc(sizeof(uint64_t) * (nruns > 0 ? nruns : 1), s);
-        g.ev = dev_alloc(sizeof(int64_t) * (nruns > 0 ? nruns : 1), s);
-        if (nruns > 0) {  // (from << 32 | to, m(from, to) << 32 | m(to, from)) per pair
-            Buf longr = dev_alloc(sizeof(int64_t) * (m / kShortRun + 1), s);
-            hipLaunchKernelGGL(k_und_runs, dim3(grid(s, nruns)), dim3(256), 0, st, P<uint64_t>(key), P<int64_t>(heads),
-                               nruns, nvalid_p, 0, P<uint64_t>(g.ek), P<int64_t>(g.ev), (uint32_t*)nullptr,
-                               P<int64_t>(longr), nlong);
-            hipLaunchKernelGGL(k_und_long, dim3(4 * s->num_cus), dim3(256), 0, st, P<uint64_t>(key), P<int64_t>(heads),
-                               nruns, nvalid_p, 0, P<int64_t>(longr), nlong, P<int64_t>(g.ev));
+        // the runs: tile head counts, their scan, then every pair's outputs (k_or_write; the fused run passes
+        // replaced head flags + compaction + k_und_runs + k_orient + k_targets + k_pair_terms, 6.1 ms at C4)
+        const int64_t ntl = (m + kOrTile - 1) / kOrTile;
+        int64_t nruns = 0;
+        Buf pre = dev_alloc(sizeof(int64_t) * (ntl + 1), s);
+        if (ntl > 0) {
+            Buf cnt = dev_alloc(sizeof(int64_t) * ntl, s);
+            hipLaunchKernelGGL(k_or_count, dim3((unsigned)ntl), dim3(kOrB), 0, st, P<uint64_t>(key), m, P<int64_t>(cnt));
             HIP_CHECK(hipGetLastError());
+            exclusive_scan_i64(P<int64_t>(cnt), P<int64_t>(pre), ntl, s);
+            nruns = read_scalar(s, P<int64_t>(pre) + ntl);
         }
-        key.reset();
-        heads.reset();
-        g.nek = nruns;
-        // coded keys (already oriented and sorted: k_orient with the identity order) and the exceptions
-        // (a fused three-pass run detection -- tile counts, heads' starts, differences -- measured 1.4 ms slower)
         g.ok = dev_alloc(sizeof(uint64_t) * (nruns > 0 ? nruns : 1), s);
         g.ov = dev_alloc(sizeof(int64_t) * (nruns > 0 ? nruns : 1), s);
-        exc = dev_alloc(sizeof(uint64_t) * 2 * (nruns > 0 ? nruns : 1), s);
-        HIP_CHECK(hipMemsetAsync(P<void>(nv), 0, sizeof(int64_t) + sizeof(unsigned long long), st));  // nlong: nexc
-        if (nruns > 0)
-            hipLaunchKernelGGL(k_orient, dim3(grid(s, nruns)), dim3(256), 0, st, P<uint64_t>(g.ek), P<int64_t>(g.ev), nruns,
-                               (const uint32_t*)nullptr, tc, P<uint64_t>(g.ok), P<int64_t>(g.ov), P<uint64_t>(exc), nlong);
-        HIP_CHECK(hipGetLastError());
+        if (!dd) g.tg = dev_alloc(sizeof(uint32_t) * (nruns > 0 ? nruns : 1), s);
+        exc = dev_alloc(sizeof(uint64_t) * 2 * (dd && nruns > 0 ? nruns : 1), s);
+        g.pair = dev_alloc(sizeof(int64_t), s);
+        HIP_CHECK(hipMemsetAsync(P<void>(g.pair), 0, sizeof(int64_t), st));
+        HIP_CHECK(hipMemsetAsync(P<void>(nv), 0, sizeof(int64_t) + sizeof(unsigned long long), st));  // nexc, nlong
+        if (nruns > 0) {
+            Buf longr = dev_alloc(sizeof(int64_t) * 2 * (m / kShortRun + 1), s);
+            Buf pp = dev_alloc(sizeof(int64_t) * (ntl + 1), s), ps = dev_alloc(sizeof(int64_t) * (ntl + 2), s);
+            HIP_CHECK(hipMemsetAsync(P<int64_t>(pp) + ntl, 0, sizeof(int64_t), st));
+            // one device: the exceptions' payloads go straight to ov (the keys stay where they are written)
+            OrOut o{P<uint64_t>(g.ok), P<uint32_t>(g.tg), P<int64_t>(g.ov), dd ? P<uint64_t>(exc) : nullptr, nlong,
+                    P<int64_t>(longr), reinterpret_cast<unsigned long long*>(nvalid_p), P<uint32_t>(g.sl), P<int64_t>(pp)};
+            hipLaunchKernelGGL(k_or_write, dim3((unsigned)ntl), dim3(kOrB), 0, st, P<uint64_t>(key), m, P<int64_t>(pre),
+                               tc, o);
+            hipLaunchKernelGGL(k_or_long, dim3(4 * s->num_cus), dim3(256), 0, st, P<uint64_t>(key), m, ntl, tc, o);
+            HIP_CHECK(hipGetLastError());
+            exclusive_scan_i64(P<int64_t>(pp), P<int64_t>(ps), ntl + 1, s);
+            HIP_CHECK(hipMemcpyAsync(P<void>(g.pair), P<int64_t>(ps) + ntl + 1, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+        }
+        key.reset();
+        g.nek = 0;  // the pair terms are in g.pair
         ne = nruns;
         ph.reset();
         if (dd) {  // the ranges in rank order (sorted), every rank's exceptions
@@ -1878,9 +2097,11 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     exc.reset();
     g.off = dev_alloc(sizeof(int64_t) * (n + 1), s);
     hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, n, 32, P<int64_t>(g.off));
-    g.tg = dev_alloc(sizeof(uint32_t) * (ne > 0 ? ne : 1), s);
-    if (ne > 0)
-        hipLaunchKernelGGL(k_targets, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, P<uint32_t>(g.tg));
+    if (!g.tg) {  // (the direct build on one device wrote them with the keys)
+        g.tg = dev_alloc(sizeof(uint32_t) * (ne > 0 ? ne : 1), s);
+        if (ne > 0)
+            hipLaunchKernelGGL(k_targets, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, P<uint32_t>(g.tg));
+    }
     // packed in-keys (key-only sort) when ids and positions fit: od(u) <= sqrt(2m) under a degree
     // order (every out-neighbour has at least u's degree), so m < 2^31 relationships bound it by 2^16
     bool packed = g.ib <= 24 && m_all < (int64_t(1) << 31);
@@ -1945,7 +2166,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
                 hipLaunchKernelGGL(k_swap_keys_sel, dim3(grid(s, nsel)), dim3(256), 0, st, P<uint64_t>(g.ok),
                                    P<int64_t>(g.off), P<int64_t>(sel), nsel, tc, P<uint64_t>(ik));
             sel.reset();
-            radix_sort_digits(s, P<uint64_t>(ik), nullptr, nsel, g.split ? tds : td);
+            radix_sort_keys(s, ik, nsel, g.split ? tds : td);
             g.ioff = dev_alloc(sizeof(int64_t) * (n + 1), s);
             hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), nsel, n,
                                g.split ? 40 : tsh, P<int64_t>(g.ioff));
@@ -1971,7 +2192,8 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
                 hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off), ne,
                                    tc, P<uint64_t>(ik), packed ? nullptr : P<int64_t>(iv));
             rk.reset();
-            radix_sort_digits(s, P<uint64_t>(ik), packed || g.split ? nullptr : P<int64_t>(iv), ne, g.split ? tds : td);
+            if (packed || g.split) radix_sort_keys(s, ik, ne, g.split ? tds : td);  // (3 passes: no copy back)
+            else radix_sort_digits(s, P<uint64_t>(ik), P<int64_t>(iv), ne, td);
             g.ioff = dev_alloc(sizeof(int64_t) * (n + 1), s);
             hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), ne, n,
                                g.split ? 40 : tsh, P<int64_t>(g.ioff));
@@ -2096,6 +2318,9 @@ uint64_t tri_count(capsmi_session* s, const TriGraph& g, int part, int nparts) {
     }
     // pair terms over this graph's undirected edges (a distributed build's ek holds this rank's pairs, so
     // every part adds its own), self terms once
+    if ((part == 0 || g.dist) && g.pair)  // the direct build's sum (a distributed build's: this rank's pairs)
+        HIP_CHECK(hipMemcpyAsync(P<unsigned long long>(out) + 1, P<void>(g.pair), sizeof(unsigned long long),
+                                 hipMemcpyDeviceToDevice, st));
     if ((part == 0 || g.dist) && g.nek > 0)
         hipLaunchKernelGGL(k_pair_terms, dim3(grid(s, g.nek)), dim3(256), 0, st, P<uint64_t>(g.ek), P<int64_t>(g.ev),
                            g.nek, P<uint32_t>(g.sl), P<unsigned long long>(out) + 1);
