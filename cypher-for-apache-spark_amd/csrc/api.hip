@@ -595,6 +595,7 @@ capsmi_status capsmi_session_create(int32_t device, capsmi_session** out) {
     HIP_CHECK(hipGetDeviceProperties(&prop, device));
     s->num_cus = prop.multiProcessorCount;
     HIP_CHECK(hipHostMalloc((void**)&s->pinned, 64, hipHostMallocDefault));
+    HIP_CHECK(hipEventCreateWithFlags(&s->ev_read, hipEventDisableTiming));
     hipMemPool_t pool;
     if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
         // keep freed pool memory mapped (no unmap / remap per query); CAPSMI_POOL_KEEP_BYTES caps what the
@@ -622,6 +623,7 @@ capsmi_status capsmi_session_destroy(capsmi_session* s) {
     }
     for (hipEvent_t e : s->ev_pool) (void)hipEventDestroy(e);
     (void)hipHostFree(s->pinned);
+    if (s->ev_read) (void)hipEventDestroy(s->ev_read);
     (void)hipStreamDestroy(s->own_stream);
     delete s;
     API_END

@@ -172,8 +172,9 @@ struct capsmi_session {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;  // current (own or external)
     int num_cus = 256;
-    // small pinned staging buffer for scalar read-backs
+    // small pinned staging buffer for scalar read-backs ([0]: read_scalar, [1]: read_scalar_async)
     int64_t* pinned = nullptr;
+    hipEvent_t ev_read = nullptr;  // read_scalar_async's copy done
     // per-kernel event timing (capsmi_session_set_profiling)
     bool prof = false;
     struct Pending {
@@ -296,6 +297,10 @@ int64_t flags_to_rows(capsmi_session* s, const uint8_t* flags, int64_t n, const 
 void gather_col(const int64_t* src, const uint8_t* src_valid, const int64_t* idx, int64_t n,
                 int64_t* dst, uint8_t* dst_valid, hipStream_t st);
 int64_t read_scalar(capsmi_session* s, const int64_t* dev);
+// the same in two halves: the copy is queued now and waited for by read_scalar_wait, so the kernels queued
+// in between keep the device busy while the host waits (one outstanding read per session)
+void read_scalar_async(capsmi_session* s, const int64_t* dev);
+int64_t read_scalar_wait(capsmi_session* s);
 void invert_u8(const uint8_t* a, uint8_t* b, int64_t n, hipStream_t st);
 void add_i64(int64_t* p, int64_t v, int64_t n, hipStream_t st);
 void i64_to_f64(const int64_t* a, int64_t* b, int64_t n, hipStream_t st);

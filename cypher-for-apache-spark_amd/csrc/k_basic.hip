@@ -223,6 +223,16 @@ int64_t read_scalar(capsmi_session* s, const int64_t* dev) {
     return s->pinned[0];
 }
 
+void read_scalar_async(capsmi_session* s, const int64_t* dev) {
+    HIP_CHECK(hipMemcpyAsync(s->pinned + 1, dev, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream));
+    HIP_CHECK(hipEventRecord(s->ev_read, s->stream));
+}
+
+int64_t read_scalar_wait(capsmi_session* s) {
+    HIP_CHECK(hipEventSynchronize(s->ev_read));
+    return s->pinned[1];
+}
+
 int64_t flags_to_indices(capsmi_session* s, const uint8_t* flags, int64_t n, Buf& out_idx) {
     hipStream_t st = s->stream;
     if (n == 0) {

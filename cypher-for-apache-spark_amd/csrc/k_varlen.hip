@@ -732,7 +732,7 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
         for (const void* f : {reinterpret_cast<const void*>(k_vl_deg), reinterpret_cast<const void*>(k_vl_w),
                               reinterpret_cast<const void*>(k_vl_t)})
             lds_attr(f, lds2);
-        Buf ody, bw, hk, hc, f2;
+        Buf ody, bw, hk, f2;  // hk: the pair table (keys, counts, overflow word)
         unsigned int* misfit = nullptr;
         RegionBloom bl{nullptr, 0, 0, 0};
         PairHash h{nullptr, nullptr, nullptr, 0};
@@ -785,6 +785,8 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
             }
         }
         if (need3) {
+            // the candidate count (the pair table's size) is read back while the W walk runs
+            read_scalar_async(s, P<int64_t>(cand));
             {
                 KernelTimer kt(s, "varlen_w");
                 Buf od32 = dev_alloc(sizeof(uint32_t) * (size_t)n, s);
@@ -793,15 +795,15 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
                 hipLaunchKernelGGL(k_vl_w, dim3(g), dim3(kVlBlock), lds2 / 2, st, cw, n, P<uint32_t>(od32),
                                    P<unsigned long long>(W));
             }
-            const int64_t nc = read_scalar(s, P<int64_t>(cand));
+            const int64_t nc = read_scalar_wait(s);
             int64_t cap = 1024;
             while (cap < 2 * nc) cap <<= 1;
-            hk = dev_alloc(sizeof(unsigned long long) * cap, s);
-            hc = dev_alloc(sizeof(unsigned int) * (cap + 1), s);
-            HIP_CHECK(hipMemsetAsync(P<void>(hk), 0, sizeof(unsigned long long) * cap, st));
-            HIP_CHECK(hipMemsetAsync(P<void>(hc), 0, sizeof(unsigned int) * (cap + 1), st));
-            h = PairHash{P<unsigned long long>(hk), P<unsigned int>(hc), P<unsigned int>(hc) + cap,
-                         (unsigned long long)(cap - 1)};
+            // keys (cap u64), counts (cap u32) and the overflow word in one zeroed block: one fill
+            const size_t hbytes = (sizeof(unsigned long long) + sizeof(unsigned int)) * cap + 16;
+            hk = dev_alloc(hbytes, s);
+            HIP_CHECK(hipMemsetAsync(P<void>(hk), 0, hbytes, st));
+            unsigned int* hcw = reinterpret_cast<unsigned int*>(P<unsigned long long>(hk) + cap);
+            h = PairHash{P<unsigned long long>(hk), hcw, hcw + cap, (unsigned long long)(cap - 1)};
             if (!use_f2) {
                 KernelTimer kt(s, "varlen_cand");
                 hipLaunchKernelGGL(k_vl_cins, dim3(grid(s, nc)), dim3(256), 0, st, P<unsigned long long>(clist),
