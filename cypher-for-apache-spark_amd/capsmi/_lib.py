@@ -107,6 +107,7 @@ _SIGS = {
     "capsmi_session_set_config": (c_int32, [P, c_char_p, c_char_p]),
     "capsmi_config_check": (c_int32, [c_char_p, c_char_p]),
     "capsmi_session_set_profiling": (c_int32, [P, c_int32]),
+    "capsmi_session_set_profiling_names": (c_int32, [P, c_char_p]),
     "capsmi_session_kernel_time": (c_int32, [P, c_char_p, POINTER(c_int64), POINTER(ctypes.c_double)]),
     "capsmi_session_kernel_bytes": (c_int32, [P, c_char_p, POINTER(ctypes.c_double)]),
     "capsmi_session_set_params": (c_int32, [P, c_int32, P]),

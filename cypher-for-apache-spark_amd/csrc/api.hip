@@ -660,6 +660,19 @@ capsmi_status capsmi_session_set_profiling(capsmi_session* s, int32_t enabled) {
     API_END
 }
 
+capsmi_status capsmi_session_set_profiling_names(capsmi_session* s, const char* names) {
+    API_BEGIN
+    need(s, "session");
+    s->prof_names.clear();
+    for (const char* p = names; p && *p;) {
+        const char* e = strchr(p, ',');
+        const std::string nm = e ? std::string(p, e) : std::string(p);
+        if (!nm.empty()) s->prof_names.insert(nm);
+        p = e ? e + 1 : nullptr;
+    }
+    API_END
+}
+
 capsmi_status capsmi_session_set_params(capsmi_session* s, int32_t nparams, const capsmi_param* params) {
     API_BEGIN
     need(s, "session");

@@ -11,6 +11,7 @@
 #include <atomic>
 #include <cstdint>
 #include <map>
+#include <set>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -177,6 +178,7 @@ struct capsmi_session {
     hipEvent_t ev_read = nullptr;  // read_scalar_async's copy done
     // per-kernel event timing (capsmi_session_set_profiling)
     bool prof = false;
+    std::set<std::string> prof_names;  // the timers that record (empty: all; capsmi_session_set_profiling_names)
     struct Pending {
         std::string name;
         hipEvent_t a, b;
@@ -218,7 +220,7 @@ struct KernelTimer {
     hipEvent_t a = nullptr, b = nullptr;
     // bytes: the launch's algorithmic bytes (inputs read once, outputs written once), if known
     KernelTimer(capsmi_session* s_, const char* n, double bytes = 0) : s(s_), name(n) {
-        if (!s->prof) return;
+        if (!s->prof || (!s->prof_names.empty() && !s->prof_names.count(name))) return;
         a = s->take_event();
         b = s->take_event();
         if (a && b) {

@@ -206,6 +206,10 @@ capsmi_status capsmi_config_check(const char* name, const char* value);
  * While enabled, each hot launch is bracketed by events on the session stream.  Enabling creates a pool of
  * events up front (resolved ones return to it), so timed queries make no event-creation calls. */
 capsmi_status capsmi_session_set_profiling(capsmi_session* s, int32_t enabled);
+/* which timers record while profiling is on: a comma-separated list of kernel names ("part_scatter1,hop2");
+ * NULL or "" = every timer (the default).  Each timed launch adds two event records to the stream (a few
+ * microseconds of device idle each), so a timed run can bracket only the launch it reports. */
+capsmi_status capsmi_session_set_profiling_names(capsmi_session* s, const char* names);
 /* resolve pending events (synchronises) and report totals for kernel `name` ("hop1", "hop2",
  * "expand_filter", "bitmap_add", ...): launches and summed milliseconds; then the counters reset. */
 capsmi_status capsmi_session_kernel_time(capsmi_session* s, const char* name, int64_t* launches, double* total_ms);

@@ -174,6 +174,7 @@ trait CapsmiLib extends Library {
   def capsmi_session_set_config(s: Pointer, name: String, value: String): Int
   def capsmi_config_check(name: String, value: String): Int
   def capsmi_session_set_profiling(s: Pointer, enabled: Int): Int
+  def capsmi_session_set_profiling_names(s: Pointer, names: String): Int
   def capsmi_session_kernel_time(s: Pointer, name: String, launches: LongByReference, totalMs: DoubleByReference): Int
   def capsmi_session_kernel_bytes(s: Pointer, name: String, bytes: DoubleByReference): Int
   def capsmi_session_set_fused(s: Pointer, enabled: Int): Int
