@@ -72,6 +72,30 @@ def test_c3_count_distinct_routed(session, scale):
     assert got == [{"n": rows, "m": rows, "d": dist_a}]
 
 
+def test_profiling_names_select_the_timers(session):
+    """capsmi_session_set_profiling_names: only the named timers record; NULL restores every timer"""
+    import ctypes
+    from capsmi import _lib
+    sg = _graph(session, 10)
+
+    def launches(name):
+        cnt, ms = ctypes.c_int64(), ctypes.c_double()
+        _lib.call("capsmi_session_kernel_time", session.handle, name, ctypes.byref(cnt), ctypes.byref(ms))
+        return cnt.value
+    _lib.call("capsmi_session_set_profiling", session.handle, 1)
+    try:
+        launches(b"hop2"), launches(b"mid_combine")  # earlier tests' totals on the shared session
+        _lib.call("capsmi_session_set_profiling_names", session.handle, b"hop2,no_such_timer")
+        _run(session, sg, C3)
+        assert launches(b"hop2") > 0 and launches(b"mid_combine") == 0
+        _lib.call("capsmi_session_set_profiling_names", session.handle, None)
+        _run(session, sg, C3)
+        assert launches(b"hop2") > 0 and launches(b"mid_combine") > 0
+    finally:
+        _lib.call("capsmi_session_set_profiling", session.handle, 0)
+        _lib.call("capsmi_session_set_profiling_names", session.handle, None)
+
+
 @pytest.mark.parametrize("scale,kind", [(13, "all"), (16, "person")])
 def test_c3_count_star_partitioned(session, scale, kind):
     """count(*) of C3 from the record partition (k_count.hip) equals the per-relationship atomic form and
