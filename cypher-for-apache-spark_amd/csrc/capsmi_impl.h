@@ -433,8 +433,12 @@ void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t
 void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, const std::vector<int>& shifts,
                        int at, const std::function<void(const uint64_t*)>& cb);
 // keys only; an odd number of passes leaves the result in the sort's other buffer, which `keys` then holds
-// (no copy back)
-void radix_sort_keys(capsmi_session* s, Buf& keys, int64_t n, const std::vector<int>& shifts);
+// (no copy back).  Key-only sorts run in tiles of kSortTile keys: a producer that counts its keys' first digit
+// per tile (hist0[d * ntiles + tile], int64, ntiles = ceil(n / kSortTile)) hands that over and the first pass
+// skips its histogram read
+constexpr int kSortTile = 4096;
+void radix_sort_keys(capsmi_session* s, Buf& keys, int64_t n, const std::vector<int>& shifts,
+                     const int64_t* hist0 = nullptr);
 void order_keys(capsmi_session* s, const int64_t* col, const uint8_t* valid, int type, bool desc, bool null_pass,
                 const int64_t* perm, int64_t n, uint64_t* key);
 

@@ -184,7 +184,8 @@ __global__ void __launch_bounds__(B) k_scatter(const uint64_t* __restrict__ keys
 
 template <int B, int IT>
 void sort_passes(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, const std::vector<int>& shifts,
-                 int at, const std::function<void(const uint64_t*)>& cb, Buf* kbuf = nullptr) {
+                 int at, const std::function<void(const uint64_t*)>& cb, Buf* kbuf = nullptr,
+                 const int64_t* hist0 = nullptr) {
     constexpr int T = B * IT;
     static std::once_flag once;  // the staged tile takes more than 64 KiB of LDS
     std::call_once(once, [] {
@@ -206,8 +207,13 @@ void sort_passes(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t n, co
     int passes = 0;
     for (const int shift : shifts) {
         {
-            hipLaunchKernelGGL((k_hist<B, IT>), dim3((unsigned)ntiles), dim3(B), 0, st, ki, n, shift, ntiles, P<int64_t>(hist));
-            exclusive_scan_i64(P<int64_t>(hist), P<int64_t>(offs), 256 * ntiles, s);
+            if (passes == 0 && hist0)  // the first digit's tile counts came with the keys
+                exclusive_scan_i64(hist0, P<int64_t>(offs), 256 * ntiles, s);
+            else {
+                hipLaunchKernelGGL((k_hist<B, IT>), dim3((unsigned)ntiles), dim3(B), 0, st, ki, n, shift, ntiles,
+                                   P<int64_t>(hist));
+                exclusive_scan_i64(P<int64_t>(hist), P<int64_t>(offs), 256 * ntiles, s);
+            }
             if (vals)
                 hipLaunchKernelGGL((k_scatter<B, IT, true>), dim3((unsigned)ntiles), dim3(B), scatter_lds<B>(T), st, ki,
                                    vi, n, shift, ntiles, P<int64_t>(offs), ko, vo);
@@ -256,9 +262,11 @@ void radix_sort_digits(capsmi_session* s, uint64_t* keys, int64_t* vals, int64_t
     radix_sort_digits(s, keys, vals, n, shifts, 0, nullptr);
 }
 
-void radix_sort_keys(capsmi_session* s, Buf& keys, int64_t n, const std::vector<int>& shifts) {
+static_assert(512 * 8 == kSortTile, "key-only sorts: 4096-key tiles");
+
+void radix_sort_keys(capsmi_session* s, Buf& keys, int64_t n, const std::vector<int>& shifts, const int64_t* hist0) {
     if (n <= 1 || shifts.empty()) return;
-    sort_passes<512, 8>(s, P<uint64_t>(keys), nullptr, n, shifts, 0, nullptr, &keys);
+    sort_passes<512, 8>(s, P<uint64_t>(keys), nullptr, n, shifts, 0, nullptr, &keys, hist0);
 }
 
 }  // namespace capsmi

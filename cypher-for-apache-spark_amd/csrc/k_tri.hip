@@ -297,18 +297,22 @@ __global__ void __launch_bounds__(256) k_deg_sample(const int64_t* __restrict__ 
 }
 
 // raw oriented keys: from << 32 | dir << 31 | to in degree-order ids (from = the lower (degree, id) end,
-// the larger rid; dir = 1 for a relationship to -> from), kNone for dropped ones; self-loops counted in sl
-__global__ void k_pack_or(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, int64_t lo,
-                          int64_t hi, const uint32_t* __restrict__ okw, int full, const uint32_t* __restrict__ rid,
-                          uint64_t* __restrict__ key, uint32_t* __restrict__ sl) {
-    constexpr int U = 4;  // relationships per lane and pass: the random rid gathers of four in flight together
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x * U;
-    for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x * U + threadIdx.x; e0 < m; e0 += stride) {
+// the larger rid; dir = 1 for a relationship to -> from), kNone for dropped ones; self-loops counted in sl.
+// HIST: the block writes whole 4096-key sort tiles and counts their first sort digit (bits hshift..+7) into
+// hist[d * ntiles + tile], so the sort's first pass skips its histogram read (radix_sort_keys' hist0)
+template <bool HIST>
+__global__ void __launch_bounds__(256) k_pack_or(const int64_t* __restrict__ src, const int64_t* __restrict__ dst,
+                                                 int64_t m, int64_t lo, int64_t hi, const uint32_t* __restrict__ okw,
+                                                 int full, const uint32_t* __restrict__ rid, uint64_t* __restrict__ key,
+                                                 uint32_t* __restrict__ sl, int64_t* __restrict__ hist, int hshift) {
+    constexpr int U = 4;  // relationships per lane and round: the random rid gathers of four in flight together
+    __shared__ unsigned int h[256];
+    auto round = [&](int64_t e0) {  // relationships e0 + j * 256
         uint64_t xs[U], xt[U];
         bool ok[U];
 #pragma unroll
         for (int j = 0; j < U; ++j) {
-            const int64_t e = e0 + (int64_t)j * blockDim.x;
+            const int64_t e = e0 + (int64_t)j * 256;
             const int64_t sv = e < m ? src[e] : lo - 1, tv = e < m ? dst[e] : lo - 1;
             ok[j] = sv >= lo && sv < hi && tv >= lo && tv < hi;
             xs[j] = ok[j] ? (uint64_t)(sv - lo) : 0;
@@ -327,7 +331,7 @@ __global__ void k_pack_or(const int64_t* __restrict__ src, const int64_t* __rest
         }
 #pragma unroll
         for (int j = 0; j < U; ++j) {
-            const int64_t e = e0 + (int64_t)j * blockDim.x;
+            const int64_t e = e0 + (int64_t)j * 256;
             if (e >= m) break;
             uint64_t k = kNone;
             if (ok[j]) {
@@ -335,7 +339,22 @@ __global__ void k_pack_or(const int64_t* __restrict__ src, const int64_t* __rest
                 else k = rs[j] > rt[j] ? ((uint64_t)rs[j] << 32) | rt[j] : ((uint64_t)rt[j] << 32) | (1u << 31) | rs[j];
             }
             key[e] = k;
+            if (HIST) atomicAdd(&h[(uint32_t)(k >> hshift) & 255u], 1u);
         }
+    };
+    if (!HIST) {
+        const int64_t stride = (int64_t)gridDim.x * 256 * U;
+        for (int64_t e0 = (int64_t)blockIdx.x * 256 * U + threadIdx.x; e0 < m; e0 += stride) round(e0);
+        return;
+    }
+    const int64_t ntiles = (m + kSortTile - 1) / kSortTile;
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // block-uniform
+        h[threadIdx.x] = 0;
+        __syncthreads();
+        for (int r = 0; r < kSortTile / (256 * U); ++r) round(t * kSortTile + (int64_t)r * 256 * U + threadIdx.x);
+        __syncthreads();
+        hist[(int64_t)threadIdx.x * ntiles + t] = h[threadIdx.x];
+        __syncthreads();  // h is cleared for the next tile
     }
 }
 
@@ -760,14 +779,17 @@ __global__ void k_vrec(const int64_t* __restrict__ off, const uint32_t* __restri
 // edge: p >= od(to), u-mode walks it), z / w = the starts of out_f(from) / out_b(from) -- so a v-mode
 // list's setup is one dependent load after its key; the in-key to << 40 | e, sorted on the digits of `to`
 // (stable: edge order within a target); the v-mode items read the records through it
-__global__ void k_swap_keys_sp(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ off, int64_t ne,
-                               TgCode tc, const uint32_t* __restrict__ tg, const uint32_t* __restrict__ rk,
-                               const uint32_t* __restrict__ fbo, const uint4* __restrict__ vrec,
-                               uint64_t* __restrict__ ik, uint4* __restrict__ rec) {
-    constexpr int U = 4;  // edges per lane and pass, loads issued together
+// A block writes whole 4096-key sort tiles and counts their first sort digit (bits hshift..+7) into hist
+// (radix_sort_keys' hist0: the in-key sort's first pass reads no histogram)
+__global__ void __launch_bounds__(256) k_swap_keys_sp(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ off,
+                                                      int64_t ne, TgCode tc, const uint32_t* __restrict__ tg,
+                                                      const uint32_t* __restrict__ rk, const uint32_t* __restrict__ fbo,
+                                                      const uint4* __restrict__ vrec, uint64_t* __restrict__ ik,
+                                                      uint4* __restrict__ rec, int64_t* __restrict__ hist, int hshift) {
+    constexpr int U = 4;  // edges per lane and round, loads issued together
     const uint32_t idm = tc.idmask();
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x * U;
-    for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x * U + threadIdx.x; e0 < ne; e0 += stride) {
+    __shared__ unsigned int h[256];
+    auto round = [&](int64_t e0) {  // edges e0 + j * 256
         uint64_t k[U];
         uint32_t w[U];
         uint2 r[U], fb[U];
@@ -775,7 +797,7 @@ __global__ void k_swap_keys_sp(const uint64_t* __restrict__ ok_, const int64_t* 
         uint32_t odt[U];
 #pragma unroll
         for (int j = 0; j < U; ++j) {
-            const int64_t e = min(e0 + (int64_t)j * blockDim.x, ne - 1);
+            const int64_t e = min(e0 + (int64_t)j * 256, ne - 1);
             k[j] = ok_[e];
             w[j] = tg[e];
             r[j] = reinterpret_cast<const uint2*>(rk)[e];
@@ -791,14 +813,25 @@ __global__ void k_swap_keys_sp(const uint64_t* __restrict__ ok_, const int64_t* 
         }
 #pragma unroll
         for (int j = 0; j < U; ++j) {
-            const int64_t e = e0 + (int64_t)j * blockDim.x;
+            const int64_t e = e0 + (int64_t)j * 256;
             if (e >= ne) break;
             const uint32_t from = (uint32_t)(k[j] >> 32), to = (uint32_t)k[j] & idm;
             const bool take = e - of[j] < (int64_t)odt[j];
             const uint32_t pfb = take ? (r[j].x - fb[j].x) | (r[j].y - fb[j].y) << 16 : 0u;
             rec[e] = make_uint4(from | (w[j] & ~idm), pfb, fb[j].x, fb[j].y);
-            ik[e] = (uint64_t)to << 40 | (uint64_t)e;
+            const uint64_t key = (uint64_t)to << 40 | (uint64_t)e;
+            ik[e] = key;
+            atomicAdd(&h[(uint32_t)(key >> hshift) & 255u], 1u);
         }
+    };
+    const int64_t ntiles = (ne + kSortTile - 1) / kSortTile;
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {  // block-uniform
+        h[threadIdx.x] = 0;
+        __syncthreads();
+        for (int q = 0; q < kSortTile / (256 * U); ++q) round(t * kSortTile + (int64_t)q * 256 * U + threadIdx.x);
+        __syncthreads();
+        hist[(int64_t)threadIdx.x * ntiles + t] = h[threadIdx.x];
+        __syncthreads();  // h is cleared for the next tile
     }
 }
 
@@ -1843,13 +1876,21 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         Buf sl0 = dev_alloc(sizeof(uint32_t) * n, s);
         HIP_CHECK(hipMemsetAsync(P<void>(sl0), 0, sizeof(uint32_t) * n, st));
         Buf key = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s);
-        {
+        Buf h0;  // one table on one device: the sort's first-digit tile counts, written with the keys
+        if (nt == 1 && !dd && m > 1) {
+            const int64_t ntl = (m + kSortTile - 1) / kSortTile;
+            h0 = dev_alloc(sizeof(int64_t) * 256 * ntl, s);
+            hipLaunchKernelGGL(k_pack_or<true>, dim3((unsigned)std::min<int64_t>(ntl, (int64_t)s->num_cus * 16)), dim3(256),
+                               0, st, srcs[0], dsts[0], m, lo, hi, P<uint32_t>(n_ok->words), n_ok->full ? 1 : 0,
+                               P<uint32_t>(rid), P<uint64_t>(key), P<uint32_t>(sl0), P<int64_t>(h0), od[0]);
+            HIP_CHECK(hipGetLastError());
+        } else {
             int64_t off = 0;
             for (int i = 0; i < nt; ++i) {
                 if (ms[i] > 0)
-                    hipLaunchKernelGGL(k_pack_or, dim3(grid(s, ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], lo, hi,
-                                       P<uint32_t>(n_ok->words), n_ok->full ? 1 : 0, P<uint32_t>(rid),
-                                       P<uint64_t>(key) + off, P<uint32_t>(sl0));
+                    hipLaunchKernelGGL(k_pack_or<false>, dim3(grid(s, ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i],
+                                       lo, hi, P<uint32_t>(n_ok->words), n_ok->full ? 1 : 0, P<uint32_t>(rid),
+                                       P<uint64_t>(key) + off, P<uint32_t>(sl0), (int64_t*)nullptr, 0);
                 off += ms[i];
             }
             HIP_CHECK(hipGetLastError());
@@ -1900,7 +1941,8 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         }
         // one sort of the raw oriented keys (the direction bit unsorted at bit 31), runs = the pairs
         ph.reset(new KernelTimer(s, "tri_sort_or"));
-        radix_sort_digits(s, P<uint64_t>(key), nullptr, m, od);
+        radix_sort_keys(s, key, m, od, P<int64_t>(h0));
+        h0.reset();
         // the runs: tile head counts, their scan, then every pair's outputs (k_or_write; the fused run passes
         // replaced head flags + compaction + k_und_runs + k_orient + k_targets + k_pair_terms, 6.1 ms at C4)
         const int64_t ntl = (m + kOrTile - 1) / kOrTile;
@@ -2184,15 +2226,19 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         } else {
             Buf ik = dev_alloc(sizeof(uint64_t) * ne, s);
             Buf iv = g.split ? dev_alloc(sizeof(uint4) * ne, s) : packed ? Buf() : dev_alloc(sizeof(int64_t) * ne, s);
-            if (g.split)  // iv: the records (k_swap_keys_sp)
-                hipLaunchKernelGGL(k_swap_keys_sp, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off),
-                                   ne, tc, P<uint32_t>(g.tg), P<uint32_t>(rk), P<uint32_t>(g.fbo), P<uint4>(g.vrec),
-                                   P<uint64_t>(ik), P<uint4>(iv));
-            else
+            Buf h0;  // split: the in-key sort's first-digit tile counts, written with the keys
+            if (g.split) {  // iv: the records (k_swap_keys_sp)
+                const int64_t ntl = (ne + kSortTile - 1) / kSortTile;
+                h0 = dev_alloc(sizeof(int64_t) * 256 * ntl, s);
+                hipLaunchKernelGGL(k_swap_keys_sp, dim3((unsigned)std::min<int64_t>(ntl, (int64_t)s->num_cus * 16)),
+                                   dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off), ne, tc, P<uint32_t>(g.tg),
+                                   P<uint32_t>(rk), P<uint32_t>(g.fbo), P<uint4>(g.vrec), P<uint64_t>(ik), P<uint4>(iv),
+                                   P<int64_t>(h0), tds[0]);
+            } else
                 hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off), ne,
                                    tc, P<uint64_t>(ik), packed ? nullptr : P<int64_t>(iv));
             rk.reset();
-            if (packed || g.split) radix_sort_keys(s, ik, ne, g.split ? tds : td);  // (3 passes: no copy back)
+            if (packed || g.split) radix_sort_keys(s, ik, ne, g.split ? tds : td, P<int64_t>(h0));  // (no copy back)
             else radix_sort_digits(s, P<uint64_t>(ik), P<int64_t>(iv), ne, td);
             g.ioff = dev_alloc(sizeof(int64_t) * (n + 1), s);
             hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), ne, n,
