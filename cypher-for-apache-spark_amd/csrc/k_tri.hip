@@ -379,6 +379,7 @@ struct OrOut {
     unsigned long long* nlong;
     const uint32_t* sl;         // self-loop counts in degree-order ids
     int64_t* pair;              // the pair terms: one partial sum per tile, the long runs' at index ntiles
+    int64_t* off;               // CSR offsets: off[from] = the from's first run (null: searched for later)
 };
 
 // the pair (from, to) = km's ids with f relationships from -> to and b to -> from: run r's outputs; returns
@@ -472,6 +473,7 @@ __global__ void __launch_bounds__(kOrB) k_or_write(const uint64_t* __restrict__ 
         if (head) {
             const int64_t r = r0 + wc[j * (kOrB / 64) + wid] + __popcll(hb & lt);
             const uint64_t km = kj & kOrMask;
+            if (o.off && (kj >> 32) != (p >> 32)) o.off[kj >> 32] = r;  // the first run of this from
             uint32_t len = 1, bk = (uint32_t)(kj >> 31) & 1u;
             int q = i + 1;
             bool ended = false;
@@ -569,6 +571,105 @@ __global__ void __launch_bounds__(256) k_or_long(const uint64_t* __restrict__ ke
         }
         __syncthreads();
     }
+}
+
+// The CSR offsets without a search: k_or_write stored off[v] at each from change and the rest hold
+// INT64_MAX; a vertex without out-edges starts where the next one does, so off becomes its suffix minimum
+// over the n + 1 entries (off[n] = ne), the largest out-degree found on the way (k_sufmin_apply).
+constexpr int kSmB = 256, kSmIt = 16, kSmTile = kSmB * kSmIt;
+
+__global__ void __launch_bounds__(kSmB) k_sufmin_tiles(const int64_t* __restrict__ off, int64_t n1,
+                                                       int64_t* __restrict__ tmin) {
+    __shared__ int64_t ws[kSmB / 64];
+    const int64_t base = (int64_t)blockIdx.x * kSmTile + threadIdx.x;
+    int64_t v = INT64_MAX;
+#pragma unroll
+    for (int k = 0; k < kSmIt; ++k)  // coalesced: a plain minimum needs no order
+        if (base + k * kSmB < n1) v = min(v, off[base + k * kSmB]);
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (int64_t)__shfl_down(v, o, 64));
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) tmin[blockIdx.x] = min(min(ws[0], ws[1]), min(ws[2], ws[3]));
+}
+
+// one workgroup: tmin[t] becomes the minimum over the tiles after t (INT64_MAX for the last)
+__global__ void __launch_bounds__(1024) k_sufmin_carry(int64_t* __restrict__ tmin, int64_t nt) {
+    __shared__ int64_t cm[1024];
+    const int64_t per = (nt + 1023) / 1024, b = (int64_t)threadIdx.x * per;
+    int64_t v = INT64_MAX;
+    for (int64_t k = 0; k < per; ++k)
+        if (b + k < nt) v = min(v, tmin[b + k]);
+    cm[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // inclusive suffix minimum over the chunk minima
+        const int64_t y = threadIdx.x + o < 1024 ? cm[threadIdx.x + o] : INT64_MAX;
+        __syncthreads();
+        cm[threadIdx.x] = min(cm[threadIdx.x], y);
+        __syncthreads();
+    }
+    int64_t run = threadIdx.x + 1 < 1024 ? cm[threadIdx.x + 1] : INT64_MAX;  // the chunks after this one
+    for (int64_t k = per - 1; k >= 0; --k)
+        if (b + k < nt) {
+            const int64_t x = tmin[b + k];
+            tmin[b + k] = run;
+            run = min(run, x);
+        }
+}
+
+// the tile is staged through LDS (coalesced loads and stores; a lane's 16 consecutive entries at a padded
+// stride of 17, so the lanes' reads fall in different banks)
+__global__ void __launch_bounds__(kSmB) k_sufmin_apply(int64_t* __restrict__ off, int64_t n1,
+                                                       const int64_t* __restrict__ carry,
+                                                       unsigned long long* __restrict__ maxod) {
+    __shared__ int64_t st[kSmB * (kSmIt + 1)];
+    __shared__ int64_t cm[kSmB];
+    const int64_t tb = (int64_t)blockIdx.x * kSmTile;
+    auto pad = [](int i) { return i + i / kSmIt; };
+#pragma unroll
+    for (int k = 0; k < kSmIt; ++k) {
+        const int i = k * kSmB + (int)threadIdx.x;
+        st[pad(i)] = tb + i < n1 ? off[tb + i] : INT64_MAX;
+    }
+    __syncthreads();
+    int64_t x[kSmIt];
+    int64_t v = INT64_MAX;
+#pragma unroll
+    for (int k = 0; k < kSmIt; ++k) {
+        x[k] = st[threadIdx.x * (kSmIt + 1) + k];
+        v = min(v, x[k]);
+    }
+    cm[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < kSmB; o <<= 1) {  // inclusive suffix minimum over the lanes
+        const int64_t y = threadIdx.x + o < kSmB ? cm[threadIdx.x + o] : INT64_MAX;
+        __syncthreads();
+        cm[threadIdx.x] = min(cm[threadIdx.x], y);
+        __syncthreads();
+    }
+    // the final value right after this lane's entries: the next lanes', then the next tile's (carry)
+    const int64_t next_first = min(threadIdx.x + 1 < kSmB ? cm[threadIdx.x + 1] : INT64_MAX, carry[blockIdx.x]);
+    int64_t run = next_first;
+#pragma unroll
+    for (int k = kSmIt - 1; k >= 0; --k) {
+        run = min(run, x[k]);
+        x[k] = run;
+    }
+    const int64_t base = tb + (int64_t)threadIdx.x * kSmIt;
+    unsigned long long best = 0;
+#pragma unroll
+    for (int k = 0; k < kSmIt; ++k) {
+        st[threadIdx.x * (kSmIt + 1) + k] = x[k];
+        const int64_t nx = k + 1 < kSmIt ? x[k + 1] : next_first;
+        if (base + k + 1 < n1) best = max(best, (unsigned long long)(nx - x[k]));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSmIt; ++k) {
+        const int i = k * kSmB + (int)threadIdx.x;
+        if (tb + i < n1) off[tb + i] = st[pad(i)];
+    }
+    for (int o = 32; o > 0; o >>= 1) best = max(best, (unsigned long long)__shfl_down(best, o, 64));
+    if ((threadIdx.x & 63) == 0 && best) atomicMax(maxod, best);
 }
 
 // sl in degree-order ids
@@ -765,11 +866,13 @@ __global__ void k_split_off(const int64_t* __restrict__ off, int64_t n, int64_t 
 // per-vertex list record of the split walks: {start of out_f(x), start of out_b(x), |out_f(x)| | |out_b(x)| << 16,
 // od(x)} -- one 16-byte load sets up both lists of an edge u -> x (and the v-mode skip test) instead of the
 // offsets' and the list starts' separate lines (lengths < 2^16: the split walks run with packed in-keys)
+// (od32: the out-degrees alone, 4 bytes a vertex, for the in-list records' random reads)
 __global__ void k_vrec(const int64_t* __restrict__ off, const uint32_t* __restrict__ fbo, int64_t n,
-                       uint4* __restrict__ vrec) {
+                       uint4* __restrict__ vrec, uint32_t* __restrict__ od32) {
     for (int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; x < n; x += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t f0 = fbo[2 * x], b0 = fbo[2 * x + 1];
-        vrec[x] = make_uint4(f0, b0, (fbo[2 * x + 2] - f0) | (fbo[2 * x + 3] - b0) << 16, (uint32_t)(off[x + 1] - off[x]));
+        const uint32_t f0 = fbo[2 * x], b0 = fbo[2 * x + 1], od = (uint32_t)(off[x + 1] - off[x]);
+        vrec[x] = make_uint4(f0, b0, (fbo[2 * x + 2] - f0) | (fbo[2 * x + 3] - b0) << 16, od);
+        od32[x] = od;
     }
 }
 
@@ -784,7 +887,7 @@ __global__ void k_vrec(const int64_t* __restrict__ off, const uint32_t* __restri
 __global__ void __launch_bounds__(256) k_swap_keys_sp(const uint64_t* __restrict__ ok_, const int64_t* __restrict__ off,
                                                       int64_t ne, TgCode tc, const uint32_t* __restrict__ tg,
                                                       const uint32_t* __restrict__ rk, const uint32_t* __restrict__ fbo,
-                                                      const uint4* __restrict__ vrec, uint64_t* __restrict__ ik,
+                                                      const uint32_t* __restrict__ od32, uint64_t* __restrict__ ik,
                                                       uint4* __restrict__ rec, int64_t* __restrict__ hist, int hshift) {
     constexpr int U = 4;  // edges per lane and round, loads issued together
     const uint32_t idm = tc.idmask();
@@ -803,13 +906,13 @@ __global__ void __launch_bounds__(256) k_swap_keys_sp(const uint64_t* __restrict
             r[j] = reinterpret_cast<const uint2*>(rk)[e];
         }
         // three lane loads per edge: off(from), the from's list starts (one 8-byte word) and od(to) from the
-        // to's 16-byte vertex record (was: off(to) and off(to + 1), and the two starts apart)
+        // 4-byte degree array (was: the to's 16-byte vertex record, and before that off(to) and off(to + 1))
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             const uint32_t from = (uint32_t)(k[j] >> 32), to = (uint32_t)k[j] & idm;
             of[j] = off[from];
             fb[j] = reinterpret_cast<const uint2*>(fbo)[from];
-            odt[j] = vrec[to].w;
+            odt[j] = od32[to];
         }
 #pragma unroll
         for (int j = 0; j < U; ++j) {
@@ -1829,6 +1932,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     int64_t* nvalid_p = P<int64_t>(nv);
     unsigned long long* nlong = reinterpret_cast<unsigned long long*>(nvalid_p + 1);
     Buf exc;
+    Buf maxod;  // the largest out-degree (u64), when the offsets pass found it
     int64_t ne = 0;
     std::unique_ptr<KernelTimer> ph;
     // the direct oriented build ("the direct oriented build" above) for ids <= 2^24; config
@@ -1962,19 +2066,36 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         g.pair = dev_alloc(sizeof(int64_t), s);
         HIP_CHECK(hipMemsetAsync(P<void>(g.pair), 0, sizeof(int64_t), st));
         HIP_CHECK(hipMemsetAsync(P<void>(nv), 0, sizeof(int64_t) + sizeof(unsigned long long), st));  // nexc, nlong
+        if (!dd) {  // one device: the CSR offsets from the run heads (k_or_write), see k_sufmin_apply
+            g.off = dev_alloc(sizeof(int64_t) * (n + 1), s);
+            fill_i64(P<int64_t>(g.off), INT64_MAX, n, st);
+            fill_i64(P<int64_t>(g.off) + n, nruns, 1, st);
+        }
         if (nruns > 0) {
             Buf longr = dev_alloc(sizeof(int64_t) * 2 * (m / kShortRun + 1), s);
             Buf pp = dev_alloc(sizeof(int64_t) * (ntl + 1), s), ps = dev_alloc(sizeof(int64_t) * (ntl + 2), s);
             HIP_CHECK(hipMemsetAsync(P<int64_t>(pp) + ntl, 0, sizeof(int64_t), st));
             // one device: the exceptions' payloads go straight to ov (the keys stay where they are written)
             OrOut o{P<uint64_t>(g.ok), P<uint32_t>(g.tg), P<int64_t>(g.ov), dd ? P<uint64_t>(exc) : nullptr, nlong,
-                    P<int64_t>(longr), reinterpret_cast<unsigned long long*>(nvalid_p), P<uint32_t>(g.sl), P<int64_t>(pp)};
+                    P<int64_t>(longr), reinterpret_cast<unsigned long long*>(nvalid_p), P<uint32_t>(g.sl), P<int64_t>(pp),
+                    P<int64_t>(g.off)};
             hipLaunchKernelGGL(k_or_write, dim3((unsigned)ntl), dim3(kOrB), 0, st, P<uint64_t>(key), m, P<int64_t>(pre),
                                tc, o);
             hipLaunchKernelGGL(k_or_long, dim3(4 * s->num_cus), dim3(256), 0, st, P<uint64_t>(key), m, ntl, tc, o);
             HIP_CHECK(hipGetLastError());
             exclusive_scan_i64(P<int64_t>(pp), P<int64_t>(ps), ntl + 1, s);
             HIP_CHECK(hipMemcpyAsync(P<void>(g.pair), P<int64_t>(ps) + ntl + 1, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+        }
+        if (!dd) {
+            const int64_t n1 = n + 1, nst = (n1 + kSmTile - 1) / kSmTile;
+            Buf tm = dev_alloc(sizeof(int64_t) * nst, s);
+            maxod = dev_alloc(sizeof(unsigned long long), s);
+            HIP_CHECK(hipMemsetAsync(P<void>(maxod), 0, sizeof(unsigned long long), st));
+            hipLaunchKernelGGL(k_sufmin_tiles, dim3((unsigned)nst), dim3(kSmB), 0, st, P<int64_t>(g.off), n1, P<int64_t>(tm));
+            hipLaunchKernelGGL(k_sufmin_carry, dim3(1), dim3(1024), 0, st, P<int64_t>(tm), nst);
+            hipLaunchKernelGGL(k_sufmin_apply, dim3((unsigned)nst), dim3(kSmB), 0, st, P<int64_t>(g.off), n1, P<int64_t>(tm),
+                               P<unsigned long long>(maxod));
+            HIP_CHECK(hipGetLastError());
         }
         key.reset();
         g.nek = 0;  // the pair terms are in g.pair
@@ -2137,8 +2258,11 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         hipLaunchKernelGGL(k_exc_place, dim3(grid(s, ne / 64 + 1)), dim3(256), 0, st, P<uint64_t>(exc), nlong,
                            P<uint64_t>(g.ok), ne, tc, P<int64_t>(g.ov));
     exc.reset();
-    g.off = dev_alloc(sizeof(int64_t) * (n + 1), s);
-    hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, n, 32, P<int64_t>(g.off));
+    if (!g.off) {  // (the direct build on one device has them from the run heads)
+        g.off = dev_alloc(sizeof(int64_t) * (n + 1), s);
+        hipLaunchKernelGGL(k_offsets, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, n, 32,
+                           P<int64_t>(g.off));
+    }
     if (!g.tg) {  // (the direct build on one device wrote them with the keys)
         g.tg = dev_alloc(sizeof(uint32_t) * (ne > 0 ? ne : 1), s);
         if (ne > 0)
@@ -2148,15 +2272,19 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
     // order (every out-neighbour has at least u's degree), so m < 2^31 relationships bound it by 2^16
     bool packed = g.ib <= 24 && m_all < (int64_t(1) << 31);
     if (packed && ne > 0) {  // (an estimated degree order does not carry the sqrt(2m) bound: check it)
-        Buf t = dev_alloc(sizeof(unsigned long long), s);
-        HIP_CHECK(hipMemsetAsync(P<void>(t), 0, sizeof(unsigned long long), st));
-        hipLaunchKernelGGL(k_max_od, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), n, P<unsigned long long>(t));
-        packed = read_scalar(s, reinterpret_cast<const int64_t*>(P<unsigned long long>(t))) < 65536;
+        if (!maxod) {
+            maxod = dev_alloc(sizeof(unsigned long long), s);
+            HIP_CHECK(hipMemsetAsync(P<void>(maxod), 0, sizeof(unsigned long long), st));
+            hipLaunchKernelGGL(k_max_od, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), n,
+                               P<unsigned long long>(maxod));
+        }
+        packed = read_scalar(s, reinterpret_cast<const int64_t*>(P<unsigned long long>(maxod))) < 65536;
     }
     // direction-split lists (coded targets); the combined walks when the codes or packed keys do not fit
     // (config tri_split = 0 forces them: tests cover that path at small sizes)
     g.split = tc.cb > 0 && packed && ne > 0 && s->cfg.tri_split;
     Buf rk;  // per oriented edge: f / b ranks (the in-lists' prefix lengths)
+    Buf od32;  // split: the out-degrees, 4 bytes a vertex (k_vrec)
     if (g.split) {
         const int64_t ntiles = (ne + kSplitTile - 1) / kSplitTile;
         Buf cnt = dev_alloc(sizeof(int64_t) * 2 * (ntiles + 1), s), pre = dev_alloc(sizeof(int64_t) * 2 * (ntiles + 1), s);
@@ -2176,8 +2304,9 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         hipLaunchKernelGGL(k_split_off, dim3(grid(s, n + 1)), dim3(256), 0, st, P<int64_t>(g.off), n, ne,
                            P<uint32_t>(rk), (uint32_t)nF, (uint32_t)(nF + nB), P<uint32_t>(g.fbo));
         g.vrec = dev_alloc(sizeof(uint4) * n, s);
+        od32 = dev_alloc(sizeof(uint32_t) * n, s);
         hipLaunchKernelGGL(k_vrec, dim3(grid(s, n)), dim3(256), 0, st, P<int64_t>(g.off), P<uint32_t>(g.fbo), n,
-                           P<uint4>(g.vrec));
+                           P<uint4>(g.vrec), P<uint32_t>(od32));
         HIP_CHECK(hipGetLastError());
     }
     // in-lists and v-mode centers (config CAPSMI_TRI_VMODE_T: the od(v) threshold; 0 = every edge from u)
@@ -2232,7 +2361,7 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
                 h0 = dev_alloc(sizeof(int64_t) * 256 * ntl, s);
                 hipLaunchKernelGGL(k_swap_keys_sp, dim3((unsigned)std::min<int64_t>(ntl, (int64_t)s->num_cus * 16)),
                                    dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off), ne, tc, P<uint32_t>(g.tg),
-                                   P<uint32_t>(rk), P<uint32_t>(g.fbo), P<uint4>(g.vrec), P<uint64_t>(ik), P<uint4>(iv),
+                                   P<uint32_t>(rk), P<uint32_t>(g.fbo), P<uint32_t>(od32), P<uint64_t>(ik), P<uint4>(iv),
                                    P<int64_t>(h0), tds[0]);
             } else
                 hipLaunchKernelGGL(k_swap_keys, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), P<int64_t>(g.off), ne,
