@@ -171,6 +171,38 @@ def test_split_word_cap(session, knobs, walk, vmode):
     assert _count(session, n, src, dst) == cpu.triangle_closed_form(n, src, dst)
 
 
+@pytest.mark.parametrize("vmode", VMODE)
+def test_run_passes_across_tiles(session, knobs, vmode):
+    """The direct build's fused run passes (k_or_count / k_or_write / k_or_long) over ~60 sort tiles of 4096
+    keys: runs of one pair's relationships from 1 to 90 keys in either or both directions (long runs past
+    kShortRun, runs crossing tile ends), self-loops (the pair terms), filtered nodes (dropped keys sorted
+    last), and the CSR offsets of vertices without out-edges filled from the next one."""
+    _vmode(knobs, session, vmode)
+    rng = np.random.default_rng(29)
+    n = 5000
+    a = rng.integers(0, n, 24000)
+    b = rng.integers(0, n, 24000)
+    keep = a != b
+    a, b = a[keep], b[keep]
+    kind = rng.random(len(a))
+    f = np.where(kind < 0.6, 1, np.where(kind < 0.8, rng.integers(2, 60, len(a)), rng.integers(1, 45, len(a))))
+    r = np.where(kind < 0.8, 0, rng.integers(1, 45, len(a)))
+    src = np.concatenate([np.repeat(a, f), np.repeat(b, r)]).astype(np.int64)
+    dst = np.concatenate([np.repeat(b, f), np.repeat(a, r)]).astype(np.int64)
+    loops = rng.choice(n, n // 10, replace=False)
+    ls = np.repeat(loops, rng.integers(1, 6, len(loops))).astype(np.int64)
+    src = np.concatenate([src, ls])
+    dst = np.concatenate([dst, ls])
+    perm = rng.permutation(len(src))
+    src, dst = src[perm], dst[perm]
+    mask = rng.random(n) < 0.8
+    keep = mask[src] & mask[dst]
+    want = cpu.triangle_closed_form(n, src[keep], dst[keep])
+    assert want > 0
+    assert _count(session, n, src, dst, mask) == want
+    assert _count(session, n, src, dst, mask, nparts=3) == want
+
+
 def _mix32(x):
     """k_tri.hip mix32 (the degree sample's hashed offset), vectorised over uint64."""
     x = x.astype(np.uint64)
