@@ -88,3 +88,11 @@ def test_config_knobs_are_checked():
     for k, v in bad:
         assert lib.capsmi_config_check(k.encode(), None if v is None else v.encode()) == _lib.ERR_ILLEGAL_ARGUMENT, (k, v)
         assert "configuration" in _lib.last_error()
+
+
+def test_profiling_names_need_a_session():
+    """capsmi_session_set_profiling_names refuses a null session (no device needed to check)."""
+    from capsmi import _lib
+    lib = _lib.load()
+    assert lib.capsmi_session_set_profiling_names(None, b"part_scatter1") == _lib.ERR_ILLEGAL_ARGUMENT
+    assert lib.capsmi_session_set_profiling_names(None, None) == _lib.ERR_ILLEGAL_ARGUMENT
