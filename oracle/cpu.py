@@ -203,6 +203,36 @@ def var_length_closed_form(n, src, dst, lo, hi, a_ok=None, b_ok=None, threads=0)
     return rows.value, g
 
 
+def var_length4_closed_form(n, src, dst, a_ok=None, b_ok=None):
+    """Per start node a: the relationship-distinct paths of exactly 4 hops a -> ... -> z with a_ok(a), b_ok(z)
+    (MATCH (a)-[*4..4]->(b); paths never repeat a relationship: VarLengthExpandPlanner.scala:97,133,179-180),
+    by inclusion-exclusion over the 15 set partitions of the hop positions {1,2,3,4} (Mobius weights
+    prod (-1)^(|B|-1) (|B|-1)!).  A block {i, j} forces r_i = r_j, which makes the walk between them a closed
+    walk: adjacent positions a self-loop, {1,3} / {2,4} a reciprocal pair, {1,4} a 2-walk back along a
+    relationship (a directed triangle through it -- the one term that is not a product of per-node vectors and
+    pair multiplicities).  Scipy sparse over the multiplicity matrix A (A[x, y] = m(x, y), self-loops on the
+    diagonal); test infrastructure.  Returns (total, per-node counts)."""
+    import scipy.sparse as sp
+    src = np.asarray(src, np.int64)
+    dst = np.asarray(dst, np.int64)
+    A = sp.csr_matrix((np.ones(len(src), np.int64), (src, dst)), shape=(n, n))
+    A.sum_duplicates()
+    s = A.diagonal().astype(np.int64)
+    b = np.ones(n, np.int64) if b_ok is None else np.asarray(b_ok).astype(np.int64)
+    a = np.ones(n, np.int64) if a_ok is None else np.asarray(a_ok).astype(np.int64)
+    Ab = A @ b
+    A2b = A @ Ab
+    M = A.multiply(A.T).tocsr()  # m(x, y) m(y, x)
+    A2 = (A @ A).tocsr()
+    W4 = A @ (A @ A2b)
+    pair1 = (s * A2b) + (A @ (s * Ab)) + (A @ (A @ (s * b)))      # {12} {23} {34}
+    pair2 = (M @ Ab) + (A @ (M @ b)) + (A.multiply(A2.T).tocsr() @ b)  # {13} {24} {14}
+    two = s * s * b * 2 + b * np.asarray(M.sum(axis=1)).ravel()     # {12}{34} {14}{23}; {13}{24}
+    three = (s * Ab) + 2 * (s * s * b) + (A @ (s * b))             # {123}; {124} {134}; {234}
+    per = (W4 - pair1 - pair2 + two + 2 * three - 6 * (s * b)) * a
+    return int(per.sum()), per
+
+
 def two_hop_undirected_closed_form(n, src, dst, a_ok=None, b_ok=None, c_ok=None, threads=0):
     """(count(*), count(DISTINCT c)) of (a)-[r1]-(b)-[r2]-(c), r1 <> r2 (closed.c)."""
     rows, d = ctypes.c_int64(), ctypes.c_int64()

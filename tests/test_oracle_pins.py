@@ -150,6 +150,44 @@ def test_closed_forms_equal_enumeration_on_rmat(scale, probs, ef):
     assert cpu.triangle_closed_form(n, src, dst, person) == cpu.triangle_enumerate(n, src[keep], dst[keep])
 
 
+@pytest.mark.parametrize("seed", range(24))
+def test_var_length4_closed_form_equals_enumeration(seed):
+    """The 4-hop relationship-distinct path count per start node (inclusion-exclusion, oracle/cpu.py) equals
+    path enumeration on random multigraphs with self-loops, reciprocal pairs and node filters -- and *1..4 is
+    the closed forms for 1..3 plus it (the count-only form's first step)."""
+    from oracle import cpu
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(2, 14))
+    m = int(rng.integers(0, 45))
+    src = rng.integers(0, n, m).astype(np.int64)
+    dst = rng.integers(0, n, m).astype(np.int64)
+    src[: m // 5] = dst[: m // 5]
+    if m >= 12:  # three relationships reversed: reciprocal pairs
+        k = m // 5
+        src[-3:], dst[-3:] = dst[k:k + 3].copy(), src[k:k + 3].copy()
+    a_ok = None if seed % 3 == 0 else (rng.random(n) < 0.8).astype(np.uint8)
+    b_ok = None if seed % 4 == 0 else (rng.random(n) < 0.7).astype(np.uint8)
+    tot, per = cpu.var_length_count(n, src, dst, 4, 4, a_ok, b_ok)
+    tot4, per4 = cpu.var_length4_closed_form(n, src, dst, a_ok, b_ok)
+    np.testing.assert_array_equal(per4, per)
+    assert tot4 == tot
+    tot14, per14 = cpu.var_length_count(n, src, dst, 1, 4, a_ok, b_ok)
+    tot13, per13 = cpu.var_length_closed_form(n, src, dst, 1, 3, a_ok, b_ok)
+    np.testing.assert_array_equal(per13 + per4, per14)
+
+
+@pytest.mark.parametrize("scale,probs,ef", [(7, (57, 19, 19), 16), (6, (45, 15, 15), 32)])
+def test_var_length4_closed_form_on_rmat(scale, probs, ef):
+    from oracle import cpu
+    n = 1 << scale
+    src, dst = cpu.rmat_edges(scale, 0, ef << scale, probs, 7)
+    person, adult = cpu.c2_masks(n, 42)
+    for a_ok, b_ok in [(None, None), (adult, person)]:
+        tot, per = cpu.var_length_count(n, src, dst, 4, 4, a_ok, b_ok)
+        tot4, per4 = cpu.var_length4_closed_form(n, src, dst, a_ok, b_ok)
+        np.testing.assert_array_equal(per4, per)
+
+
 def test_c2_masks_match_scalar_definition():
     from oracle import cpu
     n = 4096
