@@ -126,6 +126,9 @@ def parse():
                         "trigraph, each share's count timed alone -- the per-rank triangle phase without contention")
     p.add_argument("--workload", default="c3", choices=("c2", "c3", "c4", "c5"),
                    help="c3 (default, the BASELINE metric) or the single-GPU C2/C4/C5 lines (SURVEY.md 8d)")
+    p.add_argument("--c5-upper", type=int, default=3, choices=(3, 4),
+                   help="C5's upper bound: 3 (the BASELINE config) or 4 (the four-hop fused count, one GPU; a "
+                        "diagnostic line without a fixture: its parity is the tests' against enumeration)")
     return p.parse_args()
 
 
@@ -776,6 +779,9 @@ def run_single(args):
 
     wl = args.workload
     scale, ef, probs, desc, cpu_scale = SINGLE[wl]
+    up = args.c5_upper if wl == "c5" else 3
+    if up != 3:
+        desc = desc.replace("*1..3", f"*1..{up}")
     if args.scale != 26:  # --scale given explicitly
         scale = args.scale
     cpu_scale = args.cpu_scale or cpu_scale
@@ -784,6 +790,8 @@ def run_single(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dw = world > 1 or (args.dist1 and wl in ("c4", "c5"))  # --dist1: the distributed route at world size 1
+    if dw and up != 3:
+        sys.exit("bench: --c5-upper 4 is the one-GPU four-hop count (the sharded form stops at 3)")
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if dw:  # C2: rels by owner(source), local expand; C4: replicated oriented graph, vertex shares;
@@ -842,7 +850,8 @@ def run_single(args):
         sess.set_fused(route == "planner")
 
     def plan_of():  # the routed query's lazy plan (holds no rows, runs nothing until its first action)
-        return Planner(sg).run({"c4": C4_QUERY, "c5": C5_QUERY}.get(wl, C2_QUERY))
+        c5q = C5_QUERY if up == 3 else {**C5_QUERY, "clauses": [{"match": f"(a:Person)-[:KNOWS*1..{up}]->(b:Person)"}]}
+        return Planner(sg).run({"c4": C4_QUERY, "c5": c5q}.get(wl, C2_QUERY))
 
     def run_plan(plan):  # from handing the plan to the backend to the answer on the host
         t, outs = plan
@@ -887,13 +896,14 @@ def run_single(args):
             out = sh.finish()
             sh.release()
             return None, out
-        out = graph.var_length_count(sess, [rels], ok, ok, 1, 3)
+        out = graph.var_length_count(sess, [rels], ok, ok, 1, up)
         return None, out
 
     kernels = ("direct_join_probe", "radix_join_count", "radix_join_write", "bitmap_add", "expand_filter", "tri_pack",
                "tri_deg", "tri_sort_und", "tri_order", "tri_sort_or", "tri_post", "tri_work", "triangles", "part_scatter1",
                "varlen_part", "varlen_deg", "varlen_w", "varlen_rev",
-               "varlen_cand", "varlen_recip", "varlen_t", "vls_rev_part", "vls_rev_bloom", "vls_rev_cand", "vls_rev_recip")
+               "varlen_cand", "varlen_recip", "varlen_t", "varlen_4", "vls_rev_part", "vls_rev_bloom", "vls_rev_cand",
+               "vls_rev_recip")
     gate = None
     if world > 1:
         from capsmi.dist import serial_gate
@@ -930,7 +940,8 @@ def run_single(args):
     for _ in range(PROFILED_STEPS):
         step()
     kt, kbytes = read_timers()
-    dom = max(kt, key=lambda k: kt[k][1]) if kt else None
+    ranked = [k for k in kt if k != "varlen_4"]  # (the four-hop phase: several kernels, no single roofline)
+    dom = max(ranked, key=lambda k: kt[k][1]) if ranked else None
     _lib.call("capsmi_session_set_profiling_names", sess.handle, dom.encode() if dom else None)
     plan_ms = None
     if route != "direct" and not args.plan_in_step:  # as the C3 modes: each timed step executes its own
@@ -983,7 +994,7 @@ def run_single(args):
         check = "ok" if ref == res else f"MISMATCH {res} vs unsharded {ref}"
         del full
     # every line checks its answer against the committed oracle fixture (tests/golden/rmat_full.json)
-    fx = fixture(f"{wl}_s{scale}")
+    fx = fixture(f"{wl}_s{scale}") if up == 3 else None
     if fx is None or (world > 1 and wl == "c2"):
         fcheck = "no fixture for this scale" if fx is None else "rows only (output stays partitioned)"
         if fx is not None and wl == "c2":
@@ -1095,8 +1106,8 @@ def run_single(args):
     line["query"]["check_vs_fixture"] = fcheck
     if check is not None or (world > 1 and wl in ("c2", "c5")):
         line["query"]["check_vs_unsharded"] = check
-    line["cpu_baseline"] = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_single(wl, cpu_scale, ef, probs,
-                                                                                                 scale)
+    line["cpu_baseline"] = None if (args.no_cpu_baseline or world > 1 or up != 3) else cpu_baseline_single(
+        wl, cpu_scale, ef, probs, scale)
     if rank == 0:
         print(json.dumps(line), flush=True)
     sess.close()

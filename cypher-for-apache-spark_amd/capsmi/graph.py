@@ -176,7 +176,7 @@ def two_hop_mark_dst(session: Session, rels: Sequence[GpuTable], b_ok: NodeBitma
 def var_length_count(session: Session, rels: Sequence[GpuTable], a_ok: NodeBitmap, b_ok: NodeBitmap, lower: int,
                      upper: int, id_name: str = "id", count_name: str = "count", src_col: str = "source",
                      dst_col: str = "target") -> GpuTable:
-    """``MATCH (a)-[*lower..upper]->(b) WHERE a_ok(a) AND b_ok(b) RETURN id(a), count(*)`` (1 <= lower <= upper <= 3)."""
+    """``MATCH (a)-[*lower..upper]->(b) WHERE a_ok(a) AND b_ok(b) RETURN id(a), count(*)`` (0 <= lower <= upper <= 4)."""
     out = ctypes.c_void_p()
     _lib.call("capsmi_var_length_count", session.handle, len(rels), _handles(rels), src_col.encode(), dst_col.encode(),
               a_ok.handle, b_ok.handle, lower, upper, id_name.encode(), count_name.encode(), ctypes.byref(out))

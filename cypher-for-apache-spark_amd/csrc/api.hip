@@ -1776,11 +1776,13 @@ capsmi_status capsmi_var_length_count(capsmi_session* s, int32_t nrels, capsmi_t
     check_bitmap(a_ok, "a_ok");
     check_bitmap(b_ok, "b_ok");
     REQUIRE(nrels >= 0 && (nrels == 0 || rels), CAPSMI_ERR_ILLEGAL_ARGUMENT, "rels");
-    REQUIRE(lower >= 0 && lower <= upper && upper >= 1 && upper <= 3, CAPSMI_ERR_NOT_IMPLEMENTED,
-            "fused var-length count supports 0 <= lower <= upper <= 3, upper >= 1 (use the join plan otherwise)");
+    REQUIRE(lower >= 0 && lower <= upper && upper >= 1 && upper <= 4, CAPSMI_ERR_NOT_IMPLEMENTED,
+            "fused var-length count supports 0 <= lower <= upper <= 4, upper >= 1 (use the join plan otherwise)");
     REQUIRE(a_ok->lo == b_ok->lo && a_ok->hi == b_ok->hi, CAPSMI_ERR_UNSUPPORTED, "a and b scans need one id domain");
     REQUIRE(!a_ok->any_dup && !b_ok->any_dup, CAPSMI_ERR_UNSUPPORTED,
             "fused count(*) needs each node id in one scanned row");
+    REQUIRE(upper <= 3 || a_ok->hi - a_ok->lo < (int64_t(1) << 24) - 1, CAPSMI_ERR_UNSUPPORTED,
+            "fused var-length upper 4: at most 2^24 - 2 ids");
     REQUIRE(std::string(id_name) != count_name, CAPSMI_ERR_ILLEGAL_ARGUMENT, "output names must differ");
     use_device(s);
     std::vector<const int64_t*> srcs, dsts;

@@ -1889,6 +1889,45 @@ inline int bits_for(uint64_t range) {
 
 }  // namespace tri
 
+namespace tri {
+// A distributed build's exchange of oriented keys (source in bits 32+): each key to the rank of its source's
+// degree-order range, the ranges made of coarse source bins balanced by their all-reduced key counts, so a
+// source's whole list meets on one rank; returns this rank's keys (*nout of them)
+Buf to_source_range_owner(capsmi_session* s, const Buf& keys, int64_t nk, int bits, int64_t n, int W, int64_t* nout) {
+    hipStream_t st = s->stream;
+    const int hb = bits > 12 ? bits - 12 : 0;
+    const int64_t nbins = ((n - 1) >> hb) + 1;
+    Buf hist = dev_alloc(sizeof(int64_t) * (kHistBins + W + 1), s);
+    HIP_CHECK(hipMemsetAsync(P<void>(hist), 0, sizeof(int64_t) * kHistBins, st));
+    if (nk > 0)
+        hipLaunchKernelGGL(k_tri_from_hist, dim3(std::min(grid(s, nk), 4 * s->num_cus)), dim3(1024), 0, st,
+                           P<uint64_t>(keys), nk, hb, P<unsigned long long>(hist));
+    HIP_CHECK(hipGetLastError());
+    collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(hist), P<int64_t>(hist), kHistBins, CAPSMI_I64);
+    std::vector<int64_t> h(kHistBins), bb(W + 1);
+    HIP_CHECK(hipMemcpyAsync(h.data(), P<int64_t>(hist), sizeof(int64_t) * kHistBins, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    int64_t tot = 0;
+    for (int64_t b = 0; b < nbins; ++b) tot += h[b];
+    int64_t cum = 0, b = 0;
+    bb[0] = 0;
+    for (int q = 1; q < W; ++q) {
+        const int64_t want = tot * q / W;
+        while (b < nbins && cum + h[b] <= want) cum += h[b++];
+        bb[q] = b;
+    }
+    bb[W] = nbins;
+    int64_t* bbeg = P<int64_t>(hist) + kHistBins;
+    HIP_CHECK(hipMemcpyAsync(bbeg, bb.data(), sizeof(int64_t) * (W + 1), hipMemcpyHostToDevice, st));
+    Buf dest = dev_alloc(sizeof(uint64_t) * (nk > 0 ? nk : 1), s);
+    if (nk > 0)
+        hipLaunchKernelGGL(k_tri_dest_from, dim3(grid(s, nk)), dim3(256), 0, st, P<uint64_t>(keys), nk, hb, bbeg, W,
+                           P<uint64_t>(dest));
+    HIP_CHECK(hipGetLastError());
+    return exchange_words(s, P<uint64_t>(dest), P<uint64_t>(keys), nk, nout);
+}
+}  // namespace tri
+
 // Distributed (dd != null, multi-GPU C4): every rank builds from its 1/world of the
 // relationships and ends with the same replicated oriented graph.  The undirected keys go to the owner of
 // their lower end (one exchange), so each rank sorts 1/world of them and holds every relationship of its
@@ -2009,38 +2048,8 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
         if (dd) {
             // every relationship to the rank of its source's degree-order range (ranges balanced by the
             // all-reduced counts of a coarse source histogram): a pair's relationships meet on one rank
-            const int hb = bits > 12 ? bits - 12 : 0;
-            const int64_t nbins = ((n - 1) >> hb) + 1;
-            const int W = dd->world;
-            Buf hist = dev_alloc(sizeof(int64_t) * (kHistBins + W + 1), s);
-            HIP_CHECK(hipMemsetAsync(P<void>(hist), 0, sizeof(int64_t) * kHistBins, st));
-            if (m > 0)
-                hipLaunchKernelGGL(k_tri_from_hist, dim3(std::min(grid(s, m), 4 * s->num_cus)), dim3(1024), 0, st,
-                                   P<uint64_t>(key), m, hb, P<unsigned long long>(hist));
-            HIP_CHECK(hipGetLastError());
-            collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(hist), P<int64_t>(hist), kHistBins, CAPSMI_I64);
-            std::vector<int64_t> h(kHistBins), bb(W + 1);
-            HIP_CHECK(hipMemcpyAsync(h.data(), P<int64_t>(hist), sizeof(int64_t) * kHistBins, hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
-            int64_t tot = 0;
-            for (int64_t b = 0; b < nbins; ++b) tot += h[b];
-            int64_t cum = 0, b = 0;
-            bb[0] = 0;
-            for (int q = 1; q < W; ++q) {
-                const int64_t want = tot * q / W;
-                while (b < nbins && cum + h[b] <= want) cum += h[b++];
-                bb[q] = b;
-            }
-            bb[W] = nbins;
-            int64_t* bbeg = P<int64_t>(hist) + kHistBins;
-            HIP_CHECK(hipMemcpyAsync(bbeg, bb.data(), sizeof(int64_t) * (W + 1), hipMemcpyHostToDevice, st));
-            Buf dest = dev_alloc(sizeof(uint64_t) * (m > 0 ? m : 1), s);
-            if (m > 0)
-                hipLaunchKernelGGL(k_tri_dest_from, dim3(grid(s, m)), dim3(256), 0, st, P<uint64_t>(key), m, hb, bbeg, W,
-                                   P<uint64_t>(dest));
-            HIP_CHECK(hipGetLastError());
             int64_t mr = 0;
-            key = exchange_words(s, P<uint64_t>(dest), P<uint64_t>(key), m, &mr);
+            key = to_source_range_owner(s, key, m, bits, n, dd->world, &mr);
             m = mr;
         }
         // one sort of the raw oriented keys (the direction bit unsorted at bit 31), runs = the pairs
@@ -2208,38 +2217,8 @@ void tri_build(capsmi_session* s, const int64_t* const* srcs, const int64_t* con
             exc = gather_words(s, P<uint64_t>(exc), 2 * nexc, &nexc_all);
             fill_i64(reinterpret_cast<int64_t*>(nlong), nexc_all / 2, 1, st);
             // source ranges of coarse degree-order bins, balanced by the all-reduced bin counts
-            const int hb = bits > 12 ? bits - 12 : 0;
-            const int64_t nbins = ((n - 1) >> hb) + 1;
-            const int W = dd->world;
-            Buf hist = dev_alloc(sizeof(int64_t) * (kHistBins + W + 1), s);
-            HIP_CHECK(hipMemsetAsync(P<void>(hist), 0, sizeof(int64_t) * kHistBins, st));
-            if (ne > 0)
-                hipLaunchKernelGGL(k_tri_from_hist, dim3(std::min(grid(s, ne), 4 * s->num_cus)), dim3(1024), 0, st,
-                                   P<uint64_t>(g.ok), ne, hb, P<unsigned long long>(hist));
-            HIP_CHECK(hipGetLastError());
-            collective(s, CAPSMI_COLL_ALL_REDUCE_SUM, P<int64_t>(hist), P<int64_t>(hist), kHistBins, CAPSMI_I64);
-            std::vector<int64_t> h(kHistBins), bb(W + 1);
-            HIP_CHECK(hipMemcpyAsync(h.data(), P<int64_t>(hist), sizeof(int64_t) * kHistBins, hipMemcpyDeviceToHost, st));
-            HIP_CHECK(hipStreamSynchronize(st));
-            int64_t tot = 0;
-            for (int64_t b = 0; b < nbins; ++b) tot += h[b];
-            int64_t cum = 0, b = 0;
-            bb[0] = 0;
-            for (int q = 1; q < W; ++q) {
-                const int64_t want = tot * q / W;
-                while (b < nbins && cum + h[b] <= want) cum += h[b++];
-                bb[q] = b;
-            }
-            bb[W] = nbins;
-            int64_t* bbeg = P<int64_t>(hist) + kHistBins;
-            HIP_CHECK(hipMemcpyAsync(bbeg, bb.data(), sizeof(int64_t) * (W + 1), hipMemcpyHostToDevice, st));
-            Buf dest = dev_alloc(sizeof(uint64_t) * (ne > 0 ? ne : 1), s);
-            if (ne > 0)
-                hipLaunchKernelGGL(k_tri_dest_from, dim3(grid(s, ne)), dim3(256), 0, st, P<uint64_t>(g.ok), ne, hb, bbeg, W,
-                                   P<uint64_t>(dest));
-            HIP_CHECK(hipGetLastError());
             int64_t nr = 0;
-            Buf mine = exchange_words(s, P<uint64_t>(dest), P<uint64_t>(g.ok), ne, &nr);
+            Buf mine = to_source_range_owner(s, g.ok, ne, bits, n, dd->world, &nr);
             {
                 KernelTimer kt(s, "tri_sort_or");
                 radix_sort_digits(s, P<uint64_t>(mine), nullptr, nr, od);  // this rank's source range, sorted

@@ -1,6 +1,6 @@
 // k_varlen.hip -- fused BoundedVarLengthExpand + grouped count (C5), never materialising paths.
 //
-//   MATCH (a)-[r*lower..upper]->(b) WHERE a_ok(a) AND b_ok(b) RETURN id(a), count(*)   (0 <= lower <= upper <= 3,
+//   MATCH (a)-[r*lower..upper]->(b) WHERE a_ok(a) AND b_ok(b) RETURN id(a), count(*)   (0 <= lower <= upper <= 4,
 //   upper >= 1; lower = 0 adds the zero-length path, whose b is a copy of a without b's node scan)
 //
 // CAPS plans this as `upper` chained joins with an isomorphism filter per hop and a union over the
@@ -13,6 +13,7 @@
 //   len 2: sum_{r: a->b} od(b) - s(a) b_ok(a)
 //   len 3: sum_{r: a->b} [W(b) - (m(b,a) + s(b)) b_ok(b)] - s(a) (od(a) - 2 b_ok(a))
 // Four streaming passes over the relationship table plus one hash probe per relationship for m(b,a).
+// Four hops (round 6): var_length4 below.
 #include <cstdlib>
 
 #include "part_common.h"
@@ -89,7 +90,8 @@ __global__ void k_t(const int64_t* __restrict__ src, const int64_t* __restrict__
 // pass 4: per node, the count over lengths lower..upper; flags rows with count > 0
 __global__ void k_final(int64_t n, Dom d, int lower, int upper, const unsigned long long* __restrict__ od,
                         const unsigned long long* __restrict__ s, const unsigned long long* __restrict__ T2,
-                        const unsigned long long* __restrict__ T3, int64_t* __restrict__ cnt, uint8_t* __restrict__ f,
+                        const unsigned long long* __restrict__ T3, const unsigned long long* __restrict__ L4,
+                        int64_t* __restrict__ cnt, uint8_t* __restrict__ f,
                         int64_t own_lo, int64_t own_hi) {  // rows only for the owned a (relative [own_lo, own_hi))
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t a = d.lo + i;
@@ -103,6 +105,7 @@ __global__ void k_final(int64_t n, Dom d, int lower, int upper, const unsigned l
             if (lower <= 1 && upper >= 1) total += c1;
             if (lower <= 2 && upper >= 2) total += c2;
             if (lower <= 3 && upper >= 3) total += c3;
+            if (L4 && lower <= 4 && upper >= 4) total += (int64_t)L4[i];  // var_length4
         }
         cnt[i] = total;
         f[i] = total > 0 && i >= own_lo && i < own_hi ? 1 : 0;
@@ -689,6 +692,216 @@ void zero_words(capsmi_session* s, std::initializer_list<std::pair<void*, int64_
     hipLaunchKernelGGL(k_vl_zero, dim3(grid(s, nmax), k), dim3(256), 0, s->stream, z);
 }
 
+// ---- four hops ----------------------------------------------------------------------------------------
+// len 4 (a) = the relationship-distinct 4-hop paths a -> ... -> z with b_ok(z), by inclusion-exclusion over
+// the 15 set partitions of the hop positions {1,2,3,4} (Mobius weights prod (-1)^(|B|-1) (|B|-1)!; pinned
+// against path enumeration in the oracle, oracle/cpu.py var_length4_closed_form).  A block {i, j} forces
+// r_i = r_j, so the walk between them is closed: adjacent positions a self-loop, {1,3} / {2,4} a reciprocal
+// pair, {1,4} a 2-walk back along the relationship.  With A the multiplicity matrix, b the end filter,
+// s the self-loops, M(x, y) = m(x, y) m(y, x) and od = A b, W = A od (the len-3 vectors):
+//   len4 = A^4 b - [s W + A (s od) + A A (s b)] - [M od + A M b + T14] + [2 s^2 b + b M 1]
+//          + 2 [s od + 2 s^2 b + A (s b)] - 6 s b,          T14(a) = sum_{r: a -> y} b(y) sum_{r': y -> p} m(p, a)
+// Every term but T14 is a product of per-node vectors over the relationships (atomic passes) and of the
+// pair multiplicities (an exact pair table); T14 walks the 2-hop wedges a -> y -> p in balanced chunks and
+// looks each closing pair (p, a) up in the table.  Relative ids below 2^24 - 1 (the table's keys).
+struct Vl4 {  // per-node u64 sums (two's complement)
+    unsigned long long *X, *Q1, *P, *W4, *Q2, *Rb, *R1, *MAb, *ARb, *T14;
+};
+
+// per relationship x -> y: X = A W, Q1 = A (s b), P = A (s od); every pair into the table
+__global__ void k_vl4_a(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, Dom d,
+                        const unsigned long long* __restrict__ od, const unsigned long long* __restrict__ s,
+                        const unsigned long long* __restrict__ W, PairHash h, Vl4 v) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = src[e], y = dst[e];
+        if (!in_dom(d, x) || !in_dom(d, y)) continue;
+        const int64_t xi = x - d.lo, yi = y - d.lo;
+        if (W[yi]) atomicAdd(&v.X[xi], W[yi]);
+        const unsigned long long sy = s[yi];
+        if (sy) {
+            if (bok(d, y)) atomicAdd(&v.Q1[xi], sy);
+            if (od[yi]) atomicAdd(&v.P[xi], sy * od[yi]);
+        }
+        pair_insert(h, hkey((uint32_t)xi, (uint32_t)yi));
+    }
+}
+
+// per relationship x -> y: W4 = A X, Q2 = A Q1, and with r = m(y, x): Rb = M b, R1 = M 1, MAb = M od
+__global__ void k_vl4_b(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, Dom d,
+                        const unsigned long long* __restrict__ od, PairHash h, Vl4 v) {
+    const bool ovf = *h.any_ovf != 0;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = src[e], y = dst[e];
+        if (!in_dom(d, x) || !in_dom(d, y)) continue;
+        const int64_t xi = x - d.lo, yi = y - d.lo;
+        if (v.X[yi]) atomicAdd(&v.W4[xi], v.X[yi]);
+        if (v.Q1[yi]) atomicAdd(&v.Q2[xi], v.Q1[yi]);
+        const unsigned long long r = pair_count(h, hkey((uint32_t)yi, (uint32_t)xi), ovf);
+        if (r) {
+            if (bok(d, y)) atomicAdd(&v.Rb[xi], r);
+            atomicAdd(&v.R1[xi], r);
+            if (od[yi]) atomicAdd(&v.MAb[xi], r * od[yi]);
+        }
+    }
+}
+
+// per relationship x -> y: ARb = A Rb
+__global__ void k_vl4_c(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, Dom d, Vl4 v) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = src[e], y = dst[e];
+        if (!in_dom(d, x) || !in_dom(d, y)) continue;
+        const unsigned long long r = v.Rb[y - d.lo];
+        if (r) atomicAdd(&v.ARb[x - d.lo], r);
+    }
+}
+
+// the relationships as (source << 24 | target) keys, relative ids (outside the domain: ~0, sorted last)
+__global__ void k_vl4_keys(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, Dom d,
+                           uint64_t* __restrict__ key) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = src[e], y = dst[e];
+        key[e] = in_dom(d, x) && in_dom(d, y) ? ((uint64_t)(x - d.lo) << 24) | (uint64_t)(y - d.lo) : ~0ULL;
+    }
+}
+
+// CSR offsets of the sorted keys (the first key whose source is >= v), and per key its wedge count
+// b(y) * od_all(y) (od_all from the same offsets: every relationship out of y)
+__global__ void k_vl4_off(const uint64_t* __restrict__ key, int64_t m, int64_t n, int64_t* __restrict__ off) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= n; v += (int64_t)gridDim.x * blockDim.x) {
+        int64_t lo = 0, hi = m;
+        const uint64_t t = (uint64_t)v << 24;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (key[mid] < t) lo = mid + 1; else hi = mid;
+        }
+        off[v] = lo;
+    }
+}
+
+__global__ void k_vl4_wcount(const uint64_t* __restrict__ key, int64_t mv, Dom d, const int64_t* __restrict__ off,
+                             int64_t* __restrict__ wc) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < mv; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t y = (int64_t)(key[e] & 0xFFFFFF);
+        wc[e] = bok(d, d.lo + y) ? off[y + 1] - off[y] : 0;
+    }
+}
+
+// T14: each lane takes kVl4Chunk consecutive wedges (r, r') in key order -- r = a -> y, r' = y -> p -- finds
+// its first r by a search over the wedge prefix, then walks; a lane's sum for one a is added once
+constexpr int kVl4Chunk = 128;
+__global__ void k_vl4_wedges(const uint64_t* __restrict__ key, int64_t mv, const int64_t* __restrict__ off,
+                             const int64_t* __restrict__ wpre, PairHash h, unsigned long long* __restrict__ T14) {
+    const bool ovf = *h.any_ovf != 0;
+    const int64_t total = wpre[mv];
+    for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c * kVl4Chunk < total;
+         c += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t w0 = c * kVl4Chunk, w1 = min(total, w0 + kVl4Chunk);
+        int64_t lo = 0, hi = mv;  // the last r with wpre[r] <= w0
+        while (hi - lo > 1) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (wpre[mid] <= w0) lo = mid; else hi = mid;
+        }
+        int64_t r = lo;
+        uint32_t a = (uint32_t)(key[r] >> 24);
+        unsigned long long acc = 0;
+        for (int64_t w = w0; w < w1; ++w) {
+            while (wpre[r + 1] <= w) ++r;
+            const uint64_t k = key[r];
+            const uint32_t ar = (uint32_t)(k >> 24), y = (uint32_t)(k & 0xFFFFFF);
+            if (ar != a) {
+                if (acc) atomicAdd(&T14[a], acc);
+                acc = 0;
+                a = ar;
+            }
+            const uint32_t p = (uint32_t)(key[off[y] + (w - wpre[r])] & 0xFFFFFF);
+            acc += pair_count(h, hkey(p, a), ovf);
+        }
+        if (acc) atomicAdd(&T14[a], acc);
+    }
+}
+
+__global__ void k_vl4_sum(int64_t n, Dom d, const unsigned long long* __restrict__ od,
+                          const unsigned long long* __restrict__ s, const unsigned long long* __restrict__ W, Vl4 v,
+                          unsigned long long* __restrict__ L4) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t a = d.lo + i;
+        if (!aok(d, a)) {
+            L4[i] = 0;
+            continue;
+        }
+        const unsigned long long b = bok(d, a) ? 1 : 0, si = s[i], o = od[i];
+        const unsigned long long pair1 = si * W[i] + v.P[i] + v.Q2[i];
+        const unsigned long long pair2 = v.MAb[i] + v.ARb[i] + v.T14[i];
+        const unsigned long long two = 2 * si * si * b + b * v.R1[i];
+        const unsigned long long three = si * o + 2 * si * si * b + v.Q1[i];
+        L4[i] = v.W4[i] - pair1 - pair2 + two + 2 * three - 6 * si * b;  // exact mod 2^64, the count fits
+    }
+}
+
+// L4 (n u64): the per-node 4-hop counts, from od / s / W of the len-3 passes; ids below 2^24 - 1
+void var_length4(capsmi_session* s, const int64_t* const* srcs, const int64_t* const* dsts, const int64_t* ms, int nt,
+                 const Dom& d, const unsigned long long* od, const unsigned long long* sl, const unsigned long long* W,
+                 unsigned long long* L4) {
+    hipStream_t st = s->stream;
+    const int64_t n = d.hi - d.lo;
+    REQUIRE(n < (int64_t(1) << 24) - 1, CAPSMI_ERR_UNSUPPORTED, "fused var-length upper 4: at most 2^24 - 2 ids");
+    KernelTimer kt(s, "varlen_4");
+    int64_t mtot = 0;
+    for (int i = 0; i < nt; ++i) mtot += ms[i] > 0 ? ms[i] : 0;
+    const size_t nb = sizeof(unsigned long long) * (n > 0 ? n : 1);
+    Buf acc = dev_alloc(nb * 10, s);
+    HIP_CHECK(hipMemsetAsync(P<void>(acc), 0, nb * 10, st));
+    unsigned long long* base = P<unsigned long long>(acc);
+    const int64_t nw = (int64_t)(nb / sizeof(unsigned long long));
+    Vl4 v{base, base + nw, base + 2 * nw, base + 3 * nw, base + 4 * nw, base + 5 * nw, base + 6 * nw, base + 7 * nw,
+          base + 8 * nw, base + 9 * nw};
+    // the exact pair table of every relationship: a power of two >= 2 * mtot slots
+    int64_t cap = 1024;
+    while (cap < 2 * mtot) cap <<= 1;
+    const size_t hbytes = (sizeof(unsigned long long) + sizeof(unsigned int)) * cap + 16;
+    Buf hk = dev_alloc(hbytes, s);
+    HIP_CHECK(hipMemsetAsync(P<void>(hk), 0, hbytes, st));
+    unsigned int* hcw = reinterpret_cast<unsigned int*>(P<unsigned long long>(hk) + cap);
+    const PairHash h{P<unsigned long long>(hk), hcw, hcw + cap, (unsigned long long)(cap - 1)};
+    for (int i = 0; i < nt; ++i)
+        if (ms[i] > 0)
+            hipLaunchKernelGGL(k_vl4_a, dim3(grid(s, ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], d, od, sl, W, h, v);
+    for (int i = 0; i < nt; ++i)
+        if (ms[i] > 0) hipLaunchKernelGGL(k_vl4_b, dim3(grid(s, ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], d, od, h, v);
+    for (int i = 0; i < nt; ++i)
+        if (ms[i] > 0) hipLaunchKernelGGL(k_vl4_c, dim3(grid(s, ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], d, v);
+    HIP_CHECK(hipGetLastError());
+    if (mtot > 0) {  // T14 over the wedges, the relationships sorted by (source, target)
+        Buf key = dev_alloc(sizeof(uint64_t) * mtot, s);
+        int64_t off0 = 0;
+        for (int i = 0; i < nt; ++i) {
+            if (ms[i] > 0)
+                hipLaunchKernelGGL(k_vl4_keys, dim3(grid(s, ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], d,
+                                   P<uint64_t>(key) + off0);
+            off0 += ms[i] > 0 ? ms[i] : 0;
+        }
+        std::vector<int> shifts;  // 48 key bits; the out-of-domain keys (~0) sort after every valid one
+        for (int sh = 0; sh < 48; sh += 8) shifts.push_back(sh);
+        radix_sort_keys(s, key, mtot, shifts);
+        Buf off = dev_alloc(sizeof(int64_t) * (n + 2), s);
+        hipLaunchKernelGGL(k_vl4_off, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(key), mtot, n, P<int64_t>(off));
+        const int64_t mv = read_scalar(s, P<int64_t>(off) + n);  // the keys inside the domain
+        if (mv > 0) {
+            Buf wc = dev_alloc(sizeof(int64_t) * mv, s), wpre = dev_alloc(sizeof(int64_t) * (mv + 1), s);
+            hipLaunchKernelGGL(k_vl4_wcount, dim3(grid(s, mv)), dim3(256), 0, st, P<uint64_t>(key), mv, d, P<int64_t>(off),
+                               P<int64_t>(wc));
+            exclusive_scan_i64(P<int64_t>(wc), P<int64_t>(wpre), mv, s);
+            const int64_t total = read_scalar(s, P<int64_t>(wpre) + mv);
+            const int64_t chunks = (total + kVl4Chunk - 1) / kVl4Chunk;
+            if (chunks > 0)
+                hipLaunchKernelGGL(k_vl4_wedges, dim3(grid(s, chunks)), dim3(256), 0, st, P<uint64_t>(key), mv,
+                                   P<int64_t>(off), P<int64_t>(wpre), h, v.T14);
+        }
+    }
+    hipLaunchKernelGGL(k_vl4_sum, dim3(grid(s, n)), dim3(256), 0, st, n, d, od, sl, W, v, L4);
+    HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace varlen
 
 // rows (a, count) of the fused var-length grouped count; returns the table's row count
@@ -883,10 +1096,16 @@ int64_t var_length_count(capsmi_session* s, const int64_t* const* srcs, const in
         }
     }
     }  // atomic passes
+    Buf L4;
+    if (upper >= 4 && n > 0) {  // four hops: from od / sl / W
+        L4 = dev_alloc(nb, s);
+        var_length4(s, srcs, dsts, ms, nt, d, P<unsigned long long>(od), P<unsigned long long>(sl),
+                    P<unsigned long long>(W), P<unsigned long long>(L4));
+    }
     Buf cnt = dev_alloc(nb, s), flags = dev_alloc(n > 0 ? n : 1, s);
     hipLaunchKernelGGL(k_final, dim3(grid(s, n)), dim3(256), 0, st, n, d, lower, upper, P<unsigned long long>(od),
                        P<unsigned long long>(sl), P<unsigned long long>(T2), P<unsigned long long>(T3),
-                       P<int64_t>(cnt), P<uint8_t>(flags), (int64_t)0, n);
+                       P<unsigned long long>(L4), P<int64_t>(cnt), P<uint8_t>(flags), (int64_t)0, n);
     HIP_CHECK(hipGetLastError());
     // rows (lo + i, cnt[i]) of the flagged a, written before the count is read
     return flags_to_rows(s, P<uint8_t>(flags), n, P<int64_t>(cnt), d.lo, out_ids, out_cnt);
@@ -1097,8 +1316,8 @@ int64_t varlen_shard_finish(VarlenShard* v, Buf& out_ids, Buf& out_cnt) {
     Buf cnt = dev_alloc(sizeof(int64_t) * n, s), flags = dev_alloc(n, s);
     hipLaunchKernelGGL(k_final, dim3(grid(s, n)), dim3(256), 0, st, n, v->d, v->lower, v->upper,
                        reinterpret_cast<const unsigned long long*>(v->od), P<unsigned long long>(v->sl),
-                       P<unsigned long long>(v->T2), P<unsigned long long>(v->T3), P<int64_t>(cnt), P<uint8_t>(flags),
-                       v->own_lo, v->own_hi);
+                       P<unsigned long long>(v->T2), P<unsigned long long>(v->T3), (const unsigned long long*)nullptr,
+                       P<int64_t>(cnt), P<uint8_t>(flags), v->own_lo, v->own_hi);
     HIP_CHECK(hipGetLastError());
     return flags_to_rows(s, P<uint8_t>(flags), n, P<int64_t>(cnt), v->d.lo, out_ids, out_cnt);
 }

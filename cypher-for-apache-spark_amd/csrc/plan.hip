@@ -13,7 +13,7 @@
 //   Expand + node filters, count(*) ......................... expand count              ("expand_count")
 //   2 x Expand + uniqueness, count(*) / count(DISTINCT end) . two-hop kernels           ("two_hop")
 //   2 x Expand + ExpandInto closing a cycle, count(*) ....... triangle count            ("triangle")
-//   var-length 1 <= l <= u <= 3, grouped count(*) by start .. var-length count          ("var_length")
+//   var-length 0 <= l <= u <= 4, grouped count(*) by start .. var-length count          ("var_length")
 // over registered entity tables (capsmi_node_table / capsmi_rel_table), and otherwise runs the
 // operators one by one (api.hip eager_*).  Node predicates become node-scan bitmaps; ids must be
 // unique per scan and inside one window of at most 2^30 ids, else the plan runs unfused.
@@ -1621,7 +1621,9 @@ bool fused_var_length(capsmi_session* s, const capsmi_table* in, const PlanNode&
     }
     if (first || (lens.count(0) && zero_key != akey)) return false;  // a path of >= 1 hop; one start scan
     const int l = *lens.begin(), u = *lens.rbegin();
-    if (l < 0 || u > 3 || u - l + 1 != (int)lens.size()) return false;
+    // upper 4 on one device (var_length4, ids below 2^24 - 1); the sharded form stops at 3
+    if (l < 0 || u > (g_dist.on ? 3 : 4) || u - l + 1 != (int)lens.size()) return false;
+    if (u == 4 && hi - lo >= (int64_t(1) << 24) - 1) return false;
     if (g_dist.on) dist_var_length(s, views.t, bases, abm, bbm, l, u, g.a[0], ag.output, out);
     else
         check(capsmi_var_length_count(s, (int32_t)views.t.size(), views.t.data(), "s", "t", abm, bbm, l, u,

@@ -462,8 +462,8 @@ capsmi_status capsmi_undirected_count(capsmi_session* s, int32_t nrels, capsmi_t
                                       const capsmi_bitmap* b_ok, const capsmi_bitmap* c_ok, int32_t kind, int64_t* out);
 /* BoundedVarLengthExpand + grouped count, fused (C5):
  *   MATCH (a)-[r*lower..upper]->(b) WHERE a_ok(a) AND b_ok(b) RETURN id(a) AS <id_name>, count(*) AS <count_name>
- * with edge-distinct paths (VarLengthExpandPlanner.scala:83-136, 179-180), 0 <= lower <= upper <= 3,
- * upper >= 1.  lower = 0 adds the zero-length path of every a_ok node (copyEntity, :146-153, 190-210:
+ * with edge-distinct paths (VarLengthExpandPlanner.scala:83-136, 179-180), 0 <= lower <= upper <= 4,
+ * upper >= 1 (upper 4: ids below 2^24 - 1).  lower = 0 adds the zero-length path of every a_ok node (copyEntity, :146-153, 190-210:
  * b is a copy of a, without b's node scan).  One output row per a with at least one path.  a_ok and
  * b_ok must share one id domain. */
 capsmi_status capsmi_var_length_count(capsmi_session* s, int32_t nrels, capsmi_table* const* rels,

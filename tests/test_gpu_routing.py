@@ -186,6 +186,23 @@ def test_c5_var_length_routed(session, lo, hi):
         assert same_rows(_run(session, sg, q, fused=False), want)
 
 
+@pytest.mark.parametrize("lo,hi", [(1, 4), (0, 4), (4, 4)])
+def test_c5_four_hops_routed(session, lo, hi):
+    """upper = 4 routes to the fused count on one device (var_length4) and equals enumeration."""
+    from oracle import cpu
+    scale = 6
+    sg = _graph(session, scale, ef=32, probs=(45, 15, 15), rtype="KNOWS")
+    q = {"clauses": [{"match": f"(a:Person)-[:KNOWS*{lo}..{hi}]->(b:Person)"}],
+         "return": {"items": [["a", ["id", "a"]], ["n", ["count*"]]]}}
+    got = _routed(session, "var_length", lambda: _run(session, sg, q))
+    src, dst = cpu.rmat_edges(scale, 0, 32 << scale, (45, 15, 15), 42)
+    _, per_a = cpu.var_length_count(1 << scale, src, dst, max(lo, 1), hi)
+    if lo == 0:
+        per_a = per_a + 1
+    want = [{"a": int(i), "n": int(per_a[i])} for i in np.nonzero(per_a)[0]]
+    assert same_rows(got, want)
+
+
 def test_expand_count_routed(session):
     from oracle import cpu
     scale = 10

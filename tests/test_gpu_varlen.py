@@ -301,3 +301,89 @@ def test_dense_reciprocal_candidates(session, knobs, f2):
         want = {int(i): int(g[i]) for i in np.nonzero(g)[0]}
         got = dict(zip(out.column("a").values.tolist(), out.column("cnt").values.tolist()))
         assert got == want
+
+
+# ---- four hops (var_length4, oracle/cpu.py var_length4_closed_form) ----------------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(6))
+def test_four_hops_random_multigraphs(session, seed):
+    """upper = 4: self-loops, reciprocal pairs, multi-edges and both node filters against enumeration."""
+    rng = np.random.default_rng(40 + seed)
+    n = int(rng.integers(5, 120))
+    m = int(rng.integers(0, 1000))
+    src = rng.integers(0, n, m).astype(np.int64)
+    dst = rng.integers(0, n, m).astype(np.int64)
+    src[: m // 6] = dst[: m // 6]  # self-loops
+    k = m // 6
+    src[k:2 * k], dst[k:2 * k] = dst[2 * k:3 * k].copy(), src[2 * k:3 * k].copy()  # reciprocal pairs
+    a_mask = rng.random(n) < 0.7
+    b_mask = rng.random(n) < 0.6
+    for lo, hi in [(1, 4), (4, 4), (2, 4), (3, 4)]:
+        _check(session, n, src, dst, a_mask, b_mask, lo, hi)
+
+
+@pytest.mark.gpu
+def test_four_hops_ldbc_shaped_rmat(session):
+    from capsmi import graph
+    scale = 7
+    n, m = 1 << scale, 32 << scale
+    rels = graph.rmat_rels(session, scale, 0, m, graph.RMAT_LDBC, 42)
+    src, dst = cpu.rmat_edges(scale, 0, m, graph.RMAT_LDBC, 42)
+    ones = np.ones(n, dtype=bool)
+    _check(session, n, src, dst, ones, ones, 1, 4, rels=[rels])
+    _check(session, n, src, dst, ones, ones, 4, 4, rels=[rels])
+
+
+@pytest.mark.gpu
+def test_four_hops_split_tables_and_source_slices(session):
+    """Two relationship tables, a domain of several 8192-id source slices (the len <= 3 vectors from the sliced
+    passes), hubs and reciprocal copies."""
+    rng = np.random.default_rng(77)
+    n, m = 20_000, 30_000
+    src = rng.integers(0, n, m).astype(np.int64)
+    dst = rng.integers(0, n, m).astype(np.int64)
+    k = m // 5
+    src[k:2 * k], dst[k:2 * k] = dst[:k].copy(), src[:k].copy()
+    src[-200:] = dst[-200:]
+    t1, t2 = _table(session, src[:9000], dst[:9000]), _table(session, src[9000:], dst[9000:])
+    a_mask = rng.random(n) < 0.8
+    b_mask = rng.random(n) < 0.7
+    _check(session, n, src, dst, a_mask, b_mask, 1, 4, rels=[t1, t2])
+
+
+@pytest.mark.gpu
+def test_four_hops_pair_multiplicity_over_16_bits(session):
+    """The pair table's 16-bit counts wrap into the overflow word (a pair of 70,000 relationships)."""
+    from capsmi import ColumnData, I64, graph
+    rng = np.random.default_rng(23)
+    n = 30
+    pairs = [(3, 7, 70_000), (7, 3, 5), (3, 9, 2), (9, 3, 40), (9, 9, 3)]
+    src = [rng.integers(0, n, 300)]
+    dst = [rng.integers(0, n, 300)]
+    for u, v, c in pairs:
+        src.append(np.full(c, u))
+        dst.append(np.full(c, v))
+    src, dst = np.concatenate(src).astype(np.int64), np.concatenate(dst).astype(np.int64)
+    perm = rng.permutation(len(src))
+    src, dst = src[perm], dst[perm]
+    a_mask = np.ones(n, dtype=bool)
+    b_mask = rng.random(n) < 0.8
+    b_mask[[3, 7, 9]] = True
+    rels = [_table(session, src, dst)]
+    a_ok = graph.NodeBitmap(session, 0, n).add_scan(session.table([ColumnData("id", I64, np.arange(n))]))
+    b_ok = graph.NodeBitmap(session, 0, n).add_scan(session.table([ColumnData("id", I64, np.nonzero(b_mask)[0])]))
+    out = graph.var_length_count(session, rels, a_ok, b_ok, 4, 4, "a", "cnt")
+    got = dict(zip(out.column("a").values.tolist(), out.column("cnt").values.tolist()))
+    assert got == _pair_paths(n, src, dst, a_mask, b_mask, 4, 4)
+
+
+@pytest.mark.gpu
+def test_four_hops_refused_above_2_24_ids(session):
+    from capsmi import ColumnData, I64, graph
+    from capsmi._lib import UnsupportedOperationException
+    n = (1 << 24) + 77
+    rels = [_table(session, np.array([0, 1], np.int64), np.array([1, 2], np.int64))]
+    ok = graph.NodeBitmap(session, 0, n).add_scan(session.table([ColumnData("id", I64, np.arange(3))]))
+    with pytest.raises(UnsupportedOperationException, match="2\\^24"):
+        graph.var_length_count(session, rels, ok, ok, 1, 4, "a", "cnt")
