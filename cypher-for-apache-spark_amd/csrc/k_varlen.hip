@@ -786,13 +786,38 @@ __global__ void k_vl4_wcount(const uint64_t* __restrict__ key, int64_t mv, Dom d
     }
 }
 
+// the in-lists: the (source, target)-sorted keys re-sorted (stably) by target, so each target's sources
+// ascend; isrc = the sources, ioff[v] = the first whose target is >= v; tg = the out-list targets (4 bytes)
+__global__ void k_vl4_lists(const uint64_t* __restrict__ key, const uint64_t* __restrict__ ik, int64_t mv,
+                            uint32_t* __restrict__ tg, uint32_t* __restrict__ isrc) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < mv; e += (int64_t)gridDim.x * blockDim.x) {
+        tg[e] = (uint32_t)(key[e] & 0xFFFFFF);
+        isrc[e] = (uint32_t)(ik[e] >> 24);
+    }
+}
+
+__global__ void k_vl4_ioff(const uint64_t* __restrict__ ik, int64_t mv, int64_t n, int64_t* __restrict__ ioff) {
+    for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v <= n; v += (int64_t)gridDim.x * blockDim.x) {
+        int64_t lo = 0, hi = mv;
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if ((int64_t)(ik[mid] & 0xFFFFFF) < v) lo = mid + 1; else hi = mid;
+        }
+        ioff[v] = lo;
+    }
+}
+
 // T14: a wave takes 64 * kVl4Rounds consecutive wedges (r, r') in key order -- r = a -> y, r' = y -> p -- and
 // lane l the wedges wb + l + 64 k, so the lanes read consecutive entries of y's out-list together (coalesced);
-// a lane finds its first r by a search over the wedge prefix and then advances; its sum for one a is added once
+// a lane finds its first r by a search over the wedge prefix and then advances.  m(p, a) is the number of p's
+// in a's sorted in-list: a binary search there, the wave's lanes mostly on the same a (one list, cached lines)
+// -- closing pairs are rare (under 0.1 % of the wedges at C5), so most searches end on the list's bounds or
+// after a few cached probes instead of a random probe of the pair table.  A lane's sum for one a is added once.
 constexpr int kVl4Rounds = 16;
-__global__ void k_vl4_wedges(const uint64_t* __restrict__ key, int64_t mv, const int64_t* __restrict__ off,
-                             const int64_t* __restrict__ wpre, PairHash h, unsigned long long* __restrict__ T14) {
-    const bool ovf = *h.any_ovf != 0;
+__global__ void k_vl4_wedges(const uint64_t* __restrict__ key, const uint32_t* __restrict__ tg, int64_t mv,
+                             const int64_t* __restrict__ off, const int64_t* __restrict__ wpre,
+                             const uint32_t* __restrict__ isrc, const int64_t* __restrict__ ioff,
+                             unsigned long long* __restrict__ T14) {
     const int64_t total = wpre[mv];
     const int lane = threadIdx.x & 63;
     constexpr int64_t kSpan = 64 * kVl4Rounds;
@@ -806,105 +831,43 @@ __global__ void k_vl4_wedges(const uint64_t* __restrict__ key, int64_t mv, const
             const int64_t mid = (lo + hi) >> 1;
             if (wpre[mid] <= w0) lo = mid; else hi = mid;
         }
-        int64_t r = lo;
-        uint64_t k = key[r];
-        int64_t r_end = wpre[r + 1];
-        uint32_t a = (uint32_t)(k >> 24);
+        int64_t r = lo, r_end = wpre[r + 1], r_w = wpre[r];
+        uint32_t a = (uint32_t)(key[r] >> 24), y = tg[r];
+        int64_t i0 = ioff[a], i1 = ioff[a + 1];
+        uint32_t pmin = i1 > i0 ? isrc[i0] : 1u, pmax = i1 > i0 ? isrc[i1 - 1] : 0u;
+        int64_t oy = off[y];
         unsigned long long acc = 0;
         for (int64_t w = w0; w < we; w += 64) {
             if (w >= r_end) {
                 do { ++r; } while (wpre[r + 1] <= w);
-                k = key[r];
+                r_w = wpre[r];
                 r_end = wpre[r + 1];
-                const uint32_t ar = (uint32_t)(k >> 24);
+                y = tg[r];
+                oy = off[y];
+                const uint32_t ar = (uint32_t)(key[r] >> 24);
                 if (ar != a) {
                     if (acc) atomicAdd(&T14[a], acc);
                     acc = 0;
                     a = ar;
+                    i0 = ioff[a];
+                    i1 = ioff[a + 1];
+                    pmin = i1 > i0 ? isrc[i0] : 1u;
+                    pmax = i1 > i0 ? isrc[i1 - 1] : 0u;
                 }
             }
-            const uint32_t y = (uint32_t)(k & 0xFFFFFF);
-            const uint32_t p = (uint32_t)(key[off[y] + (w - wpre[r])] & 0xFFFFFF);
-            acc += pair_count(h, hkey(p, a), ovf);
+            const uint32_t p = tg[oy + (w - r_w)];
+            if (p < pmin || p > pmax) continue;
+            int64_t l = i0, h = i1;  // the first source >= p
+            while (l < h) {
+                const int64_t mid = (l + h) >> 1;
+                if (isrc[mid] < p) l = mid + 1; else h = mid;
+            }
+            while (l < i1 && isrc[l] == p) {
+                ++acc;
+                ++l;
+            }
         }
         if (acc) atomicAdd(&T14[a], acc);
-    }
-}
-
-// Hub starts (the ones with the most wedges): one workgroup per a holds a's in-neighbour set as an LDS bitmap
-// over the whole domain (n <= 2^20 ids: 128 KiB), so a wedge a -> y -> p is a bit test; only the closing pairs
-// present are probed in the pair table for their multiplicity.  The other starts keep k_vl4_wedges.
-constexpr int kVl4HubBlock = 1024;
-constexpr int64_t kVl4HubIds = int64_t(1) << 20;
-
-__global__ void k_vl4_hubflags(int64_t n, const int64_t* __restrict__ off, const int64_t* __restrict__ wpre,
-                               int64_t thr, uint8_t* __restrict__ f) {
-    for (int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; a < n; a += (int64_t)gridDim.x * blockDim.x)
-        f[a] = wpre[off[a + 1]] - wpre[off[a]] >= thr ? 1 : 0;
-}
-
-// the non-hub wedge counts (a hub's relationships walk no wedges in k_vl4_wedges) and the in-keys
-// (target << 24 | source) of the in-domain relationships
-__global__ void k_vl4_split(const uint64_t* __restrict__ key, int64_t mv, const uint8_t* __restrict__ hub,
-                            int64_t* __restrict__ wc, uint64_t* __restrict__ ikey) {
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < mv; e += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = key[e];
-        if (hub[k >> 24]) wc[e] = 0;
-        ikey[e] = ((k & 0xFFFFFF) << 24) | (k >> 24);
-    }
-}
-
-__global__ void __launch_bounds__(kVl4HubBlock) k_vl4_hub(const int64_t* __restrict__ hubs, int64_t nh, int64_t n,
-                                                         const uint64_t* __restrict__ key, const int64_t* __restrict__ off,
-                                                         const uint64_t* __restrict__ ikey,
-                                                         const int64_t* __restrict__ ioff,
-                                                         const int64_t* __restrict__ wpre, PairHash h,
-                                                         unsigned long long* __restrict__ T14) {
-    extern __shared__ uint32_t inb[];  // (n + 31) / 32 words
-    __shared__ unsigned long long part[kVl4HubBlock / 64];
-    const bool ovf = *h.any_ovf != 0;
-    const int64_t nw = (n + 31) / 32;
-    for (int64_t q = blockIdx.x; q < nh; q += gridDim.x) {  // block-uniform
-        const uint32_t a = (uint32_t)hubs[q];
-        for (int64_t i = threadIdx.x; i < nw; i += kVl4HubBlock) inb[i] = 0;
-        __syncthreads();
-        for (int64_t e = ioff[a] + threadIdx.x; e < ioff[a + 1]; e += kVl4HubBlock) {
-            const uint32_t p = (uint32_t)(ikey[e] & 0xFFFFFF);
-            atomicOr(&inb[p >> 5], 1u << (p & 31));
-        }
-        __syncthreads();
-        // a's wedges [w0, w1), over a's relationships only
-        const int64_t r0 = off[a], r1 = off[a + 1], w0 = wpre[r0], w1 = wpre[r1];
-        unsigned long long acc = 0;
-        // lane t takes the wedges w0 + t + 1024 k: consecutive lanes read consecutive out-list entries
-        if (w0 + (int64_t)threadIdx.x < w1) {
-            const int64_t ws = w0 + (int64_t)threadIdx.x;
-            int64_t lo = r0, hi = r1;  // the last r with wpre[r] <= ws
-            while (hi - lo > 1) {
-                const int64_t mid = (lo + hi) >> 1;
-                if (wpre[mid] <= ws) lo = mid; else hi = mid;
-            }
-            int64_t r = lo, r_end = wpre[r + 1];
-            uint32_t y = (uint32_t)(key[r] & 0xFFFFFF);
-            for (int64_t w = ws; w < w1; w += kVl4HubBlock) {
-                if (w >= r_end) {
-                    do { ++r; } while (wpre[r + 1] <= w);
-                    r_end = wpre[r + 1];
-                    y = (uint32_t)(key[r] & 0xFFFFFF);
-                }
-                const uint32_t p = (uint32_t)(key[off[y] + (w - wpre[r])] & 0xFFFFFF);
-                if ((inb[p >> 5] >> (p & 31)) & 1u) acc += pair_count(h, hkey(p, a), ovf);
-            }
-        }
-        for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
-        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long t = 0;
-            for (int k = 0; k < kVl4HubBlock / 64; ++k) t += part[k];
-            if (t) atomicAdd(&T14[a], t);
-        }
-        __syncthreads();  // inb and part are reused by the next hub
     }
 }
 
@@ -979,39 +942,21 @@ void var_length4(capsmi_session* s, const int64_t* const* srcs, const int64_t* c
             hipLaunchKernelGGL(k_vl4_wcount, dim3(grid(s, mv)), dim3(256), 0, st, P<uint64_t>(key), mv, d, P<int64_t>(off),
                                P<int64_t>(wc));
             exclusive_scan_i64(P<int64_t>(wc), P<int64_t>(wpre), mv, s);
-            // hub starts (at least n / 512 wedges each, domains of at most 2^20 ids): the LDS in-neighbour bitmaps
-            const int64_t thr = std::max<int64_t>(n / 512, 1024);
-            int64_t nh = 0;
-            Buf hubs, wpre2;
-            if (n <= kVl4HubIds) {
-                Buf f = dev_alloc(n, s);
-                hipLaunchKernelGGL(k_vl4_hubflags, dim3(grid(s, n)), dim3(256), 0, st, n, P<int64_t>(off), P<int64_t>(wpre),
-                                   thr, P<uint8_t>(f));
-                nh = flags_to_indices(s, P<uint8_t>(f), n, hubs);
-                if (nh > 0) {
-                    Buf ikey = dev_alloc(sizeof(uint64_t) * mv, s), ioff = dev_alloc(sizeof(int64_t) * (n + 2), s);
-                    hipLaunchKernelGGL(k_vl4_split, dim3(grid(s, mv)), dim3(256), 0, st, P<uint64_t>(key), mv, P<uint8_t>(f),
-                                       P<int64_t>(wc), P<uint64_t>(ikey));
-                    std::vector<int> sh;
-                    for (int b = 24; b < 48; b += 8) sh.push_back(b);  // by target; sources stay unordered (any order)
-                    radix_sort_keys(s, ikey, mv, sh);
-                    hipLaunchKernelGGL(k_vl4_off, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ikey), mv, n,
-                                       P<int64_t>(ioff));
-                    const size_t lds = sizeof(uint32_t) * (size_t)((n + 31) / 32);
-                    lds_attr(reinterpret_cast<const void*>(k_vl4_hub), lds);
-                    hipLaunchKernelGGL(k_vl4_hub, dim3((unsigned)std::min<int64_t>(nh, s->num_cus)), dim3(kVl4HubBlock), lds, st,
-                                       P<int64_t>(hubs), nh, n, P<uint64_t>(key), P<int64_t>(off), P<uint64_t>(ikey),
-                                       P<int64_t>(ioff), P<int64_t>(wpre), h, v.T14);
-                    wpre2 = dev_alloc(sizeof(int64_t) * (mv + 1), s);  // the other starts' wedges
-                    exclusive_scan_i64(P<int64_t>(wc), P<int64_t>(wpre2), mv, s);
-                }
-            }
-            const int64_t* wp = nh > 0 ? P<int64_t>(wpre2) : P<int64_t>(wpre);
-            const int64_t total = read_scalar(s, wp + mv);
+            // the in-lists: a stable sort of the keys by target (3 digits) keeps each target's sources ascending
+            Buf ik = dev_alloc(sizeof(uint64_t) * mv, s), tg = dev_alloc(sizeof(uint32_t) * mv, s),
+                isrc = dev_alloc(sizeof(uint32_t) * mv, s), ioff = dev_alloc(sizeof(int64_t) * (n + 2), s);
+            HIP_CHECK(hipMemcpyAsync(P<void>(ik), P<void>(key), sizeof(uint64_t) * mv, hipMemcpyDeviceToDevice, st));
+            radix_sort_keys(s, ik, mv, {0, 8, 16});
+            hipLaunchKernelGGL(k_vl4_lists, dim3(grid(s, mv)), dim3(256), 0, st, P<uint64_t>(key), P<uint64_t>(ik), mv,
+                               P<uint32_t>(tg), P<uint32_t>(isrc));
+            hipLaunchKernelGGL(k_vl4_ioff, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), mv, n, P<int64_t>(ioff));
+            ik = Buf();
+            const int64_t total = read_scalar(s, P<int64_t>(wpre) + mv);
             const int64_t wv = (total + 64 * kVl4Rounds - 1) / (64 * kVl4Rounds);  // waves
             if (wv > 0)
-                hipLaunchKernelGGL(k_vl4_wedges, dim3(grid(s, 64 * wv)), dim3(256), 0, st, P<uint64_t>(key), mv,
-                                   P<int64_t>(off), wp, h, v.T14);
+                hipLaunchKernelGGL(k_vl4_wedges, dim3(grid(s, 64 * wv)), dim3(256), 0, st, P<uint64_t>(key),
+                                   P<uint32_t>(tg), mv, P<int64_t>(off), P<int64_t>(wpre), P<uint32_t>(isrc),
+                                   P<int64_t>(ioff), v.T14);
         }
     }
     hipLaunchKernelGGL(k_vl4_sum, dim3(grid(s, n)), dim3(256), 0, st, n, d, od, sl, W, v, L4);
