@@ -807,67 +807,168 @@ __global__ void k_vl4_ioff(const uint64_t* __restrict__ ik, int64_t mv, int64_t 
     }
 }
 
-// T14: a wave takes 64 * kVl4Rounds consecutive wedges (r, r') in key order -- r = a -> y, r' = y -> p -- and
-// lane l the wedges wb + l + 64 k, so the lanes read consecutive entries of y's out-list together (coalesced);
-// a lane finds its first r by a search over the wedge prefix and then advances.  m(p, a) is the number of p's
-// in a's sorted in-list: a binary search there, the wave's lanes mostly on the same a (one list, cached lines)
-// -- closing pairs are rare (under 0.1 % of the wedges at C5), so most searches end on the list's bounds or
-// after a few cached probes instead of a random probe of the pair table.  A lane's sum for one a is added once.
-constexpr int kVl4Rounds = 16;
-__global__ void k_vl4_wedges(const uint64_t* __restrict__ key, const uint32_t* __restrict__ tg, int64_t mv,
-                             const int64_t* __restrict__ off, const int64_t* __restrict__ wpre,
-                             const uint32_t* __restrict__ isrc, const int64_t* __restrict__ ioff,
-                             unsigned long long* __restrict__ T14) {
-    const int64_t total = wpre[mv];
-    const int lane = threadIdx.x & 63;
-    constexpr int64_t kSpan = 64 * kVl4Rounds;
-    const int64_t waves = (int64_t)gridDim.x * (blockDim.x / 64);
-    for (int64_t wb = ((int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * kSpan; wb < total;
-         wb += waves * kSpan) {  // wave-uniform
-        const int64_t w0 = wb + lane, we = min(total, wb + kSpan);
-        if (w0 >= we) continue;
-        int64_t lo = 0, hi = mv;  // the last r with wpre[r] <= w0
+// T14 in load-balanced tiles of kVl4T consecutive wedges (r, r') -- r = a -> y, r' = y -> p -- over the
+// relationships with wedges, compacted (cw = the first wedge, coy = off[y], ca = a).  A tile's relationships
+// are read once, coalesced, into LDS, each wedge's owner comes from a fill-forward max scan of their start
+// positions, and lane t takes the wedges t + 512 j: consecutive lanes read consecutive entries of y's out-list.
+// m(p, a) is the number of p's in a's sorted in-list, found by a binary search: in LDS when the whole tile is
+// one start's (about half the tiles at C5) and its list fits, else in global memory (the lanes of a wave then
+// mostly on one a and its cached lines; loading every start's list of a mixed tile into LDS measured slower,
+// 19.5 -> 22.0 ms).  Closing pairs are rare (under 0.1 % of the wedges at C5), each adds one atomic.
+#ifndef VL4_EXP
+#define VL4_EXP 0
+#endif
+constexpr int kVl4B = 512, kVl4I = 4, kVl4T = kVl4B * kVl4I;
+constexpr int kVl4L = 4096;  // a single-start tile's in-list, searched in LDS, up to this many sources
+
+// per tile, its first relationship: the last k with cw[k] <= the tile's first wedge (a search per tile here,
+// all in flight at once, instead of one dependent search at the head of each tile)
+__global__ void k_vl4_tiles(const int64_t* __restrict__ cw, int64_t K, int64_t ntiles, int64_t* __restrict__ tk) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < ntiles; q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t W0 = q * kVl4T;
+        int64_t lo = 0, hi = K;
         while (hi - lo > 1) {
             const int64_t mid = (lo + hi) >> 1;
-            if (wpre[mid] <= w0) lo = mid; else hi = mid;
+            if (cw[mid] <= W0) lo = mid; else hi = mid;
         }
-        int64_t r = lo, r_end = wpre[r + 1], r_w = wpre[r];
-        uint32_t a = (uint32_t)(key[r] >> 24), y = tg[r];
-        int64_t i0 = ioff[a], i1 = ioff[a + 1];
-        uint32_t pmin = i1 > i0 ? isrc[i0] : 1u, pmax = i1 > i0 ? isrc[i1 - 1] : 0u;
-        int64_t oy = off[y];
-        unsigned long long acc = 0;
-        for (int64_t w = w0; w < we; w += 64) {
-            if (w >= r_end) {
-                do { ++r; } while (wpre[r + 1] <= w);
-                r_w = wpre[r];
-                r_end = wpre[r + 1];
-                y = tg[r];
-                oy = off[y];
-                const uint32_t ar = (uint32_t)(key[r] >> 24);
-                if (ar != a) {
-                    if (acc) atomicAdd(&T14[a], acc);
-                    acc = 0;
-                    a = ar;
-                    i0 = ioff[a];
-                    i1 = ioff[a + 1];
-                    pmin = i1 > i0 ? isrc[i0] : 1u;
-                    pmax = i1 > i0 ? isrc[i1 - 1] : 0u;
+        tk[q] = lo;
+    }
+}
+
+__global__ void k_vl4_nz(const int64_t* __restrict__ wc, int64_t mv, int64_t* __restrict__ fl) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < mv; r += (int64_t)gridDim.x * blockDim.x)
+        fl[r] = wc[r] ? 1 : 0;
+}
+
+__global__ void k_vl4_compact(const uint64_t* __restrict__ key, const uint32_t* __restrict__ tg, int64_t mv,
+                              const int64_t* __restrict__ off, const int64_t* __restrict__ wc,
+                              const int64_t* __restrict__ wpre, const int64_t* __restrict__ cpos,
+                              int64_t* __restrict__ cw, int64_t* __restrict__ coy, uint32_t* __restrict__ ca) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < mv; r += (int64_t)gridDim.x * blockDim.x) {
+        if (!wc[r]) continue;
+        const int64_t j = cpos[r];
+        cw[j] = wpre[r];
+        coy[j] = off[tg[r]];
+        ca[j] = (uint32_t)(key[r] >> 24);
+    }
+}
+
+// inclusive block scan of one value per thread (kVl4B threads), op = sum or max
+template <bool MAX>
+__device__ __forceinline__ uint32_t vl4_scan(uint32_t v, uint32_t* wtot, uint32_t& excl) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x = MAX ? max(x, y) : x + y;
+    }
+    if (lane == 63) wtot[wave] = x;
+    __syncthreads();
+    const uint32_t xp = __shfl_up(x, 1, 64);  // every lane active
+    uint32_t pre = lane > 0 ? xp : 0u;
+    for (int q = 0; q < wave; ++q) pre = MAX ? max(pre, wtot[q]) : pre + wtot[q];
+    excl = pre;
+    uint32_t all = 0;
+    for (int q = 0; q < kVl4B / 64; ++q) all = MAX ? max(all, wtot[q]) : all + wtot[q];
+    __syncthreads();  // wtot is reused by the next scan
+    return all;
+}
+
+__global__ void __launch_bounds__(kVl4B) k_vl4_wedges(const int64_t* __restrict__ cw, const int64_t* __restrict__ coy,
+                                                     const uint32_t* __restrict__ ca, const int64_t* __restrict__ tk,
+                                                     int64_t K, int64_t total,
+                                                     const uint32_t* __restrict__ tg, const uint32_t* __restrict__ isrc,
+                                                     const int64_t* __restrict__ ioff,
+                                                     unsigned long long* __restrict__ T14) {
+    __shared__ int32_t sw[kVl4T];   // first wedge of the tile's k-th relationship, relative to the tile
+    __shared__ int64_t soy[kVl4T];
+    __shared__ uint32_t sa[kVl4T];
+    __shared__ uint16_t own[kVl4T];  // wedge -> its relationship (tile-local k)
+    __shared__ uint32_t sl[kVl4L];
+    __shared__ uint32_t wtot[kVl4B / 64];
+    const int t = threadIdx.x;
+    for (int64_t W0 = (int64_t)blockIdx.x * kVl4T; W0 < total; W0 += (int64_t)gridDim.x * kVl4T) {  // block-uniform
+        for (int i = t; i < kVl4T; i += kVl4B) own[i] = 0;
+        __syncthreads();
+        const int64_t k0 = tk[W0 / kVl4T], nt = min((int64_t)kVl4T, total - W0);
+        for (int i = t; i < kVl4T && k0 + i < K; i += kVl4B) {
+            const int64_t w = cw[k0 + i];
+            if (i > 0 && w >= W0 + nt) break;  // past the tile (starts ascend)
+            sw[i] = (int32_t)(w - W0);
+            soy[i] = coy[k0 + i];
+            sa[i] = ca[k0 + i];
+            if (i > 0) own[w - W0] = (uint16_t)i;
+        }
+        __syncthreads();
+        // fill forward: own[i] = max(own[0..i]) (the starts ascend with k); thread t holds positions 4t..4t+3
+        uint32_t v[kVl4I];
+        uint32_t m = 0;
+#pragma unroll
+        for (int j = 0; j < kVl4I; ++j) {
+            m = max(m, (uint32_t)own[t * kVl4I + j]);
+            v[j] = m;
+        }
+        uint32_t pre;
+        vl4_scan<true>(m, wtot, pre);
+#pragma unroll
+        for (int j = 0; j < kVl4I; ++j) own[t * kVl4I + j] = (uint16_t)max(v[j], pre);
+        __syncthreads();
+        // a tile of one start whose in-list fits: the list into LDS, the searches there
+        const uint32_t a0 = sa[0];
+        const int64_t l0 = ioff[a0], ln = ioff[a0 + 1] - l0;
+        if (sa[own[nt - 1]] == a0 && ln <= kVl4L) {  // block-uniform
+            for (int i = t; i < ln; i += kVl4B) sl[i] = isrc[l0 + i];
+            __syncthreads();
+            unsigned long long c = 0;
+#pragma unroll
+            for (int j = 0; j < kVl4I; ++j) {
+                const int i = t + j * kVl4B;
+                if (i >= nt) break;
+                const int k = own[i];
+                const uint32_t p = tg[soy[k] + (i - sw[k])];
+#if VL4_EXP == 1
+                c += p == 0x7FFFFFu ? 1 : 0;
+                continue;
+#endif
+                int l = 0, h = (int)ln;  // the first source >= p
+                while (l < h) {
+                    const int mid = (l + h) >> 1;
+                    if (sl[mid] < p) l = mid + 1; else h = mid;
+                }
+                while (l < (int)ln && sl[l] == p) {
+                    ++c;
+                    ++l;
                 }
             }
-            const uint32_t p = tg[oy + (w - r_w)];
-            if (p < pmin || p > pmax) continue;
+            if (c) atomicAdd(&T14[a0], c);
+            __syncthreads();
+            continue;
+        }
+#pragma unroll 2
+        for (int j = 0; j < kVl4I; ++j) {
+            const int i = t + j * kVl4B;
+            if (i >= nt) break;
+            const int k = own[i];
+            const uint32_t p = tg[soy[k] + (i - sw[k])], a = sa[k];
+#if VL4_EXP == 1
+            if (p == 0x7FFFFFu) atomicAdd(&T14[a], 1ull);
+            continue;
+#endif
+            const int64_t i0 = ioff[a], i1 = ioff[a + 1];
             int64_t l = i0, h = i1;  // the first source >= p
             while (l < h) {
                 const int64_t mid = (l + h) >> 1;
                 if (isrc[mid] < p) l = mid + 1; else h = mid;
             }
+            unsigned long long c = 0;
             while (l < i1 && isrc[l] == p) {
-                ++acc;
+                ++c;
                 ++l;
             }
+            if (c) atomicAdd(&T14[a], c);
         }
-        if (acc) atomicAdd(&T14[a], acc);
+        __syncthreads();  // the tile's LDS is rewritten by the next
     }
 }
 
@@ -951,12 +1052,30 @@ void var_length4(capsmi_session* s, const int64_t* const* srcs, const int64_t* c
                                P<uint32_t>(tg), P<uint32_t>(isrc));
             hipLaunchKernelGGL(k_vl4_ioff, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), mv, n, P<int64_t>(ioff));
             ik = Buf();
-            const int64_t total = read_scalar(s, P<int64_t>(wpre) + mv);
-            const int64_t wv = (total + 64 * kVl4Rounds - 1) / (64 * kVl4Rounds);  // waves
-            if (wv > 0)
-                hipLaunchKernelGGL(k_vl4_wedges, dim3(grid(s, 64 * wv)), dim3(256), 0, st, P<uint64_t>(key),
-                                   P<uint32_t>(tg), mv, P<int64_t>(off), P<int64_t>(wpre), P<uint32_t>(isrc),
-                                   P<int64_t>(ioff), v.T14);
+            // the relationships with wedges, compacted
+            Buf fl = dev_alloc(sizeof(int64_t) * mv, s), cpos = dev_alloc(sizeof(int64_t) * (mv + 1), s);
+            hipLaunchKernelGGL(k_vl4_nz, dim3(grid(s, mv)), dim3(256), 0, st, P<int64_t>(wc), mv, P<int64_t>(fl));
+            exclusive_scan_i64(P<int64_t>(fl), P<int64_t>(cpos), mv, s);
+            fl = Buf();
+            Buf cw = dev_alloc(sizeof(int64_t) * mv, s), coy = dev_alloc(sizeof(int64_t) * mv, s),
+                ca = dev_alloc(sizeof(uint32_t) * mv, s);
+            hipLaunchKernelGGL(k_vl4_compact, dim3(grid(s, mv)), dim3(256), 0, st, P<uint64_t>(key), P<uint32_t>(tg), mv,
+                               P<int64_t>(off), P<int64_t>(wc), P<int64_t>(wpre), P<int64_t>(cpos), P<int64_t>(cw),
+                               P<int64_t>(coy), P<uint32_t>(ca));
+            int64_t kt[2];
+            HIP_CHECK(hipMemcpyAsync(&kt[0], P<int64_t>(cpos) + mv, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipMemcpyAsync(&kt[1], P<int64_t>(wpre) + mv, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+            HIP_CHECK(hipStreamSynchronize(st));
+            const int64_t K = kt[0], total = kt[1];
+            if (total > 0) {
+                const int64_t ntiles = (total + kVl4T - 1) / kVl4T;
+                Buf tk = dev_alloc(sizeof(int64_t) * ntiles, s);
+                hipLaunchKernelGGL(k_vl4_tiles, dim3(grid(s, ntiles)), dim3(256), 0, st, P<int64_t>(cw), K, ntiles,
+                                   P<int64_t>(tk));
+                hipLaunchKernelGGL(k_vl4_wedges, dim3(grid(s, ntiles * kVl4B)), dim3(kVl4B), 0, st, P<int64_t>(cw),
+                                   P<int64_t>(coy), P<uint32_t>(ca), P<int64_t>(tk), K, total, P<uint32_t>(tg),
+                                   P<uint32_t>(isrc), P<int64_t>(ioff), v.T14);
+            }
         }
     }
     hipLaunchKernelGGL(k_vl4_sum, dim3(grid(s, n)), dim3(256), 0, st, n, d, od, sl, W, v, L4);
