@@ -701,57 +701,112 @@ void zero_words(capsmi_session* s, std::initializer_list<std::pair<void*, int64_
 // s the self-loops, M(x, y) = m(x, y) m(y, x) and od = A b, W = A od (the len-3 vectors):
 //   len4 = A^4 b - [s W + A (s od) + A A (s b)] - [M od + A M b + T14] + [2 s^2 b + b M 1]
 //          + 2 [s od + 2 s^2 b + A (s b)] - 6 s b,          T14(a) = sum_{r: a -> y} b(y) sum_{r': y -> p} m(p, a)
-// Every term but T14 is a product of per-node vectors over the relationships (atomic passes) and of the
-// pair multiplicities (an exact pair table); T14 walks the 2-hop wedges a -> y -> p in balanced chunks and
-// looks each closing pair (p, a) up in the table.  Relative ids below 2^24 - 1 (the table's keys).
+// Every term but T14 is a product of per-node vectors over the relationships and of the pair multiplicities
+// m(y, x), counted in x's sorted in-list; three passes over the (source, target)-sorted relationships (one
+// atomic per source run of a wave).  T14 walks the 2-hop wedges a -> y -> p in load-balanced tiles and counts
+// each closing p in a's in-list.  Relative ids below 2^24 - 1 (the keys' fields).
 struct Vl4 {  // per-node u64 sums (two's complement)
     unsigned long long *X, *Q1, *P, *W4, *Q2, *Rb, *R1, *MAb, *ARb, *T14;
 };
 
-// per relationship x -> y: X = A W, Q1 = A (s b), P = A (s od); every pair into the table
-__global__ void k_vl4_a(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, Dom d,
-                        const unsigned long long* __restrict__ od, const unsigned long long* __restrict__ s,
-                        const unsigned long long* __restrict__ W, PairHash h, Vl4 v) {
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t x = src[e], y = dst[e];
-        if (!in_dom(d, x) || !in_dom(d, y)) continue;
-        const int64_t xi = x - d.lo, yi = y - d.lo;
-        if (W[yi]) atomicAdd(&v.X[xi], W[yi]);
-        const unsigned long long sy = s[yi];
-        if (sy) {
-            if (bok(d, y)) atomicAdd(&v.Q1[xi], sy);
-            if (od[yi]) atomicAdd(&v.P[xi], sy * od[yi]);
+// The per-relationship passes run over the (source, target)-sorted keys: the lanes of a wave hold consecutive
+// keys, so their sources form contiguous runs and each run's sum takes one atomic (a segmented sum over the
+// wave) instead of one per relationship.
+__device__ __forceinline__ void seg_add(uint32_t x, unsigned long long v, unsigned long long* __restrict__ arr) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {  // v = the sum over lanes lane .. min(lane + 2o - 1, the run's end)
+        const unsigned long long vv = __shfl_down(v, o, 64);
+        const uint32_t xx = __shfl_down(x, o, 64);
+        if (lane + o < 64 && xx == x) v += vv;
+    }
+    const uint32_t xp = __shfl_up(x, 1, 64);
+    if ((lane == 0 || xp != x) && x != 0xFFFFFFFFu && v) atomicAdd(&arr[x], v);
+}
+
+// the number of p's in x's sorted in-list (m(p, x))
+__device__ __forceinline__ unsigned long long in_count(const uint32_t* __restrict__ isrc, int64_t i0, int64_t i1,
+                                                       uint32_t p) {
+    int64_t l = i0, h = i1;
+    while (l < h) {
+        const int64_t mid = (l + h) >> 1;
+        if (isrc[mid] < p) l = mid + 1; else h = mid;
+    }
+    unsigned long long c = 0;
+    while (l < i1 && isrc[l] == p) {
+        ++c;
+        ++l;
+    }
+    return c;
+}
+
+// per relationship x -> y: X = A W, Q1 = A (s b), P = A (s od)
+__global__ void k_vl4_a(const uint64_t* __restrict__ key, int64_t mv, Dom d, const unsigned long long* __restrict__ od,
+                        const unsigned long long* __restrict__ s, const unsigned long long* __restrict__ W, Vl4 v) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x; e0 < mv; e0 += stride) {  // block-uniform
+        const int64_t e = e0 + threadIdx.x;
+        uint32_t x = 0xFFFFFFFFu;
+        unsigned long long wx = 0, q1 = 0, pp = 0;
+        if (e < mv) {
+            const uint64_t k = key[e];
+            x = (uint32_t)(k >> 24);
+            const uint32_t y = (uint32_t)(k & 0xFFFFFF);
+            wx = W[y];
+            const unsigned long long sy = s[y];
+            if (sy) {
+                if (bok(d, d.lo + y)) q1 = sy;
+                pp = sy * od[y];
+            }
         }
-        pair_insert(h, hkey((uint32_t)xi, (uint32_t)yi));
+        seg_add(x, wx, v.X);
+        seg_add(x, q1, v.Q1);
+        seg_add(x, pp, v.P);
     }
 }
 
 // per relationship x -> y: W4 = A X, Q2 = A Q1, and with r = m(y, x): Rb = M b, R1 = M 1, MAb = M od
-__global__ void k_vl4_b(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, Dom d,
-                        const unsigned long long* __restrict__ od, PairHash h, Vl4 v) {
-    const bool ovf = *h.any_ovf != 0;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t x = src[e], y = dst[e];
-        if (!in_dom(d, x) || !in_dom(d, y)) continue;
-        const int64_t xi = x - d.lo, yi = y - d.lo;
-        if (v.X[yi]) atomicAdd(&v.W4[xi], v.X[yi]);
-        if (v.Q1[yi]) atomicAdd(&v.Q2[xi], v.Q1[yi]);
-        const unsigned long long r = pair_count(h, hkey((uint32_t)yi, (uint32_t)xi), ovf);
-        if (r) {
-            if (bok(d, y)) atomicAdd(&v.Rb[xi], r);
-            atomicAdd(&v.R1[xi], r);
-            if (od[yi]) atomicAdd(&v.MAb[xi], r * od[yi]);
+__global__ void k_vl4_b(const uint64_t* __restrict__ key, int64_t mv, Dom d, const unsigned long long* __restrict__ od,
+                        const uint32_t* __restrict__ isrc, const int64_t* __restrict__ ioff, Vl4 v) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x; e0 < mv; e0 += stride) {  // block-uniform
+        const int64_t e = e0 + threadIdx.x;
+        uint32_t x = 0xFFFFFFFFu;
+        unsigned long long w4 = 0, q2 = 0, rb = 0, r1 = 0, mab = 0;
+        if (e < mv) {
+            const uint64_t k = key[e];
+            x = (uint32_t)(k >> 24);
+            const uint32_t y = (uint32_t)(k & 0xFFFFFF);
+            w4 = v.X[y];
+            q2 = v.Q1[y];
+            const unsigned long long r = in_count(isrc, ioff[x], ioff[x + 1], y);
+            if (r) {
+                if (bok(d, d.lo + y)) rb = r;
+                r1 = r;
+                mab = r * od[y];
+            }
         }
+        seg_add(x, w4, v.W4);
+        seg_add(x, q2, v.Q2);
+        seg_add(x, rb, v.Rb);
+        seg_add(x, r1, v.R1);
+        seg_add(x, mab, v.MAb);
     }
 }
 
 // per relationship x -> y: ARb = A Rb
-__global__ void k_vl4_c(const int64_t* __restrict__ src, const int64_t* __restrict__ dst, int64_t m, Dom d, Vl4 v) {
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < m; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t x = src[e], y = dst[e];
-        if (!in_dom(d, x) || !in_dom(d, y)) continue;
-        const unsigned long long r = v.Rb[y - d.lo];
-        if (r) atomicAdd(&v.ARb[x - d.lo], r);
+__global__ void k_vl4_c(const uint64_t* __restrict__ key, int64_t mv, Vl4 v) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e0 = (int64_t)blockIdx.x * blockDim.x; e0 < mv; e0 += stride) {  // block-uniform
+        const int64_t e = e0 + threadIdx.x;
+        uint32_t x = 0xFFFFFFFFu;
+        unsigned long long r = 0;
+        if (e < mv) {
+            const uint64_t k = key[e];
+            x = (uint32_t)(k >> 24);
+            r = v.Rb[k & 0xFFFFFF];
+        }
+        seg_add(x, r, v.ARb);
     }
 }
 
@@ -1007,23 +1062,7 @@ void var_length4(capsmi_session* s, const int64_t* const* srcs, const int64_t* c
     const int64_t nw = (int64_t)(nb / sizeof(unsigned long long));
     Vl4 v{base, base + nw, base + 2 * nw, base + 3 * nw, base + 4 * nw, base + 5 * nw, base + 6 * nw, base + 7 * nw,
           base + 8 * nw, base + 9 * nw};
-    // the exact pair table of every relationship: a power of two >= 2 * mtot slots
-    int64_t cap = 1024;
-    while (cap < 2 * mtot) cap <<= 1;
-    const size_t hbytes = (sizeof(unsigned long long) + sizeof(unsigned int)) * cap + 16;
-    Buf hk = dev_alloc(hbytes, s);
-    HIP_CHECK(hipMemsetAsync(P<void>(hk), 0, hbytes, st));
-    unsigned int* hcw = reinterpret_cast<unsigned int*>(P<unsigned long long>(hk) + cap);
-    const PairHash h{P<unsigned long long>(hk), hcw, hcw + cap, (unsigned long long)(cap - 1)};
-    for (int i = 0; i < nt; ++i)
-        if (ms[i] > 0)
-            hipLaunchKernelGGL(k_vl4_a, dim3(grid(s, ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], d, od, sl, W, h, v);
-    for (int i = 0; i < nt; ++i)
-        if (ms[i] > 0) hipLaunchKernelGGL(k_vl4_b, dim3(grid(s, ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], d, od, h, v);
-    for (int i = 0; i < nt; ++i)
-        if (ms[i] > 0) hipLaunchKernelGGL(k_vl4_c, dim3(grid(s, ms[i])), dim3(256), 0, st, srcs[i], dsts[i], ms[i], d, v);
-    HIP_CHECK(hipGetLastError());
-    if (mtot > 0) {  // T14 over the wedges, the relationships sorted by (source, target)
+    if (mtot > 0) {  // the relationships sorted by (source, target), and the in-lists
         Buf key = dev_alloc(sizeof(uint64_t) * mtot, s);
         int64_t off0 = 0;
         for (int i = 0; i < nt; ++i) {
@@ -1052,7 +1091,11 @@ void var_length4(capsmi_session* s, const int64_t* const* srcs, const int64_t* c
                                P<uint32_t>(tg), P<uint32_t>(isrc));
             hipLaunchKernelGGL(k_vl4_ioff, dim3(grid(s, n + 1)), dim3(256), 0, st, P<uint64_t>(ik), mv, n, P<int64_t>(ioff));
             ik = Buf();
-            // the relationships with wedges, compacted
+            hipLaunchKernelGGL(k_vl4_a, dim3(grid(s, mv)), dim3(256), 0, st, P<uint64_t>(key), mv, d, od, sl, W, v);
+            hipLaunchKernelGGL(k_vl4_b, dim3(grid(s, mv)), dim3(256), 0, st, P<uint64_t>(key), mv, d, od, P<uint32_t>(isrc),
+                               P<int64_t>(ioff), v);
+            hipLaunchKernelGGL(k_vl4_c, dim3(grid(s, mv)), dim3(256), 0, st, P<uint64_t>(key), mv, v);
+            // T14: the relationships with wedges, compacted
             Buf fl = dev_alloc(sizeof(int64_t) * mv, s), cpos = dev_alloc(sizeof(int64_t) * (mv + 1), s);
             hipLaunchKernelGGL(k_vl4_nz, dim3(grid(s, mv)), dim3(256), 0, st, P<int64_t>(wc), mv, P<int64_t>(fl));
             exclusive_scan_i64(P<int64_t>(fl), P<int64_t>(cpos), mv, s);
