@@ -870,9 +870,6 @@ __global__ void k_vl4_ioff(const uint64_t* __restrict__ ik, int64_t mv, int64_t 
 // one start's (about half the tiles at C5) and its list fits, else in global memory (the lanes of a wave then
 // mostly on one a and its cached lines; loading every start's list of a mixed tile into LDS measured slower,
 // 19.5 -> 22.0 ms).  Closing pairs are rare (under 0.1 % of the wedges at C5), each adds one atomic.
-#ifndef VL4_EXP
-#define VL4_EXP 0
-#endif
 constexpr int kVl4B = 512, kVl4I = 4, kVl4T = kVl4B * kVl4I;
 constexpr int kVl4L = 4096;  // a single-start tile's in-list, searched in LDS, up to this many sources
 
@@ -969,6 +966,20 @@ __global__ void __launch_bounds__(kVl4B) k_vl4_wedges(const int64_t* __restrict_
 #pragma unroll
         for (int j = 0; j < kVl4I; ++j) own[t * kVl4I + j] = (uint16_t)max(v[j], pre);
         __syncthreads();
+        // every wedge's closing source p first (the lane's kVl4I loads in flight together)
+        uint32_t pv[kVl4I];
+        int kv[kVl4I];
+#pragma unroll
+        for (int j = 0; j < kVl4I; ++j) {
+            const int i = t + j * kVl4B;
+            kv[j] = -1;
+            pv[j] = 0;
+            if (i < nt) {
+                const int k = own[i];
+                kv[j] = k;
+                pv[j] = tg[soy[k] + (i - sw[k])];
+            }
+        }
         // a tile of one start whose in-list fits: the list into LDS, the searches there
         const uint32_t a0 = sa[0];
         const int64_t l0 = ioff[a0], ln = ioff[a0 + 1] - l0;
@@ -978,14 +989,8 @@ __global__ void __launch_bounds__(kVl4B) k_vl4_wedges(const int64_t* __restrict_
             unsigned long long c = 0;
 #pragma unroll
             for (int j = 0; j < kVl4I; ++j) {
-                const int i = t + j * kVl4B;
-                if (i >= nt) break;
-                const int k = own[i];
-                const uint32_t p = tg[soy[k] + (i - sw[k])];
-#if VL4_EXP == 1
-                c += p == 0x7FFFFFu ? 1 : 0;
-                continue;
-#endif
+                if (kv[j] < 0) continue;
+                const uint32_t p = pv[j];
                 int l = 0, h = (int)ln;  // the first source >= p
                 while (l < h) {
                     const int mid = (l + h) >> 1;
@@ -1000,27 +1005,11 @@ __global__ void __launch_bounds__(kVl4B) k_vl4_wedges(const int64_t* __restrict_
             __syncthreads();
             continue;
         }
-#pragma unroll 2
+#pragma unroll
         for (int j = 0; j < kVl4I; ++j) {
-            const int i = t + j * kVl4B;
-            if (i >= nt) break;
-            const int k = own[i];
-            const uint32_t p = tg[soy[k] + (i - sw[k])], a = sa[k];
-#if VL4_EXP == 1
-            if (p == 0x7FFFFFu) atomicAdd(&T14[a], 1ull);
-            continue;
-#endif
-            const int64_t i0 = ioff[a], i1 = ioff[a + 1];
-            int64_t l = i0, h = i1;  // the first source >= p
-            while (l < h) {
-                const int64_t mid = (l + h) >> 1;
-                if (isrc[mid] < p) l = mid + 1; else h = mid;
-            }
-            unsigned long long c = 0;
-            while (l < i1 && isrc[l] == p) {
-                ++c;
-                ++l;
-            }
+            if (kv[j] < 0) continue;
+            const uint32_t a = sa[kv[j]];
+            const unsigned long long c = in_count(isrc, ioff[a], ioff[a + 1], pv[j]);
             if (c) atomicAdd(&T14[a], c);
         }
         __syncthreads();  // the tile's LDS is rewritten by the next
