@@ -994,7 +994,7 @@ def run_single(args):
         check = "ok" if ref == res else f"MISMATCH {res} vs unsharded {ref}"
         del full
     # every line checks its answer against the committed oracle fixture (tests/golden/rmat_full.json)
-    fx = fixture(f"{wl}_s{scale}") if up == 3 else None
+    fx = fixture(f"{wl}_s{scale}" if up == 3 else f"{wl}u{up}_s{scale}")  # c5u4_*: the *1..4 answers
     if fx is None or (world > 1 and wl == "c2"):
         fcheck = "no fixture for this scale" if fx is None else "rows only (output stays partitioned)"
         if fx is not None and wl == "c2":

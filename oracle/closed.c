@@ -275,6 +275,46 @@ int orc_var_length_closed_form(int64_t n, int64_t m, const int64_t* src, const i
 /* ---- C4 ------------------------------------------------------------------------------------- */
 /* LSD radix sort of 64-bit keys on their low `bits` bits (8-bit digits); returns the buffer that
  * holds the result (a or tmp) */
+/* The one four-hop term that is not a product of per-node vectors (cpu.py var_length4_closed_form, the block
+ * {1,4} of the hop positions): T14(a) = sum_{r: a->y} b_ok(y) sum_{r': y->p} m(p, a), the closing
+ * relationships of the 2-walks a -> y -> p counted with multiplicity = sum_y m(a,y) b_ok(y) |out(y) ∩ in(a)|
+ * over multisets, by a merge of y's sorted out-list with a's sorted in-list (the wedges are never listed). */
+int orc_vl4_t14(int64_t n, int64_t m, const int64_t* src, const int64_t* dst, const uint8_t* b_ok, int64_t* t14,
+                int nthreads) {
+    set_threads(nthreads);
+    int64_t *ooff = NULL, *otg = NULL, *ioff = NULL, *isrc = NULL;
+    if (sorted_csr(n, m, src, dst, &ooff, &otg)) return -1;
+    if (sorted_csr(n, m, dst, src, &ioff, &isrc)) { free(ooff); free(otg); return -1; }
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int64_t a = 0; a < n; ++a) {
+        int64_t t = 0;
+        const int64_t ib = ioff[a], ie = ioff[a + 1];
+        for (int64_t i = ooff[a]; i < ooff[a + 1];) {
+            const int64_t y = otg[i];
+            int64_t k = 1;  /* m(a, y): the run of y in a's sorted out-list */
+            while (i + k < ooff[a + 1] && otg[i + k] == y) ++k;
+            i += k;
+            if (!OK(b_ok, y) || ib == ie) continue;
+            int64_t u = ooff[y], ue = ooff[y + 1], v = ib, c = 0;
+            while (u < ue && v < ie) {
+                if (otg[u] < isrc[v]) ++u;
+                else if (otg[u] > isrc[v]) ++v;
+                else {
+                    const int64_t p = otg[u];
+                    int64_t cu = 0, cv = 0;
+                    while (u < ue && otg[u] == p) { ++u; ++cu; }
+                    while (v < ie && isrc[v] == p) { ++v; ++cv; }
+                    c += cu * cv;
+                }
+            }
+            t += k * c;
+        }
+        t14[a] = t;
+    }
+    free(ooff); free(otg); free(ioff); free(isrc);
+    return 0;
+}
+
 static uint64_t* radix_sort_u64(uint64_t* a, uint64_t* tmp, int64_t n, int bits) {
     for (int sh = 0; sh < bits; sh += 8) {
         int64_t cnt[257];

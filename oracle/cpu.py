@@ -62,6 +62,8 @@ def load():
         lib.orc_var_length_closed_form.restype = ctypes.c_int
         lib.orc_var_length_closed_form.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, U8P, U8P, ctypes.c_int,
                                                    ctypes.c_int, I64P, I64P, ctypes.c_int]
+        lib.orc_vl4_t14.restype = ctypes.c_int
+        lib.orc_vl4_t14.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, U8P, I64P, ctypes.c_int]
         lib.orc_triangle_closed_form.restype = ctypes.c_int
         lib.orc_triangle_closed_form.argtypes = [ctypes.c_int64, ctypes.c_int64, I64P, I64P, U8P, I64P, ctypes.c_int]
         _lib = lib
@@ -213,8 +215,8 @@ def var_length4_closed_form(n, src, dst, a_ok=None, b_ok=None):
     pair multiplicities).  Scipy sparse over the multiplicity matrix A (A[x, y] = m(x, y), self-loops on the
     diagonal); test infrastructure.  Returns (total, per-node counts)."""
     import scipy.sparse as sp
-    src = np.asarray(src, np.int64)
-    dst = np.asarray(dst, np.int64)
+    src = np.ascontiguousarray(src, np.int64)
+    dst = np.ascontiguousarray(dst, np.int64)
     A = sp.csr_matrix((np.ones(len(src), np.int64), (src, dst)), shape=(n, n))
     A.sum_duplicates()
     s = A.diagonal().astype(np.int64)
@@ -223,10 +225,13 @@ def var_length4_closed_form(n, src, dst, a_ok=None, b_ok=None):
     Ab = A @ b
     A2b = A @ Ab
     M = A.multiply(A.T).tocsr()  # m(x, y) m(y, x)
-    A2 = (A @ A).tocsr()
     W4 = A @ (A @ A2b)
     pair1 = (s * A2b) + (A @ (s * Ab)) + (A @ (A @ (s * b)))      # {12} {23} {34}
-    pair2 = (M @ Ab) + (A @ (M @ b)) + (A.multiply(A2.T).tocsr() @ b)  # {13} {24} {14}
+    t14 = np.zeros(n, np.int64)  # {14}: sum_y A(a, y) b(y) (A A)(y, a), by merges (closed.c orc_vl4_t14)
+    if load().orc_vl4_t14(n, len(src), _p64(src), _p64(dst), _p8(None if b_ok is None else np.ascontiguousarray(b_ok, np.uint8)),
+                          _p64(t14), 0):
+        raise MemoryError("orc_vl4_t14")
+    pair2 = (M @ Ab) + (A @ (M @ b)) + t14  # {13} {24} {14}
     two = s * s * b * 2 + b * np.asarray(M.sum(axis=1)).ravel()     # {12}{34} {14}{23}; {13}{24}
     three = (s * Ab) + 2 * (s * s * b) + (A @ (s * b))             # {123}; {124} {134}; {234}
     per = (W4 - pair1 - pair2 + two + 2 * three - 6 * (s * b)) * a

@@ -73,9 +73,25 @@ def c5(scale):
             "fingerprint": [cnt, str(s), str(x)], "oracle": "closed.c orc_var_length_closed_form"}
 
 
+def c5u4(scale):
+    from oracle import cpu
+    n = 1 << scale
+    src, dst = cpu.rmat_edges(scale, 0, 32 << scale, LDBC, 42)
+    _, per3 = cpu.var_length_closed_form(n, src, dst, 1, 3)
+    _, per4 = cpu.var_length4_closed_form(n, src, dst)
+    per_a = per3 + per4
+    ids = np.nonzero(per_a)[0].astype(np.int64)
+    cnt, s, x = cpu.fingerprint([ids, per_a[ids]])
+    return {"query": "MATCH (a:Person)-[:KNOWS*1..4]->(b:Person) RETURN id(a), count(*)", "scale": scale,
+            "edge_factor": 32, "rmat": list(LDBC), "seed": 42, "rows": int(len(ids)), "sum_count": int(per_a.sum()),
+            "fingerprint": [cnt, str(s), str(x)],
+            "oracle": "closed.c orc_var_length_closed_form (1..3) + cpu.py var_length4_closed_form (4)"}
+
+
 JOBS = {"c3_s26": (c3, 26), "c3_s20": (c3, 20), "c3_s16": (c3, 16), "c3u_s26": (c3u, 26),
         "c3u_s20": (c3u, 20), "c3u_s16": (c3u, 16), "c2_s24": (c2, 24), "c2_s16": (c2, 16),
-        "c4_s24": (c4, 24), "c4_s14": (c4, 14), "c5_s20": (c5, 20), "c5_s14": (c5, 14)}
+        "c4_s24": (c4, 24), "c4_s14": (c4, 14), "c5_s20": (c5, 20), "c5_s14": (c5, 14),
+        "c5u4_s20": (c5u4, 20), "c5u4_s14": (c5u4, 14)}
 
 
 def main():

@@ -144,3 +144,16 @@ def test_c5_vs_fixture(session):
     assert int(out.column("count").values.sum()) == fx["sum_count"]
     assert list(out.fingerprint(["id", "count"])) == [fx["fingerprint"][0], int(fx["fingerprint"][1]),
                                                       int(fx["fingerprint"][2])]
+
+
+def test_c5_four_hops_vs_fixture(session):
+    """*1..4 at s = 14 against the oracle's full closed form (tests/golden/make_rmat_full.py c5u4_s14)."""
+    from capsmi import graph
+    fx = _fx("c5u4_s14")
+    scale = 14
+    rels = graph.rmat_rels(session, scale, 0, 32 << scale, graph.RMAT_LDBC, 42)
+    p = graph.NodeBitmap(session, 0, 1 << scale).add_scan(graph.rmat_nodes(session, scale, graph.NODES_ALL))
+    out = graph.var_length_count(session, [rels], p, p, 1, 4)
+    assert int(out.column("count").values.sum()) == fx["sum_count"]
+    assert list(out.fingerprint(["id", "count"])) == [fx["fingerprint"][0], int(fx["fingerprint"][1]),
+                                                      int(fx["fingerprint"][2])]
