@@ -933,8 +933,7 @@ __global__ void __launch_bounds__(kVl4B) k_vl4_wedges(const int64_t* __restrict_
                                                      const uint32_t* __restrict__ tg, const uint32_t* __restrict__ isrc,
                                                      const int64_t* __restrict__ ioff,
                                                      unsigned long long* __restrict__ T14) {
-    __shared__ int32_t sw[kVl4T];   // first wedge of the tile's k-th relationship, relative to the tile
-    __shared__ int64_t soy[kVl4T];
+    __shared__ int64_t soy[kVl4T];  // off[y] of the tile's k-th relationship minus its first wedge's tile position
     __shared__ uint32_t sa[kVl4T];
     __shared__ uint16_t own[kVl4T];  // wedge -> its relationship (tile-local k)
     __shared__ uint32_t sl[kVl4L];
@@ -947,8 +946,7 @@ __global__ void __launch_bounds__(kVl4B) k_vl4_wedges(const int64_t* __restrict_
         for (int i = t; i < kVl4T && k0 + i < K; i += kVl4B) {
             const int64_t w = cw[k0 + i];
             if (i > 0 && w >= W0 + nt) break;  // past the tile (starts ascend)
-            sw[i] = (int32_t)(w - W0);
-            soy[i] = coy[k0 + i];
+            soy[i] = coy[k0 + i] - (w - W0);  // wedge at tile position i: y's out-list entry soy[k] + i
             sa[i] = ca[k0 + i];
             if (i > 0) own[w - W0] = (uint16_t)i;
         }
@@ -977,7 +975,7 @@ __global__ void __launch_bounds__(kVl4B) k_vl4_wedges(const int64_t* __restrict_
             if (i < nt) {
                 const int k = own[i];
                 kv[j] = k;
-                pv[j] = tg[soy[k] + (i - sw[k])];
+                pv[j] = tg[soy[k] + i];
             }
         }
         // a tile of one start whose in-list fits: the list into LDS, the searches there
