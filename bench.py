@@ -1106,8 +1106,8 @@ def run_single(args):
     line["query"]["check_vs_fixture"] = fcheck
     if check is not None or (world > 1 and wl in ("c2", "c5")):
         line["query"]["check_vs_unsharded"] = check
-    line["cpu_baseline"] = None if (args.no_cpu_baseline or world > 1 or up != 3) else cpu_baseline_single(
-        wl, cpu_scale, ef, probs, scale)
+    line["cpu_baseline"] = None if (args.no_cpu_baseline or world > 1) else cpu_baseline_single(
+        wl, cpu_scale, ef, probs, scale, up)
     if rank == 0:
         print(json.dumps(line), flush=True)
     sess.close()
@@ -1117,7 +1117,7 @@ def run_single(args):
         sys.exit(f"bench: result differs from the oracle fixture: {fcheck}")
 
 
-def cpu_baseline_single(wl, scale, ef, probs, full_scale):
+def cpu_baseline_single(wl, scale, ef, probs, full_scale, up=3):
     """The oracle on the host cores, OpenMP over `cores` threads (CPU restatements, not CAPS-on-Spark:
     no JVM on the box).  First line: the SAME algorithm as the device path (oracle/closed.c / rmat.c)
     -- C2 and C5 on the full workload, C4 (triangle listing, ~20 s at scale 20) on a bounded sample;
@@ -1137,9 +1137,14 @@ def cpu_baseline_single(wl, scale, ef, probs, full_scale):
     elif wl == "c4":
         rows = cpu.triangle_closed_form(n, src, dst, threads=threads)
         what = "degree-oriented triangle listing with multiplicities (oracle/closed.c orc_triangle_closed_form)"
-    else:
+    elif up == 3:
         rows, _ = cpu.var_length_closed_form(n, src, dst, 1, 3, threads=threads)
         what = "closed form with reverse multiplicities (oracle/closed.c orc_var_length_closed_form)"
+    else:  # *1..4: lengths 1..3 as above plus the four-hop inclusion-exclusion (scipy sparse + closed.c orc_vl4_t14)
+        rows, _ = cpu.var_length_closed_form(n, src, dst, 1, 3, threads=threads)
+        rows += cpu.var_length4_closed_form(n, src, dst)[0]
+        what = ("closed forms, lengths 1..3 (oracle/closed.c) and 4 (inclusion-exclusion, oracle/cpu.py "
+                "var_length4_closed_form; its sparse products single-threaded)")
     dt = time.perf_counter() - t0
     del src, dst
     line = {"value": rows / dt, "unit": "matched rows/s", "cores": threads, "kind": "port",
@@ -1158,6 +1163,8 @@ def cpu_baseline_single(wl, scale, ef, probs, full_scale):
                                            f"container, OpenMP), not re-run on this host"}
     if wl == "c2":
         return line
+    if up == 4:
+        scale = min(scale, 11)  # 4-hop enumeration: ~10^10 paths at scale 11, seconds on 8 cores
     n = 1 << scale
     src, dst = cpu.rmat_edges(scale, 0, ef << scale, probs, 42)
     t0 = time.perf_counter()
@@ -1165,7 +1172,7 @@ def cpu_baseline_single(wl, scale, ef, probs, full_scale):
         rows = cpu.triangle_enumerate(n, src, dst, threads=threads)
         what = "triangle binding enumeration (oracle/rmat.c)"
     else:
-        rows, _per_a = cpu.var_length_count(n, src, dst, 1, 3, threads=threads)
+        rows, _per_a = cpu.var_length_count(n, src, dst, 1, up, threads=threads)
         what = "edge-distinct path enumeration (oracle/rmat.c)"
     dt = time.perf_counter() - t0
     line["enumeration"] = {"value": rows / dt, "unit": "matched rows/s", "cores": threads,
