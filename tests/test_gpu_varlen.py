@@ -354,7 +354,8 @@ def test_four_hops_split_tables_and_source_slices(session):
 
 @pytest.mark.gpu
 def test_four_hops_pair_multiplicity_over_16_bits(session):
-    """The pair table's 16-bit counts wrap into the overflow word (a pair of 70,000 relationships)."""
+    """A pair of 70,000 relationships: multiplicities past 16 bits, and start 7's in-list longer than the LDS copy
+    of a one-start wedge tile (those tiles search it in global memory)."""
     from capsmi import ColumnData, I64, graph
     rng = np.random.default_rng(23)
     n = 30
