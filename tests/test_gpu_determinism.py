@@ -57,3 +57,13 @@ def test_fused_and_unfused_agree_on_fingerprints(session):
     """The routed C2 expand and the same plan through the generic joins: one row multiset."""
     sg = _graph(session, 13, kind="person")
     assert _fp(session, sg, C2, True) == _fp(session, sg, C2, False)
+
+
+def test_four_hops_twice_same_fingerprint(session):
+    """The fused *1..4 count (the four-hop wedge tiles' atomics land in any order): one answer per run."""
+    q = {"clauses": [{"match": "(a:Person)-[:FRIEND_OF*1..4]->(b:Person)"}],
+         "return": {"items": [["id", ["id", "a"]], ["count", ["count*"]]]}}
+    sg = _graph(session, 10, kind="all")
+    first = _fp(session, sg, q, True)
+    assert first == _fp(session, sg, q, True)
+    assert first[1] > 0
